@@ -1,0 +1,250 @@
+"""ctypes binding of libfmt.so (include/fmt.h), the HIP engine for gfx950.
+
+There is no CPU fallback: if the library or a gfx950 device is missing, every call raises
+`EngineUnavailable`. Result dtypes below mirror the C structs byte for byte.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfmt.so")
+
+FMT_OK = 0
+FMT_E_USAGE, FMT_E_DATA, FMT_E_CAPACITY, FMT_E_DEVICE, FMT_E_UNSUPPORTED = -1, -2, -3, -4, -5
+STATUS_NAMES = {0: "OK", -1: "USAGE", -2: "DATA", -3: "CAPACITY", -4: "DEVICE", -5: "UNSUPPORTED"}
+
+LEAF_DTYPE = np.dtype(
+    [
+        ("ins_seq", "<i4"),
+        ("rm_seq", "<i4"),
+        ("rm_clients", "<u8"),
+        ("char_off", "<u4"),
+        ("len", "<u2"),
+        ("ins_client", "<i2"),
+        ("props", "<u2"),
+        ("block", "<u2"),
+        ("pad", "<u4"),
+    ]
+)
+assert LEAF_DTYPE.itemsize == 32
+
+DOC_RESULT_DTYPE = np.dtype(
+    [
+        ("status", "<i4"),
+        ("fail_seq", "<i4"),
+        ("cur_seq", "<i4"),
+        ("min_seq", "<i4"),
+        ("n_leaves", "<u4"),
+        ("n_chars", "<u4"),
+        ("n_props", "<u4"),
+        ("n_blocks", "<u4"),
+        ("depth", "<u4"),
+        ("visible_len", "<u4"),
+        ("pad", "<u4", (2,)),
+    ]
+)
+assert DOC_RESULT_DTYPE.itemsize == 48
+
+PROPS_MAX = 4
+PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
+assert PROPSET_DTYPE.itemsize == 20
+
+MAP_SLOT_DTYPE = np.dtype([("value", "<u4"), ("birth_seq", "<u4")])
+
+
+class FmtMtBatch(ctypes.Structure):
+    _fields_ = [
+        ("ops", ctypes.c_void_p),
+        ("n_ops", ctypes.c_uint64),
+        ("doc_op_offsets", ctypes.c_void_p),
+        ("n_docs", ctypes.c_uint32),
+        ("text", ctypes.c_void_p),
+        ("text_len", ctypes.c_uint64),
+        ("doc_init", ctypes.c_void_p),
+        ("props_off", ctypes.c_void_p),
+        ("n_props_ops", ctypes.c_uint32),
+        ("props_kv", ctypes.c_void_p),
+    ]
+
+
+class FmtStats(ctypes.Structure):
+    _fields_ = [
+        ("kernel_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
+        ("ops", ctypes.c_uint64),
+        ("docs", ctypes.c_uint64),
+        ("bytes_read", ctypes.c_uint64),
+        ("bytes_written", ctypes.c_uint64),
+        ("launches", ctypes.c_uint64),
+    ]
+
+
+class FmtConfig(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("stream", ctypes.c_void_p),
+        ("reserved", ctypes.c_uint32 * 4),
+    ]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def batch_struct(batch):
+    """Build an fmt_mt_batch over a MergeTreeBatch's numpy arrays; returns (struct, keepalive)."""
+    keep = [
+        np.ascontiguousarray(batch.ops),
+        np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64),
+        np.ascontiguousarray(batch.text, dtype="<u2"),
+        np.ascontiguousarray(batch.doc_init, dtype=np.uint32),
+        np.ascontiguousarray(batch.props_off, dtype=np.uint32),
+        np.ascontiguousarray(batch.props_kv, dtype=np.uint32) if len(batch.props_kv) else np.zeros(1, np.uint32),
+    ]
+    b = FmtMtBatch(
+        _ptr(keep[0]), len(keep[0]), _ptr(keep[1]), len(keep[1]) - 1, _ptr(keep[2]), len(keep[2]),
+        _ptr(keep[3]), _ptr(keep[4]), len(keep[4]) - 1, _ptr(keep[5]),
+    )
+    return b, keep
+
+
+class EngineUnavailable(RuntimeError):
+    """libfmt.so is missing or no gfx950 device is usable. There is deliberately no fallback."""
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"fmt error {STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineUnavailable(f"{LIB_PATH} not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.fmt_open.argtypes = [ctypes.POINTER(FmtConfig), ctypes.POINTER(P)]
+        L.fmt_close.argtypes = [P]
+        L.fmt_last_error.argtypes = [P]
+        L.fmt_last_error.restype = ctypes.c_char_p
+        L.fmt_sync.argtypes = [P]
+        L.fmt_get_stats.argtypes = [P, ctypes.POINTER(FmtStats)]
+        L.fmt_device_info.argtypes = [P, ctypes.c_char_p, ctypes.c_size_t]
+        L.fmt_map_load.argtypes = [P, P, U64, P, U32, U32]
+        L.fmt_map_run.argtypes = [P]
+        L.fmt_map_fetch.argtypes = [P, P]
+        L.fmt_map_replay_device.argtypes = [P, P, P, U32, U32, P]
+        L.fmt_mt_load.argtypes = [P, ctypes.POINTER(FmtMtBatch)]
+        L.fmt_mt_run.argtypes = [P]
+        L.fmt_mt_fetch_headers.argtypes = [P, P]
+        L.fmt_mt_fetch_doc.argtypes = [P, U32, P, U32, P, U32, P, U32]
+        L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = [
+    "fmt_open", "fmt_close", "fmt_last_error", "fmt_sync", "fmt_get_stats", "fmt_device_info",
+    "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device",
+    "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_capacity",
+]
+
+
+def capacity():
+    a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    lib().fmt_mt_capacity(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return a.value, b.value, c.value
+
+
+class Engine:
+    """One fmt_ctx bound to one HIP device (one per process/rank)."""
+
+    def __init__(self, device: int = 0, stream: int | None = None):
+        L = lib()
+        cfg = FmtConfig(device, 0, stream, (ctypes.c_uint32 * 4)())
+        h = ctypes.c_void_p()
+        rc = L.fmt_open(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != FMT_OK:
+            msg = L.fmt_last_error(h).decode() if h.value else "fmt_open failed"
+            if h.value:
+                L.fmt_close(h)
+            raise EngineUnavailable(msg)
+        self.h = h
+        self._keep = None
+
+    def close(self):
+        if self.h:
+            lib().fmt_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != FMT_OK:
+            raise EngineError(rc, lib().fmt_last_error(self.h).decode())
+
+    def sync(self):
+        self._check(lib().fmt_sync(self.h))
+
+    def stats(self) -> FmtStats:
+        s = FmtStats()
+        self._check(lib().fmt_get_stats(self.h, ctypes.byref(s)))
+        return s
+
+    def device_info(self) -> str:
+        buf = ctypes.create_string_buffer(256)
+        lib().fmt_device_info(self.h, buf, 256)
+        return buf.value.decode()
+
+    # ---- SharedMap
+    def map_load(self, batch):
+        ops = np.ascontiguousarray(batch.ops)
+        offs = np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64)
+        self._check(lib().fmt_map_load(self.h, _ptr(ops), len(ops), _ptr(offs), batch.n_docs, batch.key_bound))
+        self._map_shape = (batch.n_docs, batch.key_bound)
+
+    def map_run(self):
+        self._check(lib().fmt_map_run(self.h))
+
+    def map_fetch(self) -> np.ndarray:
+        out = np.zeros(self._map_shape[0] * self._map_shape[1], dtype=MAP_SLOT_DTYPE)
+        self._check(lib().fmt_map_fetch(self.h, _ptr(out)))
+        return out.reshape(self._map_shape)
+
+    # ---- merge-tree
+    def mt_load(self, batch):
+        b, keep = batch_struct(batch)
+        self._check(lib().fmt_mt_load(self.h, ctypes.byref(b)))
+        self._mt_docs = batch.n_docs
+
+    def mt_run(self):
+        self._check(lib().fmt_mt_run(self.h))
+
+    def mt_headers(self) -> np.ndarray:
+        out = np.zeros(self._mt_docs, dtype=DOC_RESULT_DTYPE)
+        self._check(lib().fmt_mt_fetch_headers(self.h, _ptr(out)))
+        return out
+
+    def mt_doc(self, doc: int, hdr=None):
+        if hdr is None:
+            hdr = self.mt_headers()[doc]
+        nl, nc, npp = int(hdr["n_leaves"]), int(hdr["n_chars"]), int(hdr["n_props"])
+        leaves = np.zeros(max(nl, 1), dtype=LEAF_DTYPE)
+        chars = np.zeros(max(nc, 1), dtype="<u2")
+        props = np.zeros(max(npp, 1), dtype=PROPSET_DTYPE)
+        self._check(lib().fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
+        return leaves[:nl], chars[:nc], props[:npp]

@@ -1,0 +1,328 @@
+"""Host driver: pack sequenced Fluid messages into the engine's SoA op buffers.
+
+This is the batching half of the drop-in boundary. The reference handles one message at a time in
+`SharedObject.processMessages` (packages/dds/shared-object-base/src/sharedObject.ts:605-650) and
+flags that granularity itself as a performance problem (sharedObject.ts:411-413). Here a batch of
+documents' messages is packed once into the 32-byte `fmt_mt_op` / 16-byte `fmt_map_op` records of
+include/fmt.h plus a UTF-16 text arena and a props-op table, and crosses host→HBM in one copy.
+
+Semantics mirrored while packing:
+  - short client ids are interned per document in order of first appearance, the observer first,
+    a missing clientId is "server" (client.ts:831-855, getOrAddShortClientIdFromMessage);
+  - GROUP messages are flattened into member records that share the message's seq
+    (client.ts:1311-1319 applyRemoteOp GROUP branch; updateSeqNumbers runs once per message);
+  - annotate props keep JS object key order (array-index keys first, ascending) because
+    `Object.entries(op.props)` drives application order (segmentPropertiesManager.ts:80-88);
+  - values are re-serialized the way the summary does: JSON.stringify(JSON.parse(v)).
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# include/fmt.h fmt_mt_op (32 bytes)
+MT_OP_DTYPE = np.dtype(
+    [
+        ("seq", "<i4"),
+        ("ref_seq", "<i4"),
+        ("min_seq", "<i4"),
+        ("pos1", "<i4"),
+        ("pos2", "<i4"),
+        ("payload", "<u4"),
+        ("len", "<u2"),
+        ("client", "u1"),
+        ("type", "u1"),
+        ("reserved", "<u4"),
+    ]
+)
+assert MT_OP_DTYPE.itemsize == 32
+
+# include/fmt.h fmt_map_op (16 bytes)
+MAP_OP_DTYPE = np.dtype([("doc", "<u4"), ("key", "<u4"), ("seq", "<u4"), ("kind_value", "<u4")])
+assert MAP_OP_DTYPE.itemsize == 16
+
+MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
+MAP_SET, MAP_DELETE, MAP_CLEAR = 0, 1, 2
+MAP_KIND_SHIFT = 30
+MAP_VALUE_UNDEFINED = 0x3FFFFFFF
+MAP_ABSENT = 0xFFFFFFFF
+MAX_CLIENTS = 63  # short ids 1..63 (the observer is 0); remove-client sets are 64-bit masks
+
+
+class UnsupportedOp(NotImplementedError):
+    """An op kind outside the engine's current scope (FMT_E_UNSUPPORTED)."""
+
+
+def is_array_index_key(k: str) -> bool:
+    """CanonicalNumericIndexString for array indices (JS enumerates these keys first)."""
+    if not k or len(k) > 10 or (len(k) > 1 and k[0] == "0") or not k.isdigit():
+        return False
+    return int(k) < 4294967295
+
+
+def js_key_order(keys):
+    """OrdinaryOwnPropertyKeys order of a plain object built with `keys` in insertion order."""
+    idx = sorted((k for k in keys if is_array_index_key(k)), key=int)
+    return idx + [k for k in keys if not is_array_index_key(k)]
+
+
+def js_json(value) -> str:
+    """JSON.stringify for JSON-parsed values (ints, strings, bools, null, arrays, objects)."""
+    if isinstance(value, dict):
+        return "{" + ",".join(
+            json.dumps(k, ensure_ascii=False) + ":" + js_json(value[k]) for k in js_key_order(list(value))
+        ) + "}"
+    if isinstance(value, list):
+        return "[" + ",".join(js_json(v) for v in value) + "]"
+    if isinstance(value, bool) or value is None or isinstance(value, str):
+        return json.dumps(value, ensure_ascii=False)
+    if isinstance(value, int):
+        return str(value)
+    if isinstance(value, float):
+        if value.is_integer() and abs(value) < 1e21:
+            return str(int(value))
+        return repr(value)
+    raise TypeError(f"not a JSON value: {value!r}")
+
+
+def utf16(text: str) -> np.ndarray:
+    return np.frombuffer(text.encode("utf-16-le", "surrogatepass"), dtype="<u2")
+
+
+class Dictionary:
+    """Interns strings to dense ids (first come, first served)."""
+
+    def __init__(self, reserved=()):
+        self.items: list[str] = list(reserved)
+        self.ids: dict[str, int] = {s: i for i, s in enumerate(self.items)}
+
+    def intern(self, s: str) -> int:
+        i = self.ids.get(s)
+        if i is None:
+            i = len(self.items)
+            self.items.append(s)
+            self.ids[s] = i
+        return i
+
+
+@dataclass
+class MergeTreeBatch:
+    ops: np.ndarray          # MT_OP_DTYPE
+    doc_op_offsets: np.ndarray  # uint64, n_docs + 1
+    text: np.ndarray         # uint16 arena
+    doc_init: np.ndarray     # uint32 (n_docs, 2): initial text (offset, len)
+    props_off: np.ndarray    # uint32, n_props_ops + 1
+    props_kv: np.ndarray     # uint32 (key << 16) | value, value 0 = null
+    keys: list               # key id → key string
+    values: list             # value id → JSON text ("null" at id 0, meaning delete)
+    clients: list = field(default_factory=list)  # per doc: short id → long client id
+
+    @property
+    def n_docs(self) -> int:
+        return len(self.doc_op_offsets) - 1
+
+
+class _DocBuilder:
+    def __init__(self, owner: "MergeTreeStreamBuilder", observer: str):
+        self.owner = owner
+        self.client_ids = {observer: 0}
+        self.client_names = [observer]
+        self.ops: list[tuple] = []
+
+    @property
+    def n_ops(self) -> int:
+        return len(self.ops)
+
+    def short_client(self, long_id) -> int:
+        long_id = "server" if long_id is None else long_id
+        i = self.client_ids.get(long_id)
+        if i is None:
+            i = len(self.client_names)
+            if i > MAX_CLIENTS:
+                raise UnsupportedOp(f"more than {MAX_CLIENTS} clients in one document")
+            self.client_ids[long_id] = i
+            self.client_names.append(long_id)
+        return i
+
+    def add_message(self, msg: dict) -> None:
+        """Append one ISequencedDocumentMessage (type "op") with merge-tree contents."""
+        client = self.short_client(msg.get("clientId"))
+        seq = int(msg["sequenceNumber"])
+        ref = int(msg["referenceSequenceNumber"])
+        msn = int(msg["minimumSequenceNumber"])
+        contents = msg["contents"]
+        members = contents["ops"] if contents["type"] == MT_GROUP else [contents]
+        if not members:
+            members = [None]
+        for op in members:
+            self.ops.append(self.owner._pack(op, seq, ref, msn, client))
+
+    def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
+        self.ops.append(self.owner._pack(op, seq, ref_seq, min_seq, client))
+
+
+class MergeTreeStreamBuilder:
+    """Packs many documents' sequenced merge-tree messages into one MergeTreeBatch."""
+
+    def __init__(self):
+        self.keys = Dictionary()
+        self.values = Dictionary(["null"])
+        self.text: list[np.ndarray] = []
+        self.text_len = 0
+        self.props_ops: dict[tuple, int] = {}
+        self.props_list: list[tuple] = []
+        self.docs: list[_DocBuilder] = []
+        self.doc_init: list[tuple] = []
+
+    def _text(self, s: str) -> tuple:
+        u = utf16(s)
+        off = self.text_len
+        self.text.append(u)
+        self.text_len += len(u)
+        return off, len(u)
+
+    def _props_op(self, props: dict) -> int:
+        kv = []
+        for k in js_key_order(list(props)):
+            v = props[k]
+            key_id = self.keys.intern(k)
+            val_id = 0 if v is None else self.values.intern(js_json(v))
+            if key_id > 0xFFFF or val_id > 0xFFFF:
+                raise UnsupportedOp("props dictionary exceeds 65535 entries")
+            kv.append((key_id << 16) | val_id)
+        t = tuple(kv)
+        i = self.props_ops.get(t)
+        if i is None:
+            i = len(self.props_list)
+            self.props_ops[t] = i
+            self.props_list.append(t)
+        return i
+
+    def _pack(self, op, seq, ref, msn, client) -> tuple:
+        if op is None:  # empty group: only advances the collab window
+            return (seq, ref, msn, 0, 0, 0, 0, client, MT_REMOVE, 0)
+        t = op["type"]
+        if op.get("relativePos1") is not None or op.get("relativePos2") is not None:
+            raise UnsupportedOp("relative positions")
+        if t == MT_INSERT:
+            seg = op["seg"]
+            if not isinstance(seg, str):
+                if isinstance(seg, dict) and "text" in seg and not seg.get("props"):
+                    seg = seg["text"]
+                else:
+                    raise UnsupportedOp("insert of markers or pre-annotated segments")
+            off, n = self._text(seg)
+            if n > 0xFFFF:
+                raise UnsupportedOp("insert longer than 65535 UTF-16 units")
+            return (seq, ref, msn, int(op["pos1"]), -1, off, n, client, MT_INSERT, 0)
+        if t == MT_REMOVE:
+            return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_REMOVE, 0)
+        if t == MT_ANNOTATE:
+            if op.get("adjust") is not None:
+                raise UnsupportedOp("annotate adjust")
+            pid = self._props_op(op.get("props") or {})
+            return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), pid, 0, client, MT_ANNOTATE, 0)
+        raise UnsupportedOp(f"merge-tree op type {t}")
+
+    def begin_doc(self, initial_text: str = "", observer: str = "A") -> _DocBuilder:
+        d = _DocBuilder(self, observer)
+        self.docs.append(d)
+        self.doc_init.append(self._text(initial_text) if initial_text else (0, 0))
+        return d
+
+    def finish(self) -> MergeTreeBatch:
+        n = sum(d.n_ops for d in self.docs)
+        ops = np.zeros(n, dtype=MT_OP_DTYPE)
+        offs = np.zeros(len(self.docs) + 1, dtype=np.uint64)
+        i = 0
+        for di, d in enumerate(self.docs):
+            if d.ops:
+                ops[i : i + d.n_ops] = np.array(d.ops, dtype=MT_OP_DTYPE)
+            i += d.n_ops
+            offs[di + 1] = i
+        text = np.concatenate(self.text) if self.text else np.zeros(0, dtype="<u2")
+        props_off = np.zeros(len(self.props_list) + 1, dtype=np.uint32)
+        kv = []
+        for j, t in enumerate(self.props_list):
+            kv.extend(t)
+            props_off[j + 1] = len(kv)
+        return MergeTreeBatch(
+            ops=ops,
+            doc_op_offsets=offs,
+            text=np.ascontiguousarray(text, dtype="<u2"),
+            doc_init=np.asarray(self.doc_init, dtype=np.uint32).reshape(-1, 2),
+            props_off=props_off,
+            props_kv=np.asarray(kv, dtype=np.uint32),
+            keys=list(self.keys.items),
+            values=list(self.values.items),
+            clients=[list(d.client_names) for d in self.docs],
+        )
+
+
+@dataclass
+class MapBatch:
+    ops: np.ndarray             # MAP_OP_DTYPE
+    doc_op_offsets: np.ndarray  # uint64, n_docs + 1
+    key_bound: int
+    keys: list                  # key id → key string
+    values: list                # value id → JSON text
+
+    @property
+    def n_docs(self) -> int:
+        return len(self.doc_op_offsets) - 1
+
+
+class MapStreamBuilder:
+    """Packs SharedMap messages ({"type":"set"|"delete"|"clear", ...}) per document."""
+
+    def __init__(self):
+        self.keys = Dictionary()
+        self.values = Dictionary()
+        self.docs: list[list[tuple]] = []
+
+    def begin_doc(self) -> int:
+        self.docs.append([])
+        return len(self.docs) - 1
+
+    def add_message(self, doc: int, seq: int, contents: dict) -> None:
+        t = contents["type"]
+        if t == "clear":
+            self.docs[doc].append((doc, 0, seq, MAP_CLEAR << MAP_KIND_SHIFT))
+            return
+        key = self.keys.intern(contents["key"])
+        if t == "delete":
+            self.docs[doc].append((doc, key, seq, (MAP_DELETE << MAP_KIND_SHIFT)))
+        elif t == "set":
+            sv = contents["value"]
+            if sv.get("type") != "Plain":
+                raise UnsupportedOp("legacy Shared value type")
+            if "value" in sv and sv["value"] is not _MISSING:
+                vid = self.values.intern(js_json(sv["value"]))
+                if vid >= MAP_VALUE_UNDEFINED:
+                    raise UnsupportedOp("value dictionary overflow")
+            else:
+                vid = MAP_VALUE_UNDEFINED
+            self.docs[doc].append((doc, key, seq, (MAP_SET << MAP_KIND_SHIFT) | vid))
+        else:
+            raise UnsupportedOp(f"map op type {t}")
+
+    def finish(self) -> MapBatch:
+        n = sum(len(d) for d in self.docs)
+        ops = np.zeros(n, dtype=MAP_OP_DTYPE)
+        offs = np.zeros(len(self.docs) + 1, dtype=np.uint64)
+        i = 0
+        for di, d in enumerate(self.docs):
+            if d:
+                ops[i : i + len(d)] = np.array(d, dtype=MAP_OP_DTYPE)
+            i += len(d)
+            offs[di + 1] = i
+        return MapBatch(ops, offs, max(1, len(self.keys.items)), list(self.keys.items), list(self.values.items))
+
+
+class _Missing:
+    pass
+
+
+_MISSING = _Missing()

@@ -1,0 +1,223 @@
+/*
+ * fmt.h — C ABI of the MI355X batch merge engine ("fmt" = Fluid merge tree).
+ *
+ * The engine replays already-sequenced op streams for very many independent documents and
+ * produces their converged DDS state. It is the drop-in for the data-parallel hot path that the
+ * reference runs one message at a time through
+ *
+ *   SharedObjectCore.processMessagesCore            packages/dds/shared-object-base/src/sharedObject.ts:415
+ *     SharedMap.processMessagesCore                 packages/dds/map/src/map.ts:288-311
+ *       MapKernel.tryProcessMessage                 packages/dds/map/src/mapKernel.ts:619-630
+ *     SharedSegmentSequence.processMessagesCore     packages/dds/sequence/src/sequence.ts:873-919
+ *       Client.applyMsg                             packages/dds/merge-tree/src/client.ts:1358-1379
+ *   summarizeCore                                   map.ts:176-246, sequence.ts:713-728
+ *
+ * Conventions (all entry points):
+ *   - return 0 (FMT_OK) on success, a negative FMT_E_* code on failure; fmt_last_error() explains.
+ *   - FMT_E_DATA is the DataProcessingError analogue (bad remote data, mergeTree.ts:1629-1638),
+ *     FMT_E_USAGE the UsageError analogue (API misuse). Per-document failures are also reported in
+ *     that document's result status word; the first failing (doc, seq) is recorded in the context.
+ *   - Inputs are caller-owned and only read during the call. Device state is library-owned until
+ *     fmt_close(). No exception ever crosses this ABI. One context per host thread.
+ *   - Positions and lengths are UTF-16 code units (textSegment.ts:60), exactly like JS strings.
+ */
+#ifndef FMT_H_
+#define FMT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------------------
+ * Status codes
+ * ------------------------------------------------------------------------------------------- */
+#define FMT_OK 0
+#define FMT_E_USAGE (-1)       /* misuse: bad argument, wrong call order (UsageError analogue) */
+#define FMT_E_DATA (-2)        /* invalid op stream (DataProcessingError analogue) */
+#define FMT_E_CAPACITY (-3)    /* a document exceeded a per-document engine capacity */
+#define FMT_E_DEVICE (-4)      /* HIP runtime failure, or no usable gfx950 device */
+#define FMT_E_UNSUPPORTED (-5) /* op kind this engine build does not implement (e.g. obliterate) */
+
+/* ---------------------------------------------------------------------------------------------
+ * Constants mirrored from the reference
+ * ------------------------------------------------------------------------------------------- */
+/* MergeTreeDeltaType, packages/dds/merge-tree/src/ops.ts:61-71 */
+#define FMT_MT_INSERT 0
+#define FMT_MT_REMOVE 1
+#define FMT_MT_ANNOTATE 2
+#define FMT_MT_GROUP 3 /* never appears in a packed stream: group members are flattened, same seq */
+#define FMT_MT_OBLITERATE 4
+#define FMT_MT_OBLITERATE_SIDED 5
+
+/* stamps.ts / constants.ts:14-42 */
+#define FMT_UNIVERSAL_SEQ 0
+#define FMT_LOCAL_CLIENT (-1)
+#define FMT_NON_COLLAB_CLIENT (-2)
+#define FMT_NOT_REMOVED 0x7fffffff
+
+/* Map op kinds (mapKernel.ts:706-853 handlers "set" / "delete" / "clear") */
+#define FMT_MAP_SET 0u
+#define FMT_MAP_DELETE 1u
+#define FMT_MAP_CLEAR 2u
+#define FMT_MAP_KIND_SHIFT 30
+#define FMT_MAP_VALUE_MASK 0x3fffffffu
+#define FMT_MAP_VALUE_UNDEFINED 0x3fffffffu /* map.set(key, undefined): summary omits "value" */
+#define FMT_MAP_ABSENT 0xffffffffu          /* result slot: key not live */
+
+/* ---------------------------------------------------------------------------------------------
+ * Packed op records (host driver output, the bytes that cross host→HBM once per batch)
+ * ------------------------------------------------------------------------------------------- */
+
+/* One sequenced merge-tree message (ISequencedDocumentMessage, driver-definitions protocol.ts:217,
+ * with contents IMergeTreeInsertMsg / IMergeTreeRemoveMsg / IMergeTreeAnnotateMsg, ops.ts:112-235).
+ * A GROUP message is flattened into consecutive records carrying the same seq; the collab window
+ * is advanced once after the last member (client.ts:1358-1379). 32 bytes, naturally aligned. */
+typedef struct fmt_mt_op {
+  int32_t seq;      /* sequenceNumber */
+  int32_t ref_seq;  /* referenceSequenceNumber */
+  int32_t min_seq;  /* minimumSequenceNumber */
+  int32_t pos1;     /* op.pos1 */
+  int32_t pos2;     /* op.pos2, or -1 for insert */
+  uint32_t payload; /* INSERT: offset of the text in the UTF-16 arena; ANNOTATE: props-op id */
+  uint16_t len;     /* INSERT: text length in UTF-16 units (> 0) */
+  uint8_t client;   /* short client id (client.ts:831-855): 1..63 in order of first appearance */
+  uint8_t type;     /* FMT_MT_* */
+  uint32_t reserved;
+} fmt_mt_op;
+
+/* One SharedMap message: {"type":"set","key","value"} / "delete" / "clear"
+ * (map/src/internalInterfaces.ts). 16 bytes. key = per-doc key id (< key_bound); value = id of the
+ * value's serialized JSON text in the host dictionary. */
+typedef struct fmt_map_op {
+  uint32_t doc;
+  uint32_t key;
+  uint32_t seq;
+  uint32_t kind_value; /* (kind << 30) | value id */
+} fmt_map_op;
+
+/* A batch of merge-tree documents. Pointers are HOST pointers for fmt_mt_load(). */
+typedef struct fmt_mt_batch {
+  const fmt_mt_op* ops;           /* all ops, documents contiguous and in seq order */
+  uint64_t n_ops;
+  const uint64_t* doc_op_offsets; /* n_docs + 1 entries */
+  uint32_t n_docs;
+  const uint16_t* text;           /* UTF-16 arena for insert payloads and initial texts */
+  uint64_t text_len;
+  const uint32_t* doc_init;       /* optional: per doc (offset, len) of the initial text inserted
+                                     before collaboration starts (client.replay.spec.ts:30-33), or NULL */
+  const uint32_t* props_off;      /* annotate props-op table: n_props_ops + 1 offsets into props_kv */
+  uint32_t n_props_ops;
+  const uint32_t* props_kv;       /* (key_id << 16) | value_id; value_id 0 = null (delete key) */
+} fmt_mt_batch;
+
+/* ---------------------------------------------------------------------------------------------
+ * Results
+ * ------------------------------------------------------------------------------------------- */
+
+/* One merge-tree leaf (segment) of the converged tree, in document order, tombstones included. */
+typedef struct fmt_mt_leaf {
+  int32_t ins_seq;     /* insert stamp seq */
+  int32_t rm_seq;      /* first (lowest) remove stamp seq, FMT_NOT_REMOVED if not removed */
+  uint64_t rm_clients; /* set of short client ids holding a remove stamp on this leaf */
+  uint32_t char_off;   /* offset of this leaf's text in the document's char output */
+  uint16_t len;        /* cachedLength (UTF-16 units) */
+  int16_t ins_client;  /* insert stamp client */
+  uint16_t props;      /* document-local prop-set id, 0xffff = properties undefined */
+  uint16_t block;      /* index of the leaf's parent block in document order of leaf blocks */
+  uint32_t pad;
+} fmt_mt_leaf;
+
+/* Per-document result header. */
+typedef struct fmt_mt_doc_result {
+  int32_t status;      /* FMT_OK or FMT_E_* */
+  int32_t fail_seq;    /* seq of the op that failed, when status != FMT_OK */
+  int32_t cur_seq;     /* collabWindow.currentSeq */
+  int32_t min_seq;     /* collabWindow.minSeq */
+  uint32_t n_leaves;
+  uint32_t n_chars;    /* total chars of all leaves (tombstones included) */
+  uint32_t n_props;    /* number of document-local prop sets */
+  uint32_t n_blocks;   /* number of leaf blocks */
+  uint32_t depth;      /* tree depth (1 = root holds leaves) */
+  uint32_t visible_len;/* getLength() from the local perspective */
+  uint32_t pad[2];
+} fmt_mt_doc_result;
+
+/* A document-local prop set: up to FMT_MT_PROPS_MAX (key_id, value_id) pairs in JS insertion order. */
+#define FMT_MT_PROPS_MAX 4
+typedef struct fmt_mt_propset {
+  uint32_t n;
+  uint32_t kv[FMT_MT_PROPS_MAX]; /* (key_id << 16) | value_id */
+} fmt_mt_propset;
+
+/* One SharedMap result slot (per doc, per key id < key_bound). */
+typedef struct fmt_map_slot {
+  uint32_t value;     /* value id, FMT_MAP_VALUE_UNDEFINED, or FMT_MAP_ABSENT (not live) */
+  uint32_t birth_seq; /* seq of the set that created the live entry (JS Map insertion order) */
+} fmt_map_slot;
+
+/* Run statistics of the last fmt_*_run (device time measured with HIP events on the ctx stream). */
+typedef struct fmt_stats {
+  double kernel_ms;      /* replay kernel(s) only */
+  double total_ms;       /* everything launched by the run call */
+  uint64_t ops;          /* messages applied */
+  uint64_t docs;
+  uint64_t bytes_read;   /* algorithmic bytes read by the replay kernel */
+  uint64_t bytes_written;/* algorithmic bytes written by the replay kernel */
+  uint64_t launches;     /* kernel launches issued by the run call */
+} fmt_stats;
+
+/* ---------------------------------------------------------------------------------------------
+ * Context
+ * ------------------------------------------------------------------------------------------- */
+typedef struct fmt_ctx fmt_ctx;
+
+typedef struct fmt_config {
+  int32_t device;      /* HIP device ordinal */
+  uint32_t flags;      /* reserved, 0 */
+  void* stream;        /* hipStream_t to launch on (e.g. torch's current stream); NULL = own stream */
+  uint32_t reserved[4];
+} fmt_config;
+
+int fmt_open(const fmt_config* cfg, fmt_ctx** out);
+void fmt_close(fmt_ctx* ctx);
+const char* fmt_last_error(const fmt_ctx* ctx);
+int fmt_sync(fmt_ctx* ctx);
+int fmt_get_stats(const fmt_ctx* ctx, fmt_stats* out);
+/* Name of the gfx target the library was built for and the device it runs on (diagnostics). */
+int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
+
+/* ---------------------------------------------------------------------------------------------
+ * SharedMap last-writer-wins (MapKernel sequenced path, mapKernel.ts:706-853)
+ * ------------------------------------------------------------------------------------------- */
+/* Stage a batch into HBM (the one host→device crossing). ops of document d are
+ * ops[doc_op_offsets[d] .. doc_op_offsets[d+1]) in seq order; key ids < key_bound. */
+int fmt_map_load(fmt_ctx* ctx, const fmt_map_op* ops, uint64_t n_ops,
+                 const uint64_t* doc_op_offsets, uint32_t n_docs, uint32_t key_bound);
+/* Replay the staged batch (asynchronous on the ctx stream). */
+int fmt_map_run(fmt_ctx* ctx);
+/* Copy results to host: out[d * key_bound + k]. Synchronizes the ctx stream. */
+int fmt_map_fetch(fmt_ctx* ctx, fmt_map_slot* out);
+/* Zero-copy variant on caller-owned DEVICE buffers (e.g. torch tensors), launched on the ctx stream. */
+int fmt_map_replay_device(fmt_ctx* ctx, const fmt_map_op* d_ops, const uint64_t* d_doc_op_offsets,
+                          uint32_t n_docs, uint32_t key_bound, fmt_map_slot* d_out);
+
+/* ---------------------------------------------------------------------------------------------
+ * merge-tree / SharedString (Client.applyMsg observer path + zamboni, client.ts:1358-1391)
+ * ------------------------------------------------------------------------------------------- */
+int fmt_mt_load(fmt_ctx* ctx, const fmt_mt_batch* batch);
+int fmt_mt_run(fmt_ctx* ctx);
+/* Per-document result headers for all docs (n_docs entries). Synchronizes the ctx stream. */
+int fmt_mt_fetch_headers(fmt_ctx* ctx, fmt_mt_doc_result* out);
+/* One document's leaves (cap_leaves), chars (cap_chars) and prop sets (cap_props). */
+int fmt_mt_fetch_doc(fmt_ctx* ctx, uint32_t doc, fmt_mt_leaf* leaves, uint32_t cap_leaves,
+                     uint16_t* chars, uint32_t cap_chars, fmt_mt_propset* props, uint32_t cap_props);
+/* Per-document capacities of this engine build (leaves, chars, prop sets). */
+int fmt_mt_capacity(uint32_t* max_leaves, uint32_t* max_chars, uint32_t* max_props);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMT_H_ */

@@ -1,0 +1,298 @@
+// oracle/capi.cpp — TEST INFRASTRUCTURE ONLY: extern "C" surface of the parity oracle for ctypes.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+// Result layouts are the product's (include/fmt.h) so tests compare GPU and oracle field by field.
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+#include "map.hpp"
+#include "mergetree.hpp"
+
+using orc::MergeTree;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* what) {
+  g_err = what;
+  return FMT_E_DATA;
+}
+
+// Applies ops[0..n): consecutive records with the same seq form one message.
+int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* arena,
+             const uint32_t* propsOff, const uint32_t* propsKv, int32_t* failSeq) {
+  for (uint64_t i = 0; i < n; i++) {
+    const fmt_mt_op& op = ops[i];
+    try {
+      mt->applyRemote(op, arena, propsOff, propsKv);
+      if (i + 1 == n || ops[i + 1].seq != op.seq) mt->updateSeqNumbers(op.min_seq, op.seq);
+    } catch (const std::exception& e) {
+      if (failSeq) *failSeq = op.seq;
+      return fail(e.what());
+    }
+  }
+  return FMT_OK;
+}
+
+void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint32_t capLeaves,
+             uint16_t* chars, uint32_t capChars, fmt_mt_propset* props, uint32_t capProps) {
+  std::vector<const orc::Seg*> segs;
+  std::vector<int> blockOf;
+  int nBlocks = 0, depth = 0;
+  mt->collectLeaves(segs, blockOf, &nBlocks, &depth);
+  std::vector<const orc::PropMap*> sets;
+  uint32_t charOff = 0;
+  for (size_t i = 0; i < segs.size(); i++) {
+    const orc::Seg* s = segs[i];
+    uint16_t pid = 0xffff;
+    if (s->props.defined) {
+      size_t j = 0;
+      for (; j < sets.size(); j++)
+        if (sets[j]->kv == s->props.kv) break;
+      if (j == sets.size()) sets.push_back(&s->props);
+      pid = static_cast<uint16_t>(j);
+    }
+    if (leaves && i < capLeaves) {
+      fmt_mt_leaf& L = leaves[i];
+      std::memset(&L, 0, sizeof(L));
+      L.ins_seq = s->ins.seq;
+      L.ins_client = static_cast<int16_t>(s->ins.client);
+      L.rm_seq = s->removed() ? s->removes[0].seq : FMT_NOT_REMOVED;
+      uint64_t mask = 0;
+      for (const auto& r : s->removes)
+        if (r.client >= 0 && r.client < 64) mask |= 1ull << r.client;
+      L.rm_clients = mask;
+      L.char_off = charOff;
+      L.len = static_cast<uint16_t>(s->len());
+      L.props = pid;
+      L.block = static_cast<uint16_t>(blockOf[i]);
+    }
+    for (int k = 0; k < s->len(); k++) {
+      if (chars && charOff + k < capChars) chars[charOff + k] = static_cast<uint16_t>(s->text[k]);
+    }
+    charOff += static_cast<uint32_t>(s->len());
+  }
+  if (props) {
+    for (size_t j = 0; j < sets.size() && j < capProps; j++) {
+      std::memset(&props[j], 0, sizeof(props[j]));
+      props[j].n = static_cast<uint32_t>(sets[j]->kv.size());
+      for (size_t k = 0; k < sets[j]->kv.size() && k < FMT_MT_PROPS_MAX; k++)
+        props[j].kv[k] = (static_cast<uint32_t>(sets[j]->kv[k].first) << 16) | sets[j]->kv[k].second;
+    }
+  }
+  if (hdr) {
+    hdr->cur_seq = mt->currentSeq;
+    hdr->min_seq = mt->minSeq;
+    hdr->n_leaves = static_cast<uint32_t>(segs.size());
+    hdr->n_chars = charOff;
+    hdr->n_props = static_cast<uint32_t>(sets.size());
+    hdr->n_blocks = static_cast<uint32_t>(nBlocks);
+    hdr->depth = static_cast<uint32_t>(depth);
+    hdr->visible_len = static_cast<uint32_t>(mt->getLocalLength());
+  }
+}
+
+template <class F>
+void parallelFor(uint32_t begin, uint32_t end, uint32_t nThreads, F&& fn) {
+  if (nThreads <= 1 || end - begin <= 1) {
+    for (uint32_t d = begin; d < end; d++) fn(d);
+    return;
+  }
+  std::atomic<uint32_t> next{begin};
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < nThreads; t++) {
+    pool.emplace_back([&] {
+      for (uint32_t d = next.fetch_add(1); d < end; d = next.fetch_add(1)) fn(d);
+    });
+  }
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* orc_last_error() { return g_err.c_str(); }
+
+// ---------------------------------------------------------------- merge-tree, one document
+void* orc_mt_new() { return new MergeTree(); }
+void orc_mt_free(void* h) { delete static_cast<MergeTree*>(h); }
+
+int orc_mt_insert_local(void* h, int pos, const uint16_t* text, int len) {
+  try {
+    static_cast<MergeTree*>(h)->insertLocal(pos, std::u16string(reinterpret_cast<const char16_t*>(text), len));
+  } catch (const std::exception& e) {
+    return fail(e.what());
+  }
+  return FMT_OK;
+}
+
+int orc_mt_annotate_local(void* h, int start, int end, const uint32_t* kv, int n) {
+  std::vector<std::pair<uint16_t, uint16_t>> props;
+  for (int i = 0; i < n; i++) props.emplace_back(kv[i] >> 16, kv[i] & 0xffff);
+  try {
+    static_cast<MergeTree*>(h)->annotateLocal(start, end, props);
+  } catch (const std::exception& e) {
+    return fail(e.what());
+  }
+  return FMT_OK;
+}
+
+int orc_mt_remove_local(void* h, int start, int end) {
+  try {
+    static_cast<MergeTree*>(h)->removeLocal(start, end);
+  } catch (const std::exception& e) {
+    return fail(e.what());
+  }
+  return FMT_OK;
+}
+
+int orc_mt_start_collab(void* h, int client) {
+  static_cast<MergeTree*>(h)->startCollaboration(client, 0, 0);
+  return FMT_OK;
+}
+
+int orc_mt_apply_ops(void* h, const fmt_mt_op* ops, uint64_t n, const uint16_t* arena,
+                     const uint32_t* propsOff, const uint32_t* propsKv) {
+  return applyOps(static_cast<MergeTree*>(h), ops, n, arena, propsOff, propsKv, nullptr);
+}
+
+// Returns the text length; copies min(len, cap) UTF-16 units.
+int orc_mt_text(void* h, uint16_t* buf, int cap) {
+  const std::u16string t = static_cast<MergeTree*>(h)->getText();
+  for (int i = 0; i < static_cast<int>(t.size()) && i < cap; i++) buf[i] = static_cast<uint16_t>(t[i]);
+  return static_cast<int>(t.size());
+}
+
+int orc_mt_dump(void* h, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint32_t capLeaves,
+                uint16_t* chars, uint32_t capChars, fmt_mt_propset* props, uint32_t capProps) {
+  dumpDoc(static_cast<MergeTree*>(h), hdr, leaves, capLeaves, chars, capChars, props, capProps);
+  return FMT_OK;
+}
+
+// Legacy summary blobs (header, then body); returns the byte count needed for header+body.
+int orc_mt_summary(void* h, const char* const* keys, int nKeys, const char* const* values,
+                   int nValues, int chunkSize, char* out, int cap, int* headerLen, int* bodyLen) {
+  std::vector<std::string> k(keys, keys + nKeys), v(values, values + nValues);
+  orc::Summary s = static_cast<MergeTree*>(h)->summarize(k, v, chunkSize);
+  *headerLen = static_cast<int>(s.header.size());
+  *bodyLen = static_cast<int>(s.body.size());
+  const std::string all = s.header + s.body;
+  if (out) std::memcpy(out, all.data(), std::min<size_t>(all.size(), static_cast<size_t>(cap)));
+  return static_cast<int>(all.size());
+}
+
+// ---------------------------------------------------------------- merge-tree, batch replay
+// Replays documents [docBegin, docEnd) of a batch with nThreads host threads (one doc per task).
+// Output arrays are indexed by (doc - docBegin) with the given per-doc strides; any may be NULL.
+int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEnd,
+                        uint32_t nThreads, fmt_mt_doc_result* hdrs, fmt_mt_leaf* leaves,
+                        uint32_t capLeaves, uint16_t* chars, uint32_t capChars,
+                        fmt_mt_propset* props, uint32_t capProps, double* seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::atomic<int> status{FMT_OK};
+  parallelFor(docBegin, docEnd, nThreads, [&](uint32_t d) {
+    MergeTree mt;
+    const size_t i = d - docBegin;
+    int32_t failSeq = 0;
+    int st = FMT_OK;
+    if (b->doc_init != nullptr && b->doc_init[2 * d + 1] > 0) {
+      const uint32_t off = b->doc_init[2 * d], len = b->doc_init[2 * d + 1];
+      mt.insertLocal(0, std::u16string(reinterpret_cast<const char16_t*>(b->text + off), len));
+    }
+    mt.startCollaboration(0, 0, 0);
+    const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
+    st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq);
+    if (st != FMT_OK) status = st;
+    fmt_mt_doc_result* h = hdrs ? &hdrs[i] : nullptr;
+    if (h) std::memset(h, 0, sizeof(*h));
+    if (hdrs || leaves || chars || props) {
+      dumpDoc(&mt, h, leaves ? leaves + i * capLeaves : nullptr, capLeaves,
+              chars ? chars + i * static_cast<size_t>(capChars) : nullptr, capChars,
+              props ? props + i * capProps : nullptr, capProps);
+    }
+    if (h) {
+      h->status = st;
+      h->fail_seq = failSeq;
+    }
+  });
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return status.load();
+}
+
+// ---------------------------------------------------------------- SharedMap
+int orc_map_replay(const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, uint32_t keyBound,
+                   fmt_map_slot* out, uint32_t nThreads, double* seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::atomic<int> status{FMT_OK};
+  parallelFor(0, nDocs, nThreads, [&](uint32_t d) {
+    orc::MapState m(keyBound);
+    for (uint64_t i = offs[d]; i < offs[d + 1]; i++) {
+      const fmt_map_op& op = ops[i];
+      const uint32_t kind = op.kind_value >> FMT_MAP_KIND_SHIFT;
+      if (kind == FMT_MAP_CLEAR) {
+        m.clear();
+      } else if (op.key >= keyBound) {
+        status = FMT_E_DATA;
+      } else if (kind == FMT_MAP_DELETE) {
+        m.del(op.key);
+      } else {
+        m.set(op.key, op.kind_value & FMT_MAP_VALUE_MASK, op.seq);
+      }
+    }
+    if (out) m.toSlots(out + static_cast<size_t>(d) * keyBound, keyBound);
+  });
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return status.load();
+}
+
+// Summary of one document: header then each blobN, NUL-separated; returns bytes needed.
+int orc_map_summary(const fmt_map_op* ops, uint64_t begin, uint64_t end, uint32_t keyBound,
+                    const char* const* keys, int nKeys, const char* const* values, int nValues,
+                    char* out, int cap, int* nBlobs) {
+  orc::MapState m(keyBound);
+  for (uint64_t i = begin; i < end; i++) {
+    const uint32_t kind = ops[i].kind_value >> FMT_MAP_KIND_SHIFT;
+    if (kind == FMT_MAP_CLEAR) m.clear();
+    else if (kind == FMT_MAP_DELETE) m.del(ops[i].key);
+    else m.set(ops[i].key, ops[i].kind_value & FMT_MAP_VALUE_MASK, ops[i].seq);
+  }
+  std::vector<std::string> k(keys, keys + nKeys), v(values, values + nValues);
+  orc::MapSummary s = orc::summarizeMap(m.entries(), k, v);
+  std::string all = s.header;
+  all.push_back('\0');
+  for (auto& bl : s.blobs) {
+    all += bl;
+    all.push_back('\0');
+  }
+  *nBlobs = static_cast<int>(s.blobs.size());
+  if (out) std::memcpy(out, all.data(), std::min<size_t>(all.size(), static_cast<size_t>(cap)));
+  return static_cast<int>(all.size());
+}
+
+// ---------------------------------------------------------------- PRNG known answers
+void orc_xsadd_uint32(const uint32_t* seed, int nSeed, uint32_t* out, int n) {
+  orc::XSadd x(std::vector<uint32_t>(seed, seed + nSeed));
+  for (int i = 0; i < n; i++) out[i] = x.uint32();
+}
+
+// kind 0: float64, 1: uint32 (as double), 2: uint53 — one call per sample in the given order.
+void orc_xsadd_mixed(const uint32_t* seed, int nSeed, const int* kinds, double* out, int n) {
+  orc::XSadd x(std::vector<uint32_t>(seed, seed + nSeed));
+  for (int i = 0; i < n; i++) {
+    switch (kinds[i]) {
+      case 0: out[i] = x.float64(); break;
+      case 1: out[i] = static_cast<double>(x.uint32()); break;
+      default: out[i] = x.uint53(); break;
+    }
+  }
+}
+
+}  // extern "C"

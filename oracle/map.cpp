@@ -1,0 +1,146 @@
+// oracle/map.cpp — TEST INFRASTRUCTURE ONLY. See map.hpp.
+#include "map.hpp"
+
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace orc {
+
+void MapState::set(uint32_t key, uint32_t value, uint32_t seq) {
+  const int s = slot_.at(key);
+  if (s >= 0 && items_[static_cast<size_t>(s)].live) {
+    items_[static_cast<size_t>(s)].value = value;  // existing key keeps its position
+    return;
+  }
+  slot_[key] = static_cast<int>(items_.size());
+  items_.push_back({key, value, seq, true});
+}
+
+void MapState::del(uint32_t key) {
+  const int s = slot_.at(key);
+  if (s >= 0) items_[static_cast<size_t>(s)].live = false;
+  slot_[key] = -1;
+}
+
+void MapState::clear() {
+  for (auto& it : items_) {
+    if (it.live) slot_[it.key] = -1;
+    it.live = false;
+  }
+  items_.clear();
+}
+
+std::vector<MapState::Entry> MapState::entries() const {
+  std::vector<Entry> out;
+  for (const auto& it : items_)
+    if (it.live) out.push_back({it.key, it.value, it.birth});
+  return out;
+}
+
+void MapState::toSlots(fmt_map_slot* out, uint32_t keyBound) const {
+  for (uint32_t k = 0; k < keyBound; k++) out[k] = {FMT_MAP_ABSENT, 0};
+  for (const auto& it : items_)
+    if (it.live) out[it.key] = {it.value, it.birth};
+}
+
+// String.prototype.length of a UTF-8 encoded text (UTF-16 code units).
+static size_t utf16Length(const std::string& s) {
+  size_t n = 0;
+  for (size_t i = 0; i < s.size(); i++) {
+    const unsigned char c = static_cast<unsigned char>(s[i]);
+    if ((c & 0xC0) == 0x80) continue;  // continuation byte
+    n += (c >= 0xF0) ? 2 : 1;
+  }
+  return n;
+}
+
+// JSON.stringify of {key: {"type":"Plain","value":<v>}} members in JS key order.
+static void appendMember(std::string& out, bool& first, const std::string& key,
+                         const std::string* value) {
+  if (!first) out.push_back(',');
+  first = false;
+  jsonQuoteUtf8(out, key);
+  out += ":{\"type\":\"Plain\"";
+  if (value != nullptr) {
+    out += ",\"value\":";
+    out += *value;
+  }
+  out.push_back('}');
+}
+
+static std::vector<size_t> jsKeyOrder(const std::vector<MapState::Entry>& entries,
+                                      const std::vector<std::string>& keyNames) {
+  std::vector<std::pair<uint64_t, size_t>> idx;
+  std::vector<size_t> rest;
+  for (size_t i = 0; i < entries.size(); i++) {
+    uint64_t v;
+    if (isArrayIndexKey(keyNames.at(entries[i].key), &v)) idx.emplace_back(v, i);
+    else rest.push_back(i);
+  }
+  std::sort(idx.begin(), idx.end());
+  std::vector<size_t> order;
+  for (auto& e : idx) order.push_back(e.second);
+  for (size_t i : rest) order.push_back(i);
+  return order;
+}
+
+MapSummary summarizeMap(const std::vector<MapState::Entry>& entries,
+                        const std::vector<std::string>& keyNames,
+                        const std::vector<std::string>& valueJson) {
+  constexpr size_t kSeparateBlob = 8 * 1024;   // map.ts:190
+  constexpr size_t kMaxBlob = 16 * 1024;       // map.ts:194
+  const std::string kType = "Plain";
+  MapSummary out;
+  // getSerializedStorage iterates sequencedData (insertion order) into a plain object, so the
+  // object — and everything derived from Object.entries(data) — enumerates array-index keys first.
+  const std::vector<size_t> order = jsKeyOrder(entries, keyNames);
+  std::vector<size_t> headerMembers;
+  size_t currentSize = 0;
+  auto flushHeader = [&](const std::vector<size_t>& members) {
+    std::string j = "{";
+    bool first = true;
+    std::vector<MapState::Entry> sub;
+    for (size_t i : members) sub.push_back(entries[i]);
+    for (size_t k : jsKeyOrder(sub, keyNames)) {
+      const auto& e = sub[k];
+      const std::string* v = e.value == FMT_MAP_VALUE_UNDEFINED ? nullptr : &valueJson.at(e.value);
+      appendMember(j, first, keyNames.at(e.key), v);
+    }
+    j.push_back('}');
+    return j;
+  };
+  for (size_t i : order) {
+    const auto& e = entries[i];
+    const bool undef = e.value == FMT_MAP_VALUE_UNDEFINED;
+    const size_t vlen = undef ? 0 : utf16Length(valueJson.at(e.value));
+    if (!undef && vlen >= kSeparateBlob) {
+      std::string j = "{";
+      bool first = true;
+      appendMember(j, first, keyNames.at(e.key), &valueJson.at(e.value));
+      j.push_back('}');
+      out.blobs.push_back(j);
+    } else {
+      currentSize += kType.size() + 21;
+      currentSize += vlen;
+      if (currentSize > kMaxBlob) {
+        out.blobs.push_back(flushHeader(headerMembers));
+        headerMembers.clear();
+        currentSize = 0;
+      }
+      headerMembers.push_back(i);
+    }
+  }
+  std::string h = "{\"blobs\":[";
+  for (size_t b = 0; b < out.blobs.size(); b++) {
+    if (b) h.push_back(',');
+    h += "\"blob" + std::to_string(b) + "\"";
+  }
+  h += "],\"content\":";
+  h += flushHeader(headerMembers);
+  h.push_back('}');
+  out.header = h;
+  return out;
+}
+
+}  // namespace orc

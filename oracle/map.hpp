@@ -1,0 +1,52 @@
+// oracle/map.hpp — TEST INFRASTRUCTURE ONLY (parity oracle for the SharedMap LWW path).
+//
+// Restates the sequenced (remote) path of MapKernel (packages/dds/map/src/mapKernel.ts:706-853)
+// with the JS Map semantics it relies on, and SharedMap.summarizeCore (map.ts:176-246).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../include/fmt.h"
+
+namespace orc {
+
+// JS Map<string, value> restricted to the operations MapKernel uses: set keeps the position of an
+// existing key, delete/clear drop it, a later set re-appends it (ECMAScript Map insertion order).
+class MapState {
+ public:
+  explicit MapState(uint32_t keyBound) : slot_(keyBound, -1) {}
+  // mapKernel.ts:802-850 "set" remote branch: sequencedData.set(key, {value}).
+  void set(uint32_t key, uint32_t value, uint32_t seq);
+  // mapKernel.ts:761-801 "delete" remote branch: sequencedData.delete(key).
+  void del(uint32_t key);
+  // mapKernel.ts:708-760 "clear" remote branch: sequencedData.clear().
+  void clear();
+  // Live entries in Map iteration (insertion) order: (key, value, birth seq).
+  struct Entry {
+    uint32_t key, value, birth;
+  };
+  std::vector<Entry> entries() const;
+  void toSlots(fmt_map_slot* out, uint32_t keyBound) const;
+
+ private:
+  struct Item {
+    uint32_t key, value, birth;
+    bool live;
+  };
+  std::vector<int> slot_;   // key → index in items_, -1 if absent
+  std::vector<Item> items_; // append-only with tombstones; order = Map insertion order
+};
+
+// map.ts:176-246: header blob {"blobs":[...],"content":{...}} plus blobN for values ≥ 8 KiB and
+// for each 16 KiB flush; object keys enumerate array indices first (OrdinaryOwnPropertyKeys).
+struct MapSummary {
+  std::string header;
+  std::vector<std::string> blobs;  // blob0, blob1, ...
+};
+MapSummary summarizeMap(const std::vector<MapState::Entry>& entries,
+                        const std::vector<std::string>& keyNames,
+                        const std::vector<std::string>& valueJson);
+
+}  // namespace orc

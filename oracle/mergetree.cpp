@@ -1,0 +1,740 @@
+// oracle/mergetree.cpp — TEST INFRASTRUCTURE ONLY. See mergetree.hpp for scope and citations.
+#include "mergetree.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "common.hpp"
+
+namespace orc {
+
+// ------------------------------------------------------------------------------------------------
+// properties.ts:32-61 matchProperties: same key set, equal values (values are interned JSON texts,
+// so equal ids ⇔ equal primitive values). Order-insensitive; undefined matches {}.
+// ------------------------------------------------------------------------------------------------
+bool matchProperties(const PropMap& a, const PropMap& b) {
+  if (a.kv.size() != b.kv.size()) return false;
+  for (const auto& [k, v] : a.kv) {
+    bool found = false;
+    for (const auto& [k2, v2] : b.kv) {
+      if (k2 == k) {
+        if (v2 != v) return false;
+        found = true;
+        break;
+      }
+    }
+    if (!found) return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// heap.ts:54-182
+// ------------------------------------------------------------------------------------------------
+void LruHeap::add(Entry e) {
+  L_.push_back(e);
+  fixup(count());
+}
+
+LruHeap::Entry LruHeap::get() {
+  std::swap(L_[1], L_[count()]);
+  Entry x = L_.back();
+  L_.pop_back();
+  fixdown(1);
+  return x;
+}
+
+void LruHeap::fixup(int k) {
+  while (gtParent(k)) {
+    const int parent = k >> 1;
+    std::swap(L_[k], L_[parent]);
+    k = parent;
+  }
+}
+
+void LruHeap::fixdown(int k) {
+  while ((k << 1) <= count()) {
+    int j = k << 1;
+    if (j < count() && L_[j].maxSeq - L_[j + 1].maxSeq > 0) j++;
+    if (L_[k].maxSeq - L_[j].maxSeq <= 0) break;
+    std::swap(L_[k], L_[j]);
+    k = j;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Construction and node plumbing
+// ------------------------------------------------------------------------------------------------
+MergeTree::MergeTree() {
+  root_ = makeBlock(0);
+  unfinished_.childCount = -1;
+}
+
+Block* MergeTree::makeBlock(int childCount) {
+  blockPool_.push_back(std::make_unique<Block>());
+  Block* b = blockPool_.back().get();
+  b->childCount = childCount;
+  return b;
+}
+
+Seg* MergeTree::makeSeg() {
+  segPool_.push_back(std::make_unique<Seg>());
+  return segPool_.back().get();
+}
+
+// mergeTreeNodes.ts:312-323 assignChild
+void MergeTree::assignChild(Block* parent, Node* child, int index) {
+  child->parent = parent;
+  child->index = index;
+  parent->children[index] = child;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Lengths
+// ------------------------------------------------------------------------------------------------
+// perspective.ts:57-71 PerspectiveBase.isSegmentPresent
+bool MergeTree::isPresent(const Seg* s, const Perspective& p) {
+  if (!p.hasOccurred(s->ins)) return false;
+  for (const Stamp& r : s->removes)
+    if (p.hasOccurred(r)) return false;
+  return true;
+}
+
+// mergeTree.ts:720-736 leafLength: undefined once the first remove is at or below minSeq.
+int MergeTree::leafLength(const Seg* s, const Perspective& p) const {
+  if (s->removed() && minSeqHasOccurred(s->removes[0])) return kUndefinedLen;
+  return isPresent(s, p) ? s->len() : 0;
+}
+
+// mergeTree.ts:2819-2879 blockUpdate: sum of the defined child lengths, undefined if none.
+int MergeTree::localBlockLength(const Block* b) const {
+  int len = kUndefinedLen;
+  const Perspective lp = localPerspective();
+  for (int i = 0; i < b->childCount; i++) {
+    const Node* c = b->children[i];
+    const int l = c->isLeaf ? leafLength(static_cast<const Seg*>(c), lp)
+                            : localBlockLength(static_cast<const Block*>(c));
+    if (l != kUndefinedLen) len = (len == kUndefinedLen ? 0 : len) + l;
+  }
+  return len;
+}
+
+// PartialSequenceLengths.getPartialLength ≡ Σ leaf nodeLength ?? 0 (partialLengths.ts:1189-1240).
+int MergeTree::remoteBlockLength(const Block* b, const Perspective& p) const {
+  int len = 0;
+  for (int i = 0; i < b->childCount; i++) {
+    const Node* c = b->children[i];
+    if (c->isLeaf) {
+      const int l = leafLength(static_cast<const Seg*>(c), p);
+      if (l != kUndefinedLen) len += l;
+    } else {
+      len += remoteBlockLength(static_cast<const Block*>(c), p);
+    }
+  }
+  return len;
+}
+
+// mergeTree.ts:1116-1145 nodeLength
+int MergeTree::nodeLength(const Node* n, const Perspective& p) const {
+  if (n->isLeaf) return leafLength(static_cast<const Seg*>(n), p);
+  const Block* b = static_cast<const Block*>(n);
+  if (isLocalPerspective(p)) return localBlockLength(b);
+  return remoteBlockLength(b, p);
+}
+
+int MergeTree::getLocalLength() const {
+  const int l = localBlockLength(root_);
+  return l == kUndefinedLen ? 0 : l;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Inserting walk (mergeTree.ts:1811-1987)
+// ------------------------------------------------------------------------------------------------
+bool MergeTree::breakTie(int pos, const Node* node, const Stamp& stamp) const {
+  if (!node->isLeaf) return true;
+  if (pos != 0) return false;
+  const Seg* s = static_cast<const Seg*>(node);
+  return stampGreater(stamp, s->ins) ||
+         (s->removed() && s->removes[0].seq != kUnassignedSeq && stampGreater(s->removes[0], stamp));
+}
+
+// forwardExcursion(node, ...) visits every leaf after `node` regardless of visibility
+// (mergeTreeNodeWalk.ts:123-140); blockInsert's continueFrom only asks whether one exists.
+static bool subtreeHasLeaf(const Node* n) {
+  if (n->isLeaf) return true;
+  const Block* b = static_cast<const Block*>(n);
+  for (int i = 0; i < b->childCount; i++)
+    if (subtreeHasLeaf(b->children[i])) return true;
+  return false;
+}
+
+bool MergeTree::hasLeafAfter(const Block* block) const {
+  const Node* node = block;
+  while (node->parent != nullptr) {
+    const Block* p = node->parent;
+    for (int i = node->index + 1; i < p->childCount; i++)
+      if (subtreeHasLeaf(p->children[i])) return true;
+    node = p;
+  }
+  return false;
+}
+
+void MergeTree::insertingWalk(int pos, const Perspective& p, Stamp stamp, InsertCtx& ctx) {
+  InsertResult r = insertRecursive(root_, pos, p, stamp, ctx, true);
+  if (r.remainder != nullptr) updateRoot(r.remainder);
+}
+
+MergeTree::InsertResult MergeTree::insertRecursive(Block* block, int pos, const Perspective& p,
+                                                   Stamp stamp, InsertCtx& ctx, bool isLastBlock) {
+  int rem = pos;
+  int childIndex;
+  Node* newNode = nullptr;
+  bool hadChanges = false;
+  for (childIndex = 0; childIndex < block->childCount; childIndex++) {
+    Node* child = block->children[childIndex];
+    const bool isLastChildOfLastBlock = isLastBlock && childIndex == block->childCount - 1;
+    int len = nodeLength(child, p);
+    if (len == kUndefinedLen) {
+      if (!isLastChildOfLastBlock) continue;  // removed below minSeq: skipped
+      len = 0;
+    }
+    if (rem < len || (rem == len && breakTie(rem, child, stamp))) {
+      if (child->isLeaf) {
+        Seg* seg = static_cast<Seg*>(child);
+        if (ctx.isInsert) {
+          // onLeaf: the candidate replaces the current slot, the old leaf moves after it.
+          hadChanges = true;
+          assignChild(block, ctx.candidate, childIndex);
+          newNode = seg;
+          childIndex++;
+        } else {
+          // splitLeafSegment (mergeTree.ts:1768-1796)
+          if (rem > 0) {
+            newNode = splitAt(seg, rem);
+            hadChanges = true;
+            childIndex++;
+          } else {
+            return {nullptr, hadChanges};
+          }
+        }
+      } else {
+        InsertResult r = insertRecursive(static_cast<Block*>(child), rem, p, stamp, ctx,
+                                         isLastChildOfLastBlock);
+        hadChanges = hadChanges || r.hadChanges;
+        if (r.remainder == nullptr) return r;
+        if (r.remainder == &unfinished_) {
+          rem -= len;  // act as if shifted past the block
+          continue;
+        }
+        newNode = r.remainder;
+        childIndex++;
+      }
+      break;
+    }
+    rem -= len;
+  }
+  if (newNode == nullptr && rem == 0) {
+    if (ctx.isInsert) {
+      if (hasLeafAfter(block)) return {&unfinished_, hadChanges};
+      newNode = ctx.candidate;
+    }
+  }
+  if (newNode != nullptr) {
+    hadChanges = true;
+    for (int i = block->childCount; i > childIndex; i--) {
+      block->children[i] = block->children[i - 1];
+      block->children[i]->index = i;
+    }
+    assignChild(block, newNode, childIndex);
+    block->childCount++;
+    if (block->childCount < kMaxNodesInBlock) return {nullptr, hadChanges};
+    return {split(block), hadChanges};
+  }
+  return {nullptr, hadChanges};
+}
+
+// mergeTree.ts:1974-1987: keep the first half, move the second half to a new block.
+Block* MergeTree::split(Block* node) {
+  constexpr int half = kMaxNodesInBlock / 2;
+  Block* nb = makeBlock(half);
+  node->childCount = half;
+  for (int i = 0; i < half; i++) {
+    assignChild(nb, node->children[half + i], i);
+    node->children[half + i] = nullptr;
+  }
+  return nb;
+}
+
+// mergeTree.ts:1313-1320
+void MergeTree::updateRoot(Block* splitNode) {
+  Block* nr = makeBlock(2);
+  assignChild(nr, root_, 0);
+  assignChild(nr, splitNode, 1);
+  root_ = nr;
+}
+
+// mergeTreeNodes.ts:389-435 splitAt + textSegment.ts:95-103 + segmentPropertiesManager.ts:24-42.
+Seg* MergeTree::splitAt(Seg* seg, int pos) {
+  Seg* next = makeSeg();
+  next->text = seg->text.substr(static_cast<size_t>(pos));
+  seg->text.resize(static_cast<size_t>(pos));
+  next->ins = seg->ins;
+  next->removes = seg->removes;
+  if (seg->props.defined) next->props = seg->props;
+  return next;
+}
+
+// mergeTree.ts:1798-1808
+void MergeTree::ensureIntervalBoundary(int pos, const Perspective& p) {
+  InsertCtx ctx{false, nullptr};
+  insertingWalk(pos, p, Stamp{kTreeMaintSeq, p.client}, ctx);
+}
+
+// ------------------------------------------------------------------------------------------------
+// nodeMap (mergeTree.ts:2961-3020) over depthFirstNodeWalk: visits leaves of positive length
+// under `p` that lie inside [start, end) after the boundaries have been ensured.
+// ------------------------------------------------------------------------------------------------
+template <class F>
+void MergeTree::nodeMap(const Perspective& p, int start, int end, F&& leafFn) const {
+  if (end == start) return;
+  int pos = 0;
+  bool exit = false;
+  auto walk = [&](auto&& self, const Block* b) -> void {
+    for (int i = 0; i < b->childCount && !exit; i++) {
+      if (end <= pos) {
+        exit = true;
+        return;
+      }
+      const Node* n = b->children[i];
+      const int len = nodeLength(n, p);
+      const int lenAt = len == kUndefinedLen ? 0 : len;
+      if (lenAt == 0) continue;  // skip
+      const int nextPos = pos + lenAt;
+      if (start >= nextPos) {
+        pos = nextPos;
+        continue;
+      }
+      if (n->isLeaf) {
+        leafFn(const_cast<Seg*>(static_cast<const Seg*>(n)));
+        pos = nextPos;
+      } else {
+        self(self, static_cast<const Block*>(n));
+      }
+    }
+  };
+  walk(walk, root_);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Operations
+// ------------------------------------------------------------------------------------------------
+// mergeTree.ts:812-822
+void MergeTree::addToLRUSet(Seg* leaf, int seq) {
+  if (leaf->parent->needsScour != 1 && seq > currentSeq) {
+    leaf->parent->needsScour = 1;
+    heap_.add({leaf, seq});
+  }
+}
+
+// mergeTree.ts:1484-1517 insertSegments + :1555-1750 blockInsert (no obliterates in scope).
+void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp) {
+  ensureIntervalBoundary(pos, p);
+  if (seg->len() > 0) {
+    seg->ins = stamp;
+    InsertCtx ctx{true, seg};
+    insertingWalk(pos, p, stamp, ctx);
+    if (seg->parent == nullptr) throw DataError("MergeTree insert failed");
+    if (collaborating) {
+      const bool isLocal = stamp.seq == kUnassignedSeq;
+      if (!(isLocal && stamp.client == clientId) &&
+          stampGreater(seg->ins, Stamp{minSeq, kNonCollabClient}))
+        addToLRUSet(seg, seg->ins.seq);
+    }
+  }
+  if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
+}
+
+// mergeTree.ts:2292-2383 markRangeRemoved; stamps.ts:144-158 spliceIntoList.
+void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp stamp) {
+  ensureIntervalBoundary(start, p);
+  ensureIntervalBoundary(end, p);
+  std::vector<Seg*> hit;
+  nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
+  for (Seg* s : hit) {
+    if (!s->removed() || stamp.seq == kUnassignedSeq) {
+      s->removes.push_back(stamp);
+    } else {
+      int i = static_cast<int>(s->removes.size()) - 1;
+      for (; i >= 0; i--)
+        if (stampGreater(stamp, s->removes[i])) break;
+      s->removes.insert(s->removes.begin() + (i + 1), stamp);
+    }
+    if (collaborating) {
+      const bool localPending = s->removes[0].seq == kUnassignedSeq && stamp.client == clientId;
+      if (!localPending) addToLRUSet(s, stamp.seq);
+    }
+  }
+  if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
+}
+
+// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238 (raw values: for an
+// observer a remote raw change folds straight into msnConsensus, so the value is plain LWW; null
+// deletes the key; `seg.properties ??= createMap()` runs even if nothing changes).
+void MergeTree::annotateRange(int start, int end,
+                              const std::vector<std::pair<uint16_t, uint16_t>>& props,
+                              const Perspective& p, Stamp stamp) {
+  ensureIntervalBoundary(start, p);
+  ensureIntervalBoundary(end, p);
+  std::vector<Seg*> hit;
+  nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
+  for (Seg* s : hit) {
+    s->props.defined = true;
+    for (const auto& [key, value] : props) {
+      auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(),
+                             [&](const auto& e) { return e.first == key; });
+      if (value == 0) {  // null → delete
+        if (it != s->props.kv.end()) s->props.kv.erase(it);
+      } else if (it != s->props.kv.end()) {
+        it->second = value;
+      } else {
+        s->props.kv.emplace_back(key, value);
+      }
+    }
+    if (collaborating && stamp.seq != kUnassignedSeq) addToLRUSet(s, stamp.seq);
+  }
+  if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
+}
+
+// mergeTree.ts:1147-1166
+void MergeTree::setMinSeq(int min) {
+  if (min > currentSeq) throw DataError("Trying to set minSeq above currentSeq of collab window!");
+  if (minSeq > min) throw DataError("minSeq of collab window > target minSeq!");
+  if (min > minSeq) {
+    minSeq = min;
+    zamboniSegments();
+  }
+}
+
+// client.ts:1381-1391
+void MergeTree::updateSeqNumbers(int min, int seq) {
+  if (currentSeq > seq) throw DataError("Incoming op sequence# < local collabWindow's currentSequence#");
+  currentSeq = seq;
+  if (min > seq) throw DataError("Incoming op sequence# < minSequence#");
+  setMinSeq(min);
+}
+
+void MergeTree::insertLocal(int pos, const std::u16string& text) {
+  Seg* s = makeSeg();
+  s->text = text;
+  insertSegments(pos, s, localPerspective(), Stamp{collaborating ? kUnassignedSeq : 0, clientId});
+}
+
+void MergeTree::annotateLocal(int start, int end,
+                              const std::vector<std::pair<uint16_t, uint16_t>>& props) {
+  annotateRange(start, end, props, localPerspective(),
+                Stamp{collaborating ? kUnassignedSeq : 0, clientId});
+}
+
+void MergeTree::removeLocal(int start, int end) {
+  markRangeRemoved(start, end, localPerspective(),
+                   Stamp{collaborating ? kUnassignedSeq : 0, clientId});
+}
+
+void MergeTree::startCollaboration(int localClientId, int minSeqArg, int currentSeqArg) {
+  clientId = localClientId;
+  minSeq = minSeqArg;
+  collaborating = true;
+  currentSeq = currentSeqArg;
+}
+
+// client.ts:1291-1327 applyRemoteOp → applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp
+// with PriorPerspective(refSeq, clientId) and stamp {seq, clientId} (client.ts:581-611).
+void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const uint32_t* propsOff,
+                            const uint32_t* propsKv) {
+  const Perspective p{false, op.ref_seq, op.client};
+  const Stamp stamp{op.seq, op.client};
+  switch (op.type) {
+    case FMT_MT_INSERT: {
+      Seg* s = makeSeg();
+      s->text.assign(reinterpret_cast<const char16_t*>(arena + op.payload), op.len);
+      insertSegments(op.pos1, s, p, stamp);
+      break;
+    }
+    case FMT_MT_REMOVE:
+      markRangeRemoved(op.pos1, op.pos2, p, stamp);
+      break;
+    case FMT_MT_ANNOTATE: {
+      std::vector<std::pair<uint16_t, uint16_t>> kv;
+      for (uint32_t i = propsOff[op.payload]; i < propsOff[op.payload + 1]; i++)
+        kv.emplace_back(static_cast<uint16_t>(propsKv[i] >> 16), static_cast<uint16_t>(propsKv[i] & 0xffff));
+      annotateRange(op.pos1, op.pos2, kv, p, stamp);
+      break;
+    }
+    default:
+      throw DataError("unsupported op type");
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Zamboni (zamboni.ts:33-213)
+// ------------------------------------------------------------------------------------------------
+static bool canAppendText(const Seg* prev, const Seg* seg) {
+  // textSegment.ts:76-83
+  if (!prev->text.empty() && prev->text.back() == u'\n') return false;
+  return prev->len() <= kTextGranularity || seg->len() <= kTextGranularity;
+}
+
+void MergeTree::zamboniSegments() {
+  if (!collaborating) return;
+  for (int i = 0; i < kZamboniMax; i++) {
+    if (heap_.count() == 0) break;
+    if (heap_.peek().maxSeq > minSeq) break;
+    LruHeap::Entry e = heap_.get();
+    Block* block = e.seg->parent;
+    if (block != nullptr && block->needsScour != 0) {
+      std::vector<Node*> hold;
+      scourNode(block, hold);
+      block->needsScour = 0;
+      const int newCount = static_cast<int>(hold.size());
+      if (newCount < block->childCount) {
+        block->childCount = newCount;
+        for (int j = 0; j < kMaxNodesInBlock; j++) block->children[j] = nullptr;
+        for (int j = 0; j < newCount; j++) assignChild(block, hold[j], j);
+        if (block->childCount < kMaxNodesInBlock / 2 && block->parent != nullptr)
+          packParent(block->parent);
+      }
+    }
+  }
+}
+
+void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {
+  Seg* prev = nullptr;
+  const Stamp minStamp{minSeq, kNonCollabClient};
+  const Perspective lp = localPerspective();
+  for (int k = 0; k < node->childCount; k++) {
+    Node* child = node->children[k];
+    if (!child->isLeaf) {
+      hold.push_back(child);
+      prev = nullptr;
+      continue;
+    }
+    Seg* seg = static_cast<Seg*>(child);
+    if (!seg->removed()) {
+      if (stampLte(seg->ins, minStamp)) {
+        const int l = leafLength(seg, lp);
+        const bool positive = (l == kUndefinedLen ? 0 : l) > 0;
+        if (prev != nullptr && canAppendText(prev, seg) && matchProperties(prev->props, seg->props) &&
+            positive) {
+          prev->text += seg->text;  // BaseSegment.append + TextSegment.append
+          seg->parent = nullptr;    // removeMergeNodeInfo
+        } else {
+          hold.push_back(seg);
+          prev = positive ? seg : nullptr;
+        }
+      } else {
+        hold.push_back(seg);
+        prev = nullptr;
+      }
+    } else {
+      if (stampLte(seg->removes[0], minStamp)) {
+        seg->parent = nullptr;  // unlinked
+      } else {
+        hold.push_back(seg);
+      }
+      prev = nullptr;
+    }
+  }
+}
+
+void MergeTree::packParent(Block* parent) {
+  std::vector<Node*> hold;
+  for (int i = 0; i < parent->childCount; i++) {
+    Block* child = static_cast<Block*>(parent->children[i]);
+    scourNode(child, hold);
+    child->parent = nullptr;
+  }
+  for (int j = 0; j < kMaxNodesInBlock; j++) parent->children[j] = nullptr;
+  if (!hold.empty()) {
+    const int total = static_cast<int>(hold.size());
+    constexpr int half = kMaxNodesInBlock / 2;
+    int childCount = std::min(kMaxNodesInBlock - 1, total / half);
+    if (childCount < 1) childCount = 1;
+    const int base = total / childCount;
+    int remainder = total % childCount;
+    int packed = 0;
+    for (int b = 0; b < childCount; b++) {
+      int n = base;
+      if (remainder > 0) {
+        n++;
+        remainder--;
+      }
+      Block* pb = makeBlock(n);
+      for (int j = 0; j < n; j++) assignChild(pb, hold[packed++], j);
+      assignChild(parent, pb, b);
+    }
+    parent->childCount = childCount;
+  } else {
+    parent->childCount = 0;
+  }
+  if (parent->childCount < kMaxNodesInBlock / 2 && parent->parent != nullptr) {
+    packParent(parent->parent);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Readouts
+// ------------------------------------------------------------------------------------------------
+std::u16string MergeTree::getText() const {
+  std::u16string out;
+  const Perspective lp = localPerspective();
+  const int len = getLocalLength();
+  nodeMap(lp, 0, len, [&](Seg* s) { out += s->text; });
+  return out;
+}
+
+void MergeTree::collectLeaves(std::vector<const Seg*>& out, std::vector<int>& blockOfLeaf,
+                              int* nLeafBlocks, int* depth) const {
+  int blocks = 0;
+  int maxDepth = 0;
+  auto walk = [&](auto&& self, const Block* b, int d) -> void {
+    maxDepth = std::max(maxDepth, d);
+    bool leafBlock = false;
+    for (int i = 0; i < b->childCount; i++) {
+      const Node* n = b->children[i];
+      if (n->isLeaf) {
+        leafBlock = true;
+        out.push_back(static_cast<const Seg*>(n));
+        blockOfLeaf.push_back(blocks);
+      } else {
+        self(self, static_cast<const Block*>(n), d + 1);
+      }
+    }
+    if (leafBlock) blocks++;
+  };
+  walk(walk, root_, 1);
+  *nLeafBlocks = blocks;
+  *depth = maxDepth;
+}
+
+// JSON object of a property map: array-index keys first ascending, then insertion order.
+static void emitProps(std::string& out, const PropMap& pm, const std::vector<std::string>& keys,
+                      const std::vector<std::string>& values) {
+  std::vector<std::pair<uint64_t, size_t>> idx;
+  std::vector<size_t> rest;
+  for (size_t i = 0; i < pm.kv.size(); i++) {
+    uint64_t v;
+    if (isArrayIndexKey(keys.at(pm.kv[i].first), &v)) idx.emplace_back(v, i);
+    else rest.push_back(i);
+  }
+  std::sort(idx.begin(), idx.end());
+  out.push_back('{');
+  bool first = true;
+  auto one = [&](size_t i) {
+    if (!first) out.push_back(',');
+    first = false;
+    jsonQuoteUtf8(out, keys.at(pm.kv[i].first));
+    out.push_back(':');
+    out += values.at(pm.kv[i].second);
+  };
+  for (auto& e : idx) one(e.second);
+  for (size_t i : rest) one(i);
+  out.push_back('}');
+}
+
+Summary MergeTree::summarize(const std::vector<std::string>& keys,
+                             const std::vector<std::string>& values, int chunkSize) const {
+  // extractSync: leaves present at PriorPerspective(minSeq, NonCollabClient), merged while
+  // prev.canAppend(seg) && matchProperties (props for raw-only annotations = current props).
+  struct Out {
+    std::u16string text;
+    PropMap props;
+  };
+  std::vector<Out> segs;
+  const Perspective mp{false, minSeq, kNonCollabClient};
+  const int rootLen = nodeLength(root_, mp);
+  const int total = rootLen == kUndefinedLen ? 0 : rootLen;
+  nodeMap(mp, 0, total, [&](Seg* s) {
+    if (!isPresent(s, mp)) return;
+    if (!segs.empty()) {
+      Out& prev = segs.back();
+      const bool endsNl = !prev.text.empty() && prev.text.back() == u'\n';
+      const bool sizeOk = static_cast<int>(prev.text.size()) <= kTextGranularity ||
+                          s->len() <= kTextGranularity;
+      if (!endsNl && sizeOk && matchProperties(prev.props, s->props)) {
+        prev.text += s->text;
+        return;
+      }
+    }
+    segs.push_back({s->text, s->props});
+  });
+  long long totalLen = 0;
+  for (auto& o : segs) {
+    totalLen += static_cast<long long>(o.text.size());
+    if (o.props.defined && o.props.kv.empty()) o.props.defined = false;  // {} → undefined
+  }
+
+  auto chunk = [&](size_t startIndex, long long approx, bool header, size_t* count,
+                   long long* chunkLen) {
+    size_t n = 0;
+    long long len = 0;
+    while (len < approx && startIndex + n < segs.size()) {
+      len += static_cast<long long>(segs[startIndex + n].text.size());
+      n++;
+    }
+    std::string j = "{\"chunkStartSegmentIndex\":";
+    jsonInt(j, static_cast<long long>(startIndex));
+    j += ",\"chunkSegmentCount\":";
+    jsonInt(j, static_cast<long long>(n));
+    j += ",\"chunkLengthChars\":";
+    jsonInt(j, len);
+    j += ",\"totalLengthChars\":";
+    jsonInt(j, totalLen);
+    j += ",\"totalSegmentCount\":";
+    jsonInt(j, static_cast<long long>(segs.size()));
+    j += ",\"chunkSequenceNumber\":";
+    jsonInt(j, minSeq);
+    j += ",\"segmentTexts\":[";
+    for (size_t i = 0; i < n; i++) {
+      if (i) j.push_back(',');
+      const Out& o = segs[startIndex + i];
+      if (o.props.defined) {
+        j += "{\"text\":";
+        jsonQuoteUtf16(j, o.text.data(), o.text.size());
+        j += ",\"props\":";
+        emitProps(j, o.props, keys, values);
+        j.push_back('}');
+      } else {
+        jsonQuoteUtf16(j, o.text.data(), o.text.size());
+      }
+    }
+    j.push_back(']');
+    if (header) {
+      // snapshotChunks.ts:182-204 buildHeaderMetadataForLegacyChunk
+      j += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+      if (len < totalLen) j += ",{\"id\":\"body\"}";
+      j += "],\"sequenceNumber\":";
+      jsonInt(j, minSeq);
+      j += ",\"totalLength\":";
+      jsonInt(j, totalLen);
+      j += ",\"totalSegmentCount\":";
+      jsonInt(j, static_cast<long long>(segs.size()));
+      j.push_back('}');
+    }
+    j.push_back('}');
+    *count = n;
+    *chunkLen = len;
+    return j;
+  };
+  Summary s;
+  size_t c1;
+  long long l1;
+  s.header = chunk(0, chunkSize, true, &c1, &l1);
+  if (c1 < segs.size()) {
+    size_t c2;
+    long long l2;
+    s.body = chunk(c1, totalLen, false, &c2, &l2);
+  }
+  return s;
+}
+
+}  // namespace orc

@@ -1,0 +1,217 @@
+// oracle/mergetree.hpp — TEST INFRASTRUCTURE ONLY (parity oracle for the merge-tree replay path).
+//
+// A CPU restatement of the reference merge-tree for a client that never submits ops while
+// collaborating (an observer: every sequenced message is remote), plus the detached local-op path
+// used to build the SharedString snapshot fixtures. Every function cites the reference code it
+// follows (paths relative to /root/reference/packages/dds/merge-tree/src unless stated).
+//
+// What is restated exactly (it decides the segmentation that summaries expose):
+//   - the 8-slot B+tree, its 4/4 split and root growth (mergeTree.ts:1846-1987, 1313-1320)
+//   - the inserting walk with breakTie / theUnfinishedNode (mergeTree.ts:1811-1972)
+//   - ensureIntervalBoundary splits (mergeTree.ts:1768-1808), nodeMap (mergeTree.ts:2961-3020)
+//   - remove / annotate stamping (mergeTree.ts:2009-2081, 2292-2383; stamps.ts:144-158)
+//   - the zamboni LRU heap, scour and packParent (zamboni.ts:33-213; core-utils heap.ts:54-182)
+//   - raw-property LWW (segmentPropertiesManager.ts:188-238) and the legacy summary
+//     (snapshotlegacy.ts:74-262, snapshotChunks.ts:85-204)
+// What is replaced: PartialSequenceLengths is only an index; block lengths under a remote
+// perspective are evaluated directly as the sum of leaf lengths, which is exactly the invariant the
+// reference's strict checker asserts (partialLengths.ts:1189-1240).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../include/fmt.h"
+
+namespace orc {
+
+constexpr int kUnassignedSeq = -1;  // constants.ts:21
+constexpr int kTreeMaintSeq = -2;   // constants.ts:26
+constexpr int kLocalClientId = -1;  // constants.ts:31
+constexpr int kNonCollabClient = -2;  // constants.ts:36
+constexpr int kMaxNodesInBlock = 8;   // mergeTreeNodes.ts:248
+constexpr int kTextGranularity = 256;  // textSegment.ts:21
+constexpr int kUndefinedLen = -1;      // "length undefined": removed at or below minSeq
+constexpr int kZamboniMax = 2;         // zamboni.ts:25
+
+struct DataError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+struct Stamp {
+  int seq;
+  int client;
+};
+
+// stamps.ts:101-113 (the oracle never holds two unassigned stamps, so localSeq never decides).
+inline bool stampGreater(const Stamp& a, const Stamp& b) {
+  if (a.seq == kUnassignedSeq) return b.seq != kUnassignedSeq;
+  if (b.seq == kUnassignedSeq) return false;
+  return a.seq > b.seq;
+}
+inline bool stampLte(const Stamp& a, const Stamp& b) { return !stampGreater(a, b); }
+
+// perspective.ts:80-93 (PriorPerspective) and :174-184 (LocalDefaultPerspective).
+struct Perspective {
+  bool everything;  // LocalDefaultPerspective: every op has occurred
+  int refSeq;
+  int client;
+  bool hasOccurred(const Stamp& s) const {
+    if (everything) return true;
+    return (s.seq != kUnassignedSeq && s.seq <= refSeq) || s.client == client;
+  }
+};
+
+// A property map with JS insertion order (keys interned as ids by the host driver).
+struct PropMap {
+  bool defined = false;  // `seg.properties` is undefined until the first annotate
+  std::vector<std::pair<uint16_t, uint16_t>> kv;  // (key id, value id), insertion order
+};
+bool matchProperties(const PropMap& a, const PropMap& b);  // properties.ts:32-61
+
+struct Block;
+struct Node {
+  explicit Node(bool leaf) : isLeaf(leaf) {}
+  Block* parent = nullptr;
+  int index = 0;
+  const bool isLeaf;
+};
+
+struct Seg : Node {
+  Seg() : Node(true) {}
+  std::u16string text;
+  Stamp ins{0, 0};
+  std::vector<Stamp> removes;  // sorted by stamps.compare (spliceIntoList)
+  PropMap props;
+  int len() const { return static_cast<int>(text.size()); }
+  bool removed() const { return !removes.empty(); }
+};
+
+struct Block : Node {
+  Block() : Node(false) {}
+  int childCount = 0;
+  Node* children[kMaxNodesInBlock] = {};
+  int needsScour = -1;  // -1 undefined, 0 false, 1 true (mergeTreeNodes.ts MergeBlock.needsScour)
+};
+
+// core-utils/src/heap.ts:54-182 with LRUSegmentComparer (mergeTree.ts:144-147). Ported as an
+// algorithm because ties between equal maxSeq are resolved by its exact sift order.
+class LruHeap {
+ public:
+  struct Entry {
+    Seg* seg;
+    int maxSeq;
+  };
+  LruHeap() { L_.push_back({nullptr, -2}); }
+  int count() const { return static_cast<int>(L_.size()) - 1; }
+  const Entry& peek() const { return L_[1]; }
+  Entry get();
+  void add(Entry e);
+
+ private:
+  bool gtParent(int k) const { return k > 1 && L_[k >> 1].maxSeq - L_[k].maxSeq > 0; }
+  void fixup(int k);
+  void fixdown(int k);
+  std::vector<Entry> L_;
+};
+
+struct Summary {
+  std::string header;
+  std::string body;  // empty when no body chunk
+};
+
+class MergeTree {
+ public:
+  MergeTree();
+
+  // --- collaboration window (mergeTreeNodes.ts:598-696) ---
+  int clientId = kLocalClientId;
+  bool collaborating = false;
+  int minSeq = 0;
+  int currentSeq = 0;
+
+  // Detached local ops (not collaborating): stamp {seq 0, client -1}, local perspective.
+  void insertLocal(int pos, const std::u16string& text);
+  void annotateLocal(int start, int end, const std::vector<std::pair<uint16_t, uint16_t>>& props);
+  void removeLocal(int start, int end);
+  // client.ts:1700-1727 → mergeTree.ts:803-810
+  void startCollaboration(int localClientId, int minSeqArg, int currentSeqArg);
+
+  // One member op of a sequenced remote message (client.ts:1291-1327).
+  void applyRemote(const fmt_mt_op& op, const uint16_t* arena, const uint32_t* propsOff,
+                   const uint32_t* propsKv);
+  // client.ts:1381-1391 updateSeqNumbers, after the last member of a message.
+  void updateSeqNumbers(int min, int seq);
+
+  // Readouts.
+  std::u16string getText() const;     // MergeTreeTextHelper.ts:28-87 (local perspective)
+  int getLocalLength() const;
+  void collectLeaves(std::vector<const Seg*>& out, std::vector<int>& blockOfLeaf,
+                     int* nLeafBlocks, int* depth) const;
+  // snapshotlegacy.ts:195-262 extractSync + :126-193 emit (header/body blob contents).
+  Summary summarize(const std::vector<std::string>& keyNames,
+                    const std::vector<std::string>& valueJson, int chunkSize = 10000) const;
+
+ private:
+  struct InsertCtx {
+    bool isInsert;
+    Seg* candidate;
+  };
+  struct InsertResult {
+    Block* remainder;
+    bool hadChanges;
+  };
+
+  Block* makeBlock(int childCount);
+  Seg* makeSeg();
+  static void assignChild(Block* parent, Node* child, int index);
+
+  Perspective localPerspective() const { return {true, 0x7fffffff, clientId}; }
+  bool minSeqHasOccurred(const Stamp& s) const {
+    return (s.seq != kUnassignedSeq && s.seq <= minSeq) || s.client == kNonCollabClient;
+  }
+  static bool isPresent(const Seg* s, const Perspective& p);
+  int leafLength(const Seg* s, const Perspective& p) const;      // mergeTree.ts:720-736
+  int localBlockLength(const Block* b) const;                    // blockUpdate cachedLength
+  int remoteBlockLength(const Block* b, const Perspective& p) const;
+  int nodeLength(const Node* n, const Perspective& p) const;     // mergeTree.ts:1116-1145
+  bool isLocalPerspective(const Perspective& p) const {
+    return !collaborating || clientId == p.client;
+  }
+
+  void insertingWalk(int pos, const Perspective& p, Stamp stamp, InsertCtx& ctx);
+  InsertResult insertRecursive(Block* block, int pos, const Perspective& p, Stamp stamp,
+                               InsertCtx& ctx, bool isLastBlock);
+  bool breakTie(int pos, const Node* node, const Stamp& stamp) const;
+  bool hasLeafAfter(const Block* block) const;  // forwardExcursion existence (blockInsert)
+  Block* split(Block* node);
+  void updateRoot(Block* splitNode);
+  Seg* splitAt(Seg* seg, int pos);
+  void ensureIntervalBoundary(int pos, const Perspective& p);
+
+  template <class F>
+  void nodeMap(const Perspective& p, int start, int end, F&& leafFn) const;
+
+  void insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp);
+  void markRangeRemoved(int start, int end, const Perspective& p, Stamp stamp);
+  void annotateRange(int start, int end, const std::vector<std::pair<uint16_t, uint16_t>>& props,
+                     const Perspective& p, Stamp stamp);
+  void addToLRUSet(Seg* leaf, int seq);
+  void setMinSeq(int min);
+
+  void zamboniSegments();
+  void scourNode(Block* node, std::vector<Node*>& hold);
+  void packParent(Block* parent);
+
+  Block* root_;
+  Block unfinished_;  // theUnfinishedNode sentinel (mergeTree.ts:656)
+  LruHeap heap_;
+  std::vector<std::unique_ptr<Seg>> segPool_;
+  std::vector<std::unique_ptr<Block>> blockPool_;
+};
+
+}  // namespace orc

@@ -1,0 +1,201 @@
+"""ctypes binding of the parity oracle (oracle/_build/liborc.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker or the CPU baseline — never as the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liborc.so")
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.orc_mt_new.restype = P
+        L.orc_mt_free.argtypes = [P]
+        L.orc_mt_insert_local.argtypes = [P, ctypes.c_int, P, ctypes.c_int]
+        L.orc_mt_annotate_local.argtypes = [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int]
+        L.orc_mt_remove_local.argtypes = [P, ctypes.c_int, ctypes.c_int]
+        L.orc_mt_start_collab.argtypes = [P, ctypes.c_int]
+        L.orc_mt_apply_ops.argtypes = [P, P, ctypes.c_uint64, P, P, P]
+        L.orc_mt_text.argtypes = [P, P, ctypes.c_int]
+        L.orc_mt_dump.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32]
+        L.orc_mt_summary.argtypes = [P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P,
+                                     ctypes.c_int, P, P]
+        L.orc_mt_replay_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P,
+                                          ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P]
+        L.orc_map_replay.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.c_uint32, P]
+        L.orc_map_summary.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P,
+                                      ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P]
+        L.orc_xsadd_uint32.argtypes = [P, ctypes.c_int, P, ctypes.c_int]
+        L.orc_xsadd_mixed.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int]
+        L.orc_last_error.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _cstrs(strings):
+    arr = (ctypes.c_char_p * max(1, len(strings)))()
+    for i, s in enumerate(strings):
+        arr[i] = s.encode("utf-8")
+    return arr
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+class MergeTreeDoc:
+    """One observer merge-tree (or a detached local string)."""
+
+    def __init__(self):
+        self.h = lib().orc_mt_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_mt_free(self.h)
+            self.h = None
+
+    def _check(self, rc):
+        if rc != 0:
+            raise OracleError(lib().orc_last_error().decode())
+
+    def insert_local(self, pos: int, text: str):
+        u = np.frombuffer(text.encode("utf-16-le", "surrogatepass"), dtype="<u2").copy()
+        self._check(lib().orc_mt_insert_local(self.h, pos, _ptr(u), len(u)))
+
+    def annotate_local(self, start: int, end: int, kv: list[int]):
+        a = np.asarray(kv, dtype=np.uint32)
+        self._check(lib().orc_mt_annotate_local(self.h, start, end, _ptr(a), len(a)))
+
+    def remove_local(self, start: int, end: int):
+        self._check(lib().orc_mt_remove_local(self.h, start, end))
+
+    def start_collab(self, client: int = 0):
+        lib().orc_mt_start_collab(self.h, client)
+
+    def apply(self, ops: np.ndarray, arena: np.ndarray, props_off: np.ndarray, props_kv: np.ndarray):
+        ops = np.ascontiguousarray(ops)
+        self._check(lib().orc_mt_apply_ops(self.h, _ptr(ops), len(ops), _ptr(arena), _ptr(props_off),
+                                           _ptr(props_kv)))
+
+    def text(self) -> str:
+        n = lib().orc_mt_text(self.h, None, 0)
+        buf = np.zeros(max(n, 1), dtype="<u2")
+        lib().orc_mt_text(self.h, _ptr(buf), n)
+        return buf[:n].tobytes().decode("utf-16-le", "surrogatepass")
+
+    def dump(self, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=1024):
+        from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE
+
+        hdr = np.zeros(1, dtype=DOC_RESULT_DTYPE)
+        leaves = np.zeros(cap_leaves, dtype=LEAF_DTYPE)
+        chars = np.zeros(cap_chars, dtype="<u2")
+        props = np.zeros(cap_props, dtype=PROPSET_DTYPE)
+        lib().orc_mt_dump(self.h, _ptr(hdr), _ptr(leaves), cap_leaves, _ptr(chars), cap_chars,
+                          _ptr(props), cap_props)
+        h = hdr[0]
+        return h, leaves[: h["n_leaves"]], chars[: h["n_chars"]], props[: h["n_props"]]
+
+    def summary(self, keys: list[str], values: list[str], chunk_size: int = 10000):
+        k, v = _cstrs(keys), _cstrs(values)
+        hl, bl = ctypes.c_int(0), ctypes.c_int(0)
+        n = lib().orc_mt_summary(self.h, k, len(keys), v, len(values), chunk_size, None, 0,
+                                 ctypes.byref(hl), ctypes.byref(bl))
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().orc_mt_summary(self.h, k, len(keys), v, len(values), chunk_size, buf, n,
+                             ctypes.byref(hl), ctypes.byref(bl))
+        raw = buf.raw[:n]
+        header = raw[: hl.value].decode("utf-8")
+        body = raw[hl.value : hl.value + bl.value].decode("utf-8") if bl.value else None
+        return header, body
+
+
+def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096, cap_chars=1 << 16,
+                    cap_props=64, outputs=True):
+    """Replay a MergeTreeBatch; returns (headers, leaves, chars, props, seconds)."""
+    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+
+    doc_end = batch.n_docs if doc_end is None else doc_end
+    n = doc_end - doc_begin
+    hdrs = np.zeros(n, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(n * cap_leaves, dtype=LEAF_DTYPE) if outputs else None
+    chars = np.zeros(n * cap_chars, dtype="<u2") if outputs else None
+    props = np.zeros(n * cap_props, dtype=PROPSET_DTYPE) if outputs else None
+    secs = ctypes.c_double(0)
+    b, keep = batch_struct(batch)
+    rc = lib().orc_mt_replay_batch(ctypes.byref(b), doc_begin, doc_end, threads, _ptr(hdrs),
+                                   _ptr(leaves), cap_leaves, _ptr(chars), cap_chars, _ptr(props),
+                                   cap_props, ctypes.byref(secs))
+    del keep
+    if outputs:
+        leaves = leaves.reshape(n, cap_leaves)
+        chars = chars.reshape(n, cap_chars)
+        props = props.reshape(n, cap_props)
+    return rc, hdrs, leaves, chars, props, secs.value
+
+
+def map_replay(batch, threads=1):
+    """Replay a MapBatch; returns (slots[n_docs, key_bound], seconds)."""
+    from fluidframework_amd.native import MAP_SLOT_DTYPE
+
+    out = np.zeros(batch.n_docs * batch.key_bound, dtype=MAP_SLOT_DTYPE)
+    secs = ctypes.c_double(0)
+    ops = np.ascontiguousarray(batch.ops)
+    offs = np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64)
+    rc = lib().orc_map_replay(_ptr(ops), _ptr(offs), batch.n_docs, batch.key_bound, _ptr(out), threads,
+                              ctypes.byref(secs))
+    if rc != 0:
+        raise OracleError("map replay failed")
+    return out.reshape(batch.n_docs, batch.key_bound), secs.value
+
+
+def map_summary(batch, doc: int):
+    ops = np.ascontiguousarray(batch.ops)
+    b, e = int(batch.doc_op_offsets[doc]), int(batch.doc_op_offsets[doc + 1])
+    k, v = _cstrs(batch.keys), _cstrs(batch.values)
+    nb = ctypes.c_int(0)
+    n = lib().orc_map_summary(_ptr(ops), b, e, batch.key_bound, k, len(batch.keys), v, len(batch.values),
+                              None, 0, ctypes.byref(nb))
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().orc_map_summary(_ptr(ops), b, e, batch.key_bound, k, len(batch.keys), v, len(batch.values),
+                          buf, n, ctypes.byref(nb))
+    parts = buf.raw[:n].split(b"\0")
+    return parts[0].decode(), [p.decode() for p in parts[1 : 1 + nb.value]]
+
+
+def xsadd_uint32(seed, n):
+    s = np.asarray(seed, dtype=np.uint32)
+    out = np.zeros(n, dtype=np.uint32)
+    lib().orc_xsadd_uint32(_ptr(s), len(s), _ptr(out), n)
+    return out
+
+
+def xsadd_mixed(seed, kinds):
+    s = np.asarray(seed, dtype=np.uint32)
+    k = np.asarray(kinds, dtype=np.int32)
+    out = np.zeros(len(k), dtype=np.float64)
+    lib().orc_xsadd_mixed(_ptr(s), len(s), _ptr(k), _ptr(out), len(k))
+    return out

@@ -1,0 +1,141 @@
+"""The oracle pinned against the reference's own golden vectors (CPU only).
+
+  - 30 conflict-farm replay fixtures, 64 text checkpoints each (client.replay.spec.ts:20-76)
+  - SharedString legacy summary blobs (snapshotVersion.spec.ts:146-170, generateSharedStrings.ts)
+  - XSadd known answers (stochastic-test-utils/src/test/xsadd.spec.ts:11-31)
+  - SharedMap summary strings (map/src/test/mocha/map.spec.ts:142-317)
+"""
+import numpy as np
+import pytest
+
+from golden_data import replay_fixtures, snapshot_trees
+
+FIXTURES = list(replay_fixtures())
+
+
+@pytest.mark.parametrize("idx", range(len(FIXTURES)), ids=[f[0] for f in FIXTURES])
+def test_replay_fixture_text_checkpoints(orc, idx):
+    name, batch, group_end, initial, results = FIXTURES[idx]
+    doc = orc.MergeTreeDoc()
+    init = batch.doc_init[0]
+    if init[1]:
+        doc.insert_local(0, batch.text[init[0] : init[0] + init[1]].tobytes().decode("utf-16-le"))
+    doc.start_collab(0)
+    start = 0
+    for g, end in enumerate(group_end):
+        assert doc.text() == initial[g], f"group {g} initial"
+        doc.apply(batch.ops[start:end], batch.text, batch.props_off, batch.props_kv)
+        assert doc.text() == results[g], f"group {g} result"
+        start = end
+
+
+def _blobs(tree):
+    """content/{header,body} blob contents of a convertSummaryTreeToITree JSON tree."""
+    assert [e["path"] for e in tree["entries"]] == ["content"]
+    content = tree["entries"][0]["value"]["entries"]
+    out = {}
+    for e in content:
+        assert e["type"] == "Blob" and e["value"]["encoding"] == "utf-8"
+        out[e["path"]] = e["value"]["contents"]
+    return out
+
+
+def _detached_string(orc, name):
+    """generateSharedStrings.ts:34-152 for the four legacy variants without markers/intervals."""
+    doc = orc.MergeTreeDoc()
+    n, fmt = {
+        "headerOnly": (10000 // 4 // 2, "text{}"),
+        "headerAndBody": (10000 // 4 * 2, "text{}"),
+        "largeBody": (10000, "text-{}"),
+        "withAnnotations": (10000 // 4 * 2, "text{}"),
+    }[name]
+    for i in range(n):
+        doc.insert_local(0, fmt.format(i))
+    keys, values = ["bold"], ["null", "true"]
+    if name == "withAnnotations":
+        length = len(doc.text())
+        for i in range(0, length, 70):
+            doc.annotate_local(i, i + 10, [(0 << 16) | 1])
+    return doc, keys, values
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+def test_sharedstring_legacy_summary_bytes(orc, name):
+    expected = _blobs(snapshot_trees()[name])
+    doc, keys, values = _detached_string(orc, name)
+    header, body = doc.summary(keys, values)
+    assert header == expected["header"]
+    assert body == expected.get("body")
+
+
+def test_xsadd_known_answers(orc):
+    # xsadd.spec.ts:11-16
+    got = orc.xsadd_mixed([0], [0, 1, 2])
+    assert got[0] == 0.1471811873526141
+    assert got[1] == 2705912313
+    assert got[2] == 3331857606703893
+    # xsadd.spec.ts:18-31: first 10 uint32 equal the original C implementation
+    expected = [0x25ADAA92, 0x49104F14, 0xA148F1F9, 0x5EB27472, 0xA2DF62BB, 0xA30FE176, 0x8EB7F176,
+                0xD18F1191, 0xD3FDEA23, 0x3C834B7D]
+    assert orc.xsadd_uint32([0], 10).tolist() == expected
+    # unspecified seeds default to zero
+    a = orc.xsadd_mixed([0], [2])[0]
+    for s in ([0, 0], [0, 0, 0], [0, 0, 0, 0]):
+        assert orc.xsadd_mixed(s, [2])[0] == a
+
+
+def _map_batch(msgs):
+    from fluidframework_amd.streams import MapStreamBuilder
+
+    b = MapStreamBuilder()
+    d = b.begin_doc()
+    for i, m in enumerate(msgs):
+        b.add_message(d, i + 1, m)
+    return b.finish()
+
+
+def _set(k, v=None, undefined=False):
+    val = {"type": "Plain"} if undefined else {"type": "Plain", "value": v}
+    return {"type": "set", "key": k, "value": val}
+
+
+def test_map_summary_small(orc):
+    # map.spec.ts:211-236 "new serialization format for small maps"
+    header, blobs = orc.map_summary(_map_batch([_set("key", "value")]), 0)
+    assert header == '{"blobs":[],"content":{"key":{"type":"Plain","value":"value"}}}'
+    assert blobs == []
+
+
+def test_map_summary_insertion_order_and_undefined(orc):
+    # map.spec.ts:142-176 (the handle value is carried as its serialized JSON form)
+    handle = {"type": "__fluid_handle__", "url": "/subMap"}
+    msgs = [_set("first", "second"), _set("third", "fourth"), _set("fifth", undefined=True), _set("object", handle)]
+    header, blobs = orc.map_summary(_map_batch(msgs), 0)
+    assert header == (
+        '{"blobs":[],"content":{"first":{"type":"Plain","value":"second"},"third":{"type":"Plain",'
+        '"value":"fourth"},"fifth":{"type":"Plain"},"object":{"type":"Plain","value":{"type":'
+        '"__fluid_handle__","url":"/subMap"}}}}'
+    )
+
+
+def test_map_summary_big_blob(orc):
+    # map.spec.ts:256-317 "new serialization format for big maps"
+    long = "01234567890"
+    for _ in range(12):
+        long = long + long
+    header, blobs = orc.map_summary(_map_batch([_set("key", "value"), _set("longValue", long), _set("zzz", "the end")]), 0)
+    import json
+
+    assert header == json.dumps(
+        {"blobs": ["blob0"], "content": {"key": {"type": "Plain", "value": "value"}, "zzz": {"type": "Plain", "value": "the end"}}},
+        separators=(",", ":"),
+    )
+    assert blobs == [json.dumps({"longValue": {"type": "Plain", "value": long}}, separators=(",", ":"))]
+
+
+def test_map_summary_array_index_keys_first(orc):
+    # mapKernel.ts:545-551 builds a plain object: array-index keys enumerate first, ascending.
+    msgs = [_set("b", 1), _set("10", 2), _set("a", 3), _set("2", 4), {"type": "delete", "key": "b"}, _set("b", 5)]
+    header, _ = orc.map_summary(_map_batch(msgs), 0)
+    assert header == ('{"blobs":[],"content":{"2":{"type":"Plain","value":4},"10":{"type":"Plain","value":2},'
+                      '"a":{"type":"Plain","value":3},"b":{"type":"Plain","value":5}}}')

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Convert the reference's own golden fixtures into compact vectors under tests/golden/.
+
+Run in the build container (where /root/reference exists); the outputs are committed so the GPU
+box and the CPU test suite never read /root/reference at run time.
+
+Sources (data files held by the reference's own tests):
+  packages/dds/merge-tree/src/test/results/*-default-conflict-farm-0.40.json
+      replayed by client.replay.spec.ts:20-76 (64 groups of {initialText, resultText, msgs, seq})
+  packages/dds/sequence/src/test/snapshots/legacy/{headerOnly,headerAndBody,largeBody,withAnnotations}.json
+      checked by snapshotVersion.spec.ts:146-170 ("Snapshot diff")
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from fluidframework_amd.streams import MT_OP_DTYPE, MergeTreeStreamBuilder  # noqa: E402
+
+REF = "/root/reference/packages"
+RESULTS = f"{REF}/dds/merge-tree/src/test/results"
+SNAPSHOTS = f"{REF}/dds/sequence/src/test/snapshots/legacy"
+OUT = os.path.join(REPO, "tests", "golden")
+
+
+def convert_replay(path: str) -> dict:
+    groups = json.load(open(path))
+    b = MergeTreeStreamBuilder()
+    doc = b.begin_doc(initial_text=groups[0]["initialText"], observer="A")
+    group_end = []
+    result_texts = []
+    initial_texts = []
+    for g in groups:
+        initial_texts.append(g["initialText"])
+        for m in g["msgs"]:
+            assert m["type"] == "op"
+            doc.add_message(m)
+        group_end.append(doc.n_ops)
+        result_texts.append(g["resultText"])
+    batch = b.finish()
+    return {
+        "ops": batch.ops,
+        "arena": batch.text,
+        "doc_init": batch.doc_init,
+        "props_off": batch.props_off,
+        "props_kv": batch.props_kv,
+        "keys_json": np.frombuffer(json.dumps(batch.keys).encode(), dtype=np.uint8),
+        "values_json": np.frombuffer(json.dumps(batch.values).encode(), dtype=np.uint8),
+        "group_end": np.asarray(group_end, dtype=np.int64),
+        "texts_json": np.frombuffer(
+            json.dumps({"initial": initial_texts, "result": result_texts}).encode(), dtype=np.uint8
+        ),
+    }
+
+
+def main() -> None:
+    os.makedirs(OUT, exist_ok=True)
+    files = sorted(f for f in os.listdir(RESULTS) if f.endswith("-default-conflict-farm-0.40.json"))
+    bundle = {}
+    for i, f in enumerate(files):
+        d = convert_replay(os.path.join(RESULTS, f))
+        for k, v in d.items():
+            bundle[f"{i}/{k}"] = v
+    bundle["names"] = np.frombuffer(json.dumps(files).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "replay_conflict_farm_0.40.npz"), **bundle)
+    assert MT_OP_DTYPE.itemsize == 32
+
+    snaps = {}
+    for name in ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"]:
+        tree = json.load(open(os.path.join(SNAPSHOTS, name + ".json")))
+        snaps[name] = tree
+    with open(os.path.join(OUT, "snapshots_legacy.json"), "w") as fh:
+        json.dump(snaps, fh, separators=(",", ":"))
+    print(f"wrote {len(files)} replay fixtures and {len(snaps)} snapshot trees to {OUT}")
+
+
+if __name__ == "__main__":
+    main()
