@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: sequenced ops applied per second, conflict-farm replay (BASELINE.json metric).
+
+One step = one replay of a whole resident batch (inputs already in HBM) through the C ABI
+(fmt_mt_run / fmt_map_run). Default workload = T1: merge-tree conflict farm, 100k documents ×
+8 writer clients × 2000 ops per GPU (weak scaling: every rank replays its own 100k-doc shard).
+`--workload map` runs M2: SharedMap LWW, 1M documents × 8 clients × 1000 ops per GPU.
+
+Synthetic data: `--unique-docs` distinct documents are generated with the reference's PRNG and
+conflict-farm shape, then laid out `docs / unique` times as independent copies (own ops and text
+in HBM, nothing shared), so generation stays within seconds. See DESIGN.md.
+
+Launch: `python bench.py` (N=1) or `python -m torch.distributed.run --nproc-per-node N ... bench.py
+--gpus N`. Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "sequenced ops applied/sec (whole node) + achieved HBM GB/s, conflict-farm replay"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["mt", "map"], default="mt")
+    ap.add_argument("--docs", type=int, default=None, help="documents per GPU")
+    ap.add_argument("--ops-per-doc", type=int, default=None)
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--unique-docs", type=int, default=5000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample-docs", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from fluidframework_amd import native, workloads
+
+    mt = args.workload == "mt"
+    docs = args.docs or (100_000 if mt else 1_000_000)
+    opd = args.ops_per_doc or (2000 if mt else 1000)
+    seed = args.seed + 1000 * rank  # shards hold different documents
+
+    t = time.time()
+    if mt:
+        uniq = min(args.unique_docs, docs)
+        if docs % uniq:
+            raise SystemExit("--docs must be a multiple of --unique-docs")
+        batch = workloads.conflict_farm(uniq, n_clients=args.clients, ops_per_doc=opd, seed=seed, replicas=docs // uniq)
+    else:
+        batch = workloads.map_stream(docs, opd, key_pool=20, seed=seed)
+    n_ops = len(batch.ops)
+    log(rank, f"[bench] generated {docs} docs / {n_ops} ops in {time.time() - t:.1f}s")
+
+    eng = native.Engine(local_rank)
+    t = time.time()
+    if mt:
+        eng.mt_load(batch)
+    else:
+        eng.map_load(batch)
+    h2d_s = time.time() - t
+    in_bytes = batch.ops.nbytes + (batch.text.nbytes if mt else 0)
+    log(rank, f"[bench] host->HBM {in_bytes / 1e9:.2f} GB in {h2d_s:.2f}s ({eng.device_info()})")
+
+    run = eng.mt_run if mt else eng.map_run
+    for _ in range(args.warmup):
+        run()
+        eng.sync()
+    # algorithmic bytes of one launch (result sizes are known after the first run)
+    if mt:
+        hdrs = eng.mt_headers()
+        bad = int((hdrs["status"] != 0).sum())
+        if bad:
+            raise SystemExit(f"{bad} documents failed: statuses {np.unique(hdrs['status'])}")
+    else:
+        eng.map_fetch()
+    st = eng.stats()
+    bytes_per_launch = int(st.bytes_read + st.bytes_written)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        eng.sync()
+
+    kernel_ms = []
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        run()
+        kernel_ms.append(eng.stats().kernel_ms)  # waits for this launch's end event
+        log(rank, f"[bench] step {k}: kernel {kernel_ms[-1]:.1f} ms")
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total_ops = n_ops * world * args.steps
+    value = total_ops / elapsed
+    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    achieved = bytes_per_launch / (avg_kernel_ms / 1e3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # CPU baseline only ("port" of the reference path)
+
+        threads = min(16, os.cpu_count() or 1)
+        if mt:
+            sample = args.cpu_sample_docs or min(docs, 4 * threads * 80)
+            rc, _, _, _, _, secs = oracle.mt_replay_batch(batch, 0, sample, threads=threads, outputs=False)
+            sample_ops = int(batch.doc_op_offsets[sample])
+        else:
+            sample = args.cpu_sample_docs or min(docs, 40_000)
+            sub = batch.__class__(batch.ops[: int(batch.doc_op_offsets[sample])], batch.doc_op_offsets[: sample + 1],
+                                  batch.key_bound, batch.keys, batch.values)
+            _, secs = oracle.map_replay(sub, threads=threads)
+            sample_ops = int(batch.doc_op_offsets[sample])
+        cpu = {
+            "value": sample_ops / secs,
+            "unit": "ops/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"first {sample} documents ({sample_ops} ops) of the same workload, C++ oracle -O3, "
+                      f"one document per task on {threads} std::threads",
+        }
+        log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "ops/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": f"synthetic ({'conflict-farm' if mt else 'map fuzz'} shape, reference XSadd PRNG; "
+                    f"{min(args.unique_docs, docs) if mt else docs} distinct docs per GPU replicated to {docs})",
+            "config": {
+                "workload": ("T1 merge-tree conflict-farm replay" if mt else "M2 SharedMap LWW replay"),
+                "docs_per_gpu": docs,
+                "clients": args.clients,
+                "ops_per_doc": opd,
+                "ops_per_step": n_ops * world,
+                "parallelism": f"doc-shard x{world}",
+            },
+            "hbm_gbps": bytes_per_launch * world / (elapsed / args.steps) / 1e9,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": None,
+                "kernel": "mergeTreeKernel" if mt else "mapLwwKernel",
+                "bytes_per_launch": bytes_per_launch,
+                "avg_kernel_ms": avg_kernel_ms,
+            },
+            "cpu_baseline": cpu,
+            "h2d_gbps": in_bytes / h2d_s / 1e9,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,44 @@
+// kernels.h — host-side launchers of the gfx950 kernels (one .hip translation unit each).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/fmt.h"
+
+namespace fmt_kernels {
+
+// ---- SharedMap LWW (map_lww.hip)
+size_t mapLwwLdsBytes(uint32_t keyBound);
+hipError_t launchMapLww(const fmt_map_op* ops, const uint64_t* offsets, uint32_t nDocs, uint32_t keyBound,
+                        fmt_map_slot* out, int* error, int numCUs, hipStream_t stream);
+
+// ---- merge-tree replay (mergetree.hip)
+struct MtDeviceBatch {
+  const fmt_mt_op* ops;
+  const uint64_t* docOpOffsets;
+  uint32_t nDocs;
+  const uint16_t* text;
+  const uint32_t* docInit;  // (offset, len) per doc or nullptr
+  const uint32_t* propsOff;
+  const uint32_t* propsKv;
+  uint32_t nPropsOps;
+};
+
+struct MtDeviceOut {
+  fmt_mt_doc_result* headers;  // nDocs
+  fmt_mt_leaf* leaves;         // nDocs * capLeaves
+  uint16_t* chars;             // nDocs * capChars
+  fmt_mt_propset* props;       // nDocs * capProps
+};
+
+// Per-document capacities of the LDS-resident engine.
+struct MtCaps {
+  uint32_t leaves, chars, props;
+};
+MtCaps mergeTreeCaps();
+
+// Replays documents docList[0..count) (or all docs when docList == nullptr).
+hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                           uint32_t count, int numCUs, hipStream_t stream);
+
+}  // namespace fmt_kernels

@@ -1,0 +1,63 @@
+// mergetree.hip — merge-tree conflict-farm replay kernel for gfx950.
+//
+// One wavefront replays one document end to end (mt_engine.h); four documents per 256-thread
+// workgroup share the CU, each with its own LDS state (fmt_mt::Scratch, ~8.5 KiB). Documents are
+// independent, so the grid simply strides over them; there is no inter-workgroup communication.
+// The per-document sequential dependency (every op depends on the state its predecessors left) is
+// the reason this kernel is latency/LDS-bound rather than HBM-bound: its compulsory HBM traffic is
+// the 32-byte op record plus payload per op and the converged state written once per document.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "mt_engine.h"
+
+namespace fmt_kernels {
+
+constexpr int kMtWaves = 4;
+
+__global__ __launch_bounds__(64 * kMtWaves) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
+                                                                 const uint32_t* __restrict__ docList,
+                                                                 uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int wave = threadIdx.x >> 6;
+  fmt_mt::Scratch* scratch = reinterpret_cast<fmt_mt::Scratch*>(lds) + wave;
+  for (uint32_t i = blockIdx.x * kMtWaves + wave; i < count; i += gridDim.x * kMtWaves) {
+    const uint32_t d = docList ? docList[i] : i;
+    fmt_mt::DocInputs in;
+    in.ops = batch.ops;
+    in.begin = batch.docOpOffsets[d];
+    in.end = batch.docOpOffsets[d + 1];
+    in.text = batch.text;
+    in.initOff = batch.docInit ? batch.docInit[2 * d] : 0u;
+    in.initLen = batch.docInit ? batch.docInit[2 * d + 1] : 0u;
+    in.propsOff = batch.propsOff;
+    in.propsKv = batch.propsKv;
+    in.nPropsOps = batch.nPropsOps;
+    fmt_mt::DocOutputs o;
+    o.header = out.headers + d;
+    o.leaves = out.leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;
+    o.chars = out.chars + static_cast<size_t>(d) * fmt_mt::kCapChars;
+    o.props = out.props + static_cast<size_t>(d) * fmt_mt::kPropCap;
+    fmt_mt::Doc doc;
+    doc.s = scratch;
+    doc.run(in, o);
+  }
+}
+
+MtCaps mergeTreeCaps() {
+  return MtCaps{static_cast<uint32_t>(fmt_mt::kCapLeaves), static_cast<uint32_t>(fmt_mt::kCapChars),
+                static_cast<uint32_t>(fmt_mt::kPropCap)};
+}
+
+hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                           uint32_t count, int numCUs, hipStream_t stream) {
+  const size_t lds = sizeof(fmt_mt::Scratch) * kMtWaves;
+  const int blocksPerCU = static_cast<int>(160 * 1024 / lds);
+  const uint32_t wanted = (count + kMtWaves - 1) / kMtWaves;
+  const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
+  const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
+  hipLaunchKernelGGL(mergeTreeKernel, dim3(grid), dim3(64 * kMtWaves), lds, stream, batch, out, docList, count);
+  return hipGetLastError();
+}
+
+}  // namespace fmt_kernels

@@ -1,0 +1,383 @@
+// runtime.cpp — the C ABI of include/fmt.h over HIP (host side of libfmt.so).
+//
+// Owns the device, the stream, device buffers and HIP events. Inputs cross host→HBM once per batch
+// in fmt_*_load (the only PCIe traffic); fmt_*_run only launches kernels on resident data, so a
+// caller can time run() alone ("inputs already resident in HBM"). No exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <vector>
+
+#include "../../include/fmt.h"
+#include "kernels.h"
+
+namespace {
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t reserve(size_t n) {
+    if (n <= cap && p != nullptr) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t bytes = (n > 0 ? n : 1) * sizeof(T);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), bytes);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct fmt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool ownStream = false;
+  int numCUs = 256;
+  std::string arch;
+  std::string err;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  fmt_stats stats{};
+
+  // SharedMap
+  DevBuf<fmt_map_op> mapOps;
+  DevBuf<uint64_t> mapOffs;
+  DevBuf<fmt_map_slot> mapOut;
+  DevBuf<int> errWord;
+  uint64_t mapNOps = 0;
+  uint32_t mapDocs = 0, mapKeyBound = 0;
+  bool mapLoaded = false;
+
+  // merge-tree
+  DevBuf<fmt_mt_op> mtOps;
+  DevBuf<uint64_t> mtOffs;
+  DevBuf<uint16_t> mtText;
+  DevBuf<uint32_t> mtInit, mtPropsOff, mtPropsKv;
+  DevBuf<fmt_mt_doc_result> mtHdr;
+  DevBuf<fmt_mt_leaf> mtLeaves;
+  DevBuf<uint16_t> mtChars;
+  DevBuf<fmt_mt_propset> mtProps;
+  uint64_t mtNOps = 0, mtTextLen = 0, mtInsertChars = 0, mtInitChars = 0;
+  uint32_t mtDocs = 0, mtNProps = 0;
+  bool mtHasInit = false, mtLoaded = false;
+};
+
+namespace {
+
+int setErr(fmt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hipErr(fmt_ctx* c, hipError_t e, const char* what) {
+  return setErr(c, FMT_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define FMT_HIP(ctx, expr)                                 \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return hipErr((ctx), e_, #expr); \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int fmt_open(const fmt_config* cfg, fmt_ctx** out) {
+  if (out == nullptr) return FMT_E_USAGE;
+  *out = nullptr;
+  auto* c = new (std::nothrow) fmt_ctx();
+  if (c == nullptr) return FMT_E_DEVICE;
+  *out = c;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return setErr(c, FMT_E_DEVICE, "no HIP device visible");
+  c->device = cfg ? cfg->device : 0;
+  if (c->device < 0 || c->device >= n) return setErr(c, FMT_E_USAGE, "device ordinal out of range");
+  FMT_HIP(c, hipSetDevice(c->device));
+  hipDeviceProp_t prop;
+  FMT_HIP(c, hipGetDeviceProperties(&prop, c->device));
+  c->arch = prop.gcnArchName;
+  c->numCUs = prop.multiProcessorCount;
+  if (c->arch.rfind("gfx950", 0) != 0)
+    return setErr(c, FMT_E_DEVICE, "libfmt is built for gfx950 only; device is " + c->arch);
+  if (cfg && cfg->stream) {
+    c->stream = static_cast<hipStream_t>(cfg->stream);
+  } else {
+    FMT_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->ownStream = true;
+  }
+  FMT_HIP(c, hipEventCreate(&c->ev0));
+  FMT_HIP(c, hipEventCreate(&c->ev1));
+  FMT_HIP(c, c->errWord.reserve(1));
+  return FMT_OK;
+}
+
+void fmt_close(fmt_ctx* c) {
+  if (c == nullptr) return;
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->mapOps.release();
+  c->mapOffs.release();
+  c->mapOut.release();
+  c->errWord.release();
+  c->mtOps.release();
+  c->mtOffs.release();
+  c->mtText.release();
+  c->mtInit.release();
+  c->mtPropsOff.release();
+  c->mtPropsKv.release();
+  c->mtHdr.release();
+  c->mtLeaves.release();
+  c->mtChars.release();
+  c->mtProps.release();
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ownStream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* fmt_last_error(const fmt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int fmt_sync(fmt_ctx* c) {
+  if (c == nullptr) return FMT_E_USAGE;
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  return FMT_OK;
+}
+
+int fmt_get_stats(const fmt_ctx* cc, fmt_stats* out) {
+  auto* c = const_cast<fmt_ctx*>(cc);
+  if (c == nullptr || out == nullptr) return FMT_E_USAGE;
+  if (c->timed) {
+    FMT_HIP(c, hipEventSynchronize(c->ev1));
+    float ms = 0;
+    FMT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->stats.kernel_ms = ms;
+    c->stats.total_ms = ms;
+  }
+  *out = c->stats;
+  return FMT_OK;
+}
+
+int fmt_device_info(fmt_ctx* c, char* buf, size_t cap) {
+  if (c == nullptr || buf == nullptr || cap == 0) return FMT_E_USAGE;
+  std::snprintf(buf, cap, "%s device=%d CUs=%d", c->arch.c_str(), c->device, c->numCUs);
+  return FMT_OK;
+}
+
+// ------------------------------------------------------------------------------ SharedMap
+int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_t* offs, uint32_t nDocs,
+                 uint32_t keyBound) {
+  if (c == nullptr || (nOps > 0 && ops == nullptr) || offs == nullptr || keyBound == 0)
+    return setErr(c, FMT_E_USAGE, "fmt_map_load: bad arguments");
+  if (fmt_kernels::mapLwwLdsBytes(keyBound) > 160 * 1024)
+    return setErr(c, FMT_E_UNSUPPORTED, "key_bound too large for the LDS key-table path");
+  if (offs[0] != 0 || offs[nDocs] != nOps) return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
+  for (uint32_t d = 0; d < nDocs; d++) {
+    if (offs[d + 1] < offs[d]) return setErr(c, FMT_E_USAGE, "doc_op_offsets not monotone");
+    for (uint64_t i = offs[d] + 1; i < offs[d + 1]; i++) {
+      if (ops[i].seq <= ops[i - 1].seq) {
+        char m[128];
+        std::snprintf(m, sizeof m, "doc %u: seq %u after %u (ops must be in increasing seq order)", d,
+                      ops[i].seq, ops[i - 1].seq);
+        return setErr(c, FMT_E_DATA, m);
+      }
+    }
+  }
+  FMT_HIP(c, hipSetDevice(c->device));
+  FMT_HIP(c, c->mapOps.reserve(nOps));
+  FMT_HIP(c, c->mapOffs.reserve(nDocs + 1ull));
+  FMT_HIP(c, c->mapOut.reserve(static_cast<size_t>(nDocs) * keyBound));
+  if (nOps) FMT_HIP(c, hipMemcpyAsync(c->mapOps.p, ops, nOps * sizeof(fmt_map_op), hipMemcpyHostToDevice, c->stream));
+  FMT_HIP(c, hipMemcpyAsync(c->mapOffs.p, offs, (nDocs + 1ull) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  c->mapNOps = nOps;
+  c->mapDocs = nDocs;
+  c->mapKeyBound = keyBound;
+  c->mapLoaded = true;
+  return FMT_OK;
+}
+
+static int runMap(fmt_ctx* c, const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, uint32_t keyBound,
+                  uint64_t nOps, fmt_map_slot* out) {
+  FMT_HIP(c, hipSetDevice(c->device));
+  FMT_HIP(c, hipMemsetAsync(c->errWord.p, 0, sizeof(int), c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
+  FMT_HIP(c, fmt_kernels::launchMapLww(ops, offs, nDocs, keyBound, out, c->errWord.p, c->numCUs, c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  c->stats = fmt_stats{};
+  c->stats.ops = nOps;
+  c->stats.docs = nDocs;
+  c->stats.bytes_read = nOps * sizeof(fmt_map_op) + (nDocs + 1ull) * sizeof(uint64_t);
+  c->stats.bytes_written = static_cast<uint64_t>(nDocs) * keyBound * sizeof(fmt_map_slot);
+  c->stats.launches = 1;
+  return FMT_OK;
+}
+
+int fmt_map_run(fmt_ctx* c) {
+  if (c == nullptr || !c->mapLoaded) return setErr(c, FMT_E_USAGE, "fmt_map_run before fmt_map_load");
+  return runMap(c, c->mapOps.p, c->mapOffs.p, c->mapDocs, c->mapKeyBound, c->mapNOps, c->mapOut.p);
+}
+
+int fmt_map_fetch(fmt_ctx* c, fmt_map_slot* out) {
+  if (c == nullptr || out == nullptr || !c->mapLoaded) return setErr(c, FMT_E_USAGE, "fmt_map_fetch: nothing loaded");
+  int errWord = 0;
+  FMT_HIP(c, hipMemcpyAsync(&errWord, c->errWord.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipMemcpyAsync(out, c->mapOut.p, static_cast<size_t>(c->mapDocs) * c->mapKeyBound * sizeof(fmt_map_slot),
+                            hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  if (errWord) return setErr(c, FMT_E_DATA, "an op referenced a key id >= key_bound");
+  return FMT_OK;
+}
+
+int fmt_map_replay_device(fmt_ctx* c, const fmt_map_op* dOps, const uint64_t* dOffs, uint32_t nDocs,
+                          uint32_t keyBound, fmt_map_slot* dOut) {
+  if (c == nullptr || dOffs == nullptr || dOut == nullptr || keyBound == 0)
+    return setErr(c, FMT_E_USAGE, "fmt_map_replay_device: bad arguments");
+  if (fmt_kernels::mapLwwLdsBytes(keyBound) > 160 * 1024)
+    return setErr(c, FMT_E_UNSUPPORTED, "key_bound too large for the LDS key-table path");
+  return runMap(c, dOps, dOffs, nDocs, keyBound, 0, dOut);
+}
+
+// ------------------------------------------------------------------------------ merge-tree
+int fmt_mt_capacity(uint32_t* maxLeaves, uint32_t* maxChars, uint32_t* maxProps) {
+  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps();
+  if (maxLeaves) *maxLeaves = caps.leaves;
+  if (maxChars) *maxChars = caps.chars;
+  if (maxProps) *maxProps = caps.props;
+  return FMT_OK;
+}
+
+int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
+  if (c == nullptr || b == nullptr || b->doc_op_offsets == nullptr || (b->n_ops && b->ops == nullptr))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_load: bad arguments");
+  const uint32_t n = b->n_docs;
+  if (b->doc_op_offsets[0] != 0 || b->doc_op_offsets[n] != b->n_ops)
+    return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
+  uint64_t insertChars = 0;
+  for (uint64_t i = 0; i < b->n_ops; i++) {
+    const fmt_mt_op& op = b->ops[i];
+    if (op.type == FMT_MT_INSERT) {
+      if (static_cast<uint64_t>(op.payload) + op.len > b->text_len)
+        return setErr(c, FMT_E_DATA, "insert payload outside the text arena");
+      insertChars += op.len;
+    } else if (op.type == FMT_MT_ANNOTATE) {
+      if (op.payload >= b->n_props_ops) return setErr(c, FMT_E_DATA, "annotate props op id out of range");
+    } else if (op.type != FMT_MT_REMOVE) {
+      return setErr(c, FMT_E_UNSUPPORTED, "op type not supported by this engine build");
+    }
+  }
+  uint64_t initChars = 0;
+  if (b->doc_init) {
+    for (uint32_t d = 0; d < n; d++) {
+      if (static_cast<uint64_t>(b->doc_init[2 * d]) + b->doc_init[2 * d + 1] > b->text_len)
+        return setErr(c, FMT_E_DATA, "initial text outside the text arena");
+      initChars += b->doc_init[2 * d + 1];
+    }
+  }
+  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps();
+  FMT_HIP(c, hipSetDevice(c->device));
+  FMT_HIP(c, c->mtOps.reserve(b->n_ops));
+  FMT_HIP(c, c->mtOffs.reserve(n + 1ull));
+  FMT_HIP(c, c->mtText.reserve(b->text_len));
+  FMT_HIP(c, c->mtInit.reserve(2ull * n));
+  FMT_HIP(c, c->mtPropsOff.reserve(b->n_props_ops + 1ull));
+  const uint32_t nKv = b->props_off ? b->props_off[b->n_props_ops] : 0;
+  FMT_HIP(c, c->mtPropsKv.reserve(nKv));
+  FMT_HIP(c, c->mtHdr.reserve(n));
+  FMT_HIP(c, c->mtLeaves.reserve(static_cast<size_t>(n) * caps.leaves));
+  FMT_HIP(c, c->mtChars.reserve(static_cast<size_t>(n) * caps.chars));
+  FMT_HIP(c, c->mtProps.reserve(static_cast<size_t>(n) * caps.props));
+  auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+  };
+  FMT_HIP(c, cp(c->mtOps.p, b->ops, b->n_ops * sizeof(fmt_mt_op)));
+  FMT_HIP(c, cp(c->mtOffs.p, b->doc_op_offsets, (n + 1ull) * sizeof(uint64_t)));
+  FMT_HIP(c, cp(c->mtText.p, b->text, b->text_len * sizeof(uint16_t)));
+  if (b->doc_init) FMT_HIP(c, cp(c->mtInit.p, b->doc_init, 2ull * n * sizeof(uint32_t)));
+  if (b->props_off) {
+    FMT_HIP(c, cp(c->mtPropsOff.p, b->props_off, (b->n_props_ops + 1ull) * sizeof(uint32_t)));
+    FMT_HIP(c, cp(c->mtPropsKv.p, b->props_kv, nKv * sizeof(uint32_t)));
+  } else {
+    FMT_HIP(c, hipMemsetAsync(c->mtPropsOff.p, 0, sizeof(uint32_t), c->stream));
+  }
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  c->mtNOps = b->n_ops;
+  c->mtDocs = n;
+  c->mtTextLen = b->text_len;
+  c->mtNProps = b->n_props_ops;
+  c->mtHasInit = b->doc_init != nullptr;
+  c->mtInsertChars = insertChars;
+  c->mtInitChars = initChars;
+  c->mtLoaded = true;
+  return FMT_OK;
+}
+
+int fmt_mt_run(fmt_ctx* c) {
+  if (c == nullptr || !c->mtLoaded) return setErr(c, FMT_E_USAGE, "fmt_mt_run before fmt_mt_load");
+  FMT_HIP(c, hipSetDevice(c->device));
+  fmt_kernels::MtDeviceBatch db{c->mtOps.p, c->mtOffs.p, c->mtDocs, c->mtText.p,
+                                c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps};
+  fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p};
+  FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
+  FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->numCUs, c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  c->stats = fmt_stats{};
+  c->stats.ops = c->mtNOps;
+  c->stats.docs = c->mtDocs;
+  // Algorithmic bytes: every op record and every inserted UTF-16 unit read once; results written
+  // (headers + leaves + chars + prop sets) are added by fmt_mt_fetch_headers once sizes are known.
+  c->stats.bytes_read = c->mtNOps * sizeof(fmt_mt_op) + (c->mtInsertChars + c->mtInitChars) * 2 +
+                        (c->mtDocs + 1ull) * sizeof(uint64_t);
+  c->stats.bytes_written = static_cast<uint64_t>(c->mtDocs) * sizeof(fmt_mt_doc_result);
+  c->stats.launches = 1;
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_headers(fmt_ctx* c, fmt_mt_doc_result* out) {
+  if (c == nullptr || out == nullptr || !c->mtLoaded) return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_headers: nothing loaded");
+  FMT_HIP(c, hipMemcpyAsync(out, c->mtHdr.p, c->mtDocs * sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  uint64_t w = static_cast<uint64_t>(c->mtDocs) * sizeof(fmt_mt_doc_result);
+  int status = FMT_OK;
+  for (uint32_t d = 0; d < c->mtDocs; d++) {
+    w += out[d].n_leaves * sizeof(fmt_mt_leaf) + out[d].n_chars * 2ull + out[d].n_props * sizeof(fmt_mt_propset);
+    if (out[d].status != FMT_OK && status == FMT_OK) {
+      status = out[d].status;
+      char m[160];
+      std::snprintf(m, sizeof m, "doc %u failed with status %d at seq %d", d, out[d].status, out[d].fail_seq);
+      c->err = m;
+    }
+  }
+  c->stats.bytes_written = w;
+  return status;
+}
+
+int fmt_mt_fetch_doc(fmt_ctx* c, uint32_t doc, fmt_mt_leaf* leaves, uint32_t capLeaves, uint16_t* chars,
+                     uint32_t capChars, fmt_mt_propset* props, uint32_t capProps) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs) return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_doc: bad doc");
+  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps();
+  fmt_mt_doc_result h;
+  FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
+  const uint32_t nl = h.n_leaves < capLeaves ? h.n_leaves : capLeaves;
+  const uint32_t nc = h.n_chars < capChars ? h.n_chars : capChars;
+  const uint32_t np = h.n_props < capProps ? h.n_props : capProps;
+  if (leaves && nl) FMT_HIP(c, hipMemcpy(leaves, c->mtLeaves.p + static_cast<size_t>(doc) * caps.leaves, nl * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
+  if (chars && nc) FMT_HIP(c, hipMemcpy(chars, c->mtChars.p + static_cast<size_t>(doc) * caps.chars, nc * 2ull, hipMemcpyDeviceToHost));
+  if (props && np) FMT_HIP(c, hipMemcpy(props, c->mtProps.p + static_cast<size_t>(doc) * caps.props, np * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// wave.h — the handful of wave64 primitives the merge-tree engine is written against.
+//
+// The engine (mt_engine.h) is SPMD code for ONE wavefront. Per-lane values are `Lane<T>`, read and
+// written inside `FOR_LANES(l) { ... LANE(x) ... }` bodies; everything outside those bodies is
+// wave-uniform. Cross-lane movement goes only through the functions below.
+//
+// On gfx950 (device compilation) a Lane<T> is one register per lane, FOR_LANES runs its body once
+// with l = the lane id, and the primitives are ballot / readlane / shuffles. For host compilation
+// (tests only: tests/_build/libmt_emu.so) a Lane<T> is T[64] and FOR_LANES loops over the 64 lanes,
+// which lets the parity suite run the exact engine source against the oracle without a GPU.
+// Rule that keeps both identical: a FOR_LANES body never reads LDS that another lane writes in the
+// same body (split such code into a read body and a write body).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIP_DEVICE_COMPILE__)
+
+#include <hip/hip_runtime.h>
+#define FMT_DEV __device__ __forceinline__
+#define FMT_GPU 1
+
+template <class T>
+struct Lane {
+  T v;
+};
+#define LANE(x) ((x).v)
+#define FOR_LANES(l) for (int l = static_cast<int>(__lane_id()), l##_once = 1; l##_once; l##_once = 0)
+
+FMT_DEV int waveLane() { return static_cast<int>(__lane_id()); }
+
+// Make a wave-uniform value provably uniform (lives in an SGPR afterwards).
+FMT_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+FMT_DEV uint32_t uni(uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x))); }
+
+FMT_DEV uint64_t ballot(const Lane<bool>& p) { return __ballot(p.v); }
+
+template <class T>
+FMT_DEV T readlane(const Lane<T>& x, int lane) {
+  return static_cast<T>(__builtin_amdgcn_readlane(static_cast<int>(x.v), lane));
+}
+
+template <class T>
+FMT_DEV Lane<T> shflUp1(const Lane<T>& x) {
+  return Lane<T>{static_cast<T>(__shfl_up(static_cast<int>(x.v), 1))};
+}
+
+template <class T>
+FMT_DEV Lane<T> shflDown1(const Lane<T>& x) {
+  return Lane<T>{static_cast<T>(__shfl_down(static_cast<int>(x.v), 1))};
+}
+
+// Exclusive prefix sum across the wave; *total = sum over all lanes.
+FMT_DEV Lane<uint32_t> waveExclusiveSum(const Lane<uint32_t>& x, uint32_t* total) {
+  uint32_t v = x.v;
+  const int lane = waveLane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(v), d));
+    if (lane >= d) v += o;
+  }
+  *total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+  return Lane<uint32_t>{v - x.v};
+}
+
+// Exclusive prefix max across the wave (identity `init` for lane 0).
+FMT_DEV Lane<int32_t> waveExclusiveMax(const Lane<int32_t>& x, int32_t init) {
+  int32_t v = x.v;
+  const int lane = waveLane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t o = __shfl_up(v, d);
+    if (lane >= d) v = v > o ? v : o;
+  }
+  int32_t prev = __shfl_up(v, 1);
+  return Lane<int32_t>{lane == 0 ? init : prev};
+}
+
+FMT_DEV void waveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+#else  // host emulation (tests only)
+
+#include <cstring>
+#define FMT_DEV inline
+#define FMT_GPU 0
+
+template <class T>
+struct Lane {
+  T v[64];
+};
+#define LANE(x) ((x).v[l])
+#define FOR_LANES(l) for (int l = 0; l < 64; l++)
+
+inline int uni(int x) { return x; }
+inline uint32_t uni(uint32_t x) { return x; }
+
+inline uint64_t ballot(const Lane<bool>& p) {
+  uint64_t m = 0;
+  for (int l = 0; l < 64; l++)
+    if (p.v[l]) m |= 1ull << l;
+  return m;
+}
+
+template <class T>
+inline T readlane(const Lane<T>& x, int lane) {
+  return x.v[lane];
+}
+
+template <class T>
+inline Lane<T> shflUp1(const Lane<T>& x) {
+  Lane<T> r;
+  r.v[0] = x.v[0];
+  for (int l = 1; l < 64; l++) r.v[l] = x.v[l - 1];
+  return r;
+}
+
+template <class T>
+inline Lane<T> shflDown1(const Lane<T>& x) {
+  Lane<T> r;
+  for (int l = 0; l < 63; l++) r.v[l] = x.v[l + 1];
+  r.v[63] = x.v[63];
+  return r;
+}
+
+inline Lane<uint32_t> waveExclusiveSum(const Lane<uint32_t>& x, uint32_t* total) {
+  Lane<uint32_t> r;
+  uint32_t acc = 0;
+  for (int l = 0; l < 64; l++) {
+    r.v[l] = acc;
+    acc += x.v[l];
+  }
+  *total = acc;
+  return r;
+}
+
+inline Lane<int32_t> waveExclusiveMax(const Lane<int32_t>& x, int32_t init) {
+  Lane<int32_t> r;
+  int32_t acc = init;
+  for (int l = 0; l < 64; l++) {
+    r.v[l] = acc;
+    if (l == 0) acc = x.v[0];
+    else acc = acc > x.v[l] ? acc : x.v[l];
+  }
+  return r;
+}
+
+inline void waveSync() {}
+
+#endif
+
+FMT_DEV int ctz64(uint64_t m) { return __builtin_ctzll(m); }
+FMT_DEV int ctz32(uint32_t m) { return __builtin_ctz(m); }

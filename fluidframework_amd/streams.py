@@ -34,7 +34,7 @@ MT_OP_DTYPE = np.dtype(
         ("len", "<u2"),
         ("client", "u1"),
         ("type", "u1"),
-        ("reserved", "<u4"),
+        ("flags", "<u4"),
     ]
 )
 assert MT_OP_DTYPE.itemsize == 32
@@ -156,8 +156,11 @@ class _DocBuilder:
         members = contents["ops"] if contents["type"] == MT_GROUP else [contents]
         if not members:
             members = [None]
-        for op in members:
-            self.ops.append(self.owner._pack(op, seq, ref, msn, client))
+        for k, op in enumerate(members):
+            rec = self.owner._pack(op, seq, ref, msn, client)
+            if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
+                rec = rec[:-1] + (1,)
+            self.ops.append(rec)
 
     def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
         self.ops.append(self.owner._pack(op, seq, ref_seq, min_seq, client))

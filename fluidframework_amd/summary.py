@@ -1,0 +1,177 @@
+"""Summary emission from the engine's converged state (host side).
+
+  - SharedMap: SharedMap.summarizeCore (packages/dds/map/src/map.ts:176-246) over the key slots
+    produced by the map kernel; key order is the JS object order of getSerializedStorage
+    (mapKernel.ts:545-551): array-index keys ascending, then Map insertion (birth) order.
+  - SharedString legacy format: SnapshotLegacy.extractSync + emit (merge-tree/src/snapshotlegacy.ts:
+    74-262, snapshotChunks.ts:85-204) over the leaf table produced by the merge-tree kernel.
+Both are byte-identical to JSON.stringify of the reference objects.
+"""
+from __future__ import annotations
+
+import json
+
+from .streams import MAP_ABSENT, MAP_VALUE_UNDEFINED, is_array_index_key
+
+NOT_REMOVED = 0x7FFFFFFF
+TEXT_GRANULARITY = 256          # textSegment.ts:21
+SIZE_OF_FIRST_CHUNK = 10000     # snapshotlegacy.ts:55
+MIN_VALUE_SIZE_SEPARATE_BLOB = 8 * 1024  # map.ts:190
+MAX_SNAPSHOT_BLOB_SIZE = 16 * 1024       # map.ts:194
+
+
+def _q(s: str) -> str:
+    """JSON.stringify of a string (QuoteJSONString, well-formed: lone surrogates escaped)."""
+    out = ['"']
+    for ch in s:
+        c = ord(ch)
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif ch == "\b":
+            out.append("\\b")
+        elif ch == "\f":
+            out.append("\\f")
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ch == "\t":
+            out.append("\\t")
+        elif c < 0x20 or 0xD800 <= c <= 0xDFFF:
+            out.append("\\u%04x" % c)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def _utf16_len(s: str) -> int:
+    return len(s.encode("utf-16-le", "surrogatepass")) // 2
+
+
+def _js_order(keys):
+    idx = sorted((k for k in keys if is_array_index_key(k)), key=int)
+    return idx + [k for k in keys if not is_array_index_key(k)]
+
+
+# ------------------------------------------------------------------------------------------- map
+def map_summary(slots, keys, values):
+    """(header, [blob0, ...]) for one document's key slots (fmt_map_slot array)."""
+    live = [(k, int(s["value"]), int(s["birth_seq"])) for k, s in enumerate(slots) if int(s["value"]) != MAP_ABSENT]
+    live.sort(key=lambda t: t[2])  # Map insertion order = birth order
+    names = {keys[k]: (v, b) for k, v, b in live}
+    order = _js_order([keys[k] for k, _, _ in live])
+
+    def member(name):
+        v = names[name][0]
+        if v == MAP_VALUE_UNDEFINED:
+            return _q(name) + ':{"type":"Plain"}'
+        return _q(name) + ':{"type":"Plain","value":' + values[v] + "}"
+
+    blobs, header_members, size = [], [], 0
+    for name in order:
+        v = names[name][0]
+        vlen = 0 if v == MAP_VALUE_UNDEFINED else _utf16_len(values[v])
+        if v != MAP_VALUE_UNDEFINED and vlen >= MIN_VALUE_SIZE_SEPARATE_BLOB:
+            blobs.append("{" + member(name) + "}")
+        else:
+            size += len("Plain") + 21 + vlen
+            if size > MAX_SNAPSHOT_BLOB_SIZE:
+                blobs.append("{" + ",".join(member(m) for m in _js_order(header_members)) + "}")
+                header_members, size = [], 0
+            header_members.append(name)
+    header = (
+        '{"blobs":[' + ",".join(_q(f"blob{i}") for i in range(len(blobs))) + '],"content":{'
+        + ",".join(member(m) for m in _js_order(header_members)) + "}}"
+    )
+    return header, blobs
+
+
+# ------------------------------------------------------------------------------------- merge-tree
+def _props_obj(kv, keys, values):
+    pairs = [(keys[x >> 16], values[x & 0xFFFF]) for x in kv]
+    names = [k for k, _ in pairs]
+    d = dict(pairs)
+    return "{" + ",".join(_q(k) + ":" + d[k] for k in _js_order(names)) + "}"
+
+
+def _props_match(a, b):
+    """properties.ts:32-61 (undefined ≡ {}), on (key, value) id pairs."""
+    a, b = a or (), b or ()
+    if len(a) != len(b):
+        return False
+    bd = {x >> 16: x for x in b}
+    return all(bd.get(x >> 16) == x for x in a)
+
+
+def legacy_segments(header, leaves, chars, propsets, min_seq):
+    """extractSync: leaves present at PriorPerspective(minSeq, NonCollabClient), merged greedily."""
+    segs = []  # [text, props kv tuple or None]
+    for L in leaves[: int(header["n_leaves"])]:
+        ins, rm = int(L["ins_seq"]), int(L["rm_seq"])
+        if not (ins <= min_seq) or rm <= min_seq:
+            continue
+        o, n = int(L["char_off"]), int(L["len"])
+        text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
+        pid = int(L["props"])
+        props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
+        if segs:
+            prev = segs[-1]
+            if (not prev[0].endswith("\n")
+                    and (_utf16_len(prev[0]) <= TEXT_GRANULARITY or n <= TEXT_GRANULARITY)
+                    and _props_match(prev[1], props)):
+                prev[0] += text
+                continue
+        segs.append([text, props])
+    for s in segs:
+        if s[1] is not None and len(s[1]) == 0:
+            s[1] = None
+    return segs
+
+
+def legacy_summary(header, leaves, chars, propsets, keys, values, chunk_size=SIZE_OF_FIRST_CHUNK):
+    """(header_blob, body_blob or None) of the legacy SharedString summary at the doc's minSeq."""
+    min_seq = int(header["min_seq"])
+    segs = legacy_segments(header, leaves, chars, propsets, min_seq)
+    total_len = sum(_utf16_len(t) for t, _ in segs)
+
+    def chunk(start, approx, is_header):
+        n, length = 0, 0
+        while length < approx and start + n < len(segs):
+            length += _utf16_len(segs[start + n][0])
+            n += 1
+        texts = []
+        for t, p in segs[start : start + n]:
+            texts.append(_q(t) if p is None else '{"text":' + _q(t) + ',"props":' + _props_obj(p, keys, values) + "}")
+        j = (
+            f'{{"chunkStartSegmentIndex":{start},"chunkSegmentCount":{n},"chunkLengthChars":{length},'
+            f'"totalLengthChars":{total_len},"totalSegmentCount":{len(segs)},"chunkSequenceNumber":{min_seq},'
+            f'"segmentTexts":[{",".join(texts)}]'
+        )
+        if is_header:
+            ids = '[{"id":"header"}' + (',{"id":"body"}' if length < total_len else "") + "]"
+            j += (
+                f',"headerMetadata":{{"orderedChunkMetadata":{ids},"sequenceNumber":{min_seq},'
+                f'"totalLength":{total_len},"totalSegmentCount":{len(segs)}}}'
+            )
+        return j + "}", n
+
+    head, n1 = chunk(0, chunk_size, True)
+    body = chunk(n1, total_len, False)[0] if n1 < len(segs) else None
+    return head, body
+
+
+def summary_tree(header_blob, body_blob):
+    """convertSummaryTreeToITree shape of SharedString.summarizeCore's content subtree."""
+    entries = [{"path": "header", "mode": "100644", "type": "Blob",
+                "value": {"contents": header_blob, "encoding": "utf-8"}}]
+    if body_blob is not None:
+        entries.append({"path": "body", "mode": "100644", "type": "Blob",
+                        "value": {"contents": body_blob, "encoding": "utf-8"}})
+    return {"entries": [{"path": "content", "mode": "040000", "type": "Tree", "value": {"entries": entries}}]}
+
+
+def dumps_tree(tree) -> str:
+    return json.dumps(tree, indent=1)

@@ -1,0 +1,111 @@
+"""Synthetic workloads of BASELINE.json's configs (ctypes over libfmtgen.so).
+
+M1/M2: SharedMap fuzz-shaped LWW streams. T1/T2: merge-tree conflict-farm streams. See
+csrc/gen/fmtgen.cpp for how each mirrors the reference's own stochastic generators.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from .streams import MAP_OP_DTYPE, MT_OP_DTYPE, MapBatch, MergeTreeBatch, js_json
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GEN_PATH = os.path.join(HERE, "libfmtgen.so")
+_gen = None
+
+
+def _lib():
+    global _gen
+    if _gen is None:
+        if not os.path.exists(GEN_PATH):
+            subprocess.run(["make", "-s", "-C", os.path.join(HERE, "csrc", "gen")], check=True)
+        L = ctypes.CDLL(GEN_PATH)
+        P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.fmtgen_map.argtypes = [U32, U32, U32, U32, P, P, U32]
+        L.fmtgen_conflict_farm_new.argtypes = [U32, U32, U32, U32, U32, U32, U32,
+                                               ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.fmtgen_conflict_farm_new.restype = P
+        L.fmtgen_conflict_farm_copy.argtypes = [P, U32, P, P, P, U32]
+        L.fmtgen_free.argtypes = [P]
+        _gen = L
+    return _gen
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def default_threads() -> int:
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def map_value_json(value_id: int) -> str:
+    """JSON text of a synthetic map value id (ids < 50 are the integers 1..50)."""
+    return str(value_id + 1) if value_id < 50 else js_json(f"s{value_id}")
+
+
+def map_stream(n_docs: int, ops_per_doc: int, key_pool: int = 20, seed: int = 1, threads=None) -> MapBatch:
+    ops = np.zeros(n_docs * ops_per_doc, dtype=MAP_OP_DTYPE)
+    offs = np.zeros(n_docs + 1, dtype=np.uint64)
+    rc = _lib().fmtgen_map(n_docs, ops_per_doc, key_pool, seed, _p(ops), _p(offs), threads or default_threads())
+    if rc != 0:
+        raise ValueError("fmtgen_map failed")
+    keys = [str(k) for k in range(key_pool)]
+    return MapBatch(ops=ops, doc_op_offsets=offs, key_bound=key_pool, keys=keys, values=_LazyValues())
+
+
+class _LazyValues:
+    """Value dictionary materialized on demand (string values are opaque synthetic ids)."""
+
+    def __getitem__(self, i):
+        return map_value_json(i)
+
+    def __len__(self):
+        return 0x3FFFFFFF
+
+
+CLIENT_NAMES = [chr(ord("A") + i) for i in range(26)] + [chr(ord("a") + i) for i in range(26)] + [
+    chr(ord("0") + i) for i in range(12)
+]
+
+
+def conflict_farm(n_docs: int, n_clients: int = 8, ops_per_doc: int = 2000, min_length: int = 0,
+                  seed: int = 1, replicas: int = 1, threads=None) -> MergeTreeBatch:
+    """Conflict-farm merge-tree streams; `replicas` lays out that many copies of the doc set.
+
+    Props op i is {"client": CLIENT_NAMES[i]} (the 0.40 fixtures' annotate shape).
+    """
+    L = _lib()
+    threads = threads or default_threads()
+    n_ops, n_text = ctypes.c_uint64(), ctypes.c_uint64()
+    h = L.fmtgen_conflict_farm_new(n_docs, n_clients, ops_per_doc, min_length, seed, 0, threads,
+                                   ctypes.byref(n_ops), ctypes.byref(n_text))
+    if not h:
+        raise ValueError("fmtgen_conflict_farm_new failed")
+    try:
+        ops = np.zeros(n_ops.value * replicas, dtype=MT_OP_DTYPE)
+        offs = np.zeros(n_docs * replicas + 1, dtype=np.uint64)
+        text = np.zeros(max(1, n_text.value * replicas), dtype="<u2")
+        rc = L.fmtgen_conflict_farm_copy(h, replicas, _p(ops), _p(offs), _p(text), threads)
+        if rc != 0:
+            raise ValueError(f"fmtgen_conflict_farm_copy failed ({rc})")
+    finally:
+        L.fmtgen_free(h)
+    n_props = len(CLIENT_NAMES)
+    props_off = np.arange(n_props + 1, dtype=np.uint32)
+    values = ["null"] + [js_json(c) for c in CLIENT_NAMES]
+    props_kv = np.array([(0 << 16) | (i + 1) for i in range(n_props)], dtype=np.uint32)
+    return MergeTreeBatch(
+        ops=ops,
+        doc_op_offsets=offs,
+        text=text,
+        doc_init=np.zeros((n_docs * replicas, 2), dtype=np.uint32),
+        props_off=props_off,
+        props_kv=props_kv,
+        keys=["client"],
+        values=values,
+    )

@@ -73,8 +73,11 @@ extern "C" {
 
 /* One sequenced merge-tree message (ISequencedDocumentMessage, driver-definitions protocol.ts:217,
  * with contents IMergeTreeInsertMsg / IMergeTreeRemoveMsg / IMergeTreeAnnotateMsg, ops.ts:112-235).
- * A GROUP message is flattened into consecutive records carrying the same seq; the collab window
- * is advanced once after the last member (client.ts:1358-1379). 32 bytes, naturally aligned. */
+ * A GROUP message is flattened into consecutive records; every member after the first carries
+ * FMT_MT_F_GROUP_CONT and the collab window advances once after the last member
+ * (client.ts:1311-1319, 1358-1379). Separate messages that share a seq (a runtime "bunch") are NOT
+ * flagged: each advances the window, exactly as each applyMsg call does. 32 bytes. */
+#define FMT_MT_F_GROUP_CONT 1u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */
@@ -85,7 +88,7 @@ typedef struct fmt_mt_op {
   uint16_t len;     /* INSERT: text length in UTF-16 units (> 0) */
   uint8_t client;   /* short client id (client.ts:831-855): 1..63 in order of first appearance */
   uint8_t type;     /* FMT_MT_* */
-  uint32_t reserved;
+  uint32_t flags;   /* FMT_MT_F_* */
 } fmt_mt_op;
 
 /* One SharedMap message: {"type":"set","key","value"} / "delete" / "clear"

@@ -25,14 +25,14 @@ int fail(const char* what) {
   return FMT_E_DATA;
 }
 
-// Applies ops[0..n): consecutive records with the same seq form one message.
+// Applies ops[0..n): a record flagged FMT_MT_F_GROUP_CONT continues the previous message.
 int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* arena,
              const uint32_t* propsOff, const uint32_t* propsKv, int32_t* failSeq) {
   for (uint64_t i = 0; i < n; i++) {
     const fmt_mt_op& op = ops[i];
     try {
       mt->applyRemote(op, arena, propsOff, propsKv);
-      if (i + 1 == n || ops[i + 1].seq != op.seq) mt->updateSeqNumbers(op.min_seq, op.seq);
+      if (i + 1 == n || (ops[i + 1].flags & FMT_MT_F_GROUP_CONT) == 0) mt->updateSeqNumbers(op.min_seq, op.seq);
     } catch (const std::exception& e) {
       if (failSeq) *failSeq = op.seq;
       return fail(e.what());

@@ -1,0 +1,108 @@
+"""Result comparison shared by the emulation (CPU) and GPU parity tests.
+
+A document's converged state is compared field by field against the oracle: every leaf in document
+order (tombstones included) with its insert/remove stamps, remove-client set, text, properties and
+parent leaf-block ordinal, plus the collab window and tree depth. Properties are compared by value
+(document-local prop-set ids are an implementation detail).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EMU_PATH = os.path.join(HERE, "_build", "libmt_emu.so")
+_emu = None
+
+
+def emu_lib():
+    global _emu
+    if _emu is None:
+        src = os.path.join(HERE, "emu", "mt_emu.cpp")
+        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("mt_engine.h", "wave.h")]
+        if not os.path.exists(EMU_PATH) or os.path.getmtime(EMU_PATH) < max(os.path.getmtime(d) for d in deps):
+            os.makedirs(os.path.dirname(EMU_PATH), exist_ok=True)
+            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas", "-o",
+                            EMU_PATH, src], check=True)
+        L = ctypes.CDLL(EMU_PATH)
+        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 5
+        L.emu_mt_capacity.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
+        _emu = L
+    return _emu
+
+
+def emu_caps():
+    a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    emu_lib().emu_mt_capacity(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return a.value, b.value, c.value
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def emu_replay(batch):
+    """Run the engine source under host emulation; returns (headers, leaves, chars, props)."""
+    cl, cc, cp = emu_caps()
+    n = batch.n_docs
+    hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(n * cl, dtype=LEAF_DTYPE)
+    chars = np.zeros(n * cc, dtype="<u2")
+    props = np.zeros(n * cp, dtype=PROPSET_DTYPE)
+    b, keep = batch_struct(batch)
+    emu_lib().emu_mt_replay(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props))
+    del keep
+    return hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp)
+
+
+def resolve_props(pid, table):
+    if pid == 0xFFFF:
+        return None
+    ps = table[pid]
+    return tuple(int(x) for x in ps["kv"][: ps["n"]])
+
+
+HEADER_FIELDS = ["status", "cur_seq", "min_seq", "n_leaves", "n_chars", "n_blocks", "depth", "visible_len"]
+LEAF_FIELDS = ["ins_seq", "rm_seq", "rm_clients", "char_off", "len", "ins_client", "block"]
+
+
+def compare_doc(exp, got):
+    """exp/got = (header, leaves[:n], chars[:n_chars], props[:n_props]); returns a list of diffs."""
+    eh, el, ec, ep = exp
+    gh, gl, gc, gp = got
+    diffs = []
+    for f in HEADER_FIELDS:
+        if int(eh[f]) != int(gh[f]):
+            diffs.append(f"header.{f}: expected {int(eh[f])} got {int(gh[f])}")
+    if diffs:
+        return diffs
+    n = int(eh["n_leaves"])
+    for f in LEAF_FIELDS:
+        bad = np.nonzero(el[f][:n] != gl[f][:n])[0]
+        if len(bad):
+            i = int(bad[0])
+            diffs.append(f"leaf[{i}].{f}: expected {el[f][i]} got {gl[f][i]}")
+    ep_res = [resolve_props(int(p), ep) for p in el["props"][:n]]
+    gp_res = [resolve_props(int(p), gp) for p in gl["props"][:n]]
+    for i, (a, b) in enumerate(zip(ep_res, gp_res)):
+        if a != b:
+            diffs.append(f"leaf[{i}].props: expected {a} got {b}")
+            break
+    nc = int(eh["n_chars"])
+    if not np.array_equal(ec[:nc], gc[:nc]):
+        i = int(np.nonzero(ec[:nc] != gc[:nc])[0][0])
+        diffs.append(f"chars differ first at {i}")
+    return diffs
+
+
+def visible_text(hdr, leaves, chars):
+    n = int(hdr["n_leaves"])
+    out = []
+    for L in leaves[:n]:
+        if int(L["rm_seq"]) == 0x7FFFFFFF:
+            o = int(L["char_off"])
+            out.append(chars[o : o + int(L["len"])].tobytes().decode("utf-16-le", "surrogatepass"))
+    return "".join(out)

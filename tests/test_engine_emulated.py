@@ -1,0 +1,47 @@
+"""The merge-tree engine source (mt_engine.h) under host emulation vs the oracle (CPU only).
+
+The same source is compiled into the gfx950 kernel; these tests pin its algorithm before a GPU is
+involved. The GPU tests (test_gpu_parity.py) then repeat the comparison on the device.
+"""
+import numpy as np
+import pytest
+
+from fluidframework_amd import workloads
+from golden_data import prefix_batch, replay_fixtures
+from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
+
+
+@pytest.fixture(scope="module")
+def fixtures_prefix():
+    return prefix_batch(list(replay_fixtures()))
+
+
+def test_emulated_engine_matches_reference_text_checkpoints(fixtures_prefix):
+    batch, expected = fixtures_prefix
+    hdr, leaves, chars, props = emu_replay(batch)
+    assert (hdr["status"] == 0).all(), np.unique(hdr["status"])
+    for d, text in enumerate(expected):
+        assert visible_text(hdr[d], leaves[d], chars[d]) == text, f"doc {d}"
+
+
+def test_emulated_engine_matches_oracle_on_fixtures(orc, fixtures_prefix):
+    batch, _ = fixtures_prefix
+    cl, cc, cp = emu_caps()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch)
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+@pytest.mark.parametrize("n_clients,min_length", [(8, 0), (3, 0), (16, 0), (8, 64)])
+def test_emulated_engine_matches_oracle_on_conflict_farm(orc, n_clients, min_length):
+    batch = workloads.conflict_farm(40, n_clients=n_clients, ops_per_doc=1500, min_length=min_length, seed=7)
+    cl, cc, cp = emu_caps()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch)
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"

@@ -1,0 +1,154 @@
+"""GPU parity: libfmt.so on a real MI355X vs the oracle (bit-exact), through the C ABI.
+
+Run with `pytest -m gpu`. Every comparison is field by field on integer state (no tolerance).
+"""
+import numpy as np
+import pytest
+
+from fluidframework_amd import native, workloads
+from fluidframework_amd.streams import MT_OP_DTYPE, MergeTreeBatch
+from fluidframework_amd.summary import legacy_summary, map_summary
+from golden_data import prefix_batch, replay_fixtures
+from mt_compare import compare_doc, visible_text
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = native.Engine(0)
+    yield e
+    e.close()
+
+
+def _gpu_mt(engine, batch):
+    engine.mt_load(batch)
+    engine.mt_run()
+    engine.sync()
+    hdrs = np.zeros(batch.n_docs, dtype=native.DOC_RESULT_DTYPE)
+    import ctypes
+
+    native.lib().fmt_mt_fetch_headers(engine.h, hdrs.ctypes.data_as(ctypes.c_void_p))
+    return hdrs
+
+
+def _check_against_oracle(orc, engine, batch, docs=None):
+    hdrs = _gpu_mt(engine, batch)
+    cl, cc, cp = native.capacity()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=16, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    docs = range(batch.n_docs) if docs is None else docs
+    for d in docs:
+        leaves, chars, props = engine.mt_doc(d, hdrs[d])
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], leaves, chars, props))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+    return hdrs
+
+
+def test_device_is_gfx950(engine):
+    assert "gfx950" in engine.device_info()
+
+
+def test_map_lww_matches_oracle(orc, engine):
+    batch = workloads.map_stream(4000, 1000, key_pool=20, seed=5)
+    engine.map_load(batch)
+    engine.map_run()
+    got = engine.map_fetch()
+    exp, _ = orc.map_replay(batch, threads=16)
+    assert np.array_equal(got["value"], exp["value"])
+    assert np.array_equal(got["birth_seq"], exp["birth_seq"])
+    s = engine.stats()
+    assert s.ops == len(batch.ops) and s.kernel_ms > 0
+
+
+def test_map_lww_summaries_match_oracle(orc, engine):
+    batch = workloads.map_stream(64, 300, key_pool=20, seed=9)
+    engine.map_load(batch)
+    engine.map_run()
+    got = engine.map_fetch()
+    values = [workloads.map_value_json(i) for i in range(50 + 300)]
+    small = batch.__class__(batch.ops, batch.doc_op_offsets, batch.key_bound, batch.keys, values)
+    for d in range(batch.n_docs):
+        assert map_summary(got[d], batch.keys, values) == orc.map_summary(small, d)
+
+
+def test_map_lww_large_key_pool(orc, engine):
+    batch = workloads.map_stream(512, 2000, key_pool=1000, seed=11)
+    engine.map_load(batch)
+    engine.map_run()
+    got = engine.map_fetch()
+    exp, _ = orc.map_replay(batch, threads=16)
+    assert np.array_equal(got, exp)
+
+
+def test_mt_reference_fixture_checkpoints(orc, engine):
+    """All 30 conflict-farm fixtures × 64 groups: text equals the reference's resultText and the
+    whole converged tree equals the oracle's."""
+    batch, expected = prefix_batch(list(replay_fixtures()))
+    hdrs = _check_against_oracle(orc, engine, batch)
+    for d, text in enumerate(expected):
+        leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+        assert visible_text(hdrs[d], leaves, chars) == text, f"doc {d}"
+
+
+@pytest.mark.parametrize("n_clients,min_length,seed", [(8, 0, 1), (2, 0, 2), (16, 0, 3), (8, 128, 4), (31, 0, 5)])
+def test_mt_conflict_farm_matches_oracle(orc, engine, n_clients, min_length, seed):
+    batch = workloads.conflict_farm(600, n_clients=n_clients, ops_per_doc=2000, min_length=min_length, seed=seed)
+    _check_against_oracle(orc, engine, batch)
+
+
+def test_mt_summaries_match_oracle(orc, engine):
+    batch = workloads.conflict_farm(48, n_clients=8, ops_per_doc=2000, seed=21)
+    hdrs = _gpu_mt(engine, batch)
+    for d in range(batch.n_docs):
+        leaves, chars, props = engine.mt_doc(d, hdrs[d])
+        head, body = legacy_summary(hdrs[d], leaves, chars, props, batch.keys, batch.values)
+        doc = orc.MergeTreeDoc()
+        doc.start_collab(0)
+        o0, o1 = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+        doc.apply(batch.ops[o0:o1], batch.text, batch.props_off, batch.props_kv)
+        eh, eb = doc.summary(batch.keys, batch.values)
+        assert head == eh and body == eb, f"doc {d}"
+
+
+def test_mt_full_size_properties(orc, engine):
+    """T1-shaped batch (20k docs × 2k ops): every doc converges, invariants hold, and a sample
+    of documents is bit-exact with the oracle."""
+    batch = workloads.conflict_farm(2500, n_clients=8, ops_per_doc=2000, seed=33, replicas=8)
+    hdrs = _gpu_mt(engine, batch)
+    assert (hdrs["status"] == 0).all()
+    assert (hdrs["cur_seq"] == 2000).all()
+    # replicas are identical documents in distinct HBM bytes: identical results
+    n = 2500
+    for f in ("n_leaves", "n_chars", "visible_len", "n_blocks", "min_seq"):
+        assert np.array_equal(hdrs[f][:n], hdrs[f][7 * n :])
+    sample = list(range(0, batch.n_docs, 997))
+    sub = _subset(batch, sample)
+    _check_against_oracle(orc, engine, sub)
+
+
+def _subset(batch, docs):
+    ops, offs, init = [], [0], []
+    for d in docs:
+        o0, o1 = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+        ops.append(batch.ops[o0:o1])
+        offs.append(offs[-1] + o1 - o0)
+        init.append(batch.doc_init[d])
+    return MergeTreeBatch(np.concatenate(ops), np.asarray(offs, np.uint64), batch.text, np.asarray(init, np.uint32),
+                          batch.props_off, batch.props_kv, batch.keys, batch.values)
+
+
+def test_mt_reports_capacity_and_data_errors(engine):
+    """Overflowing documents and invalid streams fail per document with a status, never crash."""
+    text = np.full(4096, ord("x"), dtype="<u2")
+    ops = np.zeros(3, dtype=MT_OP_DTYPE)
+    # doc 0: two inserts totalling 3000 chars (> 2048 char capacity)
+    ops[0] = (1, 0, 0, 0, -1, 0, 1500, 1, 0, 0)
+    ops[1] = (2, 1, 0, 0, -1, 1500, 1500, 1, 0, 0)
+    # doc 1: insert past the end of an empty document (DataProcessingError)
+    ops[2] = (1, 0, 0, 5, -1, 0, 3, 1, 0, 0)
+    batch = MergeTreeBatch(ops, np.array([0, 2, 3], np.uint64), text, np.zeros((2, 2), np.uint32),
+                           np.zeros(1, np.uint32), np.zeros(0, np.uint32), [], ["null"])
+    hdrs = _gpu_mt(engine, batch)
+    assert hdrs["status"][0] == native.FMT_E_CAPACITY and hdrs["fail_seq"][0] == 2
+    assert hdrs["status"][1] == native.FMT_E_DATA and hdrs["fail_seq"][1] == 1
