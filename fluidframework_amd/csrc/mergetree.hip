@@ -15,7 +15,7 @@ namespace fmt_kernels {
 
 constexpr int kMtWaves = 4;
 
-__global__ __launch_bounds__(64 * kMtWaves) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
+__global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                  const uint32_t* __restrict__ docList,
                                                                  uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];

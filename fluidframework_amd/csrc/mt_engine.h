@@ -106,7 +106,7 @@ struct DocOutputs {
 
 class Doc {
  public:
-  Lane<uint32_t> W[5][E];
+  Lane<V8> W[5];  // W[f] element e = leaf lane*E + e
   Scratch* s;
   int n = 0;          // leaves
   int nChars = 0;
@@ -122,14 +122,12 @@ class Doc {
   DocInputs in;
 
   // ------------------------------------------------------------------ leaf array primitives
-  FMT_DEV Lane<uint32_t> selectE(const Lane<uint32_t>* arr, int e) const {
+  FMT_DEV Lane<uint32_t> selectE(const Lane<V8>& arr, int e) const {
     Lane<uint32_t> r;
     FOR_LANES(l) {
-      uint32_t v = LANE(arr[0]);
-#pragma unroll
-      for (int k = 1; k < E; k++)
-        if (e == k) v = LANE(arr[k]);
-      LANE(r) = v;
+      V8 t = LANE(arr);
+      launder(t);  // keep the dynamic index on a register value (v_movrels), never a scratch GEP
+      LANE(r) = t[e];
     }
     return r;
   }
@@ -138,8 +136,11 @@ class Doc {
 
   FMT_DEV LeafRec readLeaf(int j) const {
     LeafRec r;
-#pragma unroll
-    for (int f = 0; f < 5; f++) r.w[f] = readField(j, f);
+    r.w[0] = readField(j, 0);
+    r.w[1] = readField(j, 1);
+    r.w[2] = readField(j, 2);
+    r.w[3] = readField(j, 3);
+    r.w[4] = readField(j, 4);
     return r;
   }
 
@@ -147,59 +148,87 @@ class Doc {
     const int lane = j / E, e = j % E;
     FOR_LANES(l) {
       if (l == lane) {
-#pragma unroll
-        for (int k = 0; k < E; k++)
-          if (k == e) LANE(W[f][k]) = v;
+        V8 t = LANE(W[f]);
+        launder(t);
+        t[e] = v;
+        LANE(W[f]) = t;
       }
     }
+  }
+
+  // One field of the leaf array shifted up by one slot from index k, `rv` written at k.
+  FMT_DEV static void shiftUpField(Lane<V8>& w, int k, uint32_t rv) {
+    const Lane<uint32_t> prev7 = shflUp1(selectLast(w));
+    FOR_LANES(l) {
+      V8 v = LANE(w);
+#pragma unroll
+      for (int e = E - 1; e >= 1; e--) {
+        const int idx = l * E + e;
+        v[e] = idx > k ? v[e - 1] : (idx == k ? rv : v[e]);
+      }
+      const int idx0 = l * E;
+      v[0] = idx0 > k ? LANE(prev7) : (idx0 == k ? rv : v[0]);
+      LANE(w) = v;
+    }
+  }
+
+  // One field of the leaf array shifted down by one slot onto index k.
+  FMT_DEV static void shiftDownField(Lane<V8>& w, int k) {
+    const Lane<uint32_t> next0 = shflDown1(selectFirst(w));
+    FOR_LANES(l) {
+      V8 v = LANE(w);
+#pragma unroll
+      for (int e = 0; e < E - 1; e++) {
+        const int idx = l * E + e;
+        v[e] = idx >= k ? v[e + 1] : v[e];
+      }
+      const int idx7 = l * E + E - 1;
+      v[E - 1] = idx7 >= k ? LANE(next0) : v[E - 1];
+      LANE(w) = v;
+    }
+  }
+
+  FMT_DEV static Lane<uint32_t> selectLast(const Lane<V8>& w) {
+    Lane<uint32_t> r;
+    FOR_LANES(l) { LANE(r) = LANE(w)[E - 1]; }
+    return r;
+  }
+
+  FMT_DEV static Lane<uint32_t> selectFirst(const Lane<V8>& w) {
+    Lane<uint32_t> r;
+    FOR_LANES(l) { LANE(r) = LANE(w)[0]; }
+    return r;
   }
 
   // Insert `rec` at index k, shifting leaves k.. up by one.
   FMT_DEV bool insertLeafAt(int k, const LeafRec& rec) {
     if (n >= kCapLeaves) return fail(FMT_E_CAPACITY);
-#pragma unroll
-    for (int f = 0; f < 5; f++) {
-      const Lane<uint32_t> prev7 = shflUp1(W[f][E - 1]);
-      const uint32_t rv = rec.w[f];
-      FOR_LANES(l) {
-#pragma unroll
-        for (int e = E - 1; e >= 1; e--) {
-          const int idx = l * E + e;
-          LANE(W[f][e]) = idx > k ? LANE(W[f][e - 1]) : (idx == k ? rv : LANE(W[f][e]));
-        }
-        const int idx0 = l * E;
-        LANE(W[f][0]) = idx0 > k ? LANE(prev7) : (idx0 == k ? rv : LANE(W[f][0]));
-      }
-    }
+    shiftUpField(W[0], k, rec.w[0]);
+    shiftUpField(W[1], k, rec.w[1]);
+    shiftUpField(W[2], k, rec.w[2]);
+    shiftUpField(W[3], k, rec.w[3]);
+    shiftUpField(W[4], k, rec.w[4]);
     n++;
     return true;
   }
 
   // Remove the leaf at index k, shifting leaves k+1.. down by one.
   FMT_DEV void deleteLeafAt(int k) {
-#pragma unroll
-    for (int f = 0; f < 5; f++) {
-      const Lane<uint32_t> next0 = shflDown1(W[f][0]);
-      FOR_LANES(l) {
-#pragma unroll
-        for (int e = 0; e < E - 1; e++) {
-          const int idx = l * E + e;
-          LANE(W[f][e]) = idx >= k ? LANE(W[f][e + 1]) : LANE(W[f][e]);
-        }
-        const int idx7 = l * E + E - 1;
-        LANE(W[f][E - 1]) = idx7 >= k ? LANE(next0) : LANE(W[f][E - 1]);
-      }
-    }
+    shiftDownField(W[0], k);
+    shiftDownField(W[1], k);
+    shiftDownField(W[2], k);
+    shiftDownField(W[3], k);
+    shiftDownField(W[4], k);
     n--;
   }
 
   // Exclusive prefix of per-leaf values (document order); returns the total.
-  FMT_DEV uint32_t scanLeaves(const Lane<uint32_t>* vals, Lane<uint32_t>* excl) const {
+  FMT_DEV uint32_t scanLeaves(const Lane<V8>& vals, Lane<V8>& excl) const {
     Lane<uint32_t> laneSum;
     FOR_LANES(l) {
       uint32_t t = 0;
 #pragma unroll
-      for (int e = 0; e < E; e++) t += LANE(vals[e]);
+      for (int e = 0; e < E; e++) t += LANE(vals)[e];
       LANE(laneSum) = t;
     }
     uint32_t total;
@@ -208,8 +237,8 @@ class Doc {
       uint32_t acc = LANE(base);
 #pragma unroll
       for (int e = 0; e < E; e++) {
-        LANE(excl[e]) = acc;
-        acc += LANE(vals[e]);
+        LANE(excl)[e] = acc;
+        acc += LANE(vals)[e];
       }
     }
     return total;
@@ -217,35 +246,35 @@ class Doc {
 
   // Visible length of every leaf from PriorPerspective(refSeq, client) (perspective.ts:80-93).
   // Leaves removed at/below minSeq are never present for such a perspective (refSeq >= minSeq).
-  FMT_DEV void visLengths(int refSeq, int client, Lane<uint32_t>* vis) const {
+  FMT_DEV void visLengths(int refSeq, int client, Lane<V8>& vis) const {
     FOR_LANES(l) {
 #pragma unroll
       for (int e = 0; e < E; e++) {
         const int idx = l * E + e;
-        const uint32_t w0 = LANE(W[0][e]);
-        const int32_t ins = static_cast<int32_t>(LANE(W[1][e]));
-        const int32_t rm = static_cast<int32_t>(LANE(W[2][e]));
-        const uint32_t mask = LANE(W[3][e]);
-        const int32_t ic = fClient(LANE(W[4][e]));
+        const uint32_t w0 = LANE(W[0])[e];
+        const int32_t ins = static_cast<int32_t>(LANE(W[1])[e]);
+        const int32_t rm = static_cast<int32_t>(LANE(W[2])[e]);
+        const uint32_t mask = LANE(W[3])[e];
+        const int32_t ic = fClient(LANE(W[4])[e]);
         const bool present = idx < n && (ins <= refSeq || ic == client) &&
                              !(rm <= refSeq || ((mask >> client) & 1u));
-        LANE(vis[e]) = present ? fLen(w0) : 0u;
+        LANE(vis)[e] = present ? fLen(w0) : 0u;
       }
     }
   }
 
   // Char offset of every leaf (all leaves, tombstones included).
-  FMT_DEV void charStarts(Lane<uint32_t>* cst) const {
-    Lane<uint32_t> lens[E];
+  FMT_DEV void charStarts(Lane<V8>& cst) const {
+    Lane<V8> lens;
     FOR_LANES(l) {
 #pragma unroll
-      for (int e = 0; e < E; e++) LANE(lens[e]) = (l * E + e) < n ? fLen(LANE(W[0][e])) : 0u;
+      for (int e = 0; e < E; e++) LANE(lens)[e] = (l * E + e) < n ? fLen(LANE(W[0])[e]) : 0u;
     }
     scanLeaves(lens, cst);
   }
 
   FMT_DEV uint32_t charStartOf(int j) const {
-    Lane<uint32_t> cst[E];
+    Lane<V8> cst;
     charStarts(cst);
     return j >= n ? static_cast<uint32_t>(nChars) : readlane(selectE(cst, j % E), j / E);
   }
@@ -258,7 +287,7 @@ class Doc {
       uint32_t fe = E;
 #pragma unroll
       for (int e = E - 1; e >= 0; e--)
-        if (l * E + e < n && fBlk(LANE(W[0][e])) == b) fe = e;
+        if (l * E + e < n && fBlk(LANE(W[0])[e]) == b) fe = e;
       LANE(firstE) = fe;
       LANE(has) = fe < E;
     }
@@ -275,7 +304,7 @@ class Doc {
       uint32_t he = E;
 #pragma unroll
       for (int e = 0; e < E; e++)
-        if (l * E + e < n && fId(LANE(W[4][e])) == id) he = e;
+        if (l * E + e < n && fId(LANE(W[4])[e]) == id) he = e;
       LANE(hitE) = he;
       LANE(has) = he < E;
     }
@@ -353,8 +382,8 @@ class Doc {
       for (int e = 0; e < E; e++) {
         const int idx = l * E + e;
         if (idx >= first && idx < first + count) {
-          const uint32_t w0 = LANE(W[0][e]);
-          LANE(W[0][e]) = mkW0(fLen(w0), b, fProps(w0));
+          const uint32_t w0 = LANE(W[0])[e];
+          LANE(W[0])[e] = mkW0(fLen(w0), b, fProps(w0));
         }
       }
     }
@@ -458,17 +487,6 @@ class Doc {
     return x;
   }
 
-  // mergeTree.ts:812-822 addToLRUSet
-  FMT_DEV void addToLRU(int j, int seq) {
-    const uint32_t w0 = readField(j, 0);
-    const int b = static_cast<int>(fBlk(w0));
-    if (uni(static_cast<int>(s->blk[b].needsScour)) != 1 && seq > curSeq) {
-      s->blk[b].needsScour = 1;
-      waveSync();
-      heapAdd(seq, fId(readField(j, 4)));
-    }
-  }
-
   // ------------------------------------------------------------------ prop sets
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {  // properties.ts:32-61
     if (a == b) return true;
@@ -492,7 +510,7 @@ class Doc {
 
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
-    uint32_t kv[FMT_MT_PROPS_MAX];
+    V4 kv;
     uint32_t cnt = 0;
     if (old != kPropsUndef) {
       cnt = uni(s->props[old].n);
@@ -544,57 +562,8 @@ class Doc {
   }
 
   // ------------------------------------------------------------------ ops
-  // mergeTree.ts:1798-1808 ensureIntervalBoundary
-  FMT_DEV void ensureBoundary(int pos, int refSeq, int client) {
-    Lane<uint32_t> vis[E], st[E];
-    visLengths(refSeq, client, vis);
-    scanLeaves(vis, st);
-    Lane<uint32_t> hitE;
-    Lane<bool> has;
-    FOR_LANES(l) {
-      uint32_t he = E;
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const int sp = static_cast<int>(LANE(st[e]));
-        if (sp < pos && pos < sp + static_cast<int>(LANE(vis[e]))) he = e;
-      }
-      LANE(hitE) = he;
-      LANE(has) = he < E;
-    }
-    const uint64_t m = ballot(has);
-    if (m == 0) return;
-    const int lane = ctz64(m);
-    const int e = static_cast<int>(readlane(hitE, lane));
-    const int j = lane * E + e;
-    const int offset = pos - static_cast<int>(readlane(selectE(st, e), lane));
-    LeafRec rec = readLeaf(j);
-    const uint32_t len = fLen(rec.w[0]);
-    LeafRec tail = rec;
-    tail.w[0] = mkW0(len - static_cast<uint32_t>(offset), fBlk(rec.w[0]), fProps(rec.w[0]));
-    tail.w[4] = mkW4(nextId++, fClient(rec.w[4]));
-    writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(rec.w[0]), fProps(rec.w[0])));
-    if (!insertLeafAt(j + 1, tail)) return;
-    childAdded(static_cast<int>(fBlk(rec.w[0])));
-  }
-
-  // Leaves of positive view length inside [start, end) → per-lane bit masks.
-  FMT_DEV Lane<uint32_t> rangeHits(int start, int end, int refSeq, int client) const {
-    Lane<uint32_t> vis[E], st[E], hits;
-    visLengths(refSeq, client, vis);
-    scanLeaves(vis, st);
-    FOR_LANES(l) {
-      uint32_t h = 0;
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const int sp = static_cast<int>(LANE(st[e]));
-        if (LANE(vis[e]) > 0 && sp >= start && sp < end) h |= 1u << e;
-      }
-      LANE(hits) = h;
-    }
-    return hits;
-  }
-
-  // addToLRUSet for every hit leaf in document order: only the first hit of each block can add.
+  // addToLRUSet for every hit leaf in document order: only the first hit of each block can add
+  // (the first one sets needsScour, mergeTree.ts:812-822).
   FMT_DEV void lruForHits(const Lane<uint32_t>& hits, int seq) {
     // exclusive max-scan of (index << 8 | block) over hit leaves gives each leaf's previous hit
     Lane<int32_t> laneLast;
@@ -602,7 +571,7 @@ class Doc {
       int32_t last = -1;
 #pragma unroll
       for (int e = 0; e < E; e++)
-        if ((LANE(hits) >> e) & 1u) last = ((l * E + e) << 8) | static_cast<int32_t>(fBlk(LANE(W[0][e])));
+        if ((LANE(hits) >> e) & 1u) last = ((l * E + e) << 8) | static_cast<int32_t>(fBlk(LANE(W[0])[e]));
       LANE(laneLast) = last;
     }
     const Lane<int32_t> before = waveExclusiveMax(laneLast, -1);
@@ -614,7 +583,7 @@ class Doc {
 #pragma unroll
       for (int e = 0; e < E; e++) {
         if ((LANE(hits) >> e) & 1u) {
-          const int32_t b = static_cast<int32_t>(fBlk(LANE(W[0][e])));
+          const int32_t b = static_cast<int32_t>(fBlk(LANE(W[0])[e]));
           if (prev < 0 || (prev & 0xFF) != b) c |= 1u << e;
           prev = ((l * E + e) << 8) | b;
         }
@@ -629,138 +598,184 @@ class Doc {
       while (c) {
         const int e = ctz32(c);
         c &= c - 1;
-        addToLRU(lane * E + e, seq);
-        if (status != FMT_OK) return;
+        const int j = lane * E + e;
+        const int b = static_cast<int>(fBlk(readField(j, 0)));
+        if (uni(static_cast<int>(s->blk[b].needsScour)) != 1 && seq > curSeq) {
+          s->blk[b].needsScour = 1;
+          waveSync();
+          heapAdd(seq, fId(readField(j, 4)));
+          if (status != FMT_OK) return;
+        }
       }
       m &= m - 1;
     }
   }
 
-  // mergeTree.ts:1484-1517 insertSegments (blockInsert without obliterates)
-  FMT_DEV void insertOp(const fmt_mt_op& op) {
-    const int refSeq = op.ref_seq, client = op.client, pos = op.pos1;
-    ensureBoundary(pos, refSeq, client);
-    if (status != FMT_OK) return;
-    const int len = op.len;
-    if (len > 0) {
-      Lane<uint32_t> vis[E], st[E];
+  // One member op of a remote message (client.ts:1291-1327). The phases share one view scan:
+  //   phase < nb : ensureIntervalBoundary at pos1 (and pos2) — mergeTree.ts:1798-1808: split the
+  //                unique leaf that strictly contains the position in the op's view;
+  //   phase == nb: insert (mergeTree.ts:1484-1750) or collect the nodeMap range (mergeTree.ts:
+  //                2961-3020) for remove / annotate.
+  FMT_DEV void applyOp(const fmt_mt_op& op) {
+    const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
+    const bool isInsert = op.type == FMT_MT_INSERT;
+    const int nb = isInsert ? 1 : 2;
+    Lane<uint32_t> hits;
+    FOR_LANES(l) { LANE(hits) = 0u; }
+    for (int phase = 0;; phase++) {
+      Lane<V8> vis, st;
       visLengths(refSeq, client, vis);
       const uint32_t total = scanLeaves(vis, st);
-      Lane<uint32_t> anchorE;
-      Lane<bool> has;
-      FOR_LANES(l) {
-        uint32_t ae = E;
-#pragma unroll
-        for (int e = E - 1; e >= 0; e--) {
-          const int idx = l * E + e;
-          const bool undefinedLen = static_cast<int32_t>(LANE(W[2][e])) <= minSeq;
-          const bool skipped = undefinedLen && idx != n - 1;
-          if (idx < n && !skipped && static_cast<int>(LANE(st[e])) == pos) ae = e;
-        }
-        LANE(anchorE) = ae;
-        LANE(has) = ae < E;
-      }
-      const uint64_t m = ballot(has);
-      int j;
-      int blk;
-      if (m != 0) {
-        const int lane = ctz64(m);
-        j = lane * E + static_cast<int>(readlane(anchorE, lane));
-        blk = static_cast<int>(fBlk(readField(j, 0)));
-      } else {
-        if (pos != static_cast<int>(total)) {  // "MergeTree insert failed"
-          fail(FMT_E_DATA);
-          return;
-        }
-        j = n;
-        blk = n > 0 ? static_cast<int>(fBlk(readField(n - 1, 0))) : root;
-      }
-      if (nChars + len > kCapChars) {
-        fail(FMT_E_CAPACITY);
-        return;
-      }
-      const int cpos = static_cast<int>(charStartOf(j));
-      charsShiftUp(cpos, len);
-      const uint16_t* src = in.text + op.payload;
-      FOR_LANES(l) {
-        for (int t = l; t < len; t += 64) s->chars[cpos + t] = src[t];
-      }
-      waveSync();
-      nChars += len;
+      int insIdx = -1, blk = 0;
       LeafRec rec;
-      rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), kPropsUndef);
-      rec.w[1] = static_cast<uint32_t>(op.seq);
-      rec.w[2] = static_cast<uint32_t>(kNotRemoved);
-      rec.w[3] = 0;
-      rec.w[4] = mkW4(nextId++, client);
-      if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
-        s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
-        waveSync();
-      }
-      if (!insertLeafAt(j, rec)) return;
-      childAdded(blk);
-      if (status != FMT_OK) return;
-      addToLRU(j, op.seq);
-      if (status != FMT_OK) return;
-    }
-    zamboni();
-  }
-
-  // mergeTree.ts:2292-2383 markRangeRemoved
-  FMT_DEV void removeOp(const fmt_mt_op& op) {
-    const int refSeq = op.ref_seq, client = op.client;
-    ensureBoundary(op.pos1, refSeq, client);
-    ensureBoundary(op.pos2, refSeq, client);
-    if (status != FMT_OK) return;
-    const Lane<uint32_t> hits = rangeHits(op.pos1, op.pos2, refSeq, client);
-    const int seq = op.seq;
-    FOR_LANES(l) {
+      if (phase < nb) {
+        const int pos = phase == 0 ? op.pos1 : op.pos2;
+        Lane<uint32_t> hitE;
+        Lane<bool> has;
+        FOR_LANES(l) {
+          uint32_t he = E;
 #pragma unroll
-      for (int e = 0; e < E; e++) {
-        if ((LANE(hits) >> e) & 1u) {
-          const int32_t rm = static_cast<int32_t>(LANE(W[2][e]));
-          LANE(W[2][e]) = static_cast<uint32_t>(rm < seq ? rm : seq);
-          LANE(W[3][e]) |= 1u << client;
+          for (int e = 0; e < E; e++) {
+            const int sp = static_cast<int>(LANE(st)[e]);
+            if (sp < pos && pos < sp + static_cast<int>(LANE(vis)[e])) he = e;
+          }
+          LANE(hitE) = he;
+          LANE(has) = he < E;
         }
+        const uint64_t m = ballot(has);
+        if (m != 0) {
+          const int lane = ctz64(m);
+          const int e = static_cast<int>(readlane(hitE, lane));
+          const int j = lane * E + e;
+          const int offset = pos - static_cast<int>(readlane(selectE(st, e), lane));
+          const uint32_t w0 = readField(j, 0), w4 = readField(j, 4);
+          rec.w[0] = mkW0(fLen(w0) - static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
+          rec.w[1] = readField(j, 1);
+          rec.w[2] = readField(j, 2);
+          rec.w[3] = readField(j, 3);
+          rec.w[4] = mkW4(nextId++, fClient(w4));
+          writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0)));
+          insIdx = j + 1;
+          blk = static_cast<int>(fBlk(w0));
+        }
+      } else if (isInsert) {
+        const int pos = op.pos1, len = op.len;
+        if (len > 0) {
+          // anchor: the first leaf whose view prefix equals pos, leaves removed at/below minSeq
+          // skipped except the very last leaf (mergeTree.ts:1862-1875)
+          Lane<uint32_t> anchorE;
+          Lane<bool> has;
+          FOR_LANES(l) {
+            uint32_t ae = E;
+#pragma unroll
+            for (int e = E - 1; e >= 0; e--) {
+              const int idx = l * E + e;
+              const bool undefinedLen = static_cast<int32_t>(LANE(W[2])[e]) <= minSeq;
+              const bool skipped = undefinedLen && idx != n - 1;
+              if (idx < n && !skipped && static_cast<int>(LANE(st)[e]) == pos) ae = e;
+            }
+            LANE(anchorE) = ae;
+            LANE(has) = ae < E;
+          }
+          const uint64_t m = ballot(has);
+          if (m != 0) {
+            const int lane = ctz64(m);
+            insIdx = lane * E + static_cast<int>(readlane(anchorE, lane));
+            blk = static_cast<int>(fBlk(readField(insIdx, 0)));
+          } else {
+            if (pos != static_cast<int>(total)) {  // "MergeTree insert failed" (mergeTree.ts:1629)
+              fail(FMT_E_DATA);
+              return;
+            }
+            insIdx = n;
+            blk = n > 0 ? static_cast<int>(fBlk(readField(n - 1, 0))) : root;
+          }
+          if (nChars + len > kCapChars) {
+            fail(FMT_E_CAPACITY);
+            return;
+          }
+          const int cpos = static_cast<int>(charStartOf(insIdx));
+          charsShiftUp(cpos, len);
+          const uint16_t* src = in.text + op.payload;
+          FOR_LANES(l) {
+            for (int t = l; t < len; t += 64) s->chars[cpos + t] = src[t];
+          }
+          waveSync();
+          nChars += len;
+          rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), kPropsUndef);
+          rec.w[1] = static_cast<uint32_t>(seq);
+          rec.w[2] = static_cast<uint32_t>(kNotRemoved);
+          rec.w[3] = 0;
+          rec.w[4] = mkW4(nextId++, client);
+          if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
+            s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
+            waveSync();
+          }
+        }
+      } else {
+        const int start = op.pos1, end = op.pos2;
+        FOR_LANES(l) {
+          uint32_t h = 0;
+#pragma unroll
+          for (int e = 0; e < E; e++) {
+            const int sp = static_cast<int>(LANE(st)[e]);
+            if (LANE(vis)[e] > 0 && sp >= start && sp < end) h |= 1u << e;
+          }
+          LANE(hits) = h;
+        }
+        break;
+      }
+      if (insIdx >= 0) {
+        if (!insertLeafAt(insIdx, rec)) return;
+        childAdded(blk);
+        if (status != FMT_OK) return;
+      }
+      if (phase >= nb) {
+        if (insIdx >= 0) {
+          const int lane = insIdx / E, e = insIdx % E;
+          FOR_LANES(l) { LANE(hits) = l == lane ? (1u << e) : 0u; }
+        }
+        break;
       }
     }
-    lruForHits(hits, seq);
-    if (status != FMT_OK) return;
-    zamboni();
-  }
-
-  // mergeTree.ts:2009-2081 annotateRange
-  FMT_DEV void annotateOp(const fmt_mt_op& op) {
-    const int refSeq = op.ref_seq, client = op.client;
-    ensureBoundary(op.pos1, refSeq, client);
-    ensureBoundary(op.pos2, refSeq, client);
-    if (status != FMT_OK) return;
-    const Lane<uint32_t> hits = rangeHits(op.pos1, op.pos2, refSeq, client);
-    Lane<uint32_t> todo = hits;
-    for (;;) {
-      Lane<bool> has;
-      FOR_LANES(l) { LANE(has) = LANE(todo) != 0; }
-      const uint64_t m = ballot(has);
-      if (m == 0) break;
-      const int lane = ctz64(m);
-      const int e = ctz32(readlane(todo, lane));
-      const uint32_t old = fProps(readField(lane * E + e, 0));
-      const uint32_t nw = applyProps(old, op.payload);
-      if (status != FMT_OK) return;
+    if (op.type == FMT_MT_REMOVE) {
+      // markRangeRemoved (mergeTree.ts:2292-2383): first remove stays the lowest seq
       FOR_LANES(l) {
 #pragma unroll
-        for (int k = 0; k < E; k++) {
-          if (((LANE(todo) >> k) & 1u) && fProps(LANE(W[0][k])) == old) {
-            const uint32_t w0 = LANE(W[0][k]);
-            LANE(W[0][k]) = mkW0(fLen(w0), fBlk(w0), nw);
-            LANE(todo) &= ~(1u << k);
+        for (int e = 0; e < E; e++) {
+          if ((LANE(hits) >> e) & 1u) {
+            const int32_t rm = static_cast<int32_t>(LANE(W[2])[e]);
+            LANE(W[2])[e] = static_cast<uint32_t>(rm < seq ? rm : seq);
+            LANE(W[3])[e] |= 1u << client;
+          }
+        }
+      }
+    } else if (op.type == FMT_MT_ANNOTATE) {
+      // annotateRange (mergeTree.ts:2009-2081): one prop-set transition per distinct old set
+      Lane<uint32_t> todo = hits;
+      for (;;) {
+        Lane<bool> has;
+        FOR_LANES(l) { LANE(has) = LANE(todo) != 0; }
+        const uint64_t m = ballot(has);
+        if (m == 0) break;
+        const int lane = ctz64(m);
+        const int e = ctz32(readlane(todo, lane));
+        const uint32_t old = fProps(readField(lane * E + e, 0));
+        const uint32_t nw = applyProps(old, op.payload);
+        if (status != FMT_OK) return;
+        FOR_LANES(l) {
+#pragma unroll
+          for (int k = 0; k < E; k++) {
+            if (((LANE(todo) >> k) & 1u) && fProps(LANE(W[0])[k]) == old) {
+              const uint32_t w0 = LANE(W[0])[k];
+              LANE(W[0])[k] = mkW0(fLen(w0), fBlk(w0), nw);
+              LANE(todo) &= ~(1u << k);
+            }
           }
         }
       }
     }
-    lruForHits(hits, op.seq);
-    if (status != FMT_OK) return;
-    zamboni();
+    lruForHits(hits, seq);
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
@@ -770,7 +785,7 @@ class Doc {
     const int cnt = uni(static_cast<int>(s->blk[b].count));
     if (cnt == 0) return 0;
     const int first = firstLeafOf(static_cast<uint32_t>(b));
-    Lane<uint32_t> cst[E];
+    Lane<V8> cst;
     charStarts(cst);
     // serial decisions over <= 7 leaves: keep, merge into the previous kept leaf, or drop
     uint32_t mergeMask = 0, dropMask = 0;
@@ -780,18 +795,18 @@ class Doc {
     int kept = 0;
     for (int k = 0; k < cnt; k++) {
       const int j = first + k;
-      const LeafRec r = readLeaf(j);
-      const uint32_t len = fLen(r.w[0]);
-      const int32_t ins = static_cast<int32_t>(r.w[1]);
-      const int32_t rm = static_cast<int32_t>(r.w[2]);
-      const uint32_t cs = readlane(selectE(cst, j % E), j / E);
-      const bool lastNl = len > 0 && uni(static_cast<uint32_t>(s->chars[cs + len - 1])) == 10u;
+      const uint32_t w0 = readField(j, 0);
+      const uint32_t len = fLen(w0);
+      const int32_t ins = static_cast<int32_t>(readField(j, 1));
+      const int32_t rm = static_cast<int32_t>(readField(j, 2));
       if (rm == kNotRemoved) {
         if (ins <= minSeq) {
+          const uint32_t cs = readlane(selectE(cst, j % E), j / E);
+          const bool lastNl = len > 0 && uni(static_cast<uint32_t>(s->chars[cs + len - 1])) == 10u;
           const bool canAppend = prev >= 0 && !prevNl &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) ||
                                   len <= static_cast<uint32_t>(kGranularity)) &&
-                                 propsMatch(prevProps, fProps(r.w[0])) && len > 0;
+                                 propsMatch(prevProps, fProps(w0)) && len > 0;
           if (canAppend) {
             mergeMask |= 1u << k;
             prevLen += len;
@@ -801,8 +816,8 @@ class Doc {
           } else {
             prev = len > 0 ? j : -1;
             prevLen = len;
-            prevProps = fProps(r.w[0]);
-            prevBlk = fBlk(r.w[0]);
+            prevProps = fProps(w0);
+            prevBlk = fBlk(w0);
             prevNl = lastNl;
             kept++;
           }
@@ -834,79 +849,52 @@ class Doc {
     return kept;
   }
 
-  // zamboni.ts:83-139 packParent, iterated up the tree.
-  FMT_DEV void packParent(int p) {
-    for (;;) {
-      const int pc = uni(static_cast<int>(s->blk[p].count));
-      int total = 0;
-      const bool leafLevel = pc > 0 && uni(static_cast<int>(s->blk[uni(static_cast<int>(s->blk[p].child[0]))].leaf)) != 0;
-      int firstLeaf = -1;
-      if (leafLevel) {
-        for (int i = 0; i < pc; i++) {
-          const int c = uni(static_cast<int>(s->blk[p].child[i]));
-          const int kept = scourLeafBlock(c);
-          if (status != FMT_OK) return;
-          s->blk[c].count = static_cast<uint8_t>(kept);
-          waveSync();
-          if (kept > 0 && firstLeaf < 0) firstLeaf = firstLeafOf(static_cast<uint32_t>(c));
-          total += kept;
+  // packParent redistribution (zamboni.ts:83-139) of `total` held children into
+  // min(7, total/4) (>= 1) new blocks; leaf level re-tags the contiguous leaves, interior level
+  // re-parents the grandchildren listed in s->tmp.
+  FMT_DEV void redistribute(int p, int total, bool leafLevel, int firstLeaf) {
+    const int pc = uni(static_cast<int>(s->blk[p].count));
+    for (int i = 0; i < pc; i++) freeBlk(uni(static_cast<int>(s->blk[p].child[i])));
+    if (total > 0) {
+      int nb = total / (kMaxNodes / 2);
+      if (nb > kMaxNodes - 1) nb = kMaxNodes - 1;
+      if (nb < 1) nb = 1;
+      const int base = total / nb;
+      int rem = total % nb;
+      int consumed = 0;
+      for (int q = 0; q < nb; q++) {
+        int cnt = base;
+        if (rem > 0) {
+          cnt++;
+          rem--;
         }
-      } else {
-        for (int i = 0; i < pc; i++) {
-          const int c = uni(static_cast<int>(s->blk[p].child[i]));
-          const int cc = uni(static_cast<int>(s->blk[c].count));
-          for (int k = 0; k < cc; k++) s->tmp[total++] = uni(static_cast<int>(s->blk[c].child[k]));
+        const int id = allocBlk(leafLevel ? 1 : 0);
+        if (id < 0) return;
+        s->blk[id].count = static_cast<uint8_t>(cnt);
+        s->blk[id].parent = static_cast<uint8_t>(p);
+        if (leafLevel) {
+          tagLeaves(firstLeaf + consumed, cnt, static_cast<uint32_t>(id));
+        } else {
+          for (int k = 0; k < cnt; k++) {
+            const int g = uni(static_cast<int>(s->tmp[consumed + k]));
+            s->blk[id].child[k] = static_cast<uint8_t>(g);
+            s->blk[g].parent = static_cast<uint8_t>(id);
+          }
         }
+        s->blk[p].child[q] = static_cast<uint8_t>(id);
         waveSync();
+        consumed += cnt;
       }
-      for (int i = 0; i < pc; i++) freeBlk(uni(static_cast<int>(s->blk[p].child[i])));
-      if (total > 0) {
-        constexpr int half = kMaxNodes / 2;
-        int nb = total / half;
-        if (nb > kMaxNodes - 1) nb = kMaxNodes - 1;
-        if (nb < 1) nb = 1;
-        const int base = total / nb;
-        int rem = total % nb;
-        int consumed = 0;
-        for (int q = 0; q < nb; q++) {
-          int cnt = base;
-          if (rem > 0) {
-            cnt++;
-            rem--;
-          }
-          const int id = allocBlk(leafLevel ? 1 : 0);
-          if (id < 0) return;
-          s->blk[id].count = static_cast<uint8_t>(cnt);
-          s->blk[id].parent = static_cast<uint8_t>(p);
-          if (leafLevel) {
-            tagLeaves(firstLeaf + consumed, cnt, static_cast<uint32_t>(id));
-          } else {
-            for (int k = 0; k < cnt; k++) {
-              const int g = uni(static_cast<int>(s->tmp[consumed + k]));
-              s->blk[id].child[k] = static_cast<uint8_t>(g);
-              s->blk[g].parent = static_cast<uint8_t>(id);
-            }
-          }
-          s->blk[p].child[q] = static_cast<uint8_t>(id);
-          waveSync();
-          consumed += cnt;
-        }
-        s->blk[p].count = static_cast<uint8_t>(nb);
-      } else {
-        s->blk[p].count = 0;
-        if (p == root) s->blk[p].leaf = 1;
-      }
-      waveSync();
-      const int pp = uni(static_cast<int>(s->blk[p].parent));
-      if (uni(static_cast<int>(s->blk[p].count)) < kMaxNodes / 2 && pp != static_cast<int>(kNoBlk)) {
-        p = pp;
-        continue;
-      }
-      return;
+      s->blk[p].count = static_cast<uint8_t>(nb);
+    } else {
+      s->blk[p].count = 0;
+      if (p == root) s->blk[p].leaf = 1;
     }
+    waveSync();
   }
 
-  // zamboni.ts:33-80
+  // zamboni.ts:33-80, with packParent (zamboni.ts:83-139) folded in so that every block scour —
+  // the popped block's own and each sibling's during packParent — goes through one call site.
   FMT_DEV void zamboni() {
     for (int i = 0; i < 2; i++) {
       if (heapN == 0) break;
@@ -917,30 +905,51 @@ class Doc {
       const int b = static_cast<int>(fBlk(readField(j, 0)));
       if (uni(static_cast<int>(s->blk[b].needsScour)) == 0) continue;
       const int oldCount = uni(static_cast<int>(s->blk[b].count));
-      const int kept = scourLeafBlock(b);
-      if (status != FMT_OK) return;
-      s->blk[b].needsScour = 0;
-      waveSync();
-      if (kept < oldCount) {
-        s->blk[b].count = static_cast<uint8_t>(kept);
-        waveSync();
-        const int p = uni(static_cast<int>(s->blk[b].parent));
-        if (kept < kMaxNodes / 2 && p != static_cast<int>(kNoBlk)) packParent(p);
+      int target = b, p = -1, ci = 0, total = 0, firstLeaf = -1;
+      for (;;) {
+        const int kept = scourLeafBlock(target);
         if (status != FMT_OK) return;
+        if (p < 0) {  // the popped block itself
+          s->blk[b].needsScour = 0;
+          waveSync();
+          if (kept >= oldCount) break;
+          s->blk[b].count = static_cast<uint8_t>(kept);
+          waveSync();
+          const int parent = uni(static_cast<int>(s->blk[b].parent));
+          if (kept >= kMaxNodes / 2 || parent == static_cast<int>(kNoBlk)) break;
+          p = parent;  // packParent(parent): scour every child block of p, in order
+          ci = 0;
+          target = uni(static_cast<int>(s->blk[p].child[0]));
+          continue;
+        }
+        s->blk[target].count = static_cast<uint8_t>(kept);
+        waveSync();
+        if (kept > 0 && firstLeaf < 0) firstLeaf = firstLeafOf(static_cast<uint32_t>(target));
+        total += kept;
+        if (++ci < uni(static_cast<int>(s->blk[p].count))) {
+          target = uni(static_cast<int>(s->blk[p].child[ci]));
+          continue;
+        }
+        redistribute(p, total, true, firstLeaf);
+        if (status != FMT_OK) return;
+        // interior levels: scourNode holds block children as they are
+        for (;;) {
+          const int pp = uni(static_cast<int>(s->blk[p].parent));
+          if (uni(static_cast<int>(s->blk[p].count)) >= kMaxNodes / 2 || pp == static_cast<int>(kNoBlk)) break;
+          p = pp;
+          const int pc = uni(static_cast<int>(s->blk[p].count));
+          int held = 0;
+          for (int q = 0; q < pc; q++) {
+            const int c = uni(static_cast<int>(s->blk[p].child[q]));
+            const int cc = uni(static_cast<int>(s->blk[c].count));
+            for (int k = 0; k < cc; k++) s->tmp[held++] = uni(static_cast<int>(s->blk[c].child[k]));
+          }
+          waveSync();
+          redistribute(p, held, false, -1);
+          if (status != FMT_OK) return;
+        }
+        break;
       }
-    }
-  }
-
-  // client.ts:1381-1391 updateSeqNumbers + mergeTree.ts:1147-1166 setMinSeq
-  FMT_DEV void updateSeqNumbers(int msn, int seq) {
-    if (curSeq > seq || msn > seq || minSeq > msn) {
-      fail(FMT_E_DATA);
-      return;
-    }
-    curSeq = seq;
-    if (msn > minSeq) {
-      minSeq = msn;
-      zamboni();
     }
   }
 
@@ -955,10 +964,16 @@ class Doc {
     status = FMT_OK;
     failSeq = 0;
     nextId = 1;
+    FOR_LANES(l) {
+      V8 z;
 #pragma unroll
-    for (int f = 0; f < 5; f++)
-#pragma unroll
-      for (int e = 0; e < E; e++) FOR_LANES(l) { LANE(W[f][e]) = 0u; }
+      for (int e = 0; e < E; e++) z[e] = 0u;
+      LANE(W[0]) = z;
+      LANE(W[1]) = z;
+      LANE(W[2]) = z;
+      LANE(W[3]) = z;
+      LANE(W[4]) = z;
+    }
     FOR_LANES(l) {
       for (int i = l; i < kMaxBlocks; i += 64) s->freeList[i] = static_cast<uint8_t>(kMaxBlocks - 1 - i);
     }
@@ -982,19 +997,24 @@ class Doc {
     }
     waveSync();
     nChars = len;
-    LeafRec rec;
-    rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(root), kPropsUndef);
-    rec.w[1] = 0;
-    rec.w[2] = static_cast<uint32_t>(kNotRemoved);
-    rec.w[3] = 0;
-    rec.w[4] = mkW4(nextId++, FMT_LOCAL_CLIENT);
-    insertLeafAt(0, rec);
+    const uint32_t w0 = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(root), kPropsUndef);
+    const uint32_t w4 = mkW4(nextId++, FMT_LOCAL_CLIENT);
+    FOR_LANES(l) {
+      if (l == 0) {
+        LANE(W[0])[0] = w0;
+        LANE(W[1])[0] = 0u;
+        LANE(W[2])[0] = static_cast<uint32_t>(kNotRemoved);
+        LANE(W[3])[0] = 0u;
+        LANE(W[4])[0] = w4;
+      }
+    }
+    n = 1;
     s->blk[root].count = 1;
     waveSync();
   }
 
   FMT_DEV void replay() {
-    for (uint64_t i = in.begin; i < in.end && status == FMT_OK; i++) {
+    for (uint64_t i = in.begin; i < in.end; i++) {
       fmt_mt_op op = in.ops[i];
       op.seq = uni(op.seq);
       op.ref_seq = uni(op.ref_seq);
@@ -1007,53 +1027,58 @@ class Doc {
       op.len = static_cast<uint16_t>(lenClientType & 0xFFFF);
       op.client = static_cast<uint8_t>((lenClientType >> 16) & 0xFF);
       op.type = static_cast<uint8_t>(lenClientType >> 24);
-      if (op.client > kMaxClient) {
-        fail(FMT_E_UNSUPPORTED);
-      } else if (op.type == FMT_MT_INSERT) {
-        insertOp(op);
-      } else if (op.type == FMT_MT_REMOVE) {
-        removeOp(op);
-      } else if (op.type == FMT_MT_ANNOTATE) {
-        if (op.payload >= in.nPropsOps) fail(FMT_E_DATA);
-        else annotateOp(op);
-      } else {
-        fail(FMT_E_UNSUPPORTED);
+      if (op.client > kMaxClient || op.type > FMT_MT_ANNOTATE) fail(FMT_E_UNSUPPORTED);
+      else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
+      else applyOp(op);
+      const bool lastMember = i + 1 == in.end || (uni(in.ops[i + 1].flags) & FMT_MT_F_GROUP_CONT) == 0;
+      // zamboni once inside the op (mergeTree.ts:1510-1516, 2074-2080, 2376-2382), then, after the
+      // message's last member, updateSeqNumbers (client.ts:1381-1391) → setMinSeq
+      // (mergeTree.ts:1147-1166), which runs zamboni again only if minSeq advanced.
+      for (int z = 0; z < 2 && status == FMT_OK; z++) {
+        if (z == 1) {
+          if (!lastMember) break;
+          if (curSeq > op.seq || op.min_seq > op.seq || minSeq > op.min_seq) {
+            fail(FMT_E_DATA);
+            break;
+          }
+          curSeq = op.seq;
+          if (op.min_seq <= minSeq) break;
+          minSeq = op.min_seq;
+        }
+        zamboni();
       }
       if (status != FMT_OK) {
         failSeq = op.seq;
         break;
       }
-      const bool lastMember = i + 1 == in.end || (uni(in.ops[i + 1].flags) & FMT_MT_F_GROUP_CONT) == 0;
-      if (lastMember) updateSeqNumbers(op.min_seq, op.seq);
-      if (status != FMT_OK) failSeq = op.seq;
     }
   }
 
   FMT_DEV void writeOutputs(const DocOutputs& out) {
     // char offsets and leaf-block ordinals
-    Lane<uint32_t> cst[E];
+    Lane<V8> cst;
     charStarts(cst);
-    Lane<uint32_t> startFlag[E], ord[E];
-    const Lane<uint32_t> prevBlk7 = shflUp1(W[0][E - 1]);
+    Lane<V8> startFlag, ord;
+    const Lane<uint32_t> prevBlk7 = shflUp1(selectE(W[0], E - 1));
     FOR_LANES(l) {
 #pragma unroll
       for (int e = 0; e < E; e++) {
         const int idx = l * E + e;
-        const uint32_t b = fBlk(LANE(W[0][e]));
-        const uint32_t pb = e == 0 ? fBlk(LANE(prevBlk7)) : fBlk(LANE(W[0][e - 1]));
-        LANE(startFlag[e]) = idx < n && (idx == 0 || b != pb) ? 1u : 0u;
+        const uint32_t b = fBlk(LANE(W[0])[e]);
+        const uint32_t pb = e == 0 ? fBlk(LANE(prevBlk7)) : fBlk(LANE(W[0])[e - 1]);
+        LANE(startFlag)[e] = idx < n && (idx == 0 || b != pb) ? 1u : 0u;
       }
     }
     const uint32_t nLeafBlocks = scanLeaves(startFlag, ord);
     uint32_t visible = 0;
     {
-      Lane<uint32_t> vlen[E], tmp[E];
+      Lane<V8> vlen, tmp;
       FOR_LANES(l) {
 #pragma unroll
         for (int e = 0; e < E; e++) {
           const int idx = l * E + e;
-          const bool live = idx < n && static_cast<int32_t>(LANE(W[2][e])) == kNotRemoved;
-          LANE(vlen[e]) = live ? fLen(LANE(W[0][e])) : 0u;
+          const bool live = idx < n && static_cast<int32_t>(LANE(W[2])[e]) == kNotRemoved;
+          LANE(vlen)[e] = live ? fLen(LANE(W[0])[e]) : 0u;
         }
       }
       visible = scanLeaves(vlen, tmp);
@@ -1064,15 +1089,15 @@ class Doc {
         const int idx = l * E + e;
         if (idx < n) {
           fmt_mt_leaf L;
-          const uint32_t w0 = LANE(W[0][e]);
-          L.ins_seq = static_cast<int32_t>(LANE(W[1][e]));
-          L.rm_seq = static_cast<int32_t>(LANE(W[2][e]));
-          L.rm_clients = LANE(W[3][e]);
-          L.char_off = LANE(cst[e]);
+          const uint32_t w0 = LANE(W[0])[e];
+          L.ins_seq = static_cast<int32_t>(LANE(W[1])[e]);
+          L.rm_seq = static_cast<int32_t>(LANE(W[2])[e]);
+          L.rm_clients = LANE(W[3])[e];
+          L.char_off = LANE(cst)[e];
           L.len = static_cast<uint16_t>(fLen(w0));
-          L.ins_client = static_cast<int16_t>(fClient(LANE(W[4][e])));
+          L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[e]));
           L.props = fProps(w0) == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(fProps(w0));
-          L.block = static_cast<uint16_t>(LANE(ord[e]) + LANE(startFlag[e]) - 1u);
+          L.block = static_cast<uint16_t>(LANE(ord)[e] + LANE(startFlag)[e] - 1u);
           L.pad = 0;
           out.leaves[idx] = L;
         }

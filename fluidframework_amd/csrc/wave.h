@@ -24,10 +24,18 @@ template <class T>
 struct Lane {
   T v;
 };
+// Eight 32-bit values per lane held in VGPRs; a wave-uniform dynamic element index lowers to
+// register-relative moves (M0 / set_gpr_idx), never to scratch memory.
+typedef uint32_t V8 __attribute__((ext_vector_type(8)));
+typedef uint32_t V4 __attribute__((ext_vector_type(4)));
 #define LANE(x) ((x).v)
 #define FOR_LANES(l) for (int l = static_cast<int>(__lane_id()), l##_once = 1; l##_once; l##_once = 0)
 
 FMT_DEV int waveLane() { return static_cast<int>(__lane_id()); }
+
+// Opaque register copy: stops LLVM from folding a dynamic vector element access back into a
+// variable-index load from the enclosing object's stack slot (which would put it in scratch).
+FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }
 
 // Make a wave-uniform value provably uniform (lives in an SGPR afterwards).
 FMT_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -39,6 +47,62 @@ template <class T>
 FMT_DEV T readlane(const Lane<T>& x, int lane) {
   return static_cast<T>(__builtin_amdgcn_readlane(static_cast<int>(x.v), lane));
 }
+
+#ifndef FMT_USE_DPP
+#define FMT_USE_DPP 1
+#endif
+
+#if FMT_USE_DPP
+// GFX9 DPP controls (cdna4_isa.md §DPP): row_shr:n = 0x110+n, wave_shl:1 = 0x130, wave_shr:1 = 0x138,
+// row_bcast:15 = 0x142, row_bcast:31 = 0x143. Lanes whose DPP source is invalid (or whose row is
+// masked off) receive `old` = 0, so every step below is an ordinary add/max.
+template <int Ctrl, int RowMask = 0xF>
+FMT_DEV uint32_t dppMov(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), Ctrl, RowMask, 0xF, false));
+}
+
+template <class T>
+FMT_DEV Lane<T> shflUp1(const Lane<T>& x) {  // lane l receives lane l-1 (lane 0: 0)
+  return Lane<T>{static_cast<T>(dppMov<0x138>(static_cast<uint32_t>(x.v)))};
+}
+
+template <class T>
+FMT_DEV Lane<T> shflDown1(const Lane<T>& x) {  // lane l receives lane l+1 (lane 63: 0)
+  return Lane<T>{static_cast<T>(dppMov<0x130>(static_cast<uint32_t>(x.v)))};
+}
+
+// Inclusive wave64 prefix sum: Kogge-Stone inside 16-lane rows, then row broadcasts.
+FMT_DEV uint32_t waveInclusiveSum(uint32_t v) {
+  v += dppMov<0x111>(v);
+  v += dppMov<0x112>(v);
+  v += dppMov<0x114>(v);
+  v += dppMov<0x118>(v);
+  v += dppMov<0x142, 0xA>(v);
+  v += dppMov<0x143, 0xC>(v);
+  return v;
+}
+
+FMT_DEV Lane<uint32_t> waveExclusiveSum(const Lane<uint32_t>& x, uint32_t* total) {
+  const uint32_t v = waveInclusiveSum(x.v);
+  *total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+  return Lane<uint32_t>{v - x.v};
+}
+
+// Exclusive prefix max (values >= -1; `init` for lane 0). Max-scan on (v + 1) as unsigned so the
+// zero that invalid DPP lanes contribute is the identity.
+FMT_DEV Lane<int32_t> waveExclusiveMax(const Lane<int32_t>& x, int32_t init) {
+  uint32_t v = static_cast<uint32_t>(x.v + 1);
+  v = max(v, dppMov<0x111>(v));
+  v = max(v, dppMov<0x112>(v));
+  v = max(v, dppMov<0x114>(v));
+  v = max(v, dppMov<0x118>(v));
+  v = max(v, dppMov<0x142, 0xA>(v));
+  v = max(v, dppMov<0x143, 0xC>(v));
+  const uint32_t prev = dppMov<0x138>(v);  // exclusive: value of lane l-1
+  return Lane<int32_t>{waveLane() == 0 ? init : static_cast<int32_t>(prev) - 1};
+}
+
+#else
 
 template <class T>
 FMT_DEV Lane<T> shflUp1(const Lane<T>& x) {
@@ -76,6 +140,8 @@ FMT_DEV Lane<int32_t> waveExclusiveMax(const Lane<int32_t>& x, int32_t init) {
   return Lane<int32_t>{lane == 0 ? init : prev};
 }
 
+#endif
+
 FMT_DEV void waveSync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -91,11 +157,23 @@ template <class T>
 struct Lane {
   T v[64];
 };
+struct V8 {
+  uint32_t x[8];
+  uint32_t& operator[](int i) { return x[i]; }
+  const uint32_t& operator[](int i) const { return x[i]; }
+};
+struct V4 {
+  uint32_t x[4];
+  uint32_t& operator[](int i) { return x[i]; }
+  const uint32_t& operator[](int i) const { return x[i]; }
+};
 #define LANE(x) ((x).v[l])
 #define FOR_LANES(l) for (int l = 0; l < 64; l++)
 
 inline int uni(int x) { return x; }
 inline uint32_t uni(uint32_t x) { return x; }
+
+inline void launder(V8&) {}
 
 inline uint64_t ballot(const Lane<bool>& p) {
   uint64_t m = 0;

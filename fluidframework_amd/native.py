@@ -123,15 +123,16 @@ class EngineError(RuntimeError):
         self.code = code
 
 
-_lib = None
+_libs = {}
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise EngineUnavailable(f"{LIB_PATH} not built (run __graft_entry__.build())")
-        L = ctypes.CDLL(LIB_PATH)
+def lib(path: str | None = None) -> ctypes.CDLL:
+    """The engine library (default: the in-tree libfmt.so; `path` selects an experimental build)."""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise EngineUnavailable(f"{path} not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(path)
         P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         L.fmt_open.argtypes = [ctypes.POINTER(FmtConfig), ctypes.POINTER(P)]
         L.fmt_close.argtypes = [P]
@@ -149,8 +150,8 @@ def lib() -> ctypes.CDLL:
         L.fmt_mt_fetch_headers.argtypes = [P, P]
         L.fmt_mt_fetch_doc.argtypes = [P, U32, P, U32, P, U32, P, U32]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 EXPORTED_SYMBOLS = [
@@ -169,8 +170,8 @@ def capacity():
 class Engine:
     """One fmt_ctx bound to one HIP device (one per process/rank)."""
 
-    def __init__(self, device: int = 0, stream: int | None = None):
-        L = lib()
+    def __init__(self, device: int = 0, stream: int | None = None, lib_path: str | None = None):
+        self.L = L = lib(lib_path)
         cfg = FmtConfig(device, 0, stream, (ctypes.c_uint32 * 4)())
         h = ctypes.c_void_p()
         rc = L.fmt_open(ctypes.byref(cfg), ctypes.byref(h))
@@ -184,7 +185,7 @@ class Engine:
 
     def close(self):
         if self.h:
-            lib().fmt_close(self.h)
+            self.L.fmt_close(self.h)
             self.h = None
 
     def __del__(self):
@@ -195,48 +196,48 @@ class Engine:
 
     def _check(self, rc: int):
         if rc != FMT_OK:
-            raise EngineError(rc, lib().fmt_last_error(self.h).decode())
+            raise EngineError(rc, self.L.fmt_last_error(self.h).decode())
 
     def sync(self):
-        self._check(lib().fmt_sync(self.h))
+        self._check(self.L.fmt_sync(self.h))
 
     def stats(self) -> FmtStats:
         s = FmtStats()
-        self._check(lib().fmt_get_stats(self.h, ctypes.byref(s)))
+        self._check(self.L.fmt_get_stats(self.h, ctypes.byref(s)))
         return s
 
     def device_info(self) -> str:
         buf = ctypes.create_string_buffer(256)
-        lib().fmt_device_info(self.h, buf, 256)
+        self.L.fmt_device_info(self.h, buf, 256)
         return buf.value.decode()
 
     # ---- SharedMap
     def map_load(self, batch):
         ops = np.ascontiguousarray(batch.ops)
         offs = np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64)
-        self._check(lib().fmt_map_load(self.h, _ptr(ops), len(ops), _ptr(offs), batch.n_docs, batch.key_bound))
+        self._check(self.L.fmt_map_load(self.h, _ptr(ops), len(ops), _ptr(offs), batch.n_docs, batch.key_bound))
         self._map_shape = (batch.n_docs, batch.key_bound)
 
     def map_run(self):
-        self._check(lib().fmt_map_run(self.h))
+        self._check(self.L.fmt_map_run(self.h))
 
     def map_fetch(self) -> np.ndarray:
         out = np.zeros(self._map_shape[0] * self._map_shape[1], dtype=MAP_SLOT_DTYPE)
-        self._check(lib().fmt_map_fetch(self.h, _ptr(out)))
+        self._check(self.L.fmt_map_fetch(self.h, _ptr(out)))
         return out.reshape(self._map_shape)
 
     # ---- merge-tree
     def mt_load(self, batch):
         b, keep = batch_struct(batch)
-        self._check(lib().fmt_mt_load(self.h, ctypes.byref(b)))
+        self._check(self.L.fmt_mt_load(self.h, ctypes.byref(b)))
         self._mt_docs = batch.n_docs
 
     def mt_run(self):
-        self._check(lib().fmt_mt_run(self.h))
+        self._check(self.L.fmt_mt_run(self.h))
 
     def mt_headers(self) -> np.ndarray:
         out = np.zeros(self._mt_docs, dtype=DOC_RESULT_DTYPE)
-        self._check(lib().fmt_mt_fetch_headers(self.h, _ptr(out)))
+        self._check(self.L.fmt_mt_fetch_headers(self.h, _ptr(out)))
         return out
 
     def mt_doc(self, doc: int, hdr=None):
@@ -246,5 +247,5 @@ class Engine:
         leaves = np.zeros(max(nl, 1), dtype=LEAF_DTYPE)
         chars = np.zeros(max(nc, 1), dtype="<u2")
         props = np.zeros(max(npp, 1), dtype=PROPSET_DTYPE)
-        self._check(lib().fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
+        self._check(self.L.fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
         return leaves[:nl], chars[:nc], props[:npp]
