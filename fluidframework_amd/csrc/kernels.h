@@ -41,4 +41,7 @@ MtCaps mergeTreeCaps();
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, int numCUs, hipStream_t stream);
 
+// Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
+int mergeTreeProfile(uint64_t* out, int n, bool reset);
+
 }  // namespace fmt_kernels

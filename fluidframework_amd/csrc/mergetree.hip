@@ -15,6 +15,9 @@ namespace fmt_kernels {
 
 constexpr int kMtWaves = 4;
 
+// Diagnostic build only: per-phase shader-clock totals summed over all waves (mt_engine.h stamp()).
+__device__ unsigned long long g_mtProfile[fmt_mt::kPfCount];
+
 __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                  const uint32_t* __restrict__ docList,
                                                                  uint32_t count) {
@@ -41,7 +44,22 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
     fmt_mt::Doc doc;
     doc.s = scratch;
     doc.run(in, o);
+#if FMT_PROFILE && FMT_GPU
+    if ((threadIdx.x & 63) == 0)
+      for (int c = 0; c < fmt_mt::kPfCount; c++) atomicAdd(&g_mtProfile[c], static_cast<unsigned long long>(doc.prof[c]));
+#endif
   }
+}
+
+int mergeTreeProfile(uint64_t* out, int n, bool reset) {
+  unsigned long long h[fmt_mt::kPfCount];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mtProfile), sizeof h) != hipSuccess) return -1;
+  for (int c = 0; c < n && c < fmt_mt::kPfCount; c++) out[c] = h[c];
+  if (reset) {
+    unsigned long long z[fmt_mt::kPfCount] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_mtProfile), z, sizeof z) != hipSuccess) return -1;
+  }
+  return fmt_mt::kPfCount;
 }
 
 MtCaps mergeTreeCaps() {

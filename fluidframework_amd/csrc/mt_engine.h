@@ -104,8 +104,25 @@ struct DocOutputs {
   fmt_mt_propset* props;  // kPropCap entries
 };
 
+// Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
+#ifndef FMT_PROFILE
+#define FMT_PROFILE 0
+#endif
+enum ProfCat { kPfOpLoad, kPfScan, kPfSplit, kPfInsert, kPfRange, kPfLru, kPfZamboniOp, kPfWindow, kPfOutput, kPfCount };
+
 class Doc {
  public:
+#if FMT_PROFILE && FMT_GPU
+  uint64_t profT = 0;
+  uint64_t prof[kPfCount] = {};
+  FMT_DEV void stamp(int cat) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    prof[cat] += t - profT;
+    profT = t;
+  }
+#else
+  FMT_DEV void stamp(int) {}
+#endif
   Lane<V8> W[5];  // W[f] element e = leaf lane*E + e
   Scratch* s;
   int n = 0;          // leaves
@@ -626,6 +643,7 @@ class Doc {
       Lane<V8> vis, st;
       visLengths(refSeq, client, vis);
       const uint32_t total = scanLeaves(vis, st);
+      stamp(kPfScan);
       int insIdx = -1, blk = 0;
       LeafRec rec;
       if (phase < nb) {
@@ -730,6 +748,7 @@ class Doc {
         childAdded(blk);
         if (status != FMT_OK) return;
       }
+      stamp(phase < nb ? kPfSplit : kPfInsert);
       if (phase >= nb) {
         if (insIdx >= 0) {
           const int lane = insIdx / E, e = insIdx % E;
@@ -775,7 +794,9 @@ class Doc {
         }
       }
     }
+    stamp(kPfRange);
     lruForHits(hits, seq);
+    stamp(kPfLru);
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
@@ -1014,6 +1035,7 @@ class Doc {
   }
 
   FMT_DEV void replay() {
+    stamp(kPfOutput);
     for (uint64_t i = in.begin; i < in.end; i++) {
       fmt_mt_op op = in.ops[i];
       op.seq = uni(op.seq);
@@ -1027,6 +1049,7 @@ class Doc {
       op.len = static_cast<uint16_t>(lenClientType & 0xFFFF);
       op.client = static_cast<uint8_t>((lenClientType >> 16) & 0xFF);
       op.type = static_cast<uint8_t>(lenClientType >> 24);
+      stamp(kPfOpLoad);
       if (op.client > kMaxClient || op.type > FMT_MT_ANNOTATE) fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op);
@@ -1046,6 +1069,7 @@ class Doc {
           minSeq = op.min_seq;
         }
         zamboni();
+        stamp(z == 0 ? kPfZamboniOp : kPfWindow);
       }
       if (status != FMT_OK) {
         failSeq = op.seq;
@@ -1138,11 +1162,15 @@ class Doc {
   }
 
   FMT_DEV void run(const DocInputs& inputs, const DocOutputs& out) {
+#if FMT_PROFILE && FMT_GPU
+    profT = __builtin_amdgcn_s_memtime();
+#endif
     in = inputs;
     init();
     loadInitial();
     if (status == FMT_OK) replay();
     writeOutputs(out);
+    stamp(kPfOutput);
   }
 };
 

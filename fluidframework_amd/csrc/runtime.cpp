@@ -380,4 +380,9 @@ int fmt_mt_fetch_doc(fmt_ctx* c, uint32_t doc, fmt_mt_leaf* leaves, uint32_t cap
   return FMT_OK;
 }
 
+// Internal diagnostic (not part of fmt.h): per-phase cycle totals of a FMT_PROFILE=1 build.
+int fmt_internal_mt_profile(uint64_t* out, int n, int reset) {
+  return fmt_kernels::mergeTreeProfile(out, n, reset != 0);
+}
+
 }  // extern "C"

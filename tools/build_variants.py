@@ -44,7 +44,16 @@ LB2 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves)", "__launch_bounds__(6
 LB3 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves)", "__launch_bounds__(64 * kMtWaves, 3)")
 NODPP = ("wave.h", "#define FMT_USE_DPP 1", "#define FMT_USE_DPP 0")
 
+NOFENCE = ("wave.h", """FMT_DEV void waveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}""", """FMT_DEV void waveSync() { asm volatile("" ::: "memory"); }""")
+
+PROF = ("mt_engine.h", "#define FMT_PROFILE 0", "#define FMT_PROFILE 1")
+
 VARIANTS = {
+    "prof": [PROF],
+    "nofence": [NOFENCE],
     "base": [],
     "lb2_nodpp": [LB2, NODPP],
     "lb3": [LB3],

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-phase shader-clock breakdown of the merge-tree kernel (diagnostic FMT_PROFILE=1 build).
+
+Build: python3 tools/build_variants.py prof   →  build/variants/prof/libfmt.so
+Prints total clock ticks per phase summed over waves, the share of each, and ticks per op."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from fluidframework_amd import native, workloads  # noqa: E402
+
+PHASES = ["op_load", "scan", "split", "insert", "range", "lru", "zamboni_op", "window", "output"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=20000)
+    ap.add_argument("--unique", type=int, default=2000)
+    ap.add_argument("--lib", default=os.path.join(REPO, "build/variants/prof/libfmt.so"))
+    a = ap.parse_args()
+    batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
+    e = native.Engine(0, lib_path=a.lib)
+    fn = e.L.fmt_internal_mt_profile
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    buf = (ctypes.c_uint64 * 16)()
+    e.mt_load(batch)
+    e.mt_run()
+    e.sync()
+    fn(buf, 16, 1)  # reset after warm-up
+    e.mt_run()
+    ms = e.stats().kernel_ms
+    n = fn(buf, 16, 1)
+    tot = sum(buf[i] for i in range(n))
+    n_ops = len(batch.ops)
+    out = {"kernel_ms": ms, "ops": n_ops, "ticks_per_op": tot / n_ops,
+           "phases": {PHASES[i]: {"ticks": buf[i], "share": buf[i] / tot, "per_op": buf[i] / n_ops} for i in range(n)}}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
