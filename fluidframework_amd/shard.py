@@ -1,0 +1,128 @@
+"""Document sharding across GPUs: one rank per GPU, contiguous doc ranges.
+
+Documents are independent (no cross-document op), so a multi-GPU replay is N independent replays
+of contiguous document ranges balanced by op count, with nothing exchanged on the data path. The
+one exchange step is at the end: every rank contributes a fixed 64-byte stats record
+(`STATS_DTYPE`) to an all-gather. Over RCCL with `nccl`, or over `gloo` in the CPU tests.
+
+`state_checksum` folds per-document result headers into one order-independent 64-bit value, so the
+sum over shards equals the checksum of an unsharded replay.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .streams import MapBatch, MergeTreeBatch
+
+STATS_DTYPE = np.dtype(
+    [
+        ("rank", "<u4"),
+        ("status_bad", "<u4"),   # documents whose replay failed (status != OK)
+        ("doc_lo", "<u8"),
+        ("doc_hi", "<u8"),
+        ("ops", "<u8"),
+        ("kernel_ms", "<f8"),
+        ("elapsed_s", "<f8"),
+        ("checksum", "<u8"),     # state_checksum of this shard's documents
+        ("bytes", "<u8"),        # algorithmic bytes of this shard's launch
+    ]
+)
+assert STATS_DTYPE.itemsize == 64
+
+
+def plan_shards(doc_op_offsets: np.ndarray, world: int) -> list[tuple[int, int]]:
+    """Contiguous [lo, hi) document ranges, one per rank, balanced by op count.
+
+    Boundary k is the first document whose op prefix reaches k/world of all ops, so every rank
+    gets within one document's ops of an equal share. Ranges cover [0, n_docs) exactly."""
+    offs = np.asarray(doc_op_offsets, dtype=np.uint64)
+    n_docs = len(offs) - 1
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    total = int(offs[-1])
+    cuts = [0]
+    for k in range(1, world):
+        target = (total * k) // world
+        c = int(np.searchsorted(offs, np.uint64(target), side="left"))
+        cuts.append(min(max(c, cuts[-1]), n_docs))
+    cuts.append(n_docs)
+    return [(cuts[i], cuts[i + 1]) for i in range(world)]
+
+
+def slice_mt(batch: MergeTreeBatch, lo: int, hi: int) -> MergeTreeBatch:
+    """Documents [lo, hi) of a merge-tree batch. Text arena and prop table are shared (ops carry
+    absolute offsets into them)."""
+    o0, o1 = int(batch.doc_op_offsets[lo]), int(batch.doc_op_offsets[hi])
+    return MergeTreeBatch(
+        ops=batch.ops[o0:o1],
+        doc_op_offsets=(batch.doc_op_offsets[lo : hi + 1] - np.uint64(o0)).astype(np.uint64),
+        text=batch.text,
+        doc_init=batch.doc_init[lo:hi],
+        props_off=batch.props_off,
+        props_kv=batch.props_kv,
+        keys=batch.keys,
+        values=batch.values,
+        clients=batch.clients[lo:hi] if batch.clients else [],
+    )
+
+
+def slice_map(batch: MapBatch, lo: int, hi: int) -> MapBatch:
+    """Documents [lo, hi) of a SharedMap batch; doc ids are rebased to the shard."""
+    o0, o1 = int(batch.doc_op_offsets[lo]), int(batch.doc_op_offsets[hi])
+    ops = batch.ops[o0:o1].copy()
+    ops["doc"] -= np.uint32(lo)
+    return MapBatch(ops, (batch.doc_op_offsets[lo : hi + 1] - np.uint64(o0)).astype(np.uint64),
+                    batch.key_bound, batch.keys, batch.values)
+
+
+_HDR_FIELDS = ("status", "fail_seq", "cur_seq", "min_seq", "n_leaves", "n_chars", "n_props", "n_blocks",
+               "depth", "visible_len")
+
+
+def state_checksum(headers: np.ndarray, doc_lo: int = 0) -> int:
+    """Order-independent checksum of per-document result headers: Σ_d mix(d, header_d) mod 2^64,
+    with d the global document index, so shard checksums add up to the unsharded one."""
+    n = len(headers)
+    h = (np.arange(doc_lo, doc_lo + n, dtype=np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        for i, f in enumerate(_HDR_FIELDS):
+            v = headers[f].astype(np.int64).astype(np.uint64)
+            h ^= v + np.uint64(0x632BE59BD9B4E019) * np.uint64(i + 1)
+            h *= np.uint64(0xBF58476D1CE4E5B9)
+            h ^= h >> np.uint64(31)
+        return int(h.sum(dtype=np.uint64))
+
+
+def map_checksum(slots: np.ndarray, doc_lo: int = 0) -> int:
+    """Order-independent checksum of SharedMap result slots (n_docs × key_bound)."""
+    nd, kb = slots.shape
+    idx = (np.arange(doc_lo * kb, (doc_lo + nd) * kb, dtype=np.uint64) + np.uint64(1)).reshape(nd, kb)
+    with np.errstate(over="ignore"):
+        h = idx * np.uint64(0x9E3779B97F4A7C15)
+        h ^= slots["value"].astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+        h ^= slots["birth_seq"].astype(np.uint64) + np.uint64(0x94D049BB133111EB)
+        h *= np.uint64(0xD6E8FEB86659FD93)
+        h ^= h >> np.uint64(32)
+        return int(h.sum(dtype=np.uint64))
+
+
+def gather_stats(rec: np.ndarray, dist, device=None) -> np.ndarray:
+    """All-gather one STATS_DTYPE record per rank (the run's single exchange step).
+
+    `dist` is torch.distributed (initialised); `device` is "cuda" for nccl/RCCL, None for gloo."""
+    import torch
+
+    world = dist.get_world_size()
+    raw = np.frombuffer(np.ascontiguousarray(rec, dtype=STATS_DTYPE).tobytes(), dtype=np.uint8)
+    t = torch.from_numpy(raw.copy())
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    out = np.concatenate([p.cpu().numpy() for p in parts])
+    return np.frombuffer(out.tobytes(), dtype=STATS_DTYPE)
+
+
+def combine_checksums(stats: np.ndarray) -> int:
+    """Whole-job state checksum = Σ shard checksums mod 2^64."""
+    return int(stats["checksum"].astype(np.uint64).sum(dtype=np.uint64))

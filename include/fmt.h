@@ -184,10 +184,17 @@ typedef struct fmt_config {
   uint32_t reserved[4];
 } fmt_config;
 
+/* Context lifetime. Replaces the per-DDS state owned by each SharedMap / SharedString instance
+ * (map/src/map.ts:66 MapKernel construction; sequence/src/sequence.ts:526 Client construction): one ctx holds the replay state of many documents on one device. */
 int fmt_open(const fmt_config* cfg, fmt_ctx** out);
 void fmt_close(fmt_ctx* ctx);
+/* Message of the last failing call. Replaces the thrown DataProcessingError / UsageError text
+ * (merge-tree/src/mergeTree.ts:1629-1638; core-utils assert 0xNNN codes). */
 const char* fmt_last_error(const fmt_ctx* ctx);
+/* Wait for the ctx stream. The reference is synchronous and non-reentrant (sequence.ts:500-511); here runs are
+ * asynchronous until fmt_sync or a fetch. */
 int fmt_sync(fmt_ctx* ctx);
+/* Device time and algorithmic bytes of the last run (no reference counterpart; telemetry only). */
 int fmt_get_stats(const fmt_ctx* ctx, fmt_stats* out);
 /* Name of the gfx target the library was built for and the device it runs on (diagnostics). */
 int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
@@ -195,13 +202,17 @@ int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
 /* ---------------------------------------------------------------------------------------------
  * SharedMap last-writer-wins (MapKernel sequenced path, mapKernel.ts:706-853)
  * ------------------------------------------------------------------------------------------- */
-/* Stage a batch into HBM (the one host→device crossing). ops of document d are
+/* Stage a batch into HBM (the one host→device crossing). Together with fmt_map_run this replaces
+ * SharedMap.processMessagesCore (map/src/map.ts:288-311) → MapKernel.tryProcessMessage
+ * (map/src/mapKernel.ts:619-630) for every sequenced set/delete/clear of every document, applied
+ * in seq order (remote handlers mapKernel.ts:708-850). ops of document d are
  * ops[doc_op_offsets[d] .. doc_op_offsets[d+1]) in seq order; key ids < key_bound. */
 int fmt_map_load(fmt_ctx* ctx, const fmt_map_op* ops, uint64_t n_ops,
                  const uint64_t* doc_op_offsets, uint32_t n_docs, uint32_t key_bound);
 /* Replay the staged batch (asynchronous on the ctx stream). */
 int fmt_map_run(fmt_ctx* ctx);
-/* Copy results to host: out[d * key_bound + k]. Synchronizes the ctx stream. */
+/* Copy results to host: out[d * key_bound + k]. Synchronizes the ctx stream. Replaces reading
+ * MapKernel.sequencedData (mapKernel.ts:131) for get()/summarizeCore (map.ts:176-246). */
 int fmt_map_fetch(fmt_ctx* ctx, fmt_map_slot* out);
 /* Zero-copy variant on caller-owned DEVICE buffers (e.g. torch tensors), launched on the ctx stream. */
 int fmt_map_replay_device(fmt_ctx* ctx, const fmt_map_op* d_ops, const uint64_t* d_doc_op_offsets,
@@ -210,11 +221,18 @@ int fmt_map_replay_device(fmt_ctx* ctx, const fmt_map_op* d_ops, const uint64_t*
 /* ---------------------------------------------------------------------------------------------
  * merge-tree / SharedString (Client.applyMsg observer path + zamboni, client.ts:1358-1391)
  * ------------------------------------------------------------------------------------------- */
+/* Stage a batch into HBM. With fmt_mt_run this replaces SharedSegmentSequence.processMessagesCore
+ * (sequence/src/sequence.ts:873-919) → Client.applyMsg (merge-tree/src/client.ts:1358-1379) for
+ * every sequenced insert/remove/annotate/group message of every document (remote, observer view),
+ * including updateSeqNumbers/setMinSeq (client.ts:1381-1391, mergeTree.ts:1147-1166) and zamboni
+ * (zamboni.ts:33-213). Per-document errors land in fmt_mt_doc_result.status / fail_seq. */
 int fmt_mt_load(fmt_ctx* ctx, const fmt_mt_batch* batch);
 int fmt_mt_run(fmt_ctx* ctx);
 /* Per-document result headers for all docs (n_docs entries). Synchronizes the ctx stream. */
 int fmt_mt_fetch_headers(fmt_ctx* ctx, fmt_mt_doc_result* out);
-/* One document's leaves (cap_leaves), chars (cap_chars) and prop sets (cap_props). */
+/* One document's leaves (cap_leaves), chars (cap_chars) and prop sets (cap_props): the converged
+ * segment list that getText (MergeTreeTextHelper.ts:28-87) and Client.summarize
+ * (client.ts:1548-1587, snapshotlegacy.ts:195-262) read. */
 int fmt_mt_fetch_doc(fmt_ctx* ctx, uint32_t doc, fmt_mt_leaf* leaves, uint32_t cap_leaves,
                      uint16_t* chars, uint32_t cap_chars, fmt_mt_propset* props, uint32_t cap_props);
 /* Per-document capacities of this engine build (leaves, chars, prop sets). */
