@@ -22,7 +22,7 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
                                                                  const uint32_t* __restrict__ docList,
                                                                  uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
   fmt_mt::Scratch* scratch = reinterpret_cast<fmt_mt::Scratch*>(lds) + wave;
   for (uint32_t i = blockIdx.x * kMtWaves + wave; i < count; i += gridDim.x * kMtWaves) {
     const uint32_t d = docList ? docList[i] : i;

@@ -7,14 +7,15 @@
 // updateSeqNumbers / setMinSeq (client.ts:1381-1391, mergeTree.ts:1147-1166).
 //
 // MI355X data layout (what replaces the JS object tree):
-//   * Leaves live in VGPRs, in document order: lane l holds leaves [8l, 8l+8), five 32-bit words
-//     each (W0 len|block|props, W1 insert seq, W2 first-remove seq, W3 remove-client mask,
-//     W4 leaf id|insert client). 40 VGPRs hold up to 512 leaves. A perspective's visible length
+//   * Leaves live in VGPRs, in document order, row-major: leaf j is element j >> 6 ("row") of
+//     lane j & 63, five 32-bit words each (W0 len|block|props, W1 insert seq, W2 first-remove seq,
+//     W3 remove-client mask, W4 leaf id|insert client). 40 VGPRs hold up to 512 leaves; passes
+//     visit only the rows that hold leaves (wave-uniform guard). A perspective's visible length
 //     of every leaf, its prefix sums, and every "which leaf holds position p" question are then
 //     lane-local arithmetic plus one wave scan / ballot: no tree walk and no partial-lengths index
 //     (the reference's PartialSequenceLengths is only an index whose value must equal the sum of
-//     leaf lengths, partialLengths.ts:1189-1240). Insert/delete of a leaf is a one-slot shift of
-//     the register array (one cross-lane shuffle per word).
+//     leaf lengths, partialLengths.ts:1189-1240). Insert/delete of a leaf is a one-lane DPP shift
+//     (wave_shr / wave_shl) of the rows at and above it, with a one-lane carry between rows.
 //   * The B+tree above the leaves is kept exactly (it decides zamboni scope and therefore the
 //     segmentation that summaries expose): leaf blocks are contiguous runs of leaves tagged with a
 //     block id; interior blocks store child lists. Block table, LRU heap, prop-set table and the
@@ -33,8 +34,8 @@
 
 namespace fmt_mt {
 
-constexpr int E = 8;                 // leaves per lane
-constexpr int kCapLeaves = 64 * E;   // 512
+constexpr int kRows = 8;                // rows of 64 leaves (one V8 element per row)
+constexpr int kCapLeaves = 64 * kRows;  // 512
 constexpr int kCapChars = 2048;      // UTF-16 units per document (tombstones included)
 constexpr int kMaxBlocks = 128;
 constexpr int kHeapCap = 255;
@@ -45,6 +46,14 @@ constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:2
 constexpr uint32_t kNoBlk = 0xFF;
 constexpr uint32_t kPropsUndef = 0xFF;
 constexpr int32_t kNotRemoved = 0x7fffffff;
+
+// Uniform row loops: unrolled so that the row is a compile-time V8 element, with a wave-uniform
+// guard so rows outside [lo, hi) cost one scalar branch.
+#define FMT_PRAGMA(x) _Pragma(#x)
+#define FOR_ROWS(r, lo, hi) \
+  FMT_PRAGMA(unroll) for (int r = 0; r < kRows; r++) if (r >= (lo) && r < (hi))
+#define FOR_ROWS_DOWN(r, lo, hi) \
+  FMT_PRAGMA(unroll) for (int r = kRows - 1; r >= 0; r--) if (r >= (lo) && r < (hi))
 
 struct Blk {
   uint8_t count;
@@ -123,7 +132,7 @@ class Doc {
 #else
   FMT_DEV void stamp(int) {}
 #endif
-  Lane<V8> W[5];  // W[f] element e = leaf lane*E + e
+  Lane<V8> W[5];  // W[f] element r of lane l = field f of leaf 64 r + l
   Scratch* s;
   int n = 0;          // leaves
   int nChars = 0;
@@ -139,196 +148,166 @@ class Doc {
   DocInputs in;
 
   // ------------------------------------------------------------------ leaf array primitives
-  FMT_DEV Lane<uint32_t> selectE(const Lane<V8>& arr, int e) const {
-    Lane<uint32_t> r;
+  // Leaf j lives in row j >> 6 (element of the V8) of lane j & 63: document order runs along a
+  // row's lanes, then to the next row. Rows at or above rows() hold only empty (all-zero) slots,
+  // and every pass below visits rows [0, rows()) only, so its cost follows the live leaf count.
+  FMT_DEV int rows() const { return (n + 63) >> 6; }
+
+  FMT_DEV static Lane<uint32_t> row(const Lane<V8>& a, int r) {  // r compile-time after unrolling
+    Lane<uint32_t> x;
+    FOR_LANES(l) { LANE(x) = LANE(a)[r]; }
+    return x;
+  }
+
+  FMT_DEV static Lane<uint32_t> selectRow(const Lane<V8>& arr, int r) {  // r wave-uniform, dynamic
+    Lane<uint32_t> x;
     FOR_LANES(l) {
       V8 t = LANE(arr);
       launder(t);  // keep the dynamic index on a register value (v_movrels), never a scratch GEP
-      LANE(r) = t[e];
+      LANE(x) = t[r];
     }
-    return r;
+    return x;
   }
 
-  FMT_DEV uint32_t readField(int j, int f) const { return readlane(selectE(W[f], j % E), j / E); }
+  FMT_DEV uint32_t readField(int j, int f) const { return readlane(selectRow(W[f], j >> 6), j & 63); }
 
   FMT_DEV LeafRec readLeaf(int j) const {
     LeafRec r;
-    r.w[0] = readField(j, 0);
-    r.w[1] = readField(j, 1);
-    r.w[2] = readField(j, 2);
-    r.w[3] = readField(j, 3);
-    r.w[4] = readField(j, 4);
+#pragma unroll
+    for (int f = 0; f < 5; f++) r.w[f] = readField(j, f);
     return r;
   }
 
   FMT_DEV void writeField(int j, int f, uint32_t v) {
-    const int lane = j / E, e = j % E;
-    FOR_LANES(l) {
-      if (l == lane) {
-        V8 t = LANE(W[f]);
-        launder(t);
-        t[e] = v;
-        LANE(W[f]) = t;
+    const int rj = j >> 6, lane = j & 63;
+    FOR_ROWS(r, rj, rj + 1) {
+      FOR_LANES(l) {
+        if (l == lane) LANE(W[f])[r] = v;
       }
     }
   }
 
-  // One field of the leaf array shifted up by one slot from index k, `rv` written at k.
-  FMT_DEV static void shiftUpField(Lane<V8>& w, int k, uint32_t rv) {
-    const Lane<uint32_t> prev7 = shflUp1(selectLast(w));
-    FOR_LANES(l) {
-      V8 v = LANE(w);
-#pragma unroll
-      for (int e = E - 1; e >= 1; e--) {
-        const int idx = l * E + e;
-        v[e] = idx > k ? v[e - 1] : (idx == k ? rv : v[e]);
-      }
-      const int idx0 = l * E;
-      v[0] = idx0 > k ? LANE(prev7) : (idx0 == k ? rv : v[0]);
-      LANE(w) = v;
-    }
-  }
-
-  // One field of the leaf array shifted down by one slot onto index k.
-  FMT_DEV static void shiftDownField(Lane<V8>& w, int k) {
-    const Lane<uint32_t> next0 = shflDown1(selectFirst(w));
-    FOR_LANES(l) {
-      V8 v = LANE(w);
-#pragma unroll
-      for (int e = 0; e < E - 1; e++) {
-        const int idx = l * E + e;
-        v[e] = idx >= k ? v[e + 1] : v[e];
-      }
-      const int idx7 = l * E + E - 1;
-      v[E - 1] = idx7 >= k ? LANE(next0) : v[E - 1];
-      LANE(w) = v;
-    }
-  }
-
-  FMT_DEV static Lane<uint32_t> selectLast(const Lane<V8>& w) {
-    Lane<uint32_t> r;
-    FOR_LANES(l) { LANE(r) = LANE(w)[E - 1]; }
-    return r;
-  }
-
-  FMT_DEV static Lane<uint32_t> selectFirst(const Lane<V8>& w) {
-    Lane<uint32_t> r;
-    FOR_LANES(l) { LANE(r) = LANE(w)[0]; }
-    return r;
-  }
-
-  // Insert `rec` at index k, shifting leaves k.. up by one.
+  // Insert `rec` at index k: rows from k's row up are shifted one lane up (DPP wave_shr), each
+  // row's lane 0 taking the previous row's lane 63. Top-down, so that carry is still the old value.
   FMT_DEV bool insertLeafAt(int k, const LeafRec& rec) {
     if (n >= kCapLeaves) return fail(FMT_E_CAPACITY);
-    shiftUpField(W[0], k, rec.w[0]);
-    shiftUpField(W[1], k, rec.w[1]);
-    shiftUpField(W[2], k, rec.w[2]);
-    shiftUpField(W[3], k, rec.w[3]);
-    shiftUpField(W[4], k, rec.w[4]);
+    const int rk = k >> 6, kl = k & 63, nr = (n + 64) >> 6;
+    FOR_ROWS_DOWN(r, rk, nr) {
+#pragma unroll
+      for (int f = 0; f < 5; f++) {
+        const Lane<uint32_t> cur = row(W[f], r);
+        const Lane<uint32_t> up = shflUp1(cur);
+        if (r > rk) {
+          const uint32_t carry = readlane(row(W[f], r > 0 ? r - 1 : 0), 63);
+          FOR_LANES(l) { LANE(W[f])[r] = l == 0 ? carry : LANE(up); }
+        } else {
+          const uint32_t rv = rec.w[f];
+          FOR_LANES(l) { LANE(W[f])[r] = l > kl ? LANE(up) : (l == kl ? rv : LANE(cur)); }
+        }
+      }
+    }
     n++;
     return true;
   }
 
-  // Remove the leaf at index k, shifting leaves k+1.. down by one.
+  // Remove the leaf at index k: rows from k's row up shift one lane down (DPP wave_shl), lane 63
+  // taking the next row's lane 0 (zero past the last row, which keeps empty slots zero).
   FMT_DEV void deleteLeafAt(int k) {
-    shiftDownField(W[0], k);
-    shiftDownField(W[1], k);
-    shiftDownField(W[2], k);
-    shiftDownField(W[3], k);
-    shiftDownField(W[4], k);
+    const int rk = k >> 6, kl = k & 63, nr = rows();
+    FOR_ROWS(r, rk, nr) {
+#pragma unroll
+      for (int f = 0; f < 5; f++) {
+        const Lane<uint32_t> cur = row(W[f], r);
+        const Lane<uint32_t> dn = shflDown1(cur);
+        const uint32_t carry = r + 1 < nr ? readlane(row(W[f], r + 1 < kRows ? r + 1 : r), 0) : 0u;
+        if (r > rk) {
+          FOR_LANES(l) { LANE(W[f])[r] = l == 63 ? carry : LANE(dn); }
+        } else {
+          FOR_LANES(l) { LANE(W[f])[r] = l < kl ? LANE(cur) : (l == 63 ? carry : LANE(dn)); }
+        }
+      }
+    }
     n--;
   }
 
-  // Exclusive prefix of per-leaf values (document order); returns the total.
-  FMT_DEV uint32_t scanLeaves(const Lane<V8>& vals, Lane<V8>& excl) const {
-    Lane<uint32_t> laneSum;
-    FOR_LANES(l) {
-      uint32_t t = 0;
-#pragma unroll
-      for (int e = 0; e < E; e++) t += LANE(vals)[e];
-      LANE(laneSum) = t;
+  // Exclusive prefix (document order) of per-leaf values over rows [0, nr); returns the total.
+  // Rows >= nr of `excl` are left unset.
+  FMT_DEV static uint32_t scanRows(const Lane<V8>& vals, Lane<V8>& excl, int nr) {
+    uint32_t base = 0;
+    FOR_ROWS(r, 0, nr) {
+      uint32_t tot;
+      const Lane<uint32_t> ex = waveExclusiveSum(row(vals, r), &tot);
+      FOR_LANES(l) { LANE(excl)[r] = LANE(ex) + base; }
+      base += tot;
     }
-    uint32_t total;
-    const Lane<uint32_t> base = waveExclusiveSum(laneSum, &total);
-    FOR_LANES(l) {
-      uint32_t acc = LANE(base);
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        LANE(excl)[e] = acc;
-        acc += LANE(vals)[e];
-      }
-    }
-    return total;
+    return base;
   }
 
   // Visible length of every leaf from PriorPerspective(refSeq, client) (perspective.ts:80-93).
   // Leaves removed at/below minSeq are never present for such a perspective (refSeq >= minSeq).
-  FMT_DEV void visLengths(int refSeq, int client, Lane<V8>& vis) const {
-    FOR_LANES(l) {
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const int idx = l * E + e;
-        const uint32_t w0 = LANE(W[0])[e];
-        const int32_t ins = static_cast<int32_t>(LANE(W[1])[e]);
-        const int32_t rm = static_cast<int32_t>(LANE(W[2])[e]);
-        const uint32_t mask = LANE(W[3])[e];
-        const int32_t ic = fClient(LANE(W[4])[e]);
-        const bool present = idx < n && (ins <= refSeq || ic == client) &&
-                             !(rm <= refSeq || ((mask >> client) & 1u));
-        LANE(vis)[e] = present ? fLen(w0) : 0u;
+  // Empty slots have length 0.
+  FMT_DEV void visLengths(int refSeq, int client, Lane<V8>& vis, int nr) const {
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const uint32_t w0 = LANE(W[0])[r];
+        const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]);
+        const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
+        const uint32_t mask = LANE(W[3])[r];
+        const int32_t ic = fClient(LANE(W[4])[r]);
+        const bool present = (ins <= refSeq || ic == client) && !(rm <= refSeq || ((mask >> client) & 1u));
+        LANE(vis)[r] = present ? fLen(w0) : 0u;
       }
     }
   }
 
   // Char offset of every leaf (all leaves, tombstones included).
-  FMT_DEV void charStarts(Lane<V8>& cst) const {
+  FMT_DEV void charStarts(Lane<V8>& cst, int nr) const {
     Lane<V8> lens;
-    FOR_LANES(l) {
-#pragma unroll
-      for (int e = 0; e < E; e++) LANE(lens)[e] = (l * E + e) < n ? fLen(LANE(W[0])[e]) : 0u;
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) { LANE(lens)[r] = fLen(LANE(W[0])[r]); }
     }
-    scanLeaves(lens, cst);
+    scanRows(lens, cst, nr);
   }
 
   FMT_DEV uint32_t charStartOf(int j) const {
+    if (j >= n) return static_cast<uint32_t>(nChars);
     Lane<V8> cst;
-    charStarts(cst);
-    return j >= n ? static_cast<uint32_t>(nChars) : readlane(selectE(cst, j % E), j / E);
+    charStarts(cst, (j >> 6) + 1);
+    return readlane(selectRow(cst, j >> 6), j & 63);
+  }
+
+  // First leaf (document order) whose row bit is set in a per-lane row bitmask, or -1.
+  FMT_DEV static int firstSet(const Lane<uint32_t>& bits, int nr) {
+    FOR_ROWS(r, 0, nr) {
+      Lane<bool> p;
+      FOR_LANES(l) { LANE(p) = ((LANE(bits) >> r) & 1u) != 0; }
+      const uint64_t m = ballot(p);
+      if (m != 0) return r * 64 + ctz64(m);
+    }
+    return -1;
   }
 
   // First leaf index with block id b (leaf blocks are contiguous runs), or -1.
   FMT_DEV int firstLeafOf(uint32_t b) const {
-    Lane<uint32_t> firstE;
-    Lane<bool> has;
-    FOR_LANES(l) {
-      uint32_t fe = E;
-#pragma unroll
-      for (int e = E - 1; e >= 0; e--)
-        if (l * E + e < n && fBlk(LANE(W[0])[e]) == b) fe = e;
-      LANE(firstE) = fe;
-      LANE(has) = fe < E;
+    const int nr = rows();
+    FOR_ROWS(r, 0, nr) {
+      Lane<bool> p;
+      FOR_LANES(l) { LANE(p) = r * 64 + l < n && fBlk(LANE(W[0])[r]) == b; }
+      const uint64_t m = ballot(p);
+      if (m != 0) return r * 64 + ctz64(m);
     }
-    const uint64_t m = ballot(has);
-    if (m == 0) return -1;
-    const int lane = ctz64(m);
-    return lane * E + static_cast<int>(readlane(firstE, lane));
+    return -1;
   }
 
-  FMT_DEV int findLeafById(uint32_t id) const {
-    Lane<uint32_t> hitE;
-    Lane<bool> has;
-    FOR_LANES(l) {
-      uint32_t he = E;
-#pragma unroll
-      for (int e = 0; e < E; e++)
-        if (l * E + e < n && fId(LANE(W[4])[e]) == id) he = e;
-      LANE(hitE) = he;
-      LANE(has) = he < E;
+  FMT_DEV int findLeafById(uint32_t id) const {  // ids start at 1, so empty slots never match
+    const int nr = rows();
+    FOR_ROWS(r, 0, nr) {
+      Lane<bool> p;
+      FOR_LANES(l) { LANE(p) = fId(LANE(W[4])[r]) == id; }
+      const uint64_t m = ballot(p);
+      if (m != 0) return r * 64 + ctz64(m);
     }
-    const uint64_t m = ballot(has);
-    if (m == 0) return -1;
-    const int lane = ctz64(m);
-    return lane * E + static_cast<int>(readlane(hitE, lane));
+    return -1;
   }
 
   // ------------------------------------------------------------------ chars (LDS, doc order)
@@ -394,13 +373,14 @@ class Doc {
 
   // Re-tag leaves [first, first+count) with block id b.
   FMT_DEV void tagLeaves(int first, int count, uint32_t b) {
-    FOR_LANES(l) {
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const int idx = l * E + e;
+    if (count <= 0) return;
+    const int r0 = first >> 6, r1 = ((first + count - 1) >> 6) + 1;
+    FOR_ROWS(r, r0, r1) {
+      FOR_LANES(l) {
+        const int idx = r * 64 + l;
         if (idx >= first && idx < first + count) {
-          const uint32_t w0 = LANE(W[0])[e];
-          LANE(W[0])[e] = mkW0(fLen(w0), b, fProps(w0));
+          const uint32_t w0 = LANE(W[0])[r];
+          LANE(W[0])[r] = mkW0(fLen(w0), b, fProps(w0));
         }
       }
     }
@@ -579,223 +559,201 @@ class Doc {
   }
 
   // ------------------------------------------------------------------ ops
-  // addToLRUSet for every hit leaf in document order: only the first hit of each block can add
-  // (the first one sets needsScour, mergeTree.ts:812-822).
-  FMT_DEV void lruForHits(const Lane<uint32_t>& hits, int seq) {
-    // exclusive max-scan of (index << 8 | block) over hit leaves gives each leaf's previous hit
-    Lane<int32_t> laneLast;
-    FOR_LANES(l) {
-      int32_t last = -1;
-#pragma unroll
-      for (int e = 0; e < E; e++)
-        if ((LANE(hits) >> e) & 1u) last = ((l * E + e) << 8) | static_cast<int32_t>(fBlk(LANE(W[0])[e]));
-      LANE(laneLast) = last;
-    }
-    const Lane<int32_t> before = waveExclusiveMax(laneLast, -1);
-    Lane<uint32_t> cand;
-    Lane<bool> has;
-    FOR_LANES(l) {
-      int32_t prev = LANE(before);
-      uint32_t c = 0;
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        if ((LANE(hits) >> e) & 1u) {
-          const int32_t b = static_cast<int32_t>(fBlk(LANE(W[0])[e]));
-          if (prev < 0 || (prev & 0xFF) != b) c |= 1u << e;
-          prev = ((l * E + e) << 8) | b;
-        }
-      }
-      LANE(cand) = c;
-      LANE(has) = c != 0;
-    }
-    uint64_t m = ballot(has);
-    while (m) {
-      const int lane = ctz64(m);
-      uint32_t c = readlane(cand, lane);
-      while (c) {
-        const int e = ctz32(c);
-        c &= c - 1;
-        const int j = lane * E + e;
-        const int b = static_cast<int>(fBlk(readField(j, 0)));
-        if (uni(static_cast<int>(s->blk[b].needsScour)) != 1 && seq > curSeq) {
-          s->blk[b].needsScour = 1;
-          waveSync();
-          heapAdd(seq, fId(readField(j, 4)));
-          if (status != FMT_OK) return;
-        }
-      }
-      m &= m - 1;
+  // addToLRUSet (mergeTree.ts:812-822) for leaf j: the first registration of a block sets
+  // needsScour; later leaves of that block are no-ops until zamboni clears it.
+  FMT_DEV void lruForLeaf(int j, int b, int seq) {
+    if (uni(static_cast<int>(s->blk[b].needsScour)) != 1 && seq > curSeq) {
+      s->blk[b].needsScour = 1;
+      waveSync();
+      heapAdd(seq, fId(readField(j, 4)));
     }
   }
 
-  // One member op of a remote message (client.ts:1291-1327). The phases share one view scan:
-  //   phase < nb : ensureIntervalBoundary at pos1 (and pos2) — mergeTree.ts:1798-1808: split the
-  //                unique leaf that strictly contains the position in the op's view;
-  //   phase == nb: insert (mergeTree.ts:1484-1750) or collect the nodeMap range (mergeTree.ts:
-  //                2961-3020) for remove / annotate.
-  FMT_DEV void applyOp(const fmt_mt_op& op) {
+  // addToLRUSet for every hit leaf in document order. Leaf blocks are contiguous runs, so only a
+  // hit whose block differs from the previous hit's can register.
+  FMT_DEV void lruForHits(const Lane<uint32_t>& hits, int seq, int nr) {
+    int prevBlk = -1;
+    for (int r = 0; r < nr; r++) {
+      Lane<bool> p;
+      FOR_LANES(l) { LANE(p) = ((LANE(hits) >> r) & 1u) != 0; }
+      uint64_t m = ballot(p);
+      while (m) {
+        const int j = r * 64 + ctz64(m);
+        m &= m - 1;
+        const int b = static_cast<int>(fBlk(readField(j, 0)));
+        if (b != prevBlk) {
+          lruForLeaf(j, b, seq);
+          if (status != FMT_OK) return;
+        }
+        prevBlk = b;
+      }
+    }
+  }
+
+  // ensureIntervalBoundary (mergeTree.ts:1798-1808): split the unique leaf that strictly contains
+  // pos in the op's view. Returns false only on failure.
+  FMT_DEV bool splitAt(int pos, int refSeq, int client) {
+    const int nr = rows();
+    Lane<V8> vis, st;
+    visLengths(refSeq, client, vis, nr);
+    scanRows(vis, st, nr);
+    stamp(kPfScan);
+    FOR_ROWS(r, 0, nr) {
+      Lane<bool> p;
+      FOR_LANES(l) {
+        const int sp = static_cast<int>(LANE(st)[r]);
+        LANE(p) = sp < pos && pos < sp + static_cast<int>(LANE(vis)[r]);
+      }
+      const uint64_t m = ballot(p);
+      if (m != 0) {
+        const int lane = ctz64(m);
+        const int j = r * 64 + lane;
+        const int offset = pos - static_cast<int>(readlane(row(st, r), lane));
+        LeafRec rec;
+        const uint32_t w0 = readlane(row(W[0], r), lane);
+        rec.w[0] = mkW0(fLen(w0) - static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
+        rec.w[1] = readlane(row(W[1], r), lane);
+        rec.w[2] = readlane(row(W[2], r), lane);
+        rec.w[3] = readlane(row(W[3], r), lane);
+        rec.w[4] = mkW4(nextId++, fClient(readlane(row(W[4], r), lane)));
+        FOR_LANES(l) {
+          if (l == lane) LANE(W[0])[r] = mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
+        }
+        if (!insertLeafAt(j + 1, rec)) return false;
+        childAdded(static_cast<int>(fBlk(w0)));
+        stamp(kPfSplit);
+        return status == FMT_OK;
+      }
+    }
+    stamp(kPfSplit);
+    return true;
+  }
+
+  // insertSegments (mergeTree.ts:1484-1517) after the boundary split: the new leaf goes before the
+  // first leaf whose view prefix equals pos, leaves removed at/below minSeq skipped except the very
+  // last leaf (mergeTree.ts:1862-1875); past the end it is appended to the last leaf's block.
+  FMT_DEV void insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
-    const bool isInsert = op.type == FMT_MT_INSERT;
-    const int nb = isInsert ? 1 : 2;
+    const int pos = op.pos1, len = op.len;
+    if (len <= 0) return;
+    const int nr = rows();
+    Lane<V8> vis, st;
+    visLengths(refSeq, client, vis, nr);
+    const uint32_t total = scanRows(vis, st, nr);
+    stamp(kPfScan);
+    int insIdx = -1;
+    FOR_ROWS(r, 0, nr) {
+      if (insIdx < 0) {
+        Lane<bool> p;
+        FOR_LANES(l) {
+          const int idx = r * 64 + l;
+          const bool undefinedLen = static_cast<int32_t>(LANE(W[2])[r]) <= minSeq;
+          const bool skipped = undefinedLen && idx != n - 1;
+          LANE(p) = idx < n && !skipped && static_cast<int>(LANE(st)[r]) == pos;
+        }
+        const uint64_t m = ballot(p);
+        if (m != 0) insIdx = r * 64 + ctz64(m);
+      }
+    }
+    int blk;
+    if (insIdx >= 0) {
+      blk = static_cast<int>(fBlk(readField(insIdx, 0)));
+    } else {
+      if (pos != static_cast<int>(total)) {  // "MergeTree insert failed" (mergeTree.ts:1629)
+        fail(FMT_E_DATA);
+        return;
+      }
+      insIdx = n;
+      blk = n > 0 ? static_cast<int>(fBlk(readField(n - 1, 0))) : root;
+    }
+    if (nChars + len > kCapChars) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    const int cpos = static_cast<int>(charStartOf(insIdx));
+    charsShiftUp(cpos, len);
+    FOR_LANES(l) {
+      if (l < len) s->chars[cpos + l] = static_cast<uint16_t>(LANE(text0));
+      for (int t = l + 64; t < len; t += 64) s->chars[cpos + t] = in.text[op.payload + t];
+    }
+    waveSync();
+    nChars += len;
+    LeafRec rec;
+    rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), kPropsUndef);
+    rec.w[1] = static_cast<uint32_t>(seq);
+    rec.w[2] = static_cast<uint32_t>(kNotRemoved);
+    rec.w[3] = 0;
+    rec.w[4] = mkW4(nextId++, client);
+    if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
+      s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
+      waveSync();
+    }
+    if (!insertLeafAt(insIdx, rec)) return;
+    childAdded(blk);
+    if (status != FMT_OK) return;
+    stamp(kPfInsert);
+    lruForLeaf(insIdx, static_cast<int>(fBlk(readField(insIdx, 0))), seq);
+    stamp(kPfLru);
+  }
+
+  // One member op of a remote message (client.ts:1291-1327).
+  FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
+    const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
+    if (op.type == FMT_MT_INSERT) {
+      if (!splitAt(op.pos1, refSeq, client)) return;
+      insertText(op, text0);
+      return;
+    }
+    if (!splitAt(op.pos1, refSeq, client)) return;
+    if (!splitAt(op.pos2, refSeq, client)) return;
+    // nodeMap (mergeTree.ts:2961-3020): leaves of positive view length inside [start, end)
+    const int nr = rows();
+    const int start = op.pos1, end = op.pos2;
+    Lane<V8> vis, st;
+    visLengths(refSeq, client, vis, nr);
+    scanRows(vis, st, nr);
+    stamp(kPfScan);
     Lane<uint32_t> hits;
     FOR_LANES(l) { LANE(hits) = 0u; }
-    for (int phase = 0;; phase++) {
-      Lane<V8> vis, st;
-      visLengths(refSeq, client, vis);
-      const uint32_t total = scanLeaves(vis, st);
-      stamp(kPfScan);
-      int insIdx = -1, blk = 0;
-      LeafRec rec;
-      if (phase < nb) {
-        const int pos = phase == 0 ? op.pos1 : op.pos2;
-        Lane<uint32_t> hitE;
-        Lane<bool> has;
-        FOR_LANES(l) {
-          uint32_t he = E;
-#pragma unroll
-          for (int e = 0; e < E; e++) {
-            const int sp = static_cast<int>(LANE(st)[e]);
-            if (sp < pos && pos < sp + static_cast<int>(LANE(vis)[e])) he = e;
-          }
-          LANE(hitE) = he;
-          LANE(has) = he < E;
-        }
-        const uint64_t m = ballot(has);
-        if (m != 0) {
-          const int lane = ctz64(m);
-          const int e = static_cast<int>(readlane(hitE, lane));
-          const int j = lane * E + e;
-          const int offset = pos - static_cast<int>(readlane(selectE(st, e), lane));
-          const uint32_t w0 = readField(j, 0), w4 = readField(j, 4);
-          rec.w[0] = mkW0(fLen(w0) - static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
-          rec.w[1] = readField(j, 1);
-          rec.w[2] = readField(j, 2);
-          rec.w[3] = readField(j, 3);
-          rec.w[4] = mkW4(nextId++, fClient(w4));
-          writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0)));
-          insIdx = j + 1;
-          blk = static_cast<int>(fBlk(w0));
-        }
-      } else if (isInsert) {
-        const int pos = op.pos1, len = op.len;
-        if (len > 0) {
-          // anchor: the first leaf whose view prefix equals pos, leaves removed at/below minSeq
-          // skipped except the very last leaf (mergeTree.ts:1862-1875)
-          Lane<uint32_t> anchorE;
-          Lane<bool> has;
-          FOR_LANES(l) {
-            uint32_t ae = E;
-#pragma unroll
-            for (int e = E - 1; e >= 0; e--) {
-              const int idx = l * E + e;
-              const bool undefinedLen = static_cast<int32_t>(LANE(W[2])[e]) <= minSeq;
-              const bool skipped = undefinedLen && idx != n - 1;
-              if (idx < n && !skipped && static_cast<int>(LANE(st)[e]) == pos) ae = e;
-            }
-            LANE(anchorE) = ae;
-            LANE(has) = ae < E;
-          }
-          const uint64_t m = ballot(has);
-          if (m != 0) {
-            const int lane = ctz64(m);
-            insIdx = lane * E + static_cast<int>(readlane(anchorE, lane));
-            blk = static_cast<int>(fBlk(readField(insIdx, 0)));
-          } else {
-            if (pos != static_cast<int>(total)) {  // "MergeTree insert failed" (mergeTree.ts:1629)
-              fail(FMT_E_DATA);
-              return;
-            }
-            insIdx = n;
-            blk = n > 0 ? static_cast<int>(fBlk(readField(n - 1, 0))) : root;
-          }
-          if (nChars + len > kCapChars) {
-            fail(FMT_E_CAPACITY);
-            return;
-          }
-          const int cpos = static_cast<int>(charStartOf(insIdx));
-          charsShiftUp(cpos, len);
-          const uint16_t* src = in.text + op.payload;
-          FOR_LANES(l) {
-            for (int t = l; t < len; t += 64) s->chars[cpos + t] = src[t];
-          }
-          waveSync();
-          nChars += len;
-          rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), kPropsUndef);
-          rec.w[1] = static_cast<uint32_t>(seq);
-          rec.w[2] = static_cast<uint32_t>(kNotRemoved);
-          rec.w[3] = 0;
-          rec.w[4] = mkW4(nextId++, client);
-          if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
-            s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
-            waveSync();
-          }
-        }
-      } else {
-        const int start = op.pos1, end = op.pos2;
-        FOR_LANES(l) {
-          uint32_t h = 0;
-#pragma unroll
-          for (int e = 0; e < E; e++) {
-            const int sp = static_cast<int>(LANE(st)[e]);
-            if (LANE(vis)[e] > 0 && sp >= start && sp < end) h |= 1u << e;
-          }
-          LANE(hits) = h;
-        }
-        break;
-      }
-      if (insIdx >= 0) {
-        if (!insertLeafAt(insIdx, rec)) return;
-        childAdded(blk);
-        if (status != FMT_OK) return;
-      }
-      stamp(phase < nb ? kPfSplit : kPfInsert);
-      if (phase >= nb) {
-        if (insIdx >= 0) {
-          const int lane = insIdx / E, e = insIdx % E;
-          FOR_LANES(l) { LANE(hits) = l == lane ? (1u << e) : 0u; }
-        }
-        break;
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const int sp = static_cast<int>(LANE(st)[r]);
+        if (LANE(vis)[r] > 0 && sp >= start && sp < end) LANE(hits) |= 1u << r;
       }
     }
     if (op.type == FMT_MT_REMOVE) {
       // markRangeRemoved (mergeTree.ts:2292-2383): first remove stays the lowest seq
-      FOR_LANES(l) {
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-          if ((LANE(hits) >> e) & 1u) {
-            const int32_t rm = static_cast<int32_t>(LANE(W[2])[e]);
-            LANE(W[2])[e] = static_cast<uint32_t>(rm < seq ? rm : seq);
-            LANE(W[3])[e] |= 1u << client;
+      FOR_ROWS(r, 0, nr) {
+        FOR_LANES(l) {
+          if ((LANE(hits) >> r) & 1u) {
+            const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
+            LANE(W[2])[r] = static_cast<uint32_t>(rm < seq ? rm : seq);
+            LANE(W[3])[r] |= 1u << client;
           }
         }
       }
-    } else if (op.type == FMT_MT_ANNOTATE) {
+    } else {
       // annotateRange (mergeTree.ts:2009-2081): one prop-set transition per distinct old set
       Lane<uint32_t> todo = hits;
       for (;;) {
-        Lane<bool> has;
-        FOR_LANES(l) { LANE(has) = LANE(todo) != 0; }
-        const uint64_t m = ballot(has);
-        if (m == 0) break;
-        const int lane = ctz64(m);
-        const int e = ctz32(readlane(todo, lane));
-        const uint32_t old = fProps(readField(lane * E + e, 0));
+        const int j = firstSet(todo, nr);
+        if (j < 0) break;
+        const uint32_t old = fProps(readField(j, 0));
         const uint32_t nw = applyProps(old, op.payload);
         if (status != FMT_OK) return;
-        FOR_LANES(l) {
-#pragma unroll
-          for (int k = 0; k < E; k++) {
-            if (((LANE(todo) >> k) & 1u) && fProps(LANE(W[0])[k]) == old) {
-              const uint32_t w0 = LANE(W[0])[k];
-              LANE(W[0])[k] = mkW0(fLen(w0), fBlk(w0), nw);
-              LANE(todo) &= ~(1u << k);
+        FOR_ROWS(r, 0, nr) {
+          FOR_LANES(l) {
+            if (((LANE(todo) >> r) & 1u) && fProps(LANE(W[0])[r]) == old) {
+              const uint32_t w0 = LANE(W[0])[r];
+              LANE(W[0])[r] = mkW0(fLen(w0), fBlk(w0), nw);
+              LANE(todo) &= ~(1u << r);
             }
           }
         }
       }
     }
     stamp(kPfRange);
-    lruForHits(hits, seq);
+    lruForHits(hits, seq, nr);
     stamp(kPfLru);
   }
 
@@ -807,7 +765,7 @@ class Doc {
     if (cnt == 0) return 0;
     const int first = firstLeafOf(static_cast<uint32_t>(b));
     Lane<V8> cst;
-    charStarts(cst);
+    charStarts(cst, ((first + cnt - 1) >> 6) + 1);
     // serial decisions over <= 7 leaves: keep, merge into the previous kept leaf, or drop
     uint32_t mergeMask = 0, dropMask = 0;
     int prev = -1;
@@ -822,7 +780,7 @@ class Doc {
       const int32_t rm = static_cast<int32_t>(readField(j, 2));
       if (rm == kNotRemoved) {
         if (ins <= minSeq) {
-          const uint32_t cs = readlane(selectE(cst, j % E), j / E);
+          const uint32_t cs = readlane(selectRow(cst, j >> 6), j & 63);
           const bool lastNl = len > 0 && uni(static_cast<uint32_t>(s->chars[cs + len - 1])) == 10u;
           const bool canAppend = prev >= 0 && !prevNl &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) ||
@@ -861,7 +819,7 @@ class Doc {
       const int j = first + k;
       if ((dropMask >> k) & 1u) {
         const uint32_t len = fLen(readField(j, 0));
-        const int cs = static_cast<int>(readlane(selectE(cst, j % E), j / E));
+        const int cs = static_cast<int>(readlane(selectRow(cst, j >> 6), j & 63));
         charsShiftDown(cs + static_cast<int>(len), static_cast<int>(len));
         nChars -= static_cast<int>(len);
       }
@@ -988,7 +946,7 @@ class Doc {
     FOR_LANES(l) {
       V8 z;
 #pragma unroll
-      for (int e = 0; e < E; e++) z[e] = 0u;
+      for (int r = 0; r < kRows; r++) z[r] = 0u;
       LANE(W[0]) = z;
       LANE(W[1]) = z;
       LANE(W[2]) = z;
@@ -1034,26 +992,61 @@ class Doc {
     waveSync();
   }
 
+  // Op records are prefetched two ahead (lanes 0..7 hold the eight dwords of one fmt_mt_op) and
+  // an insert's first 64 text units one op ahead, so the global-load latency of the dependent op
+  // stream overlaps the previous op's work.
+  FMT_DEV Lane<uint32_t> fetchOp(uint64_t i) const {
+    Lane<uint32_t> x;
+    if (i < in.end) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(in.ops + i);
+      FOR_LANES(l) { LANE(x) = l < 8 ? p[l] : 0u; }
+    } else {
+      FOR_LANES(l) { LANE(x) = 0u; }
+    }
+    return x;
+  }
+
+  FMT_DEV static fmt_mt_op decodeOp(const Lane<uint32_t>& rec) {
+    fmt_mt_op op;
+    op.seq = static_cast<int32_t>(readlane(rec, 0));
+    op.ref_seq = static_cast<int32_t>(readlane(rec, 1));
+    op.min_seq = static_cast<int32_t>(readlane(rec, 2));
+    op.pos1 = static_cast<int32_t>(readlane(rec, 3));
+    op.pos2 = static_cast<int32_t>(readlane(rec, 4));
+    op.payload = readlane(rec, 5);
+    const uint32_t lct = readlane(rec, 6);
+    op.len = static_cast<uint16_t>(lct & 0xFFFF);
+    op.client = static_cast<uint8_t>((lct >> 16) & 0xFF);
+    op.type = static_cast<uint8_t>(lct >> 24);
+    op.flags = readlane(rec, 7);
+    return op;
+  }
+
+  FMT_DEV Lane<uint32_t> fetchText(const Lane<uint32_t>& rec) const {
+    const uint32_t lct = readlane(rec, 6);
+    const int len = (lct >> 24) == FMT_MT_INSERT ? static_cast<int>(lct & 0xFFFF) : 0;
+    const uint32_t payload = readlane(rec, 5);
+    Lane<uint32_t> x;
+    FOR_LANES(l) { LANE(x) = l < len ? static_cast<uint32_t>(in.text[payload + l]) : 0u; }
+    return x;
+  }
+
   FMT_DEV void replay() {
     stamp(kPfOutput);
+    Lane<uint32_t> rec0 = fetchOp(in.begin);
+    Lane<uint32_t> rec1 = fetchOp(in.begin + 1);
+    Lane<uint32_t> txt0 = fetchText(rec0);
     for (uint64_t i = in.begin; i < in.end; i++) {
-      fmt_mt_op op = in.ops[i];
-      op.seq = uni(op.seq);
-      op.ref_seq = uni(op.ref_seq);
-      op.min_seq = uni(op.min_seq);
-      op.pos1 = uni(op.pos1);
-      op.pos2 = uni(op.pos2);
-      op.payload = uni(op.payload);
-      const uint32_t lenClientType = uni(static_cast<uint32_t>(op.len) | (static_cast<uint32_t>(op.client) << 16) |
-                                         (static_cast<uint32_t>(op.type) << 24));
-      op.len = static_cast<uint16_t>(lenClientType & 0xFFFF);
-      op.client = static_cast<uint8_t>((lenClientType >> 16) & 0xFF);
-      op.type = static_cast<uint8_t>(lenClientType >> 24);
+      const fmt_mt_op op = decodeOp(rec0);
+      const Lane<uint32_t> text = txt0;
+      rec0 = rec1;
+      txt0 = fetchText(rec0);
+      rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
       if (op.client > kMaxClient || op.type > FMT_MT_ANNOTATE) fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
-      else applyOp(op);
-      const bool lastMember = i + 1 == in.end || (uni(in.ops[i + 1].flags) & FMT_MT_F_GROUP_CONT) == 0;
+      else applyOp(op, text);
+      const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       // zamboni once inside the op (mergeTree.ts:1510-1516, 2074-2080, 2376-2382), then, after the
       // message's last member, updateSeqNumbers (client.ts:1381-1391) → setMinSeq
       // (mergeTree.ts:1147-1166), which runs zamboni again only if minSeq advanced.
@@ -1079,49 +1072,47 @@ class Doc {
   }
 
   FMT_DEV void writeOutputs(const DocOutputs& out) {
+    const int nr = rows();
     // char offsets and leaf-block ordinals
     Lane<V8> cst;
-    charStarts(cst);
+    charStarts(cst, nr);
     Lane<V8> startFlag, ord;
-    const Lane<uint32_t> prevBlk7 = shflUp1(selectE(W[0], E - 1));
-    FOR_LANES(l) {
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const int idx = l * E + e;
-        const uint32_t b = fBlk(LANE(W[0])[e]);
-        const uint32_t pb = e == 0 ? fBlk(LANE(prevBlk7)) : fBlk(LANE(W[0])[e - 1]);
-        LANE(startFlag)[e] = idx < n && (idx == 0 || b != pb) ? 1u : 0u;
+    FOR_ROWS(r, 0, nr) {
+      const Lane<uint32_t> cur = row(W[0], r);
+      const Lane<uint32_t> up = shflUp1(cur);
+      const uint32_t carry = r > 0 ? readlane(row(W[0], r > 0 ? r - 1 : 0), 63) : 0u;
+      FOR_LANES(l) {
+        const int idx = r * 64 + l;
+        const uint32_t pb = fBlk(l == 0 ? carry : LANE(up));
+        LANE(startFlag)[r] = idx < n && (idx == 0 || fBlk(LANE(cur)) != pb) ? 1u : 0u;
       }
     }
-    const uint32_t nLeafBlocks = scanLeaves(startFlag, ord);
+    const uint32_t nLeafBlocks = scanRows(startFlag, ord, nr);
     uint32_t visible = 0;
     {
       Lane<V8> vlen, tmp;
-      FOR_LANES(l) {
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-          const int idx = l * E + e;
-          const bool live = idx < n && static_cast<int32_t>(LANE(W[2])[e]) == kNotRemoved;
-          LANE(vlen)[e] = live ? fLen(LANE(W[0])[e]) : 0u;
+      FOR_ROWS(r, 0, nr) {
+        FOR_LANES(l) {
+          const bool live = static_cast<int32_t>(LANE(W[2])[r]) == kNotRemoved;
+          LANE(vlen)[r] = live ? fLen(LANE(W[0])[r]) : 0u;
         }
       }
-      visible = scanLeaves(vlen, tmp);
+      visible = scanRows(vlen, tmp, nr);
     }
-    FOR_LANES(l) {
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const int idx = l * E + e;
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const int idx = r * 64 + l;
         if (idx < n) {
           fmt_mt_leaf L;
-          const uint32_t w0 = LANE(W[0])[e];
-          L.ins_seq = static_cast<int32_t>(LANE(W[1])[e]);
-          L.rm_seq = static_cast<int32_t>(LANE(W[2])[e]);
-          L.rm_clients = LANE(W[3])[e];
-          L.char_off = LANE(cst)[e];
+          const uint32_t w0 = LANE(W[0])[r];
+          L.ins_seq = static_cast<int32_t>(LANE(W[1])[r]);
+          L.rm_seq = static_cast<int32_t>(LANE(W[2])[r]);
+          L.rm_clients = LANE(W[3])[r];
+          L.char_off = LANE(cst)[r];
           L.len = static_cast<uint16_t>(fLen(w0));
-          L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[e]));
+          L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[r]));
           L.props = fProps(w0) == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(fProps(w0));
-          L.block = static_cast<uint16_t>(LANE(ord)[e] + LANE(startFlag)[e] - 1u);
+          L.block = static_cast<uint16_t>(LANE(ord)[r] + LANE(startFlag)[r] - 1u);
           L.pad = 0;
           out.leaves[idx] = L;
         }

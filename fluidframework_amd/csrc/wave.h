@@ -29,7 +29,7 @@ struct Lane {
 typedef uint32_t V8 __attribute__((ext_vector_type(8)));
 typedef uint32_t V4 __attribute__((ext_vector_type(4)));
 #define LANE(x) ((x).v)
-#define FOR_LANES(l) for (int l = static_cast<int>(__lane_id()), l##_once = 1; l##_once; l##_once = 0)
+#define FOR_LANES(l) for ([[maybe_unused]] int l = static_cast<int>(__lane_id()), l##_once = 1; l##_once; l##_once = 0)
 
 FMT_DEV int waveLane() { return static_cast<int>(__lane_id()); }
 

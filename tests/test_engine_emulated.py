@@ -45,3 +45,45 @@ def test_emulated_engine_matches_oracle_on_conflict_farm(orc, n_clients, min_len
     for d in range(batch.n_docs):
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def _no_zamboni_batch(sizes, seed=11):
+    """One client inserting 2-char runs at random visible positions with minSeq pinned at 0, so no
+    leaf is ever merged or dropped: leaf counts climb through every register row to capacity."""
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+
+    rng = np.random.default_rng(seed)
+    b = MergeTreeStreamBuilder()
+    for n_ops in sizes:
+        d = b.begin_doc()
+        length = 0
+        for k in range(n_ops):
+            seq = k + 1
+            if k % 7 == 6 and length > 4:  # some removes and annotates in the mix
+                a = int(rng.integers(0, length - 2))
+                contents = {"type": 1, "pos1": a, "pos2": a + 1} if k % 2 else \
+                    {"type": 2, "pos1": a, "pos2": a + 2, "props": {"k": int(k % 3)}}
+                if k % 2:
+                    length -= 1
+            else:
+                contents = {"type": 0, "pos1": int(rng.integers(0, length + 1)), "seg": "xy"}
+                length += 2
+            d.add_message({"clientId": "B", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+                           "minimumSequenceNumber": 0, "contents": contents})
+    return b.finish()
+
+
+def test_emulated_engine_fills_every_row_to_capacity(orc):
+    cl, cc, cp = emu_caps()
+    batch = _no_zamboni_batch([60, 130, 200, 260, 300, 400, 420, 500])
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch)
+    assert oh["n_leaves"].max() > cl  # the last documents overflow the 512-leaf engine
+    assert ((oh["n_leaves"] > 448) & (oh["n_leaves"] <= cl)).any()  # and one ends in the top row
+    for d in range(batch.n_docs):
+        if oh[d]["n_leaves"] > cl:
+            assert hdr[d]["status"] == -3, f"doc {d}: expected FMT_E_CAPACITY"
+            continue
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"

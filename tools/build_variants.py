@@ -10,13 +10,30 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "fluidframework_amd", "csrc")
 
 
-def build(name, edits):
+def _export_rev(rev, root):
+    """csrc/ and include/fmt.h as of git revision `rev` (a committed engine version to A/B against)."""
+    for rel in ("fluidframework_amd/csrc", "include"):
+        files = subprocess.run(["git", "ls-tree", "-r", "--name-only", rev, rel], cwd=REPO, check=True,
+                               capture_output=True, text=True).stdout.split()
+        for f in files:
+            if "/gen/" in f:
+                continue
+            dst = os.path.join(root, f)
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            data = subprocess.run(["git", "show", f"{rev}:{f}"], cwd=REPO, check=True, capture_output=True).stdout
+            open(dst, "wb").write(data)
+
+
+def build(name, edits, rev=None):
     root = os.path.join(REPO, "build", "variants", name)
     csrc = os.path.join(root, "fluidframework_amd", "csrc")
     shutil.rmtree(root, ignore_errors=True)
-    shutil.copytree(SRC, csrc, ignore=shutil.ignore_patterns("gen"))
-    os.makedirs(os.path.join(root, "include"), exist_ok=True)
-    shutil.copy(os.path.join(REPO, "include", "fmt.h"), os.path.join(root, "include", "fmt.h"))
+    if rev:
+        _export_rev(rev, root)
+    else:
+        shutil.copytree(SRC, csrc, ignore=shutil.ignore_patterns("gen"))
+        os.makedirs(os.path.join(root, "include"), exist_ok=True)
+        shutil.copy(os.path.join(REPO, "include", "fmt.h"), os.path.join(root, "include", "fmt.h"))
     for fname, old, new in edits:
         p = os.path.join(csrc, fname)
         s = open(p).read()
@@ -40,8 +57,9 @@ def build(name, edits):
     return out
 
 
-LB2 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves)", "__launch_bounds__(64 * kMtWaves, 2)")
-LB3 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves)", "__launch_bounds__(64 * kMtWaves, 3)")
+LB1 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves, 2)", "__launch_bounds__(64 * kMtWaves)")
+LB3 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves, 2)", "__launch_bounds__(64 * kMtWaves, 3)")
+LB4 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves, 2)", "__launch_bounds__(64 * kMtWaves, 4)")
 NODPP = ("wave.h", "#define FMT_USE_DPP 1", "#define FMT_USE_DPP 0")
 
 NOFENCE = ("wave.h", """FMT_DEV void waveSync() {
@@ -53,16 +71,20 @@ PROF = ("mt_engine.h", "#define FMT_PROFILE 0", "#define FMT_PROFILE 1")
 
 VARIANTS = {
     "prof": [PROF],
-    "nofence": [NOFENCE],
     "base": [],
-    "lb2_nodpp": [LB2, NODPP],
+    "nofence": [NOFENCE],
+    "lb1": [LB1],
     "lb3": [LB3],
-    "nolaunder": [("wave.h", 'FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }',
-                   "FMT_DEV void launder(V8&) {}")],
-    "lb2": [LB2],
+    "lb4": [LB4],
+    "nodpp": [NODPP],
 }
+REVS = {"v1": "352970f"}  # committed engines: row-per-lane leaf table (E = 8 leaves per lane)
+
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     for n in names:
-        build(n, VARIANTS[n])
+        if n in REVS:
+            build(n, [], rev=REVS[n])
+        else:
+            build(n, VARIANTS[n])
