@@ -172,6 +172,14 @@ def main():
         }
         log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
 
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of this same workload
+    # (tools/pmc_traffic.py; gfx950 FETCH_SIZE correction applied there), or null.
+    traffic = None
+    tkey = f"{args.workload}:{docs}x{opd}"
+    tpath = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get(tkey)
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -202,7 +210,9 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": None,
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_fetch_write": [traffic["fetch_bytes"], traffic["write_bytes"]] if traffic else None,
+                "traffic_source": traffic["source"][0].rsplit("/", 2)[0] if traffic else None,
                 "kernel": "mergeTreeKernel" if mt else "mapLwwKernel",
                 "limiter": ("per-document dependent op chain: VALU issue + LDS/readlane latency of one wave per "
                             "document (HBM fraction is reported for the contract; see DESIGN.md)") if mt

@@ -13,8 +13,9 @@
 // documents. Each lane owns one 16-byte op record per 64-op chunk (one coalesced dwordx4 load per
 // lane, 1 KiB per wave instruction). Per-key reductions are LDS atomics (ds_max_u32, ds_max_u64,
 // ds_min_u32) on a per-wave key table of key_bound entries. Pass 1 reduces kills, pass 2 reduces
-// sets; pass 2 re-reads the document's ops, which are L2-resident after pass 1 (HBM traffic stays
-// one read of every op). Bound: HBM bandwidth — 16 B read per op, 8 B written per key slot.
+// sets. A document of up to 1024 ops is read once into VGPRs (16 dwordx4 per lane, all issued
+// before the first LDS update) and both passes run on registers, so HBM sees every op record once.
+// Bound: HBM bandwidth — 16 B read per op, 8 B written per key slot.
 #include <hip/hip_runtime.h>
 
 #include "../../include/fmt.h"
@@ -36,7 +37,44 @@ __device__ __forceinline__ uint32_t waveMax(uint32_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void mapLwwKernel(const fmt_map_op* __restrict__ ops,
+// Reductions of one op record (pass 1: kills, pass 2: surviving sets).
+__device__ __forceinline__ void killOp(const uint4& r, uint32_t keyBound, uint32_t* kill, uint32_t& clearMax,
+                                       int* error) {
+  const uint32_t kind = r.w >> FMT_MAP_KIND_SHIFT;
+  if (kind == FMT_MAP_DELETE) {
+    if (r.y < keyBound) atomicMax(&kill[r.y], r.z);
+    else atomicOr(error, 1);
+  } else if (kind == FMT_MAP_CLEAR) {
+    clearMax = max(clearMax, r.z);
+  }
+}
+
+__device__ __forceinline__ void setOp(const uint4& r, uint32_t keyBound, const uint32_t* kill, uint32_t clearMax,
+                                      unsigned long long* last, uint32_t* first, int* error) {
+  if ((r.w >> FMT_MAP_KIND_SHIFT) != FMT_MAP_SET) return;
+  const uint32_t key = r.y, seq = r.z;
+  if (key >= keyBound) {
+    atomicOr(error, 1);
+    return;
+  }
+  if (seq > max(kill[key], clearMax)) {
+    atomicMax(&last[key], (static_cast<unsigned long long>(seq) << 32) | (r.w & FMT_MAP_VALUE_MASK));
+    atomicMin(&first[key], seq);
+  }
+}
+
+__device__ __forceinline__ void waveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Records held per lane by the single-pass path: a document of up to 64 * kRegChunks ops is read
+// from HBM exactly once into VGPRs, and both reductions run on the registers. Longer documents take
+// the two-pass streaming path (the second pass then hits L2 only partly).
+constexpr int kRegChunks = 16;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(64 * kWaves) void mapLwwKernel(const fmt_map_op* __restrict__ ops,
                                                     const uint64_t* __restrict__ offsets, uint32_t nDocs,
                                                     uint32_t keyBound, fmt_map_slot* __restrict__ out,
                                                     int* __restrict__ error) {
@@ -48,70 +86,73 @@ __global__ __launch_bounds__(256) void mapLwwKernel(const fmt_map_op* __restrict
   unsigned long long* last = reinterpret_cast<unsigned long long*>(base);
   uint32_t* kill = reinterpret_cast<uint32_t*>(base + static_cast<size_t>(keyBound) * 8);
   uint32_t* first = kill + keyBound;
+  const uint4* recs = reinterpret_cast<const uint4*>(ops);
 
   for (uint32_t doc = blockIdx.x * kWaves + wave; doc < nDocs; doc += gridDim.x * kWaves) {
-    for (uint32_t k = lane; k < keyBound; k += 64) {
-      last[k] = 0;
-      kill[k] = 0;
-      first[k] = 0xffffffffu;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     const uint64_t begin = offsets[doc], end = offsets[doc + 1];
-
-    // Pass 1: kills.
+    const uint64_t n = end - begin;
     uint32_t clearMax = 0;
-    for (uint64_t c = begin; c < end; c += 64 * kUnroll) {
-      uint4 rec[kUnroll];
+    if (n <= 64u * kRegChunks) {
+      // Issue every load of the document before touching LDS so they are all in flight together.
+      uint4 rec[kRegChunks];
+      const uint4 zero = make_uint4(0, 0, 0, 0);  // kind 0 = set of key 0 at seq 0: never survives
 #pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint64_t i = c + u * 64 + lane;
-        rec[u] = i < end ? *reinterpret_cast<const uint4*>(ops + i) : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint64_t i = c + u * 64 + lane;
-        if (i >= end) continue;
-        const uint32_t kind = rec[u].w >> FMT_MAP_KIND_SHIFT;
-        if (kind == FMT_MAP_DELETE) {
-          if (rec[u].y < keyBound) atomicMax(&kill[rec[u].y], rec[u].z);
-          else atomicOr(error, 1);
-        } else if (kind == FMT_MAP_CLEAR) {
-          clearMax = max(clearMax, rec[u].z);
+      for (int u = 0; u < kRegChunks; u++) {
+        const uint64_t i = u * 64 + lane;
+        rec[u] = zero;
+        if (u * 64u < n && i < n) {
+          // streamed once: non-temporal dwordx4 (6.1 vs 5.3 TB/s at M2, tools/bench_variants.py)
+          const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(recs + begin + i));
+          rec[u] = make_uint4(v.x, v.y, v.z, v.w);
         }
+      }
+      for (uint32_t k = lane; k < keyBound; k += 64) {
+        last[k] = 0;
+        kill[k] = 0;
+        first[k] = 0xffffffffu;
+      }
+      waveSync();
+#pragma unroll
+      for (int u = 0; u < kRegChunks; u++)
+        if (u * 64u < n && u * 64u + lane < n) killOp(rec[u], keyBound, kill, clearMax, error);
+      clearMax = waveMax(clearMax);
+      waveSync();
+#pragma unroll
+      for (int u = 0; u < kRegChunks; u++)
+        if (u * 64u < n && u * 64u + lane < n) setOp(rec[u], keyBound, kill, clearMax, last, first, error);
+    } else {
+      for (uint32_t k = lane; k < keyBound; k += 64) {
+        last[k] = 0;
+        kill[k] = 0;
+        first[k] = 0xffffffffu;
+      }
+      waveSync();
+      for (uint64_t c = begin; c < end; c += 64 * kUnroll) {
+        uint4 rec[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+          const uint64_t i = c + u * 64 + lane;
+          rec[u] = i < end ? recs[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++)
+          if (c + u * 64 + lane < end) killOp(rec[u], keyBound, kill, clearMax, error);
+      }
+      clearMax = waveMax(clearMax);
+      waveSync();
+      for (uint64_t c = begin; c < end; c += 64 * kUnroll) {
+        uint4 rec[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+          const uint64_t i = c + u * 64 + lane;
+          rec[u] = i < end ? recs[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++)
+          if (c + u * 64 + lane < end) setOp(rec[u], keyBound, kill, clearMax, last, first, error);
       }
     }
-    clearMax = waveMax(clearMax);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-
-    // Pass 2: surviving sets.
-    for (uint64_t c = begin; c < end; c += 64 * kUnroll) {
-      uint4 rec[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint64_t i = c + u * 64 + lane;
-        rec[u] = i < end ? *reinterpret_cast<const uint4*>(ops + i) : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint64_t i = c + u * 64 + lane;
-        if (i >= end) continue;
-        const uint32_t kind = rec[u].w >> FMT_MAP_KIND_SHIFT;
-        if (kind != FMT_MAP_SET) continue;
-        const uint32_t key = rec[u].y, seq = rec[u].z;
-        if (key >= keyBound) {
-          atomicOr(error, 1);
-          continue;
-        }
-        if (seq > max(kill[key], clearMax)) {
-          atomicMax(&last[key], (static_cast<unsigned long long>(seq) << 32) | (rec[u].w & FMT_MAP_VALUE_MASK));
-          atomicMin(&first[key], seq);
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    waveSync();
 
     fmt_map_slot* o = out + static_cast<uint64_t>(doc) * keyBound;
     for (uint32_t k = lane; k < keyBound; k += 64) {
@@ -121,8 +162,7 @@ __global__ __launch_bounds__(256) void mapLwwKernel(const fmt_map_op* __restrict
       s.birth_seq = l != 0 ? first[k] : 0;
       o[k] = s;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    waveSync();
   }
 }
 
@@ -132,8 +172,12 @@ hipError_t launchMapLww(const fmt_map_op* ops, const uint64_t* offsets, uint32_t
                         fmt_map_slot* out, int* error, int numCUs, hipStream_t stream) {
   const size_t lds = mapLwwLdsBytes(keyBound);
   const uint32_t wanted = (nDocs + kWaves - 1) / kWaves;
-  const int blocksPerCU = lds <= 20 * 1024 ? 8 : static_cast<int>(160 * 1024 / lds);
-  const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
+  // One resident wave of workgroups (occupancy is VGPR-limited by the register-held records).
+  int blocksPerCU = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mapLwwKernel, 64 * kWaves, lds) != hipSuccess ||
+      blocksPerCU <= 0)
+    blocksPerCU = 1;
+  const uint32_t cap = static_cast<uint32_t>(numCUs * blocksPerCU);
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
   hipLaunchKernelGGL(mapLwwKernel, dim3(grid), dim3(64 * kWaves), lds, stream, ops, offsets, nDocs, keyBound,
                      out, error);

@@ -81,6 +81,28 @@ def test_map_lww_large_key_pool(orc, engine):
     assert np.array_equal(got, exp)
 
 
+def test_map_lww_ragged_documents(orc, engine):
+    """Document lengths straddle the register-held path (≤1024 ops) and the streaming path, with
+    empty and one-op documents in between."""
+    from fluidframework_amd.streams import MapBatch
+
+    src = workloads.map_stream(64, 3000, key_pool=20, seed=13)
+    lens = [0, 1, 63, 64, 65, 1000, 1023, 1024, 1025, 2047, 3000, 0, 7, 511, 2999, 128] * 4
+    parts, offs = [], [0]
+    for d, n in enumerate(lens):
+        o = int(src.doc_op_offsets[d])
+        p = src.ops[o : o + n].copy()
+        p["doc"] = d
+        parts.append(p)
+        offs.append(offs[-1] + n)
+    batch = MapBatch(np.concatenate(parts), np.array(offs, dtype=np.uint64), src.key_bound, src.keys, src.values)
+    engine.map_load(batch)
+    engine.map_run()
+    got = engine.map_fetch()
+    exp, _ = orc.map_replay(batch, threads=16)
+    assert np.array_equal(got, exp)
+
+
 def test_mt_reference_fixture_checkpoints(orc, engine):
     """All 30 conflict-farm fixtures × 64 groups: text equals the reference's resultText and the
     whole converged tree equals the oracle's."""

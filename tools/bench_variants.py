@@ -22,11 +22,14 @@ def main():
     ap.add_argument("--docs", type=int, default=20000)
     ap.add_argument("--unique", type=int, default=2000)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--workload", choices=["mt", "map"], default="mt")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     paths = {os.path.basename(os.path.dirname(p)): p for p in glob.glob(os.path.join(REPO, "build/variants/*/libfmt.so"))}
     if a.variants:
         paths = {k: v for k, v in paths.items() if k in a.variants}
+    if a.workload == "map":
+        return bench_map(a, paths)
     batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
     ref = native.Engine(0)
     ref.mt_load(batch)
@@ -48,6 +51,33 @@ def main():
             times[name].append(e.stats().kernel_ms)
     n_ops = len(batch.ops)
     out = {name: {"ok": ok, "ms": times[name], "min_ms": min(times[name]), "mops": n_ops / min(times[name]) / 1e3}
+           for name, (e, ok) in engines.items()}
+    print(json.dumps(out))
+
+
+def bench_map(a, paths):
+    batch = workloads.map_stream(a.docs, 1000, key_pool=20, seed=5)
+    ref = native.Engine(0)
+    ref.map_load(batch)
+    ref.map_run()
+    ref_s = ref.map_fetch()
+    ref.close()
+    engines = {}
+    for name, p in sorted(paths.items()):
+        print(f"[ab] {name}", file=sys.stderr, flush=True)
+        e = native.Engine(0, lib_path=p)
+        e.map_load(batch)
+        e.map_run()
+        e.sync()
+        engines[name] = (e, bool(np.array_equal(e.map_fetch(), ref_s)))
+    times = {k: [] for k in engines}
+    for _ in range(a.rounds):
+        for name, (e, _) in engines.items():
+            e.map_run()
+            times[name].append(e.stats().kernel_ms)
+    n_ops = len(batch.ops)
+    out = {name: {"ok": ok, "ms": times[name], "min_ms": min(times[name]), "gops": n_ops / min(times[name]) / 1e6,
+                  "gbps": n_ops * 16.16 / min(times[name]) / 1e6}
            for name, (e, ok) in engines.items()}
     print(json.dumps(out))
 

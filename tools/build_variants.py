@@ -69,6 +69,17 @@ NOFENCE = ("wave.h", """FMT_DEV void waveSync() {
 
 PROF = ("mt_engine.h", "#define FMT_PROFILE 0", "#define FMT_PROFILE 1")
 
+# SharedMap kernel variants
+MAP_NT = ("map_lww.hip", "if (u * 64u < n && i < n) rec[u] = recs[begin + i];",
+          """if (u * 64u < n && i < n) {
+          typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+          const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(recs + begin + i));
+          rec[u] = make_uint4(v.x, v.y, v.z, v.w);
+        }""")
+MAP_W8 = ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 8;")
+MAP_W2 = ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 2;")
+MAP_LB2 = ("map_lww.hip", "__launch_bounds__(64 * kWaves) void mapLwwKernel", "__launch_bounds__(64 * kWaves, 2) void mapLwwKernel")
+
 VARIANTS = {
     "prof": [PROF],
     "base": [],
@@ -77,6 +88,14 @@ VARIANTS = {
     "lb3": [LB3],
     "lb4": [LB4],
     "nodpp": [NODPP],
+    "map_nt": [MAP_NT],
+    "map_w8": [MAP_W8],
+    "map_w2": [MAP_W2],
+    "map_lb2": [MAP_LB2],
+    "map_nt_w8": [MAP_NT, MAP_W8],
+    "map_nt_w2": [MAP_NT, MAP_W2],
+    "map_nt_w16": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 16;")],
+    "map_nt_w1": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 1;")],
 }
 REVS = {"v1": "352970f"}  # committed engines: row-per-lane leaf table (E = 8 leaves per lane)
 

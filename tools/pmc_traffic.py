@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""HBM traffic per kernel launch from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE run separately).
+
+Corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+  * both counters are in KiB;
+  * on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read, so it is
+    doubled before it is compared with a byte count;
+  * WRITE_SIZE is exact for 16-B-per-lane streaming stores (other widths are uncalibrated; the
+    merge-tree's 4-32 B result stores are reported uncorrected).
+
+Usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel substring>
+       <workload key> <out json>
+The output JSON maps a workload key (e.g. "mt:100000x2000") to the per-launch traffic record that
+bench.py copies into its `roofline.traffic` field when it runs the same workload.
+"""
+import csv
+import json
+import os
+import sys
+
+
+def per_launch(path, kernel, counter):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    if not vals:
+        raise SystemExit(f"{path}: no {counter} rows for {kernel}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    fetch_csv, write_csv, kernel, key, out = sys.argv[1:6]
+    f_kib, nf = per_launch(fetch_csv, kernel, "FETCH_SIZE")
+    w_kib, nw = per_launch(write_csv, kernel, "WRITE_SIZE")
+    rec = {
+        "kernel": kernel,
+        "fetch_bytes": f_kib * 1024 * 2,  # gfx950: FETCH_SIZE counts half of wide streaming reads
+        "write_bytes": w_kib * 1024,
+        "fetch_size_kib_raw": f_kib,
+        "write_size_kib_raw": w_kib,
+        "launches": [nf, nw],
+        "source": [os.path.relpath(fetch_csv), os.path.relpath(write_csv)],
+    }
+    rec["bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
+    db = json.load(open(out)) if os.path.exists(out) else {}
+    db[key] = rec
+    json.dump(db, open(out, "w"), indent=1, sort_keys=True)
+    print(key, json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
