@@ -6,9 +6,10 @@ One step = one replay of a whole resident batch (inputs already in HBM) through 
 8 writer clients × 2000 ops per GPU (weak scaling: every rank replays its own 100k-doc shard).
 `--workload map` runs M2: SharedMap LWW, 1M documents × 8 clients × 1000 ops per GPU.
 
-Synthetic data: `--unique-docs` distinct documents are generated with the reference's PRNG and
-conflict-farm shape, then laid out `docs / unique` times as independent copies (own ops and text
-in HBM, nothing shared), so generation stays within seconds. See DESIGN.md.
+Synthetic data: every document is distinct by default (generated with the reference's XSadd PRNG and
+conflict-farm shape on the host's cores, ≈20 s for T1 on 16 threads). `--unique-docs U` generates U
+distinct documents and lays them out `docs / U` times as independent copies (own ops and text in
+HBM, nothing shared) for quick experiments. See DESIGN.md.
 
 Launch: `python bench.py` (N=1) or `python -m torch.distributed.run --nproc-per-node N ... bench.py
 --gpus N`. Prints ONE JSON line on rank 0.
@@ -40,7 +41,7 @@ def main():
     ap.add_argument("--docs", type=int, default=None, help="documents per GPU")
     ap.add_argument("--ops-per-doc", type=int, default=None)
     ap.add_argument("--clients", type=int, default=8)
-    ap.add_argument("--unique-docs", type=int, default=5000)
+    ap.add_argument("--unique-docs", type=int, default=0, help="0 = all documents distinct")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
@@ -70,7 +71,7 @@ def main():
 
     t = time.time()
     if mt:
-        uniq = min(args.unique_docs, docs)
+        uniq = min(args.unique_docs or docs, docs)
         if docs % uniq:
             raise SystemExit("--docs must be a multiple of --unique-docs")
         batch = workloads.conflict_farm(uniq, n_clients=args.clients, ops_per_doc=opd, seed=seed, replicas=docs // uniq)
@@ -194,7 +195,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": f"synthetic ({'conflict-farm' if mt else 'map fuzz'} shape, reference XSadd PRNG; "
-                    f"{min(args.unique_docs, docs) if mt else docs} distinct docs per GPU replicated to {docs})",
+                    + (f"{docs} distinct docs per GPU)" if not mt or uniq == docs
+                       else f"{uniq} distinct docs per GPU replicated to {docs})"),
             "config": {
                 "workload": ("T1 merge-tree conflict-farm replay" if mt else "M2 SharedMap LWW replay"),
                 "docs_per_gpu": docs,

@@ -1,0 +1,484 @@
+"use strict";
+/**
+ * fmt.js — JavaScript batch replay driver over the N-API addon (../fmt_napi.node → libfmt.so).
+ *
+ * This is the host side a Fluid runtime calls. It mirrors the reference's DDS message surface:
+ *   SharedObjectCore.processMessagesCore(messagesCollection)   shared-object-base/src/sharedObject.ts:415
+ *   IRuntimeMessageCollection {envelope, local, messagesContent}  runtime-definitions/src/protocol.ts:80-142
+ *   SharedSegmentSequence.processMessage rebuilds each message as {...envelope, contents,
+ *     clientSequenceNumber}                                     sequence/src/sequence.ts:873-919
+ *   SharedMap.processMessagesCore → MapKernel.tryProcessMessage  map/src/map.ts:288-311, mapKernel.ts:619
+ * Instead of applying every message on the JS thread, messages of many documents are packed into
+ * the flat records of include/fmt.h (exactly as fluidframework_amd/streams.py packs them; the CPU
+ * test suite checks the two packers byte for byte) and replayed on the GPU in one async call.
+ *
+ * Written for the Node in this image (v12): CommonJS, no `??` / `?.`.
+ */
+const path = require("path");
+
+const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3; // merge-tree/src/ops.ts:61-71
+const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
+const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
+const FMT_MT_F_GROUP_CONT = 1;
+const MAX_CLIENTS = 63;
+const NOT_REMOVED = 0x7fffffff;
+const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 20;
+const PROPS_MAX = 4;
+
+let addon = null;
+/** The native addon; throws if it was not built (there is no JavaScript fallback engine). */
+function native() {
+	if (addon === null) {
+		addon = require(path.join(__dirname, "..", "fmt_napi.node"));
+	}
+	return addon;
+}
+
+class UnsupportedOp extends Error {
+	constructor(msg) {
+		super(msg);
+		this.code = "FMT_E_UNSUPPORTED";
+	}
+}
+
+/** Interns strings to dense ids, first come first served. */
+class Dictionary {
+	constructor(reserved) {
+		this.items = reserved ? reserved.slice() : [];
+		this.ids = new Map();
+		this.items.forEach((s, i) => this.ids.set(s, i));
+	}
+	intern(s) {
+		let i = this.ids.get(s);
+		if (i === undefined) {
+			i = this.items.length;
+			this.items.push(s);
+			this.ids.set(s, i);
+		}
+		return i;
+	}
+}
+
+/** Growable byte buffer of fixed-size records. */
+class RecordBuffer {
+	constructor(recordBytes) {
+		this.rb = recordBytes;
+		this.buf = new ArrayBuffer(recordBytes * 1024);
+		this.view = new DataView(this.buf);
+		this.n = 0;
+	}
+	next() {
+		if ((this.n + 1) * this.rb > this.buf.byteLength) {
+			const nb = new ArrayBuffer(this.buf.byteLength * 2);
+			new Uint8Array(nb).set(new Uint8Array(this.buf));
+			this.buf = nb;
+			this.view = new DataView(nb);
+		}
+		return this.n++ * this.rb;
+	}
+	bytes() {
+		return new Uint8Array(this.buf, 0, this.n * this.rb).slice();
+	}
+}
+
+class U16Arena {
+	constructor() {
+		this.a = new Uint16Array(4096);
+		this.n = 0;
+	}
+	push(s) {
+		const off = this.n;
+		if (this.n + s.length > this.a.length) {
+			let cap = this.a.length * 2;
+			while (cap < this.n + s.length) cap *= 2;
+			const na = new Uint16Array(cap);
+			na.set(this.a.subarray(0, this.n));
+			this.a = na;
+		}
+		for (let i = 0; i < s.length; i++) this.a[this.n + i] = s.charCodeAt(i); // UTF-16 code units
+		this.n += s.length;
+		return [off, s.length];
+	}
+	finish() {
+		return this.a.slice(0, this.n);
+	}
+}
+
+/** Per-document packing state: short client ids (client.ts:831-855, observer = 0). */
+class MergeTreeDocBuilder {
+	constructor(owner, index, observer) {
+		this.owner = owner;
+		this.index = index;
+		this.clientIds = new Map([[observer, 0]]);
+		this.clientNames = [observer];
+		this.nOps = 0;
+	}
+	shortClient(longId) {
+		const id = longId === null || longId === undefined ? "server" : longId;
+		let i = this.clientIds.get(id);
+		if (i === undefined) {
+			i = this.clientNames.length;
+			if (i > MAX_CLIENTS) throw new UnsupportedOp(`more than ${MAX_CLIENTS} clients in one document`);
+			this.clientIds.set(id, i);
+			this.clientNames.push(id);
+		}
+		return i;
+	}
+	/** One ISequencedDocumentMessage with merge-tree contents (client.applyMsg, client.ts:1358). */
+	addMessage(msg) {
+		if (this.owner.current !== this) {
+			throw new UnsupportedOp("documents must be packed contiguously (finish one before the next)");
+		}
+		const client = this.shortClient(msg.clientId);
+		const contents = msg.contents;
+		let members = contents.type === MT_GROUP ? contents.ops : [contents];
+		if (members.length === 0) members = [null]; // empty group: only advances the window
+		members.forEach((op, k) => {
+			this.owner.packOp(op, msg.sequenceNumber, msg.referenceSequenceNumber,
+				msg.minimumSequenceNumber, client, k > 0 ? FMT_MT_F_GROUP_CONT : 0);
+			this.nOps++;
+		});
+	}
+	/** SharedObjectCore.processMessagesCore shape: a bunch sharing one envelope (sequence.ts:873-919). */
+	processMessagesCore(messagesCollection) {
+		const { envelope, messagesContent } = messagesCollection;
+		if (messagesCollection.local) {
+			throw new UnsupportedOp("local (pending) ops are outside the batch replay path");
+		}
+		for (const mc of messagesContent) {
+			this.addMessage(Object.assign({}, envelope, {
+				contents: mc.contents,
+				clientSequenceNumber: mc.clientSequenceNumber,
+			}));
+		}
+	}
+}
+
+/** JS object key order (OrdinaryOwnPropertyKeys): Object.keys already yields it. */
+function jsKeyOrder(obj) {
+	return Object.keys(obj);
+}
+
+/** Packs many documents' sequenced merge-tree messages (mirror of streams.py MergeTreeStreamBuilder). */
+class MergeTreeStreamBuilder {
+	constructor() {
+		this.keys = new Dictionary();
+		this.values = new Dictionary(["null"]);
+		this.text = new U16Arena();
+		this.ops = new RecordBuffer(MT_OP_BYTES);
+		this.propsOps = new Map();
+		this.propsList = [];
+		this.docs = [];
+		this.docInit = [];
+		this.current = null;
+	}
+	beginDoc(initialText, observer) {
+		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "A" : observer);
+		this.docs.push(d);
+		this.docInit.push(initialText ? this.text.push(initialText) : [0, 0]);
+		this.current = d;
+		return d;
+	}
+	propsOp(props) {
+		const kv = [];
+		for (const k of jsKeyOrder(props)) {
+			const v = props[k];
+			const keyId = this.keys.intern(k);
+			const valId = v === null ? 0 : this.values.intern(JSON.stringify(v));
+			if (keyId > 0xffff || valId > 0xffff) throw new UnsupportedOp("props dictionary exceeds 65535 entries");
+			kv.push(((keyId << 16) | valId) >>> 0);
+		}
+		const t = kv.join(",");
+		let i = this.propsOps.get(t);
+		if (i === undefined) {
+			i = this.propsList.length;
+			this.propsOps.set(t, i);
+			this.propsList.push(kv);
+		}
+		return i;
+	}
+	packOp(op, seq, ref, msn, client, flags) {
+		const o = this.ops.next();
+		const v = this.ops.view;
+		let pos1 = 0, pos2 = 0, payload = 0, len = 0, type = MT_REMOVE;
+		if (op !== null) {
+			if (op.relativePos1 !== undefined || op.relativePos2 !== undefined) {
+				throw new UnsupportedOp("relative positions");
+			}
+			type = op.type;
+			if (type === MT_INSERT) {
+				let seg = op.seg;
+				if (typeof seg !== "string") {
+					if (seg && typeof seg === "object" && "text" in seg && !(seg.props && Object.keys(seg.props).length)) {
+						seg = seg.text;
+					} else {
+						throw new UnsupportedOp("insert of markers or pre-annotated segments");
+					}
+				}
+				const r = this.text.push(seg);
+				if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
+				pos1 = op.pos1; pos2 = -1; payload = r[0]; len = r[1];
+			} else if (type === MT_REMOVE) {
+				pos1 = op.pos1; pos2 = op.pos2;
+			} else if (type === MT_ANNOTATE) {
+				if (op.adjust !== undefined && op.adjust !== null) throw new UnsupportedOp("annotate adjust");
+				pos1 = op.pos1; pos2 = op.pos2; payload = this.propsOp(op.props || {});
+			} else {
+				throw new UnsupportedOp(`merge-tree op type ${type}`);
+			}
+		}
+		v.setInt32(o + 0, seq, true);
+		v.setInt32(o + 4, ref, true);
+		v.setInt32(o + 8, msn, true);
+		v.setInt32(o + 12, pos1, true);
+		v.setInt32(o + 16, pos2, true);
+		v.setUint32(o + 20, payload, true);
+		v.setUint16(o + 24, len, true);
+		v.setUint8(o + 26, client);
+		v.setUint8(o + 27, type);
+		v.setUint32(o + 28, flags, true);
+	}
+	/** The packed batch: the typed arrays the addon hands to fmt_mt_load. */
+	finish() {
+		const offs = new BigUint64Array(this.docs.length + 1);
+		let i = 0;
+		this.docs.forEach((d, k) => {
+			i += d.nOps;
+			offs[k + 1] = BigInt(i);
+		});
+		const propsOff = new Uint32Array(this.propsList.length + 1);
+		const kv = [];
+		this.propsList.forEach((t, j) => {
+			kv.push(...t);
+			propsOff[j + 1] = kv.length;
+		});
+		const docInit = new Uint32Array(this.docs.length * 2);
+		this.docInit.forEach((p, k) => {
+			docInit[2 * k] = p[0];
+			docInit[2 * k + 1] = p[1];
+		});
+		return {
+			ops: this.ops.bytes(),
+			docOpOffsets: offs,
+			text: this.text.finish(),
+			docInit,
+			propsOff,
+			propsKv: Uint32Array.from(kv),
+			keys: this.keys.items.slice(),
+			values: this.values.items.slice(),
+			clients: this.docs.map((d) => d.clientNames.slice()),
+			nDocs: this.docs.length,
+		};
+	}
+}
+
+/** Packs SharedMap messages (mirror of streams.py MapStreamBuilder; mapKernel.ts:706-853 kinds). */
+class MapStreamBuilder {
+	constructor() {
+		this.keys = new Dictionary();
+		this.values = new Dictionary();
+		this.ops = new RecordBuffer(MAP_OP_BYTES);
+		this.docOps = [];
+	}
+	beginDoc() {
+		this.docOps.push(0);
+		this.lastSeq = 0;
+		return this.docOps.length - 1;
+	}
+	/**
+	 * One sequenced map message. Messages of one bunch share their envelope's sequenceNumber
+	 * (sharedObject.ts:620-630), so the record carries the message's 1-based ordinal in the document
+	 * instead: strictly increasing, it keeps a bunch's order for LWW and JS Map insertion order.
+	 */
+	addMessage(doc, seq, contents) {
+		if (doc !== this.docOps.length - 1) throw new UnsupportedOp("documents must be packed contiguously");
+		if (seq < this.lastSeq) throw new Error(`map message seq ${seq} after ${this.lastSeq}: messages must arrive in seq order`);
+		this.lastSeq = seq;
+		const ordinal = this.docOps[doc] + 1;
+		const o = this.ops.next();
+		const v = this.ops.view;
+		let key = 0, kv;
+		if (contents.type === "clear") {
+			kv = (MAP_CLEAR << MAP_KIND_SHIFT) >>> 0;
+		} else if (contents.type === "delete") {
+			key = this.keys.intern(contents.key);
+			kv = (MAP_DELETE << MAP_KIND_SHIFT) >>> 0;
+		} else if (contents.type === "set") {
+			key = this.keys.intern(contents.key);
+			const sv = contents.value;
+			if (sv.type !== "Plain") throw new UnsupportedOp("legacy Shared value type");
+			let vid = MAP_VALUE_UNDEFINED;
+			if ("value" in sv && sv.value !== undefined) {
+				vid = this.values.intern(JSON.stringify(sv.value));
+				if (vid >= MAP_VALUE_UNDEFINED) throw new UnsupportedOp("value dictionary overflow");
+			}
+			kv = ((MAP_SET << MAP_KIND_SHIFT) | vid) >>> 0;
+		} else {
+			throw new UnsupportedOp(`map op type ${contents.type}`);
+		}
+		v.setUint32(o, doc, true);
+		v.setUint32(o + 4, key, true);
+		v.setUint32(o + 8, ordinal, true);
+		v.setUint32(o + 12, kv, true);
+		this.docOps[doc]++;
+	}
+	/** SharedMap.processMessagesCore shape (map.ts:288-311): one bunch for document `doc`. */
+	processMessagesCore(doc, messagesCollection) {
+		for (const mc of messagesCollection.messagesContent) {
+			this.addMessage(doc, messagesCollection.envelope.sequenceNumber, mc.contents);
+		}
+	}
+	finish() {
+		const offs = new BigUint64Array(this.docOps.length + 1);
+		let i = 0;
+		this.docOps.forEach((n, k) => {
+			i += n;
+			offs[k + 1] = BigInt(i);
+		});
+		return {
+			ops: this.ops.bytes(),
+			docOpOffsets: offs,
+			keyBound: Math.max(1, this.keys.items.length),
+			keys: this.keys.items.slice(),
+			values: this.values.items.slice(),
+			nDocs: this.docOps.length,
+		};
+	}
+}
+
+function readHeader(dv, d) {
+	const o = d * DOC_RESULT_BYTES;
+	return {
+		status: dv.getInt32(o, true),
+		failSeq: dv.getInt32(o + 4, true),
+		curSeq: dv.getInt32(o + 8, true),
+		minSeq: dv.getInt32(o + 12, true),
+		nLeaves: dv.getUint32(o + 16, true),
+		nChars: dv.getUint32(o + 20, true),
+		nProps: dv.getUint32(o + 24, true),
+		nBlocks: dv.getUint32(o + 28, true),
+		depth: dv.getUint32(o + 32, true),
+		visibleLength: dv.getUint32(o + 36, true),
+	};
+}
+
+/** Converged state of a replayed merge-tree batch (read side of SharedString). */
+class MergeTreeReplay {
+	constructor(engine, batch, headers) {
+		this.engine = engine;
+		this.batch = batch;
+		this.headerView = new DataView(headers);
+	}
+	header(doc) {
+		return readHeader(this.headerView, doc);
+	}
+	/** Leaves (segments, tombstones included), UTF-16 chars and prop sets of one document. */
+	segments(doc) {
+		const h = this.header(doc);
+		if (h.status !== 0) {
+			const e = new Error(`document ${doc} failed at seq ${h.failSeq} (status ${h.status})`);
+			e.code = h.status === -2 ? "FMT_E_DATA" : h.status === -3 ? "FMT_E_CAPACITY" : "FMT_E_UNSUPPORTED";
+			throw e;
+		}
+		const r = native().fetchDoc(this.engine.ctx, doc, h.nLeaves, h.nChars, h.nProps);
+		const lv = new DataView(r.leaves), pv = new DataView(r.props);
+		const chars = new Uint16Array(r.chars);
+		const props = [];
+		for (let p = 0; p < h.nProps; p++) {
+			const n = pv.getUint32(p * PROPSET_BYTES, true);
+			const obj = {};
+			for (let k = 0; k < n && k < PROPS_MAX; k++) {
+				const kv = pv.getUint32(p * PROPSET_BYTES + 4 + 4 * k, true);
+				const val = kv & 0xffff;
+				if (val !== 0) obj[this.batch.keys[kv >>> 16]] = JSON.parse(this.batch.values[val]);
+			}
+			props.push(obj);
+		}
+		const segs = [];
+		for (let i = 0; i < h.nLeaves; i++) {
+			const o = i * LEAF_BYTES;
+			const off = lv.getUint32(o + 16, true), len = lv.getUint16(o + 20, true);
+			const pid = lv.getUint16(o + 24, true);
+			segs.push({
+				insertSeq: lv.getInt32(o, true),
+				removedSeq: lv.getInt32(o + 4, true) === NOT_REMOVED ? undefined : lv.getInt32(o + 4, true),
+				insertClient: lv.getInt16(o + 22, true),
+				text: String.fromCharCode.apply(null, chars.subarray(off, off + len)),
+				properties: pid === 0xffff ? undefined : props[pid],
+			});
+		}
+		return segs;
+	}
+	/** MergeTreeTextHelper.getText from the local perspective (MergeTreeTextHelper.ts:28-87). */
+	getText(doc) {
+		return this.segments(doc).filter((s) => s.removedSeq === undefined).map((s) => s.text).join("");
+	}
+	getLength(doc) {
+		return this.header(doc).visibleLength;
+	}
+}
+
+/** Converged SharedMap state (MapKernel.sequencedData, mapKernel.ts:131). */
+class MapReplay {
+	constructor(batch, slots) {
+		this.batch = batch;
+		this.view = new DataView(slots);
+	}
+	/** Live entries in JS Map iteration order (insertion = birth seq of the live entry). */
+	entries(doc) {
+		const kb = this.batch.keyBound;
+		const live = [];
+		for (let k = 0; k < kb; k++) {
+			const o = (doc * kb + k) * 8;
+			const value = this.view.getUint32(o, true);
+			if (value === MAP_ABSENT) continue;
+			live.push([this.view.getUint32(o + 4, true), k, value]);
+		}
+		live.sort((a, b) => a[0] - b[0] || a[1] - b[1]);
+		return live.map(([, k, v]) => [this.batch.keys[k],
+			v === MAP_VALUE_UNDEFINED ? undefined : JSON.parse(this.batch.values[v])]);
+	}
+	get(doc, key) {
+		const k = this.batch.keys.indexOf(key);
+		if (k < 0) return undefined;
+		const value = this.view.getUint32((doc * this.batch.keyBound + k) * 8, true);
+		if (value === MAP_ABSENT || value === MAP_VALUE_UNDEFINED) return undefined;
+		return JSON.parse(this.batch.values[value]);
+	}
+}
+
+/** One engine context on one GPU (fmt_open). */
+class Engine {
+	constructor(device) {
+		this.ctx = native().open(device === undefined ? 0 : device);
+	}
+	deviceInfo() {
+		return native().deviceInfo(this.ctx);
+	}
+	stats() {
+		return native().stats(this.ctx);
+	}
+	async replayMergeTree(batch) {
+		const headers = await native().replayMergeTree(this.ctx, batch);
+		return new MergeTreeReplay(this, batch, headers);
+	}
+	async replayMap(batch) {
+		const slots = await native().replayMap(this.ctx, batch);
+		return new MapReplay(batch, slots);
+	}
+	close() {
+		native().close(this.ctx);
+	}
+}
+
+module.exports = {
+	native,
+	Engine,
+	MergeTreeStreamBuilder,
+	MapStreamBuilder,
+	MergeTreeReplay,
+	MapReplay,
+	UnsupportedOp,
+	constants: { MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MAP_SET, MAP_DELETE, MAP_CLEAR,
+		MAP_VALUE_UNDEFINED, MAP_ABSENT, FMT_MT_F_GROUP_CONT, NOT_REMOVED },
+};

@@ -1,0 +1,461 @@
+// fmt_napi.cc — N-API addon exposing libfmt.so (include/fmt.h) to Node.js.
+//
+// This is the thin native layer between the reference's JavaScript runtime and the HIP engine.
+// The reference applies one sequenced message per call, on the JS thread:
+//   SharedObjectCore.processMessagesCore   packages/dds/shared-object-base/src/sharedObject.ts:415
+//   SharedMap.processMessagesCore          packages/dds/map/src/map.ts:288-311
+//   SharedSegmentSequence.processMessagesCore  packages/dds/sequence/src/sequence.ts:873-919
+// Here one call replays a whole packed batch of many documents (fluidframework_amd/js/fmt.js packs
+// it), and the load + replay + header fetch run on a libuv worker thread through napi_async_work so
+// the JS event loop is never blocked. Errors reject the promise with an Error whose `code` is the
+// FMT_E_* name (FMT_E_DATA is the DataProcessingError analogue, mergeTree.ts:1629-1638).
+//
+// Exports:
+//   open(device) -> ctx                        fmt_open
+//   close(ctx)                                 fmt_close (also run by the ctx finalizer)
+//   deviceInfo(ctx) -> string                  fmt_device_info
+//   capacity() -> {leaves, chars, props}       fmt_mt_capacity
+//   replayMergeTree(ctx, batch) -> Promise<ArrayBuffer headers>     fmt_mt_load + fmt_mt_run + fetch
+//   fetchDoc(ctx, doc, nLeaves, nChars, nProps) -> {leaves, chars, props}   fmt_mt_fetch_doc
+//   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
+//   stats(ctx) -> {kernelMs, totalMs, ops, docs, bytesRead, bytesWritten, launches}
+//   sizes: {mtOp, mapOp, leaf, docResult, propset, mapSlot}          struct sizes for the JS views
+#include <node_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fmt.h"
+
+namespace {
+
+#define CHECK_NAPI(env, call)                                                      \
+  do {                                                                             \
+    if ((call) != napi_ok) {                                                       \
+      napi_throw_error((env), "FMT_E_USAGE", "N-API call failed: " #call);         \
+      return nullptr;                                                              \
+    }                                                                              \
+  } while (0)
+
+const char* status_name(int rc) {
+  switch (rc) {
+    case FMT_OK: return "FMT_OK";
+    case FMT_E_USAGE: return "FMT_E_USAGE";
+    case FMT_E_DATA: return "FMT_E_DATA";
+    case FMT_E_CAPACITY: return "FMT_E_CAPACITY";
+    case FMT_E_DEVICE: return "FMT_E_DEVICE";
+    case FMT_E_UNSUPPORTED: return "FMT_E_UNSUPPORTED";
+    default: return "FMT_E_UNKNOWN";
+  }
+}
+
+struct Ctx {
+  fmt_ctx* ctx = nullptr;
+  bool busy = false;  // one async replay at a time per ctx (the C ABI is one-thread-per-ctx)
+};
+
+void finalize_ctx(napi_env, void* data, void*) {
+  auto* c = static_cast<Ctx*>(data);
+  if (c->ctx) fmt_close(c->ctx);
+  delete c;
+}
+
+napi_value make_error(napi_env env, int rc, const std::string& msg) {
+  napi_value code, text, err;
+  napi_create_string_utf8(env, status_name(rc), NAPI_AUTO_LENGTH, &code);
+  napi_create_string_utf8(env, msg.c_str(), msg.size(), &text);
+  napi_create_error(env, code, text, &err);
+  napi_value status;
+  napi_create_int32(env, rc, &status);
+  napi_set_named_property(env, err, "status", status);
+  return err;
+}
+
+bool throw_fmt(napi_env env, int rc, const std::string& msg) {
+  napi_throw(env, make_error(env, rc, msg));
+  return false;
+}
+
+bool get_ctx(napi_env env, napi_value v, Ctx** out) {
+  void* p = nullptr;
+  if (napi_get_value_external(env, v, &p) != napi_ok || p == nullptr)
+    return throw_fmt(env, FMT_E_USAGE, "expected an engine context from open()");
+  *out = static_cast<Ctx*>(p);
+  if ((*out)->ctx == nullptr) return throw_fmt(env, FMT_E_USAGE, "engine context is closed");
+  return true;
+}
+
+// Bytes of an ArrayBuffer, TypedArray or DataView (nullptr/0 for undefined or null).
+bool get_bytes(napi_env env, napi_value v, const char* what, void** data, size_t* len) {
+  *data = nullptr;
+  *len = 0;
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t == napi_undefined || t == napi_null) return true;
+  bool is;
+  if (napi_is_typedarray(env, v, &is) == napi_ok && is) {
+    napi_typedarray_type tt;
+    size_t n, off;
+    napi_value ab;
+    napi_get_typedarray_info(env, v, &tt, &n, data, &ab, &off);
+    size_t elt = 1;
+    switch (tt) {
+      case napi_int16_array: case napi_uint16_array: elt = 2; break;
+      case napi_int32_array: case napi_uint32_array: case napi_float32_array: elt = 4; break;
+      case napi_float64_array: case napi_bigint64_array: case napi_biguint64_array: elt = 8; break;
+      default: elt = 1;
+    }
+    *len = n * elt;
+    return true;
+  }
+  if (napi_is_arraybuffer(env, v, &is) == napi_ok && is) {
+    napi_get_arraybuffer_info(env, v, data, len);
+    return true;
+  }
+  if (napi_is_dataview(env, v, &is) == napi_ok && is) {
+    napi_value ab;
+    size_t off;
+    napi_get_dataview_info(env, v, len, data, &ab, &off);
+    return true;
+  }
+  return throw_fmt(env, FMT_E_USAGE, std::string(what) + ": expected an ArrayBuffer or TypedArray");
+}
+
+napi_value prop(napi_env env, napi_value obj, const char* name) {
+  napi_value v = nullptr;
+  napi_get_named_property(env, obj, name, &v);
+  return v;
+}
+
+bool get_u32(napi_env env, napi_value v, const char* what, uint32_t* out) {
+  if (napi_get_value_uint32(env, v, out) != napi_ok)
+    return throw_fmt(env, FMT_E_USAGE, std::string(what) + ": expected a number");
+  return true;
+}
+
+// ------------------------------------------------------------------------------------- open/close
+napi_value Open(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int32_t device = 0;
+  if (argc >= 1) napi_get_value_int32(env, argv[0], &device);
+  fmt_config cfg;
+  std::memset(&cfg, 0, sizeof cfg);
+  cfg.device = device;
+  fmt_ctx* ctx = nullptr;
+  int rc = fmt_open(&cfg, &ctx);
+  if (rc != FMT_OK) {
+    std::string msg = ctx ? fmt_last_error(ctx) : "fmt_open failed";
+    if (ctx) fmt_close(ctx);
+    throw_fmt(env, rc, msg);
+    return nullptr;
+  }
+  auto* c = new Ctx;
+  c->ctx = ctx;
+  napi_value ext;
+  CHECK_NAPI(env, napi_create_external(env, c, finalize_ctx, nullptr, &ext));
+  return ext;
+}
+
+napi_value Close(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* p = nullptr;
+  if (argc < 1 || napi_get_value_external(env, argv[0], &p) != napi_ok || !p) {
+    throw_fmt(env, FMT_E_USAGE, "close: expected an engine context");
+    return nullptr;
+  }
+  auto* c = static_cast<Ctx*>(p);
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "close: a replay is still running on this context");
+    return nullptr;
+  }
+  if (c->ctx) fmt_close(c->ctx);
+  c->ctx = nullptr;
+  return nullptr;
+}
+
+napi_value DeviceInfo(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 1 || !get_ctx(env, argv[0], &c)) return nullptr;
+  char buf[256];
+  int rc = fmt_device_info(c->ctx, buf, sizeof buf);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  napi_value s;
+  CHECK_NAPI(env, napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &s));
+  return s;
+}
+
+napi_value Capacity(napi_env env, napi_callback_info) {
+  uint32_t l = 0, ch = 0, p = 0;
+  fmt_mt_capacity(&l, &ch, &p);
+  napi_value o, v;
+  napi_create_object(env, &o);
+  napi_create_uint32(env, l, &v);
+  napi_set_named_property(env, o, "leaves", v);
+  napi_create_uint32(env, ch, &v);
+  napi_set_named_property(env, o, "chars", v);
+  napi_create_uint32(env, p, &v);
+  napi_set_named_property(env, o, "props", v);
+  return o;
+}
+
+napi_value Stats(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 1 || !get_ctx(env, argv[0], &c)) return nullptr;
+  fmt_stats s;
+  int rc = fmt_get_stats(c->ctx, &s);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  napi_value o, v;
+  napi_create_object(env, &o);
+  auto num = [&](const char* k, double x) {
+    napi_create_double(env, x, &v);
+    napi_set_named_property(env, o, k, v);
+  };
+  num("kernelMs", s.kernel_ms);
+  num("totalMs", s.total_ms);
+  num("ops", double(s.ops));
+  num("docs", double(s.docs));
+  num("bytesRead", double(s.bytes_read));
+  num("bytesWritten", double(s.bytes_written));
+  num("launches", double(s.launches));
+  return o;
+}
+
+// ------------------------------------------------------------------------------- async replays
+struct Job {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  Ctx* c = nullptr;
+  napi_ref ctx_ref = nullptr;
+  std::vector<napi_ref> keep;  // input arrays stay alive (and unmoved) until Complete
+  bool is_map = false;
+  fmt_mt_batch mt;
+  const fmt_map_op* map_ops = nullptr;
+  uint64_t map_n_ops = 0;
+  const uint64_t* map_offs = nullptr;
+  uint32_t n_docs = 0, key_bound = 0;
+  std::vector<uint8_t> out;  // headers or map slots
+  int rc = FMT_OK;
+  std::string err;
+};
+
+void Execute(napi_env, void* p) {  // libuv worker thread: no N-API calls here
+  auto* j = static_cast<Job*>(p);
+  fmt_ctx* ctx = j->c->ctx;
+  if (j->is_map) {
+    j->rc = fmt_map_load(ctx, j->map_ops, j->map_n_ops, j->map_offs, j->n_docs, j->key_bound);
+    if (j->rc == FMT_OK) j->rc = fmt_map_run(ctx);
+    if (j->rc == FMT_OK) {
+      j->out.resize(size_t(j->n_docs) * j->key_bound * sizeof(fmt_map_slot));
+      j->rc = fmt_map_fetch(ctx, reinterpret_cast<fmt_map_slot*>(j->out.data()));
+    }
+  } else {
+    j->rc = fmt_mt_load(ctx, &j->mt);
+    if (j->rc == FMT_OK) j->rc = fmt_mt_run(ctx);
+    if (j->rc == FMT_OK) {
+      j->out.resize(size_t(j->n_docs) * sizeof(fmt_mt_doc_result));
+      j->rc = fmt_mt_fetch_headers(ctx, reinterpret_cast<fmt_mt_doc_result*>(j->out.data()));
+    }
+  }
+  if (j->rc != FMT_OK) j->err = fmt_last_error(ctx);
+}
+
+void Complete(napi_env env, napi_status, void* p) {  // JS thread
+  auto* j = static_cast<Job*>(p);
+  j->c->busy = false;
+  if (j->rc != FMT_OK) {
+    napi_reject_deferred(env, j->deferred, make_error(env, j->rc, j->err));
+  } else {
+    void* data = nullptr;
+    napi_value ab;
+    napi_create_arraybuffer(env, j->out.size(), &data, &ab);
+    if (!j->out.empty()) std::memcpy(data, j->out.data(), j->out.size());
+    napi_resolve_deferred(env, j->deferred, ab);
+  }
+  for (napi_ref r : j->keep) napi_delete_reference(env, r);
+  napi_delete_reference(env, j->ctx_ref);
+  napi_delete_async_work(env, j->work);
+  delete j;
+}
+
+bool keep_array(napi_env env, Job* j, napi_value v) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t != napi_object) return true;
+  napi_ref r;
+  if (napi_create_reference(env, v, 1, &r) != napi_ok) return false;
+  j->keep.push_back(r);
+  return true;
+}
+
+napi_value queue(napi_env env, Job* j, napi_value ctx_val, const char* name) {
+  napi_value promise, res_name;
+  napi_create_reference(env, ctx_val, 1, &j->ctx_ref);
+  napi_create_promise(env, &j->deferred, &promise);
+  napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name);
+  napi_create_async_work(env, nullptr, res_name, Execute, Complete, j, &j->work);
+  j->c->busy = true;
+  napi_queue_async_work(env, j->work);
+  return promise;
+}
+
+// replayMergeTree(ctx, {ops, docOpOffsets, text, docInit, propsOff, propsKv})
+napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 2 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "replayMergeTree: a replay is already running on this context");
+    return nullptr;
+  }
+  napi_value b = argv[1];
+  const char* names[] = {"ops", "docOpOffsets", "text", "docInit", "propsOff", "propsKv"};
+  void* d[6];
+  size_t n[6];
+  for (int i = 0; i < 6; ++i)
+    if (!get_bytes(env, prop(env, b, names[i]), names[i], &d[i], &n[i])) return nullptr;
+  if (n[0] % sizeof(fmt_mt_op) || n[1] < 8 || n[1] % 8 || n[4] < 4 || n[4] % 4 || n[5] % 4 || n[2] % 2) {
+    throw_fmt(env, FMT_E_USAGE, "replayMergeTree: buffer sizes do not match the fmt_mt_* record layouts");
+    return nullptr;
+  }
+  uint32_t n_docs = uint32_t(n[1] / 8 - 1);
+  if (d[3] && n[3] != size_t(n_docs) * 8) {
+    throw_fmt(env, FMT_E_USAGE, "replayMergeTree: docInit must hold (offset, len) per document");
+    return nullptr;
+  }
+  auto* j = new Job;
+  j->c = c;
+  j->n_docs = n_docs;
+  std::memset(&j->mt, 0, sizeof j->mt);
+  j->mt.ops = static_cast<const fmt_mt_op*>(d[0]);
+  j->mt.n_ops = n[0] / sizeof(fmt_mt_op);
+  j->mt.doc_op_offsets = static_cast<const uint64_t*>(d[1]);
+  j->mt.n_docs = n_docs;
+  j->mt.text = static_cast<const uint16_t*>(d[2]);
+  j->mt.text_len = n[2] / 2;
+  j->mt.doc_init = static_cast<const uint32_t*>(d[3]);
+  j->mt.props_off = static_cast<const uint32_t*>(d[4]);
+  j->mt.n_props_ops = uint32_t(n[4] / 4 - 1);
+  j->mt.props_kv = static_cast<const uint32_t*>(d[5]);
+  for (int i = 0; i < 6; ++i) keep_array(env, j, prop(env, b, names[i]));
+  return queue(env, j, argv[0], "fmtReplayMergeTree");
+}
+
+// replayMap(ctx, {ops, docOpOffsets, keyBound})
+napi_value ReplayMap(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 2 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "replayMap: a replay is already running on this context");
+    return nullptr;
+  }
+  napi_value b = argv[1];
+  void *ops, *offs;
+  size_t n_ops_b, n_offs_b;
+  uint32_t key_bound;
+  if (!get_bytes(env, prop(env, b, "ops"), "ops", &ops, &n_ops_b)) return nullptr;
+  if (!get_bytes(env, prop(env, b, "docOpOffsets"), "docOpOffsets", &offs, &n_offs_b)) return nullptr;
+  if (!get_u32(env, prop(env, b, "keyBound"), "keyBound", &key_bound)) return nullptr;
+  if (n_ops_b % sizeof(fmt_map_op) || n_offs_b < 8 || n_offs_b % 8 || key_bound == 0) {
+    throw_fmt(env, FMT_E_USAGE, "replayMap: buffer sizes do not match the fmt_map_* record layouts");
+    return nullptr;
+  }
+  auto* j = new Job;
+  j->c = c;
+  j->is_map = true;
+  j->map_ops = static_cast<const fmt_map_op*>(ops);
+  j->map_n_ops = n_ops_b / sizeof(fmt_map_op);
+  j->map_offs = static_cast<const uint64_t*>(offs);
+  j->n_docs = uint32_t(n_offs_b / 8 - 1);
+  j->key_bound = key_bound;
+  keep_array(env, j, prop(env, b, "ops"));
+  keep_array(env, j, prop(env, b, "docOpOffsets"));
+  return queue(env, j, argv[0], "fmtReplayMap");
+}
+
+// fetchDoc(ctx, doc, nLeaves, nChars, nProps) -> {leaves: ArrayBuffer, chars: ArrayBuffer, props: ArrayBuffer}
+napi_value FetchDoc(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 5 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchDoc: a replay is running on this context");
+    return nullptr;
+  }
+  uint32_t doc, nl, nc, np;
+  if (!get_u32(env, argv[1], "doc", &doc) || !get_u32(env, argv[2], "nLeaves", &nl) ||
+      !get_u32(env, argv[3], "nChars", &nc) || !get_u32(env, argv[4], "nProps", &np))
+    return nullptr;
+  void *l, *ch, *pr;
+  napi_value lv, cv, pv, o;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(nl) * sizeof(fmt_mt_leaf), &l, &lv));
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(nc) * 2, &ch, &cv));
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(np) * sizeof(fmt_mt_propset), &pr, &pv));
+  int rc = fmt_mt_fetch_doc(c->ctx, doc, static_cast<fmt_mt_leaf*>(l), nl, static_cast<uint16_t*>(ch), nc,
+                            static_cast<fmt_mt_propset*>(pr), np);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "leaves", lv);
+  napi_set_named_property(env, o, "chars", cv);
+  napi_set_named_property(env, o, "props", pv);
+  return o;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+  napi_property_descriptor fns[] = {
+      {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"deviceInfo", nullptr, DeviceInfo, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"capacity", nullptr, Capacity, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"stats", nullptr, Stats, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"replayMergeTree", nullptr, ReplayMergeTree, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"replayMap", nullptr, ReplayMap, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchDoc", nullptr, FetchDoc, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof fns / sizeof fns[0], fns);
+  napi_value sizes, v;
+  napi_create_object(env, &sizes);
+  auto sz = [&](const char* k, size_t x) {
+    napi_create_uint32(env, uint32_t(x), &v);
+    napi_set_named_property(env, sizes, k, v);
+  };
+  sz("mtOp", sizeof(fmt_mt_op));
+  sz("mapOp", sizeof(fmt_map_op));
+  sz("leaf", sizeof(fmt_mt_leaf));
+  sz("docResult", sizeof(fmt_mt_doc_result));
+  sz("propset", sizeof(fmt_mt_propset));
+  sz("mapSlot", sizeof(fmt_map_slot));
+  napi_set_named_property(env, exports, "sizes", sizes);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

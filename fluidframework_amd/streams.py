@@ -284,15 +284,26 @@ class MapStreamBuilder:
         self.keys = Dictionary()
         self.values = Dictionary()
         self.docs: list[list[tuple]] = []
+        self._last_seq: dict[int, int] = {}
 
     def begin_doc(self) -> int:
         self.docs.append([])
         return len(self.docs) - 1
 
     def add_message(self, doc: int, seq: int, contents: dict) -> None:
+        """One sequenced map message. Messages of one runtime bunch share their envelope's
+        sequenceNumber (sharedObject.ts:620-630, sequence.ts:882-888), so the record's `seq` field
+        carries the message's 1-based ordinal in the document's stream instead: strictly increasing,
+        it keeps a bunch's order for LWW and for JS Map insertion order (mapKernel.ts:708-850)."""
+        ops = self.docs[doc]
+        last = self._last_seq.get(doc, 0)
+        if seq < last:
+            raise ValueError(f"map message seq {seq} after {last}: messages must arrive in seq order")
+        self._last_seq[doc] = seq
+        seq = len(ops) + 1
         t = contents["type"]
         if t == "clear":
-            self.docs[doc].append((doc, 0, seq, MAP_CLEAR << MAP_KIND_SHIFT))
+            ops.append((doc, 0, seq, MAP_CLEAR << MAP_KIND_SHIFT))
             return
         key = self.keys.intern(contents["key"])
         if t == "delete":

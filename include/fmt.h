@@ -97,7 +97,10 @@ typedef struct fmt_mt_op {
 typedef struct fmt_map_op {
   uint32_t doc;
   uint32_t key;
-  uint32_t seq;
+  uint32_t seq;        /* order key, strictly increasing within the document: the host packers store
+                          the message's 1-based ordinal in the document's stream, because messages of
+                          one runtime bunch share their envelope's sequenceNumber
+                          (shared-object-base/src/sharedObject.ts:620-630) */
   uint32_t kind_value; /* (kind << 30) | value id */
 } fmt_map_op;
 
@@ -158,7 +161,8 @@ typedef struct fmt_mt_propset {
 /* One SharedMap result slot (per doc, per key id < key_bound). */
 typedef struct fmt_map_slot {
   uint32_t value;     /* value id, FMT_MAP_VALUE_UNDEFINED, or FMT_MAP_ABSENT (not live) */
-  uint32_t birth_seq; /* seq of the set that created the live entry (JS Map insertion order) */
+  uint32_t birth_seq; /* order key (fmt_map_op.seq) of the set that created the live entry: JS Map
+                         insertion order */
 } fmt_map_slot;
 
 /* Run statistics of the last fmt_*_run (device time measured with HIP events on the ctx stream). */

@@ -1,0 +1,121 @@
+"""The N-API addon (fluidframework_amd/fmt_napi.node) and the JavaScript batch driver (js/fmt.js).
+
+CPU: the addon loads in the image's Node and exports its functions; opening a context without a GPU
+rejects with FMT_E_DEVICE; the JavaScript packer produces byte-identical records to streams.py for
+the reference's replay fixtures (tests/golden/replay_msgs_0.40.json.gz, the messages
+client.replay.spec.ts:20-76 replays).
+GPU: every checkpoint of those fixtures replayed from JavaScript through the addon matches the
+fixture's resultText; a SharedMap bunch replay gives the LWW entries in JS Map order.
+"""
+import gzip
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "fluidframework_amd")
+ADDON = os.path.join(PKG, "fmt_napi.node")
+DRIVER = os.path.join(REPO, "tests", "js", "fixture_driver.js")
+GOLDEN = os.path.join(REPO, "tests", "golden", "replay_msgs_0.40.json.gz")
+
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
+
+
+@pytest.fixture(scope="module")
+def addon():
+    if not os.path.exists(ADDON):
+        subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
+        subprocess.run(["make", "-s", "-C", os.path.join(PKG, "napi")], check=True)
+    return ADDON
+
+
+def _node(*args, timeout=120):
+    return subprocess.run([NODE, *args], capture_output=True, text=True, timeout=timeout, cwd=REPO)
+
+
+def test_addon_exports(addon):
+    r = _node("-e", f"const a=require({json.dumps(addon)});"
+                    "console.log(JSON.stringify({k:Object.keys(a).sort(),s:a.sizes,c:a.capacity()}))")
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree",
+                               "replayMap", "fetchDoc", "sizes"])
+    assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 20, "mapSlot": 8}
+    assert out["c"]["leaves"] >= 512
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is present")
+def test_open_without_gpu_rejects(addon):
+    r = _node("-e", "const f=require('./fluidframework_amd/js/fmt.js');"
+                    "try{new f.Engine(0);console.log('opened')}catch(e){console.log(e.code)}")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "FMT_E_DEVICE"
+
+
+def _python_pack(stride):
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+
+    fixtures = json.load(gzip.open(GOLDEN, "rt", encoding="utf-8"))
+    b = MergeTreeStreamBuilder()
+    for fx in fixtures:
+        groups = fx["groups"]
+        for k in range(0, len(groups), stride):
+            d = b.begin_doc(initial_text=groups[0]["initialText"], observer="A")
+            for g in range(k + 1):
+                for m in groups[g]["msgs"]:
+                    d.add_message(m)
+    return b.finish()
+
+
+def test_js_packer_matches_python_packer(addon, tmp_path):
+    r = _node(DRIVER, "pack", str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    py = _python_pack(8)
+    rd = lambda n, dt: np.fromfile(tmp_path / n, dtype=dt)  # noqa: E731
+    assert rd("ops.bin", np.uint8).tobytes() == py.ops.tobytes()
+    assert np.array_equal(rd("offs.bin", np.uint64), py.doc_op_offsets)
+    assert np.array_equal(rd("text.bin", "<u2"), py.text)
+    assert np.array_equal(rd("doc_init.bin", np.uint32), py.doc_init.reshape(-1))
+    assert np.array_equal(rd("props_off.bin", np.uint32), py.props_off)
+    assert np.array_equal(rd("props_kv.bin", np.uint32), py.props_kv)
+    meta = json.load(open(tmp_path / "meta.json"))
+    assert meta["keys"] == py.keys and meta["values"] == py.values and meta["clients"] == py.clients
+
+
+def test_js_map_packer_orders_bunches(addon):
+    """Messages of one bunch share a sequenceNumber; the packer keeps their order via the ordinal."""
+    r = _node("-e", """
+const f=require('./fluidframework_amd/js/fmt.js');
+const b=new f.MapStreamBuilder(); const d=b.beginDoc();
+b.processMessagesCore(d,{envelope:{sequenceNumber:5},local:false,messagesContent:[
+ {contents:{type:'delete',key:'k'}},{contents:{type:'set',key:'k',value:{type:'Plain',value:1}}}]});
+const x=b.finish(); const v=new DataView(x.ops.buffer);
+console.log(JSON.stringify([v.getUint32(8,true),v.getUint32(24,true),x.keyBound,x.values]));""")
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout) == [1, 2, 1, ["1"]]
+
+
+@pytest.mark.gpu
+def test_js_replay_all_fixture_checkpoints_on_gpu(addon):
+    r = _node(DRIVER, "replay", timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["checked"] == 6 * 64
+    assert out["nMismatches"] == 0, out["mismatches"]
+    assert "gfx950" in out["device"]
+
+
+@pytest.mark.gpu
+def test_js_map_bunches_on_gpu(addon):
+    r = _node(DRIVER, "map", timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    # doc0: b,a set; delete b then set b (moves to the end); a updated in place (mapKernel.ts:708-850)
+    assert out["doc0"] == [["a", "y"], ["b", {"n": [1, 2]}]]
+    assert out["doc1"] == [["c", True]]
+    assert out["a0"] == "y"

@@ -9,6 +9,12 @@ Sources (data files held by the reference's own tests):
       replayed by client.replay.spec.ts:20-76 (64 groups of {initialText, resultText, msgs, seq})
   packages/dds/sequence/src/test/snapshots/legacy/{headerOnly,headerAndBody,largeBody,withAnnotations}.json
       checked by snapshotVersion.spec.ts:146-170 ("Snapshot diff")
+
+Outputs:
+  replay_conflict_farm_0.40.npz   all 30 0.40 fixtures, packed by streams.py, with every checkpoint text
+  replay_msgs_0.40.json.gz        the raw sequenced messages (ISequencedDocumentMessage JSON exactly as the
+                                  fixture holds them) of MSG_FILES, for the JavaScript driver's tests
+  snapshots_legacy.json           the legacy SharedString summary trees
 """
 import json
 import os
@@ -57,6 +63,27 @@ def convert_replay(path: str) -> dict:
     }
 
 
+MSG_FILES = [
+    "len_1-clients_2-default-conflict-farm-0.40.json",
+    "len_16-clients_4-default-conflict-farm-0.40.json",
+    "len_64-clients_8-default-conflict-farm-0.40.json",
+    "len_128-clients_8-default-conflict-farm-0.40.json",
+    "len_256-clients_4-default-conflict-farm-0.40.json",
+    "len_512-clients_8-default-conflict-farm-0.40.json",
+]
+
+
+def write_messages() -> None:
+    import gzip
+
+    out = []
+    for f in MSG_FILES:
+        groups = json.load(open(os.path.join(RESULTS, f)))
+        out.append({"name": f, "groups": groups})
+    with gzip.open(os.path.join(OUT, "replay_msgs_0.40.json.gz"), "wt", encoding="utf-8") as fh:
+        json.dump(out, fh, separators=(",", ":"), ensure_ascii=False)
+
+
 def main() -> None:
     os.makedirs(OUT, exist_ok=True)
     files = sorted(f for f in os.listdir(RESULTS) if f.endswith("-default-conflict-farm-0.40.json"))
@@ -67,6 +94,7 @@ def main() -> None:
             bundle[f"{i}/{k}"] = v
     bundle["names"] = np.frombuffer(json.dumps(files).encode(), dtype=np.uint8)
     np.savez_compressed(os.path.join(OUT, "replay_conflict_farm_0.40.npz"), **bundle)
+    write_messages()
     assert MT_OP_DTYPE.itemsize == 32
 
     snaps = {}
