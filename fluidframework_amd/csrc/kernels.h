@@ -22,6 +22,7 @@ struct MtDeviceBatch {
   const uint32_t* propsOff;
   const uint32_t* propsKv;
   uint32_t nPropsOps;
+  const uint64_t* catchupOffsets;  // per-doc catch-up slab offsets (nDocs + 1), or nullptr
 };
 
 struct MtDeviceOut {
@@ -29,6 +30,7 @@ struct MtDeviceOut {
   fmt_mt_leaf* leaves;         // nDocs * capLeaves
   uint16_t* chars;             // nDocs * capChars
   fmt_mt_propset* props;       // nDocs * capProps
+  fmt_mt_catchup_range* catchup;  // slabs at catchupOffsets, or nullptr
 };
 
 // Per-document capacities of the LDS-resident engine.

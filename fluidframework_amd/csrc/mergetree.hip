@@ -41,6 +41,14 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
     o.leaves = out.leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;
     o.chars = out.chars + static_cast<size_t>(d) * fmt_mt::kCapChars;
     o.props = out.props + static_cast<size_t>(d) * fmt_mt::kPropCap;
+    if (batch.catchupOffsets) {
+      const uint64_t c0 = batch.catchupOffsets[d], c1 = batch.catchupOffsets[d + 1];
+      o.catchup = out.catchup + c0;
+      o.catchupCap = static_cast<uint32_t>(c1 - c0);
+    } else {
+      o.catchup = nullptr;
+      o.catchupCap = 0;
+    }
     fmt_mt::Doc doc;
     doc.s = scratch;
     doc.run(in, o);

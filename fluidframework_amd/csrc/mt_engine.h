@@ -111,6 +111,8 @@ struct DocOutputs {
   fmt_mt_leaf* leaves;    // kCapLeaves entries
   uint16_t* chars;        // kCapChars entries
   fmt_mt_propset* props;  // kPropCap entries
+  fmt_mt_catchup_range* catchup;  // catchupCap entries (nullptr: no FMT_MT_F_CATCHUP ops)
+  uint32_t catchupCap;
 };
 
 // Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
@@ -145,7 +147,11 @@ class Doc {
   int status = FMT_OK;
   int failSeq = 0;
   uint32_t nextId = 1;
+  uint32_t opIdx = 0;   // index of the current op within the document
+  uint32_t cuN = 0;     // catch-up ranges recorded
   DocInputs in;
+  fmt_mt_catchup_range* cuOut = nullptr;
+  uint32_t cuCap = 0;
 
   // ------------------------------------------------------------------ leaf array primitives
   // Leaf j lives in row j >> 6 (element of the V8) of lane j & 63: document order runs along a
@@ -558,6 +564,67 @@ class Doc {
     return static_cast<uint32_t>(nProps++);
   }
 
+  // ------------------------------------------------------------------ catch-up ranges
+  // The ranges of the op's sequenceDelta event, merged as createOpsFromDelta merges them
+  // (sequence/src/sequence.ts:395-452) and recorded for the legacy summary's catch-up ops. `delta`
+  // is a per-lane row bitmask of the delta segments: the inserted leaf, the newly removed leaves, or
+  // the annotated leaves not removed. Each one's position is Client.getPosition in the local view
+  // right after the op (before its zamboni): the prefix of not-removed leaf lengths. A REMOVE range
+  // absorbs a segment starting where it starts (removed text has no local length); an ANNOTATE
+  // range one starting where it ends (the props always match: every delta segment now holds the
+  // op's own raw values for exactly the op's keys).
+  FMT_DEV void recordCatchup(const Lane<uint32_t>& delta, int type) {
+    const int nr = rows();
+    uint32_t base = 0;  // local length of the rows before r (row by row: no per-leaf prefix array)
+    int p1 = 0, p2 = 0;
+    bool open = false;
+    FOR_ROWS(r, 0, nr) {
+      Lane<uint32_t> loc;
+      Lane<bool> p;
+      FOR_LANES(l) {
+        LANE(loc) = static_cast<int32_t>(LANE(W[2])[r]) == kNotRemoved ? fLen(LANE(W[0])[r]) : 0u;
+        LANE(p) = ((LANE(delta) >> r) & 1u) != 0;
+      }
+      uint32_t tot;
+      const Lane<uint32_t> ex = waveExclusiveSum(loc, &tot);
+      uint64_t m = ballot(p);
+      while (m) {
+        const int lane = ctz64(m);
+        m &= m - 1;
+        const int pos = static_cast<int>(readlane(ex, lane) + base);
+        const int len = static_cast<int>(fLen(readlane(row(W[0], r), lane)));
+        if (open && ((type == FMT_MT_REMOVE && p1 == pos) || (type == FMT_MT_ANNOTATE && p2 == pos))) {
+          p2 += len;
+          continue;
+        }
+        if (open) emitCatchup(p1, p2, type);
+        p1 = pos;
+        p2 = pos + len;
+        open = true;
+      }
+      base += tot;
+    }
+    if (open) emitCatchup(p1, p2, type);
+  }
+
+  FMT_DEV void emitCatchup(int p1, int p2, int type) {
+    if (cuN >= cuCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    FOR_LANES(l) {
+      if (l == 0) {
+        fmt_mt_catchup_range c;
+        c.op = opIdx;
+        c.pos1 = p1;
+        c.pos2 = p2;
+        c.type = static_cast<uint32_t>(type);
+        cuOut[cuN] = c;
+      }
+    }
+    cuN++;
+  }
+
   // ------------------------------------------------------------------ ops
   // addToLRUSet (mergeTree.ts:812-822) for leaf j: the first registration of a block sets
   // needsScour; later leaves of that block are no-ops until zamboni clears it.
@@ -632,10 +699,11 @@ class Doc {
   // insertSegments (mergeTree.ts:1484-1517) after the boundary split: the new leaf goes before the
   // first leaf whose view prefix equals pos, leaves removed at/below minSeq skipped except the very
   // last leaf (mergeTree.ts:1862-1875); past the end it is appended to the last leaf's block.
-  FMT_DEV void insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
+  // Returns the new leaf's index, or -1 (nothing inserted, or failure).
+  FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
     const int pos = op.pos1, len = op.len;
-    if (len <= 0) return;
+    if (len <= 0) return -1;
     const int nr = rows();
     Lane<V8> vis, st;
     visLengths(refSeq, client, vis, nr);
@@ -661,14 +729,14 @@ class Doc {
     } else {
       if (pos != static_cast<int>(total)) {  // "MergeTree insert failed" (mergeTree.ts:1629)
         fail(FMT_E_DATA);
-        return;
+        return -1;
       }
       insIdx = n;
       blk = n > 0 ? static_cast<int>(fBlk(readField(n - 1, 0))) : root;
     }
     if (nChars + len > kCapChars) {
       fail(FMT_E_CAPACITY);
-      return;
+      return -1;
     }
     const int cpos = static_cast<int>(charStartOf(insIdx));
     charsShiftUp(cpos, len);
@@ -688,24 +756,38 @@ class Doc {
       s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
       waveSync();
     }
-    if (!insertLeafAt(insIdx, rec)) return;
+    if (!insertLeafAt(insIdx, rec)) return -1;
     childAdded(blk);
-    if (status != FMT_OK) return;
+    if (status != FMT_OK) return -1;
     stamp(kPfInsert);
     lruForLeaf(insIdx, static_cast<int>(fBlk(readField(insIdx, 0))), seq);
     stamp(kPfLru);
+    return status == FMT_OK ? insIdx : -1;
   }
 
   // One member op of a remote message (client.ts:1291-1327).
   FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
-    const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
+    const int refSeq = op.ref_seq, client = op.client;
+    const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
+    Lane<uint32_t> delta;  // catch-up: the segments of the op's delta event (row bitmask per lane)
     if (op.type == FMT_MT_INSERT) {
       if (!splitAt(op.pos1, refSeq, client)) return;
-      insertText(op, text0);
-      return;
+      const int k = insertText(op, text0);
+      if (!catchup || k < 0) return;
+      FOR_LANES(l) { LANE(delta) = l == (k & 63) ? 1u << (k >> 6) : 0u; }  // the new segment (:1497-1508)
+    } else {
+      if (!applyRange(op, delta)) return;
     }
-    if (!splitAt(op.pos1, refSeq, client)) return;
-    if (!splitAt(op.pos2, refSeq, client)) return;
+    recordCatchup(delta, op.type);  // one call site: the recording is inlined once
+  }
+
+  // Remove / annotate (after their boundary splits); fills `delta` for catch-up ops. Returns true
+  // when a catch-up recording should follow.
+  FMT_DEV bool applyRange(const fmt_mt_op& op, Lane<uint32_t>& delta) {
+    const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
+    const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
+    if (!splitAt(op.pos1, refSeq, client)) return false;
+    if (!splitAt(op.pos2, refSeq, client)) return false;
     // nodeMap (mergeTree.ts:2961-3020): leaves of positive view length inside [start, end)
     const int nr = rows();
     const int start = op.pos1, end = op.pos2;
@@ -721,12 +803,15 @@ class Doc {
         if (LANE(vis)[r] > 0 && sp >= start && sp < end) LANE(hits) |= 1u << r;
       }
     }
+    FOR_LANES(l) { LANE(delta) = 0u; }
     if (op.type == FMT_MT_REMOVE) {
-      // markRangeRemoved (mergeTree.ts:2292-2383): first remove stays the lowest seq
+      // markRangeRemoved (mergeTree.ts:2292-2383): first remove stays the lowest seq; the delta
+      // (removedSegments) is the hit leaves not removed before this op (:2314-2321)
       FOR_ROWS(r, 0, nr) {
         FOR_LANES(l) {
           if ((LANE(hits) >> r) & 1u) {
             const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
+            if (rm == kNotRemoved) LANE(delta) |= 1u << r;
             LANE(W[2])[r] = static_cast<uint32_t>(rm < seq ? rm : seq);
             LANE(W[3])[r] |= 1u << client;
           }
@@ -740,7 +825,7 @@ class Doc {
         if (j < 0) break;
         const uint32_t old = fProps(readField(j, 0));
         const uint32_t nw = applyProps(old, op.payload);
-        if (status != FMT_OK) return;
+        if (status != FMT_OK) return false;
         FOR_ROWS(r, 0, nr) {
           FOR_LANES(l) {
             if (((LANE(todo) >> r) & 1u) && fProps(LANE(W[0])[r]) == old) {
@@ -751,10 +836,18 @@ class Doc {
           }
         }
       }
+      if (catchup) {  // deltaSegments: annotated and not removed (mergeTree.ts:2045-2047)
+        FOR_ROWS(r, 0, nr) {
+          FOR_LANES(l) {
+            if (((LANE(hits) >> r) & 1u) && static_cast<int32_t>(LANE(W[2])[r]) == kNotRemoved) LANE(delta) |= 1u << r;
+          }
+        }
+      }
     }
     stamp(kPfRange);
     lruForHits(hits, seq, nr);
     stamp(kPfLru);
+    return catchup && status == FMT_OK;
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
@@ -1043,6 +1136,7 @@ class Doc {
       txt0 = fetchText(rec0);
       rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
+      opIdx = static_cast<uint32_t>(i - in.begin);
       if (op.client > kMaxClient || op.type > FMT_MT_ANNOTATE) fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op, text);
@@ -1145,8 +1239,8 @@ class Doc {
         h.n_blocks = nLeafBlocks;
         h.depth = static_cast<uint32_t>(depth);
         h.visible_len = visible;
-        h.pad[0] = 0;
-        h.pad[1] = 0;
+        h.n_catchup = cuN;
+        h.pad = 0;
         *out.header = h;
       }
     }
@@ -1157,6 +1251,9 @@ class Doc {
     profT = __builtin_amdgcn_s_memtime();
 #endif
     in = inputs;
+    cuOut = out.catchup;
+    cuCap = out.catchup ? out.catchupCap : 0u;
+    cuN = 0;
     init();
     loadInitial();
     if (status == FMT_OK) replay();

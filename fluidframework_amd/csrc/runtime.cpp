@@ -68,6 +68,10 @@ struct fmt_ctx {
   DevBuf<fmt_mt_leaf> mtLeaves;
   DevBuf<uint16_t> mtChars;
   DevBuf<fmt_mt_propset> mtProps;
+  DevBuf<uint64_t> mtCuOffs;                 // per-doc catch-up slab offsets (n_docs + 1)
+  DevBuf<fmt_mt_catchup_range> mtCatchup;    // catch-up range slabs
+  std::vector<uint64_t> mtCuOffsHost;
+  bool mtHasCatchup = false;
   uint64_t mtNOps = 0, mtTextLen = 0, mtInsertChars = 0, mtInitChars = 0;
   uint32_t mtDocs = 0, mtNProps = 0;
   bool mtHasInit = false, mtLoaded = false;
@@ -265,9 +269,10 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   const uint32_t n = b->n_docs;
   if (b->doc_op_offsets[0] != 0 || b->doc_op_offsets[n] != b->n_ops)
     return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
-  uint64_t insertChars = 0;
+  uint64_t insertChars = 0, catchupOps = 0;
   for (uint64_t i = 0; i < b->n_ops; i++) {
     const fmt_mt_op& op = b->ops[i];
+    if (op.flags & FMT_MT_F_CATCHUP) catchupOps++;
     if (op.type == FMT_MT_INSERT) {
       if (static_cast<uint64_t>(op.payload) + op.len > b->text_len)
         return setErr(c, FMT_E_DATA, "insert payload outside the text arena");
@@ -299,6 +304,21 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, c->mtLeaves.reserve(static_cast<size_t>(n) * caps.leaves));
   FMT_HIP(c, c->mtChars.reserve(static_cast<size_t>(n) * caps.chars));
   FMT_HIP(c, c->mtProps.reserve(static_cast<size_t>(n) * caps.props));
+  // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
+  // any; a document that needs more reports FMT_E_CAPACITY.
+  c->mtHasCatchup = catchupOps > 0;
+  if (c->mtHasCatchup) {
+    constexpr uint64_t kCatchupPerOp = 16, kCatchupPerDoc = 16;
+    c->mtCuOffsHost.assign(n + 1ull, 0);
+    for (uint32_t d = 0; d < n; d++) {
+      uint64_t f = 0;
+      for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
+        f += (b->ops[i].flags & FMT_MT_F_CATCHUP) ? 1 : 0;
+      c->mtCuOffsHost[d + 1] = c->mtCuOffsHost[d] + (f ? f * kCatchupPerOp + kCatchupPerDoc : 0);
+    }
+    FMT_HIP(c, c->mtCuOffs.reserve(n + 1ull));
+    FMT_HIP(c, c->mtCatchup.reserve(c->mtCuOffsHost[n]));
+  }
   auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
   };
@@ -306,6 +326,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, cp(c->mtOffs.p, b->doc_op_offsets, (n + 1ull) * sizeof(uint64_t)));
   FMT_HIP(c, cp(c->mtText.p, b->text, b->text_len * sizeof(uint16_t)));
   if (b->doc_init) FMT_HIP(c, cp(c->mtInit.p, b->doc_init, 2ull * n * sizeof(uint32_t)));
+  if (c->mtHasCatchup) FMT_HIP(c, cp(c->mtCuOffs.p, c->mtCuOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
   if (b->props_off) {
     FMT_HIP(c, cp(c->mtPropsOff.p, b->props_off, (b->n_props_ops + 1ull) * sizeof(uint32_t)));
     FMT_HIP(c, cp(c->mtPropsKv.p, b->props_kv, nKv * sizeof(uint32_t)));
@@ -328,8 +349,10 @@ int fmt_mt_run(fmt_ctx* c) {
   if (c == nullptr || !c->mtLoaded) return setErr(c, FMT_E_USAGE, "fmt_mt_run before fmt_mt_load");
   FMT_HIP(c, hipSetDevice(c->device));
   fmt_kernels::MtDeviceBatch db{c->mtOps.p, c->mtOffs.p, c->mtDocs, c->mtText.p,
-                                c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps};
-  fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p};
+                                c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps,
+                                c->mtHasCatchup ? c->mtCuOffs.p : nullptr};
+  fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
+                                c->mtHasCatchup ? c->mtCatchup.p : nullptr};
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->numCUs, c->stream));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -377,6 +400,17 @@ int fmt_mt_fetch_doc(fmt_ctx* c, uint32_t doc, fmt_mt_leaf* leaves, uint32_t cap
   if (leaves && nl) FMT_HIP(c, hipMemcpy(leaves, c->mtLeaves.p + static_cast<size_t>(doc) * caps.leaves, nl * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
   if (chars && nc) FMT_HIP(c, hipMemcpy(chars, c->mtChars.p + static_cast<size_t>(doc) * caps.chars, nc * 2ull, hipMemcpyDeviceToHost));
   if (props && np) FMT_HIP(c, hipMemcpy(props, c->mtProps.p + static_cast<size_t>(doc) * caps.props, np * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_catchup(fmt_ctx* c, uint32_t doc, fmt_mt_catchup_range* out, uint32_t cap) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_catchup: bad arguments");
+  if (!c->mtHasCatchup) return FMT_OK;
+  fmt_mt_doc_result h;
+  FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
+  const uint32_t m = h.n_catchup < cap ? h.n_catchup : cap;
+  if (m) FMT_HIP(c, hipMemcpy(out, c->mtCatchup.p + c->mtCuOffsHost[doc], m * sizeof(fmt_mt_catchup_range), hipMemcpyDeviceToHost));
   return FMT_OK;
 }
 

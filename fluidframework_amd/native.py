@@ -44,10 +44,13 @@ DOC_RESULT_DTYPE = np.dtype(
         ("n_blocks", "<u4"),
         ("depth", "<u4"),
         ("visible_len", "<u4"),
-        ("pad", "<u4", (2,)),
+        ("n_catchup", "<u4"),
+        ("pad", "<u4"),
     ]
 )
 assert DOC_RESULT_DTYPE.itemsize == 48
+
+CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("type", "<u4")])
 
 PROPS_MAX = 4
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
@@ -149,6 +152,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_run.argtypes = [P]
         L.fmt_mt_fetch_headers.argtypes = [P, P]
         L.fmt_mt_fetch_doc.argtypes = [P, U32, P, U32, P, U32, P, U32]
+        L.fmt_mt_fetch_catchup.argtypes = [P, U32, P, U32]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         _libs[path] = L
     return _libs[path]
@@ -157,7 +161,8 @@ def lib(path: str | None = None) -> ctypes.CDLL:
 EXPORTED_SYMBOLS = [
     "fmt_open", "fmt_close", "fmt_last_error", "fmt_sync", "fmt_get_stats", "fmt_device_info",
     "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device",
-    "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_capacity",
+    "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
+    "fmt_mt_capacity",
 ]
 
 
@@ -249,3 +254,12 @@ class Engine:
         props = np.zeros(max(npp, 1), dtype=PROPSET_DTYPE)
         self._check(self.L.fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
         return leaves[:nl], chars[:nc], props[:npp]
+
+    def mt_catchup(self, doc: int, hdr=None) -> np.ndarray:
+        """The document's catch-up ranges (fmt_mt_catchup_range) of its FMT_MT_F_CATCHUP ops."""
+        if hdr is None:
+            hdr = self.mt_headers()[doc]
+        n = int(hdr["n_catchup"])
+        out = np.zeros(max(n, 1), dtype=CATCHUP_DTYPE)
+        self._check(self.L.fmt_mt_fetch_catchup(self.h, doc, _ptr(out), n))
+        return out[:n]

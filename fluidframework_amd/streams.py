@@ -44,6 +44,8 @@ MAP_OP_DTYPE = np.dtype([("doc", "<u4"), ("key", "<u4"), ("seq", "<u4"), ("kind_
 assert MAP_OP_DTYPE.itemsize == 16
 
 MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
+MT_F_GROUP_CONT = 1
+MT_F_CATCHUP = 2  # include/fmt.h FMT_MT_F_CATCHUP
 MAP_SET, MAP_DELETE, MAP_CLEAR = 0, 1, 2
 MAP_KIND_SHIFT = 30
 MAP_VALUE_UNDEFINED = 0x3FFFFFFF
@@ -118,6 +120,9 @@ class MergeTreeBatch:
     keys: list               # key id → key string
     values: list             # value id → JSON text ("null" at id 0, meaning delete)
     clients: list = field(default_factory=list)  # per doc: short id → long client id
+    # per doc (only with keep_messages): [(message dict as applyMsg received it, first op index in
+    # the doc, member op count)] — what SharedSegmentSequence stashes for catch-up ops
+    messages: list = field(default_factory=list)
 
     @property
     def n_docs(self) -> int:
@@ -130,6 +135,7 @@ class _DocBuilder:
         self.client_ids = {observer: 0}
         self.client_names = [observer]
         self.ops: list[tuple] = []
+        self.messages: list[tuple] = []
 
     @property
     def n_ops(self) -> int:
@@ -156,6 +162,8 @@ class _DocBuilder:
         members = contents["ops"] if contents["type"] == MT_GROUP else [contents]
         if not members:
             members = [None]
+        if self.owner.keep_messages:
+            self.messages.append((msg, len(self.ops), len(members)))
         for k, op in enumerate(members):
             rec = self.owner._pack(op, seq, ref, msn, client)
             if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
@@ -169,7 +177,8 @@ class _DocBuilder:
 class MergeTreeStreamBuilder:
     """Packs many documents' sequenced merge-tree messages into one MergeTreeBatch."""
 
-    def __init__(self):
+    def __init__(self, keep_messages: bool = False):
+        self.keep_messages = keep_messages
         self.keys = Dictionary()
         self.values = Dictionary(["null"])
         self.text: list[np.ndarray] = []
@@ -235,7 +244,9 @@ class MergeTreeStreamBuilder:
         self.doc_init.append(self._text(initial_text) if initial_text else (0, 0))
         return d
 
-    def finish(self) -> MergeTreeBatch:
+    def finish(self, catchup: bool = False) -> MergeTreeBatch:
+        """The packed batch. With `catchup`, ops of messages that stay in the legacy summary's
+        catch-up window get FMT_MT_F_CATCHUP (see flag_catchup)."""
         n = sum(d.n_ops for d in self.docs)
         ops = np.zeros(n, dtype=MT_OP_DTYPE)
         offs = np.zeros(len(self.docs) + 1, dtype=np.uint64)
@@ -245,6 +256,8 @@ class MergeTreeStreamBuilder:
                 ops[i : i + d.n_ops] = np.array(d.ops, dtype=MT_OP_DTYPE)
             i += d.n_ops
             offs[di + 1] = i
+        if catchup:
+            flag_catchup(ops, offs)
         text = np.concatenate(self.text) if self.text else np.zeros(0, dtype="<u2")
         props_off = np.zeros(len(self.props_list) + 1, dtype=np.uint32)
         kv = []
@@ -261,7 +274,23 @@ class MergeTreeStreamBuilder:
             keys=list(self.keys.items),
             values=list(self.values.items),
             clients=[list(d.client_names) for d in self.docs],
+            messages=[list(d.messages) for d in self.docs] if self.keep_messages else [],
         )
+
+
+def flag_catchup(ops: np.ndarray, offs: np.ndarray) -> None:
+    """Set FMT_MT_F_CATCHUP on the ops whose message SharedSegmentSequence keeps for the legacy
+    summary's catch-up blob with regenerated contents: seq above the document's final minSeq
+    (processMinSequenceNumberChanged at summarize, sequence.ts:949-963, 1008-1018) and
+    refSeq != seq - 1 (needsTransformation, sequence.ts:978)."""
+    for d in range(len(offs) - 1):
+        a, b = int(offs[d]), int(offs[d + 1])
+        if a == b:
+            continue
+        seg = ops[a:b]
+        final_msn = int(seg["min_seq"][-1])
+        sel = (seg["seq"] > final_msn) & (seg["ref_seq"] != seg["seq"] - 1)
+        seg["flags"][sel] |= MT_F_CATCHUP
 
 
 @dataclass

@@ -11,7 +11,8 @@ from __future__ import annotations
 
 import json
 
-from .streams import MAP_ABSENT, MAP_VALUE_UNDEFINED, is_array_index_key
+from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_REMOVE, is_array_index_key,
+                      js_json, js_key_order)
 
 NOT_REMOVED = 0x7FFFFFFF
 TEXT_GRANULARITY = 256          # textSegment.ts:21
@@ -163,13 +164,70 @@ def legacy_summary(header, leaves, chars, propsets, keys, values, chunk_size=SIZ
     return head, body
 
 
-def summary_tree(header_blob, body_blob):
-    """convertSummaryTreeToITree shape of SharedString.summarizeCore's content subtree."""
+def catchup_messages(messages, ranges, min_seq):
+    """The legacy summary's catch-up messages for one document (sequence.ts:949-1018).
+
+    messages: [(message dict as applyMsg received it, first op index, member count)] in order
+    (MergeTreeBatch.messages[d]); ranges: the document's fmt_mt_catchup_range records (engine or
+    oracle) for its FMT_MT_F_CATCHUP ops; min_seq: the summary's minimumSequenceNumber.
+    Messages with seq <= min_seq are dropped (processMinSequenceNumberChanged); a message with
+    refSeq == seq - 1 is kept as it is; any other is a shallow copy with refSeq = seq - 1 and
+    contents regenerated from its delta ranges by createOpsFromDelta (sequence.ts:395-452): one op
+    stays bare, several (or none) become a GROUP op. Every kept message gets minimumSequenceNumber
+    = min_seq and loses `term` (sequence.ts:955-957, snapshotlegacy.ts:178-185).
+    """
+    by_op: dict[int, list] = {}
+    for r in ranges:
+        by_op.setdefault(int(r["op"]), []).append((int(r["type"]), int(r["pos1"]), int(r["pos2"])))
+    out = []
+    for msg, first, count in messages:
+        seq = int(msg["sequenceNumber"])
+        if seq <= min_seq:
+            continue
+        if int(msg["referenceSequenceNumber"]) != seq - 1:
+            contents = msg["contents"]
+            members = contents["ops"] if contents["type"] == MT_GROUP else [contents]
+            ops = []
+            for k, op in enumerate(members):
+                for t, p1, p2 in by_op.get(first + k, []):
+                    if t == MT_INSERT:  # createInsertOp(pos, segment.clone().toJSONObject())
+                        seg = op["seg"]
+                        ops.append({"pos1": p1, "seg": seg if isinstance(seg, str) else seg["text"], "type": t})
+                    elif t == MT_REMOVE:  # createRemoveRangeOp
+                        ops.append({"pos1": p1, "pos2": p2, "type": t})
+                    else:  # createAnnotateRangeOp(pos1, pos2, {...props}): the segment's value ?? null
+                        props = op.get("props") or {}
+                        ops.append({"pos1": p1, "pos2": p2, "props": {k2: props[k2] for k2 in js_key_order(list(props))},
+                                    "type": t})
+            msg = dict(msg)
+            msg["referenceSequenceNumber"] = seq - 1
+            msg["contents"] = ops[0] if len(ops) == 1 else {"ops": ops, "type": MT_GROUP}
+        else:
+            msg = dict(msg)
+        msg["minimumSequenceNumber"] = min_seq
+        msg.pop("term", None)
+        out.append(msg)
+    return out
+
+
+def catchup_blob(msgs):
+    """JSON.stringify(catchUpMsgs) (snapshotlegacy.ts:186-189), or None when there are none."""
+    if not msgs:
+        return None
+    return js_json(msgs)
+
+
+def summary_tree(header_blob, body_blob, catchup=None):
+    """convertSummaryTreeToITree shape of SharedString.summarizeCore's content subtree (blobs in
+    SnapshotLegacy.emit order: header, body, catchupOps)."""
     entries = [{"path": "header", "mode": "100644", "type": "Blob",
                 "value": {"contents": header_blob, "encoding": "utf-8"}}]
     if body_blob is not None:
         entries.append({"path": "body", "mode": "100644", "type": "Blob",
                         "value": {"contents": body_blob, "encoding": "utf-8"}})
+    if catchup is not None:
+        entries.append({"path": "catchupOps", "mode": "100644", "type": "Blob",
+                        "value": {"contents": catchup, "encoding": "utf-8"}})
     return {"entries": [{"path": "content", "mode": "040000", "type": "Tree", "value": {"entries": entries}}]}
 
 

@@ -78,6 +78,11 @@ extern "C" {
  * (client.ts:1311-1319, 1358-1379). Separate messages that share a seq (a runtime "bunch") are NOT
  * flagged: each advances the window, exactly as each applyMsg call does. 32 bytes. */
 #define FMT_MT_F_GROUP_CONT 1u
+/* Record the op's regenerated "catch-up" contents: the ranges of the sequenceDelta event it raises,
+ * merged as SharedSegmentSequence.createOpsFromDelta merges them (sequence/src/sequence.ts:395-452).
+ * The host sets it on the ops of messages that stay in the legacy summary's catch-up window
+ * (seq > final minSeq) and need transformation (refSeq != seq - 1, sequence.ts:971-1006). */
+#define FMT_MT_F_CATCHUP 2u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */
@@ -148,8 +153,22 @@ typedef struct fmt_mt_doc_result {
   uint32_t n_blocks;   /* number of leaf blocks */
   uint32_t depth;      /* tree depth (1 = root holds leaves) */
   uint32_t visible_len;/* getLength() from the local perspective */
-  uint32_t pad[2];
+  uint32_t n_catchup;  /* catch-up ranges recorded for FMT_MT_F_CATCHUP ops (fmt_mt_fetch_catchup) */
+  uint32_t pad;
 } fmt_mt_doc_result;
+
+/* One regenerated catch-up op range (a merged ISequenceDeltaRange, sequence.ts:395-452): positions
+ * are in the local view right after the op applied, before its zamboni pass
+ * (mergeTree.ts:1503-1516, 2069-2080, 2364-2382; SequenceDeltaEventClass positions via
+ * Client.getPosition, sequenceDeltaEvent.ts:91-103). INSERT: [pos1, pos1 + text length);
+ * REMOVE: newly removed segments, merged while they start at the same position; ANNOTATE:
+ * annotated segments not removed, merged while contiguous. Ranges of one op are in document order. */
+typedef struct fmt_mt_catchup_range {
+  uint32_t op;   /* index of the op record within its document (0 = doc_op_offsets[d]) */
+  int32_t pos1;
+  int32_t pos2;
+  uint32_t type; /* FMT_MT_INSERT / FMT_MT_REMOVE / FMT_MT_ANNOTATE */
+} fmt_mt_catchup_range;
 
 /* A document-local prop set: up to FMT_MT_PROPS_MAX (key_id, value_id) pairs in JS insertion order. */
 #define FMT_MT_PROPS_MAX 4
@@ -239,6 +258,10 @@ int fmt_mt_fetch_headers(fmt_ctx* ctx, fmt_mt_doc_result* out);
  * (client.ts:1548-1587, snapshotlegacy.ts:195-262) read. */
 int fmt_mt_fetch_doc(fmt_ctx* ctx, uint32_t doc, fmt_mt_leaf* leaves, uint32_t cap_leaves,
                      uint16_t* chars, uint32_t cap_chars, fmt_mt_propset* props, uint32_t cap_props);
+/* One document's catch-up ranges (header n_catchup entries, at most cap), in op order. Replaces the
+ * messagesSinceMSNChange contents SharedSegmentSequence stashes for the legacy summary's catchupOps
+ * blob (sequence.ts:949-1018, snapshotlegacy.ts:178-190). */
+int fmt_mt_fetch_catchup(fmt_ctx* ctx, uint32_t doc, fmt_mt_catchup_range* out, uint32_t cap);
 /* Per-document capacities of this engine build (leaves, chars, prop sets). */
 int fmt_mt_capacity(uint32_t* max_leaves, uint32_t* max_chars, uint32_t* max_props);
 

@@ -27,11 +27,15 @@ int fail(const char* what) {
 
 // Applies ops[0..n): a record flagged FMT_MT_F_GROUP_CONT continues the previous message.
 int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* arena,
-             const uint32_t* propsOff, const uint32_t* propsKv, int32_t* failSeq) {
+             const uint32_t* propsOff, const uint32_t* propsKv, int32_t* failSeq,
+             std::vector<fmt_mt_catchup_range>* catchup = nullptr) {
   for (uint64_t i = 0; i < n; i++) {
     const fmt_mt_op& op = ops[i];
     try {
+      mt->catchupOut = (catchup && (op.flags & FMT_MT_F_CATCHUP)) ? catchup : nullptr;
+      mt->catchupOp = static_cast<uint32_t>(i);
       mt->applyRemote(op, arena, propsOff, propsKv);
+      mt->catchupOut = nullptr;
       if (i + 1 == n || (ops[i + 1].flags & FMT_MT_F_GROUP_CONT) == 0) mt->updateSeqNumbers(op.min_seq, op.seq);
     } catch (const std::exception& e) {
       if (failSeq) *failSeq = op.seq;
@@ -195,7 +199,8 @@ int orc_mt_summary(void* h, const char* const* keys, int nKeys, const char* cons
 int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEnd,
                         uint32_t nThreads, fmt_mt_doc_result* hdrs, fmt_mt_leaf* leaves,
                         uint32_t capLeaves, uint16_t* chars, uint32_t capChars,
-                        fmt_mt_propset* props, uint32_t capProps, double* seconds) {
+                        fmt_mt_propset* props, uint32_t capProps, fmt_mt_catchup_range* catchup,
+                        uint32_t capCatchup, double* seconds) {
   const auto t0 = std::chrono::steady_clock::now();
   std::atomic<int> status{FMT_OK};
   parallelFor(docBegin, docEnd, nThreads, [&](uint32_t d) {
@@ -209,7 +214,9 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
     }
     mt.startCollaboration(0, 0, 0);
     const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
-    st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq);
+    std::vector<fmt_mt_catchup_range> cu;
+    st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq,
+                  catchup ? &cu : nullptr);
     if (st != FMT_OK) status = st;
     fmt_mt_doc_result* h = hdrs ? &hdrs[i] : nullptr;
     if (h) std::memset(h, 0, sizeof(*h));
@@ -221,7 +228,10 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
     if (h) {
       h->status = st;
       h->fail_seq = failSeq;
+      h->n_catchup = static_cast<uint32_t>(cu.size());
     }
+    if (catchup)
+      for (size_t k = 0; k < cu.size() && k < capCatchup; k++) catchup[i * capCatchup + k] = cu[k];
   });
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return status.load();

@@ -344,6 +344,7 @@ void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp st
     InsertCtx ctx{true, seg};
     insertingWalk(pos, p, stamp, ctx);
     if (seg->parent == nullptr) throw DataError("MergeTree insert failed");
+    if (catchupOut) recordDelta(FMT_MT_INSERT, {seg});  // delta callback precedes zamboni (:1497-1516)
     if (collaborating) {
       const bool isLocal = stamp.seq == kUnassignedSeq;
       if (!(isLocal && stamp.client == clientId) &&
@@ -360,8 +361,10 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
   ensureIntervalBoundary(end, p);
   std::vector<Seg*> hit;
   nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
+  std::vector<Seg*> newlyRemoved;  // removedSegments: the REMOVE delta (mergeTree.ts:2314-2321)
   for (Seg* s : hit) {
     if (!s->removed() || stamp.seq == kUnassignedSeq) {
+      if (!s->removed()) newlyRemoved.push_back(s);
       s->removes.push_back(stamp);
     } else {
       int i = static_cast<int>(s->removes.size()) - 1;
@@ -374,6 +377,7 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
       if (!localPending) addToLRUSet(s, stamp.seq);
     }
   }
+  if (catchupOut) recordDelta(FMT_MT_REMOVE, newlyRemoved);  // mergeTree.ts:2363-2368
   if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
 }
 
@@ -402,7 +406,50 @@ void MergeTree::annotateRange(int start, int end,
     }
     if (collaborating && stamp.seq != kUnassignedSeq) addToLRUSet(s, stamp.seq);
   }
+  if (catchupOut) {  // deltaSegments: annotated segments not removed (mergeTree.ts:2045-2047, 2068-2073)
+    std::vector<Seg*> delta;
+    for (Seg* s : hit)
+      if (!s->removed()) delta.push_back(s);
+    recordDelta(FMT_MT_ANNOTATE, delta);
+  }
   if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
+}
+
+// mergeTree.ts:835-856 getPosition: lengths of everything before the node, walking up the parents.
+int MergeTree::getPosition(const Node* node) const {
+  int total = 0;
+  const Perspective lp = localPerspective();
+  const Node* prev = node;
+  for (const Block* parent = node->parent; parent != nullptr; prev = parent, parent = parent->parent) {
+    for (int i = 0; i < parent->childCount; i++) {
+      const Node* c = parent->children[i];
+      if (c == prev) break;
+      const int l = nodeLength(c, lp);
+      if (l > 0) total += l;  // `?? 0`
+    }
+  }
+  return total;
+}
+
+// sequence.ts:395-452 createOpsFromDelta over one event's ranges, which SequenceDeltaEventClass
+// orders by segment (document order) with position = Client.getPosition (sequenceDeltaEvent.ts:91-103).
+// REMOVE merges a range that starts where the previous one started (removed text has no local
+// length); ANNOTATE merges a range that starts where the previous one ended when the props match —
+// they always do here: every segment's propertyDeltas holds every key of the op, and the raw value
+// the segment now holds is the op's own (segmentPropertiesManager.ts:199-235 with no pending local).
+void MergeTree::recordDelta(uint32_t type, const std::vector<Seg*>& deltaSegs) {
+  const size_t first = catchupOut->size();
+  for (const Seg* s : deltaSegs) {
+    const int pos = getPosition(s);
+    if (catchupOut->size() > first) {
+      fmt_mt_catchup_range& last = catchupOut->back();
+      if ((type == FMT_MT_REMOVE && last.pos1 == pos) || (type == FMT_MT_ANNOTATE && last.pos2 == pos)) {
+        last.pos2 += s->len();
+        continue;
+      }
+    }
+    catchupOut->push_back(fmt_mt_catchup_range{catchupOp, pos, pos + s->len(), type});
+  }
 }
 
 // mergeTree.ts:1147-1166

@@ -147,6 +147,12 @@ class MergeTree {
   // client.ts:1381-1391 updateSeqNumbers, after the last member of a message.
   void updateSeqNumbers(int min, int seq);
 
+  // Legacy catch-up ops (sequence.ts:971-1006): while set, each applied op appends the ranges of
+  // the sequenceDelta event it raises, merged the way createOpsFromDelta merges them
+  // (sequence.ts:395-452), tagged with catchupOp.
+  std::vector<fmt_mt_catchup_range>* catchupOut = nullptr;
+  uint32_t catchupOp = 0;
+
   // Readouts.
   std::u16string getText() const;     // MergeTreeTextHelper.ts:28-87 (local perspective)
   int getLocalLength() const;
@@ -192,6 +198,9 @@ class MergeTree {
   void updateRoot(Block* splitNode);
   Seg* splitAt(Seg* seg, int pos);
   void ensureIntervalBoundary(int pos, const Perspective& p);
+
+  int getPosition(const Node* node) const;  // mergeTree.ts:835-856, local perspective
+  void recordDelta(uint32_t type, const std::vector<Seg*>& deltaSegs);
 
   template <class F>
   void nodeMap(const Perspective& p, int start, int end, F&& leafFn) const;

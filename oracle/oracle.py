@@ -41,7 +41,8 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_summary.argtypes = [P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P,
                                      ctypes.c_int, P, P]
         L.orc_mt_replay_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P,
-                                          ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P]
+                                          ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P,
+                                          ctypes.c_uint32, P]
         L.orc_map_replay.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.c_uint32, P]
         L.orc_map_summary.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P,
                                       ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P]
@@ -134,9 +135,14 @@ class MergeTreeDoc:
 
 
 def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096, cap_chars=1 << 16,
-                    cap_props=64, outputs=True):
-    """Replay a MergeTreeBatch; returns (headers, leaves, chars, props, seconds)."""
-    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+                    cap_props=64, outputs=True, cap_catchup=0):
+    """Replay a MergeTreeBatch; returns (rc, headers, leaves, chars, props, seconds).
+
+    With cap_catchup > 0 the catch-up ranges of FMT_MT_F_CATCHUP ops are recorded too and returned
+    as a 7th element, shape (n_docs, cap_catchup) of CATCHUP_DTYPE (headers' n_catchup counts them).
+    """
+    from fluidframework_amd.native import (CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE,
+                                           batch_struct)
 
     doc_end = batch.n_docs if doc_end is None else doc_end
     n = doc_end - doc_begin
@@ -144,16 +150,19 @@ def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096
     leaves = np.zeros(n * cap_leaves, dtype=LEAF_DTYPE) if outputs else None
     chars = np.zeros(n * cap_chars, dtype="<u2") if outputs else None
     props = np.zeros(n * cap_props, dtype=PROPSET_DTYPE) if outputs else None
+    catchup = np.zeros(n * cap_catchup, dtype=CATCHUP_DTYPE) if cap_catchup else None
     secs = ctypes.c_double(0)
     b, keep = batch_struct(batch)
     rc = lib().orc_mt_replay_batch(ctypes.byref(b), doc_begin, doc_end, threads, _ptr(hdrs),
                                    _ptr(leaves), cap_leaves, _ptr(chars), cap_chars, _ptr(props),
-                                   cap_props, ctypes.byref(secs))
+                                   cap_props, _ptr(catchup), cap_catchup, ctypes.byref(secs))
     del keep
     if outputs:
         leaves = leaves.reshape(n, cap_leaves)
         chars = chars.reshape(n, cap_chars)
         props = props.reshape(n, cap_props)
+    if cap_catchup:
+        return rc, hdrs, leaves, chars, props, secs.value, catchup.reshape(n, cap_catchup)
     return rc, hdrs, leaves, chars, props, secs.value
 
 

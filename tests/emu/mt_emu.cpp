@@ -17,7 +17,7 @@ int emu_mt_capacity(uint32_t* leaves, uint32_t* chars, uint32_t* props) {
 
 // Same strides as the GPU result buffers (kCapLeaves / kCapChars / kPropCap per document).
 int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
-                  fmt_mt_propset* props) {
+                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup) {
   auto scratch = std::make_unique<fmt_mt::Scratch>();
   auto doc = std::make_unique<fmt_mt::Doc>();
   int status = FMT_OK;
@@ -38,6 +38,8 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
     o.leaves = leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;
     o.chars = chars + static_cast<size_t>(d) * fmt_mt::kCapChars;
     o.props = props + static_cast<size_t>(d) * fmt_mt::kPropCap;
+    o.catchup = catchup ? catchup + static_cast<size_t>(d) * capCatchup : nullptr;
+    o.catchupCap = catchup ? capCatchup : 0u;
     new (doc.get()) fmt_mt::Doc();
     doc->s = scratch.get();
     doc->run(in, o);

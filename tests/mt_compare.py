@@ -11,7 +11,7 @@ import subprocess
 
 import numpy as np
 
-from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+from fluidframework_amd.native import CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 EMU_PATH = os.path.join(HERE, "_build", "libmt_emu.so")
@@ -28,7 +28,7 @@ def emu_lib():
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas", "-o",
                             EMU_PATH, src], check=True)
         L = ctypes.CDLL(EMU_PATH)
-        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 5
+        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32]
         L.emu_mt_capacity.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
         _emu = L
     return _emu
@@ -44,18 +44,22 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def emu_replay(batch):
-    """Run the engine source under host emulation; returns (headers, leaves, chars, props)."""
+def emu_replay(batch, cap_catchup=0):
+    """Run the engine source under host emulation; returns (headers, leaves, chars, props), plus the
+    catch-up ranges (n_docs, cap_catchup) when cap_catchup > 0."""
     cl, cc, cp = emu_caps()
     n = batch.n_docs
     hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
     leaves = np.zeros(n * cl, dtype=LEAF_DTYPE)
     chars = np.zeros(n * cc, dtype="<u2")
     props = np.zeros(n * cp, dtype=PROPSET_DTYPE)
+    cu = np.zeros(n * cap_catchup, dtype=CATCHUP_DTYPE) if cap_catchup else None
     b, keep = batch_struct(batch)
-    emu_lib().emu_mt_replay(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props))
+    emu_lib().emu_mt_replay(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props),
+                            _p(cu) if cu is not None else None, cap_catchup)
     del keep
-    return hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp)
+    out = (hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp))
+    return out + (cu.reshape(n, cap_catchup),) if cap_catchup else out
 
 
 def resolve_props(pid, table):

@@ -174,3 +174,29 @@ def test_mt_reports_capacity_and_data_errors(engine):
     hdrs = _gpu_mt(engine, batch)
     assert hdrs["status"][0] == native.FMT_E_CAPACITY and hdrs["fail_seq"][0] == 2
     assert hdrs["status"][1] == native.FMT_E_DATA and hdrs["fail_seq"][1] == 1
+
+
+def test_mt_catchup_ranges_match_oracle(orc, engine):
+    """Legacy catch-up ranges (FMT_MT_F_CATCHUP ops) bit-exact vs the oracle, and the reload property."""
+    from fluidframework_amd import streams, summary
+    from test_catchup import CAP, fixture_batch, reload_text
+
+    batch, finals = fixture_batch()
+    hdrs = _gpu_mt(engine, batch)
+    rc, oh, ol, oc, op, _, ocu = orc.mt_replay_batch(batch, cap_catchup=CAP)
+    assert rc == 0 and (hdrs["status"] == 0).all()
+    for d in range(batch.n_docs):
+        n = int(oh[d]["n_catchup"])
+        got = engine.mt_catchup(d, hdrs[d])
+        assert len(got) == n and np.array_equal(got, ocu[d][:n]), d
+        leaves, chars, props = engine.mt_doc(d, hdrs[d])
+        msgs = summary.catchup_messages(batch.messages[d], got, int(hdrs[d]["min_seq"]))
+        assert reload_text(orc, hdrs[d], leaves, chars, props, batch.keys, batch.values, msgs) == finals[d]
+    cf = workloads.conflict_farm(512, n_clients=8, ops_per_doc=2000, seed=21)
+    streams.flag_catchup(cf.ops, cf.doc_op_offsets)
+    hdrs = _gpu_mt(engine, cf)
+    rc, oh, ol, oc, op, _, ocu = orc.mt_replay_batch(cf, threads=16, cap_catchup=CAP)
+    assert rc == 0 and (hdrs["status"] == 0).all()
+    for d in range(cf.n_docs):
+        n = int(oh[d]["n_catchup"])
+        assert n > 0 and np.array_equal(engine.mt_catchup(d, hdrs[d]), ocu[d][:n]), d
