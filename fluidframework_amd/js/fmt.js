@@ -15,14 +15,16 @@
  * Written for the Node in this image (v12): CommonJS, no `??` / `?.`.
  */
 const path = require("path");
+const summary = require("./summary.js");
 
 const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3; // merge-tree/src/ops.ts:61-71
 const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
 const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
-const FMT_MT_F_GROUP_CONT = 1;
+const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2;
 const MAX_CLIENTS = 63;
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 20;
+const CATCHUP_BYTES = 16;
 const PROPS_MAX = 4;
 
 let addon = null;
@@ -112,6 +114,7 @@ class MergeTreeDocBuilder {
 		this.clientIds = new Map([[observer, 0]]);
 		this.clientNames = [observer];
 		this.nOps = 0;
+		this.messages = []; // {message, firstOp, count} when the builder keeps messages
 	}
 	shortClient(longId) {
 		const id = longId === null || longId === undefined ? "server" : longId;
@@ -133,6 +136,7 @@ class MergeTreeDocBuilder {
 		const contents = msg.contents;
 		let members = contents.type === MT_GROUP ? contents.ops : [contents];
 		if (members.length === 0) members = [null]; // empty group: only advances the window
+		if (this.owner.keepMessages) this.messages.push({ message: msg, firstOp: this.nOps, count: members.length });
 		members.forEach((op, k) => {
 			this.owner.packOp(op, msg.sequenceNumber, msg.referenceSequenceNumber,
 				msg.minimumSequenceNumber, client, k > 0 ? FMT_MT_F_GROUP_CONT : 0);
@@ -161,7 +165,12 @@ function jsKeyOrder(obj) {
 
 /** Packs many documents' sequenced merge-tree messages (mirror of streams.py MergeTreeStreamBuilder). */
 class MergeTreeStreamBuilder {
-	constructor() {
+	/**
+	 * @param options - {keepMessages}: keep each document's messages (as applyMsg received them)
+	 * for the legacy summary's catch-up blob.
+	 */
+	constructor(options) {
+		this.keepMessages = !!(options && options.keepMessages);
 		this.keys = new Dictionary();
 		this.values = new Dictionary(["null"]);
 		this.text = new U16Arena();
@@ -238,14 +247,33 @@ class MergeTreeStreamBuilder {
 		v.setUint8(o + 27, type);
 		v.setUint32(o + 28, flags, true);
 	}
-	/** The packed batch: the typed arrays the addon hands to fmt_mt_load. */
-	finish() {
+	/**
+	 * The packed batch: the typed arrays the addon hands to fmt_mt_load. With {catchup: true} the
+	 * ops of messages a legacy summary keeps with regenerated contents get FMT_MT_F_CATCHUP: seq
+	 * above the document's final minSeq and refSeq != seq - 1 (sequence.ts:949-1018).
+	 */
+	finish(options) {
 		const offs = new BigUint64Array(this.docs.length + 1);
 		let i = 0;
 		this.docs.forEach((d, k) => {
 			i += d.nOps;
 			offs[k + 1] = BigInt(i);
 		});
+		if (options && options.catchup) {
+			const v = this.ops.view;
+			let a = 0;
+			for (const d of this.docs) {
+				const b = a + d.nOps;
+				if (b > a) {
+					const finalMsn = v.getInt32((b - 1) * MT_OP_BYTES + 8, true);
+					for (let o = a * MT_OP_BYTES; o < b * MT_OP_BYTES; o += MT_OP_BYTES) {
+						const seq = v.getInt32(o, true), ref = v.getInt32(o + 4, true);
+						if (seq > finalMsn && ref !== seq - 1) v.setUint32(o + 28, v.getUint32(o + 28, true) | FMT_MT_F_CATCHUP, true);
+					}
+				}
+				a = b;
+			}
+		}
 		const propsOff = new Uint32Array(this.propsList.length + 1);
 		const kv = [];
 		this.propsList.forEach((t, j) => {
@@ -267,6 +295,7 @@ class MergeTreeStreamBuilder {
 			keys: this.keys.items.slice(),
 			values: this.values.items.slice(),
 			clients: this.docs.map((d) => d.clientNames.slice()),
+			messages: this.docs.map((d) => d.messages),
 			nDocs: this.docs.length,
 		};
 	}
@@ -359,6 +388,7 @@ function readHeader(dv, d) {
 		nBlocks: dv.getUint32(o + 28, true),
 		depth: dv.getUint32(o + 32, true),
 		visibleLength: dv.getUint32(o + 36, true),
+		nCatchup: dv.getUint32(o + 40, true),
 	};
 }
 
@@ -394,20 +424,62 @@ class MergeTreeReplay {
 			}
 			props.push(obj);
 		}
+		const kvs = [];
+		for (let p = 0; p < h.nProps; p++) {
+			const n = Math.min(pv.getUint32(p * PROPSET_BYTES, true), PROPS_MAX);
+			const kv = [];
+			for (let k = 0; k < n; k++) kv.push(pv.getUint32(p * PROPSET_BYTES + 4 + 4 * k, true));
+			kvs.push(kv);
+		}
 		const segs = [];
 		for (let i = 0; i < h.nLeaves; i++) {
 			const o = i * LEAF_BYTES;
 			const off = lv.getUint32(o + 16, true), len = lv.getUint16(o + 20, true);
 			const pid = lv.getUint16(o + 24, true);
+			const rm = lv.getInt32(o + 4, true);
 			segs.push({
 				insertSeq: lv.getInt32(o, true),
-				removedSeq: lv.getInt32(o + 4, true) === NOT_REMOVED ? undefined : lv.getInt32(o + 4, true),
+				removedSeq: rm === NOT_REMOVED ? undefined : rm,
 				insertClient: lv.getInt16(o + 22, true),
 				text: String.fromCharCode.apply(null, chars.subarray(off, off + len)),
 				properties: pid === 0xffff ? undefined : props[pid],
+				kv: pid === 0xffff ? null : kvs[pid],
 			});
 		}
 		return segs;
+	}
+	/** The document's catch-up ranges (ops flagged by finish({catchup: true})). */
+	catchupRanges(doc) {
+		const n = this.header(doc).nCatchup;
+		const dv = new DataView(native().fetchCatchup(this.engine.ctx, doc, n));
+		const out = [];
+		for (let i = 0; i < n; i++) {
+			const o = i * CATCHUP_BYTES;
+			out.push({ op: dv.getUint32(o, true), pos1: dv.getInt32(o + 4, true), pos2: dv.getInt32(o + 8, true),
+				type: dv.getUint32(o + 12, true) });
+		}
+		return out;
+	}
+	/**
+	 * SharedString.summarizeCore legacy blobs at the document's minSeq (snapshotlegacy.ts:126-262):
+	 * {header, body (or undefined), catchupOps (or undefined)}. catchupOps needs a batch built with
+	 * keepMessages and finish({catchup: true}).
+	 */
+	summarize(doc) {
+		const h = this.header(doc);
+		const segs = this.segments(doc).map((s) => ({
+			insertSeq: s.insertSeq,
+			removedSeq: s.removedSeq === undefined ? NOT_REMOVED : s.removedSeq,
+			text: s.text,
+			kv: s.kv,
+		}));
+		const out = summary.legacySummary(segs, h.minSeq, this.batch.keys, this.batch.values);
+		const msgs = this.batch.messages && this.batch.messages[doc];
+		if (msgs && msgs.length) {
+			const cu = summary.catchupMessages(msgs, this.catchupRanges(doc), h.minSeq);
+			if (cu.length) out.catchupOps = JSON.stringify(cu);
+		}
+		return out;
 	}
 	/** MergeTreeTextHelper.getText from the local perspective (MergeTreeTextHelper.ts:28-87). */
 	getText(doc) {
@@ -437,6 +509,19 @@ class MapReplay {
 		live.sort((a, b) => a[0] - b[0] || a[1] - b[1]);
 		return live.map(([, k, v]) => [this.batch.keys[k],
 			v === MAP_VALUE_UNDEFINED ? undefined : JSON.parse(this.batch.values[v])]);
+	}
+	/** SharedMap.summarizeCore blobs (map.ts:176-246): {header, blobs}. */
+	summarize(doc) {
+		const kb = this.batch.keyBound;
+		const live = [];
+		for (let k = 0; k < kb; k++) {
+			const o = (doc * kb + k) * 8;
+			const value = this.view.getUint32(o, true);
+			if (value !== MAP_ABSENT) live.push([this.view.getUint32(o + 4, true), k, value]);
+		}
+		live.sort((a, b) => a[0] - b[0] || a[1] - b[1]);
+		return summary.mapSummary(live.map(([, k, v]) => [this.batch.keys[k],
+			v === MAP_VALUE_UNDEFINED ? undefined : this.batch.values[v]]));
 	}
 	get(doc, key) {
 		const k = this.batch.keys.indexOf(key);
@@ -479,6 +564,7 @@ module.exports = {
 	MergeTreeReplay,
 	MapReplay,
 	UnsupportedOp,
+	summary,
 	constants: { MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MAP_SET, MAP_DELETE, MAP_CLEAR,
-		MAP_VALUE_UNDEFINED, MAP_ABSENT, FMT_MT_F_GROUP_CONT, NOT_REMOVED },
+		MAP_VALUE_UNDEFINED, MAP_ABSENT, FMT_MT_F_GROUP_CONT, FMT_MT_F_CATCHUP, NOT_REMOVED },
 };

@@ -7,6 +7,7 @@
 //   node fixture_driver.js replay          replay them on the GPU through the N-API addon and print
 //                                          {"checked": n, "mismatches": [...]} as one JSON line
 //   node fixture_driver.js map             a SharedMap bunch replay through processMessagesCore (GPU)
+//   node fixture_driver.js summary         legacy summaries + catch-up blobs of each fixture (GPU)
 const fs = require("fs");
 const path = require("path");
 const zlib = require("zlib");
@@ -95,7 +96,31 @@ async function mapDemo() {
 	const eng = new fmt.Engine(0);
 	try {
 		const r = await eng.replayMap(batch);
-		console.log(JSON.stringify({ doc0: r.entries(0), doc1: r.entries(1), a0: r.get(0, "a") }));
+		console.log(JSON.stringify({ doc0: r.entries(0), doc1: r.entries(1), a0: r.get(0, "a"),
+			summary0: r.summarize(0).header }));
+	} finally {
+		eng.close();
+	}
+}
+
+/** Legacy summaries (with catch-up blobs) of each fixture's final state, from GPU state. */
+async function summaries() {
+	const fixtures = loadFixtures();
+	const b = new fmt.MergeTreeStreamBuilder({ keepMessages: true });
+	for (const fx of fixtures) {
+		const doc = b.beginDoc(fx.groups[0].initialText, "A");
+		for (const g of fx.groups) for (const m of g.msgs) doc.addMessage(m);
+	}
+	const batch = b.finish({ catchup: true });
+	const eng = new fmt.Engine(0);
+	try {
+		const r = await eng.replayMergeTree(batch);
+		const out = fixtures.map((fx, d) => {
+			const s = r.summarize(d);
+			return { header: s.header, body: s.body === undefined ? null : s.body,
+				catchupOps: s.catchupOps === undefined ? null : s.catchupOps };
+		});
+		console.log(JSON.stringify(out));
 	} finally {
 		eng.close();
 	}
@@ -106,9 +131,11 @@ if (mode === "pack") {
 	pack(process.argv[3]);
 } else if (mode === "replay") {
 	replay().catch((e) => { console.error(e); process.exit(1); });
+} else if (mode === "summary") {
+	summaries().catch((e) => { console.error(e); process.exit(1); });
 } else if (mode === "map") {
 	mapDemo().catch((e) => { console.error(e); process.exit(1); });
 } else {
-	console.error("usage: fixture_driver.js pack <outdir> | replay | map");
+	console.error("usage: fixture_driver.js pack <outdir> | replay | summary | map");
 	process.exit(2);
 }

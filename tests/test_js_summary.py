@@ -1,0 +1,106 @@
+"""The JavaScript summary code (fluidframework_amd/js/summary.js) on the CPU.
+
+- SharedString legacy blobs from converged state equal the reference's snapshot fixtures
+  (sequence/src/test/snapshots/legacy/*.json, snapshotVersion.spec.ts:146-170), byte for byte.
+- SharedMap summaries equal the strings map.spec.ts:142-317 asserts.
+- On the reference's replay fixture messages, legacy blobs and catch-up blobs equal the Python host's
+  (summary.py), which the GPU suite checks against the oracle.
+The converged state fed in is the oracle's (test infrastructure); the engine produces the same state
+bit for bit (test_gpu_parity.py).
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from fluidframework_amd import summary
+from test_catchup import CAP, fixture_batch
+from test_oracle_golden import _blobs, _detached_string, _map_batch, _set
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(REPO, "tests", "js", "summary_driver.js")
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node is not installed")
+
+
+def _run(cases, tmp_path):
+    f = tmp_path / "cases.json"
+    f.write_text(json.dumps(cases), encoding="utf-8")
+    r = subprocess.run([NODE, DRIVER, str(f)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def _segs(leaves, chars, props):
+    out = []
+    for L in leaves:
+        o, n = int(L["char_off"]), int(L["len"])
+        pid = int(L["props"])
+        kv = None if pid == 0xFFFF else [int(x) for x in props[pid]["kv"][: props[pid]["n"]]]
+        out.append({"insertSeq": int(L["ins_seq"]), "removedSeq": int(L["rm_seq"]),
+                    "text": chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass"), "kv": kv})
+    return out
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+def test_js_legacy_summary_matches_reference_snapshot(orc, name, tmp_path):
+    from golden_data import snapshot_trees
+
+    expected = _blobs(snapshot_trees()[name])
+    doc, keys, values = _detached_string(orc, name)
+    h, leaves, chars, props = doc.dump()
+    [got] = _run([{"kind": "string", "segs": _segs(leaves, chars, props), "minSeq": int(h["min_seq"]),
+                   "keys": keys, "values": values}], tmp_path)
+    assert got["header"] == expected["header"]
+    assert got["body"] == expected.get("body")
+
+
+def test_js_map_summaries_match_reference_strings(orc, tmp_path):
+    long = "01234567890"
+    for _ in range(12):
+        long = long + long
+    handle = {"type": "__fluid_handle__", "url": "/subMap"}
+    cases_msgs = [
+        [_set("key", "value")],
+        [_set("first", "second"), _set("third", "fourth"), _set("fifth", undefined=True), _set("object", handle)],
+        [_set("key", "value"), _set("longValue", long), _set("zzz", "the end")],
+        [_set("b", 1), _set("10", 2), _set("a", 3), _set("2", 4), {"type": "delete", "key": "b"}, _set("b", 5)],
+    ]
+    cases, want = [], []
+    for msgs in cases_msgs:
+        b = _map_batch(msgs)
+        slots, _ = orc.map_replay(b)
+        live = sorted((int(s["birth_seq"]), k, int(s["value"])) for k, s in enumerate(slots[0])
+                      if int(s["value"]) != summary.MAP_ABSENT)
+        cases.append({"kind": "map", "entries": [[b.keys[k], None if v == summary.MAP_VALUE_UNDEFINED else b.values[v]]
+                                                 for _, k, v in live]})
+        want.append(orc.map_summary(b, 0))
+    got = _run(cases, tmp_path)
+    for g, (header, blobs) in zip(got, want):
+        assert g["header"] == header and g["blobs"] == blobs
+    assert got[0]["header"] == '{"blobs":[],"content":{"key":{"type":"Plain","value":"value"}}}'
+
+
+def test_js_string_and_catchup_blobs_match_python_host(orc, tmp_path):
+    batch, _ = fixture_batch()
+    rc, h, leaves, chars, props, _, cu = orc.mt_replay_batch(batch, cap_catchup=CAP)
+    assert rc == 0
+    cases, want = [], []
+    for d in range(batch.n_docs):
+        n = int(h[d]["n_leaves"])
+        ranges = cu[d][: h[d]["n_catchup"]]
+        cases.append({
+            "kind": "string", "segs": _segs(leaves[d][:n], chars[d], props[d]), "minSeq": int(h[d]["min_seq"]),
+            "keys": batch.keys, "values": batch.values,
+            "messages": [{"message": m, "firstOp": f, "count": c} for m, f, c in batch.messages[d]],
+            "ranges": [{k: int(r[k]) for k in ("op", "pos1", "pos2", "type")} for r in ranges],
+        })
+        head, body = summary.legacy_summary(h[d], leaves[d], chars[d], props[d], batch.keys, batch.values)
+        msgs = summary.catchup_messages(batch.messages[d], ranges, int(h[d]["min_seq"]))
+        want.append((head, body, summary.catchup_blob(msgs)))
+    got = _run(cases, tmp_path)
+    for d, (g, (head, body, blob)) in enumerate(zip(got, want)):
+        assert g["header"] == head and g["body"] == body, d
+        assert blob is not None and g["catchupOps"] == blob, d

@@ -5,7 +5,8 @@ rejects with FMT_E_DEVICE; the JavaScript packer produces byte-identical records
 the reference's replay fixtures (tests/golden/replay_msgs_0.40.json.gz, the messages
 client.replay.spec.ts:20-76 replays).
 GPU: every checkpoint of those fixtures replayed from JavaScript through the addon matches the
-fixture's resultText; a SharedMap bunch replay gives the LWW entries in JS Map order.
+fixture's resultText; summarize() from GPU state (legacy blobs + catch-up ops) equals the Python
+host's; a SharedMap bunch replay gives the LWW entries in JS Map order and its summary.
 """
 import gzip
 import json
@@ -43,9 +44,10 @@ def test_addon_exports(addon):
                     "console.log(JSON.stringify({k:Object.keys(a).sort(),s:a.sizes,c:a.capacity()}))")
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
-    assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree",
+    assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
                                "replayMap", "fetchDoc", "sizes"])
-    assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 20, "mapSlot": 8}
+    assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 20, "mapSlot": 8,
+                        "catchupRange": 16}
     assert out["c"]["leaves"] >= 512
 
 
@@ -119,3 +121,24 @@ def test_js_map_bunches_on_gpu(addon):
     assert out["doc0"] == [["a", "y"], ["b", {"n": [1, 2]}]]
     assert out["doc1"] == [["c", True]]
     assert out["a0"] == "y"
+    assert out["summary0"] == ('{"blobs":[],"content":{"a":{"type":"Plain","value":"y"},'
+                               '"b":{"type":"Plain","value":{"n":[1,2]}}}}')
+
+
+@pytest.mark.gpu
+def test_js_legacy_summaries_with_catchup_on_gpu(addon, orc):
+    """summarize() from GPU state through the addon == the Python host over the oracle's state."""
+    from fluidframework_amd import summary
+    from test_catchup import CAP, fixture_batch
+
+    r = _node(DRIVER, "summary", timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    batch, _ = fixture_batch()
+    rc, h, leaves, chars, props, _, cu = orc.mt_replay_batch(batch, cap_catchup=CAP)
+    assert rc == 0 and len(got) == batch.n_docs
+    for d in range(batch.n_docs):
+        head, body = summary.legacy_summary(h[d], leaves[d], chars[d], props[d], batch.keys, batch.values)
+        msgs = summary.catchup_messages(batch.messages[d], cu[d][: h[d]["n_catchup"]], int(h[d]["min_seq"]))
+        assert got[d]["header"] == head and got[d]["body"] == body, d
+        assert got[d]["catchupOps"] == summary.catchup_blob(msgs), d
