@@ -23,6 +23,8 @@ struct MtDeviceBatch {
   const uint32_t* propsKv;
   uint32_t nPropsOps;
   const uint64_t* catchupOffsets;  // per-doc catch-up slab offsets (nDocs + 1), or nullptr
+  const fmt_mt_snapshot_doc* snapshots;  // per-doc summary loads, or nullptr
+  const fmt_mt_snapshot_seg* snapshotSegs;
 };
 
 struct MtDeviceOut {

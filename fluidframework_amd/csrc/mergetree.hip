@@ -36,6 +36,20 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
     in.propsOff = batch.propsOff;
     in.propsKv = batch.propsKv;
     in.nPropsOps = batch.nPropsOps;
+    if (batch.snapshots && batch.snapshots[d].loaded) {
+      const fmt_mt_snapshot_doc sd = batch.snapshots[d];
+      in.snapSegs = batch.snapshotSegs + sd.first_seg;
+      in.nHeader = sd.n_header;
+      in.nBody = sd.n_body;
+      in.snapMinSeq = sd.min_seq;
+      in.snapSeq = sd.seq;
+      in.loaded = 1;
+    } else {
+      in.snapSegs = nullptr;
+      in.nHeader = in.nBody = 0;
+      in.snapMinSeq = in.snapSeq = 0;
+      in.loaded = 0;
+    }
     fmt_mt::DocOutputs o;
     o.header = out.headers + d;
     o.leaves = out.leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;

@@ -104,6 +104,10 @@ struct DocInputs {
   const uint32_t* propsOff;
   const uint32_t* propsKv;
   uint32_t nPropsOps;
+  const fmt_mt_snapshot_seg* snapSegs;  // this document's summary segments (loaded != 0)
+  uint32_t nHeader, nBody;
+  int32_t snapMinSeq, snapSeq;
+  uint32_t loaded;
 };
 
 struct DocOutputs {
@@ -1085,6 +1089,142 @@ class Doc {
     waveSync();
   }
 
+  // ------------------------------------------------------------------ snapshot load (f3)
+  // SnapshotLoader (snapshotLoader.ts:59-348) for a legacy summary: the header chunk's segments
+  // rebuild the tree bottom-up, MaxNodesInBlock - 1 = 7 children per block (reloadFromSegments,
+  // mergeTree.ts:751-800); collaboration starts at (minSeq, seq) (loadHeader :189-219); each body
+  // segment is appended through insertSegments at the end (loadBody :221-311), which lands it in the
+  // last leaf's block and splits on overflow. Every loaded segment is stamped
+  // {UniversalSequenceNumber, NonCollabClient} (specToSegment :180-186). Runs right after init(),
+  // so block ids are handed out in order: level by level, leaf blocks first.
+  FMT_DEV void appendLoadedChars(uint32_t off, uint32_t len) {
+    FOR_LANES(l) {
+      for (uint32_t t = l; t < len; t += 64) s->chars[nChars + static_cast<int>(t)] = in.text[off + t];
+    }
+    waveSync();
+    nChars += static_cast<int>(len);
+  }
+
+  // Properties of the loaded leaves [first, last) whose row bits are set in `pending`: one interned
+  // prop set per distinct props op (a spec's props applied onto undefined properties).
+  FMT_DEV void loadProps(int first, int last) {
+    FOR_ROWS(r, first >> 6, (last + 63) >> 6) {
+      Lane<uint32_t> op;
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        LANE(op) = j >= first && j < last ? in.snapSegs[j].props : FMT_MT_NO_PROPS;
+      }
+      for (;;) {
+        Lane<bool> p;
+        FOR_LANES(l) { LANE(p) = LANE(op) != FMT_MT_NO_PROPS; }
+        const uint64_t m = ballot(p);
+        if (m == 0) break;
+        const uint32_t id = readlane(op, ctz64(m));
+        if (id >= in.nPropsOps) {
+          fail(FMT_E_DATA);
+          return;
+        }
+        const uint32_t pid = applyProps(kPropsUndef, id);
+        if (status != FMT_OK) return;
+        FOR_LANES(l) {
+          if (LANE(op) == id) {
+            const uint32_t w0 = LANE(W[0])[r];
+            LANE(W[0])[r] = mkW0(fLen(w0), fBlk(w0), pid);
+            LANE(op) = FMT_MT_NO_PROPS;
+          }
+        }
+      }
+    }
+  }
+
+  FMT_DEV void loadSnapshot() {
+    const int H = static_cast<int>(in.nHeader), N = static_cast<int>(in.nHeader + in.nBody);
+    if (N > kCapLeaves) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    uint32_t chars = 0;
+    for (int k = 0; k < N; k++) {
+      const uint32_t len = uni(in.snapSegs[k].len);
+      if (len == 0) {
+        fail(FMT_E_DATA);
+        return;
+      }
+      chars += len;
+    }
+    if (chars > static_cast<uint32_t>(kCapChars)) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    // Every loaded leaf in one row pass (lengths staged through the still-unused char area); slots
+    // past N stay all-zero. Header leaf j belongs to leaf block j / 7, body leaves get theirs below.
+    uint32_t* stage = reinterpret_cast<uint32_t*>(s->chars);
+    FOR_LANES(l) {
+      for (int j = l; j < N; j += 64) stage[j] = in.snapSegs[j].len;
+    }
+    waveSync();
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        const bool live = j < N;
+        LANE(W[0])[r] = live ? mkW0(stage[j], static_cast<uint32_t>(j < H ? j / 7 : 0), kPropsUndef) : 0u;
+        LANE(W[2])[r] = live ? static_cast<uint32_t>(kNotRemoved) : 0u;
+        LANE(W[4])[r] = live ? mkW4(static_cast<uint32_t>(j + 1), FMT_NON_COLLAB_CLIENT) : 0u;
+      }
+    }
+    waveSync();
+    nextId = static_cast<uint32_t>(N + 1);
+    if (H > 0) {  // reloadFromSegments: leaf blocks [0, cnt), then each level above
+      int lo = 0, cnt = (H + 6) / 7;
+      for (int b = 0; b < cnt; b++) {
+        s->blk[b].count = static_cast<uint8_t>(H - 7 * b < 7 ? H - 7 * b : 7);
+        s->blk[b].parent = static_cast<uint8_t>(kNoBlk);
+        s->blk[b].leaf = 1;
+        s->blk[b].needsScour = -1;
+      }
+      waveSync();
+      while (cnt > 1) {
+        const int nb = (cnt + 6) / 7, nlo = lo + cnt;
+        for (int q = 0; q < nb; q++) {
+          const int id = nlo + q;
+          const int c = cnt - 7 * q < 7 ? cnt - 7 * q : 7;
+          s->blk[id].count = static_cast<uint8_t>(c);
+          s->blk[id].parent = static_cast<uint8_t>(kNoBlk);
+          s->blk[id].leaf = 0;
+          s->blk[id].needsScour = -1;
+          for (int k = 0; k < c; k++) {
+            s->blk[id].child[k] = static_cast<uint8_t>(lo + 7 * q + k);
+            s->blk[lo + 7 * q + k].parent = static_cast<uint8_t>(id);
+          }
+        }
+        waveSync();
+        lo = nlo;
+        cnt = nb;
+      }
+      root = lo;
+      nFree = kMaxBlocks - (lo + 1);  // the free list hands out ids in increasing order
+    }
+    n = H;
+    minSeq = in.snapMinSeq;  // loadHeader: startOrUpdateCollaboration(minSeq, seq)
+    curSeq = in.snapSeq;
+    // loadBody: each body segment goes through the inserting walk at the end, which puts it in the
+    // last leaf's block (the empty root when there is no header) and splits on overflow
+    for (int k = H; k < N; k++) {
+      const int blk = n > 0 ? static_cast<int>(fBlk(readField(n - 1, 0))) : root;
+      if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
+        s->blk[blk].leaf = 1;
+        waveSync();
+      }
+      tagLeaves(k, 1, static_cast<uint32_t>(blk));
+      n++;
+      childAdded(blk);
+      if (status != FMT_OK) return;
+    }
+    loadProps(0, N);
+    for (int k = 0; k < N && status == FMT_OK; k++) appendLoadedChars(uni(in.snapSegs[k].text), uni(in.snapSegs[k].len));
+  }
+
   // Op records are prefetched two ahead (lanes 0..7 hold the eight dwords of one fmt_mt_op) and
   // an insert's first 64 text units one op ahead, so the global-load latency of the dependent op
   // stream overlaps the previous op's work.
@@ -1203,7 +1343,7 @@ class Doc {
           L.rm_seq = static_cast<int32_t>(LANE(W[2])[r]);
           L.rm_clients = LANE(W[3])[r];
           L.char_off = LANE(cst)[r];
-          L.len = static_cast<uint16_t>(fLen(w0));
+          L.len = fLen(w0);
           L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[r]));
           L.props = fProps(w0) == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(fProps(w0));
           L.block = static_cast<uint16_t>(LANE(ord)[r] + LANE(startFlag)[r] - 1u);
@@ -1255,7 +1395,8 @@ class Doc {
     cuCap = out.catchup ? out.catchupCap : 0u;
     cuN = 0;
     init();
-    loadInitial();
+    if (in.loaded) loadSnapshot();
+    else loadInitial();
     if (status == FMT_OK) replay();
     writeOutputs(out);
     stamp(kPfOutput);

@@ -68,6 +68,9 @@ struct fmt_ctx {
   DevBuf<fmt_mt_leaf> mtLeaves;
   DevBuf<uint16_t> mtChars;
   DevBuf<fmt_mt_propset> mtProps;
+  DevBuf<fmt_mt_snapshot_doc> mtSnap;       // per-doc summary loads (f3)
+  DevBuf<fmt_mt_snapshot_seg> mtSnapSegs;
+  bool mtHasSnap = false;
   DevBuf<uint64_t> mtCuOffs;                 // per-doc catch-up slab offsets (n_docs + 1)
   DevBuf<fmt_mt_catchup_range> mtCatchup;    // catch-up range slabs
   std::vector<uint64_t> mtCuOffsHost;
@@ -283,6 +286,22 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       return setErr(c, FMT_E_UNSUPPORTED, "op type not supported by this engine build");
     }
   }
+  if (b->snapshots) {
+    for (uint32_t d = 0; d < n; d++) {
+      const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+      if (!sd.loaded) continue;
+      if (b->snapshot_segs == nullptr || sd.first_seg + sd.n_header + sd.n_body > b->n_snapshot_segs)
+        return setErr(c, FMT_E_USAGE, "snapshot segments out of range");
+      for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++) {
+        const fmt_mt_snapshot_seg& sg = b->snapshot_segs[k];
+        if (static_cast<uint64_t>(sg.text) + sg.len > b->text_len)
+          return setErr(c, FMT_E_DATA, "snapshot segment text outside the text arena");
+        if (sg.props != FMT_MT_NO_PROPS && sg.props >= b->n_props_ops)
+          return setErr(c, FMT_E_DATA, "snapshot segment props op id out of range");
+        insertChars += sg.len;
+      }
+    }
+  }
   uint64_t initChars = 0;
   if (b->doc_init) {
     for (uint32_t d = 0; d < n; d++) {
@@ -326,6 +345,13 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, cp(c->mtOffs.p, b->doc_op_offsets, (n + 1ull) * sizeof(uint64_t)));
   FMT_HIP(c, cp(c->mtText.p, b->text, b->text_len * sizeof(uint16_t)));
   if (b->doc_init) FMT_HIP(c, cp(c->mtInit.p, b->doc_init, 2ull * n * sizeof(uint32_t)));
+  c->mtHasSnap = b->snapshots != nullptr;
+  if (c->mtHasSnap) {
+    FMT_HIP(c, c->mtSnap.reserve(n));
+    FMT_HIP(c, c->mtSnapSegs.reserve(b->n_snapshot_segs));
+    FMT_HIP(c, cp(c->mtSnap.p, b->snapshots, n * sizeof(fmt_mt_snapshot_doc)));
+    FMT_HIP(c, cp(c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg)));
+  }
   if (c->mtHasCatchup) FMT_HIP(c, cp(c->mtCuOffs.p, c->mtCuOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
   if (b->props_off) {
     FMT_HIP(c, cp(c->mtPropsOff.p, b->props_off, (b->n_props_ops + 1ull) * sizeof(uint32_t)));
@@ -350,7 +376,8 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipSetDevice(c->device));
   fmt_kernels::MtDeviceBatch db{c->mtOps.p, c->mtOffs.p, c->mtDocs, c->mtText.p,
                                 c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps,
-                                c->mtHasCatchup ? c->mtCuOffs.p : nullptr};
+                                c->mtHasCatchup ? c->mtCuOffs.p : nullptr,
+                                c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr};
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr};
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));

@@ -24,7 +24,8 @@ const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2;
 const MAX_CLIENTS = 63;
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 20;
-const CATCHUP_BYTES = 16;
+const CATCHUP_BYTES = 16, SNAPSHOT_DOC_BYTES = 32;
+const NO_PROPS = 0xffffffff;
 const PROPS_MAX = 4;
 
 let addon = null;
@@ -179,13 +180,70 @@ class MergeTreeStreamBuilder {
 		this.propsList = [];
 		this.docs = [];
 		this.docInit = [];
+		this.snapshots = []; // per doc: null or [firstSeg, nHeader, nBody, minSeq, seq]
+		this.snapshotSegs = []; // [textOff, len, propsOp]
 		this.current = null;
 	}
 	beginDoc(initialText, observer) {
 		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "A" : observer);
 		this.docs.push(d);
 		this.docInit.push(initialText ? this.text.push(initialText) : [0, 0]);
+		this.snapshots.push(null);
 		this.current = d;
+		return d;
+	}
+	/** specToSegment for a text spec: "text" or {text, props} (IJSONTextSegment). */
+	specToSeg(spec) {
+		let text, props;
+		if (typeof spec === "string") {
+			text = spec;
+		} else if (spec && typeof spec === "object" && typeof spec.text === "string" &&
+			Object.keys(spec).every((k) => k === "text" || k === "props")) {
+			text = spec.text;
+			props = spec.props;
+		} else {
+			throw new UnsupportedOp("markers and segments with merge info (SnapshotV1) are not loaded");
+		}
+		if (text.length === 0) throw new Error("empty segment in a summary chunk");
+		const [off, len] = this.text.push(text);
+		this.snapshotSegs.push([off, len, props && Object.keys(props).length ? this.propsOp(props) : NO_PROPS]);
+	}
+	/**
+	 * A document that starts from a legacy SharedString summary (SnapshotLoader,
+	 * snapshotLoader.ts:59-348): header/body chunk blobs and optionally the catchupOps blob, whose
+	 * messages become the first ops after loadCore's validation (sequence.ts:818-863).
+	 */
+	beginDocFromSummary(header, body, catchupOps, observer) {
+		const h = JSON.parse(header);
+		const md = h.headerMetadata;
+		if (md === undefined) throw new Error("header metadata not available");
+		const chunks = [h];
+		if (body !== undefined && body !== null) chunks.push(JSON.parse(body));
+		if (md.orderedChunkMetadata.length !== chunks.length) {
+			throw new Error("summary chunks do not match headerMetadata.orderedChunkMetadata");
+		}
+		const first = this.snapshotSegs.length;
+		for (const c of chunks) for (const spec of c.segmentTexts) this.specToSeg(spec);
+		const nHeader = h.segmentTexts.length, nBody = this.snapshotSegs.length - first - nHeader;
+		if (nHeader + nBody !== md.totalSegmentCount) throw new Error("Mismatch in totalSegmentCount");
+		const seq = md.sequenceNumber;
+		const minSeq = md.minSequenceNumber === undefined ? seq : md.minSequenceNumber;
+		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "snapshot" : observer);
+		this.docs.push(d);
+		this.docInit.push([0, 0]);
+		this.snapshots.push([first, nHeader, nBody, minSeq, seq]);
+		this.current = d;
+		if (catchupOps !== undefined && catchupOps !== null) {
+			let cur = seq;
+			for (const m of JSON.parse(catchupOps)) {
+				if (m.minimumSequenceNumber < minSeq || m.referenceSequenceNumber < minSeq ||
+					m.sequenceNumber <= minSeq || m.sequenceNumber < cur) {
+					throw new Error("Invalid catchup operations in snapshot");
+				}
+				cur = m.sequenceNumber;
+				d.addMessage(m);
+			}
+		}
 		return d;
 	}
 	propsOp(props) {
@@ -285,9 +343,27 @@ class MergeTreeStreamBuilder {
 			docInit[2 * k] = p[0];
 			docInit[2 * k + 1] = p[1];
 		});
+		let snapshots, snapshotSegs;
+		if (this.snapshots.some((x) => x !== null)) {
+			snapshots = new ArrayBuffer(this.docs.length * SNAPSHOT_DOC_BYTES);
+			const sv = new DataView(snapshots);
+			this.snapshots.forEach((x, k) => {
+				if (x === null) return;
+				const o = k * SNAPSHOT_DOC_BYTES;
+				sv.setBigUint64(o, BigInt(x[0]), true);
+				sv.setUint32(o + 8, x[1], true);
+				sv.setUint32(o + 12, x[2], true);
+				sv.setInt32(o + 16, x[3], true);
+				sv.setInt32(o + 20, x[4], true);
+				sv.setUint32(o + 24, 1, true);
+			});
+			snapshotSegs = Uint32Array.from([].concat(...this.snapshotSegs));
+		}
 		return {
 			ops: this.ops.bytes(),
 			docOpOffsets: offs,
+			snapshots,
+			snapshotSegs,
 			text: this.text.finish(),
 			docInit,
 			propsOff,
@@ -434,13 +510,13 @@ class MergeTreeReplay {
 		const segs = [];
 		for (let i = 0; i < h.nLeaves; i++) {
 			const o = i * LEAF_BYTES;
-			const off = lv.getUint32(o + 16, true), len = lv.getUint16(o + 20, true);
-			const pid = lv.getUint16(o + 24, true);
+			const off = lv.getUint32(o + 16, true), len = lv.getUint32(o + 20, true);
+			const pid = lv.getUint16(o + 26, true);
 			const rm = lv.getInt32(o + 4, true);
 			segs.push({
 				insertSeq: lv.getInt32(o, true),
 				removedSeq: rm === NOT_REMOVED ? undefined : rm,
-				insertClient: lv.getInt16(o + 22, true),
+				insertClient: lv.getInt16(o + 24, true),
 				text: String.fromCharCode.apply(null, chars.subarray(off, off + len)),
 				properties: pid === 0xffff ? undefined : props[pid],
 				kv: pid === 0xffff ? null : kvs[pid],

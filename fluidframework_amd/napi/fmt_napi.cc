@@ -317,7 +317,7 @@ napi_value queue(napi_env env, Job* j, napi_value ctx_val, const char* name) {
   return promise;
 }
 
-// replayMergeTree(ctx, {ops, docOpOffsets, text, docInit, propsOff, propsKv})
+// replayMergeTree(ctx, {ops, docOpOffsets, text, docInit, propsOff, propsKv, snapshots?, snapshotSegs?})
 napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -357,6 +357,26 @@ napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
   j->mt.props_off = static_cast<const uint32_t*>(d[4]);
   j->mt.n_props_ops = uint32_t(n[4] / 4 - 1);
   j->mt.props_kv = static_cast<const uint32_t*>(d[5]);
+  // optional summary loads (f3): snapshots (fmt_mt_snapshot_doc per doc) + snapshotSegs
+  void *sd, *ss;
+  size_t nsd, nss;
+  if (!get_bytes(env, prop(env, b, "snapshots"), "snapshots", &sd, &nsd) ||
+      !get_bytes(env, prop(env, b, "snapshotSegs"), "snapshotSegs", &ss, &nss)) {
+    delete j;
+    return nullptr;
+  }
+  if (sd != nullptr) {
+    if (nsd != size_t(n_docs) * sizeof(fmt_mt_snapshot_doc) || nss % sizeof(fmt_mt_snapshot_seg)) {
+      delete j;
+      throw_fmt(env, FMT_E_USAGE, "replayMergeTree: snapshots must hold one fmt_mt_snapshot_doc per document");
+      return nullptr;
+    }
+    j->mt.snapshots = static_cast<const fmt_mt_snapshot_doc*>(sd);
+    j->mt.snapshot_segs = static_cast<const fmt_mt_snapshot_seg*>(ss);
+    j->mt.n_snapshot_segs = nss / sizeof(fmt_mt_snapshot_seg);
+    keep_array(env, j, prop(env, b, "snapshots"));
+    keep_array(env, j, prop(env, b, "snapshotSegs"));
+  }
   for (int i = 0; i < 6; ++i) keep_array(env, j, prop(env, b, names[i]));
   return queue(env, j, argv[0], "fmtReplayMergeTree");
 }

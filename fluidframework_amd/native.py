@@ -23,11 +23,11 @@ LEAF_DTYPE = np.dtype(
         ("rm_seq", "<i4"),
         ("rm_clients", "<u8"),
         ("char_off", "<u4"),
-        ("len", "<u2"),
+        ("len", "<u4"),
         ("ins_client", "<i2"),
         ("props", "<u2"),
         ("block", "<u2"),
-        ("pad", "<u4"),
+        ("pad", "<u2"),
     ]
 )
 assert LEAF_DTYPE.itemsize == 32
@@ -52,6 +52,8 @@ assert DOC_RESULT_DTYPE.itemsize == 48
 
 CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("type", "<u4")])
 
+from .streams import SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE  # noqa: E402  (include/fmt.h layouts)
+
 PROPS_MAX = 4
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
 assert PROPSET_DTYPE.itemsize == 20
@@ -71,6 +73,9 @@ class FmtMtBatch(ctypes.Structure):
         ("props_off", ctypes.c_void_p),
         ("n_props_ops", ctypes.c_uint32),
         ("props_kv", ctypes.c_void_p),
+        ("snapshots", ctypes.c_void_p),
+        ("snapshot_segs", ctypes.c_void_p),
+        ("n_snapshot_segs", ctypes.c_uint64),
     ]
 
 
@@ -109,9 +114,17 @@ def batch_struct(batch):
         np.ascontiguousarray(batch.props_off, dtype=np.uint32),
         np.ascontiguousarray(batch.props_kv, dtype=np.uint32) if len(batch.props_kv) else np.zeros(1, np.uint32),
     ]
+    snaps = getattr(batch, "snapshots", None)
+    segs = getattr(batch, "snapshot_segs", None)
+    if snaps is not None:
+        keep.append(np.ascontiguousarray(snaps, dtype=SNAPSHOT_DOC_DTYPE))
+        keep.append(np.ascontiguousarray(segs, dtype=SNAPSHOT_SEG_DTYPE) if len(segs) else
+                    np.zeros(1, dtype=SNAPSHOT_SEG_DTYPE))
     b = FmtMtBatch(
         _ptr(keep[0]), len(keep[0]), _ptr(keep[1]), len(keep[1]) - 1, _ptr(keep[2]), len(keep[2]),
         _ptr(keep[3]), _ptr(keep[4]), len(keep[4]) - 1, _ptr(keep[5]),
+        _ptr(keep[6]) if snaps is not None else None, _ptr(keep[7]) if snaps is not None else None,
+        len(segs) if snaps is not None else 0,
     )
     return b, keep
 

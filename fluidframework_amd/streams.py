@@ -39,6 +39,14 @@ MT_OP_DTYPE = np.dtype(
 )
 assert MT_OP_DTYPE.itemsize == 32
 
+# include/fmt.h fmt_mt_snapshot_doc (32 bytes) / fmt_mt_snapshot_seg (12 bytes)
+SNAPSHOT_DOC_DTYPE = np.dtype([("first_seg", "<u8"), ("n_header", "<u4"), ("n_body", "<u4"),
+                               ("min_seq", "<i4"), ("seq", "<i4"), ("loaded", "<u4"), ("pad", "<u4")])
+assert SNAPSHOT_DOC_DTYPE.itemsize == 32
+SNAPSHOT_SEG_DTYPE = np.dtype([("text", "<u4"), ("len", "<u4"), ("props", "<u4")])
+assert SNAPSHOT_SEG_DTYPE.itemsize == 12
+NO_PROPS = 0xFFFFFFFF
+
 # include/fmt.h fmt_map_op (16 bytes)
 MAP_OP_DTYPE = np.dtype([("doc", "<u4"), ("key", "<u4"), ("seq", "<u4"), ("kind_value", "<u4")])
 assert MAP_OP_DTYPE.itemsize == 16
@@ -123,6 +131,9 @@ class MergeTreeBatch:
     # per doc (only with keep_messages): [(message dict as applyMsg received it, first op index in
     # the doc, member op count)] — what SharedSegmentSequence stashes for catch-up ops
     messages: list = field(default_factory=list)
+    # optional (f3): per-doc fmt_mt_snapshot_doc and the segment specs they index
+    snapshots: np.ndarray | None = None
+    snapshot_segs: np.ndarray | None = None
 
     @property
     def n_docs(self) -> int:
@@ -187,6 +198,8 @@ class MergeTreeStreamBuilder:
         self.props_list: list[tuple] = []
         self.docs: list[_DocBuilder] = []
         self.doc_init: list[tuple] = []
+        self.snapshots: list[tuple] = []  # per doc: (first_seg, n_header, n_body, min_seq, seq, loaded)
+        self.snapshot_segs: list[tuple] = []
 
     def _text(self, s: str) -> tuple:
         u = utf16(s)
@@ -242,6 +255,57 @@ class MergeTreeStreamBuilder:
         d = _DocBuilder(self, observer)
         self.docs.append(d)
         self.doc_init.append(self._text(initial_text) if initial_text else (0, 0))
+        self.snapshots.append((0, 0, 0, 0, 0, 0))
+        return d
+
+    def _spec(self, spec) -> tuple:
+        """specToSegment for a text segment spec: "text" or {"text", "props"} (IJSONTextSegment)."""
+        if isinstance(spec, str):
+            text, props = spec, None
+        elif isinstance(spec, dict) and "text" in spec and set(spec) <= {"text", "props"}:
+            text, props = spec["text"], spec.get("props")
+        else:
+            raise UnsupportedOp("markers and segments with merge info (SnapshotV1) are not loaded")
+        off, n = self._text(text)
+        if n == 0:
+            raise ValueError("empty segment in a summary chunk")
+        return (off, n, self._props_op(props) if props else NO_PROPS)
+
+    def begin_doc_from_summary(self, header: str, body: str | None = None, catchup_ops: str | None = None,
+                               observer: str = "snapshot") -> _DocBuilder:
+        """A document that starts from a legacy SharedString summary (SnapshotLoader, snapshotLoader.ts:
+        59-348): the header/body chunk blobs and, optionally, the catchupOps blob, whose messages are
+        added as the first ops after validation as SharedSegmentSequence.loadCore does (sequence.ts:
+        818-863). The loading client is `observer` (short id 0)."""
+        h = json.loads(header)
+        md = h.get("headerMetadata")
+        if md is None:
+            raise ValueError("header metadata not available")
+        chunks = [h] + ([json.loads(body)] if body is not None else [])
+        if len(md["orderedChunkMetadata"]) != len(chunks):
+            raise ValueError("summary chunks do not match headerMetadata.orderedChunkMetadata")
+        first = len(self.snapshot_segs)
+        for c in chunks:
+            for spec in c["segmentTexts"]:
+                self.snapshot_segs.append(self._spec(spec))
+        n_header = len(h["segmentTexts"])
+        n_body = len(self.snapshot_segs) - first - n_header
+        if n_header + n_body != md["totalSegmentCount"]:
+            raise ValueError("Mismatch in totalSegmentCount")  # snapshotLoader.ts:272-275
+        seq = int(md["sequenceNumber"])
+        min_seq = int(md.get("minSequenceNumber", seq))
+        d = _DocBuilder(self, observer)
+        self.docs.append(d)
+        self.doc_init.append((0, 0))
+        self.snapshots.append((first, n_header, n_body, min_seq, seq, 1))
+        if catchup_ops is not None:
+            cur = seq
+            for m in json.loads(catchup_ops):
+                if (m["minimumSequenceNumber"] < min_seq or m["referenceSequenceNumber"] < min_seq
+                        or m["sequenceNumber"] <= min_seq or m["sequenceNumber"] < cur):
+                    raise ValueError("Invalid catchup operations in snapshot")  # sequence.ts:838-858
+                cur = m["sequenceNumber"]
+                d.add_message(m)
         return d
 
     def finish(self, catchup: bool = False) -> MergeTreeBatch:
@@ -275,7 +339,18 @@ class MergeTreeStreamBuilder:
             values=list(self.values.items),
             clients=[list(d.client_names) for d in self.docs],
             messages=[list(d.messages) for d in self.docs] if self.keep_messages else [],
+            snapshots=_snapshot_array(self.snapshots),
+            snapshot_segs=np.array(self.snapshot_segs, dtype=SNAPSHOT_SEG_DTYPE),
         )
+
+
+def _snapshot_array(rows) -> np.ndarray | None:
+    if not any(r[5] for r in rows):
+        return None
+    a = np.zeros(len(rows), dtype=SNAPSHOT_DOC_DTYPE)
+    for i, (first, nh, nb, msn, seq, loaded) in enumerate(rows):
+        a[i] = (first, nh, nb, msn, seq, loaded, 0)
+    return a
 
 
 def flag_catchup(ops: np.ndarray, offs: np.ndarray) -> None:

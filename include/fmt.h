@@ -109,6 +109,30 @@ typedef struct fmt_map_op {
   uint32_t kind_value; /* (kind << 30) | value id */
 } fmt_map_op;
 
+/* A document that starts from a loaded legacy SharedString summary instead of an empty tree
+ * (SnapshotLoader, merge-tree/src/snapshotLoader.ts:59-348): the header chunk's segments rebuild
+ * the tree 7 per block (reloadFromSegments, mergeTree.ts:751-800), collaboration starts at
+ * (min_seq, seq) from the header metadata, and the body chunk's segments are appended through the
+ * inserting walk with stamp {UniversalSequenceNumber, NonCollabClient} (snapshotLoader.ts:221-311).
+ * Catch-up messages follow as ordinary ops. 32 bytes. */
+typedef struct fmt_mt_snapshot_doc {
+  uint64_t first_seg; /* index of the document's first fmt_mt_snapshot_seg */
+  uint32_t n_header;  /* segments of the header chunk */
+  uint32_t n_body;    /* segments of the body chunk(s), appended after loading the header */
+  int32_t min_seq;    /* headerMetadata.minSequenceNumber ?? sequenceNumber */
+  int32_t seq;        /* headerMetadata.sequenceNumber */
+  uint32_t loaded;    /* 0: this document does not start from a snapshot (doc_init applies) */
+  uint32_t pad;
+} fmt_mt_snapshot_doc;
+
+#define FMT_MT_NO_PROPS 0xffffffffu
+/* One segment spec of a summary chunk ("text" or {"text","props"}, IJSONTextSegment). 12 bytes. */
+typedef struct fmt_mt_snapshot_seg {
+  uint32_t text;  /* offset of the text in the UTF-16 arena */
+  uint32_t len;   /* UTF-16 units (> 0) */
+  uint32_t props; /* props-op id whose (key, value) pairs are the segment's properties, or FMT_MT_NO_PROPS */
+} fmt_mt_snapshot_seg;
+
 /* A batch of merge-tree documents. Pointers are HOST pointers for fmt_mt_load(). */
 typedef struct fmt_mt_batch {
   const fmt_mt_op* ops;           /* all ops, documents contiguous and in seq order */
@@ -122,6 +146,9 @@ typedef struct fmt_mt_batch {
   const uint32_t* props_off;      /* annotate props-op table: n_props_ops + 1 offsets into props_kv */
   uint32_t n_props_ops;
   const uint32_t* props_kv;       /* (key_id << 16) | value_id; value_id 0 = null (delete key) */
+  const fmt_mt_snapshot_doc* snapshots;   /* optional: n_docs entries, or NULL (f3: load from summary) */
+  const fmt_mt_snapshot_seg* snapshot_segs;
+  uint64_t n_snapshot_segs;
 } fmt_mt_batch;
 
 /* ---------------------------------------------------------------------------------------------
@@ -134,11 +161,11 @@ typedef struct fmt_mt_leaf {
   int32_t rm_seq;      /* first (lowest) remove stamp seq, FMT_NOT_REMOVED if not removed */
   uint64_t rm_clients; /* set of short client ids holding a remove stamp on this leaf */
   uint32_t char_off;   /* offset of this leaf's text in the document's char output */
-  uint16_t len;        /* cachedLength (UTF-16 units) */
+  uint32_t len;        /* cachedLength (UTF-16 units) */
   int16_t ins_client;  /* insert stamp client */
   uint16_t props;      /* document-local prop-set id, 0xffff = properties undefined */
   uint16_t block;      /* index of the leaf's parent block in document order of leaf blocks */
-  uint32_t pad;
+  uint16_t pad;
 } fmt_mt_leaf;
 
 /* Per-document result header. */

@@ -74,7 +74,7 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
         if (r.client >= 0 && r.client < 64) mask |= 1ull << r.client;
       L.rm_clients = mask;
       L.char_off = charOff;
-      L.len = static_cast<uint16_t>(s->len());
+      L.len = static_cast<uint32_t>(s->len());
       L.props = pid;
       L.block = static_cast<uint16_t>(blockOf[i]);
     }
@@ -208,11 +208,28 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
     const size_t i = d - docBegin;
     int32_t failSeq = 0;
     int st = FMT_OK;
-    if (b->doc_init != nullptr && b->doc_init[2 * d + 1] > 0) {
-      const uint32_t off = b->doc_init[2 * d], len = b->doc_init[2 * d + 1];
-      mt.insertLocal(0, std::u16string(reinterpret_cast<const char16_t*>(b->text + off), len));
+    if (b->snapshots != nullptr && b->snapshots[d].loaded) {
+      const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+      std::vector<MergeTree::LoadedSeg> head, body;
+      for (uint32_t k = 0; k < sd.n_header + sd.n_body; k++) {
+        const fmt_mt_snapshot_seg& sg = b->snapshot_segs[sd.first_seg + k];
+        MergeTree::LoadedSeg l;
+        l.text.assign(reinterpret_cast<const char16_t*>(b->text + sg.text), sg.len);
+        if (sg.props != FMT_MT_NO_PROPS) {
+          l.hasProps = true;
+          for (uint32_t t = b->props_off[sg.props]; t < b->props_off[sg.props + 1]; t++)
+            l.props.emplace_back(static_cast<uint16_t>(b->props_kv[t] >> 16), static_cast<uint16_t>(b->props_kv[t] & 0xffff));
+        }
+        (k < sd.n_header ? head : body).push_back(std::move(l));
+      }
+      mt.loadSnapshot(head, body, sd.min_seq, sd.seq);
+    } else {
+      if (b->doc_init != nullptr && b->doc_init[2 * d + 1] > 0) {
+        const uint32_t off = b->doc_init[2 * d], len = b->doc_init[2 * d + 1];
+        mt.insertLocal(0, std::u16string(reinterpret_cast<const char16_t*>(b->text + off), len));
+      }
+      mt.startCollaboration(0, 0, 0);
     }
-    mt.startCollaboration(0, 0, 0);
     const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
     std::vector<fmt_mt_catchup_range> cu;
     st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq,

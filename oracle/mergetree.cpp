@@ -487,6 +487,57 @@ void MergeTree::removeLocal(int start, int end) {
                    Stamp{collaborating ? kUnassignedSeq : 0, clientId});
 }
 
+void MergeTree::loadSnapshot(const std::vector<LoadedSeg>& header, const std::vector<LoadedSeg>& body,
+                             int minSeqArg, int seqArg) {
+  // specToSegment (snapshotLoader.ts:180-186): a legacy spec is inserted at {0, NonCollabClient};
+  // TextSegment.fromJSONObject adds the spec's props in their key order.
+  auto make = [&](const LoadedSeg& l) {
+    Seg* s = makeSeg();
+    s->text = l.text;
+    s->ins = Stamp{0, kNonCollabClient};
+    if (l.hasProps) {
+      s->props.defined = true;
+      for (const auto& [key, value] : l.props) {
+        auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(),
+                               [&](const auto& e) { return e.first == key; });
+        if (value == 0) {
+          if (it != s->props.kv.end()) s->props.kv.erase(it);
+        } else if (it != s->props.kv.end()) {
+          it->second = value;
+        } else {
+          s->props.kv.emplace_back(key, value);
+        }
+      }
+    }
+    return s;
+  };
+  // reloadFromSegments: bottom-up, MaxNodesInBlock - 1 = 7 children per block, layer by layer.
+  std::vector<Node*> nodes;
+  for (const LoadedSeg& l : header) nodes.push_back(make(l));
+  if (nodes.empty()) {
+    root_ = makeBlock(0);
+  } else {
+    constexpr int maxChildren = kMaxNodesInBlock - 1;
+    for (;;) {
+      std::vector<Node*> blocks;
+      for (size_t i = 0; i < nodes.size();) {
+        Block* b = makeBlock(0);
+        for (int c = 0; c < maxChildren && i < nodes.size(); c++, i++) assignChild(b, nodes[i], b->childCount++);
+        blocks.push_back(b);
+      }
+      if (blocks.size() == 1) {
+        root_ = static_cast<Block*>(blocks[0]);
+        break;
+      }
+      nodes.swap(blocks);
+    }
+  }
+  root_->parent = nullptr;
+  startCollaboration(0, minSeqArg, seqArg);  // loadHeader (snapshotLoader.ts:204-216)
+  const Perspective p{false, 0, kNonCollabClient};
+  for (const LoadedSeg& l : body) insertSegments(getLocalLength(), make(l), p, Stamp{0, kNonCollabClient});
+}
+
 void MergeTree::startCollaboration(int localClientId, int minSeqArg, int currentSeqArg) {
   clientId = localClientId;
   minSeq = minSeqArg;

@@ -134,6 +134,18 @@ class MergeTree {
   int minSeq = 0;
   int currentSeq = 0;
 
+  // A legacy summary chunk's segment spec: text and, when the spec has "props", its properties.
+  struct LoadedSeg {
+    std::u16string text;
+    bool hasProps = false;
+    std::vector<std::pair<uint16_t, uint16_t>> props;
+  };
+  // SnapshotLoader (snapshotLoader.ts:59-348): header segments rebuild the tree
+  // (reloadFromSegments, mergeTree.ts:751-800), collaboration starts at (minSeq, seq), body segments
+  // are appended through insertSegments with stamp {UniversalSequenceNumber, NonCollabClient}.
+  void loadSnapshot(const std::vector<LoadedSeg>& header, const std::vector<LoadedSeg>& body,
+                    int minSeqArg, int seqArg);
+
   // Detached local ops (not collaborating): stamp {seq 0, client -1}, local perspective.
   void insertLocal(int pos, const std::u16string& text);
   void annotateLocal(int start, int end, const std::vector<std::pair<uint16_t, uint16_t>>& props);

@@ -33,6 +33,20 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
     in.propsOff = b->props_off;
     in.propsKv = b->props_kv;
     in.nPropsOps = b->n_props_ops;
+    if (b->snapshots && b->snapshots[d].loaded) {
+      const fmt_mt_snapshot_doc sd = b->snapshots[d];
+      in.snapSegs = b->snapshot_segs + sd.first_seg;
+      in.nHeader = sd.n_header;
+      in.nBody = sd.n_body;
+      in.snapMinSeq = sd.min_seq;
+      in.snapSeq = sd.seq;
+      in.loaded = 1;
+    } else {
+      in.snapSegs = nullptr;
+      in.nHeader = in.nBody = 0;
+      in.snapMinSeq = in.snapSeq = 0;
+      in.loaded = 0;
+    }
     fmt_mt::DocOutputs o;
     o.header = headers + d;
     o.leaves = leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;

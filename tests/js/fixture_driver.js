@@ -126,11 +126,29 @@ async function summaries() {
 	}
 }
 
+/** Pack documents loaded from summaries ([[header, body, catchupOps], ...] in argv[3]) into argv[4]. */
+function packSummaries(input, outdir) {
+	const sums = JSON.parse(fs.readFileSync(input, "utf8"));
+	const b = new fmt.MergeTreeStreamBuilder();
+	for (const [h, body, cu] of sums) b.beginDocFromSummary(h, body, cu);
+	const batch = b.finish();
+	fs.mkdirSync(outdir, { recursive: true });
+	const w = (name, arr) => fs.writeFileSync(path.join(outdir, name),
+		Buffer.from(arr.buffer, arr.byteOffset, arr.byteLength));
+	w("ops.bin", batch.ops);
+	w("text.bin", batch.text);
+	w("snapshots.bin", new Uint8Array(batch.snapshots));
+	w("snapshot_segs.bin", batch.snapshotSegs);
+	w("props_kv.bin", batch.propsKv);
+}
+
 const mode = process.argv[2];
 if (mode === "pack") {
 	pack(process.argv[3]);
 } else if (mode === "replay") {
 	replay().catch((e) => { console.error(e); process.exit(1); });
+} else if (mode === "packsummaries") {
+	packSummaries(process.argv[3], process.argv[4]);
 } else if (mode === "summary") {
 	summaries().catch((e) => { console.error(e); process.exit(1); });
 } else if (mode === "map") {

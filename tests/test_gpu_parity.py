@@ -200,3 +200,19 @@ def test_mt_catchup_ranges_match_oracle(orc, engine):
     for d in range(cf.n_docs):
         n = int(oh[d]["n_catchup"])
         assert n > 0 and np.array_equal(engine.mt_catchup(d, hdrs[d]), ocu[d][:n]), d
+
+
+def test_mt_snapshot_load_matches_oracle(orc, engine):
+    """Documents loaded from legacy summaries (+ catch-up ops) replay bit-exactly vs the oracle."""
+    from test_catchup import fixture_batch
+    from test_snapshot_load import reload_batch, summaries_of
+
+    batch, finals = fixture_batch()
+    rb = reload_batch(summaries_of(orc, batch))
+    hdrs = _check_against_oracle(orc, engine, rb)
+    for d in range(rb.n_docs):
+        leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+        assert visible_text(hdrs[d], leaves, chars) == finals[d]
+    cf = workloads.conflict_farm(256, n_clients=8, ops_per_doc=1500, seed=31)
+    rb = reload_batch(summaries_of(orc, cf, chunk=60, catchup=False), keep_messages=False)
+    _check_against_oracle(orc, engine, rb)

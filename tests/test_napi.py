@@ -102,6 +102,29 @@ console.log(JSON.stringify([v.getUint32(8,true),v.getUint32(24,true),x.keyBound,
     assert json.loads(r.stdout) == [1, 2, 1, ["1"]]
 
 
+def test_js_summary_load_packing_matches_python(addon, orc, tmp_path):
+    """beginDocFromSummary packs legacy summaries (with catch-up blobs) exactly like streams.py."""
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+    from test_snapshot_load import summaries_of
+    from test_catchup import fixture_batch
+
+    batch, _ = fixture_batch()
+    sums = [s[:3] for s in summaries_of(orc, batch)]
+    (tmp_path / "in.json").write_text(json.dumps(sums))
+    r = _node(DRIVER, "packsummaries", str(tmp_path / "in.json"), str(tmp_path / "out"))
+    assert r.returncode == 0, r.stderr
+    b = MergeTreeStreamBuilder()
+    for h, body, cu in sums:
+        b.begin_doc_from_summary(h, body, cu)
+    py = b.finish()
+    out = tmp_path / "out"
+    assert (out / "ops.bin").read_bytes() == py.ops.tobytes()
+    assert (out / "text.bin").read_bytes() == py.text.tobytes()
+    assert (out / "snapshots.bin").read_bytes() == py.snapshots.tobytes()
+    assert (out / "snapshot_segs.bin").read_bytes() == py.snapshot_segs.tobytes()
+    assert (out / "props_kv.bin").read_bytes() == py.props_kv.tobytes()
+
+
 @pytest.mark.gpu
 def test_js_replay_all_fixture_checkpoints_on_gpu(addon):
     r = _node(DRIVER, "replay", timeout=300)
