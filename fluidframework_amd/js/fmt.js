@@ -427,6 +427,24 @@ class MapStreamBuilder {
 		v.setUint32(o + 12, kv, true);
 		this.docOps[doc]++;
 	}
+	/**
+	 * A document whose map starts from a SharedMap summary (SharedMap.loadCore, map.ts:251-267): the
+	 * header's "content" entries, then each blob's, in Object.entries order
+	 * (populateFromSerializable, mapKernel.ts:557-564), packed as the document's first set records.
+	 */
+	beginDocFromSummary(header, blobs) {
+		const doc = this.beginDoc();
+		const h = JSON.parse(header);
+		const parts = Array.isArray(h.blobs) ? [h.content].concat((blobs || []).map((b) => JSON.parse(b))) : [h];
+		for (const part of parts) {
+			for (const [key, ser] of Object.entries(part)) {
+				const value = { type: ser.type === undefined ? "Plain" : ser.type };
+				if ("value" in ser) value.value = ser.value;
+				this.addMessage(doc, 0, { type: "set", key, value });
+			}
+		}
+		return doc;
+	}
 	/** SharedMap.processMessagesCore shape (map.ts:288-311): one bunch for document `doc`. */
 	processMessagesCore(doc, messagesCollection) {
 		for (const mc of messagesCollection.messagesContent) {

@@ -426,6 +426,23 @@ class MapStreamBuilder:
         else:
             raise UnsupportedOp(f"map op type {t}")
 
+    def begin_doc_from_summary(self, header: str, blobs=()) -> int:
+        """A document whose map starts from a SharedMap summary (SharedMap.loadCore, map.ts:251-267):
+        the header's "content" entries, then each blob's, enter sequencedData in Object.entries
+        order (MapKernel.populateFromSerializable, mapKernel.ts:557-564). They are packed as the
+        document's first set records, so later messages apply on top in order."""
+        doc = self.begin_doc()
+        h = json.loads(header)
+        parts = [h["content"]] + [json.loads(b) for b in blobs] if isinstance(h.get("blobs"), list) else [h]
+        for part in parts:
+            for key in js_key_order(list(part)):
+                ser = part[key]
+                value = {"type": ser.get("type", "Plain")}
+                if "value" in ser:
+                    value["value"] = ser["value"]
+                self.add_message(doc, 0, {"type": "set", "key": key, "value": value})
+        return doc
+
     def finish(self) -> MapBatch:
         n = sum(len(d) for d in self.docs)
         ops = np.zeros(n, dtype=MAP_OP_DTYPE)

@@ -216,3 +216,15 @@ def test_mt_snapshot_load_matches_oracle(orc, engine):
     cf = workloads.conflict_farm(256, n_clients=8, ops_per_doc=1500, seed=31)
     rb = reload_batch(summaries_of(orc, cf, chunk=60, catchup=False), keep_messages=False)
     _check_against_oracle(orc, engine, rb)
+
+
+def test_map_split_replay_through_summary(orc, engine):
+    """Prefix replay → summary → load + the rest, on the GPU == the oracle's full replay."""
+    from test_map_load import split_replay_batches
+
+    full, resumed = split_replay_batches(orc, n_docs=256)
+    engine.map_load(resumed)
+    engine.map_run()
+    got = engine.map_fetch()
+    for d in range(full.n_docs):
+        assert map_summary(got[d], resumed.keys, resumed.values) == orc.map_summary(full, d), d
