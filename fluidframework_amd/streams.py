@@ -244,6 +244,8 @@ class MergeTreeStreamBuilder:
             return (seq, ref, msn, int(op["pos1"]), -1, off, n, client, MT_INSERT, 0)
         if t == MT_REMOVE:
             return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_REMOVE, 0)
+        if t == MT_OBLITERATE:  # non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
+            return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_OBLITERATE, 0)
         if t == MT_ANNOTATE:
             if op.get("adjust") is not None:
                 raise UnsupportedOp("annotate adjust")

@@ -281,7 +281,233 @@ Seg* MergeTree::splitAt(Seg* seg, int pos) {
   next->ins = seg->ins;
   next->removes = seg->removes;
   if (seg->props.defined) next->props = seg->props;
+  // LocalReferenceCollection.split (localReference.ts:464-483): refs at offset >= pos move over
+  std::vector<LRef*> keep;
+  for (LRef* r : seg->refs) {
+    if (r->offset >= pos) {
+      r->seg = next;
+      r->offset -= pos;
+      next->refs.push_back(r);
+    } else {
+      keep.push_back(r);
+    }
+  }
+  seg->refs.swap(keep);
   return next;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Obliterate (mergeTree.ts:515-625, 1642-1746, 2083-2290)
+// ------------------------------------------------------------------------------------------------
+// Segment ordinals compare as strings (mergeTreeNodes.ts setOrdinal, ordinal.ts): for linked
+// segments that is document order, i.e. the order of their child-index paths from the root; an
+// unlinked segment's ordinal is undefined, which SortedSegmentSet reads as "" (smallest).
+int MergeTree::ordinalCompare(const Seg* a, const Seg* b) const {
+  const bool la = a != nullptr && a->parent != nullptr, lb = b != nullptr && b->parent != nullptr;
+  if (!la || !lb) return la == lb ? 0 : (la ? 1 : -1);
+  if (a == b) return 0;
+  auto path = [](const Node* n) {
+    std::vector<int> p;
+    for (; n->parent != nullptr; n = n->parent) p.push_back(n->index);
+    std::reverse(p.begin(), p.end());
+    return p;
+  };
+  const std::vector<int> pa = path(a), pb = path(b);
+  return std::lexicographical_compare(pa.begin(), pa.end(), pb.begin(), pb.end()) ? -1 : 1;
+}
+
+int MergeTree::refCompare(const LRef* a, const LRef* b) const {
+  const int c = ordinalCompare(a->seg, b->seg);
+  return c != 0 ? c : a->offset - b->offset;
+}
+
+// SortedSet.findItemPosition (sortedSet.ts) + SortedSegmentSet.onFindEquivalent, verbatim: the
+// array is only as sorted as the ordinals were when items went in.
+std::pair<bool, size_t> MergeTree::findStart(const LRef* item) const {
+  if (obStart_.empty()) return {false, 0};
+  long start = 0, end = static_cast<long>(obStart_.size()) - 1, index = -1;
+  while (start <= end) {
+    index = start + (end - start) / 2;
+    const int c = refCompare(item, obStart_[index]);
+    if (c < 0) {
+      if (start == index) return {false, static_cast<size_t>(index)};
+      end = index - 1;
+    } else if (c > 0) {
+      if (index == end) return {false, static_cast<size_t>(index + 1)};
+      start = index + 1;
+    } else {
+      if (item == obStart_[index]) return {true, static_cast<size_t>(index)};
+      for (long b = index - 1; b >= 0 && refCompare(item, obStart_[b]) == 0; b--)
+        if (obStart_[b] == item) return {true, static_cast<size_t>(b)};
+      for (; index < static_cast<long>(obStart_.size()) && refCompare(item, obStart_[index]) == 0; index++)
+        if (obStart_[index] == item) return {true, static_cast<size_t>(index)};
+      return {false, static_cast<size_t>(index)};
+    }
+  }
+  return {false, static_cast<size_t>(index)};
+}
+
+// Obliterates.findOverlapping (mergeTree.ts:566-582): walk the starts in array order, stop at the
+// first start that is unlinked or past the segment.
+std::vector<ObliterateInfo*> MergeTree::findOverlapping(const Seg* seg) const {
+  std::vector<ObliterateInfo*> out;
+  for (const LRef* start : obStart_) {
+    const Seg* startSeg = start->seg;
+    if (startSeg != nullptr && startSeg->parent != nullptr && ordinalCompare(startSeg, seg) <= 0) {
+      const Seg* endSeg = start->ob->end.seg;
+      if (endSeg != nullptr && endSeg->parent != nullptr && ordinalCompare(endSeg, seg) >= 0)
+        out.push_back(start->ob);
+    } else {
+      break;
+    }
+  }
+  return out;
+}
+
+void MergeTree::attachRef(LRef* ref, Seg* seg, int offset) {
+  ref->seg = seg;
+  ref->offset = offset;
+  seg->refs.push_back(ref);
+}
+
+void MergeTree::detachRef(LRef* ref) {
+  if (ref->seg != nullptr) {
+    auto& v = ref->seg->refs;
+    v.erase(std::remove(v.begin(), v.end(), ref), v.end());
+  }
+  ref->seg = nullptr;
+}
+
+// Obliterates.setMinSeq (mergeTree.ts:537-545)
+void MergeTree::obliteratesSetMinSeq(int min) {
+  size_t k = 0;
+  for (; k < obSeq_.size() && obSeq_[k]->stamp.seq <= min; k++) {
+    ObliterateInfo* ob = obSeq_[k];
+    const auto pos = findStart(&ob->start);
+    if (pos.first) obStart_.erase(obStart_.begin() + static_cast<long>(pos.second));
+    detachRef(&ob->start);
+    detachRef(&ob->end);
+  }
+  obSeq_.erase(obSeq_.begin(), obSeq_.begin() + static_cast<long>(k));
+}
+
+// getContainingSegment (mergeTree.ts:858-886): the first leaf nodeMap visits in [pos, pos + 1).
+std::pair<Seg*, int> MergeTree::getContainingSegment(int pos, const Perspective& p) const {
+  Seg* found = nullptr;
+  int offset = 0;
+  int walkPos = 0;
+  bool exit = false;
+  auto walk = [&](auto&& self, const Block* b) -> void {
+    for (int i = 0; i < b->childCount && !exit; i++) {
+      if (pos + 1 <= walkPos) {
+        exit = true;
+        return;
+      }
+      const Node* n = b->children[i];
+      const int len = nodeLength(n, p);
+      const int lenAt = len == kUndefinedLen ? 0 : len;
+      if (lenAt == 0) continue;
+      const int nextPos = walkPos + lenAt;
+      if (pos >= nextPos) {
+        walkPos = nextPos;
+        continue;
+      }
+      if (n->isLeaf) {
+        found = const_cast<Seg*>(static_cast<const Seg*>(n));
+        offset = pos - walkPos;
+        exit = true;
+        return;
+      }
+      self(self, static_cast<const Block*>(n));
+    }
+  };
+  walk(walk, root_);
+  return {found, offset};
+}
+
+void MergeTree::obliterateRange(int start, int end, const Perspective& p, Stamp stamp) {
+  const int startPos = start, endPos = end;  // {start, Before} and {end - 1, After}
+  ensureIntervalBoundary(startPos, p);
+  ensureIntervalBoundary(endPos, p);
+  obPool_.push_back(std::make_unique<ObliterateInfo>());
+  ObliterateInfo* ob = obPool_.back().get();
+  ob->stamp = stamp;
+  ob->refSeq = p.refSeq;
+  const auto s0 = getContainingSegment(start, p);
+  const auto s1 = getContainingSegment(end - 1, p);
+  if (s0.first == nullptr || s1.first == nullptr) throw DataError("segments cannot be undefined");  // 0xa3f
+  ob->start.ob = ob;
+  ob->end.ob = ob;
+  attachRef(&ob->start, s0.first, s0.second);
+  attachRef(&ob->end, s1.first, s1.second);
+  obSeq_.push_back(ob);
+  const auto at = findStart(&ob->start);
+  if (!at.first) obStart_.insert(obStart_.begin() + static_cast<long>(at.second), &ob->start);
+
+  // nodeMap(perspective, markRemoved, ..., start, end, RemoteObliteratePerspective(client)):
+  // positions come from the op's view; a leaf is visited when it has length there or is not
+  // removed at all (concurrent inserts included). Blocks are only skipped when wholly before start.
+  std::vector<Seg*> newlyRemoved;
+  int pos = 0;
+  bool exit = false;
+  auto walk = [&](auto&& self, Block* b) -> void {
+    for (int i = 0; i < b->childCount && !exit; i++) {
+      if (endPos <= pos) {
+        exit = true;
+        return;
+      }
+      Node* n = b->children[i];
+      const int lenAt0 = nodeLength(n, p);
+      const int lenAt = lenAt0 == kUndefinedLen ? 0 : lenAt0;
+      if (n->isLeaf && lenAt == 0 && static_cast<Seg*>(n)->removed()) continue;
+      const int nextPos = pos + lenAt;
+      if (start >= nextPos) {
+        pos = nextPos;
+        continue;
+      }
+      if (n->isLeaf) {
+        Seg* s = static_cast<Seg*>(n);
+        if (!s->removed()) {
+          newlyRemoved.push_back(s);
+          s->removes.push_back(stamp);
+        } else {
+          int k = static_cast<int>(s->removes.size()) - 1;
+          for (; k >= 0; k--)
+            if (stampGreater(stamp, s->removes[k])) break;
+          s->removes.insert(s->removes.begin() + (k + 1), stamp);
+        }
+        if (collaborating) addToLRUSet(s, stamp.seq);
+        pos = nextPos;
+      } else {
+        self(self, static_cast<Block*>(n));
+      }
+    }
+  };
+  walk(walk, root_);
+  if (catchupOut) recordDelta(FMT_MT_OBLITERATE, newlyRemoved);
+  if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
+}
+
+void MergeTree::obliterateOnInsert(Seg* seg, const Perspective& p, Stamp stamp) {
+  if (obStart_.empty()) return;
+  const Stamp refSeqStamp{p.refSeq, stamp.client};
+  std::vector<Stamp> overlappingAcked;
+  ObliterateInfo *oldest = nullptr, *newest = nullptr;
+  for (ObliterateInfo* ob : findOverlapping(seg)) {
+    if (stampGreater(ob->stamp, refSeqStamp)) {
+      if (stamp.client != ob->stamp.client) {
+        overlappingAcked.push_back(ob->stamp);
+        if (oldest == nullptr || stampGreater(oldest->stamp, ob->stamp)) oldest = ob;
+      }
+      if (newest == nullptr || stampGreater(ob->stamp, newest->stamp)) newest = ob;
+    }
+  }
+  // every stamp here is acked, so newestAcked === newest (mergeTree.ts:1715-1725)
+  if (oldest != nullptr && newest->stamp.client != stamp.client) {
+    std::stable_sort(overlappingAcked.begin(), overlappingAcked.end(),
+                     [](const Stamp& a, const Stamp& b) { return a.seq < b.seq; });
+    seg->removes = overlappingAcked;
+  }
 }
 
 // mergeTree.ts:1798-1808
@@ -344,7 +570,9 @@ void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp st
     InsertCtx ctx{true, seg};
     insertingWalk(pos, p, stamp, ctx);
     if (seg->parent == nullptr) throw DataError("MergeTree insert failed");
-    if (catchupOut) recordDelta(FMT_MT_INSERT, {seg});  // delta callback precedes zamboni (:1497-1516)
+    if (stamp.seq != kUnassignedSeq) obliterateOnInsert(seg, p, stamp);
+    // delta callback precedes zamboni (:1497-1516); an insert obliterated on arrival raises none
+    if (catchupOut && !seg->removed()) recordDelta(FMT_MT_INSERT, {seg});
     if (collaborating) {
       const bool isLocal = stamp.seq == kUnassignedSeq;
       if (!(isLocal && stamp.client == clientId) &&
@@ -443,7 +671,8 @@ void MergeTree::recordDelta(uint32_t type, const std::vector<Seg*>& deltaSegs) {
     const int pos = getPosition(s);
     if (catchupOut->size() > first) {
       fmt_mt_catchup_range& last = catchupOut->back();
-      if ((type == FMT_MT_REMOVE && last.pos1 == pos) || (type == FMT_MT_ANNOTATE && last.pos2 == pos)) {
+      if (((type == FMT_MT_REMOVE || type == FMT_MT_OBLITERATE) && last.pos1 == pos) ||
+          (type == FMT_MT_ANNOTATE && last.pos2 == pos)) {
         last.pos2 += s->len();
         continue;
       }
@@ -458,6 +687,7 @@ void MergeTree::setMinSeq(int min) {
   if (minSeq > min) throw DataError("minSeq of collab window > target minSeq!");
   if (min > minSeq) {
     minSeq = min;
+    obliteratesSetMinSeq(min);
     zamboniSegments();
   }
 }
@@ -561,6 +791,9 @@ void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const ui
     case FMT_MT_REMOVE:
       markRangeRemoved(op.pos1, op.pos2, p, stamp);
       break;
+    case FMT_MT_OBLITERATE:
+      obliterateRange(op.pos1, op.pos2, p, stamp);
+      break;
     case FMT_MT_ANNOTATE: {
       std::vector<std::pair<uint16_t, uint16_t>> kv;
       for (uint32_t i = propsOff[op.payload]; i < propsOff[op.payload + 1]; i++)
@@ -623,6 +856,12 @@ void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {
         const bool positive = (l == kUndefinedLen ? 0 : l) > 0;
         if (prev != nullptr && canAppendText(prev, seg) && matchProperties(prev->props, seg->props) &&
             positive) {
+          for (LRef* r : seg->refs) {  // LocalReferenceCollection.append (localReference.ts:233-251)
+            r->seg = prev;
+            r->offset += prev->len();
+            prev->refs.push_back(r);
+          }
+          seg->refs.clear();
           prev->text += seg->text;  // BaseSegment.append + TextSegment.append
           seg->parent = nullptr;    // removeMergeNodeInfo
         } else {

@@ -81,14 +81,33 @@ struct Node {
   const bool isLeaf;
 };
 
+struct LRef;
 struct Seg : Node {
   Seg() : Node(true) {}
   std::u16string text;
   Stamp ins{0, 0};
   std::vector<Stamp> removes;  // sorted by stamps.compare (spliceIntoList)
   PropMap props;
+  std::vector<LRef*> refs;     // local references on this segment (localReference.ts)
   int len() const { return static_cast<int>(text.size()); }
   bool removed() const { return !removes.empty(); }
+};
+
+// A StayOnRemove local reference (localReference.ts): stays on its segment when the segment is
+// removed, follows the text across splitAt (LocalReferenceCollection.split) and zamboni appends
+// (LocalReferenceCollection.append), and keeps pointing at a segment zamboni unlinks.
+struct ObliterateInfo;
+struct LRef {
+  Seg* seg = nullptr;  // nullptr once removed (removeLocalReferencePosition)
+  int offset = 0;
+  ObliterateInfo* ob = nullptr;
+};
+
+// mergeTree.ts ObliterateInfo: the obliterated range's endpoint references and the op's stamp.
+struct ObliterateInfo {
+  LRef start, end;
+  Stamp stamp;
+  int refSeq = 0;
 };
 
 struct Block : Node {
@@ -219,6 +238,21 @@ class MergeTree {
 
   void insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp);
   void markRangeRemoved(int start, int end, const Perspective& p, Stamp stamp);
+  // obliterateRange (mergeTree.ts:2262-2290) → obliterateRangeSided (:2083-2260) with
+  // start {pos1, Before} and end {pos2 - 1, After}.
+  void obliterateRange(int start, int end, const Perspective& p, Stamp stamp);
+  // The obliterate branch of blockInsert (mergeTree.ts:1642-1746) for a new remote segment.
+  void obliterateOnInsert(Seg* seg, const Perspective& p, Stamp stamp);
+  // Obliterates (mergeTree.ts:515-625): seqOrdered + startOrdered (a SortedSegmentSet of the
+  // start references, sortedSegmentSet.ts / sortedSet.ts, restated with its binary search).
+  int ordinalCompare(const Seg* a, const Seg* b) const;
+  int refCompare(const LRef* a, const LRef* b) const;
+  std::pair<bool, size_t> findStart(const LRef* item) const;
+  std::vector<ObliterateInfo*> findOverlapping(const Seg* seg) const;
+  void obliteratesSetMinSeq(int min);
+  void attachRef(LRef* ref, Seg* seg, int offset);
+  static void detachRef(LRef* ref);
+  std::pair<Seg*, int> getContainingSegment(int pos, const Perspective& p) const;
   void annotateRange(int start, int end, const std::vector<std::pair<uint16_t, uint16_t>>& props,
                      const Perspective& p, Stamp stamp);
   void addToLRUSet(Seg* leaf, int seq);
@@ -231,6 +265,9 @@ class MergeTree {
   Block* root_;
   Block unfinished_;  // theUnfinishedNode sentinel (mergeTree.ts:656)
   LruHeap heap_;
+  std::vector<std::unique_ptr<ObliterateInfo>> obPool_;
+  std::vector<ObliterateInfo*> obSeq_;   // seqOrdered (front = lowest seq)
+  std::vector<LRef*> obStart_;           // startOrdered
   std::vector<std::unique_ptr<Seg>> segPool_;
   std::vector<std::unique_ptr<Block>> blockPool_;
 };

@@ -13,9 +13,10 @@ def _js(a):
     return json.loads(a.tobytes().decode())
 
 
-def replay_fixtures():
-    """Yields (name, batch, group_end, initial_texts, result_texts) for the 30 0.40 fixtures."""
-    z = np.load(os.path.join(GOLDEN, "replay_conflict_farm_0.40.npz"), allow_pickle=False)
+def replay_fixtures(bundle="replay_conflict_farm_0.40.npz"):
+    """Yields (name, batch, group_end, initial_texts, result_texts) for the 30 fixtures of a bundle
+    (the 0.40 conflict farms, or replay_obliterate_2.3.0.npz for the obliterate farms)."""
+    z = np.load(os.path.join(GOLDEN, bundle), allow_pickle=False)
     names = _js(z["names"])
     for i, name in enumerate(names):
         ops = z[f"{i}/ops"]

@@ -6,12 +6,14 @@ box and the CPU test suite never read /root/reference at run time.
 
 Sources (data files held by the reference's own tests):
   packages/dds/merge-tree/src/test/results/*-default-conflict-farm-0.40.json
+  packages/dds/merge-tree/src/test/results/*-conflict-farm-with-obliterate-2.3.0.json
       replayed by client.replay.spec.ts:20-76 (64 groups of {initialText, resultText, msgs, seq})
   packages/dds/sequence/src/test/snapshots/legacy/{headerOnly,headerAndBody,largeBody,withAnnotations}.json
       checked by snapshotVersion.spec.ts:146-170 ("Snapshot diff")
 
 Outputs:
   replay_conflict_farm_0.40.npz   all 30 0.40 fixtures, packed by streams.py, with every checkpoint text
+  replay_obliterate_2.3.0.npz     the 30 *-conflict-farm-with-obliterate-2.3.0 fixtures, the same way
   replay_msgs_0.40.json.gz        the raw sequenced messages (ISequencedDocumentMessage JSON exactly as the
                                   fixture holds them) of MSG_FILES, for the JavaScript driver's tests
   snapshots_legacy.json           the legacy SharedString summary trees
@@ -94,6 +96,14 @@ def main() -> None:
             bundle[f"{i}/{k}"] = v
     bundle["names"] = np.frombuffer(json.dumps(files).encode(), dtype=np.uint8)
     np.savez_compressed(os.path.join(OUT, "replay_conflict_farm_0.40.npz"), **bundle)
+    files = sorted(f for f in os.listdir(RESULTS) if f.endswith("-conflict-farm-with-obliterate-2.3.0.json"))
+    bundle = {}
+    for i, f in enumerate(files):
+        d = convert_replay(os.path.join(RESULTS, f))
+        for k, v in d.items():
+            bundle[f"{i}/{k}"] = v
+    bundle["names"] = np.frombuffer(json.dumps(files).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "replay_obliterate_2.3.0.npz"), **bundle)
     write_messages()
     assert MT_OP_DTYPE.itemsize == 32
 
