@@ -43,7 +43,7 @@ MtCaps mergeTreeCaps();
 
 // Replays documents docList[0..count) (or all docs when docList == nullptr).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, int numCUs, hipStream_t stream);
+                           uint32_t count, int numCUs, hipStream_t stream, bool obliterate);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

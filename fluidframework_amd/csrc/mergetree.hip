@@ -1,6 +1,7 @@
 // mergetree.hip — merge-tree conflict-farm replay kernel for gfx950.
 //
-// One wavefront replays one document end to end (mt_engine.h); four documents per 256-thread
+// One wavefront replays one document end to end (mt_engine.h); a batch holding obliterates runs the
+// Doc<true> instantiation, every other batch the obliterate-free Doc<false>. four documents per 256-thread
 // workgroup share the CU, each with its own LDS state (fmt_mt::Scratch, ~8.5 KiB). Documents are
 // independent, so the grid simply strides over them; there is no inter-workgroup communication.
 // The per-document sequential dependency (every op depends on the state its predecessors left) is
@@ -18,6 +19,7 @@ constexpr int kMtWaves = 4;
 // Diagnostic build only: per-phase shader-clock totals summed over all waves (mt_engine.h stamp()).
 __device__ unsigned long long g_mtProfile[fmt_mt::kPfCount];
 
+template <bool Ob>
 __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                  const uint32_t* __restrict__ docList,
                                                                  uint32_t count) {
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
       o.catchup = nullptr;
       o.catchupCap = 0;
     }
-    fmt_mt::Doc doc;
+    fmt_mt::Doc<Ob> doc;
     doc.s = scratch;
     doc.run(in, o);
 #if FMT_PROFILE && FMT_GPU
@@ -90,13 +92,22 @@ MtCaps mergeTreeCaps() {
 }
 
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, int numCUs, hipStream_t stream) {
+                           uint32_t count, int numCUs, hipStream_t stream, bool obliterate) {
   const size_t lds = sizeof(fmt_mt::Scratch) * kMtWaves;
-  const int blocksPerCU = static_cast<int>(160 * 1024 / lds);
+  // One resident wave of workgroups: every workgroup strides over the same number of documents,
+  // so none waits behind the residency limit (VGPRs cap this kernel at 2 waves/SIMD).
+  int blocksPerCU = 0;
+  const hipError_t e = obliterate
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<true>, 64 * kMtWaves, lds)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<false>, 64 * kMtWaves, lds);
+  if (e != hipSuccess) return e;
   const uint32_t wanted = (count + kMtWaves - 1) / kMtWaves;
   const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
-  hipLaunchKernelGGL(mergeTreeKernel, dim3(grid), dim3(64 * kMtWaves), lds, stream, batch, out, docList, count);
+  if (obliterate)
+    hipLaunchKernelGGL(mergeTreeKernel<true>, dim3(grid), dim3(64 * kMtWaves), lds, stream, batch, out, docList, count);
+  else
+    hipLaunchKernelGGL(mergeTreeKernel<false>, dim3(grid), dim3(64 * kMtWaves), lds, stream, batch, out, docList, count);
   return hipGetLastError();
 }
 

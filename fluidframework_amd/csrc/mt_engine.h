@@ -43,6 +43,7 @@ constexpr int kPropCap = 32;
 constexpr int kMaxClient = 31;       // remove-client set is a 32-bit mask
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
 constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:21)
+constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
 constexpr uint32_t kNoBlk = 0xFF;
 constexpr uint32_t kPropsUndef = 0xFF;
 constexpr int32_t kNotRemoved = 0x7fffffff;
@@ -73,6 +74,14 @@ struct PropSet {
   uint32_t kv[FMT_MT_PROPS_MAX];
 };
 
+// One live obliterate (mergeTree.ts ObliterateInfo): its endpoint references as (leaf id, offset)
+// — id 0 once the reference is removed — and its stamp.
+struct ObEnt {
+  uint32_t startId, endId;
+  int32_t startOff, endOff;
+  int32_t seq, client;
+};
+
 // Per-wave LDS state.
 struct Scratch {
   uint16_t chars[kCapChars];
@@ -81,6 +90,9 @@ struct Scratch {
   PropSet props[kPropCap];
   uint8_t freeList[kMaxBlocks];
   uint32_t tmp[64];
+  ObEnt ob[kObCap];          // slots
+  uint8_t obSeq[kObCap];     // Obliterates.seqOrdered: slots in seq order
+  uint8_t obStart[kObCap];   // Obliterates.startOrdered: slots in SortedSegmentSet order
 };
 
 // Leaf word fields.
@@ -125,6 +137,9 @@ struct DocOutputs {
 #endif
 enum ProfCat { kPfOpLoad, kPfScan, kPfSplit, kPfInsert, kPfRange, kPfLru, kPfZamboniOp, kPfWindow, kPfOutput, kPfCount };
 
+// Ob: the engine variant that also replays obliterates (f1). Without obliterates in a batch the
+// runtime launches Doc<false>, whose code is exactly the obliterate-free engine.
+template <bool Ob>
 class Doc {
  public:
 #if FMT_PROFILE && FMT_GPU
@@ -152,6 +167,9 @@ class Doc {
   int failSeq = 0;
   uint32_t nextId = 1;
   uint32_t opIdx = 0;   // index of the current op within the document
+  int obSeqN = 0;       // live obliterates (seqOrdered length)
+  int obStartN = 0;     // startOrdered length (can exceed obSeqN: a failed SortedSet.remove)
+  uint64_t obUsed = 0;  // slot bitmap
   uint32_t cuN = 0;     // catch-up ranges recorded
   DocInputs in;
   fmt_mt_catchup_range* cuOut = nullptr;
@@ -597,7 +615,8 @@ class Doc {
         m &= m - 1;
         const int pos = static_cast<int>(readlane(ex, lane) + base);
         const int len = static_cast<int>(fLen(readlane(row(W[0], r), lane)));
-        if (open && ((type == FMT_MT_REMOVE && p1 == pos) || (type == FMT_MT_ANNOTATE && p2 == pos))) {
+        if (open && (((type == FMT_MT_REMOVE || type == FMT_MT_OBLITERATE) && p1 == pos) ||
+                     (type == FMT_MT_ANNOTATE && p2 == pos))) {
           p2 += len;
           continue;
         }
@@ -687,6 +706,9 @@ class Doc {
         rec.w[2] = readlane(row(W[2], r), lane);
         rec.w[3] = readlane(row(W[3], r), lane);
         rec.w[4] = mkW4(nextId++, fClient(readlane(row(W[4], r), lane)));
+        if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
+          if (obUsed != 0) obRefsMove(fId(readlane(row(W[4], r), lane)), fId(rec.w[4]), offset, -offset);
+        }
         FOR_LANES(l) {
           if (l == lane) LANE(W[0])[r] = mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
         }
@@ -764,9 +786,178 @@ class Doc {
     childAdded(blk);
     if (status != FMT_OK) return -1;
     stamp(kPfInsert);
+    if constexpr (Ob) {
+      if (obStartN > 0) obliterateOnInsert(insIdx, refSeq, client);
+    }
     lruForLeaf(insIdx, static_cast<int>(fBlk(readField(insIdx, 0))), seq);
     stamp(kPfLru);
     return status == FMT_OK ? insIdx : -1;
+  }
+
+  // ------------------------------------------------------------------ obliterates (f1)
+  // Obliterates (mergeTree.ts:515-625). A reference's "ordinal" is its leaf's document index, or
+  // "" (smallest) once the leaf is gone from the tree or the reference was removed.
+  FMT_DEV int leafOf(uint32_t id) const { return id == 0 ? -1 : findLeafById(id); }
+
+  FMT_DEV static int ordinalCompare(int ia, int ib) {
+    if (ia < 0 || ib < 0) return (ia < 0) == (ib < 0) ? 0 : (ia < 0 ? -1 : 1);
+    return ia < ib ? -1 : (ia > ib ? 1 : 0);
+  }
+
+  FMT_DEV int startCompare(int a, int b) const {  // SortedSegmentSet.compare on start references
+    const int c = ordinalCompare(leafOf(uni(s->ob[a].startId)), leafOf(uni(s->ob[b].startId)));
+    return c != 0 ? c : uni(s->ob[a].startOff) - uni(s->ob[b].startOff);
+  }
+
+  // SortedSet.findItemPosition + SortedSegmentSet.onFindEquivalent (sortedSet.ts,
+  // sortedSegmentSet.ts), verbatim: the array is only as sorted as the ordinals were at insertion.
+  FMT_DEV int findStart(int slot, bool* exists) const {
+    *exists = false;
+    if (obStartN == 0) return 0;
+    int start = 0, end = obStartN - 1, index = -1;
+    while (start <= end) {
+      index = start + (end - start) / 2;
+      const int at = uni(static_cast<int>(s->obStart[index]));
+      const int c = startCompare(slot, at);
+      if (c < 0) {
+        if (start == index) return index;
+        end = index - 1;
+      } else if (c > 0) {
+        if (index == end) return index + 1;
+        start = index + 1;
+      } else {
+        if (at == slot) {
+          *exists = true;
+          return index;
+        }
+        for (int b = index - 1; b >= 0 && startCompare(slot, uni(static_cast<int>(s->obStart[b]))) == 0; b--)
+          if (uni(static_cast<int>(s->obStart[b])) == slot) {
+            *exists = true;
+            return b;
+          }
+        for (; index < obStartN && startCompare(slot, uni(static_cast<int>(s->obStart[index]))) == 0; index++)
+          if (uni(static_cast<int>(s->obStart[index])) == slot) {
+            *exists = true;
+            return index;
+          }
+        return index;
+      }
+    }
+    return index;
+  }
+
+  // References on leaf `from` at offset >= minOff move to leaf `to`, offset += add (split: the
+  // right part; zamboni append: every reference of the appended leaf).
+  FMT_DEV void obRefsMove(uint32_t from, uint32_t to, int minOff, int add) {
+    for (int k = 0; k < kObCap; k++) {
+      if (((obUsed >> k) & 1ull) == 0) continue;
+      const uint32_t sid = uni(s->ob[k].startId), eid = uni(s->ob[k].endId);
+      const int so = uni(s->ob[k].startOff), eo = uni(s->ob[k].endOff);
+      waveSync();
+      if (sid == from && so >= minOff) {
+        s->ob[k].startId = to;
+        s->ob[k].startOff = so + add;
+      }
+      if (eid == from && eo >= minOff) {
+        s->ob[k].endId = to;
+        s->ob[k].endOff = eo + add;
+      }
+      waveSync();
+    }
+  }
+
+  FMT_DEV bool obAdd(uint32_t sId, int sOff, uint32_t eId, int eOff, int seq, int client) {
+    if (obUsed == ~0ull) return fail(FMT_E_CAPACITY);
+    const int slot = ctz64(~obUsed);
+    obUsed |= 1ull << slot;
+    s->ob[slot].startId = sId;
+    s->ob[slot].startOff = sOff;
+    s->ob[slot].endId = eId;
+    s->ob[slot].endOff = eOff;
+    s->ob[slot].seq = seq;
+    s->ob[slot].client = client;
+    s->obSeq[obSeqN] = static_cast<uint8_t>(slot);
+    waveSync();
+    obSeqN++;
+    bool exists;
+    const int at = findStart(slot, &exists);
+    if (!exists) {
+      if (obStartN >= kObCap) return fail(FMT_E_CAPACITY);
+      for (int i = obStartN; i > at; i--) {
+        const uint8_t v = s->obStart[i - 1];
+        waveSync();
+        s->obStart[i] = v;
+      }
+      s->obStart[at] = static_cast<uint8_t>(slot);
+      waveSync();
+      obStartN++;
+    }
+    return true;
+  }
+
+  // Obliterates.setMinSeq (mergeTree.ts:537-545), before zamboni: drop obliterates at/below minSeq
+  // from both lists and remove their references.
+  FMT_DEV void obSetMinSeq() {
+    int k = 0;
+    for (; k < obSeqN && uni(s->ob[uni(static_cast<int>(s->obSeq[k]))].seq) <= minSeq; k++) {
+      const int slot = uni(static_cast<int>(s->obSeq[k]));
+      bool exists;
+      const int at = findStart(slot, &exists);
+      if (exists) {
+        for (int i = at; i + 1 < obStartN; i++) {
+          const uint8_t v = s->obStart[i + 1];
+          waveSync();
+          s->obStart[i] = v;
+        }
+        waveSync();
+        obStartN--;
+      }
+      s->ob[slot].startId = 0;  // removeLocalReferencePosition
+      s->ob[slot].endId = 0;
+      waveSync();
+      if (!exists) continue;  // still listed in startOrdered: its slot stays taken
+      obUsed &= ~(1ull << slot);
+    }
+    if (k > 0) {
+      for (int i = 0; i + k < obSeqN; i++) {
+        const uint8_t v = s->obSeq[i + k];
+        waveSync();
+        s->obSeq[i] = v;
+      }
+      waveSync();
+      obSeqN -= k;
+    }
+  }
+
+  // blockInsert's obliterate branch (mergeTree.ts:1642-1746) for the new leaf k: every overlapping
+  // obliterate the inserter had not seen (seq > refSeq); when one is from another client and the
+  // newest is not the inserter's own, the leaf starts out removed by those other clients' ones.
+  FMT_DEV void obliterateOnInsert(int k, int refSeq, int client) {
+    int minSeqOther = kNotRemoved, newestSeq = -1, newestClient = -1;
+    uint32_t mask = 0;
+    bool any = false;
+    for (int i = 0; i < obStartN; i++) {  // Obliterates.findOverlapping (:566-582)
+      const int slot = uni(static_cast<int>(s->obStart[i]));
+      const int si = leafOf(uni(s->ob[slot].startId));
+      if (!(si >= 0 && si <= k)) break;
+      const int ei = leafOf(uni(s->ob[slot].endId));
+      if (!(ei >= 0 && ei >= k)) continue;
+      const int oseq = uni(s->ob[slot].seq), ocl = uni(s->ob[slot].client);
+      if (oseq <= refSeq) continue;
+      if (ocl != client) {
+        any = true;
+        mask |= 1u << ocl;
+        if (oseq < minSeqOther) minSeqOther = oseq;
+      }
+      if (oseq > newestSeq) {
+        newestSeq = oseq;
+        newestClient = ocl;
+      }
+    }
+    if (any && newestClient != client) {
+      writeField(k, 2, static_cast<uint32_t>(minSeqOther));
+      writeField(k, 3, mask);
+    }
   }
 
   // One member op of a remote message (client.ts:1291-1327).
@@ -778,6 +969,9 @@ class Doc {
       if (!splitAt(op.pos1, refSeq, client)) return;
       const int k = insertText(op, text0);
       if (!catchup || k < 0) return;
+      if constexpr (Ob) {  // an insert obliterated on arrival raises no delta (:1497-1508)
+        if (static_cast<int32_t>(readField(k, 2)) != kNotRemoved) return;
+      }
       FOR_LANES(l) { LANE(delta) = l == (k & 63) ? 1u << (k >> 6) : 0u; }  // the new segment (:1497-1508)
     } else {
       if (!applyRange(op, delta)) return;
@@ -801,14 +995,49 @@ class Doc {
     stamp(kPfScan);
     Lane<uint32_t> hits;
     FOR_LANES(l) { LANE(hits) = 0u; }
-    FOR_ROWS(r, 0, nr) {
-      FOR_LANES(l) {
-        const int sp = static_cast<int>(LANE(st)[r]);
-        if (LANE(vis)[r] > 0 && sp >= start && sp < end) LANE(hits) |= 1u << r;
+    bool obliterate = false;
+    if constexpr (Ob) obliterate = op.type == FMT_MT_OBLITERATE;
+    if (!obliterate) {
+      FOR_ROWS(r, 0, nr) {
+        FOR_LANES(l) {
+          const int sp = static_cast<int>(LANE(st)[r]);
+          if (LANE(vis)[r] > 0 && sp >= start && sp < end) LANE(hits) |= 1u << r;
+        }
       }
+    } else {
+      // obliterateRangeSided (mergeTree.ts:2083-2260) with start {pos1, Before}, end {pos2-1, After}:
+      // nodeMap under RemoteObliteratePerspective visits a leaf when it has length in the op's view
+      // or is not removed at all (so concurrent inserts strictly inside are caught), positions from
+      // the op's view: st < end, start < st + vis. Endpoint references go to the leaves holding
+      // pos1 and pos2 - 1 in the op's view (getContainingSegment, :858-886).
+      int sLeaf = -1, eLeaf = -1, sOff = 0, eOff = 0;
+      FOR_ROWS(r, 0, nr) {
+        Lane<bool> ps, pe;
+        FOR_LANES(l) {
+          const int sp = static_cast<int>(LANE(st)[r]), v = static_cast<int>(LANE(vis)[r]);
+          const bool removed = static_cast<int32_t>(LANE(W[2])[r]) != kNotRemoved;
+          if (!(v == 0 && removed) && r * 64 + l < n && sp < end && start < sp + v) LANE(hits) |= 1u << r;
+          LANE(ps) = v > 0 && sp <= start && start < sp + v;
+          LANE(pe) = v > 0 && sp <= end - 1 && end - 1 < sp + v;
+        }
+        const uint64_t ms = ballot(ps), me = ballot(pe);
+        if (sLeaf < 0 && ms != 0) {
+          sLeaf = r * 64 + ctz64(ms);
+          sOff = start - static_cast<int>(readlane(row(st, r), ctz64(ms)));
+        }
+        if (eLeaf < 0 && me != 0) {
+          eLeaf = r * 64 + ctz64(me);
+          eOff = end - 1 - static_cast<int>(readlane(row(st, r), ctz64(me)));
+        }
+      }
+      if (sLeaf < 0 || eLeaf < 0) {  // "segments cannot be undefined" (0xa3f)
+        fail(FMT_E_DATA);
+        return false;
+      }
+      if (!obAdd(fId(readField(sLeaf, 4)), sOff, fId(readField(eLeaf, 4)), eOff, seq, client)) return false;
     }
     FOR_LANES(l) { LANE(delta) = 0u; }
-    if (op.type == FMT_MT_REMOVE) {
+    if (op.type == FMT_MT_REMOVE || obliterate) {
       // markRangeRemoved (mergeTree.ts:2292-2383): first remove stays the lowest seq; the delta
       // (removedSegments) is the hit leaves not removed before this op (:2314-2321)
       FOR_ROWS(r, 0, nr) {
@@ -885,6 +1114,9 @@ class Doc {
                                  propsMatch(prevProps, fProps(w0)) && len > 0;
           if (canAppend) {
             mergeMask |= 1u << k;
+            if constexpr (Ob) {  // LocalReferenceCollection.append (localReference.ts:233-251)
+              if (obUsed != 0) obRefsMove(fId(readField(j, 4)), fId(readField(prev, 4)), 0, static_cast<int>(prevLen));
+            }
             prevLen += len;
             prevNl = lastNl;
             // the head keeps its index until the deletions below, so its length can be set now
@@ -1040,6 +1272,9 @@ class Doc {
     status = FMT_OK;
     failSeq = 0;
     nextId = 1;
+    obSeqN = 0;
+    obStartN = 0;
+    obUsed = 0;
     FOR_LANES(l) {
       V8 z;
 #pragma unroll
@@ -1277,7 +1512,8 @@ class Doc {
       rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
       opIdx = static_cast<uint32_t>(i - in.begin);
-      if (op.client > kMaxClient || op.type > FMT_MT_ANNOTATE) fail(FMT_E_UNSUPPORTED);
+      if (op.client > kMaxClient || (op.type > FMT_MT_ANNOTATE && !(Ob && op.type == FMT_MT_OBLITERATE)))
+        fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op, text);
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
@@ -1294,6 +1530,7 @@ class Doc {
           curSeq = op.seq;
           if (op.min_seq <= minSeq) break;
           minSeq = op.min_seq;
+          if constexpr (Ob) obSetMinSeq();
         }
         zamboni();
         stamp(z == 0 ? kPfZamboniOp : kPfWindow);

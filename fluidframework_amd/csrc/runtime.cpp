@@ -71,6 +71,7 @@ struct fmt_ctx {
   DevBuf<fmt_mt_snapshot_doc> mtSnap;       // per-doc summary loads (f3)
   DevBuf<fmt_mt_snapshot_seg> mtSnapSegs;
   bool mtHasSnap = false;
+  bool mtObliterate = false;                 // batch holds obliterates: launch the Doc<true> kernel
   DevBuf<uint64_t> mtCuOffs;                 // per-doc catch-up slab offsets (n_docs + 1)
   DevBuf<fmt_mt_catchup_range> mtCatchup;    // catch-up range slabs
   std::vector<uint64_t> mtCuOffsHost;
@@ -273,6 +274,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   if (b->doc_op_offsets[0] != 0 || b->doc_op_offsets[n] != b->n_ops)
     return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
   uint64_t insertChars = 0, catchupOps = 0;
+  bool obliterates = false;
   for (uint64_t i = 0; i < b->n_ops; i++) {
     const fmt_mt_op& op = b->ops[i];
     if (op.flags & FMT_MT_F_CATCHUP) catchupOps++;
@@ -282,6 +284,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       insertChars += op.len;
     } else if (op.type == FMT_MT_ANNOTATE) {
       if (op.payload >= b->n_props_ops) return setErr(c, FMT_E_DATA, "annotate props op id out of range");
+    } else if (op.type == FMT_MT_OBLITERATE) {
+      obliterates = true;
     } else if (op.type != FMT_MT_REMOVE) {
       return setErr(c, FMT_E_UNSUPPORTED, "op type not supported by this engine build");
     }
@@ -365,6 +369,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtTextLen = b->text_len;
   c->mtNProps = b->n_props_ops;
   c->mtHasInit = b->doc_init != nullptr;
+  c->mtObliterate = obliterates;
   c->mtInsertChars = insertChars;
   c->mtInitChars = initChars;
   c->mtLoaded = true;
@@ -381,7 +386,7 @@ int fmt_mt_run(fmt_ctx* c) {
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr};
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
-  FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->numCUs, c->stream));
+  FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->numCUs, c->stream, c->mtObliterate));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   c->stats = fmt_stats{};

@@ -17,7 +17,7 @@
 const path = require("path");
 const summary = require("./summary.js");
 
-const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3; // merge-tree/src/ops.ts:61-71
+const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3, MT_OBLITERATE = 4; // ops.ts:61-71
 const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
 const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
 const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2;
@@ -285,8 +285,8 @@ class MergeTreeStreamBuilder {
 				const r = this.text.push(seg);
 				if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
 				pos1 = op.pos1; pos2 = -1; payload = r[0]; len = r[1];
-			} else if (type === MT_REMOVE) {
-				pos1 = op.pos1; pos2 = op.pos2;
+			} else if (type === MT_REMOVE || type === MT_OBLITERATE) {
+				pos1 = op.pos1; pos2 = op.pos2; // non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
 			} else if (type === MT_ANNOTATE) {
 				if (op.adjust !== undefined && op.adjust !== null) throw new UnsupportedOp("annotate adjust");
 				pos1 = op.pos1; pos2 = op.pos2; payload = this.propsOp(op.props || {});

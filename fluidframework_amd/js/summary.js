@@ -11,7 +11,7 @@
  *     catch-up ops                          sequence/src/sequence.ts:395-452, 949-1018
  * Here JSON.stringify does the serialising, so JS key order comes for free.
  */
-const MT_INSERT = 0, MT_REMOVE = 1, MT_GROUP = 3;
+const MT_INSERT = 0, MT_REMOVE = 1, MT_GROUP = 3, MT_OBLITERATE = 4;
 const NOT_REMOVED = 0x7fffffff;
 const TEXT_GRANULARITY = 256; // textSegment.ts:21
 const SIZE_OF_FIRST_CHUNK = 10000; // snapshotlegacy.ts:55
@@ -153,7 +153,8 @@ function catchupMessages(messages, ranges, minSeq) {
 				for (const r of byOp.get(firstOp + k) || []) {
 					if (r.type === MT_INSERT) {
 						ops.push({ pos1: r.pos1, seg: typeof op.seg === "string" ? op.seg : op.seg.text, type: r.type });
-					} else if (r.type === MT_REMOVE) {
+					} else if (r.type === MT_REMOVE || r.type === MT_OBLITERATE) {
+						// createRemoveRangeOp / createObliterateRangeOp
 						ops.push({ pos1: r.pos1, pos2: r.pos2, type: r.type });
 					} else {
 						ops.push({ pos1: r.pos1, pos2: r.pos2, props: Object.assign({}, op.props || {}), type: r.type });

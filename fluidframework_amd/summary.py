@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import json
 
-from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_REMOVE, is_array_index_key,
+from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_OBLITERATE, MT_REMOVE, is_array_index_key,
                       js_json, js_key_order)
 
 NOT_REMOVED = 0x7FFFFFFF
@@ -193,7 +193,7 @@ def catchup_messages(messages, ranges, min_seq):
                     if t == MT_INSERT:  # createInsertOp(pos, segment.clone().toJSONObject())
                         seg = op["seg"]
                         ops.append({"pos1": p1, "seg": seg if isinstance(seg, str) else seg["text"], "type": t})
-                    elif t == MT_REMOVE:  # createRemoveRangeOp
+                    elif t in (MT_REMOVE, MT_OBLITERATE):  # createRemoveRangeOp / createObliterateRangeOp
                         ops.append({"pos1": p1, "pos2": p2, "type": t})
                     else:  # createAnnotateRangeOp(pos1, pos2, {...props}): the segment's value ?? null
                         props = op.get("props") or {}

@@ -6,20 +6,11 @@
 
 #include "../../fluidframework_amd/csrc/mt_engine.h"
 
-extern "C" {
-
-int emu_mt_capacity(uint32_t* leaves, uint32_t* chars, uint32_t* props) {
-  *leaves = fmt_mt::kCapLeaves;
-  *chars = fmt_mt::kCapChars;
-  *props = fmt_mt::kPropCap;
-  return 0;
-}
-
-// Same strides as the GPU result buffers (kCapLeaves / kCapChars / kPropCap per document).
-int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
-                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup) {
+template <bool Ob>
+static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                     fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup) {
   auto scratch = std::make_unique<fmt_mt::Scratch>();
-  auto doc = std::make_unique<fmt_mt::Doc>();
+  auto doc = std::make_unique<fmt_mt::Doc<Ob>>();
   int status = FMT_OK;
   for (uint32_t d = 0; d < b->n_docs; d++) {
     std::memset(scratch.get(), 0xCD, sizeof(fmt_mt::Scratch));  // poison: state must be initialized
@@ -54,12 +45,31 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
     o.props = props + static_cast<size_t>(d) * fmt_mt::kPropCap;
     o.catchup = catchup ? catchup + static_cast<size_t>(d) * capCatchup : nullptr;
     o.catchupCap = catchup ? capCatchup : 0u;
-    new (doc.get()) fmt_mt::Doc();
+    new (doc.get()) fmt_mt::Doc<Ob>();
     doc->s = scratch.get();
     doc->run(in, o);
     if (headers[d].status != FMT_OK && status == FMT_OK) status = headers[d].status;
   }
   return status;
+}
+
+extern "C" {
+
+int emu_mt_capacity(uint32_t* leaves, uint32_t* chars, uint32_t* props) {
+  *leaves = fmt_mt::kCapLeaves;
+  *chars = fmt_mt::kCapChars;
+  *props = fmt_mt::kPropCap;
+  return 0;
+}
+
+// Same strides as the GPU result buffers (kCapLeaves / kCapChars / kPropCap per document). Like
+// the runtime, batches holding obliterates run the Doc<true> variant (or always, with forceOb).
+int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb) {
+  bool ob = forceOb != 0;
+  for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE;
+  return ob ? replayAll<true>(b, headers, leaves, chars, props, catchup, capCatchup)
+            : replayAll<false>(b, headers, leaves, chars, props, catchup, capCatchup);
 }
 
 }  // extern "C"

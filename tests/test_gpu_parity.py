@@ -228,3 +228,15 @@ def test_map_split_replay_through_summary(orc, engine):
     got = engine.map_fetch()
     for d in range(full.n_docs):
         assert map_summary(got[d], resumed.keys, resumed.values) == orc.map_summary(full, d), d
+
+
+def test_mt_obliterate_fixture_checkpoints(orc, engine):
+    """f1: all 1920 text checkpoints of the 30 reference obliterate fixtures, engine == oracle."""
+    from golden_data import prefix_batch
+    from test_obliterate import OB_FIXTURES
+
+    batch, expected = prefix_batch(OB_FIXTURES)
+    hdrs = _check_against_oracle(orc, engine, batch)
+    for d, text in enumerate(expected):
+        leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+        assert visible_text(hdrs[d], leaves, chars) == text, d

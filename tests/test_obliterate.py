@@ -28,3 +28,45 @@ def test_oracle_obliterate_fixture_checkpoints(orc, idx):
         doc.apply(batch.ops[start:end], batch.text, batch.props_off, batch.props_kv)
         assert doc.text() == results[g], f"group {g} result"
         start = end
+
+
+@pytest.fixture(scope="module")
+def ob_prefix():
+    from golden_data import prefix_batch
+
+    return prefix_batch(OB_FIXTURES)
+
+
+def test_emulated_engine_obliterate_fixture_checkpoints(ob_prefix):
+    from mt_compare import emu_replay, visible_text
+
+    batch, expected = ob_prefix
+    hdr, leaves, chars, props = emu_replay(batch)
+    assert (hdr["status"] == 0).all(), hdr["status"]
+    bad = [d for d, text in enumerate(expected) if visible_text(hdr[d], leaves[d], chars[d]) != text]
+    assert not bad, f"{len(bad)} checkpoints differ, first doc {bad[0]}"
+
+
+def test_emulated_engine_obliterate_matches_oracle(orc, ob_prefix):
+    from mt_compare import compare_doc, emu_caps, emu_replay
+
+    batch, _ = ob_prefix
+    cl, cc, cp = emu_caps()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch)
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_obliterate_variant_matches_plain_engine_without_obliterates(orc):
+    """Doc<true> on obliterate-free streams is the plain engine bit for bit."""
+    from fluidframework_amd import workloads
+    from mt_compare import compare_doc, emu_replay
+
+    batch = workloads.conflict_farm(24, n_clients=8, ops_per_doc=1200, seed=13)
+    a = emu_replay(batch)
+    b = emu_replay(batch, force_ob=True)
+    for d in range(batch.n_docs):
+        assert not compare_doc(tuple(x[d] for x in a), tuple(x[d] for x in b)), d
