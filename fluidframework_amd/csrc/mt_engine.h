@@ -680,14 +680,29 @@ class Doc {
     }
   }
 
-  // ensureIntervalBoundary (mergeTree.ts:1798-1808): split the unique leaf that strictly contains
-  // pos in the op's view. Returns false only on failure.
-  FMT_DEV bool splitAt(int pos, int refSeq, int client) {
-    const int nr = rows();
-    Lane<V8> vis, st;
-    visLengths(refSeq, client, vis, nr);
-    scanRows(vis, st, nr);
-    stamp(kPfScan);
+  // splitLeafSegment (mergeTree.ts:1768-1796) of leaf j at `offset` (0 < offset < len): the right
+  // part becomes leaf j + 1 of the same block, with a fresh id and the same stamps and props.
+  FMT_DEV bool splitLeafAt(int j, int offset) {
+    LeafRec rec;
+    const uint32_t w0 = readField(j, 0);
+    const uint32_t w4 = readField(j, 4);
+    rec.w[0] = mkW0(fLen(w0) - static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
+    rec.w[1] = readField(j, 1);
+    rec.w[2] = readField(j, 2);
+    rec.w[3] = readField(j, 3);
+    rec.w[4] = mkW4(nextId++, fClient(w4));
+    if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
+      if (obUsed != 0) obRefsMove(fId(w4), fId(rec.w[4]), offset, -offset);
+    }
+    writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0)));
+    if (!insertLeafAt(j + 1, rec)) return false;
+    childAdded(static_cast<int>(fBlk(w0)));
+    stamp(kPfSplit);
+    return status == FMT_OK;
+  }
+
+  // The leaf that strictly contains view position pos (st < pos < st + vis), or -1; *stOut = its st.
+  FMT_DEV static int containing(const Lane<V8>& vis, const Lane<V8>& st, int pos, int nr, int* stOut) {
     FOR_ROWS(r, 0, nr) {
       Lane<bool> p;
       FOR_LANES(l) {
@@ -696,30 +711,47 @@ class Doc {
       }
       const uint64_t m = ballot(p);
       if (m != 0) {
-        const int lane = ctz64(m);
-        const int j = r * 64 + lane;
-        const int offset = pos - static_cast<int>(readlane(row(st, r), lane));
-        LeafRec rec;
-        const uint32_t w0 = readlane(row(W[0], r), lane);
-        rec.w[0] = mkW0(fLen(w0) - static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
-        rec.w[1] = readlane(row(W[1], r), lane);
-        rec.w[2] = readlane(row(W[2], r), lane);
-        rec.w[3] = readlane(row(W[3], r), lane);
-        rec.w[4] = mkW4(nextId++, fClient(readlane(row(W[4], r), lane)));
-        if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
-          if (obUsed != 0) obRefsMove(fId(readlane(row(W[4], r), lane)), fId(rec.w[4]), offset, -offset);
-        }
-        FOR_LANES(l) {
-          if (l == lane) LANE(W[0])[r] = mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0));
-        }
-        if (!insertLeafAt(j + 1, rec)) return false;
-        childAdded(static_cast<int>(fBlk(w0)));
-        stamp(kPfSplit);
-        return status == FMT_OK;
+        *stOut = static_cast<int>(readlane(row(st, r), ctz64(m)));
+        return r * 64 + ctz64(m);
       }
     }
-    stamp(kPfSplit);
-    return true;
+    return -1;
+  }
+
+  // ensureIntervalBoundary (mergeTree.ts:1798-1808): split the unique leaf that strictly contains
+  // pos in the op's view. Returns false only on failure. (Obliterate's path; inserts and
+  // remove/annotate resolve their boundaries from their one view scan instead.)
+  FMT_DEV bool splitAt(int pos, int refSeq, int client) {
+    const int nr = rows();
+    Lane<V8> vis, st;
+    visLengths(refSeq, client, vis, nr);
+    scanRows(vis, st, nr);
+    stamp(kPfScan);
+    int sp = 0;
+    const int j = containing(vis, st, pos, nr, &sp);
+    if (j < 0) {
+      stamp(kPfSplit);
+      return true;
+    }
+    return splitLeafAt(j, pos - sp);
+  }
+
+  // A row bitmask (bit r of lane l = leaf 64 r + l) after inserting a leaf at index k with bit b:
+  // bits at k and above move up one leaf, exactly like insertLeafAt moves the leaves.
+  FMT_DEV static Lane<uint32_t> maskInsert(const Lane<uint32_t>& m, int k, bool b) {
+    const Lane<uint32_t> up = shflUp1(m);
+    const uint32_t carry = readlane(m, 63) << 1;
+    const int rk = k >> 6, kl = k & 63;
+    Lane<uint32_t> out;
+    FOR_LANES(l) {
+      const int keepRows = k > l ? (k - l + 63) >> 6 : 0;  // rows r with 64 r + l < k
+      const uint32_t keep = keepRows >= 32 ? ~0u : (1u << keepRows) - 1u;
+      const uint32_t shifted = l == 0 ? carry : LANE(up);
+      uint32_t v = (LANE(m) & keep) | (shifted & ~keep);
+      if (l == kl) v = (v & ~(1u << rk)) | (b ? 1u << rk : 0u);
+      LANE(out) = v;
+    }
+    return out;
   }
 
   // insertSegments (mergeTree.ts:1484-1517) after the boundary split: the new leaf goes before the
@@ -729,13 +761,18 @@ class Doc {
   FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
     const int pos = op.pos1, len = op.len;
-    if (len <= 0) return -1;
     const int nr = rows();
     Lane<V8> vis, st;
     visLengths(refSeq, client, vis, nr);
     const uint32_t total = scanRows(vis, st, nr);
     stamp(kPfScan);
-    int insIdx = -1;
+    // ensureIntervalBoundary(pos) from the same scan: a split leaves every view start in place, and
+    // the right part (view start pos) is then the first leaf at pos.
+    int sp = 0;
+    const int js = containing(vis, st, pos, nr, &sp);
+    if (js >= 0 && !splitLeafAt(js, pos - sp)) return -1;
+    if (len <= 0) return -1;
+    int insIdx = js >= 0 ? js + 1 : -1;
     FOR_ROWS(r, 0, nr) {
       if (insIdx < 0) {
         Lane<bool> p;
@@ -962,11 +999,9 @@ class Doc {
 
   // One member op of a remote message (client.ts:1291-1327).
   FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
-    const int refSeq = op.ref_seq, client = op.client;
     const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
     Lane<uint32_t> delta;  // catch-up: the segments of the op's delta event (row bitmask per lane)
     if (op.type == FMT_MT_INSERT) {
-      if (!splitAt(op.pos1, refSeq, client)) return;
       const int k = insertText(op, text0);
       if (!catchup || k < 0) return;
       if constexpr (Ob) {  // an insert obliterated on arrival raises no delta (:1497-1508)
@@ -984,27 +1019,49 @@ class Doc {
   FMT_DEV bool applyRange(const fmt_mt_op& op, Lane<uint32_t>& delta) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
     const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
-    if (!splitAt(op.pos1, refSeq, client)) return false;
-    if (!splitAt(op.pos2, refSeq, client)) return false;
-    // nodeMap (mergeTree.ts:2961-3020): leaves of positive view length inside [start, end)
-    const int nr = rows();
-    const int start = op.pos1, end = op.pos2;
-    Lane<V8> vis, st;
-    visLengths(refSeq, client, vis, nr);
-    scanRows(vis, st, nr);
-    stamp(kPfScan);
-    Lane<uint32_t> hits;
-    FOR_LANES(l) { LANE(hits) = 0u; }
     bool obliterate = false;
     if constexpr (Ob) obliterate = op.type == FMT_MT_OBLITERATE;
+    const int start = op.pos1, end = op.pos2;
+    Lane<uint32_t> hits;
+    FOR_LANES(l) { LANE(hits) = 0u; }
+    int nr;
     if (!obliterate) {
+      // One view scan serves both boundary splits (ensureIntervalBoundary, mergeTree.ts:1798-1808)
+      // and nodeMap's hit set (:2961-3020, leaves of positive view length inside [start, end)):
+      // a split moves no view start, it only adds a leaf whose view start is the boundary.
+      nr = rows();
+      Lane<V8> vis, st;
+      visLengths(refSeq, client, vis, nr);
+      scanRows(vis, st, nr);
+      stamp(kPfScan);
       FOR_ROWS(r, 0, nr) {
         FOR_LANES(l) {
           const int sp = static_cast<int>(LANE(st)[r]);
           if (LANE(vis)[r] > 0 && sp >= start && sp < end) LANE(hits) |= 1u << r;
         }
       }
+      int s1 = 0, s2 = 0;
+      const int j1 = containing(vis, st, start, nr, &s1);
+      const int j2 = containing(vis, st, end, nr, &s2);
+      if (j1 >= 0) {  // the right part of j1 starts at `start`: a hit
+        if (!splitLeafAt(j1, start - s1)) return false;
+        hits = maskInsert(hits, j1 + 1, true);
+      }
+      if (j2 >= 0) {  // the right part of j2 starts at `end`: not a hit
+        const int jj = j1 < 0 || j1 > j2 ? j2 : (j1 < j2 ? j2 + 1 : j1 + 1);
+        const int off = j1 == j2 ? end - start : end - s2;
+        if (!splitLeafAt(jj, off)) return false;
+        hits = maskInsert(hits, jj + 1, false);
+      }
+      nr = rows();
     } else {
+      if (!splitAt(op.pos1, refSeq, client)) return false;
+      if (!splitAt(op.pos2, refSeq, client)) return false;
+      nr = rows();
+      Lane<V8> vis, st;
+      visLengths(refSeq, client, vis, nr);
+      scanRows(vis, st, nr);
+      stamp(kPfScan);
       // obliterateRangeSided (mergeTree.ts:2083-2260) with start {pos1, Before}, end {pos2-1, After}:
       // nodeMap under RemoteObliteratePerspective visits a leaf when it has length in the op's view
       // or is not removed at all (so concurrent inserts strictly inside are caught), positions from

@@ -80,8 +80,11 @@ MAP_W8 = ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 8;
 MAP_W2 = ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 2;")
 MAP_LB2 = ("map_lww.hip", "__launch_bounds__(64 * kWaves) void mapLwwKernel", "__launch_bounds__(64 * kWaves, 2) void mapLwwKernel")
 
+NOLOAD = ("mt_engine.h", "    if (in.loaded) loadSnapshot();", "    if (false) loadSnapshot();")
+
 VARIANTS = {
     "prof": [PROF],
+    "noload": [NOLOAD],
     "base": [],
     "nofence": [NOFENCE],
     "lb1": [LB1],

@@ -1,11 +1,11 @@
 #!/bin/bash
-# GPU parity tests on the in-tree library, then interleaved A/B of build/variants/*, then the
-# per-phase profile of the prof variant (if built). Each GPU step has its own time limit.
+# Same-process A/B of build/variants/* on the T1-shaped workload, then the phase profile variant.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 \
- && timeout -k 10 600 python3 tools/bench_variants.py --docs 20000 --unique 2000 --rounds 3 "$@" > gpurun_out/ab.json 2> gpurun_out/ab.err \
- && { [ ! -f build/variants/prof/libfmt.so ] || timeout -k 10 300 python3 tools/mt_phase_profile.py > gpurun_out/phases.json 2> gpurun_out/phases.err; }
-echo "exit $?"
+timeout -k 10 400 python3 tools/bench_variants.py --docs 20000 --unique 20000 --rounds 3 "$@" > gpurun_out/ab.json 2> gpurun_out/ab.err \
+ && timeout -k 10 300 python3 tools/mt_phase_profile.py --docs 20000 --unique 20000 > gpurun_out/phases.json 2> gpurun_out/phases.err
+rc=$?
+cat gpurun_out/ab.json
+exit $rc
