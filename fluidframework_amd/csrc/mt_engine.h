@@ -135,7 +135,10 @@ struct DocOutputs {
 #ifndef FMT_PROFILE
 #define FMT_PROFILE 0
 #endif
-enum ProfCat { kPfOpLoad, kPfScan, kPfSplit, kPfInsert, kPfRange, kPfLru, kPfZamboniOp, kPfWindow, kPfOutput, kPfCount };
+enum ProfCat {
+  kPfOpLoad, kPfScan, kPfSplit, kPfInsert, kPfRange, kPfLru, kPfZamboniOp, kPfWindow, kPfOutput,
+  kPfInsChars, kPfInsShift, kPfZFind, kPfZChars, kPfZSerial, kPfZDelete, kPfZPack, kPfCount
+};
 
 // Ob: the engine variant that also replays obliterates (f1). Without obliterates in a batch the
 // runtime launches Doc<false>, whose code is exactly the obliterate-free engine.
@@ -295,6 +298,22 @@ class Doc {
       FOR_LANES(l) { LANE(lens)[r] = fLen(LANE(W[0])[r]); }
     }
     scanRows(lens, cst, nr);
+  }
+
+  // Char offset of leaf j: the lengths of the leaves before it, summed per lane over the rows and
+  // then once across the wave (no per-row scans).
+  FMT_DEV uint32_t charOffsetOf(int j) const {
+    if (j >= n) return static_cast<uint32_t>(nChars);
+    Lane<uint32_t> acc;
+    FOR_LANES(l) { LANE(acc) = 0u; }
+    FOR_ROWS(r, 0, (j >> 6) + 1) {
+      FOR_LANES(l) {
+        if (r * 64 + l < j) LANE(acc) += fLen(LANE(W[0])[r]);
+      }
+    }
+    uint32_t total;
+    waveExclusiveSum(acc, &total);
+    return total;
   }
 
   FMT_DEV uint32_t charStartOf(int j) const {
@@ -801,7 +820,7 @@ class Doc {
       fail(FMT_E_CAPACITY);
       return -1;
     }
-    const int cpos = static_cast<int>(charStartOf(insIdx));
+    const int cpos = static_cast<int>(charOffsetOf(insIdx));
     charsShiftUp(cpos, len);
     FOR_LANES(l) {
       if (l < len) s->chars[cpos + l] = static_cast<uint16_t>(LANE(text0));
@@ -809,6 +828,7 @@ class Doc {
     }
     waveSync();
     nChars += len;
+    stamp(kPfInsChars);
     LeafRec rec;
     rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), kPropsUndef);
     rec.w[1] = static_cast<uint32_t>(seq);
@@ -820,6 +840,7 @@ class Doc {
       waveSync();
     }
     if (!insertLeafAt(insIdx, rec)) return -1;
+    stamp(kPfInsShift);
     childAdded(blk);
     if (status != FMT_OK) return -1;
     stamp(kPfInsert);
@@ -1147,8 +1168,26 @@ class Doc {
     const int cnt = uni(static_cast<int>(s->blk[b].count));
     if (cnt == 0) return 0;
     const int first = firstLeafOf(static_cast<uint32_t>(b));
-    Lane<V8> cst;
-    charStarts(cst, ((first + cnt - 1) >> 6) + 1);
+    // One pass packs what the decisions need for every leaf of the block (at most 2 rows):
+    // len | props << 16 | removed << 24 | removed at/below minSeq << 25 | insert at/below minSeq << 26
+    const int r0 = first >> 6, r1 = (first + cnt - 1) >> 6;
+    Lane<uint32_t> pk0, pk1;
+    FOR_LANES(l) {
+      LANE(pk0) = 0u;
+      LANE(pk1) = 0u;
+    }
+    FOR_ROWS(r, r0, r1 + 1) {
+      FOR_LANES(l) {
+        const uint32_t w0 = LANE(W[0])[r];
+        const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]), rm = static_cast<int32_t>(LANE(W[2])[r]);
+        const uint32_t p = fLen(w0) | (fProps(w0) << 16) | (rm != kNotRemoved ? 1u << 24 : 0u) |
+                           (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u);
+        if (r == r0) LANE(pk0) = p;
+        else LANE(pk1) = p;
+      }
+    }
+    uint32_t cs = charOffsetOf(first);  // running char offset of leaf first + k
+    stamp(kPfZChars);
     // serial decisions over <= 7 leaves: keep, merge into the previous kept leaf, or drop
     uint32_t mergeMask = 0, dropMask = 0;
     int prev = -1;
@@ -1157,18 +1196,16 @@ class Doc {
     int kept = 0;
     for (int k = 0; k < cnt; k++) {
       const int j = first + k;
-      const uint32_t w0 = readField(j, 0);
-      const uint32_t len = fLen(w0);
-      const int32_t ins = static_cast<int32_t>(readField(j, 1));
-      const int32_t rm = static_cast<int32_t>(readField(j, 2));
-      if (rm == kNotRemoved) {
-        if (ins <= minSeq) {
-          const uint32_t cs = readlane(selectRow(cst, j >> 6), j & 63);
+      const uint32_t p = (j >> 6) == r0 ? readlane(pk0, j & 63) : readlane(pk1, j & 63);
+      const uint32_t len = p & 0xFFFFu, props = (p >> 16) & 0xFFu;
+      s->tmp[k] = cs;  // char offset, for the deletions below
+      if (((p >> 24) & 1u) == 0) {
+        if ((p >> 26) & 1u) {
           const bool lastNl = len > 0 && uni(static_cast<uint32_t>(s->chars[cs + len - 1])) == 10u;
           const bool canAppend = prev >= 0 && !prevNl &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) ||
                                   len <= static_cast<uint32_t>(kGranularity)) &&
-                                 propsMatch(prevProps, fProps(w0)) && len > 0;
+                                 propsMatch(prevProps, props) && len > 0;
           if (canAppend) {
             mergeMask |= 1u << k;
             if constexpr (Ob) {  // LocalReferenceCollection.append (localReference.ts:233-251)
@@ -1181,8 +1218,8 @@ class Doc {
           } else {
             prev = len > 0 ? j : -1;
             prevLen = len;
-            prevProps = fProps(w0);
-            prevBlk = fBlk(w0);
+            prevProps = props;
+            prevBlk = static_cast<uint32_t>(b);
             prevNl = lastNl;
             kept++;
           }
@@ -1191,26 +1228,30 @@ class Doc {
           kept++;
         }
       } else {
-        if (rm <= minSeq) {
+        if ((p >> 25) & 1u) {
           dropMask |= 1u << k;
         } else {
           kept++;
         }
         prev = -1;
       }
+      cs += len;
     }
+    waveSync();
+    stamp(kPfZSerial);
     // remove merged / dropped leaves from the highest index down (lower indices stay valid)
     for (int k = cnt - 1; k >= 0; k--) {
       if ((((mergeMask | dropMask) >> k) & 1u) == 0) continue;
       const int j = first + k;
       if ((dropMask >> k) & 1u) {
         const uint32_t len = fLen(readField(j, 0));
-        const int cs = static_cast<int>(readlane(selectRow(cst, j >> 6), j & 63));
-        charsShiftDown(cs + static_cast<int>(len), static_cast<int>(len));
+        const int c0 = uni(static_cast<int>(s->tmp[k]));
+        charsShiftDown(c0 + static_cast<int>(len), static_cast<int>(len));
         nChars -= static_cast<int>(len);
       }
       deleteLeafAt(j);
     }
+    stamp(kPfZDelete);
     return kept;
   }
 
@@ -1256,6 +1297,7 @@ class Doc {
       if (p == root) s->blk[p].leaf = 1;
     }
     waveSync();
+    stamp(kPfZPack);
   }
 
   // zamboni.ts:33-80, with packParent (zamboni.ts:83-139) folded in so that every block scour —
@@ -1266,6 +1308,7 @@ class Doc {
       if (heapSeq(1) > minSeq) break;
       const HeapEnt ent = heapGet();
       const int j = findLeafById(ent.leafId);
+      stamp(kPfZFind);
       if (j < 0) continue;  // unlinked or appended: segment.parent is undefined
       const int b = static_cast<int>(fBlk(readField(j, 0)));
       if (uni(static_cast<int>(s->blk[b].needsScour)) == 0) continue;

@@ -14,7 +14,8 @@ sys.path.insert(0, REPO)
 
 from fluidframework_amd import native, workloads  # noqa: E402
 
-PHASES = ["op_load", "scan", "split", "insert", "range", "lru", "zamboni_op", "window", "output"]
+PHASES = ["op_load", "scan", "split", "insert", "range", "lru", "zamboni_op", "window", "output",
+          "ins_chars", "ins_shift", "z_find", "z_chars", "z_serial", "z_delete", "z_pack"]
 
 
 def main():
