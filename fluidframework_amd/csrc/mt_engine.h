@@ -261,6 +261,45 @@ class Doc {
     n--;
   }
 
+  // Delete the leaves first + k for every bit k < cnt of `dead` in one pass: leaf i of the result
+  // comes from the (i - first)-th surviving leaf of the block, or from i + d after it (d = deleted
+  // count <= 7, so from the same row or the next). Empty slots past the new end stay zero.
+  FMT_DEV void deleteLeaves(int first, int cnt, uint32_t dead) {
+    const int d = __builtin_popcount(dead);
+    if (d == 0) return;
+    const int nr = rows(), nNew = n - d, keptEnd = first + cnt - d;
+    FOR_ROWS(r, first >> 6, nr) {
+      Lane<int> src;
+      Lane<bool> fromNext, live;
+      FOR_LANES(l) {
+        const int i = r * 64 + l;
+        int from = i + d;
+        if (i < first) {
+          from = i;
+        } else if (i < keptEnd) {
+          int seen = 0;
+#pragma unroll
+          for (int k = 0; k < kMaxNodes; k++) {
+            if (k < cnt && ((dead >> k) & 1u) == 0) {
+              if (seen == i - first) from = first + k;
+              seen++;
+            }
+          }
+        }
+        LANE(src) = from & 63;
+        LANE(fromNext) = (from >> 6) > r;
+        LANE(live) = i < nNew;
+      }
+#pragma unroll
+      for (int f = 0; f < 5; f++) {
+        const Lane<uint32_t> a = gather(row(W[f], r), src);
+        const Lane<uint32_t> b = gather(row(W[f], r + 1 < kRows ? r + 1 : r), src);
+        FOR_LANES(l) { LANE(W[f])[r] = LANE(live) ? (LANE(fromNext) && r + 1 < kRows ? LANE(b) : LANE(a)) : 0u; }
+      }
+    }
+    n = nNew;
+  }
+
   // Exclusive prefix (document order) of per-leaf values over rows [0, nr); returns the total.
   // Rows >= nr of `excl` are left unset.
   FMT_DEV static uint32_t scanRows(const Lane<V8>& vals, Lane<V8>& excl, int nr) {
@@ -1198,7 +1237,8 @@ class Doc {
       const int j = first + k;
       const uint32_t p = (j >> 6) == r0 ? readlane(pk0, j & 63) : readlane(pk1, j & 63);
       const uint32_t len = p & 0xFFFFu, props = (p >> 16) & 0xFFu;
-      s->tmp[k] = cs;  // char offset, for the deletions below
+      s->tmp[k] = cs;  // char offset and length, for the deletions below
+      s->tmp[kMaxNodes + k] = len;
       if (((p >> 24) & 1u) == 0) {
         if ((p >> 26) & 1u) {
           const bool lastNl = len > 0 && uni(static_cast<uint32_t>(s->chars[cs + len - 1])) == 10u;
@@ -1239,18 +1279,38 @@ class Doc {
     }
     waveSync();
     stamp(kPfZSerial);
-    // remove merged / dropped leaves from the highest index down (lower indices stay valid)
-    for (int k = cnt - 1; k >= 0; k--) {
-      if ((((mergeMask | dropMask) >> k) & 1u) == 0) continue;
-      const int j = first + k;
-      if ((dropMask >> k) & 1u) {
-        const uint32_t len = fLen(readField(j, 0));
-        const int c0 = uni(static_cast<int>(s->tmp[k]));
-        charsShiftDown(c0 + static_cast<int>(len), static_cast<int>(len));
-        nChars -= static_cast<int>(len);
+    // Dropped leaves take their text with them: one pass moves every later char down by the dropped
+    // lengths before it (chars of merged leaves stay, they already follow their head's).
+    if (dropMask != 0) {
+      uint32_t c0 = 0, dropped = 0;
+      for (int k = cnt - 1; k >= 0; k--)
+        if ((dropMask >> k) & 1u) c0 = uni(s->tmp[k]);
+      for (int k = 0; k < cnt; k++)
+        if ((dropMask >> k) & 1u) dropped += uni(s->tmp[kMaxNodes + k]);
+      const int newChars = nChars - static_cast<int>(dropped);
+      for (int base = static_cast<int>(c0); base < newChars; base += 64) {
+        Lane<uint32_t> v;
+        FOR_LANES(l) {
+          const int c = base + l;
+          uint32_t shift = 0, before = 0;
+          for (int k = 0; k < cnt; k++) {
+            if ((dropMask >> k) & 1u) {
+              const uint32_t ks = uni(s->tmp[k]), kl = uni(s->tmp[kMaxNodes + k]);
+              if (static_cast<uint32_t>(c) >= ks - before) shift += kl;
+              before += kl;
+            }
+          }
+          LANE(v) = c < newChars ? s->chars[c + static_cast<int>(shift)] : 0u;
+        }
+        waveSync();
+        FOR_LANES(l) {
+          if (base + l < newChars) s->chars[base + l] = static_cast<uint16_t>(LANE(v));
+        }
+        waveSync();
       }
-      deleteLeafAt(j);
+      nChars = newChars;
     }
+    deleteLeaves(first, cnt, mergeMask | dropMask);
     stamp(kPfZDelete);
     return kept;
   }

@@ -142,6 +142,11 @@ FMT_DEV Lane<int32_t> waveExclusiveMax(const Lane<int32_t>& x, int32_t init) {
 
 #endif
 
+// Lane l receives lane src[l] of x (ds_bpermute_b32: a crossbar shuffle through the LDS unit).
+FMT_DEV Lane<uint32_t> gather(const Lane<uint32_t>& x, const Lane<int>& src) {
+  return Lane<uint32_t>{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src.v << 2, static_cast<int>(x.v)))};
+}
+
 FMT_DEV void waveSync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -222,6 +227,12 @@ inline Lane<int32_t> waveExclusiveMax(const Lane<int32_t>& x, int32_t init) {
     if (l == 0) acc = x.v[0];
     else acc = acc > x.v[l] ? acc : x.v[l];
   }
+  return r;
+}
+
+inline Lane<uint32_t> gather(const Lane<uint32_t>& x, const Lane<int>& src) {
+  Lane<uint32_t> r;
+  for (int l = 0; l < 64; l++) r.v[l] = x.v[src.v[l] & 63];
   return r;
 }
 
