@@ -627,12 +627,17 @@ class Doc {
         cnt++;
       }
     }
-    for (int p = 0; p < nProps; p++) {
-      if (uni(s->props[p].n) != cnt) continue;
-      bool same = true;
-      for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-        if (i < cnt) same = same && uni(s->props[p].kv[i]) == kv[i];
-      if (same) return static_cast<uint32_t>(p);
+    {  // interned already? lane p checks prop set p (kPropCap <= 64: one ballot)
+      Lane<bool> same;
+      FOR_LANES(l) {
+        bool eq = l < nProps && s->props[l].n == cnt;
+#pragma unroll
+        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
+          if (i < cnt) eq = eq && s->props[l].kv[i] == kv[i];
+        LANE(same) = eq;
+      }
+      const uint64_t m = ballot(same);
+      if (m != 0) return static_cast<uint32_t>(ctz64(m));
     }
     if (nProps >= kPropCap) {
       fail(FMT_E_CAPACITY);
@@ -717,23 +722,21 @@ class Doc {
     }
   }
 
-  // addToLRUSet for every hit leaf in document order. Leaf blocks are contiguous runs, so only a
-  // hit whose block differs from the previous hit's can register.
+  // addToLRUSet for every hit leaf in document order. Leaf blocks are contiguous runs, so only the
+  // first hit of each block can register: take the first remaining hit, register its block, clear
+  // that block's hits, repeat (one pass per distinct block instead of one step per hit leaf).
   FMT_DEV void lruForHits(const Lane<uint32_t>& hits, int seq, int nr) {
-    int prevBlk = -1;
-    for (int r = 0; r < nr; r++) {
-      Lane<bool> p;
-      FOR_LANES(l) { LANE(p) = ((LANE(hits) >> r) & 1u) != 0; }
-      uint64_t m = ballot(p);
-      while (m) {
-        const int j = r * 64 + ctz64(m);
-        m &= m - 1;
-        const int b = static_cast<int>(fBlk(readField(j, 0)));
-        if (b != prevBlk) {
-          lruForLeaf(j, b, seq);
-          if (status != FMT_OK) return;
+    Lane<uint32_t> todo = hits;
+    for (;;) {
+      const int j = firstSet(todo, nr);
+      if (j < 0) return;
+      const uint32_t b = fBlk(readField(j, 0));
+      lruForLeaf(j, static_cast<int>(b), seq);
+      if (status != FMT_OK) return;
+      FOR_ROWS(r, 0, nr) {
+        FOR_LANES(l) {
+          if (fBlk(LANE(W[0])[r]) == b) LANE(todo) &= ~(1u << r);
         }
-        prevBlk = b;
       }
     }
   }
