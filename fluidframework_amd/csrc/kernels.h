@@ -35,15 +35,20 @@ struct MtDeviceOut {
   fmt_mt_catchup_range* catchup;  // slabs at catchupOffsets, or nullptr
 };
 
-// Per-document capacities of the LDS-resident engine.
+// Per-document capacities of the small (LDS-text) and large (HBM-text) engine tiers.
 struct MtCaps {
   uint32_t leaves, chars, props;
 };
-MtCaps mergeTreeCaps();
+MtCaps mergeTreeCaps(bool large);
 
-// Replays documents docList[0..count) (or all docs when docList == nullptr).
+// Small tier: replays documents docList[0..count) (or all docs when docList == nullptr); documents
+// that overflow it are listed in esc (esc[0] = count, then ids) when esc != nullptr.
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, int numCUs, hipStream_t stream, bool obliterate);
+                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate);
+
+// Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
+hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

@@ -14,20 +14,26 @@
 
 namespace fmt_kernels {
 
-constexpr int kMtWaves = 4;
+constexpr int kMtWaves = 4;     // small tier: 4 documents per workgroup, 2 waves/SIMD
+constexpr int kMtWavesLarge = 1;  // large tier: one document per workgroup, 1 wave/SIMD (VGPRs)
 
 // Diagnostic build only: per-phase shader-clock totals summed over all waves (mt_engine.h stamp()).
 __device__ unsigned long long g_mtProfile[fmt_mt::kPfCount];
 
-template <bool Ob>
-__global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
-                                                                 const uint32_t* __restrict__ docList,
-                                                                 uint32_t count) {
+// Small tier over all documents (docList == nullptr) or a list; documents that overflow it are
+// appended to esc (esc[0] = count, esc[1..] = document ids) for the large-tier pass. The large tier
+// runs over that list, writing leaves/chars/props to slab i of the list (headers stay per doc).
+template <bool Ob, class C, int Waves, int WavesPerEU>
+__global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
+                                                                      const uint32_t* __restrict__ docList,
+                                                                      uint32_t count, uint32_t* esc) {
+  using Doc = fmt_mt::Doc<Ob, C>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
-  fmt_mt::Scratch* scratch = reinterpret_cast<fmt_mt::Scratch*>(lds) + wave;
-  for (uint32_t i = blockIdx.x * kMtWaves + wave; i < count; i += gridDim.x * kMtWaves) {
+  fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds) + wave;
+  for (uint32_t i = blockIdx.x * Waves + wave; i < count; i += gridDim.x * Waves) {
     const uint32_t d = docList ? docList[i] : i;
+    const size_t slot = C::kHbmChars ? i : d;
     fmt_mt::DocInputs in;
     in.ops = batch.ops;
     in.begin = batch.docOpOffsets[d];
@@ -54,9 +60,9 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
     }
     fmt_mt::DocOutputs o;
     o.header = out.headers + d;
-    o.leaves = out.leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;
-    o.chars = out.chars + static_cast<size_t>(d) * fmt_mt::kCapChars;
-    o.props = out.props + static_cast<size_t>(d) * fmt_mt::kPropCap;
+    o.leaves = out.leaves + slot * Doc::kCapLeaves;
+    o.chars = out.chars + slot * Doc::kCapChars;
+    o.props = out.props + slot * Doc::kPropCap;
     if (batch.catchupOffsets) {
       const uint64_t c0 = batch.catchupOffsets[d], c1 = batch.catchupOffsets[d + 1];
       o.catchup = out.catchup + c0;
@@ -65,9 +71,13 @@ __global__ __launch_bounds__(64 * kMtWaves, 2) void mergeTreeKernel(MtDeviceBatc
       o.catchup = nullptr;
       o.catchupCap = 0;
     }
-    fmt_mt::Doc<Ob> doc;
+    Doc doc;
     doc.s = scratch;
     doc.run(in, o);
+    if (esc != nullptr && doc.status == FMT_E_CAPACITY && (threadIdx.x & 63) == 0) {
+      const uint32_t k = atomicAdd(esc, 1u);
+      esc[1 + k] = d;
+    }
 #if FMT_PROFILE && FMT_GPU
     if ((threadIdx.x & 63) == 0)
       for (int c = 0; c < fmt_mt::kPfCount; c++) atomicAdd(&g_mtProfile[c], static_cast<unsigned long long>(doc.prof[c]));
@@ -86,29 +96,43 @@ int mergeTreeProfile(uint64_t* out, int n, bool reset) {
   return fmt_mt::kPfCount;
 }
 
-MtCaps mergeTreeCaps() {
-  return MtCaps{static_cast<uint32_t>(fmt_mt::kCapLeaves), static_cast<uint32_t>(fmt_mt::kCapChars),
-                static_cast<uint32_t>(fmt_mt::kPropCap)};
+MtCaps mergeTreeCaps(bool large) {
+  if (large)
+    return MtCaps{static_cast<uint32_t>(fmt_mt::Doc<false, fmt_mt::LargeTier>::kCapLeaves),
+                  static_cast<uint32_t>(fmt_mt::LargeTier::kCapChars), static_cast<uint32_t>(fmt_mt::LargeTier::kPropCap)};
+  return MtCaps{static_cast<uint32_t>(fmt_mt::Doc<false, fmt_mt::SmallTier>::kCapLeaves),
+                static_cast<uint32_t>(fmt_mt::SmallTier::kCapChars), static_cast<uint32_t>(fmt_mt::SmallTier::kPropCap)};
+}
+
+template <bool Ob, class C, int Waves, int WavesPerEU>
+static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                             uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream) {
+  const size_t lds = sizeof(fmt_mt::Scratch<C>) * Waves;
+  // One resident wave of workgroups: every workgroup strides over the same number of documents,
+  // so none waits behind the residency limit (VGPRs cap the small tier at 2 waves/SIMD).
+  int blocksPerCU = 0;
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<Ob, C, Waves, WavesPerEU>, 64 * Waves, lds);
+  if (e != hipSuccess) return e;
+  const uint32_t wanted = (count + Waves - 1) / Waves;
+  const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
+  const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
+  hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
+                     docList, count, esc);
+  return hipGetLastError();
 }
 
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, int numCUs, hipStream_t stream, bool obliterate) {
-  const size_t lds = sizeof(fmt_mt::Scratch) * kMtWaves;
-  // One resident wave of workgroups: every workgroup strides over the same number of documents,
-  // so none waits behind the residency limit (VGPRs cap this kernel at 2 waves/SIMD).
-  int blocksPerCU = 0;
-  const hipError_t e = obliterate
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<true>, 64 * kMtWaves, lds)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<false>, 64 * kMtWaves, lds);
-  if (e != hipSuccess) return e;
-  const uint32_t wanted = (count + kMtWaves - 1) / kMtWaves;
-  const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
-  const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
+                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate) {
+  if (obliterate) return launchTier<true, fmt_mt::SmallTier, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+  return launchTier<false, fmt_mt::SmallTier, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+}
+
+hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate) {
   if (obliterate)
-    hipLaunchKernelGGL(mergeTreeKernel<true>, dim3(grid), dim3(64 * kMtWaves), lds, stream, batch, out, docList, count);
-  else
-    hipLaunchKernelGGL(mergeTreeKernel<false>, dim3(grid), dim3(64 * kMtWaves), lds, stream, batch, out, docList, count);
-  return hipGetLastError();
+    return launchTier<true, fmt_mt::LargeTier, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+  return launchTier<false, fmt_mt::LargeTier, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
 }
 
 }  // namespace fmt_kernels

@@ -34,34 +34,63 @@
 
 namespace fmt_mt {
 
-constexpr int kRows = 8;                // rows of 64 leaves (one V8 element per row)
-constexpr int kCapLeaves = 64 * kRows;  // 512
-constexpr int kCapChars = 2048;      // UTF-16 units per document (tombstones included)
-constexpr int kMaxBlocks = 128;
-constexpr int kHeapCap = 255;
-constexpr int kPropCap = 32;
 constexpr int kMaxClient = 31;       // remove-client set is a 32-bit mask
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
 constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:21)
 constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
-constexpr uint32_t kNoBlk = 0xFF;
-constexpr uint32_t kPropsUndef = 0xFF;
 constexpr int32_t kNotRemoved = 0x7fffffff;
+
+// Capacity tiers. Every document first replays in the small tier (leaves in 40 VGPRs, text in
+// LDS, 2 waves/SIMD). A document that overflows it (FMT_E_CAPACITY) is replayed again from its
+// inputs in the large tier: 32 register rows (2048 leaves in 160 VGPRs, 1 wave/SIMD), 10-bit
+// block ids, and the text in the document's HBM output slab instead of LDS. Same engine source.
+// W0 = len | block << kLenBits | props << (kLenBits + kBlkBits).
+struct SmallTier {
+  static constexpr int kRows = 8;          // rows of 64 leaves (one VR element per row)
+  static constexpr int kCapChars = 2048;   // UTF-16 units per document (tombstones included)
+  static constexpr int kMaxBlocks = 128;
+  static constexpr int kHeapCap = 255;
+  static constexpr int kPropCap = 32;
+  static constexpr int kLenBits = 16, kBlkBits = 8;  // props: the remaining 8 bits
+  static constexpr bool kHbmChars = false;
+  static constexpr bool kUnroll = true;     // rows are compile-time VGPR elements
+  using BId = uint8_t;
+  using VR = V8;
+};
+
+struct LargeTier {
+  static constexpr int kRows = 32;
+  static constexpr int kCapChars = 131071;  // a leaf length (17 bits) can hold all of them
+  static constexpr int kMaxBlocks = 1023;   // ids 0..1022; 1023 = no block
+  static constexpr int kHeapCap = 1023;     // at most one heap entry per block (needsScour)
+  static constexpr int kPropCap = 31;       // ids 0..30; 31 = properties undefined
+  static constexpr int kLenBits = 17, kBlkBits = 10;  // props: the remaining 5 bits
+  static constexpr bool kHbmChars = true;
+  static constexpr bool kUnroll = false;    // rows indexed at run time (private memory)
+  using BId = uint16_t;
+  using VR = V32;
+};
 
 // Uniform row loops: unrolled so that the row is a compile-time V8 element, with a wave-uniform
 // guard so rows outside [lo, hi) cost one scalar branch.
 #define FMT_PRAGMA(x) _Pragma(#x)
-#define FOR_ROWS(r, lo, hi) \
-  FMT_PRAGMA(unroll) for (int r = 0; r < kRows; r++) if (r >= (lo) && r < (hi))
-#define FOR_ROWS_DOWN(r, lo, hi) \
-  FMT_PRAGMA(unroll) for (int r = kRows - 1; r >= 0; r--) if (r >= (lo) && r < (hi))
+// (Large tier: rolled loops over exactly [lo, hi), rows indexed at run time.)
+#define FOR_ROWS(r, lo, hi)                                                                            \
+  FMT_PRAGMA(unroll kRowUnroll)                                                                      \
+  for (int r = kRowUnroll > 1 ? 0 : (lo); r < (kRowUnroll > 1 ? kRows : ((hi) < kRows ? (hi) : kRows)); r++) \
+    if (r >= (lo) && r < (hi))
+#define FOR_ROWS_DOWN(r, lo, hi)                                                                          \
+  FMT_PRAGMA(unroll kRowUnroll)                                                                        \
+  for (int r = kRowUnroll > 1 ? kRows - 1 : ((hi) < kRows ? (hi) : kRows) - 1; r >= (kRowUnroll > 1 ? 0 : (lo)); r--) \
+    if (r >= (lo) && r < (hi))
 
+template <class BId>
 struct Blk {
   uint8_t count;
-  uint8_t parent;
+  BId parent;
   uint8_t leaf;        // children are leaves
   int8_t needsScour;   // -1 undefined, 0 false, 1 true
-  uint8_t child[kMaxNodes];
+  BId child[kMaxNodes];
 };
 
 struct HeapEnt {
@@ -82,24 +111,21 @@ struct ObEnt {
   int32_t seq, client;
 };
 
-// Per-wave LDS state.
+// Per-wave LDS state (the large tier keeps its text in HBM: chars[] is then a stub).
+template <class C>
 struct Scratch {
-  uint16_t chars[kCapChars];
-  Blk blk[kMaxBlocks];
-  HeapEnt heap[kHeapCap + 1];  // 1-based
-  PropSet props[kPropCap];
-  uint8_t freeList[kMaxBlocks];
+  uint16_t chars[C::kHbmChars ? 2 : C::kCapChars];
+  Blk<typename C::BId> blk[C::kMaxBlocks];
+  HeapEnt heap[C::kHeapCap + 1];  // 1-based
+  PropSet props[C::kPropCap];
+  typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
   uint8_t obSeq[kObCap];     // Obliterates.seqOrdered: slots in seq order
   uint8_t obStart[kObCap];   // Obliterates.startOrdered: slots in SortedSegmentSet order
 };
 
-// Leaf word fields.
-FMT_DEV uint32_t fLen(uint32_t w0) { return w0 & 0xFFFFu; }
-FMT_DEV uint32_t fBlk(uint32_t w0) { return (w0 >> 16) & 0xFFu; }
-FMT_DEV uint32_t fProps(uint32_t w0) { return w0 >> 24; }
-FMT_DEV uint32_t mkW0(uint32_t len, uint32_t blk, uint32_t props) { return len | (blk << 16) | (props << 24); }
+// Leaf word fields (W0's packing is per tier, see Doc).
 FMT_DEV uint32_t fId(uint32_t w4) { return w4 & 0xFFFFFFu; }
 FMT_DEV int32_t fClient(uint32_t w4) { return static_cast<int32_t>(static_cast<int8_t>(w4 >> 24)); }
 FMT_DEV uint32_t mkW4(uint32_t id, int32_t client) { return (id & 0xFFFFFFu) | (static_cast<uint32_t>(client & 0xFF) << 24); }
@@ -125,7 +151,7 @@ struct DocInputs {
 struct DocOutputs {
   fmt_mt_doc_result* header;
   fmt_mt_leaf* leaves;    // kCapLeaves entries
-  uint16_t* chars;        // kCapChars entries
+  uint16_t* chars;        // kCapChars entries (the large tier's working text)
   fmt_mt_propset* props;  // kPropCap entries
   fmt_mt_catchup_range* catchup;  // catchupCap entries (nullptr: no FMT_MT_F_CATCHUP ops)
   uint32_t catchupCap;
@@ -142,9 +168,30 @@ enum ProfCat {
 
 // Ob: the engine variant that also replays obliterates (f1). Without obliterates in a batch the
 // runtime launches Doc<false>, whose code is exactly the obliterate-free engine.
-template <bool Ob>
+template <bool Ob, class C = SmallTier>
 class Doc {
  public:
+  using VR = typename C::VR;
+  using BId = typename C::BId;
+  static constexpr int kRows = C::kRows;
+  static constexpr int kRowUnroll = C::kUnroll ? C::kRows : 1;
+  static constexpr int kCapLeaves = 64 * kRows;
+  static constexpr int kCapChars = C::kCapChars;
+  static constexpr int kMaxBlocks = C::kMaxBlocks;
+  static constexpr int kHeapCap = C::kHeapCap;
+  static constexpr int kPropCap = C::kPropCap;
+  static constexpr uint32_t kLenMask = (1u << C::kLenBits) - 1u;
+  static constexpr uint32_t kNoBlk = (1u << C::kBlkBits) - 1u;
+  static constexpr uint32_t kPropsUndef = (1u << (32 - C::kLenBits - C::kBlkBits)) - 1u;
+  static_assert(kMaxBlocks <= static_cast<int>(kNoBlk) && kPropCap <= static_cast<int>(kPropsUndef), "W0 field widths");
+  static_assert(kRows <= 32, "row bitmasks are 32-bit");
+  FMT_DEV static uint32_t fLen(uint32_t w0) { return w0 & kLenMask; }
+  FMT_DEV static uint32_t fBlk(uint32_t w0) { return (w0 >> C::kLenBits) & kNoBlk; }
+  FMT_DEV static uint32_t fProps(uint32_t w0) { return w0 >> (C::kLenBits + C::kBlkBits); }
+  FMT_DEV static uint32_t mkW0(uint32_t len, uint32_t blk, uint32_t props) {
+    return len | (blk << C::kLenBits) | (props << (C::kLenBits + C::kBlkBits));
+  }
+
 #if FMT_PROFILE && FMT_GPU
   uint64_t profT = 0;
   uint64_t prof[kPfCount] = {};
@@ -156,8 +203,9 @@ class Doc {
 #else
   FMT_DEV void stamp(int) {}
 #endif
-  Lane<V8> W[5];  // W[f] element r of lane l = field f of leaf 64 r + l
-  Scratch* s;
+  Lane<VR> W[5];  // W[f] element r of lane l = field f of leaf 64 r + l
+  Scratch<C>* s;
+  uint16_t* gch = nullptr;  // large tier: the document's text, in its HBM output slab
   int n = 0;          // leaves
   int nChars = 0;
   int root = 0;
@@ -184,18 +232,22 @@ class Doc {
   // and every pass below visits rows [0, rows()) only, so its cost follows the live leaf count.
   FMT_DEV int rows() const { return (n + 63) >> 6; }
 
-  FMT_DEV static Lane<uint32_t> row(const Lane<V8>& a, int r) {  // r compile-time after unrolling
+  FMT_DEV static Lane<uint32_t> row(const Lane<VR>& a, int r) {  // r compile-time after unrolling
     Lane<uint32_t> x;
     FOR_LANES(l) { LANE(x) = LANE(a)[r]; }
     return x;
   }
 
-  FMT_DEV static Lane<uint32_t> selectRow(const Lane<V8>& arr, int r) {  // r wave-uniform, dynamic
+  FMT_DEV static Lane<uint32_t> selectRow(const Lane<VR>& arr, int r) {  // r wave-uniform, dynamic
     Lane<uint32_t> x;
     FOR_LANES(l) {
-      V8 t = LANE(arr);
-      launder(t);  // keep the dynamic index on a register value (v_movrels), never a scratch GEP
-      LANE(x) = t[r];
+      if constexpr (C::kUnroll) {
+        VR t = LANE(arr);
+        launder(t);  // keep the dynamic index on a register value (v_movrels), never a scratch GEP
+        LANE(x) = t[r];
+      } else {
+        LANE(x) = LANE(arr)[r];
+      }
     }
     return x;
   }
@@ -302,7 +354,7 @@ class Doc {
 
   // Exclusive prefix (document order) of per-leaf values over rows [0, nr); returns the total.
   // Rows >= nr of `excl` are left unset.
-  FMT_DEV static uint32_t scanRows(const Lane<V8>& vals, Lane<V8>& excl, int nr) {
+  FMT_DEV static uint32_t scanRows(const Lane<VR>& vals, Lane<VR>& excl, int nr) {
     uint32_t base = 0;
     FOR_ROWS(r, 0, nr) {
       uint32_t tot;
@@ -316,7 +368,7 @@ class Doc {
   // Visible length of every leaf from PriorPerspective(refSeq, client) (perspective.ts:80-93).
   // Leaves removed at/below minSeq are never present for such a perspective (refSeq >= minSeq).
   // Empty slots have length 0.
-  FMT_DEV void visLengths(int refSeq, int client, Lane<V8>& vis, int nr) const {
+  FMT_DEV void visLengths(int refSeq, int client, Lane<VR>& vis, int nr) const {
     FOR_ROWS(r, 0, nr) {
       FOR_LANES(l) {
         const uint32_t w0 = LANE(W[0])[r];
@@ -331,8 +383,8 @@ class Doc {
   }
 
   // Char offset of every leaf (all leaves, tombstones included).
-  FMT_DEV void charStarts(Lane<V8>& cst, int nr) const {
-    Lane<V8> lens;
+  FMT_DEV void charStarts(Lane<VR>& cst, int nr) const {
+    Lane<VR> lens;
     FOR_ROWS(r, 0, nr) {
       FOR_LANES(l) { LANE(lens)[r] = fLen(LANE(W[0])[r]); }
     }
@@ -357,7 +409,7 @@ class Doc {
 
   FMT_DEV uint32_t charStartOf(int j) const {
     if (j >= n) return static_cast<uint32_t>(nChars);
-    Lane<V8> cst;
+    Lane<VR> cst;
     charStarts(cst, (j >> 6) + 1);
     return readlane(selectRow(cst, j >> 6), j & 63);
   }
@@ -396,19 +448,29 @@ class Doc {
     return -1;
   }
 
-  // ------------------------------------------------------------------ chars (LDS, doc order)
+  // ------------------------------------------------------------------ chars (doc order)
+  // Small tier: LDS. Large tier: the document's HBM output slab (written by this wave only).
+  FMT_DEV uint32_t chRead(int i) const {
+    if constexpr (C::kHbmChars) return loadCoherent(gch + i);
+    else return s->chars[i];
+  }
+  FMT_DEV void chWrite(int i, uint32_t v) {
+    if constexpr (C::kHbmChars) gch[i] = static_cast<uint16_t>(v);
+    else s->chars[i] = static_cast<uint16_t>(v);
+  }
+
   FMT_DEV void charsShiftUp(int from, int by) {  // chars[from..nChars) → chars[from+by..)
     const int count = nChars - from;
     for (int top = count - 1; top >= 0; top -= 64) {
       Lane<uint32_t> v;
       FOR_LANES(l) {
         const int t = top - l;
-        LANE(v) = t >= 0 ? s->chars[from + t] : 0u;
+        LANE(v) = t >= 0 ? chRead(from + t) : 0u;
       }
       waveSync();
       FOR_LANES(l) {
         const int t = top - l;
-        if (t >= 0) s->chars[from + t + by] = static_cast<uint16_t>(LANE(v));
+        if (t >= 0) chWrite(from + t + by, LANE(v));
       }
       waveSync();
     }
@@ -419,12 +481,12 @@ class Doc {
       Lane<uint32_t> v;
       FOR_LANES(l) {
         const int t = base + l;
-        LANE(v) = t < nChars ? s->chars[t] : 0u;
+        LANE(v) = t < nChars ? chRead(t) : 0u;
       }
       waveSync();
       FOR_LANES(l) {
         const int t = base + l;
-        if (t < nChars) s->chars[t - by] = static_cast<uint16_t>(LANE(v));
+        if (t < nChars) chWrite(t - by, LANE(v));
       }
       waveSync();
     }
@@ -443,7 +505,7 @@ class Doc {
       return -1;
     }
     const int id = s->freeList[--nFree];
-    Blk& b = s->blk[id];
+    auto& b = s->blk[id];
     b.count = 0;
     b.parent = kNoBlk;
     b.leaf = leafType;
@@ -453,7 +515,7 @@ class Doc {
   }
 
   FMT_DEV void freeBlk(int id) {
-    s->freeList[nFree++] = static_cast<uint8_t>(id);
+    s->freeList[nFree++] = static_cast<BId>(id);
     waveSync();
   }
 
@@ -489,8 +551,8 @@ class Doc {
       } else {
         for (int i = 0; i < half; i++) {
           const int c = uni(static_cast<int>(s->blk[b].child[half + i]));
-          s->blk[nb].child[i] = static_cast<uint8_t>(c);
-          s->blk[c].parent = static_cast<uint8_t>(nb);
+          s->blk[nb].child[i] = static_cast<BId>(c);
+          s->blk[c].parent = static_cast<BId>(nb);
         }
       }
       s->blk[b].count = half;
@@ -501,10 +563,10 @@ class Doc {
         const int r = allocBlk(0);
         if (r < 0) return;
         s->blk[r].count = 2;
-        s->blk[r].child[0] = static_cast<uint8_t>(b);
-        s->blk[r].child[1] = static_cast<uint8_t>(nb);
-        s->blk[b].parent = static_cast<uint8_t>(r);
-        s->blk[nb].parent = static_cast<uint8_t>(r);
+        s->blk[r].child[0] = static_cast<BId>(b);
+        s->blk[r].child[1] = static_cast<BId>(nb);
+        s->blk[b].parent = static_cast<BId>(r);
+        s->blk[nb].parent = static_cast<BId>(r);
         waveSync();
         root = r;
         return;
@@ -515,10 +577,10 @@ class Doc {
       for (int i = pc; i > idx + 1; i--) {
         const int c = uni(static_cast<int>(s->blk[p].child[i - 1]));
         waveSync();
-        s->blk[p].child[i] = static_cast<uint8_t>(c);
+        s->blk[p].child[i] = static_cast<BId>(c);
       }
-      s->blk[p].child[idx + 1] = static_cast<uint8_t>(nb);
-      s->blk[nb].parent = static_cast<uint8_t>(p);
+      s->blk[p].child[idx + 1] = static_cast<BId>(nb);
+      s->blk[nb].parent = static_cast<BId>(p);
       s->blk[p].count = static_cast<uint8_t>(pc + 1);
       waveSync();
       cnt = pc + 1;
@@ -763,7 +825,7 @@ class Doc {
   }
 
   // The leaf that strictly contains view position pos (st < pos < st + vis), or -1; *stOut = its st.
-  FMT_DEV static int containing(const Lane<V8>& vis, const Lane<V8>& st, int pos, int nr, int* stOut) {
+  FMT_DEV static int containing(const Lane<VR>& vis, const Lane<VR>& st, int pos, int nr, int* stOut) {
     FOR_ROWS(r, 0, nr) {
       Lane<bool> p;
       FOR_LANES(l) {
@@ -784,7 +846,7 @@ class Doc {
   // remove/annotate resolve their boundaries from their one view scan instead.)
   FMT_DEV bool splitAt(int pos, int refSeq, int client) {
     const int nr = rows();
-    Lane<V8> vis, st;
+    Lane<VR> vis, st;
     visLengths(refSeq, client, vis, nr);
     scanRows(vis, st, nr);
     stamp(kPfScan);
@@ -823,7 +885,7 @@ class Doc {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
     const int pos = op.pos1, len = op.len;
     const int nr = rows();
-    Lane<V8> vis, st;
+    Lane<VR> vis, st;
     visLengths(refSeq, client, vis, nr);
     const uint32_t total = scanRows(vis, st, nr);
     stamp(kPfScan);
@@ -865,8 +927,8 @@ class Doc {
     const int cpos = static_cast<int>(charOffsetOf(insIdx));
     charsShiftUp(cpos, len);
     FOR_LANES(l) {
-      if (l < len) s->chars[cpos + l] = static_cast<uint16_t>(LANE(text0));
-      for (int t = l + 64; t < len; t += 64) s->chars[cpos + t] = in.text[op.payload + t];
+      if (l < len) chWrite(cpos + l, LANE(text0));
+      for (int t = l + 64; t < len; t += 64) chWrite(cpos + t, in.text[op.payload + t]);
     }
     waveSync();
     nChars += len;
@@ -1093,7 +1155,7 @@ class Doc {
       // and nodeMap's hit set (:2961-3020, leaves of positive view length inside [start, end)):
       // a split moves no view start, it only adds a leaf whose view start is the boundary.
       nr = rows();
-      Lane<V8> vis, st;
+      Lane<VR> vis, st;
       visLengths(refSeq, client, vis, nr);
       scanRows(vis, st, nr);
       stamp(kPfScan);
@@ -1121,7 +1183,7 @@ class Doc {
       if (!splitAt(op.pos1, refSeq, client)) return false;
       if (!splitAt(op.pos2, refSeq, client)) return false;
       nr = rows();
-      Lane<V8> vis, st;
+      Lane<VR> vis, st;
       visLengths(refSeq, client, vis, nr);
       scanRows(vis, st, nr);
       stamp(kPfScan);
@@ -1211,7 +1273,7 @@ class Doc {
     if (cnt == 0) return 0;
     const int first = firstLeafOf(static_cast<uint32_t>(b));
     // One pass packs what the decisions need for every leaf of the block (at most 2 rows):
-    // len | props << 16 | removed << 24 | removed at/below minSeq << 25 | insert at/below minSeq << 26
+    // len | props << kLenBits | removed << 24 | removed at/below minSeq << 25 | insert at/below minSeq << 26
     const int r0 = first >> 6, r1 = (first + cnt - 1) >> 6;
     Lane<uint32_t> pk0, pk1;
     FOR_LANES(l) {
@@ -1222,7 +1284,7 @@ class Doc {
       FOR_LANES(l) {
         const uint32_t w0 = LANE(W[0])[r];
         const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]), rm = static_cast<int32_t>(LANE(W[2])[r]);
-        const uint32_t p = fLen(w0) | (fProps(w0) << 16) | (rm != kNotRemoved ? 1u << 24 : 0u) |
+        const uint32_t p = fLen(w0) | (fProps(w0) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
                            (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u);
         if (r == r0) LANE(pk0) = p;
         else LANE(pk1) = p;
@@ -1239,12 +1301,12 @@ class Doc {
     for (int k = 0; k < cnt; k++) {
       const int j = first + k;
       const uint32_t p = (j >> 6) == r0 ? readlane(pk0, j & 63) : readlane(pk1, j & 63);
-      const uint32_t len = p & 0xFFFFu, props = (p >> 16) & 0xFFu;
+      const uint32_t len = p & kLenMask, props = (p >> C::kLenBits) & kPropsUndef;
       s->tmp[k] = cs;  // char offset and length, for the deletions below
       s->tmp[kMaxNodes + k] = len;
       if (((p >> 24) & 1u) == 0) {
         if ((p >> 26) & 1u) {
-          const bool lastNl = len > 0 && uni(static_cast<uint32_t>(s->chars[cs + len - 1])) == 10u;
+          const bool lastNl = len > 0 && uni(chRead(static_cast<int>(cs + len - 1))) == 10u;
           const bool canAppend = prev >= 0 && !prevNl &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) ||
                                   len <= static_cast<uint32_t>(kGranularity)) &&
@@ -1303,11 +1365,11 @@ class Doc {
               before += kl;
             }
           }
-          LANE(v) = c < newChars ? s->chars[c + static_cast<int>(shift)] : 0u;
+          LANE(v) = c < newChars ? chRead(c + static_cast<int>(shift)) : 0u;
         }
         waveSync();
         FOR_LANES(l) {
-          if (base + l < newChars) s->chars[base + l] = static_cast<uint16_t>(LANE(v));
+          if (base + l < newChars) chWrite(base + l, LANE(v));
         }
         waveSync();
       }
@@ -1340,17 +1402,17 @@ class Doc {
         const int id = allocBlk(leafLevel ? 1 : 0);
         if (id < 0) return;
         s->blk[id].count = static_cast<uint8_t>(cnt);
-        s->blk[id].parent = static_cast<uint8_t>(p);
+        s->blk[id].parent = static_cast<BId>(p);
         if (leafLevel) {
           tagLeaves(firstLeaf + consumed, cnt, static_cast<uint32_t>(id));
         } else {
           for (int k = 0; k < cnt; k++) {
             const int g = uni(static_cast<int>(s->tmp[consumed + k]));
-            s->blk[id].child[k] = static_cast<uint8_t>(g);
-            s->blk[g].parent = static_cast<uint8_t>(id);
+            s->blk[id].child[k] = static_cast<BId>(g);
+            s->blk[g].parent = static_cast<BId>(id);
           }
         }
-        s->blk[p].child[q] = static_cast<uint8_t>(id);
+        s->blk[p].child[q] = static_cast<BId>(id);
         waveSync();
         consumed += cnt;
       }
@@ -1439,7 +1501,7 @@ class Doc {
     obStartN = 0;
     obUsed = 0;
     FOR_LANES(l) {
-      V8 z;
+      VR z;
 #pragma unroll
       for (int r = 0; r < kRows; r++) z[r] = 0u;
       LANE(W[0]) = z;
@@ -1449,7 +1511,7 @@ class Doc {
       LANE(W[4]) = z;
     }
     FOR_LANES(l) {
-      for (int i = l; i < kMaxBlocks; i += 64) s->freeList[i] = static_cast<uint8_t>(kMaxBlocks - 1 - i);
+      for (int i = l; i < kMaxBlocks; i += 64) s->freeList[i] = static_cast<BId>(kMaxBlocks - 1 - i);
     }
     waveSync();
     nFree = kMaxBlocks;
@@ -1461,13 +1523,13 @@ class Doc {
   FMT_DEV void loadInitial() {
     const int len = static_cast<int>(in.initLen);
     if (len == 0) return;
-    if (len > kCapChars || len > 0xFFFF) {
+    if (len > kCapChars || static_cast<uint32_t>(len) > kLenMask) {
       fail(FMT_E_CAPACITY);
       return;
     }
     const uint16_t* src = in.text + in.initOff;
     FOR_LANES(l) {
-      for (int t = l; t < len; t += 64) s->chars[t] = src[t];
+      for (int t = l; t < len; t += 64) chWrite(t, src[t]);
     }
     waveSync();
     nChars = len;
@@ -1497,7 +1559,7 @@ class Doc {
   // so block ids are handed out in order: level by level, leaf blocks first.
   FMT_DEV void appendLoadedChars(uint32_t off, uint32_t len) {
     FOR_LANES(l) {
-      for (uint32_t t = l; t < len; t += 64) s->chars[nChars + static_cast<int>(t)] = in.text[off + t];
+      for (uint32_t t = l; t < len; t += 64) chWrite(nChars + static_cast<int>(t), in.text[off + t]);
     }
     waveSync();
     nChars += static_cast<int>(len);
@@ -1556,17 +1618,21 @@ class Doc {
     }
     // Every loaded leaf in one row pass (lengths staged through the still-unused char area); slots
     // past N stay all-zero. Header leaf j belongs to leaf block j / 7, body leaves get theirs below.
+    // (the large tier reads the lengths straight from the segment records)
     uint32_t* stage = reinterpret_cast<uint32_t*>(s->chars);
-    FOR_LANES(l) {
-      for (int j = l; j < N; j += 64) stage[j] = in.snapSegs[j].len;
+    if constexpr (!C::kHbmChars) {
+      FOR_LANES(l) {
+        for (int j = l; j < N; j += 64) stage[j] = in.snapSegs[j].len;
+      }
+      waveSync();
     }
-    waveSync();
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
       FOR_LANES(l) {
         const int j = r * 64 + l;
         const bool live = j < N;
-        LANE(W[0])[r] = live ? mkW0(stage[j], static_cast<uint32_t>(j < H ? j / 7 : 0), kPropsUndef) : 0u;
+        const uint32_t len = live ? (C::kHbmChars ? in.snapSegs[j].len : stage[j]) : 0u;
+        LANE(W[0])[r] = live ? mkW0(len, static_cast<uint32_t>(j < H ? j / 7 : 0), kPropsUndef) : 0u;
         LANE(W[2])[r] = live ? static_cast<uint32_t>(kNotRemoved) : 0u;
         LANE(W[4])[r] = live ? mkW4(static_cast<uint32_t>(j + 1), FMT_NON_COLLAB_CLIENT) : 0u;
       }
@@ -1577,7 +1643,7 @@ class Doc {
       int lo = 0, cnt = (H + 6) / 7;
       for (int b = 0; b < cnt; b++) {
         s->blk[b].count = static_cast<uint8_t>(H - 7 * b < 7 ? H - 7 * b : 7);
-        s->blk[b].parent = static_cast<uint8_t>(kNoBlk);
+        s->blk[b].parent = static_cast<BId>(kNoBlk);
         s->blk[b].leaf = 1;
         s->blk[b].needsScour = -1;
       }
@@ -1588,12 +1654,12 @@ class Doc {
           const int id = nlo + q;
           const int c = cnt - 7 * q < 7 ? cnt - 7 * q : 7;
           s->blk[id].count = static_cast<uint8_t>(c);
-          s->blk[id].parent = static_cast<uint8_t>(kNoBlk);
+          s->blk[id].parent = static_cast<BId>(kNoBlk);
           s->blk[id].leaf = 0;
           s->blk[id].needsScour = -1;
           for (int k = 0; k < c; k++) {
-            s->blk[id].child[k] = static_cast<uint8_t>(lo + 7 * q + k);
-            s->blk[lo + 7 * q + k].parent = static_cast<uint8_t>(id);
+            s->blk[id].child[k] = static_cast<BId>(lo + 7 * q + k);
+            s->blk[lo + 7 * q + k].parent = static_cast<BId>(id);
           }
         }
         waveSync();
@@ -1708,9 +1774,9 @@ class Doc {
   FMT_DEV void writeOutputs(const DocOutputs& out) {
     const int nr = rows();
     // char offsets and leaf-block ordinals
-    Lane<V8> cst;
+    Lane<VR> cst;
     charStarts(cst, nr);
-    Lane<V8> startFlag, ord;
+    Lane<VR> startFlag, ord;
     FOR_ROWS(r, 0, nr) {
       const Lane<uint32_t> cur = row(W[0], r);
       const Lane<uint32_t> up = shflUp1(cur);
@@ -1724,7 +1790,7 @@ class Doc {
     const uint32_t nLeafBlocks = scanRows(startFlag, ord, nr);
     uint32_t visible = 0;
     {
-      Lane<V8> vlen, tmp;
+      Lane<VR> vlen, tmp;
       FOR_ROWS(r, 0, nr) {
         FOR_LANES(l) {
           const bool live = static_cast<int32_t>(LANE(W[2])[r]) == kNotRemoved;
@@ -1753,7 +1819,8 @@ class Doc {
       }
     }
     FOR_LANES(l) {
-      for (int t = l; t < nChars; t += 64) out.chars[t] = s->chars[t];
+      if constexpr (!C::kHbmChars)
+        for (int t = l; t < nChars; t += 64) out.chars[t] = s->chars[t];
       for (int p = l; p < nProps; p += 64) {
         fmt_mt_propset ps;
         ps.n = s->props[p].n;
@@ -1794,6 +1861,7 @@ class Doc {
     cuOut = out.catchup;
     cuCap = out.catchup ? out.catchupCap : 0u;
     cuN = 0;
+    if constexpr (C::kHbmChars) gch = out.chars;
     init();
     if (in.loaded) loadSnapshot();
     else loadInitial();

@@ -68,6 +68,11 @@ struct fmt_ctx {
   DevBuf<fmt_mt_leaf> mtLeaves;
   DevBuf<uint16_t> mtChars;
   DevBuf<fmt_mt_propset> mtProps;
+  DevBuf<uint32_t> mtEsc;                    // small-tier overflow list: [0] = count, then doc ids
+  DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
+  DevBuf<uint16_t> mtBigChars;
+  DevBuf<fmt_mt_propset> mtBigProps;
+  std::vector<int32_t> mtBigSlot;            // doc -> large-tier slab, or -1
   DevBuf<fmt_mt_snapshot_doc> mtSnap;       // per-doc summary loads (f3)
   DevBuf<fmt_mt_snapshot_seg> mtSnapSegs;
   bool mtHasSnap = false;
@@ -149,6 +154,14 @@ void fmt_close(fmt_ctx* c) {
   c->mtLeaves.release();
   c->mtChars.release();
   c->mtProps.release();
+  c->mtEsc.release();
+  c->mtBigLeaves.release();
+  c->mtBigChars.release();
+  c->mtBigProps.release();
+  c->mtSnap.release();
+  c->mtSnapSegs.release();
+  c->mtCuOffs.release();
+  c->mtCatchup.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ownStream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -260,10 +273,12 @@ int fmt_map_replay_device(fmt_ctx* c, const fmt_map_op* dOps, const uint64_t* dO
 
 // ------------------------------------------------------------------------------ merge-tree
 int fmt_mt_capacity(uint32_t* maxLeaves, uint32_t* maxChars, uint32_t* maxProps) {
-  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps();
-  if (maxLeaves) *maxLeaves = caps.leaves;
-  if (maxChars) *maxChars = caps.chars;
-  if (maxProps) *maxProps = caps.props;
+  // A document is replayed in the large tier when it overflows the small one, so the limits are
+  // the large tier's (the small tier's prop-set table is one larger: report the larger).
+  const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true), small = fmt_kernels::mergeTreeCaps(false);
+  if (maxLeaves) *maxLeaves = big.leaves;
+  if (maxChars) *maxChars = big.chars;
+  if (maxProps) *maxProps = big.props > small.props ? big.props : small.props;
   return FMT_OK;
 }
 
@@ -314,7 +329,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       initChars += b->doc_init[2 * d + 1];
     }
   }
-  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps();
+  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(false);
   FMT_HIP(c, hipSetDevice(c->device));
   FMT_HIP(c, c->mtOps.reserve(b->n_ops));
   FMT_HIP(c, c->mtOffs.reserve(n + 1ull));
@@ -327,6 +342,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, c->mtLeaves.reserve(static_cast<size_t>(n) * caps.leaves));
   FMT_HIP(c, c->mtChars.reserve(static_cast<size_t>(n) * caps.chars));
   FMT_HIP(c, c->mtProps.reserve(static_cast<size_t>(n) * caps.props));
+  FMT_HIP(c, c->mtEsc.reserve(n + 1ull));
+  c->mtBigSlot.assign(n, -1);
   // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
   // any; a document that needs more reports FMT_E_CAPACITY.
   c->mtHasCatchup = catchupOps > 0;
@@ -385,8 +402,28 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr};
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr};
+  FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
-  FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->numCUs, c->stream, c->mtObliterate));
+  FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->mtEsc.p, c->numCUs, c->stream,
+                                          c->mtObliterate));
+  // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
+  uint32_t nEsc = 0;
+  FMT_HIP(c, hipMemcpyAsync(&nEsc, c->mtEsc.p, sizeof nEsc, hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  c->mtBigSlot.assign(c->mtDocs, -1);
+  if (nEsc > 0) {
+    const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true);
+    FMT_HIP(c, c->mtBigLeaves.reserve(static_cast<size_t>(nEsc) * big.leaves));
+    FMT_HIP(c, c->mtBigChars.reserve(static_cast<size_t>(nEsc) * big.chars));
+    FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
+    fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
+                                  c->mtHasCatchup ? c->mtCatchup.p : nullptr};
+    FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate));
+    std::vector<uint32_t> list(nEsc);
+    FMT_HIP(c, hipMemcpyAsync(list.data(), c->mtEsc.p + 1, nEsc * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < nEsc; i++) c->mtBigSlot[list[i]] = static_cast<int32_t>(i);
+  }
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   c->stats = fmt_stats{};
@@ -397,7 +434,7 @@ int fmt_mt_run(fmt_ctx* c) {
   c->stats.bytes_read = c->mtNOps * sizeof(fmt_mt_op) + (c->mtInsertChars + c->mtInitChars) * 2 +
                         (c->mtDocs + 1ull) * sizeof(uint64_t);
   c->stats.bytes_written = static_cast<uint64_t>(c->mtDocs) * sizeof(fmt_mt_doc_result);
-  c->stats.launches = 1;
+  c->stats.launches = nEsc > 0 ? 2 : 1;
   return FMT_OK;
 }
 
@@ -423,15 +460,20 @@ int fmt_mt_fetch_headers(fmt_ctx* c, fmt_mt_doc_result* out) {
 int fmt_mt_fetch_doc(fmt_ctx* c, uint32_t doc, fmt_mt_leaf* leaves, uint32_t capLeaves, uint16_t* chars,
                      uint32_t capChars, fmt_mt_propset* props, uint32_t capProps) {
   if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs) return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_doc: bad doc");
-  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps();
+  const int32_t slot = doc < c->mtBigSlot.size() ? c->mtBigSlot[doc] : -1;
+  const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(slot >= 0);
+  const size_t at = slot >= 0 ? static_cast<size_t>(slot) : doc;
+  const fmt_mt_leaf* dLeaves = slot >= 0 ? c->mtBigLeaves.p : c->mtLeaves.p;
+  const uint16_t* dChars = slot >= 0 ? c->mtBigChars.p : c->mtChars.p;
+  const fmt_mt_propset* dProps = slot >= 0 ? c->mtBigProps.p : c->mtProps.p;
   fmt_mt_doc_result h;
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
   const uint32_t nl = h.n_leaves < capLeaves ? h.n_leaves : capLeaves;
   const uint32_t nc = h.n_chars < capChars ? h.n_chars : capChars;
   const uint32_t np = h.n_props < capProps ? h.n_props : capProps;
-  if (leaves && nl) FMT_HIP(c, hipMemcpy(leaves, c->mtLeaves.p + static_cast<size_t>(doc) * caps.leaves, nl * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
-  if (chars && nc) FMT_HIP(c, hipMemcpy(chars, c->mtChars.p + static_cast<size_t>(doc) * caps.chars, nc * 2ull, hipMemcpyDeviceToHost));
-  if (props && np) FMT_HIP(c, hipMemcpy(props, c->mtProps.p + static_cast<size_t>(doc) * caps.props, np * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost));
+  if (leaves && nl) FMT_HIP(c, hipMemcpy(leaves, dLeaves + at * caps.leaves, nl * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
+  if (chars && nc) FMT_HIP(c, hipMemcpy(chars, dChars + at * caps.chars, nc * 2ull, hipMemcpyDeviceToHost));
+  if (props && np) FMT_HIP(c, hipMemcpy(props, dProps + at * caps.props, np * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost));
   return FMT_OK;
 }
 

@@ -37,6 +37,22 @@ FMT_DEV int waveLane() { return static_cast<int>(__lane_id()); }
 // variable-index load from the enclosing object's stack slot (which would put it in scratch).
 FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }
 
+// Large-tier rows: a plain per-lane array indexed at run time (private memory), so the row loops
+// stay rolled and the 32-row engine compiles in seconds.
+template <int N>
+struct VecN {
+  uint32_t x[N];
+  FMT_DEV uint32_t& operator[](int i) { return x[i]; }
+  FMT_DEV const uint32_t& operator[](int i) const { return x[i]; }
+};
+using V32 = VecN<32>;
+
+// A UTF-16 unit of a global buffer that other lanes of this wave wrote: an agent-scope load is
+// served by L2 (never a stale vector-L1 line).
+FMT_DEV uint32_t loadCoherent(const uint16_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Make a wave-uniform value provably uniform (lives in an SGPR afterwards).
 FMT_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 FMT_DEV uint32_t uni(uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x))); }
@@ -162,11 +178,14 @@ template <class T>
 struct Lane {
   T v[64];
 };
-struct V8 {
-  uint32_t x[8];
+template <int N>
+struct VecN {
+  uint32_t x[N];
   uint32_t& operator[](int i) { return x[i]; }
   const uint32_t& operator[](int i) const { return x[i]; }
 };
+using V8 = VecN<8>;
+using V32 = VecN<32>;
 struct V4 {
   uint32_t x[4];
   uint32_t& operator[](int i) { return x[i]; }
@@ -179,6 +198,8 @@ inline int uni(int x) { return x; }
 inline uint32_t uni(uint32_t x) { return x; }
 
 inline void launder(V8&) {}
+
+inline uint32_t loadCoherent(const uint16_t* p) { return *p; }
 
 inline uint64_t ballot(const Lane<bool>& p) {
   uint64_t m = 0;

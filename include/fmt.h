@@ -277,6 +277,9 @@ int fmt_map_replay_device(fmt_ctx* ctx, const fmt_map_op* d_ops, const uint64_t*
  * including updateSeqNumbers/setMinSeq (client.ts:1381-1391, mergeTree.ts:1147-1166) and zamboni
  * (zamboni.ts:33-213). Per-document errors land in fmt_mt_doc_result.status / fail_seq. */
 int fmt_mt_load(fmt_ctx* ctx, const fmt_mt_batch* batch);
+/* Replays every loaded document. Documents first run in the small tier (512 leaves, 2048 UTF-16
+ * units); those that overflow it are replayed again, from their inputs, in the large tier (2048
+ * leaves, 131071 units, text in HBM) before this returns. Stats cover both launches. */
 int fmt_mt_run(fmt_ctx* ctx);
 /* Per-document result headers for all docs (n_docs entries). Synchronizes the ctx stream. */
 int fmt_mt_fetch_headers(fmt_ctx* ctx, fmt_mt_doc_result* out);
@@ -289,7 +292,8 @@ int fmt_mt_fetch_doc(fmt_ctx* ctx, uint32_t doc, fmt_mt_leaf* leaves, uint32_t c
  * messagesSinceMSNChange contents SharedSegmentSequence stashes for the legacy summary's catchupOps
  * blob (sequence.ts:949-1018, snapshotlegacy.ts:178-190). */
 int fmt_mt_fetch_catchup(fmt_ctx* ctx, uint32_t doc, fmt_mt_catchup_range* out, uint32_t cap);
-/* Per-document capacities of this engine build (leaves, chars, prop sets). */
+/* Per-document capacities of this engine build (leaves, chars, prop sets): the large tier's, which
+ * is where a document that outgrows the small tier ends up. */
 int fmt_mt_capacity(uint32_t* max_leaves, uint32_t* max_chars, uint32_t* max_props);
 
 #ifdef __cplusplus

@@ -6,14 +6,15 @@
 
 #include "../../fluidframework_amd/csrc/mt_engine.h"
 
-template <bool Ob>
+template <bool Ob, class C>
 static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                      fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup) {
-  auto scratch = std::make_unique<fmt_mt::Scratch>();
-  auto doc = std::make_unique<fmt_mt::Doc<Ob>>();
+  using Doc = fmt_mt::Doc<Ob, C>;
+  auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
+  auto doc = std::make_unique<Doc>();
   int status = FMT_OK;
   for (uint32_t d = 0; d < b->n_docs; d++) {
-    std::memset(scratch.get(), 0xCD, sizeof(fmt_mt::Scratch));  // poison: state must be initialized
+    std::memset(scratch.get(), 0xCD, sizeof(fmt_mt::Scratch<C>));  // poison: state must be initialized
     fmt_mt::DocInputs in;
     in.ops = b->ops;
     in.begin = b->doc_op_offsets[d];
@@ -40,12 +41,12 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     }
     fmt_mt::DocOutputs o;
     o.header = headers + d;
-    o.leaves = leaves + static_cast<size_t>(d) * fmt_mt::kCapLeaves;
-    o.chars = chars + static_cast<size_t>(d) * fmt_mt::kCapChars;
-    o.props = props + static_cast<size_t>(d) * fmt_mt::kPropCap;
+    o.leaves = leaves + static_cast<size_t>(d) * Doc::kCapLeaves;
+    o.chars = chars + static_cast<size_t>(d) * Doc::kCapChars;
+    o.props = props + static_cast<size_t>(d) * Doc::kPropCap;
     o.catchup = catchup ? catchup + static_cast<size_t>(d) * capCatchup : nullptr;
     o.catchupCap = catchup ? capCatchup : 0u;
-    new (doc.get()) fmt_mt::Doc<Ob>();
+    new (doc.get()) Doc();
     doc->s = scratch.get();
     doc->run(in, o);
     if (headers[d].status != FMT_OK && status == FMT_OK) status = headers[d].status;
@@ -55,21 +56,35 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
 
 extern "C" {
 
-int emu_mt_capacity(uint32_t* leaves, uint32_t* chars, uint32_t* props) {
-  *leaves = fmt_mt::kCapLeaves;
-  *chars = fmt_mt::kCapChars;
-  *props = fmt_mt::kPropCap;
+// large = 0: the small tier (registers + LDS text); 1: the large tier (HBM text) that the runtime
+// replays overflowing documents in.
+int emu_mt_capacity(int large, uint32_t* leaves, uint32_t* chars, uint32_t* props) {
+  if (large) {
+    *leaves = fmt_mt::Doc<false, fmt_mt::LargeTier>::kCapLeaves;
+    *chars = fmt_mt::LargeTier::kCapChars;
+    *props = fmt_mt::LargeTier::kPropCap;
+  } else {
+    *leaves = fmt_mt::Doc<false, fmt_mt::SmallTier>::kCapLeaves;
+    *chars = fmt_mt::SmallTier::kCapChars;
+    *props = fmt_mt::SmallTier::kPropCap;
+  }
   return 0;
 }
 
-// Same strides as the GPU result buffers (kCapLeaves / kCapChars / kPropCap per document). Like
-// the runtime, batches holding obliterates run the Doc<true> variant (or always, with forceOb).
+// Same strides as the GPU result buffers of the tier (kCapLeaves / kCapChars / kPropCap per
+// document). Like the runtime, batches holding obliterates run the Doc<true> variant (or always,
+// with forceOb).
 int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
-                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb) {
+                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb, int large) {
   bool ob = forceOb != 0;
   for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE;
-  return ob ? replayAll<true>(b, headers, leaves, chars, props, catchup, capCatchup)
-            : replayAll<false>(b, headers, leaves, chars, props, catchup, capCatchup);
+  using S = fmt_mt::SmallTier;
+  using G = fmt_mt::LargeTier;
+  if (large)
+    return ob ? replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup)
+              : replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup);
+  return ob ? replayAll<true, S>(b, headers, leaves, chars, props, catchup, capCatchup)
+            : replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup);
 }
 
 }  // extern "C"

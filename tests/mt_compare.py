@@ -28,15 +28,15 @@ def emu_lib():
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas", "-o",
                             EMU_PATH, src], check=True)
         L = ctypes.CDLL(EMU_PATH)
-        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int]
-        L.emu_mt_capacity.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
+        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        L.emu_mt_capacity.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         _emu = L
     return _emu
 
 
-def emu_caps():
+def emu_caps(large=False):
     a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-    emu_lib().emu_mt_capacity(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    emu_lib().emu_mt_capacity(int(large), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
     return a.value, b.value, c.value
 
 
@@ -44,10 +44,11 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def emu_replay(batch, cap_catchup=0, force_ob=False):
-    """Run the engine source under host emulation; returns (headers, leaves, chars, props), plus the
-    catch-up ranges (n_docs, cap_catchup) when cap_catchup > 0."""
-    cl, cc, cp = emu_caps()
+def emu_replay(batch, cap_catchup=0, force_ob=False, large=False):
+    """Run the engine source under host emulation (small tier, or the large tier the runtime replays
+    overflowing documents in); returns (headers, leaves, chars, props), plus the catch-up ranges
+    (n_docs, cap_catchup) when cap_catchup > 0."""
+    cl, cc, cp = emu_caps(large)
     n = batch.n_docs
     hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
     leaves = np.zeros(n * cl, dtype=LEAF_DTYPE)
@@ -56,7 +57,7 @@ def emu_replay(batch, cap_catchup=0, force_ob=False):
     cu = np.zeros(n * cap_catchup, dtype=CATCHUP_DTYPE) if cap_catchup else None
     b, keep = batch_struct(batch)
     emu_lib().emu_mt_replay(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props),
-                            _p(cu) if cu is not None else None, cap_catchup, int(force_ob))
+                            _p(cu) if cu is not None else None, cap_catchup, int(force_ob), int(large))
     del keep
     out = (hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp))
     return out + (cu.reshape(n, cap_catchup),) if cap_catchup else out

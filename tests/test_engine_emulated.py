@@ -87,3 +87,52 @@ def test_emulated_engine_fills_every_row_to_capacity(orc):
             continue
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+# ---- large tier (documents that overflow the small tier replay again in it, on the GPU) ----------
+
+def test_large_tier_matches_oracle_on_fixtures(orc, fixtures_prefix):
+    """The rolled, HBM-text large tier is the same engine: bit-exact vs the oracle where both fit."""
+    batch, expected = fixtures_prefix
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch, large=True)
+    for d in range(batch.n_docs):
+        assert visible_text(hdr[d], leaves[d], chars[d]) == expected[d], f"doc {d}"
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_large_tier_fills_every_row_to_capacity(orc):
+    """Documents of 600..2300 leaves: beyond the small tier's 512, up to and past the large tier's 2048."""
+    cl, cc, cp = emu_caps(large=True)
+    small_leaves = emu_caps()[0]
+    batch = _no_zamboni_batch([400, 1000, 1500, 1650, 1800], seed=5)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=8192, cap_chars=1 << 17, cap_props=64)
+    assert rc == 0
+    assert oh["n_leaves"].max() > cl and ((oh["n_leaves"] > small_leaves) & (oh["n_leaves"] <= cl)).sum() >= 2
+    small = emu_replay(batch)[0]
+    hdr, leaves, chars, props = emu_replay(batch, large=True)
+    for d in range(batch.n_docs):
+        if oh[d]["n_leaves"] > small_leaves:
+            assert small[d]["status"] == -3, f"doc {d}: the small tier must overflow"
+        if oh[d]["n_leaves"] > cl:
+            assert hdr[d]["status"] == -3, f"doc {d}: expected FMT_E_CAPACITY"
+            continue
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_large_tier_matches_oracle_on_long_conflict_farm(orc):
+    """Conflict-farm documents long enough to outgrow 2048 UTF-16 units / 512 leaves."""
+    batch = workloads.conflict_farm(6, n_clients=8, ops_per_doc=4000, min_length=3000, seed=21)
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=6, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    small_cl, small_cc, _ = emu_caps()
+    assert ((oh["n_leaves"] > small_cl) | (oh["n_chars"] > small_cc)).any()
+    hdr, leaves, chars, props = emu_replay(batch, large=True)
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"

@@ -4,8 +4,8 @@ SnapshotLoader (merge-tree/src/snapshotLoader.ts:59-348) + reloadFromSegments (m
 + SharedSegmentSequence.loadCore's catch-up replay (sequence/src/sequence.ts:818-863).
 
 Pinned by the reference's own legacy snapshot fixtures: loading each and summarizing again gives
-the fixture's blobs byte for byte (oracle; these documents exceed the engine's per-document LDS
-capacity). Then, on the reference's replay fixture messages and on generated conflict farms:
+the fixture's blobs byte for byte (oracle, and the engine's large tier: these documents overflow
+the small tier's 512 leaves / 2048 UTF-16 units). Then, on the reference's replay fixture messages and on generated conflict farms:
   - the engine (emulated here, the GPU in -m gpu) equals the oracle bit for bit after a load;
   - summary → load (+ catch-up ops) → summary is a fixed point, and the loaded document's text after
     its catch-up ops equals the original replay's final text.
@@ -32,6 +32,26 @@ def test_oracle_load_resummarize_reference_snapshot(orc, name):
     rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
     assert rc == 0
     head, body = summary.legacy_summary(h[0], l[0], c[0], p[0], batch.keys, batch.values)
+    assert head == blobs["header"] and body == blobs.get("body")
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+def test_large_tier_loads_reference_snapshot(orc, name):
+    """The reference snapshots (8.9k-89k chars, up to 1112 segments) overflow the small tier and load
+    in the large tier (emulated here; on the GPU the runtime escalates them by itself): engine ==
+    oracle, and summarizing again gives the fixture's blobs byte for byte."""
+    blobs = _blobs(snapshot_trees()[name])
+    b = MergeTreeStreamBuilder()
+    b.begin_doc_from_summary(blobs["header"], blobs.get("body"))
+    batch = b.finish()
+    assert emu_replay(batch)[0][0]["status"] == native.FMT_E_CAPACITY
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    eh, el, ec, ep = emu_replay(batch, large=True)
+    assert eh[0]["status"] == 0
+    assert not compare_doc((oh[0], ol[0], oc[0], op[0]), (eh[0], el[0], ec[0], ep[0]))
+    head, body = summary.legacy_summary(eh[0], el[0], ec[0], ep[0], batch.keys, batch.values)
     assert head == blobs["header"] and body == blobs.get("body")
 
 
