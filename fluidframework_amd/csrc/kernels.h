@@ -25,6 +25,7 @@ struct MtDeviceBatch {
   const uint64_t* catchupOffsets;  // per-doc catch-up slab offsets (nDocs + 1), or nullptr
   const fmt_mt_snapshot_doc* snapshots;  // per-doc summary loads, or nullptr
   const fmt_mt_snapshot_seg* snapshotSegs;
+  const uint64_t* rmOrderOffsets;  // per-doc remove-order slab offsets (nDocs + 1), or nullptr
 };
 
 struct MtDeviceOut {
@@ -33,6 +34,7 @@ struct MtDeviceOut {
   uint16_t* chars;             // nDocs * capChars
   fmt_mt_propset* props;       // nDocs * capProps
   fmt_mt_catchup_range* catchup;  // slabs at catchupOffsets, or nullptr
+  fmt_mt_remove_order* rmOrder;   // slabs at rmOrderOffsets, or nullptr
 };
 
 // Per-document capacities of the small (LDS-text) and large (HBM-text) engine tiers.
@@ -44,11 +46,12 @@ MtCaps mergeTreeCaps(bool large);
 // Small tier: replays documents docList[0..count) (or all docs when docList == nullptr); documents
 // that overflow it are listed in esc (esc[0] = count, then ids) when esc != nullptr.
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate);
+                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate,
+                           bool removeOrder);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate);
+                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

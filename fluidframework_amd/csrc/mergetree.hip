@@ -23,11 +23,11 @@ __device__ unsigned long long g_mtProfile[fmt_mt::kPfCount];
 // Small tier over all documents (docList == nullptr) or a list; documents that overflow it are
 // appended to esc (esc[0] = count, esc[1..] = document ids) for the large-tier pass. The large tier
 // runs over that list, writing leaves/chars/props to slab i of the list (headers stay per doc).
-template <bool Ob, class C, int Waves, int WavesPerEU>
+template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                       const uint32_t* __restrict__ docList,
                                                                       uint32_t count, uint32_t* esc) {
-  using Doc = fmt_mt::Doc<Ob, C>;
+  using Doc = fmt_mt::Doc<Ob, C, Rm>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
   fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds) + wave;
@@ -71,6 +71,14 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
       o.catchup = nullptr;
       o.catchupCap = 0;
     }
+    if (batch.rmOrderOffsets) {
+      const uint64_t r0 = batch.rmOrderOffsets[d], r1 = batch.rmOrderOffsets[d + 1];
+      o.rmOrder = out.rmOrder + r0;
+      o.rmOrderCap = static_cast<uint32_t>(r1 - r0);
+    } else {
+      o.rmOrder = nullptr;
+      o.rmOrderCap = 0;
+    }
     Doc doc;
     doc.s = scratch;
     doc.run(in, o);
@@ -104,7 +112,7 @@ MtCaps mergeTreeCaps(bool large) {
                 static_cast<uint32_t>(fmt_mt::SmallTier::kCapChars), static_cast<uint32_t>(fmt_mt::SmallTier::kPropCap)};
 }
 
-template <bool Ob, class C, int Waves, int WavesPerEU>
+template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                              uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream) {
   const size_t lds = sizeof(fmt_mt::Scratch<C>) * Waves;
@@ -112,27 +120,34 @@ static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out,
   // so none waits behind the residency limit (VGPRs cap the small tier at 2 waves/SIMD).
   int blocksPerCU = 0;
   const hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<Ob, C, Waves, WavesPerEU>, 64 * Waves, lds);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>, 64 * Waves, lds);
   if (e != hipSuccess) return e;
   const uint32_t wanted = (count + Waves - 1) / Waves;
   const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
-  hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
+  hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
                      docList, count, esc);
   return hipGetLastError();
 }
 
+// Variants: obliterates (Ob), or the remove-order recording of SnapshotV1 batches (Rm; the host
+// rejects batches that would need both), or neither.
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate) {
-  if (obliterate) return launchTier<true, fmt_mt::SmallTier, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
-  return launchTier<false, fmt_mt::SmallTier, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate,
+                           bool removeOrder) {
+  using S = fmt_mt::SmallTier;
+  if (obliterate) return launchTier<true, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+  if (removeOrder) return launchTier<false, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+  return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
 }
 
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate) {
-  if (obliterate)
-    return launchTier<true, fmt_mt::LargeTier, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
-  return launchTier<false, fmt_mt::LargeTier, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder) {
+  using G = fmt_mt::LargeTier;
+  if (obliterate) return launchTier<true, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+  if (removeOrder)
+    return launchTier<false, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+  return launchTier<false, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
 }
 
 }  // namespace fmt_kernels

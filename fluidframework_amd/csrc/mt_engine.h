@@ -155,6 +155,8 @@ struct DocOutputs {
   fmt_mt_propset* props;  // kPropCap entries
   fmt_mt_catchup_range* catchup;  // catchupCap entries (nullptr: no FMT_MT_F_CATCHUP ops)
   uint32_t catchupCap;
+  fmt_mt_remove_order* rmOrder;   // rmOrderCap entries (nullptr: no FMT_MT_F_RMORDER ops)
+  uint32_t rmOrderCap;
 };
 
 // Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
@@ -168,7 +170,9 @@ enum ProfCat {
 
 // Ob: the engine variant that also replays obliterates (f1). Without obliterates in a batch the
 // runtime launches Doc<false>, whose code is exactly the obliterate-free engine.
-template <bool Ob, class C = SmallTier>
+// Rm: the variant that records the remove order for SnapshotV1 summaries (FMT_MT_F_RMORDER ops);
+// batches without such ops run the Rm = false code, which has none of it.
+template <bool Ob, class C = SmallTier, bool Rm = false>
 class Doc {
  public:
   using VR = typename C::VR;
@@ -225,6 +229,13 @@ class Doc {
   DocInputs in;
   fmt_mt_catchup_range* cuOut = nullptr;
   uint32_t cuCap = 0;
+  uint32_t rmN = 0;     // remove-order entries recorded (HBM slab, leaf ids until writeOutputs)
+  fmt_mt_remove_order* rmOut = nullptr;
+  uint32_t rmCap = 0;
+  int rmPendN = 0;      // split copies waiting for rmFlush (at most two splits per op)
+  uint32_t rmPendFrom0 = 0, rmPendTo0 = 0, rmPendFrom1 = 0, rmPendTo1 = 0;
+  bool rmHitsSet = false;
+  Lane<uint32_t> rmHits;  // leaves a flagged REMOVE found already removed (row bitmask per lane)
 
   // ------------------------------------------------------------------ leaf array primitives
   // Leaf j lives in row j >> 6 (element of the V8) of lane j & 63: document order runs along a
@@ -773,6 +784,57 @@ class Doc {
     cuN++;
   }
 
+  // ------------------------------------------------------------------ remove order (SnapshotV1)
+  // A flagged REMOVE that hits an already-removed leaf adds a later remove stamp to it
+  // (spliceIntoList, stamps.ts:144-158: remote stamps arrive in seq order, so they append). The
+  // summary's removedClientIds (snapshotV1.ts:235-250) need that order, which the remove-client
+  // mask W3 does not keep: each such stamp is appended to the document's HBM slab as (leaf id,
+  // client). Rare (concurrent overlapping removes), so lane 0 writes one entry at a time.
+  FMT_DEV void rmAppend(uint32_t id, int client) {
+    if (rmN >= rmCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    FOR_LANES(l) {
+      if (l == 0) {
+        fmt_mt_remove_order e;
+        e.leaf = id;
+        e.client = client;
+        rmOut[rmN] = e;
+      }
+    }
+    rmN++;
+  }
+
+  // Deferred to one call site per op (replay, before zamboni), so the rare recording code is inlined
+  // once: the right parts of split multi-removed leaves inherit their entries (splitLeafSegment
+  // copies the remove stamps, mergeTreeNodes.ts:389-435), in split order; then every leaf the
+  // flagged REMOVE found already removed gets the op's stamp.
+  FMT_DEV void rmFlush(int client) {
+    for (int q = 0; q < rmPendN && status == FMT_OK; q++) {
+      const uint32_t from = q == 0 ? rmPendFrom0 : rmPendFrom1, to = q == 0 ? rmPendTo0 : rmPendTo1;
+      const uint32_t n0 = rmN;
+      for (uint32_t k = 0; k < n0 && status == FMT_OK; k++) {
+        if (uni(loadCoherent(&rmOut[k].leaf)) == from)
+          rmAppend(to, static_cast<int>(uni(loadCoherent(reinterpret_cast<const uint32_t*>(&rmOut[k].client)))));
+      }
+    }
+    rmPendN = 0;
+    if (rmHitsSet) {
+      rmHitsSet = false;
+      Lane<uint32_t> todo = rmHits;
+      const int nr = rows();
+      for (;;) {
+        const int j = firstSet(todo, nr);
+        if (j < 0 || status != FMT_OK) break;
+        FOR_LANES(l) {
+          if (l == (j & 63)) LANE(todo) &= ~(1u << (j >> 6));
+        }
+        rmAppend(fId(readField(j, 4)), client);
+      }
+    }
+  }
+
   // ------------------------------------------------------------------ ops
   // addToLRUSet (mergeTree.ts:812-822) for leaf j: the first registration of a block sets
   // needsScour; later leaves of that block are no-ops until zamboni clears it.
@@ -816,6 +878,18 @@ class Doc {
     rec.w[4] = mkW4(nextId++, fClient(w4));
     if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
       if (obUsed != 0) obRefsMove(fId(w4), fId(rec.w[4]), offset, -offset);
+    }
+    if constexpr (Rm) {
+      if (rmN > 0 && __builtin_popcount(rec.w[3]) >= 2) {  // copied in rmFlush
+        if (rmPendN == 0) {
+          rmPendFrom0 = fId(w4);
+          rmPendTo0 = fId(rec.w[4]);
+        } else {
+          rmPendFrom1 = fId(w4);
+          rmPendTo1 = fId(rec.w[4]);
+        }
+        rmPendN++;
+      }
     }
     writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0)));
     if (!insertLeafAt(j + 1, rec)) return false;
@@ -1219,6 +1293,16 @@ class Doc {
       if (!obAdd(fId(readField(sLeaf, 4)), sOff, fId(readField(eLeaf, 4)), eOff, seq, client)) return false;
     }
     FOR_LANES(l) { LANE(delta) = 0u; }
+    if (Rm && op.type == FMT_MT_REMOVE && (op.flags & FMT_MT_F_RMORDER) != 0) {  // recorded in rmFlush
+      FOR_LANES(l) {
+        uint32_t m = 0;
+        FOR_ROWS(r, 0, nr) {
+          if (((LANE(hits) >> r) & 1u) && static_cast<int32_t>(LANE(W[2])[r]) != kNotRemoved) m |= 1u << r;
+        }
+        LANE(rmHits) = m;
+      }
+      rmHitsSet = true;
+    }
     if (op.type == FMT_MT_REMOVE || obliterate) {
       // markRangeRemoved (mergeTree.ts:2292-2383): first remove stays the lowest seq; the delta
       // (removedSegments) is the hit leaves not removed before this op (:2314-2321)
@@ -1745,6 +1829,9 @@ class Doc {
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op, text);
+      if constexpr (Rm) {
+        if (rmPendN > 0 || rmHitsSet) rmFlush(op.client);
+      }
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       // zamboni once inside the op (mergeTree.ts:1510-1516, 2074-2080, 2376-2382), then, after the
       // message's last member, updateSeqNumbers (client.ts:1381-1391) → setMinSeq
@@ -1829,6 +1916,14 @@ class Doc {
         out.props[p] = ps;
       }
     }
+    // remove-order entries: leaf id -> final leaf index (FMT_MT_LEAF_GONE once zamboni dropped it)
+    for (uint32_t k = 0; Rm && k < rmN; k++) {
+      const uint32_t id = uni(loadCoherent(&rmOut[k].leaf));
+      const int j = findLeafById(id);
+      FOR_LANES(l) {
+        if (l == 0) rmOut[k].leaf = j >= 0 ? static_cast<uint32_t>(j) : FMT_MT_LEAF_GONE;
+      }
+    }
     int depth = 1;
     for (int b = root; uni(static_cast<int>(s->blk[b].leaf)) == 0 && uni(static_cast<int>(s->blk[b].count)) > 0;
          b = uni(static_cast<int>(s->blk[b].child[0])))
@@ -1847,7 +1942,7 @@ class Doc {
         h.depth = static_cast<uint32_t>(depth);
         h.visible_len = visible;
         h.n_catchup = cuN;
-        h.pad = 0;
+        h.n_rm_order = rmN;
         *out.header = h;
       }
     }
@@ -1861,6 +1956,9 @@ class Doc {
     cuOut = out.catchup;
     cuCap = out.catchup ? out.catchupCap : 0u;
     cuN = 0;
+    rmOut = out.rmOrder;
+    rmCap = out.rmOrder ? out.rmOrderCap : 0u;
+    rmN = 0;
     if constexpr (C::kHbmChars) gch = out.chars;
     init();
     if (in.loaded) loadSnapshot();

@@ -81,6 +81,10 @@ struct fmt_ctx {
   DevBuf<fmt_mt_catchup_range> mtCatchup;    // catch-up range slabs
   std::vector<uint64_t> mtCuOffsHost;
   bool mtHasCatchup = false;
+  DevBuf<uint64_t> mtRmOffs;                 // per-doc remove-order slab offsets (n_docs + 1)
+  DevBuf<fmt_mt_remove_order> mtRmOrder;     // remove-order slabs (FMT_MT_F_RMORDER ops)
+  std::vector<uint64_t> mtRmOffsHost;
+  bool mtHasRmOrder = false;
   uint64_t mtNOps = 0, mtTextLen = 0, mtInsertChars = 0, mtInitChars = 0;
   uint32_t mtDocs = 0, mtNProps = 0;
   bool mtHasInit = false, mtLoaded = false;
@@ -162,6 +166,8 @@ void fmt_close(fmt_ctx* c) {
   c->mtSnapSegs.release();
   c->mtCuOffs.release();
   c->mtCatchup.release();
+  c->mtRmOffs.release();
+  c->mtRmOrder.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ownStream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -288,11 +294,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   const uint32_t n = b->n_docs;
   if (b->doc_op_offsets[0] != 0 || b->doc_op_offsets[n] != b->n_ops)
     return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
-  uint64_t insertChars = 0, catchupOps = 0;
+  uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
   bool obliterates = false;
   for (uint64_t i = 0; i < b->n_ops; i++) {
     const fmt_mt_op& op = b->ops[i];
     if (op.flags & FMT_MT_F_CATCHUP) catchupOps++;
+    if (op.flags & FMT_MT_F_RMORDER) rmOrderOps++;
     if (op.type == FMT_MT_INSERT) {
       if (static_cast<uint64_t>(op.payload) + op.len > b->text_len)
         return setErr(c, FMT_E_DATA, "insert payload outside the text arena");
@@ -359,6 +366,23 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, c->mtCuOffs.reserve(n + 1ull));
     FMT_HIP(c, c->mtCatchup.reserve(c->mtCuOffsHost[n]));
   }
+  // Remove-order slabs: kRmPerOp entries per flagged remove plus kRmPerDoc per document that has
+  // any (split copies included); a document that needs more reports FMT_E_CAPACITY.
+  c->mtHasRmOrder = rmOrderOps > 0;
+  if (c->mtHasRmOrder && obliterates)
+    return setErr(c, FMT_E_UNSUPPORTED, "remove order (FMT_MT_F_RMORDER) in a batch with obliterates");
+  if (c->mtHasRmOrder) {
+    constexpr uint64_t kRmPerOp = 64, kRmPerDoc = 256;
+    c->mtRmOffsHost.assign(n + 1ull, 0);
+    for (uint32_t d = 0; d < n; d++) {
+      uint64_t f = 0;
+      for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
+        f += (b->ops[i].flags & FMT_MT_F_RMORDER) ? 1 : 0;
+      c->mtRmOffsHost[d + 1] = c->mtRmOffsHost[d] + (f ? f * kRmPerOp + kRmPerDoc : 0);
+    }
+    FMT_HIP(c, c->mtRmOffs.reserve(n + 1ull));
+    FMT_HIP(c, c->mtRmOrder.reserve(c->mtRmOffsHost[n]));
+  }
   auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
   };
@@ -374,6 +398,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg)));
   }
   if (c->mtHasCatchup) FMT_HIP(c, cp(c->mtCuOffs.p, c->mtCuOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
+  if (c->mtHasRmOrder) FMT_HIP(c, cp(c->mtRmOffs.p, c->mtRmOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
   if (b->props_off) {
     FMT_HIP(c, cp(c->mtPropsOff.p, b->props_off, (b->n_props_ops + 1ull) * sizeof(uint32_t)));
     FMT_HIP(c, cp(c->mtPropsKv.p, b->props_kv, nKv * sizeof(uint32_t)));
@@ -399,13 +424,14 @@ int fmt_mt_run(fmt_ctx* c) {
   fmt_kernels::MtDeviceBatch db{c->mtOps.p, c->mtOffs.p, c->mtDocs, c->mtText.p,
                                 c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps,
                                 c->mtHasCatchup ? c->mtCuOffs.p : nullptr,
-                                c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr};
+                                c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr,
+                                c->mtHasRmOrder ? c->mtRmOffs.p : nullptr};
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
-                                c->mtHasCatchup ? c->mtCatchup.p : nullptr};
+                                c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->mtEsc.p, c->numCUs, c->stream,
-                                          c->mtObliterate));
+                                          c->mtObliterate, c->mtHasRmOrder));
   // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
   uint32_t nEsc = 0;
   FMT_HIP(c, hipMemcpyAsync(&nEsc, c->mtEsc.p, sizeof nEsc, hipMemcpyDeviceToHost, c->stream));
@@ -417,8 +443,9 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigChars.reserve(static_cast<size_t>(nEsc) * big.chars));
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
-                                  c->mtHasCatchup ? c->mtCatchup.p : nullptr};
-    FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate));
+                                  c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
+    FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
+                                                 c->mtHasRmOrder));
     std::vector<uint32_t> list(nEsc);
     FMT_HIP(c, hipMemcpyAsync(list.data(), c->mtEsc.p + 1, nEsc * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     FMT_HIP(c, hipStreamSynchronize(c->stream));
@@ -485,6 +512,17 @@ int fmt_mt_fetch_catchup(fmt_ctx* c, uint32_t doc, fmt_mt_catchup_range* out, ui
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
   const uint32_t m = h.n_catchup < cap ? h.n_catchup : cap;
   if (m) FMT_HIP(c, hipMemcpy(out, c->mtCatchup.p + c->mtCuOffsHost[doc], m * sizeof(fmt_mt_catchup_range), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out, uint32_t cap) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_remove_order: bad arguments");
+  if (!c->mtHasRmOrder) return FMT_OK;
+  fmt_mt_doc_result h;
+  FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
+  const uint32_t m = h.n_rm_order < cap ? h.n_rm_order : cap;
+  if (m) FMT_HIP(c, hipMemcpy(out, c->mtRmOrder.p + c->mtRmOffsHost[doc], m * sizeof(fmt_mt_remove_order), hipMemcpyDeviceToHost));
   return FMT_OK;
 }
 

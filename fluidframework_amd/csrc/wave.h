@@ -52,6 +52,9 @@ using V32 = VecN<32>;
 FMT_DEV uint32_t loadCoherent(const uint16_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+FMT_DEV uint32_t loadCoherent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Make a wave-uniform value provably uniform (lives in an SGPR afterwards).
 FMT_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -200,6 +203,7 @@ inline uint32_t uni(uint32_t x) { return x; }
 inline void launder(V8&) {}
 
 inline uint32_t loadCoherent(const uint16_t* p) { return *p; }
+inline uint32_t loadCoherent(const uint32_t* p) { return *p; }
 
 inline uint64_t ballot(const Lane<bool>& p) {
   uint64_t m = 0;

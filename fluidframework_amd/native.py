@@ -45,10 +45,14 @@ DOC_RESULT_DTYPE = np.dtype(
         ("depth", "<u4"),
         ("visible_len", "<u4"),
         ("n_catchup", "<u4"),
-        ("pad", "<u4"),
+        ("n_rm_order", "<u4"),
     ]
 )
 assert DOC_RESULT_DTYPE.itemsize == 48
+
+# fmt_mt_remove_order: a later remove stamp of a leaf (leaf index, client); FMT_MT_LEAF_GONE leaf
+RM_ORDER_DTYPE = np.dtype([("leaf", "<u4"), ("client", "<i4")])
+LEAF_GONE = 0xFFFFFFFF
 
 CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("type", "<u4")])
 
@@ -166,6 +170,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_headers.argtypes = [P, P]
         L.fmt_mt_fetch_doc.argtypes = [P, U32, P, U32, P, U32, P, U32]
         L.fmt_mt_fetch_catchup.argtypes = [P, U32, P, U32]
+        L.fmt_mt_fetch_remove_order.argtypes = [P, U32, P, U32]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         _libs[path] = L
     return _libs[path]
@@ -175,7 +180,7 @@ EXPORTED_SYMBOLS = [
     "fmt_open", "fmt_close", "fmt_last_error", "fmt_sync", "fmt_get_stats", "fmt_device_info",
     "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
-    "fmt_mt_capacity",
+    "fmt_mt_fetch_remove_order", "fmt_mt_capacity",
 ]
 
 
@@ -267,6 +272,15 @@ class Engine:
         props = np.zeros(max(npp, 1), dtype=PROPSET_DTYPE)
         self._check(self.L.fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
         return leaves[:nl], chars[:nc], props[:npp]
+
+    def mt_remove_order(self, doc: int, hdr=None) -> np.ndarray:
+        """The document's remove-order entries (fmt_mt_remove_order) of its FMT_MT_F_RMORDER ops."""
+        if hdr is None:
+            hdr = self.mt_headers()[doc]
+        n = int(hdr["n_rm_order"])
+        out = np.zeros(max(n, 1), dtype=RM_ORDER_DTYPE)
+        self._check(self.L.fmt_mt_fetch_remove_order(self.h, doc, _ptr(out), n))
+        return out[:n]
 
     def mt_catchup(self, doc: int, hdr=None) -> np.ndarray:
         """The document's catch-up ranges (fmt_mt_catchup_range) of its FMT_MT_F_CATCHUP ops."""

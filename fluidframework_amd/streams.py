@@ -54,6 +54,7 @@ assert MAP_OP_DTYPE.itemsize == 16
 MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
 MT_F_GROUP_CONT = 1
 MT_F_CATCHUP = 2  # include/fmt.h FMT_MT_F_CATCHUP
+MT_F_RMORDER = 4  # include/fmt.h FMT_MT_F_RMORDER
 MAP_SET, MAP_DELETE, MAP_CLEAR = 0, 1, 2
 MAP_KIND_SHIFT = 30
 MAP_VALUE_UNDEFINED = 0x3FFFFFFF
@@ -273,24 +274,34 @@ class MergeTreeStreamBuilder:
             raise ValueError("empty segment in a summary chunk")
         return (off, n, self._props_op(props) if props else NO_PROPS)
 
-    def begin_doc_from_summary(self, header: str, body: str | None = None, catchup_ops: str | None = None,
+    def begin_doc_from_summary(self, header: str, body=None, catchup_ops: str | None = None,
                                observer: str = "snapshot") -> _DocBuilder:
-        """A document that starts from a legacy SharedString summary (SnapshotLoader, snapshotLoader.ts:
-        59-348): the header/body chunk blobs and, optionally, the catchupOps blob, whose messages are
-        added as the first ops after validation as SharedSegmentSequence.loadCore does (sequence.ts:
-        818-863). The loading client is `observer` (short id 0)."""
+        """A document that starts from a SharedString summary (SnapshotLoader, snapshotLoader.ts:
+        59-348): the header/body chunk blobs (a legacy "body", or SnapshotV1's "body_0", "body_1", ...
+        as a list, toLatestVersion snapshotChunks.ts:151-180) and, optionally, the legacy catchupOps
+        blob, whose messages are added as the first ops after validation as
+        SharedSegmentSequence.loadCore does (sequence.ts:818-863). The loading client is `observer`
+        (short id 0). V1 segments that carry merge info (seq/client/removed stamps above minSeq) are
+        not supported by this loader."""
         h = json.loads(header)
         md = h.get("headerMetadata")
         if md is None:
             raise ValueError("header metadata not available")
-        chunks = [h] + ([json.loads(body)] if body is not None else [])
+        bodies = [] if body is None else ([body] if isinstance(body, str) else list(body))
+        chunks = [h] + [json.loads(b) for b in bodies]
         if len(md["orderedChunkMetadata"]) != len(chunks):
             raise ValueError("summary chunks do not match headerMetadata.orderedChunkMetadata")
+
+        def specs(c):
+            return c["segments"] if c.get("version") == "1" else c["segmentTexts"]
+
         first = len(self.snapshot_segs)
         for c in chunks:
-            for spec in c["segmentTexts"]:
+            for spec in specs(c):
+                if isinstance(spec, dict) and "json" in spec:
+                    raise UnsupportedOp("SnapshotV1 segments with merge info")
                 self.snapshot_segs.append(self._spec(spec))
-        n_header = len(h["segmentTexts"])
+        n_header = len(specs(h))
         n_body = len(self.snapshot_segs) - first - n_header
         if n_header + n_body != md["totalSegmentCount"]:
             raise ValueError("Mismatch in totalSegmentCount")  # snapshotLoader.ts:272-275
@@ -310,9 +321,10 @@ class MergeTreeStreamBuilder:
                 d.add_message(m)
         return d
 
-    def finish(self, catchup: bool = False) -> MergeTreeBatch:
+    def finish(self, catchup: bool = False, remove_order: bool = False) -> MergeTreeBatch:
         """The packed batch. With `catchup`, ops of messages that stay in the legacy summary's
-        catch-up window get FMT_MT_F_CATCHUP (see flag_catchup)."""
+        catch-up window get FMT_MT_F_CATCHUP (see flag_catchup); with `remove_order`, the removes
+        a SnapshotV1 summary needs get FMT_MT_F_RMORDER (see flag_remove_order)."""
         n = sum(d.n_ops for d in self.docs)
         ops = np.zeros(n, dtype=MT_OP_DTYPE)
         offs = np.zeros(len(self.docs) + 1, dtype=np.uint64)
@@ -324,6 +336,8 @@ class MergeTreeStreamBuilder:
             offs[di + 1] = i
         if catchup:
             flag_catchup(ops, offs)
+        if remove_order:
+            flag_remove_order(ops, offs)
         text = np.concatenate(self.text) if self.text else np.zeros(0, dtype="<u2")
         props_off = np.zeros(len(self.props_list) + 1, dtype=np.uint32)
         kv = []
@@ -368,6 +382,20 @@ def flag_catchup(ops: np.ndarray, offs: np.ndarray) -> None:
         final_msn = int(seg["min_seq"][-1])
         sel = (seg["seq"] > final_msn) & (seg["ref_seq"] != seg["seq"] - 1)
         seg["flags"][sel] |= MT_F_CATCHUP
+
+
+def flag_remove_order(ops: np.ndarray, offs: np.ndarray) -> None:
+    """Set FMT_MT_F_RMORDER on the REMOVE ops above the document's final minSeq: the only ones that
+    can add a later remove stamp to a leaf that a SnapshotV1 summary lists with merge info
+    (snapshotV1.ts:207-265 skips leaves removed at/below minSeq)."""
+    for d in range(len(offs) - 1):
+        a, b = int(offs[d]), int(offs[d + 1])
+        if a == b:
+            continue
+        seg = ops[a:b]
+        final_msn = int(seg["min_seq"][-1])
+        sel = (seg["seq"] > final_msn) & (seg["type"] == MT_REMOVE)
+        seg["flags"][sel] |= MT_F_RMORDER
 
 
 @dataclass

@@ -5,6 +5,9 @@
     (mapKernel.ts:545-551): array-index keys ascending, then Map insertion (birth) order.
   - SharedString legacy format: SnapshotLegacy.extractSync + emit (merge-tree/src/snapshotlegacy.ts:
     74-262, snapshotChunks.ts:85-204) over the leaf table produced by the merge-tree kernel.
+  - SharedString SnapshotV1 format (newMergeTreeSnapshotFormat, client.ts:1569-1580):
+    SnapshotV1.extractSync + emit (merge-tree/src/snapshotV1.ts:90-265) with merge info for the
+    segments above minSeq; removedClientIds come from the kernel's remove-order slab.
 Both are byte-identical to JSON.stringify of the reference objects.
 """
 from __future__ import annotations
@@ -162,6 +165,110 @@ def legacy_summary(header, leaves, chars, propsets, keys, values, chunk_size=SIZ
     head, n1 = chunk(0, chunk_size, True)
     body = chunk(n1, total_len, False)[0] if n1 < len(segs) else None
     return head, body
+
+
+# ------------------------------------------------------------------------------ SnapshotV1 (f2)
+V1_CHUNK_SIZE = 10000  # SnapshotV1.chunkSize (snapshotV1.ts:44)
+
+
+def removers_from_engine(leaves, n_leaves, rm_order, doc_ops):
+    """Ordered remove-stamp clients per removed leaf: the first remover is the client of the op whose
+    seq is the leaf's rm_seq; later ones are the kernel's remove-order entries (seq order)."""
+    seq_client = {int(s): int(c) for s, c in zip(doc_ops["seq"], doc_ops["client"])}
+    out = {}
+    for i in range(n_leaves):
+        rm = int(leaves[i]["rm_seq"])
+        if rm != NOT_REMOVED and rm in seq_client:
+            out[i] = [seq_client[rm]]
+    for e in rm_order:
+        j = int(e["leaf"])
+        if j != 0xFFFFFFFF and j in out:
+            out[j].append(int(e["client"]))
+    return out
+
+
+def v1_segments(header, leaves, chars, propsets, keys, values, client_names, removers):
+    """SnapshotV1.extractSync (snapshotV1.ts:170-276): [(json text, cachedLength)] per summary segment.
+    Leaves removed at/below minSeq are skipped (the merge chain continues across them); acked,
+    not-removed leaves at/below minSeq merge while canAppend && matchProperties; every other leaf is
+    written with its merge info."""
+    min_seq = int(header["min_seq"])
+    out = []
+    prev = None  # [text, props]
+
+    def seg_json(text, props):
+        if props is None or len(props) == 0:
+            return _q(text)
+        return '{"text":' + _q(text) + ',"props":' + _props_obj(props, keys, values) + "}"
+
+    def flush():
+        if prev is not None:
+            out.append((seg_json(prev[0], prev[1]), _utf16_len(prev[0])))
+
+    for i in range(int(header["n_leaves"])):
+        L = leaves[i]
+        ins, rm = int(L["ins_seq"]), int(L["rm_seq"])
+        removed = rm != NOT_REMOVED
+        if removed and rm <= min_seq:
+            continue
+        o, n = int(L["char_off"]), int(L["len"])
+        text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
+        pid = int(L["props"])
+        props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
+        if ins <= min_seq and not removed:
+            if prev is None:
+                prev = [text, props]
+            elif (not prev[0].endswith("\n")
+                  and (_utf16_len(prev[0]) <= TEXT_GRANULARITY or n <= TEXT_GRANULARITY)
+                  and _props_match(prev[1], props)):
+                prev[0] += text
+            else:
+                flush()
+                prev = [text, props]
+            continue
+        flush()
+        prev = None
+        raw = '{"json":' + seg_json(text, props)
+        if ins > min_seq:
+            raw += f',"seq":{ins},"client":' + _q(client_names[int(L["ins_client"])])
+        if removed:
+            ids = removers.get(i)
+            if not ids:
+                raise ValueError(f"leaf {i}: remove order unknown (flag removes with FMT_MT_F_RMORDER)")
+            raw += (f',"removedSeq":{rm},"removedClient":' + _q(client_names[ids[0]])
+                    + ',"removedClientIds":[' + ",".join(_q(client_names[c]) for c in ids) + "]")
+        out.append((raw + "}", n))
+    flush()
+    return out
+
+
+def v1_summary(header, leaves, chars, propsets, keys, values, client_names, removers,
+               chunk_size=V1_CHUNK_SIZE):
+    """(header_blob, [body_0, body_1, ...]) of SnapshotV1.emit (snapshotV1.ts:126-168)."""
+    segs = v1_segments(header, leaves, chars, propsets, keys, values, client_names, removers)
+    chunks = []  # (start, count, length)
+    start = 0
+    while True:  # do { ... } while (totalSegmentCount < segments.length)
+        n, length = 0, 0
+        while length < chunk_size and start + n < len(segs):
+            length += segs[start + n][1]
+            n += 1
+        chunks.append((start, n, length))
+        start += n
+        if start >= len(segs):
+            break
+    total_len = sum(c[2] for c in chunks)
+
+    def body_of(c):
+        s0, n, length = c
+        return (f'{{"version":"1","segmentCount":{n},"length":{length},"segments":['
+                + ",".join(t for t, _ in segs[s0 : s0 + n]) + f'],"startIndex":{s0}')
+
+    ids = ",".join(['{"id":"header"}'] + [f'{{"id":"body_{k}"}}' for k in range(len(chunks) - 1)])
+    head = (body_of(chunks[0]) + f',"headerMetadata":{{"minSequenceNumber":{int(header["min_seq"])},'
+            f'"sequenceNumber":{int(header["cur_seq"])},"orderedChunkMetadata":[{ids}],'
+            f'"totalLength":{total_len},"totalSegmentCount":{len(segs)}}}}}')
+    return head, [body_of(c) + "}" for c in chunks[1:]]
 
 
 def catchup_messages(messages, ranges, min_seq):

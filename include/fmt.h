@@ -83,6 +83,12 @@ extern "C" {
  * The host sets it on the ops of messages that stay in the legacy summary's catch-up window
  * (seq > final minSeq) and need transformation (refSeq != seq - 1, sequence.ts:971-1006). */
 #define FMT_MT_F_CATCHUP 2u
+/* Record the remove order (SnapshotV1 merge info, merge-tree/src/snapshotV1.ts:235-250): for every
+ * leaf this REMOVE hits that is already removed, append (leaf, client) to the document's remove-order
+ * slab, so the summary can list removedClientIds in stamp order (stamps.ts:144-158). The host sets it
+ * on the REMOVE ops with seq > the document's final minSeq (only leaves removed above minSeq carry
+ * merge info). The first remover is the client of the op whose seq is the leaf's rm_seq. */
+#define FMT_MT_F_RMORDER 4u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */
@@ -181,7 +187,7 @@ typedef struct fmt_mt_doc_result {
   uint32_t depth;      /* tree depth (1 = root holds leaves) */
   uint32_t visible_len;/* getLength() from the local perspective */
   uint32_t n_catchup;  /* catch-up ranges recorded for FMT_MT_F_CATCHUP ops (fmt_mt_fetch_catchup) */
-  uint32_t pad;
+  uint32_t n_rm_order; /* remove-order entries recorded for FMT_MT_F_RMORDER ops (fmt_mt_fetch_remove_order) */
 } fmt_mt_doc_result;
 
 /* One regenerated catch-up op range (a merged ISequenceDeltaRange, sequence.ts:395-452): positions
@@ -196,6 +202,15 @@ typedef struct fmt_mt_catchup_range {
   int32_t pos2;
   uint32_t type; /* FMT_MT_INSERT / FMT_MT_REMOVE / FMT_MT_ANNOTATE */
 } fmt_mt_catchup_range;
+
+/* One later remover of a leaf (the second, third, ... remove stamp, in seq order across the slab):
+ * `leaf` is the index in the document's final leaf list, or FMT_MT_LEAF_GONE when that leaf was
+ * dropped by zamboni before the end. A split leaf's entries are copied to its right part. */
+#define FMT_MT_LEAF_GONE 0xffffffffu
+typedef struct fmt_mt_remove_order {
+  uint32_t leaf;
+  int32_t client; /* short client id of the remove stamp */
+} fmt_mt_remove_order;
 
 /* A document-local prop set: up to FMT_MT_PROPS_MAX (key_id, value_id) pairs in JS insertion order. */
 #define FMT_MT_PROPS_MAX 4
@@ -292,6 +307,9 @@ int fmt_mt_fetch_doc(fmt_ctx* ctx, uint32_t doc, fmt_mt_leaf* leaves, uint32_t c
  * messagesSinceMSNChange contents SharedSegmentSequence stashes for the legacy summary's catchupOps
  * blob (sequence.ts:949-1018, snapshotlegacy.ts:178-190). */
 int fmt_mt_fetch_catchup(fmt_ctx* ctx, uint32_t doc, fmt_mt_catchup_range* out, uint32_t cap);
+/* One document's remove-order entries (header n_rm_order entries, at most cap), in recording order:
+ * with the first remover they give SnapshotV1's removedClientIds (snapshotV1.ts:235-250). */
+int fmt_mt_fetch_remove_order(fmt_ctx* ctx, uint32_t doc, fmt_mt_remove_order* out, uint32_t cap);
 /* Per-document capacities of this engine build (leaves, chars, prop sets): the large tier's, which
  * is where a document that outgrows the small tier ends up. */
 int fmt_mt_capacity(uint32_t* max_leaves, uint32_t* max_chars, uint32_t* max_props);

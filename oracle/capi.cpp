@@ -193,6 +193,32 @@ int orc_mt_summary(void* h, const char* const* keys, int nKeys, const char* cons
   return static_cast<int>(all.size());
 }
 
+// The document's initial state: a loaded summary (f3) or its initial text, then collaboration.
+void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d) {
+  if (b->snapshots != nullptr && b->snapshots[d].loaded) {
+    const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+    std::vector<MergeTree::LoadedSeg> head, body;
+    for (uint32_t k = 0; k < sd.n_header + sd.n_body; k++) {
+      const fmt_mt_snapshot_seg& sg = b->snapshot_segs[sd.first_seg + k];
+      MergeTree::LoadedSeg l;
+      l.text.assign(reinterpret_cast<const char16_t*>(b->text + sg.text), sg.len);
+      if (sg.props != FMT_MT_NO_PROPS) {
+        l.hasProps = true;
+        for (uint32_t t = b->props_off[sg.props]; t < b->props_off[sg.props + 1]; t++)
+          l.props.emplace_back(static_cast<uint16_t>(b->props_kv[t] >> 16), static_cast<uint16_t>(b->props_kv[t] & 0xffff));
+      }
+      (k < sd.n_header ? head : body).push_back(std::move(l));
+    }
+    mt.loadSnapshot(head, body, sd.min_seq, sd.seq);
+  } else {
+    if (b->doc_init != nullptr && b->doc_init[2 * d + 1] > 0) {
+      const uint32_t off = b->doc_init[2 * d], len = b->doc_init[2 * d + 1];
+      mt.insertLocal(0, std::u16string(reinterpret_cast<const char16_t*>(b->text + off), len));
+    }
+    mt.startCollaboration(0, 0, 0);
+  }
+}
+
 // ---------------------------------------------------------------- merge-tree, batch replay
 // Replays documents [docBegin, docEnd) of a batch with nThreads host threads (one doc per task).
 // Output arrays are indexed by (doc - docBegin) with the given per-doc strides; any may be NULL.
@@ -208,28 +234,7 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
     const size_t i = d - docBegin;
     int32_t failSeq = 0;
     int st = FMT_OK;
-    if (b->snapshots != nullptr && b->snapshots[d].loaded) {
-      const fmt_mt_snapshot_doc& sd = b->snapshots[d];
-      std::vector<MergeTree::LoadedSeg> head, body;
-      for (uint32_t k = 0; k < sd.n_header + sd.n_body; k++) {
-        const fmt_mt_snapshot_seg& sg = b->snapshot_segs[sd.first_seg + k];
-        MergeTree::LoadedSeg l;
-        l.text.assign(reinterpret_cast<const char16_t*>(b->text + sg.text), sg.len);
-        if (sg.props != FMT_MT_NO_PROPS) {
-          l.hasProps = true;
-          for (uint32_t t = b->props_off[sg.props]; t < b->props_off[sg.props + 1]; t++)
-            l.props.emplace_back(static_cast<uint16_t>(b->props_kv[t] >> 16), static_cast<uint16_t>(b->props_kv[t] & 0xffff));
-        }
-        (k < sd.n_header ? head : body).push_back(std::move(l));
-      }
-      mt.loadSnapshot(head, body, sd.min_seq, sd.seq);
-    } else {
-      if (b->doc_init != nullptr && b->doc_init[2 * d + 1] > 0) {
-        const uint32_t off = b->doc_init[2 * d], len = b->doc_init[2 * d + 1];
-        mt.insertLocal(0, std::u16string(reinterpret_cast<const char16_t*>(b->text + off), len));
-      }
-      mt.startCollaboration(0, 0, 0);
-    }
+    startDoc(mt, b, d);
     const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
     std::vector<fmt_mt_catchup_range> cu;
     st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq,
@@ -255,6 +260,30 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
 }
 
 // ---------------------------------------------------------------- SharedMap
+// Every remove stamp of every final leaf of document d, in stamp order: (leaf index, client) pairs
+// into out[2 * k], at most cap pairs. Returns the number of pairs, or a negative FMT_E_* code.
+int orc_mt_removers(const fmt_mt_batch* b, uint32_t d, int32_t* out, uint32_t cap) {
+  MergeTree mt;
+  startDoc(mt, b, d);
+  const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
+  const int st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, nullptr);
+  if (st != FMT_OK) return st;
+  std::vector<const orc::Seg*> segs;
+  std::vector<int> blockOf;
+  int nBlocks = 0, depth = 0;
+  mt.collectLeaves(segs, blockOf, &nBlocks, &depth);
+  uint32_t k = 0;
+  for (size_t i = 0; i < segs.size(); i++)
+    for (const auto& r : segs[i]->removes) {
+      if (k < cap) {
+        out[2 * k] = static_cast<int32_t>(i);
+        out[2 * k + 1] = r.client;
+      }
+      k++;
+    }
+  return static_cast<int>(k);
+}
+
 int orc_map_replay(const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, uint32_t keyBound,
                    fmt_map_slot* out, uint32_t nThreads, double* seconds) {
   const auto t0 = std::chrono::steady_clock::now();

@@ -40,6 +40,7 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_dump.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_mt_summary.argtypes = [P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P,
                                      ctypes.c_int, P, P]
+        L.orc_mt_removers.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_mt_replay_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P,
                                           ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P,
                                           ctypes.c_uint32, P]
@@ -208,3 +209,19 @@ def xsadd_mixed(seed, kinds):
     out = np.zeros(len(k), dtype=np.float64)
     lib().orc_xsadd_mixed(_ptr(s), len(s), _ptr(k), _ptr(out), len(k))
     return out
+
+
+def mt_removers(batch, doc: int, cap: int = 1 << 16):
+    """Every remove stamp of every final leaf of `doc`, in stamp order: {leaf index: [client, ...]}."""
+    from fluidframework_amd.native import batch_struct
+
+    out = np.zeros(2 * cap, dtype=np.int32)
+    b, keep = batch_struct(batch)
+    n = lib().orc_mt_removers(ctypes.byref(b), doc, _ptr(out), cap)
+    del keep
+    if n < 0:
+        raise OracleError(f"remove-order replay failed ({n})")
+    res = {}
+    for k in range(min(n, cap)):
+        res.setdefault(int(out[2 * k]), []).append(int(out[2 * k + 1]))
+    return res

@@ -6,10 +6,11 @@
 
 #include "../../fluidframework_amd/csrc/mt_engine.h"
 
-template <bool Ob, class C>
+template <bool Ob, class C, bool Rm = false>
 static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
-                     fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup) {
-  using Doc = fmt_mt::Doc<Ob, C>;
+                     fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
+                     fmt_mt_remove_order* rmOrder, uint32_t capRm) {
+  using Doc = fmt_mt::Doc<Ob, C, Rm>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
   int status = FMT_OK;
@@ -46,6 +47,8 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     o.props = props + static_cast<size_t>(d) * Doc::kPropCap;
     o.catchup = catchup ? catchup + static_cast<size_t>(d) * capCatchup : nullptr;
     o.catchupCap = catchup ? capCatchup : 0u;
+    o.rmOrder = rmOrder ? rmOrder + static_cast<size_t>(d) * capRm : nullptr;
+    o.rmOrderCap = rmOrder ? capRm : 0u;
     new (doc.get()) Doc();
     doc->s = scratch.get();
     doc->run(in, o);
@@ -75,16 +78,23 @@ int emu_mt_capacity(int large, uint32_t* leaves, uint32_t* chars, uint32_t* prop
 // document). Like the runtime, batches holding obliterates run the Doc<true> variant (or always,
 // with forceOb).
 int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
-                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb, int large) {
+                  fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb, int large,
+                  fmt_mt_remove_order* rmOrder, uint32_t capRm) {
   bool ob = forceOb != 0;
   for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE;
   using S = fmt_mt::SmallTier;
   using G = fmt_mt::LargeTier;
-  if (large)
-    return ob ? replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup)
-              : replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup);
-  return ob ? replayAll<true, S>(b, headers, leaves, chars, props, catchup, capCatchup)
-            : replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup);
+  bool rm = false;
+  for (uint64_t i = 0; i < b->n_ops && !rm; i++) rm = (b->ops[i].flags & FMT_MT_F_RMORDER) != 0;
+  if (rm && ob) return FMT_E_UNSUPPORTED;
+  if (large) {
+    if (ob) return replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+    if (rm) return replayAll<false, G, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+    return replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+  }
+  if (ob) return replayAll<true, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+  if (rm) return replayAll<false, S, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+  return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
 }
 
 }  // extern "C"

@@ -87,6 +87,6 @@ def _intern(lst, x):
     return len(lst) - 1
 
 
-def snapshot_trees():
-    with open(os.path.join(GOLDEN, "snapshots_legacy.json")) as fh:
+def snapshot_trees(version="legacy"):
+    with open(os.path.join(GOLDEN, f"snapshots_{version}.json")) as fh:
         return json.load(fh)

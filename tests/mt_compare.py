@@ -11,7 +11,8 @@ import subprocess
 
 import numpy as np
 
-from fluidframework_amd.native import CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+from fluidframework_amd.native import (CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, RM_ORDER_DTYPE,
+                                       batch_struct)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 EMU_PATH = os.path.join(HERE, "_build", "libmt_emu.so")
@@ -28,7 +29,8 @@ def emu_lib():
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas", "-o",
                             EMU_PATH, src], check=True)
         L = ctypes.CDLL(EMU_PATH)
-        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                                              ctypes.c_void_p, ctypes.c_uint32]
         L.emu_mt_capacity.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         _emu = L
     return _emu
@@ -44,10 +46,11 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def emu_replay(batch, cap_catchup=0, force_ob=False, large=False):
+def emu_replay(batch, cap_catchup=0, force_ob=False, large=False, cap_rm=0):
     """Run the engine source under host emulation (small tier, or the large tier the runtime replays
     overflowing documents in); returns (headers, leaves, chars, props), plus the catch-up ranges
-    (n_docs, cap_catchup) when cap_catchup > 0."""
+    (n_docs, cap_catchup) when cap_catchup > 0, then the remove-order entries (n_docs, cap_rm) when
+    cap_rm > 0."""
     cl, cc, cp = emu_caps(large)
     n = batch.n_docs
     hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
@@ -55,12 +58,18 @@ def emu_replay(batch, cap_catchup=0, force_ob=False, large=False):
     chars = np.zeros(n * cc, dtype="<u2")
     props = np.zeros(n * cp, dtype=PROPSET_DTYPE)
     cu = np.zeros(n * cap_catchup, dtype=CATCHUP_DTYPE) if cap_catchup else None
+    rm = np.zeros(n * cap_rm, dtype=RM_ORDER_DTYPE) if cap_rm else None
     b, keep = batch_struct(batch)
     emu_lib().emu_mt_replay(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props),
-                            _p(cu) if cu is not None else None, cap_catchup, int(force_ob), int(large))
+                            _p(cu) if cu is not None else None, cap_catchup, int(force_ob), int(large),
+                            _p(rm) if rm is not None else None, cap_rm)
     del keep
     out = (hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp))
-    return out + (cu.reshape(n, cap_catchup),) if cap_catchup else out
+    if cap_catchup:
+        out = out + (cu.reshape(n, cap_catchup),)
+    if cap_rm:
+        out = out + (rm.reshape(n, cap_rm),)
+    return out
 
 
 def resolve_props(pid, table):

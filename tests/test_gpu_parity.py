@@ -280,3 +280,53 @@ def test_mt_obliterate_fixture_checkpoints(orc, engine):
     for d, text in enumerate(expected):
         leaves, chars, _ = engine.mt_doc(d, hdrs[d])
         assert visible_text(hdrs[d], leaves, chars) == text, d
+
+
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+def test_mt_v1_fixture_round_trip_on_gpu(orc, engine, name):
+    """The reference's SnapshotV1 fixtures load on the GPU (large tier) and summarize again as V1 to
+    the fixture's blobs byte for byte."""
+    from fluidframework_amd.summary import v1_summary
+    from test_snapshot_v1 import _load_v1
+
+    batch, head, bodies = _load_v1(name)
+    hdrs = _check_against_oracle(orc, engine, batch)
+    leaves, chars, props = engine.mt_doc(0, hdrs[0])
+    assert v1_summary(hdrs[0], leaves, chars, props, batch.keys, batch.values, batch.clients[0], {}) == (head, bodies)
+
+
+def _removers_check(orc, engine, batch, names):
+    from fluidframework_amd.summary import NOT_REMOVED, removers_from_engine, v1_summary
+
+    hdrs = _check_against_oracle(orc, engine, batch)
+    multi = 0
+    for d in range(batch.n_docs):
+        leaves, chars, props = engine.mt_doc(d, hdrs[d])
+        ops = batch.ops[int(batch.doc_op_offsets[d]) : int(batch.doc_op_offsets[d + 1])]
+        got = removers_from_engine(leaves, int(hdrs[d]["n_leaves"]), engine.mt_remove_order(d, hdrs[d]), ops)
+        want = orc.mt_removers(batch, d)
+        ms = int(hdrs[d]["min_seq"])
+        for i in range(int(hdrs[d]["n_leaves"])):
+            rm = int(leaves[i]["rm_seq"])
+            if rm != NOT_REMOVED and rm > ms:
+                assert got.get(i) == want.get(i), (d, i)
+                multi += len(want[i]) > 1
+        if names is not None:
+            assert v1_summary(hdrs[d], leaves, chars, props, batch.keys, batch.values, names(d), got) == \
+                v1_summary(hdrs[d], leaves, chars, props, batch.keys, batch.values, names(d), want), d
+    return multi
+
+
+def test_mt_v1_remove_order_on_reference_fixture_messages(orc, engine):
+    from test_snapshot_v1 import _collab_batch
+
+    batch = _collab_batch()
+    assert _removers_check(orc, engine, batch, lambda d: batch.clients[d]) > 0
+
+
+def test_mt_v1_remove_order_on_conflict_farm(orc, engine):
+    from fluidframework_amd.streams import flag_remove_order
+
+    batch = workloads.conflict_farm(2000, n_clients=8, ops_per_doc=1000, seed=31)
+    flag_remove_order(batch.ops, batch.doc_op_offsets)
+    assert _removers_check(orc, engine, batch, None) > 0

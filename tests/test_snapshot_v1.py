@@ -1,0 +1,169 @@
+"""SharedString SnapshotV1 summaries (merge-tree/src/snapshotV1.ts:90-265,
+snapshotChunks.ts:141-180, chosen by newMergeTreeSnapshotFormat in Client.summarize, client.ts:1569).
+
+Pinned by the reference's own v1 fixtures (sequence/src/test/snapshots/v1/*.json, committed under
+tests/golden/snapshots_v1.json): each loads (V1 chunks, or the legacy fixture of the same string) and
+summarizes again to the fixture's blobs byte for byte — oracle and the engine's large tier.
+
+Merge info (seq/client above minSeq, removedSeq/removedClient/removedClientIds) appears only for
+collaborative documents, which no reference fixture holds: that part is pinned by the oracle only
+(it keeps every remove stamp in order, stamps.ts:144-158). The engine's remove-order slab
+(FMT_MT_F_RMORDER) plus the first remover's op give the same ordered lists and the same bytes.
+"""
+import numpy as np
+import pytest
+
+from fluidframework_amd import summary
+from fluidframework_amd.streams import MergeTreeStreamBuilder, UnsupportedOp, flag_remove_order
+from golden_data import snapshot_trees
+from mt_compare import compare_doc, emu_caps, emu_replay
+from test_catchup import fixture_batch
+
+NAMES = ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"]
+
+
+def _v1_blobs(tree):
+    assert [e["path"] for e in tree["entries"]] == ["content"]
+    content = {e["path"]: e["value"]["contents"] for e in tree["entries"][0]["value"]["entries"]}
+    bodies = [content[f"body_{k}"] for k in range(len(content) - 1)]
+    assert set(content) == {"header", *[f"body_{k}" for k in range(len(bodies))]}
+    return content["header"], bodies
+
+
+def _load_v1(name):
+    head, bodies = _v1_blobs(snapshot_trees("v1")[name])
+    b = MergeTreeStreamBuilder()
+    b.begin_doc_from_summary(head, bodies)
+    return b.finish(), head, bodies
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_v1_fixture_round_trip(orc, name):
+    batch, head, bodies = _load_v1(name)
+    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+    assert rc == 0
+    got = summary.v1_summary(h[0], l[0], c[0], p[0], batch.keys, batch.values, batch.clients[0], {})
+    assert got == (head, bodies)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_legacy_fixture_resummarizes_as_v1_fixture(orc, name):
+    """The legacy and v1 fixtures are the same strings: load legacy, emit V1, get the v1 fixture."""
+    from test_oracle_golden import _blobs
+
+    blobs = _blobs(snapshot_trees()[name])
+    b = MergeTreeStreamBuilder()
+    b.begin_doc_from_summary(blobs["header"], blobs.get("body"))
+    batch = b.finish()
+    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+    assert rc == 0
+    _, head, bodies = _load_v1(name)
+    assert summary.v1_summary(h[0], l[0], c[0], p[0], batch.keys, batch.values, batch.clients[0], {}) == (head, bodies)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_engine_large_tier_v1_fixture_round_trip(name):
+    batch, head, bodies = _load_v1(name)
+    eh, el, ec, ep = emu_replay(batch, large=True)
+    assert eh[0]["status"] == 0
+    assert summary.v1_summary(eh[0], el[0], ec[0], ep[0], batch.keys, batch.values, batch.clients[0], {}) == (head, bodies)
+
+
+def test_v1_merge_info_segments_are_not_loadable():
+    head = ('{"version":"1","segmentCount":1,"length":1,"segments":[{"json":"a","seq":3,"client":"B"}],'
+            '"startIndex":0,"headerMetadata":{"minSequenceNumber":1,"sequenceNumber":3,'
+            '"orderedChunkMetadata":[{"id":"header"}],"totalLength":1,"totalSegmentCount":1}}')
+    with pytest.raises(UnsupportedOp):
+        MergeTreeStreamBuilder().begin_doc_from_summary(head, [])
+
+
+def _collab_batch():
+    batch, _ = fixture_batch()
+    batch.ops["flags"] &= ~np.uint32(2)  # no catch-up recording (FMT_MT_F_CATCHUP) here
+    flag_remove_order(batch.ops, batch.doc_op_offsets)
+    return batch
+
+
+def _doc_ops(batch, d):
+    return batch.ops[int(batch.doc_op_offsets[d]) : int(batch.doc_op_offsets[d + 1])]
+
+
+def test_engine_remove_order_matches_oracle_stamps():
+    """Engine (emulated) remove order == the oracle's remove stamp lists for every leaf removed above
+    minSeq; V1 summaries with merge info are byte-identical."""
+    import oracle as orc
+
+    batch = _collab_batch()
+    cl, cc, cp = emu_caps()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    assert rc == 0
+    eh, el, ec, ep, erm = emu_replay(batch, cap_rm=8192)
+    multi = 0
+    for d in range(batch.n_docs):
+        assert not compare_doc((oh[d], ol[d], oc[d], op[d]), (eh[d], el[d], ec[d], ep[d]))
+        want = orc.mt_removers(batch, d)
+        got = summary.removers_from_engine(el[d], int(eh[d]["n_leaves"]), erm[d][: eh[d]["n_rm_order"]],
+                                           _doc_ops(batch, d))
+        ms = int(eh[d]["min_seq"])
+        for i in range(int(eh[d]["n_leaves"])):
+            rm = int(el[d][i]["rm_seq"])
+            if rm != summary.NOT_REMOVED and rm > ms:
+                assert got.get(i) == want.get(i), (d, i)
+                multi += len(want[i]) > 1
+        v_or = summary.v1_summary(oh[d], ol[d], oc[d], op[d], batch.keys, batch.values, batch.clients[d], want)
+        v_en = summary.v1_summary(eh[d], el[d], ec[d], ep[d], batch.keys, batch.values, batch.clients[d], got)
+        assert v_or == v_en, d
+    assert multi > 0  # overlapping removes (more than one removedClientId) are exercised
+
+
+def test_v1_merge_info_shape():
+    """Segments above minSeq carry seq/client, removed ones removedSeq/removedClient/removedClientIds,
+    in the key order SnapshotV1.extractSync assigns them (snapshotV1.ts:226-250)."""
+    import json
+
+    import oracle as orc
+
+    batch = _collab_batch()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    seen_removed = seen_ins = 0
+    for d in range(batch.n_docs):
+        head, bodies = summary.v1_summary(oh[d], ol[d], oc[d], op[d], batch.keys, batch.values, batch.clients[d],
+                                          orc.mt_removers(batch, d))
+        segs = [s for blob in [head] + bodies for s in json.loads(blob)["segments"]]
+        for s in segs:
+            if isinstance(s, dict) and "json" in s:
+                keys = list(s)
+                assert keys[0] == "json"
+                if "seq" in s:
+                    seen_ins += 1
+                    assert keys[1:3] == ["seq", "client"] and s["seq"] > oh[d]["min_seq"]
+                if "removedSeq" in s:
+                    seen_removed += 1
+                    assert keys[-3:] == ["removedSeq", "removedClient", "removedClientIds"]
+                    assert s["removedClient"] == s["removedClientIds"][0]
+        meta = json.loads(head)["headerMetadata"]
+        assert meta["minSequenceNumber"] == oh[d]["min_seq"] and meta["sequenceNumber"] == oh[d]["cur_seq"]
+        assert [m["id"] for m in meta["orderedChunkMetadata"]] == ["header"] + [f"body_{k}" for k in range(len(bodies))]
+    assert seen_removed > 0 and seen_ins > 0
+
+
+def test_engine_remove_order_matches_oracle_on_conflict_farm():
+    import oracle as orc
+    from fluidframework_amd import workloads
+
+    batch = workloads.conflict_farm(24, n_clients=8, ops_per_doc=1000, seed=31)
+    flag_remove_order(batch.ops, batch.doc_op_offsets)
+    eh, el, ec, ep, erm = emu_replay(batch, cap_rm=1 << 14)
+    assert (eh["status"] == 0).all()
+    multi = 0
+    for d in range(batch.n_docs):
+        want = orc.mt_removers(batch, d)
+        got = summary.removers_from_engine(el[d], int(eh[d]["n_leaves"]), erm[d][: eh[d]["n_rm_order"]],
+                                           _doc_ops(batch, d))
+        ms = int(eh[d]["min_seq"])
+        for i in range(int(eh[d]["n_leaves"])):
+            rm = int(el[d][i]["rm_seq"])
+            if rm != summary.NOT_REMOVED and rm > ms:
+                assert got.get(i) == want.get(i), (d, i)
+                multi += len(want[i]) > 2
+    assert multi > 0  # three or more removers: the order the remove-client mask cannot give

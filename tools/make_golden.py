@@ -17,6 +17,7 @@ Outputs:
   replay_msgs_0.40.json.gz        the raw sequenced messages (ISequencedDocumentMessage JSON exactly as the
                                   fixture holds them) of MSG_FILES, for the JavaScript driver's tests
   snapshots_legacy.json           the legacy SharedString summary trees
+  snapshots_v1.json               the SnapshotV1 summary trees of the same strings (v1/*.json)
 """
 import json
 import os
@@ -32,6 +33,7 @@ from fluidframework_amd.streams import MT_OP_DTYPE, MergeTreeStreamBuilder  # no
 REF = "/root/reference/packages"
 RESULTS = f"{REF}/dds/merge-tree/src/test/results"
 SNAPSHOTS = f"{REF}/dds/sequence/src/test/snapshots/legacy"
+SNAPSHOTS_V1 = f"{REF}/dds/sequence/src/test/snapshots/v1"
 OUT = os.path.join(REPO, "tests", "golden")
 
 
@@ -113,7 +115,18 @@ def main() -> None:
         snaps[name] = tree
     with open(os.path.join(OUT, "snapshots_legacy.json"), "w") as fh:
         json.dump(snaps, fh, separators=(",", ":"))
+    write_v1_snapshots()
     print(f"wrote {len(files)} replay fixtures and {len(snaps)} snapshot trees to {OUT}")
+
+
+def write_v1_snapshots():
+    """sequence/src/test/snapshots/v1/*.json: SnapshotV1 summaries of the same detached strings
+    (generateSharedStrings.ts with newMergeTreeSnapshotFormat), checked by snapshotVersion.spec.ts."""
+    snaps = {}
+    for name in ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"]:
+        snaps[name] = json.load(open(os.path.join(SNAPSHOTS_V1, name + ".json")))
+    with open(os.path.join(OUT, "snapshots_v1.json"), "w") as fh:
+        json.dump(snaps, fh, separators=(",", ":"))
 
 
 if __name__ == "__main__":
