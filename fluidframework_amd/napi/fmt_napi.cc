@@ -18,6 +18,7 @@
 //   replayMergeTree(ctx, batch) -> Promise<ArrayBuffer headers>     fmt_mt_load + fmt_mt_run + fetch
 //   fetchDoc(ctx, doc, nLeaves, nChars, nProps) -> {leaves, chars, props}   fmt_mt_fetch_doc
 //   fetchCatchup(ctx, doc, n) -> ArrayBuffer                         fmt_mt_fetch_catchup
+//   fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer                     fmt_mt_fetch_remove_order
 //   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
 //   stats(ctx) -> {kernelMs, totalMs, ops, docs, bytesRead, bytesWritten, launches}
 //   sizes: {mtOp, mapOp, leaf, docResult, propset, mapSlot}          struct sizes for the JS views
@@ -473,6 +474,30 @@ napi_value FetchCatchup(napi_env env, napi_callback_info info) {
   return ab;
 }
 
+// fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer of n fmt_mt_remove_order records (SnapshotV1)
+napi_value FetchRemoveOrder(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 3 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchRemoveOrder: a replay is running on this context");
+    return nullptr;
+  }
+  uint32_t doc, n;
+  if (!get_u32(env, argv[1], "doc", &doc) || !get_u32(env, argv[2], "n", &n)) return nullptr;
+  void* p;
+  napi_value ab;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(n) * sizeof(fmt_mt_remove_order), &p, &ab));
+  int rc = fmt_mt_fetch_remove_order(c->ctx, doc, static_cast<fmt_mt_remove_order*>(p), n);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  return ab;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor fns[] = {
       {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
@@ -484,6 +509,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"replayMap", nullptr, ReplayMap, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchDoc", nullptr, FetchDoc, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchCatchup", nullptr, FetchCatchup, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchRemoveOrder", nullptr, FetchRemoveOrder, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
   };
   napi_define_properties(env, exports, sizeof fns / sizeof fns[0], fns);
   napi_value sizes, v;
