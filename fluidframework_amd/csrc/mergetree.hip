@@ -20,13 +20,13 @@ constexpr int kMtWavesLarge = 1;  // large tier: one document per workgroup, 1 w
 // Diagnostic build only: per-phase shader-clock totals summed over all waves (mt_engine.h stamp()).
 __device__ unsigned long long g_mtProfile[fmt_mt::kPfCount];
 
-// Small tier over all documents (docList == nullptr) or a list; documents that overflow it are
-// appended to esc (esc[0] = count, esc[1..] = document ids) for the large-tier pass. The large tier
-// runs over that list, writing leaves/chars/props to slab i of the list (headers stay per doc).
+// Small tier over all documents (docList == nullptr) or a list. The large tier runs over the list
+// of documents that overflowed it, writing leaves/chars/props to slab i of the list (headers stay
+// per document).
 template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                       const uint32_t* __restrict__ docList,
-                                                                      uint32_t count, uint32_t* esc) {
+                                                                      uint32_t count) {
   using Doc = fmt_mt::Doc<Ob, C, Rm>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
       o.catchup = nullptr;
       o.catchupCap = 0;
     }
-    if (batch.rmOrderOffsets) {
+    if (Rm && batch.rmOrderOffsets) {
       const uint64_t r0 = batch.rmOrderOffsets[d], r1 = batch.rmOrderOffsets[d + 1];
       o.rmOrder = out.rmOrder + r0;
       o.rmOrderCap = static_cast<uint32_t>(r1 - r0);
@@ -82,10 +82,6 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     Doc doc;
     doc.s = scratch;
     doc.run(in, o);
-    if (esc != nullptr && doc.status == FMT_E_CAPACITY && (threadIdx.x & 63) == 0) {
-      const uint32_t k = atomicAdd(esc, 1u);
-      esc[1 + k] = d;
-    }
 #if FMT_PROFILE && FMT_GPU
     if ((threadIdx.x & 63) == 0)
       for (int c = 0; c < fmt_mt::kPfCount; c++) atomicAdd(&g_mtProfile[c], static_cast<unsigned long long>(doc.prof[c]));
@@ -112,6 +108,17 @@ MtCaps mergeTreeCaps(bool large) {
                 static_cast<uint32_t>(fmt_mt::SmallTier::kCapChars), static_cast<uint32_t>(fmt_mt::SmallTier::kPropCap)};
 }
 
+// The documents the small tier could not hold (FMT_E_CAPACITY): esc[0] = count, esc[1..] = ids.
+__global__ __launch_bounds__(256) void collectOverflowKernel(const fmt_mt_doc_result* __restrict__ headers,
+                                                             uint32_t nDocs, uint32_t* esc) {
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nDocs; d += gridDim.x * blockDim.x) {
+    if (headers[d].status == FMT_E_CAPACITY) {
+      const uint32_t k = atomicAdd(esc, 1u);
+      esc[1 + k] = d;
+    }
+  }
+}
+
 template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                              uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream) {
@@ -126,7 +133,12 @@ static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out,
   const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
   hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
-                     docList, count, esc);
+                     docList, count);
+  if (esc != nullptr) {
+    const uint32_t g = (batch.nDocs + 255) / 256;
+    hipLaunchKernelGGL(collectOverflowKernel, dim3(g < 1024 ? (g > 0 ? g : 1) : 1024), dim3(256), 0, stream, out.headers,
+                       batch.nDocs, esc);
+  }
   return hipGetLastError();
 }
 
