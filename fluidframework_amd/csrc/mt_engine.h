@@ -118,6 +118,8 @@ struct Scratch {
   Blk<typename C::BId> blk[C::kMaxBlocks];
   HeapEnt heap[C::kHeapCap + 1];  // 1-based
   PropSet props[C::kPropCap];
+  uint32_t propEq[C::kPropCap];  // bit b of propEq[a]: matchProperties(set a, set b)
+  uint32_t propsEmpty;           // bit p: prop set p has no keys (matches undefined properties)
   typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
@@ -644,24 +646,47 @@ class Doc {
   }
 
   // ------------------------------------------------------------------ prop sets
-  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {  // properties.ts:32-61
+  // matchProperties (properties.ts:32-61; undefined ≡ {}) from the match matrix kept at interning.
+  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {
     if (a == b) return true;
-    const uint32_t na = a == kPropsUndef ? 0u : uni(s->props[a].n);
-    const uint32_t nb = b == kPropsUndef ? 0u : uni(s->props[b].n);
-    if (na != nb) return false;
-    for (uint32_t i = 0; i < na; i++) {
-      const uint32_t kv = uni(s->props[a].kv[i]);
-      bool found = false;
-      for (uint32_t k = 0; k < nb; k++) {
-        const uint32_t kv2 = uni(s->props[b].kv[k]);
-        if ((kv2 >> 16) == (kv >> 16)) {
-          if (kv2 != kv) return false;
-          found = true;
+    if (a == kPropsUndef) return ((uni(s->propsEmpty) >> b) & 1u) != 0;
+    if (b == kPropsUndef) return ((uni(s->propsEmpty) >> a) & 1u) != 0;
+    return ((uni(s->propEq[a]) >> b) & 1u) != 0;
+  }
+
+  // A new prop set q (kv[0..cnt)) was interned: lane p < q compares set p with it as maps
+  // (same size, every key of one present with the same value in the other), then both rows of the
+  // match matrix are updated.
+  FMT_DEV void propsIndex(int q, const V4& kv, uint32_t cnt) {
+    Lane<bool> eq;
+    FOR_LANES(l) {
+      bool m = l < q && s->props[l].n == cnt;
+      if (m) {
+#pragma unroll
+        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
+          if (i < cnt) {
+            bool found = false;
+#pragma unroll
+            for (uint32_t k = 0; k < FMT_MT_PROPS_MAX; k++)
+              if (k < cnt && (s->props[l].kv[k] >> 16) == (kv[i] >> 16)) found = s->props[l].kv[k] == kv[i];
+            m = m && found;
+          }
         }
       }
-      if (!found) return false;
+      LANE(eq) = m;
     }
-    return true;
+    const uint64_t mq = ballot(eq);
+    waveSync();
+    const uint32_t empty = uni(s->propsEmpty);
+    waveSync();
+    FOR_LANES(l) {
+      if (l < q && ((mq >> l) & 1ull)) s->propEq[l] |= 1u << q;
+      if (l == 0) {
+        s->propEq[q] = static_cast<uint32_t>(mq) | (1u << q);
+        s->propsEmpty = empty | (cnt == 0 ? 1u << q : 0u);
+      }
+    }
+    waveSync();
   }
 
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
@@ -716,6 +741,7 @@ class Doc {
       fail(FMT_E_CAPACITY);
       return 0;
     }
+    propsIndex(nProps, kv, cnt);
     s->props[nProps].n = cnt;
     for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) s->props[nProps].kv[i] = kv[i];
     waveSync();
@@ -1358,23 +1384,36 @@ class Doc {
     const int first = firstLeafOf(static_cast<uint32_t>(b));
     // One pass packs what the decisions need for every leaf of the block (at most 2 rows):
     // len | props << kLenBits | removed << 24 | removed at/below minSeq << 25 | insert at/below minSeq << 26
+    // | last UTF-16 unit is '\n' << 27 (TextSegment.canAppend, textSegment.ts:76-93: one LDS read for
+    // all leaves, at their char offsets from a scan of the block's lengths)
     const int r0 = first >> 6, r1 = (first + cnt - 1) >> 6;
     Lane<uint32_t> pk0, pk1;
     FOR_LANES(l) {
       LANE(pk0) = 0u;
       LANE(pk1) = 0u;
     }
+    uint32_t cs = charOffsetOf(first);  // running char offset of leaf first + k
+    uint32_t rowBase = cs;
     FOR_ROWS(r, r0, r1 + 1) {
+      Lane<uint32_t> blen;
+      FOR_LANES(l) {
+        const int idx = r * 64 + l;
+        LANE(blen) = idx >= first && idx < first + cnt ? fLen(LANE(W[0])[r]) : 0u;
+      }
+      uint32_t tot;
+      const Lane<uint32_t> ex = waveExclusiveSum(blen, &tot);
       FOR_LANES(l) {
         const uint32_t w0 = LANE(W[0])[r];
         const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]), rm = static_cast<int32_t>(LANE(W[2])[r]);
+        const uint32_t bl = LANE(blen);
+        const bool nl = bl > 0 && chRead(static_cast<int>(rowBase + LANE(ex) + bl - 1)) == 10u;
         const uint32_t p = fLen(w0) | (fProps(w0) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
-                           (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u);
+                           (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u) | (nl ? 1u << 27 : 0u);
         if (r == r0) LANE(pk0) = p;
         else LANE(pk1) = p;
       }
+      rowBase += tot;
     }
-    uint32_t cs = charOffsetOf(first);  // running char offset of leaf first + k
     stamp(kPfZChars);
     // serial decisions over <= 7 leaves: keep, merge into the previous kept leaf, or drop
     uint32_t mergeMask = 0, dropMask = 0;
@@ -1390,7 +1429,7 @@ class Doc {
       s->tmp[kMaxNodes + k] = len;
       if (((p >> 24) & 1u) == 0) {
         if ((p >> 26) & 1u) {
-          const bool lastNl = len > 0 && uni(chRead(static_cast<int>(cs + len - 1))) == 10u;
+          const bool lastNl = ((p >> 27) & 1u) != 0;
           const bool canAppend = prev >= 0 && !prevNl &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) ||
                                   len <= static_cast<uint32_t>(kGranularity)) &&
@@ -1596,6 +1635,7 @@ class Doc {
     }
     FOR_LANES(l) {
       for (int i = l; i < kMaxBlocks; i += 64) s->freeList[i] = static_cast<BId>(kMaxBlocks - 1 - i);
+      if (l == 0) s->propsEmpty = 0;
     }
     waveSync();
     nFree = kMaxBlocks;

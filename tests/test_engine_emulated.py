@@ -136,3 +136,37 @@ def test_large_tier_matches_oracle_on_long_conflict_farm(orc):
     for d in range(batch.n_docs):
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_emulated_engine_newline_segments_stop_appends(orc):
+    """Zamboni appends stop after a segment ending in '\\n' (TextSegment.canAppend,
+    textSegment.ts:76-93); texts with newlines, acked at once (minSeq = seq - 1), both tiers."""
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+
+    rng = np.random.default_rng(3)
+    b = MergeTreeStreamBuilder()
+    pieces = ["a\n", "bc", "\n", "xyz\n", "q", "rs", "\nt"]
+    for doc in range(6):
+        d = b.begin_doc()
+        length = 0
+        for k in range(300):
+            seq = k + 1
+            if k % 5 == 4 and length > 3:
+                a = int(rng.integers(0, length - 1))
+                contents = {"type": 1, "pos1": a, "pos2": a + 1}
+                length -= 1
+            else:
+                t = pieces[int(rng.integers(0, len(pieces)))]
+                contents = {"type": 0, "pos1": int(rng.integers(0, length + 1)), "seg": t}
+                length += len(t)
+            d.add_message({"clientId": "BC"[k % 2], "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+                           "minimumSequenceNumber": max(0, seq - 1 - doc), "contents": contents})
+    batch = b.finish()
+    for large in (False, True):
+        cl, cc, cp = emu_caps(large)
+        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=cl, cap_chars=cc, cap_props=64)
+        assert rc == 0
+        hdr, leaves, chars, props = emu_replay(batch, large=large)
+        for d in range(batch.n_docs):
+            diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+            assert not diffs, f"doc {d}: {diffs[:5]}"

@@ -57,9 +57,10 @@ def build(name, edits, rev=None):
     return out
 
 
-LB1 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves, 2)", "__launch_bounds__(64 * kMtWaves)")
-LB3 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves, 2)", "__launch_bounds__(64 * kMtWaves, 3)")
-LB4 = ("mergetree.hip", "__launch_bounds__(64 * kMtWaves, 2)", "__launch_bounds__(64 * kMtWaves, 4)")
+_LB = "return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);"
+LB1 = ("mergetree.hip", _LB, _LB.replace("kMtWaves, 2>", "kMtWaves, 1>"))
+LB3 = ("mergetree.hip", _LB, _LB.replace("kMtWaves, 2>", "kMtWaves, 3>"))
+LB4 = ("mergetree.hip", _LB, _LB.replace("kMtWaves, 2>", "kMtWaves, 4>"))
 NODPP = ("wave.h", "#define FMT_USE_DPP 1", "#define FMT_USE_DPP 0")
 
 NOFENCE = ("wave.h", """FMT_DEV void waveSync() {
@@ -100,7 +101,7 @@ VARIANTS = {
     "map_nt_w16": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 16;")],
     "map_nt_w1": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 1;")],
 }
-REVS = {"v1": "352970f"}  # committed engines: row-per-lane leaf table (E = 8 leaves per lane)
+REVS = {"v1": "352970f", "head": "1001e33"}  # committed engines to A/B against
 
 
 if __name__ == "__main__":
