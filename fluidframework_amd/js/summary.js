@@ -129,6 +129,75 @@ function legacySummary(segs, minSeq, keys, values, chunkSize) {
 }
 
 /**
+ * SnapshotV1 (newMergeTreeSnapshotFormat; snapshotV1.ts:90-265): every segment above minSeq with its
+ * merge info, the rest merged as in extractSync, chunked by SnapshotV1.chunkSize = 10000 lengths.
+ * @param segs - leaves in order: {insertSeq, insertClient, removedSeq (or NOT_REMOVED), text, kv}
+ * @param removers - {leaf index: [short client ids of its remove stamps, in stamp order]}
+ * @returns {header, bodies} - the blobs "header", "body_0", "body_1", ...
+ */
+function v1Summary(segs, minSeq, curSeq, keys, values, clientNames, removers, chunkSize) {
+	const out = []; // [json value, cachedLength]
+	let prev = null;
+	const segJson = (text, kv) => (kv === null || kv.length === 0 ? text : { text, props: propsObject(kv, keys, values) });
+	const flush = () => {
+		if (prev !== null) out.push([segJson(prev.text, prev.kv), prev.text.length]);
+	};
+	segs.forEach((s, i) => {
+		const removed = s.removedSeq !== NOT_REMOVED;
+		if (removed && s.removedSeq <= minSeq) return;
+		if (s.insertSeq <= minSeq && !removed) {
+			if (prev === null) prev = { text: s.text, kv: s.kv };
+			else if (!prev.text.endsWith("\n") &&
+				(prev.text.length <= TEXT_GRANULARITY || s.text.length <= TEXT_GRANULARITY) &&
+				propsMatch(prev.kv, s.kv)) prev = { text: prev.text + s.text, kv: prev.kv };
+			else {
+				flush();
+				prev = { text: s.text, kv: s.kv };
+			}
+			return;
+		}
+		flush();
+		prev = null;
+		const raw = { json: segJson(s.text, s.kv) };
+		if (s.insertSeq > minSeq) {
+			raw.seq = s.insertSeq;
+			raw.client = clientNames[s.insertClient];
+		}
+		if (removed) {
+			const ids = removers[i];
+			if (!ids || ids.length === 0) throw new Error(`leaf ${i}: remove order unknown`);
+			raw.removedSeq = s.removedSeq;
+			raw.removedClient = clientNames[ids[0]];
+			raw.removedClientIds = ids.map((c) => clientNames[c]);
+		}
+		out.push([raw, s.text.length]);
+	});
+	flush();
+	const size = chunkSize === undefined ? 10000 : chunkSize;
+	const chunks = [];
+	let start = 0;
+	do {
+		let n = 0, length = 0;
+		while (length < size && start + n < out.length) {
+			length += out[start + n][1];
+			n++;
+		}
+		chunks.push({ version: "1", segmentCount: n, length, segments: out.slice(start, start + n).map((x) => x[0]),
+			startIndex: start, headerMetadata: undefined });
+		start += n;
+	} while (start < out.length);
+	const header = chunks[0];
+	header.headerMetadata = {
+		minSequenceNumber: minSeq,
+		sequenceNumber: curSeq,
+		orderedChunkMetadata: [{ id: "header" }].concat(chunks.slice(1).map((_, k) => ({ id: `body_${k}` }))),
+		totalLength: chunks.reduce((n, c) => n + c.length, 0),
+		totalSegmentCount: out.length,
+	};
+	return { header: JSON.stringify(header), bodies: chunks.slice(1).map((c) => JSON.stringify(c)) };
+}
+
+/**
  * Catch-up messages (sequence.ts:949-1018): messages after minSeq, transformed ones rebuilt from
  * their delta ranges the way createOpsFromDelta builds them (sequence.ts:395-452).
  * @param messages - [{message, firstOp, count}] as the batch builder kept them.
@@ -175,4 +244,4 @@ function catchupMessages(messages, ranges, minSeq) {
 	return out;
 }
 
-module.exports = { mapSummary, legacySegments, legacySummary, catchupMessages, NOT_REMOVED };
+module.exports = { mapSummary, legacySegments, legacySummary, v1Summary, catchupMessages, NOT_REMOVED };

@@ -3,12 +3,16 @@
 // results as one JSON line. Case kinds:
 //   {kind: "string", segs, minSeq, keys, values, messages?, ranges?} → {header, body, catchupOps}
 //   {kind: "map", entries}                                           → {header, blobs}
+//   {kind: "v1", segs, minSeq, curSeq, keys, values, clients, removers} → {header, bodies}
 const fs = require("fs");
 const path = require("path");
 const summary = require(path.join(__dirname, "..", "..", "fluidframework_amd", "js", "summary.js"));
 
 const cases = JSON.parse(fs.readFileSync(process.argv[2], "utf8"));
 const out = cases.map((c) => {
+	if (c.kind === "v1") {
+		return summary.v1Summary(c.segs, c.minSeq, c.curSeq, c.keys, c.values, c.clients, c.removers);
+	}
 	if (c.kind === "map") {
 		return summary.mapSummary(c.entries.map(([k, v]) => [k, v === null ? undefined : v]));
 	}

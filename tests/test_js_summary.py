@@ -39,7 +39,7 @@ def _segs(leaves, chars, props):
         o, n = int(L["char_off"]), int(L["len"])
         pid = int(L["props"])
         kv = None if pid == 0xFFFF else [int(x) for x in props[pid]["kv"][: props[pid]["n"]]]
-        out.append({"insertSeq": int(L["ins_seq"]), "removedSeq": int(L["rm_seq"]),
+        out.append({"insertSeq": int(L["ins_seq"]), "insertClient": int(L["ins_client"]), "removedSeq": int(L["rm_seq"]),
                     "text": chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass"), "kv": kv})
     return out
 
@@ -104,3 +104,31 @@ def test_js_string_and_catchup_blobs_match_python_host(orc, tmp_path):
     for d, (g, (head, body, blob)) in enumerate(zip(got, want)):
         assert g["header"] == head and g["body"] == body, d
         assert blob is not None and g["catchupOps"] == blob, d
+
+
+def test_js_v1_summaries_match_reference_and_python_host(orc, tmp_path):
+    """SnapshotV1 from JS: the reference's v1 fixtures byte for byte, and on the reference's replay
+    fixture messages (merge info with ordered removedClientIds) the Python host's bytes."""
+    from test_snapshot_v1 import NAMES, _collab_batch, _load_v1
+
+    cases, want = [], []
+    for name in NAMES:
+        batch, head, bodies = _load_v1(name)
+        rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+        n = int(h[0]["n_leaves"])
+        cases.append({"kind": "v1", "segs": _segs(leaves[0][:n], chars[0], props[0]), "minSeq": int(h[0]["min_seq"]),
+                      "curSeq": int(h[0]["cur_seq"]), "keys": batch.keys, "values": batch.values,
+                      "clients": batch.clients[0], "removers": {}})
+        want.append((head, bodies))
+    batch = _collab_batch()
+    rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    for d in range(batch.n_docs):
+        n = int(h[d]["n_leaves"])
+        rem = orc.mt_removers(batch, d)
+        cases.append({"kind": "v1", "segs": _segs(leaves[d][:n], chars[d], props[d]), "minSeq": int(h[d]["min_seq"]),
+                      "curSeq": int(h[d]["cur_seq"]), "keys": batch.keys, "values": batch.values,
+                      "clients": batch.clients[d], "removers": {str(k): v for k, v in rem.items()}})
+        want.append(summary.v1_summary(h[d], leaves[d], chars[d], props[d], batch.keys, batch.values, batch.clients[d], rem))
+    got = _run(cases, tmp_path)
+    for k, (g, (head, bodies)) in enumerate(zip(got, want)):
+        assert g["header"] == head and g["bodies"] == bodies, k
