@@ -221,6 +221,7 @@ def main():
                            else "HBM streaming of 16-byte op records",
                 "bytes_per_launch": bytes_per_launch,
                 "avg_kernel_ms": avg_kernel_ms,
+                "lds_bank_conflict_rate": traffic.get("lds_bank_conflict_rate") if traffic else None,
             },
             "cpu_baseline": cpu,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",

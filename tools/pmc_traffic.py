@@ -9,7 +9,9 @@ Corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
     merge-tree's 4-32 B result stores are reported uncorrected).
 
 Usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel substring>
-       <workload key> <out json>
+       <workload key> <out json> [<lds counter_collection.csv>]
+With the LDS pass (SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE) the record also carries the kernel's
+LDS bank-conflict rate: conflict cycles / LDS-active cycles, summed over the launch's waves.
 The output JSON maps a workload key (e.g. "mt:100000x2000") to the per-launch traffic record that
 bench.py copies into its `roofline.traffic` field when it runs the same workload.
 """
@@ -41,6 +43,11 @@ def main():
         "source": [os.path.relpath(fetch_csv), os.path.relpath(write_csv)],
     }
     rec["bytes"] = rec["fetch_bytes"] + rec["write_bytes"]
+    if len(sys.argv) > 6:
+        conf, _ = per_launch(sys.argv[6], kernel, "SQ_LDS_BANK_CONFLICT")
+        act, _ = per_launch(sys.argv[6], kernel, "SQ_LDS_IDX_ACTIVE")
+        rec["lds_bank_conflict_rate"] = conf / act if act else None
+        rec["source"].append(os.path.relpath(sys.argv[6]))
     db = json.load(open(out)) if os.path.exists(out) else {}
     db[key] = rec
     json.dump(db, open(out, "w"), indent=1, sort_keys=True)
