@@ -20,7 +20,7 @@ const summary = require("./summary.js");
 const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3, MT_OBLITERATE = 4; // ops.ts:61-71
 const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
 const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
-const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2;
+const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
 const MAX_CLIENTS = 63;
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 20;
@@ -308,7 +308,9 @@ class MergeTreeStreamBuilder {
 	/**
 	 * The packed batch: the typed arrays the addon hands to fmt_mt_load. With {catchup: true} the
 	 * ops of messages a legacy summary keeps with regenerated contents get FMT_MT_F_CATCHUP: seq
-	 * above the document's final minSeq and refSeq != seq - 1 (sequence.ts:949-1018).
+	 * above the document's final minSeq and refSeq != seq - 1 (sequence.ts:949-1018). With
+	 * {removeOrder: true} the REMOVE ops above the final minSeq get FMT_MT_F_RMORDER, which the
+	 * SnapshotV1 summary needs (summarizeV1).
 	 */
 	finish(options) {
 		const offs = new BigUint64Array(this.docs.length + 1);
@@ -317,6 +319,21 @@ class MergeTreeStreamBuilder {
 			i += d.nOps;
 			offs[k + 1] = BigInt(i);
 		});
+		if (options && options.removeOrder) {
+			const v = this.ops.view;
+			let a = 0;
+			for (const d of this.docs) {
+				const b = a + d.nOps;
+				if (b > a) {
+					const finalMsn = v.getInt32((b - 1) * MT_OP_BYTES + 8, true);
+					for (let o = a * MT_OP_BYTES; o < b * MT_OP_BYTES; o += MT_OP_BYTES) {
+						if (v.getInt32(o, true) > finalMsn && v.getUint8(o + 27) === MT_REMOVE)
+							v.setUint32(o + 28, v.getUint32(o + 28, true) | FMT_MT_F_RMORDER, true);
+					}
+				}
+				a = b;
+			}
+		}
 		if (options && options.catchup) {
 			const v = this.ops.view;
 			let a = 0;
@@ -483,6 +500,7 @@ function readHeader(dv, d) {
 		depth: dv.getUint32(o + 32, true),
 		visibleLength: dv.getUint32(o + 36, true),
 		nCatchup: dv.getUint32(o + 40, true),
+		nRmOrder: dv.getUint32(o + 44, true),
 	};
 }
 
@@ -574,6 +592,45 @@ class MergeTreeReplay {
 			if (cu.length) out.catchupOps = JSON.stringify(cu);
 		}
 		return out;
+	}
+	/**
+	 * The ordered remove-stamp clients of every removed leaf: the first remover is the client of the
+	 * op whose seq is the leaf's removedSeq, later ones come from the kernel's remove-order slab
+	 * (ops flagged by finish({removeOrder: true})). {leaf index: [short client ids]}.
+	 */
+	removers(doc, segs) {
+		const h = this.header(doc);
+		const seqClient = new Map();
+		const ops = new DataView(this.batch.ops.buffer, this.batch.ops.byteOffset, this.batch.ops.byteLength);
+		for (let i = Number(this.batch.docOpOffsets[doc]); i < Number(this.batch.docOpOffsets[doc + 1]); i++)
+			seqClient.set(ops.getInt32(i * MT_OP_BYTES, true), ops.getUint8(i * MT_OP_BYTES + 26));
+		const out = {};
+		segs.forEach((s, i) => {
+			if (s.removedSeq !== undefined && seqClient.has(s.removedSeq)) out[i] = [seqClient.get(s.removedSeq)];
+		});
+		const dv = new DataView(native().fetchRemoveOrder(this.engine.ctx, doc, h.nRmOrder));
+		for (let k = 0; k < h.nRmOrder; k++) {
+			const leaf = dv.getUint32(8 * k, true), client = dv.getInt32(8 * k + 4, true);
+			if (leaf !== 0xffffffff && out[leaf]) out[leaf].push(client);
+		}
+		return out;
+	}
+	/**
+	 * SharedString.summarizeCore in the SnapshotV1 format (newMergeTreeSnapshotFormat,
+	 * snapshotV1.ts:90-265): {header, bodies} for the blobs header, body_0, body_1, ...
+	 */
+	summarizeV1(doc) {
+		const h = this.header(doc);
+		const segs = this.segments(doc);
+		const rem = this.removers(doc, segs);
+		const v1 = segs.map((s) => ({
+			insertSeq: s.insertSeq,
+			insertClient: s.insertClient,
+			removedSeq: s.removedSeq === undefined ? NOT_REMOVED : s.removedSeq,
+			text: s.text,
+			kv: s.kv,
+		}));
+		return summary.v1Summary(v1, h.minSeq, h.curSeq, this.batch.keys, this.batch.values, this.batch.clients[doc], rem);
 	}
 	/** MergeTreeTextHelper.getText from the local perspective (MergeTreeTextHelper.ts:28-87). */
 	getText(doc) {

@@ -8,6 +8,7 @@
 //                                          {"checked": n, "mismatches": [...]} as one JSON line
 //   node fixture_driver.js map             a SharedMap bunch replay through processMessagesCore (GPU)
 //   node fixture_driver.js summary         legacy summaries + catch-up blobs of each fixture (GPU)
+//   node fixture_driver.js v1              SnapshotV1 summaries of each fixture (GPU)
 const fs = require("fs");
 const path = require("path");
 const zlib = require("zlib");
@@ -126,6 +127,24 @@ async function summaries() {
 	}
 }
 
+/** SnapshotV1 summaries of each fixture's final state from GPU state (remove order recorded). */
+async function summariesV1() {
+	const fixtures = loadFixtures();
+	const b = new fmt.MergeTreeStreamBuilder();
+	for (const fx of fixtures) {
+		const doc = b.beginDoc(fx.groups[0].initialText, "A");
+		for (const g of fx.groups) for (const m of g.msgs) doc.addMessage(m);
+	}
+	const batch = b.finish({ removeOrder: true });
+	const eng = new fmt.Engine(0);
+	try {
+		const r = await eng.replayMergeTree(batch);
+		console.log(JSON.stringify(fixtures.map((fx, d) => r.summarizeV1(d))));
+	} finally {
+		eng.close();
+	}
+}
+
 /** Pack documents loaded from summaries ([[header, body, catchupOps], ...] in argv[3]) into argv[4]. */
 function packSummaries(input, outdir) {
 	const sums = JSON.parse(fs.readFileSync(input, "utf8"));
@@ -151,6 +170,8 @@ if (mode === "pack") {
 	packSummaries(process.argv[3], process.argv[4]);
 } else if (mode === "summary") {
 	summaries().catch((e) => { console.error(e); process.exit(1); });
+} else if (mode === "v1") {
+	summariesV1().catch((e) => { console.error(e); process.exit(1); });
 } else if (mode === "map") {
 	mapDemo().catch((e) => { console.error(e); process.exit(1); });
 } else {

@@ -166,3 +166,22 @@ def test_js_legacy_summaries_with_catchup_on_gpu(addon, orc):
         msgs = summary.catchup_messages(batch.messages[d], cu[d][: h[d]["n_catchup"]], int(h[d]["min_seq"]))
         assert got[d]["header"] == head and got[d]["body"] == body, d
         assert got[d]["catchupOps"] == summary.catchup_blob(msgs), d
+
+
+@pytest.mark.gpu
+def test_js_v1_summaries_on_gpu(addon, orc):
+    """summarizeV1() from GPU state (remove-order slab through the addon) == the Python host over
+    the oracle's state and remove stamps."""
+    from fluidframework_amd import summary
+    from test_snapshot_v1 import _collab_batch
+
+    r = _node(DRIVER, "v1", timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    batch = _collab_batch()
+    rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    assert rc == 0 and len(got) == batch.n_docs
+    for d in range(batch.n_docs):
+        head, bodies = summary.v1_summary(h[d], leaves[d], chars[d], props[d], batch.keys, batch.values,
+                                          batch.clients[d], orc.mt_removers(batch, d))
+        assert got[d]["header"] == head and got[d]["bodies"] == bodies, d
