@@ -34,7 +34,6 @@
 
 namespace fmt_mt {
 
-constexpr int kMaxClient = 31;       // remove-client set is a 32-bit mask
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
 constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:21)
 constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
@@ -54,6 +53,8 @@ struct SmallTier {
   static constexpr int kLenBits = 16, kBlkBits = 8;  // props: the remaining 8 bits
   static constexpr bool kHbmChars = false;
   static constexpr bool kUnroll = true;     // rows are compile-time VGPR elements
+  static constexpr int kWords = 5;          // remove-client set: W3 (writers 1..31)
+  static constexpr int kMaxClient = 31;
   using BId = uint8_t;
   using VR = V8;
 };
@@ -67,6 +68,8 @@ struct LargeTier {
   static constexpr int kLenBits = 17, kBlkBits = 10;  // props: the remaining 5 bits
   static constexpr bool kHbmChars = true;
   static constexpr bool kUnroll = false;    // rows indexed at run time (private memory)
+  static constexpr int kWords = 6;          // remove-client set: W3 (ids 0..31) + W5 (ids 32..63)
+  static constexpr int kMaxClient = 63;
   using BId = uint16_t;
   using VR = V32;
 };
@@ -133,7 +136,7 @@ FMT_DEV int32_t fClient(uint32_t w4) { return static_cast<int32_t>(static_cast<i
 FMT_DEV uint32_t mkW4(uint32_t id, int32_t client) { return (id & 0xFFFFFFu) | (static_cast<uint32_t>(client & 0xFF) << 24); }
 
 struct LeafRec {
-  uint32_t w[5];
+  uint32_t w[6];  // W0..W4, and W5 in the large tier
 };
 
 struct DocInputs {
@@ -209,7 +212,9 @@ class Doc {
 #else
   FMT_DEV void stamp(int) {}
 #endif
-  Lane<VR> W[5];  // W[f] element r of lane l = field f of leaf 64 r + l
+  static constexpr int kWords = C::kWords;
+  static constexpr int kMaxClient = C::kMaxClient;
+  Lane<VR> W[kWords];  // W[f] element r of lane l = field f of leaf 64 r + l
   Scratch<C>* s;
   uint16_t* gch = nullptr;  // large tier: the document's text, in its HBM output slab
   int n = 0;          // leaves
@@ -270,7 +275,7 @@ class Doc {
   FMT_DEV LeafRec readLeaf(int j) const {
     LeafRec r;
 #pragma unroll
-    for (int f = 0; f < 5; f++) r.w[f] = readField(j, f);
+    for (int f = 0; f < kWords; f++) r.w[f] = readField(j, f);
     return r;
   }
 
@@ -290,7 +295,7 @@ class Doc {
     const int rk = k >> 6, kl = k & 63, nr = (n + 64) >> 6;
     FOR_ROWS_DOWN(r, rk, nr) {
 #pragma unroll
-      for (int f = 0; f < 5; f++) {
+      for (int f = 0; f < kWords; f++) {
         const Lane<uint32_t> cur = row(W[f], r);
         const Lane<uint32_t> up = shflUp1(cur);
         if (r > rk) {
@@ -312,7 +317,7 @@ class Doc {
     const int rk = k >> 6, kl = k & 63, nr = rows();
     FOR_ROWS(r, rk, nr) {
 #pragma unroll
-      for (int f = 0; f < 5; f++) {
+      for (int f = 0; f < kWords; f++) {
         const Lane<uint32_t> cur = row(W[f], r);
         const Lane<uint32_t> dn = shflDown1(cur);
         const uint32_t carry = r + 1 < nr ? readlane(row(W[f], r + 1 < kRows ? r + 1 : r), 0) : 0u;
@@ -356,7 +361,7 @@ class Doc {
         LANE(live) = i < nNew;
       }
 #pragma unroll
-      for (int f = 0; f < 5; f++) {
+      for (int f = 0; f < kWords; f++) {
         const Lane<uint32_t> a = gather(row(W[f], r), src);
         const Lane<uint32_t> b = gather(row(W[f], r + 1 < kRows ? r + 1 : r), src);
         FOR_LANES(l) { LANE(W[f])[r] = LANE(live) ? (LANE(fromNext) && r + 1 < kRows ? LANE(b) : LANE(a)) : 0u; }
@@ -378,6 +383,15 @@ class Doc {
     return base;
   }
 
+  // Whether `client` holds a remove stamp on leaf 64 r + l (the remove-client set: W3, plus W5 for
+  // ids 32..63 in the large tier).
+  FMT_DEV bool removedBy(int l, int r, int client) const {
+    if constexpr (kWords > 5) {
+      if (client >= 32) return ((LANE(W[kWords - 1])[r] >> (client - 32)) & 1u) != 0;
+    }
+    return ((LANE(W[3])[r] >> client) & 1u) != 0;
+  }
+
   // Visible length of every leaf from PriorPerspective(refSeq, client) (perspective.ts:80-93).
   // Leaves removed at/below minSeq are never present for such a perspective (refSeq >= minSeq).
   // Empty slots have length 0.
@@ -387,9 +401,8 @@ class Doc {
         const uint32_t w0 = LANE(W[0])[r];
         const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]);
         const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
-        const uint32_t mask = LANE(W[3])[r];
         const int32_t ic = fClient(LANE(W[4])[r]);
-        const bool present = (ins <= refSeq || ic == client) && !(rm <= refSeq || ((mask >> client) & 1u));
+        const bool present = (ins <= refSeq || ic == client) && !(rm <= refSeq || removedBy(l, r, client));
         LANE(vis)[r] = present ? fLen(w0) : 0u;
       }
     }
@@ -902,11 +915,12 @@ class Doc {
     rec.w[2] = readField(j, 2);
     rec.w[3] = readField(j, 3);
     rec.w[4] = mkW4(nextId++, fClient(w4));
+    rec.w[5] = kWords > 5 ? readField(j, kWords - 1) : 0u;
     if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
       if (obUsed != 0) obRefsMove(fId(w4), fId(rec.w[4]), offset, -offset);
     }
     if constexpr (Rm) {
-      if (rmN > 0 && __builtin_popcount(rec.w[3]) >= 2) {  // copied in rmFlush
+      if (rmN > 0 && __builtin_popcount(rec.w[3]) + __builtin_popcount(rec.w[5]) >= 2) {  // copied in rmFlush
         if (rmPendN == 0) {
           rmPendFrom0 = fId(w4);
           rmPendTo0 = fId(rec.w[4]);
@@ -1039,6 +1053,7 @@ class Doc {
     rec.w[2] = static_cast<uint32_t>(kNotRemoved);
     rec.w[3] = 0;
     rec.w[4] = mkW4(nextId++, client);
+    rec.w[5] = 0;
     if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
       s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
       waveSync();
@@ -1196,7 +1211,7 @@ class Doc {
   // newest is not the inserter's own, the leaf starts out removed by those other clients' ones.
   FMT_DEV void obliterateOnInsert(int k, int refSeq, int client) {
     int minSeqOther = kNotRemoved, newestSeq = -1, newestClient = -1;
-    uint32_t mask = 0;
+    uint64_t mask = 0;
     bool any = false;
     for (int i = 0; i < obStartN; i++) {  // Obliterates.findOverlapping (:566-582)
       const int slot = uni(static_cast<int>(s->obStart[i]));
@@ -1208,7 +1223,7 @@ class Doc {
       if (oseq <= refSeq) continue;
       if (ocl != client) {
         any = true;
-        mask |= 1u << ocl;
+        mask |= 1ull << ocl;
         if (oseq < minSeqOther) minSeqOther = oseq;
       }
       if (oseq > newestSeq) {
@@ -1218,7 +1233,8 @@ class Doc {
     }
     if (any && newestClient != client) {
       writeField(k, 2, static_cast<uint32_t>(minSeqOther));
-      writeField(k, 3, mask);
+      writeField(k, 3, static_cast<uint32_t>(mask));
+      if constexpr (kWords > 5) writeField(k, kWords - 1, static_cast<uint32_t>(mask >> 32));
     }
   }
 
@@ -1338,7 +1354,8 @@ class Doc {
             const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
             if (rm == kNotRemoved) LANE(delta) |= 1u << r;
             LANE(W[2])[r] = static_cast<uint32_t>(rm < seq ? rm : seq);
-            LANE(W[3])[r] |= 1u << client;
+            if (kWords > 5 && client >= 32) LANE(W[kWords - 1])[r] |= 1u << (client - 32);
+            else LANE(W[3])[r] |= 1u << client;
           }
         }
       }
@@ -1631,6 +1648,7 @@ class Doc {
       LANE(W[1]) = z;
       LANE(W[2]) = z;
       LANE(W[3]) = z;
+      if constexpr (kWords > 5) LANE(W[kWords - 1]) = z;
       LANE(W[4]) = z;
     }
     FOR_LANES(l) {
@@ -1865,7 +1883,9 @@ class Doc {
       rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
       opIdx = static_cast<uint32_t>(i - in.begin);
-      if (op.client > kMaxClient || (op.type > FMT_MT_ANNOTATE && !(Ob && op.type == FMT_MT_OBLITERATE)))
+      if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63
+        fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
+      else if (op.type > FMT_MT_ANNOTATE && !(Ob && op.type == FMT_MT_OBLITERATE))
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op, text);
@@ -1935,6 +1955,7 @@ class Doc {
           L.ins_seq = static_cast<int32_t>(LANE(W[1])[r]);
           L.rm_seq = static_cast<int32_t>(LANE(W[2])[r]);
           L.rm_clients = LANE(W[3])[r];
+          if constexpr (kWords > 5) L.rm_clients |= static_cast<uint64_t>(LANE(W[kWords - 1])[r]) << 32;
           L.char_off = LANE(cst)[r];
           L.len = fLen(w0);
           L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[r]));
