@@ -32,6 +32,8 @@
 #include "../../include/fmt.h"
 #include "wave.h"
 
+#include <type_traits>
+
 namespace fmt_mt {
 
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
@@ -41,9 +43,10 @@ constexpr int32_t kNotRemoved = 0x7fffffff;
 
 // Capacity tiers. Every document first replays in the small tier (leaves in 40 VGPRs, text in
 // LDS, 2 waves/SIMD). A document that overflows it (FMT_E_CAPACITY) is replayed again from its
-// inputs in the large tier: 32 register rows (2048 leaves in 160 VGPRs, 1 wave/SIMD), 10-bit
-// block ids, and the text in the document's HBM output slab instead of LDS. Same engine source.
-// W0 = len | block << kLenBits | props << (kLenBits + kBlkBits).
+// inputs in the large tier: 32 rows of 2048 leaves in per-lane private memory, 10-bit block ids,
+// 63 writers, 64 prop sets, and the text in the document's HBM output slab instead of LDS. Same
+// engine source. Small: W0 = len | block << kLenBits | props << (kLenBits + kBlkBits); large:
+// W0 = len | block << kLenBits, props in W6.
 struct SmallTier {
   static constexpr int kRows = 8;          // rows of 64 leaves (one VR element per row)
   static constexpr int kCapChars = 2048;   // UTF-16 units per document (tombstones included)
@@ -55,6 +58,7 @@ struct SmallTier {
   static constexpr bool kUnroll = true;     // rows are compile-time VGPR elements
   static constexpr int kWords = 5;          // remove-client set: W3 (writers 1..31)
   static constexpr int kMaxClient = 31;
+  static constexpr bool kPropsWord = false; // prop-set id in W0
   using BId = uint8_t;
   using VR = V8;
 };
@@ -64,12 +68,13 @@ struct LargeTier {
   static constexpr int kCapChars = 131071;  // a leaf length (17 bits) can hold all of them
   static constexpr int kMaxBlocks = 1023;   // ids 0..1022; 1023 = no block
   static constexpr int kHeapCap = 1023;     // at most one heap entry per block (needsScour)
-  static constexpr int kPropCap = 31;       // ids 0..30; 31 = properties undefined
-  static constexpr int kLenBits = 17, kBlkBits = 10;  // props: the remaining 5 bits
+  static constexpr int kPropCap = 64;       // prop-set ids in their own word W6; 0xFFFF = undefined
+  static constexpr int kLenBits = 17, kBlkBits = 10;
   static constexpr bool kHbmChars = true;
   static constexpr bool kUnroll = false;    // rows indexed at run time (private memory)
-  static constexpr int kWords = 6;          // remove-client set: W3 (ids 0..31) + W5 (ids 32..63)
+  static constexpr int kWords = 7;          // remove-client set: W3 (ids 0..31) + W5 (ids 32..63); W6 props
   static constexpr int kMaxClient = 63;
+  static constexpr bool kPropsWord = true;  // prop-set id in W6 (up to 64 sets)
   using BId = uint16_t;
   using VR = V32;
 };
@@ -121,8 +126,9 @@ struct Scratch {
   Blk<typename C::BId> blk[C::kMaxBlocks];
   HeapEnt heap[C::kHeapCap + 1];  // 1-based
   PropSet props[C::kPropCap];
-  uint32_t propEq[C::kPropCap];  // bit b of propEq[a]: matchProperties(set a, set b)
-  uint32_t propsEmpty;           // bit p: prop set p has no keys (matches undefined properties)
+  typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type propEq[C::kPropCap];  // bit b of
+                                 // propEq[a]: matchProperties(set a, set b)
+  typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type propsEmpty;  // bit p: set p has no keys
   typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
@@ -136,7 +142,7 @@ FMT_DEV int32_t fClient(uint32_t w4) { return static_cast<int32_t>(static_cast<i
 FMT_DEV uint32_t mkW4(uint32_t id, int32_t client) { return (id & 0xFFFFFFu) | (static_cast<uint32_t>(client & 0xFF) << 24); }
 
 struct LeafRec {
-  uint32_t w[6];  // W0..W4, and W5 in the large tier
+  uint32_t w[7];  // W0..W4, and W5, W6 in the large tier
 };
 
 struct DocInputs {
@@ -191,14 +197,17 @@ class Doc {
   static constexpr int kPropCap = C::kPropCap;
   static constexpr uint32_t kLenMask = (1u << C::kLenBits) - 1u;
   static constexpr uint32_t kNoBlk = (1u << C::kBlkBits) - 1u;
-  static constexpr uint32_t kPropsUndef = (1u << (32 - C::kLenBits - C::kBlkBits)) - 1u;
+  static constexpr bool kPW = C::kPropsWord;
+  static constexpr uint32_t kPropsUndef = kPW ? 0xFFFFu : (1u << (32 - C::kLenBits - C::kBlkBits)) - 1u;
+  using PMask = typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type;
   static_assert(kMaxBlocks <= static_cast<int>(kNoBlk) && kPropCap <= static_cast<int>(kPropsUndef), "W0 field widths");
   static_assert(kRows <= 32, "row bitmasks are 32-bit");
   FMT_DEV static uint32_t fLen(uint32_t w0) { return w0 & kLenMask; }
   FMT_DEV static uint32_t fBlk(uint32_t w0) { return (w0 >> C::kLenBits) & kNoBlk; }
-  FMT_DEV static uint32_t fProps(uint32_t w0) { return w0 >> (C::kLenBits + C::kBlkBits); }
+  // (large tier: W0 holds no props; mkW0 ignores them and W6 keeps them)
+  FMT_DEV static uint32_t fProps(uint32_t w0) { return kPW ? 0u : w0 >> (C::kLenBits + C::kBlkBits); }
   FMT_DEV static uint32_t mkW0(uint32_t len, uint32_t blk, uint32_t props) {
-    return len | (blk << C::kLenBits) | (props << (C::kLenBits + C::kBlkBits));
+    return kPW ? len | (blk << C::kLenBits) : len | (blk << C::kLenBits) | (props << (C::kLenBits + C::kBlkBits));
   }
 
 #if FMT_PROFILE && FMT_GPU
@@ -271,6 +280,24 @@ class Doc {
   }
 
   FMT_DEV uint32_t readField(int j, int f) const { return readlane(selectRow(W[f], j >> 6), j & 63); }
+
+  // Prop-set id of leaf j / of leaf 64 r + l inside a FOR_LANES body, and setting it.
+  FMT_DEV uint32_t propsAt(int j) const {
+    if constexpr (kPW) return readField(j, kWords - 1);
+    else return fProps(readField(j, 0));
+  }
+  FMT_DEV uint32_t propsL(int l, int r) const {
+    if constexpr (kPW) return LANE(W[kWords - 1])[r];
+    else return fProps(LANE(W[0])[r]);
+  }
+  FMT_DEV void setPropsL(int l, int r, uint32_t p) {
+    if constexpr (kPW) {
+      LANE(W[kWords - 1])[r] = p;
+    } else {
+      const uint32_t w0 = LANE(W[0])[r];
+      LANE(W[0])[r] = mkW0(fLen(w0), fBlk(w0), p);
+    }
+  }
 
   FMT_DEV LeafRec readLeaf(int j) const {
     LeafRec r;
@@ -387,7 +414,7 @@ class Doc {
   // ids 32..63 in the large tier).
   FMT_DEV bool removedBy(int l, int r, int client) const {
     if constexpr (kWords > 5) {
-      if (client >= 32) return ((LANE(W[kWords - 1])[r] >> (client - 32)) & 1u) != 0;
+      if (client >= 32) return ((LANE(W[5])[r] >> (client - 32)) & 1u) != 0;
     }
     return ((LANE(W[3])[r] >> client) & 1u) != 0;
   }
@@ -662,9 +689,14 @@ class Doc {
   // matchProperties (properties.ts:32-61; undefined ≡ {}) from the match matrix kept at interning.
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {
     if (a == b) return true;
-    if (a == kPropsUndef) return ((uni(s->propsEmpty) >> b) & 1u) != 0;
-    if (b == kPropsUndef) return ((uni(s->propsEmpty) >> a) & 1u) != 0;
-    return ((uni(s->propEq[a]) >> b) & 1u) != 0;
+    if (a == kPropsUndef) return ((uniM(s->propsEmpty) >> b) & 1u) != 0;
+    if (b == kPropsUndef) return ((uniM(s->propsEmpty) >> a) & 1u) != 0;
+    return ((uniM(s->propEq[a]) >> b) & 1u) != 0;
+  }
+
+  FMT_DEV static uint32_t uniM(uint32_t x) { return uni(x); }
+  FMT_DEV static uint64_t uniM(uint64_t x) {
+    return static_cast<uint64_t>(uni(static_cast<uint32_t>(x))) | (static_cast<uint64_t>(uni(static_cast<uint32_t>(x >> 32))) << 32);
   }
 
   // A new prop set q (kv[0..cnt)) was interned: lane p < q compares set p with it as maps
@@ -690,13 +722,13 @@ class Doc {
     }
     const uint64_t mq = ballot(eq);
     waveSync();
-    const uint32_t empty = uni(s->propsEmpty);
+    const PMask empty = uniM(s->propsEmpty);
     waveSync();
     FOR_LANES(l) {
-      if (l < q && ((mq >> l) & 1ull)) s->propEq[l] |= 1u << q;
+      if (l < q && ((mq >> l) & 1ull)) s->propEq[l] |= PMask(1) << q;
       if (l == 0) {
-        s->propEq[q] = static_cast<uint32_t>(mq) | (1u << q);
-        s->propsEmpty = empty | (cnt == 0 ? 1u << q : 0u);
+        s->propEq[q] = static_cast<PMask>(mq) | (PMask(1) << q);
+        s->propsEmpty = empty | (cnt == 0 ? PMask(1) << q : PMask(0));
       }
     }
     waveSync();
@@ -915,7 +947,8 @@ class Doc {
     rec.w[2] = readField(j, 2);
     rec.w[3] = readField(j, 3);
     rec.w[4] = mkW4(nextId++, fClient(w4));
-    rec.w[5] = kWords > 5 ? readField(j, kWords - 1) : 0u;
+    rec.w[5] = kWords > 5 ? readField(j, 5) : 0u;
+    rec.w[6] = kPW ? readField(j, kWords - 1) : 0u;
     if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
       if (obUsed != 0) obRefsMove(fId(w4), fId(rec.w[4]), offset, -offset);
     }
@@ -1054,6 +1087,7 @@ class Doc {
     rec.w[3] = 0;
     rec.w[4] = mkW4(nextId++, client);
     rec.w[5] = 0;
+    rec.w[6] = kPropsUndef;
     if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
       s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
       waveSync();
@@ -1234,7 +1268,7 @@ class Doc {
     if (any && newestClient != client) {
       writeField(k, 2, static_cast<uint32_t>(minSeqOther));
       writeField(k, 3, static_cast<uint32_t>(mask));
-      if constexpr (kWords > 5) writeField(k, kWords - 1, static_cast<uint32_t>(mask >> 32));
+      if constexpr (kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
     }
   }
 
@@ -1354,7 +1388,7 @@ class Doc {
             const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
             if (rm == kNotRemoved) LANE(delta) |= 1u << r;
             LANE(W[2])[r] = static_cast<uint32_t>(rm < seq ? rm : seq);
-            if (kWords > 5 && client >= 32) LANE(W[kWords - 1])[r] |= 1u << (client - 32);
+            if (kWords > 5 && client >= 32) LANE(W[kWords > 5 ? 5 : 3])[r] |= 1u << (client - 32);
             else LANE(W[3])[r] |= 1u << client;
           }
         }
@@ -1365,14 +1399,13 @@ class Doc {
       for (;;) {
         const int j = firstSet(todo, nr);
         if (j < 0) break;
-        const uint32_t old = fProps(readField(j, 0));
+        const uint32_t old = propsAt(j);
         const uint32_t nw = applyProps(old, op.payload);
         if (status != FMT_OK) return false;
         FOR_ROWS(r, 0, nr) {
           FOR_LANES(l) {
-            if (((LANE(todo) >> r) & 1u) && fProps(LANE(W[0])[r]) == old) {
-              const uint32_t w0 = LANE(W[0])[r];
-              LANE(W[0])[r] = mkW0(fLen(w0), fBlk(w0), nw);
+            if (((LANE(todo) >> r) & 1u) && propsL(l, r) == old) {
+              setPropsL(l, r, nw);
               LANE(todo) &= ~(1u << r);
             }
           }
@@ -1424,7 +1457,8 @@ class Doc {
         const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]), rm = static_cast<int32_t>(LANE(W[2])[r]);
         const uint32_t bl = LANE(blen);
         const bool nl = bl > 0 && chRead(static_cast<int>(rowBase + LANE(ex) + bl - 1)) == 10u;
-        const uint32_t p = fLen(w0) | (fProps(w0) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
+        const uint32_t pr = propsL(l, r);
+        const uint32_t p = fLen(w0) | ((kPW ? (pr == kPropsUndef ? 0x7Fu : pr) : pr) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
                            (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u) | (nl ? 1u << 27 : 0u);
         if (r == r0) LANE(pk0) = p;
         else LANE(pk1) = p;
@@ -1441,7 +1475,8 @@ class Doc {
     for (int k = 0; k < cnt; k++) {
       const int j = first + k;
       const uint32_t p = (j >> 6) == r0 ? readlane(pk0, j & 63) : readlane(pk1, j & 63);
-      const uint32_t len = p & kLenMask, props = (p >> C::kLenBits) & kPropsUndef;
+      const uint32_t len = p & kLenMask, pp = (p >> C::kLenBits) & (kPW ? 0x7Fu : kPropsUndef);
+      const uint32_t props = kPW && pp == 0x7Fu ? kPropsUndef : pp;
       s->tmp[k] = cs;  // char offset and length, for the deletions below
       s->tmp[kMaxNodes + k] = len;
       if (((p >> 24) & 1u) == 0) {
@@ -1648,7 +1683,10 @@ class Doc {
       LANE(W[1]) = z;
       LANE(W[2]) = z;
       LANE(W[3]) = z;
-      if constexpr (kWords > 5) LANE(W[kWords - 1]) = z;
+      if constexpr (kWords > 5) {
+        LANE(W[5]) = z;
+        LANE(W[kWords - 1]) = z;
+      }
       LANE(W[4]) = z;
     }
     FOR_LANES(l) {
@@ -1684,6 +1722,7 @@ class Doc {
         LANE(W[2])[0] = static_cast<uint32_t>(kNotRemoved);
         LANE(W[3])[0] = 0u;
         LANE(W[4])[0] = w4;
+        if constexpr (kPW) LANE(W[kWords - 1])[0] = kPropsUndef;
       }
     }
     n = 1;
@@ -1730,8 +1769,7 @@ class Doc {
         if (status != FMT_OK) return;
         FOR_LANES(l) {
           if (LANE(op) == id) {
-            const uint32_t w0 = LANE(W[0])[r];
-            LANE(W[0])[r] = mkW0(fLen(w0), fBlk(w0), pid);
+            setPropsL(l, r, pid);
             LANE(op) = FMT_MT_NO_PROPS;
           }
         }
@@ -1777,6 +1815,7 @@ class Doc {
         LANE(W[0])[r] = live ? mkW0(len, static_cast<uint32_t>(j < H ? j / 7 : 0), kPropsUndef) : 0u;
         LANE(W[2])[r] = live ? static_cast<uint32_t>(kNotRemoved) : 0u;
         LANE(W[4])[r] = live ? mkW4(static_cast<uint32_t>(j + 1), FMT_NON_COLLAB_CLIENT) : 0u;
+        if constexpr (kPW) LANE(W[kWords - 1])[r] = live ? kPropsUndef : 0u;
       }
     }
     waveSync();
@@ -1955,11 +1994,12 @@ class Doc {
           L.ins_seq = static_cast<int32_t>(LANE(W[1])[r]);
           L.rm_seq = static_cast<int32_t>(LANE(W[2])[r]);
           L.rm_clients = LANE(W[3])[r];
-          if constexpr (kWords > 5) L.rm_clients |= static_cast<uint64_t>(LANE(W[kWords - 1])[r]) << 32;
+          if constexpr (kWords > 5) L.rm_clients |= static_cast<uint64_t>(LANE(W[5])[r]) << 32;
           L.char_off = LANE(cst)[r];
           L.len = fLen(w0);
           L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[r]));
-          L.props = fProps(w0) == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(fProps(w0));
+          const uint32_t pid = propsL(l, r);
+          L.props = pid == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(pid);
           L.block = static_cast<uint16_t>(LANE(ord)[r] + LANE(startFlag)[r] - 1u);
           L.pad = 0;
           out.leaves[idx] = L;

@@ -176,11 +176,10 @@ def test_emulated_engine_newline_segments_stop_appends(orc):
 def test_many_writers_overflow_to_large_tier(orc, n_clients):
     """More than 31 writers (T3's 64 clients: the observer + 63): the small tier's 32-bit remove-client
     set overflows (FMT_E_CAPACITY, so the runtime escalates) and the large tier's W3 + W5 set holds
-    them; bit-exact vs the oracle."""
+    them, with one prop set per writer's annotate value (up to 64 sets in W6); bit-exact vs the
+    oracle."""
     batch = workloads.conflict_farm(8, n_clients=n_clients, ops_per_doc=1500, seed=13)
     assert batch.ops["client"].max() > 31
-    ann = batch.ops["type"] == 2  # annotate with 4 distinct prop sets (the prop-set cap is 31)
-    batch.ops["payload"][ann] %= 4
     small = emu_replay(batch)[0]
     assert (small["status"] == -3).any()
     cl, cc, cp = emu_caps(large=True)
@@ -189,6 +188,7 @@ def test_many_writers_overflow_to_large_tier(orc, n_clients):
     hdr, leaves, chars, props = emu_replay(batch, large=True)
     assert (hdr["status"] == 0).all()
     assert any((leaves[d][: hdr[d]["n_leaves"]]["rm_clients"] >> np.uint64(32)).any() for d in range(batch.n_docs))
+    assert hdr["n_props"].max() > 32
     for d in range(batch.n_docs):
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
