@@ -1286,7 +1286,8 @@ class Doc {
     } else {
       if (!applyRange(op, delta)) return;
     }
-    recordCatchup(delta, op.type);  // one call site: the recording is inlined once
+    // one call site: the recording is inlined once; a sided obliterate raises OBLITERATE (:2249-2253)
+    recordCatchup(delta, op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
   }
 
   // Remove / annotate (after their boundary splits); fills `delta` for catch-up ops. Returns true
@@ -1295,7 +1296,7 @@ class Doc {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
     const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
     bool obliterate = false;
-    if constexpr (Ob) obliterate = op.type == FMT_MT_OBLITERATE;
+    if constexpr (Ob) obliterate = op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED;
     const int start = op.pos1, end = op.pos2;
     Lane<uint32_t> hits;
     FOR_LANES(l) { LANE(hits) = 0u; }
@@ -1330,36 +1331,48 @@ class Doc {
       }
       nr = rows();
     } else {
-      if (!splitAt(op.pos1, refSeq, client)) return false;
-      if (!splitAt(op.pos2, refSeq, client)) return false;
+      // obliterateRangeSided (mergeTree.ts:2083-2260). Places {pos, before?}: a non-sided op is
+      // {pos1, Before} .. {pos2 - 1, After} (:2282-2286); a sided one carries its sides in flags
+      // (client.ts:680-700). The boundaries are the places' Before edges (:2090-2091).
+      const bool sided = op.type == FMT_MT_OBLITERATE_SIDED;
+      const bool sB = !sided || (op.flags & FMT_MT_F_START_BEFORE) != 0;
+      const bool eB = sided && (op.flags & FMT_MT_F_END_BEFORE) != 0;
+      const int sPl = op.pos1, ePl = sided ? op.pos2 : op.pos2 - 1;
+      const int startPos = sB ? sPl : sPl + 1, endPos = eB ? ePl : ePl + 1, endW = ePl + 1;
+      if (!splitAt(startPos, refSeq, client)) return false;
+      if (!splitAt(endPos, refSeq, client)) return false;
       nr = rows();
       Lane<VR> vis, st;
       visLengths(refSeq, client, vis, nr);
       scanRows(vis, st, nr);
       stamp(kPfScan);
-      // obliterateRangeSided (mergeTree.ts:2083-2260) with start {pos1, Before}, end {pos2-1, After}:
-      // nodeMap under RemoteObliteratePerspective visits a leaf when it has length in the op's view
-      // or is not removed at all (so concurrent inserts strictly inside are caught), positions from
-      // the op's view: st < end, start < st + vis. Endpoint references go to the leaves holding
-      // pos1 and pos2 - 1 in the op's view (getContainingSegment, :858-886).
+      // nodeMap(start.pos, end.pos + 1) under RemoteObliteratePerspective visits a leaf when it has
+      // length in the op's view or is not removed at all (so concurrent inserts strictly inside are
+      // caught), positions from the op's view: st < end.pos + 1, start.pos < st + vis. markRemoved
+      // skips the exclusive endpoints (:2145-2152): a start After leaf whose full length ends at
+      // the start boundary, an end Before leaf present in the op's view that starts at the end
+      // boundary. Endpoint references go to the leaves holding start.pos and end.pos in the op's
+      // view (getContainingSegment, :858-886).
       int sLeaf = -1, eLeaf = -1, sOff = 0, eOff = 0;
       FOR_ROWS(r, 0, nr) {
         Lane<bool> ps, pe;
         FOR_LANES(l) {
           const int sp = static_cast<int>(LANE(st)[r]), v = static_cast<int>(LANE(vis)[r]);
           const bool removed = static_cast<int32_t>(LANE(W[2])[r]) != kNotRemoved;
-          if (!(v == 0 && removed) && r * 64 + l < n && sp < end && start < sp + v) LANE(hits) |= 1u << r;
-          LANE(ps) = v > 0 && sp <= start && start < sp + v;
-          LANE(pe) = v > 0 && sp <= end - 1 && end - 1 < sp + v;
+          const bool excl = (!sB && startPos == sp + static_cast<int>(fLen(LANE(W[0])[r]))) ||
+                            (eB && endPos == sp && v > 0);
+          if (!(v == 0 && removed) && !excl && r * 64 + l < n && sp < endW && sPl < sp + v) LANE(hits) |= 1u << r;
+          LANE(ps) = v > 0 && sp <= sPl && sPl < sp + v;
+          LANE(pe) = v > 0 && sp <= ePl && ePl < sp + v;
         }
         const uint64_t ms = ballot(ps), me = ballot(pe);
         if (sLeaf < 0 && ms != 0) {
           sLeaf = r * 64 + ctz64(ms);
-          sOff = start - static_cast<int>(readlane(row(st, r), ctz64(ms)));
+          sOff = sPl - static_cast<int>(readlane(row(st, r), ctz64(ms)));
         }
         if (eLeaf < 0 && me != 0) {
           eLeaf = r * 64 + ctz64(me);
-          eOff = end - 1 - static_cast<int>(readlane(row(st, r), ctz64(me)));
+          eOff = ePl - static_cast<int>(readlane(row(st, r), ctz64(me)));
         }
       }
       if (sLeaf < 0 || eLeaf < 0) {  // "segments cannot be undefined" (0xa3f)
@@ -1924,7 +1937,7 @@ class Doc {
       opIdx = static_cast<uint32_t>(i - in.begin);
       if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63
         fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
-      else if (op.type > FMT_MT_ANNOTATE && !(Ob && op.type == FMT_MT_OBLITERATE))
+      else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op, text);

@@ -306,7 +306,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       insertChars += op.len;
     } else if (op.type == FMT_MT_ANNOTATE) {
       if (op.payload >= b->n_props_ops) return setErr(c, FMT_E_DATA, "annotate props op id out of range");
-    } else if (op.type == FMT_MT_OBLITERATE) {
+    } else if (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED) {
       obliterates = true;
     } else if (op.type != FMT_MT_REMOVE) {
       return setErr(c, FMT_E_UNSUPPORTED, "op type not supported by this engine build");

@@ -17,10 +17,11 @@
 const path = require("path");
 const summary = require("./summary.js");
 
-const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3, MT_OBLITERATE = 4; // ops.ts:61-71
+const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3, MT_OBLITERATE = 4, MT_OBLITERATE_SIDED = 5; // ops.ts:61-71
 const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
 const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
 const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
+const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate places (client.ts:680-700)
 const MAX_CLIENTS = 63;
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 20;
@@ -287,6 +288,9 @@ class MergeTreeStreamBuilder {
 				pos1 = op.pos1; pos2 = -1; payload = r[0]; len = r[1];
 			} else if (type === MT_REMOVE || type === MT_OBLITERATE) {
 				pos1 = op.pos1; pos2 = op.pos2; // non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
+			} else if (type === MT_OBLITERATE_SIDED) {
+				pos1 = op.pos1.pos; pos2 = op.pos2.pos;
+				flags |= (op.pos1.before ? FMT_MT_F_START_BEFORE : 0) | (op.pos2.before ? FMT_MT_F_END_BEFORE : 0);
 			} else if (type === MT_ANNOTATE) {
 				if (op.adjust !== undefined && op.adjust !== null) throw new UnsupportedOp("annotate adjust");
 				pos1 = op.pos1; pos2 = op.pos2; payload = this.propsOp(op.props || {});

@@ -52,6 +52,7 @@ MAP_OP_DTYPE = np.dtype([("doc", "<u4"), ("key", "<u4"), ("seq", "<u4"), ("kind_
 assert MAP_OP_DTYPE.itemsize == 16
 
 MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
+MT_F_START_BEFORE, MT_F_END_BEFORE = 8, 16  # fmt.h FMT_MT_F_START_BEFORE / FMT_MT_F_END_BEFORE
 MT_F_GROUP_CONT = 1
 MT_F_CATCHUP = 2  # include/fmt.h FMT_MT_F_CATCHUP
 MT_F_RMORDER = 4  # include/fmt.h FMT_MT_F_RMORDER
@@ -179,7 +180,7 @@ class _DocBuilder:
         for k, op in enumerate(members):
             rec = self.owner._pack(op, seq, ref, msn, client)
             if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
-                rec = rec[:-1] + (1,)
+                rec = rec[:-1] + (rec[-1] | 1,)
             self.ops.append(rec)
 
     def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
@@ -247,6 +248,10 @@ class MergeTreeStreamBuilder:
             return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_REMOVE, 0)
         if t == MT_OBLITERATE:  # non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
             return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_OBLITERATE, 0)
+        if t == MT_OBLITERATE_SIDED:  # places {pos, before} (client.ts:680-700); sides in flags
+            p1, p2 = op["pos1"], op["pos2"]
+            flags = (MT_F_START_BEFORE if p1["before"] else 0) | (MT_F_END_BEFORE if p2["before"] else 0)
+            return (seq, ref, msn, int(p1["pos"]), int(p2["pos"]), 0, 0, client, MT_OBLITERATE_SIDED, flags)
         if t == MT_ANNOTATE:
             if op.get("adjust") is not None:
                 raise UnsupportedOp("annotate adjust")

@@ -89,6 +89,12 @@ extern "C" {
  * on the REMOVE ops with seq > the document's final minSeq (only leaves removed above minSeq carry
  * merge info). The first remover is the client of the op whose seq is the leaf's rm_seq. */
 #define FMT_MT_F_RMORDER 4u
+/* FMT_MT_OBLITERATE_SIDED (mergeTreeEnableSidedObliterate, client.ts:680-700): pos1/pos2 hold
+ * start.pos / end.pos of the InteriorSequencePlaces and these bits their sides (set = Side.Before,
+ * clear = Side.After). A non-sided FMT_MT_OBLITERATE (pos1, pos2) is the sided {pos1, Before} ..
+ * {pos2 - 1, After} (mergeTree.ts:2282-2286). */
+#define FMT_MT_F_START_BEFORE 8u
+#define FMT_MT_F_END_BEFORE 16u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */

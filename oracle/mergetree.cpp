@@ -425,8 +425,12 @@ std::pair<Seg*, int> MergeTree::getContainingSegment(int pos, const Perspective&
   return {found, offset};
 }
 
-void MergeTree::obliterateRange(int start, int end, const Perspective& p, Stamp stamp) {
-  const int startPos = start, endPos = end;  // {start, Before} and {end - 1, After}
+// obliterateRangeSided (mergeTree.ts:2083-2260). `start`/`end` are the places' pos; the boundaries
+// are the places' Before edges ({p, After} is the edge at p + 1, :2090-2091).
+void MergeTree::obliterateRange(int start, bool startBefore, int endPlace, bool endBefore, const Perspective& p,
+                                Stamp stamp) {
+  const int startPos = startBefore ? start : start + 1, endPos = endBefore ? endPlace : endPlace + 1;
+  const int end = endPlace + 1;  // nodeMap(start.pos, end.pos + 1): the end reference's segment included
   ensureIntervalBoundary(startPos, p);
   ensureIntervalBoundary(endPos, p);
   obPool_.push_back(std::make_unique<ObliterateInfo>());
@@ -434,7 +438,7 @@ void MergeTree::obliterateRange(int start, int end, const Perspective& p, Stamp 
   ob->stamp = stamp;
   ob->refSeq = p.refSeq;
   const auto s0 = getContainingSegment(start, p);
-  const auto s1 = getContainingSegment(end - 1, p);
+  const auto s1 = getContainingSegment(endPlace, p);
   if (s0.first == nullptr || s1.first == nullptr) throw DataError("segments cannot be undefined");  // 0xa3f
   ob->start.ob = ob;
   ob->end.ob = ob;
@@ -452,7 +456,7 @@ void MergeTree::obliterateRange(int start, int end, const Perspective& p, Stamp 
   bool exit = false;
   auto walk = [&](auto&& self, Block* b) -> void {
     for (int i = 0; i < b->childCount && !exit; i++) {
-      if (endPos <= pos) {
+      if (end <= pos) {
         exit = true;
         return;
       }
@@ -467,6 +471,12 @@ void MergeTree::obliterateRange(int start, int end, const Perspective& p, Stamp 
       }
       if (n->isLeaf) {
         Seg* s = static_cast<Seg*>(n);
+        // markRemoved's exclusive endpoints (:2145-2152): walked (so concurrent inserts between
+        // them and the range are reached) but not removed
+        if ((!startBefore && startPos == pos + s->len()) || (endBefore && endPos == pos && lenAt > 0)) {
+          pos = nextPos;
+          continue;
+        }
         if (!s->removed()) {
           newlyRemoved.push_back(s);
           s->removes.push_back(stamp);
@@ -791,8 +801,12 @@ void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const ui
     case FMT_MT_REMOVE:
       markRangeRemoved(op.pos1, op.pos2, p, stamp);
       break;
-    case FMT_MT_OBLITERATE:
-      obliterateRange(op.pos1, op.pos2, p, stamp);
+    case FMT_MT_OBLITERATE:  // {pos1, Before} .. {pos2 - 1, After} (mergeTree.ts:2282-2286)
+      obliterateRange(op.pos1, true, op.pos2 - 1, false, p, stamp);
+      break;
+    case FMT_MT_OBLITERATE_SIDED:  // client.ts:680-700
+      obliterateRange(op.pos1, (op.flags & FMT_MT_F_START_BEFORE) != 0, op.pos2,
+                      (op.flags & FMT_MT_F_END_BEFORE) != 0, p, stamp);
       break;
     case FMT_MT_ANNOTATE: {
       std::vector<std::pair<uint16_t, uint16_t>> kv;

@@ -240,7 +240,8 @@ class MergeTree {
   void markRangeRemoved(int start, int end, const Perspective& p, Stamp stamp);
   // obliterateRange (mergeTree.ts:2262-2290) → obliterateRangeSided (:2083-2260) with
   // start {pos1, Before} and end {pos2 - 1, After}.
-  void obliterateRange(int start, int end, const Perspective& p, Stamp stamp);
+  // obliterateRangeSided: start/end InteriorSequencePlaces {pos, before?} (mergeTree.ts:2083-2260)
+  void obliterateRange(int startPos, bool startBefore, int endPos, bool endBefore, const Perspective& p, Stamp stamp);
   // The obliterate branch of blockInsert (mergeTree.ts:1642-1746) for a new remote segment.
   void obliterateOnInsert(Seg* seg, const Perspective& p, Stamp stamp);
   // Obliterates (mergeTree.ts:515-625): seqOrdered + startOrdered (a SortedSegmentSet of the

@@ -81,7 +81,7 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
                   fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb, int large,
                   fmt_mt_remove_order* rmOrder, uint32_t capRm) {
   bool ob = forceOb != 0;
-  for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE;
+  for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE || b->ops[i].type == FMT_MT_OBLITERATE_SIDED;
   using S = fmt_mt::SmallTier;
   using G = fmt_mt::LargeTier;
   bool rm = false;

@@ -282,6 +282,25 @@ def test_mt_obliterate_fixture_checkpoints(orc, engine):
         assert visible_text(hdrs[d], leaves, chars) == text, d
 
 
+@pytest.mark.parametrize("rng_seed", [None, 5, 9])
+def test_mt_sided_obliterate_on_gpu(orc, engine, rng_seed):
+    """Sided obliterate (type 5): the reference obliterate fixtures re-encoded as equivalent sided ops
+    reach every text checkpoint (pinned); with exclusive start/end places moved in (rng_seed), engine ==
+    oracle bit for bit (parity unpinned: no reference fixture holds an exclusive place)."""
+    from golden_data import prefix_batch
+    from test_obliterate import OB_FIXTURES
+    from test_obliterate_sided import as_sided
+
+    batch, expected = prefix_batch(OB_FIXTURES[::3])
+    batch.ops = as_sided(batch.ops, None if rng_seed is None else np.random.default_rng(rng_seed))
+    hdrs = _check_against_oracle(orc, engine, batch)
+    assert (hdrs["status"] == 0).all()
+    if rng_seed is None:
+        for d, text in enumerate(expected):
+            leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+            assert visible_text(hdrs[d], leaves, chars) == text, d
+
+
 @pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
 def test_mt_v1_fixture_round_trip_on_gpu(orc, engine, name):
     """The reference's SnapshotV1 fixtures load on the GPU (large tier) and summarize again as V1 to
