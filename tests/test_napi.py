@@ -90,6 +90,35 @@ def test_js_packer_matches_python_packer(addon, tmp_path):
     assert meta["keys"] == py.keys and meta["values"] == py.values and meta["clients"] == py.clients
 
 
+def test_js_packer_sided_obliterate_matches_python(addon):
+    """Type 5 places {pos, before} pack as pos + FMT_MT_F_START_BEFORE / FMT_MT_F_END_BEFORE, alone
+    and as a GROUP member (with FMT_MT_F_GROUP_CONT), identically in the JS and Python packers."""
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+
+    sided = {"type": 5, "pos1": {"pos": 1, "before": False}, "pos2": {"pos": 3, "before": True}}
+    msgs = [
+        {"clientId": "B", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+         "contents": sided},
+        {"clientId": "C", "sequenceNumber": 2, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+         "contents": {"type": 3, "ops": [{"type": 1, "pos1": 0, "pos2": 1},
+                                          {"type": 5, "pos1": {"pos": 0, "before": True},
+                                           "pos2": {"pos": 1, "before": False}}]}},
+    ]
+    js = (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          "const b=new fmt.MergeTreeStreamBuilder();const d=b.beginDoc('abcdef','A');"
+          f"for(const m of {json.dumps(msgs)}) d.addMessage(m);"
+          "const r=b.finish();process.stdout.write(Buffer.from(r.ops.buffer,r.ops.byteOffset,r.ops.byteLength).toString('hex'))")
+    r = _node("-e", js)
+    assert r.returncode == 0, r.stderr
+    sb = MergeTreeStreamBuilder()
+    d = sb.begin_doc("abcdef")
+    for m in msgs:
+        d.add_message(m)
+    py = sb.finish()
+    assert bytes.fromhex(r.stdout.strip()) == py.ops.tobytes()
+    assert [int(f) for f in py.ops["flags"]] == [16, 0, 8 | 1]
+
+
 def test_js_map_packer_orders_bunches(addon):
     """Messages of one bunch share a sequenceNumber; the packer keeps their order via the ordinal."""
     r = _node("-e", """
