@@ -154,3 +154,25 @@ def test_host_packs_sided_places_and_exclusive_start_catches_concurrent_insert(o
     grp = _msg(1, 0, "B", {"type": 3, "ops": [{"type": 1, "pos1": 0, "pos2": 1}, sided["contents"]]})
     batch, _ = _replay_text(orc, [grp])
     assert int(batch.ops[1]["flags"]) == F_END_BEFORE | 1
+
+
+@pytest.mark.parametrize("rng_seed", [None, 5])
+def test_emulated_engine_sided_catchup_ranges_match_oracle(orc, rng_seed):
+    """Legacy catch-up ops (sequence.ts:395-452): a sided obliterate raises an OBLITERATE delta
+    (mergeTree.ts:2249-2253), merged like the non-sided one; engine ranges == oracle ranges."""
+    from fluidframework_amd import streams
+    from mt_compare import emu_replay
+
+    cap = 4096
+    batch, _ = _sided_prefix(None if rng_seed is None else np.random.default_rng(rng_seed))
+    streams.flag_catchup(batch.ops, batch.doc_op_offsets)
+    rc, oh, *_rest, ocu = orc.mt_replay_batch(batch, cap_catchup=cap)
+    eh, *_e, ecu = emu_replay(batch, cap_catchup=cap)
+    checked = 0
+    for d in range(batch.n_docs):
+        if int(eh[d]["status"]) == FMT_E_CAPACITY:  # replayed in the large tier by the runtime
+            continue
+        n = int(oh[d]["n_catchup"])
+        assert int(eh[d]["n_catchup"]) == n and np.array_equal(ecu[d][:n], ocu[d][:n]), d
+        checked += int((ocu[d][:n]["type"] == 4).sum())
+    assert checked > 0  # obliterate ranges were among those compared
