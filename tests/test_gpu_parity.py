@@ -301,6 +301,28 @@ def test_mt_sided_obliterate_on_gpu(orc, engine, rng_seed):
             assert visible_text(hdrs[d], leaves, chars) == text, d
 
 
+def test_mt_sided_obliterate_catchup_ranges_on_gpu(orc, engine):
+    """Catch-up ranges of sided obliterates with exclusive places (OBLITERATE deltas) == oracle."""
+    from fluidframework_amd import streams
+    from test_obliterate import OB_FIXTURES
+    from test_obliterate_sided import as_sided
+
+    cap = 4096
+    batch, _ = prefix_batch(OB_FIXTURES[::3])
+    batch.ops = as_sided(batch.ops, np.random.default_rng(5))
+    streams.flag_catchup(batch.ops, batch.doc_op_offsets)
+    hdrs = _gpu_mt(engine, batch)
+    rc, oh, ol, oc, op, _, ocu = orc.mt_replay_batch(batch, threads=16, cap_catchup=cap)
+    assert rc == 0 and (hdrs["status"] == 0).all(), np.unique(hdrs["status"])
+    obl = 0
+    for d in range(batch.n_docs):
+        n = int(oh[d]["n_catchup"])
+        got = engine.mt_catchup(d, hdrs[d])
+        assert len(got) == n and np.array_equal(got, ocu[d][:n]), d
+        obl += int((got["type"] == 4).sum())
+    assert obl > 0
+
+
 @pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
 def test_mt_v1_fixture_round_trip_on_gpu(orc, engine, name):
     """The reference's SnapshotV1 fixtures load on the GPU (large tier) and summarize again as V1 to
