@@ -9,8 +9,11 @@ namespace fmt_kernels {
 
 // ---- SharedMap LWW (map_lww.hip)
 size_t mapLwwLdsBytes(uint32_t keyBound);
+// key pools beyond the LDS table take the HBM-table path, which needs 2 * key_bound u32 of scratch
+// per document (nullptr otherwise)
+bool mapLwwNeedsScratch(uint32_t keyBound);
 hipError_t launchMapLww(const fmt_map_op* ops, const uint64_t* offsets, uint32_t nDocs, uint32_t keyBound,
-                        fmt_map_slot* out, int* error, int numCUs, hipStream_t stream);
+                        fmt_map_slot* out, int* error, int numCUs, hipStream_t stream, uint32_t* scratch);
 
 // ---- merge-tree replay (mergetree.hip)
 struct MtDeviceBatch {

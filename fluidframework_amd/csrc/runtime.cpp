@@ -54,6 +54,7 @@ struct fmt_ctx {
   DevBuf<fmt_map_op> mapOps;
   DevBuf<uint64_t> mapOffs;
   DevBuf<fmt_map_slot> mapOut;
+  DevBuf<uint32_t> mapScratch;  // kill / first tables of the HBM-table path (large key pools)
   DevBuf<int> errWord;
   uint64_t mapNOps = 0;
   uint32_t mapDocs = 0, mapKeyBound = 0;
@@ -147,6 +148,7 @@ void fmt_close(fmt_ctx* c) {
   c->mapOps.release();
   c->mapOffs.release();
   c->mapOut.release();
+  c->mapScratch.release();
   c->errWord.release();
   c->mtOps.release();
   c->mtOffs.release();
@@ -207,8 +209,6 @@ int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_
                  uint32_t keyBound) {
   if (c == nullptr || (nOps > 0 && ops == nullptr) || offs == nullptr || keyBound == 0)
     return setErr(c, FMT_E_USAGE, "fmt_map_load: bad arguments");
-  if (fmt_kernels::mapLwwLdsBytes(keyBound) > 160 * 1024)
-    return setErr(c, FMT_E_UNSUPPORTED, "key_bound too large for the LDS key-table path");
   if (offs[0] != 0 || offs[nDocs] != nOps) return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
   for (uint32_t d = 0; d < nDocs; d++) {
     if (offs[d + 1] < offs[d]) return setErr(c, FMT_E_USAGE, "doc_op_offsets not monotone");
@@ -238,9 +238,14 @@ int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_
 static int runMap(fmt_ctx* c, const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, uint32_t keyBound,
                   uint64_t nOps, fmt_map_slot* out) {
   FMT_HIP(c, hipSetDevice(c->device));
+  uint32_t* scratch = nullptr;
+  if (fmt_kernels::mapLwwNeedsScratch(keyBound)) {  // key pool beyond the LDS table: HBM tables
+    FMT_HIP(c, c->mapScratch.reserve(static_cast<size_t>(nDocs) * keyBound * 2));
+    scratch = c->mapScratch.p;
+  }
   FMT_HIP(c, hipMemsetAsync(c->errWord.p, 0, sizeof(int), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
-  FMT_HIP(c, fmt_kernels::launchMapLww(ops, offs, nDocs, keyBound, out, c->errWord.p, c->numCUs, c->stream));
+  FMT_HIP(c, fmt_kernels::launchMapLww(ops, offs, nDocs, keyBound, out, c->errWord.p, c->numCUs, c->stream, scratch));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   c->stats = fmt_stats{};
@@ -272,8 +277,6 @@ int fmt_map_replay_device(fmt_ctx* c, const fmt_map_op* dOps, const uint64_t* dO
                           uint32_t keyBound, fmt_map_slot* dOut) {
   if (c == nullptr || dOffs == nullptr || dOut == nullptr || keyBound == 0)
     return setErr(c, FMT_E_USAGE, "fmt_map_replay_device: bad arguments");
-  if (fmt_kernels::mapLwwLdsBytes(keyBound) > 160 * 1024)
-    return setErr(c, FMT_E_UNSUPPORTED, "key_bound too large for the LDS key-table path");
   return runMap(c, dOps, dOffs, nDocs, keyBound, 0, dOut);
 }
 

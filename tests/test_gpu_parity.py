@@ -81,6 +81,21 @@ def test_map_lww_large_key_pool(orc, engine):
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("n_docs,n_ops,key_pool", [(512, 2000, 5000), (24, 3000, 1 << 20)])
+def test_map_lww_key_pool_beyond_lds(orc, engine, n_docs, n_ops, key_pool):
+    """Key pools over the LDS table's 2560 ids (SURVEY §8d's U[0, 2^20) variant) replay with the key
+    tables in HBM (mapLwwHbmKernel + mapLwwFinishKernel), bit-exact vs the oracle."""
+    batch = workloads.map_stream(n_docs, n_ops, key_pool=key_pool, seed=23)
+    engine.map_load(batch)
+    engine.map_run()
+    got = engine.map_fetch()
+    exp, _ = orc.map_replay(batch, threads=16)
+    assert np.array_equal(got, exp)
+    assert int((got["value"] != 0xFFFFFFFF).sum()) > n_docs  # live keys were found
+    engine.map_run()  # a second run over the same tables gives the same state
+    assert np.array_equal(engine.map_fetch(), exp)
+
+
 def test_map_lww_ragged_documents(orc, engine):
     """Document lengths straddle the register-held path (≤1024 ops) and the streaming path, with
     empty and one-op documents in between."""
