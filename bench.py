@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--unique-docs", type=int, default=0, help="0 = all documents distinct")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--key-pool", type=int, default=20, help="map: key ids per document (> 2560 takes the HBM-table path)")
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -76,7 +77,7 @@ def main():
             raise SystemExit("--docs must be a multiple of --unique-docs")
         batch = workloads.conflict_farm(uniq, n_clients=args.clients, ops_per_doc=opd, seed=seed, replicas=docs // uniq)
     else:
-        batch = workloads.map_stream(docs, opd, key_pool=20, seed=seed)
+        batch = workloads.map_stream(docs, opd, key_pool=args.key_pool, seed=seed)
     n_ops = len(batch.ops)
     log(rank, f"[bench] generated {docs} docs / {n_ops} ops in {time.time() - t:.1f}s")
 
@@ -176,7 +177,7 @@ def main():
     # HBM bytes per launch from the committed rocprofv3 PMC passes of this same workload
     # (tools/pmc_traffic.py; gfx950 FETCH_SIZE correction applied there), or null.
     traffic = None
-    tkey = f"{args.workload}:{docs}x{opd}"
+    tkey = f"{args.workload}:{docs}x{opd}" + ("" if mt or args.key_pool == 20 else f"k{args.key_pool}")
     tpath = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath)).get(tkey)
@@ -202,6 +203,7 @@ def main():
                 "docs_per_gpu": docs,
                 "clients": args.clients,
                 "ops_per_doc": opd,
+                **({} if mt or args.key_pool == 20 else {"key_pool": args.key_pool}),
                 "ops_per_step": n_ops * world,
                 "parallelism": f"doc-shard x{world}",
             },
