@@ -277,7 +277,9 @@ int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
  * SharedMap.processMessagesCore (map/src/map.ts:288-311) → MapKernel.tryProcessMessage
  * (map/src/mapKernel.ts:619-630) for every sequenced set/delete/clear of every document, applied
  * in seq order (remote handlers mapKernel.ts:708-850). ops of document d are
- * ops[doc_op_offsets[d] .. doc_op_offsets[d+1]) in seq order; key ids < key_bound. */
+ * ops[doc_op_offsets[d] .. doc_op_offsets[d+1]) in seq order; key ids < key_bound. Up to 2560
+ * key ids the per-key tables live in LDS; larger key_bound takes the HBM-table kernel (2 * key_bound
+ * u32 of device scratch per document, owned by the ctx). */
 int fmt_map_load(fmt_ctx* ctx, const fmt_map_op* ops, uint64_t n_ops,
                  const uint64_t* doc_op_offsets, uint32_t n_docs, uint32_t key_bound);
 /* Replay the staged batch (asynchronous on the ctx stream). */
