@@ -170,31 +170,25 @@ size_t mapLwwLdsBytes(uint32_t keyBound) { return static_cast<size_t>(kWaves) * 
 
 // Key pools too large for the per-wave LDS table (more than 2560 key ids): the same two reductions
 // with the key tables in HBM. `last` is the output slot itself viewed as one u64 per (doc, key);
-// kill and first live in a scratch slab of 2 * key_bound u32 per document; each wave initialises
-// its own document's tables. One wave per document:
+// kill and first live in a scratch slab of 2 * key_bound u32 per document (all kill rows, then all
+// first rows), filled by hipMemsetAsync before the launch. One wave per document:
 // pass 1 (kills) and pass 2 (surviving sets) are device-scope atomics; pass 2 reads kill[] with
 // agent-scope loads, so a line another wave pulled into this CU's L1 is never read stale.
 // mapLwwFinish then turns each slot's (seq << 32 | value) into (value, birth seq).
 __global__ __launch_bounds__(64 * kWaves) void mapLwwHbmKernel(const fmt_map_op* __restrict__ ops,
                                                        const uint64_t* __restrict__ offsets, uint32_t nDocs,
                                                        uint32_t keyBound, unsigned long long* __restrict__ last,
-                                                       uint32_t* __restrict__ scratch, int* __restrict__ error) {
+                                                       uint32_t* __restrict__ killAll, uint32_t* __restrict__ firstAll,
+                                                       int* __restrict__ error) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const uint4* recs = reinterpret_cast<const uint4*>(ops);
   for (uint32_t doc = blockIdx.x * kWaves + wave; doc < nDocs; doc += gridDim.x * kWaves) {
     const uint64_t begin = offsets[doc], end = offsets[doc + 1];
-    uint32_t* kill = scratch + static_cast<uint64_t>(doc) * keyBound * 2;
-    uint32_t* first = kill + keyBound;
-    unsigned long long* lastD = last + static_cast<uint64_t>(doc) * keyBound;
-    for (uint32_t k = lane; k < keyBound; k += 64) {
-      lastD[k] = 0;
-      kill[k] = 0;
-      first[k] = 0xffffffffu;
-    }
-    // the table stores complete before this wave's atomics reach them
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    __builtin_amdgcn_wave_barrier();
+    const uint64_t row = static_cast<uint64_t>(doc) * keyBound;
+    uint32_t* kill = killAll + row;
+    uint32_t* first = firstAll + row;
+    unsigned long long* lastD = last + row;
     uint32_t clearMax = 0;
     for (uint64_t i = begin + lane; i < end; i += 64) {
       const uint4 r = recs[i];
@@ -225,15 +219,13 @@ __global__ __launch_bounds__(64 * kWaves) void mapLwwHbmKernel(const fmt_map_op*
   }
 }
 
-__global__ void mapLwwFinishKernel(uint64_t nSlots, uint32_t keyBound, fmt_map_slot* __restrict__ out,
-                                   const uint32_t* __restrict__ scratch) {
+__global__ void mapLwwFinishKernel(uint64_t nSlots, fmt_map_slot* __restrict__ out, const uint32_t* __restrict__ first) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nSlots;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const unsigned long long l = reinterpret_cast<const unsigned long long*>(out)[i];
-    const uint64_t doc = i / keyBound, k = i - doc * keyBound;
     fmt_map_slot s;
     s.value = l != 0 ? static_cast<uint32_t>(l) : FMT_MAP_ABSENT;
-    s.birth_seq = l != 0 ? scratch[doc * keyBound * 2 + keyBound + k] : 0;
+    s.birth_seq = l != 0 ? first[i] : 0;
     out[i] = s;
   }
 }
@@ -244,14 +236,20 @@ hipError_t launchMapLww(const fmt_map_op* ops, const uint64_t* offsets, uint32_t
                         fmt_map_slot* out, int* error, int numCUs, hipStream_t stream, uint32_t* scratch) {
   if (mapLwwNeedsScratch(keyBound)) {
     const uint64_t nSlots = static_cast<uint64_t>(nDocs) * keyBound;
-    hipError_t e;
+    uint32_t* kill = scratch;
+    uint32_t* first = scratch + nSlots;
+    // tables start as last = 0, kill = 0, first = 0xffffffff (fill kernels at full HBM rate)
+    hipError_t e = hipMemsetAsync(out, 0, nSlots * sizeof(fmt_map_slot), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(kill, 0, nSlots * sizeof(uint32_t), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(first, 0xff, nSlots * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
     const uint32_t grid = nDocs == 0 ? 1 : (nDocs + kWaves - 1) / kWaves;
     hipLaunchKernelGGL(mapLwwHbmKernel, dim3(grid < 65535u * 16 ? grid : 65535u * 16), dim3(64 * kWaves), 0, stream,
-                       ops, offsets, nDocs, keyBound, reinterpret_cast<unsigned long long*>(out), scratch, error);
+                       ops, offsets, nDocs, keyBound, reinterpret_cast<unsigned long long*>(out), kill, first, error);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint64_t blocks = (nSlots + 255) / 256;
     hipLaunchKernelGGL(mapLwwFinishKernel, dim3(blocks < 65536 ? (blocks ? blocks : 1) : 65536), dim3(256), 0, stream,
-                       nSlots, keyBound, out, scratch);
+                       nSlots, out, first);
     return hipGetLastError();
   }
   const size_t lds = mapLwwLdsBytes(keyBound);
