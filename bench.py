@@ -32,13 +32,46 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpus():
+    """The host cores this process may actually run on, and the CPU model (the CPU
+    baseline's pool is sized to the host's cores, stated with the model). os.cpu_count() counts the
+    whole machine; the affinity mask and the cgroup CPU quota bound what this process gets."""
+    n = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = n
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = n_aff if quota is None else max(1, min(n_aff, int(quota + 0.999)))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "cpu_count": n, "affinity": n_aff, "cgroup_quota_cpus": quota, "usable": usable}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["mt", "map"], default="mt")
-    ap.add_argument("--docs", type=int, default=None, help="documents per GPU")
+    ap.add_argument("--workload", choices=["mt", "t2", "map"], default="mt",
+                    help="mt: T1 (per-GPU shard of 100k docs); t2: one 1M-doc batch partitioned over the ranks "
+                         "(the default for mt when --gpus > 1); map: M2")
+    ap.add_argument("--docs", type=int, default=None,
+                    help="documents per GPU (mt, map) or in the whole batch (t2)")
+    ap.add_argument("--gather-docs", type=int, default=256,
+                    help="t2: legacy summaries per shard gathered to rank 0 by the gatherv (0 = none)")
     ap.add_argument("--ops-per-doc", type=int, default=None)
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--unique-docs", type=int, default=0, help="0 = all documents distinct")
@@ -47,6 +80,7 @@ def main():
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline pool (0 = every usable host core)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -65,17 +99,32 @@ def main():
 
     from fluidframework_amd import native, workloads
 
-    mt = args.workload == "mt"
-    docs = args.docs or (100_000 if mt else 1_000_000)
+    from fluidframework_amd import shard
+
+    mt = args.workload in ("mt", "t2")
+    t2 = args.workload == "t2" or (mt and world > 1)
     opd = args.ops_per_doc or (2000 if mt else 1000)
-    seed = args.seed + 1000 * rank  # shards hold different documents
+    if t2:
+        # T2: ONE batch of total_docs documents (every document has opd ops), partitioned over the
+        # ranks by shard.plan_shards; each rank generates exactly its shard's streams (doc_base).
+        total_docs = args.docs or 1_000_000
+        lo, hi = shard.plan_shards(np.arange(total_docs + 1, dtype=np.uint64) * np.uint64(opd), world)[rank]
+        docs, doc_base = hi - lo, lo
+    else:
+        docs = args.docs or (100_000 if mt else 1_000_000)
+        total_docs, doc_base = docs * world, rank * docs  # weak scaling: every rank its own docs
+    seed = args.seed if mt else args.seed + 1000 * rank
 
     t = time.time()
+    uniq = docs
     if mt:
         uniq = min(args.unique_docs or docs, docs)
         if docs % uniq:
             raise SystemExit("--docs must be a multiple of --unique-docs")
-        batch = workloads.conflict_farm(uniq, n_clients=args.clients, ops_per_doc=opd, seed=seed, replicas=docs // uniq)
+        if t2 and uniq != docs:
+            raise SystemExit("t2 generates every document of its shard (no --unique-docs)")
+        batch = workloads.conflict_farm(uniq, n_clients=args.clients, ops_per_doc=opd, seed=seed,
+                                        replicas=docs // uniq, doc_base=doc_base)
     else:
         batch = workloads.map_stream(docs, opd, key_pool=args.key_pool, seed=seed)
     n_ops = len(batch.ops)
@@ -121,32 +170,51 @@ def main():
         log(rank, f"[bench] step {k}: kernel {kernel_ms[-1]:.1f} ms")
     barrier()
     elapsed = time.perf_counter() - t0
-    # the run's one exchange step: a 64-byte stats record per rank
-    from fluidframework_amd import shard
-
+    # the run's exchange step: a 64-byte stats record per rank, all-gathered, and for
+    # T2 the shards' legacy summaries gathered to rank 0 (gatherv)
     rec = np.zeros(1, dtype=shard.STATS_DTYPE)
-    rec["rank"], rec["doc_lo"], rec["doc_hi"] = rank, rank * docs, (rank + 1) * docs
+    rec["rank"], rec["doc_lo"], rec["doc_hi"] = rank, doc_base, doc_base + docs
     rec["ops"], rec["elapsed_s"], rec["bytes"] = n_ops, elapsed, bytes_per_launch
     rec["kernel_ms"] = sum(kernel_ms) / len(kernel_ms)
     if mt:
         hdrs = eng.mt_headers()
         rec["status_bad"] = int((hdrs["status"] != 0).sum())
-        rec["checksum"] = shard.state_checksum(hdrs, rank * docs)
+        rec["checksum"] = shard.state_checksum(hdrs, doc_base)
     else:
-        rec["checksum"] = shard.map_checksum(eng.map_fetch(), rank * docs)
+        rec["checksum"] = shard.map_checksum(eng.map_fetch(), doc_base)
     stats = shard.gather_stats(rec, dist, device="cuda") if dist is not None else rec
+    gathered = None
+    if t2 and args.gather_docs > 0:
+        from fluidframework_amd.summary import legacy_summary
+
+        t = time.perf_counter()
+        blobs = []
+        for d in range(min(args.gather_docs, docs)):
+            lv, ch, pr = eng.mt_doc(d, hdrs[d])
+            head, body = legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values)
+            blobs.append(head.encode("utf-8", "surrogatepass") + b"\0" + (body or "").encode("utf-8", "surrogatepass"))
+        build_s = time.perf_counter() - t
+        t = time.perf_counter()
+        allb = shard.gather_blobs(blobs, dist, device="cuda") if dist is not None else blobs
+        gather_s = time.perf_counter() - t
+        if rank == 0:
+            gathered = {"docs": len(allb), "bytes": int(sum(len(b) for b in allb)), "gather_ms": gather_s * 1e3,
+                        "build_ms_rank0": build_s * 1e3,
+                        "what": f"legacy summaries (header, body) of the first {args.gather_docs} documents of every "
+                                "shard, gathered to rank 0 (all-gather of byte counts + grouped send/recv)"}
     elapsed = float(stats["elapsed_s"].max())
-    total_ops = n_ops * world * args.steps
+    total_ops = int(stats["ops"].sum()) * args.steps
     value = total_ops / elapsed
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_per_launch / (avg_kernel_ms / 1e3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not t2:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline only ("port" of the reference path)
 
-        threads = min(16, os.cpu_count() or 1)
+        hc = host_cpus()
+        threads = args.cpu_threads or hc["usable"]
         # bounded sample: consecutive chunks of the same batch until >= --cpu-seconds of CPU work
         chunk = args.cpu_sample_docs or (min(docs, 4 * threads * 80) if mt else min(docs, 200_000))
         secs, sample_ops, sample_docs, lo = 0.0, 0, 0, 0
@@ -171,6 +239,8 @@ def main():
             "seconds": secs,
             "sample": f"{sample_docs} documents ({sample_ops} ops) of the same workload in chunks of {chunk}, "
                       f"C++ oracle -O3, one document per task on {threads} std::threads",
+            "cpu_model": hc["model"],
+            "host_cpus": {k: hc[k] for k in ("cpu_count", "affinity", "cgroup_quota_cpus")},
         }
         log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
 
@@ -192,15 +262,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if t2 else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": f"synthetic ({'conflict-farm' if mt else 'map fuzz'} shape, reference XSadd PRNG; "
-                    + (f"{docs} distinct docs per GPU)" if not mt or uniq == docs
+                    + (f"one {total_docs}-doc batch partitioned by shard.plan_shards)" if t2
+                       else f"{docs} distinct docs per GPU)" if not mt or uniq == docs
                        else f"{uniq} distinct docs per GPU replicated to {docs})"),
             "config": {
-                "workload": ("T1 merge-tree conflict-farm replay" if mt else "M2 SharedMap LWW replay"),
+                "workload": (f"T2 merge-tree conflict-farm replay, {total_docs} docs doc-sharded over {world} GPU(s)" if t2
+                             else "T1 merge-tree conflict-farm replay" if mt else "M2 SharedMap LWW replay"),
                 "docs_per_gpu": docs,
+                "docs_total": total_docs,
                 "clients": args.clients,
                 "ops_per_doc": opd,
                 **({} if mt or args.key_pool == 20 else {"key_pool": args.key_pool}),
@@ -217,7 +290,8 @@ def main():
                 "traffic": traffic["bytes"] if traffic else None,
                 "traffic_fetch_write": [traffic["fetch_bytes"], traffic["write_bytes"]] if traffic else None,
                 "traffic_source": traffic["source"][0].rsplit("/", 2)[0] if traffic else None,
-                "kernel": "mergeTreeKernel" if mt else "mapLwwKernel",
+                "kernel": "mergeTreeKernel" if mt else ("mapLwwKernel" if args.key_pool <= 2560
+                                                         else "mapLwwHbmKernel+mapLwwFinishKernel"),
                 "limiter": ("per-document dependent op chain: VALU issue + LDS/readlane latency of one wave per "
                             "document (HBM fraction is reported for the contract; see DESIGN.md)") if mt
                            else "HBM streaming of 16-byte op records",
@@ -227,6 +301,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
+            "summary_gather": gathered,
             "failed_docs": int(stats["status_bad"].sum()),
             "h2d_gbps": in_bytes / h2d_s / 1e9,
         }

@@ -277,15 +277,18 @@ struct CfHandle {
   std::vector<uint64_t> opOff, textOff;
 };
 
+// Documents doc_base .. doc_base + n_docs - 1 of the (conceptually unbounded) document set: a shard
+// of a large batch (T2) is generated by its own rank with the same per-document streams.
 void* fmtgen_conflict_farm_new(uint32_t n_docs, uint32_t n_clients, uint32_t ops_per_doc,
                                uint32_t min_length_fixed, uint32_t seed, uint32_t annotate_props_base,
-                               uint32_t threads, uint64_t* n_ops, uint64_t* n_text) {
+                               uint32_t threads, uint64_t* n_ops, uint64_t* n_text, uint32_t doc_base) {
   if (n_clients == 0 || n_clients > 63) return nullptr;
   auto* h = new CfHandle();
   h->docs.resize(n_docs);
-  parallelFor(n_docs, threads, [&](uint32_t d) {
+  parallelFor(n_docs, threads, [&](uint32_t i) {
+    const uint32_t d = doc_base + i;
     const uint32_t minLength = min_length_fixed ? min_length_fixed : (1u << (d % 10));
-    genConflictFarmDoc(h->docs[d], d, n_clients, ops_per_doc, minLength, seed, annotate_props_base);
+    genConflictFarmDoc(h->docs[i], d, n_clients, ops_per_doc, minLength, seed, annotate_props_base);
   });
   h->opOff.assign(n_docs + 1, 0);
   h->textOff.assign(n_docs + 1, 0);

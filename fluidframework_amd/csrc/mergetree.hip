@@ -109,10 +109,14 @@ MtCaps mergeTreeCaps(bool large) {
 }
 
 // The documents the small tier could not hold (FMT_E_CAPACITY): esc[0] = count, esc[1..] = ids.
-__global__ __launch_bounds__(256) void collectOverflowKernel(const fmt_mt_doc_result* __restrict__ headers,
+// A limit the large tier shares (fmt_mt::kCapacityFinal) is reported as FMT_E_CAPACITY without
+// escalation.
+__global__ __launch_bounds__(256) void collectOverflowKernel(fmt_mt_doc_result* __restrict__ headers,
                                                              uint32_t nDocs, uint32_t* esc) {
   for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nDocs; d += gridDim.x * blockDim.x) {
-    if (headers[d].status == FMT_E_CAPACITY) {
+    const int st = headers[d].status;
+    if (st == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;
+    if (st == FMT_E_CAPACITY) {
       const uint32_t k = atomicAdd(esc, 1u);
       esc[1 + k] = d;
     }

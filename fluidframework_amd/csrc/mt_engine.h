@@ -40,6 +40,7 @@ constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
 constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:21)
 constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
 constexpr int32_t kNotRemoved = 0x7fffffff;
+constexpr int kCapacityFinal = -33;  // internal status (small tier only), never leaves the runtime
 
 // Capacity tiers. Every document first replays in the small tier (leaves in 40 VGPRs, text in
 // LDS, 2 waves/SIMD). A document that overflows it (FMT_E_CAPACITY) is replayed again from its
@@ -198,6 +199,11 @@ class Doc {
   static constexpr uint32_t kLenMask = (1u << C::kLenBits) - 1u;
   static constexpr uint32_t kNoBlk = (1u << C::kBlkBits) - 1u;
   static constexpr bool kPW = C::kPropsWord;
+  // A limit both tiers share (keys per prop set, catch-up / remove-order slabs, live obliterates):
+  // the small tier reports it as kCapacityFinal so that the overflow list does not replay the
+  // document in the large tier only to fail again; collectOverflowKernel turns it into
+  // FMT_E_CAPACITY. Every other capacity failure of the small tier escalates.
+  static constexpr int kCapFinal = C::kHbmChars ? FMT_E_CAPACITY : kCapacityFinal;
   static constexpr uint32_t kPropsUndef = kPW ? 0xFFFFu : (1u << (32 - C::kLenBits - C::kBlkBits)) - 1u;
   using PMask = typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type;
   static_assert(kMaxBlocks <= static_cast<int>(kNoBlk) && kPropCap <= static_cast<int>(kPropsUndef), "W0 field widths");
@@ -762,7 +768,7 @@ class Doc {
           if (i == pos) kv[i] = e;
       } else {
         if (cnt >= FMT_MT_PROPS_MAX) {
-          fail(FMT_E_CAPACITY);
+          fail(kCapFinal);
           return 0;
         }
         for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
@@ -839,7 +845,7 @@ class Doc {
 
   FMT_DEV void emitCatchup(int p1, int p2, int type) {
     if (cuN >= cuCap) {
-      fail(FMT_E_CAPACITY);
+      fail(kCapFinal);
       return;
     }
     FOR_LANES(l) {
@@ -863,7 +869,7 @@ class Doc {
   // client). Rare (concurrent overlapping removes), so lane 0 writes one entry at a time.
   FMT_DEV void rmAppend(uint32_t id, int client) {
     if (rmN >= rmCap) {
-      fail(FMT_E_CAPACITY);
+      fail(kCapFinal);
       return;
     }
     FOR_LANES(l) {
@@ -1178,7 +1184,7 @@ class Doc {
   }
 
   FMT_DEV bool obAdd(uint32_t sId, int sOff, uint32_t eId, int eOff, int seq, int client) {
-    if (obUsed == ~0ull) return fail(FMT_E_CAPACITY);
+    if (obUsed == ~0ull) return fail(kCapFinal);
     const int slot = ctz64(~obUsed);
     obUsed |= 1ull << slot;
     s->ob[slot].startId = sId;
@@ -1193,7 +1199,7 @@ class Doc {
     bool exists;
     const int at = findStart(slot, &exists);
     if (!exists) {
-      if (obStartN >= kObCap) return fail(FMT_E_CAPACITY);
+      if (obStartN >= kObCap) return fail(kCapFinal);
       for (int i = obStartN; i > at; i--) {
         const uint8_t v = s->obStart[i - 1];
         waveSync();

@@ -46,8 +46,9 @@ struct fmt_ctx {
   int numCUs = 256;
   std::string arch;
   std::string err;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the run's (first) launch
+  hipEvent_t ev2 = nullptr, ev3 = nullptr;  // around a second launch (large-tier replay), if any
+  bool timed = false, timed2 = false;
   fmt_stats stats{};
 
   // SharedMap
@@ -138,6 +139,8 @@ int fmt_open(const fmt_config* cfg, fmt_ctx** out) {
   }
   FMT_HIP(c, hipEventCreate(&c->ev0));
   FMT_HIP(c, hipEventCreate(&c->ev1));
+  FMT_HIP(c, hipEventCreate(&c->ev2));
+  FMT_HIP(c, hipEventCreate(&c->ev3));
   FMT_HIP(c, c->errWord.reserve(1));
   return FMT_OK;
 }
@@ -172,6 +175,8 @@ void fmt_close(fmt_ctx* c) {
   c->mtRmOrder.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  if (c->ev3) (void)hipEventDestroy(c->ev3);
   if (c->ownStream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -191,6 +196,12 @@ int fmt_get_stats(const fmt_ctx* cc, fmt_stats* out) {
     FMT_HIP(c, hipEventSynchronize(c->ev1));
     float ms = 0;
     FMT_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (c->timed2) {
+      float ms2 = 0;
+      FMT_HIP(c, hipEventSynchronize(c->ev3));
+      FMT_HIP(c, hipEventElapsedTime(&ms2, c->ev2, c->ev3));
+      ms += ms2;
+    }
     c->stats.kernel_ms = ms;
     c->stats.total_ms = ms;
   }
@@ -248,12 +259,21 @@ static int runMap(fmt_ctx* c, const fmt_map_op* ops, const uint64_t* offs, uint3
   FMT_HIP(c, fmt_kernels::launchMapLww(ops, offs, nDocs, keyBound, out, c->errWord.p, c->numCUs, c->stream, scratch));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
+  c->timed2 = false;
   c->stats = fmt_stats{};
   c->stats.ops = nOps;
   c->stats.docs = nDocs;
+  const uint64_t nSlots = static_cast<uint64_t>(nDocs) * keyBound;
   c->stats.bytes_read = nOps * sizeof(fmt_map_op) + (nDocs + 1ull) * sizeof(uint64_t);
-  c->stats.bytes_written = static_cast<uint64_t>(nDocs) * keyBound * sizeof(fmt_map_slot);
+  c->stats.bytes_written = nSlots * sizeof(fmt_map_slot);
   c->stats.launches = 1;
+  if (scratch != nullptr) {
+    // HBM-table path: three table fills (8 B slot + 4 B kill + 4 B first per slot) and the finish
+    // pass (reads slot + first, writes the slot) on top of the op stream and the kernel's atomics
+    c->stats.bytes_written += nSlots * 16;
+    c->stats.bytes_read += nSlots * 12;
+    c->stats.launches = 5;
+  }
   return FMT_OK;
 }
 
@@ -277,7 +297,19 @@ int fmt_map_replay_device(fmt_ctx* c, const fmt_map_op* dOps, const uint64_t* dO
                           uint32_t keyBound, fmt_map_slot* dOut) {
   if (c == nullptr || dOffs == nullptr || dOut == nullptr || keyBound == 0)
     return setErr(c, FMT_E_USAGE, "fmt_map_replay_device: bad arguments");
+  // the HBM-table path runs 64-bit atomics on the output slots viewed as u64
+  if (fmt_kernels::mapLwwNeedsScratch(keyBound) && (reinterpret_cast<uintptr_t>(dOut) & 7u) != 0)
+    return setErr(c, FMT_E_USAGE, "fmt_map_replay_device: d_out must be 8-byte aligned for key_bound > 2560");
   return runMap(c, dOps, dOffs, nDocs, keyBound, 0, dOut);
+}
+
+int fmt_map_check(fmt_ctx* c) {
+  if (c == nullptr) return FMT_E_USAGE;
+  int errWord = 0;
+  FMT_HIP(c, hipMemcpyAsync(&errWord, c->errWord.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  if (errWord) return setErr(c, FMT_E_DATA, "an op referenced a key id >= key_bound");
+  return FMT_OK;
 }
 
 // ------------------------------------------------------------------------------ merge-tree
@@ -435,6 +467,8 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->mtEsc.p, c->numCUs, c->stream,
                                           c->mtObliterate, c->mtHasRmOrder));
+  FMT_HIP(c, hipEventRecord(c->ev1, c->stream));  // device time excludes the host read-back below
+  c->timed2 = false;
   // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
   uint32_t nEsc = 0;
   FMT_HIP(c, hipMemcpyAsync(&nEsc, c->mtEsc.p, sizeof nEsc, hipMemcpyDeviceToHost, c->stream));
@@ -447,14 +481,16 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
                                   c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
+    FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
                                                  c->mtHasRmOrder));
+    FMT_HIP(c, hipEventRecord(c->ev3, c->stream));
+    c->timed2 = true;
     std::vector<uint32_t> list(nEsc);
     FMT_HIP(c, hipMemcpyAsync(list.data(), c->mtEsc.p + 1, nEsc * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     FMT_HIP(c, hipStreamSynchronize(c->stream));
     for (uint32_t i = 0; i < nEsc; i++) c->mtBigSlot[list[i]] = static_cast<int32_t>(i);
   }
-  FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
   c->timed = true;
   c->stats = fmt_stats{};
   c->stats.ops = c->mtNOps;

@@ -165,6 +165,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_map_run.argtypes = [P]
         L.fmt_map_fetch.argtypes = [P, P]
         L.fmt_map_replay_device.argtypes = [P, P, P, U32, U32, P]
+        L.fmt_map_check.argtypes = [P]
         L.fmt_mt_load.argtypes = [P, ctypes.POINTER(FmtMtBatch)]
         L.fmt_mt_run.argtypes = [P]
         L.fmt_mt_fetch_headers.argtypes = [P, P]
@@ -178,7 +179,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
 
 EXPORTED_SYMBOLS = [
     "fmt_open", "fmt_close", "fmt_last_error", "fmt_sync", "fmt_get_stats", "fmt_device_info",
-    "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device",
+    "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device", "fmt_map_check",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_remove_order", "fmt_mt_capacity",
 ]
@@ -243,6 +244,14 @@ class Engine:
 
     def map_run(self):
         self._check(self.L.fmt_map_run(self.h))
+
+    def map_replay_device(self, d_ops: int, d_offsets: int, n_docs: int, key_bound: int, d_out: int):
+        """fmt_map_replay_device on caller-owned device pointers (e.g. torch tensors' data_ptr())."""
+        self._check(self.L.fmt_map_replay_device(self.h, d_ops, d_offsets, n_docs, key_bound, d_out))
+
+    def map_check(self):
+        """Raises EngineError(FMT_E_DATA) when the last map run saw a key id >= key_bound."""
+        self._check(self.L.fmt_map_check(self.h))
 
     def map_fetch(self) -> np.ndarray:
         out = np.zeros(self._map_shape[0] * self._map_shape[1], dtype=MAP_SLOT_DTYPE)

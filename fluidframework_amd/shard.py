@@ -126,3 +126,68 @@ def gather_stats(rec: np.ndarray, dist, device=None) -> np.ndarray:
 def combine_checksums(stats: np.ndarray) -> int:
     """Whole-job state checksum = Σ shard checksums mod 2^64."""
     return int(stats["checksum"].astype(np.uint64).sum(dtype=np.uint64))
+
+
+def gather_blobs(blobs: list, dist, device=None):
+    """Gatherv of variable-length byte blobs to rank 0 (the summaries the shards'
+    summarizeCore would produce, shared-object-base/src/sharedObject.ts:889, end up with one
+    summarizer). Every rank passes its blobs in document order; rank 0 gets all ranks' blobs in rank
+    order (so in global document order for contiguous shards), the others None.
+
+    Step 1: all-gather of each rank's (blob count, payload bytes). Step 2: every rank > 0 sends its
+    blob lengths and its concatenated payload to rank 0 as one group of point-to-point ops
+    (batch_isend_irecv on RCCL; isend/irecv on gloo). `device` is "cuda" for nccl, None for gloo."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    lens = np.array([len(b) for b in blobs], dtype=np.int64)
+    payload = np.frombuffer(b"".join(blobs), dtype=np.uint8)
+    dev = device or "cpu"
+    sizes = torch.tensor([len(blobs), payload.size], dtype=torch.int64, device=dev)
+    parts = [torch.empty_like(sizes) for _ in range(world)]
+    dist.all_gather(parts, sizes)
+    sizes = [tuple(int(x) for x in p.cpu().tolist()) for p in parts]
+
+    def p2p(ops):
+        if not ops:
+            return
+        if device is not None:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        else:
+            works = [(dist.isend if op.op is dist.isend else dist.irecv)(op.tensor, op.peer) for op in ops]
+            for w in works:
+                w.wait()
+
+    if rank != 0:
+        ops = []
+        if len(blobs):
+            ops.append(dist.P2POp(dist.isend, torch.from_numpy(lens).to(dev), 0))
+        if payload.size:
+            ops.append(dist.P2POp(dist.isend, torch.from_numpy(payload.copy()).to(dev), 0))
+        p2p(ops)
+        return None
+    recv = {}
+    ops = []
+    for r in range(1, world):
+        n, nb = sizes[r]
+        lt = torch.empty(n, dtype=torch.int64, device=dev) if n else None
+        pt = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else None
+        recv[r] = (lt, pt)
+        if lt is not None:
+            ops.append(dist.P2POp(dist.irecv, lt, r))
+        if pt is not None:
+            ops.append(dist.P2POp(dist.irecv, pt, r))
+    p2p(ops)
+    out = list(blobs)
+    for r in range(1, world):
+        lt, pt = recv[r]
+        if lt is None:
+            continue
+        ln = lt.cpu().numpy()
+        raw = pt.cpu().numpy().tobytes() if pt is not None else b""
+        o = 0
+        for k in ln:
+            out.append(raw[o : o + int(k)])
+            o += int(k)
+    return out

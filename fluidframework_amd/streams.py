@@ -80,16 +80,38 @@ def js_key_order(keys):
     return idx + [k for k in keys if not is_array_index_key(k)]
 
 
+_JS_ESC = {'"': '\\"', "\\": "\\\\", "\b": "\\b", "\f": "\\f", "\n": "\\n", "\r": "\\r", "\t": "\\t"}
+
+
+def js_quote(s: str) -> str:
+    """JSON.stringify of a string (ECMAScript QuoteJSONString, well-formed JSON.stringify: lone
+    surrogates are escaped as \\udXXX, which json.dumps(ensure_ascii=False) would write raw)."""
+    out = ['"']
+    for ch in s:
+        c = ord(ch)
+        e = _JS_ESC.get(ch)
+        if e is not None:
+            out.append(e)
+        elif c < 0x20 or 0xD800 <= c <= 0xDFFF:
+            out.append("\\u%04x" % c)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
 def js_json(value) -> str:
     """JSON.stringify for JSON-parsed values (ints, strings, bools, null, arrays, objects)."""
     if isinstance(value, dict):
         return "{" + ",".join(
-            json.dumps(k, ensure_ascii=False) + ":" + js_json(value[k]) for k in js_key_order(list(value))
+            js_quote(k) + ":" + js_json(value[k]) for k in js_key_order(list(value))
         ) + "}"
     if isinstance(value, list):
         return "[" + ",".join(js_json(v) for v in value) + "]"
-    if isinstance(value, bool) or value is None or isinstance(value, str):
-        return json.dumps(value, ensure_ascii=False)
+    if isinstance(value, str):
+        return js_quote(value)
+    if isinstance(value, bool) or value is None:
+        return json.dumps(value)
     if isinstance(value, int):
         return str(value)
     if isinstance(value, float):

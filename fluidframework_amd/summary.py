@@ -15,7 +15,7 @@ from __future__ import annotations
 import json
 
 from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_OBLITERATE, MT_REMOVE, is_array_index_key,
-                      js_json, js_key_order)
+                      js_json, js_key_order, js_quote)
 
 NOT_REMOVED = 0x7FFFFFFF
 TEXT_GRANULARITY = 256          # textSegment.ts:21
@@ -24,31 +24,7 @@ MIN_VALUE_SIZE_SEPARATE_BLOB = 8 * 1024  # map.ts:190
 MAX_SNAPSHOT_BLOB_SIZE = 16 * 1024       # map.ts:194
 
 
-def _q(s: str) -> str:
-    """JSON.stringify of a string (QuoteJSONString, well-formed: lone surrogates escaped)."""
-    out = ['"']
-    for ch in s:
-        c = ord(ch)
-        if ch == '"':
-            out.append('\\"')
-        elif ch == "\\":
-            out.append("\\\\")
-        elif ch == "\b":
-            out.append("\\b")
-        elif ch == "\f":
-            out.append("\\f")
-        elif ch == "\n":
-            out.append("\\n")
-        elif ch == "\r":
-            out.append("\\r")
-        elif ch == "\t":
-            out.append("\\t")
-        elif c < 0x20 or 0xD800 <= c <= 0xDFFF:
-            out.append("\\u%04x" % c)
-        else:
-            out.append(ch)
-    out.append('"')
-    return "".join(out)
+_q = js_quote  # JSON.stringify of a string (lone surrogates escaped)
 
 
 def _utf16_len(s: str) -> int:

@@ -27,7 +27,7 @@ def _lib():
         P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         L.fmtgen_map.argtypes = [U32, U32, U32, U32, P, P, U32]
         L.fmtgen_conflict_farm_new.argtypes = [U32, U32, U32, U32, U32, U32, U32,
-                                               ctypes.POINTER(U64), ctypes.POINTER(U64)]
+                                               ctypes.POINTER(U64), ctypes.POINTER(U64), U32]
         L.fmtgen_conflict_farm_new.restype = P
         L.fmtgen_conflict_farm_copy.argtypes = [P, U32, P, P, P, U32]
         L.fmtgen_free.argtypes = [P]
@@ -40,7 +40,11 @@ def _p(a):
 
 
 def default_threads() -> int:
-    return max(1, min(16, os.cpu_count() or 1))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def map_value_json(value_id: int) -> str:
@@ -74,16 +78,18 @@ CLIENT_NAMES = [chr(ord("A") + i) for i in range(26)] + [chr(ord("a") + i) for i
 
 
 def conflict_farm(n_docs: int, n_clients: int = 8, ops_per_doc: int = 2000, min_length: int = 0,
-                  seed: int = 1, replicas: int = 1, threads=None) -> MergeTreeBatch:
+                  seed: int = 1, replicas: int = 1, threads=None, doc_base: int = 0) -> MergeTreeBatch:
     """Conflict-farm merge-tree streams; `replicas` lays out that many copies of the doc set.
 
+    Documents are doc_base .. doc_base + n_docs - 1 of the seed's document set, so a shard of a big
+    batch is generated alone with exactly the streams the whole batch would hold.
     Props op i is {"client": CLIENT_NAMES[i]} (the 0.40 fixtures' annotate shape).
     """
     L = _lib()
     threads = threads or default_threads()
     n_ops, n_text = ctypes.c_uint64(), ctypes.c_uint64()
     h = L.fmtgen_conflict_farm_new(n_docs, n_clients, ops_per_doc, min_length, seed, 0, threads,
-                                   ctypes.byref(n_ops), ctypes.byref(n_text))
+                                   ctypes.byref(n_ops), ctypes.byref(n_text), doc_base)
     if not h:
         raise ValueError("fmtgen_conflict_farm_new failed")
     try:

@@ -287,9 +287,14 @@ int fmt_map_run(fmt_ctx* ctx);
 /* Copy results to host: out[d * key_bound + k]. Synchronizes the ctx stream. Replaces reading
  * MapKernel.sequencedData (mapKernel.ts:131) for get()/summarizeCore (map.ts:176-246). */
 int fmt_map_fetch(fmt_ctx* ctx, fmt_map_slot* out);
-/* Zero-copy variant on caller-owned DEVICE buffers (e.g. torch tensors), launched on the ctx stream. */
+/* Zero-copy variant on caller-owned DEVICE buffers (e.g. torch tensors), launched on the ctx stream.
+ * For key_bound > 2560 (the HBM-table path) d_out must be 8-byte aligned (FMT_E_USAGE otherwise).
+ * Bad key ids (>= key_bound) are reported by fmt_map_check. */
 int fmt_map_replay_device(fmt_ctx* ctx, const fmt_map_op* d_ops, const uint64_t* d_doc_op_offsets,
                           uint32_t n_docs, uint32_t key_bound, fmt_map_slot* d_out);
+/* Synchronizes the ctx stream; FMT_E_DATA when an op of the last map run referenced a key id
+ * >= key_bound (the remote op the reference would reject while processing it, mapKernel.ts:619-630). */
+int fmt_map_check(fmt_ctx* ctx);
 
 /* ---------------------------------------------------------------------------------------------
  * merge-tree / SharedString (Client.applyMsg observer path + zamboni, client.ts:1358-1391)

@@ -52,6 +52,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     new (doc.get()) Doc();
     doc->s = scratch.get();
     doc->run(in, o);
+    if (headers[d].status == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;  // as collectOverflowKernel
     if (headers[d].status != FMT_OK && status == FMT_OK) status = headers[d].status;
   }
   return status;

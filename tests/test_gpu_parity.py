@@ -81,10 +81,12 @@ def test_map_lww_large_key_pool(orc, engine):
     assert np.array_equal(got, exp)
 
 
-@pytest.mark.parametrize("n_docs,n_ops,key_pool", [(512, 2000, 5000), (24, 3000, 1 << 20)])
+@pytest.mark.parametrize("n_docs,n_ops,key_pool",
+                         [(512, 2000, 1000), (256, 2000, 2560), (256, 2000, 2561), (512, 2000, 5000), (24, 3000, 1 << 20)])
 def test_map_lww_key_pool_beyond_lds(orc, engine, n_docs, n_ops, key_pool):
-    """Key pools over the LDS table's 2560 ids (SURVEY §8d's U[0, 2^20) variant) replay with the key
-    tables in HBM (mapLwwHbmKernel + mapLwwFinishKernel), bit-exact vs the oracle."""
+    """Key pools around and over the LDS table's 2560 ids (SURVEY §8d's U[0, 2^20) variant): 2560 ids
+    take the LDS kernel with 160 KiB of dynamic LDS per workgroup, 2561 the HBM-table kernels
+    (mapLwwHbmKernel + mapLwwFinishKernel); both sides of the switch bit-exact vs the oracle."""
     batch = workloads.map_stream(n_docs, n_ops, key_pool=key_pool, seed=23)
     engine.map_load(batch)
     engine.map_run()
@@ -395,3 +397,35 @@ def test_mt_many_writers_escalate_to_large_tier(orc, engine):
     hdrs = _check_against_oracle(orc, engine, many)
     assert (hdrs["status"] == 0).all()
     assert engine.stats().launches == 2
+
+
+@pytest.mark.parametrize("key_pool", [20, 5000])
+def test_map_replay_device_buffers_and_bad_keys(orc, engine, key_pool):
+    """fmt_map_replay_device on torch-owned device buffers equals the staged path; an op whose key
+    id is >= key_bound is reported by fmt_map_check (FMT_E_DATA), on both the LDS and the HBM path."""
+    import torch
+
+    from fluidframework_amd.native import FMT_E_DATA, MAP_SLOT_DTYPE, EngineError
+
+    batch = workloads.map_stream(64, 600, key_pool=key_pool, seed=31)
+    exp, _ = orc.map_replay(batch, threads=16)
+    raw = torch.from_numpy(np.ascontiguousarray(batch.ops).view(np.uint8).copy()).cuda()
+    offs = torch.from_numpy(np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64).view(np.int64).copy()).cuda()
+    out = torch.zeros(batch.n_docs * key_pool * 8, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    engine.map_replay_device(raw.data_ptr(), offs.data_ptr(), batch.n_docs, key_pool, out.data_ptr())
+    engine.map_check()
+    got = out.cpu().numpy().view(MAP_SLOT_DTYPE).reshape(batch.n_docs, key_pool)
+    assert np.array_equal(got, exp)
+    bad = np.ascontiguousarray(batch.ops).copy()
+    bad["key"][5] = key_pool + 3
+    bad["kind_value"][5] = 0  # a set
+    raw_bad = torch.from_numpy(bad.view(np.uint8).copy()).cuda()
+    torch.cuda.synchronize()
+    engine.map_replay_device(raw_bad.data_ptr(), offs.data_ptr(), batch.n_docs, key_pool, out.data_ptr())
+    with pytest.raises(EngineError) as ei:
+        engine.map_check()
+    assert ei.value.code == FMT_E_DATA
+    if key_pool > 2560:  # the HBM path's u64 view of d_out needs 8-byte alignment
+        with pytest.raises(EngineError):
+            engine.map_replay_device(raw.data_ptr(), offs.data_ptr(), batch.n_docs, key_pool, out.data_ptr() + 4)

@@ -139,3 +139,11 @@ def test_map_summary_array_index_keys_first(orc):
     header, _ = orc.map_summary(_map_batch(msgs), 0)
     assert header == ('{"blobs":[],"content":{"2":{"type":"Plain","value":4},"10":{"type":"Plain","value":2},'
                       '"a":{"type":"Plain","value":3},"b":{"type":"Plain","value":5}}}')
+
+
+def test_map_summary_lone_surrogate_value_is_escaped(orc):
+    # Well-formed JSON.stringify (ES2019) escapes a lone surrogate as \udXXX; the Python packer
+    # (streams.js_json) must write the same bytes as the JS host (fmt.js) and the reference.
+    # Parity unpinned: no reference fixture holds such a value.
+    header, _ = orc.map_summary(_map_batch([_set("k", "a\ud800b"), _set("j", "\udfff")]), 0)
+    assert header == '{"blobs":[],"content":{"k":{"type":"Plain","value":"a\\ud800b"},"j":{"type":"Plain","value":"\\udfff"}}}'

@@ -97,3 +97,50 @@ def test_gloo_world2_shards_reproduce_unsharded(orc, tmp_path):
     assert stats["doc_hi"][0] == stats["doc_lo"][1]
     rc, whole, *_ = orc.mt_replay_batch(batch, outputs=False)
     assert shard.combine_checksums(stats) == shard.state_checksum(whole)
+
+
+def test_shard_generation_equals_slicing():
+    """A shard generated alone (doc_base) holds exactly the whole batch's streams for its documents."""
+    whole = workloads.conflict_farm(10, n_clients=4, ops_per_doc=300, seed=7)
+    part = workloads.conflict_farm(4, n_clients=4, ops_per_doc=300, seed=7, doc_base=3)
+    sl = shard.slice_mt(whole, 3, 7)
+    keys = ("seq", "ref_seq", "min_seq", "pos1", "pos2", "len", "client", "type")
+    for k in keys:
+        assert np.array_equal(part.ops[k], sl.ops[k]), k
+    ins = part.ops["type"] == 0
+    for i in np.nonzero(ins)[0][:200]:
+        a, b = int(part.ops["payload"][i]), int(sl.ops["payload"][i])
+        n = int(part.ops["len"][i])
+        assert np.array_equal(part.text[a : a + n], whole.text[b : b + n])
+
+
+def _gather_main(rank, world, port, out_path):
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+
+    from fluidframework_amd import shard as sh
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    # rank 1 has no blobs; rank 2 has an empty blob among others
+    mine = {0: [b"a", b"bc" * 1000], 1: [], 2: [b"", "é€😀".encode(), b"\0x"]}[rank]
+    out = sh.gather_blobs(mine, dist)
+    if rank == 0:
+        with open(out_path, "wb") as f:
+            for b in out:
+                f.write(len(b).to_bytes(8, "little") + b)
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_blobs_world3(tmp_path):
+    out = str(tmp_path / "blobs.bin")
+    mp.start_processes(_gather_main, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
+    raw = open(out, "rb").read()
+    got, o = [], 0
+    while o < len(raw):
+        n = int.from_bytes(raw[o : o + 8], "little")
+        got.append(raw[o + 8 : o + 8 + n])
+        o += 8 + n
+    assert got == [b"a", b"bc" * 1000, b"", "é€😀".encode(), b"\0x"]
