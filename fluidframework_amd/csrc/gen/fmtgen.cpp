@@ -327,4 +327,84 @@ int fmtgen_conflict_farm_copy(void* handle, uint32_t replicas, fmt_mt_op* out_op
 
 void fmtgen_free(void* handle) { delete static_cast<CfHandle*>(handle); }
 
+// T3 (BASELINE config 5): ONE SharedString loaded from a summary of n_segments segments (length
+// U[1,8], letters a..z, no props), then n_ops sequenced messages from n_clients writers (short ids
+// 1..n_clients) with deep refSeq windows: every op's refSeq lags its seq by U[0, max_lag) (clamped to
+// stay non-decreasing per client) and msn = min over clients of their latest refSeq (the MSN rule of
+// mocks.ts:587-604 / deli clientSeqManager.ts:131). Op kinds insert / remove / annotate with equal
+// weight as in the conflict farm (mergeTreeOperationRunner.ts:341-429), but remove / annotate ranges
+// are local edits of U[1, max_range] chars: the farm's end = U[start+1, len] would delete a third of
+// a 10M-segment document per remove, leaving no large document after a few dozen ops.
+// Positions are drawn below a lower bound of the op's perspective length (PriorPerspective(refSeq,
+// client), perspective.ts:80-93): initial chars + all inserted chars - all remove range lengths -
+// the chars inserted by messages the op has not seen (seq > refSeq), so every op is valid.
+// Outputs: out_segs[n_segments] = (text offset, len, FMT_MT_NO_PROPS); out_text (capacity
+// n_segments * 8 + n_ops * 3 units) = the segments' text, then the insert payloads; out_ops[n_ops].
+// Returns the number of text units written, or a negative FMT_E_* code.
+int64_t fmtgen_t3(uint32_t n_segments, uint32_t n_ops, uint32_t n_clients, uint32_t max_lag, uint32_t max_range,
+                  uint32_t seed, uint32_t annotate_props_base, fmt_mt_snapshot_seg* out_segs, uint16_t* out_text,
+                  fmt_mt_op* out_ops) {
+  if (n_clients == 0 || n_clients > 63 || max_lag == 0 || max_range == 0) return FMT_E_USAGE;
+  Rng rng(0xdeadbeefu, 0xfeedbedu, 0x7733u, seed);
+  uint64_t t = 0;
+  int64_t chars = 0;
+  for (uint32_t k = 0; k < n_segments; k++) {
+    const uint32_t len = static_cast<uint32_t>(rng.integer(1, 8));
+    out_segs[k] = fmt_mt_snapshot_seg{static_cast<uint32_t>(t), len, FMT_MT_NO_PROPS};
+    for (uint32_t c = 0; c < len; c++) out_text[t++] = static_cast<uint16_t>('a' + rng.integer(0, 25));
+    chars += len;
+  }
+  // lower bound of every perspective's length, and the inserted chars per seq (for the unseen ones)
+  int64_t lb = chars;
+  std::vector<int64_t> insPrefix(static_cast<size_t>(n_ops) + 1, 0);  // chars inserted by seqs 1..s
+  std::vector<int32_t> lastRef(n_clients + 1, 0);
+  int32_t msn = 0;
+  for (uint32_t i = 0; i < n_ops; i++) {
+    const int32_t seq = static_cast<int32_t>(i + 1);
+    const int client = static_cast<int>(rng.integer(1, n_clients));
+    const int32_t lagCap = std::min<int32_t>(seq - 1, static_cast<int32_t>(max_lag) - 1);
+    const int32_t lag = lagCap > 0 ? static_cast<int32_t>(rng.integer(0, lagCap)) : 0;
+    const int32_t ref = std::max(lastRef[client], seq - 1 - lag);
+    lastRef[client] = ref;
+    int32_t m = ref;
+    for (uint32_t c = 1; c <= n_clients; c++) m = std::min(m, lastRef[c]);
+    msn = std::max(msn, m);
+    const int64_t unseen = insPrefix[i] - insPrefix[static_cast<size_t>(ref)];
+    const int64_t len = std::max<int64_t>(0, lb - unseen);
+    fmt_mt_op op{};
+    op.seq = seq;
+    op.ref_seq = ref;
+    op.min_seq = msn;
+    op.client = static_cast<uint8_t>(client);
+    int kind = len == 0 ? FMT_MT_INSERT : static_cast<int>(rng.integer(0, 2));
+    kind = kind == 0 ? FMT_MT_REMOVE : kind == 1 ? FMT_MT_ANNOTATE : FMT_MT_INSERT;
+    if (len == 0) kind = FMT_MT_INSERT;
+    op.type = static_cast<uint8_t>(kind);
+    insPrefix[i + 1] = insPrefix[i];
+    if (kind == FMT_MT_INSERT) {
+      const int reps = static_cast<int>(rng.integer(1, 3));
+      op.pos1 = static_cast<int32_t>(rng.integer(0, len));
+      op.pos2 = -1;
+      op.payload = static_cast<uint32_t>(t);
+      op.len = static_cast<uint16_t>(reps);
+      for (int r = 0; r < reps; r++) out_text[t++] = clientChar(client);
+      lb += reps;
+      insPrefix[i + 1] += reps;
+    } else {
+      const int64_t start = rng.integer(0, len - 1);
+      const int64_t n = rng.integer(1, max_range);
+      const int64_t end = std::min(start + n, len);
+      op.pos1 = static_cast<int32_t>(start);
+      op.pos2 = static_cast<int32_t>(end);
+      if (kind == FMT_MT_REMOVE) {
+        lb -= end - start;
+      } else {
+        op.payload = annotate_props_base + static_cast<uint32_t>(client);  // {"client": name}
+      }
+    }
+    out_ops[i] = op;
+  }
+  return static_cast<int64_t>(t);
+}
+
 }  // extern "C"

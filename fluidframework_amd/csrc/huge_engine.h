@@ -1,0 +1,1852 @@
+// huge_engine.h — merge-tree observer replay of ONE very large document (BASELINE config 5, T3:
+// 10M segments, 64 clients, refSeq windows thousands of ops deep) on ONE wavefront, state in HBM.
+//
+// Same reference semantics as mt_engine.h (Client.applyMsg → insertSegments / markRangeRemoved /
+// annotateRange, mergeTree.ts:1484-1517, 2009-2081, 2292-2383; zamboni.ts:33-213 with its LRU heap
+// core-utils/src/heap.ts:54-182; setMinSeq mergeTree.ts:1147-1166), but the document no longer fits
+// one wave's registers, so the leaf list is paged:
+//
+//   * Leaf blocks of the exact B+tree (≤ 8 leaves, mergeTreeNodes.ts:248) ARE the pages: each leaf
+//     block stores its leaves inline (SoA fields, 8 slots). Interior blocks hold child block ids. The
+//     tree decides zamboni scope and the segmentation summaries expose, so it is kept exactly.
+//   * The leaf blocks in document order are listed by groups: gOrder (LDS) lists the groups in
+//     document order; each group lists up to kSlotCap leaf blocks (HBM) with each block's stable
+//     length. A block split inserts a slot; packParent removes slots; a full group splits.
+//   * Length index (what PartialSequenceLengths is to the reference, partialLengths.ts:973-1005; only
+//     an index, :1189-1240): a leaf's length from PriorPerspective(refSeq, client) differs from its
+//     length at minSeq only if it was inserted or removed in the collaboration window. Such "window
+//     leaves" are kept in a window table (HBM, a few thousand entries: one per leaf inserted or removed
+//     above minSeq) tagged with their group and leaf block; every other leaf contributes its fixed
+//     length to its block's and group's stable sums. Resolving a view position is then: one pass of
+//     the wave over the window table (per-group corrections, LDS atomics) + a scan over the groups
+//     (LDS), a scan over one group's slots (two coalesced loads per 64 slots + that group's window
+//     corrections), and the ≤ 8 leaves of one block evaluated directly.
+//   * When minSeq advances, window entries whose insert and remove are both at or below it graduate
+//     into the stable sums (their length no longer depends on the perspective).
+//   * The LRU heap (verbatim heap.ts sift order) lives in LDS. Text: each leaf names a run of one
+//     UTF-16 arena (the batch's text, then a merge area where zamboni appends build their text).
+//
+// Every decision that mt_engine.h makes with a view scan over all leaves is made here on the first
+// qualifying leaf of the hierarchical search (the same flat rules, proven there against the oracle):
+//   ensureIntervalBoundary: split the leaf that strictly contains pos in the op's view;
+//   insert: before the first leaf whose view start is pos, skipping leaves removed at/below minSeq
+//           except the very last leaf (mergeTree.ts:1862-1875), into that leaf's block; past the
+//           end into the last leaf's block;
+//   nodeMap: the leaves of positive view length inside [start, end).
+#pragma once
+
+#include "../../include/fmt.h"
+#include "wave.h"
+
+namespace fmt_huge {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kMaxNodes = 8;          // MaxNodesInBlock (mergeTreeNodes.ts:248)
+constexpr int kGranularity = 256;     // TextSegmentGranularity (textSegment.ts:21)
+constexpr int32_t kNotRemoved = 0x7fffffff;
+#ifndef FMT_HUGE_SLOTCAP  // (the emulation tests also build tiny groups to exercise group splits)
+#define FMT_HUGE_SLOTCAP 2048
+#define FMT_HUGE_FILL 1024
+#endif
+constexpr int kSlotCap = FMT_HUGE_SLOTCAP;  // leaf blocks listed per group
+constexpr int kGroupCap = 2048;       // groups
+constexpr int kHeapCap = 10240;       // LRU heap entries (≈ blocks registered in one window)
+constexpr int kPropCap = 4096;        // interned prop sets per document
+constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
+
+// Leaf meta word: insert client (int8) | prop set id << 8 (0xFFFF = properties undefined)
+FMT_DEV int32_t mClient(uint32_t m) { return static_cast<int32_t>(static_cast<int8_t>(m & 0xFFu)); }
+FMT_DEV uint32_t mProps(uint32_t m) { return (m >> 8) & 0xFFFFu; }
+FMT_DEV uint32_t mkMeta(int32_t client, uint32_t props) { return (static_cast<uint32_t>(client) & 0xFFu) | (props << 8); }
+constexpr uint32_t kNoProps = 0xFFFFu;
+
+// Window meta word: insert client (int8) | first remover (u8) << 8 | "more removers" << 16
+FMT_DEV uint32_t wFirstRm(uint32_t m) { return (m >> 8) & 0xFFu; }
+
+struct HeapEnt {
+  int32_t maxSeq;
+  uint32_t leafId;
+};
+
+// Device buffers of one huge document (all sized by the runtime from host-side bounds).
+struct HugeState {
+  // leaf fields, [blockCap * 8]: slot k of leaf block b at b * 8 + k
+  uint32_t* lLen;
+  int32_t* lIns;
+  int32_t* lRm;
+  uint32_t* lMlo;
+  uint32_t* lMhi;
+  uint32_t* lId;
+  uint32_t* lText;
+  uint32_t* lMeta;
+  // blocks [blockCap]
+  uint32_t* bCount;
+  uint32_t* bParent;
+  uint32_t* bLeaf;
+  int32_t* bScour;
+  uint32_t* bChild;   // [blockCap * 8] (interior blocks)
+  uint32_t* bGroup;   // leaf blocks: group id
+  uint32_t* bSlot;    // leaf blocks: slot in the group
+  uint32_t* freeBlk;  // [blockCap] stack of freed block ids
+  uint32_t blockCap;
+  // groups [kGroupCap * kSlotCap]
+  uint32_t* gSlotBlk;
+  int32_t* gSlotStable;
+  // leaf id → leaf block / window entry, [idCap]
+  uint32_t* leafBlk;
+  uint32_t* winIdx;
+  uint32_t idCap;
+  // window table [winCap]
+  int32_t* wIns;
+  int32_t* wRm;
+  uint32_t* wLen;
+  uint32_t* wMeta;
+  uint32_t* wGroup;
+  uint32_t* wBlk;
+  uint32_t* wLeaf;
+  uint32_t winCap;
+  // text arena (batch text, then the merge area) and prop sets
+  uint16_t* text;
+  uint64_t textLen;   // batch text (read-only part)
+  uint64_t textCap;
+  uint32_t* props;    // [kPropCap * 5]: n, kv[4]
+};
+
+// LDS state of the wave.
+struct HugeLds {
+  uint16_t gOrder[kGroupCap];    // group ids in document order
+  int32_t gStable[kGroupCap];    // by group id: Σ stable lengths of its slots
+  uint32_t gCount[kGroupCap];    // by group id: slots
+  int32_t gCorr[kGroupCap];      // by group id: window correction of the current perspective
+  int32_t gStart[kGroupCap];     // by position: view start of group gOrder[k]
+  int32_t sLen[kSlotCap];        // the group being searched: view length per slot
+  uint32_t sBlk[kSlotCap];
+  HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
+  uint32_t tmp[256];
+};
+
+struct HugeInputs {
+  const fmt_mt_op* ops;
+  uint64_t begin, end;
+  const uint32_t* propsOff;
+  const uint32_t* propsKv;
+  uint32_t nPropsOps;
+  const fmt_mt_snapshot_seg* segs;  // loaded header chunk
+  uint32_t nSegs;
+  int32_t snapMinSeq, snapSeq;
+};
+
+// A leaf found by the hierarchical search.
+struct Hit {
+  bool found;
+  int gpos;        // position of its group in gOrder
+  int slot;        // slot of its block in the group
+  uint32_t blk;
+  int k;           // slot in the block
+  int st;          // view start of the leaf
+  int vis;         // view length of the leaf
+};
+
+class HugeDoc {
+ public:
+  HugeState S;
+  HugeLds* L;
+  HugeInputs in;
+  int root = 0;
+  int nGroups = 0;
+  uint32_t nextBlock = 0, nFree = 0;
+  int nProps = 0;
+  uint32_t nextId = 1;
+  uint32_t nWin = 0;
+  uint64_t textTop = 0;
+  int heapN = 0;
+  int curSeq = 0, minSeq = 0;
+  int status = FMT_OK, failSeq = 0;
+  uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
+  // shader-clock totals per phase (diagnostics, written to HugeOut::prof): 0 replay, 1 window pass
+  // (groups), 2 window pass (slots), 3 zamboni, 4 graduation, 5 load, 6 output, 7 finds
+  uint64_t prof[8] = {};
+  FMT_DEV static uint64_t clk() {
+#if FMT_GPU
+    return __builtin_amdgcn_s_memtime();
+#else
+    return 0;
+#endif
+  }
+  bool corrValid = false;    // gCorr / gStart hold the current op's perspective
+
+  FMT_DEV bool fail(int code) {
+    if (status == FMT_OK) status = code;
+    return false;
+  }
+
+  // ------------------------------------------------------------------ small helpers
+  // Every read of HBM state this wave wrote goes through an agent-scope load (served by L2, never a
+  // stale vector-L1 line); rd() inside FOR_LANES bodies, ldu()/ldi() for wave-uniform values.
+  FMT_DEV static uint32_t rd(const uint32_t* p) { return loadCoherent(p); }
+  FMT_DEV static int32_t rd(const int32_t* p) { return loadCoherent(p); }
+  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(loadCoherent(p)); }
+  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadCoherent(p)); }
+  // one lane stores a wave-uniform value
+  template <class T>
+  FMT_DEV static void st1(T* p, T v) {
+    FOR_LANES(l) {
+      if (l == 0) *p = v;
+    }
+  }
+  FMT_DEV static bool removedBy(uint32_t mlo, uint32_t mhi, int c) {
+    return c < 32 ? ((mlo >> c) & 1u) != 0 : ((mhi >> (c - 32)) & 1u) != 0;
+  }
+  // leaf length from PriorPerspective(r, c) (perspective.ts:80-93)
+  FMT_DEV static int visOf(uint32_t len, int32_t ins, int32_t rm, uint32_t mlo, uint32_t mhi, int32_t ic, int r, int c) {
+    const bool present = (ins <= r || ic == c) && !(rm <= r || removedBy(mlo, mhi, c));
+    return present ? static_cast<int>(len) : 0;
+  }
+
+  FMT_DEV uint32_t allocBlk(uint32_t leaf) {
+    uint32_t b;
+    if (nFree > 0) {
+      b = ldu(S.freeBlk + --nFree);
+    } else {
+      if (nextBlock >= S.blockCap) {
+        fail(FMT_E_CAPACITY);
+        return kNone;
+      }
+      b = nextBlock++;
+    }
+    st1(S.bCount + b, 0u);
+    st1(S.bParent + b, kNone);
+    st1(S.bLeaf + b, leaf);
+    st1(S.bScour + b, -1);
+    return b;
+  }
+  FMT_DEV void freeBlock(uint32_t b) {
+    st1(S.freeBlk + nFree, b);
+    nFree++;
+  }
+
+  // ------------------------------------------------------------------ window table
+  FMT_DEV void winAdd(uint32_t id, int32_t ins, int32_t rm, uint32_t len, uint32_t meta, uint32_t grp, uint32_t blk) {
+    if (nWin >= S.winCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    const uint32_t w = nWin++;
+    FOR_LANES(l) {
+      if (l == 0) {
+        S.wIns[w] = ins;
+        S.wRm[w] = rm;
+        S.wLen[w] = len;
+        S.wMeta[w] = meta;
+        S.wGroup[w] = grp;
+        S.wBlk[w] = blk;
+        S.wLeaf[w] = id;
+        S.winIdx[id] = w;
+      }
+    }
+  }
+  FMT_DEV void winRemove(uint32_t w) {  // swap-remove
+    const uint32_t last = nWin - 1;
+    const uint32_t id = ldu(S.wLeaf + w);
+    if (w != last) {
+      const int32_t a = ldi(S.wIns + last), b = ldi(S.wRm + last);
+      const uint32_t c = ldu(S.wLen + last), d = ldu(S.wMeta + last), e = ldu(S.wGroup + last),
+                     f = ldu(S.wBlk + last), g = ldu(S.wLeaf + last);
+      FOR_LANES(l) {
+        if (l == 0) {
+          S.wIns[w] = a;
+          S.wRm[w] = b;
+          S.wLen[w] = c;
+          S.wMeta[w] = d;
+          S.wGroup[w] = e;
+          S.wBlk[w] = f;
+          S.wLeaf[w] = g;
+          S.winIdx[g] = w;
+        }
+      }
+    }
+    st1(S.winIdx + id, kNone);
+    nWin = last;
+  }
+
+  // ------------------------------------------------------------------ stable sums
+  // Stable length of a leaf: its length for every perspective at/above minSeq (non-window leaves).
+  FMT_DEV void addStable(uint32_t blk, int delta) {
+    if (delta == 0) return;
+    const uint32_t g = ldu(S.bGroup + blk), s = ldu(S.bSlot + blk);
+    int32_t* p = S.gSlotStable + static_cast<size_t>(g) * kSlotCap + s;
+    const int32_t v = ldi(p);
+    st1(p, v + delta);
+    L->gStable[g] += delta;  // (uniform LDS store)
+    waveSync();
+  }
+
+  // Recompute the stable length of a leaf block from its leaves (non-window leaves only).
+  FMT_DEV int blockStable(uint32_t b) {
+    const uint32_t cnt = ldu(S.bCount + b);
+    Lane<int> v;
+    FOR_LANES(l) {
+      int x = 0;
+      if (l < static_cast<int>(cnt)) {
+        const size_t i = static_cast<size_t>(b) * 8 + l;
+        const bool win = rd(S.winIdx + (rd(S.lId + i))) != kNone;
+        x = (!win && rd(S.lRm + i) == kNotRemoved) ? static_cast<int>(rd(S.lLen + i)) : 0;
+      }
+      LANE(v) = x;
+    }
+    uint32_t tot;
+    Lane<uint32_t> vu;
+    FOR_LANES(l) { LANE(vu) = static_cast<uint32_t>(LANE(v)); }
+    waveExclusiveSum(vu, &tot);
+    return static_cast<int>(tot);
+  }
+
+  // ------------------------------------------------------------------ group lists
+  FMT_DEV uint32_t* slotBlkPtr(uint32_t g) { return S.gSlotBlk + static_cast<size_t>(g) * kSlotCap; }
+  FMT_DEV int32_t* slotStPtr(uint32_t g) { return S.gSlotStable + static_cast<size_t>(g) * kSlotCap; }
+
+  FMT_DEV int groupPos(uint32_t g) const {  // position of group g in gOrder
+    for (int base = 0; base < nGroups; base += 64) {
+      Lane<bool> p;
+      FOR_LANES(l) { LANE(p) = base + l < nGroups && L->gOrder[base + l] == g; }
+      const uint64_t m = ballot(p);
+      if (m) return base + ctz64(m);
+    }
+    return -1;
+  }
+
+  // Insert leaf block nb into group g at slot `at` with stable length st (slots at/after shift up).
+  // Splits the group first when it is full; returns false on failure.
+  FMT_DEV bool slotInsert(uint32_t g, int at, uint32_t nb, int st) {
+    int cnt = static_cast<int>(L->gCount[g]);
+    if (cnt >= kSlotCap) {
+      if (!groupSplit(g)) return false;
+      cnt = static_cast<int>(L->gCount[g]);
+      if (at > cnt) {  // the slot moved to the new group
+        const int gp = groupPos(g);
+        const uint32_t g2 = L->gOrder[gp + 1];
+        return slotInsert(g2, at - cnt, nb, st);
+      }
+    }
+    uint32_t* sb = slotBlkPtr(g);
+    int32_t* ss = slotStPtr(g);
+    for (int top = cnt - 1; top >= at; top -= 64) {  // shift [at, cnt) up by one, top-down
+      Lane<uint32_t> b;
+      Lane<int32_t> s;
+      FOR_LANES(l) {
+        const int i = top - l;
+        if (i >= at) {
+          LANE(b) = sb[i];
+          LANE(s) = ss[i];
+        }
+      }
+      waveSync();
+      FOR_LANES(l) {
+        const int i = top - l;
+        if (i >= at) {
+          sb[i + 1] = LANE(b);
+          ss[i + 1] = LANE(s);
+          S.bSlot[LANE(b)] = static_cast<uint32_t>(i + 1);
+        }
+      }
+      waveSync();
+    }
+    FOR_LANES(l) {
+      if (l == 0) {
+        sb[at] = nb;
+        ss[at] = st;
+        S.bSlot[nb] = static_cast<uint32_t>(at);
+        S.bGroup[nb] = g;
+      }
+    }
+    L->gCount[g] = static_cast<uint32_t>(cnt + 1);
+    L->gStable[g] += st;
+    waveSync();
+    return true;
+  }
+
+  // Remove slots [at, at + n) of group g (their blocks are being freed or moved); returns the
+  // stable length they held.
+  FMT_DEV void slotRemove(uint32_t g, int at, int n) {
+    const int cnt = static_cast<int>(L->gCount[g]);
+    uint32_t* sb = slotBlkPtr(g);
+    int32_t* ss = slotStPtr(g);
+    int removed = 0;
+    for (int i = at; i < at + n; i++) removed += ldi(ss + i);
+    for (int base = at + n; base < cnt; base += 64) {
+      Lane<uint32_t> b;
+      Lane<int32_t> s;
+      FOR_LANES(l) {
+        const int i = base + l;
+        if (i < cnt) {
+          LANE(b) = sb[i];
+          LANE(s) = ss[i];
+        }
+      }
+      waveSync();
+      FOR_LANES(l) {
+        const int i = base + l;
+        if (i < cnt) {
+          sb[i - n] = LANE(b);
+          ss[i - n] = LANE(s);
+          S.bSlot[LANE(b)] = static_cast<uint32_t>(i - n);
+        }
+      }
+      waveSync();
+    }
+    L->gCount[g] = static_cast<uint32_t>(cnt - n);
+    L->gStable[g] -= removed;
+    waveSync();
+  }
+
+  // A full group splits in two halves; the new group follows it in gOrder. Window entries of
+  // blocks that moved are re-tagged.
+  FMT_DEV bool groupSplit(uint32_t g) {
+    if (nGroups >= kGroupCap) return fail(FMT_E_CAPACITY);
+    const uint32_t g2 = static_cast<uint32_t>(nGroups);  // group ids are never freed
+    const int cnt = static_cast<int>(L->gCount[g]), half = cnt / 2, moved = cnt - half;
+    uint32_t* sb = slotBlkPtr(g);
+    int32_t* ss = slotStPtr(g);
+    uint32_t* db = slotBlkPtr(g2);
+    int32_t* ds = slotStPtr(g2);
+    Lane<int32_t> acc;
+    FOR_LANES(l) { LANE(acc) = 0; }
+    for (int base = 0; base < moved; base += 64) {
+      FOR_LANES(l) {
+        const int i = base + l;
+        if (i < moved) {
+          const uint32_t b = sb[half + i];
+          const int32_t s = ss[half + i];
+          db[i] = b;
+          ds[i] = s;
+          S.bGroup[b] = g2;
+          S.bSlot[b] = static_cast<uint32_t>(i);
+          LANE(acc) += s;
+        }
+      }
+    }
+    uint32_t tot;
+    Lane<uint32_t> au;
+    FOR_LANES(l) { LANE(au) = static_cast<uint32_t>(LANE(acc)); }
+    waveExclusiveSum(au, &tot);
+    const int gp = groupPos(g);
+    for (int k = nGroups; k > gp + 1; k--) {
+      const uint16_t v = L->gOrder[k - 1];
+      waveSync();
+      L->gOrder[k] = v;
+    }
+    L->gOrder[gp + 1] = static_cast<uint16_t>(g2);
+    L->gCount[g] = static_cast<uint32_t>(half);
+    L->gCount[g2] = static_cast<uint32_t>(moved);
+    L->gStable[g] -= static_cast<int32_t>(tot);
+    L->gStable[g2] = static_cast<int32_t>(tot);
+    L->gCorr[g2] = 0;
+    waveSync();
+    nGroups++;
+    // window entries follow their blocks
+    for (uint32_t base = 0; base < nWin; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t w = base + l;
+        if (w < nWin && rd(S.wGroup + w) == g) S.wGroup[w] = rd(S.bGroup + (rd(S.wBlk + w)));
+      }
+    }
+    corrValid = false;
+    return true;
+  }
+
+  // ------------------------------------------------------------------ perspective corrections
+  // gCorr[g] = Σ view length of the window leaves of group g (their stable contribution is 0), and
+  // gStart[k] = view start of the k-th group, for PriorPerspective(r, c).
+  FMT_DEV void groupCorrections(int r, int c) {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[1], t0_};
+    FOR_LANES(l) {
+      for (int g = l; g < nGroups; g += 64) L->gCorr[g] = 0;
+    }
+    waveSync();
+    for (uint32_t base = 0; base < nWin; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t w = base + l;
+        if (w < nWin) {
+          const uint32_t m = rd(S.wMeta + w);
+          const int32_t ins = rd(S.wIns + w), rm = rd(S.wRm + w);
+          int v;
+          if ((m >> 16) & 1u) {  // several removers: the leaf's full remover set
+            const uint32_t id = rd(S.wLeaf + w);
+            const uint32_t b = rd(S.leafBlk + id);
+            const int bc = static_cast<int>(rd(S.bCount + b));  // (slots past the count hold stale leaves)
+            uint32_t mlo = 0, mhi = 0;
+            for (int k = 0; k < bc; k++) {
+              const size_t i = static_cast<size_t>(b) * 8 + k;
+              if (rd(S.lId + i) == id) {
+                mlo = rd(S.lMlo + i);
+                mhi = rd(S.lMhi + i);
+              }
+            }
+            v = visOf(rd(S.wLen + w), ins, rm, mlo, mhi, mClient(m), r, c);
+          } else {
+            const uint32_t f = wFirstRm(m);
+            const bool byC = rm != kNotRemoved && static_cast<int>(f) == c;
+            v = ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(rd(S.wLen + w)) : 0;
+          }
+          if (v) atomicAddLds(&L->gCorr[rd(S.wGroup + w)], v);
+        }
+      }
+    }
+    waveSync();
+    int32_t base = 0;
+    for (int k0 = 0; k0 < nGroups; k0 += 64) {
+      Lane<uint32_t> len;
+      FOR_LANES(l) {
+        const int k = k0 + l;
+        uint32_t x = 0;
+        if (k < nGroups) {
+          const uint32_t g = L->gOrder[k];
+          x = static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
+        }
+        LANE(len) = x;
+      }
+      uint32_t tot;
+      const Lane<uint32_t> ex = waveExclusiveSum(len, &tot);
+      FOR_LANES(l) {
+        if (k0 + l < nGroups) L->gStart[k0 + l] = base + static_cast<int32_t>(LANE(ex));
+      }
+      base += static_cast<int32_t>(tot);
+    }
+    waveSync();
+    corrValid = true;
+  }
+
+  FMT_DEV int totalView() const {
+    if (nGroups == 0) return 0;
+    const uint32_t g = L->gOrder[nGroups - 1];
+    return uni(L->gStart[nGroups - 1] + L->gStable[g] + L->gCorr[g]);
+  }
+
+  // Slot view lengths of group g into L->sLen / L->sBlk (stable + that group's window corrections).
+  FMT_DEV void slotLengths(uint32_t g, int r, int c) {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[2], t0_};
+    const int cnt = static_cast<int>(L->gCount[g]);
+    const uint32_t* sb = slotBlkPtr(g);
+    const int32_t* ss = slotStPtr(g);
+    FOR_LANES(l) {
+      for (int i = l; i < cnt; i += 64) {
+        L->sBlk[i] = sb[i];
+        L->sLen[i] = ss[i];
+      }
+    }
+    waveSync();
+    for (uint32_t base = 0; base < nWin; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t w = base + l;
+        if (w < nWin && rd(S.wGroup + w) == g) {
+          const uint32_t m = rd(S.wMeta + w);
+          const int32_t ins = rd(S.wIns + w), rm = rd(S.wRm + w);
+          int v;
+          if ((m >> 16) & 1u) {
+            const uint32_t id = rd(S.wLeaf + w);
+            const uint32_t b = rd(S.leafBlk + id);
+            const int bc = static_cast<int>(rd(S.bCount + b));  // (slots past the count hold stale leaves)
+            uint32_t mlo = 0, mhi = 0;
+            for (int k = 0; k < bc; k++) {
+              const size_t i = static_cast<size_t>(b) * 8 + k;
+              if (rd(S.lId + i) == id) {
+                mlo = rd(S.lMlo + i);
+                mhi = rd(S.lMhi + i);
+              }
+            }
+            v = visOf(rd(S.wLen + w), ins, rm, mlo, mhi, mClient(m), r, c);
+          } else {
+            const uint32_t f = wFirstRm(m);
+            const bool byC = rm != kNotRemoved && static_cast<int>(f) == c;
+            v = ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(rd(S.wLen + w)) : 0;
+          }
+          if (v) atomicAddLds(&L->sLen[rd(S.bSlot + (rd(S.wBlk + w)))], v);
+        }
+      }
+    }
+    waveSync();
+  }
+
+  // ------------------------------------------------------------------ the hierarchical search
+  // The first leaf (document order) with st <= p < st + vis, or st == p, vis == 0 and not skipped
+  // (removed at/below minSeq, unless it is the document's very last leaf).
+  FMT_DEV Hit find(int p, int r, int c) {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[7], t0_};
+    Hit h;
+    h.found = false;
+    if (!corrValid) groupCorrections(r, c);
+    // first group whose end reaches p
+    int k = -1;
+    for (int k0 = 0; k0 < nGroups && k < 0; k0 += 64) {
+      Lane<bool> q;
+      FOR_LANES(l) {
+        const int kk = k0 + l;
+        bool ok = false;
+        if (kk < nGroups) {
+          const uint32_t g = L->gOrder[kk];
+          ok = L->gStart[kk] + L->gStable[g] + L->gCorr[g] >= p;
+        }
+        LANE(q) = ok;
+      }
+      const uint64_t m = ballot(q);
+      if (m) k = k0 + ctz64(m);
+    }
+    if (k < 0) return h;
+    for (; k < nGroups; k++) {
+      const uint32_t g = L->gOrder[k];
+      slotLengths(g, r, c);
+      const int cnt = static_cast<int>(L->gCount[g]);
+      int base = uni(L->gStart[k]);
+      for (int s0 = 0; s0 < cnt; s0 += 64) {
+        Lane<uint32_t> len;
+        FOR_LANES(l) { LANE(len) = s0 + l < cnt ? static_cast<uint32_t>(L->sLen[s0 + l]) : 0u; }
+        uint32_t tot;
+        const Lane<uint32_t> ex = waveExclusiveSum(len, &tot);
+        // candidate slots: end >= p, in order
+        Lane<bool> q;
+        FOR_LANES(l) { LANE(q) = s0 + l < cnt && base + static_cast<int>(LANE(ex) + LANE(len)) >= p; }
+        uint64_t m = ballot(q);
+        while (m) {
+          const int lane = ctz64(m);
+          m &= m - 1;
+          const int s = s0 + lane;
+          const int bst = base + static_cast<int>(readlane(ex, lane));
+          if (bst > p) return h;  // passed p: nothing qualifies (cannot happen for valid ops)
+          if (leafInBlock(L->sBlk[s], bst, p, r, c, h)) {
+            h.gpos = k;
+            h.slot = s;
+            return h;
+          }
+        }
+        base += static_cast<int>(tot);
+      }
+    }
+    return h;
+  }
+
+  // Search one leaf block whose view start is bst.
+  FMT_DEV bool leafInBlock(uint32_t b, int bst, int p, int r, int c, Hit& h) {
+    const uint32_t cnt = ldu(S.bCount + b);
+    Lane<uint32_t> vis;
+    Lane<bool> skipped;
+    FOR_LANES(l) {
+      uint32_t v = 0;
+      bool sk = false;
+      if (l < static_cast<int>(cnt)) {
+        const size_t i = static_cast<size_t>(b) * 8 + l;
+        const int32_t rm = rd(S.lRm + i);
+        v = static_cast<uint32_t>(visOf(rd(S.lLen + i), rd(S.lIns + i), rm, rd(S.lMlo + i), rd(S.lMhi + i), mClient(rd(S.lMeta + i)), r, c));
+        sk = rm <= minSeq && !(b == lastBlk && l == static_cast<int>(cnt) - 1);
+      }
+      LANE(vis) = v;
+      LANE(skipped) = sk;
+    }
+    uint32_t tot;
+    const Lane<uint32_t> ex = waveExclusiveSum(vis, &tot);
+    Lane<bool> q;
+    FOR_LANES(l) {
+      const int st = bst + static_cast<int>(LANE(ex));
+      const int v = static_cast<int>(LANE(vis));
+      LANE(q) = l < static_cast<int>(cnt) && ((st <= p && p < st + v) || (st == p && v == 0 && !LANE(skipped)));
+    }
+    const uint64_t m = ballot(q);
+    if (!m) return false;
+    const int k = ctz64(m);
+    h.found = true;
+    h.blk = b;
+    h.k = k;
+    h.st = bst + static_cast<int>(readlane(ex, k));
+    h.vis = static_cast<int>(readlane(vis, k));
+    return true;
+  }
+
+  // ------------------------------------------------------------------ leaves inside a block
+  FMT_DEV size_t li(uint32_t b, int k) const { return static_cast<size_t>(b) * 8 + k; }
+
+  struct Leaf {
+    uint32_t len;
+    int32_t ins, rm;
+    uint32_t mlo, mhi, id, text, meta;
+  };
+  FMT_DEV Leaf getLeaf(uint32_t b, int k) const {
+    const size_t i = li(b, k);
+    Leaf x;
+    x.len = ldu(S.lLen + i);
+    x.ins = ldi(S.lIns + i);
+    x.rm = ldi(S.lRm + i);
+    x.mlo = ldu(S.lMlo + i);
+    x.mhi = ldu(S.lMhi + i);
+    x.id = ldu(S.lId + i);
+    x.text = ldu(S.lText + i);
+    x.meta = ldu(S.lMeta + i);
+    return x;
+  }
+  FMT_DEV void putLeaf(uint32_t b, int k, const Leaf& x) {
+    const size_t i = li(b, k);
+    FOR_LANES(l) {
+      if (l == 0) {
+        S.lLen[i] = x.len;
+        S.lIns[i] = x.ins;
+        S.lRm[i] = x.rm;
+        S.lMlo[i] = x.mlo;
+        S.lMhi[i] = x.mhi;
+        S.lId[i] = x.id;
+        S.lText[i] = x.text;
+        S.lMeta[i] = x.meta;
+        S.leafBlk[x.id] = b;
+      }
+    }
+  }
+  // Shift leaves [k, cnt) of block b up by one (room at k); the caller puts the new leaf.
+  FMT_DEV void shiftUp(uint32_t b, int k, int cnt) {
+    Lane<uint32_t> f[8];
+    FOR_LANES(l) {
+      if (l >= k && l < cnt) {
+        const size_t i = li(b, l);
+        LANE(f[0]) = rd(S.lLen + i);
+        LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
+        LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
+        LANE(f[3]) = rd(S.lMlo + i);
+        LANE(f[4]) = rd(S.lMhi + i);
+        LANE(f[5]) = rd(S.lId + i);
+        LANE(f[6]) = rd(S.lText + i);
+        LANE(f[7]) = rd(S.lMeta + i);
+      }
+    }
+    waveSync();
+    FOR_LANES(l) {
+      if (l >= k && l < cnt) {
+        const size_t i = li(b, l + 1);
+        S.lLen[i] = LANE(f[0]);
+        S.lIns[i] = static_cast<int32_t>(LANE(f[1]));
+        S.lRm[i] = static_cast<int32_t>(LANE(f[2]));
+        S.lMlo[i] = LANE(f[3]);
+        S.lMhi[i] = LANE(f[4]);
+        S.lId[i] = LANE(f[5]);
+        S.lText[i] = LANE(f[6]);
+        S.lMeta[i] = LANE(f[7]);
+      }
+    }
+    waveSync();
+  }
+
+  // Move leaves [from, cnt) of block a to the front of block b (b's leaves shift up by the count).
+  FMT_DEV void moveLeaves(uint32_t a, int from, int cnt, uint32_t b) {
+    const int n = cnt - from;
+    if (n <= 0) return;
+    Lane<uint32_t> f[8];
+    FOR_LANES(l) {
+      if (l < n) {
+        const size_t i = li(a, from + l);
+        LANE(f[0]) = rd(S.lLen + i);
+        LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
+        LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
+        LANE(f[3]) = rd(S.lMlo + i);
+        LANE(f[4]) = rd(S.lMhi + i);
+        LANE(f[5]) = rd(S.lId + i);
+        LANE(f[6]) = rd(S.lText + i);
+        LANE(f[7]) = rd(S.lMeta + i);
+      }
+    }
+    waveSync();
+    FOR_LANES(l) {
+      if (l < n) {
+        const size_t i = li(b, l);
+        S.lLen[i] = LANE(f[0]);
+        S.lIns[i] = static_cast<int32_t>(LANE(f[1]));
+        S.lRm[i] = static_cast<int32_t>(LANE(f[2]));
+        S.lMlo[i] = LANE(f[3]);
+        S.lMhi[i] = LANE(f[4]);
+        S.lId[i] = LANE(f[5]);
+        S.lText[i] = LANE(f[6]);
+        S.lMeta[i] = LANE(f[7]);
+        S.leafBlk[LANE(f[5])] = b;
+        const uint32_t w = rd(S.winIdx + (LANE(f[5])));
+        if (w != kNone) S.wBlk[w] = b;
+      }
+    }
+    waveSync();
+  }
+
+  // Window entries of block b's leaves name b and its group.
+  FMT_DEV void retagWindow(uint32_t b) {
+    const uint32_t cnt = ldu(S.bCount + b), g = ldu(S.bGroup + b);
+    FOR_LANES(l) {
+      if (l < static_cast<int>(cnt)) {
+        const uint32_t w = rd(S.winIdx + rd(S.lId + li(b, l)));
+        if (w != kNone) {
+          S.wGroup[w] = g;
+          S.wBlk[w] = b;
+        }
+      }
+    }
+    waveSync();
+  }
+
+  // ------------------------------------------------------------------ B+tree
+  FMT_DEV uint32_t childAt(uint32_t p, int i) const { return ldu(S.bChild + static_cast<size_t>(p) * 8 + i); }
+  FMT_DEV void setChild(uint32_t p, int i, uint32_t c) {
+    st1(S.bChild + static_cast<size_t>(p) * 8 + i, c);
+    st1(S.bParent + c, p);
+  }
+
+  // A child was inserted into block b: split on overflow (mergeTree.ts:1946-1987), propagate, grow
+  // the root (:1313-1320). Leaf blocks split 4/4 into a new leaf block listed in the next slot.
+  FMT_DEV void childAdded(uint32_t b) {
+    uint32_t cnt = ldu(S.bCount + b) + 1;
+    st1(S.bCount + b, cnt);
+    while (cnt >= static_cast<uint32_t>(kMaxNodes)) {
+      const uint32_t leaf = ldu(S.bLeaf + b);
+      const uint32_t nb = allocBlk(leaf);
+      if (nb == kNone) return;
+      constexpr int half = kMaxNodes / 2;
+      if (leaf) {
+        // the new block takes leaves 4..7; both stable sums are recomputed from their leaves
+        const uint32_t g = ldu(S.bGroup + b);
+        const int s = static_cast<int>(ldu(S.bSlot + b));
+        st1(S.bGroup + nb, g);  // (tentative: a group split in slotInsert may move it)
+        moveLeaves(b, half, kMaxNodes, nb);
+        st1(S.bCount + b, static_cast<uint32_t>(half));
+        st1(S.bCount + nb, static_cast<uint32_t>(half));
+        const int oldSt = ldi(slotStPtr(g) + s);
+        const int stB = blockStable(b), stN = blockStable(nb);
+        st1(slotStPtr(g) + s, stB);
+        L->gStable[g] += stB - oldSt;
+        waveSync();
+        if (!slotInsert(g, s + 1, nb, stN)) return;
+        retagWindow(nb);
+        if (lastBlk == b) lastBlk = nb;
+      } else {
+        for (int i = 0; i < half; i++) setChild(nb, i, childAt(b, half + i));
+        st1(S.bCount + b, static_cast<uint32_t>(half));
+        st1(S.bCount + nb, static_cast<uint32_t>(half));
+      }
+      const uint32_t p = ldu(S.bParent + b);
+      if (p == kNone) {
+        const uint32_t r = allocBlk(0);
+        if (r == kNone) return;
+        st1(S.bCount + r, 2u);
+        setChild(r, 0, b);
+        setChild(r, 1, nb);
+        root = static_cast<int>(r);
+        return;
+      }
+      const uint32_t pc = ldu(S.bCount + p);
+      int idx = 0;
+      while (idx < static_cast<int>(pc) && childAt(p, idx) != b) idx++;
+      for (int i = static_cast<int>(pc); i > idx + 1; i--) setChild(p, i, childAt(p, i - 1));
+      setChild(p, idx + 1, nb);
+      st1(S.bCount + p, pc + 1);
+      cnt = pc + 1;
+      b = p;
+    }
+  }
+
+  // ------------------------------------------------------------------ LRU heap (heap.ts)
+  FMT_DEV int heapSeq(int k) const { return uni(L->heap[k].maxSeq); }
+  FMT_DEV void heapSwap(int a, int b) {
+    const HeapEnt x = L->heap[a], y = L->heap[b];
+    waveSync();
+    L->heap[a] = y;
+    L->heap[b] = x;
+    waveSync();
+  }
+  FMT_DEV void heapAdd(int maxSeq, uint32_t leafId) {
+    if (heapN >= kHeapCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    heapN++;
+    L->heap[heapN].maxSeq = maxSeq;
+    L->heap[heapN].leafId = leafId;
+    waveSync();
+    int k = heapN;
+    while (k > 1 && heapSeq(k >> 1) - heapSeq(k) > 0) {
+      heapSwap(k, k >> 1);
+      k >>= 1;
+    }
+  }
+  FMT_DEV HeapEnt heapGet() {
+    heapSwap(1, heapN);
+    HeapEnt x;
+    x.maxSeq = uni(L->heap[heapN].maxSeq);
+    x.leafId = uni(L->heap[heapN].leafId);
+    heapN--;
+    int k = 1;
+    while ((k << 1) <= heapN) {
+      int j = k << 1;
+      if (j < heapN && heapSeq(j) - heapSeq(j + 1) > 0) j++;
+      if (heapSeq(k) - heapSeq(j) <= 0) break;
+      heapSwap(k, j);
+      k = j;
+    }
+    return x;
+  }
+
+  // addToLRUSet (mergeTree.ts:812-822): the first registration of a block sets needsScour.
+  FMT_DEV void lru(uint32_t b, uint32_t leafId, int seq) {
+    if (ldi(S.bScour + b) != 1 && seq > curSeq) {
+      st1(S.bScour + b, 1);
+      heapAdd(seq, leafId);
+    }
+  }
+
+  // ------------------------------------------------------------------ props
+  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {  // properties.ts:32-61, undefined ≡ {}
+    if (a == b) return true;
+    const uint32_t na = a == kNoProps ? 0u : ldu(S.props + a * 5), nb = b == kNoProps ? 0u : ldu(S.props + b * 5);
+    if (na != nb) return false;
+    for (uint32_t i = 0; i < na; i++) {
+      const uint32_t x = ldu(S.props + a * 5 + 1 + i);
+      bool found = false;
+      for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t y = ldu(S.props + b * 5 + 1 + j);
+        if ((y >> 16) == (x >> 16)) found = y == x;
+      }
+      if (!found) return false;
+    }
+    return true;
+  }
+  // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
+  FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
+    uint32_t kv[FMT_MT_PROPS_MAX] = {0, 0, 0, 0};
+    uint32_t cnt = 0;
+    if (old != kNoProps) {
+      cnt = ldu(S.props + old * 5);
+      for (uint32_t i = 0; i < cnt; i++) kv[i] = ldu(S.props + old * 5 + 1 + i);
+    }
+    const uint32_t a = ldu(in.propsOff + opId), b = ldu(in.propsOff + opId + 1);
+    for (uint32_t t = a; t < b; t++) {
+      const uint32_t e = ldu(in.propsKv + t);
+      uint32_t pos = cnt;
+      for (uint32_t i = 0; i < cnt; i++)
+        if ((kv[i] >> 16) == (e >> 16)) pos = i;
+      if ((e & 0xFFFFu) == 0) {
+        if (pos < cnt) {
+          for (uint32_t i = pos; i + 1 < cnt; i++) kv[i] = kv[i + 1];
+          cnt--;
+        }
+      } else if (pos < cnt) {
+        kv[pos] = e;
+      } else {
+        if (cnt >= FMT_MT_PROPS_MAX) {
+          fail(FMT_E_CAPACITY);
+          return kNoProps;
+        }
+        kv[cnt++] = e;
+      }
+    }
+    for (int base = 0; base < nProps; base += 64) {  // interned already?
+      Lane<bool> same;
+      FOR_LANES(l) {
+        const int p = base + l;
+        bool eq = p < nProps && rd(S.props + (p * 5)) == cnt;
+        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
+          if (i < cnt) eq = eq && rd(S.props + (p * 5 + 1 + i)) == kv[i];
+        LANE(same) = eq;
+      }
+      const uint64_t m = ballot(same);
+      if (m) return static_cast<uint32_t>(base + ctz64(m));
+    }
+    if (nProps >= kPropCap) {
+      fail(FMT_E_CAPACITY);
+      return kNoProps;
+    }
+    const uint32_t id = static_cast<uint32_t>(nProps++);
+    FOR_LANES(l) {
+      if (l == 0) {
+        S.props[id * 5] = cnt;
+        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) S.props[id * 5 + 1 + i] = kv[i];
+      }
+    }
+    waveSync();
+    return id;
+  }
+
+  // ------------------------------------------------------------------ op pieces
+  // splitLeafSegment (mergeTree.ts:1768-1796) of leaf (b, k) at offset o (0 < o < len): the right part
+  // follows it in the same block, with a fresh id; a window leaf's right part joins the window table.
+  FMT_DEV bool splitLeaf(uint32_t b, int k, int o) {
+    Leaf x = getLeaf(b, k);
+    if (nextId >= S.idCap) return fail(FMT_E_CAPACITY);
+    Leaf y = x;
+    y.id = nextId++;
+    y.len = x.len - static_cast<uint32_t>(o);
+    y.text = x.text + static_cast<uint32_t>(o);
+    x.len = static_cast<uint32_t>(o);
+    const uint32_t cnt = ldu(S.bCount + b);
+    shiftUp(b, k + 1, static_cast<int>(cnt));
+    putLeaf(b, k, x);
+    putLeaf(b, k + 1, y);
+    const uint32_t w = ldu(S.winIdx + x.id);
+    if (w != kNone) {
+      st1(S.wLen + w, x.len);
+      winAdd(y.id, y.ins, y.rm, y.len, ldu(S.wMeta + w), ldu(S.bGroup + b), b);
+    } else {
+      st1(S.winIdx + y.id, kNone);
+    }
+    childAdded(b);
+    return status == FMT_OK;
+  }
+
+  // After a split the right part's location: it followed (b, k) before childAdded may have moved it.
+  FMT_DEV void locate(uint32_t id, uint32_t* b, int* k) const {
+    const uint32_t bb = ldu(S.leafBlk + id);
+    const uint32_t cnt = ldu(S.bCount + bb);
+    Lane<bool> q;
+    FOR_LANES(l) { LANE(q) = l < static_cast<int>(cnt) && rd(S.lId + (li(bb, l))) == id; }
+    const uint64_t m = ballot(q);
+    *b = bb;
+    *k = m ? ctz64(m) : -1;
+  }
+
+  // ensureIntervalBoundary(p) in the op's view: split the leaf strictly containing p.
+  FMT_DEV bool boundary(int p, int r, int c) {
+    const Hit h = find(p, r, c);
+    if (!h.found || h.st >= p) return true;
+    return splitLeaf(h.blk, h.k, p - h.st);
+  }
+
+  FMT_DEV void insertText(const fmt_mt_op& op) {
+    const int r = op.ref_seq, c = op.client, p = op.pos1;
+    if (!boundary(p, r, c)) return;
+    if (op.len == 0) return;
+    Hit h = find(p, r, c);
+    uint32_t b;
+    int k;
+    if (h.found) {
+      b = h.blk;
+      k = h.k;
+    } else {
+      if (p != totalView()) {  // "MergeTree insert failed" (mergeTree.ts:1629)
+        fail(FMT_E_DATA);
+        return;
+      }
+      if (lastBlk == kNone) {  // empty document: the empty root becomes a leaf block
+        fail(FMT_E_UNSUPPORTED);
+        return;
+      }
+      b = lastBlk;
+      k = static_cast<int>(ldu(S.bCount + b));
+    }
+    if (nextId >= S.idCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    Leaf x;
+    x.len = op.len;
+    x.ins = op.seq;
+    x.rm = kNotRemoved;
+    x.mlo = x.mhi = 0;
+    x.id = nextId++;
+    x.text = op.payload;
+    x.meta = mkMeta(c, kNoProps);
+    const uint32_t cnt = ldu(S.bCount + b);
+    shiftUp(b, k, static_cast<int>(cnt));
+    putLeaf(b, k, x);
+    winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, ldu(S.bGroup + b), b);
+    childAdded(b);
+    if (status != FMT_OK) return;
+    uint32_t bb;
+    int kk;
+    locate(x.id, &bb, &kk);
+    lru(bb, x.id, op.seq);
+  }
+
+  // markRangeRemoved / annotateRange over the leaves of positive view length in [start, end).
+  FMT_DEV void applyRange(const fmt_mt_op& op) {
+    const int r = op.ref_seq, c = op.client, seq = op.seq;
+    const int start = op.pos1, end = op.pos2;
+    if (!boundary(start, r, c) || !boundary(end, r, c)) return;
+    if (end <= start) return;
+    Hit h = find(start, r, c);
+    if (!h.found) return;
+#ifdef FMT_HUGE_CHECK
+    if (getenv("HUGE_DEBUG_SEQ") && atoi(getenv("HUGE_DEBUG_SEQ")) == seq)
+      std::fprintf(stderr, "range seq %d [%d,%d): hit gpos %d slot %d blk %u k %d st %d vis %d nGroups %d group %u count %u\n", seq, start,
+                   end, h.gpos, h.slot, h.blk, h.k, h.st, h.vis, nGroups, L->gOrder[h.gpos], L->gCount[L->gOrder[h.gpos]]);
+#endif
+#ifdef FMT_HUGE_CHECK
+    checkInvariants(seq);
+    if (getenv("HUGE_DEBUG_SEQ") && atoi(getenv("HUGE_DEBUG_SEQ")) == seq) {
+      for (int kk = 0; kk < 3; kk++) {
+        const uint32_t gg = L->gOrder[kk];
+        std::fprintf(stderr, "  gOrder[%d]=%u count %u:", kk, gg, L->gCount[gg]);
+        for (uint32_t q = 0; q < L->gCount[gg]; q++) std::fprintf(stderr, " %u", S.gSlotBlk[static_cast<size_t>(gg) * kSlotCap + q]);
+        std::fprintf(stderr, "\n");
+      }
+    }
+#endif
+    // walk forward from the first leaf at `start` (view start h.st == start)
+    int k = h.gpos, s = h.slot;
+    uint32_t g = L->gOrder[k];
+    int pos = h.st;
+    int first = h.k;
+    for (;;) {
+      const uint32_t b = L->sBlk[s];
+      const uint32_t cnt = ldu(S.bCount + b);
+#ifdef FMT_HUGE_CHECK
+      if (getenv("HUGE_DEBUG_SEQ") && atoi(getenv("HUGE_DEBUG_SEQ")) == seq)
+        std::fprintf(stderr, "  walk k %d g %u s %d blk %u cnt %u first %d pos %d\n", k, g, s, b, cnt, first, pos);
+#endif
+      bool done = false;
+      for (int j = first; j < static_cast<int>(cnt); j++) {
+        if (pos >= end) {
+          done = true;
+          break;
+        }
+        Leaf x = getLeaf(b, j);
+        const int v = visOf(x.len, x.ins, x.rm, x.mlo, x.mhi, mClient(x.meta), r, c);
+        if (v > 0) {
+          if (op.type == FMT_MT_REMOVE) removeLeaf(b, j, x, seq, c);
+          else annotateLeaf(b, j, x, op.payload);
+          if (status != FMT_OK) return;
+          lru(b, x.id, seq);
+          if (status != FMT_OK) return;
+        }
+        pos += v;
+      }
+      if (done || pos >= end) break;
+      first = 0;
+      bool more = true;
+      for (++s; s >= static_cast<int>(L->gCount[g]);) {  // next slot, skipping empty groups
+        if (++k >= nGroups) {
+          more = false;
+          break;
+        }
+        g = L->gOrder[k];
+        slotLengths(g, r, c);
+        s = 0;
+      }
+      if (!more) break;
+    }
+  }
+
+  FMT_DEV void removeLeaf(uint32_t b, int j, Leaf& x, int seq, int c) {
+    const bool was = x.rm != kNotRemoved;
+    if (!was) x.rm = seq;
+    if (c < 32) x.mlo |= 1u << c;
+    else x.mhi |= 1u << (c - 32);
+    putLeaf(b, j, x);
+    const uint32_t w = ldu(S.winIdx + x.id);
+    if (w == kNone) {  // a stable leaf enters the window: its length leaves the stable sums
+      addStable(b, -static_cast<int>(x.len));
+      winAdd(x.id, x.ins, x.rm, x.len, (mkMeta(mClient(x.meta), 0) & 0xFFu) | (static_cast<uint32_t>(c) << 8),
+             ldu(S.bGroup + b), b);
+    } else if (!was) {
+      st1(S.wRm + w, x.rm);
+      st1(S.wMeta + w, (ldu(S.wMeta + w) & 0xFFu) | (static_cast<uint32_t>(c) << 8));
+    } else {
+      st1(S.wMeta + w, ldu(S.wMeta + w) | (1u << 16));  // a later remover: full set from the leaf
+    }
+    corrValid = false;
+  }
+
+  FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId) {
+    const uint32_t np = applyProps(mProps(x.meta), opId);
+    if (status != FMT_OK) return;
+    x.meta = (x.meta & 0xFFu) | (np << 8);
+    putLeaf(b, j, x);
+  }
+
+  // ------------------------------------------------------------------ minSeq
+  // Window entries whose insert and first remove are both at/below minSeq graduate into the stable
+  // sums (mergeTree.ts:1147-1166 moves the window; their length is now the same for every view).
+  FMT_DEV void graduate() {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[4], t0_};
+    uint32_t w = 0;
+    while (w < nWin) {
+      const uint32_t base = w;
+      Lane<bool> q;
+      FOR_LANES(l) {
+        const uint32_t i = base + l;
+        bool g = false;
+        if (i < nWin) {
+          const int32_t rm = rd(S.wRm + i);
+          g = rd(S.wIns + i) <= minSeq && (rm == kNotRemoved || rm <= minSeq);
+        }
+        LANE(q) = g;
+      }
+      const uint64_t m = ballot(q);
+      if (!m) {
+        w += 64;
+        continue;
+      }
+      const uint32_t e = base + static_cast<uint32_t>(ctz64(m));
+      const int32_t rm = ldi(S.wRm + e);
+      const uint32_t len = ldu(S.wLen + e), blk = ldu(S.wBlk + e);
+      winRemove(e);  // the entry moved into e is examined next
+      if (rm == kNotRemoved) addStable(blk, static_cast<int>(len));
+      w = e;
+    }
+    corrValid = false;
+  }
+
+  // ------------------------------------------------------------------ zamboni (zamboni.ts:33-213)
+  // scourNode over leaf block b: drops leaves removed at/below minSeq, appends acked same-props
+  // appendable leaves onto the previous kept leaf (their text is copied to the merge area).
+  // Returns the new leaf count.
+  FMT_DEV int scourLeaves(uint32_t b) {
+    const int cnt = static_cast<int>(ldu(S.bCount + b));
+    Leaf kept[kMaxNodes];
+    int nk = 0;
+    int prev = -1;
+    uint32_t firstText[kMaxNodes];   // merge runs: text of each piece, appended at the end
+    int runStart[kMaxNodes], runLen[kMaxNodes];
+    for (int i = 0; i < kMaxNodes; i++) runLen[i] = 0;
+    uint32_t pieceText[kMaxNodes], pieceLen[kMaxNodes];
+    int pieceOwner[kMaxNodes];
+    int nPieces = 0;
+    for (int k = 0; k < cnt; k++) {
+      Leaf x = getLeaf(b, k);
+      if (x.rm == kNotRemoved) {
+        if (x.ins <= minSeq) {
+          bool canAppend = false;
+          if (prev >= 0 && x.len > 0) {
+            const Leaf& pv = kept[prev];
+            const uint32_t lastCh = pv.len > 0 ? textAt(pieceLast(prev, pieceText, pieceLen, pieceOwner, nPieces)) : 0u;
+            canAppend = lastCh != 10u && (pv.len <= static_cast<uint32_t>(kGranularity) || x.len <= static_cast<uint32_t>(kGranularity)) &&
+                        propsMatch(mProps(pv.meta), mProps(x.meta));
+          }
+          if (canAppend) {
+            kept[prev].len += x.len;
+            pieceText[nPieces] = x.text;
+            pieceLen[nPieces] = x.len;
+            pieceOwner[nPieces] = prev;
+            nPieces++;
+            runLen[prev]++;
+            st1(S.leafBlk + x.id, kNone);  // segment.parent = undefined (appended)
+          } else {
+            kept[nk] = x;
+            pieceText[nPieces] = x.text;
+            pieceLen[nPieces] = x.len;
+            pieceOwner[nPieces] = nk;
+            nPieces++;
+            runStart[nk] = k;
+            prev = x.len > 0 ? nk : -1;
+            nk++;
+          }
+        } else {
+          kept[nk] = x;
+          pieceText[nPieces] = x.text;
+          pieceLen[nPieces] = x.len;
+          pieceOwner[nPieces] = nk;
+          nPieces++;
+          nk++;
+          prev = -1;
+        }
+      } else {
+        if (x.rm <= minSeq) {
+          st1(S.leafBlk + x.id, kNone);  // unlinked
+          const uint32_t w = ldu(S.winIdx + x.id);
+          if (w != kNone) winRemove(w);  // (graduated already; kept for safety)
+        } else {
+          kept[nk] = x;
+          pieceText[nPieces] = x.text;
+          pieceLen[nPieces] = x.len;
+          pieceOwner[nPieces] = nk;
+          nPieces++;
+          nk++;
+        }
+        prev = -1;
+      }
+    }
+    (void)firstText;
+    (void)runStart;
+    if (nk == cnt) return cnt;  // nothing dropped or appended
+    // merged leaves get their text built once in the merge area
+    for (int q = 0; q < nk; q++) {
+      if (runLen[q] == 0) continue;
+      const uint32_t total = kept[q].len;
+      if (textTop + total > S.textCap) {
+        fail(FMT_E_CAPACITY);
+        return cnt;
+      }
+      const uint32_t dst = static_cast<uint32_t>(textTop);
+      uint32_t o = 0;
+      for (int pi = 0; pi < nPieces; pi++) {
+        if (pieceOwner[pi] != q) continue;
+        copyText(dst + o, pieceText[pi], pieceLen[pi]);
+        o += pieceLen[pi];
+      }
+      textTop += total;
+      kept[q].text = dst;
+    }
+    for (int q = 0; q < nk; q++) putLeaf(b, q, kept[q]);
+    st1(S.bCount + b, static_cast<uint32_t>(nk));
+    return nk;
+  }
+
+  FMT_DEV static int pieceLast(int owner, const uint32_t* pt, const uint32_t* pl, const int* po, int n) {
+    int last = -1;
+    for (int i = 0; i < n; i++)
+      if (po[i] == owner) last = i;
+    return static_cast<int>(pt[last] + pl[last] - 1);
+  }
+  FMT_DEV uint32_t textAt(int i) const { return loadCoherent(S.text + i); }
+  FMT_DEV void copyText(uint32_t dst, uint32_t src, uint32_t n) {
+    for (uint32_t base = 0; base < n; base += 64) {
+      Lane<uint32_t> v;
+      FOR_LANES(l) { LANE(v) = base + l < n ? loadCoherent(S.text + src + base + l) : 0u; }
+      waveSync();
+      FOR_LANES(l) {
+        if (base + l < n) S.text[dst + base + l] = static_cast<uint16_t>(LANE(v));
+      }
+      waveSync();
+    }
+  }
+
+  // packParent (zamboni.ts:83-139) at the leaf level: every child leaf block of p is scoured, the held
+  // leaves are redistributed into min(7, total / 4) (>= 1) blocks. The first of p's old blocks are
+  // reused for the new ones (block identity is not observable); the rest are freed and unlisted.
+  FMT_DEV void packLeafParent(uint32_t p) {
+    const int pc = static_cast<int>(ldu(S.bCount + p));
+    int total = 0;
+    for (int i = 0; i < pc; i++) total += scourLeaves(childAt(p, i));
+    if (status != FMT_OK) return;
+    // stage every held leaf (document order) in LDS tmp as (block, slot) pairs → gather records
+    constexpr int kMaxHeld = kMaxNodes * kMaxNodes;
+    uint32_t oldBlk[kMaxNodes];
+    for (int i = 0; i < pc; i++) oldBlk[i] = childAt(p, i);
+    Leaf held[kMaxHeld];
+    int n = 0;
+    for (int i = 0; i < pc; i++) {
+      const uint32_t b = oldBlk[i];
+      const int cnt = static_cast<int>(ldu(S.bCount + b));
+      for (int k = 0; k < cnt; k++) held[n++] = getLeaf(b, k);
+    }
+    const uint32_t g0 = ldu(S.bGroup + oldBlk[0]);
+    const int s0 = static_cast<int>(ldu(S.bSlot + oldBlk[0]));
+    int nb = 0;
+    if (total > 0) {
+      nb = total / (kMaxNodes / 2);
+      if (nb > kMaxNodes - 1) nb = kMaxNodes - 1;
+      if (nb < 1) nb = 1;
+    }
+    uint32_t newBlk[kMaxNodes];  // the first old blocks are reused, more are allocated when nb > pc
+    for (int q = 0; q < nb; q++) {
+      newBlk[q] = q < pc ? oldBlk[q] : allocBlk(1);
+      if (newBlk[q] == kNone) return;
+    }
+    // unlist the old blocks (they are consecutive slots, possibly across groups), then list the new
+    int removedStable = 0;
+    for (int i = 0; i < pc; i++) {
+      const uint32_t b = oldBlk[i];
+      const uint32_t g = ldu(S.bGroup + b);
+      const int s = static_cast<int>(ldu(S.bSlot + b));
+      removedStable += ldi(slotStPtr(g) + s);
+      slotRemove(g, s, 1);
+    }
+    (void)removedStable;
+    const int base = nb ? total / nb : 0;
+    int rem = nb ? total % nb : 0;
+    int consumed = 0;
+    uint32_t gIns = g0;
+    int sIns = s0;
+    if (sIns > static_cast<int>(L->gCount[gIns])) sIns = static_cast<int>(L->gCount[gIns]);
+    for (int q = 0; q < nb; q++) {
+      int cnt = base;
+      if (rem > 0) {
+        cnt++;
+        rem--;
+      }
+      const uint32_t b = newBlk[q];
+      st1(S.bLeaf + b, 1u);
+      for (int k = 0; k < cnt; k++) {
+        putLeaf(b, k, held[consumed + k]);
+        const uint32_t w = ldu(S.winIdx + held[consumed + k].id);
+        if (w != kNone) st1(S.wBlk + w, b);
+      }
+      st1(S.bCount + b, static_cast<uint32_t>(cnt));
+      st1(S.bParent + b, p);
+      st1(S.bScour + b, -1);
+      st1(S.bChild + static_cast<size_t>(p) * 8 + q, b);
+      consumed += cnt;
+      const int stB = blockStable(b);
+      if (!slotInsert(gIns, sIns, b, stB)) return;
+      gIns = ldu(S.bGroup + b);
+      sIns = static_cast<int>(ldu(S.bSlot + b)) + 1;
+    }
+    for (int q = 0; q < nb; q++) retagWindow(newBlk[q]);  // re-listed leaves: block and group
+    for (int i = nb; i < pc; i++) {
+      st1(S.bCount + oldBlk[i], 0u);
+      freeBlock(oldBlk[i]);
+    }
+    st1(S.bCount + p, static_cast<uint32_t>(nb));
+    if (nb == 0 && static_cast<int>(p) == root) fail(FMT_E_UNSUPPORTED);  // document emptied by zamboni
+    if (lastBlk != kNone) updateLastBlk();
+    corrValid = false;
+  }
+
+  FMT_DEV void updateLastBlk() {
+    lastBlk = kNone;
+    for (int k = nGroups - 1; k >= 0 && lastBlk == kNone; k--) {
+      const uint32_t g = L->gOrder[k];
+      const uint32_t cnt = L->gCount[g];
+      if (cnt > 0) lastBlk = ldu(slotBlkPtr(g) + cnt - 1);
+    }
+  }
+
+  // packParent above the leaf level: grandchildren blocks redistributed (no leaf moves).
+  FMT_DEV void packInterior(uint32_t p) {
+    const int pc = static_cast<int>(ldu(S.bCount + p));
+    uint32_t held[kMaxNodes * kMaxNodes];
+    uint32_t old[kMaxNodes];
+    int n = 0;
+    for (int i = 0; i < pc; i++) {
+      const uint32_t c = childAt(p, i);
+      old[i] = c;
+      const int cc = static_cast<int>(ldu(S.bCount + c));
+      for (int k = 0; k < cc; k++) held[n++] = childAt(c, k);
+    }
+    int nb = 0;
+    if (n > 0) {
+      nb = n / (kMaxNodes / 2);
+      if (nb > kMaxNodes - 1) nb = kMaxNodes - 1;
+      if (nb < 1) nb = 1;
+    }
+    const int base = nb ? n / nb : 0;
+    int rem = nb ? n % nb : 0;
+    int consumed = 0;
+    for (int q = 0; q < nb; q++) {
+      int cnt = base;
+      if (rem > 0) {
+        cnt++;
+        rem--;
+      }
+      const uint32_t b = q < pc ? old[q] : allocBlk(0);
+      if (b == kNone) return;
+      st1(S.bLeaf + b, 0u);
+      for (int k = 0; k < cnt; k++) setChild(b, k, held[consumed + k]);
+      st1(S.bCount + b, static_cast<uint32_t>(cnt));
+      st1(S.bScour + b, -1);
+      setChild(p, q, b);
+      consumed += cnt;
+    }
+    for (int i = nb; i < pc; i++) freeBlock(old[i]);
+    st1(S.bCount + p, static_cast<uint32_t>(nb));
+  }
+
+  FMT_DEV void zamboni() {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[3], t0_};
+    for (int i = 0; i < 2; i++) {
+      if (heapN == 0) break;
+      if (heapSeq(1) > minSeq) break;
+      const HeapEnt e = heapGet();
+      const uint32_t b = ldu(S.leafBlk + e.leafId);
+      if (b == kNone) continue;  // unlinked or appended
+      if (ldi(S.bScour + b) == 0) continue;
+      const int oldCount = static_cast<int>(ldu(S.bCount + b));
+      const int kept = scourLeaves(b);
+      if (status != FMT_OK) return;
+      st1(S.bScour + b, 0);
+      if (kept >= oldCount) continue;
+      const uint32_t parent = ldu(S.bParent + b);
+      if (kept >= kMaxNodes / 2 || parent == kNone) continue;
+      packLeafParent(parent);
+      if (status != FMT_OK) return;
+      uint32_t p = parent;
+      for (;;) {
+        const uint32_t pp = ldu(S.bParent + p);
+        if (ldu(S.bCount + p) >= static_cast<uint32_t>(kMaxNodes / 2) || pp == kNone) break;
+        p = pp;
+        packInterior(p);
+        if (status != FMT_OK) return;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ load (f3, header chunk only)
+  // reloadFromSegments (mergeTree.ts:751-800): 7 leaves per block, layer by layer; every loaded
+  // segment stamped {UniversalSequenceNumber, NonCollabClient} (snapshotLoader.ts:180-186).
+  // Blocks are numbered leaf level first; groups take kFill leaf blocks each.
+  FMT_DEV void load() {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[5], t0_};
+    const uint32_t N = in.nSegs;
+    const uint32_t nLeafBlk = (N + 6) / 7;
+    if (N == 0 || nLeafBlk > S.blockCap || N + 1 > S.idCap) {
+      fail(N == 0 ? FMT_E_UNSUPPORTED : FMT_E_CAPACITY);
+      return;
+    }
+    for (uint32_t base = 0; base < N; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t j = base + l;
+        if (j < N) {
+          const uint32_t b = j / 7, k = j % 7;
+          const size_t i = static_cast<size_t>(b) * 8 + k;
+          const fmt_mt_snapshot_seg sg = in.segs[j];
+          S.lLen[i] = sg.len;
+          S.lIns[i] = 0;
+          S.lRm[i] = kNotRemoved;
+          S.lMlo[i] = 0;
+          S.lMhi[i] = 0;
+          S.lId[i] = j + 1;
+          S.lText[i] = sg.text;
+          S.lMeta[i] = mkMeta(FMT_NON_COLLAB_CLIENT, kNoProps);
+          S.leafBlk[j + 1] = b;
+          S.winIdx[j + 1] = kNone;
+        }
+      }
+    }
+    nextId = N + 1;
+    // leaf blocks: count, parent later; stable sums; group lists
+    uint32_t cntL = nLeafBlk;
+    nGroups = static_cast<int>((nLeafBlk + kFill - 1) / kFill);
+    if (nGroups > kGroupCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    for (uint32_t base = 0; base < nLeafBlk; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t b = base + l;
+        if (b < nLeafBlk) {
+          const uint32_t c = (N - 7 * b) < 7 ? N - 7 * b : 7;
+          S.bCount[b] = c;
+          S.bLeaf[b] = 1;
+          S.bScour[b] = -1;
+          S.bParent[b] = kNone;
+          int st = 0;
+          for (uint32_t k = 0; k < c; k++) st += static_cast<int>(rd(S.lLen + (static_cast<size_t>(b) * 8 + k)));
+          const uint32_t g = b / kFill, s = b % kFill;
+          S.bGroup[b] = g;
+          S.bSlot[b] = s;
+          S.gSlotBlk[static_cast<size_t>(g) * kSlotCap + s] = b;
+          S.gSlotStable[static_cast<size_t>(g) * kSlotCap + s] = st;
+        }
+      }
+    }
+    waveSync();
+    for (int g = 0; g < nGroups; g++) {
+      const uint32_t lo = static_cast<uint32_t>(g) * kFill, hi = lo + kFill < nLeafBlk ? lo + kFill : nLeafBlk;
+      Lane<uint32_t> acc;
+      FOR_LANES(l) { LANE(acc) = 0; }
+      for (uint32_t base = lo; base < hi; base += 64) {
+        FOR_LANES(l) {
+          if (base + l < hi) LANE(acc) += static_cast<uint32_t>(rd(S.gSlotStable + (static_cast<size_t>(g) * kSlotCap + (base + l - lo))));
+        }
+      }
+      uint32_t tot;
+      waveExclusiveSum(acc, &tot);
+      L->gOrder[g] = static_cast<uint16_t>(g);
+      L->gStable[g] = static_cast<int32_t>(tot);
+      L->gCount[g] = hi - lo;
+      L->gCorr[g] = 0;
+      waveSync();
+    }
+    // interior levels, 7 children per block
+    uint32_t lo = 0, next = nLeafBlk;
+    while (cntL > 1) {
+      const uint32_t nb = (cntL + 6) / 7;
+      if (next + nb > S.blockCap) {
+        fail(FMT_E_CAPACITY);
+        return;
+      }
+      for (uint32_t base = 0; base < nb; base += 64) {
+        FOR_LANES(l) {
+          const uint32_t q = base + l;
+          if (q < nb) {
+            const uint32_t id = next + q;
+            const uint32_t c = cntL - 7 * q < 7 ? cntL - 7 * q : 7;
+            S.bCount[id] = c;
+            S.bLeaf[id] = 0;
+            S.bScour[id] = -1;
+            S.bParent[id] = kNone;
+            for (uint32_t k = 0; k < c; k++) {
+              S.bChild[static_cast<size_t>(id) * 8 + k] = lo + 7 * q + k;
+              S.bParent[lo + 7 * q + k] = id;
+            }
+          }
+        }
+      }
+      waveSync();
+      lo = next;
+      next += nb;
+      cntL = nb;
+    }
+    root = static_cast<int>(lo);
+    nextBlock = next;
+    lastBlk = nLeafBlk - 1;
+    minSeq = in.snapMinSeq;
+    curSeq = in.snapSeq;
+  }
+
+  // ------------------------------------------------------------------ driver
+  FMT_DEV Lane<uint32_t> fetchOp(uint64_t i) const {
+    Lane<uint32_t> x;
+    if (i < in.end) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(in.ops + i);
+      FOR_LANES(l) { LANE(x) = l < 8 ? p[l] : 0u; }
+    } else {
+      FOR_LANES(l) { LANE(x) = 0u; }
+    }
+    return x;
+  }
+  FMT_DEV static fmt_mt_op decodeOp(const Lane<uint32_t>& rec) {
+    fmt_mt_op op;
+    op.seq = static_cast<int32_t>(readlane(rec, 0));
+    op.ref_seq = static_cast<int32_t>(readlane(rec, 1));
+    op.min_seq = static_cast<int32_t>(readlane(rec, 2));
+    op.pos1 = static_cast<int32_t>(readlane(rec, 3));
+    op.pos2 = static_cast<int32_t>(readlane(rec, 4));
+    op.payload = readlane(rec, 5);
+    const uint32_t lct = readlane(rec, 6);
+    op.len = static_cast<uint16_t>(lct & 0xFFFF);
+    op.client = static_cast<uint8_t>((lct >> 16) & 0xFF);
+    op.type = static_cast<uint8_t>(lct >> 24);
+    op.flags = readlane(rec, 7);
+    return op;
+  }
+
+  FMT_DEV void replay() {
+    const uint64_t t0_ = clk();
+    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[0], t0_};
+    Lane<uint32_t> rec0 = fetchOp(in.begin), rec1 = fetchOp(in.begin + 1);
+    for (uint64_t i = in.begin; i < in.end; i++) {
+      const fmt_mt_op op = decodeOp(rec0);
+      rec0 = rec1;
+      rec1 = fetchOp(i + 2);
+      corrValid = false;
+#ifdef FMT_HUGE_CHECK
+      checkPerspective(op.seq, op.ref_seq, op.client);
+#endif
+      if (op.client > 63) fail(FMT_E_UNSUPPORTED);
+      else if (op.type == FMT_MT_INSERT) insertText(op);
+      else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
+        if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
+        else applyRange(op);
+      } else {
+        fail(FMT_E_UNSUPPORTED);  // obliterate: the small / large tiers only
+      }
+      if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER)) != 0) fail(FMT_E_UNSUPPORTED);
+      const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
+      for (int z = 0; z < 2 && status == FMT_OK; z++) {
+        if (z == 1) {
+          if (!lastMember) break;
+          if (curSeq > op.seq || op.min_seq > op.seq || minSeq > op.min_seq) {
+            fail(FMT_E_DATA);
+            break;
+          }
+          curSeq = op.seq;
+          if (op.min_seq <= minSeq) break;
+          minSeq = op.min_seq;
+          graduate();
+        }
+        zamboni();
+      }
+#ifdef FMT_HUGE_CHECK
+      if (status == FMT_OK) checkInvariants(op.seq);
+#endif
+      if (status != FMT_OK) {
+        failSeq = op.seq;
+        break;
+      }
+    }
+  }
+
+#ifdef FMT_HUGE_CHECK
+  // Host emulation only: the perspective lengths of groups and slots equal the leaves' sums.
+  void checkPerspective(int seq, int r, int c) {
+    groupCorrections(r, c);
+    for (int k = 0; k < nGroups; k++) {
+      const uint32_t g = L->gOrder[k];
+      long brute = 0;
+      slotLengths(g, r, c);
+      for (uint32_t s = 0; s < L->gCount[g]; s++) {
+        const uint32_t b = S.gSlotBlk[static_cast<size_t>(g) * kSlotCap + s];
+        long bl = 0;
+        for (uint32_t j = 0; j < S.bCount[b]; j++) {
+          const size_t i = li(b, static_cast<int>(j));
+          bl += visOf(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c);
+        }
+        if (bl != L->sLen[s]) {
+          std::fprintf(stderr, "seq %d: slot %u of group %u (block %u) view %ld, index %d (stable %d) r=%d c=%d minSeq=%d\n", seq, s, g, b, bl,
+                       L->sLen[s], S.gSlotStable[static_cast<size_t>(g) * kSlotCap + s], r, c, minSeq);
+          for (uint32_t j = 0; j < S.bCount[b]; j++) {
+            const size_t i = li(b, static_cast<int>(j));
+            const uint32_t w = S.winIdx[S.lId[i]];
+            std::fprintf(stderr, "  leaf id %u len %u ins %d rm %d mask %x:%x ic %d vis %d win %d", S.lId[i], S.lLen[i], S.lIns[i], S.lRm[i],
+                         S.lMhi[i], S.lMlo[i], mClient(S.lMeta[i]),
+                         visOf(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c), w == kNone ? -1 : (int)w);
+            if (w != kNone) std::fprintf(stderr, " | w ins %d rm %d len %u meta %x grp %u blk %u", S.wIns[w], S.wRm[w], S.wLen[w], S.wMeta[w], S.wGroup[w], S.wBlk[w]);
+            std::fprintf(stderr, "\n");
+          }
+          fail(FMT_E_DATA);
+          return;
+        }
+        brute += bl;
+      }
+      if (brute != L->gStable[g] + L->gCorr[g]) {
+        std::fprintf(stderr, "seq %d: group %u view %ld, index %d + %d\n", seq, g, brute, L->gStable[g], L->gCorr[g]);
+        fail(FMT_E_DATA);
+        return;
+      }
+    }
+    corrValid = false;
+  }
+
+  // Host emulation only (tests/emu/huge_emu.cpp): every index structure agrees with the leaves.
+  void checkInvariants(int seq) {
+    auto bad = [&](const char* what, long a, long b) {
+      std::fprintf(stderr, "seq %d: %s (%ld vs %ld)\n", seq, what, a, b);
+      fail(FMT_E_DATA);
+    };
+    long nw = 0;
+    for (int k = 0; k < nGroups; k++) {
+      const uint32_t g = L->gOrder[k];
+      long sum = 0;
+      for (uint32_t s = 0; s < L->gCount[g]; s++) {
+        const uint32_t b = S.gSlotBlk[static_cast<size_t>(g) * kSlotCap + s];
+        if (S.bGroup[b] != g || S.bSlot[b] != s) return bad("block group/slot", b, s);
+        long st = 0;
+        for (uint32_t j = 0; j < S.bCount[b]; j++) {
+          const size_t i = li(b, static_cast<int>(j));
+          const uint32_t id = S.lId[i];
+          if (S.leafBlk[id] != b) return bad("leafBlk", id, b);
+          const bool shouldWin = S.lIns[i] > minSeq || (S.lRm[i] != kNotRemoved && S.lRm[i] > minSeq);
+          const uint32_t w = S.winIdx[id];
+          if (shouldWin != (w != kNone)) return bad("window membership", id, shouldWin);
+          if (w != kNone) {
+            nw++;
+            if (S.wLeaf[w] != id || S.wBlk[w] != b || S.wGroup[w] != g || S.wLen[w] != S.lLen[i] || S.wIns[w] != S.lIns[i] ||
+                S.wRm[w] != S.lRm[i])
+              return bad("window entry", id, w);
+          } else if (S.lRm[i] == kNotRemoved) {
+            st += S.lLen[i];
+          }
+        }
+        if (st != S.gSlotStable[static_cast<size_t>(g) * kSlotCap + s]) return bad("slot stable", st, S.gSlotStable[static_cast<size_t>(g) * kSlotCap + s]);
+        sum += st;
+      }
+      if (sum != L->gStable[g]) return bad("group stable", sum, L->gStable[g]);
+    }
+    if (nw != static_cast<long>(nWin)) bad("window count", nw, nWin);
+  }
+#endif
+
+  // Converged state in document order: fmt_mt_leaf records (block = leaf-block ordinal, low 16 bits,
+  // pad = high 16 bits), the text of every leaf (tombstones included), the prop sets, the header.
+  // Eight leaf blocks per wave step: lane l handles slot l % 8 of block l / 8.
+  FMT_DEV void writeOutputs(fmt_mt_doc_result* hdr, fmt_mt_leaf* outLeaves, uint64_t capLeaves, uint16_t* outChars,
+                            uint64_t capChars, fmt_mt_propset* outProps) {
+    uint64_t nLeaves = 0, nChars = 0, visible = 0;
+    uint32_t nBlocks = 0;
+    for (int k = 0; k < nGroups && status == FMT_OK; k++) {
+      const uint32_t g = L->gOrder[k];
+      const int cnt = static_cast<int>(L->gCount[g]);
+      const uint32_t* sb = slotBlkPtr(g);
+      for (int s0 = 0; s0 < cnt; s0 += 8) {
+        Lane<uint32_t> valid, len, vlen, blockStart;
+        Lane<size_t> idx;
+        FOR_LANES(l) {
+          const int s = s0 + l / 8, j = l % 8;
+          uint32_t v = 0, ln = 0, vl = 0, bs = 0;
+          size_t i = 0;
+          if (s < cnt) {
+            const uint32_t b = rd(sb + s);
+            const uint32_t bc = rd(S.bCount + b);
+            bs = (j == 0 && bc > 0) ? 1u : 0u;
+            if (j < static_cast<int>(bc)) {
+              i = li(b, j);
+              v = 1;
+              ln = rd(S.lLen + i);
+              vl = rd(S.lRm + i) == kNotRemoved ? ln : 0u;
+            }
+          }
+          LANE(valid) = v;
+          LANE(len) = ln;
+          LANE(vlen) = vl;
+          LANE(blockStart) = bs;
+          LANE(idx) = i;
+        }
+        uint32_t tv, tl, tvl, tb;
+        const Lane<uint32_t> ev = waveExclusiveSum(valid, &tv);
+        const Lane<uint32_t> el = waveExclusiveSum(len, &tl);
+        const Lane<uint32_t> eb = waveExclusiveSum(blockStart, &tb);
+        waveExclusiveSum(vlen, &tvl);
+        if (nLeaves + tv > capLeaves || nChars + tl > capChars) {
+          fail(FMT_E_CAPACITY);
+          break;
+        }
+        FOR_LANES(l) {
+          if (LANE(valid)) {
+            const size_t i = LANE(idx);
+            const uint64_t o = nLeaves + LANE(ev);
+            const uint64_t co = nChars + LANE(el);
+            const uint32_t blk = nBlocks + LANE(eb) - ((l % 8) != 0 ? 1u : 0u);  // this block's ordinal
+            fmt_mt_leaf x;
+            x.ins_seq = rd(S.lIns + i);
+            x.rm_seq = rd(S.lRm + i);
+            x.rm_clients = static_cast<uint64_t>(rd(S.lMlo + i)) | (static_cast<uint64_t>(rd(S.lMhi + i)) << 32);
+            x.char_off = static_cast<uint32_t>(co);
+            x.len = LANE(len);
+            const uint32_t m = rd(S.lMeta + i);
+            x.ins_client = static_cast<int16_t>(mClient(m));
+            x.props = static_cast<uint16_t>(mProps(m));
+            x.block = static_cast<uint16_t>(blk & 0xFFFFu);
+            x.pad = static_cast<uint16_t>(blk >> 16);
+            outLeaves[o] = x;
+            const uint32_t t = rd(S.lText + i);
+            for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(loadCoherent(S.text + t + c));
+          }
+        }
+        nLeaves += tv;
+        nChars += tl;
+        visible += tvl;
+        nBlocks += tb;
+      }
+    }
+    FOR_LANES(l) {
+      for (int p = l; p < nProps; p += 64) {
+        fmt_mt_propset ps;
+        ps.n = rd(S.props + p * 5);
+        for (int k = 0; k < FMT_MT_PROPS_MAX; k++) ps.kv[k] = rd(S.props + p * 5 + 1 + k);
+        outProps[p] = ps;
+      }
+    }
+    const int d = status == FMT_OK ? depth() : 0;
+    FOR_LANES(l) {
+      if (l == 0) {
+        fmt_mt_doc_result h;
+        h.status = status;
+        h.fail_seq = failSeq;
+        h.cur_seq = curSeq;
+        h.min_seq = minSeq;
+        h.n_leaves = static_cast<uint32_t>(nLeaves);
+        h.n_chars = static_cast<uint32_t>(nChars);
+        h.n_props = static_cast<uint32_t>(nProps);
+        h.n_blocks = nBlocks;
+        h.depth = static_cast<uint32_t>(d);
+        h.visible_len = static_cast<uint32_t>(visible);
+        h.n_catchup = 0;
+        h.n_rm_order = 0;
+        *hdr = h;
+      }
+    }
+  }
+
+  FMT_DEV int depth() const {
+    int d = 1;
+    for (uint32_t b = static_cast<uint32_t>(root); ldu(S.bLeaf + b) == 0 && ldu(S.bCount + b) > 0; b = childAt(b, 0)) d++;
+    return d;
+  }
+
+  FMT_DEV void run(const HugeInputs& inputs) {
+    in = inputs;
+    heapN = 0;
+    nWin = 0;
+    nFree = 0;
+    nProps = 0;
+    textTop = S.textLen;
+    status = FMT_OK;
+    load();
+    if (status == FMT_OK) replay();
+  }
+};
+
+}  // namespace fmt_huge

@@ -1,0 +1,42 @@
+// hugedoc.hip — replay of very large documents (BASELINE config 5, T3) for gfx950: one wavefront per
+// document, its state in HBM (huge_engine.h), its LRU heap and group directory in LDS.
+//
+// A single document's ops form one dependency chain, so a document is replayed by one wave and
+// several huge documents run side by side (one per workgroup / CU). What bounds a step is the latency
+// of the dependent HBM/L2 round trips of one op (window pass, group scan, a slot list, one leaf
+// block, the block/heap updates), not bandwidth.
+#include <hip/hip_runtime.h>
+
+#include "huge_engine.h"
+#include "kernels.h"
+
+namespace fmt_kernels {
+
+__global__ __launch_bounds__(64) void hugeDocKernel(const fmt_huge::HugeState* __restrict__ states,
+                                                    const fmt_huge::HugeInputs* __restrict__ inputs,
+                                                    const HugeOut* __restrict__ outs, uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+    fmt_huge::HugeDoc doc;
+    doc.S = states[i];
+    doc.L = reinterpret_cast<fmt_huge::HugeLds*>(lds);
+    doc.run(inputs[i]);
+    const HugeOut o = outs[i];
+    const uint64_t t0 = fmt_huge::HugeDoc::clk();
+    doc.writeOutputs(o.header, o.leaves, o.capLeaves, o.chars, o.capChars, o.props);
+    doc.prof[6] += fmt_huge::HugeDoc::clk() - t0;
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < 8; k++) o.prof[k] = doc.prof[k];
+  }
+}
+
+size_t hugeLdsBytes() { return sizeof(fmt_huge::HugeLds); }
+
+hipError_t launchHugeDocs(const fmt_huge::HugeState* states, const fmt_huge::HugeInputs* inputs, const HugeOut* outs,
+                          uint32_t count, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(hugeDocKernel, dim3(count), dim3(64), sizeof(fmt_huge::HugeLds), stream, states, inputs, outs, count);
+  return hipGetLastError();
+}
+
+}  // namespace fmt_kernels

@@ -60,3 +60,26 @@ hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& o
 int mergeTreeProfile(uint64_t* out, int n, bool reset);
 
 }  // namespace fmt_kernels
+
+// ---- huge documents (hugedoc.hip, huge_engine.h): one wave per document, state in HBM
+namespace fmt_huge {
+struct HugeState;
+struct HugeInputs;
+}  // namespace fmt_huge
+
+namespace fmt_kernels {
+
+struct HugeOut {
+  fmt_mt_doc_result* header;
+  fmt_mt_leaf* leaves;
+  uint64_t capLeaves;
+  uint16_t* chars;
+  uint64_t capChars;
+  fmt_mt_propset* props;
+  unsigned long long* prof;  // [8] shader-clock totals per phase (huge_engine.h HugeDoc::prof)
+};
+size_t hugeLdsBytes();
+hipError_t launchHugeDocs(const fmt_huge::HugeState* states, const fmt_huge::HugeInputs* inputs, const HugeOut* outs,
+                          uint32_t count, hipStream_t stream);
+
+}  // namespace fmt_kernels

@@ -112,8 +112,10 @@ MtCaps mergeTreeCaps(bool large) {
 // A limit the large tier shares (fmt_mt::kCapacityFinal) is reported as FMT_E_CAPACITY without
 // escalation.
 __global__ __launch_bounds__(256) void collectOverflowKernel(fmt_mt_doc_result* __restrict__ headers,
-                                                             uint32_t nDocs, uint32_t* esc) {
-  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < nDocs; d += gridDim.x * blockDim.x) {
+                                                             const uint32_t* __restrict__ docList, uint32_t nDocs,
+                                                             uint32_t* esc) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nDocs; i += gridDim.x * blockDim.x) {
+    const uint32_t d = docList ? docList[i] : i;
     const int st = headers[d].status;
     if (st == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;
     if (st == FMT_E_CAPACITY) {
@@ -138,10 +140,10 @@ static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out,
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
   hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
                      docList, count);
-  if (esc != nullptr) {
-    const uint32_t g = (batch.nDocs + 255) / 256;
+  if (esc != nullptr) {  // over the documents this launch replayed
+    const uint32_t g = (count + 255) / 256;
     hipLaunchKernelGGL(collectOverflowKernel, dim3(g < 1024 ? (g > 0 ? g : 1) : 1024), dim3(256), 0, stream, out.headers,
-                       batch.nDocs, esc);
+                       docList, count, esc);
   }
   return hipGetLastError();
 }

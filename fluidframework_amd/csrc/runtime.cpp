@@ -5,6 +5,7 @@
 // caller can time run() alone ("inputs already resident in HBM"). No exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <exception>
@@ -12,6 +13,7 @@
 #include <vector>
 
 #include "../../include/fmt.h"
+#include "huge_engine.h"
 #include "kernels.h"
 
 namespace {
@@ -87,6 +89,20 @@ struct fmt_ctx {
   DevBuf<fmt_mt_remove_order> mtRmOrder;     // remove-order slabs (FMT_MT_F_RMORDER ops)
   std::vector<uint64_t> mtRmOffsHost;
   bool mtHasRmOrder = false;
+  // huge documents (T3, huge_engine.h): one wave each, state in per-document HBM buffers
+  struct HugeDocBufs {
+    std::vector<void*> allocs;
+    fmt_huge::HugeState state{};
+    fmt_huge::HugeInputs in{};
+    fmt_kernels::HugeOut out{};
+  };
+  std::vector<HugeDocBufs> huge;             // per huge document
+  std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
+  DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
+  uint32_t mtNSmall = 0;
+  DevBuf<fmt_huge::HugeState> hugeStates;
+  DevBuf<fmt_huge::HugeInputs> hugeInputs;
+  DevBuf<fmt_kernels::HugeOut> hugeOuts;
   uint64_t mtNOps = 0, mtTextLen = 0, mtInsertChars = 0, mtInitChars = 0;
   uint32_t mtDocs = 0, mtNProps = 0;
   bool mtHasInit = false, mtLoaded = false;
@@ -173,6 +189,13 @@ void fmt_close(fmt_ctx* c) {
   c->mtCatchup.release();
   c->mtRmOffs.release();
   c->mtRmOrder.release();
+  for (auto& h : c->huge)
+    for (void* p : h.allocs) (void)hipFree(p);
+  c->huge.clear();
+  c->mtSmallList.release();
+  c->hugeStates.release();
+  c->hugeInputs.release();
+  c->hugeOuts.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -449,6 +472,112 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtObliterate = obliterates;
   c->mtInsertChars = insertChars;
   c->mtInitChars = initChars;
+  // Huge documents: a summary-loaded document with more segments or text than the large tier holds
+  // is replayed by the huge-document engine (huge_engine.h: one wave, state in HBM). It loads from
+  // one header chunk; catch-up / remove-order recording and obliterates stay with the other tiers.
+  for (auto& h : c->huge)
+    for (void* p : h.allocs) (void)hipFree(p);
+  c->huge.clear();
+  c->mtHugeSlot.assign(n, -1);
+  if (b->snapshots) {
+    const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true);
+    for (uint32_t d = 0; d < n; d++) {
+      const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+      if (!sd.loaded) continue;
+      uint64_t chars = 0;
+      for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++) chars += b->snapshot_segs[k].len;
+      if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
+      if (sd.n_body != 0)
+        return setErr(c, FMT_E_UNSUPPORTED, "a document beyond the large tier must load from one header chunk (n_body = 0)");
+      const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1], nOps = o1 - o0;
+      for (uint64_t i = o0; i < o1; i++)
+        if (b->ops[i].flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER))
+          return setErr(c, FMT_E_UNSUPPORTED, "catch-up / remove-order recording in a document beyond the large tier");
+      c->mtHugeSlot[d] = static_cast<int32_t>(c->huge.size());
+      c->huge.emplace_back();
+      auto& H = c->huge.back();
+      auto alloc = [&](size_t bytes, void** out) -> hipError_t {
+        hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+        if (e == hipSuccess) H.allocs.push_back(*out);
+        return e;
+      };
+      const uint64_t N = sd.n_header;
+      fmt_huge::HugeState& S = H.state;
+      S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
+      S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
+      S.winCap = static_cast<uint32_t>(3 * nOps + 1024);
+      const uint64_t textCap = std::min<uint64_t>(b->text_len + 256 * nOps + 65536, 0xFFFFFFF0ull);
+      const size_t nl = static_cast<size_t>(S.blockCap) * 8, nb = S.blockCap;
+      void* p;
+#define FMT_ALLOC(field, T, count)                        \
+  FMT_HIP(c, alloc((count) * sizeof(T), &p));              \
+  S.field = static_cast<T*>(p);
+      FMT_ALLOC(lLen, uint32_t, nl) FMT_ALLOC(lIns, int32_t, nl) FMT_ALLOC(lRm, int32_t, nl)
+      FMT_ALLOC(lMlo, uint32_t, nl) FMT_ALLOC(lMhi, uint32_t, nl) FMT_ALLOC(lId, uint32_t, nl)
+      FMT_ALLOC(lText, uint32_t, nl) FMT_ALLOC(lMeta, uint32_t, nl)
+      FMT_ALLOC(bCount, uint32_t, nb) FMT_ALLOC(bParent, uint32_t, nb) FMT_ALLOC(bLeaf, uint32_t, nb)
+      FMT_ALLOC(bScour, int32_t, nb) FMT_ALLOC(bChild, uint32_t, nb * 8) FMT_ALLOC(bGroup, uint32_t, nb)
+      FMT_ALLOC(bSlot, uint32_t, nb) FMT_ALLOC(freeBlk, uint32_t, nb)
+      FMT_ALLOC(gSlotBlk, uint32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
+      FMT_ALLOC(gSlotStable, int32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
+      FMT_ALLOC(leafBlk, uint32_t, S.idCap) FMT_ALLOC(winIdx, uint32_t, S.idCap)
+      FMT_ALLOC(wIns, int32_t, S.winCap) FMT_ALLOC(wRm, int32_t, S.winCap) FMT_ALLOC(wLen, uint32_t, S.winCap)
+      FMT_ALLOC(wMeta, uint32_t, S.winCap) FMT_ALLOC(wGroup, uint32_t, S.winCap) FMT_ALLOC(wBlk, uint32_t, S.winCap)
+      FMT_ALLOC(wLeaf, uint32_t, S.winCap)
+      FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * 5)
+#undef FMT_ALLOC
+      S.textLen = b->text_len;
+      S.textCap = textCap;
+      FMT_HIP(c, hipMemcpyAsync(S.text, b->text, b->text_len * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+      fmt_huge::HugeInputs& I = H.in;
+      I.ops = c->mtOps.p;
+      I.begin = o0;
+      I.end = o1;
+      I.propsOff = c->mtPropsOff.p;
+      I.propsKv = c->mtPropsKv.p;
+      I.nPropsOps = b->n_props_ops;
+      I.segs = c->mtSnapSegs.p + sd.first_seg;
+      I.nSegs = static_cast<uint32_t>(N);
+      I.snapMinSeq = sd.min_seq;
+      I.snapSeq = sd.seq;
+      fmt_kernels::HugeOut& O = H.out;
+      O.header = c->mtHdr.p + d;
+      O.capLeaves = N + 3 * nOps + 8;
+      O.capChars = b->text_len + 8;
+      FMT_HIP(c, alloc(O.capLeaves * sizeof(fmt_mt_leaf), &p));
+      O.leaves = static_cast<fmt_mt_leaf*>(p);
+      FMT_HIP(c, alloc(O.capChars * sizeof(uint16_t), &p));
+      O.chars = static_cast<uint16_t*>(p);
+      FMT_HIP(c, alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p));
+      O.props = static_cast<fmt_mt_propset*>(p);
+      FMT_HIP(c, alloc(8 * sizeof(unsigned long long), &p));
+      O.prof = static_cast<unsigned long long*>(p);
+    }
+  }
+  if (!c->huge.empty()) {
+    const size_t nh = c->huge.size();
+    std::vector<uint32_t> small;
+    for (uint32_t d = 0; d < n; d++)
+      if (c->mtHugeSlot[d] < 0) small.push_back(d);
+    c->mtNSmall = static_cast<uint32_t>(small.size());
+    FMT_HIP(c, c->mtSmallList.reserve(small.size()));
+    FMT_HIP(c, c->hugeStates.reserve(nh));
+    FMT_HIP(c, c->hugeInputs.reserve(nh));
+    FMT_HIP(c, c->hugeOuts.reserve(nh));
+    std::vector<fmt_huge::HugeState> hs(nh);
+    std::vector<fmt_huge::HugeInputs> hi(nh);
+    std::vector<fmt_kernels::HugeOut> ho(nh);
+    for (size_t i = 0; i < nh; i++) {
+      hs[i] = c->huge[i].state;
+      hi[i] = c->huge[i].in;
+      ho[i] = c->huge[i].out;
+    }
+    FMT_HIP(c, cp(c->mtSmallList.p, small.data(), small.size() * sizeof(uint32_t)));
+    FMT_HIP(c, cp(c->hugeStates.p, hs.data(), nh * sizeof(fmt_huge::HugeState)));
+    FMT_HIP(c, cp(c->hugeInputs.p, hi.data(), nh * sizeof(fmt_huge::HugeInputs)));
+    FMT_HIP(c, cp(c->hugeOuts.p, ho.data(), nh * sizeof(fmt_kernels::HugeOut)));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));
+  }
   c->mtLoaded = true;
   return FMT_OK;
 }
@@ -465,8 +594,13 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
-  FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, nullptr, c->mtDocs, c->mtEsc.p, c->numCUs, c->stream,
-                                          c->mtObliterate, c->mtHasRmOrder));
+  const bool hasHuge = !c->huge.empty();
+  if (!hasHuge || c->mtNSmall > 0)
+    FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
+                                            c->mtEsc.p, c->numCUs, c->stream, c->mtObliterate, c->mtHasRmOrder));
+  if (hasHuge)
+    FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p,
+                                           static_cast<uint32_t>(c->huge.size()), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));  // device time excludes the host read-back below
   c->timed2 = false;
   // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
@@ -526,6 +660,19 @@ int fmt_mt_fetch_headers(fmt_ctx* c, fmt_mt_doc_result* out) {
 int fmt_mt_fetch_doc(fmt_ctx* c, uint32_t doc, fmt_mt_leaf* leaves, uint32_t capLeaves, uint16_t* chars,
                      uint32_t capChars, fmt_mt_propset* props, uint32_t capProps) {
   if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs) return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_doc: bad doc");
+  const int32_t hslot = doc < c->mtHugeSlot.size() ? c->mtHugeSlot[doc] : -1;
+  if (hslot >= 0) {  // a huge document: its own output buffers
+    const fmt_kernels::HugeOut& O = c->huge[static_cast<size_t>(hslot)].out;
+    fmt_mt_doc_result h;
+    FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
+    const uint32_t nl = h.n_leaves < capLeaves ? h.n_leaves : capLeaves;
+    const uint32_t nc = h.n_chars < capChars ? h.n_chars : capChars;
+    const uint32_t np = h.n_props < capProps ? h.n_props : capProps;
+    if (leaves && nl) FMT_HIP(c, hipMemcpy(leaves, O.leaves, nl * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
+    if (chars && nc) FMT_HIP(c, hipMemcpy(chars, O.chars, nc * 2ull, hipMemcpyDeviceToHost));
+    if (props && np) FMT_HIP(c, hipMemcpy(props, O.props, np * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost));
+    return FMT_OK;
+  }
   const int32_t slot = doc < c->mtBigSlot.size() ? c->mtBigSlot[doc] : -1;
   const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(slot >= 0);
   const size_t at = slot >= 0 ? static_cast<size_t>(slot) : doc;
@@ -562,6 +709,15 @@ int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
   const uint32_t m = h.n_rm_order < cap ? h.n_rm_order : cap;
   if (m) FMT_HIP(c, hipMemcpy(out, c->mtRmOrder.p + c->mtRmOffsHost[doc], m * sizeof(fmt_mt_remove_order), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+// Internal diagnostic (not part of fmt.h): shader-clock totals per phase of a huge document's last
+// replay (huge_engine.h HugeDoc::prof), 8 values; FMT_E_USAGE if `doc` is not a huge document.
+int fmt_internal_huge_profile(fmt_ctx* c, uint32_t doc, uint64_t* out) {
+  if (c == nullptr || out == nullptr || doc >= c->mtHugeSlot.size() || c->mtHugeSlot[doc] < 0) return FMT_E_USAGE;
+  FMT_HIP(c, hipMemcpy(out, c->huge[static_cast<size_t>(c->mtHugeSlot[doc])].out.prof, 8 * sizeof(uint64_t),
+                       hipMemcpyDeviceToHost));
   return FMT_OK;
 }
 

@@ -55,6 +55,11 @@ FMT_DEV uint32_t loadCoherent(const uint16_t* p) {
 FMT_DEV uint32_t loadCoherent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+FMT_DEV int32_t loadCoherent(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// LDS add from one lane of many (ds_add_u32); the host emulation runs lanes one after another.
+FMT_DEV void atomicAddLds(int32_t* p, int v) { atomicAdd(p, v); }
 
 // Make a wave-uniform value provably uniform (lives in an SGPR afterwards).
 FMT_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -204,6 +209,8 @@ inline void launder(V8&) {}
 
 inline uint32_t loadCoherent(const uint16_t* p) { return *p; }
 inline uint32_t loadCoherent(const uint32_t* p) { return *p; }
+inline int32_t loadCoherent(const int32_t* p) { return *p; }
+inline void atomicAddLds(int32_t* p, int v) { *p += v; }
 
 inline uint64_t ballot(const Lane<bool>& p) {
   uint64_t m = 0;

@@ -282,6 +282,16 @@ class Engine:
         self._check(self.L.fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
         return leaves[:nl], chars[:nc], props[:npp]
 
+    def huge_profile(self, doc: int):
+        """Diagnostics: shader-clock totals per phase of a huge document's last replay
+        (replay, window pass groups, window pass slots, zamboni, graduation, load, output, finds)."""
+        out = np.zeros(8, dtype=np.uint64)
+        f = self.L.fmt_internal_huge_profile
+        f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        self._check(f(self.h, doc, _ptr(out)))
+        names = ["replay", "window_groups", "window_slots", "zamboni", "graduate", "load", "output", "find"]
+        return dict(zip(names, (int(x) for x in out)))
+
     def mt_remove_order(self, doc: int, hdr=None) -> np.ndarray:
         """The document's remove-order entries (fmt_mt_remove_order) of its FMT_MT_F_RMORDER ops."""
         if hdr is None:

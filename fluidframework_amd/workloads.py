@@ -11,7 +11,8 @@ import subprocess
 
 import numpy as np
 
-from .streams import MAP_OP_DTYPE, MT_OP_DTYPE, MapBatch, MergeTreeBatch, js_json
+from .streams import (MAP_OP_DTYPE, MT_OP_DTYPE, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
+                      MergeTreeBatch, js_json)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GEN_PATH = os.path.join(HERE, "libfmtgen.so")
@@ -31,6 +32,8 @@ def _lib():
         L.fmtgen_conflict_farm_new.restype = P
         L.fmtgen_conflict_farm_copy.argtypes = [P, U32, P, P, P, U32]
         L.fmtgen_free.argtypes = [P]
+        L.fmtgen_t3.argtypes = [U32, U32, U32, U32, U32, U32, U32, P, P, P]
+        L.fmtgen_t3.restype = ctypes.c_int64
         _gen = L
     return _gen
 
@@ -114,4 +117,32 @@ def conflict_farm(n_docs: int, n_clients: int = 8, ops_per_doc: int = 2000, min_
         props_kv=props_kv,
         keys=["client"],
         values=values,
+    )
+
+
+def t3_stream(n_segments: int = 10_000_000, n_ops: int = 10_000_000, n_clients: int = 63, max_lag: int = 4096,
+              max_range: int = 8, seed: int = 1) -> MergeTreeBatch:
+    """T3 (BASELINE.json config 5): one SharedString of n_segments segments loaded from a summary
+    (one header chunk), then n_ops messages from n_clients writers with refSeq lag U[0, max_lag).
+    See fmtgen_t3 in csrc/gen/fmtgen.cpp for the shape and why ranges are local edits."""
+    ops = np.zeros(n_ops, dtype=MT_OP_DTYPE)
+    segs = np.zeros(n_segments, dtype=SNAPSHOT_SEG_DTYPE)
+    text = np.zeros(n_segments * 8 + n_ops * 3 + 1, dtype="<u2")
+    n_text = _lib().fmtgen_t3(n_segments, n_ops, n_clients, max_lag, max_range, seed, 0, _p(segs), _p(text), _p(ops))
+    if n_text < 0:
+        raise ValueError(f"fmtgen_t3 failed ({n_text})")
+    snaps = np.zeros(1, dtype=SNAPSHOT_DOC_DTYPE)
+    snaps["first_seg"], snaps["n_header"], snaps["n_body"], snaps["loaded"] = 0, n_segments, 0, 1
+    n_props = len(CLIENT_NAMES)
+    return MergeTreeBatch(
+        ops=ops,
+        doc_op_offsets=np.array([0, n_ops], dtype=np.uint64),
+        text=text[: max(1, n_text)].copy(),
+        doc_init=np.zeros((1, 2), dtype=np.uint32),
+        props_off=np.arange(n_props + 1, dtype=np.uint32),
+        props_kv=np.array([(0 << 16) | (i + 1) for i in range(n_props)], dtype=np.uint32),
+        keys=["client"],
+        values=["null"] + [js_json(c) for c in CLIENT_NAMES],
+        snapshots=snaps,
+        snapshot_segs=segs,
     )

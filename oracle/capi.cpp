@@ -77,6 +77,7 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
       L.len = static_cast<uint32_t>(s->len());
       L.props = pid;
       L.block = static_cast<uint16_t>(blockOf[i]);
+      L.pad = static_cast<uint16_t>(static_cast<uint32_t>(blockOf[i]) >> 16);  // block ordinal, high half
     }
     for (int k = 0; k < s->len(); k++) {
       if (chars && charOff + k < capChars) chars[charOff + k] = static_cast<uint16_t>(s->text[k]);
@@ -193,8 +194,11 @@ int orc_mt_summary(void* h, const char* const* keys, int nKeys, const char* cons
   return static_cast<int>(all.size());
 }
 
+std::atomic<int> g_indexed{0};  // orc_set_index: replays use the remote-length index (BlockIdx)
+
 // The document's initial state: a loaded summary (f3) or its initial text, then collaboration.
 void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d) {
+  if (g_indexed.load()) mt.enableIndex();
   if (b->snapshots != nullptr && b->snapshots[d].loaded) {
     const fmt_mt_snapshot_doc& sd = b->snapshots[d];
     std::vector<MergeTree::LoadedSeg> head, body;
@@ -258,6 +262,39 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return status.load();
 }
+
+// Replays ONE document: its initial state, then at most maxOps of its ops (all with maxOps = 0), timing
+// the load and the ops separately (the T3 CPU baseline times the ops). Dumps like orc_mt_replay_batch.
+int orc_mt_replay_timed(const fmt_mt_batch* b, uint32_t d, uint64_t maxOps, double* loadSeconds,
+                        double* opsSeconds, uint64_t* opsDone, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves,
+                        uint32_t capLeaves, uint16_t* chars, uint32_t capChars, fmt_mt_propset* props,
+                        uint32_t capProps) {
+  MergeTree mt;
+  const auto t0 = std::chrono::steady_clock::now();
+  startDoc(mt, b, d);
+  const auto t1 = std::chrono::steady_clock::now();
+  const uint64_t o0 = b->doc_op_offsets[d];
+  uint64_t n = b->doc_op_offsets[d + 1] - o0;
+  if (maxOps && maxOps < n) {
+    n = maxOps;  // stop at a message boundary
+    while (n < b->doc_op_offsets[d + 1] - o0 && (b->ops[o0 + n].flags & FMT_MT_F_GROUP_CONT)) n++;
+  }
+  int32_t failSeq = 0;
+  const int st = applyOps(&mt, b->ops + o0, n, b->text, b->props_off, b->props_kv, &failSeq);
+  const auto t2 = std::chrono::steady_clock::now();
+  if (loadSeconds) *loadSeconds = std::chrono::duration<double>(t1 - t0).count();
+  if (opsSeconds) *opsSeconds = std::chrono::duration<double>(t2 - t1).count();
+  if (opsDone) *opsDone = n;
+  if (hdr) std::memset(hdr, 0, sizeof(*hdr));
+  if (hdr || leaves || chars || props) dumpDoc(&mt, hdr, leaves, capLeaves, chars, capChars, props, capProps);
+  if (hdr) {
+    hdr->status = st;
+    hdr->fail_seq = failSeq;
+  }
+  return st;
+}
+
+void orc_set_index(int on) { g_indexed = on; }
 
 // ---------------------------------------------------------------- SharedMap
 // Every remove stamp of every final leaf of document d, in stamp order: (leaf index, client) pairs

@@ -121,6 +121,7 @@ int MergeTree::localBlockLength(const Block* b) const {
 
 // PartialSequenceLengths.getPartialLength ≡ Σ leaf nodeLength ?? 0 (partialLengths.ts:1189-1240).
 int MergeTree::remoteBlockLength(const Block* b, const Perspective& p) const {
+  if (indexed_) return static_cast<int>(const_cast<MergeTree*>(this)->idxLength(const_cast<Block*>(b), p));
   int len = 0;
   for (int i = 0; i < b->childCount; i++) {
     const Node* c = b->children[i];
@@ -211,6 +212,7 @@ MergeTree::InsertResult MergeTree::insertRecursive(Block* block, int pos, const 
           // splitLeafSegment (mergeTree.ts:1768-1796)
           if (rem > 0) {
             newNode = splitAt(seg, rem);
+            lastSplit_ = {seg, static_cast<Seg*>(newNode)};
             hadChanges = true;
             childIndex++;
           } else {
@@ -256,6 +258,7 @@ MergeTree::InsertResult MergeTree::insertRecursive(Block* block, int pos, const 
 // mergeTree.ts:1974-1987: keep the first half, move the second half to a new block.
 Block* MergeTree::split(Block* node) {
   constexpr int half = kMaxNodesInBlock / 2;
+  idxMarkDirty(node);  // both halves are re-indexed from their children (nb is new)
   Block* nb = makeBlock(half);
   node->childCount = half;
   for (int i = 0; i < half; i++) {
@@ -477,7 +480,8 @@ void MergeTree::obliterateRange(int start, bool startBefore, int endPlace, bool 
           pos = nextPos;
           continue;
         }
-        if (!s->removed()) {
+        const bool wasRemoved = s->removed();
+        if (!wasRemoved) {
           newlyRemoved.push_back(s);
           s->removes.push_back(stamp);
         } else {
@@ -486,6 +490,7 @@ void MergeTree::obliterateRange(int start, bool startBefore, int endPlace, bool 
             if (stampGreater(stamp, s->removes[k])) break;
           s->removes.insert(s->removes.begin() + (k + 1), stamp);
         }
+        if (indexed_) idxOnRemove(s, stamp.client, wasRemoved);
         if (collaborating) addToLRUSet(s, stamp.seq);
         pos = nextPos;
       } else {
@@ -523,7 +528,9 @@ void MergeTree::obliterateOnInsert(Seg* seg, const Perspective& p, Stamp stamp) 
 // mergeTree.ts:1798-1808
 void MergeTree::ensureIntervalBoundary(int pos, const Perspective& p) {
   InsertCtx ctx{false, nullptr};
+  lastSplit_ = {nullptr, nullptr};
   insertingWalk(pos, p, Stamp{kTreeMaintSeq, p.client}, ctx);
+  if (indexed_ && lastSplit_.second != nullptr) idxOnSplit(lastSplit_.first, lastSplit_.second);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -581,6 +588,7 @@ void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp st
     insertingWalk(pos, p, stamp, ctx);
     if (seg->parent == nullptr) throw DataError("MergeTree insert failed");
     if (stamp.seq != kUnassignedSeq) obliterateOnInsert(seg, p, stamp);
+    if (indexed_) idxOnNewLeaf(seg);
     // delta callback precedes zamboni (:1497-1516); an insert obliterated on arrival raises none
     if (catchupOut && !seg->removed()) recordDelta(FMT_MT_INSERT, {seg});
     if (collaborating) {
@@ -601,6 +609,7 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
   nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
   std::vector<Seg*> newlyRemoved;  // removedSegments: the REMOVE delta (mergeTree.ts:2314-2321)
   for (Seg* s : hit) {
+    const bool wasRemoved = s->removed();
     if (!s->removed() || stamp.seq == kUnassignedSeq) {
       if (!s->removed()) newlyRemoved.push_back(s);
       s->removes.push_back(stamp);
@@ -610,6 +619,7 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
         if (stampGreater(stamp, s->removes[i])) break;
       s->removes.insert(s->removes.begin() + (i + 1), stamp);
     }
+    if (indexed_) idxOnRemove(s, stamp.client, wasRemoved);
     if (collaborating) {
       const bool localPending = s->removes[0].seq == kUnassignedSeq && stamp.client == clientId;
       if (!localPending) addToLRUSet(s, stamp.seq);
@@ -929,6 +939,182 @@ void MergeTree::packParent(Block* parent) {
   }
   if (parent->childCount < kMaxNodesInBlock / 2 && parent->parent != nullptr) {
     packParent(parent->parent);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Remote-perspective length index (BlockIdx, see mergetree.hpp)
+// ------------------------------------------------------------------------------------------------
+namespace {
+int rm1Of(const Seg* s) { return s->removed() ? s->removes[0].seq : 0x7fffffff; }
+bool removedByClient(const Seg* s, int c) {
+  for (const Stamp& r : s->removes)
+    if (r.client == c) return true;
+  return false;
+}
+void checkAcked(const Seg* s) {
+  if (s->ins.seq == kUnassignedSeq) throw DataError("length index: unacknowledged insert");
+  for (const Stamp& r : s->removes)
+    if (r.seq == kUnassignedSeq) throw DataError("length index: unacknowledged remove");
+}
+// Whether leaf s can still change PriorPerspective(r, c) lengths for some r >= minSeq beyond its events.
+bool clientRelevant(const Seg* s, int c, int minSeq) {
+  if (s->ins.client == c && s->ins.seq > minSeq) return true;
+  return s->removed() && rm1Of(s) > minSeq && removedByClient(s, c);
+}
+void addClientEntry(BlockIdx& ix, int client, Seg* s) {
+  for (auto& e : ix.clients) {
+    if (e.first != client) continue;
+    for (Seg* t : e.second)
+      if (t == s) return;
+    e.second.push_back(s);
+    return;
+  }
+  ix.clients.push_back({client, {s}});
+}
+}  // namespace
+
+void MergeTree::idxMarkDirty(Block* b) {
+  if (indexed_) b->idxDirty = true;
+}
+
+void MergeTree::idxAppendEvent(Block* b, int seq, int64_t delta) {
+  BlockIdx& ix = *b->idx;
+  if (seq <= minSeq) {
+    ix.k0 += delta;
+    return;
+  }
+  if (!ix.evSeq.empty() && seq < ix.evSeq.back()) {  // out of order: re-index from the children
+    b->idxDirty = true;
+    return;
+  }
+  ix.evSeq.push_back(seq);
+  ix.evCum.push_back((ix.evCum.empty() ? 0 : ix.evCum.back()) + delta);
+  // fold the prefix at or below minSeq into k0 once it is half the list
+  if (ix.evSeq.size() >= 64 && ix.evSeq[ix.evSeq.size() / 2] <= minSeq) {
+    const size_t k = static_cast<size_t>(std::upper_bound(ix.evSeq.begin(), ix.evSeq.end(), minSeq) - ix.evSeq.begin());
+    const int64_t folded = ix.evCum[k - 1];
+    ix.k0 += folded;
+    ix.evSeq.erase(ix.evSeq.begin(), ix.evSeq.begin() + static_cast<long>(k));
+    ix.evCum.erase(ix.evCum.begin(), ix.evCum.begin() + static_cast<long>(k));
+    for (int64_t& c : ix.evCum) c -= folded;
+  }
+}
+
+void MergeTree::idxAddClient(Block* b, int client, Seg* s) {
+  if (client < 0) return;  // LocalClientId / NonCollabClient never query
+  addClientEntry(*b->idx, client, s);
+}
+
+void MergeTree::idxLeafTerms(Seg* s, BlockIdx& ix) {
+  checkAcked(s);
+  const int64_t len = s->len();
+  const int ins = s->ins.seq;
+  if (ins <= minSeq) ix.k0 += len;
+  else ix.evSeq.push_back(ins), ix.evCum.push_back(len);  // (seq, delta): sorted and summed by idxRebuild
+  if (s->removed()) {
+    const int m = std::max(ins, rm1Of(s));
+    if (m <= minSeq) ix.k0 -= len;
+    else ix.evSeq.push_back(m), ix.evCum.push_back(-len);
+  }
+  if (s->ins.client >= 0 && clientRelevant(s, s->ins.client, minSeq)) addClientEntry(ix, s->ins.client, s);
+  for (const Stamp& r : s->removes)
+    if (r.client >= 0 && clientRelevant(s, r.client, minSeq)) addClientEntry(ix, r.client, s);
+}
+
+void MergeTree::idxRebuild(Block* b) {
+  auto ix = std::make_unique<BlockIdx>();
+  for (int i = 0; i < b->childCount; i++) {
+    Node* n = b->children[i];
+    if (n->isLeaf) {
+      idxLeafTerms(static_cast<Seg*>(n), *ix);
+      continue;
+    }
+    Block* c = static_cast<Block*>(n);
+    if (!c->idx || c->idxDirty) idxRebuild(c);
+    const BlockIdx& ci = *c->idx;
+    ix->k0 += ci.k0;
+    for (size_t j = 0; j < ci.evSeq.size(); j++) {
+      const int64_t d = ci.evCum[j] - (j ? ci.evCum[j - 1] : 0);
+      if (ci.evSeq[j] <= minSeq) ix->k0 += d;
+      else ix->evSeq.push_back(ci.evSeq[j]), ix->evCum.push_back(d);
+    }
+    for (const auto& e : ci.clients)
+      for (Seg* t : e.second)
+        if (clientRelevant(t, e.first, minSeq)) addClientEntry(*ix, e.first, t);
+  }
+  // (seq, delta) pairs → sorted by seq with prefix sums
+  std::vector<std::pair<int, int64_t>> ev(ix->evSeq.size());
+  for (size_t j = 0; j < ev.size(); j++) ev[j] = {ix->evSeq[j], ix->evCum[j]};
+  std::stable_sort(ev.begin(), ev.end(), [](const auto& a, const auto& c) { return a.first < c.first; });
+  int64_t cum = 0;
+  for (size_t j = 0; j < ev.size(); j++) {
+    cum += ev[j].second;
+    ix->evSeq[j] = ev[j].first;
+    ix->evCum[j] = cum;
+  }
+  b->idx = std::move(ix);
+  b->idxDirty = false;
+}
+
+int64_t MergeTree::idxLength(Block* b, const Perspective& p) {
+  if (!b->idx || b->idxDirty) idxRebuild(b);
+  BlockIdx& ix = *b->idx;
+  const int r = p.refSeq, c = p.client;
+  const size_t k = static_cast<size_t>(std::upper_bound(ix.evSeq.begin(), ix.evSeq.end(), r) - ix.evSeq.begin());
+  int64_t len = ix.k0 + (k ? ix.evCum[k - 1] : 0);
+  for (auto& e : ix.clients) {
+    if (e.first != c) continue;
+    auto& v = e.second;
+    size_t w = 0;
+    for (size_t j = 0; j < v.size(); j++) {
+      Seg* s = v[j];
+      if (!clientRelevant(s, c, minSeq)) continue;  // dropped lazily
+      v[w++] = s;
+      const int ins = s->ins.seq, rm1 = rm1Of(s);
+      const bool inR = removedByClient(s, c);
+      if (inR && ins <= r && r < rm1) len -= s->len();
+      if (!inR && s->ins.client == c && ins > r && rm1 > r) len += s->len();
+    }
+    v.resize(w);
+    break;
+  }
+  return len;
+}
+
+void MergeTree::idxOnNewLeaf(Seg* s) {
+  checkAcked(s);
+  const int64_t len = s->len();
+  for (Block* a = s->parent; a != nullptr; a = a->parent) {
+    if (!a->idx || a->idxDirty) continue;  // re-indexed from its children on next use
+    idxAppendEvent(a, s->ins.seq, len);
+    if (s->removed()) idxAppendEvent(a, std::max(s->ins.seq, rm1Of(s)), -len);
+    if (!a->idx || a->idxDirty) continue;
+    if (clientRelevant(s, s->ins.client, minSeq)) idxAddClient(a, s->ins.client, s);
+    for (const Stamp& r : s->removes)
+      if (clientRelevant(s, r.client, minSeq)) idxAddClient(a, r.client, s);
+  }
+}
+
+void MergeTree::idxOnSplit(Seg* left, Seg* right) {
+  // the parts' lengths still sum to the original's: events stand; the right part needs the left
+  // part's client entries
+  for (Block* a = right->parent; a != nullptr; a = a->parent) {
+    if (!a->idx || a->idxDirty) continue;
+    if (clientRelevant(right, right->ins.client, minSeq)) idxAddClient(a, right->ins.client, right);
+    for (const Stamp& r : right->removes)
+      if (clientRelevant(right, r.client, minSeq)) idxAddClient(a, r.client, right);
+  }
+  (void)left;
+}
+
+void MergeTree::idxOnRemove(Seg* s, int client, bool wasRemoved) {
+  checkAcked(s);
+  for (Block* a = s->parent; a != nullptr; a = a->parent) {
+    if (!a->idx || a->idxDirty) continue;
+    if (!wasRemoved) idxAppendEvent(a, std::max(s->ins.seq, rm1Of(s)), -static_cast<int64_t>(s->len()));
+    if (!a->idx || a->idxDirty) continue;
+    if (clientRelevant(s, client, minSeq)) idxAddClient(a, client, s);
   }
 }
 

@@ -110,11 +110,29 @@ struct ObliterateInfo {
   int refSeq = 0;
 };
 
+// Length index of a block for remote perspectives (what PartialSequenceLengths is to the
+// reference, partialLengths.ts:180-230, 973-1005; only an index: its value is Σ leaf lengths,
+// partialLengths.ts:1189-1240). A leaf w contributes len·[ins ≤ r ∧ rm1 > r ∧ c ∉ R] +
+// len·[ins > r ∧ ic = c ∧ rm1 > r ∧ c ∉ R] to PriorPerspective(r, c), r ≥ minSeq. The first term is
+// len·([ins ≤ r] − [max(ins, rm1) ≤ r]): a +len event at ins and a −len event at max(ins, rm1),
+// kept in seq order with prefix sums (events at or below the fold point are constants in k0);
+// the second and the c ∈ R correction come from the few leaves each client inserted or removed in
+// the collaboration window, evaluated from the leaves themselves.
+struct BlockIdx {
+  int64_t k0 = 0;                          // folded events
+  std::vector<int> evSeq;                  // event seqs, non-decreasing
+  std::vector<int64_t> evCum;              // prefix sums of the event deltas
+  std::vector<std::pair<int, std::vector<struct Seg*>>> clients;  // client → leaves (inserted by it or
+                                                                  // removed by it, in the window)
+};
+
 struct Block : Node {
   Block() : Node(false) {}
   int childCount = 0;
   Node* children[kMaxNodesInBlock] = {};
   int needsScour = -1;  // -1 undefined, 0 false, 1 true (mergeTreeNodes.ts MergeBlock.needsScour)
+  std::unique_ptr<BlockIdx> idx;  // remote-perspective length index (MergeTree::enableIndex)
+  bool idxDirty = true;           // rebuilt from the children before its next use
 };
 
 // core-utils/src/heap.ts:54-182 with LRUSegmentComparer (mergeTree.ts:144-147). Ported as an
@@ -178,6 +196,12 @@ class MergeTree {
   // client.ts:1381-1391 updateSeqNumbers, after the last member of a message.
   void updateSeqNumbers(int min, int seq);
 
+  // Maintain the per-block remote length index (BlockIdx) instead of summing leaf lengths over the
+  // subtree on every query: O(log window + the querying client's window leaves) per block, which
+  // makes a 10M-segment document (BASELINE config 5, T3) replayable. Results are identical; only
+  // valid for an observer replay (every stamp acknowledged). Call before loading or applying ops.
+  void enableIndex() { indexed_ = true; }
+
   // Legacy catch-up ops (sequence.ts:971-1006): while set, each applied op appends the ranges of
   // the sequenceDelta event it raises, merged the way createOpsFromDelta merges them
   // (sequence.ts:395-452), tagged with catchupOp.
@@ -214,7 +238,7 @@ class MergeTree {
   static bool isPresent(const Seg* s, const Perspective& p);
   int leafLength(const Seg* s, const Perspective& p) const;      // mergeTree.ts:720-736
   int localBlockLength(const Block* b) const;                    // blockUpdate cachedLength
-  int remoteBlockLength(const Block* b, const Perspective& p) const;
+  int remoteBlockLength(const Block* b, const Perspective& p) const;  // const_cast inside when indexed
   int nodeLength(const Node* n, const Perspective& p) const;     // mergeTree.ts:1116-1145
   bool isLocalPerspective(const Perspective& p) const {
     return !collaborating || clientId == p.client;
@@ -262,6 +286,19 @@ class MergeTree {
   void zamboniSegments();
   void scourNode(Block* node, std::vector<Node*>& hold);
   void packParent(Block* parent);
+
+  // BlockIdx maintenance (indexed_ only)
+  bool indexed_ = false;
+  std::pair<Seg*, Seg*> lastSplit_{nullptr, nullptr};  // the split ensureIntervalBoundary made
+  void idxMarkDirty(Block* b);
+  void idxRebuild(Block* b);
+  int64_t idxLength(Block* b, const Perspective& p);
+  void idxAppendEvent(Block* b, int seq, int64_t delta);
+  void idxAddClient(Block* b, int client, Seg* s);
+  void idxOnNewLeaf(Seg* s);                  // after insertion (+ obliterateOnInsert)
+  void idxOnSplit(Seg* left, Seg* right);     // right part of a split, linked after left
+  void idxOnRemove(Seg* s, int client, bool wasRemoved);  // after a remove stamp was added
+  void idxLeafTerms(Seg* s, BlockIdx& ix);    // a leaf's events and client entries, for rebuilds
 
   Block* root_;
   Block unfinished_;  // theUnfinishedNode sentinel (mergeTree.ts:656)

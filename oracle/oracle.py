@@ -44,6 +44,9 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_replay_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P,
                                           ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P,
                                           ctypes.c_uint32, P]
+        L.orc_mt_replay_timed.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P, ctypes.c_uint32, P,
+                                          ctypes.c_uint32, P, ctypes.c_uint32]
+        L.orc_set_index.argtypes = [ctypes.c_int]
         L.orc_map_replay.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.c_uint32, P]
         L.orc_map_summary.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P,
                                       ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P]
@@ -165,6 +168,29 @@ def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096
     if cap_catchup:
         return rc, hdrs, leaves, chars, props, secs.value, catchup.reshape(n, cap_catchup)
     return rc, hdrs, leaves, chars, props, secs.value
+
+
+def set_index(on: bool):
+    """Replays use the per-block remote-length index (MergeTree::enableIndex): same results, O(log)
+    block lengths instead of subtree sums (what makes a 10M-segment T3 document replayable)."""
+    lib().orc_set_index(1 if on else 0)
+
+
+def mt_replay_timed(batch, doc=0, max_ops=0, cap_leaves=0, cap_chars=0, cap_props=64):
+    """Replay one document (its first max_ops ops; all with 0), timing load and ops separately.
+    Returns (rc, header, leaves, chars, props, load_s, ops_s, ops_done)."""
+    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+
+    hdr = np.zeros(1, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(max(cap_leaves, 1), dtype=LEAF_DTYPE)
+    chars = np.zeros(max(cap_chars, 1), dtype="<u2")
+    props = np.zeros(max(cap_props, 1), dtype=PROPSET_DTYPE)
+    ls, os_, nd = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_uint64(0)
+    b, keep = batch_struct(batch)
+    rc = lib().orc_mt_replay_timed(ctypes.byref(b), doc, max_ops, ctypes.byref(ls), ctypes.byref(os_), ctypes.byref(nd),
+                                   _ptr(hdr), _ptr(leaves), cap_leaves, _ptr(chars), cap_chars, _ptr(props), cap_props)
+    del keep
+    return rc, hdr[0], leaves[:cap_leaves], chars[:cap_chars], props, ls.value, os_.value, nd.value
 
 
 def map_replay(batch, threads=1):

@@ -1,0 +1,80 @@
+// huge_emu.cpp — TEST INFRASTRUCTURE ONLY: the huge-document engine (huge_engine.h, BASELINE
+// config 5 / T3) compiled for the host with the 64-lane emulation of wave.h, so the CPU suite checks
+// its logic against the oracle without a GPU. Never loaded by the product.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#ifdef FMT_HUGE_CHECK_BUILD
+#define FMT_HUGE_CHECK 1
+#endif
+
+#include "../../fluidframework_amd/csrc/huge_engine.h"
+
+using namespace fmt_huge;
+
+extern "C" {
+
+// Replays document d of the batch (a summary-loaded document, header chunk only) into the caller's
+// output arrays (fmt_mt_fetch_doc layout). Returns the document status.
+int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+                    uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
+  const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+  const uint64_t nOps = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
+  const uint32_t N = sd.n_header;
+  HugeState S{};
+  S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
+  S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
+  S.winCap = static_cast<uint32_t>(3 * nOps + 1024);
+  const uint64_t textCap = b->text_len + 256 * nOps + 65536;
+  std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6);
+  std::vector<int32_t> i32(static_cast<size_t>(S.blockCap) * 8 * 2);
+  size_t o = 0, oi = 0;
+  auto U = [&](size_t n) { uint32_t* p = u32.data() + o; o += n; return p; };
+  auto I = [&](size_t n) { int32_t* p = i32.data() + oi; oi += n; return p; };
+  const size_t nl = static_cast<size_t>(S.blockCap) * 8;
+  S.lLen = U(nl); S.lMlo = U(nl); S.lMhi = U(nl); S.lId = U(nl); S.lText = U(nl); S.lMeta = U(nl);
+  S.lIns = I(nl); S.lRm = I(nl);
+  std::vector<uint32_t> blk(static_cast<size_t>(S.blockCap) * 14);
+  std::vector<int32_t> bsc(S.blockCap);
+  S.bCount = blk.data(); S.bParent = S.bCount + S.blockCap; S.bLeaf = S.bParent + S.blockCap;
+  S.bChild = S.bLeaf + S.blockCap; S.bGroup = S.bChild + 8ull * S.blockCap; S.bSlot = S.bGroup + S.blockCap;
+  S.freeBlk = S.bSlot + S.blockCap; S.bScour = bsc.data();
+  std::vector<uint32_t> gsb(static_cast<size_t>(kGroupCap) * kSlotCap);
+  std::vector<int32_t> gss(static_cast<size_t>(kGroupCap) * kSlotCap);
+  S.gSlotBlk = gsb.data(); S.gSlotStable = gss.data();
+  std::vector<uint32_t> ids(2ull * S.idCap, kNone);
+  S.leafBlk = ids.data(); S.winIdx = ids.data() + S.idCap;
+  std::vector<uint32_t> wu(5ull * S.winCap);
+  std::vector<int32_t> wi(2ull * S.winCap);
+  S.wLen = wu.data(); S.wMeta = S.wLen + S.winCap; S.wGroup = S.wMeta + S.winCap; S.wBlk = S.wGroup + S.winCap;
+  S.wLeaf = S.wBlk + S.winCap; S.wIns = wi.data(); S.wRm = S.wIns + S.winCap;
+  std::vector<uint16_t> text(textCap);
+  std::memcpy(text.data(), b->text, b->text_len * 2);
+  S.text = text.data(); S.textLen = b->text_len; S.textCap = textCap;
+  std::vector<uint32_t> pr(static_cast<size_t>(kPropCap) * 5);
+  S.props = pr.data();
+  auto lds = std::make_unique<HugeLds>();
+  std::memset(lds.get(), 0xCD, sizeof(HugeLds));
+  auto doc = std::make_unique<HugeDoc>();
+  doc->S = S;
+  doc->L = lds.get();
+  HugeInputs in;
+  in.ops = b->ops;
+  in.begin = b->doc_op_offsets[d];
+  in.end = b->doc_op_offsets[d + 1];
+  in.propsOff = b->props_off;
+  in.propsKv = b->props_kv;
+  in.nPropsOps = b->n_props_ops;
+  in.segs = b->snapshot_segs + sd.first_seg;
+  in.nSegs = N;
+  in.snapMinSeq = sd.min_seq;
+  in.snapSeq = sd.seq;
+  doc->run(in);
+  doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props);
+  return hdr->status;
+}
+
+}  // extern "C"

@@ -36,6 +36,50 @@ def emu_lib():
     return _emu
 
 
+_huge = {}
+
+
+def huge_emu_lib(tiny_groups=False):
+    """The huge-document engine (csrc/huge_engine.h, T3) under host emulation, with its index
+    invariants checked after every op (FMT_HUGE_CHECK). tiny_groups: 16 slots per group, 8 at load,
+    so that group splits and cross-group walks happen on small documents."""
+    if tiny_groups not in _huge:
+        name = "libhuge_emu_tiny.so" if tiny_groups else "libhuge_emu.so"
+        path = os.path.join(HERE, "_build", name)
+        src = os.path.join(HERE, "emu", "huge_emu.cpp")
+        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("huge_engine.h", "wave.h")]
+        if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(d) for d in deps):
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            extra = ["-DFMT_HUGE_SLOTCAP=16", "-DFMT_HUGE_FILL=8"] if tiny_groups else []
+            subprocess.run(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+                            "-DFMT_HUGE_CHECK_BUILD"] + extra + ["-o", path, src], check=True)
+        L = ctypes.CDLL(path)
+        L.emu_huge_replay.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        _huge[tiny_groups] = L
+    return _huge[tiny_groups]
+
+
+def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=False):
+    """(header, leaves, chars, props) of document `doc` replayed by the emulated huge engine."""
+    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+
+    segs = int(batch.snapshots[doc]["n_header"])
+    nops = int(batch.doc_op_offsets[doc + 1] - batch.doc_op_offsets[doc])
+    cap_leaves = cap_leaves or segs + 3 * nops + 8
+    cap_chars = cap_chars or len(batch.text) + 8
+    hdr = np.zeros(1, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(cap_leaves, dtype=LEAF_DTYPE)
+    chars = np.zeros(cap_chars, dtype="<u2")
+    props = np.zeros(4096, dtype=PROPSET_DTYPE)
+    b, keep = batch_struct(batch)
+    huge_emu_lib(tiny_groups).emu_huge_replay(ctypes.addressof(b), doc, _p(hdr), _p(leaves), cap_leaves, _p(chars), cap_chars,
+                                   _p(props))
+    del keep
+    h = hdr[0]
+    return h, leaves[: int(h["n_leaves"])], chars[: int(h["n_chars"])], props[: int(h["n_props"])]
+
+
 def emu_caps(large=False):
     a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
     emu_lib().emu_mt_capacity(int(large), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
@@ -80,7 +124,7 @@ def resolve_props(pid, table):
 
 
 HEADER_FIELDS = ["status", "cur_seq", "min_seq", "n_leaves", "n_chars", "n_blocks", "depth", "visible_len"]
-LEAF_FIELDS = ["ins_seq", "rm_seq", "rm_clients", "char_off", "len", "ins_client", "block"]
+LEAF_FIELDS = ["ins_seq", "rm_seq", "rm_clients", "char_off", "len", "ins_client", "block", "pad"]
 
 
 def compare_doc(exp, got):

@@ -1,0 +1,125 @@
+"""T3 on the GPU (BASELINE config 5): documents beyond the large tier are replayed by the huge-document
+engine (csrc/huge_engine.h, hugedoc.hip) through the same C ABI, bit-exact against the oracle (with
+its remote-length index): every leaf field, the text, the prop sets, the header."""
+import copy
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import native, workloads
+from mt_compare import compare_doc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = native.Engine(0)
+    yield e
+    e.close()
+
+
+def _oracle(orc, batch, doc=0):
+    orc.set_index(True)
+    try:
+        sub = _one_doc(batch, doc)
+        segs = int(sub.snapshots[0]["n_header"]) if sub.snapshots is not None and sub.snapshots[0]["loaded"] else 0
+        nops = len(sub.ops)
+        rc, h, lv, ch, pr, *_ = orc.mt_replay_timed(sub, 0, 0, cap_leaves=segs + 3 * nops + 4096,
+                                                    cap_chars=len(sub.text) + 8, cap_props=4096)
+    finally:
+        orc.set_index(False)
+    return rc, (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
+
+
+def _one_doc(batch, d):
+    b = copy.copy(batch)
+    o0, o1 = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+    b.ops = batch.ops[o0:o1]
+    b.doc_op_offsets = np.array([0, o1 - o0], dtype=np.uint64)
+    b.doc_init = batch.doc_init[d : d + 1]
+    if batch.snapshots is not None:
+        b.snapshots = batch.snapshots[d : d + 1]
+    return b
+
+
+def _concat(batches):
+    """One batch holding every document of `batches` (same props table: conflict farm and T3 share it)."""
+    from fluidframework_amd.streams import SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE
+
+    ops, offs, texts, init, snaps, segs = [], [0], [], [], [], []
+    tbase, sbase = 0, 0
+    for b in batches:
+        o = b.ops.copy()
+        o["payload"][o["type"] == 0] += tbase
+        ops.append(o)
+        offs.extend((np.asarray(b.doc_op_offsets[1:], dtype=np.int64) + offs[-1]).tolist())
+        texts.append(b.text)
+        di = b.doc_init.copy()
+        di[:, 0] += tbase
+        init.append(di)
+        if b.snapshots is not None:
+            sd = b.snapshots.copy()
+            sd["first_seg"] += sbase
+            sg = b.snapshot_segs.copy()
+            sg["text"] += tbase
+            snaps.append(sd)
+            segs.append(sg)
+            sbase += len(sg)
+        else:
+            snaps.append(np.zeros(b.n_docs, dtype=SNAPSHOT_DOC_DTYPE))
+        tbase += len(b.text)
+    first = batches[0]
+    return first.__class__(
+        ops=np.concatenate(ops), doc_op_offsets=np.asarray(offs, dtype=np.uint64), text=np.concatenate(texts),
+        doc_init=np.concatenate(init), props_off=first.props_off, props_kv=first.props_kv, keys=first.keys,
+        values=first.values, snapshots=np.concatenate(snaps),
+        snapshot_segs=np.concatenate(segs) if segs else np.zeros(0, dtype=SNAPSHOT_SEG_DTYPE))
+
+
+@pytest.mark.parametrize("segs,ops,clients,lag,rng,seed", [
+    (5000, 8000, 63, 4096, 8, 3),
+    (60000, 40000, 63, 4096, 8, 4),
+    (30000, 20000, 16, 1000, 300, 5),
+])
+def test_huge_doc_matches_oracle(orc, engine, segs, ops, clients, lag, rng, seed):
+    batch = workloads.t3_stream(segs, ops, n_clients=clients, max_lag=lag, max_range=rng, seed=seed)
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+
+
+def test_mixed_batch_small_large_and_huge_documents(orc, engine):
+    """Huge documents replay beside ordinary ones (small tier) in one fmt_mt_run."""
+    farm = workloads.conflict_farm(24, n_clients=8, ops_per_doc=600, seed=8)
+    t3a = workloads.t3_stream(3000, 4000, n_clients=31, max_lag=700, seed=9)
+    t3b = workloads.t3_stream(9000, 6000, n_clients=63, max_lag=4096, max_range=20, seed=10)
+    batch = _concat([farm, t3a, farm, t3b])
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert (hdrs["status"] == 0).all()
+    for d in range(batch.n_docs):
+        rc, exp = _oracle(orc, batch, d)
+        assert rc == 0
+        lv, ch, pr = engine.mt_doc(d, hdrs[d])
+        assert compare_doc(exp, (hdrs[d], lv, ch, pr)) == [], d
+    engine.mt_run()  # a second run over the same state replays from the inputs again
+    assert np.array_equal(engine.mt_headers(), hdrs)
+
+
+def test_t3_million_segments(orc, engine):
+    batch = workloads.t3_stream(1_000_000, 100_000, n_clients=63, max_lag=4096, seed=12)
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []

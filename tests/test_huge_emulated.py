@@ -1,0 +1,37 @@
+"""The huge-document engine (csrc/huge_engine.h: paged leaf blocks, group lists, window table —
+the T3 path, BASELINE config 5) under host emulation, bit-exact against the oracle on T3-shaped
+documents: every leaf field, the text, the prop sets and the header."""
+import pytest
+
+from fluidframework_amd import workloads
+from mt_compare import compare_doc, emu_huge_replay
+
+
+def _oracle_doc(orc, batch):
+    orc.set_index(True)
+    try:
+        segs = int(batch.snapshots[0]["n_header"])
+        nops = len(batch.ops)
+        rc, h, lv, ch, pr, *_ = orc.mt_replay_timed(batch, 0, 0, cap_leaves=segs + 3 * nops + 8,
+                                                    cap_chars=len(batch.text) + 8, cap_props=4096)
+    finally:
+        orc.set_index(False)
+    return rc, (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
+
+
+@pytest.mark.parametrize("segs,ops,clients,lag,rng,seed,tiny", [
+    (200, 300, 4, 16, 8, 1, False),
+    (2000, 3000, 16, 300, 8, 2, False),
+    (5000, 8000, 63, 4096, 8, 3, False),
+    (30000, 20000, 63, 4096, 40, 4, False),
+    (3000, 6000, 31, 500, 8, 5, True),
+    (2000, 8000, 63, 2000, 200, 6, True),
+    (700, 12000, 8, 64, 30, 7, True),
+])
+def test_huge_engine_matches_oracle(orc, segs, ops, clients, lag, rng, seed, tiny):
+    batch = workloads.t3_stream(segs, ops, n_clients=clients, max_lag=lag, max_range=rng, seed=seed)
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=tiny)
+    assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+    assert compare_doc(exp, got) == []
