@@ -122,6 +122,7 @@ struct HugeLds {
   int32_t sLen[kSlotCap];        // the group being searched: view length per slot
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
+  uint32_t held[8][kMaxNodes * kMaxNodes];  // packParent: the held leaves' 8 fields, document order
   uint32_t tmp[256];
 };
 
@@ -174,6 +175,12 @@ class HugeDoc {
 #endif
   }
   bool corrValid = false;    // gCorr / gStart hold the current op's perspective
+  uint32_t epoch = 0;        // bumped by every change of the index (window table, slots, stable sums)
+  uint32_t slotCacheG = kNone, slotCacheEpoch = 0;  // sLen / sBlk hold group slotCacheG at that epoch
+  FMT_DEV void invalidate() {
+    corrValid = false;
+    epoch++;
+  }
 
   FMT_DEV bool fail(int code) {
     if (status == FMT_OK) status = code;
@@ -181,12 +188,13 @@ class HugeDoc {
   }
 
   // ------------------------------------------------------------------ small helpers
-  // Every read of HBM state this wave wrote goes through an agent-scope load (served by L2, never a
-  // stale vector-L1 line); rd() inside FOR_LANES bodies, ldu()/ldi() for wave-uniform values.
-  FMT_DEV static uint32_t rd(const uint32_t* p) { return loadCoherent(p); }
-  FMT_DEV static int32_t rd(const int32_t* p) { return loadCoherent(p); }
-  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(loadCoherent(p)); }
-  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadCoherent(p)); }
+  // Every read of HBM state goes through a workgroup-scope load: a vector load served by this CU's
+  // L1 (which the wave's own stores keep current; no other CU writes this document's state), never
+  // a scalar-cache load. rd() inside FOR_LANES bodies, ldu()/ldi() for wave-uniform values.
+  FMT_DEV static uint32_t rd(const uint32_t* p) { return loadWg(p); }
+  FMT_DEV static int32_t rd(const int32_t* p) { return loadWg(p); }
+  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(loadWg(p)); }
+  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadWg(p)); }
   // one lane stores a wave-uniform value
   template <class T>
   FMT_DEV static void st1(T* p, T v) {
@@ -227,6 +235,7 @@ class HugeDoc {
 
   // ------------------------------------------------------------------ window table
   FMT_DEV void winAdd(uint32_t id, int32_t ins, int32_t rm, uint32_t len, uint32_t meta, uint32_t grp, uint32_t blk) {
+    invalidate();
     if (nWin >= S.winCap) {
       fail(FMT_E_CAPACITY);
       return;
@@ -246,6 +255,7 @@ class HugeDoc {
     }
   }
   FMT_DEV void winRemove(uint32_t w) {  // swap-remove
+    invalidate();
     const uint32_t last = nWin - 1;
     const uint32_t id = ldu(S.wLeaf + w);
     if (w != last) {
@@ -272,6 +282,7 @@ class HugeDoc {
   // ------------------------------------------------------------------ stable sums
   // Stable length of a leaf: its length for every perspective at/above minSeq (non-window leaves).
   FMT_DEV void addStable(uint32_t blk, int delta) {
+    invalidate();
     if (delta == 0) return;
     const uint32_t g = ldu(S.bGroup + blk), s = ldu(S.bSlot + blk);
     int32_t* p = S.gSlotStable + static_cast<size_t>(g) * kSlotCap + s;
@@ -302,8 +313,8 @@ class HugeDoc {
   }
 
   // ------------------------------------------------------------------ group lists
-  FMT_DEV uint32_t* slotBlkPtr(uint32_t g) { return S.gSlotBlk + static_cast<size_t>(g) * kSlotCap; }
-  FMT_DEV int32_t* slotStPtr(uint32_t g) { return S.gSlotStable + static_cast<size_t>(g) * kSlotCap; }
+  FMT_DEV uint32_t* slotBlkPtr(uint32_t g) const { return S.gSlotBlk + static_cast<size_t>(g) * kSlotCap; }
+  FMT_DEV int32_t* slotStPtr(uint32_t g) const { return S.gSlotStable + static_cast<size_t>(g) * kSlotCap; }
 
   FMT_DEV int groupPos(uint32_t g) const {  // position of group g in gOrder
     for (int base = 0; base < nGroups; base += 64) {
@@ -318,6 +329,7 @@ class HugeDoc {
   // Insert leaf block nb into group g at slot `at` with stable length st (slots at/after shift up).
   // Splits the group first when it is full; returns false on failure.
   FMT_DEV bool slotInsert(uint32_t g, int at, uint32_t nb, int st) {
+    invalidate();
     int cnt = static_cast<int>(L->gCount[g]);
     if (cnt >= kSlotCap) {
       if (!groupSplit(g)) return false;
@@ -330,23 +342,31 @@ class HugeDoc {
     }
     uint32_t* sb = slotBlkPtr(g);
     int32_t* ss = slotStPtr(g);
-    for (int top = cnt - 1; top >= at; top -= 64) {  // shift [at, cnt) up by one, top-down
-      Lane<uint32_t> b;
-      Lane<int32_t> s;
+    // shift [at, cnt) up by one, top-down in chunks of 4 x 64 slots: a chunk's loads are all in
+    // flight before its stores (it writes only into slots the chunk above has already read)
+    for (int top = cnt - 1; top >= at; top -= 256) {
+      Lane<uint32_t> b[4];
+      Lane<int32_t> st[4];
       FOR_LANES(l) {
-        const int i = top - l;
-        if (i >= at) {
-          LANE(b) = sb[i];
-          LANE(s) = ss[i];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = top - 64 * u - l;
+          if (i >= at) {
+            LANE(b[u]) = rd(sb + i);
+            LANE(st[u]) = rd(ss + i);
+          }
         }
       }
       waveSync();
       FOR_LANES(l) {
-        const int i = top - l;
-        if (i >= at) {
-          sb[i + 1] = LANE(b);
-          ss[i + 1] = LANE(s);
-          S.bSlot[LANE(b)] = static_cast<uint32_t>(i + 1);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = top - 64 * u - l;
+          if (i >= at) {
+            sb[i + 1] = LANE(b[u]);
+            ss[i + 1] = LANE(st[u]);
+            S.bSlot[LANE(b[u])] = static_cast<uint32_t>(i + 1);
+          }
         }
       }
       waveSync();
@@ -368,28 +388,35 @@ class HugeDoc {
   // Remove slots [at, at + n) of group g (their blocks are being freed or moved); returns the
   // stable length they held.
   FMT_DEV void slotRemove(uint32_t g, int at, int n) {
+    invalidate();
     const int cnt = static_cast<int>(L->gCount[g]);
     uint32_t* sb = slotBlkPtr(g);
     int32_t* ss = slotStPtr(g);
     int removed = 0;
     for (int i = at; i < at + n; i++) removed += ldi(ss + i);
-    for (int base = at + n; base < cnt; base += 64) {
-      Lane<uint32_t> b;
-      Lane<int32_t> s;
+    for (int base = at + n; base < cnt; base += 256) {  // shift down by n, bottom-up, 4 x 64 per chunk
+      Lane<uint32_t> b[4];
+      Lane<int32_t> st[4];
       FOR_LANES(l) {
-        const int i = base + l;
-        if (i < cnt) {
-          LANE(b) = sb[i];
-          LANE(s) = ss[i];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = base + 64 * u + l;
+          if (i < cnt) {
+            LANE(b[u]) = rd(sb + i);
+            LANE(st[u]) = rd(ss + i);
+          }
         }
       }
       waveSync();
       FOR_LANES(l) {
-        const int i = base + l;
-        if (i < cnt) {
-          sb[i - n] = LANE(b);
-          ss[i - n] = LANE(s);
-          S.bSlot[LANE(b)] = static_cast<uint32_t>(i - n);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = base + 64 * u + l;
+          if (i < cnt) {
+            sb[i - n] = LANE(b[u]);
+            ss[i - n] = LANE(st[u]);
+            S.bSlot[LANE(b[u])] = static_cast<uint32_t>(i - n);
+          }
         }
       }
       waveSync();
@@ -415,8 +442,8 @@ class HugeDoc {
       FOR_LANES(l) {
         const int i = base + l;
         if (i < moved) {
-          const uint32_t b = sb[half + i];
-          const int32_t s = ss[half + i];
+          const uint32_t b = rd(sb + half + i);
+          const int32_t s = rd(ss + half + i);
           db[i] = b;
           ds[i] = s;
           S.bGroup[b] = g2;
@@ -450,11 +477,67 @@ class HugeDoc {
         if (w < nWin && rd(S.wGroup + w) == g) S.wGroup[w] = rd(S.bGroup + (rd(S.wBlk + w)));
       }
     }
-    corrValid = false;
+    invalidate();
     return true;
   }
 
   // ------------------------------------------------------------------ perspective corrections
+  // View length of window entry w (fields already loaded) for PriorPerspective(r, c).
+  FMT_DEV int winVis(uint32_t w, int32_t ins, int32_t rm, uint32_t len, uint32_t m, int r, int c) const {
+    if ((m >> 16) & 1u) {  // several removers: the leaf's full remover set
+      const uint32_t id = rd(S.wLeaf + w);
+      const uint32_t b = rd(S.leafBlk + id);
+      const int bc = static_cast<int>(rd(S.bCount + b));  // (slots past the count hold stale leaves)
+      uint32_t mlo = 0, mhi = 0;
+      for (int k = 0; k < bc; k++) {
+        const size_t i = static_cast<size_t>(b) * 8 + k;
+        if (rd(S.lId + i) == id) {
+          mlo = rd(S.lMlo + i);
+          mhi = rd(S.lMhi + i);
+        }
+      }
+      return visOf(len, ins, rm, mlo, mhi, mClient(m), r, c);
+    }
+    const bool byC = rm != kNotRemoved && static_cast<int>(wFirstRm(m)) == c;
+    return ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(len) : 0;
+  }
+
+  // One pass over the window table, 4 x 64 entries per step with every load of a step in flight
+  // together: for each entry of positive view length (and of group `only`, unless kNone), add it to
+  // gCorr[group] (bySlot false) or to sLen[slot of its block] (bySlot true).
+  FMT_DEV void windowPass(int r, int c, uint32_t only, bool bySlot) {
+    for (uint32_t base = 0; base < nWin; base += 256) {
+      Lane<int32_t> ins[4], rm[4];
+      Lane<uint32_t> len[4], m[4], grp[4];
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t w = base + 64 * u + l;
+          if (w < nWin) {
+            LANE(ins[u]) = rd(S.wIns + w);
+            LANE(rm[u]) = rd(S.wRm + w);
+            LANE(len[u]) = rd(S.wLen + w);
+            LANE(m[u]) = rd(S.wMeta + w);
+            LANE(grp[u]) = rd(S.wGroup + w);
+          }
+        }
+      }
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t w = base + 64 * u + l;
+          if (w < nWin && (only == kNone || LANE(grp[u]) == only)) {
+            const int v = winVis(w, LANE(ins[u]), LANE(rm[u]), LANE(len[u]), LANE(m[u]), r, c);
+            if (v) {
+              if (bySlot) atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + w))], v);
+              else atomicAddLds(&L->gCorr[LANE(grp[u])], v);
+            }
+          }
+        }
+      }
+    }
+    waveSync();
+  }
   // gCorr[g] = Σ view length of the window leaves of group g (their stable contribution is 0), and
   // gStart[k] = view start of the k-th group, for PriorPerspective(r, c).
   FMT_DEV void groupCorrections(int r, int c) {
@@ -464,36 +547,7 @@ class HugeDoc {
       for (int g = l; g < nGroups; g += 64) L->gCorr[g] = 0;
     }
     waveSync();
-    for (uint32_t base = 0; base < nWin; base += 64) {
-      FOR_LANES(l) {
-        const uint32_t w = base + l;
-        if (w < nWin) {
-          const uint32_t m = rd(S.wMeta + w);
-          const int32_t ins = rd(S.wIns + w), rm = rd(S.wRm + w);
-          int v;
-          if ((m >> 16) & 1u) {  // several removers: the leaf's full remover set
-            const uint32_t id = rd(S.wLeaf + w);
-            const uint32_t b = rd(S.leafBlk + id);
-            const int bc = static_cast<int>(rd(S.bCount + b));  // (slots past the count hold stale leaves)
-            uint32_t mlo = 0, mhi = 0;
-            for (int k = 0; k < bc; k++) {
-              const size_t i = static_cast<size_t>(b) * 8 + k;
-              if (rd(S.lId + i) == id) {
-                mlo = rd(S.lMlo + i);
-                mhi = rd(S.lMhi + i);
-              }
-            }
-            v = visOf(rd(S.wLen + w), ins, rm, mlo, mhi, mClient(m), r, c);
-          } else {
-            const uint32_t f = wFirstRm(m);
-            const bool byC = rm != kNotRemoved && static_cast<int>(f) == c;
-            v = ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(rd(S.wLen + w)) : 0;
-          }
-          if (v) atomicAddLds(&L->gCorr[rd(S.wGroup + w)], v);
-        }
-      }
-    }
-    waveSync();
+    windowPass(r, c, kNone, false);
     int32_t base = 0;
     for (int k0 = 0; k0 < nGroups; k0 += 64) {
       Lane<uint32_t> len;
@@ -525,48 +579,39 @@ class HugeDoc {
 
   // Slot view lengths of group g into L->sLen / L->sBlk (stable + that group's window corrections).
   FMT_DEV void slotLengths(uint32_t g, int r, int c) {
+    slotCacheG = g;
+    slotCacheEpoch = epoch;
     const uint64_t t0_ = clk();
     struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[2], t0_};
     const int cnt = static_cast<int>(L->gCount[g]);
     const uint32_t* sb = slotBlkPtr(g);
     const int32_t* ss = slotStPtr(g);
-    FOR_LANES(l) {
-      for (int i = l; i < cnt; i += 64) {
-        L->sBlk[i] = sb[i];
-        L->sLen[i] = ss[i];
-      }
-    }
-    waveSync();
-    for (uint32_t base = 0; base < nWin; base += 64) {
+    for (int base = 0; base < cnt; base += 256) {  // 4 x 64 slots per step, loads in flight together
+      Lane<uint32_t> bb[4];
+      Lane<int32_t> sv[4];
       FOR_LANES(l) {
-        const uint32_t w = base + l;
-        if (w < nWin && rd(S.wGroup + w) == g) {
-          const uint32_t m = rd(S.wMeta + w);
-          const int32_t ins = rd(S.wIns + w), rm = rd(S.wRm + w);
-          int v;
-          if ((m >> 16) & 1u) {
-            const uint32_t id = rd(S.wLeaf + w);
-            const uint32_t b = rd(S.leafBlk + id);
-            const int bc = static_cast<int>(rd(S.bCount + b));  // (slots past the count hold stale leaves)
-            uint32_t mlo = 0, mhi = 0;
-            for (int k = 0; k < bc; k++) {
-              const size_t i = static_cast<size_t>(b) * 8 + k;
-              if (rd(S.lId + i) == id) {
-                mlo = rd(S.lMlo + i);
-                mhi = rd(S.lMhi + i);
-              }
-            }
-            v = visOf(rd(S.wLen + w), ins, rm, mlo, mhi, mClient(m), r, c);
-          } else {
-            const uint32_t f = wFirstRm(m);
-            const bool byC = rm != kNotRemoved && static_cast<int>(f) == c;
-            v = ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(rd(S.wLen + w)) : 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = base + 64 * u + l;
+          if (i < cnt) {
+            LANE(bb[u]) = rd(sb + i);
+            LANE(sv[u]) = rd(ss + i);
           }
-          if (v) atomicAddLds(&L->sLen[rd(S.bSlot + (rd(S.wBlk + w)))], v);
+        }
+      }
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int i = base + 64 * u + l;
+          if (i < cnt) {
+            L->sBlk[i] = LANE(bb[u]);
+            L->sLen[i] = LANE(sv[u]);
+          }
         }
       }
     }
     waveSync();
+    windowPass(r, c, g, true);
   }
 
   // ------------------------------------------------------------------ the hierarchical search
@@ -597,7 +642,7 @@ class HugeDoc {
     if (k < 0) return h;
     for (; k < nGroups; k++) {
       const uint32_t g = L->gOrder[k];
-      slotLengths(g, r, c);
+      if (slotCacheG != g || slotCacheEpoch != epoch) slotLengths(g, r, c);
       const int cnt = static_cast<int>(L->gCount[g]);
       int base = uni(L->gStart[k]);
       for (int s0 = 0; s0 < cnt; s0 += 64) {
@@ -735,6 +780,7 @@ class HugeDoc {
 
   // Move leaves [from, cnt) of block a to the front of block b (b's leaves shift up by the count).
   FMT_DEV void moveLeaves(uint32_t a, int from, int cnt, uint32_t b) {
+    invalidate();
     const int n = cnt - from;
     if (n <= 0) return;
     Lane<uint32_t> f[8];
@@ -773,6 +819,7 @@ class HugeDoc {
 
   // Window entries of block b's leaves name b and its group.
   FMT_DEV void retagWindow(uint32_t b) {
+    invalidate();
     const uint32_t cnt = ldu(S.bCount + b), g = ldu(S.bGroup + b);
     FOR_LANES(l) {
       if (l < static_cast<int>(cnt)) {
@@ -969,11 +1016,13 @@ class HugeDoc {
   // ------------------------------------------------------------------ op pieces
   // splitLeafSegment (mergeTree.ts:1768-1796) of leaf (b, k) at offset o (0 < o < len): the right part
   // follows it in the same block, with a fresh id; a window leaf's right part joins the window table.
-  FMT_DEV bool splitLeaf(uint32_t b, int k, int o) {
+  FMT_DEV bool splitLeaf(uint32_t b, int k, int o, uint32_t* rightId = nullptr) {
+    invalidate();
     Leaf x = getLeaf(b, k);
     if (nextId >= S.idCap) return fail(FMT_E_CAPACITY);
     Leaf y = x;
     y.id = nextId++;
+    if (rightId) *rightId = y.id;
     y.len = x.len - static_cast<uint32_t>(o);
     y.text = x.text + static_cast<uint32_t>(o);
     x.len = static_cast<uint32_t>(o);
@@ -1003,23 +1052,35 @@ class HugeDoc {
     *k = m ? ctz64(m) : -1;
   }
 
-  // ensureIntervalBoundary(p) in the op's view: split the leaf strictly containing p.
-  FMT_DEV bool boundary(int p, int r, int c) {
-    const Hit h = find(p, r, c);
-    if (!h.found || h.st >= p) return true;
-    return splitLeaf(h.blk, h.k, p - h.st);
+  // The leaf block after b in document order (kNone at the end).
+  FMT_DEV uint32_t nextBlockOf(uint32_t b) const {
+    uint32_t g = ldu(S.bGroup + b);
+    uint32_t s = ldu(S.bSlot + b) + 1;
+    if (s < L->gCount[g]) return ldu(slotBlkPtr(g) + s);
+    for (int k = groupPos(g) + 1; k < nGroups; k++) {
+      g = L->gOrder[k];
+      if (L->gCount[g] > 0) return ldu(slotBlkPtr(g));
+    }
+    return kNone;
   }
 
+  // insertSegments (mergeTree.ts:1484-1517): ensureIntervalBoundary(p) then the inserting walk, both
+  // from one search: the new leaf goes before the first qualifying leaf at p, or before the right part
+  // of the leaf that strictly contained p.
   FMT_DEV void insertText(const fmt_mt_op& op) {
     const int r = op.ref_seq, c = op.client, p = op.pos1;
-    if (!boundary(p, r, c)) return;
-    if (op.len == 0) return;
-    Hit h = find(p, r, c);
+    const Hit h = find(p, r, c);
     uint32_t b;
     int k;
     if (h.found) {
-      b = h.blk;
-      k = h.k;
+      if (h.st < p) {
+        uint32_t right;
+        if (!splitLeaf(h.blk, h.k, p - h.st, &right)) return;
+        locate(right, &b, &k);
+      } else {
+        b = h.blk;
+        k = h.k;
+      }
     } else {
       if (p != totalView()) {  // "MergeTree insert failed" (mergeTree.ts:1629)
         fail(FMT_E_DATA);
@@ -1032,6 +1093,7 @@ class HugeDoc {
       b = lastBlk;
       k = static_cast<int>(ldu(S.bCount + b));
     }
+    if (op.len == 0) return;
     if (nextId >= S.idCap) {
       fail(FMT_E_CAPACITY);
       return;
@@ -1048,6 +1110,7 @@ class HugeDoc {
     shiftUp(b, k, static_cast<int>(cnt));
     putLeaf(b, k, x);
     winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, ldu(S.bGroup + b), b);
+    invalidate();
     childAdded(b);
     if (status != FMT_OK) return;
     uint32_t bb;
@@ -1056,72 +1119,95 @@ class HugeDoc {
     lru(bb, x.id, op.seq);
   }
 
-  // markRangeRemoved / annotateRange over the leaves of positive view length in [start, end).
+  // View lengths of the leaves of block b (lane k = leaf k) from PriorPerspective(r, c).
+  FMT_DEV Lane<uint32_t> blockVis(uint32_t b, uint32_t cnt, int r, int c) const {
+    Lane<uint32_t> vis;
+    FOR_LANES(l) {
+      uint32_t v = 0;
+      if (l < static_cast<int>(cnt)) {
+        const size_t i = li(b, l);
+        v = static_cast<uint32_t>(visOf(rd(S.lLen + i), rd(S.lIns + i), rd(S.lRm + i), rd(S.lMlo + i), rd(S.lMhi + i),
+                                        mClient(rd(S.lMeta + i)), r, c));
+      }
+      LANE(vis) = v;
+    }
+    return vis;
+  }
+
+  // markRangeRemoved / annotateRange (mergeTree.ts:2009-2081, 2292-2383) from one search: the leaf
+  // at `start` and the leaf strictly containing `end` are found before either boundary split
+  // (ensureIntervalBoundary moves no view position), then the hits are walked block by block:
+  // the leaves of positive view length inside [start, end).
   FMT_DEV void applyRange(const fmt_mt_op& op) {
     const int r = op.ref_seq, c = op.client, seq = op.seq;
     const int start = op.pos1, end = op.pos2;
-    if (!boundary(start, r, c) || !boundary(end, r, c)) return;
-    if (end <= start) return;
-    Hit h = find(start, r, c);
-    if (!h.found) return;
-#ifdef FMT_HUGE_CHECK
-    if (getenv("HUGE_DEBUG_SEQ") && atoi(getenv("HUGE_DEBUG_SEQ")) == seq)
-      std::fprintf(stderr, "range seq %d [%d,%d): hit gpos %d slot %d blk %u k %d st %d vis %d nGroups %d group %u count %u\n", seq, start,
-                   end, h.gpos, h.slot, h.blk, h.k, h.st, h.vis, nGroups, L->gOrder[h.gpos], L->gCount[L->gOrder[h.gpos]]);
-#endif
-#ifdef FMT_HUGE_CHECK
-    checkInvariants(seq);
-    if (getenv("HUGE_DEBUG_SEQ") && atoi(getenv("HUGE_DEBUG_SEQ")) == seq) {
-      for (int kk = 0; kk < 3; kk++) {
-        const uint32_t gg = L->gOrder[kk];
-        std::fprintf(stderr, "  gOrder[%d]=%u count %u:", kk, gg, L->gCount[gg]);
-        for (uint32_t q = 0; q < L->gCount[gg]; q++) std::fprintf(stderr, " %u", S.gSlotBlk[static_cast<size_t>(gg) * kSlotCap + q]);
-        std::fprintf(stderr, "\n");
+    const Hit h = find(start, r, c);
+    if (!h.found) return;  // nothing at or after start: no boundary, no hit
+    const uint32_t idStart = ldu(S.lId + li(h.blk, h.k));
+    // the leaf strictly containing end, walking from the start leaf
+    uint32_t idEnd = kNone;
+    int offEnd = 0;
+    {
+      uint32_t b = h.blk;
+      int k = h.k, pos = h.st;
+      while (b != kNone && pos < end && idEnd == kNone) {
+        const uint32_t cnt = ldu(S.bCount + b);
+        const Lane<uint32_t> vis = blockVis(b, cnt, r, c);
+        for (; k < static_cast<int>(cnt) && pos < end; k++) {
+          const int v = static_cast<int>(readlane(vis, k));
+          if (pos < end && end < pos + v) {
+            idEnd = ldu(S.lId + li(b, k));
+            offEnd = end - pos;
+            break;
+          }
+          pos += v;
+        }
+        if (idEnd == kNone && pos < end) {
+          b = nextBlockOf(b);
+          k = 0;
+        }
       }
     }
-#endif
-    // walk forward from the first leaf at `start` (view start h.st == start)
-    int k = h.gpos, s = h.slot;
-    uint32_t g = L->gOrder[k];
-    int pos = h.st;
-    int first = h.k;
-    for (;;) {
-      const uint32_t b = L->sBlk[s];
+    uint32_t first = idStart;
+    if (h.st < start) {  // ensureIntervalBoundary(start)
+      uint32_t right;
+      if (!splitLeaf(h.blk, h.k, start - h.st, &right)) return;
+      if (idEnd == idStart) {
+        idEnd = right;
+        offEnd -= start - h.st;
+      }
+      first = right;
+    }
+    if (idEnd != kNone && offEnd > 0) {  // ensureIntervalBoundary(end)
+      uint32_t b;
+      int k;
+      locate(idEnd, &b, &k);
+      if (!splitLeaf(b, k, offEnd)) return;
+    }
+    if (end <= start) return;
+    uint32_t b;
+    int k;
+    locate(first, &b, &k);
+    int pos = start;
+    while (b != kNone && pos < end) {
       const uint32_t cnt = ldu(S.bCount + b);
-#ifdef FMT_HUGE_CHECK
-      if (getenv("HUGE_DEBUG_SEQ") && atoi(getenv("HUGE_DEBUG_SEQ")) == seq)
-        std::fprintf(stderr, "  walk k %d g %u s %d blk %u cnt %u first %d pos %d\n", k, g, s, b, cnt, first, pos);
-#endif
-      bool done = false;
-      for (int j = first; j < static_cast<int>(cnt); j++) {
-        if (pos >= end) {
-          done = true;
-          break;
-        }
-        Leaf x = getLeaf(b, j);
-        const int v = visOf(x.len, x.ins, x.rm, x.mlo, x.mhi, mClient(x.meta), r, c);
+      const Lane<uint32_t> vis = blockVis(b, cnt, r, c);
+      for (; k < static_cast<int>(cnt) && pos < end; k++) {
+        const int v = static_cast<int>(readlane(vis, k));
         if (v > 0) {
-          if (op.type == FMT_MT_REMOVE) removeLeaf(b, j, x, seq, c);
-          else annotateLeaf(b, j, x, op.payload);
+          Leaf x = getLeaf(b, k);
+          if (op.type == FMT_MT_REMOVE) removeLeaf(b, k, x, seq, c);
+          else annotateLeaf(b, k, x, op.payload);
           if (status != FMT_OK) return;
           lru(b, x.id, seq);
           if (status != FMT_OK) return;
         }
         pos += v;
       }
-      if (done || pos >= end) break;
-      first = 0;
-      bool more = true;
-      for (++s; s >= static_cast<int>(L->gCount[g]);) {  // next slot, skipping empty groups
-        if (++k >= nGroups) {
-          more = false;
-          break;
-        }
-        g = L->gOrder[k];
-        slotLengths(g, r, c);
-        s = 0;
+      if (pos < end) {
+        b = nextBlockOf(b);
+        k = 0;
       }
-      if (!more) break;
     }
   }
 
@@ -1142,7 +1228,7 @@ class HugeDoc {
     } else {
       st1(S.wMeta + w, ldu(S.wMeta + w) | (1u << 16));  // a later remover: full set from the leaf
     }
-    corrValid = false;
+    invalidate();
   }
 
   FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId) {
@@ -1183,7 +1269,7 @@ class HugeDoc {
       if (rm == kNotRemoved) addStable(blk, static_cast<int>(len));
       w = e;
     }
-    corrValid = false;
+    invalidate();
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts:33-213)
@@ -1192,94 +1278,166 @@ class HugeDoc {
   // Returns the new leaf count.
   FMT_DEV int scourLeaves(uint32_t b) {
     const int cnt = static_cast<int>(ldu(S.bCount + b));
-    Leaf kept[kMaxNodes];
-    int nk = 0;
-    int prev = -1;
-    uint32_t firstText[kMaxNodes];   // merge runs: text of each piece, appended at the end
-    int runStart[kMaxNodes], runLen[kMaxNodes];
-    for (int i = 0; i < kMaxNodes; i++) runLen[i] = 0;
-    uint32_t pieceText[kMaxNodes], pieceLen[kMaxNodes];
-    int pieceOwner[kMaxNodes];
-    int nPieces = 0;
+    if (cnt == 0) return 0;
+    // every leaf of the block in one vector load per field (lane k = leaf k), plus its last unit
+    Lane<uint32_t> f[8];
+    Lane<uint32_t> lastCh;
+    FOR_LANES(l) {
+      const int k = l < cnt ? l : 0;
+      const size_t i = li(b, k);
+      LANE(f[0]) = rd(S.lLen + i);
+      LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
+      LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
+      LANE(f[3]) = rd(S.lMlo + i);
+      LANE(f[4]) = rd(S.lMhi + i);
+      LANE(f[5]) = rd(S.lId + i);
+      LANE(f[6]) = rd(S.lText + i);
+      LANE(f[7]) = rd(S.lMeta + i);
+      const uint32_t ln = LANE(f[0]);
+      LANE(lastCh) = ln > 0 ? loadWg(S.text + LANE(f[6]) + ln - 1) : 0u;
+    }
+    // serial decisions over <= 8 leaves (zamboni.ts:141-213): dest nibble k = output slot of leaf k,
+    // 0xF = dropped; a leaf appended onto the previous kept leaf takes that leaf's slot
+    uint32_t dest = 0, heads = 0;  // heads: bit q = output slot q keeps a merged run
+    uint32_t headLen[kMaxNodes];
+    int nk = 0, prev = -1;
+    uint32_t prevLen = 0, prevProps = 0, prevLast = 0;
     for (int k = 0; k < cnt; k++) {
-      Leaf x = getLeaf(b, k);
-      if (x.rm == kNotRemoved) {
-        if (x.ins <= minSeq) {
-          bool canAppend = false;
-          if (prev >= 0 && x.len > 0) {
-            const Leaf& pv = kept[prev];
-            const uint32_t lastCh = pv.len > 0 ? textAt(pieceLast(prev, pieceText, pieceLen, pieceOwner, nPieces)) : 0u;
-            canAppend = lastCh != 10u && (pv.len <= static_cast<uint32_t>(kGranularity) || x.len <= static_cast<uint32_t>(kGranularity)) &&
-                        propsMatch(mProps(pv.meta), mProps(x.meta));
-          }
+      const uint32_t len = readlane(f[0], k);
+      const int32_t ins = static_cast<int32_t>(readlane(f[1], k)), rm = static_cast<int32_t>(readlane(f[2], k));
+      const uint32_t props = mProps(readlane(f[7], k)), lc = readlane(lastCh, k);
+      uint32_t d;
+      if (rm == kNotRemoved) {
+        if (ins <= minSeq) {
+          const bool canAppend = prev >= 0 && len > 0 && prevLast != 10u &&
+                                 (prevLen <= static_cast<uint32_t>(kGranularity) || len <= static_cast<uint32_t>(kGranularity)) &&
+                                 propsMatch(prevProps, props);
           if (canAppend) {
-            kept[prev].len += x.len;
-            pieceText[nPieces] = x.text;
-            pieceLen[nPieces] = x.len;
-            pieceOwner[nPieces] = prev;
-            nPieces++;
-            runLen[prev]++;
-            st1(S.leafBlk + x.id, kNone);  // segment.parent = undefined (appended)
+            d = static_cast<uint32_t>(prev);
+            prevLen += len;
+            prevLast = lc;
+            headLen[prev] = prevLen;
+            heads |= 1u << prev;
           } else {
-            kept[nk] = x;
-            pieceText[nPieces] = x.text;
-            pieceLen[nPieces] = x.len;
-            pieceOwner[nPieces] = nk;
-            nPieces++;
-            runStart[nk] = k;
-            prev = x.len > 0 ? nk : -1;
+            d = static_cast<uint32_t>(nk);
+            headLen[nk] = len;
+            prev = len > 0 ? nk : -1;
+            prevLen = len;
+            prevProps = props;
+            prevLast = lc;
             nk++;
           }
         } else {
-          kept[nk] = x;
-          pieceText[nPieces] = x.text;
-          pieceLen[nPieces] = x.len;
-          pieceOwner[nPieces] = nk;
-          nPieces++;
-          nk++;
+          d = static_cast<uint32_t>(nk++);
           prev = -1;
         }
       } else {
-        if (x.rm <= minSeq) {
-          st1(S.leafBlk + x.id, kNone);  // unlinked
-          const uint32_t w = ldu(S.winIdx + x.id);
-          if (w != kNone) winRemove(w);  // (graduated already; kept for safety)
+        if (rm <= minSeq) {
+          d = 0xFu;
         } else {
-          kept[nk] = x;
-          pieceText[nPieces] = x.text;
-          pieceLen[nPieces] = x.len;
-          pieceOwner[nPieces] = nk;
-          nPieces++;
-          nk++;
+          d = static_cast<uint32_t>(nk++);
         }
         prev = -1;
       }
+      dest |= d << (4 * k);
     }
-    (void)firstText;
-    (void)runStart;
     if (nk == cnt) return cnt;  // nothing dropped or appended
-    // merged leaves get their text built once in the merge area
+    // merged runs: their text is rebuilt once in the merge area (lane t copies unit t)
+    uint32_t runDst[kMaxNodes];
+    uint32_t need = 0;
     for (int q = 0; q < nk; q++) {
-      if (runLen[q] == 0) continue;
-      const uint32_t total = kept[q].len;
-      if (textTop + total > S.textCap) {
-        fail(FMT_E_CAPACITY);
-        return cnt;
+      if ((heads >> q) & 1u) {
+        runDst[q] = static_cast<uint32_t>(textTop + need);
+        need += headLen[q];
+      } else {
+        runDst[q] = 0;
       }
-      const uint32_t dst = static_cast<uint32_t>(textTop);
-      uint32_t o = 0;
-      for (int pi = 0; pi < nPieces; pi++) {
-        if (pieceOwner[pi] != q) continue;
-        copyText(dst + o, pieceText[pi], pieceLen[pi]);
-        o += pieceLen[pi];
-      }
-      textTop += total;
-      kept[q].text = dst;
     }
-    for (int q = 0; q < nk; q++) putLeaf(b, q, kept[q]);
+    if (textTop + need > S.textCap) {
+      fail(FMT_E_CAPACITY);
+      return cnt;
+    }
+    if (need) {
+      // per leaf k of a merged run: its offset inside the run
+      uint32_t runOff[kMaxNodes], srcStart[kMaxNodes];  // (uniform)
+      uint32_t acc[kMaxNodes] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint32_t flat = 0;
+      for (int k = 0; k < cnt; k++) {
+        const uint32_t d = (dest >> (4 * k)) & 0xFu;
+        srcStart[k] = flat;
+        if (d != 0xFu && ((heads >> d) & 1u)) {
+          runOff[k] = acc[d];
+          acc[d] += readlane(f[0], k);
+          flat += readlane(f[0], k);
+        } else {
+          runOff[k] = 0xFFFFFFFFu;
+        }
+      }
+      for (uint32_t base = 0; base < flat; base += 64) {
+        Lane<uint32_t> v, dstIdx;
+        FOR_LANES(l) {
+          const uint32_t t = base + l;
+          uint32_t val = 0, di = 0xFFFFFFFFu;
+          if (t < flat) {
+            for (int k = 0; k < cnt; k++) {
+              if (runOff[k] != 0xFFFFFFFFu && t >= srcStart[k] && t < srcStart[k] + readlaneU(f[0], k)) {
+                const uint32_t d = (dest >> (4 * k)) & 0xFu;
+                const uint32_t o = t - srcStart[k];
+                val = loadWg(S.text + readlaneU(f[6], k) + o);
+                di = runDst[d] + runOff[k] + o;
+              }
+            }
+          }
+          LANE(v) = val;
+          LANE(dstIdx) = di;
+        }
+        waveSync();
+        FOR_LANES(l) {
+          if (LANE(dstIdx) != 0xFFFFFFFFu) S.text[LANE(dstIdx)] = static_cast<uint16_t>(LANE(v));
+        }
+        waveSync();
+      }
+      textTop += need;
+    }
+    // output slot q takes its head leaf (the first leaf with dest q); gone leaves leave the tree
+    Lane<int> src;
+    FOR_LANES(l) {
+      int sidx = 0;
+      for (int k = cnt - 1; k >= 0; k--)
+        if (((dest >> (4 * k)) & 0xFu) == static_cast<uint32_t>(l)) sidx = k;
+      LANE(src) = sidx;
+    }
+    Lane<uint32_t> g[8];
+#pragma unroll
+    for (int x = 0; x < 8; x++) g[x] = gather(f[x], src);
+    FOR_LANES(l) {
+      if (l < nk) {
+        const size_t i = li(b, l);
+        const bool merged = ((heads >> l) & 1u) != 0;
+        S.lLen[i] = merged ? headLen[l] : LANE(g[0]);
+        S.lIns[i] = static_cast<int32_t>(LANE(g[1]));
+        S.lRm[i] = static_cast<int32_t>(LANE(g[2]));
+        S.lMlo[i] = LANE(g[3]);
+        S.lMhi[i] = LANE(g[4]);
+        S.lId[i] = LANE(g[5]);
+        S.lText[i] = merged ? runDst[l] : LANE(g[6]);
+        S.lMeta[i] = LANE(g[7]);
+      }
+      if (l < cnt) {  // appended or dropped leaves: segment.parent = undefined
+        const uint32_t d = (dest >> (4 * l)) & 0xFu;
+        bool head = d != 0xFu;  // the first leaf with output slot d (lane-local: no cross-lane read)
+        for (int k = 0; k < kMaxNodes; k++)
+          if (k < l && ((dest >> (4 * k)) & 0xFu) == d) head = false;
+        if (!head) S.leafBlk[LANE(f[5])] = kNone;
+      }
+    }
+    waveSync();
     st1(S.bCount + b, static_cast<uint32_t>(nk));
     return nk;
   }
+
+  FMT_DEV static uint32_t readlaneU(const Lane<uint32_t>& x, int k) { return readlane(x, k); }
+  FMT_DEV static uint32_t readlaneU(const Lane<int>& x, int k) { return static_cast<uint32_t>(readlane(x, k)); }
 
   FMT_DEV static int pieceLast(int owner, const uint32_t* pt, const uint32_t* pl, const int* po, int n) {
     int last = -1;
@@ -1287,11 +1445,11 @@ class HugeDoc {
       if (po[i] == owner) last = i;
     return static_cast<int>(pt[last] + pl[last] - 1);
   }
-  FMT_DEV uint32_t textAt(int i) const { return loadCoherent(S.text + i); }
+  FMT_DEV uint32_t textAt(int i) const { return loadWg(S.text + i); }
   FMT_DEV void copyText(uint32_t dst, uint32_t src, uint32_t n) {
     for (uint32_t base = 0; base < n; base += 64) {
       Lane<uint32_t> v;
-      FOR_LANES(l) { LANE(v) = base + l < n ? loadCoherent(S.text + src + base + l) : 0u; }
+      FOR_LANES(l) { LANE(v) = base + l < n ? loadWg(S.text + src + base + l) : 0u; }
       waveSync();
       FOR_LANES(l) {
         if (base + l < n) S.text[dst + base + l] = static_cast<uint16_t>(LANE(v));
@@ -1305,81 +1463,116 @@ class HugeDoc {
   // reused for the new ones (block identity is not observable); the rest are freed and unlisted.
   FMT_DEV void packLeafParent(uint32_t p) {
     const int pc = static_cast<int>(ldu(S.bCount + p));
-    int total = 0;
-    for (int i = 0; i < pc; i++) total += scourLeaves(childAt(p, i));
-    if (status != FMT_OK) return;
-    // stage every held leaf (document order) in LDS tmp as (block, slot) pairs → gather records
-    constexpr int kMaxHeld = kMaxNodes * kMaxNodes;
     uint32_t oldBlk[kMaxNodes];
     for (int i = 0; i < pc; i++) oldBlk[i] = childAt(p, i);
-    Leaf held[kMaxHeld];
-    int n = 0;
+    // scour every child, staging its held leaves (document order) in LDS
+    int total = 0;
     for (int i = 0; i < pc; i++) {
       const uint32_t b = oldBlk[i];
-      const int cnt = static_cast<int>(ldu(S.bCount + b));
-      for (int k = 0; k < cnt; k++) held[n++] = getLeaf(b, k);
+      const int cnt = scourLeaves(b);
+      if (status != FMT_OK) return;
+      FOR_LANES(l) {
+        if (l < cnt) {
+          const size_t x = li(b, l);
+          L->held[0][total + l] = rd(S.lLen + x);
+          L->held[1][total + l] = static_cast<uint32_t>(rd(S.lIns + x));
+          L->held[2][total + l] = static_cast<uint32_t>(rd(S.lRm + x));
+          L->held[3][total + l] = rd(S.lMlo + x);
+          L->held[4][total + l] = rd(S.lMhi + x);
+          L->held[5][total + l] = rd(S.lId + x);
+          L->held[6][total + l] = rd(S.lText + x);
+          L->held[7][total + l] = rd(S.lMeta + x);
+        }
+      }
+      waveSync();
+      total += cnt;
     }
-    const uint32_t g0 = ldu(S.bGroup + oldBlk[0]);
-    const int s0 = static_cast<int>(ldu(S.bSlot + oldBlk[0]));
     int nb = 0;
     if (total > 0) {
       nb = total / (kMaxNodes / 2);
       if (nb > kMaxNodes - 1) nb = kMaxNodes - 1;
       if (nb < 1) nb = 1;
     }
-    uint32_t newBlk[kMaxNodes];  // the first old blocks are reused, more are allocated when nb > pc
-    for (int q = 0; q < nb; q++) {
-      newBlk[q] = q < pc ? oldBlk[q] : allocBlk(1);
-      if (newBlk[q] == kNone) return;
-    }
-    // unlist the old blocks (they are consecutive slots, possibly across groups), then list the new
-    int removedStable = 0;
-    for (int i = 0; i < pc; i++) {
-      const uint32_t b = oldBlk[i];
-      const uint32_t g = ldu(S.bGroup + b);
-      const int s = static_cast<int>(ldu(S.bSlot + b));
-      removedStable += ldi(slotStPtr(g) + s);
-      slotRemove(g, s, 1);
-    }
-    (void)removedStable;
+    // The new blocks reuse the first old blocks' ids AND their slots (document order is unchanged);
+    // old blocks past nb are unlisted and freed, extra new blocks are listed after the last old one.
     const int base = nb ? total / nb : 0;
     int rem = nb ? total % nb : 0;
     int consumed = 0;
-    uint32_t gIns = g0;
-    int sIns = s0;
-    if (sIns > static_cast<int>(L->gCount[gIns])) sIns = static_cast<int>(L->gCount[gIns]);
     for (int q = 0; q < nb; q++) {
       int cnt = base;
       if (rem > 0) {
         cnt++;
         rem--;
       }
-      const uint32_t b = newBlk[q];
-      st1(S.bLeaf + b, 1u);
-      for (int k = 0; k < cnt; k++) {
-        putLeaf(b, k, held[consumed + k]);
-        const uint32_t w = ldu(S.winIdx + held[consumed + k].id);
-        if (w != kNone) st1(S.wBlk + w, b);
+      uint32_t b;
+      if (q < pc) {
+        b = oldBlk[q];
+      } else {
+        b = allocBlk(1);
+        if (b == kNone) return;
+        const uint32_t pb = L->tmp[q - 1];  // (q >= pc >= 1) the previous new block
+        const uint32_t g = ldu(S.bGroup + pb);
+        st1(S.bGroup + b, g);
+        st1(S.bCount + b, 0u);
+        if (!slotInsert(g, static_cast<int>(ldu(S.bSlot + pb)) + 1, b, 0)) return;
       }
+      L->tmp[q] = b;
+      waveSync();
+      const uint32_t g = ldu(S.bGroup + b);
+      FOR_LANES(l) {
+        if (l < cnt) {
+          const size_t x = li(b, l);
+          const int h = consumed + l;
+          const uint32_t id = L->held[5][h];
+          S.lLen[x] = L->held[0][h];
+          S.lIns[x] = static_cast<int32_t>(L->held[1][h]);
+          S.lRm[x] = static_cast<int32_t>(L->held[2][h]);
+          S.lMlo[x] = L->held[3][h];
+          S.lMhi[x] = L->held[4][h];
+          S.lId[x] = id;
+          S.lText[x] = L->held[6][h];
+          S.lMeta[x] = L->held[7][h];
+          S.leafBlk[id] = b;
+          const uint32_t w = rd(S.winIdx + id);
+          if (w != kNone) {
+            S.wBlk[w] = b;
+            S.wGroup[w] = g;
+          }
+        }
+      }
+      waveSync();
       st1(S.bCount + b, static_cast<uint32_t>(cnt));
+      st1(S.bLeaf + b, 1u);
       st1(S.bParent + b, p);
       st1(S.bScour + b, -1);
       st1(S.bChild + static_cast<size_t>(p) * 8 + q, b);
       consumed += cnt;
       const int stB = blockStable(b);
-      if (!slotInsert(gIns, sIns, b, stB)) return;
-      gIns = ldu(S.bGroup + b);
-      sIns = static_cast<int>(ldu(S.bSlot + b)) + 1;
+      const int s0 = static_cast<int>(ldu(S.bSlot + b));
+      int32_t* sp = slotStPtr(g) + s0;
+      const int32_t old = ldi(sp);
+      st1(sp, stB);
+      L->gStable[g] += stB - old;
+      waveSync();
     }
-    for (int q = 0; q < nb; q++) retagWindow(newBlk[q]);  // re-listed leaves: block and group
+    // unlist and free the old blocks past nb (consecutive slots, possibly in two groups)
     for (int i = nb; i < pc; i++) {
-      st1(S.bCount + oldBlk[i], 0u);
-      freeBlock(oldBlk[i]);
+      const uint32_t b = oldBlk[i];
+      const uint32_t g = ldu(S.bGroup + b);
+      const int s0 = static_cast<int>(ldu(S.bSlot + b));
+      int run = 1;  // the following old blocks in the same group are the next slots
+      while (i + run < pc && ldu(S.bGroup + oldBlk[i + run]) == g) run++;
+      slotRemove(g, s0, run);
+      for (int k = 0; k < run; k++) {
+        st1(S.bCount + oldBlk[i + k], 0u);
+        freeBlock(oldBlk[i + k]);
+      }
+      i += run - 1;
     }
     st1(S.bCount + p, static_cast<uint32_t>(nb));
     if (nb == 0 && static_cast<int>(p) == root) fail(FMT_E_UNSUPPORTED);  // document emptied by zamboni
     if (lastBlk != kNone) updateLastBlk();
-    corrValid = false;
+    invalidate();
   }
 
   FMT_DEV void updateLastBlk() {
@@ -1611,7 +1804,7 @@ class HugeDoc {
       const fmt_mt_op op = decodeOp(rec0);
       rec0 = rec1;
       rec1 = fetchOp(i + 2);
-      corrValid = false;
+      invalidate();
 #ifdef FMT_HUGE_CHECK
       checkPerspective(op.seq, op.ref_seq, op.client);
 #endif
@@ -1687,7 +1880,7 @@ class HugeDoc {
         return;
       }
     }
-    corrValid = false;
+    invalidate();
   }
 
   // Host emulation only (tests/emu/huge_emu.cpp): every index structure agrees with the leaves.
@@ -1792,7 +1985,7 @@ class HugeDoc {
             x.pad = static_cast<uint16_t>(blk >> 16);
             outLeaves[o] = x;
             const uint32_t t = rd(S.lText + i);
-            for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(loadCoherent(S.text + t + c));
+            for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(loadWg(S.text + t + c));
           }
         }
         nLeaves += tv;

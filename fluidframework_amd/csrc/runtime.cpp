@@ -505,7 +505,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       fmt_huge::HugeState& S = H.state;
       S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
       S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
-      S.winCap = static_cast<uint32_t>(3 * nOps + 1024);
+      S.winCap = S.idCap;  // every leaf can be in the window (a wide remove puts many there)
       const uint64_t textCap = std::min<uint64_t>(b->text_len + 256 * nOps + 65536, 0xFFFFFFF0ull);
       const size_t nl = static_cast<size_t>(S.blockCap) * 8, nb = S.blockCap;
       void* p;

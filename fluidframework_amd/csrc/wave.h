@@ -58,6 +58,12 @@ FMT_DEV uint32_t loadCoherent(const uint32_t* p) {
 FMT_DEV int32_t loadCoherent(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A global value this workgroup wrote: a workgroup-scope atomic load is a plain vector load (served by
+// the CU's L1, which this CU's own stores keep current) that the compiler never turns into a scalar
+// (K$) load, whose cache vector stores do not update.
+FMT_DEV uint32_t loadWg(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+FMT_DEV int32_t loadWg(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+FMT_DEV uint32_t loadWg(const uint16_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // LDS add from one lane of many (ds_add_u32); the host emulation runs lanes one after another.
 FMT_DEV void atomicAddLds(int32_t* p, int v) { atomicAdd(p, v); }
 
@@ -210,6 +216,9 @@ inline void launder(V8&) {}
 inline uint32_t loadCoherent(const uint16_t* p) { return *p; }
 inline uint32_t loadCoherent(const uint32_t* p) { return *p; }
 inline int32_t loadCoherent(const int32_t* p) { return *p; }
+inline uint32_t loadWg(const uint32_t* p) { return *p; }
+inline int32_t loadWg(const int32_t* p) { return *p; }
+inline uint32_t loadWg(const uint16_t* p) { return *p; }
 inline void atomicAddLds(int32_t* p, int v) { *p += v; }
 
 inline uint64_t ballot(const Lane<bool>& p) {

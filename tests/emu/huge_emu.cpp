@@ -27,7 +27,7 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   HugeState S{};
   S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
   S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
-  S.winCap = static_cast<uint32_t>(3 * nOps + 1024);
+  S.winCap = S.idCap;  // every leaf can be in the window (wide removes)
   const uint64_t textCap = b->text_len + 256 * nOps + 65536;
   std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6);
   std::vector<int32_t> i32(static_cast<size_t>(S.blockCap) * 8 * 2);
