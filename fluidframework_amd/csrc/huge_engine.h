@@ -60,8 +60,23 @@ FMT_DEV uint32_t mProps(uint32_t m) { return (m >> 8) & 0xFFFFu; }
 FMT_DEV uint32_t mkMeta(int32_t client, uint32_t props) { return (static_cast<uint32_t>(client) & 0xFFu) | (props << 8); }
 constexpr uint32_t kNoProps = 0xFFFFu;
 
-// Window meta word: insert client (int8) | first remover (u8) << 8 | "more removers" << 16
+// Window meta word: insert client (int8) | first remover (u8) << 8 | "more removers" << 16; the
+// record's word 3 adds the entry's group << 17
 FMT_DEV uint32_t wFirstRm(uint32_t m) { return (m >> 8) & 0xFFu; }
+constexpr uint32_t kWMetaMask = 0x1FFFFu;
+constexpr int kWGroupShift = 17;
+constexpr int kWinList = 1024;  // LDS list of one group's visible window entries (slot pass)
+
+typedef uint32_t u32x4 __attribute__((vector_size(16)));
+FMT_DEV u32x4 ld4(const uint32_t* p) {  // one 16-byte vector load (p 16-byte aligned)
+#if FMT_GPU
+  return *reinterpret_cast<const u32x4*>(p);
+#else
+  u32x4 v;
+  __builtin_memcpy(&v, p, sizeof v);
+  return v;
+#endif
+}
 
 struct HeapEnt {
   int32_t maxSeq;
@@ -96,12 +111,9 @@ struct HugeState {
   uint32_t* leafBlk;
   uint32_t* winIdx;
   uint32_t idCap;
-  // window table [winCap]
-  int32_t* wIns;
-  int32_t* wRm;
-  uint32_t* wLen;
-  uint32_t* wMeta;
-  uint32_t* wGroup;
+  // window table [winCap]: one 16-byte record per entry {ins, rm, len, meta | group << 17} (one
+  // vector load per entry in the window passes), plus the entry's leaf block and leaf id
+  uint32_t* wRec;
   uint32_t* wBlk;
   uint32_t* wLeaf;
   uint32_t winCap;
@@ -122,8 +134,9 @@ struct HugeLds {
   int32_t sLen[kSlotCap];        // the group being searched: view length per slot
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
-  uint32_t held[8][kMaxNodes * kMaxNodes];  // packParent: the held leaves' 8 fields, document order
   uint32_t tmp[256];
+  uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
+  int32_t wlVis[kWinList];
 };
 
 struct HugeInputs {
@@ -164,9 +177,18 @@ class HugeDoc {
   int curSeq = 0, minSeq = 0;
   int status = FMT_OK, failSeq = 0;
   uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
-  // shader-clock totals per phase (diagnostics, written to HugeOut::prof): 0 replay, 1 window pass
-  // (groups), 2 window pass (slots), 3 zamboni, 4 graduation, 5 load, 6 output, 7 finds
-  uint64_t prof[8] = {};
+  // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
+  // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
+  // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
+  // 12 insert, 13 range ops, 14 leaf split, 15 interior pack
+  static constexpr int kProf = 16;
+  uint64_t prof[kProf] = {};
+  struct ProfScope {
+    uint64_t& a;
+    uint64_t t;
+    FMT_DEV explicit ProfScope(uint64_t& acc) : a(acc), t(clk()) {}
+    FMT_DEV ~ProfScope() { a += clk() - t; }
+  };
   FMT_DEV static uint64_t clk() {
 #if FMT_GPU
     return __builtin_amdgcn_s_memtime();
@@ -243,11 +265,11 @@ class HugeDoc {
     const uint32_t w = nWin++;
     FOR_LANES(l) {
       if (l == 0) {
-        S.wIns[w] = ins;
-        S.wRm[w] = rm;
-        S.wLen[w] = len;
-        S.wMeta[w] = meta;
-        S.wGroup[w] = grp;
+        uint32_t* rec = S.wRec + static_cast<size_t>(w) * 4;
+        rec[0] = static_cast<uint32_t>(ins);
+        rec[1] = static_cast<uint32_t>(rm);
+        rec[2] = len;
+        rec[3] = (meta & kWMetaMask) | (grp << kWGroupShift);
         S.wBlk[w] = blk;
         S.wLeaf[w] = id;
         S.winIdx[id] = w;
@@ -259,16 +281,16 @@ class HugeDoc {
     const uint32_t last = nWin - 1;
     const uint32_t id = ldu(S.wLeaf + w);
     if (w != last) {
-      const int32_t a = ldi(S.wIns + last), b = ldi(S.wRm + last);
-      const uint32_t c = ldu(S.wLen + last), d = ldu(S.wMeta + last), e = ldu(S.wGroup + last),
-                     f = ldu(S.wBlk + last), g = ldu(S.wLeaf + last);
+      const uint32_t* src = S.wRec + static_cast<size_t>(last) * 4;
+      const uint32_t a = ldu(src), b = ldu(src + 1), c = ldu(src + 2), d = ldu(src + 3);
+      const uint32_t f = ldu(S.wBlk + last), g = ldu(S.wLeaf + last);
       FOR_LANES(l) {
         if (l == 0) {
-          S.wIns[w] = a;
-          S.wRm[w] = b;
-          S.wLen[w] = c;
-          S.wMeta[w] = d;
-          S.wGroup[w] = e;
+          uint32_t* rec = S.wRec + static_cast<size_t>(w) * 4;
+          rec[0] = a;
+          rec[1] = b;
+          rec[2] = c;
+          rec[3] = d;
           S.wBlk[w] = f;
           S.wLeaf[w] = g;
           S.winIdx[g] = w;
@@ -277,6 +299,14 @@ class HugeDoc {
     }
     st1(S.winIdx + id, kNone);
     nWin = last;
+  }
+
+  FMT_DEV uint32_t* wWord(uint32_t w, int f) const { return S.wRec + static_cast<size_t>(w) * 4 + f; }
+  FMT_DEV uint32_t* wWord3(uint32_t w) const { return wWord(w, 3); }
+  // an entry's leaf moved to block b (of group g)
+  FMT_DEV void wRetag(uint32_t w, uint32_t b, uint32_t g) {
+    S.wBlk[w] = b;
+    *wWord3(w) = (rd(wWord3(w)) & kWMetaMask) | (g << kWGroupShift);
   }
 
   // ------------------------------------------------------------------ stable sums
@@ -329,15 +359,17 @@ class HugeDoc {
   // Insert leaf block nb into group g at slot `at` with stable length st (slots at/after shift up).
   // Splits the group first when it is full; returns false on failure.
   FMT_DEV bool slotInsert(uint32_t g, int at, uint32_t nb, int st) {
+    ProfScope ps_(prof[10]);
     invalidate();
     int cnt = static_cast<int>(L->gCount[g]);
     if (cnt >= kSlotCap) {
       if (!groupSplit(g)) return false;
       cnt = static_cast<int>(L->gCount[g]);
-      if (at > cnt) {  // the slot moved to the new group
+      if (at > cnt) {  // the slot moved to the new group (half full: no second split)
         const int gp = groupPos(g);
-        const uint32_t g2 = L->gOrder[gp + 1];
-        return slotInsert(g2, at - cnt, nb, st);
+        g = L->gOrder[gp + 1];
+        at -= cnt;
+        cnt = static_cast<int>(L->gCount[g]);
       }
     }
     uint32_t* sb = slotBlkPtr(g);
@@ -388,6 +420,7 @@ class HugeDoc {
   // Remove slots [at, at + n) of group g (their blocks are being freed or moved); returns the
   // stable length they held.
   FMT_DEV void slotRemove(uint32_t g, int at, int n) {
+    ProfScope ps_(prof[10]);
     invalidate();
     const int cnt = static_cast<int>(L->gCount[g]);
     uint32_t* sb = slotBlkPtr(g);
@@ -474,7 +507,10 @@ class HugeDoc {
     for (uint32_t base = 0; base < nWin; base += 64) {
       FOR_LANES(l) {
         const uint32_t w = base + l;
-        if (w < nWin && rd(S.wGroup + w) == g) S.wGroup[w] = rd(S.bGroup + (rd(S.wBlk + w)));
+        if (w < nWin) {
+          const uint32_t m = rd(wWord3(w));
+          if ((m >> kWGroupShift) == g) *wWord3(w) = (m & kWMetaMask) | (rd(S.bGroup + (rd(S.wBlk + w))) << kWGroupShift);
+        }
       }
     }
     invalidate();
@@ -502,37 +538,74 @@ class HugeDoc {
     return ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(len) : 0;
   }
 
-  // One pass over the window table, 4 x 64 entries per step with every load of a step in flight
-  // together: for each entry of positive view length (and of group `only`, unless kNone), add it to
-  // gCorr[group] (bySlot false) or to sLen[slot of its block] (bySlot true).
+  // One pass over the window table, 16 x 64 records per step with every load of a step in flight
+  // together (one 16-byte load per record): for each entry of positive view length, add it to
+  // gCorr[group] (bySlot false); or (bySlot true) for each such entry of group `only`, add it to
+  // sLen[slot of its block] — those entries are first listed in LDS, then their blocks' slots are
+  // loaded for the whole list at once.
+  static constexpr int kPassU = 16;
   FMT_DEV void windowPass(int r, int c, uint32_t only, bool bySlot) {
-    for (uint32_t base = 0; base < nWin; base += 256) {
-      Lane<int32_t> ins[4], rm[4];
-      Lane<uint32_t> len[4], m[4], grp[4];
+    int nList = 0;
+    for (uint32_t base = 0; base < nWin; base += 64 * kPassU) {
+      Lane<u32x4> rec[kPassU];
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kPassU; u++) {
           const uint32_t w = base + 64 * u + l;
-          if (w < nWin) {
-            LANE(ins[u]) = rd(S.wIns + w);
-            LANE(rm[u]) = rd(S.wRm + w);
-            LANE(len[u]) = rd(S.wLen + w);
-            LANE(m[u]) = rd(S.wMeta + w);
-            LANE(grp[u]) = rd(S.wGroup + w);
-          }
+          if (w < nWin) LANE(rec[u]) = ld4(S.wRec + static_cast<size_t>(w) * 4);
         }
       }
+      Lane<uint32_t> vis[kPassU];
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kPassU; u++) {
           const uint32_t w = base + 64 * u + l;
-          if (w < nWin && (only == kNone || LANE(grp[u]) == only)) {
-            const int v = winVis(w, LANE(ins[u]), LANE(rm[u]), LANE(len[u]), LANE(m[u]), r, c);
-            if (v) {
-              if (bySlot) atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + w))], v);
-              else atomicAddLds(&L->gCorr[LANE(grp[u])], v);
+          uint32_t v = 0;
+          if (w < nWin) {
+            const u32x4 x = LANE(rec[u]);
+            const uint32_t grp = x[3] >> kWGroupShift;
+            if (only == kNone || grp == only) {
+              v = static_cast<uint32_t>(winVis(w, static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, r, c));
+              if (v && !bySlot) atomicAddLds(&L->gCorr[grp], static_cast<int>(v));
             }
           }
+          LANE(vis[u]) = v;
+        }
+      }
+      if (bySlot) {
+        // compact this step's hits into the LDS list (entry, view length)
+#pragma unroll
+        for (int u = 0; u < kPassU; u++) {
+          Lane<bool> hit;
+          FOR_LANES(l) { LANE(hit) = LANE(vis[u]) != 0; }
+          const uint64_t m = ballot(hit);
+          if (!m) continue;
+          if (nList + 64 > kWinList) {
+            flushSlotList(nList);
+            nList = 0;
+          }
+          FOR_LANES(l) {
+            if ((m >> l) & 1ull) {
+              const int at = nList + __builtin_popcountll(m & ((1ull << l) - 1));
+              L->wlEnt[at] = base + 64 * u + l;
+              L->wlVis[at] = static_cast<int32_t>(LANE(vis[u]));
+            }
+          }
+          nList += __builtin_popcountll(m);
+        }
+      }
+    }
+    if (bySlot && nList) flushSlotList(nList);
+    waveSync();
+  }
+  // sLen[slot of the block of listed entry i] += its view length, for the n listed entries.
+  FMT_DEV void flushSlotList(int n) {
+    waveSync();
+    for (int base = 0; base < n; base += 64) {
+      FOR_LANES(l) {
+        if (base + l < n) {
+          const uint32_t w = L->wlEnt[base + l];
+          atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + w))], L->wlVis[base + l]);
         }
       }
     }
@@ -541,8 +614,7 @@ class HugeDoc {
   // gCorr[g] = Σ view length of the window leaves of group g (their stable contribution is 0), and
   // gStart[k] = view start of the k-th group, for PriorPerspective(r, c).
   FMT_DEV void groupCorrections(int r, int c) {
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[1], t0_};
+    ProfScope ps_(prof[1]);
     FOR_LANES(l) {
       for (int g = l; g < nGroups; g += 64) L->gCorr[g] = 0;
     }
@@ -581,8 +653,7 @@ class HugeDoc {
   FMT_DEV void slotLengths(uint32_t g, int r, int c) {
     slotCacheG = g;
     slotCacheEpoch = epoch;
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[2], t0_};
+    ProfScope ps_(prof[2]);
     const int cnt = static_cast<int>(L->gCount[g]);
     const uint32_t* sb = slotBlkPtr(g);
     const int32_t* ss = slotStPtr(g);
@@ -618,8 +689,7 @@ class HugeDoc {
   // The first leaf (document order) with st <= p < st + vis, or st == p, vis == 0 and not skipped
   // (removed at/below minSeq, unless it is the document's very last leaf).
   FMT_DEV Hit find(int p, int r, int c) {
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[7], t0_};
+    ProfScope ps_(prof[7]);
     Hit h;
     h.found = false;
     if (!corrValid) groupCorrections(r, c);
@@ -824,10 +894,7 @@ class HugeDoc {
     FOR_LANES(l) {
       if (l < static_cast<int>(cnt)) {
         const uint32_t w = rd(S.winIdx + rd(S.lId + li(b, l)));
-        if (w != kNone) {
-          S.wGroup[w] = g;
-          S.wBlk[w] = b;
-        }
+        if (w != kNone) wRetag(w, b, g);
       }
     }
     waveSync();
@@ -894,43 +961,56 @@ class HugeDoc {
 
   // ------------------------------------------------------------------ LRU heap (heap.ts)
   FMT_DEV int heapSeq(int k) const { return uni(L->heap[k].maxSeq); }
-  FMT_DEV void heapSwap(int a, int b) {
-    const HeapEnt x = L->heap[a], y = L->heap[b];
-    waveSync();
-    L->heap[a] = y;
-    L->heap[b] = x;
-    waveSync();
-  }
+  // heap.ts sift order, moving a hole instead of swapping (the same final arrangement)
   FMT_DEV void heapAdd(int maxSeq, uint32_t leafId) {
+    ProfScope ps_(prof[11]);
     if (heapN >= kHeapCap) {
       fail(FMT_E_CAPACITY);
       return;
     }
-    heapN++;
-    L->heap[heapN].maxSeq = maxSeq;
-    L->heap[heapN].leafId = leafId;
-    waveSync();
-    int k = heapN;
-    while (k > 1 && heapSeq(k >> 1) - heapSeq(k) > 0) {
-      heapSwap(k, k >> 1);
+    int k = ++heapN;
+    while (k > 1) {
+      const HeapEnt up = L->heap[k >> 1];
+      if (!(uni(up.maxSeq) - maxSeq > 0)) break;
+      waveSync();
+      L->heap[k] = up;
       k >>= 1;
     }
+    waveSync();
+    L->heap[k].maxSeq = maxSeq;
+    L->heap[k].leafId = leafId;
+    waveSync();
   }
   FMT_DEV HeapEnt heapGet() {
-    heapSwap(1, heapN);
-    HeapEnt x;
-    x.maxSeq = uni(L->heap[heapN].maxSeq);
-    x.leafId = uni(L->heap[heapN].leafId);
+    ProfScope ps_(prof[11]);
+    HeapEnt top;
+    top.maxSeq = uni(L->heap[1].maxSeq);
+    top.leafId = uni(L->heap[1].leafId);
+    const HeapEnt x = L->heap[heapN];  // the last entry sifts down from the root
+    const int xs = uni(x.maxSeq);
+    waveSync();
     heapN--;
     int k = 1;
     while ((k << 1) <= heapN) {
       int j = k << 1;
-      if (j < heapN && heapSeq(j) - heapSeq(j + 1) > 0) j++;
-      if (heapSeq(k) - heapSeq(j) <= 0) break;
-      heapSwap(k, j);
+      int js = heapSeq(j);
+      if (j < heapN) {
+        const int j2 = heapSeq(j + 1);
+        if (js - j2 > 0) {
+          j++;
+          js = j2;
+        }
+      }
+      if (xs - js <= 0) break;
+      const HeapEnt c = L->heap[j];
+      waveSync();
+      L->heap[k] = c;
       k = j;
     }
-    return x;
+    waveSync();
+    if (heapN >= 1) L->heap[k] = x;
+    waveSync();
+    return top;
   }
 
   // addToLRUSet (mergeTree.ts:812-822): the first registration of a block sets needsScour.
@@ -1017,6 +1097,7 @@ class HugeDoc {
   // splitLeafSegment (mergeTree.ts:1768-1796) of leaf (b, k) at offset o (0 < o < len): the right part
   // follows it in the same block, with a fresh id; a window leaf's right part joins the window table.
   FMT_DEV bool splitLeaf(uint32_t b, int k, int o, uint32_t* rightId = nullptr) {
+    ProfScope ps_(prof[14]);
     invalidate();
     Leaf x = getLeaf(b, k);
     if (nextId >= S.idCap) return fail(FMT_E_CAPACITY);
@@ -1032,8 +1113,8 @@ class HugeDoc {
     putLeaf(b, k + 1, y);
     const uint32_t w = ldu(S.winIdx + x.id);
     if (w != kNone) {
-      st1(S.wLen + w, x.len);
-      winAdd(y.id, y.ins, y.rm, y.len, ldu(S.wMeta + w), ldu(S.bGroup + b), b);
+      st1(wWord(w, 2), x.len);
+      winAdd(y.id, y.ins, y.rm, y.len, ldu(wWord3(w)) & kWMetaMask, ldu(S.bGroup + b), b);
     } else {
       st1(S.winIdx + y.id, kNone);
     }
@@ -1068,6 +1149,7 @@ class HugeDoc {
   // from one search: the new leaf goes before the first qualifying leaf at p, or before the right part
   // of the leaf that strictly contained p.
   FMT_DEV void insertText(const fmt_mt_op& op) {
+    ProfScope ps_(prof[12]);
     const int r = op.ref_seq, c = op.client, p = op.pos1;
     const Hit h = find(p, r, c);
     uint32_t b;
@@ -1139,6 +1221,7 @@ class HugeDoc {
   // (ensureIntervalBoundary moves no view position), then the hits are walked block by block:
   // the leaves of positive view length inside [start, end).
   FMT_DEV void applyRange(const fmt_mt_op& op) {
+    ProfScope ps_(prof[13]);
     const int r = op.ref_seq, c = op.client, seq = op.seq;
     const int start = op.pos1, end = op.pos2;
     const Hit h = find(start, r, c);
@@ -1223,10 +1306,11 @@ class HugeDoc {
       winAdd(x.id, x.ins, x.rm, x.len, (mkMeta(mClient(x.meta), 0) & 0xFFu) | (static_cast<uint32_t>(c) << 8),
              ldu(S.bGroup + b), b);
     } else if (!was) {
-      st1(S.wRm + w, x.rm);
-      st1(S.wMeta + w, (ldu(S.wMeta + w) & 0xFFu) | (static_cast<uint32_t>(c) << 8));
+      const uint32_t m3 = ldu(wWord3(w));
+      st1(wWord(w, 1), static_cast<uint32_t>(x.rm));
+      st1(wWord3(w), (m3 & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(c) << 8));
     } else {
-      st1(S.wMeta + w, ldu(S.wMeta + w) | (1u << 16));  // a later remover: full set from the leaf
+      st1(wWord3(w), ldu(wWord3(w)) | (1u << 16));  // a later remover: full set from the leaf
     }
     invalidate();
   }
@@ -1242,8 +1326,7 @@ class HugeDoc {
   // Window entries whose insert and first remove are both at/below minSeq graduate into the stable
   // sums (mergeTree.ts:1147-1166 moves the window; their length is now the same for every view).
   FMT_DEV void graduate() {
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[4], t0_};
+    ProfScope ps_(prof[4]);
     uint32_t w = 0;
     while (w < nWin) {
       const uint32_t base = w;
@@ -1252,8 +1335,8 @@ class HugeDoc {
         const uint32_t i = base + l;
         bool g = false;
         if (i < nWin) {
-          const int32_t rm = rd(S.wRm + i);
-          g = rd(S.wIns + i) <= minSeq && (rm == kNotRemoved || rm <= minSeq);
+          const int32_t rm = static_cast<int32_t>(rd(wWord(i, 1)));
+          g = static_cast<int32_t>(rd(wWord(i, 0))) <= minSeq && (rm == kNotRemoved || rm <= minSeq);
         }
         LANE(q) = g;
       }
@@ -1263,8 +1346,8 @@ class HugeDoc {
         continue;
       }
       const uint32_t e = base + static_cast<uint32_t>(ctz64(m));
-      const int32_t rm = ldi(S.wRm + e);
-      const uint32_t len = ldu(S.wLen + e), blk = ldu(S.wBlk + e);
+      const int32_t rm = static_cast<int32_t>(ldu(wWord(e, 1)));
+      const uint32_t len = ldu(wWord(e, 2)), blk = ldu(S.wBlk + e);
       winRemove(e);  // the entry moved into e is examined next
       if (rm == kNotRemoved) addStable(blk, static_cast<int>(len));
       w = e;
@@ -1273,19 +1356,14 @@ class HugeDoc {
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts:33-213)
-  // scourNode over leaf block b: drops leaves removed at/below minSeq, appends acked same-props
-  // appendable leaves onto the previous kept leaf (their text is copied to the merge area).
-  // Returns the new leaf count.
-  FMT_DEV int scourLeaves(uint32_t b) {
-    const int cnt = static_cast<int>(ldu(S.bCount + b));
-    if (cnt == 0) return 0;
-    // every leaf of the block in one vector load per field (lane k = leaf k), plus its last unit
-    Lane<uint32_t> f[8];
-    Lane<uint32_t> lastCh;
+  // Leaves of up to 8 leaf blocks in one vector load per field: lane 8i + k = leaf k of blocks[i]
+  // (cntL: block i's leaf count in every lane of its octet), plus each leaf's last text unit.
+  FMT_DEV void loadOctets(const Lane<uint32_t>& blk, const Lane<int>& cntL, Lane<uint32_t>* f, Lane<uint32_t>& lastCh) const {
     FOR_LANES(l) {
-      const int k = l < cnt ? l : 0;
-      const size_t i = li(b, k);
-      LANE(f[0]) = rd(S.lLen + i);
+      const int k = l & 7;
+      const bool on = k < LANE(cntL);
+      const size_t i = li(LANE(blk), on ? k : 0);
+      LANE(f[0]) = on ? rd(S.lLen + i) : 0u;
       LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
       LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
       LANE(f[3]) = rd(S.lMlo + i);
@@ -1296,276 +1374,305 @@ class HugeDoc {
       const uint32_t ln = LANE(f[0]);
       LANE(lastCh) = ln > 0 ? loadWg(S.text + LANE(f[6]) + ln - 1) : 0u;
     }
-    // serial decisions over <= 8 leaves (zamboni.ts:141-213): dest nibble k = output slot of leaf k,
-    // 0xF = dropped; a leaf appended onto the previous kept leaf takes that leaf's slot
-    uint32_t dest = 0, heads = 0;  // heads: bit q = output slot q keeps a merged run
-    uint32_t headLen[kMaxNodes];
-    int nk = 0, prev = -1;
-    uint32_t prevLen = 0, prevProps = 0, prevLast = 0;
-    for (int k = 0; k < cnt; k++) {
-      const uint32_t len = readlane(f[0], k);
-      const int32_t ins = static_cast<int32_t>(readlane(f[1], k)), rm = static_cast<int32_t>(readlane(f[2], k));
-      const uint32_t props = mProps(readlane(f[7], k)), lc = readlane(lastCh, k);
-      uint32_t d;
-      if (rm == kNotRemoved) {
-        if (ins <= minSeq) {
+  }
+
+  // scourNode decisions (zamboni.ts:141-213) over loaded octets, serial per block: dst[s] = output
+  // index taken by source lane s (-1: dropped); a leaf appended onto the previous kept leaf takes its
+  // run head's output. Merged runs are consecutive source lanes, so their text, concatenated in lane
+  // order, is written to the merge area at mergeBase (lane s's units at mergeBase + flat[s]).
+  struct ScourPlan {
+    Lane<int> dst, srcOf;
+    Lane<uint32_t> outLen, flat;
+    uint64_t heads;  // bit j: output j is a merged run
+    int total;
+    uint32_t mergeBase;
+  };
+  FMT_DEV bool scourPlan(const Lane<uint32_t>* f, const Lane<uint32_t>& lastCh, const Lane<int>& cntL, int nBlk, ScourPlan& P) {
+    FOR_LANES(l) {
+      LANE(P.dst) = -1;
+      LANE(P.srcOf) = 0;
+      LANE(P.outLen) = 0;
+    }
+    P.heads = 0;
+    P.total = 0;
+    for (int i = 0; i < nBlk; i++) {
+      const int cnt = readlane(cntL, 8 * i);
+      int prev = -1;
+      uint32_t prevLen = 0, prevProps = 0, prevLast = 0;
+      for (int k = 0; k < cnt; k++) {
+        const int s = 8 * i + k;
+        const uint32_t len = readlane(f[0], s);
+        const int32_t ins = static_cast<int32_t>(readlane(f[1], s)), rm = static_cast<int32_t>(readlane(f[2], s));
+        if (rm == kNotRemoved && ins <= minSeq) {
+          const uint32_t props = mProps(readlane(f[7], s)), lc = readlane(lastCh, s);
           const bool canAppend = prev >= 0 && len > 0 && prevLast != 10u &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) || len <= static_cast<uint32_t>(kGranularity)) &&
                                  propsMatch(prevProps, props);
           if (canAppend) {
-            d = static_cast<uint32_t>(prev);
+            setLane(P.dst, s, prev);
             prevLen += len;
             prevLast = lc;
-            headLen[prev] = prevLen;
-            heads |= 1u << prev;
+            setLane(P.outLen, prev, prevLen);
+            P.heads |= 1ull << prev;
           } else {
-            d = static_cast<uint32_t>(nk);
-            headLen[nk] = len;
-            prev = len > 0 ? nk : -1;
+            setLane(P.dst, s, P.total);
+            setLane(P.srcOf, P.total, s);
+            setLane(P.outLen, P.total, len);
+            prev = len > 0 ? P.total : -1;
             prevLen = len;
             prevProps = props;
             prevLast = lc;
-            nk++;
+            P.total++;
           }
         } else {
-          d = static_cast<uint32_t>(nk++);
+          if (!(rm != kNotRemoved && rm <= minSeq)) {
+            setLane(P.dst, s, P.total);
+            setLane(P.srcOf, P.total, s);
+            setLane(P.outLen, P.total, len);
+            P.total++;
+          }
           prev = -1;
         }
-      } else {
-        if (rm <= minSeq) {
-          d = 0xFu;
-        } else {
-          d = static_cast<uint32_t>(nk++);
-        }
-        prev = -1;
       }
-      dest |= d << (4 * k);
     }
-    if (nk == cnt) return cnt;  // nothing dropped or appended
-    // merged runs: their text is rebuilt once in the merge area (lane t copies unit t)
-    uint32_t runDst[kMaxNodes];
+    Lane<uint32_t> member;
+    FOR_LANES(l) {
+      const int d = LANE(P.dst);
+      LANE(member) = (d >= 0 && ((P.heads >> d) & 1ull)) ? LANE(f[0]) : 0u;
+    }
     uint32_t need = 0;
-    for (int q = 0; q < nk; q++) {
-      if ((heads >> q) & 1u) {
-        runDst[q] = static_cast<uint32_t>(textTop + need);
-        need += headLen[q];
-      } else {
-        runDst[q] = 0;
-      }
-    }
-    if (textTop + need > S.textCap) {
-      fail(FMT_E_CAPACITY);
-      return cnt;
-    }
-    if (need) {
-      // per leaf k of a merged run: its offset inside the run
-      uint32_t runOff[kMaxNodes], srcStart[kMaxNodes];  // (uniform)
-      uint32_t acc[kMaxNodes] = {0, 0, 0, 0, 0, 0, 0, 0};
-      uint32_t flat = 0;
-      for (int k = 0; k < cnt; k++) {
-        const uint32_t d = (dest >> (4 * k)) & 0xFu;
-        srcStart[k] = flat;
-        if (d != 0xFu && ((heads >> d) & 1u)) {
-          runOff[k] = acc[d];
-          acc[d] += readlane(f[0], k);
-          flat += readlane(f[0], k);
-        } else {
-          runOff[k] = 0xFFFFFFFFu;
-        }
-      }
-      for (uint32_t base = 0; base < flat; base += 64) {
-        Lane<uint32_t> v, dstIdx;
+    P.flat = waveExclusiveSum(member, &need);
+    P.mergeBase = static_cast<uint32_t>(textTop);
+    if (!need) return true;
+    if (textTop + need > S.textCap) return fail(FMT_E_CAPACITY);
+    for (uint32_t base = 0; base < need; base += 64) {
+      // source lane of unit t: the last lane whose flat start is <= t (binary search by gathers;
+      // flat is non-decreasing over lanes)
+      Lane<int> pos;
+      FOR_LANES(l) { LANE(pos) = 0; }
+      for (int step = 32; step >= 1; step >>= 1) {
+        Lane<int> cand;
+        FOR_LANES(l) { LANE(cand) = LANE(pos) + step; }
+        const Lane<uint32_t> v = gather(P.flat, cand);
         FOR_LANES(l) {
-          const uint32_t t = base + l;
-          uint32_t val = 0, di = 0xFFFFFFFFu;
-          if (t < flat) {
-            for (int k = 0; k < cnt; k++) {
-              if (runOff[k] != 0xFFFFFFFFu && t >= srcStart[k] && t < srcStart[k] + readlaneU(f[0], k)) {
-                const uint32_t d = (dest >> (4 * k)) & 0xFu;
-                const uint32_t o = t - srcStart[k];
-                val = loadWg(S.text + readlaneU(f[6], k) + o);
-                di = runDst[d] + runOff[k] + o;
-              }
-            }
-          }
-          LANE(v) = val;
-          LANE(dstIdx) = di;
+          if (LANE(v) <= base + static_cast<uint32_t>(l)) LANE(pos) = LANE(cand);
         }
-        waveSync();
-        FOR_LANES(l) {
-          if (LANE(dstIdx) != 0xFFFFFFFFu) S.text[LANE(dstIdx)] = static_cast<uint16_t>(LANE(v));
-        }
-        waveSync();
       }
-      textTop += need;
-    }
-    // output slot q takes its head leaf (the first leaf with dest q); gone leaves leave the tree
-    Lane<int> src;
-    FOR_LANES(l) {
-      int sidx = 0;
-      for (int k = cnt - 1; k >= 0; k--)
-        if (((dest >> (4 * k)) & 0xFu) == static_cast<uint32_t>(l)) sidx = k;
-      LANE(src) = sidx;
-    }
-    Lane<uint32_t> g[8];
-#pragma unroll
-    for (int x = 0; x < 8; x++) g[x] = gather(f[x], src);
-    FOR_LANES(l) {
-      if (l < nk) {
-        const size_t i = li(b, l);
-        const bool merged = ((heads >> l) & 1u) != 0;
-        S.lLen[i] = merged ? headLen[l] : LANE(g[0]);
-        S.lIns[i] = static_cast<int32_t>(LANE(g[1]));
-        S.lRm[i] = static_cast<int32_t>(LANE(g[2]));
-        S.lMlo[i] = LANE(g[3]);
-        S.lMhi[i] = LANE(g[4]);
-        S.lId[i] = LANE(g[5]);
-        S.lText[i] = merged ? runDst[l] : LANE(g[6]);
-        S.lMeta[i] = LANE(g[7]);
-      }
-      if (l < cnt) {  // appended or dropped leaves: segment.parent = undefined
-        const uint32_t d = (dest >> (4 * l)) & 0xFu;
-        bool head = d != 0xFu;  // the first leaf with output slot d (lane-local: no cross-lane read)
-        for (int k = 0; k < kMaxNodes; k++)
-          if (k < l && ((dest >> (4 * k)) & 0xFu) == d) head = false;
-        if (!head) S.leafBlk[LANE(f[5])] = kNone;
-      }
-    }
-    waveSync();
-    st1(S.bCount + b, static_cast<uint32_t>(nk));
-    return nk;
-  }
-
-  FMT_DEV static uint32_t readlaneU(const Lane<uint32_t>& x, int k) { return readlane(x, k); }
-  FMT_DEV static uint32_t readlaneU(const Lane<int>& x, int k) { return static_cast<uint32_t>(readlane(x, k)); }
-
-  FMT_DEV static int pieceLast(int owner, const uint32_t* pt, const uint32_t* pl, const int* po, int n) {
-    int last = -1;
-    for (int i = 0; i < n; i++)
-      if (po[i] == owner) last = i;
-    return static_cast<int>(pt[last] + pl[last] - 1);
-  }
-  FMT_DEV uint32_t textAt(int i) const { return loadWg(S.text + i); }
-  FMT_DEV void copyText(uint32_t dst, uint32_t src, uint32_t n) {
-    for (uint32_t base = 0; base < n; base += 64) {
+      const Lane<uint32_t> st = gather(P.flat, pos), tx = gather(f[6], pos);
       Lane<uint32_t> v;
-      FOR_LANES(l) { LANE(v) = base + l < n ? loadWg(S.text + src + base + l) : 0u; }
+      FOR_LANES(l) {
+        const uint32_t t = base + l;
+        LANE(v) = t < need ? loadWg(S.text + LANE(tx) + (t - LANE(st))) : 0u;
+      }
       waveSync();
       FOR_LANES(l) {
-        if (base + l < n) S.text[dst + base + l] = static_cast<uint16_t>(LANE(v));
+        const uint32_t t = base + l;
+        if (t < need) S.text[textTop + t] = static_cast<uint16_t>(LANE(v));
       }
       waveSync();
+    }
+    textTop += need;
+    return true;
+  }
+
+  // Source lanes whose leaf left the tree (dropped, or appended onto its run head): for each, the
+  // callback's leaf id gets parent = undefined (leafBlk kNone).
+  FMT_DEV void unlinkGone(const ScourPlan& P, const Lane<uint32_t>* f, const Lane<int>& cntL) {
+    Lane<uint32_t> srcU;
+    Lane<int> dd;
+    FOR_LANES(l) {
+      LANE(srcU) = static_cast<uint32_t>(LANE(P.srcOf));
+      LANE(dd) = LANE(P.dst) < 0 ? 0 : LANE(P.dst);
+    }
+    const Lane<uint32_t> headSrc = gather(srcU, dd);
+    FOR_LANES(l) {
+      const bool valid = (l & 7) < LANE(cntL);
+      if (valid && (LANE(P.dst) < 0 || LANE(headSrc) != static_cast<uint32_t>(l))) S.leafBlk[LANE(f[5])] = kNone;
+    }
+  }
+
+  // scourNode over leaf block b: drops leaves removed at/below minSeq, appends acked same-props
+  // appendable leaves onto the previous kept leaf. Returns the new leaf count.
+  FMT_DEV int scourLeaves(uint32_t b) {
+    ProfScope ps_(prof[8]);
+    const int cnt = static_cast<int>(ldu(S.bCount + b));
+    if (cnt == 0) return 0;
+    Lane<uint32_t> blk, f[8], lastCh;
+    Lane<int> cntL;
+    FOR_LANES(l) {
+      LANE(blk) = b;
+      LANE(cntL) = l < 8 ? cnt : 0;
+    }
+    loadOctets(blk, cntL, f, lastCh);
+    ScourPlan P;
+    if (!scourPlan(f, lastCh, cntL, 1, P)) return cnt;
+    if (P.total == cnt) return cnt;  // nothing dropped or appended
+    Lane<uint32_t> g8[8];
+#pragma unroll
+    for (int x = 0; x < 8; x++) g8[x] = gather(f[x], P.srcOf);
+    const Lane<uint32_t> runSt = gather(P.flat, P.srcOf);
+    waveSync();
+    FOR_LANES(l) {
+      if (l < P.total) {
+        const size_t i = li(b, l);
+        const bool merged = ((P.heads >> l) & 1ull) != 0;
+        S.lLen[i] = merged ? LANE(P.outLen) : LANE(g8[0]);
+        S.lIns[i] = static_cast<int32_t>(LANE(g8[1]));
+        S.lRm[i] = static_cast<int32_t>(LANE(g8[2]));
+        S.lMlo[i] = LANE(g8[3]);
+        S.lMhi[i] = LANE(g8[4]);
+        S.lId[i] = LANE(g8[5]);
+        S.lText[i] = merged ? P.mergeBase + LANE(runSt) : LANE(g8[6]);
+        S.lMeta[i] = LANE(g8[7]);
+      }
+    }
+    unlinkGone(P, f, cntL);
+    waveSync();
+    st1(S.bCount + b, static_cast<uint32_t>(P.total));
+    return P.total;
+  }
+
+  FMT_DEV static void setLane(Lane<uint32_t>& x, int idx, uint32_t v) {
+    FOR_LANES(l) {
+      if (l == idx) LANE(x) = v;
+    }
+  }
+  FMT_DEV static void setLane(Lane<int>& x, int idx, int v) {
+    FOR_LANES(l) {
+      if (l == idx) LANE(x) = v;
     }
   }
 
   // packParent (zamboni.ts:83-139) at the leaf level: every child leaf block of p is scoured, the held
   // leaves are redistributed into min(7, total / 4) (>= 1) blocks. The first of p's old blocks are
   // reused for the new ones (block identity is not observable); the rest are freed and unlisted.
+  // All children are scoured together: lane 8i + k holds leaf k of child i (≤ 7 x 7 leaves), so the
+  // whole pack is a handful of dependent memory rounds instead of one scour per child.
   FMT_DEV void packLeafParent(uint32_t p) {
+    ProfScope ps_(prof[9]);
     const int pc = static_cast<int>(ldu(S.bCount + p));
-    uint32_t oldBlk[kMaxNodes];
-    for (int i = 0; i < pc; i++) oldBlk[i] = childAt(p, i);
-    // scour every child, staging its held leaves (document order) in LDS
-    int total = 0;
-    for (int i = 0; i < pc; i++) {
-      const uint32_t b = oldBlk[i];
-      const int cnt = scourLeaves(b);
-      if (status != FMT_OK) return;
-      FOR_LANES(l) {
-        if (l < cnt) {
-          const size_t x = li(b, l);
-          L->held[0][total + l] = rd(S.lLen + x);
-          L->held[1][total + l] = static_cast<uint32_t>(rd(S.lIns + x));
-          L->held[2][total + l] = static_cast<uint32_t>(rd(S.lRm + x));
-          L->held[3][total + l] = rd(S.lMlo + x);
-          L->held[4][total + l] = rd(S.lMhi + x);
-          L->held[5][total + l] = rd(S.lId + x);
-          L->held[6][total + l] = rd(S.lText + x);
-          L->held[7][total + l] = rd(S.lMeta + x);
-        }
-      }
-      waveSync();
-      total += cnt;
-    }
+    Lane<uint32_t> chl, f[8], lastCh;
+    Lane<int> cntL;
+    FOR_LANES(l) { LANE(chl) = (l >> 3) < pc ? rd(S.bChild + (static_cast<size_t>(p) * 8 + (l >> 3))) : 0u; }
+    FOR_LANES(l) { LANE(cntL) = (l >> 3) < pc ? static_cast<int>(rd(S.bCount + LANE(chl))) : 0; }
+    loadOctets(chl, cntL, f, lastCh);
+    ScourPlan P;
+    if (!scourPlan(f, lastCh, cntL, pc, P)) return;
+    const int total = P.total;
+    const uint64_t heads = P.heads;
+    const Lane<int>& srcOf = P.srcOf;
+    const Lane<uint32_t>& outLen = P.outLen;
+    const uint32_t mergeBase = P.mergeBase;
+    // redistribution: nb blocks, the first `rem` of them one leaf longer
     int nb = 0;
     if (total > 0) {
       nb = total / (kMaxNodes / 2);
       if (nb > kMaxNodes - 1) nb = kMaxNodes - 1;
       if (nb < 1) nb = 1;
     }
-    // The new blocks reuse the first old blocks' ids AND their slots (document order is unchanged);
-    // old blocks past nb are unlisted and freed, extra new blocks are listed after the last old one.
     const int base = nb ? total / nb : 0;
-    int rem = nb ? total % nb : 0;
-    int consumed = 0;
+    const int rem = nb ? total % nb : 0;
+    // new block ids: the old blocks' ids (and slots) first, extra blocks listed after the previous one
+    Lane<uint32_t> blkQ;
+    FOR_LANES(l) { LANE(blkQ) = 0u; }
+    uint32_t prevB = kNone;
     for (int q = 0; q < nb; q++) {
-      int cnt = base;
-      if (rem > 0) {
-        cnt++;
-        rem--;
-      }
       uint32_t b;
       if (q < pc) {
-        b = oldBlk[q];
+        b = readlane(chl, 8 * q);
       } else {
         b = allocBlk(1);
         if (b == kNone) return;
-        const uint32_t pb = L->tmp[q - 1];  // (q >= pc >= 1) the previous new block
-        const uint32_t g = ldu(S.bGroup + pb);
+        const uint32_t g = ldu(S.bGroup + prevB);
         st1(S.bGroup + b, g);
         st1(S.bCount + b, 0u);
-        if (!slotInsert(g, static_cast<int>(ldu(S.bSlot + pb)) + 1, b, 0)) return;
+        if (!slotInsert(g, static_cast<int>(ldu(S.bSlot + prevB)) + 1, b, 0)) return;
       }
-      L->tmp[q] = b;
-      waveSync();
-      const uint32_t g = ldu(S.bGroup + b);
-      FOR_LANES(l) {
-        if (l < cnt) {
-          const size_t x = li(b, l);
-          const int h = consumed + l;
-          const uint32_t id = L->held[5][h];
-          S.lLen[x] = L->held[0][h];
-          S.lIns[x] = static_cast<int32_t>(L->held[1][h]);
-          S.lRm[x] = static_cast<int32_t>(L->held[2][h]);
-          S.lMlo[x] = L->held[3][h];
-          S.lMhi[x] = L->held[4][h];
-          S.lId[x] = id;
-          S.lText[x] = L->held[6][h];
-          S.lMeta[x] = L->held[7][h];
-          S.leafBlk[id] = b;
-          const uint32_t w = rd(S.winIdx + id);
-          if (w != kNone) {
-            S.wBlk[w] = b;
-            S.wGroup[w] = g;
-          }
+      setLane(blkQ, q, b);
+      prevB = b;
+    }
+    // output j -> block q, slot kq
+    Lane<int> qOf, kOf;
+    FOR_LANES(l) {
+      const int j = l;
+      const int big = rem * (base + 1);
+      int q = 0, kq = 0;
+      if (j < total) {
+        if (j < big) {
+          q = j / (base + 1);
+          kq = j - q * (base + 1);
+        } else {
+          q = rem + (j - big) / base;
+          kq = (j - big) - (q - rem) * base;
         }
       }
-      waveSync();
-      st1(S.bCount + b, static_cast<uint32_t>(cnt));
-      st1(S.bLeaf + b, 1u);
-      st1(S.bParent + b, p);
-      st1(S.bScour + b, -1);
-      st1(S.bChild + static_cast<size_t>(p) * 8 + q, b);
-      consumed += cnt;
-      const int stB = blockStable(b);
-      const int s0 = static_cast<int>(ldu(S.bSlot + b));
-      int32_t* sp = slotStPtr(g) + s0;
-      const int32_t old = ldi(sp);
-      st1(sp, stB);
-      L->gStable[g] += stB - old;
-      waveSync();
+      LANE(qOf) = q;
+      LANE(kOf) = kq;
     }
+    Lane<uint32_t> g8[8];
+#pragma unroll
+    for (int x = 0; x < 8; x++) g8[x] = gather(f[x], srcOf);
+    const Lane<uint32_t> blkJ = gather(blkQ, qOf), runSt = gather(P.flat, srcOf);
+    FOR_LANES(l) {
+      if (l < kMaxNodes) L->tmp[l] = 0u;
+    }
+    waveSync();
+    FOR_LANES(l) {
+      if (l < total) {
+        const uint32_t b = LANE(blkJ);
+        const size_t x = li(b, LANE(kOf));
+        const bool merged = ((heads >> l) & 1ull) != 0;
+        const uint32_t id = LANE(g8[5]);
+        const uint32_t len = merged ? LANE(outLen) : LANE(g8[0]);
+        S.lLen[x] = len;
+        S.lIns[x] = static_cast<int32_t>(LANE(g8[1]));
+        S.lRm[x] = static_cast<int32_t>(LANE(g8[2]));
+        S.lMlo[x] = LANE(g8[3]);
+        S.lMhi[x] = LANE(g8[4]);
+        S.lId[x] = id;
+        S.lText[x] = merged ? mergeBase + LANE(runSt) : LANE(g8[6]);
+        S.lMeta[x] = LANE(g8[7]);
+        S.leafBlk[id] = b;
+        const uint32_t w = rd(S.winIdx + id);
+        if (w != kNone) wRetag(w, b, rd(S.bGroup + b));
+        const int c = (w == kNone && static_cast<int32_t>(LANE(g8[2])) == kNotRemoved) ? static_cast<int>(len) : 0;
+        atomicAddLds(reinterpret_cast<int32_t*>(&L->tmp[LANE(qOf)]), c);
+      }
+    }
+    waveSync();
+    unlinkGone(P, f, cntL);
+    waveSync();
+    // block records and slot stable sums (lane q)
+    FOR_LANES(l) {
+      if (l < nb) {
+        const uint32_t b = LANE(blkQ);
+        const int cnt = l < rem ? base + 1 : base;
+        S.bCount[b] = static_cast<uint32_t>(cnt);
+        S.bLeaf[b] = 1u;
+        S.bParent[b] = p;
+        S.bScour[b] = -1;
+        S.bChild[static_cast<size_t>(p) * 8 + l] = b;
+        const uint32_t g = rd(S.bGroup + b), s0 = rd(S.bSlot + b);
+        int32_t* sp = S.gSlotStable + static_cast<size_t>(g) * kSlotCap + s0;
+        const int32_t stB = static_cast<int32_t>(L->tmp[l]);
+        const int32_t old = rd(sp);
+        *sp = stB;
+        atomicAddLds(&L->gStable[g], stB - old);
+      }
+    }
+    waveSync();
     // unlist and free the old blocks past nb (consecutive slots, possibly in two groups)
     for (int i = nb; i < pc; i++) {
-      const uint32_t b = oldBlk[i];
+      const uint32_t b = readlane(chl, 8 * i);
       const uint32_t g = ldu(S.bGroup + b);
       const int s0 = static_cast<int>(ldu(S.bSlot + b));
       int run = 1;  // the following old blocks in the same group are the next slots
-      while (i + run < pc && ldu(S.bGroup + oldBlk[i + run]) == g) run++;
+      while (i + run < pc && ldu(S.bGroup + readlane(chl, 8 * (i + run))) == g) run++;
       slotRemove(g, s0, run);
       for (int k = 0; k < run; k++) {
-        st1(S.bCount + oldBlk[i + k], 0u);
-        freeBlock(oldBlk[i + k]);
+        const uint32_t ob = readlane(chl, 8 * (i + k));
+        st1(S.bCount + ob, 0u);
+        freeBlock(ob);
       }
       i += run - 1;
     }
@@ -1584,18 +1691,31 @@ class HugeDoc {
     }
   }
 
-  // packParent above the leaf level: grandchildren blocks redistributed (no leaf moves).
+  // packParent above the leaf level: grandchildren blocks redistributed (no leaf moves). Lane 8i + k
+  // holds grandchild k of child i; output j (document order) goes to block q, slot kq.
   FMT_DEV void packInterior(uint32_t p) {
+    ProfScope ps_(prof[15]);
     const int pc = static_cast<int>(ldu(S.bCount + p));
-    uint32_t held[kMaxNodes * kMaxNodes];
-    uint32_t old[kMaxNodes];
-    int n = 0;
-    for (int i = 0; i < pc; i++) {
-      const uint32_t c = childAt(p, i);
-      old[i] = c;
-      const int cc = static_cast<int>(ldu(S.bCount + c));
-      for (int k = 0; k < cc; k++) held[n++] = childAt(c, k);
+    Lane<uint32_t> chl, gc, one;
+    Lane<int> cc;
+    FOR_LANES(l) { LANE(chl) = (l >> 3) < pc ? rd(S.bChild + (static_cast<size_t>(p) * 8 + (l >> 3))) : 0u; }
+    FOR_LANES(l) { LANE(cc) = (l >> 3) < pc ? static_cast<int>(rd(S.bCount + LANE(chl))) : 0; }
+    FOR_LANES(l) {
+      const bool on = (l & 7) < LANE(cc);
+      LANE(gc) = on ? rd(S.bChild + (static_cast<size_t>(LANE(chl)) * 8 + (l & 7))) : 0u;
+      LANE(one) = on ? 1u : 0u;
     }
+    // output index of each grandchild (document order), and the source lane of each output
+    uint32_t nU;
+    const Lane<uint32_t> outIdx = waveExclusiveSum(one, &nU);
+    const int n = static_cast<int>(nU);
+    FOR_LANES(l) {
+      if (LANE(one)) L->tmp[LANE(outIdx)] = static_cast<uint32_t>(l);
+    }
+    waveSync();
+    Lane<int> src;
+    FOR_LANES(l) { LANE(src) = l < n ? static_cast<int>(L->tmp[l]) : 0; }
+    waveSync();
     int nb = 0;
     if (n > 0) {
       nb = n / (kMaxNodes / 2);
@@ -1603,30 +1723,53 @@ class HugeDoc {
       if (nb < 1) nb = 1;
     }
     const int base = nb ? n / nb : 0;
-    int rem = nb ? n % nb : 0;
-    int consumed = 0;
+    const int rem = nb ? n % nb : 0;
+    Lane<uint32_t> blkQ;
+    FOR_LANES(l) { LANE(blkQ) = 0u; }
     for (int q = 0; q < nb; q++) {
-      int cnt = base;
-      if (rem > 0) {
-        cnt++;
-        rem--;
-      }
-      const uint32_t b = q < pc ? old[q] : allocBlk(0);
+      const uint32_t b = q < pc ? readlane(chl, 8 * q) : allocBlk(0);
       if (b == kNone) return;
-      st1(S.bLeaf + b, 0u);
-      for (int k = 0; k < cnt; k++) setChild(b, k, held[consumed + k]);
-      st1(S.bCount + b, static_cast<uint32_t>(cnt));
-      st1(S.bScour + b, -1);
-      setChild(p, q, b);
-      consumed += cnt;
+      setLane(blkQ, q, b);
     }
-    for (int i = nb; i < pc; i++) freeBlock(old[i]);
+    Lane<int> qOf, kOf;
+    FOR_LANES(l) {
+      const int big = rem * (base + 1);
+      int q = 0, kq = 0;
+      if (l < n) {
+        if (l < big) {
+          q = l / (base + 1);
+          kq = l - q * (base + 1);
+        } else {
+          q = rem + (l - big) / base;
+          kq = (l - big) - (q - rem) * base;
+        }
+      }
+      LANE(qOf) = q;
+      LANE(kOf) = kq;
+    }
+    const Lane<uint32_t> held = gather(gc, src), blkJ = gather(blkQ, qOf);
+    waveSync();
+    FOR_LANES(l) {
+      if (l < n) {
+        S.bChild[static_cast<size_t>(LANE(blkJ)) * 8 + LANE(kOf)] = LANE(held);
+        S.bParent[LANE(held)] = LANE(blkJ);
+      }
+      if (l < nb) {
+        const uint32_t b = LANE(blkQ);
+        S.bLeaf[b] = 0u;
+        S.bCount[b] = static_cast<uint32_t>(l < rem ? base + 1 : base);
+        S.bScour[b] = -1;
+        S.bChild[static_cast<size_t>(p) * 8 + l] = b;
+        S.bParent[b] = p;
+      }
+    }
+    waveSync();
+    for (int i = nb; i < pc; i++) freeBlock(readlane(chl, 8 * i));
     st1(S.bCount + p, static_cast<uint32_t>(nb));
   }
 
   FMT_DEV void zamboni() {
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[3], t0_};
+    ProfScope ps_(prof[3]);
     for (int i = 0; i < 2; i++) {
       if (heapN == 0) break;
       if (heapSeq(1) > minSeq) break;
@@ -1659,8 +1802,7 @@ class HugeDoc {
   // segment stamped {UniversalSequenceNumber, NonCollabClient} (snapshotLoader.ts:180-186).
   // Blocks are numbered leaf level first; groups take kFill leaf blocks each.
   FMT_DEV void load() {
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[5], t0_};
+    ProfScope ps_(prof[5]);
     const uint32_t N = in.nSegs;
     const uint32_t nLeafBlk = (N + 6) / 7;
     if (N == 0 || nLeafBlk > S.blockCap || N + 1 > S.idCap) {
@@ -1797,8 +1939,7 @@ class HugeDoc {
   }
 
   FMT_DEV void replay() {
-    const uint64_t t0_ = clk();
-    struct Stamp_ { uint64_t& a; uint64_t t; FMT_DEV ~Stamp_() { a += clk() - t; } } st_{prof[0], t0_};
+    ProfScope ps_(prof[0]);
     Lane<uint32_t> rec0 = fetchOp(in.begin), rec1 = fetchOp(in.begin + 1);
     for (uint64_t i = in.begin; i < in.end; i++) {
       const fmt_mt_op op = decodeOp(rec0);
@@ -1866,7 +2007,7 @@ class HugeDoc {
             std::fprintf(stderr, "  leaf id %u len %u ins %d rm %d mask %x:%x ic %d vis %d win %d", S.lId[i], S.lLen[i], S.lIns[i], S.lRm[i],
                          S.lMhi[i], S.lMlo[i], mClient(S.lMeta[i]),
                          visOf(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c), w == kNone ? -1 : (int)w);
-            if (w != kNone) std::fprintf(stderr, " | w ins %d rm %d len %u meta %x grp %u blk %u", S.wIns[w], S.wRm[w], S.wLen[w], S.wMeta[w], S.wGroup[w], S.wBlk[w]);
+            if (w != kNone) std::fprintf(stderr, " | w ins %d rm %d len %u meta %x grp %u blk %u", S.wRec[4 * w], S.wRec[4 * w + 1], S.wRec[4 * w + 2], S.wRec[4 * w + 3] & kWMetaMask, S.wRec[4 * w + 3] >> kWGroupShift, S.wBlk[w]);
             std::fprintf(stderr, "\n");
           }
           fail(FMT_E_DATA);
@@ -1906,8 +2047,8 @@ class HugeDoc {
           if (shouldWin != (w != kNone)) return bad("window membership", id, shouldWin);
           if (w != kNone) {
             nw++;
-            if (S.wLeaf[w] != id || S.wBlk[w] != b || S.wGroup[w] != g || S.wLen[w] != S.lLen[i] || S.wIns[w] != S.lIns[i] ||
-                S.wRm[w] != S.lRm[i])
+            if (S.wLeaf[w] != id || S.wBlk[w] != b || (S.wRec[4 * w + 3] >> kWGroupShift) != g || S.wRec[4 * w + 2] != S.lLen[i] ||
+                static_cast<int32_t>(S.wRec[4 * w]) != S.lIns[i] || static_cast<int32_t>(S.wRec[4 * w + 1]) != S.lRm[i])
               return bad("window entry", id, w);
           } else if (S.lRm[i] == kNotRemoved) {
             st += S.lLen[i];

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(64) void hugeDocKernel(const fmt_huge::HugeState* _
     doc.writeOutputs(o.header, o.leaves, o.capLeaves, o.chars, o.capChars, o.props);
     doc.prof[6] += fmt_huge::HugeDoc::clk() - t0;
     if ((threadIdx.x & 63) == 0)
-      for (int k = 0; k < 8; k++) o.prof[k] = doc.prof[k];
+      for (int k = 0; k < fmt_huge::HugeDoc::kProf; k++) o.prof[k] = doc.prof[k];
   }
 }
 
