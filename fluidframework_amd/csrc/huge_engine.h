@@ -135,6 +135,7 @@ struct HugeLds {
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
   uint32_t tmp[256];
+  uint16_t pClass[kPropCap];     // prop set id -> its match class (the first set with the same content)
   uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
   int32_t wlVis[kWinList];
 };
@@ -256,11 +257,11 @@ class HugeDoc {
   }
 
   // ------------------------------------------------------------------ window table
-  FMT_DEV void winAdd(uint32_t id, int32_t ins, int32_t rm, uint32_t len, uint32_t meta, uint32_t grp, uint32_t blk) {
+  FMT_DEV uint32_t winAdd(uint32_t id, int32_t ins, int32_t rm, uint32_t len, uint32_t meta, uint32_t grp, uint32_t blk) {
     invalidate();
     if (nWin >= S.winCap) {
       fail(FMT_E_CAPACITY);
-      return;
+      return kNone;
     }
     const uint32_t w = nWin++;
     FOR_LANES(l) {
@@ -275,6 +276,7 @@ class HugeDoc {
         S.winIdx[id] = w;
       }
     }
+    return w;
   }
   FMT_DEV void winRemove(uint32_t w) {  // swap-remove
     invalidate();
@@ -322,24 +324,13 @@ class HugeDoc {
     waveSync();
   }
 
-  // Recompute the stable length of a leaf block from its leaves (non-window leaves only).
-  FMT_DEV int blockStable(uint32_t b) {
-    const uint32_t cnt = ldu(S.bCount + b);
-    Lane<int> v;
-    FOR_LANES(l) {
-      int x = 0;
-      if (l < static_cast<int>(cnt)) {
-        const size_t i = static_cast<size_t>(b) * 8 + l;
-        const bool win = rd(S.winIdx + (rd(S.lId + i))) != kNone;
-        x = (!win && rd(S.lRm + i) == kNotRemoved) ? static_cast<int>(rd(S.lLen + i)) : 0;
-      }
-      LANE(v) = x;
-    }
-    uint32_t tot;
-    Lane<uint32_t> vu;
-    FOR_LANES(l) { LANE(vu) = static_cast<uint32_t>(LANE(v)); }
-    waveExclusiveSum(vu, &tot);
-    return static_cast<int>(tot);
+  FMT_DEV void addStableAt(uint32_t g, uint32_t s, int delta) {  // block in slot s of group g
+    invalidate();
+    int32_t* p = S.gSlotStable + static_cast<size_t>(g) * kSlotCap + s;
+    const int32_t v = ldi(p);
+    st1(p, v + delta);
+    L->gStable[g] += delta;
+    waveSync();
   }
 
   // ------------------------------------------------------------------ group lists
@@ -355,6 +346,8 @@ class HugeDoc {
     }
     return -1;
   }
+
+  static constexpr int kShiftU = 16;  // slot-list passes: 16 x 64 slots per step
 
   // Insert leaf block nb into group g at slot `at` with stable length st (slots at/after shift up).
   // Splits the group first when it is full; returns false on failure.
@@ -374,14 +367,14 @@ class HugeDoc {
     }
     uint32_t* sb = slotBlkPtr(g);
     int32_t* ss = slotStPtr(g);
-    // shift [at, cnt) up by one, top-down in chunks of 4 x 64 slots: a chunk's loads are all in
+    // shift [at, cnt) up by one, top-down in chunks of kShiftU x 64 slots: a chunk's loads are all in
     // flight before its stores (it writes only into slots the chunk above has already read)
-    for (int top = cnt - 1; top >= at; top -= 256) {
-      Lane<uint32_t> b[4];
-      Lane<int32_t> st[4];
+    for (int top = cnt - 1; top >= at; top -= 64 * kShiftU) {
+      Lane<uint32_t> b[kShiftU];
+      Lane<int32_t> st[kShiftU];
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kShiftU; u++) {
           const int i = top - 64 * u - l;
           if (i >= at) {
             LANE(b[u]) = rd(sb + i);
@@ -392,7 +385,7 @@ class HugeDoc {
       waveSync();
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kShiftU; u++) {
           const int i = top - 64 * u - l;
           if (i >= at) {
             sb[i + 1] = LANE(b[u]);
@@ -425,14 +418,17 @@ class HugeDoc {
     const int cnt = static_cast<int>(L->gCount[g]);
     uint32_t* sb = slotBlkPtr(g);
     int32_t* ss = slotStPtr(g);
-    int removed = 0;
-    for (int i = at; i < at + n; i++) removed += ldi(ss + i);
-    for (int base = at + n; base < cnt; base += 256) {  // shift down by n, bottom-up, 4 x 64 per chunk
-      Lane<uint32_t> b[4];
-      Lane<int32_t> st[4];
+    Lane<uint32_t> rv;  // (n <= 64)
+    FOR_LANES(l) { LANE(rv) = l < n ? static_cast<uint32_t>(rd(ss + at + l)) : 0u; }
+    uint32_t removedU;
+    waveExclusiveSum(rv, &removedU);
+    const int removed = static_cast<int>(removedU);
+    for (int base = at + n; base < cnt; base += 64 * kShiftU) {  // shift down by n, bottom-up
+      Lane<uint32_t> b[kShiftU];
+      Lane<int32_t> st[kShiftU];
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kShiftU; u++) {
           const int i = base + 64 * u + l;
           if (i < cnt) {
             LANE(b[u]) = rd(sb + i);
@@ -443,7 +439,7 @@ class HugeDoc {
       waveSync();
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kShiftU; u++) {
           const int i = base + 64 * u + l;
           if (i < cnt) {
             sb[i - n] = LANE(b[u]);
@@ -657,12 +653,12 @@ class HugeDoc {
     const int cnt = static_cast<int>(L->gCount[g]);
     const uint32_t* sb = slotBlkPtr(g);
     const int32_t* ss = slotStPtr(g);
-    for (int base = 0; base < cnt; base += 256) {  // 4 x 64 slots per step, loads in flight together
-      Lane<uint32_t> bb[4];
-      Lane<int32_t> sv[4];
+    for (int base = 0; base < cnt; base += 64 * kShiftU) {  // kShiftU x 64 slots per step, loads in flight together
+      Lane<uint32_t> bb[kShiftU];
+      Lane<int32_t> sv[kShiftU];
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kShiftU; u++) {
           const int i = base + 64 * u + l;
           if (i < cnt) {
             LANE(bb[u]) = rd(sb + i);
@@ -672,7 +668,7 @@ class HugeDoc {
       }
       FOR_LANES(l) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kShiftU; u++) {
           const int i = base + 64 * u + l;
           if (i < cnt) {
             L->sBlk[i] = LANE(bb[u]);
@@ -815,91 +811,6 @@ class HugeDoc {
       }
     }
   }
-  // Shift leaves [k, cnt) of block b up by one (room at k); the caller puts the new leaf.
-  FMT_DEV void shiftUp(uint32_t b, int k, int cnt) {
-    Lane<uint32_t> f[8];
-    FOR_LANES(l) {
-      if (l >= k && l < cnt) {
-        const size_t i = li(b, l);
-        LANE(f[0]) = rd(S.lLen + i);
-        LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
-        LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
-        LANE(f[3]) = rd(S.lMlo + i);
-        LANE(f[4]) = rd(S.lMhi + i);
-        LANE(f[5]) = rd(S.lId + i);
-        LANE(f[6]) = rd(S.lText + i);
-        LANE(f[7]) = rd(S.lMeta + i);
-      }
-    }
-    waveSync();
-    FOR_LANES(l) {
-      if (l >= k && l < cnt) {
-        const size_t i = li(b, l + 1);
-        S.lLen[i] = LANE(f[0]);
-        S.lIns[i] = static_cast<int32_t>(LANE(f[1]));
-        S.lRm[i] = static_cast<int32_t>(LANE(f[2]));
-        S.lMlo[i] = LANE(f[3]);
-        S.lMhi[i] = LANE(f[4]);
-        S.lId[i] = LANE(f[5]);
-        S.lText[i] = LANE(f[6]);
-        S.lMeta[i] = LANE(f[7]);
-      }
-    }
-    waveSync();
-  }
-
-  // Move leaves [from, cnt) of block a to the front of block b (b's leaves shift up by the count).
-  FMT_DEV void moveLeaves(uint32_t a, int from, int cnt, uint32_t b) {
-    invalidate();
-    const int n = cnt - from;
-    if (n <= 0) return;
-    Lane<uint32_t> f[8];
-    FOR_LANES(l) {
-      if (l < n) {
-        const size_t i = li(a, from + l);
-        LANE(f[0]) = rd(S.lLen + i);
-        LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
-        LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
-        LANE(f[3]) = rd(S.lMlo + i);
-        LANE(f[4]) = rd(S.lMhi + i);
-        LANE(f[5]) = rd(S.lId + i);
-        LANE(f[6]) = rd(S.lText + i);
-        LANE(f[7]) = rd(S.lMeta + i);
-      }
-    }
-    waveSync();
-    FOR_LANES(l) {
-      if (l < n) {
-        const size_t i = li(b, l);
-        S.lLen[i] = LANE(f[0]);
-        S.lIns[i] = static_cast<int32_t>(LANE(f[1]));
-        S.lRm[i] = static_cast<int32_t>(LANE(f[2]));
-        S.lMlo[i] = LANE(f[3]);
-        S.lMhi[i] = LANE(f[4]);
-        S.lId[i] = LANE(f[5]);
-        S.lText[i] = LANE(f[6]);
-        S.lMeta[i] = LANE(f[7]);
-        S.leafBlk[LANE(f[5])] = b;
-        const uint32_t w = rd(S.winIdx + (LANE(f[5])));
-        if (w != kNone) S.wBlk[w] = b;
-      }
-    }
-    waveSync();
-  }
-
-  // Window entries of block b's leaves name b and its group.
-  FMT_DEV void retagWindow(uint32_t b) {
-    invalidate();
-    const uint32_t cnt = ldu(S.bCount + b), g = ldu(S.bGroup + b);
-    FOR_LANES(l) {
-      if (l < static_cast<int>(cnt)) {
-        const uint32_t w = rd(S.winIdx + rd(S.lId + li(b, l)));
-        if (w != kNone) wRetag(w, b, g);
-      }
-    }
-    waveSync();
-  }
-
   // ------------------------------------------------------------------ B+tree
   FMT_DEV uint32_t childAt(uint32_t p, int i) const { return ldu(S.bChild + static_cast<size_t>(p) * 8 + i); }
   FMT_DEV void setChild(uint32_t p, int i, uint32_t c) {
@@ -907,38 +818,134 @@ class HugeDoc {
     st1(S.bParent + c, p);
   }
 
-  // A child was inserted into block b: split on overflow (mergeTree.ts:1946-1987), propagate, grow
-  // the root (:1313-1320). Leaf blocks split 4/4 into a new leaf block listed in the next slot.
-  FMT_DEV void childAdded(uint32_t b) {
-    uint32_t cnt = ldu(S.bCount + b) + 1;
-    st1(S.bCount + b, cnt);
-    while (cnt >= static_cast<uint32_t>(kMaxNodes)) {
-      const uint32_t leaf = ldu(S.bLeaf + b);
-      const uint32_t nb = allocBlk(leaf);
-      if (nb == kNone) return;
-      constexpr int half = kMaxNodes / 2;
-      if (leaf) {
-        // the new block takes leaves 4..7; both stable sums are recomputed from their leaves
-        const uint32_t g = ldu(S.bGroup + b);
-        const int s = static_cast<int>(ldu(S.bSlot + b));
-        st1(S.bGroup + nb, g);  // (tentative: a group split in slotInsert may move it)
-        moveLeaves(b, half, kMaxNodes, nb);
-        st1(S.bCount + b, static_cast<uint32_t>(half));
-        st1(S.bCount + nb, static_cast<uint32_t>(half));
-        const int oldSt = ldi(slotStPtr(g) + s);
-        const int stB = blockStable(b), stN = blockStable(nb);
-        st1(slotStPtr(g) + s, stB);
-        L->gStable[g] += stB - oldSt;
-        waveSync();
-        if (!slotInsert(g, s + 1, nb, stN)) return;
-        retagWindow(nb);
-        if (lastBlk == b) lastBlk = nb;
-      } else {
-        for (int i = 0; i < half; i++) setChild(nb, i, childAt(b, half + i));
-        st1(S.bCount + b, static_cast<uint32_t>(half));
-        st1(S.bCount + nb, static_cast<uint32_t>(half));
+  // A leaf block held in registers (lane l = leaf l: fields f, window entry wi), with its count,
+  // group, slot and parent; edits are made in registers and written back by commitBlock.
+  struct BlockRegs {
+    Lane<uint32_t> f[8], wi;
+    int cnt;
+    uint32_t b, g, s, parent;
+  };
+  FMT_DEV void loadBlock(uint32_t b, BlockRegs& R) const {
+    R.b = b;
+    R.cnt = static_cast<int>(ldu(S.bCount + b));
+    R.g = ldu(S.bGroup + b);
+    R.s = ldu(S.bSlot + b);
+    R.parent = ldu(S.bParent + b);
+    FOR_LANES(l) {
+      const size_t i = li(b, l & 7);
+      LANE(R.f[0]) = rd(S.lLen + i);
+      LANE(R.f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
+      LANE(R.f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
+      LANE(R.f[3]) = rd(S.lMlo + i);
+      LANE(R.f[4]) = rd(S.lMhi + i);
+      LANE(R.f[5]) = rd(S.lId + i);
+      LANE(R.f[6]) = rd(S.lText + i);
+      LANE(R.f[7]) = rd(S.lMeta + i);
+    }
+    FOR_LANES(l) { LANE(R.wi) = l < R.cnt ? rd(S.winIdx + LANE(R.f[5])) : kNone; }
+  }
+  FMT_DEV static Leaf regLeaf(const BlockRegs& R, int k) {
+    Leaf x;
+    x.len = readlane(R.f[0], k);
+    x.ins = static_cast<int32_t>(readlane(R.f[1], k));
+    x.rm = static_cast<int32_t>(readlane(R.f[2], k));
+    x.mlo = readlane(R.f[3], k);
+    x.mhi = readlane(R.f[4], k);
+    x.id = readlane(R.f[5], k);
+    x.text = readlane(R.f[6], k);
+    x.meta = readlane(R.f[7], k);
+    return x;
+  }
+  // Insert leaf x (window entry w) at position k: leaves k.. move up one lane.
+  FMT_DEV static void regsInsert(BlockRegs& R, int k, const Leaf& x, uint32_t w) {
+    Lane<int> src;
+    FOR_LANES(l) { LANE(src) = l > k ? l - 1 : l; }
+#pragma unroll
+    for (int i = 0; i < 8; i++) R.f[i] = gather(R.f[i], src);
+    R.wi = gather(R.wi, src);
+    FOR_LANES(l) {
+      if (l == k) {
+        LANE(R.f[0]) = x.len;
+        LANE(R.f[1]) = static_cast<uint32_t>(x.ins);
+        LANE(R.f[2]) = static_cast<uint32_t>(x.rm);
+        LANE(R.f[3]) = x.mlo;
+        LANE(R.f[4]) = x.mhi;
+        LANE(R.f[5]) = x.id;
+        LANE(R.f[6]) = x.text;
+        LANE(R.f[7]) = x.meta;
+        LANE(R.wi) = w;
       }
-      const uint32_t p = ldu(S.bParent + b);
+    }
+    R.cnt++;
+  }
+  FMT_DEV void storeLeafLane(uint32_t b, int k, const BlockRegs& R, int l) {
+    const size_t i = li(b, k);
+    S.lLen[i] = LANE(R.f[0]);
+    S.lIns[i] = static_cast<int32_t>(LANE(R.f[1]));
+    S.lRm[i] = static_cast<int32_t>(LANE(R.f[2]));
+    S.lMlo[i] = LANE(R.f[3]);
+    S.lMhi[i] = LANE(R.f[4]);
+    S.lId[i] = LANE(R.f[5]);
+    S.lText[i] = LANE(R.f[6]);
+    S.lMeta[i] = LANE(R.f[7]);
+  }
+
+  // Write the block back. A block that reached MaxNodesInBlock leaves splits (mergeTree.ts:1946-1987):
+  // leaves 4..7 go to a new leaf block listed in the next slot, both stable sums are recomputed from
+  // the registers, and the new block is inserted after b in the parent chain. Returns the new block
+  // (kNone when there was no split).
+  FMT_DEV uint32_t commitBlock(BlockRegs& R) {
+    constexpr int half = kMaxNodes / 2;
+    const uint32_t b = R.b;
+    if (R.cnt < kMaxNodes) {
+      FOR_LANES(l) {
+        if (l < R.cnt) storeLeafLane(b, l, R, l);
+      }
+      waveSync();
+      st1(S.bCount + b, static_cast<uint32_t>(R.cnt));
+      return kNone;
+    }
+    const uint32_t nb = allocBlk(1);
+    if (nb == kNone) return kNone;
+    st1(S.bGroup + nb, R.g);  // (tentative: a group split in slotInsert may move it)
+    Lane<uint32_t> stv;
+    FOR_LANES(l) {
+      const bool stable = l < kMaxNodes && LANE(R.wi) == kNone && static_cast<int32_t>(LANE(R.f[2])) == kNotRemoved;
+      LANE(stv) = stable ? LANE(R.f[0]) : 0u;
+      if (l < half) storeLeafLane(b, l, R, l);
+      else if (l < kMaxNodes) {
+        storeLeafLane(nb, l - half, R, l);
+        S.leafBlk[LANE(R.f[5])] = nb;
+      }
+    }
+    uint32_t stTot;
+    const Lane<uint32_t> stEx = waveExclusiveSum(stv, &stTot);
+    const int stB = static_cast<int>(readlane(stEx, half)), stN = static_cast<int>(stTot) - stB;
+    waveSync();
+    st1(S.bCount + b, static_cast<uint32_t>(half));
+    st1(S.bCount + nb, static_cast<uint32_t>(half));
+    int32_t* sp = slotStPtr(R.g) + R.s;
+    const int32_t oldSt = ldi(sp);
+    st1(sp, stB);
+    L->gStable[R.g] += stB - oldSt;
+    waveSync();
+    invalidate();
+    if (!slotInsert(R.g, static_cast<int>(R.s) + 1, nb, stN)) return kNone;
+    const uint32_t g2 = ldu(S.bGroup + nb);
+    FOR_LANES(l) {
+      if (l >= half && l < kMaxNodes && LANE(R.wi) != kNone) wRetag(LANE(R.wi), nb, g2);
+    }
+    waveSync();
+    if (lastBlk == b) lastBlk = nb;
+    addChildAfter(R.parent, b, nb);
+    return nb;
+  }
+
+  // Insert block nb after its sibling b into parent p, splitting full interior blocks upward and
+  // growing the root (mergeTree.ts:1313-1320, 1946-1987).
+  FMT_DEV void addChildAfter(uint32_t p, uint32_t b, uint32_t nb) {
+    constexpr int half = kMaxNodes / 2;
+    for (;;) {
       if (p == kNone) {
         const uint32_t r = allocBlk(0);
         if (r == kNone) return;
@@ -948,14 +955,51 @@ class HugeDoc {
         root = static_cast<int>(r);
         return;
       }
-      const uint32_t pc = ldu(S.bCount + p);
-      int idx = 0;
-      while (idx < static_cast<int>(pc) && childAt(p, idx) != b) idx++;
-      for (int i = static_cast<int>(pc); i > idx + 1; i--) setChild(p, i, childAt(p, i - 1));
-      setChild(p, idx + 1, nb);
-      st1(S.bCount + p, pc + 1);
-      cnt = pc + 1;
+      const int pc = static_cast<int>(ldu(S.bCount + p));
+      Lane<uint32_t> ch;
+      Lane<bool> isB;
+      FOR_LANES(l) {
+        LANE(ch) = rd(S.bChild + (static_cast<size_t>(p) * 8 + (l & 7)));
+        LANE(isB) = l < pc && LANE(ch) == b;
+      }
+      const int idx = ctz64(ballot(isB));
+      Lane<int> src;
+      FOR_LANES(l) { LANE(src) = l <= idx ? l : l - 1; }
+      Lane<uint32_t> ch2 = gather(ch, src);
+      FOR_LANES(l) {
+        if (l == idx + 1) LANE(ch2) = nb;
+      }
+      const int cnt = pc + 1;
+      if (cnt < kMaxNodes) {
+        FOR_LANES(l) {
+          if (l > idx && l < cnt) S.bChild[static_cast<size_t>(p) * 8 + l] = LANE(ch2);
+          if (l == 0) {
+            S.bParent[nb] = p;
+            S.bCount[p] = static_cast<uint32_t>(cnt);
+          }
+        }
+        waveSync();
+        return;
+      }
+      const uint32_t np = allocBlk(0);
+      if (np == kNone) return;
+      FOR_LANES(l) {
+        if (l > idx && l < half) S.bChild[static_cast<size_t>(p) * 8 + l] = LANE(ch2);
+        if (l >= half && l < kMaxNodes) {
+          S.bChild[static_cast<size_t>(np) * 8 + (l - half)] = LANE(ch2);
+          S.bParent[LANE(ch2)] = np;
+        }
+        if (l == 0) {
+          if (idx + 1 < half) S.bParent[nb] = p;
+          S.bCount[p] = static_cast<uint32_t>(half);
+          S.bCount[np] = static_cast<uint32_t>(half);
+        }
+      }
+      waveSync();
+      const uint32_t pp = ldu(S.bParent + p);
       b = p;
+      nb = np;
+      p = pp;
     }
   }
 
@@ -1022,21 +1066,10 @@ class HugeDoc {
   }
 
   // ------------------------------------------------------------------ props
-  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {  // properties.ts:32-61, undefined ≡ {}
-    if (a == b) return true;
-    const uint32_t na = a == kNoProps ? 0u : ldu(S.props + a * 5), nb = b == kNoProps ? 0u : ldu(S.props + b * 5);
-    if (na != nb) return false;
-    for (uint32_t i = 0; i < na; i++) {
-      const uint32_t x = ldu(S.props + a * 5 + 1 + i);
-      bool found = false;
-      for (uint32_t j = 0; j < nb; j++) {
-        const uint32_t y = ldu(S.props + b * 5 + 1 + j);
-        if ((y >> 16) == (x >> 16)) found = y == x;
-      }
-      if (!found) return false;
-    }
-    return true;
-  }
+  // matchProperties (properties.ts:32-61, undefined ≡ {}) as equality of match classes: interned
+  // sets with the same (key, value) content in any key order share the class of the first of them.
+  FMT_DEV uint32_t propClass(uint32_t a) const { return a == kNoProps ? 0xFFFFu : L->pClass[a]; }
+  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || uni(propClass(a)) == uni(propClass(b)); }
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
     uint32_t kv[FMT_MT_PROPS_MAX] = {0, 0, 0, 0};
@@ -1082,11 +1115,32 @@ class HugeDoc {
       fail(FMT_E_CAPACITY);
       return kNoProps;
     }
-    const uint32_t id = static_cast<uint32_t>(nProps++);
+    const uint32_t id = static_cast<uint32_t>(nProps);
+    uint32_t cls = cnt == 0 ? 0xFFFFu : id;
+    for (int base = 0; cnt > 0 && base < nProps && cls == id; base += 64) {  // same content, other key order?
+      Lane<bool> same;
+      FOR_LANES(l) {
+        const int p = base + l;
+        bool eq = p < nProps && rd(S.props + (p * 5)) == cnt;
+        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
+          if (i < cnt) {
+            bool found = false;
+            for (uint32_t j = 0; j < FMT_MT_PROPS_MAX; j++)
+              if (j < cnt && rd(S.props + (p * 5 + 1 + j)) == kv[i]) found = true;
+            eq = eq && found;
+          }
+        }
+        LANE(same) = eq;
+      }
+      const uint64_t m = ballot(same);
+      if (m) cls = static_cast<uint32_t>(base + ctz64(m));
+    }
+    nProps++;
     FOR_LANES(l) {
       if (l == 0) {
         S.props[id * 5] = cnt;
         for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) S.props[id * 5 + 1 + i] = kv[i];
+        L->pClass[id] = static_cast<uint16_t>(cls);
       }
     }
     waveSync();
@@ -1096,10 +1150,12 @@ class HugeDoc {
   // ------------------------------------------------------------------ op pieces
   // splitLeafSegment (mergeTree.ts:1768-1796) of leaf (b, k) at offset o (0 < o < len): the right part
   // follows it in the same block, with a fresh id; a window leaf's right part joins the window table.
-  FMT_DEV bool splitLeaf(uint32_t b, int k, int o, uint32_t* rightId = nullptr) {
+  // R: the block in registers (loaded here); on return *rb/*rk locate the right part.
+  FMT_DEV bool splitLeaf(BlockRegs& R, uint32_t b, int k, int o, uint32_t* rightId, uint32_t* rb, int* rk) {
     ProfScope ps_(prof[14]);
     invalidate();
-    Leaf x = getLeaf(b, k);
+    loadBlock(b, R);
+    Leaf x = regLeaf(R, k);
     if (nextId >= S.idCap) return fail(FMT_E_CAPACITY);
     Leaf y = x;
     y.id = nextId++;
@@ -1107,22 +1163,30 @@ class HugeDoc {
     y.len = x.len - static_cast<uint32_t>(o);
     y.text = x.text + static_cast<uint32_t>(o);
     x.len = static_cast<uint32_t>(o);
-    const uint32_t cnt = ldu(S.bCount + b);
-    shiftUp(b, k + 1, static_cast<int>(cnt));
-    putLeaf(b, k, x);
-    putLeaf(b, k + 1, y);
-    const uint32_t w = ldu(S.winIdx + x.id);
+    const uint32_t w = readlane(R.wi, k);
+    uint32_t wy = kNone;
     if (w != kNone) {
       st1(wWord(w, 2), x.len);
-      winAdd(y.id, y.ins, y.rm, y.len, ldu(wWord3(w)) & kWMetaMask, ldu(S.bGroup + b), b);
+      wy = winAdd(y.id, y.ins, y.rm, y.len, ldu(wWord3(w)) & kWMetaMask, R.g, b);
     } else {
       st1(S.winIdx + y.id, kNone);
     }
-    childAdded(b);
+    setLane(R.f[0], k, x.len);
+    regsInsert(R, k + 1, y, wy);
+    st1(S.leafBlk + y.id, b);
+    const uint32_t nb = commitBlock(R);
+    if (nb != kNone && k + 1 >= kMaxNodes / 2) {
+      *rb = nb;
+      *rk = k + 1 - kMaxNodes / 2;
+    } else {
+      *rb = b;
+      *rk = k + 1;
+    }
+    if (nb != kNone) R.b = kNone;  // the registers no longer describe one block
     return status == FMT_OK;
   }
 
-  // After a split the right part's location: it followed (b, k) before childAdded may have moved it.
+  // Where leaf `id` is now (its block from leafBlk, its slot by id).
   FMT_DEV void locate(uint32_t id, uint32_t* b, int* k) const {
     const uint32_t bb = ldu(S.leafBlk + id);
     const uint32_t cnt = ldu(S.bCount + bb);
@@ -1134,9 +1198,9 @@ class HugeDoc {
   }
 
   // The leaf block after b in document order (kNone at the end).
-  FMT_DEV uint32_t nextBlockOf(uint32_t b) const {
-    uint32_t g = ldu(S.bGroup + b);
-    uint32_t s = ldu(S.bSlot + b) + 1;
+  FMT_DEV uint32_t nextBlockOf(uint32_t b) const { return nextBlockAt(ldu(S.bGroup + b), ldu(S.bSlot + b)); }
+  FMT_DEV uint32_t nextBlockAt(uint32_t g, uint32_t s) const {  // after slot s of group g
+    s++;
     if (s < L->gCount[g]) return ldu(slotBlkPtr(g) + s);
     for (int k = groupPos(g) + 1; k < nGroups; k++) {
       g = L->gOrder[k];
@@ -1154,11 +1218,11 @@ class HugeDoc {
     const Hit h = find(p, r, c);
     uint32_t b;
     int k;
+    BlockRegs R;
+    R.b = kNone;
     if (h.found) {
       if (h.st < p) {
-        uint32_t right;
-        if (!splitLeaf(h.blk, h.k, p - h.st, &right)) return;
-        locate(right, &b, &k);
+        if (!splitLeaf(R, h.blk, h.k, p - h.st, nullptr, &b, &k)) return;
       } else {
         b = h.blk;
         k = h.k;
@@ -1173,13 +1237,15 @@ class HugeDoc {
         return;
       }
       b = lastBlk;
-      k = static_cast<int>(ldu(S.bCount + b));
+      k = -1;
     }
     if (op.len == 0) return;
     if (nextId >= S.idCap) {
       fail(FMT_E_CAPACITY);
       return;
     }
+    if (R.b != b) loadBlock(b, R);  // (after a split without overflow the block is still in registers)
+    if (k < 0) k = R.cnt;
     Leaf x;
     x.len = op.len;
     x.ins = op.seq;
@@ -1188,17 +1254,12 @@ class HugeDoc {
     x.id = nextId++;
     x.text = op.payload;
     x.meta = mkMeta(c, kNoProps);
-    const uint32_t cnt = ldu(S.bCount + b);
-    shiftUp(b, k, static_cast<int>(cnt));
-    putLeaf(b, k, x);
-    winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, ldu(S.bGroup + b), b);
-    invalidate();
-    childAdded(b);
+    const uint32_t wx = winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, R.g, b);
+    regsInsert(R, k, x, wx);
+    st1(S.leafBlk + x.id, b);
+    const uint32_t nb = commitBlock(R);
     if (status != FMT_OK) return;
-    uint32_t bb;
-    int kk;
-    locate(x.id, &bb, &kk);
-    lru(bb, x.id, op.seq);
+    lru(nb != kNone && k >= kMaxNodes / 2 ? nb : b, x.id, op.seq);
   }
 
   // View lengths of the leaves of block b (lane k = leaf k) from PriorPerspective(r, c).
@@ -1228,8 +1289,8 @@ class HugeDoc {
     if (!h.found) return;  // nothing at or after start: no boundary, no hit
     const uint32_t idStart = ldu(S.lId + li(h.blk, h.k));
     // the leaf strictly containing end, walking from the start leaf
-    uint32_t idEnd = kNone;
-    int offEnd = 0;
+    uint32_t idEnd = kNone, endB = kNone;
+    int offEnd = 0, endK = 0;
     {
       uint32_t b = h.blk;
       int k = h.k, pos = h.st;
@@ -1241,6 +1302,8 @@ class HugeDoc {
           if (pos < end && end < pos + v) {
             idEnd = ldu(S.lId + li(b, k));
             offEnd = end - pos;
+            endB = b;
+            endK = k;
             break;
           }
           pos += v;
@@ -1251,68 +1314,114 @@ class HugeDoc {
         }
       }
     }
-    uint32_t first = idStart;
+    // boundary splits; the leaves' positions are tracked while no split overflows a block
+    BlockRegs R;
+    uint32_t fb = h.blk;  // the first leaf of the range
+    int fk = h.k;
+    uint32_t firstIdv = idStart;
     if (h.st < start) {  // ensureIntervalBoundary(start)
       uint32_t right;
-      if (!splitLeaf(h.blk, h.k, start - h.st, &right)) return;
+      if (!splitLeaf(R, h.blk, h.k, start - h.st, &right, &fb, &fk)) return;
+      firstIdv = right;
       if (idEnd == idStart) {
         idEnd = right;
         offEnd -= start - h.st;
+        endB = fb;
+        endK = fk;
+      } else if (R.b == kNone) {
+        endB = kNone;  // moved by an overflow: locate below
+      } else if (endB == h.blk) {
+        endK++;
       }
-      first = right;
     }
     if (idEnd != kNone && offEnd > 0) {  // ensureIntervalBoundary(end)
-      uint32_t b;
-      int k;
-      locate(idEnd, &b, &k);
-      if (!splitLeaf(b, k, offEnd)) return;
+      if (endB == kNone) locate(idEnd, &endB, &endK);
+      uint32_t rb;
+      int rk;
+      if (!splitLeaf(R, endB, endK, offEnd, nullptr, &rb, &rk)) return;
+      if (R.b == kNone) locate(firstIdv, &fb, &fk);  // an overflow may have moved the first leaf
     }
     if (end <= start) return;
-    uint32_t b;
-    int k;
-    locate(first, &b, &k);
+    uint32_t b = fb;
+    int k = fk;
     int pos = start;
     while (b != kNone && pos < end) {
+      // the block's leaves, their window entries and the block's list position in one round each
       const uint32_t cnt = ldu(S.bCount + b);
-      const Lane<uint32_t> vis = blockVis(b, cnt, r, c);
+      const uint32_t g = ldu(S.bGroup + b), s = ldu(S.bSlot + b);
+      bool scour = ldi(S.bScour + b) == 1;
+      Lane<uint32_t> f[8], wi, vis;
+      FOR_LANES(l) {
+        const size_t i = li(b, l < static_cast<int>(cnt) ? l : 0);
+        LANE(f[0]) = rd(S.lLen + i);
+        LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
+        LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
+        LANE(f[3]) = rd(S.lMlo + i);
+        LANE(f[4]) = rd(S.lMhi + i);
+        LANE(f[5]) = rd(S.lId + i);
+        LANE(f[6]) = rd(S.lText + i);
+        LANE(f[7]) = rd(S.lMeta + i);
+      }
+      FOR_LANES(l) {
+        LANE(wi) = rd(S.winIdx + LANE(f[5]));
+        LANE(vis) = l < static_cast<int>(cnt)
+                        ? static_cast<uint32_t>(visOf(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
+                                                      LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c))
+                        : 0u;
+      }
+      int stableDelta = 0;
       for (; k < static_cast<int>(cnt) && pos < end; k++) {
         const int v = static_cast<int>(readlane(vis, k));
         if (v > 0) {
-          Leaf x = getLeaf(b, k);
-          if (op.type == FMT_MT_REMOVE) removeLeaf(b, k, x, seq, c);
+          Leaf x;
+          x.len = readlane(f[0], k);
+          x.ins = static_cast<int32_t>(readlane(f[1], k));
+          x.rm = static_cast<int32_t>(readlane(f[2], k));
+          x.mlo = readlane(f[3], k);
+          x.mhi = readlane(f[4], k);
+          x.id = readlane(f[5], k);
+          x.text = readlane(f[6], k);
+          x.meta = readlane(f[7], k);
+          if (op.type == FMT_MT_REMOVE) stableDelta += removeLeaf(b, k, x, seq, c, readlane(wi, k), g);
           else annotateLeaf(b, k, x, op.payload);
           if (status != FMT_OK) return;
-          lru(b, x.id, seq);
-          if (status != FMT_OK) return;
+          if (!scour && seq > curSeq) {  // addToLRUSet (mergeTree.ts:812-822), once per block
+            st1(S.bScour + b, 1);
+            heapAdd(seq, x.id);
+            scour = true;
+            if (status != FMT_OK) return;
+          }
         }
         pos += v;
       }
+      if (stableDelta) addStableAt(g, s, stableDelta);
       if (pos < end) {
-        b = nextBlockOf(b);
+        b = nextBlockAt(g, s);
         k = 0;
       }
     }
   }
 
-  FMT_DEV void removeLeaf(uint32_t b, int j, Leaf& x, int seq, int c) {
+  // Remove leaf (b, j) (window entry w, block group g); returns the change of b's stable sum.
+  FMT_DEV int removeLeaf(uint32_t b, int j, Leaf& x, int seq, int c, uint32_t w, uint32_t g) {
     const bool was = x.rm != kNotRemoved;
     if (!was) x.rm = seq;
     if (c < 32) x.mlo |= 1u << c;
     else x.mhi |= 1u << (c - 32);
     putLeaf(b, j, x);
-    const uint32_t w = ldu(S.winIdx + x.id);
+    invalidate();
     if (w == kNone) {  // a stable leaf enters the window: its length leaves the stable sums
-      addStable(b, -static_cast<int>(x.len));
-      winAdd(x.id, x.ins, x.rm, x.len, (mkMeta(mClient(x.meta), 0) & 0xFFu) | (static_cast<uint32_t>(c) << 8),
-             ldu(S.bGroup + b), b);
-    } else if (!was) {
+      winAdd(x.id, x.ins, x.rm, x.len, (mkMeta(mClient(x.meta), 0) & 0xFFu) | (static_cast<uint32_t>(c) << 8), g, b);
+      return -static_cast<int>(x.len);
+    }
+    if (!was) {
       const uint32_t m3 = ldu(wWord3(w));
       st1(wWord(w, 1), static_cast<uint32_t>(x.rm));
       st1(wWord3(w), (m3 & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(c) << 8));
     } else {
       st1(wWord3(w), ldu(wWord3(w)) | (1u << 16));  // a later remover: full set from the leaf
     }
-    invalidate();
+    return 0;
   }
 
   FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId) {
@@ -1388,6 +1497,68 @@ class HugeDoc {
     uint32_t mergeBase;
   };
   FMT_DEV bool scourPlan(const Lane<uint32_t>* f, const Lane<uint32_t>& lastCh, const Lane<int>& cntL, int nBlk, ScourPlan& P) {
+    if (!scourDecideWide(f, lastCh, cntL, P)) scourDecideSerial(f, lastCh, cntL, nBlk, P);
+    return scourText(f, P);
+  }
+
+  // The decisions lane-parallel. Leaf s appends onto its run iff it and leaf s-1 (same block) are
+  // acked, not removed and non-empty, s-1 does not end in '\n', their props match, and (s's length
+  // <= TextSegmentGranularity or its run so far is): the last condition is decided here only when
+  // s is short; otherwise (returns false) the serial rule decides.
+  FMT_DEV bool scourDecideWide(const Lane<uint32_t>* f, const Lane<uint32_t>& lastCh, const Lane<int>& cntL, ScourPlan& P) {
+    Lane<uint32_t> ak, cls;
+    Lane<bool> dropL;
+    FOR_LANES(l) {
+      const bool valid = (l & 7) < LANE(cntL);
+      const int32_t ins = static_cast<int32_t>(LANE(f[1])), rm = static_cast<int32_t>(LANE(f[2]));
+      LANE(ak) = (valid && rm == kNotRemoved && ins <= minSeq && LANE(f[0]) > 0) ? 1u : 0u;  // acked, kept, non-empty
+      LANE(dropL) = valid && rm != kNotRemoved && rm <= minSeq;
+      LANE(cls) = propClass(mProps(LANE(f[7])));
+    }
+    const Lane<uint32_t> akP = shflUp1(ak), lastP = shflUp1(lastCh), clsP = shflUp1(cls);
+    Lane<bool> app, longApp;
+    FOR_LANES(l) {
+      const bool a = (l & 7) != 0 && LANE(ak) && LANE(akP) && LANE(lastP) != 10u && LANE(clsP) == LANE(cls);
+      LANE(app) = a;
+      LANE(longApp) = a && LANE(f[0]) > static_cast<uint32_t>(kGranularity);
+    }
+    if (ballot(longApp)) return false;
+    // output index of each opening lane (kept, not appended), and the latest opener at/before each lane
+    Lane<uint32_t> opens;
+    FOR_LANES(l) { LANE(opens) = ((l & 7) < LANE(cntL) && !LANE(dropL) && !LANE(app)) ? 1u : 0u; }
+    uint32_t total;
+    const Lane<uint32_t> outIdx = waveExclusiveSum(opens, &total);
+    Lane<int32_t> op;
+    FOR_LANES(l) { LANE(op) = LANE(opens) ? static_cast<int32_t>(LANE(outIdx)) : -1; }
+    const Lane<int32_t> lastOpen = waveExclusiveMax(op, -1);
+    FOR_LANES(l) {
+      LANE(P.dst) = LANE(opens) ? static_cast<int>(LANE(outIdx)) : (LANE(app) ? LANE(lastOpen) : -1);
+      if (l < kMaxNodes * kMaxNodes) L->tmp[l] = 0u;
+    }
+    waveSync();
+    FOR_LANES(l) {
+      if (LANE(opens)) L->tmp[64 + LANE(outIdx)] = static_cast<uint32_t>(l);
+      if (LANE(P.dst) >= 0) atomicAddLds(reinterpret_cast<int32_t*>(&L->tmp[LANE(P.dst)]), static_cast<int>(LANE(f[0])));
+    }
+    waveSync();
+    FOR_LANES(l) {
+      LANE(P.srcOf) = l < static_cast<int>(total) ? static_cast<int>(L->tmp[64 + l]) : 0;
+      LANE(P.outLen) = l < static_cast<int>(total) ? L->tmp[l] : 0u;
+    }
+    waveSync();
+    // output j is a merged run iff the lane after its opener appended
+    Lane<uint32_t> appU;
+    FOR_LANES(l) { LANE(appU) = LANE(app) ? 1u : 0u; }
+    const Lane<uint32_t> nextApp = shflDown1(appU);
+    const Lane<uint32_t> headJ = gather(nextApp, P.srcOf);
+    Lane<bool> hb;
+    FOR_LANES(l) { LANE(hb) = l < static_cast<int>(total) && LANE(headJ) != 0; }
+    P.heads = ballot(hb);
+    P.total = static_cast<int>(total);
+    return true;
+  }
+
+  FMT_DEV void scourDecideSerial(const Lane<uint32_t>* f, const Lane<uint32_t>& lastCh, const Lane<int>& cntL, int nBlk, ScourPlan& P) {
     FOR_LANES(l) {
       LANE(P.dst) = -1;
       LANE(P.srcOf) = 0;
@@ -1435,6 +1606,10 @@ class HugeDoc {
         }
       }
     }
+  }
+
+  // The merged runs' text, concatenated in lane order, into the merge area.
+  FMT_DEV bool scourText(const Lane<uint32_t>* f, ScourPlan& P) {
     Lane<uint32_t> member;
     FOR_LANES(l) {
       const int d = LANE(P.dst);

@@ -12,6 +12,8 @@
 
 namespace fmt_kernels {
 
+static_assert(sizeof(fmt_huge::HugeLds) <= 160 * 1024, "the huge-document LDS state must fit one CU's LDS");
+
 __global__ __launch_bounds__(64) void hugeDocKernel(const fmt_huge::HugeState* __restrict__ states,
                                                     const fmt_huge::HugeInputs* __restrict__ inputs,
                                                     const HugeOut* __restrict__ outs, uint32_t count) {

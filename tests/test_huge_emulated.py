@@ -35,3 +35,29 @@ def test_huge_engine_matches_oracle(orc, segs, ops, clients, lag, rng, seed, tin
     got = emu_huge_replay(batch, tiny_groups=tiny)
     assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
     assert compare_doc(exp, got) == []
+
+
+def test_huge_engine_prop_sets_in_other_key_order_match(orc):
+    """matchProperties ignores key order: clients 2k and 2k+1 annotate {a, b} with the same values in
+    opposite key orders, so zamboni appends across their leaves (the engine's prop match classes;
+    comparing prop set ids instead makes this case differ from the oracle)."""
+    import dataclasses
+
+    import numpy as np
+
+    from fluidframework_amd.streams import js_json
+    batch = workloads.t3_stream(300, 20000, n_clients=4, max_lag=64, max_range=100, seed=1)
+    n = len(batch.props_off) - 1
+    kv = []
+    for c in range(n):
+        pa, pb = (0 << 16) | (1 + (c // 2) % 3), (1 << 16) | 1
+        kv += [pa, pb] if c % 2 == 0 else [pb, pa]
+    batch = dataclasses.replace(batch, props_off=np.arange(0, 2 * n + 1, 2, dtype=np.uint32),
+                                props_kv=np.array(kv, dtype=np.uint32), keys=["a", "b"],
+                                values=["null"] + [js_json(i) for i in range(8)])
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    for tiny in (False, True):
+        got = emu_huge_replay(batch, tiny_groups=tiny)
+        assert int(got[0]["status"]) == 0
+        assert compare_doc(exp, got) == []
