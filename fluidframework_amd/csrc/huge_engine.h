@@ -68,6 +68,16 @@ constexpr int kWGroupShift = 17;
 constexpr int kWinList = 1024;  // LDS list of one group's visible window entries (slot pass)
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));
+typedef uint32_t u32x2 __attribute__((vector_size(8)));
+FMT_DEV u32x2 ld2(const uint32_t* p) {  // one 8-byte vector load (p 8-byte aligned)
+#if FMT_GPU
+  return *reinterpret_cast<const u32x2*>(p);
+#else
+  u32x2 v;
+  __builtin_memcpy(&v, p, sizeof v);
+  return v;
+#endif
+}
 FMT_DEV u32x4 ld4(const uint32_t* p) {  // one 16-byte vector load (p 16-byte aligned)
 #if FMT_GPU
   return *reinterpret_cast<const u32x4*>(p);
@@ -114,6 +124,7 @@ struct HugeState {
   // window table [winCap]: one 16-byte record per entry {ins, rm, len, meta | group << 17} (one
   // vector load per entry in the window passes), plus the entry's leaf block and leaf id
   uint32_t* wRec;
+  uint32_t* wMask;  // [winCap * 2]: the leaf's remove-client set (lo, hi), loaded with the record
   uint32_t* wBlk;
   uint32_t* wLeaf;
   uint32_t winCap;
@@ -136,6 +147,7 @@ struct HugeLds {
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
   uint32_t tmp[256];
   uint16_t pClass[kPropCap];     // prop set id -> its match class (the first set with the same content)
+  int32_t cmd[8];                // pass command from wave 0 to the helper waves (HugeDoc::PassCmd)
   uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
   int32_t wlVis[kWinList];
 };
@@ -181,8 +193,10 @@ class HugeDoc {
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
-  // 12 insert, 13 range ops, 14 leaf split, 15 interior pack
-  static constexpr int kProf = 16;
+  // 12 insert, 13 range ops, 14 leaf split, 15 interior pack; counts: 16 group passes, 17 slot
+  // passes, 18 Σ window entries at group passes, 19 Σ groups at group passes; 20 wave 0's window
+  // share time, 21 group scan time
+  static constexpr int kProf = 24;
   uint64_t prof[kProf] = {};
   struct ProfScope {
     uint64_t& a;
@@ -257,7 +271,8 @@ class HugeDoc {
   }
 
   // ------------------------------------------------------------------ window table
-  FMT_DEV uint32_t winAdd(uint32_t id, int32_t ins, int32_t rm, uint32_t len, uint32_t meta, uint32_t grp, uint32_t blk) {
+  FMT_DEV uint32_t winAdd(uint32_t id, int32_t ins, int32_t rm, uint32_t len, uint32_t meta, uint32_t grp, uint32_t blk,
+                         uint32_t mlo = 0, uint32_t mhi = 0) {
     invalidate();
     if (nWin >= S.winCap) {
       fail(FMT_E_CAPACITY);
@@ -271,6 +286,8 @@ class HugeDoc {
         rec[1] = static_cast<uint32_t>(rm);
         rec[2] = len;
         rec[3] = (meta & kWMetaMask) | (grp << kWGroupShift);
+        S.wMask[2 * w] = mlo;
+        S.wMask[2 * w + 1] = mhi;
         S.wBlk[w] = blk;
         S.wLeaf[w] = id;
         S.winIdx[id] = w;
@@ -285,6 +302,7 @@ class HugeDoc {
     if (w != last) {
       const uint32_t* src = S.wRec + static_cast<size_t>(last) * 4;
       const uint32_t a = ldu(src), b = ldu(src + 1), c = ldu(src + 2), d = ldu(src + 3);
+      const uint32_t ml = ldu(S.wMask + 2 * last), mh = ldu(S.wMask + 2 * last + 1);
       const uint32_t f = ldu(S.wBlk + last), g = ldu(S.wLeaf + last);
       FOR_LANES(l) {
         if (l == 0) {
@@ -293,6 +311,8 @@ class HugeDoc {
           rec[1] = b;
           rec[2] = c;
           rec[3] = d;
+          S.wMask[2 * w] = ml;
+          S.wMask[2 * w + 1] = mh;
           S.wBlk[w] = f;
           S.wLeaf[w] = g;
           S.winIdx[g] = w;
@@ -515,53 +535,159 @@ class HugeDoc {
 
   // ------------------------------------------------------------------ perspective corrections
   // View length of window entry w (fields already loaded) for PriorPerspective(r, c).
-  FMT_DEV int winVis(uint32_t w, int32_t ins, int32_t rm, uint32_t len, uint32_t m, int r, int c) const {
-    if ((m >> 16) & 1u) {  // several removers: the leaf's full remover set
-      const uint32_t id = rd(S.wLeaf + w);
-      const uint32_t b = rd(S.leafBlk + id);
-      const int bc = static_cast<int>(rd(S.bCount + b));  // (slots past the count hold stale leaves)
-      uint32_t mlo = 0, mhi = 0;
-      for (int k = 0; k < bc; k++) {
-        const size_t i = static_cast<size_t>(b) * 8 + k;
-        if (rd(S.lId + i) == id) {
-          mlo = rd(S.lMlo + i);
-          mhi = rd(S.lMhi + i);
-        }
-      }
-      return visOf(len, ins, rm, mlo, mhi, mClient(m), r, c);
-    }
-    const bool byC = rm != kNotRemoved && static_cast<int>(wFirstRm(m)) == c;
-    return ((ins <= r || mClient(m) == c) && !(rm <= r || byC)) ? static_cast<int>(len) : 0;
+  FMT_DEV static int winVis(int32_t ins, int32_t rm, uint32_t len, uint32_t m, uint32_t mlo, uint32_t mhi, int r, int c) {
+    return visOf(len, ins, rm, mlo, mhi, mClient(m), r, c);
   }
 
-  // One pass over the window table, 16 x 64 records per step with every load of a step in flight
-  // together (one 16-byte load per record): for each entry of positive view length, add it to
-  // gCorr[group] (bySlot false); or (bySlot true) for each such entry of group `only`, add it to
-  // sLen[slot of its block] — those entries are first listed in LDS, then their blocks' slots are
-  // loaded for the whole list at once.
-  static constexpr int kPassU = 16;
-  FMT_DEV void windowPass(int r, int c, uint32_t only, bool bySlot) {
-    int nList = 0;
-    for (uint32_t base = 0; base < nWin; base += 64 * kPassU) {
-      Lane<u32x4> rec[kPassU];
-      FOR_LANES(l) {
+  // ---- passes shared by the workgroup's waves. Wave 0 replays; when it needs a pass it posts the
+  // command in LDS and the kWaves waves (one per SIMD) each take every kWaves-th step of it, between
+  // workgroup barriers. (Host emulation: wave 0 runs every share itself.)
+  static constexpr int kWaves = 4;
+  static constexpr int kListPerWave = kWinList / kWaves;
+  enum : int { kCmdExit = 0, kCmdGroups = 1, kCmdSlots = 2 };
+  struct PassCmd {
+    int op, r, c;
+    uint32_t g, nWin;
+  };
+  FMT_DEV void runPass(int op, int r, int c, uint32_t g) {
+    const PassCmd cmd{op, r, c, g, nWin};
+    FOR_LANES(l) {
+      if (l == 0) {
+        L->cmd[0] = op;
+        L->cmd[1] = r;
+        L->cmd[2] = c;
+        L->cmd[3] = static_cast<int32_t>(g);
+        L->cmd[4] = static_cast<int32_t>(nWin);
+      }
+    }
+    waveSync();
+#if FMT_GPU
+    groupBarrier();
+    if (op == kCmdSlots) {
+      slotShare(cmd, 0);
+      groupBarrier();
+    }
+    {
+      ProfScope psW_(prof[20]);
+      windowShare(cmd, 0);
+    }
+    groupBarrier();
+#else
+    if (op == kCmdSlots)
+      for (int w = 0; w < kWaves; w++) slotShare(cmd, w);
+    for (int w = 0; w < kWaves; w++) windowShare(cmd, w);
+#endif
+  }
+  // Helper waves 1..kWaves-1: serve pass commands until wave 0 posts kCmdExit.
+  FMT_DEV void helperLoop(int wave) {
+    for (;;) {
+      groupBarrier();
+      const PassCmd cmd{uni(L->cmd[0]), uni(L->cmd[1]), uni(L->cmd[2]), static_cast<uint32_t>(uni(L->cmd[3])),
+                        static_cast<uint32_t>(uni(L->cmd[4]))};
+      if (cmd.op == kCmdExit) return;
+      if (cmd.op == kCmdSlots) {
+        slotShare(cmd, wave);
+        groupBarrier();
+      }
+      windowShare(cmd, wave);
+      groupBarrier();
+    }
+  }
+  FMT_DEV void postExit() {  // wave 0, after the replay: releases the helper waves
+    FOR_LANES(l) {
+      if (l == 0) L->cmd[0] = kCmdExit;
+    }
+    waveSync();
+#if FMT_GPU
+    groupBarrier();
+#endif
+  }
+
+  // Slots of group cmd.g into sLen / sBlk (their stable lengths), this wave's steps.
+  FMT_DEV void slotShare(const PassCmd& cmd, int wave) {
+    const uint32_t g = cmd.g;
+    const int cnt = static_cast<int>(L->gCount[g]);
+    const uint32_t* sb = slotBlkPtr(g);
+    const int32_t* ss = slotStPtr(g);
+    // 64-slot pieces dealt round-robin to the waves: piece (u * kWaves + wave) of each step
+    for (int base = 0; base < cnt; base += kWaves * 64 * kShiftU) {
+      Lane<uint32_t> bb[kShiftU];
+      Lane<int32_t> sv[kShiftU];
 #pragma unroll
-        for (int u = 0; u < kPassU; u++) {
-          const uint32_t w = base + 64 * u + l;
-          if (w < nWin) LANE(rec[u]) = ld4(S.wRec + static_cast<size_t>(w) * 4);
+      for (int u = 0; u < kShiftU; u++) {
+        const int p0 = base + (u * kWaves + wave) * 64;
+        if (p0 < cnt) {
+          FOR_LANES(l) {
+            const int i = p0 + l;
+            if (i < cnt) {
+              LANE(bb[u]) = rd(sb + i);
+              LANE(sv[u]) = rd(ss + i);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kShiftU; u++) {
+        const int p0 = base + (u * kWaves + wave) * 64;
+        if (p0 < cnt) {
+          FOR_LANES(l) {
+            const int i = p0 + l;
+            if (i < cnt) {
+              L->sBlk[i] = LANE(bb[u]);
+              L->sLen[i] = LANE(sv[u]);
+            }
+          }
+        }
+      }
+    }
+    waveSync();
+  }
+
+  // This wave's steps of one pass over the window table, 16 x 64 records per step with every load of
+  // a step in flight together (one 16-byte load per record): for each entry of positive view length,
+  // add it to gCorr[group] (kCmdGroups); or (kCmdSlots) for each such entry of group cmd.g, add it
+  // to sLen[slot of its block] — those entries are first listed in this wave's part of the LDS list,
+  // then their blocks' slots are loaded for the whole list at once.
+  static constexpr int kPassU = 16;
+  FMT_DEV void windowShare(const PassCmd& cmd, int wave) {
+    const int r = cmd.r, c = cmd.c;
+    const uint32_t n = cmd.nWin;
+    const bool bySlot = cmd.op == kCmdSlots;
+    const uint32_t only = bySlot ? cmd.g : kNone;
+    uint32_t* lEnt = L->wlEnt + wave * kListPerWave;
+    int32_t* lVis = L->wlVis + wave * kListPerWave;
+    int nList = 0;
+    // 64-record pieces dealt round-robin to the waves: piece (u * kWaves + wave) of each step
+    for (uint32_t base = 0; base < n; base += kWaves * 64 * kPassU) {
+      Lane<u32x4> rec[kPassU];
+      Lane<u32x2> msk[kPassU];
+      int nu = 0;  // this wave's pieces in this step
+#pragma unroll
+      for (int u = 0; u < kPassU; u++) {
+        const uint32_t p0 = base + static_cast<uint32_t>(u * kWaves + wave) * 64;
+        if (p0 < n) {
+          nu = u + 1;
+          FOR_LANES(l) {
+            const uint32_t w = p0 + l;
+            if (w < n) {
+              LANE(rec[u]) = ld4(S.wRec + static_cast<size_t>(w) * 4);
+              LANE(msk[u]) = ld2(S.wMask + static_cast<size_t>(w) * 2);
+            }
+          }
         }
       }
       Lane<uint32_t> vis[kPassU];
       FOR_LANES(l) {
 #pragma unroll
         for (int u = 0; u < kPassU; u++) {
-          const uint32_t w = base + 64 * u + l;
+          const uint32_t w = base + static_cast<uint32_t>(u * kWaves + wave) * 64 + l;
           uint32_t v = 0;
-          if (w < nWin) {
+          if (u < nu && w < n) {
             const u32x4 x = LANE(rec[u]);
             const uint32_t grp = x[3] >> kWGroupShift;
             if (only == kNone || grp == only) {
-              v = static_cast<uint32_t>(winVis(w, static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, r, c));
+              const u32x2 mk = LANE(msk[u]);
+              v = static_cast<uint32_t>(winVis(static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, mk[0], mk[1], r, c));
               if (v && !bySlot) atomicAddLds(&L->gCorr[grp], static_cast<int>(v));
             }
           }
@@ -569,40 +695,36 @@ class HugeDoc {
         }
       }
       if (bySlot) {
-        // compact this step's hits into the LDS list (entry, view length)
 #pragma unroll
         for (int u = 0; u < kPassU; u++) {
           Lane<bool> hit;
-          FOR_LANES(l) { LANE(hit) = LANE(vis[u]) != 0; }
+          FOR_LANES(l) { LANE(hit) = u < nu && LANE(vis[u]) != 0; }
           const uint64_t m = ballot(hit);
           if (!m) continue;
-          if (nList + 64 > kWinList) {
-            flushSlotList(nList);
+          if (nList + 64 > kListPerWave) {
+            flushSlotList(lEnt, lVis, nList);
             nList = 0;
           }
           FOR_LANES(l) {
             if ((m >> l) & 1ull) {
               const int at = nList + __builtin_popcountll(m & ((1ull << l) - 1));
-              L->wlEnt[at] = base + 64 * u + l;
-              L->wlVis[at] = static_cast<int32_t>(LANE(vis[u]));
+              lEnt[at] = base + static_cast<uint32_t>(u * kWaves + wave) * 64 + l;
+              lVis[at] = static_cast<int32_t>(LANE(vis[u]));
             }
           }
           nList += __builtin_popcountll(m);
         }
       }
     }
-    if (bySlot && nList) flushSlotList(nList);
+    if (bySlot && nList) flushSlotList(lEnt, lVis, nList);
     waveSync();
   }
   // sLen[slot of the block of listed entry i] += its view length, for the n listed entries.
-  FMT_DEV void flushSlotList(int n) {
+  FMT_DEV void flushSlotList(const uint32_t* lEnt, const int32_t* lVis, int n) {
     waveSync();
     for (int base = 0; base < n; base += 64) {
       FOR_LANES(l) {
-        if (base + l < n) {
-          const uint32_t w = L->wlEnt[base + l];
-          atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + w))], L->wlVis[base + l]);
-        }
+        if (base + l < n) atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + lEnt[base + l]))], lVis[base + l]);
       }
     }
     waveSync();
@@ -615,7 +737,11 @@ class HugeDoc {
       for (int g = l; g < nGroups; g += 64) L->gCorr[g] = 0;
     }
     waveSync();
-    windowPass(r, c, kNone, false);
+    prof[16]++;
+    prof[18] += nWin;
+    prof[19] += static_cast<uint64_t>(nGroups);
+    runPass(kCmdGroups, r, c, kNone);
+    ProfScope psScan_(prof[21]);
     int32_t base = 0;
     for (int k0 = 0; k0 < nGroups; k0 += 64) {
       Lane<uint32_t> len;
@@ -650,35 +776,8 @@ class HugeDoc {
     slotCacheG = g;
     slotCacheEpoch = epoch;
     ProfScope ps_(prof[2]);
-    const int cnt = static_cast<int>(L->gCount[g]);
-    const uint32_t* sb = slotBlkPtr(g);
-    const int32_t* ss = slotStPtr(g);
-    for (int base = 0; base < cnt; base += 64 * kShiftU) {  // kShiftU x 64 slots per step, loads in flight together
-      Lane<uint32_t> bb[kShiftU];
-      Lane<int32_t> sv[kShiftU];
-      FOR_LANES(l) {
-#pragma unroll
-        for (int u = 0; u < kShiftU; u++) {
-          const int i = base + 64 * u + l;
-          if (i < cnt) {
-            LANE(bb[u]) = rd(sb + i);
-            LANE(sv[u]) = rd(ss + i);
-          }
-        }
-      }
-      FOR_LANES(l) {
-#pragma unroll
-        for (int u = 0; u < kShiftU; u++) {
-          const int i = base + 64 * u + l;
-          if (i < cnt) {
-            L->sBlk[i] = LANE(bb[u]);
-            L->sLen[i] = LANE(sv[u]);
-          }
-        }
-      }
-    }
-    waveSync();
-    windowPass(r, c, g, true);
+    prof[17]++;
+    runPass(kCmdSlots, r, c, g);
   }
 
   // ------------------------------------------------------------------ the hierarchical search
@@ -1167,7 +1266,7 @@ class HugeDoc {
     uint32_t wy = kNone;
     if (w != kNone) {
       st1(wWord(w, 2), x.len);
-      wy = winAdd(y.id, y.ins, y.rm, y.len, ldu(wWord3(w)) & kWMetaMask, R.g, b);
+      wy = winAdd(y.id, y.ins, y.rm, y.len, ldu(wWord3(w)) & kWMetaMask, R.g, b, y.mlo, y.mhi);
     } else {
       st1(S.winIdx + y.id, kNone);
     }
@@ -1411,7 +1510,7 @@ class HugeDoc {
     putLeaf(b, j, x);
     invalidate();
     if (w == kNone) {  // a stable leaf enters the window: its length leaves the stable sums
-      winAdd(x.id, x.ins, x.rm, x.len, (mkMeta(mClient(x.meta), 0) & 0xFFu) | (static_cast<uint32_t>(c) << 8), g, b);
+      winAdd(x.id, x.ins, x.rm, x.len, (mkMeta(mClient(x.meta), 0) & 0xFFu) | (static_cast<uint32_t>(c) << 8), g, b, x.mlo, x.mhi);
       return -static_cast<int>(x.len);
     }
     if (!was) {
@@ -1419,8 +1518,10 @@ class HugeDoc {
       st1(wWord(w, 1), static_cast<uint32_t>(x.rm));
       st1(wWord3(w), (m3 & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(c) << 8));
     } else {
-      st1(wWord3(w), ldu(wWord3(w)) | (1u << 16));  // a later remover: full set from the leaf
+      st1(wWord3(w), ldu(wWord3(w)) | (1u << 16));  // a later remover
     }
+    st1(S.wMask + 2 * w, x.mlo);
+    st1(S.wMask + 2 * w + 1, x.mhi);
     return 0;
   }
 
@@ -2223,7 +2324,8 @@ class HugeDoc {
           if (w != kNone) {
             nw++;
             if (S.wLeaf[w] != id || S.wBlk[w] != b || (S.wRec[4 * w + 3] >> kWGroupShift) != g || S.wRec[4 * w + 2] != S.lLen[i] ||
-                static_cast<int32_t>(S.wRec[4 * w]) != S.lIns[i] || static_cast<int32_t>(S.wRec[4 * w + 1]) != S.lRm[i])
+                static_cast<int32_t>(S.wRec[4 * w]) != S.lIns[i] || static_cast<int32_t>(S.wRec[4 * w + 1]) != S.lRm[i] ||
+                S.wMask[2 * w] != S.lMlo[i] || S.wMask[2 * w + 1] != S.lMhi[i])
               return bad("window entry", id, w);
           } else if (S.lRm[i] == kNotRemoved) {
             st += S.lLen[i];

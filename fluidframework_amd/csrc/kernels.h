@@ -76,7 +76,7 @@ struct HugeOut {
   uint16_t* chars;
   uint64_t capChars;
   fmt_mt_propset* props;
-  unsigned long long* prof;  // [16] shader-clock totals per phase (huge_engine.h HugeDoc::prof)
+  unsigned long long* prof;  // [24] shader-clock totals per phase (huge_engine.h HugeDoc::prof)
 };
 size_t hugeLdsBytes();
 hipError_t launchHugeDocs(const fmt_huge::HugeState* states, const fmt_huge::HugeInputs* inputs, const HugeOut* outs,

@@ -521,7 +521,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       FMT_ALLOC(gSlotBlk, uint32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
       FMT_ALLOC(gSlotStable, int32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
       FMT_ALLOC(leafBlk, uint32_t, S.idCap) FMT_ALLOC(winIdx, uint32_t, S.idCap)
-      FMT_ALLOC(wRec, uint32_t, static_cast<size_t>(S.winCap) * 4) FMT_ALLOC(wBlk, uint32_t, S.winCap)
+      FMT_ALLOC(wRec, uint32_t, static_cast<size_t>(S.winCap) * 4) FMT_ALLOC(wMask, uint32_t, static_cast<size_t>(S.winCap) * 2)
+      FMT_ALLOC(wBlk, uint32_t, S.winCap)
       FMT_ALLOC(wLeaf, uint32_t, S.winCap)
       FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * 5)
 #undef FMT_ALLOC
@@ -549,7 +550,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       O.chars = static_cast<uint16_t*>(p);
       FMT_HIP(c, alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p));
       O.props = static_cast<fmt_mt_propset*>(p);
-      FMT_HIP(c, alloc(16 * sizeof(unsigned long long), &p));
+      FMT_HIP(c, alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p));
       O.prof = static_cast<unsigned long long*>(p);
     }
   }
@@ -712,10 +713,10 @@ int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out
 }
 
 // Internal diagnostic (not part of fmt.h): shader-clock totals per phase of a huge document's last
-// replay (huge_engine.h HugeDoc::prof), 16 values; FMT_E_USAGE if `doc` is not a huge document.
+// replay (huge_engine.h HugeDoc::prof), HugeDoc::kProf values; FMT_E_USAGE if `doc` is not a huge document.
 int fmt_internal_huge_profile(fmt_ctx* c, uint32_t doc, uint64_t* out) {
   if (c == nullptr || out == nullptr || doc >= c->mtHugeSlot.size() || c->mtHugeSlot[doc] < 0) return FMT_E_USAGE;
-  FMT_HIP(c, hipMemcpy(out, c->huge[static_cast<size_t>(c->mtHugeSlot[doc])].out.prof, 16 * sizeof(uint64_t),
+  FMT_HIP(c, hipMemcpy(out, c->huge[static_cast<size_t>(c->mtHugeSlot[doc])].out.prof, fmt_huge::HugeDoc::kProf * sizeof(uint64_t),
                        hipMemcpyDeviceToHost));
   return FMT_OK;
 }

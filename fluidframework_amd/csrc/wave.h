@@ -182,6 +182,10 @@ FMT_DEV void waveSync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Workgroup barrier (all waves; LDS and memory ordered across it). Call only from wave-uniform
+// control flow on every wave the same number of times.
+FMT_DEV void groupBarrier() { __syncthreads(); }
+
 #else  // host emulation (tests only)
 
 #include <cstring>
@@ -278,6 +282,7 @@ inline Lane<uint32_t> gather(const Lane<uint32_t>& x, const Lane<int>& src) {
 }
 
 inline void waveSync() {}
+inline void groupBarrier() {}
 
 #endif
 

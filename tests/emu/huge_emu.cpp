@@ -47,8 +47,8 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   S.gSlotBlk = gsb.data(); S.gSlotStable = gss.data();
   std::vector<uint32_t> ids(2ull * S.idCap, kNone);
   S.leafBlk = ids.data(); S.winIdx = ids.data() + S.idCap;
-  std::vector<uint32_t> wu(6ull * S.winCap);
-  S.wRec = wu.data(); S.wBlk = S.wRec + 4ull * S.winCap; S.wLeaf = S.wBlk + S.winCap;
+  std::vector<uint32_t> wu(8ull * S.winCap);
+  S.wRec = wu.data(); S.wMask = S.wRec + 4ull * S.winCap; S.wBlk = S.wMask + 2ull * S.winCap; S.wLeaf = S.wBlk + S.winCap;
   std::vector<uint16_t> text(textCap);
   std::memcpy(text.data(), b->text, b->text_len * 2);
   S.text = text.data(); S.textLen = b->text_len; S.textCap = textCap;
