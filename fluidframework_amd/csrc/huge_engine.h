@@ -1343,6 +1343,15 @@ class HugeDoc {
       fail(FMT_E_CAPACITY);
       return;
     }
+    uint32_t insProps = kNoProps;  // seg {text, props}: properties = clone(props) (textSegment.ts:41-52)
+    if (op.pos2 > 0) {
+      if (static_cast<uint32_t>(op.pos2 - 1) >= in.nPropsOps) {
+        fail(FMT_E_DATA);
+        return;
+      }
+      insProps = applyProps(kNoProps, static_cast<uint32_t>(op.pos2 - 1));
+      if (status != FMT_OK) return;
+    }
     if (R.b != b) loadBlock(b, R);  // (after a split without overflow the block is still in registers)
     if (k < 0) k = R.cnt;
     Leaf x;
@@ -1352,7 +1361,7 @@ class HugeDoc {
     x.mlo = x.mhi = 0;
     x.id = nextId++;
     x.text = op.payload;
-    x.meta = mkMeta(c, kNoProps);
+    x.meta = mkMeta(c, insProps);
     const uint32_t wx = winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, R.g, b);
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);

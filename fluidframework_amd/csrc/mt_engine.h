@@ -69,13 +69,13 @@ struct LargeTier {
   static constexpr int kCapChars = 131071;  // a leaf length (17 bits) can hold all of them
   static constexpr int kMaxBlocks = 1023;   // ids 0..1022; 1023 = no block
   static constexpr int kHeapCap = 1023;     // at most one heap entry per block (needsScour)
-  static constexpr int kPropCap = 64;       // prop-set ids in their own word W6; 0xFFFF = undefined
+  static constexpr int kPropCap = 256;      // prop-set ids in their own word W6; 0xFFFF = undefined
   static constexpr int kLenBits = 17, kBlkBits = 10;
   static constexpr bool kHbmChars = true;
   static constexpr bool kUnroll = false;    // rows indexed at run time (private memory)
   static constexpr int kWords = 7;          // remove-client set: W3 (ids 0..31) + W5 (ids 32..63); W6 props
   static constexpr int kMaxClient = 63;
-  static constexpr bool kPropsWord = true;  // prop-set id in W6 (up to 64 sets)
+  static constexpr bool kPropsWord = true;  // prop-set id in W6
   using BId = uint16_t;
   using VR = V32;
 };
@@ -127,9 +127,7 @@ struct Scratch {
   Blk<typename C::BId> blk[C::kMaxBlocks];
   HeapEnt heap[C::kHeapCap + 1];  // 1-based
   PropSet props[C::kPropCap];
-  typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type propEq[C::kPropCap];  // bit b of
-                                 // propEq[a]: matchProperties(set a, set b)
-  typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type propsEmpty;  // bit p: set p has no keys
+  uint16_t propCls[C::kPropCap];  // match class: the first interned set with the same content (empty: 0xFFFF)
   typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
@@ -205,7 +203,6 @@ class Doc {
   // FMT_E_CAPACITY. Every other capacity failure of the small tier escalates.
   static constexpr int kCapFinal = C::kHbmChars ? FMT_E_CAPACITY : kCapacityFinal;
   static constexpr uint32_t kPropsUndef = kPW ? 0xFFFFu : (1u << (32 - C::kLenBits - C::kBlkBits)) - 1u;
-  using PMask = typename std::conditional<(C::kPropCap > 32), uint64_t, uint32_t>::type;
   static_assert(kMaxBlocks <= static_cast<int>(kNoBlk) && kPropCap <= static_cast<int>(kPropsUndef), "W0 field widths");
   static_assert(kRows <= 32, "row bitmasks are 32-bit");
   FMT_DEV static uint32_t fLen(uint32_t w0) { return w0 & kLenMask; }
@@ -692,50 +689,41 @@ class Doc {
   }
 
   // ------------------------------------------------------------------ prop sets
-  // matchProperties (properties.ts:32-61; undefined ≡ {}) from the match matrix kept at interning.
-  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const {
-    if (a == b) return true;
-    if (a == kPropsUndef) return ((uniM(s->propsEmpty) >> b) & 1u) != 0;
-    if (b == kPropsUndef) return ((uniM(s->propsEmpty) >> a) & 1u) != 0;
-    return ((uniM(s->propEq[a]) >> b) & 1u) != 0;
-  }
+  // matchProperties (properties.ts:32-61; undefined ≡ {}) as equality of match classes, kept when
+  // sets are interned: sets with the same (key, value) content in any key order share the class of
+  // the first of them; the empty set's class is undefined's.
+  FMT_DEV uint32_t propCls(uint32_t a) const { return a == kPropsUndef ? 0xFFFFu : static_cast<uint32_t>(uni(static_cast<uint32_t>(s->propCls[a]))); }
+  FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || propCls(a) == propCls(b); }
 
-  FMT_DEV static uint32_t uniM(uint32_t x) { return uni(x); }
-  FMT_DEV static uint64_t uniM(uint64_t x) {
-    return static_cast<uint64_t>(uni(static_cast<uint32_t>(x))) | (static_cast<uint64_t>(uni(static_cast<uint32_t>(x >> 32))) << 32);
-  }
-
-  // A new prop set q (kv[0..cnt)) was interned: lane p < q compares set p with it as maps
-  // (same size, every key of one present with the same value in the other), then both rows of the
-  // match matrix are updated.
+  // The class of a new set q (kv[0..cnt)): lane p < q compares set p with it as maps (same size,
+  // every key of one present with the same value in the other); the first match names the class.
   FMT_DEV void propsIndex(int q, const V4& kv, uint32_t cnt) {
-    Lane<bool> eq;
-    FOR_LANES(l) {
-      bool m = l < q && s->props[l].n == cnt;
-      if (m) {
+    uint32_t cls = cnt == 0 ? 0xFFFFu : static_cast<uint32_t>(q);
+    for (int base = 0; cnt > 0 && base < q && cls == static_cast<uint32_t>(q); base += 64) {
+      Lane<bool> eq;
+      FOR_LANES(l) {
+        const int p = base + l;
+        bool m = p < q && s->props[p].n == cnt;
+        if (m) {
 #pragma unroll
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
-          if (i < cnt) {
-            bool found = false;
+          for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
+            if (i < cnt) {
+              bool found = false;
 #pragma unroll
-            for (uint32_t k = 0; k < FMT_MT_PROPS_MAX; k++)
-              if (k < cnt && (s->props[l].kv[k] >> 16) == (kv[i] >> 16)) found = s->props[l].kv[k] == kv[i];
-            m = m && found;
+              for (uint32_t k = 0; k < FMT_MT_PROPS_MAX; k++)
+                if (k < cnt && (s->props[p].kv[k] >> 16) == (kv[i] >> 16)) found = s->props[p].kv[k] == kv[i];
+              m = m && found;
+            }
           }
         }
+        LANE(eq) = m;
       }
-      LANE(eq) = m;
+      const uint64_t mq = ballot(eq);
+      if (mq) cls = static_cast<uint32_t>(base + ctz64(mq));
     }
-    const uint64_t mq = ballot(eq);
-    waveSync();
-    const PMask empty = uniM(s->propsEmpty);
     waveSync();
     FOR_LANES(l) {
-      if (l < q && ((mq >> l) & 1ull)) s->propEq[l] |= PMask(1) << q;
-      if (l == 0) {
-        s->propEq[q] = static_cast<PMask>(mq) | (PMask(1) << q);
-        s->propsEmpty = empty | (cnt == 0 ? PMask(1) << q : PMask(0));
-      }
+      if (l == 0) s->propCls[q] = static_cast<uint16_t>(cls);
     }
     waveSync();
   }
@@ -776,17 +764,18 @@ class Doc {
         cnt++;
       }
     }
-    {  // interned already? lane p checks prop set p (kPropCap <= 64: one ballot)
+    for (int base = 0; base < nProps; base += 64) {  // interned already? lane p checks prop set base + p
       Lane<bool> same;
       FOR_LANES(l) {
-        bool eq = l < nProps && s->props[l].n == cnt;
+        const int p = base + l;
+        bool eq = p < nProps && s->props[p].n == cnt;
 #pragma unroll
         for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-          if (i < cnt) eq = eq && s->props[l].kv[i] == kv[i];
+          if (i < cnt) eq = eq && s->props[p].kv[i] == kv[i];
         LANE(same) = eq;
       }
       const uint64_t m = ballot(same);
-      if (m != 0) return static_cast<uint32_t>(ctz64(m));
+      if (m != 0) return static_cast<uint32_t>(base + ctz64(m));
     }
     if (nProps >= kPropCap) {
       fail(FMT_E_CAPACITY);
@@ -1048,6 +1037,17 @@ class Doc {
     const int js = containing(vis, st, pos, nr, &sp);
     if (js >= 0 && !splitLeafAt(js, pos - sp)) return -1;
     if (len <= 0) return -1;
+    // seg {text, props}: the new segment's properties = clone(props) (textSegment.ts:41-52,
+    // mergeTreeNodes.ts:343-347): raw LWW of the props op onto an empty set
+    uint32_t insProps = kPropsUndef;
+    if (op.pos2 > 0) {
+      if (static_cast<uint32_t>(op.pos2 - 1) >= in.nPropsOps) {
+        fail(FMT_E_DATA);
+        return -1;
+      }
+      insProps = applyProps(kPropsUndef, static_cast<uint32_t>(op.pos2 - 1));
+      if (status != FMT_OK) return -1;
+    }
     int insIdx = js >= 0 ? js + 1 : -1;
     FOR_ROWS(r, 0, nr) {
       if (insIdx < 0) {
@@ -1087,13 +1087,13 @@ class Doc {
     nChars += len;
     stamp(kPfInsChars);
     LeafRec rec;
-    rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), kPropsUndef);
+    rec.w[0] = mkW0(static_cast<uint32_t>(len), static_cast<uint32_t>(blk), insProps);
     rec.w[1] = static_cast<uint32_t>(seq);
     rec.w[2] = static_cast<uint32_t>(kNotRemoved);
     rec.w[3] = 0;
     rec.w[4] = mkW4(nextId++, client);
     rec.w[5] = 0;
-    rec.w[6] = kPropsUndef;
+    rec.w[6] = insProps;
     if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
       s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
       waveSync();
@@ -1710,7 +1710,6 @@ class Doc {
     }
     FOR_LANES(l) {
       for (int i = l; i < kMaxBlocks; i += 64) s->freeList[i] = static_cast<BId>(kMaxBlocks - 1 - i);
-      if (l == 0) s->propsEmpty = 0;
     }
     waveSync();
     nFree = kMaxBlocks;

@@ -276,16 +276,19 @@ class MergeTreeStreamBuilder {
 			type = op.type;
 			if (type === MT_INSERT) {
 				let seg = op.seg;
-				if (typeof seg !== "string") {
-					if (seg && typeof seg === "object" && "text" in seg && !(seg.props && Object.keys(seg.props).length)) {
+				let props = null;
+				if (typeof seg !== "string") { // IJSONTextSegment {text, props} (textSegment.ts:44-52)
+					if (seg && typeof seg === "object" && "text" in seg && Object.keys(seg).every((k) => k === "text" || k === "props")) {
+						props = seg.props === undefined ? null : seg.props;
 						seg = seg.text;
 					} else {
-						throw new UnsupportedOp("insert of markers or pre-annotated segments");
+						throw new UnsupportedOp("insert of markers");
 					}
 				}
 				const r = this.text.push(seg);
 				if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
-				pos1 = op.pos1; pos2 = -1; payload = r[0]; len = r[1];
+				// pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
+				pos1 = op.pos1; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1];
 			} else if (type === MT_REMOVE || type === MT_OBLITERATE) {
 				pos1 = op.pos1; pos2 = op.pos2; // non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
 			} else if (type === MT_OBLITERATE_SIDED) {

@@ -203,6 +203,14 @@ function v1Summary(segs, minSeq, curSeq, keys, values, clientNames, removers, ch
  * @param messages - [{message, firstOp, count}] as the batch builder kept them.
  * @param ranges - [{op, pos1, pos2, type}] catch-up ranges of the document (engine output).
  */
+function insertSegJson(seg) {
+	if (typeof seg === "string") return seg;
+	if (seg.props === undefined || seg.props === null) return seg.text;
+	const props = {};
+	for (const [k, v] of Object.entries(seg.props)) if (v !== undefined && v !== null) props[k] = v;
+	return { text: seg.text, props };
+}
+
 function catchupMessages(messages, ranges, minSeq) {
 	const byOp = new Map();
 	for (const r of ranges) {
@@ -221,7 +229,9 @@ function catchupMessages(messages, ranges, minSeq) {
 			members.forEach((op, k) => {
 				for (const r of byOp.get(firstOp + k) || []) {
 					if (r.type === MT_INSERT) {
-						ops.push({ pos1: r.pos1, seg: typeof op.seg === "string" ? op.seg : op.seg.text, type: r.type });
+						// createInsertOp(pos, segment.clone().toJSONObject()): {text, props} when the
+						// segment has properties (textSegment.ts:62-66; clone(props) drops nulls)
+						ops.push({ pos1: r.pos1, seg: insertSegJson(op.seg), type: r.type });
 					} else if (r.type === MT_REMOVE || r.type === MT_OBLITERATE) {
 						// createRemoveRangeOp / createObliterateRangeOp
 						ops.push({ pos1: r.pos1, pos2: r.pos2, type: r.type });

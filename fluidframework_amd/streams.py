@@ -257,15 +257,19 @@ class MergeTreeStreamBuilder:
             raise UnsupportedOp("relative positions")
         if t == MT_INSERT:
             seg = op["seg"]
-            if not isinstance(seg, str):
-                if isinstance(seg, dict) and "text" in seg and not seg.get("props"):
+            props = None
+            if not isinstance(seg, str):  # IJSONTextSegment {text, props} (textSegment.ts:44-52)
+                if isinstance(seg, dict) and "text" in seg and set(seg) <= {"text", "props"}:
+                    props = seg.get("props")
                     seg = seg["text"]
                 else:
-                    raise UnsupportedOp("insert of markers or pre-annotated segments")
+                    raise UnsupportedOp("insert of markers")
             off, n = self._text(seg)
             if n > 0xFFFF:
                 raise UnsupportedOp("insert longer than 65535 UTF-16 units")
-            return (seq, ref, msn, int(op["pos1"]), -1, off, n, client, MT_INSERT, 0)
+            # pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
+            pos2 = -1 if props is None else self._props_op(props) + 1
+            return (seq, ref, msn, int(op["pos1"]), pos2, off, n, client, MT_INSERT, 0)
         if t == MT_REMOVE:
             return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_REMOVE, 0)
         if t == MT_OBLITERATE:  # non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}

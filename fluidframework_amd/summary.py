@@ -247,6 +247,17 @@ def v1_summary(header, leaves, chars, propsets, keys, values, client_names, remo
     return head, [body_of(c) + "}" for c in chunks[1:]]
 
 
+def _insert_seg_json(seg):
+    """TextSegment.toJSONObject of the inserted segment (textSegment.ts:62-66): the text, or
+    {text, props} when it has properties (clone(props) drops null values, properties.ts:68-95)."""
+    if isinstance(seg, str):
+        return seg
+    props = seg.get("props")
+    if props is None:
+        return seg["text"]
+    return {"text": seg["text"], "props": {k: props[k] for k in js_key_order(list(props)) if props[k] is not None}}
+
+
 def catchup_messages(messages, ranges, min_seq):
     """The legacy summary's catch-up messages for one document (sequence.ts:949-1018).
 
@@ -274,8 +285,7 @@ def catchup_messages(messages, ranges, min_seq):
             for k, op in enumerate(members):
                 for t, p1, p2 in by_op.get(first + k, []):
                     if t == MT_INSERT:  # createInsertOp(pos, segment.clone().toJSONObject())
-                        seg = op["seg"]
-                        ops.append({"pos1": p1, "seg": seg if isinstance(seg, str) else seg["text"], "type": t})
+                        ops.append({"pos1": p1, "seg": _insert_seg_json(op["seg"]), "type": t})
                     elif t in (MT_REMOVE, MT_OBLITERATE):  # createRemoveRangeOp / createObliterateRangeOp
                         ops.append({"pos1": p1, "pos2": p2, "type": t})
                     else:  # createAnnotateRangeOp(pos1, pos2, {...props}): the segment's value ?? null

@@ -11,7 +11,7 @@ import subprocess
 
 import numpy as np
 
-from .streams import (MAP_OP_DTYPE, MT_OP_DTYPE, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
+from .streams import (MAP_OP_DTYPE, MT_INSERT, MT_OP_DTYPE, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
                       MergeTreeBatch, js_json)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -146,3 +146,27 @@ def t3_stream(n_segments: int = 10_000_000, n_ops: int = 10_000_000, n_clients: 
         snapshots=snaps,
         snapshot_segs=segs,
     )
+
+
+def with_insert_props(batch: MergeTreeBatch, every: int = 3) -> MergeTreeBatch:
+    """A copy of a conflict-farm batch where every `every`-th insert (by seq) carries a segment
+    spec {text, props} (SharedString.insertText(pos, text, props), sharedString.ts:198-200): by
+    turns the client's {"client"} set, a two-key {"color", "client"} set, or {"color": null} (an
+    empty property set: null values are dropped, properties.ts:68-95)."""
+    import dataclasses
+
+    ops = batch.ops.copy()
+    n = len(batch.props_off) - 1
+    kc, vr = len(batch.keys), len(batch.values)
+    kv, off = [int(x) for x in batch.props_kv], [int(x) for x in batch.props_off]
+    for c in range(n):  # n + c: {"color": red|blue, "client": c}
+        kv += [(kc << 16) | (vr + (c & 1)), int(batch.props_kv[off[c]])]
+        off.append(len(kv))
+    kv.append(kc << 16)  # 2n: {"color": null}
+    off.append(len(kv))
+    ins = (ops["type"] == MT_INSERT) & (ops["seq"] % every == 0)
+    pick = (ops["seq"] // every + ops["client"].astype(np.int32)) % 3
+    pid = np.where(pick == 0, ops["client"].astype(np.int32), np.where(pick == 1, n + ops["client"].astype(np.int32), 2 * n))
+    ops["pos2"] = np.where(ins, pid + 1, ops["pos2"])
+    return dataclasses.replace(batch, ops=ops, props_off=np.asarray(off, np.uint32), props_kv=np.asarray(kv, np.uint32),
+                               keys=batch.keys + ["color"], values=batch.values + [js_json("red"), js_json("blue")])

@@ -100,7 +100,7 @@ typedef struct fmt_mt_op {
   int32_t ref_seq;  /* referenceSequenceNumber */
   int32_t min_seq;  /* minimumSequenceNumber */
   int32_t pos1;     /* op.pos1 */
-  int32_t pos2;     /* op.pos2, or -1 for insert */
+  int32_t pos2;     /* op.pos2; INSERT: props-op id + 1 of a {text, props} segment, <= 0 for a string */
   uint32_t payload; /* INSERT: offset of the text in the UTF-16 arena; ANNOTATE: props-op id */
   uint16_t len;     /* INSERT: text length in UTF-16 units (> 0) */
   uint8_t client;   /* short client id (client.ts:831-855): 1..63 in order of first appearance */

@@ -805,6 +805,24 @@ void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const ui
     case FMT_MT_INSERT: {
       Seg* s = makeSeg();
       s->text.assign(reinterpret_cast<const char16_t*>(arena + op.payload), op.len);
+      // seg {text, props}: TextSegment.make(text, props) → BaseSegment's `properties = clone(props)`
+      // (textSegment.ts:41-52, mergeTreeNodes.ts:343-347; clone = extend({}, props): null values
+      // dropped, properties.ts:68-95). pos2 = props-op id + 1 (0: a plain string segment).
+      if (op.pos2 > 0) {
+        const uint32_t id = static_cast<uint32_t>(op.pos2 - 1);
+        s->props.defined = true;
+        for (uint32_t i = propsOff[id]; i < propsOff[id + 1]; i++) {
+          const uint16_t key = static_cast<uint16_t>(propsKv[i] >> 16), value = static_cast<uint16_t>(propsKv[i] & 0xffff);
+          auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(), [&](const auto& e) { return e.first == key; });
+          if (value == 0) {
+            if (it != s->props.kv.end()) s->props.kv.erase(it);
+          } else if (it != s->props.kv.end()) {
+            it->second = value;
+          } else {
+            s->props.kv.emplace_back(key, value);
+          }
+        }
+      }
       insertSegments(op.pos1, s, p, stamp);
       break;
     }

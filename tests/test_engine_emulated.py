@@ -192,3 +192,22 @@ def test_many_writers_overflow_to_large_tier(orc, n_clients):
     for d in range(batch.n_docs):
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+@pytest.mark.parametrize("n_clients", [8, 16, 24])
+def test_inserts_with_props_match_oracle(orc, n_clients):
+    """Insert ops whose segment spec carries props ({text, props}: TextSegment.make(text, props)):
+    one- and two-key sets and an all-null set. Documents that overflow the small tier (more prop
+    sets or writers than it holds) are compared from the large tier, as the runtime escalates them."""
+    batch = workloads.with_insert_props(workloads.conflict_farm(30, n_clients=n_clients, ops_per_doc=1500, seed=19))
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+    assert rc == 0
+    small = emu_replay(batch)
+    large = emu_replay(batch, large=True)
+    assert (large[0]["status"] == 0).all(), np.unique(large[0]["status"])
+    assert set(np.unique(small[0]["status"])) <= {0, -3}
+    for d in range(batch.n_docs):
+        hdr, leaves, chars, props = small if int(small[0]["status"][d]) == 0 else large
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"

@@ -123,3 +123,16 @@ def test_t3_million_segments(orc, engine):
     assert int(hdrs[0]["status"]) == 0
     lv, ch, pr = engine.mt_doc(0, hdrs[0])
     assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+
+
+def test_huge_inserts_with_props(orc, engine):
+    """seg {text, props} inserts in a huge document (prop sets interned up to 4096)."""
+    batch = workloads.with_insert_props(workloads.t3_stream(200_000, 30_000, n_clients=32, max_lag=1024, max_range=8, seed=23))
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    leaves, chars, props = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], leaves, chars, props)) == []

@@ -35,7 +35,7 @@ def _gpu_mt(engine, batch):
 def _check_against_oracle(orc, engine, batch, docs=None):
     hdrs = _gpu_mt(engine, batch)
     cl, cc, cp = native.capacity()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=16, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=16, cap_leaves=cl, cap_chars=cc, cap_props=max(cp, 256))
     assert rc == 0
     docs = range(batch.n_docs) if docs is None else docs
     for d in docs:
@@ -134,6 +134,15 @@ def test_mt_reference_fixture_checkpoints(orc, engine):
 def test_mt_conflict_farm_matches_oracle(orc, engine, n_clients, min_length, seed):
     batch = workloads.conflict_farm(600, n_clients=n_clients, ops_per_doc=2000, min_length=min_length, seed=seed)
     _check_against_oracle(orc, engine, batch)
+
+
+@pytest.mark.parametrize("n_clients", [8, 24])
+def test_mt_inserts_with_props_match_oracle(orc, engine, n_clients):
+    """seg {text, props} inserts (one- and two-key sets, an all-null set): small tier, and with 24
+    writers the documents whose prop sets overflow it escalate to the large tier (256 sets)."""
+    batch = workloads.with_insert_props(workloads.conflict_farm(64, n_clients=n_clients, ops_per_doc=2000, seed=29))
+    hdrs = _check_against_oracle(orc, engine, batch)
+    assert (hdrs["status"] == 0).all()
 
 
 def test_mt_summaries_match_oracle(orc, engine):

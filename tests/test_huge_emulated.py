@@ -61,3 +61,13 @@ def test_huge_engine_prop_sets_in_other_key_order_match(orc):
         got = emu_huge_replay(batch, tiny_groups=tiny)
         assert int(got[0]["status"]) == 0
         assert compare_doc(exp, got) == []
+
+
+def test_huge_engine_inserts_with_props(orc):
+    """seg {text, props} inserts (TextSegment.make(text, props)) in a huge document."""
+    batch = workloads.with_insert_props(workloads.t3_stream(3000, 8000, n_clients=16, max_lag=300, max_range=8, seed=9))
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=True)
+    assert int(got[0]["status"]) == 0
+    assert compare_doc(exp, got) == []

@@ -1,0 +1,128 @@
+"""Inserts whose segment spec carries properties: `seg: {text, props}`, what
+SharedString.insertText(pos, text, props) sends (sharedString.ts:198-200). The new segment's
+properties are clone(props) (TextSegment.make, textSegment.ts:41-52; BaseSegment,
+mergeTreeNodes.ts:343-347): null values are dropped (properties.ts:68-95), so {"k": null} gives an
+empty (defined) property set. The packers put the props-op id + 1 in the insert's pos2.
+
+No reference fixture holds such an insert in a collaborative stream, so parity is pinned by the
+oracle restatement: engine == oracle bit for bit (emulated here, the GPU in test_gpu_parity.py), the
+JS packer == the Python packer byte for byte, and the catch-up op regenerated for such an insert
+carries {text, props} (createInsertOp(pos, segment.clone().toJSONObject()), sequence.ts:395-452).
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import streams, summary
+from fluidframework_amd.streams import MergeTreeStreamBuilder
+from mt_compare import compare_doc, emu_caps, emu_replay
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+
+
+def _messages():
+    """Three writers with lagging refSeqs: string inserts, {text, props} inserts (one key, two keys,
+    an all-null set, an empty props object), a GROUP with a props insert, annotates and removes."""
+    m = []
+
+    def add(client, seq, ref, contents, msn=0):
+        m.append({"clientId": client, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+                  "minimumSequenceNumber": msn, "contents": contents})
+
+    add("B", 1, 0, {"type": 0, "pos1": 0, "seg": {"text": "hello ", "props": {"bold": True}}})
+    add("C", 2, 0, {"type": 0, "pos1": 0, "seg": "plain "})
+    add("D", 3, 1, {"type": 0, "pos1": 3, "seg": {"text": "XY", "props": {"color": "red", "bold": None}}})
+    add("B", 4, 2, {"type": 0, "pos1": 5, "seg": {"text": "zz", "props": {"1": 7, "color": "blue"}}}, msn=1)
+    add("C", 5, 3, {"type": 2, "pos1": 2, "pos2": 9, "props": {"bold": False}}, msn=2)
+    add("D", 6, 4, {"type": 3, "ops": [{"type": 0, "pos1": 1, "seg": {"text": "g", "props": {"k": None}}},
+                                       {"type": 0, "pos1": 0, "seg": {"text": "e", "props": {}}}]}, msn=3)
+    add("B", 7, 5, {"type": 1, "pos1": 4, "pos2": 6}, msn=3)
+    add("C", 8, 6, {"type": 0, "pos1": 2, "seg": {"text": "tail\n", "props": {"bold": True}}}, msn=3)
+    add("D", 9, 8, {"type": 0, "pos1": 0, "seg": {"text": "hd", "props": {"bold": True}}}, msn=3)
+    return m
+
+
+def _batch(keep=False):
+    b = MergeTreeStreamBuilder(keep_messages=keep)
+    d = b.begin_doc("", observer="A")
+    for msg in _messages():
+        d.add_message(msg)
+    return b.finish(catchup=keep)
+
+
+def test_packer_puts_props_op_in_pos2():
+    batch = _batch()
+    ins = batch.ops[batch.ops["type"] == streams.MT_INSERT]
+    assert [int(x) for x in ins["pos2"]] == [1, -1, 2, 3, 5, 6, 1, 1]  # (props op 3: the annotate's)
+    sets = [[(batch.keys[kv >> 16], batch.values[kv & 0xFFFF]) for kv in batch.props_kv[batch.props_off[i]:batch.props_off[i + 1]]]
+            for i in range(len(batch.props_off) - 1)]
+    assert sets[1] == [("color", '"red"'), ("bold", "null")]
+    assert sets[2] == [("1", "7"), ("color", '"blue"')]  # JS key order: array-index keys first
+    assert sets[4] == [("k", "null")] and sets[5] == []
+
+
+def test_oracle_and_engine_apply_insert_props(orc):
+    batch = _batch()
+    for large in (False, True):
+        cl, cc, cp = emu_caps(large=large)
+        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+        assert rc == 0
+        hdr, leaves, chars, props = emu_replay(batch, large=large)
+        assert int(hdr[0]["status"]) == 0
+        assert compare_doc((oh[0], ol[0], oc[0], op[0]), (hdr[0], leaves[0], chars[0], props[0])) == []
+    # the sets the leaves hold: the two-key insert set survives as sent (JS key order), and no set
+    # holds a null value (clone(props) drops them)
+    h, lv, pr = oh[0], ol[0], op[0]
+    used = {int(L["props"]) for L in lv[: int(h["n_leaves"])]} - {0xFFFF}
+    sets = [[(batch.keys[kv >> 16], batch.values[kv & 0xFFFF]) for kv in pr[p]["kv"][: pr[p]["n"]]] for p in used]
+    assert [("1", "7"), ("color", '"blue"')] in sets
+    assert all(v != "null" for st in sets for _, v in st)
+
+
+def test_catchup_insert_keeps_props(orc):
+    batch = _batch(keep=True)
+    cap = 256
+    rc, oh, ol, oc, op, _, ocu = orc.mt_replay_batch(batch, cap_catchup=cap)
+    assert rc == 0
+    eh, el, ec, ep, ecu = emu_replay(batch, cap_catchup=cap)
+    n = int(oh[0]["n_catchup"])
+    assert int(eh[0]["n_catchup"]) == n and np.array_equal(ecu[0][:n], ocu[0][:n])
+    msgs = summary.catchup_messages(batch.messages[0], ocu[0][:n], int(oh[0]["min_seq"]))
+    segs = [op_["seg"] for msg in msgs for op_ in (msg["contents"]["ops"] if msg["contents"]["type"] == 3 else [msg["contents"]])
+            if op_["type"] == 0]
+    assert {"text": "g", "props": {}} in segs and {"text": "e", "props": {}} in segs
+    assert all(isinstance(s, str) or set(s) == {"text", "props"} for s in segs)
+    for s in segs:
+        if isinstance(s, dict):
+            assert None not in s["props"].values()
+
+
+@pytest.mark.skipif(NODE is None, reason="node is not installed")
+def test_js_packer_and_catchup_match_python():
+    msgs = _messages()
+    js = (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          f"const sm=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'summary.js'))});"
+          "const b=new fmt.MergeTreeStreamBuilder();const d=b.beginDoc('','A');"
+          f"for(const m of {json.dumps(msgs)}) d.addMessage(m);"
+          "const r=b.finish();"
+          "const ranges=[{op:0,pos1:0,pos2:0,type:0},{op:5,pos1:1,pos2:0,type:0},{op:6,pos1:0,pos2:0,type:0}];"
+          f"const kept={json.dumps(msgs)}.map((m,i)=>({{message:m,firstOp:[0,1,2,3,4,5,7,8,9][i]}}));"
+          "const cu=sm.catchupMessages(kept.slice(0,1).concat(kept.slice(5,6)),ranges,0);"
+          "process.stdout.write(JSON.stringify({ops:Buffer.from(r.ops.buffer,r.ops.byteOffset,r.ops.byteLength).toString('hex'),"
+          "off:Array.from(r.propsOff),kv:Array.from(r.propsKv),cu}))")
+    r = subprocess.run([NODE, "-e", js], capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    py = _batch()
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert out["off"] == [int(x) for x in py.props_off] and out["kv"] == [int(x) for x in py.props_kv]
+    ranges = [{"op": 0, "pos1": 0, "pos2": 0, "type": 0}, {"op": 5, "pos1": 1, "pos2": 0, "type": 0},
+              {"op": 6, "pos1": 0, "pos2": 0, "type": 0}]
+    kept = [(m, f, 1) for m, f in zip(msgs, [0, 1, 2, 3, 4, 5, 7, 8, 9])]
+    cu = summary.catchup_messages([kept[0], kept[5]], ranges, 0)
+    assert json.loads(summary.catchup_blob(cu)) == out["cu"]
