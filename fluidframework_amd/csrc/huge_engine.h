@@ -52,6 +52,7 @@ constexpr int kSlotCap = FMT_HUGE_SLOTCAP;  // leaf blocks listed per group
 constexpr int kGroupCap = 2048;       // groups
 constexpr int kHeapCap = 10240;       // LRU heap entries (≈ blocks registered in one window)
 constexpr int kPropCap = 4096;        // interned prop sets per document
+constexpr int kPropWords = 1 + FMT_MT_PROPS_MAX;  // a prop set in HBM: n, kv[]
 constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
 
 // Leaf meta word: insert client (int8) | prop set id << 8 (0xFFFF = properties undefined)
@@ -132,7 +133,7 @@ struct HugeState {
   uint16_t* text;
   uint64_t textLen;   // batch text (read-only part)
   uint64_t textCap;
-  uint32_t* props;    // [kPropCap * 5]: n, kv[4]
+  uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
 };
 
 // LDS state of the wave.
@@ -1171,11 +1172,11 @@ class HugeDoc {
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || uni(propClass(a)) == uni(propClass(b)); }
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
-    uint32_t kv[FMT_MT_PROPS_MAX] = {0, 0, 0, 0};
+    uint32_t kv[FMT_MT_PROPS_MAX] = {};
     uint32_t cnt = 0;
     if (old != kNoProps) {
-      cnt = ldu(S.props + old * 5);
-      for (uint32_t i = 0; i < cnt; i++) kv[i] = ldu(S.props + old * 5 + 1 + i);
+      cnt = ldu(S.props + old * kPropWords);
+      for (uint32_t i = 0; i < cnt; i++) kv[i] = ldu(S.props + old * kPropWords + 1 + i);
     }
     const uint32_t a = ldu(in.propsOff + opId), b = ldu(in.propsOff + opId + 1);
     for (uint32_t t = a; t < b; t++) {
@@ -1202,9 +1203,9 @@ class HugeDoc {
       Lane<bool> same;
       FOR_LANES(l) {
         const int p = base + l;
-        bool eq = p < nProps && rd(S.props + (p * 5)) == cnt;
+        bool eq = p < nProps && rd(S.props + (p * kPropWords)) == cnt;
         for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-          if (i < cnt) eq = eq && rd(S.props + (p * 5 + 1 + i)) == kv[i];
+          if (i < cnt) eq = eq && rd(S.props + (p * kPropWords + 1 + i)) == kv[i];
         LANE(same) = eq;
       }
       const uint64_t m = ballot(same);
@@ -1220,12 +1221,12 @@ class HugeDoc {
       Lane<bool> same;
       FOR_LANES(l) {
         const int p = base + l;
-        bool eq = p < nProps && rd(S.props + (p * 5)) == cnt;
+        bool eq = p < nProps && rd(S.props + (p * kPropWords)) == cnt;
         for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
           if (i < cnt) {
             bool found = false;
             for (uint32_t j = 0; j < FMT_MT_PROPS_MAX; j++)
-              if (j < cnt && rd(S.props + (p * 5 + 1 + j)) == kv[i]) found = true;
+              if (j < cnt && rd(S.props + (p * kPropWords + 1 + j)) == kv[i]) found = true;
             eq = eq && found;
           }
         }
@@ -1237,8 +1238,8 @@ class HugeDoc {
     nProps++;
     FOR_LANES(l) {
       if (l == 0) {
-        S.props[id * 5] = cnt;
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) S.props[id * 5 + 1 + i] = kv[i];
+        S.props[id * kPropWords] = cnt;
+        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) S.props[id * kPropWords + 1 + i] = kv[i];
         L->pClass[id] = static_cast<uint16_t>(cls);
       }
     }
@@ -2424,8 +2425,8 @@ class HugeDoc {
     FOR_LANES(l) {
       for (int p = l; p < nProps; p += 64) {
         fmt_mt_propset ps;
-        ps.n = rd(S.props + p * 5);
-        for (int k = 0; k < FMT_MT_PROPS_MAX; k++) ps.kv[k] = rd(S.props + p * 5 + 1 + k);
+        ps.n = rd(S.props + p * kPropWords);
+        for (int k = 0; k < FMT_MT_PROPS_MAX; k++) ps.kv[k] = rd(S.props + p * kPropWords + 1 + k);
         outProps[p] = ps;
       }
     }

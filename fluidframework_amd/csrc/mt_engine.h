@@ -128,6 +128,7 @@ struct Scratch {
   HeapEnt heap[C::kHeapCap + 1];  // 1-based
   PropSet props[C::kPropCap];
   uint16_t propCls[C::kPropCap];  // match class: the first interned set with the same content (empty: 0xFFFF)
+  uint32_t kvWork[FMT_MT_PROPS_MAX];  // applyProps' working set (wave-uniform)
   typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
@@ -695,26 +696,21 @@ class Doc {
   FMT_DEV uint32_t propCls(uint32_t a) const { return a == kPropsUndef ? 0xFFFFu : static_cast<uint32_t>(uni(static_cast<uint32_t>(s->propCls[a]))); }
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || propCls(a) == propCls(b); }
 
-  // The class of a new set q (kv[0..cnt)): lane p < q compares set p with it as maps (same size,
-  // every key of one present with the same value in the other); the first match names the class.
-  FMT_DEV void propsIndex(int q, const V4& kv, uint32_t cnt) {
+  // The class of a new set q (s->kvWork[0..cnt)): lane p < q compares set p with it as maps (same
+  // size, every key of one present with the same value in the other); the first match names it.
+  FMT_DEV void propsIndex(int q, uint32_t cnt) {
     uint32_t cls = cnt == 0 ? 0xFFFFu : static_cast<uint32_t>(q);
     for (int base = 0; cnt > 0 && base < q && cls == static_cast<uint32_t>(q); base += 64) {
       Lane<bool> eq;
       FOR_LANES(l) {
         const int p = base + l;
         bool m = p < q && s->props[p].n == cnt;
-        if (m) {
-#pragma unroll
-          for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
-            if (i < cnt) {
-              bool found = false;
-#pragma unroll
-              for (uint32_t k = 0; k < FMT_MT_PROPS_MAX; k++)
-                if (k < cnt && (s->props[p].kv[k] >> 16) == (kv[i] >> 16)) found = s->props[p].kv[k] == kv[i];
-              m = m && found;
-            }
-          }
+        for (uint32_t i = 0; m && i < cnt; i++) {
+          const uint32_t x = s->kvWork[i];
+          bool found = false;
+          for (uint32_t k = 0; k < cnt; k++)
+            if ((s->props[p].kv[k] >> 16) == (x >> 16)) found = s->props[p].kv[k] == x;
+          m = found;
         }
         LANE(eq) = m;
       }
@@ -729,49 +725,53 @@ class Doc {
   }
 
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
+  // The working set lives in LDS (kvWork, lane k = key slot k), so the sets' width costs no registers.
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
-    V4 kv;
-    uint32_t cnt = 0;
-    if (old != kPropsUndef) {
-      cnt = uni(s->props[old].n);
-      for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) kv[i] = i < cnt ? uni(s->props[old].kv[i]) : 0u;
-    } else {
-      for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) kv[i] = 0;
+    uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
+    FOR_LANES(l) {
+      if (l < FMT_MT_PROPS_MAX) s->kvWork[l] = (old != kPropsUndef && l < static_cast<int>(cnt)) ? s->props[old].kv[l] : 0u;
     }
+    waveSync();
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
     for (uint32_t t = a; t < b; t++) {
       const uint32_t e = uni(in.propsKv[t]);
       const uint32_t key = e >> 16;
-      uint32_t pos = cnt;
-      for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-        if (i < cnt && (kv[i] >> 16) == key) pos = i;
+      Lane<bool> hit;
+      FOR_LANES(l) { LANE(hit) = l < static_cast<int>(cnt) && (s->kvWork[l] >> 16) == key; }
+      const uint64_t m = ballot(hit);
+      const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
         if (pos < cnt) {
-          for (uint32_t i = 0; i + 1 < FMT_MT_PROPS_MAX; i++)
-            if (i >= pos && i + 1 < cnt) kv[i] = kv[i + 1];
+          Lane<uint32_t> v;
+          FOR_LANES(l) { LANE(v) = (l < FMT_MT_PROPS_MAX - 1 && l >= static_cast<int>(pos)) ? s->kvWork[l + 1] : 0u; }
+          waveSync();
+          FOR_LANES(l) {
+            if (l >= static_cast<int>(pos) && l + 1 < static_cast<int>(cnt)) s->kvWork[l] = LANE(v);
+          }
           cnt--;
         }
       } else if (pos < cnt) {
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-          if (i == pos) kv[i] = e;
+        FOR_LANES(l) {
+          if (l == static_cast<int>(pos)) s->kvWork[l] = e;
+        }
       } else {
         if (cnt >= FMT_MT_PROPS_MAX) {
           fail(kCapFinal);
           return 0;
         }
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-          if (i == cnt) kv[i] = e;
+        FOR_LANES(l) {
+          if (l == static_cast<int>(cnt)) s->kvWork[l] = e;
+        }
         cnt++;
       }
+      waveSync();
     }
     for (int base = 0; base < nProps; base += 64) {  // interned already? lane p checks prop set base + p
       Lane<bool> same;
       FOR_LANES(l) {
         const int p = base + l;
         bool eq = p < nProps && s->props[p].n == cnt;
-#pragma unroll
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-          if (i < cnt) eq = eq && s->props[p].kv[i] == kv[i];
+        for (uint32_t i = 0; eq && i < cnt; i++) eq = s->props[p].kv[i] == s->kvWork[i];
         LANE(same) = eq;
       }
       const uint64_t m = ballot(same);
@@ -781,9 +781,11 @@ class Doc {
       fail(FMT_E_CAPACITY);
       return 0;
     }
-    propsIndex(nProps, kv, cnt);
-    s->props[nProps].n = cnt;
-    for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) s->props[nProps].kv[i] = kv[i];
+    propsIndex(nProps, cnt);
+    FOR_LANES(l) {
+      if (l == 0) s->props[nProps].n = cnt;
+      if (l < FMT_MT_PROPS_MAX) s->props[nProps].kv[l] = s->kvWork[l];
+    }
     waveSync();
     return static_cast<uint32_t>(nProps++);
   }
@@ -2027,12 +2029,13 @@ class Doc {
     FOR_LANES(l) {
       if constexpr (!C::kHbmChars)
         for (int t = l; t < nChars; t += 64) out.chars[t] = s->chars[t];
-      for (int p = l; p < nProps; p += 64) {
-        fmt_mt_propset ps;
-        ps.n = s->props[p].n;
-#pragma unroll
-        for (int k = 0; k < FMT_MT_PROPS_MAX; k++) ps.kv[k] = s->props[p].kv[k];
-        out.props[p] = ps;
+    }
+    {  // prop sets word by word (lane = one word of the flat table): no per-lane struct copies
+      constexpr int kPW = 1 + FMT_MT_PROPS_MAX;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(out.props);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(s->props);
+      FOR_LANES(l) {
+        for (int t = l; t < nProps * kPW; t += 64) dst[t] = src[t];
       }
     }
     // remove-order entries: leaf id -> final leaf index (FMT_MT_LEAF_GONE once zamboni dropped it)

@@ -524,7 +524,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       FMT_ALLOC(wRec, uint32_t, static_cast<size_t>(S.winCap) * 4) FMT_ALLOC(wMask, uint32_t, static_cast<size_t>(S.winCap) * 2)
       FMT_ALLOC(wBlk, uint32_t, S.winCap)
       FMT_ALLOC(wLeaf, uint32_t, S.winCap)
-      FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * 5)
+      FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * fmt_huge::kPropWords)
 #undef FMT_ALLOC
       S.textLen = b->text_len;
       S.textCap = textCap;

@@ -28,6 +28,7 @@ struct Lane {
 // register-relative moves (M0 / set_gpr_idx), never to scratch memory.
 typedef uint32_t V8 __attribute__((ext_vector_type(8)));
 typedef uint32_t V4 __attribute__((ext_vector_type(4)));
+typedef uint32_t VKV __attribute__((ext_vector_type(FMT_MT_PROPS_MAX)));  // one prop set's (key, value) words
 #define LANE(x) ((x).v)
 #define FOR_LANES(l) for ([[maybe_unused]] int l = static_cast<int>(__lane_id()), l##_once = 1; l##_once; l##_once = 0)
 
@@ -209,6 +210,7 @@ struct V4 {
   uint32_t& operator[](int i) { return x[i]; }
   const uint32_t& operator[](int i) const { return x[i]; }
 };
+using VKV = VecN<FMT_MT_PROPS_MAX>;
 #define LANE(x) ((x).v[l])
 #define FOR_LANES(l) for (int l = 0; l < 64; l++)
 

@@ -24,10 +24,10 @@ const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
 const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate places (client.ts:680-700)
 const MAX_CLIENTS = 63;
 const NOT_REMOVED = 0x7fffffff;
-const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 20;
+const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 36;
 const CATCHUP_BYTES = 16, SNAPSHOT_DOC_BYTES = 32;
 const NO_PROPS = 0xffffffff;
-const PROPS_MAX = 4;
+const PROPS_MAX = 8;
 
 let addon = null;
 /** The native addon; throws if it was not built (there is no JavaScript fallback engine). */

@@ -58,9 +58,9 @@ CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("typ
 
 from .streams import SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE  # noqa: E402  (include/fmt.h layouts)
 
-PROPS_MAX = 4
+PROPS_MAX = 8
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
-assert PROPSET_DTYPE.itemsize == 20
+assert PROPSET_DTYPE.itemsize == 36
 
 MAP_SLOT_DTYPE = np.dtype([("value", "<u4"), ("birth_seq", "<u4")])
 

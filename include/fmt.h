@@ -219,7 +219,7 @@ typedef struct fmt_mt_remove_order {
 } fmt_mt_remove_order;
 
 /* A document-local prop set: up to FMT_MT_PROPS_MAX (key_id, value_id) pairs in JS insertion order. */
-#define FMT_MT_PROPS_MAX 4
+#define FMT_MT_PROPS_MAX 8
 typedef struct fmt_mt_propset {
   uint32_t n;
   uint32_t kv[FMT_MT_PROPS_MAX]; /* (key_id << 16) | value_id */

@@ -52,7 +52,7 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   std::vector<uint16_t> text(textCap);
   std::memcpy(text.data(), b->text, b->text_len * 2);
   S.text = text.data(); S.textLen = b->text_len; S.textCap = textCap;
-  std::vector<uint32_t> pr(static_cast<size_t>(kPropCap) * 5);
+  std::vector<uint32_t> pr(static_cast<size_t>(kPropCap) * kPropWords);
   S.props = pr.data();
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));

@@ -126,3 +126,55 @@ def test_js_packer_and_catchup_match_python():
     kept = [(m, f, 1) for m, f in zip(msgs, [0, 1, 2, 3, 4, 5, 7, 8, 9])]
     cu = summary.catchup_messages([kept[0], kept[5]], ranges, 0)
     assert json.loads(summary.catchup_blob(cu)) == out["cu"]
+
+
+def _wide_messages(n_keys):
+    """Writers annotating and inserting with up to n_keys keys per set, keys in differing orders,
+    null deletes mixed in."""
+    keys = [f"k{i}" for i in range(n_keys)]
+    m = []
+    seq = 0
+
+    def add(client, ref, contents, msn=0):
+        nonlocal seq
+        seq += 1
+        m.append({"clientId": client, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+                  "minimumSequenceNumber": msn, "contents": contents})
+
+    add("B", 0, {"type": 0, "pos1": 0, "seg": "abcdefghijklmnopqrstuvwxyz"})
+    for r in range(12):
+        ks = keys[r % 3:] + keys[: r % 3]
+        props = {k: (None if (r % 4 == 3 and i == 0) else i + r) for i, k in enumerate(ks)}
+        add("BCD"[r % 3], max(0, seq - 2), {"type": 2, "pos1": r % 7, "pos2": 10 + r % 9, "props": props}, msn=max(0, seq - 3))
+        add("CDB"[r % 3], max(0, seq - 1), {"type": 0, "pos1": r, "seg": {"text": "+", "props": dict(reversed(list(props.items())))}},
+            msn=max(0, seq - 3))
+    return m
+
+
+@pytest.mark.parametrize("n_keys", [5, 8])
+def test_prop_sets_up_to_eight_keys_match_oracle(orc, n_keys):
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc("", observer="A")
+    for msg in _wide_messages(n_keys):
+        d.add_message(msg)
+    batch = b.finish()
+    assert max(int(batch.props_off[i + 1] - batch.props_off[i]) for i in range(len(batch.props_off) - 1)) == n_keys
+    for large in (False, True):
+        cl, cc, cp = emu_caps(large=large)
+        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+        assert rc == 0
+        hdr, leaves, chars, props = emu_replay(batch, large=large)
+        if not large and int(hdr[0]["status"]) == -3:
+            continue  # more prop sets than the small tier holds: the runtime escalates to the large tier
+        assert int(hdr[0]["status"]) == 0
+        assert compare_doc((oh[0], ol[0], oc[0], op[0]), (hdr[0], leaves[0], chars[0], props[0])) == []
+        assert max(int(p["n"]) for p in op[0][: int(oh[0]["n_props"])]) == n_keys
+
+
+def test_prop_set_beyond_eight_keys_is_a_capacity_error():
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc("", observer="A")
+    for msg in _wide_messages(9):
+        d.add_message(msg)
+    hdr, *_ = emu_replay(b.finish(), large=True)
+    assert int(hdr[0]["status"]) == -3  # FMT_E_CAPACITY (include/fmt.h FMT_MT_PROPS_MAX)

@@ -47,7 +47,7 @@ def test_addon_exports(addon):
     assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
                                "fetchRemoveOrder",
                                "replayMap", "fetchDoc", "sizes"])
-    assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 20, "mapSlot": 8,
+    assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
                         "catchupRange": 16}
     assert out["c"]["leaves"] >= 512
 
