@@ -59,6 +59,8 @@ constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
 FMT_DEV int32_t mClient(uint32_t m) { return static_cast<int32_t>(static_cast<int8_t>(m & 0xFFu)); }
 FMT_DEV uint32_t mProps(uint32_t m) { return (m >> 8) & 0xFFFFu; }
 FMT_DEV uint32_t mkMeta(int32_t client, uint32_t props) { return (static_cast<uint32_t>(client) & 0xFFu) | (props << 8); }
+constexpr uint32_t kMetaMarker = 1u << 24;  // the leaf is a Marker (mergeTreeNodes.ts:495-564)
+FMT_DEV bool mMarker(uint32_t m) { return (m & kMetaMarker) != 0; }
 constexpr uint32_t kNoProps = 0xFFFFu;
 
 // Window meta word: insert client (int8) | first remover (u8) << 8 | "more removers" << 16; the
@@ -1362,7 +1364,7 @@ class HugeDoc {
     x.mlo = x.mhi = 0;
     x.id = nextId++;
     x.text = op.payload;
-    x.meta = mkMeta(c, insProps);
+    x.meta = mkMeta(c, insProps) | ((op.flags & FMT_MT_F_MARKER) != 0 ? kMetaMarker : 0u);
     const uint32_t wx = winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, R.g, b);
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);
@@ -1538,7 +1540,7 @@ class HugeDoc {
   FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId) {
     const uint32_t np = applyProps(mProps(x.meta), opId);
     if (status != FMT_OK) return;
-    x.meta = (x.meta & 0xFFu) | (np << 8);
+    x.meta = (x.meta & ~(0xFFFFu << 8)) | (np << 8);
     putLeaf(b, j, x);
   }
 
@@ -1622,7 +1624,7 @@ class HugeDoc {
     FOR_LANES(l) {
       const bool valid = (l & 7) < LANE(cntL);
       const int32_t ins = static_cast<int32_t>(LANE(f[1])), rm = static_cast<int32_t>(LANE(f[2]));
-      LANE(ak) = (valid && rm == kNotRemoved && ins <= minSeq && LANE(f[0]) > 0) ? 1u : 0u;  // acked, kept, non-empty
+      LANE(ak) = (valid && rm == kNotRemoved && ins <= minSeq && LANE(f[0]) > 0 && !mMarker(LANE(f[7]))) ? 1u : 0u;  // acked, kept, non-empty text
       LANE(dropL) = valid && rm != kNotRemoved && rm <= minSeq;
       LANE(cls) = propClass(mProps(LANE(f[7])));
     }
@@ -1687,7 +1689,8 @@ class HugeDoc {
         const int32_t ins = static_cast<int32_t>(readlane(f[1], s)), rm = static_cast<int32_t>(readlane(f[2], s));
         if (rm == kNotRemoved && ins <= minSeq) {
           const uint32_t props = mProps(readlane(f[7], s)), lc = readlane(lastCh, s);
-          const bool canAppend = prev >= 0 && len > 0 && prevLast != 10u &&
+          const bool marker = mMarker(readlane(f[7], s));  // Marker: canAppend false both ways
+          const bool canAppend = prev >= 0 && len > 0 && !marker && prevLast != 10u &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) || len <= static_cast<uint32_t>(kGranularity)) &&
                                  propsMatch(prevProps, props);
           if (canAppend) {
@@ -1700,7 +1703,7 @@ class HugeDoc {
             setLane(P.dst, s, P.total);
             setLane(P.srcOf, P.total, s);
             setLane(P.outLen, P.total, len);
-            prev = len > 0 ? P.total : -1;
+            prev = len > 0 && !marker ? P.total : -1;
             prevLen = len;
             prevProps = props;
             prevLast = lc;
@@ -2102,14 +2105,14 @@ class HugeDoc {
           const uint32_t b = j / 7, k = j % 7;
           const size_t i = static_cast<size_t>(b) * 8 + k;
           const fmt_mt_snapshot_seg sg = in.segs[j];
-          S.lLen[i] = sg.len;
+          S.lLen[i] = sg.len & ~FMT_MT_SEG_MARKER;
           S.lIns[i] = 0;
           S.lRm[i] = kNotRemoved;
           S.lMlo[i] = 0;
           S.lMhi[i] = 0;
           S.lId[i] = j + 1;
           S.lText[i] = sg.text;
-          S.lMeta[i] = mkMeta(FMT_NON_COLLAB_CLIENT, kNoProps);
+          S.lMeta[i] = mkMeta(FMT_NON_COLLAB_CLIENT, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
           S.leafBlk[j + 1] = b;
           S.winIdx[j + 1] = kNone;
         }
@@ -2410,7 +2413,7 @@ class HugeDoc {
             x.ins_client = static_cast<int16_t>(mClient(m));
             x.props = static_cast<uint16_t>(mProps(m));
             x.block = static_cast<uint16_t>(blk & 0xFFFFu);
-            x.pad = static_cast<uint16_t>(blk >> 16);
+            x.pad = static_cast<uint16_t>((blk >> 16) | (mMarker(m) ? FMT_MT_LEAF_MARKER : 0u));
             outLeaves[o] = x;
             const uint32_t t = rd(S.lText + i);
             for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(loadWg(S.text + t + c));

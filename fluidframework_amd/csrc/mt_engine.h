@@ -69,7 +69,7 @@ struct LargeTier {
   static constexpr int kCapChars = 131071;  // a leaf length (17 bits) can hold all of them
   static constexpr int kMaxBlocks = 1023;   // ids 0..1022; 1023 = no block
   static constexpr int kHeapCap = 1023;     // at most one heap entry per block (needsScour)
-  static constexpr int kPropCap = 256;      // prop-set ids in their own word W6; 0xFFFF = undefined
+  static constexpr int kPropCap = 1024;     // prop-set ids in their own word W6; 0xFFFF = undefined
   static constexpr int kLenBits = 17, kBlkBits = 10;
   static constexpr bool kHbmChars = true;
   static constexpr bool kUnroll = false;    // rows indexed at run time (private memory)
@@ -137,9 +137,12 @@ struct Scratch {
 };
 
 // Leaf word fields (W0's packing is per tier, see Doc).
-FMT_DEV uint32_t fId(uint32_t w4) { return w4 & 0xFFFFFFu; }
+// W4 = leaf id (23 bits) | Marker flag << 23 | insert client << 24
+constexpr uint32_t kW4Marker = 1u << 23;
+FMT_DEV uint32_t fId(uint32_t w4) { return w4 & 0x7FFFFFu; }
+FMT_DEV bool fMarker(uint32_t w4) { return (w4 & kW4Marker) != 0; }
 FMT_DEV int32_t fClient(uint32_t w4) { return static_cast<int32_t>(static_cast<int8_t>(w4 >> 24)); }
-FMT_DEV uint32_t mkW4(uint32_t id, int32_t client) { return (id & 0xFFFFFFu) | (static_cast<uint32_t>(client & 0xFF) << 24); }
+FMT_DEV uint32_t mkW4(uint32_t id, int32_t client) { return (id & 0x7FFFFFu) | (static_cast<uint32_t>(client & 0xFF) << 24); }
 
 struct LeafRec {
   uint32_t w[7];  // W0..W4, and W5, W6 in the large tier
@@ -1093,7 +1096,7 @@ class Doc {
     rec.w[1] = static_cast<uint32_t>(seq);
     rec.w[2] = static_cast<uint32_t>(kNotRemoved);
     rec.w[3] = 0;
-    rec.w[4] = mkW4(nextId++, client);
+    rec.w[4] = mkW4(nextId++, client) | ((op.flags & FMT_MT_F_MARKER) != 0 ? kW4Marker : 0u);  // Marker.make
     rec.w[5] = 0;
     rec.w[6] = insProps;
     if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
@@ -1480,7 +1483,8 @@ class Doc {
         const bool nl = bl > 0 && chRead(static_cast<int>(rowBase + LANE(ex) + bl - 1)) == 10u;
         const uint32_t pr = propsL(l, r);
         const uint32_t p = fLen(w0) | ((kPW ? (pr == kPropsUndef ? 0x7Fu : pr) : pr) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
-                           (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u) | (nl ? 1u << 27 : 0u);
+                           (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u) | (nl ? 1u << 27 : 0u) |
+                           (fMarker(LANE(W[4])[r]) ? 1u << 28 : 0u);
         if (r == r0) LANE(pk0) = p;
         else LANE(pk1) = p;
       }
@@ -1503,7 +1507,8 @@ class Doc {
       if (((p >> 24) & 1u) == 0) {
         if ((p >> 26) & 1u) {
           const bool lastNl = ((p >> 27) & 1u) != 0;
-          const bool canAppend = prev >= 0 && !prevNl &&
+          const bool marker = ((p >> 28) & 1u) != 0;  // Marker: never appends, nothing appends onto it
+          const bool canAppend = prev >= 0 && !prevNl && !marker &&
                                  (prevLen <= static_cast<uint32_t>(kGranularity) ||
                                   len <= static_cast<uint32_t>(kGranularity)) &&
                                  propsMatch(prevProps, props) && len > 0;
@@ -1517,7 +1522,7 @@ class Doc {
             // the head keeps its index until the deletions below, so its length can be set now
             writeField(prev, 0, mkW0(prevLen, prevBlk, prevProps));
           } else {
-            prev = len > 0 ? j : -1;
+            prev = len > 0 && !marker ? j : -1;
             prevLen = len;
             prevProps = props;
             prevBlk = static_cast<uint32_t>(b);
@@ -1805,7 +1810,7 @@ class Doc {
     }
     uint32_t chars = 0;
     for (int k = 0; k < N; k++) {
-      const uint32_t len = uni(in.snapSegs[k].len);
+      const uint32_t len = uni(in.snapSegs[k].len) & ~FMT_MT_SEG_MARKER;
       if (len == 0) {
         fail(FMT_E_DATA);
         return;
@@ -1822,7 +1827,7 @@ class Doc {
     uint32_t* stage = reinterpret_cast<uint32_t*>(s->chars);
     if constexpr (!C::kHbmChars) {
       FOR_LANES(l) {
-        for (int j = l; j < N; j += 64) stage[j] = in.snapSegs[j].len;
+        for (int j = l; j < N; j += 64) stage[j] = in.snapSegs[j].len;  // (with FMT_MT_SEG_MARKER)
       }
       waveSync();
     }
@@ -1831,10 +1836,11 @@ class Doc {
       FOR_LANES(l) {
         const int j = r * 64 + l;
         const bool live = j < N;
-        const uint32_t len = live ? (C::kHbmChars ? in.snapSegs[j].len : stage[j]) : 0u;
+        const uint32_t lenF = live ? (C::kHbmChars ? in.snapSegs[j].len : stage[j]) : 0u;
+        const uint32_t len = lenF & ~FMT_MT_SEG_MARKER;
         LANE(W[0])[r] = live ? mkW0(len, static_cast<uint32_t>(j < H ? j / 7 : 0), kPropsUndef) : 0u;
         LANE(W[2])[r] = live ? static_cast<uint32_t>(kNotRemoved) : 0u;
-        LANE(W[4])[r] = live ? mkW4(static_cast<uint32_t>(j + 1), FMT_NON_COLLAB_CLIENT) : 0u;
+        LANE(W[4])[r] = live ? mkW4(static_cast<uint32_t>(j + 1), FMT_NON_COLLAB_CLIENT) | ((lenF & FMT_MT_SEG_MARKER) != 0 ? kW4Marker : 0u) : 0u;
         if constexpr (kPW) LANE(W[kWords - 1])[r] = live ? kPropsUndef : 0u;
       }
     }
@@ -1887,7 +1893,8 @@ class Doc {
       if (status != FMT_OK) return;
     }
     loadProps(0, N);
-    for (int k = 0; k < N && status == FMT_OK; k++) appendLoadedChars(uni(in.snapSegs[k].text), uni(in.snapSegs[k].len));
+    for (int k = 0; k < N && status == FMT_OK; k++)
+      appendLoadedChars(uni(in.snapSegs[k].text), uni(in.snapSegs[k].len) & ~FMT_MT_SEG_MARKER);
   }
 
   // Op records are prefetched two ahead (lanes 0..7 hold the eight dwords of one fmt_mt_op) and
@@ -2021,7 +2028,7 @@ class Doc {
           const uint32_t pid = propsL(l, r);
           L.props = pid == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(pid);
           L.block = static_cast<uint16_t>(LANE(ord)[r] + LANE(startFlag)[r] - 1u);
-          L.pad = 0;
+          L.pad = fMarker(LANE(W[4])[r]) ? FMT_MT_LEAF_MARKER : 0u;
           out.leaves[idx] = L;
         }
       }

@@ -378,11 +378,14 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
         return setErr(c, FMT_E_USAGE, "snapshot segments out of range");
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++) {
         const fmt_mt_snapshot_seg& sg = b->snapshot_segs[k];
-        if (static_cast<uint64_t>(sg.text) + sg.len > b->text_len)
+        const uint32_t len = sg.len & ~FMT_MT_SEG_MARKER;
+        if ((sg.len & FMT_MT_SEG_MARKER) != 0 && len != 1)
+          return setErr(c, FMT_E_DATA, "a marker segment has length 1");
+        if (static_cast<uint64_t>(sg.text) + len > b->text_len)
           return setErr(c, FMT_E_DATA, "snapshot segment text outside the text arena");
         if (sg.props != FMT_MT_NO_PROPS && sg.props >= b->n_props_ops)
           return setErr(c, FMT_E_DATA, "snapshot segment props op id out of range");
-        insertChars += sg.len;
+        insertChars += len;
       }
     }
   }
@@ -485,7 +488,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
       if (!sd.loaded) continue;
       uint64_t chars = 0;
-      for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++) chars += b->snapshot_segs[k].len;
+      for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
+        chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
       if (sd.n_body != 0)
         return setErr(c, FMT_E_UNSUPPORTED, "a document beyond the large tier must load from one header chunk (n_body = 0)");

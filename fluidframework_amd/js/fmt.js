@@ -22,6 +22,18 @@ const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
 const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
 const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
 const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate places (client.ts:680-700)
+const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER = 0x8000; // Marker segments
+
+/** The refType of a Marker spec {marker: {refType}, props?} (IJSONMarkerSegment), or null. */
+function markerRefType(spec) {
+	if (!(spec && typeof spec === "object" && "marker" in spec)) return null;
+	if (!Object.keys(spec).every((k) => k === "marker" || k === "props") || !spec.marker || typeof spec.marker !== "object") {
+		throw new UnsupportedOp("marker spec");
+	}
+	const r = spec.marker.refType;
+	if (!Number.isInteger(r) || r < 0 || r > 0xffff) throw new UnsupportedOp("marker refType");
+	return r;
+}
 const MAX_CLIENTS = 63;
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 36;
@@ -196,6 +208,13 @@ class MergeTreeStreamBuilder {
 	/** specToSegment for a text spec: "text" or {text, props} (IJSONTextSegment). */
 	specToSeg(spec) {
 		let text, props;
+		const rtype = markerRefType(spec);
+		if (rtype !== null) {
+			const [off] = this.text.push(String.fromCharCode(rtype));
+			const p = spec.props;
+			this.snapshotSegs.push([off, (1 | FMT_MT_SEG_MARKER) >>> 0, p && Object.keys(p).length ? this.propsOp(p) : NO_PROPS]);
+			return;
+		}
 		if (typeof spec === "string") {
 			text = spec;
 		} else if (spec && typeof spec === "object" && typeof spec.text === "string" &&
@@ -277,18 +296,25 @@ class MergeTreeStreamBuilder {
 			if (type === MT_INSERT) {
 				let seg = op.seg;
 				let props = null;
-				if (typeof seg !== "string") { // IJSONTextSegment {text, props} (textSegment.ts:44-52)
-					if (seg && typeof seg === "object" && "text" in seg && Object.keys(seg).every((k) => k === "text" || k === "props")) {
-						props = seg.props === undefined ? null : seg.props;
-						seg = seg.text;
-					} else {
-						throw new UnsupportedOp("insert of markers");
+				const rtype = markerRefType(seg);
+				if (rtype !== null) { // Marker.make(refType, props): len 1, its arena unit = refType
+					const p = seg.props === undefined ? null : seg.props;
+					pos1 = op.pos1; pos2 = p === null ? -1 : this.propsOp(p) + 1;
+					payload = this.text.push(String.fromCharCode(rtype))[0]; len = 1; flags |= FMT_MT_F_MARKER;
+				} else {
+					if (typeof seg !== "string") { // IJSONTextSegment {text, props} (textSegment.ts:44-52)
+						if (seg && typeof seg === "object" && "text" in seg && Object.keys(seg).every((k) => k === "text" || k === "props")) {
+							props = seg.props === undefined ? null : seg.props;
+							seg = seg.text;
+						} else {
+							throw new UnsupportedOp("segment spec");
+						}
 					}
+					const r = this.text.push(seg);
+					if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
+					// pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
+					pos1 = op.pos1; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1];
 				}
-				const r = this.text.push(seg);
-				if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
-				// pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
-				pos1 = op.pos1; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1];
 			} else if (type === MT_REMOVE || type === MT_OBLITERATE) {
 				pos1 = op.pos1; pos2 = op.pos2; // non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
 			} else if (type === MT_OBLITERATE_SIDED) {
@@ -556,7 +582,10 @@ class MergeTreeReplay {
 			const off = lv.getUint32(o + 16, true), len = lv.getUint32(o + 20, true);
 			const pid = lv.getUint16(o + 26, true);
 			const rm = lv.getInt32(o + 4, true);
+			const marker = (lv.getUint16(o + 30, true) & FMT_MT_LEAF_MARKER) !== 0;
 			segs.push({
+				marker, // a Marker segment: its one char unit is its refType
+				refType: marker ? chars[off] : undefined,
 				insertSeq: lv.getInt32(o, true),
 				removedSeq: rm === NOT_REMOVED ? undefined : rm,
 				insertClient: lv.getInt16(o + 24, true),
@@ -591,6 +620,7 @@ class MergeTreeReplay {
 			removedSeq: s.removedSeq === undefined ? NOT_REMOVED : s.removedSeq,
 			text: s.text,
 			kv: s.kv,
+			refType: s.refType,
 		}));
 		const out = summary.legacySummary(segs, h.minSeq, this.batch.keys, this.batch.values);
 		const msgs = this.batch.messages && this.batch.messages[doc];
@@ -636,12 +666,13 @@ class MergeTreeReplay {
 			removedSeq: s.removedSeq === undefined ? NOT_REMOVED : s.removedSeq,
 			text: s.text,
 			kv: s.kv,
+			refType: s.refType,
 		}));
 		return summary.v1Summary(v1, h.minSeq, h.curSeq, this.batch.keys, this.batch.values, this.batch.clients[doc], rem);
 	}
 	/** MergeTreeTextHelper.getText from the local perspective (MergeTreeTextHelper.ts:28-87). */
 	getText(doc) {
-		return this.segments(doc).filter((s) => s.removedSeq === undefined).map((s) => s.text).join("");
+		return this.segments(doc).filter((s) => s.removedSeq === undefined && !s.marker).map((s) => s.text).join("");
 	}
 	getLength(doc) {
 		return this.header(doc).visibleLength;

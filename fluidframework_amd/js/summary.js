@@ -78,16 +78,28 @@ function legacySegments(segs, minSeq) {
 	for (const s of segs) {
 		if (!(s.insertSeq <= minSeq) || s.removedSeq <= minSeq) continue;
 		const prev = out[out.length - 1];
-		if (prev && !prev.text.endsWith("\n") &&
+		// canAppend: both TextSegments (a Marker never appends, mergeTreeNodes.ts:557-559)
+		if (prev && prev.refType === undefined && s.refType === undefined && !prev.text.endsWith("\n") &&
 			(prev.text.length <= TEXT_GRANULARITY || s.text.length <= TEXT_GRANULARITY) &&
 			propsMatch(prev.kv, s.kv)) {
 			prev.text += s.text;
 			continue;
 		}
-		out.push({ text: s.text, kv: s.kv });
+		out.push({ text: s.text, kv: s.kv, refType: s.refType });
 	}
 	for (const s of out) if (s.kv && s.kv.length === 0) s.kv = null; // empty props → undefined
 	return out;
+}
+
+/** toJSONObject: a TextSegment's text or {text, props}; a Marker's {marker: {refType}, props?}. */
+function segJsonOf(s, keys, values) {
+	const hasProps = s.kv !== null && s.kv !== undefined && s.kv.length > 0;
+	if (s.refType !== undefined) {
+		const m = { marker: { refType: s.refType } };
+		if (hasProps) m.props = propsObject(s.kv, keys, values);
+		return m;
+	}
+	return hasProps ? { text: s.text, props: propsObject(s.kv, keys, values) } : s.text;
 }
 
 /** SnapshotLegacy emit: the header chunk (>= sizeOfFirstChunk chars) and the body chunk, if any. */
@@ -100,8 +112,7 @@ function legacySummary(segs, minSeq, keys, values, chunkSize) {
 			length += segments[start + n].text.length;
 			n++;
 		}
-		const texts = segments.slice(start, start + n).map((s) =>
-			s.kv === null ? s.text : { text: s.text, props: propsObject(s.kv, keys, values) });
+		const texts = segments.slice(start, start + n).map((s) => segJsonOf(s, keys, values));
 		const j = {
 			chunkStartSegmentIndex: start,
 			chunkSegmentCount: n,
@@ -138,27 +149,26 @@ function legacySummary(segs, minSeq, keys, values, chunkSize) {
 function v1Summary(segs, minSeq, curSeq, keys, values, clientNames, removers, chunkSize) {
 	const out = []; // [json value, cachedLength]
 	let prev = null;
-	const segJson = (text, kv) => (kv === null || kv.length === 0 ? text : { text, props: propsObject(kv, keys, values) });
 	const flush = () => {
-		if (prev !== null) out.push([segJson(prev.text, prev.kv), prev.text.length]);
+		if (prev !== null) out.push([segJsonOf(prev, keys, values), prev.text.length]);
 	};
 	segs.forEach((s, i) => {
 		const removed = s.removedSeq !== NOT_REMOVED;
 		if (removed && s.removedSeq <= minSeq) return;
 		if (s.insertSeq <= minSeq && !removed) {
-			if (prev === null) prev = { text: s.text, kv: s.kv };
-			else if (!prev.text.endsWith("\n") &&
+			if (prev === null) prev = { text: s.text, kv: s.kv, refType: s.refType };
+			else if (prev.refType === undefined && s.refType === undefined && !prev.text.endsWith("\n") &&
 				(prev.text.length <= TEXT_GRANULARITY || s.text.length <= TEXT_GRANULARITY) &&
 				propsMatch(prev.kv, s.kv)) prev = { text: prev.text + s.text, kv: prev.kv };
 			else {
 				flush();
-				prev = { text: s.text, kv: s.kv };
+				prev = { text: s.text, kv: s.kv, refType: s.refType };
 			}
 			return;
 		}
 		flush();
 		prev = null;
-		const raw = { json: segJson(s.text, s.kv) };
+		const raw = { json: segJsonOf(s, keys, values) };
 		if (s.insertSeq > minSeq) {
 			raw.seq = s.insertSeq;
 			raw.client = clientNames[s.insertClient];
@@ -205,6 +215,14 @@ function v1Summary(segs, minSeq, curSeq, keys, values, clientNames, removers, ch
  */
 function insertSegJson(seg) {
 	if (typeof seg === "string") return seg;
+	if (seg && typeof seg === "object" && "marker" in seg) { // Marker.clone().toJSONObject()
+		const m = { marker: { refType: seg.marker.refType } };
+		if (seg.props !== undefined && seg.props !== null) {
+			m.props = {};
+			for (const [k, v] of Object.entries(seg.props)) if (v !== undefined && v !== null) m.props[k] = v;
+		}
+		return m;
+	}
 	if (seg.props === undefined || seg.props === null) return seg.text;
 	const props = {};
 	for (const [k, v] of Object.entries(seg.props)) if (v !== undefined && v !== null) props[k] = v;

@@ -53,6 +53,22 @@ assert MAP_OP_DTYPE.itemsize == 16
 
 MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
 MT_F_START_BEFORE, MT_F_END_BEFORE = 8, 16  # fmt.h FMT_MT_F_START_BEFORE / FMT_MT_F_END_BEFORE
+MT_F_MARKER = 32  # fmt.h FMT_MT_F_MARKER: insert of a Marker segment
+MT_SEG_MARKER = 0x80000000  # fmt.h FMT_MT_SEG_MARKER (snapshot segment len flag)
+MT_LEAF_MARKER = 0x8000  # fmt.h FMT_MT_LEAF_MARKER (fmt_mt_leaf.pad flag)
+
+
+def marker_ref_type(spec) -> int | None:
+    """The refType of a Marker segment spec {\"marker\": {\"refType\"}, \"props\"?} (IJSONMarkerSegment,
+    mergeTreeNodes.ts:514-525), or None when `spec` is not a marker."""
+    if not (isinstance(spec, dict) and "marker" in spec):
+        return None
+    if not set(spec) <= {"marker", "props"} or not isinstance(spec["marker"], dict):
+        raise UnsupportedOp("marker spec")
+    ref = spec["marker"].get("refType")
+    if not isinstance(ref, int) or isinstance(ref, bool) or not 0 <= ref <= 0xFFFF:
+        raise UnsupportedOp("marker refType")
+    return ref
 MT_F_GROUP_CONT = 1
 MT_F_CATCHUP = 2  # include/fmt.h FMT_MT_F_CATCHUP
 MT_F_RMORDER = 4  # include/fmt.h FMT_MT_F_RMORDER
@@ -232,6 +248,13 @@ class MergeTreeStreamBuilder:
         self.text_len += len(u)
         return off, len(u)
 
+    def _unit(self, v: int) -> int:
+        """One UTF-16 unit in the arena (a Marker's refType); returns its offset."""
+        off = self.text_len
+        self.text.append(np.array([v], dtype="<u2"))
+        self.text_len += 1
+        return off
+
     def _props_op(self, props: dict) -> int:
         kv = []
         for k in js_key_order(list(props)):
@@ -258,12 +281,17 @@ class MergeTreeStreamBuilder:
         if t == MT_INSERT:
             seg = op["seg"]
             props = None
+            rtype = marker_ref_type(seg)
+            if rtype is not None:  # Marker.make(refType, props): len 1, its arena unit = refType
+                props = seg.get("props")
+                pos2 = -1 if props is None else self._props_op(props) + 1
+                return (seq, ref, msn, int(op["pos1"]), pos2, self._unit(rtype), 1, client, MT_INSERT, MT_F_MARKER)
             if not isinstance(seg, str):  # IJSONTextSegment {text, props} (textSegment.ts:44-52)
                 if isinstance(seg, dict) and "text" in seg and set(seg) <= {"text", "props"}:
                     props = seg.get("props")
                     seg = seg["text"]
                 else:
-                    raise UnsupportedOp("insert of markers")
+                    raise UnsupportedOp("segment spec")
             off, n = self._text(seg)
             if n > 0xFFFF:
                 raise UnsupportedOp("insert longer than 65535 UTF-16 units")
@@ -293,7 +321,11 @@ class MergeTreeStreamBuilder:
         return d
 
     def _spec(self, spec) -> tuple:
-        """specToSegment for a text segment spec: "text" or {"text", "props"} (IJSONTextSegment)."""
+        """specToSegment: "text", {"text", "props"} (IJSONTextSegment) or a Marker spec."""
+        rtype = marker_ref_type(spec)
+        if rtype is not None:
+            props = spec.get("props")
+            return (self._unit(rtype), 1 | MT_SEG_MARKER, self._props_op(props) if props else NO_PROPS)
         if isinstance(spec, str):
             text, props = spec, None
         elif isinstance(spec, dict) and "text" in spec and set(spec) <= {"text", "props"}:

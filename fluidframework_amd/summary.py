@@ -14,8 +14,8 @@ from __future__ import annotations
 
 import json
 
-from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_OBLITERATE, MT_REMOVE, is_array_index_key,
-                      js_json, js_key_order, js_quote)
+from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_LEAF_MARKER, MT_OBLITERATE, MT_REMOVE,
+                      is_array_index_key, js_json, js_key_order, js_quote, marker_ref_type)
 
 NOT_REMOVED = 0x7FFFFFFF
 TEXT_GRANULARITY = 256          # textSegment.ts:21
@@ -77,6 +77,20 @@ def _props_obj(kv, keys, values):
     return "{" + ",".join(_q(k) + ":" + d[k] for k in _js_order(names)) + "}"
 
 
+def _seg_json(text, props, marker, keys, values):
+    """toJSONObject of a summary segment (props already normalized: None when undefined or {}):
+    a TextSegment's text or {text, props} (textSegment.ts:62-66), a Marker's {marker: {refType},
+    props?} (mergeTreeNodes.ts:514-518; its one unit is the refType)."""
+    if marker:
+        j = '{"marker":{"refType":' + str(ord(text[0]) if isinstance(text, str) else int(text[0])) + "}"
+        if props:
+            j += ',"props":' + _props_obj(props, keys, values)
+        return j + "}"
+    if not props:
+        return _q(text)
+    return '{"text":' + _q(text) + ',"props":' + _props_obj(props, keys, values) + "}"
+
+
 def _props_match(a, b):
     """properties.ts:32-61 (undefined ≡ {}), on (key, value) id pairs."""
     a, b = a or (), b or ()
@@ -87,24 +101,26 @@ def _props_match(a, b):
 
 
 def legacy_segments(header, leaves, chars, propsets, min_seq):
-    """extractSync: leaves present at PriorPerspective(minSeq, NonCollabClient), merged greedily."""
-    segs = []  # [text, props kv tuple or None]
+    """extractSync: leaves present at PriorPerspective(minSeq, NonCollabClient), merged greedily
+    (prev.canAppend(seg): both TextSegments; a Marker never appends, mergeTreeNodes.ts:557-559)."""
+    segs = []  # [text, props kv tuple or None, marker]
     for L in leaves[: int(header["n_leaves"])]:
         ins, rm = int(L["ins_seq"]), int(L["rm_seq"])
         if not (ins <= min_seq) or rm <= min_seq:
             continue
         o, n = int(L["char_off"]), int(L["len"])
         text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
+        marker = (int(L["pad"]) & MT_LEAF_MARKER) != 0
         pid = int(L["props"])
         props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
         if segs:
             prev = segs[-1]
-            if (not prev[0].endswith("\n")
+            if (not prev[2] and not marker and not prev[0].endswith("\n")
                     and (_utf16_len(prev[0]) <= TEXT_GRANULARITY or n <= TEXT_GRANULARITY)
                     and _props_match(prev[1], props)):
                 prev[0] += text
                 continue
-        segs.append([text, props])
+        segs.append([text, props, marker])
     for s in segs:
         if s[1] is not None and len(s[1]) == 0:
             s[1] = None
@@ -115,16 +131,14 @@ def legacy_summary(header, leaves, chars, propsets, keys, values, chunk_size=SIZ
     """(header_blob, body_blob or None) of the legacy SharedString summary at the doc's minSeq."""
     min_seq = int(header["min_seq"])
     segs = legacy_segments(header, leaves, chars, propsets, min_seq)
-    total_len = sum(_utf16_len(t) for t, _ in segs)
+    total_len = sum(_utf16_len(t) for t, _, _ in segs)
 
     def chunk(start, approx, is_header):
         n, length = 0, 0
         while length < approx and start + n < len(segs):
             length += _utf16_len(segs[start + n][0])
             n += 1
-        texts = []
-        for t, p in segs[start : start + n]:
-            texts.append(_q(t) if p is None else '{"text":' + _q(t) + ',"props":' + _props_obj(p, keys, values) + "}")
+        texts = [_seg_json(t, p, m, keys, values) for t, p, m in segs[start : start + n]]
         j = (
             f'{{"chunkStartSegmentIndex":{start},"chunkSegmentCount":{n},"chunkLengthChars":{length},'
             f'"totalLengthChars":{total_len},"totalSegmentCount":{len(segs)},"chunkSequenceNumber":{min_seq},'
@@ -170,16 +184,14 @@ def v1_segments(header, leaves, chars, propsets, keys, values, client_names, rem
     written with its merge info."""
     min_seq = int(header["min_seq"])
     out = []
-    prev = None  # [text, props]
+    prev = None  # [text, props, marker]
 
-    def seg_json(text, props):
-        if props is None or len(props) == 0:
-            return _q(text)
-        return '{"text":' + _q(text) + ',"props":' + _props_obj(props, keys, values) + "}"
+    def seg_json(text, props, marker):
+        return _seg_json(text, props or None, marker, keys, values)
 
     def flush():
         if prev is not None:
-            out.append((seg_json(prev[0], prev[1]), _utf16_len(prev[0])))
+            out.append((seg_json(prev[0], prev[1], prev[2]), _utf16_len(prev[0])))
 
     for i in range(int(header["n_leaves"])):
         L = leaves[i]
@@ -189,22 +201,23 @@ def v1_segments(header, leaves, chars, propsets, keys, values, client_names, rem
             continue
         o, n = int(L["char_off"]), int(L["len"])
         text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
+        marker = (int(L["pad"]) & MT_LEAF_MARKER) != 0
         pid = int(L["props"])
         props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
         if ins <= min_seq and not removed:
             if prev is None:
-                prev = [text, props]
-            elif (not prev[0].endswith("\n")
+                prev = [text, props, marker]
+            elif (not prev[2] and not marker and not prev[0].endswith("\n")
                   and (_utf16_len(prev[0]) <= TEXT_GRANULARITY or n <= TEXT_GRANULARITY)
                   and _props_match(prev[1], props)):
                 prev[0] += text
             else:
                 flush()
-                prev = [text, props]
+                prev = [text, props, marker]
             continue
         flush()
         prev = None
-        raw = '{"json":' + seg_json(text, props)
+        raw = '{"json":' + seg_json(text, props, marker)
         if ins > min_seq:
             raw += f',"seq":{ins},"client":' + _q(client_names[int(L["ins_client"])])
         if removed:
@@ -248,10 +261,17 @@ def v1_summary(header, leaves, chars, propsets, keys, values, client_names, remo
 
 
 def _insert_seg_json(seg):
-    """TextSegment.toJSONObject of the inserted segment (textSegment.ts:62-66): the text, or
-    {text, props} when it has properties (clone(props) drops null values, properties.ts:68-95)."""
+    """toJSONObject of the inserted segment's clone: a TextSegment's text, or {text, props} when it
+    has properties (textSegment.ts:62-66; clone(props) drops null values, properties.ts:68-95); a
+    Marker's {marker: {refType}, props?} (mergeTreeNodes.ts:514-518)."""
     if isinstance(seg, str):
         return seg
+    if marker_ref_type(seg) is not None:
+        out = {"marker": {"refType": seg["marker"]["refType"]}}
+        props = seg.get("props")
+        if props is not None:
+            out["props"] = {k: props[k] for k in js_key_order(list(props)) if props[k] is not None}
+        return out
     props = seg.get("props")
     if props is None:
         return seg["text"]

@@ -95,6 +95,10 @@ extern "C" {
  * {pos2 - 1, After} (mergeTree.ts:2282-2286). */
 #define FMT_MT_F_START_BEFORE 8u
 #define FMT_MT_F_END_BEFORE 16u
+/* INSERT of a Marker segment (seg {"marker": {"refType"}, "props"?}, mergeTreeNodes.ts:495-564):
+ * cachedLength 1, never appended to or onto (canAppend false); len = 1 and the one arena unit at
+ * payload holds its refType (ReferenceType bit flags). */
+#define FMT_MT_F_MARKER 32u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */
@@ -138,6 +142,9 @@ typedef struct fmt_mt_snapshot_doc {
 } fmt_mt_snapshot_doc;
 
 #define FMT_MT_NO_PROPS 0xffffffffu
+/* fmt_mt_snapshot_seg.len flag: the spec is a Marker ({"marker": {"refType"}, "props"?}); its one
+ * arena unit holds the refType. */
+#define FMT_MT_SEG_MARKER 0x80000000u
 /* One segment spec of a summary chunk ("text" or {"text","props"}, IJSONTextSegment). 12 bytes. */
 typedef struct fmt_mt_snapshot_seg {
   uint32_t text;  /* offset of the text in the UTF-16 arena */
@@ -177,8 +184,10 @@ typedef struct fmt_mt_leaf {
   int16_t ins_client;  /* insert stamp client */
   uint16_t props;      /* document-local prop-set id, 0xffff = properties undefined */
   uint16_t block;      /* index of the leaf's parent block in document order of leaf blocks */
-  uint16_t pad;
+  uint16_t pad;        /* FMT_MT_LEAF_MARKER | block ordinal bits 16..30 (documents beyond 65535 leaf blocks) */
 } fmt_mt_leaf;
+/* fmt_mt_leaf.pad flag: the leaf is a Marker (its one char unit is its refType). */
+#define FMT_MT_LEAF_MARKER 0x8000u
 
 /* Per-document result header. */
 typedef struct fmt_mt_doc_result {

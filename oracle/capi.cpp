@@ -77,7 +77,7 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
       L.len = static_cast<uint32_t>(s->len());
       L.props = pid;
       L.block = static_cast<uint16_t>(blockOf[i]);
-      L.pad = static_cast<uint16_t>(static_cast<uint32_t>(blockOf[i]) >> 16);  // block ordinal, high half
+      L.pad = static_cast<uint16_t>((static_cast<uint32_t>(blockOf[i]) >> 16) | (s->marker ? FMT_MT_LEAF_MARKER : 0u));
     }
     for (int k = 0; k < s->len(); k++) {
       if (chars && charOff + k < capChars) chars[charOff + k] = static_cast<uint16_t>(s->text[k]);
@@ -205,7 +205,8 @@ void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d) {
     for (uint32_t k = 0; k < sd.n_header + sd.n_body; k++) {
       const fmt_mt_snapshot_seg& sg = b->snapshot_segs[sd.first_seg + k];
       MergeTree::LoadedSeg l;
-      l.text.assign(reinterpret_cast<const char16_t*>(b->text + sg.text), sg.len);
+      l.marker = (sg.len & FMT_MT_SEG_MARKER) != 0;
+      l.text.assign(reinterpret_cast<const char16_t*>(b->text + sg.text), sg.len & ~FMT_MT_SEG_MARKER);
       if (sg.props != FMT_MT_NO_PROPS) {
         l.hasProps = true;
         for (uint32_t t = b->props_off[sg.props]; t < b->props_off[sg.props + 1]; t++)

@@ -744,6 +744,7 @@ void MergeTree::loadSnapshot(const std::vector<LoadedSeg>& header, const std::ve
   auto make = [&](const LoadedSeg& l) {
     Seg* s = makeSeg();
     s->text = l.text;
+    s->marker = l.marker;
     s->ins = Stamp{0, kNonCollabClient};
     if (l.hasProps) {
       s->props.defined = true;
@@ -805,6 +806,7 @@ void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const ui
     case FMT_MT_INSERT: {
       Seg* s = makeSeg();
       s->text.assign(reinterpret_cast<const char16_t*>(arena + op.payload), op.len);
+      s->marker = (op.flags & FMT_MT_F_MARKER) != 0;  // Marker.make(refType, props)
       // seg {text, props}: TextSegment.make(text, props) → BaseSegment's `properties = clone(props)`
       // (textSegment.ts:41-52, mergeTreeNodes.ts:343-347; clone = extend({}, props): null values
       // dropped, properties.ts:68-95). pos2 = props-op id + 1 (0: a plain string segment).
@@ -852,7 +854,8 @@ void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const ui
 // Zamboni (zamboni.ts:33-213)
 // ------------------------------------------------------------------------------------------------
 static bool canAppendText(const Seg* prev, const Seg* seg) {
-  // textSegment.ts:76-83
+  // textSegment.ts:76-83 (TextSegment.is(segment)); Marker.canAppend is false (mergeTreeNodes.ts:557-559)
+  if (prev->marker || seg->marker) return false;
   if (!prev->text.empty() && prev->text.back() == u'\n') return false;
   return prev->len() <= kTextGranularity || seg->len() <= kTextGranularity;
 }
@@ -1143,7 +1146,9 @@ std::u16string MergeTree::getText() const {
   std::u16string out;
   const Perspective lp = localPerspective();
   const int len = getLocalLength();
-  nodeMap(lp, 0, len, [&](Seg* s) { out += s->text; });
+  nodeMap(lp, 0, len, [&](Seg* s) {
+    if (!s->marker) out += s->text;  // getText collects TextSegments only (MergeTreeTextHelper.ts:60-87)
+  });
   return out;
 }
 
@@ -1203,6 +1208,7 @@ Summary MergeTree::summarize(const std::vector<std::string>& keys,
   struct Out {
     std::u16string text;
     PropMap props;
+    bool marker;
   };
   std::vector<Out> segs;
   const Perspective mp{false, minSeq, kNonCollabClient};
@@ -1215,12 +1221,12 @@ Summary MergeTree::summarize(const std::vector<std::string>& keys,
       const bool endsNl = !prev.text.empty() && prev.text.back() == u'\n';
       const bool sizeOk = static_cast<int>(prev.text.size()) <= kTextGranularity ||
                           s->len() <= kTextGranularity;
-      if (!endsNl && sizeOk && matchProperties(prev.props, s->props)) {
+      if (!prev.marker && !s->marker && !endsNl && sizeOk && matchProperties(prev.props, s->props)) {
         prev.text += s->text;
         return;
       }
     }
-    segs.push_back({s->text, s->props});
+    segs.push_back({s->text, s->props, s->marker});
   });
   long long totalLen = 0;
   for (auto& o : segs) {
@@ -1252,7 +1258,16 @@ Summary MergeTree::summarize(const std::vector<std::string>& keys,
     for (size_t i = 0; i < n; i++) {
       if (i) j.push_back(',');
       const Out& o = segs[startIndex + i];
-      if (o.props.defined) {
+      if (o.marker) {  // Marker.toJSONObject: {marker: {refType}} + props when defined
+        j += "{\"marker\":{\"refType\":";
+        jsonInt(j, static_cast<long long>(o.text[0]));
+        j += "}";
+        if (o.props.defined) {
+          j += ",\"props\":";
+          emitProps(j, o.props, keys, values);
+        }
+        j.push_back('}');
+      } else if (o.props.defined) {
         j += "{\"text\":";
         jsonQuoteUtf16(j, o.text.data(), o.text.size());
         j += ",\"props\":";

@@ -84,7 +84,8 @@ struct Node {
 struct LRef;
 struct Seg : Node {
   Seg() : Node(true) {}
-  std::u16string text;
+  std::u16string text;  // a Marker's one unit is its refType
+  bool marker = false;  // Marker segment (mergeTreeNodes.ts:495-564): cachedLength 1, never appends
   Stamp ins{0, 0};
   std::vector<Stamp> removes;  // sorted by stamps.compare (spliceIntoList)
   PropMap props;
@@ -174,6 +175,7 @@ class MergeTree {
   // A legacy summary chunk's segment spec: text and, when the spec has "props", its properties.
   struct LoadedSeg {
     std::u16string text;
+    bool marker = false;  // {"marker": {"refType"}}: text = the refType unit
     bool hasProps = false;
     std::vector<std::pair<uint16_t, uint16_t>> props;
   };

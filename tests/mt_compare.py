@@ -160,7 +160,7 @@ def visible_text(hdr, leaves, chars):
     n = int(hdr["n_leaves"])
     out = []
     for L in leaves[:n]:
-        if int(L["rm_seq"]) == 0x7FFFFFFF:
+        if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000:  # (markers: no text)
             o = int(L["char_off"])
             out.append(chars[o : o + int(L["len"])].tobytes().decode("utf-16-le", "surrogatepass"))
     return "".join(out)

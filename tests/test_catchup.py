@@ -41,7 +41,7 @@ def fixture_batch():
 def _text(h, leaves, chars):
     out = []
     for L in leaves[: int(h["n_leaves"])]:
-        if int(L["rm_seq"]) == 0x7FFFFFFF:
+        if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000:  # (markers: no text)
             o, n = int(L["char_off"]), int(L["len"])
             out.append(chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass"))
     return "".join(out)
@@ -51,7 +51,7 @@ def reload_text(orc, h, leaves, chars, props, keys, values, msgs):
     """Text after loading the legacy summary at minSeq and applying its catch-up messages."""
     segs = summary.legacy_segments(h, leaves, chars, props, int(h["min_seq"]))
     b = MergeTreeStreamBuilder()
-    d = b.begin_doc("".join(t for t, _ in segs), observer="observer")
+    d = b.begin_doc("".join(t for t, _, m in segs if not m), observer="observer")
     for m in msgs:
         d.add_message(m)
     rb = b.finish()

@@ -27,7 +27,7 @@ def test_emulated_engine_matches_reference_text_checkpoints(fixtures_prefix):
 def test_emulated_engine_matches_oracle_on_fixtures(orc, fixtures_prefix):
     batch, _ = fixtures_prefix
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     hdr, leaves, chars, props = emu_replay(batch)
     for d in range(batch.n_docs):
@@ -39,7 +39,7 @@ def test_emulated_engine_matches_oracle_on_fixtures(orc, fixtures_prefix):
 def test_emulated_engine_matches_oracle_on_conflict_farm(orc, n_clients, min_length):
     batch = workloads.conflict_farm(40, n_clients=n_clients, ops_per_doc=1500, min_length=min_length, seed=7)
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     hdr, leaves, chars, props = emu_replay(batch)
     for d in range(batch.n_docs):
@@ -76,7 +76,7 @@ def _no_zamboni_batch(sizes, seed=11):
 def test_emulated_engine_fills_every_row_to_capacity(orc):
     cl, cc, cp = emu_caps()
     batch = _no_zamboni_batch([60, 130, 200, 260, 300, 400, 420, 500])
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
     assert rc == 0
     hdr, leaves, chars, props = emu_replay(batch)
     assert oh["n_leaves"].max() > cl  # the last documents overflow the 512-leaf engine
@@ -95,7 +95,7 @@ def test_large_tier_matches_oracle_on_fixtures(orc, fixtures_prefix):
     """The rolled, HBM-text large tier is the same engine: bit-exact vs the oracle where both fit."""
     batch, expected = fixtures_prefix
     cl, cc, cp = emu_caps(large=True)
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     hdr, leaves, chars, props = emu_replay(batch, large=True)
     for d in range(batch.n_docs):
@@ -109,7 +109,7 @@ def test_large_tier_fills_every_row_to_capacity(orc):
     cl, cc, cp = emu_caps(large=True)
     small_leaves = emu_caps()[0]
     batch = _no_zamboni_batch([400, 1000, 1500, 1650, 1800], seed=5)
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=8192, cap_chars=1 << 17, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
     assert rc == 0
     assert oh["n_leaves"].max() > cl and ((oh["n_leaves"] > small_leaves) & (oh["n_leaves"] <= cl)).sum() >= 2
     small = emu_replay(batch)[0]
@@ -128,7 +128,7 @@ def test_large_tier_matches_oracle_on_long_conflict_farm(orc):
     """Conflict-farm documents long enough to outgrow 2048 UTF-16 units / 512 leaves."""
     batch = workloads.conflict_farm(6, n_clients=8, ops_per_doc=4000, min_length=3000, seed=21)
     cl, cc, cp = emu_caps(large=True)
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=6, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=6, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     small_cl, small_cc, _ = emu_caps()
     assert ((oh["n_leaves"] > small_cl) | (oh["n_chars"] > small_cc)).any()
@@ -164,7 +164,7 @@ def test_emulated_engine_newline_segments_stop_appends(orc):
     batch = b.finish()
     for large in (False, True):
         cl, cc, cp = emu_caps(large)
-        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=cl, cap_chars=cc, cap_props=64)
+        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=cl, cap_chars=cc, cap_props=1024)
         assert rc == 0
         hdr, leaves, chars, props = emu_replay(batch, large=large)
         for d in range(batch.n_docs):
@@ -183,7 +183,7 @@ def test_many_writers_overflow_to_large_tier(orc, n_clients):
     small = emu_replay(batch)[0]
     assert (small["status"] == -3).any()
     cl, cc, cp = emu_caps(large=True)
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     hdr, leaves, chars, props = emu_replay(batch, large=True)
     assert (hdr["status"] == 0).all()

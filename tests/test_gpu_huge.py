@@ -136,3 +136,23 @@ def test_huge_inserts_with_props(orc, engine):
     assert rc == 0
     leaves, chars, props = engine.mt_doc(0, hdrs[0])
     assert compare_doc(exp, (hdrs[0], leaves, chars, props)) == []
+
+
+def test_huge_loaded_markers(orc, engine):
+    """Marker segments in a huge document's summary (every third 1-unit spec) on the GPU."""
+    import dataclasses
+
+    from fluidframework_amd.streams import MT_SEG_MARKER
+    batch = workloads.t3_stream(200_000, 20_000, n_clients=16, max_lag=512, max_range=8, seed=31)
+    segs = batch.snapshot_segs.copy()
+    idx = np.nonzero(segs["len"] == 1)[0][::3]
+    segs["len"][idx] = 1 | MT_SEG_MARKER
+    batch = dataclasses.replace(batch, snapshot_segs=segs)
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    leaves, chars, props = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], leaves, chars, props)) == []

@@ -145,6 +145,21 @@ def test_mt_inserts_with_props_match_oracle(orc, engine, n_clients):
     assert (hdrs["status"] == 0).all()
 
 
+def test_mt_marker_and_props_inserts_match_oracle(orc, engine):
+    """Marker inserts and {text, props} inserts (tests/test_insert_props.py's streams) on the GPU."""
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+    from test_insert_props import _marker_messages, _messages, _wide_messages
+
+    b = MergeTreeStreamBuilder()
+    for msgs in (_messages(), _marker_messages(), _wide_messages(8)):
+        d = b.begin_doc("", observer="A")
+        for m in msgs:
+            d.add_message(m)
+    batch = b.finish()
+    hdrs = _check_against_oracle(orc, engine, batch)
+    assert (hdrs["status"] == 0).all()
+
+
 def test_mt_summaries_match_oracle(orc, engine):
     batch = workloads.conflict_farm(48, n_clients=8, ops_per_doc=2000, seed=21)
     hdrs = _gpu_mt(engine, batch)
@@ -224,7 +239,7 @@ def test_mt_large_documents_escalate_to_large_tier(orc, engine):
     assert engine.stats().launches == 2
 
 
-@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"])
 def test_mt_reference_snapshots_load_on_gpu(orc, engine, name):
     """The reference's legacy snapshot fixtures (8.9k-89k chars, up to 1112 segments) load into the
     engine (large tier) and summarize again to the fixture's blobs byte for byte."""
@@ -349,7 +364,7 @@ def test_mt_sided_obliterate_catchup_ranges_on_gpu(orc, engine):
     assert obl > 0
 
 
-@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"])
 def test_mt_v1_fixture_round_trip_on_gpu(orc, engine, name):
     """The reference's SnapshotV1 fixtures load on the GPU (large tier) and summarize again as V1 to
     the fixture's blobs byte for byte."""

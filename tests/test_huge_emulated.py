@@ -71,3 +71,25 @@ def test_huge_engine_inserts_with_props(orc):
     got = emu_huge_replay(batch, tiny_groups=True)
     assert int(got[0]["status"]) == 0
     assert compare_doc(exp, got) == []
+
+
+def test_huge_engine_loaded_markers(orc):
+    """A huge document whose summary holds Marker segments (every third 1-unit spec becomes one, so
+    the generated ops' positions stay valid; its arena unit is the refType): markers never append in
+    zamboni and keep their flag through the replay."""
+    import dataclasses
+
+    import numpy as np
+
+    from fluidframework_amd.streams import MT_LEAF_MARKER, MT_SEG_MARKER
+    batch = workloads.t3_stream(4000, 8000, n_clients=16, max_lag=300, max_range=8, seed=5)
+    segs = batch.snapshot_segs.copy()
+    idx = np.nonzero(segs["len"] == 1)[0][::3]
+    segs["len"][idx] = 1 | MT_SEG_MARKER
+    batch = dataclasses.replace(batch, snapshot_segs=segs)
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=True)
+    assert int(got[0]["status"]) == 0
+    assert compare_doc(exp, got) == []
+    assert int((exp[1]["pad"] & MT_LEAF_MARKER != 0).sum()) > 50

@@ -178,3 +178,93 @@ def test_prop_set_beyond_eight_keys_is_a_capacity_error():
         d.add_message(msg)
     hdr, *_ = emu_replay(b.finish(), large=True)
     assert int(hdr[0]["status"]) == -3  # FMT_E_CAPACITY (include/fmt.h FMT_MT_PROPS_MAX)
+
+
+def _marker_messages():
+    """Marker inserts (Marker.make(refType, props), mergeTreeNodes.ts:495-564) between text inserts of
+    lagging writers; minSeq advances so zamboni runs: no text appends onto or across a marker."""
+    m = []
+    seq = 0
+
+    def add(client, ref, contents, msn):
+        nonlocal seq
+        seq += 1
+        m.append({"clientId": client, "sequenceNumber": seq, "referenceSequenceNumber": ref,
+                  "minimumSequenceNumber": msn, "contents": contents})
+
+    add("B", 0, {"type": 0, "pos1": 0, "seg": "abcdef"}, 0)
+    add("C", 1, {"type": 0, "pos1": 3, "seg": {"marker": {"refType": 1}, "props": {"markerId": "m1", "ItemType": "Paragraph"}}}, 0)
+    add("D", 1, {"type": 0, "pos1": 0, "seg": {"marker": {"refType": 0}}}, 1)
+    add("B", 3, {"type": 0, "pos1": 5, "seg": "XY"}, 2)
+    add("C", 3, {"type": 0, "pos1": 8, "seg": {"marker": {"refType": 0x40}, "props": {"k": None}}}, 2)
+    add("D", 5, {"type": 2, "pos1": 0, "pos2": 6, "props": {"bold": True}}, 3)
+    add("B", 6, {"type": 0, "pos1": 2, "seg": "zz"}, 5)
+    add("C", 7, {"type": 1, "pos1": 1, "pos2": 2}, 6)
+    add("D", 7, {"type": 0, "pos1": 4, "seg": "qq"}, 7)
+    for k in range(20):  # text runs that zamboni merges around the markers
+        add("BCD"[k % 3], seq, {"type": 0, "pos1": (k * 5) % (seq + 3), "seg": "t" + str(k)}, seq - 1)
+    return m
+
+
+def test_markers_match_oracle_and_keep_out_of_text(orc):
+    b = MergeTreeStreamBuilder(keep_messages=True)
+    d = b.begin_doc("", observer="A")
+    for msg in _marker_messages():
+        d.add_message(msg)
+    batch = b.finish(catchup=True)
+    assert int((batch.ops["flags"] & streams.MT_F_MARKER != 0).sum()) == 3
+    for large in (False, True):
+        cl, cc, cp = emu_caps(large=large)
+        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+        assert rc == 0
+        hdr, leaves, chars, props = emu_replay(batch, large=large)
+        assert int(hdr[0]["status"]) == 0
+        assert compare_doc((oh[0], ol[0], oc[0], op[0]), (hdr[0], leaves[0], chars[0], props[0])) == []
+    lv = ol[0][: int(oh[0]["n_leaves"])]
+    marks = [L for L in lv if int(L["pad"]) & streams.MT_LEAF_MARKER]
+    assert len(marks) == 3 and all(int(L["len"]) == 1 for L in marks)
+    assert sorted(int(oc[0][int(L["char_off"])]) for L in marks) == [0, 1, 0x40]
+    # the summaries write the markers as {"marker": {"refType"}, "props"?}
+    head, body = summary.legacy_summary(oh[0], ol[0], oc[0], op[0], batch.keys, batch.values)
+    segs = json.loads(head)["segmentTexts"] + (json.loads(body)["segmentTexts"] if body else [])
+    ms = [x for x in segs if isinstance(x, dict) and "marker" in x]
+    assert len(ms) == 3 and set(ms[0]) <= {"marker", "props"}
+    assert any(x["marker"] == {"refType": 1} and x["props"]["markerId"] == "m1" for x in ms)
+    text = "".join(s if isinstance(s, str) else s.get("text", "") for s in segs)
+    assert len(text) + 3 == json.loads(head)["totalLengthChars"]
+
+
+@pytest.mark.skipif(NODE is None, reason="node is not installed")
+def test_js_packer_markers_match_python():
+    msgs = _marker_messages()
+    js = (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          "const b=new fmt.MergeTreeStreamBuilder();const d=b.beginDoc('','A');"
+          f"for(const m of {json.dumps(msgs)}) d.addMessage(m);"
+          "const r=b.finish();"
+          "process.stdout.write(JSON.stringify({ops:Buffer.from(r.ops.buffer,r.ops.byteOffset,r.ops.byteLength).toString('hex'),"
+          "text:Array.from(r.text),off:Array.from(r.propsOff),kv:Array.from(r.propsKv)}))")
+    r = subprocess.run([NODE, "-e", js], capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc("", observer="A")
+    for msg in msgs:
+        d.add_message(msg)
+    py = b.finish()
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert out["text"] == [int(x) for x in py.text]
+    assert out["off"] == [int(x) for x in py.props_off] and out["kv"] == [int(x) for x in py.props_kv]
+
+
+def test_catchup_marker_insert_json(orc):
+    b = MergeTreeStreamBuilder(keep_messages=True)
+    d = b.begin_doc("", observer="A")
+    for msg in _marker_messages()[:6]:
+        d.add_message(msg)
+    batch = b.finish(catchup=True)
+    rc, oh, ol, oc, op, _, ocu = orc.mt_replay_batch(batch, cap_catchup=64)
+    assert rc == 0
+    n = int(oh[0]["n_catchup"])
+    msgs = summary.catchup_messages(batch.messages[0], ocu[0][:n], int(oh[0]["min_seq"]))
+    segs = [msg["contents"]["seg"] for msg in msgs if msg["contents"].get("type") == 0]
+    assert {"marker": {"refType": 0x40}, "props": {}} in segs  # {"k": null} → properties {} (clone drops nulls)

@@ -39,18 +39,32 @@ def _segs(leaves, chars, props):
         o, n = int(L["char_off"]), int(L["len"])
         pid = int(L["props"])
         kv = None if pid == 0xFFFF else [int(x) for x in props[pid]["kv"][: props[pid]["n"]]]
-        out.append({"insertSeq": int(L["ins_seq"]), "insertClient": int(L["ins_client"]), "removedSeq": int(L["rm_seq"]),
-                    "text": chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass"), "kv": kv})
+        seg = {"insertSeq": int(L["ins_seq"]), "insertClient": int(L["ins_client"]), "removedSeq": int(L["rm_seq"]),
+               "text": chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass"), "kv": kv}
+        if int(L["pad"]) & 0x8000:  # FMT_MT_LEAF_MARKER: its one unit is the refType
+            seg["refType"] = int(chars[o])
+        out.append(seg)
     return out
 
 
-@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"])
 def test_js_legacy_summary_matches_reference_snapshot(orc, name, tmp_path):
     from golden_data import snapshot_trees
 
     expected = _blobs(snapshot_trees()[name])
-    doc, keys, values = _detached_string(orc, name)
-    h, leaves, chars, props = doc.dump()
+    if name == "withMarkers":  # (no generator restatement: the state is the fixture loaded into the oracle)
+        from fluidframework_amd.streams import MergeTreeStreamBuilder
+
+        b = MergeTreeStreamBuilder()
+        b.begin_doc_from_summary(expected["header"], expected.get("body"))
+        batch = b.finish()
+        rc, hh, ll, cc, pp, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=1024)
+        assert rc == 0
+        h, leaves, chars, props = hh[0], ll[0][: int(hh[0]["n_leaves"])], cc[0], pp[0]
+        keys, values = batch.keys, batch.values
+    else:
+        doc, keys, values = _detached_string(orc, name)
+        h, leaves, chars, props = doc.dump()
     [got] = _run([{"kind": "string", "segs": _segs(leaves, chars, props), "minSeq": int(h["min_seq"]),
                    "keys": keys, "values": values}], tmp_path)
     assert got["header"] == expected["header"]
@@ -114,14 +128,14 @@ def test_js_v1_summaries_match_reference_and_python_host(orc, tmp_path):
     cases, want = [], []
     for name in NAMES:
         batch, head, bodies = _load_v1(name)
-        rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+        rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=1024)
         n = int(h[0]["n_leaves"])
         cases.append({"kind": "v1", "segs": _segs(leaves[0][:n], chars[0], props[0]), "minSeq": int(h[0]["min_seq"]),
                       "curSeq": int(h[0]["cur_seq"]), "keys": batch.keys, "values": batch.values,
                       "clients": batch.clients[0], "removers": {}})
         want.append((head, bodies))
     batch = _collab_batch()
-    rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
     for d in range(batch.n_docs):
         n = int(h[d]["n_leaves"])
         rem = orc.mt_removers(batch, d)

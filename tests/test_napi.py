@@ -208,7 +208,7 @@ def test_js_v1_summaries_on_gpu(addon, orc):
     assert r.returncode == 0, r.stderr
     got = json.loads(r.stdout.strip().splitlines()[-1])
     batch = _collab_batch()
-    rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    rc, h, leaves, chars, props, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
     assert rc == 0 and len(got) == batch.n_docs
     for d in range(batch.n_docs):
         head, bodies = summary.v1_summary(h[d], leaves[d], chars[d], props[d], batch.keys, batch.values,

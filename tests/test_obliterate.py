@@ -52,7 +52,7 @@ def test_emulated_engine_obliterate_matches_oracle(orc, ob_prefix):
 
     batch, _ = ob_prefix
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     hdr, leaves, chars, props = emu_replay(batch)
     for d in range(batch.n_docs):

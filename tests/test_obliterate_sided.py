@@ -71,7 +71,7 @@ def _oracle_vs_emu(orc, batch):
     from mt_compare import compare_doc, emu_caps, emu_replay
 
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     hdr, leaves, chars, props = emu_replay(batch)
     over = hdr["status"] == FMT_E_CAPACITY  # the runtime replays these again in the large tier
     for d in np.flatnonzero(~over):
@@ -82,7 +82,7 @@ def _oracle_vs_emu(orc, batch):
         assert not diffs, f"doc {d}: {diffs[:5]}"
     if over.any():
         cl, cc, cp = emu_caps(True)
-        rc, oh2, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=64)
+        rc, oh2, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
         hdr, leaves, chars, props = emu_replay(batch, large=True)
         for d in np.flatnonzero(over):
             assert int(hdr[d]["status"]) == int(oh2[d]["status"]) == 0, d

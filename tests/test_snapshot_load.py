@@ -23,19 +23,19 @@ from test_oracle_golden import _blobs
 CHUNK = 40  # small first chunk so that short documents get a body chunk too
 
 
-@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"])
 def test_oracle_load_resummarize_reference_snapshot(orc, name):
     blobs = _blobs(snapshot_trees()[name])
     b = MergeTreeStreamBuilder()
     b.begin_doc_from_summary(blobs["header"], blobs.get("body"))
     batch = b.finish()
-    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=1024)
     assert rc == 0
     head, body = summary.legacy_summary(h[0], l[0], c[0], p[0], batch.keys, batch.values)
     assert head == blobs["header"] and body == blobs.get("body")
 
 
-@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"])
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"])
 def test_large_tier_loads_reference_snapshot(orc, name):
     """The reference snapshots (8.9k-89k chars, up to 1112 segments) overflow the small tier and load
     in the large tier (emulated here; on the GPU the runtime escalates them by itself): engine ==
@@ -46,7 +46,7 @@ def test_large_tier_loads_reference_snapshot(orc, name):
     batch = b.finish()
     assert emu_replay(batch)[0][0]["status"] == native.FMT_E_CAPACITY
     cl, cc, cp = emu_caps(large=True)
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     eh, el, ec, ep = emu_replay(batch, large=True)
     assert eh[0]["status"] == 0
@@ -104,7 +104,7 @@ def test_emulated_engine_matches_oracle_after_load(orc):
     batch, _ = fixture_batch()
     rb = reload_batch(summaries_of(orc, batch))
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(rb, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(rb, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     eh, el, ec, ep = emu_replay(rb)
     for d in range(rb.n_docs):
@@ -118,7 +118,7 @@ def test_emulated_engine_load_conflict_farm_summaries(orc, seed):
     sums = summaries_of(orc, cf, chunk=60, catchup=False)
     rb = reload_batch(sums, keep_messages=False)
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(rb, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(rb, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     eh, el, ec, ep = emu_replay(rb)
     for d in range(rb.n_docs):

@@ -19,7 +19,7 @@ from golden_data import snapshot_trees
 from mt_compare import compare_doc, emu_caps, emu_replay
 from test_catchup import fixture_batch
 
-NAMES = ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"]
+NAMES = ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"]
 
 
 def _v1_blobs(tree):
@@ -40,7 +40,7 @@ def _load_v1(name):
 @pytest.mark.parametrize("name", NAMES)
 def test_oracle_v1_fixture_round_trip(orc, name):
     batch, head, bodies = _load_v1(name)
-    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=1024)
     assert rc == 0
     got = summary.v1_summary(h[0], l[0], c[0], p[0], batch.keys, batch.values, batch.clients[0], {})
     assert got == (head, bodies)
@@ -55,7 +55,7 @@ def test_legacy_fixture_resummarizes_as_v1_fixture(orc, name):
     b = MergeTreeStreamBuilder()
     b.begin_doc_from_summary(blobs["header"], blobs.get("body"))
     batch = b.finish()
-    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=64)
+    rc, h, l, c, p, _ = orc.mt_replay_batch(batch, cap_leaves=1 << 16, cap_chars=1 << 20, cap_props=1024)
     assert rc == 0
     _, head, bodies = _load_v1(name)
     assert summary.v1_summary(h[0], l[0], c[0], p[0], batch.keys, batch.values, batch.clients[0], {}) == (head, bodies)
@@ -95,7 +95,7 @@ def test_engine_remove_order_matches_oracle_stamps():
 
     batch = _collab_batch()
     cl, cc, cp = emu_caps()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=1024)
     assert rc == 0
     eh, el, ec, ep, erm = emu_replay(batch, cap_rm=8192)
     multi = 0
@@ -124,7 +124,7 @@ def test_v1_merge_info_shape():
     import oracle as orc
 
     batch = _collab_batch()
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
     seen_removed = seen_ins = 0
     for d in range(batch.n_docs):
         head, bodies = summary.v1_summary(oh[d], ol[d], oc[d], op[d], batch.keys, batch.values, batch.clients[d],

@@ -8,7 +8,7 @@ Sources (data files held by the reference's own tests):
   packages/dds/merge-tree/src/test/results/*-default-conflict-farm-0.40.json
   packages/dds/merge-tree/src/test/results/*-conflict-farm-with-obliterate-2.3.0.json
       replayed by client.replay.spec.ts:20-76 (64 groups of {initialText, resultText, msgs, seq})
-  packages/dds/sequence/src/test/snapshots/legacy/{headerOnly,headerAndBody,largeBody,withAnnotations}.json
+  packages/dds/sequence/src/test/snapshots/legacy/{headerOnly,headerAndBody,largeBody,withAnnotations,withMarkers}.json
       checked by snapshotVersion.spec.ts:146-170 ("Snapshot diff")
 
 Outputs:
@@ -109,25 +109,38 @@ def main() -> None:
     write_messages()
     assert MT_OP_DTYPE.itemsize == 32
 
+    n = write_snapshots()
+    print(f"wrote {len(files)} replay fixtures and {n} snapshot trees to {OUT}")
+
+
+SNAPSHOT_NAMES = ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"]
+
+
+def write_snapshots():
+    """The legacy and V1 summary trees (data files of the reference's tests, copied as JSON)."""
     snaps = {}
-    for name in ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"]:
-        tree = json.load(open(os.path.join(SNAPSHOTS, name + ".json")))
-        snaps[name] = tree
+    for name in SNAPSHOT_NAMES:
+        snaps[name] = json.load(open(os.path.join(SNAPSHOTS, name + ".json")))
     with open(os.path.join(OUT, "snapshots_legacy.json"), "w") as fh:
         json.dump(snaps, fh, separators=(",", ":"))
     write_v1_snapshots()
-    print(f"wrote {len(files)} replay fixtures and {len(snaps)} snapshot trees to {OUT}")
+    return len(snaps)
 
 
 def write_v1_snapshots():
     """sequence/src/test/snapshots/v1/*.json: SnapshotV1 summaries of the same detached strings
     (generateSharedStrings.ts with newMergeTreeSnapshotFormat), checked by snapshotVersion.spec.ts."""
     snaps = {}
-    for name in ["headerOnly", "headerAndBody", "largeBody", "withAnnotations"]:
+    for name in SNAPSHOT_NAMES:
         snaps[name] = json.load(open(os.path.join(SNAPSHOTS_V1, name + ".json")))
     with open(os.path.join(OUT, "snapshots_v1.json"), "w") as fh:
         json.dump(snaps, fh, separators=(",", ":"))
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+
+    if sys.argv[1:] == ["--snapshots-only"]:
+        print(f"wrote {write_snapshots()} snapshot trees to {OUT}")
+    else:
+        main()
