@@ -144,7 +144,6 @@ struct HugeLds {
   int32_t gStable[kGroupCap];    // by group id: Σ stable lengths of its slots
   uint32_t gCount[kGroupCap];    // by group id: slots
   int32_t gCorr[kGroupCap];      // by group id: window correction of the current perspective
-  int32_t gStart[kGroupCap];     // by position: view start of group gOrder[k]
   int32_t sLen[kSlotCap];        // the group being searched: view length per slot
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
@@ -214,7 +213,7 @@ class HugeDoc {
     return 0;
 #endif
   }
-  bool corrValid = false;    // gCorr / gStart hold the current op's perspective
+  bool corrValid = false;    // gCorr holds the current op's perspective
   uint32_t epoch = 0;        // bumped by every change of the index (window table, slots, stable sums)
   uint32_t slotCacheG = kNone, slotCacheEpoch = 0;  // sLen / sBlk hold group slotCacheG at that epoch
   FMT_DEV void invalidate() {
@@ -732,8 +731,7 @@ class HugeDoc {
     }
     waveSync();
   }
-  // gCorr[g] = Σ view length of the window leaves of group g (their stable contribution is 0), and
-  // gStart[k] = view start of the k-th group, for PriorPerspective(r, c).
+  // gCorr[g] = Σ view length of the window leaves of group g (their stable contribution is 0)
   FMT_DEV void groupCorrections(int r, int c) {
     ProfScope ps_(prof[1]);
     FOR_LANES(l) {
@@ -744,34 +742,32 @@ class HugeDoc {
     prof[18] += nWin;
     prof[19] += static_cast<uint64_t>(nGroups);
     runPass(kCmdGroups, r, c, kNone);
-    ProfScope psScan_(prof[21]);
-    int32_t base = 0;
-    for (int k0 = 0; k0 < nGroups; k0 += 64) {
-      Lane<uint32_t> len;
-      FOR_LANES(l) {
-        const int k = k0 + l;
-        uint32_t x = 0;
-        if (k < nGroups) {
-          const uint32_t g = L->gOrder[k];
-          x = static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
-        }
-        LANE(len) = x;
-      }
-      uint32_t tot;
-      const Lane<uint32_t> ex = waveExclusiveSum(len, &tot);
-      FOR_LANES(l) {
-        if (k0 + l < nGroups) L->gStart[k0 + l] = base + static_cast<int32_t>(LANE(ex));
-      }
-      base += static_cast<int32_t>(tot);
-    }
-    waveSync();
     corrValid = true;
   }
 
+  // View length of the groups at positions [k0, k0 + 64) (lane l: position k0 + l; 0 past the end).
+  FMT_DEV Lane<uint32_t> groupLens(int k0) const {
+    Lane<uint32_t> len;
+    FOR_LANES(l) {
+      const int k = k0 + l;
+      uint32_t x = 0;
+      if (k < nGroups) {
+        const uint32_t g = L->gOrder[k];
+        x = static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
+      }
+      LANE(len) = x;
+    }
+    return len;
+  }
+
   FMT_DEV int totalView() const {
-    if (nGroups == 0) return 0;
-    const uint32_t g = L->gOrder[nGroups - 1];
-    return uni(L->gStart[nGroups - 1] + L->gStable[g] + L->gCorr[g]);
+    uint32_t total = 0;
+    for (int k0 = 0; k0 < nGroups; k0 += 64) {
+      uint32_t tot;
+      waveExclusiveSum(groupLens(k0), &tot);
+      total += tot;
+    }
+    return static_cast<int>(total);
   }
 
   // Slot view lengths of group g into L->sLen / L->sBlk (stable + that group's window corrections).
@@ -791,28 +787,31 @@ class HugeDoc {
     Hit h;
     h.found = false;
     if (!corrValid) groupCorrections(r, c);
-    // first group whose end reaches p
-    int k = -1;
-    for (int k0 = 0; k0 < nGroups && k < 0; k0 += 64) {
-      Lane<bool> q;
-      FOR_LANES(l) {
-        const int kk = k0 + l;
-        bool ok = false;
-        if (kk < nGroups) {
-          const uint32_t g = L->gOrder[kk];
-          ok = L->gStart[kk] + L->gStable[g] + L->gCorr[g] >= p;
+    // first group whose end reaches p: running view start over 64-group chunks (one wave scan each,
+    // stopping at the chunk that holds it)
+    int k = -1, base = 0;
+    {
+      ProfScope psScan_(prof[21]);
+      for (int k0 = 0; k0 < nGroups && k < 0; k0 += 64) {
+        const Lane<uint32_t> len = groupLens(k0);
+        uint32_t tot;
+        const Lane<uint32_t> ex = waveExclusiveSum(len, &tot);
+        Lane<bool> q;
+        FOR_LANES(l) { LANE(q) = k0 + l < nGroups && base + static_cast<int>(LANE(ex) + LANE(len)) >= p; }
+        const uint64_t m = ballot(q);
+        if (m) {
+          k = k0 + ctz64(m);
+          base += static_cast<int>(readlane(ex, ctz64(m)));
+        } else {
+          base += static_cast<int>(tot);
         }
-        LANE(q) = ok;
       }
-      const uint64_t m = ballot(q);
-      if (m) k = k0 + ctz64(m);
     }
     if (k < 0) return h;
-    for (; k < nGroups; k++) {
+    for (; k < nGroups; k++) {  // (base: the view start of group position k)
       const uint32_t g = L->gOrder[k];
       if (slotCacheG != g || slotCacheEpoch != epoch) slotLengths(g, r, c);
       const int cnt = static_cast<int>(L->gCount[g]);
-      int base = uni(L->gStart[k]);
       for (int s0 = 0; s0 < cnt; s0 += 64) {
         Lane<uint32_t> len;
         FOR_LANES(l) { LANE(len) = s0 + l < cnt ? static_cast<uint32_t>(L->sLen[s0 + l]) : 0u; }
