@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--unique-docs", type=int, default=0, help="0 = all documents distinct")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--key-pool", type=int, default=20, help="map: key ids per document (> 2560 takes the HBM-table path)")
+    ap.add_argument("--sparse", action="store_true",
+                    help="map: the sparse path (LDS hash reduce-by-key, one entry per live key; any key pool)")
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -137,13 +139,15 @@ def main():
     t = time.time()
     if mt:
         eng.mt_load(batch)
+    elif args.sparse:
+        eng.map_load_sparse(batch)
     else:
         eng.map_load(batch)
     h2d_s = time.time() - t
     in_bytes = batch.ops.nbytes + (batch.text.nbytes if mt else 0)
     log(rank, f"[bench] host->HBM {in_bytes / 1e9:.2f} GB in {h2d_s:.2f}s ({eng.device_info()})")
 
-    run = eng.mt_run if mt else eng.map_run
+    run = eng.mt_run if mt else (eng.map_run_sparse if args.sparse else eng.map_run)
     for _ in range(args.warmup):
         run()
         eng.sync()
@@ -153,6 +157,8 @@ def main():
         bad = int((hdrs["status"] != 0).sum())
         if bad:
             raise SystemExit(f"{bad} documents failed: statuses {np.unique(hdrs['status'])}")
+    elif args.sparse:
+        eng.map_fetch_sparse()
     else:
         eng.map_fetch()
     st = eng.stats()
@@ -183,6 +189,8 @@ def main():
         hdrs = eng.mt_headers()
         rec["status_bad"] = int((hdrs["status"] != 0).sum())
         rec["checksum"] = shard.state_checksum(hdrs, doc_base)
+    elif args.sparse:
+        rec["checksum"] = shard.map_sparse_checksum(*eng.map_fetch_sparse(), doc_base)
     else:
         rec["checksum"] = shard.map_checksum(eng.map_fetch(), doc_base)
     stats = shard.gather_stats(rec, dist, device="cuda") if dist is not None else rec
@@ -212,7 +220,8 @@ def main():
     achieved = bytes_per_launch / (avg_kernel_ms / 1e3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not t2:
+    # (the sparse map line has none: the oracle's dense per-(doc, key) output would dominate its time)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not t2 and not args.sparse:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline only ("port" of the reference path)
 
@@ -274,7 +283,8 @@ def main():
                        else f"{uniq} distinct docs per GPU replicated to {docs})"),
             "config": {
                 "workload": (f"T2 merge-tree conflict-farm replay, {total_docs} docs doc-sharded over {world} GPU(s)" if t2
-                             else "T1 merge-tree conflict-farm replay" if mt else "M2 SharedMap LWW replay"),
+                             else "T1 merge-tree conflict-farm replay" if mt
+                             else "M2 SharedMap LWW replay" + (", sparse output" if args.sparse else "")),
                 "docs_per_gpu": docs,
                 "docs_total": total_docs,
                 "clients": args.clients,
@@ -293,8 +303,8 @@ def main():
                 "traffic": traffic["bytes"] if traffic else None,
                 "traffic_fetch_write": [traffic["fetch_bytes"], traffic["write_bytes"]] if traffic else None,
                 "traffic_source": traffic["source"][0].rsplit("/", 2)[0] if traffic else None,
-                "kernel": "mergeTreeKernel" if mt else ("mapLwwKernel" if args.key_pool <= 2560
-                                                         else "mapLwwHbmKernel+mapLwwFinishKernel"),
+                "kernel": "mergeTreeKernel" if mt else ("mapSparseKernel" if args.sparse else "mapLwwKernel"
+                                                         if args.key_pool <= 2560 else "mapLwwHbmKernel+mapLwwFinishKernel"),
                 "limiter": ("per-document dependent op chain: VALU issue + LDS/readlane latency of one wave per "
                             "document (HBM fraction is reported for the contract; see DESIGN.md)") if mt
                            else "HBM streaming of 16-byte op records",

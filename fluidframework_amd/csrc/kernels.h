@@ -12,6 +12,11 @@ size_t mapLwwLdsBytes(uint32_t keyBound);
 // key pools beyond the LDS table take the HBM-table path, which needs 2 * key_bound u32 of scratch
 // per document (nullptr otherwise)
 bool mapLwwNeedsScratch(uint32_t keyBound);
+size_t mapSparseLdsBytes();
+hipError_t launchMapSparse(const fmt_map_op* ops, const uint64_t* offsets, uint32_t nDocs, uint32_t keyBound,
+                           fmt_map_entry* out, uint32_t* counts, int* error, int numCUs, hipStream_t stream);
+hipError_t launchMapSparsePack(const fmt_map_entry* in, const uint64_t* offsets, const uint32_t* counts,
+                               const uint64_t* packedOff, uint32_t nDocs, fmt_map_entry* packed, hipStream_t stream);
 hipError_t launchMapLww(const fmt_map_op* ops, const uint64_t* offsets, uint32_t nDocs, uint32_t keyBound,
                         fmt_map_slot* out, int* error, int numCUs, hipStream_t stream, uint32_t* scratch);
 

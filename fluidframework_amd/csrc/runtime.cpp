@@ -62,6 +62,11 @@ struct fmt_ctx {
   uint64_t mapNOps = 0;
   uint32_t mapDocs = 0, mapKeyBound = 0;
   bool mapLoaded = false;
+  // SharedMap, sparse path: entries at each document's op offset, live counts, packed copy
+  DevBuf<fmt_map_entry> mapEntries, mapPacked;
+  DevBuf<uint32_t> mapCounts;
+  DevBuf<uint64_t> mapPackedOff;
+  bool mapSparse = false;
 
   // merge-tree
   DevBuf<fmt_mt_op> mtOps;
@@ -168,6 +173,10 @@ void fmt_close(fmt_ctx* c) {
   c->mapOffs.release();
   c->mapOut.release();
   c->mapScratch.release();
+  c->mapEntries.release();
+  c->mapPacked.release();
+  c->mapCounts.release();
+  c->mapPackedOff.release();
   c->errWord.release();
   c->mtOps.release();
   c->mtOffs.release();
@@ -239,8 +248,8 @@ int fmt_device_info(fmt_ctx* c, char* buf, size_t cap) {
 }
 
 // ------------------------------------------------------------------------------ SharedMap
-int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_t* offs, uint32_t nDocs,
-                 uint32_t keyBound) {
+static int mapValidate(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_t* offs, uint32_t nDocs,
+                       uint32_t keyBound) {
   if (c == nullptr || (nOps > 0 && ops == nullptr) || offs == nullptr || keyBound == 0)
     return setErr(c, FMT_E_USAGE, "fmt_map_load: bad arguments");
   if (offs[0] != 0 || offs[nDocs] != nOps) return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
@@ -255,10 +264,20 @@ int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_
       }
     }
   }
+  return FMT_OK;
+}
+
+static int mapStage(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_t* offs, uint32_t nDocs,
+                    uint32_t keyBound, bool sparse) {
   FMT_HIP(c, hipSetDevice(c->device));
   FMT_HIP(c, c->mapOps.reserve(nOps));
   FMT_HIP(c, c->mapOffs.reserve(nDocs + 1ull));
-  FMT_HIP(c, c->mapOut.reserve(static_cast<size_t>(nDocs) * keyBound));
+  if (sparse) {
+    FMT_HIP(c, c->mapEntries.reserve(nOps));
+    FMT_HIP(c, c->mapCounts.reserve(nDocs));
+  } else {
+    FMT_HIP(c, c->mapOut.reserve(static_cast<size_t>(nDocs) * keyBound));
+  }
   if (nOps) FMT_HIP(c, hipMemcpyAsync(c->mapOps.p, ops, nOps * sizeof(fmt_map_op), hipMemcpyHostToDevice, c->stream));
   FMT_HIP(c, hipMemcpyAsync(c->mapOffs.p, offs, (nDocs + 1ull) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   FMT_HIP(c, hipStreamSynchronize(c->stream));
@@ -266,6 +285,67 @@ int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_
   c->mapDocs = nDocs;
   c->mapKeyBound = keyBound;
   c->mapLoaded = true;
+  c->mapSparse = sparse;
+  return FMT_OK;
+}
+
+int fmt_map_load(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_t* offs, uint32_t nDocs,
+                 uint32_t keyBound) {
+  const int rc = mapValidate(c, ops, nOps, offs, nDocs, keyBound);
+  return rc != FMT_OK ? rc : mapStage(c, ops, nOps, offs, nDocs, keyBound, false);
+}
+
+int fmt_map_load_sparse(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint64_t* offs, uint32_t nDocs,
+                        uint32_t keyBound) {
+  const int rc = mapValidate(c, ops, nOps, offs, nDocs, keyBound);
+  return rc != FMT_OK ? rc : mapStage(c, ops, nOps, offs, nDocs, keyBound, true);
+}
+
+int fmt_map_run_sparse(fmt_ctx* c) {
+  if (c == nullptr || !c->mapLoaded || !c->mapSparse) return setErr(c, FMT_E_USAGE, "fmt_map_run_sparse before fmt_map_load_sparse");
+  FMT_HIP(c, hipSetDevice(c->device));
+  FMT_HIP(c, hipMemsetAsync(c->errWord.p, 0, sizeof(int), c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
+  FMT_HIP(c, fmt_kernels::launchMapSparse(c->mapOps.p, c->mapOffs.p, c->mapDocs, c->mapKeyBound, c->mapEntries.p,
+                                          c->mapCounts.p, c->errWord.p, c->numCUs, c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
+  c->timed = true;
+  c->timed2 = false;
+  c->stats = fmt_stats{};
+  c->stats.ops = c->mapNOps;
+  c->stats.docs = c->mapDocs;
+  c->stats.bytes_read = c->mapNOps * sizeof(fmt_map_op) + (c->mapDocs + 1ull) * sizeof(uint64_t);
+  c->stats.bytes_written = static_cast<uint64_t>(c->mapDocs) * sizeof(uint32_t);  // + entries, at fetch
+  c->stats.launches = 1;
+  return FMT_OK;
+}
+
+int fmt_map_fetch_sparse(fmt_ctx* c, uint32_t* counts, fmt_map_entry* entries, uint64_t capEntries, uint64_t* nEntries) {
+  if (c == nullptr || counts == nullptr || !c->mapLoaded || !c->mapSparse)
+    return setErr(c, FMT_E_USAGE, "fmt_map_fetch_sparse: nothing loaded");
+  FMT_HIP(c, hipSetDevice(c->device));
+  int errWord = 0;
+  FMT_HIP(c, hipMemcpyAsync(&errWord, c->errWord.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipMemcpyAsync(counts, c->mapCounts.p, c->mapDocs * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  std::vector<uint64_t> packedOff(c->mapDocs + 1ull, 0);
+  for (uint32_t d = 0; d < c->mapDocs; d++) packedOff[d + 1] = packedOff[d] + counts[d];
+  const uint64_t n = packedOff[c->mapDocs];
+  if (nEntries) *nEntries = n;
+  c->stats.bytes_written = static_cast<uint64_t>(c->mapDocs) * sizeof(uint32_t) + n * sizeof(fmt_map_entry);
+  if (entries != nullptr) {
+    if (capEntries < n) return setErr(c, FMT_E_USAGE, "fmt_map_fetch_sparse: cap_entries below the live entries");
+    FMT_HIP(c, c->mapPackedOff.reserve(c->mapDocs + 1ull));
+    FMT_HIP(c, c->mapPacked.reserve(n));
+    FMT_HIP(c, hipMemcpyAsync(c->mapPackedOff.p, packedOff.data(), (c->mapDocs + 1ull) * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, c->stream));
+    FMT_HIP(c, fmt_kernels::launchMapSparsePack(c->mapEntries.p, c->mapOffs.p, c->mapCounts.p, c->mapPackedOff.p,
+                                                c->mapDocs, c->mapPacked.p, c->stream));
+    FMT_HIP(c, hipMemcpyAsync(entries, c->mapPacked.p, n * sizeof(fmt_map_entry), hipMemcpyDeviceToHost, c->stream));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  if (errWord & 1) return setErr(c, FMT_E_DATA, "an op referenced a key id >= key_bound");
+  if (errWord & 2) return setErr(c, FMT_E_CAPACITY, "a document exceeded the sparse path's keys or ops per document");
   return FMT_OK;
 }
 
@@ -301,12 +381,13 @@ static int runMap(fmt_ctx* c, const fmt_map_op* ops, const uint64_t* offs, uint3
 }
 
 int fmt_map_run(fmt_ctx* c) {
-  if (c == nullptr || !c->mapLoaded) return setErr(c, FMT_E_USAGE, "fmt_map_run before fmt_map_load");
+  if (c == nullptr || !c->mapLoaded || c->mapSparse) return setErr(c, FMT_E_USAGE, "fmt_map_run before fmt_map_load");
   return runMap(c, c->mapOps.p, c->mapOffs.p, c->mapDocs, c->mapKeyBound, c->mapNOps, c->mapOut.p);
 }
 
 int fmt_map_fetch(fmt_ctx* c, fmt_map_slot* out) {
-  if (c == nullptr || out == nullptr || !c->mapLoaded) return setErr(c, FMT_E_USAGE, "fmt_map_fetch: nothing loaded");
+  if (c == nullptr || out == nullptr || !c->mapLoaded || c->mapSparse)
+    return setErr(c, FMT_E_USAGE, "fmt_map_fetch: nothing loaded");
   int errWord = 0;
   FMT_HIP(c, hipMemcpyAsync(&errWord, c->errWord.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   FMT_HIP(c, hipMemcpyAsync(out, c->mapOut.p, static_cast<size_t>(c->mapDocs) * c->mapKeyBound * sizeof(fmt_map_slot),

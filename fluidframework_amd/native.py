@@ -63,6 +63,7 @@ PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
 assert PROPSET_DTYPE.itemsize == 36
 
 MAP_SLOT_DTYPE = np.dtype([("value", "<u4"), ("birth_seq", "<u4")])
+MAP_ENTRY_DTYPE = np.dtype([("key", "<u4"), ("value", "<u4"), ("birth_seq", "<u4")])  # fmt_map_entry
 
 
 class FmtMtBatch(ctypes.Structure):
@@ -166,6 +167,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_map_fetch.argtypes = [P, P]
         L.fmt_map_replay_device.argtypes = [P, P, P, U32, U32, P]
         L.fmt_map_check.argtypes = [P]
+        L.fmt_map_load_sparse.argtypes = [P, P, U64, P, U32, U32]
+        L.fmt_map_run_sparse.argtypes = [P]
+        L.fmt_map_fetch_sparse.argtypes = [P, P, P, U64, ctypes.POINTER(U64)]
         L.fmt_mt_load.argtypes = [P, ctypes.POINTER(FmtMtBatch)]
         L.fmt_mt_run.argtypes = [P]
         L.fmt_mt_fetch_headers.argtypes = [P, P]
@@ -180,6 +184,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
 EXPORTED_SYMBOLS = [
     "fmt_open", "fmt_close", "fmt_last_error", "fmt_sync", "fmt_get_stats", "fmt_device_info",
     "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device", "fmt_map_check",
+    "fmt_map_load_sparse", "fmt_map_run_sparse", "fmt_map_fetch_sparse",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_remove_order", "fmt_mt_capacity",
 ]
@@ -257,6 +262,26 @@ class Engine:
         out = np.zeros(self._map_shape[0] * self._map_shape[1], dtype=MAP_SLOT_DTYPE)
         self._check(self.L.fmt_map_fetch(self.h, _ptr(out)))
         return out.reshape(self._map_shape)
+
+    # sparse path (key pools of any size): one entry per live key, per document in birth order
+    def map_load_sparse(self, batch):
+        ops = np.ascontiguousarray(batch.ops)
+        offs = np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64)
+        self._check(self.L.fmt_map_load_sparse(self.h, _ptr(ops), len(ops), _ptr(offs), batch.n_docs, batch.key_bound))
+        self._map_shape = (batch.n_docs, batch.key_bound)
+        self._map_nops = len(ops)
+
+    def map_run_sparse(self):
+        self._check(self.L.fmt_map_run_sparse(self.h))
+
+    def map_fetch_sparse(self):
+        """(counts[n_docs], entries[sum(counts)]) with MAP_ENTRY_DTYPE, documents in order."""
+        counts = np.zeros(self._map_shape[0], dtype=np.uint32)
+        n = ctypes.c_uint64()
+        self._check(self.L.fmt_map_fetch_sparse(self.h, _ptr(counts), None, 0, ctypes.byref(n)))
+        entries = np.zeros(max(n.value, 1), dtype=MAP_ENTRY_DTYPE)
+        self._check(self.L.fmt_map_fetch_sparse(self.h, _ptr(counts), _ptr(entries), n.value, ctypes.byref(n)))
+        return counts, entries[: n.value]
 
     # ---- merge-tree
     def mt_load(self, batch):

@@ -106,6 +106,18 @@ def map_checksum(slots: np.ndarray, doc_lo: int = 0) -> int:
         return int(h.sum(dtype=np.uint64))
 
 
+def map_sparse_checksum(counts: np.ndarray, entries: np.ndarray, doc_lo: int = 0) -> int:
+    """Order-independent checksum of sparse SharedMap entries (fmt_map_entry per live key)."""
+    doc = np.repeat(np.arange(doc_lo, doc_lo + len(counts), dtype=np.uint64), counts.astype(np.int64))
+    with np.errstate(over="ignore"):
+        h = (doc * np.uint64(0x100000000) + entries["key"].astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        h ^= entries["value"].astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)
+        h ^= entries["birth_seq"].astype(np.uint64) + np.uint64(0x94D049BB133111EB)
+        h *= np.uint64(0xD6E8FEB86659FD93)
+        h ^= h >> np.uint64(32)
+        return int(h.sum(dtype=np.uint64))
+
+
 def gather_stats(rec: np.ndarray, dist, device=None) -> np.ndarray:
     """All-gather one STATS_DTYPE record per rank (the run's single exchange step).
 

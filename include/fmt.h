@@ -305,6 +305,28 @@ int fmt_map_replay_device(fmt_ctx* ctx, const fmt_map_op* d_ops, const uint64_t*
  * >= key_bound (the remote op the reference would reject while processing it, mapKernel.ts:619-630). */
 int fmt_map_check(fmt_ctx* ctx);
 
+/* Sparse LWW for key pools of any size (key_bound up to 2^32 - 1): the per-key reductions run in
+ * a per-document LDS hash table and the result is one entry per LIVE key, in JS Map insertion order
+ * (birth seq ascending; map.ts:176-246 orders array-index keys first on top of that). Limits per
+ * document: FMT_MAP_SPARSE_MAX_KEYS distinct keys and FMT_MAP_SPARSE_MAX_OPS ops (beyond them the
+ * document gets no entries and fmt_map_fetch_sparse returns FMT_E_CAPACITY). */
+typedef struct fmt_map_entry {
+  uint32_t key;
+  uint32_t value;      /* value id (FMT_MAP_VALUE_UNDEFINED: set with value undefined) */
+  uint32_t birth_seq;  /* seq of the first set after the key's last delete/clear */
+} fmt_map_entry;
+#define FMT_MAP_SPARSE_MAX_KEYS 2048
+#define FMT_MAP_SPARSE_MAX_OPS 16384
+/* Stage a batch for the sparse path (no dense per-(doc, key) output is allocated). */
+int fmt_map_load_sparse(fmt_ctx* ctx, const fmt_map_op* ops, uint64_t n_ops,
+                        const uint64_t* doc_op_offsets, uint32_t n_docs, uint32_t key_bound);
+/* Replay it (asynchronous on the ctx stream). */
+int fmt_map_run_sparse(fmt_ctx* ctx);
+/* counts[d] = live entries of document d (n_docs entries); entries of all documents packed in
+ * document order into `entries` (cap_entries; *n_entries = their total). Synchronizes. */
+int fmt_map_fetch_sparse(fmt_ctx* ctx, uint32_t* counts, fmt_map_entry* entries, uint64_t cap_entries,
+                         uint64_t* n_entries);
+
 /* ---------------------------------------------------------------------------------------------
  * merge-tree / SharedString (Client.applyMsg observer path + zamboni, client.ts:1358-1391)
  * ------------------------------------------------------------------------------------------- */

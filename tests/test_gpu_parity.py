@@ -98,6 +98,61 @@ def test_map_lww_key_pool_beyond_lds(orc, engine, n_docs, n_ops, key_pool):
     assert np.array_equal(engine.map_fetch(), exp)
 
 
+def _dense_to_sparse(exp):
+    """Oracle dense slots -> per document [(key, value, birth)] in birth order (JS Map order)."""
+    out = []
+    for d in range(exp.shape[0]):
+        live = np.nonzero(exp["value"][d] != 0xFFFFFFFF)[0]
+        rows = sorted((int(exp["birth_seq"][d][k]), int(k), int(exp["value"][d][k])) for k in live)
+        out.append([(k, v, b) for b, k, v in rows])
+    return out
+
+
+@pytest.mark.parametrize("n_docs,n_ops,key_pool", [(200, 1000, 20), (64, 1000, 5000), (24, 1000, 1 << 20),
+                                                   (16, 3000, 1 << 20)])
+def test_map_sparse_matches_oracle(orc, engine, n_docs, n_ops, key_pool):
+    """Sparse LWW (map_sparse.hip: LDS hash reduce-by-key, one entry per live key in birth order):
+    equal to the oracle's dense result, small and 2^20 key pools, register and streaming paths."""
+    batch = workloads.map_stream(n_docs, n_ops, key_pool=key_pool, seed=41)
+    engine.map_load_sparse(batch)
+    engine.map_run_sparse()
+    counts, entries = engine.map_fetch_sparse()
+    exp, _ = orc.map_replay(batch, threads=16)
+    want = _dense_to_sparse(exp)
+    assert [len(w) for w in want] == [int(c) for c in counts]
+    o = 0
+    for d in range(n_docs):
+        got = [(int(e["key"]), int(e["value"]), int(e["birth_seq"])) for e in entries[o : o + int(counts[d])]]
+        o += int(counts[d])
+        assert got == want[d], d
+    engine.map_run_sparse()  # a second run gives the same entries
+    c2, e2 = engine.map_fetch_sparse()
+    assert np.array_equal(c2, counts) and np.array_equal(e2, entries)
+
+
+def test_map_sparse_limits(engine):
+    """A key id >= key_bound is FMT_E_DATA; a document with more distinct keys than the table holds
+    is FMT_E_CAPACITY (its count 0), the other documents unaffected."""
+    from fluidframework_amd.streams import MapBatch
+
+    src = workloads.map_stream(4, 3000, key_pool=1 << 20, seed=43)
+    bad = MapBatch(src.ops.copy(), src.doc_op_offsets, 1000, src.keys, src.values)
+    engine.map_load_sparse(bad)
+    engine.map_run_sparse()
+    with pytest.raises(native.EngineError) as ei:
+        engine.map_fetch_sparse()
+    assert ei.value.code == native.FMT_E_DATA
+    ops = src.ops.copy()
+    o0, o1 = int(src.doc_op_offsets[1]), int(src.doc_op_offsets[2])
+    ops["kind_value"][o0:o1] = ops["kind_value"][o0:o1] & 0x3FFFFFFF  # all sets
+    ops["key"][o0:o1] = np.arange(o1 - o0, dtype=np.uint32) * 7 + 1   # 3000 distinct keys
+    engine.map_load_sparse(MapBatch(ops, src.doc_op_offsets, src.key_bound, src.keys, src.values))
+    engine.map_run_sparse()
+    with pytest.raises(native.EngineError) as ei:
+        engine.map_fetch_sparse()
+    assert ei.value.code == native.FMT_E_CAPACITY
+
+
 def test_map_lww_ragged_documents(orc, engine):
     """Document lengths straddle the register-held path (≤1024 ops) and the streaming path, with
     empty and one-op documents in between."""
