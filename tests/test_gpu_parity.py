@@ -109,7 +109,7 @@ def _dense_to_sparse(exp):
 
 
 @pytest.mark.parametrize("n_docs,n_ops,key_pool", [(200, 1000, 20), (64, 1000, 5000), (24, 1000, 1 << 20),
-                                                   (16, 3000, 1 << 20)])
+                                                   (16, 1800, 1 << 20), (16, 3000, 1500)])
 def test_map_sparse_matches_oracle(orc, engine, n_docs, n_ops, key_pool):
     """Sparse LWW (map_sparse.hip: LDS hash reduce-by-key, one entry per live key in birth order):
     equal to the oracle's dense result, small and 2^20 key pools, register and streaming paths."""
