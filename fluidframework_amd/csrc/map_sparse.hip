@@ -166,12 +166,29 @@ __global__ __launch_bounds__(64 * kSpWaves) void mapSparseKernel(const fmt_map_o
       spSync();
       continue;
     }
-    // births of live keys into the bitmap, then word prefixes (one wave scan over per-lane sums)
-    for (uint32_t s = lane; s < kSpSlots; s += 64) {
-      const uint32_t f = w->first[s];
-      if (w->key[s] != kSpEmpty && f != kSpEmpty) atomicOr(&w->born[f >> 5], 1u << (f & 31));
+    // every slot of this lane (kSlotsPerLane, unrolled): live keys mark their births in the bitmap,
+    // and the value / birth-seq loads of all of them are issued before any is used
+    constexpr int kPer = kSpSlots / 64;
+    uint32_t sk[kPer], sf[kPer], sl[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      const uint32_t sl0 = lane + 64 * i;
+      sk[i] = w->key[sl0];
+      sf[i] = w->first[sl0];
+      sl[i] = w->last[sl0];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; i++)
+      if (sk[i] != kSpEmpty && sf[i] != kSpEmpty) atomicOr(&w->born[sf[i] >> 5], 1u << (sf[i] & 31));
+    uint32_t val[kPer], bseq[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      const bool live = sk[i] != kSpEmpty && sf[i] != kSpEmpty;
+      val[i] = live ? recs[begin + sl[i]].w : 0u;
+      bseq[i] = live ? recs[begin + sf[i]].z : 0u;
     }
     spSync();
+    // word prefixes of the birth bitmap (one wave scan over per-lane sums)
     const uint32_t nWords = (n + 31) / 32, per = (nWords + 63) / 64;
     uint32_t mine = 0;
     for (uint32_t k = 0; k < per; k++) {
@@ -194,14 +211,15 @@ __global__ __launch_bounds__(64 * kSpWaves) void mapSparseKernel(const fmt_map_o
     }
     spSync();
     fmt_map_entry* o = out + begin;
-    for (uint32_t s = lane; s < kSpSlots; s += 64) {
-      const uint32_t f = w->first[s];
-      if (w->key[s] == kSpEmpty || f == kSpEmpty) continue;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      if (sk[i] == kSpEmpty || sf[i] == kSpEmpty) continue;
+      const uint32_t f = sf[i];
       const uint32_t rank = w->wordBase[f >> 5] + __popc(w->born[f >> 5] & ((1u << (f & 31)) - 1u));
       fmt_map_entry e;
-      e.key = w->key[s];
-      e.value = recs[begin + w->last[s]].w & FMT_MAP_VALUE_MASK;
-      e.birth_seq = recs[begin + f].z;
+      e.key = sk[i];
+      e.value = val[i] & FMT_MAP_VALUE_MASK;
+      e.birth_seq = bseq[i];
       o[rank] = e;
     }
     if (lane == 0) counts[doc] = total;
