@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--unique-docs", type=int, default=0, help="0 = all documents distinct")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--key-pool", type=int, default=20, help="map: key ids per document (> 2560 takes the HBM-table path)")
+    ap.add_argument("--no-summaries", action="store_true",
+                    help="mt: skip the bulk legacy summaries of every document after the timed steps")
     ap.add_argument("--sparse", action="store_true",
                     help="map: the sparse path (LDS hash reduce-by-key, one entry per live key; any key pool)")
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
@@ -213,6 +215,27 @@ def main():
                         "build_ms_rank0": build_s * 1e3,
                         "what": f"legacy summaries (header, body) of the first {args.gather_docs} documents of every "
                                 "shard, gathered to rank 0 (all-gather of byte counts + grouped send/recv)"}
+    summaries = None
+    if mt and not t2 and not args.no_summaries:
+        # every document's legacy summary from the converged state (device merge + host JSON on the
+        # usable cores), timed apart from the replay; a sample checked against the Python host
+        from fluidframework_amd.summary import legacy_summary
+
+        st_threads = host_cpus()["usable"]
+        tm = eng.mt_summarize_legacy(batch.keys, batch.values, threads=st_threads)
+        total_ms = tm["kernel_ms"] + tm["fetch_ms"] + tm["format_ms"]
+        checked = 0
+        for d in range(0, docs, max(1, docs // 16)):
+            lv, ch, pr = eng.mt_doc(d, hdrs[d])
+            if eng.mt_summary(d) != legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values):
+                raise SystemExit(f"bulk summary of document {d} differs from the Python host's")
+            checked += 1
+        summaries = {"docs": docs, "summaries_per_s": docs / (total_ms / 1e3), **tm, "total_ms": total_ms,
+                     "checked_vs_python": checked,
+                     "what": "legacy SharedString summary (header + body chunk) of every document: extractSync "
+                             "merge on the GPU (summaryRunsKernel), JSON on host threads; catch-up ops not included"}
+        log(rank, f"[bench] summaries: {summaries['summaries_per_s']:.3g}/s ({total_ms:.1f} ms: kernel "
+                  f"{tm['kernel_ms']:.1f}, fetch {tm['fetch_ms']:.1f}, format {tm['format_ms']:.1f} on {tm['threads']} threads)")
     elapsed = float(stats["elapsed_s"].max())
     total_ops = int(stats["ops"].sum()) * args.steps
     value = total_ops / elapsed
@@ -315,6 +338,7 @@ def main():
             "cpu_baseline": cpu,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
             "summary_gather": gathered,
+            "summaries": summaries,
             "failed_docs": int(stats["status_bad"].sum()),
             "h2d_gbps": in_bytes / h2d_s / 1e9,
         }

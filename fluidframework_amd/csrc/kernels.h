@@ -46,6 +46,25 @@ struct MtDeviceOut {
 };
 
 // Per-document capacities of the small (LDS-text) and large (HBM-text) engine tiers.
+// Bulk legacy summaries (summary.hip): a document's result buffers, its runs and its output spans.
+struct SumView {
+  const fmt_mt_leaf* leaves;
+  const uint16_t* chars;
+  const fmt_mt_propset* props;
+};
+struct SumRun {
+  uint32_t len;    // UTF-16 units of the merged segment
+  uint16_t props;  // prop set id of its head leaf (0xffff: undefined)
+  uint16_t flags;  // 1: a Marker (its one unit is the refType)
+};
+struct SumDocOut {
+  unsigned long long run_off, text_off;
+  uint32_t n_runs, n_units, status, pad;
+};
+hipError_t launchSummaryRuns(const fmt_mt_doc_result* hdrs, const SumView* views, uint32_t nDocs, SumRun* runs,
+                             uint16_t* text, unsigned long long* cursors, SumDocOut* docOut, int numCUs,
+                             hipStream_t stream);
+
 struct MtCaps {
   uint32_t leaves, chars, props;
 };

@@ -6,7 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <thread>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -103,6 +105,15 @@ struct fmt_ctx {
   };
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
+  // bulk legacy summaries (fmt_mt_summarize_legacy): device runs / text, host blobs
+  DevBuf<fmt_kernels::SumView> sumViews;
+  DevBuf<fmt_kernels::SumRun> sumRuns;
+  DevBuf<uint16_t> sumText;
+  DevBuf<unsigned long long> sumCursors;
+  DevBuf<fmt_kernels::SumDocOut> sumDocs;
+  std::vector<std::string> sumBlobs;          // per document: header, then body
+  std::vector<uint32_t> sumSplit;             // per document: header length in sumBlobs[d]
+  std::vector<int32_t> sumStatus;
   DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
   uint32_t mtNSmall = 0;
   DevBuf<fmt_huge::HugeState> hugeStates;
@@ -772,6 +783,279 @@ int fmt_mt_fetch_doc(fmt_ctx* c, uint32_t doc, fmt_mt_leaf* leaves, uint32_t cap
   if (leaves && nl) FMT_HIP(c, hipMemcpy(leaves, dLeaves + at * caps.leaves, nl * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
   if (chars && nc) FMT_HIP(c, hipMemcpy(chars, dChars + at * caps.chars, nc * 2ull, hipMemcpyDeviceToHost));
   if (props && np) FMT_HIP(c, hipMemcpy(props, dProps + at * caps.props, np * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+// ------------------------------------------------------------------ bulk legacy summaries
+namespace {
+
+// JSON.stringify of a UTF-16 string (well-formed: lone surrogates as \udXXX), as UTF-8.
+void jsonQuote16(std::string& o, const uint16_t* s, size_t n) {
+  static const char* hex = "0123456789abcdef";
+  o.push_back('"');
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t c = s[i];
+    if (c == '"') o += "\\\"";
+    else if (c == '\\') o += "\\\\";
+    else if (c == '\b') o += "\\b";
+    else if (c == '\f') o += "\\f";
+    else if (c == '\n') o += "\\n";
+    else if (c == '\r') o += "\\r";
+    else if (c == '\t') o += "\\t";
+    else if (c < 0x20) {
+      o += "\\u00";
+      o.push_back(hex[c >> 4]);
+      o.push_back(hex[c & 15]);
+    } else if (c < 0x80) {
+      o.push_back(static_cast<char>(c));
+    } else if (c < 0x800) {
+      o.push_back(static_cast<char>(0xC0 | (c >> 6)));
+      o.push_back(static_cast<char>(0x80 | (c & 0x3F)));
+    } else if (c >= 0xD800 && c <= 0xDBFF && i + 1 < n && s[i + 1] >= 0xDC00 && s[i + 1] <= 0xDFFF) {
+      const uint32_t cp = 0x10000 + ((c - 0xD800) << 10) + (s[i + 1] - 0xDC00);
+      i++;
+      o.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+      o.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+      o.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    } else if (c >= 0xD800 && c <= 0xDFFF) {
+      o += "\\u";
+      for (int k = 12; k >= 0; k -= 4) o.push_back(hex[(c >> k) & 15]);
+    } else {
+      o.push_back(static_cast<char>(0xE0 | (c >> 12)));
+      o.push_back(static_cast<char>(0x80 | ((c >> 6) & 0x3F)));
+      o.push_back(static_cast<char>(0x80 | (c & 0x3F)));
+    }
+  }
+  o.push_back('"');
+}
+
+// A quoted key "digits" that is a canonical array index (< 2^32 - 1): its value, else -1.
+int64_t arrayIndexOfQuoted(const std::string& q) {
+  if (q.size() < 3 || q.size() > 12 || q.front() != '"' || q.back() != '"') return -1;
+  const size_t n = q.size() - 2;
+  if (n > 1 && q[1] == '0') return -1;
+  int64_t v = 0;
+  for (size_t i = 1; i + 1 < q.size(); i++) {
+    if (q[i] < '0' || q[i] > '9') return -1;
+    v = v * 10 + (q[i] - '0');
+  }
+  return v < 4294967295LL ? v : -1;
+}
+
+struct SumDict {
+  std::vector<std::string> keys, values;  // keys JSON-quoted, values JSON texts (UTF-8)
+  std::vector<int64_t> keyIndex;          // array-index value of each key, or -1
+};
+
+// A prop set as a JSON object in JS own-property order: array-index keys ascending, then the
+// others in insertion order (properties' key order, snapshotChunks.ts via JSON.stringify).
+void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D) {
+  const uint32_t n = ps.n < FMT_MT_PROPS_MAX ? ps.n : FMT_MT_PROPS_MAX;
+  uint32_t order[FMT_MT_PROPS_MAX];
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; i++)
+    if (D.keyIndex[ps.kv[i] >> 16] >= 0) order[m++] = i;
+  std::sort(order, order + m, [&](uint32_t a, uint32_t b) { return D.keyIndex[ps.kv[a] >> 16] < D.keyIndex[ps.kv[b] >> 16]; });
+  for (uint32_t i = 0; i < n; i++)
+    if (D.keyIndex[ps.kv[i] >> 16] < 0) order[m++] = i;
+  o.push_back('{');
+  for (uint32_t j = 0; j < m; j++) {
+    if (j) o.push_back(',');
+    const uint32_t kv = ps.kv[order[j]];
+    o += D.keys[kv >> 16];
+    o.push_back(':');
+    o += D.values[kv & 0xFFFFu];
+  }
+  o.push_back('}');
+}
+
+// SnapshotLegacy.emit for one document (snapshotlegacy.ts:161-190 + snapshotChunks.ts:85-204):
+// the header chunk (runs until >= chunk units) and, when runs remain, the body chunk.
+void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* runs, uint32_t nRuns,
+                 const uint16_t* text, const fmt_mt_propset* props, int32_t minSeq, uint32_t chunk,
+                 const SumDict& D) {
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nRuns; i++) total += runs[i].len;
+  std::vector<uint64_t> start(nRuns + 1, 0);
+  for (uint32_t i = 0; i < nRuns; i++) start[i + 1] = start[i] + runs[i].len;
+  auto emit = [&](uint32_t s0, uint64_t approx, bool header, uint32_t* count) {
+    uint32_t n = 0;
+    uint64_t len = 0;
+    while (len < approx && s0 + n < nRuns) len += runs[s0 + n++].len;
+    out += "{\"chunkStartSegmentIndex\":" + std::to_string(s0) + ",\"chunkSegmentCount\":" + std::to_string(n) +
+           ",\"chunkLengthChars\":" + std::to_string(len) + ",\"totalLengthChars\":" + std::to_string(total) +
+           ",\"totalSegmentCount\":" + std::to_string(nRuns) + ",\"chunkSequenceNumber\":" + std::to_string(minSeq) +
+           ",\"segmentTexts\":[";
+    for (uint32_t i = s0; i < s0 + n; i++) {
+      if (i > s0) out.push_back(',');
+      const fmt_kernels::SumRun& r = runs[i];
+      const bool hasProps = r.props != 0xFFFFu && props[r.props].n > 0;
+      if (r.flags & 1u) {  // Marker.toJSONObject
+        out += "{\"marker\":{\"refType\":" + std::to_string(text[start[i]]) + "}";
+        if (hasProps) {
+          out += ",\"props\":";
+          propsObject(out, props[r.props], D);
+        }
+        out.push_back('}');
+      } else if (hasProps) {
+        out += "{\"text\":";
+        jsonQuote16(out, text + start[i], r.len);
+        out += ",\"props\":";
+        propsObject(out, props[r.props], D);
+        out.push_back('}');
+      } else {
+        jsonQuote16(out, text + start[i], r.len);
+      }
+    }
+    out.push_back(']');
+    if (header) {
+      out += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+      if (len < total) out += ",{\"id\":\"body\"}";
+      out += "],\"sequenceNumber\":" + std::to_string(minSeq) + ",\"totalLength\":" + std::to_string(total) +
+             ",\"totalSegmentCount\":" + std::to_string(nRuns) + "}";
+    }
+    out.push_back('}');
+    *count = n;
+  };
+  uint32_t n1 = 0, n2 = 0;
+  emit(0, chunk, true, &n1);
+  *split = static_cast<uint32_t>(out.size());
+  if (n1 < nRuns) emit(n1, total, false, &n2);
+}
+
+}  // namespace
+
+int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys, const char* const* values,
+                            uint32_t nValues, uint32_t chunk, uint32_t threads, fmt_summary_timing* timing) {
+  if (c == nullptr || !c->mtLoaded || (nKeys && keys == nullptr) || (nValues && values == nullptr))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_summarize_legacy: bad arguments");
+  using clk = std::chrono::steady_clock;
+  FMT_HIP(c, hipSetDevice(c->device));
+  const uint32_t nd = c->mtDocs;
+  std::vector<fmt_mt_doc_result> hdr(nd);
+  FMT_HIP(c, hipMemcpyAsync(hdr.data(), c->mtHdr.p, nd * sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  // every document's result buffers (small tier, large-tier slab, or huge tier)
+  std::vector<fmt_kernels::SumView> views(nd);
+  std::vector<fmt_mt_propset*> propsDev(nd);
+  uint64_t capRuns = 0, capText = 0;
+  for (uint32_t d = 0; d < nd; d++) {
+    const int32_t hs = d < c->mtHugeSlot.size() ? c->mtHugeSlot[d] : -1;
+    if (hs >= 0) {
+      const fmt_kernels::HugeOut& O = c->huge[static_cast<size_t>(hs)].out;
+      views[d] = {O.leaves, O.chars, O.props};
+    } else {
+      const int32_t slot = d < c->mtBigSlot.size() ? c->mtBigSlot[d] : -1;
+      const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(slot >= 0);
+      const size_t at = slot >= 0 ? static_cast<size_t>(slot) : d;
+      views[d] = {(slot >= 0 ? c->mtBigLeaves.p : c->mtLeaves.p) + at * caps.leaves,
+                  (slot >= 0 ? c->mtBigChars.p : c->mtChars.p) + at * caps.chars,
+                  (slot >= 0 ? c->mtBigProps.p : c->mtProps.p) + at * caps.props};
+    }
+    propsDev[d] = const_cast<fmt_mt_propset*>(views[d].props);
+    capRuns += hdr[d].n_leaves;
+    capText += hdr[d].n_chars;
+  }
+  FMT_HIP(c, c->sumViews.reserve(nd));
+  FMT_HIP(c, c->sumRuns.reserve(capRuns));
+  FMT_HIP(c, c->sumText.reserve(capText));
+  FMT_HIP(c, c->sumCursors.reserve(2));
+  FMT_HIP(c, c->sumDocs.reserve(nd));
+  FMT_HIP(c, hipMemcpyAsync(c->sumViews.p, views.data(), nd * sizeof(fmt_kernels::SumView), hipMemcpyHostToDevice, c->stream));
+  FMT_HIP(c, hipMemsetAsync(c->sumCursors.p, 0, 2 * sizeof(unsigned long long), c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
+  FMT_HIP(c, fmt_kernels::launchSummaryRuns(c->mtHdr.p, c->sumViews.p, nd, c->sumRuns.p, c->sumText.p, c->sumCursors.p,
+                                            c->sumDocs.p, c->numCUs, c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev3, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  float kms = 0.f;
+  FMT_HIP(c, hipEventElapsedTime(&kms, c->ev2, c->ev3));
+  // fetch: per-document spans, runs, text and the prop sets the runs name
+  const auto t0 = clk::now();
+  unsigned long long cur[2];
+  FMT_HIP(c, hipMemcpy(cur, c->sumCursors.p, sizeof cur, hipMemcpyDeviceToHost));
+  std::vector<fmt_kernels::SumDocOut> docs(nd);
+  std::vector<fmt_kernels::SumRun> runs(cur[0] ? cur[0] : 1);
+  std::vector<uint16_t> text(cur[1] ? cur[1] : 1);
+  FMT_HIP(c, hipMemcpyAsync(docs.data(), c->sumDocs.p, nd * sizeof(fmt_kernels::SumDocOut), hipMemcpyDeviceToHost, c->stream));
+  if (cur[0]) FMT_HIP(c, hipMemcpyAsync(runs.data(), c->sumRuns.p, cur[0] * sizeof(fmt_kernels::SumRun), hipMemcpyDeviceToHost, c->stream));
+  if (cur[1]) FMT_HIP(c, hipMemcpyAsync(text.data(), c->sumText.p, cur[1] * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+  // prop sets: the small tier's slab in one copy, the other documents' tables one by one
+  const uint32_t smallCap = fmt_kernels::mergeTreeCaps(false).props;
+  std::vector<fmt_mt_propset> smallProps(static_cast<size_t>(nd) * smallCap + 1);
+  FMT_HIP(c, hipMemcpyAsync(smallProps.data(), c->mtProps.p, static_cast<size_t>(nd) * smallCap * sizeof(fmt_mt_propset),
+                            hipMemcpyDeviceToHost, c->stream));
+  std::vector<const fmt_mt_propset*> propsHost(nd);
+  std::vector<std::vector<fmt_mt_propset>> otherProps;
+  for (uint32_t d = 0; d < nd; d++) {
+    const bool small = !((d < c->mtHugeSlot.size() && c->mtHugeSlot[d] >= 0) || (d < c->mtBigSlot.size() && c->mtBigSlot[d] >= 0));
+    if (small || hdr[d].n_props == 0) {
+      propsHost[d] = smallProps.data() + static_cast<size_t>(d) * smallCap;
+      continue;
+    }
+    otherProps.emplace_back(hdr[d].n_props);
+    FMT_HIP(c, hipMemcpyAsync(otherProps.back().data(), propsDev[d], hdr[d].n_props * sizeof(fmt_mt_propset),
+                              hipMemcpyDeviceToHost, c->stream));
+    propsHost[d] = otherProps.back().data();
+  }
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  const auto t1 = clk::now();
+  // format on host threads
+  SumDict D;
+  D.keys.assign(keys, keys + nKeys);
+  D.values.assign(values, values + nValues);
+  D.keyIndex.resize(nKeys);
+  for (uint32_t k = 0; k < nKeys; k++) D.keyIndex[k] = arrayIndexOfQuoted(D.keys[k]);
+  c->sumBlobs.assign(nd, std::string());
+  c->sumSplit.assign(nd, 0);
+  c->sumStatus.assign(nd, FMT_OK);
+  const uint32_t nt = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < nt; t++)
+    pool.emplace_back([&, t] {
+      for (uint32_t d = t; d < nd; d += nt) {
+        const fmt_kernels::SumDocOut& o = docs[d];
+        if (static_cast<int32_t>(o.status) != FMT_OK) {
+          c->sumStatus[d] = static_cast<int32_t>(o.status);
+          continue;
+        }
+        bool bad = false;
+        for (uint32_t i = 0; i < o.n_runs; i++)
+          if (runs[o.run_off + i].props != 0xFFFFu && runs[o.run_off + i].props >= hdr[d].n_props) bad = true;
+        if (bad) {
+          c->sumStatus[d] = FMT_E_DATA;
+          continue;
+        }
+        c->sumBlobs[d].reserve(o.n_units + 64ull * o.n_runs + 256);
+        legacyBlobs(c->sumBlobs[d], &c->sumSplit[d], runs.data() + o.run_off, o.n_runs, text.data() + o.text_off,
+                    propsHost[d], hdr[d].min_seq, chunk ? chunk : 10000u, D);
+      }
+    });
+  for (auto& th : pool) th.join();
+  const auto t2 = clk::now();
+  if (timing) {
+    timing->kernel_ms = kms;
+    timing->fetch_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    timing->format_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    uint64_t bytes = 0;
+    for (const auto& b : c->sumBlobs) bytes += b.size();
+    timing->bytes = bytes;
+    timing->threads = nt;
+  }
+  return FMT_OK;
+}
+
+int fmt_mt_summary_blobs(fmt_ctx* c, uint32_t doc, const char** header, size_t* headerLen, const char** body,
+                         size_t* bodyLen) {
+  if (c == nullptr || doc >= c->sumBlobs.size()) return setErr(c, FMT_E_USAGE, "fmt_mt_summary_blobs: no summary for doc");
+  if (c->sumStatus[doc] != FMT_OK) return setErr(c, c->sumStatus[doc], "document has no summary (replay status)");
+  const std::string& b = c->sumBlobs[doc];
+  const size_t split = c->sumSplit[doc];
+  if (header) *header = b.data();
+  if (headerLen) *headerLen = split;
+  if (body) *body = b.data() + split;
+  if (bodyLen) *bodyLen = b.size() - split;
   return FMT_OK;
 }
 

@@ -138,6 +138,11 @@ class EngineUnavailable(RuntimeError):
     """libfmt.so is missing or no gfx950 device is usable. There is deliberately no fallback."""
 
 
+class FmtSummaryTiming(ctypes.Structure):  # fmt_summary_timing
+    _fields_ = [("kernel_ms", ctypes.c_double), ("fetch_ms", ctypes.c_double), ("format_ms", ctypes.c_double),
+                ("bytes", ctypes.c_uint64), ("threads", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
 class EngineError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"fmt error {STATUS_NAMES.get(code, code)}: {msg}")
@@ -168,6 +173,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_map_replay_device.argtypes = [P, P, P, U32, U32, P]
         L.fmt_map_check.argtypes = [P]
         L.fmt_map_load_sparse.argtypes = [P, P, U64, P, U32, U32]
+        L.fmt_mt_summarize_legacy.argtypes = [P, P, U32, P, U32, U32, U32, ctypes.POINTER(FmtSummaryTiming)]
+        L.fmt_mt_summary_blobs.argtypes = [P, U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                           ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t)]
         L.fmt_map_run_sparse.argtypes = [P]
         L.fmt_map_fetch_sparse.argtypes = [P, P, P, U64, ctypes.POINTER(U64)]
         L.fmt_mt_load.argtypes = [P, ctypes.POINTER(FmtMtBatch)]
@@ -185,6 +193,7 @@ EXPORTED_SYMBOLS = [
     "fmt_open", "fmt_close", "fmt_last_error", "fmt_sync", "fmt_get_stats", "fmt_device_info",
     "fmt_map_load", "fmt_map_run", "fmt_map_fetch", "fmt_map_replay_device", "fmt_map_check",
     "fmt_map_load_sparse", "fmt_map_run_sparse", "fmt_map_fetch_sparse",
+    "fmt_mt_summarize_legacy", "fmt_mt_summary_blobs",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_remove_order", "fmt_mt_capacity",
 ]
@@ -282,6 +291,30 @@ class Engine:
         entries = np.zeros(max(n.value, 1), dtype=MAP_ENTRY_DTYPE)
         self._check(self.L.fmt_map_fetch_sparse(self.h, _ptr(counts), _ptr(entries), n.value, ctypes.byref(n)))
         return counts, entries[: n.value]
+
+    # ---- bulk legacy summaries of the last merge-tree run
+    def mt_summarize_legacy(self, keys, values, chunk: int = 10000, threads: int = 0) -> dict:
+        """fmt_mt_summarize_legacy: every document's legacy summary blobs (device merge + host JSON);
+        returns the timing. Blobs: mt_summary(doc)."""
+        from .streams import js_quote
+
+        kq = [js_quote(k).encode("utf-8") for k in keys]
+        vq = [v.encode("utf-8") for v in values]
+        ka = (ctypes.c_char_p * max(len(kq), 1))(*kq)
+        va = (ctypes.c_char_p * max(len(vq), 1))(*vq)
+        t = FmtSummaryTiming()
+        self._check(self.L.fmt_mt_summarize_legacy(self.h, ka, len(kq), va, len(vq), chunk, threads, ctypes.byref(t)))
+        return {"kernel_ms": t.kernel_ms, "fetch_ms": t.fetch_ms, "format_ms": t.format_ms, "bytes": int(t.bytes),
+                "threads": int(t.threads)}
+
+    def mt_summary(self, doc: int):
+        """(header, body or None) of document `doc` from the last mt_summarize_legacy."""
+        h, b = ctypes.c_char_p(), ctypes.c_char_p()
+        hl, bl = ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(self.L.fmt_mt_summary_blobs(self.h, doc, ctypes.byref(h), ctypes.byref(hl), ctypes.byref(b), ctypes.byref(bl)))
+        head = ctypes.string_at(h, hl.value).decode("utf-8")
+        body = ctypes.string_at(b, bl.value).decode("utf-8") if bl.value else None
+        return head, body
 
     # ---- merge-tree
     def mt_load(self, batch):

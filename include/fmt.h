@@ -279,6 +279,26 @@ int fmt_get_stats(const fmt_ctx* ctx, fmt_stats* out);
 /* Name of the gfx target the library was built for and the device it runs on (diagnostics). */
 int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
 
+/* Bulk legacy SharedString summaries of every document of the last fmt_mt_run (replaces
+ * SharedString.summarizeCore → SnapshotLegacy.extractSync + emit, snapshotlegacy.ts:74-262 and
+ * snapshotChunks.ts:85-204, for all documents at once; catch-up ops are not included): the segment
+ * merge runs on the device (one wave per document), the JSON on `threads` host threads (0 = up to
+ * 16). keys: the batch's key strings JSON-quoted; values: the value JSON texts (UTF-8). */
+typedef struct fmt_summary_timing {
+  double kernel_ms;   /* device merge (events) */
+  double fetch_ms;    /* device -> host of runs, text and prop sets */
+  double format_ms;   /* host JSON */
+  uint64_t bytes;     /* blob bytes produced */
+  uint32_t threads;
+  uint32_t pad;
+} fmt_summary_timing;
+int fmt_mt_summarize_legacy(fmt_ctx* ctx, const char* const* keys, uint32_t n_keys, const char* const* values,
+                            uint32_t n_values, uint32_t chunk_size, uint32_t threads, fmt_summary_timing* timing);
+/* Document d's blobs from the last fmt_mt_summarize_legacy (valid until the next one): header and
+ * body (body_len 0: no body chunk). The replay's status when the document failed. */
+int fmt_mt_summary_blobs(fmt_ctx* ctx, uint32_t doc, const char** header, size_t* header_len, const char** body,
+                         size_t* body_len);
+
 /* ---------------------------------------------------------------------------------------------
  * SharedMap last-writer-wins (MapKernel sequenced path, mapKernel.ts:706-853)
  * ------------------------------------------------------------------------------------------- */

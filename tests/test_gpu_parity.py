@@ -508,3 +508,41 @@ def test_map_replay_device_buffers_and_bad_keys(orc, engine, key_pool):
     if key_pool > 2560:  # the HBM path's u64 view of d_out needs 8-byte alignment
         with pytest.raises(EngineError):
             engine.map_replay_device(raw.data_ptr(), offs.data_ptr(), batch.n_docs, key_pool, out.data_ptr() + 4)
+
+
+def test_mt_bulk_legacy_summaries_match_host(engine):
+    """fmt_mt_summarize_legacy (device extractSync merge + C++ JSON on host threads) equals the
+    Python host's legacy_summary of the same state, document by document: conflict farms with
+    props inserts (small tier and escalated documents), and the reference snapshots loaded (markers,
+    annotations, header + body chunks)."""
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+    from golden_data import snapshot_trees
+    from test_oracle_golden import _blobs
+
+    batch = workloads.with_insert_props(workloads.conflict_farm(300, n_clients=24, ops_per_doc=2000, seed=47))
+    hdrs = _gpu_mt(engine, batch)
+    t = engine.mt_summarize_legacy(batch.keys, batch.values)
+    assert t["bytes"] > 0
+    for d in range(batch.n_docs):
+        lv, ch, pr = engine.mt_doc(d, hdrs[d])
+        assert engine.mt_summary(d) == legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values), d
+    b = MergeTreeStreamBuilder()
+    names = ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"]
+    blobs = [_blobs(snapshot_trees()[n]) for n in names]
+    for bl in blobs:
+        b.begin_doc_from_summary(bl["header"], bl.get("body"))
+    sb = b.finish()
+    _gpu_mt(engine, sb)
+    engine.mt_summarize_legacy(sb.keys, sb.values)
+    for d, bl in enumerate(blobs):
+        assert engine.mt_summary(d) == (bl["header"], bl.get("body")), names[d]
+
+
+def test_mt_bulk_legacy_summary_of_a_huge_document(orc, engine):
+    batch = workloads.t3_stream(100_000, 20_000, n_clients=16, max_lag=512, max_range=8, seed=53)
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert engine.mt_summary(0) == legacy_summary(hdrs[0], lv, ch, pr, batch.keys, batch.values)
