@@ -39,8 +39,9 @@ def build(name, edits, rev=None):
         s = open(p).read()
         assert old in s, (name, fname, old[:50])
         open(p, "w").write(s.replace(old, new))
-    objs = []
-    for f in ["runtime.cpp", "map_lww.hip", "mergetree.hip"]:
+    # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc)
+    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o", "hugedoc.o")]
+    for f in ["runtime.cpp", "mergetree.hip"]:
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
                "-x", "hip", "-c", "-o", o, os.path.join(csrc, f)]
@@ -81,6 +82,12 @@ MAP_W8 = ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 8;
 MAP_W2 = ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 2;")
 MAP_LB2 = ("map_lww.hip", "__launch_bounds__(64 * kWaves) void mapLwwKernel", "__launch_bounds__(64 * kWaves, 2) void mapLwwKernel")
 
+ROWS4 = [("mt_engine.h", "  static constexpr int kRows = 8;          // rows of 64 leaves (one VR element per row)",
+          "  static constexpr int kRows = 4;          // rows of 64 leaves (one VR element per row)"),
+         ("mt_engine.h", "  using VR = V8;\n};\n\nstruct LargeTier", "  using VR = V4;\n};\n\nstruct LargeTier"),
+         ("wave.h", 'FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }',
+          'FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }\nFMT_DEV void launder(V4& v) { asm volatile("" : "+v"(v)); }')]
+
 NOLOAD = ("mt_engine.h", "    if (in.loaded) loadSnapshot();", "    if (false) loadSnapshot();")
 
 VARIANTS = {
@@ -92,6 +99,8 @@ VARIANTS = {
     "lb3": [LB3],
     "lb4": [LB4],
     "nodpp": [NODPP],
+    "rows4": ROWS4,
+    "rows4_lb3": ROWS4 + [LB3],
     "map_nt": [MAP_NT],
     "map_w8": [MAP_W8],
     "map_w2": [MAP_W2],
