@@ -334,6 +334,9 @@ def main():
                 "bytes_per_launch": bytes_per_launch,
                 "avg_kernel_ms": avg_kernel_ms,
                 "lds_bank_conflict_rate": traffic.get("lds_bank_conflict_rate") if traffic else None,
+                # what does bound the merge-tree kernel: instruction issue of the per-document op
+                # chains (SQ/GRBM PMC passes of this workload, tools/pmc_issue.py)
+                "issue": _issue_record(traffic) if mt else None,
             },
             "cpu_baseline": cpu,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
@@ -346,6 +349,25 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _issue_record(traffic):
+    """roofline.issue from the committed instruction-issue PMC passes (profiles/traffic.json)."""
+    rec = traffic.get("issue") if traffic else None
+    if not rec:
+        return None
+    split = rec.get("wave_cycle_split", {})
+    return {
+        "insts_per_op": rec.get("insts_per_op"),
+        "valu_busy": rec.get("valu_busy"),
+        "issue_busy": rec.get("issue_busy"),
+        "wave_cycles_active": split.get("active_inst_any"),
+        "wave_cycles_waitcnt": split.get("wait_any"),
+        "wave_cycles_issue_stall": split.get("wait_inst_any"),
+        "source": rec["source"][0].rsplit("/", 2)[0],
+        "note": "VALU busy = 4*SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); wave-cycle split from "
+                "SQ_WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_ANY (waitcnt) + WAIT_INST_ANY (issue stall)",
+    }
 
 
 def _wait(eng, rank, what, every=30.0, run=None):

@@ -70,11 +70,14 @@ struct MtCaps {
 };
 MtCaps mergeTreeCaps(bool large);
 
-// Small tier: replays documents docList[0..count) (or all docs when docList == nullptr); documents
-// that overflow it are listed in esc (esc[0] = count, then ids) when esc != nullptr.
+// Compact + small tiers: replays documents docList[0..count) (or all docs when docList == nullptr);
+// documents that overflow the small tier are listed in esc (esc[0] = count, then ids) when esc !=
+// nullptr. A plain batch (no obliterates, no remove order) with esc2 != nullptr starts in the compact
+// tier and lists its overflow in esc2 (count + 1 entries) for the small tier. esc[0] and esc2[0] must
+// be zero before the call.
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate,
-                           bool removeOrder);
+                           uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
+                           bool obliterate, bool removeOrder);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,

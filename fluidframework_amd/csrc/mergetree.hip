@@ -1,171 +1,54 @@
-// mergetree.hip — merge-tree conflict-farm replay kernel for gfx950.
+// mergetree.hip — merge-tree replay, small tier (8 register rows: 512 leaves, 2 waves/SIMD), the
+// overflow-list kernel and the tier cascade (kernel template: mergetree_kernel.h).
 //
-// One wavefront replays one document end to end (mt_engine.h); a batch holding obliterates runs the
-// Doc<true> instantiation, every other batch the obliterate-free Doc<false>. four documents per 256-thread
-// workgroup share the CU, each with its own LDS state (fmt_mt::Scratch, ~8.5 KiB). Documents are
-// independent, so the grid simply strides over them; there is no inter-workgroup communication.
-// The per-document sequential dependency (every op depends on the state its predecessors left) is
-// the reason this kernel is latency/LDS-bound rather than HBM-bound: its compulsory HBM traffic is
-// the 32-byte op record plus payload per op and the converged state written once per document.
-#include <hip/hip_runtime.h>
-
-#include "kernels.h"
-#include "mt_engine.h"
+// A plain batch replays every document in the compact tier first (mergetree_compact.hip: 4 rows,
+// 3 waves/SIMD); the documents it overflows replay in this tier from a device-side list; those this
+// tier overflows go to the large tier (mergetree_large.hip) after the host reads the list length.
+// Batches holding obliterates or remove-order recording start in this tier.
+#define FMT_MT_COLLECT_DEFINE 1
+#include "mergetree_kernel.h"
 
 namespace fmt_kernels {
 
-constexpr int kMtWaves = 4;     // small tier: 4 documents per workgroup, 2 waves/SIMD
-constexpr int kMtWavesLarge = 1;  // large tier: one document per workgroup, 1 wave/SIMD (VGPRs)
+constexpr int kMtWaves = 4;  // small tier: 4 documents per workgroup, 2 waves/SIMD
 
-// Diagnostic build only: per-phase shader-clock totals summed over all waves (mt_engine.h stamp()).
-__device__ unsigned long long g_mtProfile[fmt_mt::kPfCount];
-
-// Small tier over all documents (docList == nullptr) or a list. The large tier runs over the list
-// of documents that overflowed it, writing leaves/chars/props to slab i of the list (headers stay
-// per document).
-template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
-__global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
-                                                                      const uint32_t* __restrict__ docList,
-                                                                      uint32_t count) {
-  using Doc = fmt_mt::Doc<Ob, C, Rm>;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
-  fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds) + wave;
-  for (uint32_t i = blockIdx.x * Waves + wave; i < count; i += gridDim.x * Waves) {
-    const uint32_t d = docList ? docList[i] : i;
-    const size_t slot = C::kHbmChars ? i : d;
-    fmt_mt::DocInputs in;
-    in.ops = batch.ops;
-    in.begin = batch.docOpOffsets[d];
-    in.end = batch.docOpOffsets[d + 1];
-    in.text = batch.text;
-    in.initOff = batch.docInit ? batch.docInit[2 * d] : 0u;
-    in.initLen = batch.docInit ? batch.docInit[2 * d + 1] : 0u;
-    in.propsOff = batch.propsOff;
-    in.propsKv = batch.propsKv;
-    in.nPropsOps = batch.nPropsOps;
-    if (batch.snapshots && batch.snapshots[d].loaded) {
-      const fmt_mt_snapshot_doc sd = batch.snapshots[d];
-      in.snapSegs = batch.snapshotSegs + sd.first_seg;
-      in.nHeader = sd.n_header;
-      in.nBody = sd.n_body;
-      in.snapMinSeq = sd.min_seq;
-      in.snapSeq = sd.seq;
-      in.loaded = 1;
-    } else {
-      in.snapSegs = nullptr;
-      in.nHeader = in.nBody = 0;
-      in.snapMinSeq = in.snapSeq = 0;
-      in.loaded = 0;
-    }
-    fmt_mt::DocOutputs o;
-    o.header = out.headers + d;
-    o.leaves = out.leaves + slot * Doc::kCapLeaves;
-    o.chars = out.chars + slot * Doc::kCapChars;
-    o.props = out.props + slot * Doc::kPropCap;
-    if (batch.catchupOffsets) {
-      const uint64_t c0 = batch.catchupOffsets[d], c1 = batch.catchupOffsets[d + 1];
-      o.catchup = out.catchup + c0;
-      o.catchupCap = static_cast<uint32_t>(c1 - c0);
-    } else {
-      o.catchup = nullptr;
-      o.catchupCap = 0;
-    }
-    if (Rm && batch.rmOrderOffsets) {
-      const uint64_t r0 = batch.rmOrderOffsets[d], r1 = batch.rmOrderOffsets[d + 1];
-      o.rmOrder = out.rmOrder + r0;
-      o.rmOrderCap = static_cast<uint32_t>(r1 - r0);
-    } else {
-      o.rmOrder = nullptr;
-      o.rmOrderCap = 0;
-    }
-    Doc doc;
-    doc.s = scratch;
-    doc.run(in, o);
-#if FMT_PROFILE && FMT_GPU
-    if ((threadIdx.x & 63) == 0)
-      for (int c = 0; c < fmt_mt::kPfCount; c++) atomicAdd(&g_mtProfile[c], static_cast<unsigned long long>(doc.prof[c]));
-#endif
-  }
-}
+int mergeTreeProfileCompact(uint64_t* out, int n, bool reset);
+int mergeTreeProfileLarge(uint64_t* out, int n, bool reset);
 
 int mergeTreeProfile(uint64_t* out, int n, bool reset) {
-  unsigned long long h[fmt_mt::kPfCount];
-  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mtProfile), sizeof h) != hipSuccess) return -1;
-  for (int c = 0; c < n && c < fmt_mt::kPfCount; c++) out[c] = h[c];
-  if (reset) {
-    unsigned long long z[fmt_mt::kPfCount] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_mtProfile), z, sizeof z) != hipSuccess) return -1;
-  }
+  for (int c = 0; c < n; c++) out[c] = 0;
+  if (addTuProfile(out, n, reset) < 0 || mergeTreeProfileCompact(out, n, reset) < 0 ||
+      mergeTreeProfileLarge(out, n, reset) < 0)
+    return -1;
   return fmt_mt::kPfCount;
 }
 
 MtCaps mergeTreeCaps(bool large) {
   if (large)
-    return MtCaps{static_cast<uint32_t>(fmt_mt::Doc<false, fmt_mt::LargeTier>::kCapLeaves),
-                  static_cast<uint32_t>(fmt_mt::LargeTier::kCapChars), static_cast<uint32_t>(fmt_mt::LargeTier::kPropCap)};
-  return MtCaps{static_cast<uint32_t>(fmt_mt::Doc<false, fmt_mt::SmallTier>::kCapLeaves),
-                static_cast<uint32_t>(fmt_mt::SmallTier::kCapChars), static_cast<uint32_t>(fmt_mt::SmallTier::kPropCap)};
+    return MtCaps{static_cast<uint32_t>(Slab<fmt_mt::LargeTier>::kLeaves), static_cast<uint32_t>(Slab<fmt_mt::LargeTier>::kChars),
+                  static_cast<uint32_t>(Slab<fmt_mt::LargeTier>::kProps)};
+  return MtCaps{static_cast<uint32_t>(Slab<fmt_mt::SmallTier>::kLeaves), static_cast<uint32_t>(Slab<fmt_mt::SmallTier>::kChars),
+                static_cast<uint32_t>(Slab<fmt_mt::SmallTier>::kProps)};
 }
 
-// The documents the small tier could not hold (FMT_E_CAPACITY): esc[0] = count, esc[1..] = ids.
-// A limit the large tier shares (fmt_mt::kCapacityFinal) is reported as FMT_E_CAPACITY without
-// escalation.
-__global__ __launch_bounds__(256) void collectOverflowKernel(fmt_mt_doc_result* __restrict__ headers,
-                                                             const uint32_t* __restrict__ docList, uint32_t nDocs,
-                                                             uint32_t* esc) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nDocs; i += gridDim.x * blockDim.x) {
-    const uint32_t d = docList ? docList[i] : i;
-    const int st = headers[d].status;
-    if (st == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;
-    if (st == FMT_E_CAPACITY) {
-      const uint32_t k = atomicAdd(esc, 1u);
-      esc[1 + k] = d;
-    }
-  }
-}
+hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream);
 
-template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
-static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                             uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream) {
-  const size_t lds = sizeof(fmt_mt::Scratch<C>) * Waves;
-  // One resident wave of workgroups: every workgroup strides over the same number of documents,
-  // so none waits behind the residency limit (VGPRs cap the small tier at 2 waves/SIMD).
-  int blocksPerCU = 0;
-  const hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>, 64 * Waves, lds);
-  if (e != hipSuccess) return e;
-  const uint32_t wanted = (count + Waves - 1) / Waves;
-  const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
-  const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
-  hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
-                     docList, count);
-  if (esc != nullptr) {  // over the documents this launch replayed
-    const uint32_t g = (count + 255) / 256;
-    hipLaunchKernelGGL(collectOverflowKernel, dim3(g < 1024 ? (g > 0 ? g : 1) : 1024), dim3(256), 0, stream, out.headers,
-                       docList, count, esc);
-  }
-  return hipGetLastError();
-}
-
-// Variants: obliterates (Ob), or the remove-order recording of SnapshotV1 batches (Rm; the host
-// rejects batches that would need both), or neither.
+// Variants: obliterates (Ob) and/or the remove-order recording of SnapshotV1 batches (Rm).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, bool obliterate,
-                           bool removeOrder) {
+                           uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
+                           bool obliterate, bool removeOrder) {
   using S = fmt_mt::SmallTier;
+  if (obliterate && removeOrder)
+    return launchTier<true, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
   if (obliterate) return launchTier<true, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
   if (removeOrder) return launchTier<false, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
-  return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
-}
-
-hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder) {
-  using G = fmt_mt::LargeTier;
-  if (obliterate) return launchTier<true, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
-  if (removeOrder)
-    return launchTier<false, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
-  return launchTier<false, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+  if (esc == nullptr || esc2 == nullptr)
+    return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+  // compact tier over everything → overflow list esc2 → this tier over that list → overflow list esc
+  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream);
+  if (e != hipSuccess) return e;
+  return launchTier<false, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2);
 }
 
 }  // namespace fmt_kernels

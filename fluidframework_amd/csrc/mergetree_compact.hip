@@ -1,0 +1,17 @@
+// mergetree_compact.hip — merge-tree replay, compact tier (4 register rows: 256 leaves; 168 VGPRs,
+// 3 waves/SIMD). Plain batches start here; see mergetree.hip for the cascade.
+#include "mergetree_kernel.h"
+
+namespace fmt_kernels {
+
+constexpr int kMtWavesCompact = 4;  // 4 documents per workgroup, 3 waves/SIMD
+
+int mergeTreeProfileCompact(uint64_t* out, int n, bool reset) { return addTuProfile(out, n, reset); }
+
+hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
+                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream) {
+  return launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 3>(batch, out, docList, count, esc, numCUs,
+                                                                          stream);
+}
+
+}  // namespace fmt_kernels

@@ -64,6 +64,15 @@ struct SmallTier {
   using VR = V8;
 };
 
+// The compact tier: the small tier's layout with 4 register rows (256 leaves), so the replay kernel
+// fits 168 VGPRs and runs 3 waves per SIMD instead of 2 (more waves to cover the LDS and readlane
+// latency of each wave's dependent op chain). Plain batches replay in it first; a document that
+// outgrows it replays again in the small tier (runtime cascade).
+struct CompactTier : SmallTier {
+  static constexpr int kRows = 4;
+  using VR = V4;
+};
+
 struct LargeTier {
   static constexpr int kRows = 32;
   static constexpr int kCapChars = 131071;  // a leaf length (17 bits) can hold all of them
@@ -856,12 +865,14 @@ class Doc {
   }
 
   // ------------------------------------------------------------------ remove order (SnapshotV1)
-  // A flagged REMOVE that hits an already-removed leaf adds a later remove stamp to it
-  // (spliceIntoList, stamps.ts:144-158: remote stamps arrive in seq order, so they append). The
-  // summary's removedClientIds (snapshotV1.ts:235-250) need that order, which the remove-client
-  // mask W3 does not keep: each such stamp is appended to the document's HBM slab as (leaf id,
-  // client). Rare (concurrent overlapping removes), so lane 0 writes one entry at a time.
-  FMT_DEV void rmAppend(uint32_t id, int client) {
+  // A flagged REMOVE or obliterate that hits an already-removed leaf adds a later remove stamp to it
+  // (spliceIntoList, stamps.ts:144-158: remote stamps arrive in seq order, so they append), and an
+  // obliterate-on-insert can give a new leaf several. The summary's removedClientIds and
+  // movedSeqs / movedClientIds (snapshotV1.ts:235-264) need them in order, by kind, which the
+  // remove-client mask W3 does not keep: each such stamp is appended to the document's HBM slab as
+  // (leaf id, client, seq, kind). Rare (concurrent overlapping removes), so lane 0 writes one entry
+  // at a time.
+  FMT_DEV void rmAppend(uint32_t id, int client, int seq, uint32_t kind) {
     if (rmN >= rmCap) {
       fail(kCapFinal);
       return;
@@ -871,6 +882,8 @@ class Doc {
         fmt_mt_remove_order e;
         e.leaf = id;
         e.client = client;
+        e.seq = seq;
+        e.kind = kind;
         rmOut[rmN] = e;
       }
     }
@@ -881,13 +894,15 @@ class Doc {
   // once: the right parts of split multi-removed leaves inherit their entries (splitLeafSegment
   // copies the remove stamps, mergeTreeNodes.ts:389-435), in split order; then every leaf the
   // flagged REMOVE found already removed gets the op's stamp.
-  FMT_DEV void rmFlush(int client) {
+  FMT_DEV void rmFlush(int client, int seq, uint32_t kind) {
     for (int q = 0; q < rmPendN && status == FMT_OK; q++) {
       const uint32_t from = q == 0 ? rmPendFrom0 : rmPendFrom1, to = q == 0 ? rmPendTo0 : rmPendTo1;
       const uint32_t n0 = rmN;
       for (uint32_t k = 0; k < n0 && status == FMT_OK; k++) {
         if (uni(loadCoherent(&rmOut[k].leaf)) == from)
-          rmAppend(to, static_cast<int>(uni(loadCoherent(reinterpret_cast<const uint32_t*>(&rmOut[k].client)))));
+          rmAppend(to, static_cast<int>(uni(loadCoherent(reinterpret_cast<const uint32_t*>(&rmOut[k].client)))),
+                   static_cast<int>(uni(loadCoherent(reinterpret_cast<const uint32_t*>(&rmOut[k].seq)))),
+                   uni(loadCoherent(&rmOut[k].kind)));
       }
     }
     rmPendN = 0;
@@ -901,7 +916,7 @@ class Doc {
         FOR_LANES(l) {
           if (l == (j & 63)) LANE(todo) &= ~(1u << (j >> 6));
         }
-        rmAppend(fId(readField(j, 4)), client);
+        rmAppend(fId(readField(j, 4)), client, seq, kind);
       }
     }
   }
@@ -953,7 +968,7 @@ class Doc {
       if (obUsed != 0) obRefsMove(fId(w4), fId(rec.w[4]), offset, -offset);
     }
     if constexpr (Rm) {
-      if (rmN > 0 && __builtin_popcount(rec.w[3]) + __builtin_popcount(rec.w[5]) >= 2) {  // copied in rmFlush
+      if (rmN > 0 && static_cast<int32_t>(rec.w[2]) != kNotRemoved) {  // its entries, if any: copied in rmFlush
         if (rmPendN == 0) {
           rmPendFrom0 = fId(w4);
           rmPendTo0 = fId(rec.w[4]);
@@ -1109,7 +1124,7 @@ class Doc {
     if (status != FMT_OK) return -1;
     stamp(kPfInsert);
     if constexpr (Ob) {
-      if (obStartN > 0) obliterateOnInsert(insIdx, refSeq, client);
+      if (obStartN > 0) obliterateOnInsert(insIdx, refSeq, client, Rm && (op.flags & FMT_MT_F_RMORDER) != 0);
     }
     lruForLeaf(insIdx, static_cast<int>(fBlk(readField(insIdx, 0))), seq);
     stamp(kPfLru);
@@ -1254,7 +1269,7 @@ class Doc {
   // blockInsert's obliterate branch (mergeTree.ts:1642-1746) for the new leaf k: every overlapping
   // obliterate the inserter had not seen (seq > refSeq); when one is from another client and the
   // newest is not the inserter's own, the leaf starts out removed by those other clients' ones.
-  FMT_DEV void obliterateOnInsert(int k, int refSeq, int client) {
+  FMT_DEV void obliterateOnInsert(int k, int refSeq, int client, bool record) {
     int minSeqOther = kNotRemoved, newestSeq = -1, newestClient = -1;
     uint64_t mask = 0;
     bool any = false;
@@ -1280,6 +1295,28 @@ class Doc {
       writeField(k, 2, static_cast<uint32_t>(minSeqOther));
       writeField(k, 3, static_cast<uint32_t>(mask));
       if constexpr (kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
+      // SnapshotV1: the leaf's stamps are overlappingAcked sorted by seq (:1715-1725); the first is
+      // rm_seq, every other one is a remove-order entry (the host sorts a leaf's entries by seq)
+      if constexpr (Rm) {
+        if (record) {
+          const uint32_t id = fId(readField(k, 4));
+          bool firstSkipped = false;
+          for (int i = 0; i < obStartN && status == FMT_OK; i++) {
+            const int slot = uni(static_cast<int>(s->obStart[i]));
+            const int si = leafOf(uni(s->ob[slot].startId));
+            if (!(si >= 0 && si <= k)) break;
+            const int ei = leafOf(uni(s->ob[slot].endId));
+            if (!(ei >= 0 && ei >= k)) continue;
+            const int oseq = uni(s->ob[slot].seq), ocl = uni(s->ob[slot].client);
+            if (oseq <= refSeq || ocl == client) continue;
+            if (!firstSkipped && oseq == minSeqOther) {
+              firstSkipped = true;
+              continue;
+            }
+            rmAppend(id, ocl, oseq, FMT_MT_RM_SLICE);
+          }
+        }
+      }
     }
   }
 
@@ -1393,7 +1430,7 @@ class Doc {
       if (!obAdd(fId(readField(sLeaf, 4)), sOff, fId(readField(eLeaf, 4)), eOff, seq, client)) return false;
     }
     FOR_LANES(l) { LANE(delta) = 0u; }
-    if (Rm && op.type == FMT_MT_REMOVE && (op.flags & FMT_MT_F_RMORDER) != 0) {  // recorded in rmFlush
+    if (Rm && (op.type == FMT_MT_REMOVE || obliterate) && (op.flags & FMT_MT_F_RMORDER) != 0) {  // recorded in rmFlush
       FOR_LANES(l) {
         uint32_t m = 0;
         FOR_ROWS(r, 0, nr) {
@@ -1956,7 +1993,8 @@ class Doc {
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
       else applyOp(op, text);
       if constexpr (Rm) {
-        if (rmPendN > 0 || rmHitsSet) rmFlush(op.client);
+        if (rmPendN > 0 || rmHitsSet)
+          rmFlush(op.client, op.seq, op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE);
       }
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       // zamboni once inside the op (mergeTree.ts:1510-1516, 2074-2080, 2376-2382), then, after the

@@ -80,6 +80,7 @@ struct fmt_ctx {
   DevBuf<uint16_t> mtChars;
   DevBuf<fmt_mt_propset> mtProps;
   DevBuf<uint32_t> mtEsc;                    // small-tier overflow list: [0] = count, then doc ids
+  DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (plain batches), same layout
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
   DevBuf<uint16_t> mtBigChars;
   DevBuf<fmt_mt_propset> mtBigProps;
@@ -200,6 +201,7 @@ void fmt_close(fmt_ctx* c) {
   c->mtChars.release();
   c->mtProps.release();
   c->mtEsc.release();
+  c->mtEsc2.release();
   c->mtBigLeaves.release();
   c->mtBigChars.release();
   c->mtBigProps.release();
@@ -503,6 +505,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, c->mtChars.reserve(static_cast<size_t>(n) * caps.chars));
   FMT_HIP(c, c->mtProps.reserve(static_cast<size_t>(n) * caps.props));
   FMT_HIP(c, c->mtEsc.reserve(n + 1ull));
+  FMT_HIP(c, c->mtEsc2.reserve(n + 1ull));
   c->mtBigSlot.assign(n, -1);
   // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
   // any; a document that needs more reports FMT_E_CAPACITY.
@@ -522,8 +525,6 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   // Remove-order slabs: kRmPerOp entries per flagged remove plus kRmPerDoc per document that has
   // any (split copies included); a document that needs more reports FMT_E_CAPACITY.
   c->mtHasRmOrder = rmOrderOps > 0;
-  if (c->mtHasRmOrder && obliterates)
-    return setErr(c, FMT_E_UNSUPPORTED, "remove order (FMT_MT_F_RMORDER) in a batch with obliterates");
   if (c->mtHasRmOrder) {
     constexpr uint64_t kRmPerOp = 64, kRmPerDoc = 256;
     c->mtRmOffsHost.assign(n + 1ull, 0);
@@ -689,11 +690,13 @@ int fmt_mt_run(fmt_ctx* c) {
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
+  FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   const bool hasHuge = !c->huge.empty();
   if (!hasHuge || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
-                                            c->mtEsc.p, c->numCUs, c->stream, c->mtObliterate, c->mtHasRmOrder));
+                                            c->mtEsc.p, c->mtEsc2.p, c->numCUs, c->stream, c->mtObliterate,
+                                            c->mtHasRmOrder));
   if (hasHuge)
     FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p,
                                            static_cast<uint32_t>(c->huge.size()), c->stream));
@@ -730,7 +733,8 @@ int fmt_mt_run(fmt_ctx* c) {
   c->stats.bytes_read = c->mtNOps * sizeof(fmt_mt_op) + (c->mtInsertChars + c->mtInitChars) * 2 +
                         (c->mtDocs + 1ull) * sizeof(uint64_t);
   c->stats.bytes_written = static_cast<uint64_t>(c->mtDocs) * sizeof(fmt_mt_doc_result);
-  c->stats.launches = nEsc > 0 ? 2 : 1;
+  // compact + small tier (plain batches) or small tier alone, then the large tier when it ran
+  c->stats.launches = (!c->mtObliterate && !c->mtHasRmOrder ? 2 : 1) + (nEsc > 0 ? 1 : 0);
   return FMT_OK;
 }
 

@@ -37,6 +37,7 @@ FMT_DEV int waveLane() { return static_cast<int>(__lane_id()); }
 // Opaque register copy: stops LLVM from folding a dynamic vector element access back into a
 // variable-index load from the enclosing object's stack slot (which would put it in scratch).
 FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }
+FMT_DEV void launder(V4& v) { asm volatile("" : "+v"(v)); }
 
 // Large-tier rows: a plain per-lane array indexed at run time (private memory), so the row loops
 // stay rolled and the 32-row engine compiles in seconds.
@@ -217,7 +218,8 @@ using VKV = VecN<FMT_MT_PROPS_MAX>;
 inline int uni(int x) { return x; }
 inline uint32_t uni(uint32_t x) { return x; }
 
-inline void launder(V8&) {}
+template <class T>
+inline void launder(T&) {}
 
 inline uint32_t loadCoherent(const uint16_t* p) { return *p; }
 inline uint32_t loadCoherent(const uint32_t* p) { return *p; }

@@ -342,7 +342,8 @@ class MergeTreeStreamBuilder {
 	 * The packed batch: the typed arrays the addon hands to fmt_mt_load. With {catchup: true} the
 	 * ops of messages a legacy summary keeps with regenerated contents get FMT_MT_F_CATCHUP: seq
 	 * above the document's final minSeq and refSeq != seq - 1 (sequence.ts:949-1018). With
-	 * {removeOrder: true} the REMOVE ops above the final minSeq get FMT_MT_F_RMORDER, which the
+	 * {removeOrder: true} the REMOVE and obliterate ops above the final minSeq (and, in documents
+	 * holding obliterates, the INSERTs: obliterate-on-insert) get FMT_MT_F_RMORDER, which the
 	 * SnapshotV1 summary needs (summarizeV1).
 	 */
 	finish(options) {
@@ -359,8 +360,12 @@ class MergeTreeStreamBuilder {
 				const b = a + d.nOps;
 				if (b > a) {
 					const finalMsn = v.getInt32((b - 1) * MT_OP_BYTES + 8, true);
+					const isOb = (t) => t === MT_OBLITERATE || t === MT_OBLITERATE_SIDED;
+					let anyOb = false;
+					for (let o = a * MT_OP_BYTES; o < b * MT_OP_BYTES; o += MT_OP_BYTES) anyOb = anyOb || isOb(v.getUint8(o + 27));
 					for (let o = a * MT_OP_BYTES; o < b * MT_OP_BYTES; o += MT_OP_BYTES) {
-						if (v.getInt32(o, true) > finalMsn && v.getUint8(o + 27) === MT_REMOVE)
+						const t = v.getUint8(o + 27);
+						if (v.getInt32(o, true) > finalMsn && (t === MT_REMOVE || isOb(t) || (anyOb && t === MT_INSERT)))
 							v.setUint32(o + 28, v.getUint32(o + 28, true) | FMT_MT_F_RMORDER, true);
 					}
 				}
@@ -631,24 +636,38 @@ class MergeTreeReplay {
 		return out;
 	}
 	/**
-	 * The ordered remove-stamp clients of every removed leaf: the first remover is the client of the
-	 * op whose seq is the leaf's removedSeq, later ones come from the kernel's remove-order slab
-	 * (ops flagged by finish({removeOrder: true})). {leaf index: [short client ids]}.
+	 * The remove stamps of every removed leaf in stamp order: the first is the op whose seq is the
+	 * leaf's removedSeq (its client; kind 0 for a REMOVE, 1 for an obliterate), later ones come from
+	 * the kernel's remove-order slab (ops flagged by finish({removeOrder: true})), sorted by seq.
+	 * {leaf index: [[short client id, seq, kind], ...]}.
 	 */
 	removers(doc, segs) {
 		const h = this.header(doc);
-		const seqClient = new Map();
+		const first = new Map();
 		const ops = new DataView(this.batch.ops.buffer, this.batch.ops.byteOffset, this.batch.ops.byteLength);
-		for (let i = Number(this.batch.docOpOffsets[doc]); i < Number(this.batch.docOpOffsets[doc + 1]); i++)
-			seqClient.set(ops.getInt32(i * MT_OP_BYTES, true), ops.getUint8(i * MT_OP_BYTES + 26));
+		for (let i = Number(this.batch.docOpOffsets[doc]); i < Number(this.batch.docOpOffsets[doc + 1]); i++) {
+			const seq = ops.getInt32(i * MT_OP_BYTES, true), t = ops.getUint8(i * MT_OP_BYTES + 27);
+			if ((t === MT_REMOVE || t === MT_OBLITERATE || t === MT_OBLITERATE_SIDED) && !first.has(seq))
+				first.set(seq, [ops.getUint8(i * MT_OP_BYTES + 26), t === MT_REMOVE ? 0 : 1]);
+		}
 		const out = {};
 		segs.forEach((s, i) => {
-			if (s.removedSeq !== undefined && seqClient.has(s.removedSeq)) out[i] = [seqClient.get(s.removedSeq)];
+			if (s.removedSeq !== undefined && first.has(s.removedSeq)) {
+				const f = first.get(s.removedSeq);
+				out[i] = [[f[0], s.removedSeq, f[1]]];
+			}
 		});
+		const later = {};
 		const dv = new DataView(native().fetchRemoveOrder(this.engine.ctx, doc, h.nRmOrder));
-		for (let k = 0; k < h.nRmOrder; k++) {
-			const leaf = dv.getUint32(8 * k, true), client = dv.getInt32(8 * k + 4, true);
-			if (leaf !== 0xffffffff && out[leaf]) out[leaf].push(client);
+		for (let k = 0; k < h.nRmOrder; k++) { // fmt_mt_remove_order: leaf, client, seq, kind (16 B)
+			const leaf = dv.getUint32(16 * k, true);
+			if (leaf !== 0xffffffff && out[leaf])
+				(later[leaf] = later[leaf] || []).push([dv.getInt32(16 * k + 4, true), dv.getInt32(16 * k + 8, true),
+					dv.getUint32(16 * k + 12, true)]);
+		}
+		for (const leaf of Object.keys(later)) {
+			const es = later[leaf].map((e, k) => [e, k]).sort((x, y) => x[0][1] - y[0][1] || x[1] - y[1]);
+			for (const e of es) out[leaf].push(e[0]);
 		}
 		return out;
 	}

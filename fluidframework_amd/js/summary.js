@@ -143,7 +143,8 @@ function legacySummary(segs, minSeq, keys, values, chunkSize) {
  * SnapshotV1 (newMergeTreeSnapshotFormat; snapshotV1.ts:90-265): every segment above minSeq with its
  * merge info, the rest merged as in extractSync, chunked by SnapshotV1.chunkSize = 10000 lengths.
  * @param segs - leaves in order: {insertSeq, insertClient, removedSeq (or NOT_REMOVED), text, kv}
- * @param removers - {leaf index: [short client ids of its remove stamps, in stamp order]}
+ * @param removers - {leaf index: [[short client id, seq, kind], ...] of its remove stamps in stamp
+ *   order; kind 0 = setRemove, 1 = sliceRemove (obliterate)}
  * @returns {header, bodies} - the blobs "header", "body_0", "body_1", ...
  */
 function v1Summary(segs, minSeq, curSeq, keys, values, clientNames, removers, chunkSize) {
@@ -174,11 +175,19 @@ function v1Summary(segs, minSeq, curSeq, keys, values, clientNames, removers, ch
 			raw.client = clientNames[s.insertClient];
 		}
 		if (removed) {
-			const ids = removers[i];
-			if (!ids || ids.length === 0) throw new Error(`leaf ${i}: remove order unknown`);
-			raw.removedSeq = s.removedSeq;
-			raw.removedClient = clientNames[ids[0]];
-			raw.removedClientIds = ids.map((c) => clientNames[c]);
+			const stamps = removers[i];
+			if (!stamps || stamps.length === 0) throw new Error(`leaf ${i}: remove order unknown`);
+			const sets = stamps.filter((x) => x[2] === 0), moves = stamps.filter((x) => x[2] === 1);
+			if (sets.length > 0) { // snapshotV1.ts:235-250
+				raw.removedSeq = sets[0][1];
+				raw.removedClient = clientNames[sets[0][0]];
+				raw.removedClientIds = sets.map((x) => clientNames[x[0]]);
+			}
+			if (moves.length > 0) { // sliceRemove stamps, "moves" in this format (snapshotV1.ts:252-264)
+				raw.movedSeq = moves[0][1];
+				raw.movedSeqs = moves.map((x) => x[1]);
+				raw.movedClientIds = moves.map((x) => clientNames[x[0]]);
+			}
 		}
 		out.push([raw, s.text.length]);
 	});

@@ -50,8 +50,9 @@ DOC_RESULT_DTYPE = np.dtype(
 )
 assert DOC_RESULT_DTYPE.itemsize == 48
 
-# fmt_mt_remove_order: a later remove stamp of a leaf (leaf index, client); FMT_MT_LEAF_GONE leaf
-RM_ORDER_DTYPE = np.dtype([("leaf", "<u4"), ("client", "<i4")])
+# fmt_mt_remove_order: a later remove stamp of a leaf (leaf index, client, seq, kind 0 = setRemove /
+# 1 = sliceRemove); FMT_MT_LEAF_GONE leaf
+RM_ORDER_DTYPE = np.dtype([("leaf", "<u4"), ("client", "<i4"), ("seq", "<i4"), ("kind", "<u4")])
 LEAF_GONE = 0xFFFFFFFF
 
 CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("type", "<u4")])

@@ -448,16 +448,21 @@ def flag_catchup(ops: np.ndarray, offs: np.ndarray) -> None:
 
 
 def flag_remove_order(ops: np.ndarray, offs: np.ndarray) -> None:
-    """Set FMT_MT_F_RMORDER on the REMOVE ops above the document's final minSeq: the only ones that
-    can add a later remove stamp to a leaf that a SnapshotV1 summary lists with merge info
-    (snapshotV1.ts:207-265 skips leaves removed at/below minSeq)."""
+    """Set FMT_MT_F_RMORDER on the REMOVE, obliterate and INSERT ops above the document's final
+    minSeq: the only ones that can add a later remove stamp to a leaf that a SnapshotV1 summary lists
+    with merge info (snapshotV1.ts:207-265 skips leaves removed at/below minSeq); an INSERT only
+    through obliterate-on-insert (mergeTree.ts:1642-1746), so inserts are flagged in documents that
+    hold obliterates."""
     for d in range(len(offs) - 1):
         a, b = int(offs[d]), int(offs[d + 1])
         if a == b:
             continue
         seg = ops[a:b]
         final_msn = int(seg["min_seq"][-1])
-        sel = (seg["seq"] > final_msn) & (seg["type"] == MT_REMOVE)
+        t = seg["type"]
+        ob = (t == MT_OBLITERATE) | (t == MT_OBLITERATE_SIDED)
+        kinds = (t == MT_REMOVE) | ob | ((t == MT_INSERT) & bool(ob.any()))
+        sel = (seg["seq"] > final_msn) & kinds
         seg["flags"][sel] |= MT_F_RMORDER
 
 

@@ -14,7 +14,8 @@ from __future__ import annotations
 
 import json
 
-from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_LEAF_MARKER, MT_OBLITERATE, MT_REMOVE,
+from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_LEAF_MARKER, MT_OBLITERATE,
+                      MT_OBLITERATE_SIDED, MT_REMOVE,
                       is_array_index_key, js_json, js_key_order, js_quote, marker_ref_type)
 
 NOT_REMOVED = 0x7FFFFFFF
@@ -162,18 +163,28 @@ V1_CHUNK_SIZE = 10000  # SnapshotV1.chunkSize (snapshotV1.ts:44)
 
 
 def removers_from_engine(leaves, n_leaves, rm_order, doc_ops):
-    """Ordered remove-stamp clients per removed leaf: the first remover is the client of the op whose
-    seq is the leaf's rm_seq; later ones are the kernel's remove-order entries (seq order)."""
-    seq_client = {int(s): int(c) for s, c in zip(doc_ops["seq"], doc_ops["client"])}
+    """Remove stamps per removed leaf, in stamp order: {leaf: [(client, seq, kind), ...]}, kind 0 =
+    setRemove, 1 = sliceRemove (stamps.ts RemoveOperationStamp). The first stamp is the op whose seq
+    is the leaf's rm_seq (its client, and its type: REMOVE or an obliterate); later ones are the
+    kernel's remove-order entries, which carry their own seq and kind (stamps.ts:144-158 keeps remote
+    stamps in seq order, so the entries of one leaf are sorted by seq)."""
+    first = {}
+    for s, c, t in zip(doc_ops["seq"], doc_ops["client"], doc_ops["type"]):
+        if int(t) in (MT_REMOVE, MT_OBLITERATE, MT_OBLITERATE_SIDED):
+            first.setdefault(int(s), (int(c), 0 if int(t) == MT_REMOVE else 1))
     out = {}
     for i in range(n_leaves):
         rm = int(leaves[i]["rm_seq"])
-        if rm != NOT_REMOVED and rm in seq_client:
-            out[i] = [seq_client[rm]]
+        if rm != NOT_REMOVED and rm in first:
+            c, k = first[rm]
+            out[i] = [(c, rm, k)]
+    later = {}
     for e in rm_order:
         j = int(e["leaf"])
         if j != 0xFFFFFFFF and j in out:
-            out[j].append(int(e["client"]))
+            later.setdefault(j, []).append((int(e["client"]), int(e["seq"]), int(e["kind"])))
+    for j, es in later.items():
+        out[j].extend(sorted(es, key=lambda x: x[1]))
     return out
 
 
@@ -221,11 +232,17 @@ def v1_segments(header, leaves, chars, propsets, keys, values, client_names, rem
         if ins > min_seq:
             raw += f',"seq":{ins},"client":' + _q(client_names[int(L["ins_client"])])
         if removed:
-            ids = removers.get(i)
-            if not ids:
+            stamps = removers.get(i)
+            if not stamps:
                 raise ValueError(f"leaf {i}: remove order unknown (flag removes with FMT_MT_F_RMORDER)")
-            raw += (f',"removedSeq":{rm},"removedClient":' + _q(client_names[ids[0]])
-                    + ',"removedClientIds":[' + ",".join(_q(client_names[c]) for c in ids) + "]")
+            sets = [st for st in stamps if st[2] == 0]
+            moves = [st for st in stamps if st[2] == 1]
+            if sets:  # setRemove stamps (snapshotV1.ts:235-250)
+                raw += (f',"removedSeq":{sets[0][1]},"removedClient":' + _q(client_names[sets[0][0]])
+                        + ',"removedClientIds":[' + ",".join(_q(client_names[st[0]]) for st in sets) + "]")
+            if moves:  # sliceRemove stamps: "moves" in this format (snapshotV1.ts:252-264)
+                raw += (f',"movedSeq":{moves[0][1]},"movedSeqs":[' + ",".join(str(st[1]) for st in moves)
+                        + '],"movedClientIds":[' + ",".join(_q(client_names[st[0]]) for st in moves) + "]")
         out.append((raw + "}", n))
     flush()
     return out

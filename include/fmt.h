@@ -83,11 +83,13 @@ extern "C" {
  * The host sets it on the ops of messages that stay in the legacy summary's catch-up window
  * (seq > final minSeq) and need transformation (refSeq != seq - 1, sequence.ts:971-1006). */
 #define FMT_MT_F_CATCHUP 2u
-/* Record the remove order (SnapshotV1 merge info, merge-tree/src/snapshotV1.ts:235-250): for every
- * leaf this REMOVE hits that is already removed, append (leaf, client) to the document's remove-order
- * slab, so the summary can list removedClientIds in stamp order (stamps.ts:144-158). The host sets it
- * on the REMOVE ops with seq > the document's final minSeq (only leaves removed above minSeq carry
- * merge info). The first remover is the client of the op whose seq is the leaf's rm_seq. */
+/* Record the remove order (SnapshotV1 merge info, merge-tree/src/snapshotV1.ts:207-265): for every
+ * leaf this REMOVE or obliterate hits that is already removed, append (leaf, client, seq, kind) to
+ * the document's remove-order slab, so the summary can list removedClientIds and movedSeqs /
+ * movedClientIds in stamp order (stamps.ts:144-158); on an INSERT, the second and later stamps an
+ * obliterate-on-insert gives the new leaf (mergeTree.ts:1642-1746). The host sets it on the REMOVE,
+ * obliterate and INSERT ops with seq > the document's final minSeq (only leaves removed above minSeq
+ * carry merge info). The first stamp is the op whose seq is the leaf's rm_seq. */
 #define FMT_MT_F_RMORDER 4u
 /* FMT_MT_OBLITERATE_SIDED (mergeTreeEnableSidedObliterate, client.ts:680-700): pos1/pos2 hold
  * start.pos / end.pos of the InteriorSequencePlaces and these bits their sides (set = Side.Before,
@@ -218,13 +220,18 @@ typedef struct fmt_mt_catchup_range {
   uint32_t type; /* FMT_MT_INSERT / FMT_MT_REMOVE / FMT_MT_ANNOTATE */
 } fmt_mt_catchup_range;
 
-/* One later remover of a leaf (the second, third, ... remove stamp, in seq order across the slab):
- * `leaf` is the index in the document's final leaf list, or FMT_MT_LEAF_GONE when that leaf was
- * dropped by zamboni before the end. A split leaf's entries are copied to its right part. */
+/* One later remove stamp of a leaf (the second, third, ... of its stamps.ts remove list; the first
+ * is the leaf's rm_seq): `leaf` is the index in the document's final leaf list, or FMT_MT_LEAF_GONE
+ * when that leaf was dropped by zamboni before the end. A split leaf's entries are copied to its
+ * right part. The entries of one leaf sorted by seq follow the stamp order. 16 bytes. */
 #define FMT_MT_LEAF_GONE 0xffffffffu
+#define FMT_MT_RM_SET 0u   /* "setRemove": a REMOVE op (markRangeRemoved) */
+#define FMT_MT_RM_SLICE 1u /* "sliceRemove": an obliterate, incl. obliterate-on-insert (mergeTree.ts:2270) */
 typedef struct fmt_mt_remove_order {
   uint32_t leaf;
   int32_t client; /* short client id of the remove stamp */
+  int32_t seq;    /* the stamp's seq (SnapshotV1 movedSeqs) */
+  uint32_t kind;  /* FMT_MT_RM_SET / FMT_MT_RM_SLICE */
 } fmt_mt_remove_order;
 
 /* A document-local prop set: up to FMT_MT_PROPS_MAX (key_id, value_id) pairs in JS insertion order. */

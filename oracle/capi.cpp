@@ -298,8 +298,9 @@ int orc_mt_replay_timed(const fmt_mt_batch* b, uint32_t d, uint64_t maxOps, doub
 void orc_set_index(int on) { g_indexed = on; }
 
 // ---------------------------------------------------------------- SharedMap
-// Every remove stamp of every final leaf of document d, in stamp order: (leaf index, client) pairs
-// into out[2 * k], at most cap pairs. Returns the number of pairs, or a negative FMT_E_* code.
+// Every remove stamp of every final leaf of document d, in stamp order: (leaf index, client, seq,
+// kind) quads into out[4 * k] (kind 0 = setRemove, 1 = sliceRemove), at most cap quads. Returns the
+// number of quads, or a negative FMT_E_* code.
 int orc_mt_removers(const fmt_mt_batch* b, uint32_t d, int32_t* out, uint32_t cap) {
   MergeTree mt;
   startDoc(mt, b, d);
@@ -314,8 +315,10 @@ int orc_mt_removers(const fmt_mt_batch* b, uint32_t d, int32_t* out, uint32_t ca
   for (size_t i = 0; i < segs.size(); i++)
     for (const auto& r : segs[i]->removes) {
       if (k < cap) {
-        out[2 * k] = static_cast<int32_t>(i);
-        out[2 * k + 1] = r.client;
+        out[4 * k] = static_cast<int32_t>(i);
+        out[4 * k + 1] = r.client;
+        out[4 * k + 2] = r.seq;
+        out[4 * k + 3] = r.kind;
       }
       k++;
     }

@@ -432,6 +432,7 @@ std::pair<Seg*, int> MergeTree::getContainingSegment(int pos, const Perspective&
 // are the places' Before edges ({p, After} is the edge at p + 1, :2090-2091).
 void MergeTree::obliterateRange(int start, bool startBefore, int endPlace, bool endBefore, const Perspective& p,
                                 Stamp stamp) {
+  stamp.kind = 1;  // sliceRemove (mergeTree.ts:2270)
   const int startPos = startBefore ? start : start + 1, endPos = endBefore ? endPlace : endPlace + 1;
   const int end = endPlace + 1;  // nodeMap(start.pos, end.pos + 1): the end reference's segment included
   ensureIntervalBoundary(startPos, p);

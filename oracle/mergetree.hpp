@@ -42,9 +42,12 @@ struct DataError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// A remove stamp's kind (stamps.ts RemoveOperationStamp.type): 0 = "setRemove" (markRangeRemoved),
+// 1 = "sliceRemove" (obliterate, incl. obliterate-on-insert). Insert stamps leave it 0.
 struct Stamp {
   int seq;
   int client;
+  int kind = 0;
 };
 
 // stamps.ts:101-113 (the oracle never holds two unassigned stamps, so localSeq never decides).

@@ -238,10 +238,11 @@ def xsadd_mixed(seed, kinds):
 
 
 def mt_removers(batch, doc: int, cap: int = 1 << 16):
-    """Every remove stamp of every final leaf of `doc`, in stamp order: {leaf index: [client, ...]}."""
+    """Every remove stamp of every final leaf of `doc`, in stamp order:
+    {leaf index: [(client, seq, kind), ...]} with kind 0 = setRemove, 1 = sliceRemove (obliterate)."""
     from fluidframework_amd.native import batch_struct
 
-    out = np.zeros(2 * cap, dtype=np.int32)
+    out = np.zeros(4 * cap, dtype=np.int32)
     b, keep = batch_struct(batch)
     n = lib().orc_mt_removers(ctypes.byref(b), doc, _ptr(out), cap)
     del keep
@@ -249,5 +250,6 @@ def mt_removers(batch, doc: int, cap: int = 1 << 16):
         raise OracleError(f"remove-order replay failed ({n})")
     res = {}
     for k in range(min(n, cap)):
-        res.setdefault(int(out[2 * k]), []).append(int(out[2 * k + 1]))
+        q = out[4 * k : 4 * k + 4]
+        res.setdefault(int(q[0]), []).append((int(q[1]), int(q[2]), int(q[3])))
     return res

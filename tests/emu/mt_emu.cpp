@@ -61,9 +61,13 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
 extern "C" {
 
 // large = 0: the small tier (registers + LDS text); 1: the large tier (HBM text) that the runtime
-// replays overflowing documents in.
+// replays overflowing documents in; 2: the compact tier (4 register rows) plain batches start in.
 int emu_mt_capacity(int large, uint32_t* leaves, uint32_t* chars, uint32_t* props) {
-  if (large) {
+  if (large == 2) {
+    *leaves = fmt_mt::Doc<false, fmt_mt::CompactTier>::kCapLeaves;
+    *chars = fmt_mt::CompactTier::kCapChars;
+    *props = fmt_mt::CompactTier::kPropCap;
+  } else if (large) {
     *leaves = fmt_mt::Doc<false, fmt_mt::LargeTier>::kCapLeaves;
     *chars = fmt_mt::LargeTier::kCapChars;
     *props = fmt_mt::LargeTier::kPropCap;
@@ -87,12 +91,15 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   using G = fmt_mt::LargeTier;
   bool rm = false;
   for (uint64_t i = 0; i < b->n_ops && !rm; i++) rm = (b->ops[i].flags & FMT_MT_F_RMORDER) != 0;
-  if (rm && ob) return FMT_E_UNSUPPORTED;
-  if (large) {
+  if (large == 2 && !ob && !rm) return replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup,
+                                                                             capCatchup, rmOrder, capRm);
+  if (large == 1) {
+    if (ob && rm) return replayAll<true, G, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
     if (ob) return replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
     if (rm) return replayAll<false, G, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
     return replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   }
+  if (ob && rm) return replayAll<true, S, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (ob) return replayAll<true, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (rm) return replayAll<false, S, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);

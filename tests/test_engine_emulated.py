@@ -89,6 +89,44 @@ def test_emulated_engine_fills_every_row_to_capacity(orc):
         assert not diffs, f"doc {d}: {diffs[:5]}"
 
 
+# ---- compact tier (4 register rows: plain batches start in it, on the GPU) --------------------------
+
+@pytest.mark.parametrize("n_clients", [8, 3])
+def test_compact_tier_matches_oracle_on_conflict_farm(orc, n_clients):
+    """The 4-row compact tier is the same engine source: bit-exact vs the oracle on T1-shaped
+    documents; a document it cannot hold reports FMT_E_CAPACITY (the runtime then replays it in the
+    small tier)."""
+    batch = workloads.conflict_farm(40, n_clients=n_clients, ops_per_doc=1500, seed=17)
+    cl, cc, cp = emu_caps(large=2)
+    assert cl == 256
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=4096, cap_chars=cc, cap_props=1024)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch, large=2)
+    fit = 0
+    for d in range(batch.n_docs):
+        if hdr[d]["status"] == -3:
+            continue
+        fit += 1
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+    assert fit >= 30
+
+
+def test_compact_tier_fills_every_row_to_capacity(orc):
+    cl, cc, cp = emu_caps(large=2)
+    batch = _no_zamboni_batch([60, 130, 200, 230, 250, 260, 300])
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=4, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch, large=2)
+    assert oh["n_leaves"].max() > cl and ((oh["n_leaves"] > 192) & (oh["n_leaves"] <= cl)).any()
+    for d in range(batch.n_docs):
+        if oh[d]["n_leaves"] > cl:
+            assert hdr[d]["status"] == -3, f"doc {d}: expected FMT_E_CAPACITY"
+            continue
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
 # ---- large tier (documents that overflow the small tier replay again in it, on the GPU) ----------
 
 def test_large_tier_matches_oracle_on_fixtures(orc, fixtures_prefix):

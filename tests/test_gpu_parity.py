@@ -291,7 +291,7 @@ def test_mt_large_documents_escalate_to_large_tier(orc, engine):
     hdrs = _check_against_oracle(orc, engine, batch)
     assert (hdrs["status"] == 0).all()
     assert ((hdrs["n_leaves"] > 512) | (hdrs["n_chars"] > 2048)).sum() >= 12
-    assert engine.stats().launches == 2
+    assert engine.stats().launches == 3  # compact tier, small tier over its overflow, large tier
 
 
 @pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"])
@@ -469,13 +469,23 @@ def test_mt_v1_remove_order_on_conflict_farm(orc, engine):
     assert _removers_check(orc, engine, batch, None) > 0
 
 
+def test_mt_v1_remove_order_with_obliterates(orc, engine):
+    """SnapshotV1 merge info of obliterated segments (movedSeq/movedSeqs/movedClientIds) on the
+    reference's obliterate fixture messages: the Ob x Rm engine variant's stamps == the oracle's, and
+    the V1 summaries are byte-identical (parity unpinned beyond the oracle, see test_snapshot_v1)."""
+    from test_snapshot_v1 import obliterate_v1_batch
+
+    batch = obliterate_v1_batch()
+    assert _removers_check(orc, engine, batch, lambda d: batch.clients[d]) > 0
+
+
 def test_mt_many_writers_escalate_to_large_tier(orc, engine):
     """Documents with up to 63 writers (T3's 64 clients incl. the observer) mixed with ordinary ones:
     the small tier's 31-writer remove-client set overflows and the large tier replays them."""
     many = workloads.conflict_farm(16, n_clients=63, ops_per_doc=1500, seed=13)
     hdrs = _check_against_oracle(orc, engine, many)
     assert (hdrs["status"] == 0).all()
-    assert engine.stats().launches == 2
+    assert engine.stats().launches == 3  # compact tier, small tier over its overflow, large tier
 
 
 @pytest.mark.parametrize("key_pool", [20, 5000])

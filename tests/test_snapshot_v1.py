@@ -167,3 +167,80 @@ def test_engine_remove_order_matches_oracle_on_conflict_farm():
                 assert got.get(i) == want.get(i), (d, i)
                 multi += len(want[i]) > 2
     assert multi > 0  # three or more removers: the order the remove-client mask cannot give
+
+
+def obliterate_v1_batch(stride=8):
+    """The reference's obliterate conflict-farm fixtures (2.3.0), one document per 8th text
+    checkpoint (the fixtures' last checkpoint included), flagged for SnapshotV1 merge info."""
+    from dataclasses import replace
+
+    from golden_data import prefix_batch, replay_fixtures
+
+    batch, _ = prefix_batch(list(replay_fixtures("replay_obliterate_2.3.0.npz")))
+    keep = [d for d in range(batch.n_docs) if d % stride == stride - 1]
+    offs, ops, init = [0], [], []
+    for d in keep:
+        a, b = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+        ops.append(batch.ops[a:b])
+        offs.append(offs[-1] + (b - a))
+        init.append(batch.doc_init[d])
+    sub = replace(batch, ops=np.concatenate(ops).copy(), doc_op_offsets=np.asarray(offs, dtype=np.uint64),
+                  doc_init=np.asarray(init, dtype=np.uint32), clients=[[f"client-{i}" for i in range(64)]] * len(keep))
+    flag_remove_order(sub.ops, sub.doc_op_offsets)
+    return sub
+
+
+def test_engine_remove_order_with_obliterates_matches_oracle():
+    """SnapshotV1 merge info of obliterated segments (movedSeq / movedSeqs / movedClientIds,
+    snapshotV1.ts:252-264) beside removedClientIds: the engine's stamps (first from rm_seq, later
+    ones from the remove-order slab with their seq and kind) == the oracle's stamp lists, and the V1
+    summaries are byte-identical. Parity unpinned: no reference fixture holds a V1 summary of a
+    collaborative obliterate document; the oracle restates mergeTree.ts's stamp bookkeeping."""
+    import oracle as orc
+
+    batch = obliterate_v1_batch()
+    eh, el, ec, ep, erm = emu_replay(batch, cap_rm=1 << 14)
+    assert (eh["status"] == 0).all()
+    moved = multi_moved = both = 0
+    for d in range(batch.n_docs):
+        want = orc.mt_removers(batch, d)
+        got = summary.removers_from_engine(el[d], int(eh[d]["n_leaves"]), erm[d][: eh[d]["n_rm_order"]],
+                                           _doc_ops(batch, d))
+        ms = int(eh[d]["min_seq"])
+        for i in range(int(eh[d]["n_leaves"])):
+            rm = int(el[d][i]["rm_seq"])
+            if rm != summary.NOT_REMOVED and rm > ms:
+                assert got.get(i) == want.get(i), (d, i, got.get(i), want.get(i))
+                kinds = [k for _, _, k in want[i]]
+                moved += 1 in kinds
+                multi_moved += kinds.count(1) > 1
+                both += 0 in kinds and 1 in kinds
+        v_en = summary.v1_summary(eh[d], el[d], ec[d], ep[d], batch.keys, batch.values, batch.clients[d], got)
+        v_or = summary.v1_summary(eh[d], el[d], ec[d], ep[d], batch.keys, batch.values, batch.clients[d], want)
+        assert v_en == v_or, d
+    assert moved > 0 and multi_moved > 0 and both > 0, (moved, multi_moved, both)
+
+
+def test_v1_moved_info_json_shape():
+    """A removed-and-obliterated segment carries removedSeq/removedClient/removedClientIds, then
+    movedSeq/movedSeqs/movedClientIds, in snapshotV1.ts's field order."""
+    import json
+
+    import oracle as orc
+
+    batch = obliterate_v1_batch()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
+    assert rc == 0
+    seen = 0
+    for d in range(batch.n_docs):
+        head, bodies = summary.v1_summary(oh[d], ol[d], oc[d], op[d], batch.keys, batch.values, batch.clients[d],
+                                          orc.mt_removers(batch, d))
+        for blob in [head] + bodies:
+            for s in json.loads(blob)["segments"]:
+                if isinstance(s, dict) and "movedSeq" in s:
+                    seen += 1
+                    keys = list(s)
+                    assert keys[-3:] == ["movedSeq", "movedSeqs", "movedClientIds"]
+                    assert s["movedSeq"] == s["movedSeqs"][0] and len(s["movedSeqs"]) == len(s["movedClientIds"])
+                    assert s["movedSeqs"] == sorted(s["movedSeqs"])
+    assert seen > 0

@@ -50,7 +50,8 @@ def main():
             e.mt_run()
             times[name].append(e.stats().kernel_ms)
     n_ops = len(batch.ops)
-    out = {name: {"ok": ok, "ms": times[name], "min_ms": min(times[name]), "mops": n_ops / min(times[name]) / 1e3}
+    out = {name: {"ok": ok, "ms": times[name], "min_ms": min(times[name]), "mops": n_ops / min(times[name]) / 1e3,
+                  "launches": int(e.stats().launches)}
            for name, (e, ok) in engines.items()}
     print(json.dumps(out))
 

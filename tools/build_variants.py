@@ -41,7 +41,7 @@ def build(name, edits, rev=None):
         open(p, "w").write(s.replace(old, new))
     # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc)
     objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o", "hugedoc.o")]
-    for f in ["runtime.cpp", "mergetree.hip"]:
+    for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip"]:
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
                "-x", "hip", "-c", "-o", o, os.path.join(csrc, f)]
@@ -51,7 +51,7 @@ def build(name, edits, rev=None):
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", out] + objs, check=True)
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-variable",
                         "-c", "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage",
-                        os.path.join(csrc, "mergetree.hip")], capture_output=True, text=True)
+                        os.path.join(csrc, "mergetree_compact.hip")], capture_output=True, text=True)
     info = [l.split("remark:")[1].strip() for l in r.stderr.splitlines()
             if "remark" in l and any(k in l for k in ("VGPRs:", "AGPRs", "Scratch", "Occupancy"))]
     print(name, "|", "; ".join(info))
@@ -84,9 +84,7 @@ MAP_LB2 = ("map_lww.hip", "__launch_bounds__(64 * kWaves) void mapLwwKernel", "_
 
 ROWS4 = [("mt_engine.h", "  static constexpr int kRows = 8;          // rows of 64 leaves (one VR element per row)",
           "  static constexpr int kRows = 4;          // rows of 64 leaves (one VR element per row)"),
-         ("mt_engine.h", "  using VR = V8;\n};\n\nstruct LargeTier", "  using VR = V4;\n};\n\nstruct LargeTier"),
-         ("wave.h", 'FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }',
-          'FMT_DEV void launder(V8& v) { asm volatile("" : "+v"(v)); }\nFMT_DEV void launder(V4& v) { asm volatile("" : "+v"(v)); }')]
+         ("mt_engine.h", "  using VR = V8;\n};\n\nstruct LargeTier", "  using VR = V4;\n};\n\nstruct LargeTier")]
 
 NOLOAD = ("mt_engine.h", "    if (in.loaded) loadSnapshot();", "    if (false) loadSnapshot();")
 
