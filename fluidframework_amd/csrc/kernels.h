@@ -43,7 +43,10 @@ struct MtDeviceOut {
   fmt_mt_propset* props;       // nDocs * capProps
   fmt_mt_catchup_range* catchup;  // slabs at catchupOffsets, or nullptr
   fmt_mt_remove_order* rmOrder;   // slabs at rmOrderOffsets, or nullptr
+  uint32_t* ckpt;                 // plain batches: per-document compact → small tier checkpoints, or nullptr
 };
+// Bytes of one document's tier checkpoint (mt_engine.h Doc::kCkptWords).
+size_t mergeTreeCheckpointBytes();
 
 // Per-document capacities of the small (LDS-text) and large (HBM-text) engine tiers.
 // Bulk legacy summaries (summary.hip): a document's result buffers, its runs and its output spans.

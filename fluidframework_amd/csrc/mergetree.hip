@@ -31,6 +31,8 @@ MtCaps mergeTreeCaps(bool large) {
                 static_cast<uint32_t>(Slab<fmt_mt::SmallTier>::kProps)};
 }
 
+size_t mergeTreeCheckpointBytes() { return sizeof(uint32_t) * fmt_mt::Doc<false, fmt_mt::CompactTier>::kCkptWords; }
+
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                   uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream);
 

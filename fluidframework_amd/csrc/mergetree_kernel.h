@@ -101,6 +101,14 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
       o.rmOrder = nullptr;
       o.rmOrderCap = 0;
     }
+    if (Doc::kSavesCkpt || Doc::kResumesCkpt) {
+      o.ckpt = out.ckpt ? out.ckpt + static_cast<size_t>(d) * Doc::kCkptWords : nullptr;
+      o.ckptResume = Doc::kResumesCkpt && o.ckpt != nullptr &&
+                     __builtin_amdgcn_readfirstlane(out.headers[d].status) == fmt_mt::kCkptEscalate;
+    } else {
+      o.ckpt = nullptr;
+      o.ckptResume = false;
+    }
     Doc doc;
     doc.s = scratch;
     doc.run(in, o);
@@ -127,7 +135,7 @@ __global__ __launch_bounds__(256) void collectOverflowKernel(fmt_mt_doc_result* 
     const uint32_t d = docList ? docList[i] : i;
     const int st = headers[d].status;
     if (st == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;
-    if (st == FMT_E_CAPACITY) {
+    if (st == FMT_E_CAPACITY || st == fmt_mt::kCkptEscalate) {
       const uint32_t k = atomicAdd(esc, 1u);
       esc[1 + k] = d;
     }

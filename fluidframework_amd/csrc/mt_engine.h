@@ -32,6 +32,7 @@
 #include "../../include/fmt.h"
 #include "wave.h"
 
+#include <cstddef>
 #include <type_traits>
 
 namespace fmt_mt {
@@ -41,6 +42,7 @@ constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:2
 constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
 constexpr int32_t kNotRemoved = 0x7fffffff;
 constexpr int kCapacityFinal = -33;  // internal status (small tier only), never leaves the runtime
+constexpr int kCkptEscalate = -34;   // internal status: the compact tier stopped at a checkpoint (Doc::saveCkpt)
 
 // Capacity tiers. Every document first replays in the small tier (leaves in 40 VGPRs, text in
 // LDS, 2 waves/SIMD). A document that overflows it (FMT_E_CAPACITY) is replayed again from its
@@ -180,6 +182,8 @@ struct DocOutputs {
   uint32_t catchupCap;
   fmt_mt_remove_order* rmOrder;   // rmOrderCap entries (nullptr: no FMT_MT_F_RMORDER ops)
   uint32_t rmOrderCap;
+  uint32_t* ckpt;                 // the document's tier checkpoint (kCkptWords), or nullptr
+  bool ckptResume;                // small tier: resume from the checkpoint the compact tier left
 };
 
 // Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
@@ -268,6 +272,88 @@ class Doc {
   uint32_t rmPendFrom0 = 0, rmPendTo0 = 0, rmPendFrom1 = 0, rmPendTo1 = 0;
   bool rmHitsSet = false;
   Lane<uint32_t> rmHits;  // leaves a flagged REMOVE found already removed (row bitmask per lane)
+
+  // ------------------------------------------------------------------ tier checkpoint
+  // A plain document (no obliterates, no remove order) in the compact tier that is about to outgrow
+  // its 4 register rows stops before the op (one op adds at most two leaves: an insert's split plus
+  // the new leaf, or a range op's two boundary splits) and leaves its whole state in its HBM
+  // checkpoint: the scalars, the leaf words of the compact rows and the LDS scratch (same layout in
+  // both tiers). The small tier resumes it from that op instead of replaying it from its first op.
+  static constexpr bool kSavesCkpt = !C::kHbmChars && C::kRows < SmallTier::kRows && !Ob && !Rm;
+  static constexpr bool kResumesCkpt = !C::kHbmChars && C::kRows == SmallTier::kRows && !Ob && !Rm;
+  static constexpr int kCkptRows = CompactTier::kRows;
+  static constexpr int kCkptHead = 16;
+  static constexpr int kCkptScratchWords = static_cast<int>((offsetof(Scratch<SmallTier>, tmp) + 3) / 4);
+  static constexpr int kCkptWords = kCkptHead + 5 * kCkptRows * 64 + kCkptScratchWords;
+  uint32_t* ckpt = nullptr;
+
+  FMT_DEV void saveCkpt(uint64_t next) {
+    uint32_t* ck = ckpt;
+    FOR_LANES(l) {
+      if (l == 0) {
+        ck[0] = static_cast<uint32_t>(next);
+        ck[1] = static_cast<uint32_t>(next >> 32);
+        ck[2] = static_cast<uint32_t>(n);
+        ck[3] = static_cast<uint32_t>(nChars);
+        ck[4] = static_cast<uint32_t>(root);
+        ck[5] = static_cast<uint32_t>(nFree);
+        ck[6] = static_cast<uint32_t>(heapN);
+        ck[7] = static_cast<uint32_t>(nProps);
+        ck[8] = static_cast<uint32_t>(curSeq);
+        ck[9] = static_cast<uint32_t>(minSeq);
+        ck[10] = static_cast<uint32_t>(failSeq);
+        ck[11] = nextId;
+        ck[12] = cuN;
+      }
+    }
+    FOR_LANES(l) {
+#pragma unroll
+      for (int f = 0; f < 5; f++) {
+#pragma unroll
+        for (int r = 0; r < kCkptRows && r < kRows; r++) ck[kCkptHead + (f * kCkptRows + r) * 64 + l] = LANE(W[f])[r];
+      }
+    }
+    waveSync();  // every LDS write of the op stream has landed
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(s);
+    uint32_t* dst = ck + kCkptHead + 5 * kCkptRows * 64;
+    FOR_LANES(l) {
+      for (int t = l; t < kCkptScratchWords; t += 64) dst[t] = src[t];
+    }
+  }
+
+  // Returns the op index to resume at.
+  FMT_DEV uint64_t restoreCkpt() {
+    const uint32_t* ck = ckpt;
+    const uint64_t next = uni(ck[0]) | (static_cast<uint64_t>(uni(ck[1])) << 32);
+    n = static_cast<int>(uni(ck[2]));
+    nChars = static_cast<int>(uni(ck[3]));
+    root = static_cast<int>(uni(ck[4]));
+    nFree = static_cast<int>(uni(ck[5]));
+    heapN = static_cast<int>(uni(ck[6]));
+    nProps = static_cast<int>(uni(ck[7]));
+    curSeq = static_cast<int>(uni(ck[8]));
+    minSeq = static_cast<int>(uni(ck[9]));
+    failSeq = static_cast<int>(uni(ck[10]));
+    nextId = uni(ck[11]);
+    cuN = uni(ck[12]);
+    status = FMT_OK;
+    FOR_LANES(l) {
+#pragma unroll
+      for (int f = 0; f < 5; f++) {
+        VR z;
+#pragma unroll
+        for (int r = 0; r < kRows; r++) z[r] = r < kCkptRows ? ck[kCkptHead + (f * kCkptRows + r) * 64 + l] : 0u;
+        LANE(W[f]) = z;
+      }
+    }
+    const uint32_t* src = ck + kCkptHead + 5 * kCkptRows * 64;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(s);
+    FOR_LANES(l) {
+      for (int t = l; t < kCkptScratchWords; t += 64) dst[t] = src[t];
+    }
+    waveSync();
+    return next;
+  }
 
   // ------------------------------------------------------------------ leaf array primitives
   // Leaf j lives in row j >> 6 (element of the V8) of lane j & 63: document order runs along a
@@ -1973,12 +2059,19 @@ class Doc {
     return x;
   }
 
-  FMT_DEV void replay() {
+  FMT_DEV void replay(uint64_t first) {
     stamp(kPfOutput);
-    Lane<uint32_t> rec0 = fetchOp(in.begin);
-    Lane<uint32_t> rec1 = fetchOp(in.begin + 1);
+    Lane<uint32_t> rec0 = fetchOp(first);
+    Lane<uint32_t> rec1 = fetchOp(first + 1);
     Lane<uint32_t> txt0 = fetchText(rec0);
-    for (uint64_t i = in.begin; i < in.end; i++) {
+    for (uint64_t i = first; i < in.end; i++) {
+      if constexpr (kSavesCkpt) {
+        if (n + 2 > kCapLeaves && ckpt != nullptr) {  // the next op could outgrow the compact rows
+          saveCkpt(i);
+          status = kCkptEscalate;
+          return;
+        }
+      }
       const fmt_mt_op op = decodeOp(rec0);
       const Lane<uint32_t> text = txt0;
       rec0 = rec1;
@@ -2127,10 +2220,22 @@ class Doc {
     rmCap = out.rmOrder ? out.rmOrderCap : 0u;
     rmN = 0;
     if constexpr (C::kHbmChars) gch = out.chars;
+    ckpt = out.ckpt;
     init();
-    if (in.loaded) loadSnapshot();
-    else loadInitial();
-    if (status == FMT_OK) replay();
+    uint64_t first = in.begin;
+    if (kResumesCkpt && ckpt != nullptr && out.ckptResume) {
+      first = restoreCkpt();
+    } else {
+      if (in.loaded) loadSnapshot();
+      else loadInitial();
+    }
+    if (status == FMT_OK) replay(first);
+    if (kSavesCkpt && status == kCkptEscalate) {  // the small tier writes everything else
+      FOR_LANES(l) {
+        if (l == 0) out.header->status = status;
+      }
+      return;
+    }
     writeOutputs(out);
     stamp(kPfOutput);
   }

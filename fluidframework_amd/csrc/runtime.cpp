@@ -81,6 +81,7 @@ struct fmt_ctx {
   DevBuf<fmt_mt_propset> mtProps;
   DevBuf<uint32_t> mtEsc;                    // small-tier overflow list: [0] = count, then doc ids
   DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (plain batches), same layout
+  DevBuf<uint32_t> mtCkpt;                   // plain batches: per-document compact → small tier checkpoints
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
   DevBuf<uint16_t> mtBigChars;
   DevBuf<fmt_mt_propset> mtBigProps;
@@ -202,6 +203,7 @@ void fmt_close(fmt_ctx* c) {
   c->mtProps.release();
   c->mtEsc.release();
   c->mtEsc2.release();
+  c->mtCkpt.release();
   c->mtBigLeaves.release();
   c->mtBigChars.release();
   c->mtBigProps.release();
@@ -566,6 +568,10 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtNProps = b->n_props_ops;
   c->mtHasInit = b->doc_init != nullptr;
   c->mtObliterate = obliterates;
+  // A plain batch starts in the compact tier; a document about to outgrow it stops at a checkpoint
+  // (≈15 KiB per document) that the small tier resumes from.
+  if (!obliterates && !c->mtHasRmOrder)
+    FMT_HIP(c, c->mtCkpt.reserve(static_cast<size_t>(n) * (fmt_kernels::mergeTreeCheckpointBytes() / sizeof(uint32_t))));
   c->mtInsertChars = insertChars;
   c->mtInitChars = initChars;
   // Huge documents: a summary-loaded document with more segments or text than the large tier holds
@@ -687,8 +693,10 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasCatchup ? c->mtCuOffs.p : nullptr,
                                 c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr,
                                 c->mtHasRmOrder ? c->mtRmOffs.p : nullptr};
+  const bool plain = !c->mtObliterate && !c->mtHasRmOrder;
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
-                                c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
+                                c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
+                                plain ? c->mtCkpt.p : nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -713,7 +721,8 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigChars.reserve(static_cast<size_t>(nEsc) * big.chars));
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
-                                  c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr};
+                                  c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
+                                  nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
                                                  c->mtHasRmOrder));

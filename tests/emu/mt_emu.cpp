@@ -6,15 +6,20 @@
 
 #include "../../fluidframework_amd/csrc/mt_engine.h"
 
+// ckpt (plain batches): per-document tier checkpoints; the compact tier saves, the small tier resumes
+// the documents whose header says kCkptEscalate and, with onlyEscalated, replays only those and the
+// documents that overflowed (the runtime's cascade over the overflow list).
 template <bool Ob, class C, bool Rm = false>
 static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                      fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
-                     fmt_mt_remove_order* rmOrder, uint32_t capRm) {
+                     fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* ckpt = nullptr,
+                     bool onlyEscalated = false, size_t leafStride = 0) {
   using Doc = fmt_mt::Doc<Ob, C, Rm>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
   int status = FMT_OK;
   for (uint32_t d = 0; d < b->n_docs; d++) {
+    if (onlyEscalated && headers[d].status != FMT_E_CAPACITY && headers[d].status != fmt_mt::kCkptEscalate) continue;
     std::memset(scratch.get(), 0xCD, sizeof(fmt_mt::Scratch<C>));  // poison: state must be initialized
     fmt_mt::DocInputs in;
     in.ops = b->ops;
@@ -42,17 +47,20 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     }
     fmt_mt::DocOutputs o;
     o.header = headers + d;
-    o.leaves = leaves + static_cast<size_t>(d) * Doc::kCapLeaves;
+    o.leaves = leaves + static_cast<size_t>(d) * (leafStride ? leafStride : Doc::kCapLeaves);
     o.chars = chars + static_cast<size_t>(d) * Doc::kCapChars;
     o.props = props + static_cast<size_t>(d) * Doc::kPropCap;
     o.catchup = catchup ? catchup + static_cast<size_t>(d) * capCatchup : nullptr;
     o.catchupCap = catchup ? capCatchup : 0u;
     o.rmOrder = rmOrder ? rmOrder + static_cast<size_t>(d) * capRm : nullptr;
     o.rmOrderCap = rmOrder ? capRm : 0u;
+    o.ckpt = ckpt && (Doc::kSavesCkpt || Doc::kResumesCkpt) ? ckpt + static_cast<size_t>(d) * Doc::kCkptWords : nullptr;
+    o.ckptResume = o.ckpt != nullptr && Doc::kResumesCkpt && headers[d].status == fmt_mt::kCkptEscalate;
     new (doc.get()) Doc();
     doc->s = scratch.get();
     doc->run(in, o);
     if (headers[d].status == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;  // as collectOverflowKernel
+    if (headers[d].status == fmt_mt::kCkptEscalate) continue;  // the small tier resumes it
     if (headers[d].status != FMT_OK && status == FMT_OK) status = headers[d].status;
   }
   return status;
@@ -61,8 +69,10 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
 extern "C" {
 
 // large = 0: the small tier (registers + LDS text); 1: the large tier (HBM text) that the runtime
-// replays overflowing documents in; 2: the compact tier (4 register rows) plain batches start in.
+// replays overflowing documents in; 2: the compact tier (4 register rows) plain batches start in;
+// 3: the compact → small cascade with checkpoints (small-tier strides).
 int emu_mt_capacity(int large, uint32_t* leaves, uint32_t* chars, uint32_t* props) {
+  if (large == 3) large = 0;
   if (large == 2) {
     *leaves = fmt_mt::Doc<false, fmt_mt::CompactTier>::kCapLeaves;
     *chars = fmt_mt::CompactTier::kCapChars;
@@ -93,6 +103,14 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   for (uint64_t i = 0; i < b->n_ops && !rm; i++) rm = (b->ops[i].flags & FMT_MT_F_RMORDER) != 0;
   if (large == 2 && !ob && !rm) return replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup,
                                                                              capCatchup, rmOrder, capRm);
+  if (large == 3 && !ob && !rm) {  // the runtime's cascade: compact tier with checkpoints, then the small tier
+    using D = fmt_mt::Doc<false, fmt_mt::CompactTier>;
+    std::unique_ptr<uint32_t[]> ck(new uint32_t[static_cast<size_t>(b->n_docs) * D::kCkptWords]);
+    const size_t stride = fmt_mt::Doc<false, S>::kCapLeaves;
+    replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(),
+                                          false, stride);
+    return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(), true);
+  }
   if (large == 1) {
     if (ob && rm) return replayAll<true, G, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
     if (ob) return replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);

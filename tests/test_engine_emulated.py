@@ -112,6 +112,44 @@ def test_compact_tier_matches_oracle_on_conflict_farm(orc, n_clients):
     assert fit >= 30
 
 
+@pytest.mark.parametrize("n_clients,seed", [(8, 1), (3, 2), (16, 3)])
+def test_compact_to_small_cascade_resumes_from_checkpoints(orc, n_clients, seed):
+    """The runtime's cascade for plain batches: the compact tier stops a document before the op that
+    could outgrow its 256 leaves and saves its state; the small tier resumes it from that op. Every
+    document == oracle bit for bit, and checkpoints were taken."""
+    batch = workloads.conflict_farm(120, n_clients=n_clients, ops_per_doc=2000, seed=seed)
+    cl, cc, cp = emu_caps(large=3)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    assert rc == 0
+    compact = emu_replay(batch, large=2)[0]
+    assert (compact["status"] == -3).sum() >= 5  # documents that outgrow the compact rows
+    hdr, leaves, chars, props = emu_replay(batch, large=3)
+    assert (hdr["status"] == 0).all()
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_compact_cascade_with_catchup_and_props(orc):
+    """Checkpointed documents keep their catch-up ranges (recorded before and after the checkpoint)
+    and prop sets."""
+    from fluidframework_amd.streams import flag_catchup
+
+    batch = workloads.conflict_farm(60, n_clients=8, ops_per_doc=2000, seed=9)
+    flag_catchup(batch.ops, batch.doc_op_offsets)
+    cl, cc, cp = emu_caps(large=3)
+    rc, oh, ol, oc, op, _, ocu = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024,
+                                                     cap_catchup=4096)
+    assert rc == 0
+    hdr, leaves, chars, props, cu = emu_replay(batch, large=3, cap_catchup=4096)
+    assert (hdr["status"] == 0).all()
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+        n = int(oh[d]["n_catchup"])
+        assert int(hdr[d]["n_catchup"]) == n and np.array_equal(cu[d][:n], ocu[d][:n]), d
+
+
 def test_compact_tier_fills_every_row_to_capacity(orc):
     cl, cc, cp = emu_caps(large=2)
     batch = _no_zamboni_batch([60, 130, 200, 230, 250, 260, 300])

@@ -25,14 +25,19 @@ from collections import defaultdict
 def main():
     kernel, key, ops, simds, out = sys.argv[1:6]
     ops, simds = float(ops), int(simds)
-    vals = defaultdict(list)
+    per = os.environ.get("PMC_PER") or kernel  # the dispatch that marks one run (see pmc_traffic.py)
+    vals = defaultdict(float)
+    runs = defaultdict(set)
     sources = []
     for path in sys.argv[6:]:
         sources.append(os.path.relpath(path))
         for r in csv.DictReader(open(path)):
             if kernel in r["Kernel_Name"]:
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    c = {k: sum(v) / len(v) for k, v in vals.items()}
+                name = r["Counter_Name"]
+                vals[name] += float(r["Counter_Value"])
+                if per in r["Kernel_Name"]:
+                    runs[name].add((path, r["Dispatch_Id"]))  # GRBM_ sits in several passes
+    c = {k: v / max(len(runs[k]), 1) for k, v in vals.items()}
     if not c:
         raise SystemExit(f"no rows for {kernel}")
     rec = {"kernel": kernel, "ops_per_launch": ops, "counters": c, "source": sources}
