@@ -66,6 +66,9 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     in.propsOff = batch.propsOff;
     in.propsKv = batch.propsKv;
     in.nPropsOps = batch.nPropsOps;
+    in.relpos = batch.relpos;
+    in.nRelpos = batch.relpos ? batch.nRelpos : 0u;
+    in.markerKey = batch.markerKey;
     if (batch.snapshots && batch.snapshots[d].loaded) {
       const fmt_mt_snapshot_doc sd = batch.snapshots[d];
       in.snapSegs = batch.snapshotSegs + sd.first_seg;

@@ -171,6 +171,9 @@ struct DocInputs {
   uint32_t nHeader, nBody;
   int32_t snapMinSeq, snapSeq;
   uint32_t loaded;
+  const fmt_mt_relpos* relpos;  // FMT_MT_F_REL1/REL2 ops index it (nullptr: none in the batch)
+  uint32_t nRelpos;
+  uint32_t markerKey;           // key id of "markerId"
 };
 
 struct DocOutputs {
@@ -1406,6 +1409,75 @@ class Doc {
     }
   }
 
+  // ------------------------------------------------------------------ relative positions
+  // posFromRelativePos (mergeTree.ts:1462-1483): the marker whose "markerId" property holds the id
+  // (idToMarker: markers stay findable until zamboni unlinks them; with ids unique per document that
+  // is every marker leaf still in the tree), its start in the op's perspective, then the side and
+  // offset. Returns -1 when no marker holds the id.
+  FMT_DEV int posFromRelativePos(uint32_t idx, int refSeq, int client) {
+    const uint32_t mid = uni(loadCoherent(&in.relpos[idx].marker_id));
+    const int offset = static_cast<int>(uni(loadCoherent(reinterpret_cast<const uint32_t*>(&in.relpos[idx].offset))));
+    const bool before = (uni(loadCoherent(&in.relpos[idx].flags)) & FMT_MT_REL_BEFORE) != 0;
+    if (mid == FMT_MT_NO_MARKER || in.markerKey == FMT_MT_NO_MARKER) return -1;
+    const uint32_t want = (in.markerKey << 16) | (mid & 0xFFFFu);
+    const int nr = rows();
+    Lane<uint32_t> hits;
+    FOR_LANES(l) {
+      uint32_t m = 0;
+      FOR_ROWS(r, 0, nr) {
+        const uint32_t pid = propsL(l, r);
+        if (r * 64 + l < n && fMarker(LANE(W[4])[r]) && pid != kPropsUndef && mid <= 0xFFFFu) {
+          const uint32_t cnt = s->props[pid].n;
+          bool f = false;
+          for (uint32_t k = 0; k < cnt && k < FMT_MT_PROPS_MAX; k++) f = f || s->props[pid].kv[k] == want;
+          if (f) m |= 1u << r;
+        }
+      }
+      LANE(hits) = m;
+    }
+    // several markers with one id (ids are meant to be unique): the last inserted one, as
+    // idToMarker.set on insert leaves it
+    int j = -1, best = -1;
+    for (Lane<uint32_t> todo = hits;;) {
+      const int k = firstSet(todo, nr);
+      if (k < 0) break;
+      FOR_LANES(l) {
+        if (l == (k & 63)) LANE(todo) &= ~(1u << (k >> 6));
+      }
+      const int ins = static_cast<int>(readField(k, 1));
+      if (ins >= best) {
+        best = ins;
+        j = k;
+      }
+    }
+    if (j < 0) return -1;
+    Lane<VR> vis, st;
+    visLengths(refSeq, client, vis, nr);
+    scanRows(vis, st, nr);
+    int pos = static_cast<int>(readlane(selectRow(st, j >> 6), j & 63));
+    if (before) pos -= offset;
+    else pos += static_cast<int>(fLen(readField(j, 0))) + offset;
+    return pos;
+  }
+
+  // getValidOpRange (client.ts:758-767): an undefined pos1 / pos2 comes from relativePos1 / 2.
+  FMT_DEV bool resolveRelative(fmt_mt_op& op) {
+    for (int k = 0; k < 2; k++) {
+      if ((op.flags & (k == 0 ? FMT_MT_F_REL1 : FMT_MT_F_REL2)) == 0) continue;
+      const int32_t idx = k == 0 ? op.pos1 : op.pos2;
+      const int pos = idx >= 0 && static_cast<uint32_t>(idx) < in.nRelpos
+                          ? posFromRelativePos(static_cast<uint32_t>(idx), op.ref_seq, op.client)
+                          : -1;
+      if (pos < 0) {
+        fail(FMT_E_DATA);
+        return false;
+      }
+      if (k == 0) op.pos1 = pos;
+      else op.pos2 = pos;
+    }
+    return true;
+  }
+
   // One member op of a remote message (client.ts:1291-1327).
   FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
     const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
@@ -2072,7 +2144,7 @@ class Doc {
           return;
         }
       }
-      const fmt_mt_op op = decodeOp(rec0);
+      fmt_mt_op op = decodeOp(rec0);
       const Lane<uint32_t> text = txt0;
       rec0 = rec1;
       txt0 = fetchText(rec0);
@@ -2084,7 +2156,7 @@ class Doc {
       else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
-      else applyOp(op, text);
+      else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
       if constexpr (Rm) {
         if (rmPendN > 0 || rmHitsSet)
           rmFlush(op.client, op.seq, op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE);

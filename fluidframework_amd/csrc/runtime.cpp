@@ -88,6 +88,8 @@ struct fmt_ctx {
   std::vector<int32_t> mtBigSlot;            // doc -> large-tier slab, or -1
   DevBuf<fmt_mt_snapshot_doc> mtSnap;       // per-doc summary loads (f3)
   DevBuf<fmt_mt_snapshot_seg> mtSnapSegs;
+  DevBuf<fmt_mt_relpos> mtRelpos;            // relative positions (FMT_MT_F_REL1/REL2 ops)
+  uint32_t mtNRelpos = 0, mtMarkerKey = FMT_MT_NO_MARKER;
   bool mtHasSnap = false;
   bool mtObliterate = false;                 // batch holds obliterates: launch the Doc<true> kernel
   DevBuf<uint64_t> mtCuOffs;                 // per-doc catch-up slab offsets (n_docs + 1)
@@ -209,6 +211,7 @@ void fmt_close(fmt_ctx* c) {
   c->mtBigProps.release();
   c->mtSnap.release();
   c->mtSnapSegs.release();
+  c->mtRelpos.release();
   c->mtCuOffs.release();
   c->mtCatchup.release();
   c->mtRmOffs.release();
@@ -553,6 +556,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtSnap.p, b->snapshots, n * sizeof(fmt_mt_snapshot_doc)));
     FMT_HIP(c, cp(c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg)));
   }
+  c->mtNRelpos = b->relpos ? b->n_relpos : 0u;
+  c->mtMarkerKey = b->marker_id_key;
+  if (c->mtNRelpos) {
+    FMT_HIP(c, c->mtRelpos.reserve(c->mtNRelpos));
+    FMT_HIP(c, cp(c->mtRelpos.p, b->relpos, c->mtNRelpos * sizeof(fmt_mt_relpos)));
+  }
   if (c->mtHasCatchup) FMT_HIP(c, cp(c->mtCuOffs.p, c->mtCuOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
   if (c->mtHasRmOrder) FMT_HIP(c, cp(c->mtRmOffs.p, c->mtRmOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
   if (b->props_off) {
@@ -594,8 +603,9 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
         return setErr(c, FMT_E_UNSUPPORTED, "a document beyond the large tier must load from one header chunk (n_body = 0)");
       const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1], nOps = o1 - o0;
       for (uint64_t i = o0; i < o1; i++)
-        if (b->ops[i].flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER))
-          return setErr(c, FMT_E_UNSUPPORTED, "catch-up / remove-order recording in a document beyond the large tier");
+        if (b->ops[i].flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2))
+          return setErr(c, FMT_E_UNSUPPORTED,
+                        "catch-up / remove-order recording or relative positions in a document beyond the large tier");
       c->mtHugeSlot[d] = static_cast<int32_t>(c->huge.size());
       c->huge.emplace_back();
       auto& H = c->huge.back();
@@ -692,7 +702,8 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps,
                                 c->mtHasCatchup ? c->mtCuOffs.p : nullptr,
                                 c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr,
-                                c->mtHasRmOrder ? c->mtRmOffs.p : nullptr};
+                                c->mtHasRmOrder ? c->mtRmOffs.p : nullptr, c->mtNRelpos ? c->mtRelpos.p : nullptr,
+                                c->mtNRelpos, c->mtMarkerKey};
   const bool plain = !c->mtObliterate && !c->mtHasRmOrder;
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,

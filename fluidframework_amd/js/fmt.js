@@ -23,6 +23,9 @@ const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
 const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
 const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate places (client.ts:680-700)
 const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER = 0x8000; // Marker segments
+// legacy relativePos1/2 (ops.ts IRelativePosition): pos1/pos2 index the relpos table (fmt_mt_relpos, 16 B)
+const FMT_MT_F_REL1 = 64, FMT_MT_F_REL2 = 128, FMT_MT_NO_MARKER = 0xffffffff, FMT_MT_REL_BEFORE = 1;
+const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 
 /** The refType of a Marker spec {marker: {refType}, props?} (IJSONMarkerSegment), or null. */
 function markerRefType(spec) {
@@ -195,6 +198,7 @@ class MergeTreeStreamBuilder {
 		this.docInit = [];
 		this.snapshots = []; // per doc: null or [firstSeg, nHeader, nBody, minSeq, seq]
 		this.snapshotSegs = []; // [textOff, len, propsOp]
+		this.relpos = []; // [marker value id, offset, flags]
 		this.current = null;
 	}
 	beginDoc(initialText, observer) {
@@ -284,22 +288,42 @@ class MergeTreeStreamBuilder {
 		}
 		return i;
 	}
+	/** An IRelativePosition {id?, before?, offset?}: its row in the relpos table (streams.py _relpos). */
+	relposOf(rp) {
+		const marker = rp.id ? this.values.intern(JSON.stringify(rp.id)) : FMT_MT_NO_MARKER;
+		this.keys.intern(MARKER_ID_KEY);
+		this.relpos.push([marker, rp.offset !== undefined && rp.offset !== null ? rp.offset : 0, rp.before ? FMT_MT_REL_BEFORE : 0]);
+		return this.relpos.length - 1;
+	}
+	/** [pos1, pos2, flags]: getValidOpRange (client.ts:758-767) takes the numbers and falls back to
+	 * relativePos1/2 only when they are undefined. */
+	positions(op, withPos2) {
+		let p1 = op.pos1, p2 = withPos2 ? op.pos2 : undefined, f = 0;
+		if ((p1 === undefined || p1 === null) && op.relativePos1 !== undefined && op.relativePos1 !== null) {
+			p1 = this.relposOf(op.relativePos1);
+			f |= FMT_MT_F_REL1;
+		}
+		if (withPos2 && (p2 === undefined || p2 === null) && op.relativePos2 !== undefined && op.relativePos2 !== null) {
+			p2 = this.relposOf(op.relativePos2);
+			f |= FMT_MT_F_REL2;
+		}
+		return [p1, p2, f];
+	}
 	packOp(op, seq, ref, msn, client, flags) {
 		const o = this.ops.next();
 		const v = this.ops.view;
 		let pos1 = 0, pos2 = 0, payload = 0, len = 0, type = MT_REMOVE;
 		if (op !== null) {
-			if (op.relativePos1 !== undefined || op.relativePos2 !== undefined) {
-				throw new UnsupportedOp("relative positions");
-			}
 			type = op.type;
 			if (type === MT_INSERT) {
+				const rp = this.positions(op, false);
+				flags |= rp[2];
 				let seg = op.seg;
 				let props = null;
 				const rtype = markerRefType(seg);
 				if (rtype !== null) { // Marker.make(refType, props): len 1, its arena unit = refType
 					const p = seg.props === undefined ? null : seg.props;
-					pos1 = op.pos1; pos2 = p === null ? -1 : this.propsOp(p) + 1;
+					pos1 = rp[0]; pos2 = p === null ? -1 : this.propsOp(p) + 1;
 					payload = this.text.push(String.fromCharCode(rtype))[0]; len = 1; flags |= FMT_MT_F_MARKER;
 				} else {
 					if (typeof seg !== "string") { // IJSONTextSegment {text, props} (textSegment.ts:44-52)
@@ -313,16 +337,21 @@ class MergeTreeStreamBuilder {
 					const r = this.text.push(seg);
 					if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
 					// pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
-					pos1 = op.pos1; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1];
+					pos1 = rp[0]; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1];
 				}
-			} else if (type === MT_REMOVE || type === MT_OBLITERATE) {
+			} else if (type === MT_REMOVE) {
+				const rp = this.positions(op, true);
+				pos1 = rp[0]; pos2 = rp[1]; flags |= rp[2];
+			} else if (type === MT_OBLITERATE) {
 				pos1 = op.pos1; pos2 = op.pos2; // non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
 			} else if (type === MT_OBLITERATE_SIDED) {
 				pos1 = op.pos1.pos; pos2 = op.pos2.pos;
 				flags |= (op.pos1.before ? FMT_MT_F_START_BEFORE : 0) | (op.pos2.before ? FMT_MT_F_END_BEFORE : 0);
 			} else if (type === MT_ANNOTATE) {
 				if (op.adjust !== undefined && op.adjust !== null) throw new UnsupportedOp("annotate adjust");
-				pos1 = op.pos1; pos2 = op.pos2; payload = this.propsOp(op.props || {});
+				const rp = this.positions(op, true);
+				pos1 = rp[0]; pos2 = rp[1]; flags |= rp[2];
+				payload = this.propsOp(op.props || {});
 			} else {
 				throw new UnsupportedOp(`merge-tree op type ${type}`);
 			}
@@ -428,6 +457,8 @@ class MergeTreeStreamBuilder {
 			clients: this.docs.map((d) => d.clientNames.slice()),
 			messages: this.docs.map((d) => d.messages),
 			nDocs: this.docs.length,
+			relpos: this.relpos.length ? Uint32Array.from([].concat(...this.relpos.map((r) => [r[0], r[1] >>> 0, r[2], 0]))) : undefined,
+			markerIdKey: this.relpos.length && this.keys.ids.has(MARKER_ID_KEY) ? this.keys.ids.get(MARKER_ID_KEY) : FMT_MT_NO_MARKER,
 		};
 	}
 }

@@ -378,6 +378,28 @@ napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
     keep_array(env, j, prop(env, b, "snapshots"));
     keep_array(env, j, prop(env, b, "snapshotSegs"));
   }
+  // optional legacy relative positions: relpos (fmt_mt_relpos rows) + markerIdKey
+  void* rp;
+  size_t nrp;
+  if (!get_bytes(env, prop(env, b, "relpos"), "relpos", &rp, &nrp)) {
+    delete j;
+    return nullptr;
+  }
+  j->mt.marker_id_key = FMT_MT_NO_MARKER;
+  if (rp != nullptr) {
+    if (nrp % sizeof(fmt_mt_relpos)) {
+      delete j;
+      throw_fmt(env, FMT_E_USAGE, "replayMergeTree: relpos must hold whole fmt_mt_relpos rows");
+      return nullptr;
+    }
+    j->mt.relpos = static_cast<const fmt_mt_relpos*>(rp);
+    j->mt.n_relpos = uint32_t(nrp / sizeof(fmt_mt_relpos));
+    if (!get_u32(env, prop(env, b, "markerIdKey"), "markerIdKey", &j->mt.marker_id_key)) {
+      delete j;
+      return nullptr;
+    }
+    keep_array(env, j, prop(env, b, "relpos"));
+  }
   for (int i = 0; i < 6; ++i) keep_array(env, j, prop(env, b, names[i]));
   return queue(env, j, argv[0], "fmtReplayMergeTree");
 }

@@ -57,7 +57,7 @@ LEAF_GONE = 0xFFFFFFFF
 
 CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("type", "<u4")])
 
-from .streams import SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE  # noqa: E402  (include/fmt.h layouts)
+from .streams import NO_MARKER, RELPOS_DTYPE, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE  # noqa: E402  (include/fmt.h layouts)
 
 PROPS_MAX = 8
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
@@ -82,6 +82,9 @@ class FmtMtBatch(ctypes.Structure):
         ("snapshots", ctypes.c_void_p),
         ("snapshot_segs", ctypes.c_void_p),
         ("n_snapshot_segs", ctypes.c_uint64),
+        ("relpos", ctypes.c_void_p),
+        ("n_relpos", ctypes.c_uint32),
+        ("marker_id_key", ctypes.c_uint32),
     ]
 
 
@@ -126,12 +129,18 @@ def batch_struct(batch):
         keep.append(np.ascontiguousarray(snaps, dtype=SNAPSHOT_DOC_DTYPE))
         keep.append(np.ascontiguousarray(segs, dtype=SNAPSHOT_SEG_DTYPE) if len(segs) else
                     np.zeros(1, dtype=SNAPSHOT_SEG_DTYPE))
+    relpos = getattr(batch, "relpos", None)
+    rel = np.ascontiguousarray(relpos, dtype=RELPOS_DTYPE) if relpos is not None and len(relpos) else None
     b = FmtMtBatch(
         _ptr(keep[0]), len(keep[0]), _ptr(keep[1]), len(keep[1]) - 1, _ptr(keep[2]), len(keep[2]),
         _ptr(keep[3]), _ptr(keep[4]), len(keep[4]) - 1, _ptr(keep[5]),
         _ptr(keep[6]) if snaps is not None else None, _ptr(keep[7]) if snaps is not None else None,
         len(segs) if snaps is not None else 0,
+        _ptr(rel) if rel is not None else None, len(rel) if rel is not None else 0,
+        int(getattr(batch, "marker_id_key", NO_MARKER)),
     )
+    if rel is not None:
+        keep.append(rel)
     return b, keep
 
 

@@ -54,6 +54,12 @@ assert MAP_OP_DTYPE.itemsize == 16
 MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
 MT_F_START_BEFORE, MT_F_END_BEFORE = 8, 16  # fmt.h FMT_MT_F_START_BEFORE / FMT_MT_F_END_BEFORE
 MT_F_MARKER = 32  # fmt.h FMT_MT_F_MARKER: insert of a Marker segment
+MT_F_REL1, MT_F_REL2 = 64, 128  # fmt.h FMT_MT_F_REL1/REL2: pos1/pos2 index the relpos table
+# fmt_mt_relpos: an IRelativePosition {id, before, offset} (ops.ts IRelativePosition)
+RELPOS_DTYPE = np.dtype([("marker_id", "<u4"), ("offset", "<i4"), ("flags", "<u4"), ("pad", "<u4")])
+NO_MARKER = 0xFFFFFFFF  # fmt.h FMT_MT_NO_MARKER
+REL_BEFORE = 1  # fmt.h FMT_MT_REL_BEFORE
+MARKER_ID_KEY = "markerId"  # reservedMarkerIdKey (merge-tree/src/ops.ts)
 MT_SEG_MARKER = 0x80000000  # fmt.h FMT_MT_SEG_MARKER (snapshot segment len flag)
 MT_LEAF_MARKER = 0x8000  # fmt.h FMT_MT_LEAF_MARKER (fmt_mt_leaf.pad flag)
 
@@ -174,6 +180,9 @@ class MergeTreeBatch:
     # optional (f3): per-doc fmt_mt_snapshot_doc and the segment specs they index
     snapshots: np.ndarray | None = None
     snapshot_segs: np.ndarray | None = None
+    # optional (legacy relativePos1/2): RELPOS_DTYPE table and the key id of "markerId"
+    relpos: np.ndarray | None = None
+    marker_id_key: int = NO_MARKER
 
     @property
     def n_docs(self) -> int:
@@ -240,6 +249,31 @@ class MergeTreeStreamBuilder:
         self.doc_init: list[tuple] = []
         self.snapshots: list[tuple] = []  # per doc: (first_seg, n_header, n_body, min_seq, seq, loaded)
         self.snapshot_segs: list[tuple] = []
+        self.relpos: list[tuple] = []  # (marker value id, offset, flags, 0)
+
+    def _relpos(self, rp: dict) -> int:
+        """An IRelativePosition {id?, before?, offset?}: its row in the relpos table. The id is looked
+        up as the JSON value a marker's "markerId" property holds (an id no marker holds resolves to
+        no marker: posFromRelativePos returns -1, mergeTree.ts:1462-1483)."""
+        mid = rp.get("id")
+        marker = self.values.intern(js_json(mid)) if mid else NO_MARKER
+        self.keys.intern(MARKER_ID_KEY)
+        off = rp.get("offset")
+        self.relpos.append((marker, int(off) if off is not None else 0, REL_BEFORE if rp.get("before") else 0, 0))
+        return len(self.relpos) - 1
+
+    def _positions(self, op) -> tuple:
+        """(pos1, pos2, flags) of a range/insert op: getValidOpRange (client.ts:758-767) takes pos1/pos2
+        and falls back to relativePos1/2 only when the number is undefined."""
+        flags = 0
+        p1, p2 = op.get("pos1"), op.get("pos2")
+        if p1 is None and op.get("relativePos1") is not None:
+            p1, flags = self._relpos(op["relativePos1"]), flags | MT_F_REL1
+        if p2 is None and op.get("relativePos2") is not None:
+            p2, flags = self._relpos(op["relativePos2"]), flags | MT_F_REL2
+        if p1 is None:
+            raise ValueError("op without pos1 or relativePos1")
+        return int(p1), (int(p2) if p2 is not None else None), flags
 
     def _text(self, s: str) -> tuple:
         u = utf16(s)
@@ -276,16 +310,15 @@ class MergeTreeStreamBuilder:
         if op is None:  # empty group: only advances the collab window
             return (seq, ref, msn, 0, 0, 0, 0, client, MT_REMOVE, 0)
         t = op["type"]
-        if op.get("relativePos1") is not None or op.get("relativePos2") is not None:
-            raise UnsupportedOp("relative positions")
         if t == MT_INSERT:
+            p1, _, rel = self._positions({"pos1": op.get("pos1"), "relativePos1": op.get("relativePos1")})
             seg = op["seg"]
             props = None
             rtype = marker_ref_type(seg)
             if rtype is not None:  # Marker.make(refType, props): len 1, its arena unit = refType
                 props = seg.get("props")
                 pos2 = -1 if props is None else self._props_op(props) + 1
-                return (seq, ref, msn, int(op["pos1"]), pos2, self._unit(rtype), 1, client, MT_INSERT, MT_F_MARKER)
+                return (seq, ref, msn, p1, pos2, self._unit(rtype), 1, client, MT_INSERT, MT_F_MARKER | rel)
             if not isinstance(seg, str):  # IJSONTextSegment {text, props} (textSegment.ts:44-52)
                 if isinstance(seg, dict) and "text" in seg and set(seg) <= {"text", "props"}:
                     props = seg.get("props")
@@ -297,9 +330,10 @@ class MergeTreeStreamBuilder:
                 raise UnsupportedOp("insert longer than 65535 UTF-16 units")
             # pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
             pos2 = -1 if props is None else self._props_op(props) + 1
-            return (seq, ref, msn, int(op["pos1"]), pos2, off, n, client, MT_INSERT, 0)
+            return (seq, ref, msn, p1, pos2, off, n, client, MT_INSERT, rel)
         if t == MT_REMOVE:
-            return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_REMOVE, 0)
+            p1, p2, rel = self._positions(op)
+            return (seq, ref, msn, p1, p2, 0, 0, client, MT_REMOVE, rel)
         if t == MT_OBLITERATE:  # non-sided obliterate: {pos1, Before} .. {pos2 - 1, After}
             return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0, client, MT_OBLITERATE, 0)
         if t == MT_OBLITERATE_SIDED:  # places {pos, before} (client.ts:680-700); sides in flags
@@ -309,8 +343,9 @@ class MergeTreeStreamBuilder:
         if t == MT_ANNOTATE:
             if op.get("adjust") is not None:
                 raise UnsupportedOp("annotate adjust")
+            p1, p2, rel = self._positions(op)
             pid = self._props_op(op.get("props") or {})
-            return (seq, ref, msn, int(op["pos1"]), int(op["pos2"]), pid, 0, client, MT_ANNOTATE, 0)
+            return (seq, ref, msn, p1, p2, pid, 0, client, MT_ANNOTATE, rel)
         raise UnsupportedOp(f"merge-tree op type {t}")
 
     def begin_doc(self, initial_text: str = "", observer: str = "A") -> _DocBuilder:
@@ -420,6 +455,8 @@ class MergeTreeStreamBuilder:
             messages=[list(d.messages) for d in self.docs] if self.keep_messages else [],
             snapshots=_snapshot_array(self.snapshots),
             snapshot_segs=np.array(self.snapshot_segs, dtype=SNAPSHOT_SEG_DTYPE),
+            relpos=np.array(self.relpos, dtype=RELPOS_DTYPE) if self.relpos else None,
+            marker_id_key=self.keys.ids.get(MARKER_ID_KEY, NO_MARKER) if self.relpos else NO_MARKER,
         )
 
 

@@ -101,6 +101,12 @@ extern "C" {
  * cachedLength 1, never appended to or onto (canAppend false); len = 1 and the one arena unit at
  * payload holds its refType (ReferenceType bit flags). */
 #define FMT_MT_F_MARKER 32u
+/* Legacy relative positions (ops.ts:115-117, IRelativePosition): the op's pos1 (REL1) / pos2 (REL2)
+ * was undefined and its relativePos1 / relativePos2 names a marker; the field then holds an index
+ * into fmt_mt_batch.relpos. Resolved in the op's perspective as posFromRelativePos does
+ * (mergeTree.ts:1462-1483, via client.ts:760-767 getValidOpRange). */
+#define FMT_MT_F_REL1 64u
+#define FMT_MT_F_REL2 128u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */
@@ -113,6 +119,19 @@ typedef struct fmt_mt_op {
   uint8_t type;     /* FMT_MT_* */
   uint32_t flags;   /* FMT_MT_F_* */
 } fmt_mt_op;
+
+/* An IRelativePosition {id, before, offset}: `marker_id` is the value id (props_kv dictionary) of the
+ * marker's id string, i.e. the value its "markerId" property holds (FMT_MT_NO_MARKER when the
+ * position names none); the position is the marker's start in the op's perspective, minus
+ * `offset` when `before`, else plus the marker's length (1) and `offset`. 16 bytes. */
+#define FMT_MT_NO_MARKER 0xffffffffu
+#define FMT_MT_REL_BEFORE 1u
+typedef struct fmt_mt_relpos {
+  uint32_t marker_id;
+  int32_t offset; /* 0 when the position has none */
+  uint32_t flags; /* FMT_MT_REL_BEFORE */
+  uint32_t pad;
+} fmt_mt_relpos;
 
 /* One SharedMap message: {"type":"set","key","value"} / "delete" / "clear"
  * (map/src/internalInterfaces.ts). 16 bytes. key = per-doc key id (< key_bound); value = id of the
@@ -170,6 +189,9 @@ typedef struct fmt_mt_batch {
   const fmt_mt_snapshot_doc* snapshots;   /* optional: n_docs entries, or NULL (f3: load from summary) */
   const fmt_mt_snapshot_seg* snapshot_segs;
   uint64_t n_snapshot_segs;
+  const fmt_mt_relpos* relpos;    /* optional: the relative positions FMT_MT_F_REL1/REL2 ops index, or NULL */
+  uint32_t n_relpos;
+  uint32_t marker_id_key;         /* key id of "markerId" (reservedMarkerIdKey), FMT_MT_NO_MARKER if none */
 } fmt_mt_batch;
 
 /* ---------------------------------------------------------------------------------------------

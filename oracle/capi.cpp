@@ -199,6 +199,9 @@ std::atomic<int> g_indexed{0};  // orc_set_index: replays use the remote-length 
 // The document's initial state: a loaded summary (f3) or its initial text, then collaboration.
 void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d) {
   if (g_indexed.load()) mt.enableIndex();
+  mt.relpos = b->relpos;
+  mt.nRelpos = b->relpos ? b->n_relpos : 0;
+  mt.markerIdKey = b->marker_id_key;
   if (b->snapshots != nullptr && b->snapshots[d].loaded) {
     const fmt_mt_snapshot_doc& sd = b->snapshots[d];
     std::vector<MergeTree::LoadedSeg> head, body;

@@ -665,9 +665,10 @@ void MergeTree::annotateRange(int start, int end,
 }
 
 // mergeTree.ts:835-856 getPosition: lengths of everything before the node, walking up the parents.
-int MergeTree::getPosition(const Node* node) const {
+int MergeTree::getPosition(const Node* node) const { return getPosition(node, localPerspective()); }
+
+int MergeTree::getPosition(const Node* node, const Perspective& lp) const {
   int total = 0;
-  const Perspective lp = localPerspective();
   const Node* prev = node;
   for (const Block* parent = node->parent; parent != nullptr; prev = parent, parent = parent->parent) {
     for (int i = 0; i < parent->childCount; i++) {
@@ -678,6 +679,32 @@ int MergeTree::getPosition(const Node* node) const {
     }
   }
   return total;
+}
+
+uint32_t markerIdOf(const Seg* s, uint32_t key) {  // Marker.getId(): properties[reservedMarkerIdKey]
+  if (!s->marker || key == FMT_MT_NO_MARKER) return FMT_MT_NO_MARKER;
+  for (const auto& [k, v] : s->props.kv)
+    if (k == key) return v;
+  return FMT_MT_NO_MARKER;
+}
+
+void MergeTree::registerMarker(Seg* s) {
+  const uint32_t id = markerIdOf(s, markerIdKey);
+  if (id != FMT_MT_NO_MARKER) idToMarker[id] = s;
+}
+
+void MergeTree::unlinkMarker(const Seg* s) {
+  const uint32_t id = markerIdOf(s, markerIdKey);
+  if (id != FMT_MT_NO_MARKER) idToMarker.erase(id);
+}
+
+int MergeTree::posFromRelativePos(const fmt_mt_relpos& rp, const Perspective& p) const {
+  const auto it = rp.marker_id == FMT_MT_NO_MARKER ? idToMarker.end() : idToMarker.find(rp.marker_id);
+  if (it == idToMarker.end()) return -1;
+  int pos = getPosition(it->second, p);
+  if (rp.flags & FMT_MT_REL_BEFORE) pos -= rp.offset;
+  else pos += it->second->len() + rp.offset;  // cachedLength (1 for a marker)
+  return pos;
 }
 
 // sequence.ts:395-452 createOpsFromDelta over one event's ranges, which SequenceDeltaEventClass
@@ -761,6 +788,7 @@ void MergeTree::loadSnapshot(const std::vector<LoadedSeg>& header, const std::ve
         }
       }
     }
+    if (s->marker) registerMarker(s);  // blockUpdate (mergeTree.ts:2833-2841): loaded markers are present
     return s;
   };
   // reloadFromSegments: bottom-up, MaxNodesInBlock - 1 = 7 children per block, layer by layer.
@@ -799,9 +827,18 @@ void MergeTree::startCollaboration(int localClientId, int minSeqArg, int current
 
 // client.ts:1291-1327 applyRemoteOp → applyInsertOp / applyRemoveRangeOp / applyAnnotateRangeOp
 // with PriorPerspective(refSeq, clientId) and stamp {seq, clientId} (client.ts:581-611).
-void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const uint32_t* propsOff,
+void MergeTree::applyRemote(const fmt_mt_op& opIn, const uint16_t* arena, const uint32_t* propsOff,
                             const uint32_t* propsKv) {
-  const Perspective p{false, op.ref_seq, op.client};
+  const Perspective p{false, opIn.ref_seq, opIn.client};
+  fmt_mt_op op = opIn;
+  // getValidOpRange (client.ts:758-767): an undefined pos1/pos2 comes from relativePos1/2
+  for (int k = 0; k < 2; k++) {
+    if ((op.flags & (k == 0 ? FMT_MT_F_REL1 : FMT_MT_F_REL2)) == 0) continue;
+    int32_t& pos = k == 0 ? op.pos1 : op.pos2;
+    if (pos < 0 || static_cast<uint32_t>(pos) >= nRelpos) throw DataError("relative position index out of range");
+    pos = posFromRelativePos(relpos[pos], p);
+    if (pos < 0) throw DataError("relative position names no marker");
+  }
   const Stamp stamp{op.seq, op.client};
   switch (op.type) {
     case FMT_MT_INSERT: {
@@ -826,6 +863,7 @@ void MergeTree::applyRemote(const fmt_mt_op& op, const uint16_t* arena, const ui
           }
         }
       }
+      if (s->marker) registerMarker(s);  // idToMarker.set (mergeTree.ts:1614-1620)
       insertSegments(op.pos1, s, p, stamp);
       break;
     }
@@ -920,6 +958,7 @@ void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {
       }
     } else {
       if (stampLte(seg->removes[0], minStamp)) {
+        if (seg->marker) unlinkMarker(seg);  // zamboni.ts:202-204
         seg->parent = nullptr;  // unlinked
       } else {
         hold.push_back(seg);

@@ -19,6 +19,7 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -212,6 +213,10 @@ class MergeTree {
   // (sequence.ts:395-452), tagged with catchupOp.
   std::vector<fmt_mt_catchup_range>* catchupOut = nullptr;
   uint32_t catchupOp = 0;
+  // Legacy relative positions (FMT_MT_F_REL1/REL2): the batch's table and the "markerId" key id.
+  const fmt_mt_relpos* relpos = nullptr;
+  uint32_t nRelpos = 0;
+  uint32_t markerIdKey = FMT_MT_NO_MARKER;
 
   // Readouts.
   std::u16string getText() const;     // MergeTreeTextHelper.ts:28-87 (local perspective)
@@ -260,6 +265,15 @@ class MergeTree {
   void ensureIntervalBoundary(int pos, const Perspective& p);
 
   int getPosition(const Node* node) const;  // mergeTree.ts:835-856, local perspective
+  int getPosition(const Node* node, const Perspective& p) const;
+  // mergeTree.ts:1462-1483 posFromRelativePos (-1 when the id names no marker)
+  int posFromRelativePos(const fmt_mt_relpos& rp, const Perspective& p) const;
+  // idToMarker (mergeTree.ts:675): marker id (value id of its "markerId" property) → marker; set when
+  // a marker is inserted (:1614-1620) or loaded (blockUpdate, :2833-2841), deleted when zamboni
+  // unlinks a marker (unlinkMarker, :738-743; zamboni.ts:202-204)
+  std::map<uint32_t, Seg*> idToMarker;
+  void registerMarker(Seg* s);
+  void unlinkMarker(const Seg* s);
   void recordDelta(uint32_t type, const std::vector<Seg*>& deltaSegs);
 
   template <class F>

@@ -31,6 +31,9 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     in.propsOff = b->props_off;
     in.propsKv = b->props_kv;
     in.nPropsOps = b->n_props_ops;
+    in.relpos = b->relpos;
+    in.nRelpos = b->relpos ? b->n_relpos : 0u;
+    in.markerKey = b->marker_id_key;
     if (b->snapshots && b->snapshots[d].loaded) {
       const fmt_mt_snapshot_doc sd = b->snapshots[d];
       in.snapSegs = b->snapshot_segs + sd.first_seg;

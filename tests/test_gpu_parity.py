@@ -556,3 +556,21 @@ def test_mt_bulk_legacy_summary_of_a_huge_document(orc, engine):
     engine.mt_summarize_legacy(batch.keys, batch.values)
     lv, ch, pr = engine.mt_doc(0, hdrs[0])
     assert engine.mt_summary(0) == legacy_summary(hdrs[0], lv, ch, pr, batch.keys, batch.values)
+
+
+def test_mt_relative_positions_on_gpu(orc, engine):
+    """Legacy relativePos1/2 ops (marker-relative positions resolved in the op's perspective): the
+    hand cases and generated collaborative streams (markers with their own prop sets, so the runtime
+    escalates most of them to the large tier) == the oracle bit for bit."""
+    from test_relative_pos import _batch, hand_cases, relative_farm
+    from mt_compare import visible_text
+
+    cases = hand_cases()
+    batch = _batch(cases)
+    hdrs = _check_against_oracle(orc, engine, batch)
+    for d, (_, _, want) in enumerate(cases):
+        leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+        assert visible_text(hdrs[d], leaves, chars) == want
+    farm, _ = relative_farm()
+    hdrs = _check_against_oracle(orc, engine, farm)
+    assert (hdrs["status"] == 0).all()

@@ -214,3 +214,50 @@ def test_js_v1_summaries_on_gpu(addon, orc):
         head, bodies = summary.v1_summary(h[d], leaves[d], chars[d], props[d], batch.keys, batch.values,
                                           batch.clients[d], orc.mt_removers(batch, d))
         assert got[d]["header"] == head and got[d]["bodies"] == bodies, d
+
+
+def _relative_messages():
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_relative_pos import hand_cases
+
+    return hand_cases()
+
+
+def test_js_packer_relative_positions_match_python(addon):
+    """relativePos1/2 pack as FMT_MT_F_REL1/REL2 ops indexing the relpos table, with the marker id
+    interned as the value its "markerId" property holds, identically in the JS and Python packers."""
+    from test_relative_pos import _batch
+
+    cases = _relative_messages()
+    docs = [{"init": init, "msgs": msgs} for msgs, init, _ in cases]
+    js = (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          "const b=new fmt.MergeTreeStreamBuilder();"
+          f"for(const x of {json.dumps(docs)}){{const d=b.beginDoc(x.init,'A');for(const m of x.msgs) d.addMessage(m);}}"
+          "const r=b.finish();const hex=(a)=>Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
+          "process.stdout.write(JSON.stringify({ops:hex(r.ops),relpos:hex(r.relpos),key:r.markerIdKey,"
+          "keys:r.keys,values:r.values}))")
+    r = _node("-e", js)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    py = _batch(cases)
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert bytes.fromhex(out["relpos"]) == py.relpos.tobytes()
+    assert out["key"] == py.marker_id_key and out["keys"] == py.keys and out["values"] == py.values
+
+
+@pytest.mark.gpu
+def test_js_relative_positions_on_gpu(addon):
+    """The JS driver replays relativePos ops through the addon; getText equals the hand cases."""
+    cases = _relative_messages()
+    docs = [{"init": init, "msgs": msgs} for msgs, init, _ in cases]
+    js = (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          "(async()=>{const b=new fmt.MergeTreeStreamBuilder();"
+          f"for(const x of {json.dumps(docs)}){{const d=b.beginDoc(x.init,'A');for(const m of x.msgs) d.addMessage(m);}}"
+          "const e=new fmt.Engine(0);const r=await e.replayMergeTree(b.finish());"
+          f"const t=[];for(let i=0;i<{len(cases)};i++) t.push(r.getText(i));e.close();"
+          "process.stdout.write(JSON.stringify(t));})().catch((e)=>{console.error(e);process.exit(1);});")
+    r = _node("-e", js, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout) == [want for _, _, want in cases]

@@ -1,0 +1,166 @@
+"""Legacy relative positions (relativePos1/2, ops.ts:115-117): positions named by a marker id and
+resolved in the op's perspective (mergeTree.ts:1462-1483 posFromRelativePos, via client.ts:758-767).
+
+No reference fixture holds such messages (current SharedString resolves insertTextRelative locally
+and sends a number, sharedString.ts:160-193), so the hand cases below state their expected text
+from the reference's rules; the engine (emulated here, on the GPU in test_gpu_parity.py) must equal
+the oracle bit for bit on them and on generated streams that mix relative and numeric ops.
+"""
+import numpy as np
+import pytest
+
+from fluidframework_amd.streams import MT_F_REL1, MT_F_REL2, MergeTreeStreamBuilder
+from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
+
+
+def _msg(client, seq, ref, contents, msn=0):
+    return {"clientId": client, "sequenceNumber": seq, "referenceSequenceNumber": ref, "minimumSequenceNumber": msn,
+            "contents": contents}
+
+
+def _marker(pos, mid, ref_type=1):
+    return {"type": 0, "pos1": pos, "seg": {"marker": {"refType": ref_type}, "props": {"markerId": mid}}}
+
+
+def hand_cases():
+    """(messages, initial text, expected final text) per document."""
+    cases = []
+    # after the marker (+ its length 1), with and without an offset
+    cases.append(([_msg("B", 1, 0, _marker(1, "m1")),
+                   _msg("B", 2, 1, {"type": 0, "relativePos1": {"id": "m1"}, "seg": "X"}),
+                   _msg("B", 3, 2, {"type": 0, "relativePos1": {"id": "m1", "offset": 2}, "seg": "Y"})],
+                  "abc", "aXbYc"))
+    # before the marker, minus an offset
+    cases.append(([_msg("B", 1, 0, _marker(2, "m1")),
+                   _msg("C", 2, 1, {"type": 0, "relativePos1": {"id": "m1", "before": True}, "seg": "X"}),
+                   _msg("C", 3, 2, {"type": 0, "relativePos1": {"id": "m1", "before": True, "offset": 2},
+                                    "seg": "Y"})],
+                  "abcd", "aYbXcd"))
+    # the op's perspective: C has not seen B's "ZZ" insert at 0 (ref 1), so its position after the
+    # marker is 2 in its own view, and the insert lands right after the marker
+    cases.append(([_msg("B", 1, 0, _marker(1, "m1")),
+                   _msg("B", 2, 1, {"type": 0, "pos1": 0, "seg": "ZZ"}),
+                   _msg("C", 3, 1, {"type": 0, "relativePos1": {"id": "m1"}, "seg": "X"})],
+                  "abc", "ZZaXbc"))
+    # remove and annotate ranges between two markers
+    cases.append(([_msg("B", 1, 0, _marker(1, "s")),
+                   _msg("B", 2, 1, _marker(5, "e")),
+                   _msg("C", 3, 2, {"type": 1, "relativePos1": {"id": "s"}, "relativePos2": {"id": "e", "before": True}}),
+                   _msg("C", 4, 3, {"type": 2, "relativePos1": {"id": "s", "before": True}, "pos2": 4,
+                                    "props": {"bold": True}})],
+                  "abcdefg", "aefg"))
+    # pos1 given wins over relativePos1 (getValidOpRange takes the number when defined)
+    cases.append(([_msg("B", 1, 0, _marker(3, "m")),
+                   _msg("B", 2, 1, {"type": 0, "pos1": 0, "relativePos1": {"id": "m"}, "seg": "Q"})],
+                  "xyz", "Qxyz"))
+    return cases
+
+
+def _batch(cases):
+    b = MergeTreeStreamBuilder()
+    for msgs, init, _ in cases:
+        d = b.begin_doc(init)
+        for m in msgs:
+            d.add_message(m)
+    return b.finish()
+
+
+def test_packer_flags_relative_positions():
+    batch = _batch(hand_cases())
+    rel = (batch.ops["flags"] & (MT_F_REL1 | MT_F_REL2)) != 0
+    assert rel.sum() == 7 and batch.relpos is not None and len(batch.relpos) == 8
+    assert batch.keys[batch.marker_id_key] == "markerId"
+
+
+def test_oracle_hand_cases(orc):
+    cases = hand_cases()
+    batch = _batch(cases)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=4096, cap_chars=1 << 16, cap_props=64)
+    assert rc == 0
+    for d, (_, _, want) in enumerate(cases):
+        assert visible_text(oh[d], ol[d], oc[d]) == want, d
+
+
+def test_engine_hand_cases(orc):
+    cases = hand_cases()
+    batch = _batch(cases)
+    cl, cc, cp = emu_caps()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    hdr, leaves, chars, props = emu_replay(batch)
+    for d, (_, _, want) in enumerate(cases):
+        assert visible_text(hdr[d], leaves[d], chars[d]) == want, d
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_unknown_marker_id_is_a_data_error(orc):
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc("abc")
+    d.add_message(_msg("B", 1, 0, {"type": 0, "relativePos1": {"id": "nope"}, "seg": "X"}))
+    batch = b.finish()
+    rc, oh, *_ = orc.mt_replay_batch(batch, cap_leaves=64, cap_chars=64, cap_props=8)
+    assert oh[0]["status"] == -2 and oh[0]["fail_seq"] == 1
+    hdr, *_ = emu_replay(batch)
+    assert hdr[0]["status"] == -2 and hdr[0]["fail_seq"] == 1
+
+
+def relative_farm(n_docs=24, n_ops=400, seed=3):
+    """Generated collaborative streams: clients insert markers with unique ids and then insert,
+    remove and annotate relative to markers they have seen (positions resolved against what each
+    client had seen, so every op is valid in its own perspective)."""
+    import oracle as orc
+
+    rng = np.random.default_rng(seed)
+    b = MergeTreeStreamBuilder()
+    for doc in range(n_docs):
+        d = b.begin_doc("seed text for relative positions")
+        names = ["B", "C", "D"]
+        markers = []  # (id, seq inserted)
+        seq, msn = 0, 0
+        for k in range(n_ops):
+            seq += 1
+            client = names[int(rng.integers(0, 3))]
+            lag = int(rng.integers(0, 4))
+            ref = max(msn, seq - 1 - lag)
+            seen = [m for m, s in markers if s <= ref]
+            r = rng.random()
+            if r < 0.15 or not seen:
+                mid = f"d{doc}m{k}"
+                op = _marker(0, mid)
+                markers.append((mid, seq))
+                op["pos1"] = 0
+            elif r < 0.55:
+                rp = {"id": seen[int(rng.integers(0, len(seen)))], "before": bool(rng.integers(0, 2))}
+                if rng.random() < 0.3:
+                    rp["offset"] = 0
+                op = {"type": 0, "relativePos1": rp, "seg": "xy"[: int(rng.integers(1, 3))]}
+            elif r < 0.8:
+                a = seen[int(rng.integers(0, len(seen)))]
+                op = {"type": 1, "relativePos1": {"id": a, "before": True}, "relativePos2": {"id": a}}
+                markers = [m for m in markers if m[0] != a]  # no later op names a removed marker
+            else:
+                a = seen[int(rng.integers(0, len(seen)))]
+                op = {"type": 2, "relativePos1": {"id": a, "before": True}, "relativePos2": {"id": a},
+                      "props": {"k": int(rng.integers(0, 3))}}
+            if k % 17 == 16:
+                msn = max(msn, seq - 8)
+            d.add_message(_msg(client, seq, ref, op, msn))
+    batch = b.finish()
+    rc, oh, *_ = orc.mt_replay_batch(batch, threads=8, outputs=False)
+    return batch, oh
+
+
+def test_engine_matches_oracle_on_relative_farm(orc):
+    batch, oh_status = relative_farm()
+    ok = oh_status["status"] == 0
+    assert ok.all(), (oh_status["status"], oh_status["fail_seq"])
+    # every marker carries its own prop set ({markerId}): most documents outgrow the small tier's
+    # 32 prop sets and replay in the large tier, as the runtime escalates them on the GPU
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    hdr, leaves, chars, props = emu_replay(batch, large=True)
+    for d in range(batch.n_docs):
+        assert hdr[d]["status"] == oh[d]["status"] and hdr[d]["fail_seq"] == oh[d]["fail_seq"], d
+        if oh[d]["status"] == 0:
+            diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+            assert not diffs, f"doc {d}: {diffs[:5]}"
