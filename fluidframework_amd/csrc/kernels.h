@@ -34,6 +34,8 @@ struct MtDeviceBatch {
   const fmt_mt_snapshot_doc* snapshots;  // per-doc summary loads, or nullptr
   const fmt_mt_snapshot_seg* snapshotSegs;
   const uint64_t* rmOrderOffsets;  // per-doc remove-order slab offsets (nDocs + 1), or nullptr
+  const fmt_mt_snapshot_info* snapshotInfo;  // SnapshotV1 merge info per snapshot segment, or nullptr
+  const fmt_mt_stamp* snapshotStamps;
   const fmt_mt_relpos* relpos;     // relative positions (FMT_MT_F_REL1/REL2 ops), or nullptr
   uint32_t nRelpos;
   uint32_t markerKey;              // key id of "markerId", FMT_MT_NO_MARKER if none

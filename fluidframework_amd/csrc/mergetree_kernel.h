@@ -72,6 +72,8 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     if (batch.snapshots && batch.snapshots[d].loaded) {
       const fmt_mt_snapshot_doc sd = batch.snapshots[d];
       in.snapSegs = batch.snapshotSegs + sd.first_seg;
+      in.snapInfo = batch.snapshotInfo ? batch.snapshotInfo + sd.first_seg : nullptr;
+      in.snapStamps = batch.snapshotStamps;
       in.nHeader = sd.n_header;
       in.nBody = sd.n_body;
       in.snapMinSeq = sd.min_seq;
@@ -79,6 +81,8 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
       in.loaded = 1;
     } else {
       in.snapSegs = nullptr;
+      in.snapInfo = nullptr;
+      in.snapStamps = nullptr;
       in.nHeader = in.nBody = 0;
       in.snapMinSeq = in.snapSeq = 0;
       in.loaded = 0;

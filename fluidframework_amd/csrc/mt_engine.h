@@ -171,6 +171,8 @@ struct DocInputs {
   uint32_t nHeader, nBody;
   int32_t snapMinSeq, snapSeq;
   uint32_t loaded;
+  const fmt_mt_snapshot_info* snapInfo;  // SnapshotV1 merge info parallel to snapSegs, or nullptr
+  const fmt_mt_stamp* snapStamps;
   const fmt_mt_relpos* relpos;  // FMT_MT_F_REL1/REL2 ops index it (nullptr: none in the batch)
   uint32_t nRelpos;
   uint32_t markerKey;           // key id of "markerId"
@@ -1997,6 +1999,50 @@ class Doc {
     }
   }
 
+  // SnapshotV1 merge info (specToSegment, snapshotLoader.ts:105-175) of header segments: the insert
+  // stamp, and the remove stamps folded into the leaf's first remove seq and remove-client set.
+  FMT_DEV bool loadMergeInfo(int H, int N) {
+    const int nr = (N + 63) >> 6;
+    Lane<bool> bad, wide;  // body-chunk merge info (host-rejected); more writers than this tier holds
+    FOR_LANES(l) {
+      LANE(bad) = false;
+      LANE(wide) = false;
+    }
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        if (j < N) {
+          const fmt_mt_snapshot_info inf = in.snapInfo[j];
+          if (j >= H && (inf.ins_seq != 0 || inf.rm_count != 0)) LANE(bad) = true;
+          int32_t rm = kNotRemoved;
+          uint64_t mask = 0;
+          for (uint32_t t = 0; t < inf.rm_count; t++) {
+            const fmt_mt_stamp st = in.snapStamps[inf.rm_first + t];
+            rm = st.seq < rm ? st.seq : rm;
+            if (st.client < 0 || st.client > kMaxClient) LANE(wide) = true;
+            else mask |= 1ull << st.client;
+          }
+          if (inf.ins_client > kMaxClient) LANE(wide) = true;
+          LANE(W[1])[r] = static_cast<uint32_t>(inf.ins_seq);
+          LANE(W[2])[r] = static_cast<uint32_t>(rm);
+          LANE(W[3])[r] = static_cast<uint32_t>(mask);
+          if constexpr (kWords > 5) LANE(W[5])[r] = static_cast<uint32_t>(mask >> 32);
+          const uint32_t w4 = LANE(W[4])[r];
+          LANE(W[4])[r] = mkW4(fId(w4), inf.ins_client) | (w4 & kW4Marker);
+        }
+      }
+    }
+    if (ballot(bad) != 0) {
+      fail(FMT_E_UNSUPPORTED);
+      return false;
+    }
+    if (ballot(wide) != 0) {
+      fail(FMT_E_CAPACITY);
+      return false;
+    }
+    return true;
+  }
+
   FMT_DEV void loadSnapshot() {
     const int H = static_cast<int>(in.nHeader), N = static_cast<int>(in.nHeader + in.nBody);
     if (N > kCapLeaves) {
@@ -2040,6 +2086,7 @@ class Doc {
       }
     }
     waveSync();
+    if (in.snapInfo != nullptr && !loadMergeInfo(H, N)) return;
     nextId = static_cast<uint32_t>(N + 1);
     if (H > 0) {  // reloadFromSegments: leaf blocks [0, cnt), then each level above
       int lo = 0, cnt = (H + 6) / 7;

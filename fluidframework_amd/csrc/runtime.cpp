@@ -89,6 +89,9 @@ struct fmt_ctx {
   DevBuf<fmt_mt_snapshot_doc> mtSnap;       // per-doc summary loads (f3)
   DevBuf<fmt_mt_snapshot_seg> mtSnapSegs;
   DevBuf<fmt_mt_relpos> mtRelpos;            // relative positions (FMT_MT_F_REL1/REL2 ops)
+  DevBuf<fmt_mt_snapshot_info> mtSnapInfo;   // SnapshotV1 merge info of loaded segments
+  DevBuf<fmt_mt_stamp> mtSnapStamps;
+  bool mtHasSnapInfo = false;
   uint32_t mtNRelpos = 0, mtMarkerKey = FMT_MT_NO_MARKER;
   bool mtHasSnap = false;
   bool mtObliterate = false;                 // batch holds obliterates: launch the Doc<true> kernel
@@ -212,6 +215,8 @@ void fmt_close(fmt_ctx* c) {
   c->mtSnap.release();
   c->mtSnapSegs.release();
   c->mtRelpos.release();
+  c->mtSnapInfo.release();
+  c->mtSnapStamps.release();
   c->mtCuOffs.release();
   c->mtCatchup.release();
   c->mtRmOffs.release();
@@ -556,6 +561,13 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtSnap.p, b->snapshots, n * sizeof(fmt_mt_snapshot_doc)));
     FMT_HIP(c, cp(c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg)));
   }
+  c->mtHasSnapInfo = c->mtHasSnap && b->snapshot_info != nullptr;
+  if (c->mtHasSnapInfo) {
+    FMT_HIP(c, c->mtSnapInfo.reserve(b->n_snapshot_segs));
+    FMT_HIP(c, c->mtSnapStamps.reserve(b->n_snapshot_stamps));
+    FMT_HIP(c, cp(c->mtSnapInfo.p, b->snapshot_info, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_info)));
+    FMT_HIP(c, cp(c->mtSnapStamps.p, b->snapshot_stamps, b->n_snapshot_stamps * sizeof(fmt_mt_stamp)));
+  }
   c->mtNRelpos = b->relpos ? b->n_relpos : 0u;
   c->mtMarkerKey = b->marker_id_key;
   if (c->mtNRelpos) {
@@ -602,6 +614,11 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       if (sd.n_body != 0)
         return setErr(c, FMT_E_UNSUPPORTED, "a document beyond the large tier must load from one header chunk (n_body = 0)");
       const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1], nOps = o1 - o0;
+      if (b->snapshot_info != nullptr) {
+        for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header; k++)
+          if (b->snapshot_info[k].ins_seq != 0 || b->snapshot_info[k].rm_count != 0)
+            return setErr(c, FMT_E_UNSUPPORTED, "SnapshotV1 merge info in a document beyond the large tier");
+      }
       for (uint64_t i = o0; i < o1; i++)
         if (b->ops[i].flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2))
           return setErr(c, FMT_E_UNSUPPORTED,
@@ -702,7 +719,9 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps,
                                 c->mtHasCatchup ? c->mtCuOffs.p : nullptr,
                                 c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr,
-                                c->mtHasRmOrder ? c->mtRmOffs.p : nullptr, c->mtNRelpos ? c->mtRelpos.p : nullptr,
+                                c->mtHasRmOrder ? c->mtRmOffs.p : nullptr,
+                                c->mtHasSnapInfo ? c->mtSnapInfo.p : nullptr, c->mtHasSnapInfo ? c->mtSnapStamps.p : nullptr,
+                                c->mtNRelpos ? c->mtRelpos.p : nullptr,
                                 c->mtNRelpos, c->mtMarkerKey};
   const bool plain = !c->mtObliterate && !c->mtHasRmOrder;
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,

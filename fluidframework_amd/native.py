@@ -57,7 +57,8 @@ LEAF_GONE = 0xFFFFFFFF
 
 CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("type", "<u4")])
 
-from .streams import NO_MARKER, RELPOS_DTYPE, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE  # noqa: E402  (include/fmt.h layouts)
+from .streams import (NO_MARKER, RELPOS_DTYPE, SNAPSHOT_DOC_DTYPE, SNAPSHOT_INFO_DTYPE, SNAPSHOT_SEG_DTYPE,  # noqa: E402
+                      STAMP_DTYPE)  # (include/fmt.h layouts)
 
 PROPS_MAX = 8
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
@@ -85,6 +86,9 @@ class FmtMtBatch(ctypes.Structure):
         ("relpos", ctypes.c_void_p),
         ("n_relpos", ctypes.c_uint32),
         ("marker_id_key", ctypes.c_uint32),
+        ("snapshot_info", ctypes.c_void_p),
+        ("snapshot_stamps", ctypes.c_void_p),
+        ("n_snapshot_stamps", ctypes.c_uint64),
     ]
 
 
@@ -141,6 +145,14 @@ def batch_struct(batch):
     )
     if rel is not None:
         keep.append(rel)
+    info = getattr(batch, "snapshot_info", None)
+    if snaps is not None and info is not None:
+        inf = np.ascontiguousarray(info, dtype=SNAPSHOT_INFO_DTYPE)
+        st = getattr(batch, "snapshot_stamps", None)
+        stp = np.ascontiguousarray(st, dtype=STAMP_DTYPE) if st is not None and len(st) else np.zeros(1, STAMP_DTYPE)
+        b.snapshot_info, b.snapshot_stamps = _ptr(inf), _ptr(stp)
+        b.n_snapshot_stamps = 0 if st is None else len(st)
+        keep += [inf, stp]
     return b, keep
 
 

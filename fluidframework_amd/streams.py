@@ -44,6 +44,10 @@ SNAPSHOT_DOC_DTYPE = np.dtype([("first_seg", "<u8"), ("n_header", "<u4"), ("n_bo
                                ("min_seq", "<i4"), ("seq", "<i4"), ("loaded", "<u4"), ("pad", "<u4")])
 assert SNAPSHOT_DOC_DTYPE.itemsize == 32
 SNAPSHOT_SEG_DTYPE = np.dtype([("text", "<u4"), ("len", "<u4"), ("props", "<u4")])
+# fmt_mt_snapshot_info / fmt_mt_stamp: SnapshotV1 merge info of loaded header segments
+SNAPSHOT_INFO_DTYPE = np.dtype([("ins_seq", "<i4"), ("ins_client", "<i4"), ("rm_first", "<u4"), ("rm_count", "<u4")])
+STAMP_DTYPE = np.dtype([("seq", "<i4"), ("client", "<i4"), ("kind", "<u4"), ("pad", "<u4")])
+NON_COLLAB_CLIENT = -2  # fmt.h FMT_NON_COLLAB_CLIENT
 assert SNAPSHOT_SEG_DTYPE.itemsize == 12
 NO_PROPS = 0xFFFFFFFF
 
@@ -183,6 +187,9 @@ class MergeTreeBatch:
     # optional (legacy relativePos1/2): RELPOS_DTYPE table and the key id of "markerId"
     relpos: np.ndarray | None = None
     marker_id_key: int = NO_MARKER
+    # optional (SnapshotV1 merge info): per snapshot segment SNAPSHOT_INFO_DTYPE, and the stamps
+    snapshot_info: np.ndarray | None = None
+    snapshot_stamps: np.ndarray | None = None
 
     @property
     def n_docs(self) -> int:
@@ -250,6 +257,9 @@ class MergeTreeStreamBuilder:
         self.snapshots: list[tuple] = []  # per doc: (first_seg, n_header, n_body, min_seq, seq, loaded)
         self.snapshot_segs: list[tuple] = []
         self.relpos: list[tuple] = []  # (marker value id, offset, flags, 0)
+        self.snapshot_info: list[tuple] = []  # per snapshot segment: (ins_seq, ins_client, rm_first, rm_count)
+        self.snapshot_stamps: list[tuple] = []  # (seq, client, kind, 0)
+        self.has_merge_info = False
 
     def _relpos(self, rp: dict) -> int:
         """An IRelativePosition {id?, before?, offset?}: its row in the relpos table. The id is looked
@@ -379,8 +389,9 @@ class MergeTreeStreamBuilder:
         as a list, toLatestVersion snapshotChunks.ts:151-180) and, optionally, the legacy catchupOps
         blob, whose messages are added as the first ops after validation as
         SharedSegmentSequence.loadCore does (sequence.ts:818-863). The loading client is `observer`
-        (short id 0). V1 segments that carry merge info (seq/client/removed stamps above minSeq) are
-        not supported by this loader."""
+        (short id 0). V1 header-chunk segments that carry merge info (seq/client/removed and moved
+        stamps above minSeq) load with their stamps as specToSegment builds them
+        (snapshotLoader.ts:105-175); body-chunk segments with merge info are not supported."""
         h = json.loads(header)
         md = h.get("headerMetadata")
         if md is None:
@@ -393,19 +404,24 @@ class MergeTreeStreamBuilder:
         def specs(c):
             return c["segments"] if c.get("version") == "1" else c["segmentTexts"]
 
+        d = _DocBuilder(self, observer)
         first = len(self.snapshot_segs)
-        for c in chunks:
+        for ci, c in enumerate(chunks):
             for spec in specs(c):
-                if isinstance(spec, dict) and "json" in spec:
-                    raise UnsupportedOp("SnapshotV1 segments with merge info")
+                info = (0, NON_COLLAB_CLIENT, 0, 0)
+                if isinstance(spec, dict) and "json" in spec:  # hasMergeInfo
+                    if ci > 0:
+                        raise UnsupportedOp("SnapshotV1 body-chunk segments with merge info")
+                    info = self._merge_info(spec, d)
+                    spec = spec["json"]
                 self.snapshot_segs.append(self._spec(spec))
+                self.snapshot_info.append(info)
         n_header = len(specs(h))
         n_body = len(self.snapshot_segs) - first - n_header
         if n_header + n_body != md["totalSegmentCount"]:
             raise ValueError("Mismatch in totalSegmentCount")  # snapshotLoader.ts:272-275
         seq = int(md["sequenceNumber"])
         min_seq = int(md.get("minSequenceNumber", seq))
-        d = _DocBuilder(self, observer)
         self.docs.append(d)
         self.doc_init.append((0, 0))
         self.snapshots.append((first, n_header, n_body, min_seq, seq, 1))
@@ -418,6 +434,32 @@ class MergeTreeStreamBuilder:
                 cur = m["sequenceNumber"]
                 d.add_message(m)
         return d
+
+    def _merge_info(self, spec: dict, d: _DocBuilder) -> tuple:
+        """specToSegment's stamps (snapshotLoader.ts:105-175): insert {seq ?? 0, client ?? NonCollab};
+        setRemove stamps at removedSeq for every removedClientIds entry (removedClient alone in the
+        back-compat format), sliceRemove stamps movedSeqs[i] / movedClientIds[i], sorted by seq
+        (opstampUtils.compare; Array.prototype.sort is stable)."""
+        self.has_merge_info = True
+        ins_seq = int(spec.get("seq", 0))
+        ins_client = d.short_client(spec["client"]) if spec.get("client") is not None else NON_COLLAB_CLIENT
+        stamps = []
+        if spec.get("removedSeq") is not None:
+            ids = spec.get("removedClientIds")
+            if ids is None and spec.get("removedClient") is not None:
+                ids = [spec["removedClient"]]
+            if ids is None:
+                raise ValueError("must have removedClient ids")  # 0xaac
+            stamps += [(int(spec["removedSeq"]), d.short_client(c), 0) for c in ids]
+        if spec.get("movedSeq") is not None:
+            seqs, ids = spec.get("movedSeqs"), spec.get("movedClientIds")
+            if seqs is None or ids is None or len(seqs) != len(ids):
+                raise ValueError("must have movedIds ids")  # 0xaa5 / 0xb5f
+            stamps += [(int(s), d.short_client(c), 1) for s, c in zip(seqs, ids)]
+        stamps.sort(key=lambda x: x[0])
+        first = len(self.snapshot_stamps)
+        self.snapshot_stamps += [(s, c, k, 0) for s, c, k in stamps]
+        return (ins_seq, ins_client, first, len(stamps))
 
     def finish(self, catchup: bool = False, remove_order: bool = False) -> MergeTreeBatch:
         """The packed batch. With `catchup`, ops of messages that stay in the legacy summary's
@@ -456,6 +498,8 @@ class MergeTreeStreamBuilder:
             snapshots=_snapshot_array(self.snapshots),
             snapshot_segs=np.array(self.snapshot_segs, dtype=SNAPSHOT_SEG_DTYPE),
             relpos=np.array(self.relpos, dtype=RELPOS_DTYPE) if self.relpos else None,
+            snapshot_info=np.array(self.snapshot_info, dtype=SNAPSHOT_INFO_DTYPE) if self.has_merge_info else None,
+            snapshot_stamps=np.array(self.snapshot_stamps, dtype=STAMP_DTYPE) if self.has_merge_info else None,
             marker_id_key=self.keys.ids.get(MARKER_ID_KEY, NO_MARKER) if self.relpos else NO_MARKER,
         )
 

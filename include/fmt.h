@@ -173,6 +173,26 @@ typedef struct fmt_mt_snapshot_seg {
   uint32_t props; /* props-op id whose (key, value) pairs are the segment's properties, or FMT_MT_NO_PROPS */
 } fmt_mt_snapshot_seg;
 
+/* SnapshotV1 merge info of a loaded segment (IJSONSegmentWithMergeInfo, snapshotLoader.ts:105-175
+ * specToSegment), parallel to fmt_mt_snapshot_seg: its insert stamp (seq 0 and client
+ * FMT_NON_COLLAB_CLIENT for a segment without merge info) and its remove stamps
+ * snapshot_stamps[rm_first .. rm_first + rm_count) in stamp order. 16 bytes. Header-chunk segments
+ * only (reloadFromSegments places them as they are). */
+typedef struct fmt_mt_snapshot_info {
+  int32_t ins_seq;
+  int32_t ins_client; /* short client id, or FMT_NON_COLLAB_CLIENT */
+  uint32_t rm_first;
+  uint32_t rm_count;
+} fmt_mt_snapshot_info;
+/* One remove stamp of a loaded segment: setRemove stamps carry the spec's removedSeq for every
+ * removedClientIds entry, sliceRemove stamps movedSeqs[i] / movedClientIds[i]. 16 bytes. */
+typedef struct fmt_mt_stamp {
+  int32_t seq;
+  int32_t client;
+  uint32_t kind; /* FMT_MT_RM_SET / FMT_MT_RM_SLICE */
+  uint32_t pad;
+} fmt_mt_stamp;
+
 /* A batch of merge-tree documents. Pointers are HOST pointers for fmt_mt_load(). */
 typedef struct fmt_mt_batch {
   const fmt_mt_op* ops;           /* all ops, documents contiguous and in seq order */
@@ -192,6 +212,9 @@ typedef struct fmt_mt_batch {
   const fmt_mt_relpos* relpos;    /* optional: the relative positions FMT_MT_F_REL1/REL2 ops index, or NULL */
   uint32_t n_relpos;
   uint32_t marker_id_key;         /* key id of "markerId" (reservedMarkerIdKey), FMT_MT_NO_MARKER if none */
+  const fmt_mt_snapshot_info* snapshot_info; /* optional: n_snapshot_segs entries (V1 merge info), or NULL */
+  const fmt_mt_stamp* snapshot_stamps;
+  uint64_t n_snapshot_stamps;
 } fmt_mt_batch;
 
 /* ---------------------------------------------------------------------------------------------

@@ -215,6 +215,14 @@ void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d) {
         for (uint32_t t = b->props_off[sg.props]; t < b->props_off[sg.props + 1]; t++)
           l.props.emplace_back(static_cast<uint16_t>(b->props_kv[t] >> 16), static_cast<uint16_t>(b->props_kv[t] & 0xffff));
       }
+      if (b->snapshot_info != nullptr) {  // SnapshotV1 merge info (header segments)
+        const fmt_mt_snapshot_info& inf = b->snapshot_info[sd.first_seg + k];
+        l.ins = orc::Stamp{inf.ins_seq, inf.ins_client};
+        for (uint32_t t = 0; t < inf.rm_count; t++) {
+          const fmt_mt_stamp& st = b->snapshot_stamps[inf.rm_first + t];
+          l.removes.push_back(orc::Stamp{st.seq, st.client, static_cast<int>(st.kind)});
+        }
+      }
       (k < sd.n_header ? head : body).push_back(std::move(l));
     }
     mt.loadSnapshot(head, body, sd.min_seq, sd.seq);

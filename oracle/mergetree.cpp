@@ -773,7 +773,8 @@ void MergeTree::loadSnapshot(const std::vector<LoadedSeg>& header, const std::ve
     Seg* s = makeSeg();
     s->text = l.text;
     s->marker = l.marker;
-    s->ins = Stamp{0, kNonCollabClient};
+    s->ins = l.ins;
+    s->removes = l.removes;
     if (l.hasProps) {
       s->props.defined = true;
       for (const auto& [key, value] : l.props) {

@@ -182,6 +182,8 @@ class MergeTree {
     bool marker = false;  // {"marker": {"refType"}}: text = the refType unit
     bool hasProps = false;
     std::vector<std::pair<uint16_t, uint16_t>> props;
+    Stamp ins{0, kNonCollabClient};  // SnapshotV1 merge info (specToSegment, snapshotLoader.ts:105-175)
+    std::vector<Stamp> removes;      // in stamp order
   };
   // SnapshotLoader (snapshotLoader.ts:59-348): header segments rebuild the tree
   // (reloadFromSegments, mergeTree.ts:751-800), collaboration starts at (minSeq, seq), body segments

@@ -37,6 +37,8 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     if (b->snapshots && b->snapshots[d].loaded) {
       const fmt_mt_snapshot_doc sd = b->snapshots[d];
       in.snapSegs = b->snapshot_segs + sd.first_seg;
+      in.snapInfo = b->snapshot_info ? b->snapshot_info + sd.first_seg : nullptr;
+      in.snapStamps = b->snapshot_stamps;
       in.nHeader = sd.n_header;
       in.nBody = sd.n_body;
       in.snapMinSeq = sd.min_seq;
@@ -44,6 +46,8 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
       in.loaded = 1;
     } else {
       in.snapSegs = nullptr;
+      in.snapInfo = nullptr;
+      in.snapStamps = nullptr;
       in.nHeader = in.nBody = 0;
       in.snapMinSeq = in.snapSeq = 0;
       in.loaded = 0;

@@ -574,3 +574,17 @@ def test_mt_relative_positions_on_gpu(orc, engine):
     farm, _ = relative_farm()
     hdrs = _check_against_oracle(orc, engine, farm)
     assert (hdrs["status"] == 0).all()
+
+
+def test_mt_v1_merge_info_load_on_gpu(orc, engine):
+    """SnapshotV1 summaries with merge info (mid-stream summaries of the reference's replay fixtures)
+    load with their stamps and replay the remaining messages: engine == oracle bit for bit, and the
+    final text is the fixture's resultText."""
+    from mt_compare import visible_text
+    from test_snapshot_v1 import v1_reload_batches
+
+    batch, expected = v1_reload_batches()
+    hdrs = _check_against_oracle(orc, engine, batch)
+    for d, want in enumerate(expected):
+        leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+        assert visible_text(hdrs[d], leaves, chars) == want, d

@@ -10,13 +10,15 @@ collaborative documents, which no reference fixture holds: that part is pinned b
 (it keeps every remove stamp in order, stamps.ts:144-158). The engine's remove-order slab
 (FMT_MT_F_RMORDER) plus the first remover's op give the same ordered lists and the same bytes.
 """
+import json
+
 import numpy as np
 import pytest
 
 from fluidframework_amd import summary
 from fluidframework_amd.streams import MergeTreeStreamBuilder, UnsupportedOp, flag_remove_order
 from golden_data import snapshot_trees
-from mt_compare import compare_doc, emu_caps, emu_replay
+from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
 from test_catchup import fixture_batch
 
 NAMES = ["headerOnly", "headerAndBody", "largeBody", "withAnnotations", "withMarkers"]
@@ -69,12 +71,26 @@ def test_engine_large_tier_v1_fixture_round_trip(name):
     assert summary.v1_summary(eh[0], el[0], ec[0], ep[0], batch.keys, batch.values, batch.clients[0], {}) == (head, bodies)
 
 
-def test_v1_merge_info_segments_are_not_loadable():
-    head = ('{"version":"1","segmentCount":1,"length":1,"segments":[{"json":"a","seq":3,"client":"B"}],'
-            '"startIndex":0,"headerMetadata":{"minSequenceNumber":1,"sequenceNumber":3,'
-            '"orderedChunkMetadata":[{"id":"header"}],"totalLength":1,"totalSegmentCount":1}}')
-    with pytest.raises(UnsupportedOp):
-        MergeTreeStreamBuilder().begin_doc_from_summary(head, [])
+def test_v1_merge_info_segments_load_with_their_stamps():
+    """specToSegment (snapshotLoader.ts:105-175): the insert stamp from seq/client; setRemove stamps
+    at removedSeq for every removedClientIds entry (removedClient alone in the back-compat format);
+    sliceRemove stamps from movedSeqs/movedClientIds; all sorted by seq."""
+    segs = [{"json": "a", "seq": 3, "client": "B"},
+            {"json": "bc", "removedSeq": 4, "removedClient": "C"},
+            {"json": "d", "seq": 2, "client": "C", "removedSeq": 5, "removedClient": "B", "removedClientIds": ["B", "D"],
+             "movedSeq": 4, "movedSeqs": [4, 6], "movedClientIds": ["D", "B"]}]
+    head = json.dumps({"version": "1", "segmentCount": 3, "length": 4, "segments": segs, "startIndex": 0,
+                       "headerMetadata": {"minSequenceNumber": 1, "sequenceNumber": 6,
+                                          "orderedChunkMetadata": [{"id": "header"}], "totalLength": 4,
+                                          "totalSegmentCount": 3}})
+    b = MergeTreeStreamBuilder()
+    b.begin_doc_from_summary(head, [])
+    batch = b.finish()
+    assert batch.clients[0] == ["snapshot", "B", "C", "D"]
+    info = [tuple(int(x) for x in r) for r in batch.snapshot_info]
+    assert info == [(3, 1, 0, 0), (0, -2, 0, 1), (2, 2, 1, 4)]
+    st = [tuple(int(x) for x in r)[:3] for r in batch.snapshot_stamps]
+    assert st == [(4, 2, 0), (4, 3, 1), (5, 1, 0), (5, 3, 0), (6, 1, 1)]
 
 
 def _collab_batch():
@@ -244,3 +260,69 @@ def test_v1_moved_info_json_shape():
                     assert s["movedSeq"] == s["movedSeqs"][0] and len(s["movedSeqs"]) == len(s["movedClientIds"])
                     assert s["movedSeqs"] == sorted(s["movedSeqs"])
     assert seen > 0
+
+
+def v1_reload_batches(groups_at=(16, 40)):
+    """For each reference replay fixture (tests/golden/replay_msgs_0.40.json.gz) and cut group g:
+    the messages up to g are replayed by the oracle and summarized as SnapshotV1 with merge info;
+    a second batch loads that summary (header-chunk segments with seq/client/removed/moved stamps)
+    and applies the fixture's remaining messages. Returns (batch2, expected final texts)."""
+    import gzip
+    import os
+
+    import oracle as orc
+
+    fixtures = json.load(gzip.open(os.path.join(os.path.dirname(__file__), "golden", "replay_msgs_0.40.json.gz"),
+                                   "rt", encoding="utf-8"))
+    b2 = MergeTreeStreamBuilder()
+    expected, merge_info = [], 0
+    for fx in fixtures:
+        groups = fx["groups"]
+        for g in groups_at:
+            b1 = MergeTreeStreamBuilder()
+            d = b1.begin_doc(groups[0]["initialText"], observer="A")
+            for k in range(g + 1):
+                for m in groups[k]["msgs"]:
+                    d.add_message(m)
+            batch1 = b1.finish(remove_order=True)
+            rc, h, l, c, p, _ = orc.mt_replay_batch(batch1, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
+            assert rc == 0
+            head, bodies = summary.v1_summary(h[0], l[0], c[0], p[0], batch1.keys, batch1.values,
+                                              batch1.clients[0], orc.mt_removers(batch1, 0))
+            assert bodies == []
+            merge_info += head.count('"json":')
+            d2 = b2.begin_doc_from_summary(head, [], observer="A")
+            for k in range(g + 1, len(groups)):
+                for m in groups[k]["msgs"]:
+                    d2.add_message(m)
+            expected.append(groups[-1]["resultText"])
+    assert merge_info > 0
+    return b2.finish(), expected
+
+
+def test_v1_merge_info_load_then_replay_matches_reference_text():
+    """Load a SnapshotV1 summary whose segments carry merge info (specToSegment's stamps), apply the
+    rest of the reference's messages: the final text is the fixture's resultText (pinned by the
+    reference), and the engine (emulated) == the oracle bit for bit."""
+    import oracle as orc
+
+    batch, expected = v1_reload_batches()
+    assert batch.snapshot_info is not None and len(batch.snapshot_stamps) > 0
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=512, cap_chars=2048, cap_props=1024)
+    assert rc == 0
+    eh, el, ec, ep = emu_replay(batch)
+    for d, want in enumerate(expected):
+        assert visible_text(oh[d], ol[d], oc[d]) == want, d
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (eh[d], el[d], ec[d], ep[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_v1_body_chunk_merge_info_is_rejected():
+    head = json.dumps({"version": "1", "segmentCount": 1, "length": 2, "segments": ["ab"], "startIndex": 0,
+                       "headerMetadata": {"minSequenceNumber": 0, "sequenceNumber": 5, "totalLength": 3,
+                                          "totalSegmentCount": 2,
+                                          "orderedChunkMetadata": [{"id": "header"}, {"id": "body_0"}]}})
+    body = json.dumps({"version": "1", "segmentCount": 1, "length": 1, "startIndex": 1,
+                       "segments": [{"json": "c", "seq": 3, "client": "B"}]})
+    with pytest.raises(UnsupportedOp):
+        MergeTreeStreamBuilder().begin_doc_from_summary(head, [body])
