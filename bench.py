@@ -77,6 +77,9 @@ def main():
                     help="t2: legacy summaries per shard gathered to rank 0 by the gatherv (0 = none)")
     ap.add_argument("--ops-per-doc", type=int, default=None)
     ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--min-length", type=int, default=0,
+                    help="mt: keep every document at least this many UTF-16 units long (0 = T1's cycling "
+                         "minLength); above 2048 the documents replay in the large tier")
     ap.add_argument("--unique-docs", type=int, default=0, help="0 = all documents distinct")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--key-pool", type=int, default=20, help="map: key ids per document (> 2560 takes the HBM-table path)")
@@ -131,7 +134,7 @@ def main():
         if t2 and uniq != docs:
             raise SystemExit("t2 generates every document of its shard (no --unique-docs)")
         batch = workloads.conflict_farm(uniq, n_clients=args.clients, ops_per_doc=opd, seed=seed,
-                                        replicas=docs // uniq, doc_base=doc_base)
+                                        replicas=docs // uniq, doc_base=doc_base, min_length=args.min_length)
     else:
         batch = workloads.map_stream(docs, opd, key_pool=args.key_pool, seed=seed)
     n_ops = len(batch.ops)
@@ -282,7 +285,8 @@ def main():
     # HBM bytes per launch from the committed rocprofv3 PMC passes of this same workload
     # (tools/pmc_traffic.py; gfx950 FETCH_SIZE correction applied there), or null.
     traffic = None
-    tkey = f"{args.workload}:{docs}x{opd}" + ("" if mt or args.key_pool == 20 else f"k{args.key_pool}")
+    tkey = (f"{args.workload}:{docs}x{opd}" + ("" if mt or args.key_pool == 20 else f"k{args.key_pool}")
+            + (f"m{args.min_length}" if mt and args.min_length else ""))
     tpath = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath)).get(tkey)
@@ -306,7 +310,8 @@ def main():
                        else f"{uniq} distinct docs per GPU replicated to {docs})"),
             "config": {
                 "workload": (f"T2 merge-tree conflict-farm replay, {total_docs} docs doc-sharded over {world} GPU(s)" if t2
-                             else "T1 merge-tree conflict-farm replay" if mt
+                             else (f"merge-tree conflict-farm replay, documents kept >= {args.min_length} UTF-16 units"
+                                   if args.min_length else "T1 merge-tree conflict-farm replay") if mt
                              else "M2 SharedMap LWW replay" + (", sparse output" if args.sparse else "")),
                 "docs_per_gpu": docs,
                 "docs_total": total_docs,

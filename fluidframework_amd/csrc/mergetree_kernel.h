@@ -37,8 +37,8 @@ static inline int addTuProfile(uint64_t* out, int n, bool reset) {
 template <class C>
 struct Slab {
   static constexpr size_t kLeaves = C::kHbmChars ? 64 * C::kRows : 64 * fmt_mt::SmallTier::kRows;
-  static constexpr size_t kChars = C::kCapChars;
-  static constexpr size_t kProps = C::kPropCap;
+  static constexpr size_t kChars = C::kHbmChars ? C::kCapChars : fmt_mt::SmallTier::kCapChars;
+  static constexpr size_t kProps = C::kHbmChars ? C::kPropCap : fmt_mt::SmallTier::kPropCap;
 };
 
 // A tier over all documents (docList == nullptr) or a list of countDev[0] (when countDev is set:

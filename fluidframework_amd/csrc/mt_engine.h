@@ -52,7 +52,9 @@ constexpr int kCkptEscalate = -34;   // internal status: the compact tier stoppe
 // W0 = len | block << kLenBits, props in W6.
 struct SmallTier {
   static constexpr int kRows = 8;          // rows of 64 leaves (one VR element per row)
-  static constexpr int kCapChars = 2048;   // UTF-16 units per document (tombstones included)
+  // UTF-16 units per document (tombstones included): the LDS left per wave at 2 waves/SIMD (8 per
+  // CU: 8 × 19168 B of Scratch fits the 160 KiB)
+  static constexpr int kCapChars = 6144;
   static constexpr int kMaxBlocks = 128;
   static constexpr int kHeapCap = 255;
   static constexpr int kPropCap = 32;
@@ -72,6 +74,7 @@ struct SmallTier {
 // outgrows it replays again in the small tier (runtime cascade).
 struct CompactTier : SmallTier {
   static constexpr int kRows = 4;
+  static constexpr int kCapChars = 2048;  // 12 waves/CU × 10976 B of Scratch
   using VR = V4;
 };
 
@@ -286,10 +289,17 @@ class Doc {
   // both tiers). The small tier resumes it from that op instead of replaying it from its first op.
   static constexpr bool kSavesCkpt = !C::kHbmChars && C::kRows < SmallTier::kRows && !Ob && !Rm;
   static constexpr bool kResumesCkpt = !C::kHbmChars && C::kRows == SmallTier::kRows && !Ob && !Rm;
+  // layout: 16 head words | leaf words of the compact rows | the compact tier's chars | the rest of
+  // the scratch (blk .. tmp: the same fields in both tiers; only the chars array differs in size)
   static constexpr int kCkptRows = CompactTier::kRows;
   static constexpr int kCkptHead = 16;
-  static constexpr int kCkptScratchWords = static_cast<int>((offsetof(Scratch<SmallTier>, tmp) + 3) / 4);
-  static constexpr int kCkptWords = kCkptHead + 5 * kCkptRows * 64 + kCkptScratchWords;
+  static constexpr int kCkptCharWords = CompactTier::kCapChars / 2;
+  static constexpr int kCkptRestWords =
+      static_cast<int>((offsetof(Scratch<CompactTier>, tmp) - offsetof(Scratch<CompactTier>, blk) + 3) / 4);
+  static_assert(offsetof(Scratch<CompactTier>, tmp) - offsetof(Scratch<CompactTier>, blk) ==
+                    offsetof(Scratch<SmallTier>, tmp) - offsetof(Scratch<SmallTier>, blk),
+                "checkpointed scratch fields");
+  static constexpr int kCkptWords = kCkptHead + 5 * kCkptRows * 64 + kCkptCharWords + kCkptRestWords;
   uint32_t* ckpt = nullptr;
 
   FMT_DEV void saveCkpt(uint64_t next) {
@@ -319,10 +329,13 @@ class Doc {
       }
     }
     waveSync();  // every LDS write of the op stream has landed
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(s);
+    const uint32_t* chars = reinterpret_cast<const uint32_t*>(s->chars);
+    const uint32_t* rest = reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(s) + offsetof(Scratch<C>, blk));
     uint32_t* dst = ck + kCkptHead + 5 * kCkptRows * 64;
+    const int charWords = (nChars + 1) / 2;
     FOR_LANES(l) {
-      for (int t = l; t < kCkptScratchWords; t += 64) dst[t] = src[t];
+      for (int t = l; t < charWords; t += 64) dst[t] = chars[t];
+      for (int t = l; t < kCkptRestWords; t += 64) dst[kCkptCharWords + t] = rest[t];
     }
   }
 
@@ -352,9 +365,12 @@ class Doc {
       }
     }
     const uint32_t* src = ck + kCkptHead + 5 * kCkptRows * 64;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(s);
+    uint32_t* chars = reinterpret_cast<uint32_t*>(s->chars);
+    uint32_t* rest = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(s) + offsetof(Scratch<C>, blk));
+    const int charWords = (nChars + 1) / 2;
     FOR_LANES(l) {
-      for (int t = l; t < kCkptScratchWords; t += 64) dst[t] = src[t];
+      for (int t = l; t < charWords; t += 64) chars[t] = src[t];
+      for (int t = l; t < kCkptRestWords; t += 64) rest[t] = src[kCkptCharWords + t];
     }
     waveSync();
     return next;
@@ -2184,14 +2200,16 @@ class Doc {
     Lane<uint32_t> rec1 = fetchOp(first + 1);
     Lane<uint32_t> txt0 = fetchText(rec0);
     for (uint64_t i = first; i < in.end; i++) {
+      fmt_mt_op op = decodeOp(rec0);
       if constexpr (kSavesCkpt) {
-        if (n + 2 > kCapLeaves && ckpt != nullptr) {  // the next op could outgrow the compact rows
+        // the op could outgrow the compact rows (at most two new leaves) or its text
+        if (ckpt != nullptr &&
+            (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(op.len) > kCapChars))) {
           saveCkpt(i);
           status = kCkptEscalate;
           return;
         }
       }
-      fmt_mt_op op = decodeOp(rec0);
       const Lane<uint32_t> text = txt0;
       rec0 = rec1;
       txt0 = fetchText(rec0);

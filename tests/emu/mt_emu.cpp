@@ -13,7 +13,7 @@ template <bool Ob, class C, bool Rm = false>
 static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                      fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
                      fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* ckpt = nullptr,
-                     bool onlyEscalated = false, size_t leafStride = 0) {
+                     bool onlyEscalated = false, size_t leafStride = 0, size_t charStride = 0) {
   using Doc = fmt_mt::Doc<Ob, C, Rm>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
@@ -55,7 +55,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     fmt_mt::DocOutputs o;
     o.header = headers + d;
     o.leaves = leaves + static_cast<size_t>(d) * (leafStride ? leafStride : Doc::kCapLeaves);
-    o.chars = chars + static_cast<size_t>(d) * Doc::kCapChars;
+    o.chars = chars + static_cast<size_t>(d) * (charStride ? charStride : Doc::kCapChars);
     o.props = props + static_cast<size_t>(d) * Doc::kPropCap;
     o.catchup = catchup ? catchup + static_cast<size_t>(d) * capCatchup : nullptr;
     o.catchupCap = catchup ? capCatchup : 0u;
@@ -115,7 +115,7 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
     std::unique_ptr<uint32_t[]> ck(new uint32_t[static_cast<size_t>(b->n_docs) * D::kCkptWords]);
     const size_t stride = fmt_mt::Doc<false, S>::kCapLeaves;
     replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(),
-                                          false, stride);
+                                          false, stride, S::kCapChars);
     return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(), true);
   }
   if (large == 1) {

@@ -130,6 +130,24 @@ def test_compact_to_small_cascade_resumes_from_checkpoints(orc, n_clients, seed)
         assert not diffs, f"doc {d}: {diffs[:5]}"
 
 
+def test_compact_cascade_checkpoints_long_texts(orc):
+    """Documents kept above 3000 UTF-16 units: the compact tier (2048 units) checkpoints before the
+    insert that would outgrow its text, and the small tier (6144 units) resumes them."""
+    batch = workloads.conflict_farm(24, n_clients=8, ops_per_doc=2000, min_length=3000, seed=21)
+    cl, cc, cp = emu_caps(large=3)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=4096, cap_chars=1 << 16, cap_props=1024)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch, large=3)
+    fits = (oh["n_leaves"] <= cl) & (oh["n_chars"] <= cc)
+    assert (oh["n_chars"][fits] > 2048).sum() >= 5, oh["n_chars"][fits]
+    for d in range(batch.n_docs):
+        if hdr[d]["status"] == -3:  # beyond the small tier too (the runtime's large tier takes it)
+            continue
+        assert hdr[d]["status"] == 0
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
 def test_compact_cascade_with_catchup_and_props(orc):
     """Checkpointed documents keep their catch-up ranges (recorded before and after the checkpoint)
     and prop sets."""
