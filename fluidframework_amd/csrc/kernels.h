@@ -49,6 +49,9 @@ struct MtDeviceOut {
   fmt_mt_catchup_range* catchup;  // slabs at catchupOffsets, or nullptr
   fmt_mt_remove_order* rmOrder;   // slabs at rmOrderOffsets, or nullptr
   uint32_t* ckpt;                 // plain batches: per-document compact → small tier checkpoints, or nullptr
+  // large tier over a plain batch: the small tier's result slabs, where it left its checkpoints
+  const fmt_mt_leaf* smallLeaves;
+  const uint16_t* smallChars;
 };
 // Bytes of one document's tier checkpoint (mt_engine.h Doc::kCkptWords).
 size_t mergeTreeCheckpointBytes();

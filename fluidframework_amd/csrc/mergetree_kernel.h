@@ -116,6 +116,21 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
       o.ckpt = nullptr;
       o.ckptResume = false;
     }
+    o.bigCkpt = nullptr;
+    o.bigCkptChars = nullptr;
+    if constexpr (Doc::kSavesBig) {  // plain batches (out.ckpt set): the small tier's own slabs
+      if (out.ckpt != nullptr) {
+        o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);
+        o.bigCkptChars = o.chars;
+      }
+    }
+    if constexpr (Doc::kResumesBig) {
+      if (out.smallLeaves != nullptr) {
+        o.bigCkpt = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(out.smallLeaves + d * Slab<fmt_mt::SmallTier>::kLeaves));
+        o.bigCkptChars = const_cast<uint16_t*>(out.smallChars + d * Slab<fmt_mt::SmallTier>::kChars);
+        o.ckptResume = __builtin_amdgcn_readfirstlane(out.headers[d].status) == fmt_mt::kCkptEscalate;
+      }
+    }
     Doc doc;
     doc.s = scratch;
     doc.run(in, o);

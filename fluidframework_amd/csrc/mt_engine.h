@@ -191,7 +191,11 @@ struct DocOutputs {
   fmt_mt_remove_order* rmOrder;   // rmOrderCap entries (nullptr: no FMT_MT_F_RMORDER ops)
   uint32_t rmOrderCap;
   uint32_t* ckpt;                 // the document's tier checkpoint (kCkptWords), or nullptr
-  bool ckptResume;                // small tier: resume from the checkpoint the compact tier left
+  bool ckptResume;                // resume from the checkpoint the tier below left
+  // small → large tier: the small tier leaves its checkpoint in its own result slabs (leaves slab:
+  // head, leaf words, scratch; chars slab: the text), where the large tier reads it
+  uint32_t* bigCkpt;              // small tier: its leaves slab; large tier: the small slab to read
+  uint16_t* bigCkptChars;
 };
 
 // Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
@@ -301,6 +305,123 @@ class Doc {
                 "checkpointed scratch fields");
   static constexpr int kCkptWords = kCkptHead + 5 * kCkptRows * 64 + kCkptCharWords + kCkptRestWords;
   uint32_t* ckpt = nullptr;
+
+  // small → large (plain batches): the small tier stops before an op that could outgrow its 512
+  // leaves or 6144 units, or that comes from a writer past its 31; the large tier converts its state
+  // (W0 packing and 8-bit block ids of the small tier, text into the HBM slab).
+  static constexpr bool kSavesBig = !C::kHbmChars && C::kRows == SmallTier::kRows && !Ob && !Rm;
+  static constexpr bool kResumesBig = C::kHbmChars && !Ob && !Rm;
+  static constexpr int kBigRows = SmallTier::kRows;
+  static constexpr int kBigRestWords =
+      static_cast<int>((offsetof(Scratch<SmallTier>, tmp) - offsetof(Scratch<SmallTier>, blk) + 3) / 4);
+  static_assert(kCkptHead + 5 * kBigRows * 64 + kBigRestWords <= 64 * SmallTier::kRows * 8,
+                "the small tier's checkpoint fits its leaves slab");
+  uint32_t* bigCkpt = nullptr;
+  uint16_t* bigCkptChars = nullptr;
+
+  FMT_DEV void saveBig(uint64_t next) {
+    uint32_t* ck = bigCkpt;
+    FOR_LANES(l) {
+      if (l == 0) {
+        ck[0] = static_cast<uint32_t>(next);
+        ck[1] = static_cast<uint32_t>(next >> 32);
+        ck[2] = static_cast<uint32_t>(n);
+        ck[3] = static_cast<uint32_t>(nChars);
+        ck[4] = static_cast<uint32_t>(root);
+        ck[5] = static_cast<uint32_t>(nFree);
+        ck[6] = static_cast<uint32_t>(heapN);
+        ck[7] = static_cast<uint32_t>(nProps);
+        ck[8] = static_cast<uint32_t>(curSeq);
+        ck[9] = static_cast<uint32_t>(minSeq);
+        ck[10] = static_cast<uint32_t>(failSeq);
+        ck[11] = nextId;
+        ck[12] = cuN;
+      }
+    }
+    FOR_LANES(l) {
+#pragma unroll
+      for (int f = 0; f < 5; f++) {
+#pragma unroll
+        for (int r = 0; r < kBigRows && r < kRows; r++) ck[kCkptHead + (f * kBigRows + r) * 64 + l] = LANE(W[f])[r];
+      }
+    }
+    waveSync();
+    const uint32_t* rest = reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(s) + offsetof(Scratch<C>, blk));
+    uint32_t* dst = ck + kCkptHead + 5 * kBigRows * 64;
+    FOR_LANES(l) {
+      for (int t = l; t < kBigRestWords; t += 64) dst[t] = rest[t];
+      if constexpr (!C::kHbmChars)
+        for (int t = l; t < nChars; t += 64) bigCkptChars[t] = s->chars[t];
+    }
+  }
+
+  // The large tier takes over a document the small tier checkpointed. Returns the op to resume at.
+  FMT_DEV uint64_t restoreBig() {
+    const uint32_t* ck = bigCkpt;
+    const uint64_t next = uni(ck[0]) | (static_cast<uint64_t>(uni(ck[1])) << 32);
+    n = static_cast<int>(uni(ck[2]));
+    nChars = static_cast<int>(uni(ck[3]));
+    root = static_cast<int>(uni(ck[4]));
+    const int smallFree = static_cast<int>(uni(ck[5]));
+    heapN = static_cast<int>(uni(ck[6]));
+    nProps = static_cast<int>(uni(ck[7]));
+    curSeq = static_cast<int>(uni(ck[8]));
+    minSeq = static_cast<int>(uni(ck[9]));
+    failSeq = static_cast<int>(uni(ck[10]));
+    nextId = uni(ck[11]);
+    cuN = uni(ck[12]);
+    status = FMT_OK;
+    // small-tier W0 = len (16 bits) | block (8) | props (8, 255 undefined)
+    constexpr uint32_t kSmallNoProps = 255u, kSmallNoBlk = 255u;
+    FOR_ROWS(r, 0, kRows) {
+      FOR_LANES(l) {
+        uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
+        if (r < kBigRows)
+          for (int f = 0; f < 5; f++) w[f] = ck[kCkptHead + (f * kBigRows + r) * 64 + l];
+        const bool live = r * 64 + l < n;
+        const uint32_t sp = w[0] >> 24;
+        LANE(W[0])[r] = live ? mkW0(w[0] & 0xFFFFu, (w[0] >> 16) & 0xFFu, 0u) : 0u;
+        LANE(W[1])[r] = w[1];
+        LANE(W[2])[r] = w[2];
+        LANE(W[3])[r] = w[3];
+        LANE(W[4])[r] = w[4];
+        if constexpr (kWords > 5) {
+          LANE(W[5])[r] = 0u;
+          LANE(W[kWords - 1])[r] = live ? (sp == kSmallNoProps ? kPropsUndef : sp) : 0u;
+        }
+      }
+    }
+    // the small scratch image from its blk field on: blocks, heap, prop sets, match classes, free list
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(ck + kCkptHead + 5 * kBigRows * 64) -
+                               offsetof(Scratch<SmallTier>, blk);
+    const Scratch<SmallTier>* sm = reinterpret_cast<const Scratch<SmallTier>*>(img);
+    const auto blkId = [&](uint32_t b) -> BId { return static_cast<BId>(b == kSmallNoBlk ? kNoBlk : b); };
+    FOR_LANES(l) {
+      for (int b = l; b < SmallTier::kMaxBlocks; b += 64) {
+        const Blk<uint8_t> src = sm->blk[b];
+        Blk<BId>& d = s->blk[b];
+        d.count = src.count;
+        d.parent = blkId(src.parent);
+        d.leaf = src.leaf;
+        d.needsScour = src.needsScour;
+        for (int c = 0; c < kMaxNodes; c++) d.child[c] = blkId(src.child[c]);
+      }
+      for (int k = l; k <= heapN; k += 64) s->heap[k] = sm->heap[k];
+      for (int k = l; k < nProps; k += 64) {
+        s->props[k] = sm->props[k];
+        s->propCls[k] = sm->propCls[k];
+      }
+      // free list: the ids the small tier never had at the bottom, its own free ids on top (popped first)
+      const int extra = kMaxBlocks - SmallTier::kMaxBlocks;
+      for (int k = l; k < extra; k += 64) s->freeList[k] = static_cast<BId>(kMaxBlocks - 1 - k);
+      for (int k = l; k < smallFree; k += 64) s->freeList[extra + k] = static_cast<BId>(sm->freeList[k]);
+      if constexpr (C::kHbmChars)
+        for (int t = l; t < nChars; t += 64) gch[t] = bigCkptChars[t];
+    }
+    nFree = kMaxBlocks - SmallTier::kMaxBlocks + smallFree;
+    waveSync();
+    return next;
+  }
 
   FMT_DEV void saveCkpt(uint64_t next) {
     uint32_t* ck = ckpt;
@@ -2201,11 +2322,17 @@ class Doc {
     Lane<uint32_t> txt0 = fetchText(rec0);
     for (uint64_t i = first; i < in.end; i++) {
       fmt_mt_op op = decodeOp(rec0);
-      if constexpr (kSavesCkpt) {
-        // the op could outgrow the compact rows (at most two new leaves) or its text
-        if (ckpt != nullptr &&
-            (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(op.len) > kCapChars))) {
-          saveCkpt(i);
+      if constexpr (kSavesCkpt || kSavesBig) {
+        // the op could outgrow the rows (at most two new leaves), the text, or (small tier) the
+        // writer set of this tier
+        // (the small tier also stops near its block and prop-set limits, which the large tier's
+        // 1023 / 1024 lift: an op's splits allocate a few blocks, an annotate a few sets)
+        if ((kSavesCkpt ? ckpt != nullptr : bigCkpt != nullptr) &&
+            (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(op.len) > kCapChars) ||
+             (kSavesBig && (op.client > kMaxClient || nFree < 16 ||
+                            ((op.type == FMT_MT_ANNOTATE || op.type == FMT_MT_INSERT) && nProps > kPropCap - 4))))) {
+          if constexpr (kSavesCkpt) saveCkpt(i);
+          else saveBig(i);
           status = kCkptEscalate;
           return;
         }
@@ -2360,14 +2487,18 @@ class Doc {
     ckpt = out.ckpt;
     init();
     uint64_t first = in.begin;
+    bigCkpt = out.bigCkpt;
+    bigCkptChars = out.bigCkptChars;
     if (kResumesCkpt && ckpt != nullptr && out.ckptResume) {
       first = restoreCkpt();
+    } else if (kResumesBig && bigCkpt != nullptr && out.ckptResume) {
+      first = restoreBig();
     } else {
       if (in.loaded) loadSnapshot();
       else loadInitial();
     }
     if (status == FMT_OK) replay(first);
-    if (kSavesCkpt && status == kCkptEscalate) {  // the small tier writes everything else
+    if ((kSavesCkpt || kSavesBig) && status == kCkptEscalate) {  // the next tier writes everything else
       FOR_LANES(l) {
         if (l == 0) out.header->status = status;
       }

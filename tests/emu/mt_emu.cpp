@@ -13,7 +13,8 @@ template <bool Ob, class C, bool Rm = false>
 static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                      fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
                      fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* ckpt = nullptr,
-                     bool onlyEscalated = false, size_t leafStride = 0, size_t charStride = 0) {
+                     bool onlyEscalated = false, size_t leafStride = 0, size_t charStride = 0,
+                     const fmt_mt_leaf* smallLeaves = nullptr, const uint16_t* smallChars = nullptr) {
   using Doc = fmt_mt::Doc<Ob, C, Rm>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
@@ -63,6 +64,17 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     o.rmOrderCap = rmOrder ? capRm : 0u;
     o.ckpt = ckpt && (Doc::kSavesCkpt || Doc::kResumesCkpt) ? ckpt + static_cast<size_t>(d) * Doc::kCkptWords : nullptr;
     o.ckptResume = o.ckpt != nullptr && Doc::kResumesCkpt && headers[d].status == fmt_mt::kCkptEscalate;
+    o.bigCkpt = nullptr;
+    o.bigCkptChars = nullptr;
+    if (Doc::kSavesBig && ckpt != nullptr) {  // the small tier of a plain cascade: its own slabs
+      o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);
+      o.bigCkptChars = o.chars;
+    }
+    if (Doc::kResumesBig && smallLeaves != nullptr) {
+      o.bigCkpt = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(smallLeaves + static_cast<size_t>(d) * 512));
+      o.bigCkptChars = const_cast<uint16_t*>(smallChars + static_cast<size_t>(d) * fmt_mt::SmallTier::kCapChars);
+      o.ckptResume = headers[d].status == fmt_mt::kCkptEscalate;
+    }
     new (doc.get()) Doc();
     doc->s = scratch.get();
     doc->run(in, o);
@@ -77,9 +89,11 @@ extern "C" {
 
 // large = 0: the small tier (registers + LDS text); 1: the large tier (HBM text) that the runtime
 // replays overflowing documents in; 2: the compact tier (4 register rows) plain batches start in;
-// 3: the compact → small cascade with checkpoints (small-tier strides).
+// 3: the compact → small cascade with checkpoints (small-tier strides); 4: the whole compact → small
+// → large cascade (large-tier strides).
 int emu_mt_capacity(int large, uint32_t* leaves, uint32_t* chars, uint32_t* props) {
   if (large == 3) large = 0;
+  if (large == 4) large = 1;
   if (large == 2) {
     *leaves = fmt_mt::Doc<false, fmt_mt::CompactTier>::kCapLeaves;
     *chars = fmt_mt::CompactTier::kCapChars;
@@ -110,6 +124,28 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   for (uint64_t i = 0; i < b->n_ops && !rm; i++) rm = (b->ops[i].flags & FMT_MT_F_RMORDER) != 0;
   if (large == 2 && !ob && !rm) return replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup,
                                                                              capCatchup, rmOrder, capRm);
+  if (large == 4 && !ob && !rm) {  // the whole cascade: compact → small → large, results at large strides
+    using D = fmt_mt::Doc<false, fmt_mt::CompactTier>;
+    using DS = fmt_mt::Doc<false, S>;
+    using DL = fmt_mt::Doc<false, G>;
+    const size_t n = b->n_docs;
+    std::unique_ptr<uint32_t[]> ck(new uint32_t[n * D::kCkptWords]);
+    std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
+    std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
+    std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
+    replayAll<false, fmt_mt::CompactTier>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm,
+                                          ck.get(), false, DS::kCapLeaves, S::kCapChars);
+    replayAll<false, S>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm, ck.get(), true);
+    for (size_t d = 0; d < n; d++) {  // documents done below the large tier: results to the large strides
+      const fmt_mt_doc_result& h = headers[d];
+      if (h.status == FMT_E_CAPACITY || h.status == fmt_mt::kCkptEscalate) continue;
+      std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));
+      std::memcpy(chars + d * G::kCapChars, sc.get() + d * S::kCapChars, h.n_chars * sizeof(uint16_t));
+      std::memcpy(props + d * G::kPropCap, sp.get() + d * S::kPropCap, h.n_props * sizeof(fmt_mt_propset));
+    }
+    return replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr, true, 0, 0,
+                               sl.get(), sc.get());
+  }
   if (large == 3 && !ob && !rm) {  // the runtime's cascade: compact tier with checkpoints, then the small tier
     using D = fmt_mt::Doc<false, fmt_mt::CompactTier>;
     std::unique_ptr<uint32_t[]> ck(new uint32_t[static_cast<size_t>(b->n_docs) * D::kCkptWords]);

@@ -141,9 +141,27 @@ def test_compact_cascade_checkpoints_long_texts(orc):
     fits = (oh["n_leaves"] <= cl) & (oh["n_chars"] <= cc)
     assert (oh["n_chars"][fits] > 2048).sum() >= 5, oh["n_chars"][fits]
     for d in range(batch.n_docs):
-        if hdr[d]["status"] == -3:  # beyond the small tier too (the runtime's large tier takes it)
+        if hdr[d]["status"] in (-3, -34):  # beyond the small tier too (the runtime's large tier takes it)
             continue
         assert hdr[d]["status"] == 0
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+@pytest.mark.parametrize("n_clients,min_length,n_ops", [(8, 3000, 2000), (40, 0, 1500)])
+def test_full_cascade_resumes_in_the_large_tier(orc, n_clients, min_length, n_ops):
+    """compact → small → large with checkpoints: documents past 512 leaves, 6144 units or 31
+    writers leave the small tier at an op boundary and the large tier converts its state (W0 packing,
+    8-bit block ids, text into the HBM slab) and resumes them; every document == oracle."""
+    batch = workloads.conflict_farm(24, n_clients=n_clients, ops_per_doc=n_ops, min_length=min_length, seed=33)
+    cl, cc, cp = emu_caps(large=4)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+    assert rc == 0
+    small = emu_replay(batch, large=3)[0]
+    assert (small["status"] == -34).sum() >= 2  # checkpointed for the large tier
+    hdr, leaves, chars, props = emu_replay(batch, large=4)
+    assert (hdr["status"] == 0).all(), hdr["status"]
+    for d in range(batch.n_docs):
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
 
