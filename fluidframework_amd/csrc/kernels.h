@@ -85,14 +85,16 @@ MtCaps mergeTreeCaps(bool large);
 // documents that overflow the small tier are listed in esc (esc[0] = count, then ids) when esc !=
 // nullptr. A plain batch (no obliterates, no remove order) with esc2 != nullptr starts in the compact
 // tier and lists its overflow in esc2 (count + 1 entries) for the small tier. esc[0] and esc2[0] must
-// be zero before the call.
+// be zero before the call. sched: 3 zeroed device counters (compact, small, large) from which the
+// tiers deal documents to waves dynamically (nullptr: static grid-stride shares).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
-                           bool obliterate, bool removeOrder);
+                           bool obliterate, bool removeOrder, uint32_t* sched);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder);
+                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
+                                uint32_t* next);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

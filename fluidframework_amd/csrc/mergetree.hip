@@ -34,23 +34,26 @@ MtCaps mergeTreeCaps(bool large) {
 size_t mergeTreeCheckpointBytes() { return sizeof(uint32_t) * fmt_mt::Doc<false, fmt_mt::CompactTier>::kCkptWords; }
 
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream);
+                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next);
 
 // Variants: obliterates (Ob) and/or the remove-order recording of SnapshotV1 batches (Rm).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
-                           bool obliterate, bool removeOrder) {
+                           bool obliterate, bool removeOrder, uint32_t* sched) {
   using S = fmt_mt::SmallTier;
+  uint32_t* n1 = sched ? sched + 1 : nullptr;
   if (obliterate && removeOrder)
-    return launchTier<true, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
-  if (obliterate) return launchTier<true, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
-  if (removeOrder) return launchTier<false, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+    return launchTier<true, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
+  if (obliterate)
+    return launchTier<true, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
+  if (removeOrder)
+    return launchTier<false, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   if (esc == nullptr || esc2 == nullptr)
-    return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream);
+    return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   // compact tier over everything → overflow list esc2 → this tier over that list → overflow list esc
-  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream);
+  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream, sched);
   if (e != hipSuccess) return e;
-  return launchTier<false, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2);
+  return launchTier<false, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
 }
 
 }  // namespace fmt_kernels

@@ -9,9 +9,9 @@ constexpr int kMtWavesCompact = 4;  // 4 documents per workgroup, 3 waves/SIMD
 int mergeTreeProfileCompact(uint64_t* out, int n, bool reset) { return addTuProfile(out, n, reset); }
 
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream) {
+                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next) {
   return launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 3>(batch, out, docList, count, esc, numCUs,
-                                                                          stream);
+                                                                          stream, nullptr, next);
 }
 
 }  // namespace fmt_kernels

@@ -47,13 +47,23 @@ struct Slab {
 template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                       const uint32_t* __restrict__ docList,
-                                                                      uint32_t count, const uint32_t* countDev) {
+                                                                      uint32_t count, const uint32_t* countDev,
+                                                                      uint32_t* next) {
   using Doc = fmt_mt::Doc<Ob, C, Rm>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
   fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds) + wave;
   if (countDev != nullptr) count = __builtin_amdgcn_readfirstlane(*countDev);
-  for (uint32_t i = blockIdx.x * Waves + wave; i < count; i += gridDim.x * Waves) {
+  // Documents are dealt one at a time from a device counter (next != nullptr): a wave that finishes
+  // early takes the next document, so the launch ends when the work does, not when the unluckiest
+  // static share of documents does. Every wave leaves once the counter passes `count`.
+  for (uint32_t i = next ? 0u : blockIdx.x * Waves + wave;; i += next ? 0u : gridDim.x * Waves) {
+    if (next != nullptr) {
+      uint32_t v = 0;
+      if ((threadIdx.x & 63) == 0) v = atomicAdd(next, 1u);
+      i = __builtin_amdgcn_readfirstlane(v);
+    }
+    if (i >= count) break;
     const uint32_t d = docList ? docList[i] : i;
     const size_t slot = C::kHbmChars ? i : d;
     fmt_mt::DocInputs in;
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(256) void collectOverflowKernel(fmt_mt_doc_result* 
 template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                              uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream,
-                             const uint32_t* countDev = nullptr) {
+                             const uint32_t* countDev = nullptr, uint32_t* next = nullptr) {
   const size_t lds = sizeof(fmt_mt::Scratch<C>) * Waves;
   // One resident wave of workgroups: every workgroup strides over the same number of documents,
   // so none waits behind the residency limit (VGPRs cap the small tier at 2 waves/SIMD).
@@ -181,7 +191,7 @@ static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out,
   const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
   hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
-                     docList, count, countDev);
+                     docList, count, countDev, next);
   if (esc != nullptr) {  // over the documents this launch replayed
     const uint32_t g = (count + 255) / 256;
     hipLaunchKernelGGL(collectOverflowKernel, dim3(g < 1024 ? (g > 0 ? g : 1) : 1024), dim3(256), 0, stream, out.headers,

@@ -9,14 +9,16 @@ constexpr int kMtWavesLarge = 1;  // large tier: one document per workgroup, 1 w
 int mergeTreeProfileLarge(uint64_t* out, int n, bool reset) { return addTuProfile(out, n, reset); }
 
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder) {
+                                uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
+                                uint32_t* next) {
   using G = fmt_mt::LargeTier;
   if (obliterate && removeOrder)
-    return launchTier<true, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
-  if (obliterate) return launchTier<true, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+    return launchTier<true, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
+  if (obliterate)
+    return launchTier<true, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (removeOrder)
-    return launchTier<false, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
-  return launchTier<false, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream);
+    return launchTier<false, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
+  return launchTier<false, G, false, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
 }
 
 }  // namespace fmt_kernels

@@ -82,6 +82,7 @@ struct fmt_ctx {
   DevBuf<uint32_t> mtEsc;                    // small-tier overflow list: [0] = count, then doc ids
   DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (plain batches), same layout
   DevBuf<uint32_t> mtCkpt;                   // plain batches: per-document compact → small tier checkpoints
+  DevBuf<uint32_t> mtSched;                  // per-tier document counters (dynamic dealing to waves)
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
   DevBuf<uint16_t> mtBigChars;
   DevBuf<fmt_mt_propset> mtBigProps;
@@ -208,6 +209,7 @@ void fmt_close(fmt_ctx* c) {
   c->mtProps.release();
   c->mtEsc.release();
   c->mtEsc2.release();
+  c->mtSched.release();
   c->mtCkpt.release();
   c->mtBigLeaves.release();
   c->mtBigChars.release();
@@ -516,6 +518,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, c->mtProps.reserve(static_cast<size_t>(n) * caps.props));
   FMT_HIP(c, c->mtEsc.reserve(n + 1ull));
   FMT_HIP(c, c->mtEsc2.reserve(n + 1ull));
+  FMT_HIP(c, c->mtSched.reserve(4));
   c->mtBigSlot.assign(n, -1);
   // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
   // any; a document that needs more reports FMT_E_CAPACITY.
@@ -729,12 +732,13 @@ int fmt_mt_run(fmt_ctx* c) {
                                 plain ? c->mtCkpt.p : nullptr, nullptr, nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
+  FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   const bool hasHuge = !c->huge.empty();
   if (!hasHuge || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->numCUs, c->stream, c->mtObliterate,
-                                            c->mtHasRmOrder));
+                                            c->mtHasRmOrder, c->mtSched.p));
   if (hasHuge)
     FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p,
                                            static_cast<uint32_t>(c->huge.size()), c->stream));
@@ -755,7 +759,7 @@ int fmt_mt_run(fmt_ctx* c) {
                                   nullptr, plain ? c->mtLeaves.p : nullptr, plain ? c->mtChars.p : nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
-                                                 c->mtHasRmOrder));
+                                                 c->mtHasRmOrder, c->mtSched.p + 2));
     FMT_HIP(c, hipEventRecord(c->ev3, c->stream));
     c->timed2 = true;
     std::vector<uint32_t> list(nEsc);

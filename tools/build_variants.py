@@ -92,6 +92,7 @@ VARIANTS = {
     "prof": [PROF],
     "noload": [NOLOAD],
     "base": [],
+    "cur": [],
     "nofence": [NOFENCE],
     "lb1": [LB1],
     "lb3": [LB3],
@@ -108,7 +109,7 @@ VARIANTS = {
     "map_nt_w16": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 16;")],
     "map_nt_w1": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 1;")],
 }
-REVS = {"v1": "352970f", "head": "6b38e0f"}  # committed engines to A/B against
+REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD"}  # committed engines to A/B against
 
 
 if __name__ == "__main__":
