@@ -323,8 +323,9 @@ void fmt_close(fmt_ctx* ctx);
 /* Message of the last failing call. Replaces the thrown DataProcessingError / UsageError text
  * (merge-tree/src/mergeTree.ts:1629-1638; core-utils assert 0xNNN codes). */
 const char* fmt_last_error(const fmt_ctx* ctx);
-/* Wait for the ctx stream. The reference is synchronous and non-reentrant (sequence.ts:500-511); here runs are
- * asynchronous until fmt_sync or a fetch. */
+/* Wait for the ctx stream. The reference is synchronous and non-reentrant (sequence.ts:500-511). Map runs
+ * are asynchronous until fmt_sync or a fetch; fmt_mt_run returns once the replay is done (it reads
+ * the overflow count on the host to size the large-tier launch). */
 int fmt_sync(fmt_ctx* ctx);
 /* Device time and algorithmic bytes of the last run (no reference counterpart; telemetry only). */
 int fmt_get_stats(const fmt_ctx* ctx, fmt_stats* out);
@@ -408,9 +409,12 @@ int fmt_map_fetch_sparse(fmt_ctx* ctx, uint32_t* counts, fmt_map_entry* entries,
  * including updateSeqNumbers/setMinSeq (client.ts:1381-1391, mergeTree.ts:1147-1166) and zamboni
  * (zamboni.ts:33-213). Per-document errors land in fmt_mt_doc_result.status / fail_seq. */
 int fmt_mt_load(fmt_ctx* ctx, const fmt_mt_batch* batch);
-/* Replays every loaded document. Documents first run in the small tier (512 leaves, 2048 UTF-16
- * units); those that overflow it are replayed again, from their inputs, in the large tier (2048
- * leaves, 131071 units, text in HBM) before this returns. Stats cover both launches. */
+/* Replays every loaded document and returns when it is done. Plain batches start in the compact tier
+ * (256 leaves, 2048 UTF-16 units); a document about to outgrow a tier stops at an op boundary, saves
+ * its state, and the next tier resumes it: the small tier (512 leaves, 6144 units), then the large
+ * tier (2048 leaves, 131071 units, text in HBM). Batches with obliterates or remove-order recording
+ * start in the small tier, and a document that overflows inside an op replays again from its
+ * inputs in the next tier. Stats cover every launch. */
 int fmt_mt_run(fmt_ctx* ctx);
 /* Per-document result headers for all docs (n_docs entries). Synchronizes the ctx stream. */
 int fmt_mt_fetch_headers(fmt_ctx* ctx, fmt_mt_doc_result* out);
