@@ -88,8 +88,8 @@ MtCaps mergeTreeCaps(bool large);
 // be zero before the call. sched: 3 zeroed device counters (compact, small, large) from which the
 // tiers deal documents to waves dynamically (nullptr: static grid-stride shares).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
-                           bool obliterate, bool removeOrder, uint32_t* sched);
+                           uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,

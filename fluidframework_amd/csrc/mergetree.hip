@@ -36,10 +36,56 @@ size_t mergeTreeCheckpointBytes() { return sizeof(uint32_t) * fmt_mt::Doc<false,
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                   uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next);
 
+// The compact tier's overflow list in[0] = n, in[1..n] reordered into out by remaining ops,
+// longest first (64 buckets between 0 and the largest remainder): with documents dealt to waves
+// in list order, the small-tier pass then ends on short documents (longest-processing-time first).
+// A checkpointed document has ops [ckpt next, end) left, any other one its whole stream.
+constexpr int kOrderBuckets = 64;
+__global__ __launch_bounds__(1024) void orderByRemainingKernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                               const fmt_mt_doc_result* __restrict__ headers,
+                                                               const uint64_t* __restrict__ offs,
+                                                               const uint32_t* __restrict__ ckpt, uint32_t ckptWords) {
+  __shared__ uint32_t cnt[kOrderBuckets], base[kOrderBuckets], maxRem;
+  const uint32_t n = in[0];
+  if (threadIdx.x < kOrderBuckets) cnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) maxRem = 0;
+  __syncthreads();
+  auto remaining = [&](uint32_t d) -> uint32_t {
+    uint64_t first = offs[d];
+    if (headers[d].status == fmt_mt::kCkptEscalate) {
+      const uint32_t* h = ckpt + static_cast<size_t>(d) * ckptWords;
+      first = h[0] | (static_cast<uint64_t>(h[1]) << 32);
+    }
+    const uint64_t r = offs[d + 1] - first;
+    return r > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(r);
+  };
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicMax(&maxRem, remaining(in[1 + i]));
+  __syncthreads();
+  const uint64_t span = static_cast<uint64_t>(maxRem) + 1;
+  auto bucket = [&](uint32_t r) -> uint32_t {  // 0 = the longest remainders
+    return kOrderBuckets - 1 - static_cast<uint32_t>(static_cast<uint64_t>(r) * kOrderBuckets / span);
+  };
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[bucket(remaining(in[1 + i]))], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int b = 0; b < kOrderBuckets; b++) {
+      base[b] = s;
+      s += cnt[b];
+    }
+    out[0] = n;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t d = in[1 + i];
+    out[1 + atomicAdd(&base[bucket(remaining(d))], 1u)] = d;
+  }
+}
+
 // Variants: obliterates (Ob) and/or the remove-order recording of SnapshotV1 batches (Rm).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                           uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
-                           bool obliterate, bool removeOrder, uint32_t* sched) {
+                           uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched) {
   using S = fmt_mt::SmallTier;
   uint32_t* n1 = sched ? sched + 1 : nullptr;
   if (obliterate && removeOrder)
@@ -53,6 +99,12 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
   // compact tier over everything → overflow list esc2 → this tier over that list → overflow list esc
   hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream, sched);
   if (e != hipSuccess) return e;
+  if (esc3 != nullptr && out.ckpt != nullptr) {  // longest remaining streams first
+    hipLaunchKernelGGL(orderByRemainingKernel, dim3(1), dim3(1024), 0, stream, esc2, esc3, out.headers,
+                       batch.docOpOffsets, out.ckpt,
+                       static_cast<uint32_t>(fmt_mt::Doc<false, fmt_mt::CompactTier>::kCkptWords));
+    esc2 = esc3;
+  }
   return launchTier<false, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
 }
 

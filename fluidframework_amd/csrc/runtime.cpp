@@ -81,6 +81,7 @@ struct fmt_ctx {
   DevBuf<fmt_mt_propset> mtProps;
   DevBuf<uint32_t> mtEsc;                    // small-tier overflow list: [0] = count, then doc ids
   DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (plain batches), same layout
+  DevBuf<uint32_t> mtEsc3;                   // the same list, longest remaining streams first
   DevBuf<uint32_t> mtCkpt;                   // plain batches: per-document compact → small tier checkpoints
   DevBuf<uint32_t> mtSched;                  // per-tier document counters (dynamic dealing to waves)
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
@@ -209,6 +210,7 @@ void fmt_close(fmt_ctx* c) {
   c->mtProps.release();
   c->mtEsc.release();
   c->mtEsc2.release();
+  c->mtEsc3.release();
   c->mtSched.release();
   c->mtCkpt.release();
   c->mtBigLeaves.release();
@@ -518,6 +520,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   FMT_HIP(c, c->mtProps.reserve(static_cast<size_t>(n) * caps.props));
   FMT_HIP(c, c->mtEsc.reserve(n + 1ull));
   FMT_HIP(c, c->mtEsc2.reserve(n + 1ull));
+  FMT_HIP(c, c->mtEsc3.reserve(n + 1ull));
   FMT_HIP(c, c->mtSched.reserve(4));
   c->mtBigSlot.assign(n, -1);
   // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
@@ -737,7 +740,8 @@ int fmt_mt_run(fmt_ctx* c) {
   const bool hasHuge = !c->huge.empty();
   if (!hasHuge || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
-                                            c->mtEsc.p, c->mtEsc2.p, c->numCUs, c->stream, c->mtObliterate,
+                                            c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,
+                                            c->mtObliterate,
                                             c->mtHasRmOrder, c->mtSched.p));
   if (hasHuge)
     FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p,
