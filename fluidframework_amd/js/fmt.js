@@ -26,6 +26,7 @@ const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER =
 // legacy relativePos1/2 (ops.ts IRelativePosition): pos1/pos2 index the relpos table (fmt_mt_relpos, 16 B)
 const FMT_MT_F_REL1 = 64, FMT_MT_F_REL2 = 128, FMT_MT_NO_MARKER = 0xffffffff, FMT_MT_REL_BEFORE = 1;
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
+const FMT_NON_COLLAB_CLIENT = -2; // fmt.h: the insert client of a segment without merge info
 
 /** The refType of a Marker spec {marker: {refType}, props?} (IJSONMarkerSegment), or null. */
 function markerRefType(spec) {
@@ -199,6 +200,9 @@ class MergeTreeStreamBuilder {
 		this.snapshots = []; // per doc: null or [firstSeg, nHeader, nBody, minSeq, seq]
 		this.snapshotSegs = []; // [textOff, len, propsOp]
 		this.relpos = []; // [marker value id, offset, flags]
+		this.snapshotInfo = []; // per snapshot segment: [insSeq, insClient, rmFirst, rmCount] (V1 merge info)
+		this.snapshotStamps = []; // [seq, client, kind]
+		this.hasMergeInfo = false;
 		this.current = null;
 	}
 	beginDoc(initialText, observer) {
@@ -233,26 +237,67 @@ class MergeTreeStreamBuilder {
 		this.snapshotSegs.push([off, len, props && Object.keys(props).length ? this.propsOp(props) : NO_PROPS]);
 	}
 	/**
-	 * A document that starts from a legacy SharedString summary (SnapshotLoader,
-	 * snapshotLoader.ts:59-348): header/body chunk blobs and optionally the catchupOps blob, whose
-	 * messages become the first ops after loadCore's validation (sequence.ts:818-863).
+	 * specToSegment's stamps for a V1 segment with merge info (snapshotLoader.ts:105-175): insert
+	 * {seq ?? 0, client ?? NonCollabClient}; setRemove stamps at removedSeq per removedClientIds entry
+	 * (removedClient alone in the back-compat format); sliceRemove stamps movedSeqs[i] /
+	 * movedClientIds[i]; sorted by seq (stable). Mirrors streams.py _merge_info.
+	 */
+	mergeInfo(spec, d) {
+		this.hasMergeInfo = true;
+		const insSeq = spec.seq === undefined ? 0 : spec.seq;
+		const insClient = spec.client === undefined || spec.client === null ? FMT_NON_COLLAB_CLIENT : d.shortClient(spec.client);
+		const stamps = [];
+		if (spec.removedSeq !== undefined) {
+			let ids = spec.removedClientIds;
+			if (ids === undefined && spec.removedClient !== undefined) ids = [spec.removedClient];
+			if (ids === undefined) throw new Error("must have removedClient ids");
+			for (const c of ids) stamps.push([spec.removedSeq, d.shortClient(c), 0]);
+		}
+		if (spec.movedSeq !== undefined) {
+			const seqs = spec.movedSeqs, ids = spec.movedClientIds;
+			if (seqs === undefined || ids === undefined || seqs.length !== ids.length) throw new Error("must have movedIds ids");
+			seqs.forEach((s, i) => stamps.push([s, d.shortClient(ids[i]), 1]));
+		}
+		const sorted = stamps.map((x, i) => [x, i]).sort((a, b) => a[0][0] - b[0][0] || a[1] - b[1]).map((x) => x[0]);
+		const first = this.snapshotStamps.length;
+		for (const x of sorted) this.snapshotStamps.push(x);
+		return [insSeq, insClient, first, sorted.length];
+	}
+	/**
+	 * A document that starts from a SharedString summary (SnapshotLoader, snapshotLoader.ts:59-348):
+	 * a legacy header + optional body, or SnapshotV1's header + body_0, body_1, ... (pass the bodies
+	 * as an array), and optionally the legacy catchupOps blob, whose messages become the first ops
+	 * after loadCore's validation (sequence.ts:818-863). V1 header segments with merge info keep
+	 * their stamps; body-chunk segments with merge info are not supported (mirrors streams.py).
 	 */
 	beginDocFromSummary(header, body, catchupOps, observer) {
 		const h = JSON.parse(header);
 		const md = h.headerMetadata;
 		if (md === undefined) throw new Error("header metadata not available");
 		const chunks = [h];
-		if (body !== undefined && body !== null) chunks.push(JSON.parse(body));
+		if (body !== undefined && body !== null) for (const b of Array.isArray(body) ? body : [body]) chunks.push(JSON.parse(b));
 		if (md.orderedChunkMetadata.length !== chunks.length) {
 			throw new Error("summary chunks do not match headerMetadata.orderedChunkMetadata");
 		}
+		const specsOf = (c) => (c.version === "1" ? c.segments : c.segmentTexts);
+		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "snapshot" : observer);
 		const first = this.snapshotSegs.length;
-		for (const c of chunks) for (const spec of c.segmentTexts) this.specToSeg(spec);
-		const nHeader = h.segmentTexts.length, nBody = this.snapshotSegs.length - first - nHeader;
+		chunks.forEach((c, ci) => {
+			for (let spec of specsOf(c)) {
+				let info = [0, FMT_NON_COLLAB_CLIENT, 0, 0];
+				if (spec && typeof spec === "object" && "json" in spec) { // hasMergeInfo
+					if (ci > 0) throw new UnsupportedOp("SnapshotV1 body-chunk segments with merge info");
+					info = this.mergeInfo(spec, d);
+					spec = spec.json;
+				}
+				this.specToSeg(spec);
+				this.snapshotInfo.push(info);
+			}
+		});
+		const nHeader = specsOf(h).length, nBody = this.snapshotSegs.length - first - nHeader;
 		if (nHeader + nBody !== md.totalSegmentCount) throw new Error("Mismatch in totalSegmentCount");
 		const seq = md.sequenceNumber;
 		const minSeq = md.minSequenceNumber === undefined ? seq : md.minSequenceNumber;
-		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "snapshot" : observer);
 		this.docs.push(d);
 		this.docInit.push([0, 0]);
 		this.snapshots.push([first, nHeader, nBody, minSeq, seq]);
@@ -458,6 +503,8 @@ class MergeTreeStreamBuilder {
 			messages: this.docs.map((d) => d.messages),
 			nDocs: this.docs.length,
 			relpos: this.relpos.length ? Uint32Array.from([].concat(...this.relpos.map((r) => [r[0], r[1] >>> 0, r[2], 0]))) : undefined,
+			snapshotInfo: this.hasMergeInfo ? Uint32Array.from([].concat(...this.snapshotInfo.map((r) => [r[0] >>> 0, r[1] >>> 0, r[2], r[3]]))) : undefined,
+			snapshotStamps: this.hasMergeInfo ? Uint32Array.from([].concat(...this.snapshotStamps.map((r) => [r[0] >>> 0, r[1] >>> 0, r[2], 0]))) : undefined,
 			markerIdKey: this.relpos.length && this.keys.ids.has(MARKER_ID_KEY) ? this.keys.ids.get(MARKER_ID_KEY) : FMT_MT_NO_MARKER,
 		};
 	}

@@ -377,6 +377,26 @@ napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
     j->mt.n_snapshot_segs = nss / sizeof(fmt_mt_snapshot_seg);
     keep_array(env, j, prop(env, b, "snapshots"));
     keep_array(env, j, prop(env, b, "snapshotSegs"));
+    // optional SnapshotV1 merge info: snapshotInfo (fmt_mt_snapshot_info per segment) + snapshotStamps
+    void *si, *st;
+    size_t nsi, nst;
+    if (!get_bytes(env, prop(env, b, "snapshotInfo"), "snapshotInfo", &si, &nsi) ||
+        !get_bytes(env, prop(env, b, "snapshotStamps"), "snapshotStamps", &st, &nst)) {
+      delete j;
+      return nullptr;
+    }
+    if (si != nullptr) {
+      if (nsi != j->mt.n_snapshot_segs * sizeof(fmt_mt_snapshot_info) || nst % sizeof(fmt_mt_stamp)) {
+        delete j;
+        throw_fmt(env, FMT_E_USAGE, "replayMergeTree: snapshotInfo must hold one fmt_mt_snapshot_info per segment");
+        return nullptr;
+      }
+      j->mt.snapshot_info = static_cast<const fmt_mt_snapshot_info*>(si);
+      j->mt.snapshot_stamps = static_cast<const fmt_mt_stamp*>(st);
+      j->mt.n_snapshot_stamps = nst / sizeof(fmt_mt_stamp);
+      keep_array(env, j, prop(env, b, "snapshotInfo"));
+      if (st != nullptr) keep_array(env, j, prop(env, b, "snapshotStamps"));
+    }
   }
   // optional legacy relative positions: relpos (fmt_mt_relpos rows) + markerIdKey
   void* rp;

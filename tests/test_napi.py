@@ -261,3 +261,52 @@ def test_js_relative_positions_on_gpu(addon):
     r = _node("-e", js, timeout=300)
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout) == [want for _, _, want in cases]
+
+
+def _v1_reload_js(cases):
+    docs = [{"head": h, "msgs": m} for h, m, _ in cases]
+    return (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+            "const b=new fmt.MergeTreeStreamBuilder();"
+            f"for(const x of {json.dumps(docs)}){{const d=b.beginDocFromSummary(x.head,[],null,'A');"
+            "for(const m of x.msgs) d.addMessage(m);}")
+
+
+def test_js_v1_merge_info_load_matches_python(addon, tmp_path):
+    """SnapshotV1 header chunks with merge info load through the JS packer into the same segment
+    specs, merge-info rows and stamps as the Python host's (begin_doc_from_summary)."""
+    from test_snapshot_v1 import v1_reload_batches, v1_reload_inputs
+
+    cases = v1_reload_inputs()
+    js = _v1_reload_js(cases) + (
+        "const r=b.finish();const hex=(a)=>a===undefined?'':Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
+        "process.stdout.write(JSON.stringify({ops:hex(r.ops),segs:hex(r.snapshotSegs),info:hex(r.snapshotInfo),"
+        "stamps:hex(r.snapshotStamps),snaps:hex(new Uint8Array(r.snapshots)),clients:r.clients}))")
+    script = tmp_path / "v1_load.js"
+    script.write_text(js)
+    r = _node(str(script), timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    py, _ = v1_reload_batches()
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert bytes.fromhex(out["segs"]) == py.snapshot_segs.tobytes()
+    assert bytes.fromhex(out["info"]) == py.snapshot_info.tobytes()
+    assert bytes.fromhex(out["stamps"]) == py.snapshot_stamps.tobytes()
+    assert bytes.fromhex(out["snaps"]) == py.snapshots.tobytes()
+    assert out["clients"] == py.clients
+
+
+@pytest.mark.gpu
+def test_js_v1_merge_info_load_on_gpu(addon, tmp_path):
+    """The JS driver loads mid-stream V1 summaries with merge info, replays the rest of the
+    reference's messages through the addon, and reaches the fixtures' resultText."""
+    from test_snapshot_v1 import v1_reload_inputs
+
+    cases = v1_reload_inputs()
+    js = ("(async()=>{" + _v1_reload_js(cases) + "const e=new fmt.Engine(0);const r=await e.replayMergeTree(b.finish());"
+          f"const t=[];for(let i=0;i<{len(cases)};i++) t.push(r.getText(i));e.close();"
+          "process.stdout.write(JSON.stringify(t));})().catch((e)=>{console.error(e);process.exit(1);});")
+    script = tmp_path / "v1_load_gpu.js"
+    script.write_text(js)
+    r = _node(str(script), timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout) == [want for _, _, want in cases]

@@ -262,11 +262,10 @@ def test_v1_moved_info_json_shape():
     assert seen > 0
 
 
-def v1_reload_batches(groups_at=(16, 40)):
+def v1_reload_inputs(groups_at=(16, 40)):
     """For each reference replay fixture (tests/golden/replay_msgs_0.40.json.gz) and cut group g:
-    the messages up to g are replayed by the oracle and summarized as SnapshotV1 with merge info;
-    a second batch loads that summary (header-chunk segments with seq/client/removed/moved stamps)
-    and applies the fixture's remaining messages. Returns (batch2, expected final texts)."""
+    the messages up to g are replayed by the oracle and summarized as SnapshotV1 with merge info.
+    Returns [(header blob, the fixture's remaining messages, expected final text)]."""
     import gzip
     import os
 
@@ -274,8 +273,7 @@ def v1_reload_batches(groups_at=(16, 40)):
 
     fixtures = json.load(gzip.open(os.path.join(os.path.dirname(__file__), "golden", "replay_msgs_0.40.json.gz"),
                                    "rt", encoding="utf-8"))
-    b2 = MergeTreeStreamBuilder()
-    expected, merge_info = [], 0
+    out, merge_info = [], 0
     for fx in fixtures:
         groups = fx["groups"]
         for g in groups_at:
@@ -291,12 +289,22 @@ def v1_reload_batches(groups_at=(16, 40)):
                                               batch1.clients[0], orc.mt_removers(batch1, 0))
             assert bodies == []
             merge_info += head.count('"json":')
-            d2 = b2.begin_doc_from_summary(head, [], observer="A")
-            for k in range(g + 1, len(groups)):
-                for m in groups[k]["msgs"]:
-                    d2.add_message(m)
-            expected.append(groups[-1]["resultText"])
+            rest = [m for k in range(g + 1, len(groups)) for m in groups[k]["msgs"]]
+            out.append((head, rest, groups[-1]["resultText"]))
     assert merge_info > 0
+    return out
+
+
+def v1_reload_batches(groups_at=(16, 40)):
+    """A batch that loads each v1_reload_inputs summary (header-chunk segments with seq/client/
+    removed/moved stamps) and applies the fixture's remaining messages. Returns (batch, texts)."""
+    b2 = MergeTreeStreamBuilder()
+    expected = []
+    for head, rest, want in v1_reload_inputs(groups_at):
+        d2 = b2.begin_doc_from_summary(head, [], observer="A")
+        for m in rest:
+            d2.add_message(m)
+        expected.append(want)
     return b2.finish(), expected
 
 
