@@ -83,6 +83,7 @@ struct fmt_ctx {
   DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (plain batches), same layout
   DevBuf<uint32_t> mtEsc3;                   // the same list, longest remaining streams first
   DevBuf<uint32_t> mtCkpt;                   // plain batches: per-document compact → small tier checkpoints
+  bool mtCkptOk = false;                     // allocated for this batch (else tiers replay overflow from op 0)
   DevBuf<uint32_t> mtSched;                  // per-tier document counters (dynamic dealing to waves)
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
   DevBuf<uint16_t> mtBigChars;
@@ -597,8 +598,14 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtObliterate = obliterates;
   // A plain batch starts in the compact tier; a document about to outgrow it stops at a checkpoint
   // (≈15 KiB per document) that the small tier resumes from.
-  if (!obliterates && !c->mtHasRmOrder)
-    FMT_HIP(c, c->mtCkpt.reserve(static_cast<size_t>(n) * (fmt_kernels::mergeTreeCheckpointBytes() / sizeof(uint32_t))));
+  c->mtCkptOk = false;
+  if (!obliterates && !c->mtHasRmOrder) {
+    // (a batch too large for the checkpoints still replays: overflowing documents then restart in
+    // the next tier from their first op, as batches with obliterates do)
+    c->mtCkptOk = c->mtCkpt.reserve(static_cast<size_t>(n) * (fmt_kernels::mergeTreeCheckpointBytes() / sizeof(uint32_t))) ==
+                  hipSuccess;
+    if (!c->mtCkptOk) (void)hipGetLastError();
+  }
   c->mtInsertChars = insertChars;
   c->mtInitChars = initChars;
   // Huge documents: a summary-loaded document with more segments or text than the large tier holds
@@ -732,7 +739,7 @@ int fmt_mt_run(fmt_ctx* c) {
   const bool plain = !c->mtObliterate && !c->mtHasRmOrder;
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
-                                plain ? c->mtCkpt.p : nullptr, nullptr, nullptr};
+                                plain && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));

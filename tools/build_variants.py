@@ -93,6 +93,10 @@ VARIANTS = {
     "noload": [NOLOAD],
     "base": [],
     "cur": [],
+    "cw2": [("mergetree_compact.hip", "constexpr int kMtWavesCompact = 4;", "constexpr int kMtWavesCompact = 2;")],
+    "cw1": [("mergetree_compact.hip", "constexpr int kMtWavesCompact = 4;", "constexpr int kMtWavesCompact = 1;")],
+    "sw2": [("mergetree.hip", "constexpr int kMtWaves = 4;  // small tier: 4 documents per workgroup, 2 waves/SIMD",
+             "constexpr int kMtWaves = 2;  // small tier: 4 documents per workgroup, 2 waves/SIMD")],
     "nofence": [NOFENCE],
     "lb1": [LB1],
     "lb3": [LB3],
