@@ -202,6 +202,10 @@ struct DocOutputs {
 #ifndef FMT_PROFILE
 #define FMT_PROFILE 0
 #endif
+// Diagnostic / A-B switch: op records through scalar loads (see Doc::fetchOp).
+#ifndef FMT_SCALAR_OPS
+#define FMT_SCALAR_OPS 0
+#endif
 enum ProfCat {
   kPfOpLoad, kPfScan, kPfSplit, kPfInsert, kPfRange, kPfLru, kPfZamboniOp, kPfWindow, kPfOutput,
   kPfInsChars, kPfInsShift, kPfZFind, kPfZChars, kPfZSerial, kPfZDelete, kPfZPack, kPfCount
@@ -2276,10 +2280,34 @@ class Doc {
       appendLoadedChars(uni(in.snapSegs[k].text), uni(in.snapSegs[k].len) & ~FMT_MT_SEG_MARKER);
   }
 
-  // Op records are prefetched two ahead (lanes 0..7 hold the eight dwords of one fmt_mt_op) and
-  // an insert's first 64 text units one op ahead, so the global-load latency of the dependent op
-  // stream overlaps the previous op's work.
-  FMT_DEV Lane<uint32_t> fetchOp(uint64_t i) const {
+  // Op records are prefetched two ahead and an insert's first 64 text units one op ahead, so the
+  // global-load latency of the dependent op stream overlaps the previous op's work. A record is
+  // either eight lanes of one vector load (lanes 0..7 hold its dwords, read back with v_readlane) or,
+  // with FMT_SCALAR_OPS, eight SGPRs of one scalar load (the address is wave-uniform).
+#if FMT_SCALAR_OPS && FMT_GPU
+  struct OpRec {
+    uint32_t w[8];
+  };
+  FMT_DEV OpRec fetchOp(uint64_t i) const {
+    OpRec r;
+    typedef const __attribute__((address_space(4))) uint32_t* ConstPtr;
+    if (i < in.end) {
+      const uint64_t a = reinterpret_cast<uintptr_t>(in.ops + i);
+      const uint64_t au = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a))) |
+                          (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a >> 32)))) << 32);
+      const ConstPtr p = (ConstPtr)(au);  // NOLINT: address-space cast (a wave-uniform address in SGPRs)
+#pragma unroll
+      for (int k = 0; k < 8; k++) r.w[k] = p[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) r.w[k] = 0u;
+    }
+    return r;
+  }
+  FMT_DEV static uint32_t recWord(const OpRec& r, int k) { return r.w[k]; }
+#else
+  using OpRec = Lane<uint32_t>;
+  FMT_DEV OpRec fetchOp(uint64_t i) const {
     Lane<uint32_t> x;
     if (i < in.end) {
       const uint32_t* p = reinterpret_cast<const uint32_t*>(in.ops + i);
@@ -2289,27 +2317,29 @@ class Doc {
     }
     return x;
   }
+  FMT_DEV static uint32_t recWord(const OpRec& r, int k) { return readlane(r, k); }
+#endif
 
-  FMT_DEV static fmt_mt_op decodeOp(const Lane<uint32_t>& rec) {
+  FMT_DEV static fmt_mt_op decodeOp(const OpRec& rec) {
     fmt_mt_op op;
-    op.seq = static_cast<int32_t>(readlane(rec, 0));
-    op.ref_seq = static_cast<int32_t>(readlane(rec, 1));
-    op.min_seq = static_cast<int32_t>(readlane(rec, 2));
-    op.pos1 = static_cast<int32_t>(readlane(rec, 3));
-    op.pos2 = static_cast<int32_t>(readlane(rec, 4));
-    op.payload = readlane(rec, 5);
-    const uint32_t lct = readlane(rec, 6);
+    op.seq = static_cast<int32_t>(recWord(rec, 0));
+    op.ref_seq = static_cast<int32_t>(recWord(rec, 1));
+    op.min_seq = static_cast<int32_t>(recWord(rec, 2));
+    op.pos1 = static_cast<int32_t>(recWord(rec, 3));
+    op.pos2 = static_cast<int32_t>(recWord(rec, 4));
+    op.payload = recWord(rec, 5);
+    const uint32_t lct = recWord(rec, 6);
     op.len = static_cast<uint16_t>(lct & 0xFFFF);
     op.client = static_cast<uint8_t>((lct >> 16) & 0xFF);
     op.type = static_cast<uint8_t>(lct >> 24);
-    op.flags = readlane(rec, 7);
+    op.flags = recWord(rec, 7);
     return op;
   }
 
-  FMT_DEV Lane<uint32_t> fetchText(const Lane<uint32_t>& rec) const {
-    const uint32_t lct = readlane(rec, 6);
+  FMT_DEV Lane<uint32_t> fetchText(const OpRec& rec) const {
+    const uint32_t lct = recWord(rec, 6);
     const int len = (lct >> 24) == FMT_MT_INSERT ? static_cast<int>(lct & 0xFFFF) : 0;
-    const uint32_t payload = readlane(rec, 5);
+    const uint32_t payload = recWord(rec, 5);
     Lane<uint32_t> x;
     FOR_LANES(l) { LANE(x) = l < len ? static_cast<uint32_t>(in.text[payload + l]) : 0u; }
     return x;
@@ -2317,8 +2347,8 @@ class Doc {
 
   FMT_DEV void replay(uint64_t first) {
     stamp(kPfOutput);
-    Lane<uint32_t> rec0 = fetchOp(first);
-    Lane<uint32_t> rec1 = fetchOp(first + 1);
+    OpRec rec0 = fetchOp(first);
+    OpRec rec1 = fetchOp(first + 1);
     Lane<uint32_t> txt0 = fetchText(rec0);
     for (uint64_t i = first; i < in.end; i++) {
       fmt_mt_op op = decodeOp(rec0);
@@ -2353,7 +2383,7 @@ class Doc {
         if (rmPendN > 0 || rmHitsSet)
           rmFlush(op.client, op.seq, op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE);
       }
-      const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
+      const bool lastMember = i + 1 == in.end || (recWord(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       // zamboni once inside the op (mergeTree.ts:1510-1516, 2074-2080, 2376-2382), then, after the
       // message's last member, updateSeqNumbers (client.ts:1381-1391) → setMinSeq
       // (mergeTree.ts:1147-1166), which runs zamboni again only if minSeq advanced.

@@ -93,6 +93,7 @@ VARIANTS = {
     "noload": [NOLOAD],
     "base": [],
     "cur": [],
+    "sops": [("mt_engine.h", "#define FMT_SCALAR_OPS 0", "#define FMT_SCALAR_OPS 1")],
     "cw2": [("mergetree_compact.hip", "constexpr int kMtWavesCompact = 4;", "constexpr int kMtWavesCompact = 2;")],
     "cw1": [("mergetree_compact.hip", "constexpr int kMtWavesCompact = 4;", "constexpr int kMtWavesCompact = 1;")],
     "sw2": [("mergetree.hip", "constexpr int kMtWaves = 4;  // small tier: 4 documents per workgroup, 2 waves/SIMD",
