@@ -65,9 +65,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["mt", "t2", "t3", "map"], default="mt",
+    ap.add_argument("--workload", choices=["mt", "t2", "t3", "map", "ob"], default="mt",
                     help="mt: T1 (per-GPU shard of 100k docs); t2: one 1M-doc batch partitioned over the ranks "
-                         "(the default for mt when --gpus > 1); t3: one SharedString of 10M segments; map: M2")
+                         "(the default for mt when --gpus > 1); t3: one SharedString of 10M segments; map: M2; "
+                         "ob: the reference's 30 obliterate conflict farms replicated to --docs documents")
     ap.add_argument("--segments", type=int, default=10_000_000, help="t3: segments of the loaded document")
     ap.add_argument("--t3-ops", type=int, default=10_000_000, help="t3: sequenced ops replayed")
     ap.add_argument("--cpu-ops", type=int, default=200_000, help="t3: ops of the CPU baseline sample")
@@ -111,9 +112,10 @@ def main():
 
     if args.workload == "t3":
         return bench_t3(args, rank, world, local_rank, dist)
-    mt = args.workload in ("mt", "t2")
-    t2 = args.workload == "t2" or (mt and world > 1)
-    opd = args.ops_per_doc or (2000 if mt else 1000)
+    ob = args.workload == "ob"
+    mt = args.workload in ("mt", "t2", "ob")
+    t2 = args.workload == "t2" or (args.workload == "mt" and world > 1)
+    opd = 2040 if ob else args.ops_per_doc or (2000 if mt else 1000)
     if t2:
         # T2: ONE batch of total_docs documents (every document has opd ops), partitioned over the
         # ranks by shard.plan_shards; each rank generates exactly its shard's streams (doc_base).
@@ -127,7 +129,16 @@ def main():
 
     t = time.time()
     uniq = docs
-    if mt:
+    if ob:
+        # the reference's obliterate farms (2.3.0 fixtures, 30 documents of 2040 ops with the
+        # sequenced messages the reference recorded), cycled to `docs` documents
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from golden_data import replay_fixtures
+
+        fixtures = list(replay_fixtures("replay_obliterate_2.3.0.npz"))
+        uniq = len(fixtures)
+        batch = workloads.replicate_batches([f[1] for f in fixtures], docs)
+    elif mt:
         uniq = min(args.unique_docs or docs, docs)
         if docs % uniq:
             raise SystemExit("--docs must be a multiple of --unique-docs")
@@ -162,6 +173,8 @@ def main():
         bad = int((hdrs["status"] != 0).sum())
         if bad:
             raise SystemExit(f"{bad} documents failed: statuses {np.unique(hdrs['status'])}")
+        if ob:
+            _check_obliterate_farms(eng, hdrs, fixtures, docs)
     elif args.sparse:
         eng.map_fetch_sparse()
     else:
@@ -219,7 +232,7 @@ def main():
                         "what": f"legacy summaries (header, body) of the first {args.gather_docs} documents of every "
                                 "shard, gathered to rank 0 (all-gather of byte counts + grouped send/recv)"}
     summaries = None
-    if mt and not t2 and not args.no_summaries:
+    if mt and not t2 and not ob and not args.no_summaries:
         # every document's legacy summary from the converged state (device merge + host JSON on the
         # usable cores), timed apart from the replay; a sample checked against the Python host
         from fluidframework_amd.summary import legacy_summary
@@ -304,12 +317,15 @@ def main():
             "scaling": "strong" if t2 else "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": f"synthetic ({'conflict-farm' if mt else 'map fuzz'} shape, reference XSadd PRNG; "
-                    + (f"one {total_docs}-doc batch partitioned by shard.plan_shards)" if t2
-                       else f"{docs} distinct docs per GPU)" if not mt or uniq == docs
-                       else f"{uniq} distinct docs per GPU replicated to {docs})"),
+            "data": (f"reference fixtures: the 30 obliterate conflict farms (merge-tree 2.3.0 results), cycled to "
+                     f"{docs} docs per GPU" if ob else
+                     f"synthetic ({'conflict-farm' if mt else 'map fuzz'} shape, reference XSadd PRNG; "
+                     + (f"one {total_docs}-doc batch partitioned by shard.plan_shards)" if t2
+                        else f"{docs} distinct docs per GPU)" if not mt or uniq == docs
+                        else f"{uniq} distinct docs per GPU replicated to {docs})")),
             "config": {
-                "workload": (f"T2 merge-tree conflict-farm replay, {total_docs} docs doc-sharded over {world} GPU(s)" if t2
+                "workload": ("merge-tree conflict farms with obliterate (reference fixtures) replay" if ob
+                             else f"T2 merge-tree conflict-farm replay, {total_docs} docs doc-sharded over {world} GPU(s)" if t2
                              else (f"merge-tree conflict-farm replay, documents kept >= {args.min_length} UTF-16 units"
                                    if args.min_length else "T1 merge-tree conflict-farm replay") if mt
                              else "M2 SharedMap LWW replay" + (", sparse output" if args.sparse else "")),
@@ -354,6 +370,27 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _check_obliterate_farms(eng, hdrs, fixtures, docs):
+    """Every copy of a fixture ends in the same state, and the first copies hold the text the
+    reference recorded as the farm's final result."""
+    import numpy as np
+
+    from fluidframework_amd.shard import _HDR_FIELDS
+
+    n = len(fixtures)
+    for f in _HDR_FIELDS:
+        col = hdrs[f]
+        if not (col == col[np.arange(docs) % n]).all():
+            raise SystemExit(f"obliterate farm copies disagree on {f}")
+    for d in range(min(n, docs)):
+        lv, ch, _ = eng.mt_doc(d, hdrs[d])
+        text = "".join(ch[int(L["char_off"]):int(L["char_off"]) + int(L["len"])].tobytes().decode("utf-16-le", "surrogatepass")
+                       for L in lv[:int(hdrs[d]["n_leaves"])]
+                       if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000)
+        if text != fixtures[d][4][-1]:
+            raise SystemExit(f"obliterate farm {fixtures[d][0]}: final text differs from the reference's")
 
 
 def _issue_record(traffic):

@@ -11,7 +11,7 @@ import subprocess
 
 import numpy as np
 
-from .streams import (MAP_OP_DTYPE, MT_INSERT, MT_OP_DTYPE, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
+from .streams import (MAP_OP_DTYPE, MT_ANNOTATE, MT_INSERT, MT_OP_DTYPE, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
                       MergeTreeBatch, js_json)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -170,3 +170,75 @@ def with_insert_props(batch: MergeTreeBatch, every: int = 3) -> MergeTreeBatch:
     ops["pos2"] = np.where(ins, pid + 1, ops["pos2"])
     return dataclasses.replace(batch, ops=ops, props_off=np.asarray(off, np.uint32), props_kv=np.asarray(kv, np.uint32),
                                keys=batch.keys + ["color"], values=batch.values + [js_json("red"), js_json("blue")])
+
+
+def replicate_batches(batches, n_docs: int) -> MergeTreeBatch:
+    """One batch of n_docs documents cycling over the single-document batches given (plain streams:
+    no summaries, relative positions or merge info), every copy with its own text in the arena.
+
+    Used for the obliterate workload: the reference's 30 obliterate conflict farms
+    (merge-tree/src/test/results/*-conflict-farm-with-obliterate-2.3.0.json, committed as
+    tests/golden/replay_obliterate_2.3.0.npz) laid out as a batch of T1's size. Keys, values and
+    props ops of the sources are merged; annotate payloads, insert props (pos2 - 1) and text offsets
+    are rebased per copy.
+    """
+    keys, values = [], ["null"]
+    kid, vid = {}, {"null": 0}
+    kv_parts, off_parts, props_base = [], [], []
+    n_props = 0
+    for b in batches:
+        if b.snapshots is not None or b.relpos is not None or b.snapshot_info is not None:
+            raise ValueError("replicate_batches takes plain streams")
+        if len(b.doc_op_offsets) != 2:
+            raise ValueError("replicate_batches takes single-document batches")
+        for k in b.keys:
+            if k not in kid:
+                kid[k] = len(keys)
+                keys.append(k)
+        kmap = np.array([kid[k] for k in b.keys] or [0], dtype=np.uint32)
+        vmap = np.zeros(max(len(b.values), 1), dtype=np.uint32)
+        for i, v in enumerate(b.values):
+            if v not in vid:
+                vid[v] = len(values)
+                values.append(v)
+            vmap[i] = vid[v]
+        kv = b.props_kv.astype(np.uint32)
+        kv_parts.append((kmap[kv >> 16] << 16) | vmap[kv & 0xFFFF])
+        off_parts.append(b.props_off[1:].astype(np.uint64) + sum(len(p) for p in kv_parts[:-1]))
+        props_base.append(n_props)
+        n_props += len(b.props_off) - 1
+    props_off = np.concatenate([np.zeros(1, dtype=np.uint64)] + off_parts).astype(np.uint32)
+    props_kv = np.concatenate(kv_parts) if kv_parts else np.zeros(0, dtype=np.uint32)
+
+    src = [i % len(batches) for i in range(n_docs)]
+    n_ops = sum(len(batches[s].ops) for s in src)
+    n_text = sum(len(batches[s].text) for s in src)
+    if n_text >= 1 << 32:
+        raise ValueError("text arena beyond 32-bit offsets")
+    ops = np.empty(n_ops, dtype=MT_OP_DTYPE)
+    text = np.empty(max(n_text, 1), dtype="<u2")
+    offs = np.zeros(n_docs + 1, dtype=np.uint64)
+    doc_init = np.zeros((n_docs, 2), dtype=np.uint32)
+    # per source: which ops take a text offset / a props id
+    shapes = []
+    for s, b in enumerate(batches):
+        t = b.ops["type"]
+        ins = t == MT_INSERT
+        shapes.append((ins, t == MT_ANNOTATE, ins & (b.ops["pos2"] > 0)))
+    o = tx = 0
+    for d, s in enumerate(src):
+        b = batches[s]
+        ins, ann, iprops = shapes[s]
+        k = len(b.ops)
+        blk = ops[o : o + k]
+        blk[:] = b.ops
+        blk["payload"][ins] += np.uint32(tx)
+        blk["payload"][ann] += np.uint32(props_base[s])
+        blk["pos2"][iprops] += np.int32(props_base[s])
+        text[tx : tx + len(b.text)] = b.text
+        doc_init[d] = (int(b.doc_init[0][0]) + tx, int(b.doc_init[0][1]))
+        o += k
+        tx += len(b.text)
+        offs[d + 1] = o
+    return MergeTreeBatch(ops=ops, doc_op_offsets=offs, text=text, doc_init=doc_init, props_off=props_off,
+                          props_kv=props_kv, keys=keys, values=values)
