@@ -173,8 +173,6 @@ def main():
         bad = int((hdrs["status"] != 0).sum())
         if bad:
             raise SystemExit(f"{bad} documents failed: statuses {np.unique(hdrs['status'])}")
-        if ob:
-            _check_obliterate_farms(eng, hdrs, fixtures, docs)
     elif args.sparse:
         eng.map_fetch_sparse()
     else:
@@ -207,6 +205,8 @@ def main():
         hdrs = eng.mt_headers()
         rec["status_bad"] = int((hdrs["status"] != 0).sum())
         rec["checksum"] = shard.state_checksum(hdrs, doc_base)
+        if ob:
+            _check_obliterate_farms(eng, hdrs, fixtures, docs)
     elif args.sparse:
         rec["checksum"] = shard.map_sparse_checksum(*eng.map_fetch_sparse(), doc_base)
     else:
