@@ -34,7 +34,8 @@ MtCaps mergeTreeCaps(bool large) {
 size_t mergeTreeCheckpointBytes() { return sizeof(uint32_t) * fmt_mt::Doc<false, fmt_mt::CompactTier>::kCkptWords; }
 
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
-                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next);
+                                  uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next,
+                                  bool obliterate);
 
 // The compact tier's overflow list in[0] = n, in[1..n] reordered into out by remaining ops,
 // longest first (64 buckets between 0 and the largest remainder): with documents dealt to waves
@@ -90,14 +91,14 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
   uint32_t* n1 = sched ? sched + 1 : nullptr;
   if (obliterate && removeOrder)
     return launchTier<true, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
-  if (obliterate)
+  if (obliterate && (esc == nullptr || esc2 == nullptr))
     return launchTier<true, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   if (removeOrder)
     return launchTier<false, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   if (esc == nullptr || esc2 == nullptr)
     return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   // compact tier over everything → overflow list esc2 → this tier over that list → overflow list esc
-  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream, sched);
+  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream, sched, obliterate);
   if (e != hipSuccess) return e;
   if (esc3 != nullptr && out.ckpt != nullptr) {  // longest remaining streams first
     hipLaunchKernelGGL(orderByRemainingKernel, dim3(1), dim3(1024), 0, stream, esc2, esc3, out.headers,
@@ -105,6 +106,8 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
                        static_cast<uint32_t>(fmt_mt::Doc<false, fmt_mt::CompactTier>::kCkptWords));
     esc2 = esc3;
   }
+  if (obliterate)
+    return launchTier<true, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
   return launchTier<false, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
 }
 

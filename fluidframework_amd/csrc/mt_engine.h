@@ -290,15 +290,17 @@ class Doc {
   Lane<uint32_t> rmHits;  // leaves a flagged REMOVE found already removed (row bitmask per lane)
 
   // ------------------------------------------------------------------ tier checkpoint
-  // A plain document (no obliterates, no remove order) in the compact tier that is about to outgrow
-  // its 4 register rows stops before the op (one op adds at most two leaves: an insert's split plus
-  // the new leaf, or a range op's two boundary splits) and leaves its whole state in its HBM
-  // checkpoint: the scalars, the leaf words of the compact rows and the LDS scratch (same layout in
-  // both tiers). The small tier resumes it from that op instead of replaying it from its first op.
-  static constexpr bool kSavesCkpt = !C::kHbmChars && C::kRows < SmallTier::kRows && !Ob && !Rm;
-  static constexpr bool kResumesCkpt = !C::kHbmChars && C::kRows == SmallTier::kRows && !Ob && !Rm;
+  // A document without remove-order recording in the compact tier that is about to outgrow its 4
+  // register rows stops before the op (one op adds at most two leaves: an insert's split plus the
+  // new leaf, or a range op's — obliterate's too — two boundary splits) and leaves its whole state
+  // in its HBM checkpoint: the scalars, the leaf words of the compact rows and the LDS scratch (same
+  // layout in both tiers). The small tier resumes it from that op instead of replaying it from its
+  // first op.
+  static constexpr bool kSavesCkpt = !C::kHbmChars && C::kRows < SmallTier::kRows && !Rm;
+  static constexpr bool kResumesCkpt = !C::kHbmChars && C::kRows == SmallTier::kRows && !Rm;
   // layout: 16 head words | leaf words of the compact rows | the compact tier's chars | the rest of
-  // the scratch (blk .. tmp: the same fields in both tiers; only the chars array differs in size)
+  // the scratch (blk .. tmp: the same fields in both tiers; only the chars array differs in size) |
+  // the live obliterates (ob .. obStart; Ob only, head words 13..15 hold their counts and bitmap)
   static constexpr int kCkptRows = CompactTier::kRows;
   static constexpr int kCkptHead = 16;
   static constexpr int kCkptCharWords = CompactTier::kCapChars / 2;
@@ -307,7 +309,12 @@ class Doc {
   static_assert(offsetof(Scratch<CompactTier>, tmp) - offsetof(Scratch<CompactTier>, blk) ==
                     offsetof(Scratch<SmallTier>, tmp) - offsetof(Scratch<SmallTier>, blk),
                 "checkpointed scratch fields");
-  static constexpr int kCkptWords = kCkptHead + 5 * kCkptRows * 64 + kCkptCharWords + kCkptRestWords;
+  static constexpr int kCkptObWords =
+      static_cast<int>((offsetof(Scratch<CompactTier>, obStart) + kObCap - offsetof(Scratch<CompactTier>, ob) + 3) / 4);
+  static_assert(offsetof(Scratch<CompactTier>, obStart) - offsetof(Scratch<CompactTier>, ob) ==
+                    offsetof(Scratch<SmallTier>, obStart) - offsetof(Scratch<SmallTier>, ob),
+                "checkpointed obliterate fields");
+  static constexpr int kCkptWords = kCkptHead + 5 * kCkptRows * 64 + kCkptCharWords + kCkptRestWords + kCkptObWords;
   uint32_t* ckpt = nullptr;
 
   // small → large (plain batches): the small tier stops before an op that could outgrow its 512
@@ -444,6 +451,11 @@ class Doc {
         ck[10] = static_cast<uint32_t>(failSeq);
         ck[11] = nextId;
         ck[12] = cuN;
+        if constexpr (Ob) {
+          ck[13] = static_cast<uint32_t>(obSeqN) | (static_cast<uint32_t>(obStartN) << 16);
+          ck[14] = static_cast<uint32_t>(obUsed);
+          ck[15] = static_cast<uint32_t>(obUsed >> 32);
+        }
       }
     }
     FOR_LANES(l) {
@@ -462,6 +474,12 @@ class Doc {
       for (int t = l; t < charWords; t += 64) dst[t] = chars[t];
       for (int t = l; t < kCkptRestWords; t += 64) dst[kCkptCharWords + t] = rest[t];
     }
+    if constexpr (Ob) {
+      const uint32_t* obw = reinterpret_cast<const uint32_t*>(s->ob);
+      FOR_LANES(l) {
+        for (int t = l; t < kCkptObWords; t += 64) dst[kCkptCharWords + kCkptRestWords + t] = obw[t];
+      }
+    }
   }
 
   // Returns the op index to resume at.
@@ -479,6 +497,12 @@ class Doc {
     failSeq = static_cast<int>(uni(ck[10]));
     nextId = uni(ck[11]);
     cuN = uni(ck[12]);
+    if constexpr (Ob) {
+      const uint32_t c13 = uni(ck[13]);
+      obSeqN = static_cast<int>(c13 & 0xFFFFu);
+      obStartN = static_cast<int>(c13 >> 16);
+      obUsed = uni(ck[14]) | (static_cast<uint64_t>(uni(ck[15])) << 32);
+    }
     status = FMT_OK;
     FOR_LANES(l) {
 #pragma unroll
@@ -496,6 +520,12 @@ class Doc {
     FOR_LANES(l) {
       for (int t = l; t < charWords; t += 64) chars[t] = src[t];
       for (int t = l; t < kCkptRestWords; t += 64) rest[t] = src[kCkptCharWords + t];
+    }
+    if constexpr (Ob) {
+      uint32_t* obw = reinterpret_cast<uint32_t*>(s->ob);
+      FOR_LANES(l) {
+        for (int t = l; t < kCkptObWords; t += 64) obw[t] = src[kCkptCharWords + kCkptRestWords + t];
+      }
     }
     waveSync();
     return next;

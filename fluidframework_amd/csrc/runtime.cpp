@@ -80,9 +80,9 @@ struct fmt_ctx {
   DevBuf<uint16_t> mtChars;
   DevBuf<fmt_mt_propset> mtProps;
   DevBuf<uint32_t> mtEsc;                    // small-tier overflow list: [0] = count, then doc ids
-  DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (plain batches), same layout
+  DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (no remove order), same layout
   DevBuf<uint32_t> mtEsc3;                   // the same list, longest remaining streams first
-  DevBuf<uint32_t> mtCkpt;                   // plain batches: per-document compact → small tier checkpoints
+  DevBuf<uint32_t> mtCkpt;                   // per-document compact → small tier checkpoints
   bool mtCkptOk = false;                     // allocated for this batch (else tiers replay overflow from op 0)
   DevBuf<uint32_t> mtSched;                  // per-tier document counters (dynamic dealing to waves)
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
@@ -596,10 +596,10 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtNProps = b->n_props_ops;
   c->mtHasInit = b->doc_init != nullptr;
   c->mtObliterate = obliterates;
-  // A plain batch starts in the compact tier; a document about to outgrow it stops at a checkpoint
-  // (≈15 KiB per document) that the small tier resumes from.
+  // A batch without remove-order recording starts in the compact tier; a document about to outgrow
+  // it stops at a checkpoint (≈17 KiB per document) that the small tier resumes from.
   c->mtCkptOk = false;
-  if (!obliterates && !c->mtHasRmOrder) {
+  if (!c->mtHasRmOrder) {
     // (a batch too large for the checkpoints still replays: overflowing documents then restart in
     // the next tier from their first op, as batches with obliterates do)
     c->mtCkptOk = c->mtCkpt.reserve(static_cast<size_t>(n) * (fmt_kernels::mergeTreeCheckpointBytes() / sizeof(uint32_t))) ==
@@ -739,7 +739,7 @@ int fmt_mt_run(fmt_ctx* c) {
   const bool plain = !c->mtObliterate && !c->mtHasRmOrder;
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
-                                plain && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
+                                !c->mtHasRmOrder && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
@@ -787,8 +787,8 @@ int fmt_mt_run(fmt_ctx* c) {
   c->stats.bytes_read = c->mtNOps * sizeof(fmt_mt_op) + (c->mtInsertChars + c->mtInitChars) * 2 +
                         (c->mtDocs + 1ull) * sizeof(uint64_t);
   c->stats.bytes_written = static_cast<uint64_t>(c->mtDocs) * sizeof(fmt_mt_doc_result);
-  // compact + small tier (plain batches) or small tier alone, then the large tier when it ran
-  c->stats.launches = (!c->mtObliterate && !c->mtHasRmOrder ? 2 : 1) + (nEsc > 0 ? 1 : 0);
+  // compact + small tier (no remove-order recording) or small tier alone, then the large tier when it ran
+  c->stats.launches = (!c->mtHasRmOrder ? 2 : 1) + (nEsc > 0 ? 1 : 0);
   return FMT_OK;
 }
 

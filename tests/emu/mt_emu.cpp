@@ -85,6 +85,20 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
   return status;
 }
 
+// The runtime's compact → small cascade with checkpoints (results at small-tier strides).
+template <bool Ob>
+static int cascadeCompactSmall(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                               fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
+                               fmt_mt_remove_order* rmOrder, uint32_t capRm) {
+  using S = fmt_mt::SmallTier;
+  using D = fmt_mt::Doc<Ob, fmt_mt::CompactTier>;
+  std::unique_ptr<uint32_t[]> ck(new uint32_t[static_cast<size_t>(b->n_docs) * D::kCkptWords]);
+  const size_t stride = fmt_mt::Doc<Ob, S>::kCapLeaves;
+  replayAll<Ob, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(),
+                                     false, stride, S::kCapChars);
+  return replayAll<Ob, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(), true);
+}
+
 extern "C" {
 
 // large = 0: the small tier (registers + LDS text); 1: the large tier (HBM text) that the runtime
@@ -122,8 +136,9 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   using G = fmt_mt::LargeTier;
   bool rm = false;
   for (uint64_t i = 0; i < b->n_ops && !rm; i++) rm = (b->ops[i].flags & FMT_MT_F_RMORDER) != 0;
-  if (large == 2 && !ob && !rm) return replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup,
-                                                                             capCatchup, rmOrder, capRm);
+  if (large == 2 && !rm)
+    return ob ? replayAll<true, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm)
+              : replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (large == 4 && !ob && !rm) {  // the whole cascade: compact → small → large, results at large strides
     using D = fmt_mt::Doc<false, fmt_mt::CompactTier>;
     using DS = fmt_mt::Doc<false, S>;
@@ -146,14 +161,9 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
     return replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr, true, 0, 0,
                                sl.get(), sc.get());
   }
-  if (large == 3 && !ob && !rm) {  // the runtime's cascade: compact tier with checkpoints, then the small tier
-    using D = fmt_mt::Doc<false, fmt_mt::CompactTier>;
-    std::unique_ptr<uint32_t[]> ck(new uint32_t[static_cast<size_t>(b->n_docs) * D::kCkptWords]);
-    const size_t stride = fmt_mt::Doc<false, S>::kCapLeaves;
-    replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(),
-                                          false, stride, S::kCapChars);
-    return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(), true);
-  }
+  if (large == 3 && !rm)  // the runtime's cascade: compact tier with checkpoints, then the small tier
+    return ob ? cascadeCompactSmall<true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm)
+              : cascadeCompactSmall<false>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (large == 1) {
     if (ob && rm) return replayAll<true, G, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
     if (ob) return replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);

@@ -378,6 +378,21 @@ def test_mt_obliterate_fixture_checkpoints(orc, engine):
         assert visible_text(hdrs[d], leaves, chars) == text, d
 
 
+def test_mt_obliterate_farms_through_compact_cascade(orc, engine):
+    """The 30 whole obliterate farms, cycled to 600 documents (bench.py --workload ob's batch): the
+    compact tier checkpoints the documents that outgrow it, live obliterates included, and the small
+    tier resumes them — engine == oracle, final texts == the reference's."""
+    from fluidframework_amd.workloads import replicate_batches
+    from test_obliterate import OB_FIXTURES
+
+    batch = replicate_batches([f[1] for f in OB_FIXTURES], 600)
+    hdrs = _check_against_oracle(orc, engine, batch)
+    assert engine.stats().launches == 2  # compact tier, small tier over its overflow
+    for d in range(len(OB_FIXTURES)):
+        leaves, chars, _ = engine.mt_doc(d, hdrs[d])
+        assert visible_text(hdrs[d], leaves, chars) == OB_FIXTURES[d][4][-1], d
+
+
 @pytest.mark.parametrize("rng_seed", [None, 5, 9])
 def test_mt_sided_obliterate_on_gpu(orc, engine, rng_seed):
     """Sided obliterate (type 5): the reference obliterate fixtures re-encoded as equivalent sided ops

@@ -70,3 +70,40 @@ def test_obliterate_variant_matches_plain_engine_without_obliterates(orc):
     b = emu_replay(batch, force_ob=True)
     for d in range(batch.n_docs):
         assert not compare_doc(tuple(x[d] for x in a), tuple(x[d] for x in b)), d
+
+
+def test_emulated_compact_cascade_obliterate_matches_oracle(orc, ob_prefix):
+    """The runtime's cascade for obliterate batches: the compact tier stops a document before an op
+    that could outgrow it and leaves its state — live obliterates included — in its checkpoint; the
+    small tier resumes from that op and must end bit for bit where the oracle does."""
+    from mt_compare import compare_doc, emu_caps, emu_replay
+
+    batch, expected = ob_prefix
+    compact = emu_replay(batch, large=2)[0]
+    overflowed = int((compact["status"] == -3).sum())  # FMT_E_CAPACITY: the compact tier alone cannot hold them
+    assert overflowed > 20, overflowed
+    cl, cc, cp = emu_caps(large=3)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    hdr, leaves, chars, props = emu_replay(batch, large=3)
+    for d in range(batch.n_docs):
+        assert hdr[d]["status"] == oh[d]["status"], (d, hdr[d]["status"], oh[d]["status"])
+        if oh[d]["status"] == 0:
+            diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+            assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_emulated_compact_cascade_full_obliterate_farms(orc):
+    """The 30 whole farms (bench.py --workload ob cycles them) through the cascade: final texts as
+    the reference recorded them, state bit for bit as the oracle's."""
+    from fluidframework_amd.workloads import replicate_batches
+    from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
+
+    batch = replicate_batches([f[1] for f in OB_FIXTURES], len(OB_FIXTURES))
+    cl, cc, cp = emu_caps(large=3)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    hdr, leaves, chars, props = emu_replay(batch, large=3)
+    for d, f in enumerate(OB_FIXTURES):
+        assert hdr[d]["status"] == oh[d]["status"] == 0, (d, hdr[d]["status"])
+        assert visible_text(hdr[d], leaves[d], chars[d]) == f[4][-1], f[0]
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
