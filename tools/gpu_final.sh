@@ -1,6 +1,7 @@
 #!/bin/bash
 # End-of-round pass at HEAD: GPU parity suite, smoke, then one bench line per workload (T1 default,
-# T2 slice, M2, M2 sparse with keys U[0, 2^20), T3 reduced, long documents), each step time-limited.
+# T2 slice, M2, M2 sparse with keys U[0, 2^20), T3 reduced, long documents, obliterate farms), each
+# step time-limited.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -22,7 +23,9 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout
  && timeout -k 10 600 python -u bench.py --workload t3 --segments 1000000 --t3-ops 200000 --steps 2 --warmup 1 --cpu-ops 100000 > $OUT/bench_T3_reduced.log 2>&1 \
  && step T3 \
  && timeout -k 10 600 python bench.py --min-length 3000 --docs 20000 --no-summaries --steps 2 > $OUT/bench_long_docs.log 2>&1 \
- && step long
+ && step long \
+ && timeout -k 10 600 python bench.py --workload ob --steps 3 > $OUT/bench_ob.log 2>&1 \
+ && step ob
 rc=$?
 tail -3 $OUT/pytest_gpu.log; for f in $OUT/bench_*.log; do echo "$f: $(tail -1 $f | cut -c1-200)"; done
 exit $rc

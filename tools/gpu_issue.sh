@@ -5,9 +5,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/issue
+OUT=gpurun_out/${OUTDIR:-issue}
 mkdir -p $OUT
-B="python3 bench.py --no-cpu-baseline --no-summaries --steps 1 --warmup 0"
+W=${W:-}  # workload arguments (default T1), e.g. W="--workload ob"
+B="python3 bench.py $W --no-cpu-baseline --no-summaries --steps 1 --warmup 0"
 AB=${AB:-}
 step() { echo "[$(date +%T)] $1" >> $OUT/progress.txt; }
 step start
@@ -15,7 +16,7 @@ if [ -n "$AB" ]; then
   timeout -k 10 500 python3 tools/bench_variants.py --docs 20000 --unique 20000 --rounds 3 $AB > $OUT/ab.json 2> $OUT/ab.err || exit $?
   step ab
 fi
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_T1 -o run -- python3 bench.py --no-cpu-baseline --no-summaries --steps 2 --warmup 1 > $OUT/trace_T1.log 2>&1 \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_T1 -o run -- python3 bench.py $W --no-cpu-baseline --no-summaries --steps 2 --warmup 1 > $OUT/trace_T1.log 2>&1 \
  && step trace \
  && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- $B > $OUT/pmc_fetch.log 2>&1 \
  && step fetch \
