@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-js-baseline", action="store_true", help="map: skip the JS worker_threads baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline pool (0 = every usable host core)")
     args = ap.parse_args()
 
@@ -258,7 +259,7 @@ def main():
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     achieved = bytes_per_launch / (avg_kernel_ms / 1e3) / 1e9
 
-    cpu = None
+    cpu = cpu_js = None
     # (the sparse map line has none: the oracle's dense per-(doc, key) output would dominate its time)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not t2 and not args.sparse:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -294,6 +295,10 @@ def main():
             "host_cpus": {k: hc[k] for k in ("cpu_count", "affinity", "cgroup_quota_cpus")},
         }
         log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
+        if not mt and not args.no_js_baseline:
+            cpu_js = _js_map_baseline(oracle, batch, docs, threads, args.cpu_seconds / 2)
+            if cpu_js is not None:
+                log(rank, f"[bench] JS baseline {cpu_js['value']:.3g} ops/s on {threads} worker_threads")
 
     # HBM bytes per launch from the committed rocprofv3 PMC passes of this same workload
     # (tools/pmc_traffic.py; gfx950 FETCH_SIZE correction applied there), or null.
@@ -360,6 +365,8 @@ def main():
                 "issue": _issue_record(traffic) if mt else None,
             },
             "cpu_baseline": cpu,
+            # secondary: the plain-JS observer restatement on worker_threads
+            **({"cpu_baseline_js": cpu_js} if cpu_js is not None else {}),
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
             "summary_gather": gathered,
             "summaries": summaries,
@@ -370,6 +377,34 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _js_map_baseline(oracle, batch, docs, workers, seconds):
+    """The JS restatement (oracle/js/map_observer.js) on `workers` worker_threads over the first
+    documents of the batch, passes repeated to about `seconds` of work; checked against the C++
+    oracle's entries on that sample. None when node is absent."""
+    import shutil
+    import subprocess
+
+    import numpy as np
+
+    if shutil.which("node") is None:
+        return None
+    n = min(docs, 20_000)
+    o1 = int(batch.doc_op_offsets[n])
+    sub = batch.__class__(batch.ops[:o1], batch.doc_op_offsets[: n + 1], batch.key_bound, batch.keys, batch.values)
+    hashes, st = oracle.js_map_replay(sub, workers)
+    slots, _ = oracle.map_replay(sub, threads=workers)
+    if not np.array_equal(hashes, oracle.map_entry_hashes(slots)):
+        raise SystemExit("JS baseline: final maps differ from the C++ oracle's")
+    reps = max(1, int(seconds / max(st["seconds"], 1e-3)))
+    _, st = oracle.js_map_replay(sub, workers, reps=reps)
+    node_v = subprocess.run(["node", "--version"], capture_output=True, text=True).stdout.strip()
+    return {"value": st["ops_per_s"], "unit": "ops/s", "cores": workers, "kind": "JS restatement, not the reference",
+            "seconds": st["seconds"],
+            "sample": f"{n} documents ({o1} ops) of the same workload, {st['reps']} passes, plain-JS Map per document "
+                      f"(oracle/js/map_observer.js) on {workers} worker_threads, Node {node_v}; final maps checked "
+                      "equal to the C++ oracle's"}
 
 
 def _check_obliterate_farms(eng, hdrs, fixtures, docs):

@@ -253,3 +253,49 @@ def mt_removers(batch, doc: int, cap: int = 1 << 16):
         q = out[4 * k : 4 * k + 4]
         res.setdefault(int(q[0]), []).append((int(q[1]), int(q[2]), int(q[3])))
     return res
+
+
+def js_map_replay(batch, workers, tmpdir=None, reps=1):
+    """The JS restatement of the SharedMap observer path (oracle/js/map_observer.js) on `workers`
+    worker_threads: returns (per-document entry hashes, its JSON stats line). CPU baseline only."""
+    import json
+    import shutil
+    import subprocess
+    import tempfile
+
+    node = shutil.which("node")
+    if node is None:
+        raise OracleError("node is not on PATH")
+    d = tempfile.mkdtemp(dir=tmpdir)
+    try:
+        ops = os.path.join(d, "ops.bin")
+        offs = os.path.join(d, "offs.bin")
+        keys = os.path.join(d, "keys.json")
+        out = os.path.join(d, "hashes.bin")
+        np.ascontiguousarray(batch.ops).tofile(ops)
+        np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64).tofile(offs)
+        names = list(batch.keys) + [str(k) for k in range(len(batch.keys), batch.key_bound)]
+        with open(keys, "w") as f:
+            json.dump(names, f)
+        script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "js", "map_observer.js")
+        r = subprocess.run([node, script, ops, offs, keys, str(workers), out, str(reps)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise OracleError(f"map_observer.js failed: {r.stderr[-2000:]}")
+        return np.fromfile(out, dtype=np.uint32), json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def map_entry_hashes(slots):
+    """Per-document hash of the live entries in Map iteration order (birth seq), as map_observer.js
+    folds them: FNV-1a-style over (key id, value id)."""
+    slots = np.asarray(slots)
+    out = np.zeros(len(slots), dtype=np.uint32)
+    for d in range(len(slots)):
+        live = np.nonzero(slots[d]["value"] != 0xFFFFFFFF)[0]
+        h = 0x811C9DC5
+        for k in live[np.argsort(slots[d]["birth_seq"][live], kind="stable")]:
+            h = ((h ^ int(k)) * 16777619) & 0xFFFFFFFF
+            h = ((h ^ int(slots[d]["value"][k])) * 16777619) & 0xFFFFFFFF
+        out[d] = h
+    return out
