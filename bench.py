@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-js-baseline", action="store_true", help="map: skip the JS worker_threads baseline")
+    ap.add_argument("--no-js-baseline", action="store_true", help="skip the JS worker_threads baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline pool (0 = every usable host core)")
     args = ap.parse_args()
 
@@ -295,8 +295,8 @@ def main():
             "host_cpus": {k: hc[k] for k in ("cpu_count", "affinity", "cgroup_quota_cpus")},
         }
         log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
-        if not mt and not args.no_js_baseline:
-            cpu_js = _js_map_baseline(oracle, batch, docs, threads, args.cpu_seconds / 2)
+        if not args.no_js_baseline and not ob:
+            cpu_js = (_js_mt_baseline if mt else _js_map_baseline)(oracle, batch, docs, threads, args.cpu_seconds / 2)
             if cpu_js is not None:
                 log(rank, f"[bench] JS baseline {cpu_js['value']:.3g} ops/s on {threads} worker_threads")
 
@@ -405,6 +405,45 @@ def _js_map_baseline(oracle, batch, docs, workers, seconds):
             "sample": f"{n} documents ({o1} ops) of the same workload, {st['reps']} passes, plain-JS Map per document "
                       f"(oracle/js/map_observer.js) on {workers} worker_threads, Node {node_v}; final maps checked "
                       "equal to the C++ oracle's"}
+
+
+def _js_mt_baseline(oracle, batch, docs, workers, seconds):
+    """The JS restatement (oracle/js/mt_observer.js: flat segment list, no B+tree) on `workers`
+    worker_threads over the first documents of the batch, passes repeated to about `seconds`; the
+    first 256 documents' final texts checked against the C++ oracle's. None when node is absent."""
+    import shutil
+    import subprocess
+
+    if shutil.which("node") is None:
+        return None
+    n = min(docs, 4 * workers * 64)
+    o1 = int(batch.doc_op_offsets[n])
+    sub = _mt_prefix(batch, n)
+    hashes, st = oracle.js_mt_replay(sub, workers)
+    k = min(n, 256)
+    rc, oh, ol, oc, _, _ = oracle.mt_replay_batch(sub, 0, k, threads=workers, cap_leaves=8192, cap_chars=1 << 17,
+                                                  cap_props=1024)
+    for d in range(k):
+        if oh[d]["status"] == 0 and oracle.text_hash(oracle.visible_units(oh[d], ol[d], oc[d])) != hashes[d]:
+            raise SystemExit(f"JS baseline: document {d} ends with a different text than the C++ oracle's")
+    reps = max(1, int(seconds / max(st["seconds"], 1e-3)))
+    if reps > 1:
+        _, st = oracle.js_mt_replay(sub, workers, reps=reps)
+    node_v = subprocess.run(["node", "--version"], capture_output=True, text=True).stdout.strip()
+    return {"value": st["ops_per_s"], "unit": "ops/s", "cores": workers, "kind": "JS restatement, not the reference",
+            "seconds": st["seconds"],
+            "sample": f"{n} documents ({o1} ops) of the same workload, {st['reps']} pass(es), plain-JS flat segment "
+                      f"list per document (oracle/js/mt_observer.js; no B+tree) on {workers} worker_threads, Node "
+                      f"{node_v}; final texts of the first {k} checked equal to the C++ oracle's"}
+
+
+def _mt_prefix(batch, n):
+    """The first n documents of a merge-tree batch (shared text and props tables)."""
+    from dataclasses import replace
+
+    o1 = int(batch.doc_op_offsets[n])
+    return replace(batch, ops=batch.ops[:o1], doc_op_offsets=batch.doc_op_offsets[: n + 1],
+                   doc_init=batch.doc_init[:n] if batch.doc_init is not None else None, clients=[], messages=[])
 
 
 def _check_obliterate_farms(eng, hdrs, fixtures, docs):

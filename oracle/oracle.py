@@ -299,3 +299,51 @@ def map_entry_hashes(slots):
             h = ((h ^ int(slots[d]["value"][k])) * 16777619) & 0xFFFFFFFF
         out[d] = h
     return out
+
+
+def js_mt_replay(batch, workers, tmpdir=None, reps=1):
+    """The JS restatement of the SharedString observer path (oracle/js/mt_observer.js) on `workers`
+    worker_threads: returns (per-document FNV-1a hashes of the final text, its JSON stats line).
+    CPU baseline only."""
+    import json
+    import shutil
+    import subprocess
+    import tempfile
+
+    node = shutil.which("node")
+    if node is None:
+        raise OracleError("node is not on PATH")
+    d = tempfile.mkdtemp(dir=tmpdir)
+    try:
+        n = batch.n_docs
+        np.ascontiguousarray(batch.ops).tofile(os.path.join(d, "ops.bin"))
+        np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64).tofile(os.path.join(d, "offs.bin"))
+        np.ascontiguousarray(batch.text, dtype="<u2").tofile(os.path.join(d, "text.bin"))
+        init = batch.doc_init if batch.doc_init is not None else np.zeros((n, 2), dtype=np.uint32)
+        np.ascontiguousarray(init, dtype=np.uint32).tofile(os.path.join(d, "init.bin"))
+        np.ascontiguousarray(batch.props_off, dtype=np.uint32).tofile(os.path.join(d, "props_off.bin"))
+        np.ascontiguousarray(batch.props_kv, dtype=np.uint32).tofile(os.path.join(d, "props_kv.bin"))
+        with open(os.path.join(d, "meta.json"), "w") as f:
+            json.dump({"keys": list(batch.keys), "values": list(batch.values)}, f)
+        script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "js", "mt_observer.js")
+        r = subprocess.run([node, script, d, str(workers), str(reps)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise OracleError(f"mt_observer.js failed: {r.stderr[-2000:]}")
+        return np.fromfile(os.path.join(d, "hashes.bin"), dtype=np.uint32)[:n], json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def text_hash(units) -> int:
+    """FNV-1a over UTF-16 code units, as mt_observer.js folds a document's final text."""
+    h = 0x811C9DC5
+    for u in np.asarray(units, dtype=np.uint16).tolist():
+        h = ((h ^ u) * 16777619) & 0xFFFFFFFF
+    return h
+
+
+def visible_units(hdr, leaves, chars):
+    """The UTF-16 units of a replayed document's visible text (oracle outputs)."""
+    parts = [chars[int(L["char_off"]): int(L["char_off"]) + int(L["len"])] for L in leaves[: int(hdr["n_leaves"])]
+             if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000]
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint16)

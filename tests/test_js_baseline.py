@@ -42,3 +42,26 @@ def test_js_map_observer_clear_and_reinsert_order(orc):
     slots, _ = orc.map_replay(batch)
     hashes, _ = orc.js_map_replay(batch, 1)
     assert np.array_equal(hashes, orc.map_entry_hashes(slots))
+
+
+@pytest.mark.parametrize("n_clients,min_length,workers", [(2, 0, 1), (8, 0, 4), (8, 3000, 2)])
+def test_js_mt_observer_matches_oracle_text(orc, n_clients, min_length, workers):
+    """The plain-JS SharedString observer ends every conflict-farm document with the oracle's text."""
+    batch = workloads.conflict_farm(40, n_clients=n_clients, ops_per_doc=1500, seed=11, min_length=min_length)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    assert rc == 0
+    hashes, stats = orc.js_mt_replay(batch, workers)
+    assert stats["docs"] == 40 and stats["ops"] == len(batch.ops)
+    want = [orc.text_hash(orc.visible_units(oh[d], ol[d], oc[d])) for d in range(40)]
+    assert hashes.tolist() == want
+
+
+def test_js_mt_observer_on_reference_fixtures(orc):
+    """...and the 0.40 conflict-farm fixtures' final texts as the reference recorded them."""
+    from golden_data import replay_fixtures
+
+    fx = list(replay_fixtures())
+    batch = workloads.replicate_batches([f[1] for f in fx], len(fx))
+    hashes, _ = orc.js_mt_replay(batch, 2)
+    for d, f in enumerate(fx):
+        assert hashes[d] == orc.text_hash(np.frombuffer(f[4][-1].encode("utf-16-le"), dtype="<u2")), f[0]
