@@ -118,7 +118,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
       o.rmOrder = nullptr;
       o.rmOrderCap = 0;
     }
-    if (Doc::kSavesCkpt || Doc::kResumesCkpt) {
+    if (Doc::kSavesCkpt || Doc::kResumesCkpt || (Ob && Doc::kResumesBig)) {  // (large tier: live obliterates)
       o.ckpt = out.ckpt ? out.ckpt + static_cast<size_t>(d) * Doc::kCkptWords : nullptr;
       o.ckptResume = Doc::kResumesCkpt && o.ckpt != nullptr &&
                      __builtin_amdgcn_readfirstlane(out.headers[d].status) == fmt_mt::kCkptEscalate;
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     }
     o.bigCkpt = nullptr;
     o.bigCkptChars = nullptr;
-    if constexpr (Doc::kSavesBig) {  // plain batches (out.ckpt set): the small tier's own slabs
+    if constexpr (Doc::kSavesBig) {  // batches without remove order (out.ckpt set): the small tier's own slabs
       if (out.ckpt != nullptr) {
         o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);
         o.bigCkptChars = o.chars;

@@ -320,8 +320,11 @@ class Doc {
   // small → large (plain batches): the small tier stops before an op that could outgrow its 512
   // leaves or 6144 units, or that comes from a writer past its 31; the large tier converts its state
   // (W0 packing and 8-bit block ids of the small tier, text into the HBM slab).
-  static constexpr bool kSavesBig = !C::kHbmChars && C::kRows == SmallTier::kRows && !Ob && !Rm;
-  static constexpr bool kResumesBig = C::kHbmChars && !Ob && !Rm;
+  // (Ob: the live-obliterate table goes to the end of the document's compact checkpoint slot, free
+  // once the small tier has resumed from it; head words 13..15 of the slab hold its counts and bitmap)
+  static constexpr bool kSavesBig = !C::kHbmChars && C::kRows == SmallTier::kRows && !Rm;
+  static constexpr bool kResumesBig = C::kHbmChars && !Rm;
+  static constexpr int kCkptObOff = kCkptWords - kCkptObWords;
   static constexpr int kBigRows = SmallTier::kRows;
   static constexpr int kBigRestWords =
       static_cast<int>((offsetof(Scratch<SmallTier>, tmp) - offsetof(Scratch<SmallTier>, blk) + 3) / 4);
@@ -347,6 +350,17 @@ class Doc {
         ck[10] = static_cast<uint32_t>(failSeq);
         ck[11] = nextId;
         ck[12] = cuN;
+        if constexpr (Ob) {
+          ck[13] = static_cast<uint32_t>(obSeqN) | (static_cast<uint32_t>(obStartN) << 16);
+          ck[14] = static_cast<uint32_t>(obUsed);
+          ck[15] = static_cast<uint32_t>(obUsed >> 32);
+        }
+      }
+    }
+    if constexpr (Ob) {
+      const uint32_t* obw = reinterpret_cast<const uint32_t*>(s->ob);
+      FOR_LANES(l) {
+        for (int t = l; t < kCkptObWords; t += 64) ckpt[kCkptObOff + t] = obw[t];
       }
     }
     FOR_LANES(l) {
@@ -381,6 +395,16 @@ class Doc {
     failSeq = static_cast<int>(uni(ck[10]));
     nextId = uni(ck[11]);
     cuN = uni(ck[12]);
+    if constexpr (Ob) {
+      const uint32_t c13 = uni(ck[13]);
+      obSeqN = static_cast<int>(c13 & 0xFFFFu);
+      obStartN = static_cast<int>(c13 >> 16);
+      obUsed = uni(ck[14]) | (static_cast<uint64_t>(uni(ck[15])) << 32);
+      uint32_t* obw = reinterpret_cast<uint32_t*>(s->ob);
+      FOR_LANES(l) {
+        for (int t = l; t < kCkptObWords; t += 64) obw[t] = ckpt[kCkptObOff + t];
+      }
+    }
     status = FMT_OK;
     // small-tier W0 = len (16 bits) | block (8) | props (8, 255 undefined)
     constexpr uint32_t kSmallNoProps = 255u, kSmallNoBlk = 255u;
@@ -2380,6 +2404,7 @@ class Doc {
     OpRec rec0 = fetchOp(first);
     OpRec rec1 = fetchOp(first + 1);
     Lane<uint32_t> txt0 = fetchText(rec0);
+    const bool canSave = kSavesCkpt ? ckpt != nullptr : bigCkpt != nullptr && (!Ob || ckpt != nullptr);
     for (uint64_t i = first; i < in.end; i++) {
       fmt_mt_op op = decodeOp(rec0);
       if constexpr (kSavesCkpt || kSavesBig) {
@@ -2387,10 +2412,13 @@ class Doc {
         // writer set of this tier
         // (the small tier also stops near its block and prop-set limits, which the large tier's
         // 1023 / 1024 lift: an op's splits allocate a few blocks, an annotate a few sets)
-        if ((kSavesCkpt ? ckpt != nullptr : bigCkpt != nullptr) &&
+        if (canSave &&
             (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(op.len) > kCapChars) ||
-             (kSavesBig && (op.client > kMaxClient || nFree < 16 ||
-                            ((op.type == FMT_MT_ANNOTATE || op.type == FMT_MT_INSERT) && nProps > kPropCap - 4))))) {
+             (kSavesBig && (op.client > kMaxClient ||
+                            // (margins: plain batches only — obliterate documents near them mostly
+                            // finish in this tier, measured on the obliterate farms)
+                            (!Ob && (nFree < 16 || ((op.type == FMT_MT_ANNOTATE || op.type == FMT_MT_INSERT) &&
+                                                    nProps > kPropCap - 4))))))) {
           if constexpr (kSavesCkpt) saveCkpt(i);
           else saveBig(i);
           status = kCkptEscalate;

@@ -736,7 +736,6 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasSnapInfo ? c->mtSnapInfo.p : nullptr, c->mtHasSnapInfo ? c->mtSnapStamps.p : nullptr,
                                 c->mtNRelpos ? c->mtRelpos.p : nullptr,
                                 c->mtNRelpos, c->mtMarkerKey};
-  const bool plain = !c->mtObliterate && !c->mtHasRmOrder;
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
                                 !c->mtHasRmOrder && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
@@ -767,7 +766,8 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
                                   c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
-                                  nullptr, plain ? c->mtLeaves.p : nullptr, plain ? c->mtChars.p : nullptr};
+                                  c->mtObliterate && !c->mtHasRmOrder && c->mtCkptOk ? c->mtCkpt.p : nullptr,
+                                  !c->mtHasRmOrder ? c->mtLeaves.p : nullptr, !c->mtHasRmOrder ? c->mtChars.p : nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
                                                  c->mtHasRmOrder, c->mtSched.p + 2));

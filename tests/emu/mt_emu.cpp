@@ -62,11 +62,12 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     o.catchupCap = catchup ? capCatchup : 0u;
     o.rmOrder = rmOrder ? rmOrder + static_cast<size_t>(d) * capRm : nullptr;
     o.rmOrderCap = rmOrder ? capRm : 0u;
-    o.ckpt = ckpt && (Doc::kSavesCkpt || Doc::kResumesCkpt) ? ckpt + static_cast<size_t>(d) * Doc::kCkptWords : nullptr;
+    o.ckpt = ckpt && (Doc::kSavesCkpt || Doc::kResumesCkpt || (Ob && Doc::kResumesBig))
+                 ? ckpt + static_cast<size_t>(d) * Doc::kCkptWords : nullptr;
     o.ckptResume = o.ckpt != nullptr && Doc::kResumesCkpt && headers[d].status == fmt_mt::kCkptEscalate;
     o.bigCkpt = nullptr;
     o.bigCkptChars = nullptr;
-    if (Doc::kSavesBig && ckpt != nullptr) {  // the small tier of a plain cascade: its own slabs
+    if (Doc::kSavesBig && ckpt != nullptr) {  // the small tier of a cascade: its own slabs
       o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);
       o.bigCkptChars = o.chars;
     }
@@ -97,6 +98,36 @@ static int cascadeCompactSmall(const fmt_mt_batch* b, fmt_mt_doc_result* headers
   replayAll<Ob, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(),
                                      false, stride, S::kCapChars);
   return replayAll<Ob, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, ck.get(), true);
+}
+
+// The whole cascade: compact → small → large with both checkpoints (results at large-tier strides).
+template <bool Ob>
+static int fullCascade(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                       fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
+                       fmt_mt_remove_order* rmOrder, uint32_t capRm) {
+  using S = fmt_mt::SmallTier;
+  using G = fmt_mt::LargeTier;
+  using D = fmt_mt::Doc<Ob, fmt_mt::CompactTier>;
+  using DS = fmt_mt::Doc<Ob, S>;
+  using DL = fmt_mt::Doc<Ob, G>;
+  const size_t n = b->n_docs;
+  std::unique_ptr<uint32_t[]> ck(new uint32_t[n * D::kCkptWords]);
+  std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
+  std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
+  std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
+  replayAll<Ob, fmt_mt::CompactTier>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm,
+                                     ck.get(), false, DS::kCapLeaves, S::kCapChars);
+  replayAll<Ob, S>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm, ck.get(), true);
+  for (size_t d = 0; d < n; d++) {  // documents done below the large tier: results to the large strides
+    const fmt_mt_doc_result& h = headers[d];
+    if (h.status == FMT_E_CAPACITY || h.status == fmt_mt::kCkptEscalate) continue;
+    std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));
+    std::memcpy(chars + d * G::kCapChars, sc.get() + d * S::kCapChars, h.n_chars * sizeof(uint16_t));
+    std::memcpy(props + d * G::kPropCap, sp.get() + d * S::kPropCap, h.n_props * sizeof(fmt_mt_propset));
+  }
+  // (the large tier reads the live-obliterate table from the checkpoint slots, Ob only)
+  return replayAll<Ob, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, Ob ? ck.get() : nullptr,
+                          true, 0, 0, sl.get(), sc.get());
 }
 
 extern "C" {
@@ -139,28 +170,9 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   if (large == 2 && !rm)
     return ob ? replayAll<true, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm)
               : replayAll<false, fmt_mt::CompactTier>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
-  if (large == 4 && !ob && !rm) {  // the whole cascade: compact → small → large, results at large strides
-    using D = fmt_mt::Doc<false, fmt_mt::CompactTier>;
-    using DS = fmt_mt::Doc<false, S>;
-    using DL = fmt_mt::Doc<false, G>;
-    const size_t n = b->n_docs;
-    std::unique_ptr<uint32_t[]> ck(new uint32_t[n * D::kCkptWords]);
-    std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
-    std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
-    std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
-    replayAll<false, fmt_mt::CompactTier>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm,
-                                          ck.get(), false, DS::kCapLeaves, S::kCapChars);
-    replayAll<false, S>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm, ck.get(), true);
-    for (size_t d = 0; d < n; d++) {  // documents done below the large tier: results to the large strides
-      const fmt_mt_doc_result& h = headers[d];
-      if (h.status == FMT_E_CAPACITY || h.status == fmt_mt::kCkptEscalate) continue;
-      std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));
-      std::memcpy(chars + d * G::kCapChars, sc.get() + d * S::kCapChars, h.n_chars * sizeof(uint16_t));
-      std::memcpy(props + d * G::kPropCap, sp.get() + d * S::kPropCap, h.n_props * sizeof(fmt_mt_propset));
-    }
-    return replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr, true, 0, 0,
-                               sl.get(), sc.get());
-  }
+  if (large == 4 && !rm)  // the whole cascade: compact → small → large, results at large strides
+    return ob ? fullCascade<true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm)
+              : fullCascade<false>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (large == 3 && !rm)  // the runtime's cascade: compact tier with checkpoints, then the small tier
     return ob ? cascadeCompactSmall<true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm)
               : cascadeCompactSmall<false>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);

@@ -82,9 +82,11 @@ def test_emulated_compact_cascade_obliterate_matches_oracle(orc, ob_prefix):
     compact = emu_replay(batch, large=2)[0]
     overflowed = int((compact["status"] == -3).sum())  # FMT_E_CAPACITY: the compact tier alone cannot hold them
     assert overflowed > 20, overflowed
-    cl, cc, cp = emu_caps(large=3)
+    # (the whole cascade: a few documents reach the small tier's block / prop-set margins and go on
+    # to the large tier through the small tier's checkpoint)
+    cl, cc, cp = emu_caps(large=4)
     rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
-    hdr, leaves, chars, props = emu_replay(batch, large=3)
+    hdr, leaves, chars, props = emu_replay(batch, large=4)
     for d in range(batch.n_docs):
         assert hdr[d]["status"] == oh[d]["status"], (d, hdr[d]["status"], oh[d]["status"])
         if oh[d]["status"] == 0:
@@ -99,11 +101,50 @@ def test_emulated_compact_cascade_full_obliterate_farms(orc):
     from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
 
     batch = replicate_batches([f[1] for f in OB_FIXTURES], len(OB_FIXTURES))
-    cl, cc, cp = emu_caps(large=3)
+    cl, cc, cp = emu_caps(large=4)
     rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
-    hdr, leaves, chars, props = emu_replay(batch, large=3)
+    hdr, leaves, chars, props = emu_replay(batch, large=4)
     for d, f in enumerate(OB_FIXTURES):
         assert hdr[d]["status"] == oh[d]["status"] == 0, (d, hdr[d]["status"])
         assert visible_text(hdr[d], leaves[d], chars[d]) == f[4][-1], f[0]
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def long_obliterate_farms(extra=6000):
+    """The 30 farms with `extra` UTF-16 units appended to each initial text: every document outgrows
+    the small tier's 6144 units while obliterates are live (positions stay valid: the text only
+    grows at its end)."""
+    from dataclasses import replace
+
+    import numpy as np
+
+    from fluidframework_amd.workloads import replicate_batches
+
+    batch = replicate_batches([f[1] for f in OB_FIXTURES], len(OB_FIXTURES))
+    text, init = [batch.text], np.array(batch.doc_init)
+    off = len(batch.text)
+    for d in range(batch.n_docs):
+        o, n = int(init[d][0]), int(init[d][1])
+        block = np.concatenate([batch.text[o : o + n], np.full(extra, ord("y") + d % 3, dtype="<u2")])
+        text.append(block)
+        init[d] = (off, len(block))
+        off += len(block)
+    return replace(batch, text=np.concatenate(text).astype("<u2"), doc_init=init)
+
+
+def test_emulated_full_cascade_with_live_obliterates(orc):
+    """Obliterate documents past the small tier: the small tier checkpoints into its slabs and the
+    live-obliterate table into the compact checkpoint slot; the large tier resumes — == oracle."""
+    from mt_compare import compare_doc, emu_caps, emu_replay
+
+    batch = long_obliterate_farms()
+    small = emu_replay(batch, large=3)[0]
+    assert (small["status"] == -34).sum() >= 15  # stopped at a small → large checkpoint
+    cl, cc, cp = emu_caps(large=4)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    hdr, leaves, chars, props = emu_replay(batch, large=4)
+    for d in range(batch.n_docs):
+        assert hdr[d]["status"] == oh[d]["status"] == 0, (d, hdr[d]["status"], oh[d]["status"])
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
