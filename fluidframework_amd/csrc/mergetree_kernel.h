@@ -41,6 +41,13 @@ struct Slab {
   static constexpr size_t kProps = C::kHbmChars ? C::kPropCap : fmt_mt::SmallTier::kPropCap;
 };
 
+// LDS bytes per wave: batches without obliterates never touch the live-obliterate table at the end
+// of Scratch (1.6 KiB), which is what lets the compact tier hold 4 waves per SIMD (16 × 9312 B).
+template <class C, bool Ob>
+constexpr size_t scratchBytes() {
+  return Ob ? sizeof(fmt_mt::Scratch<C>) : (offsetof(fmt_mt::Scratch<C>, ob) + 15) & ~static_cast<size_t>(15);
+}
+
 // A tier over all documents (docList == nullptr) or a list of countDev[0] (when countDev is set:
 // the overflow list a previous launch built on the device) or `count` documents. The large tier
 // writes leaves/chars/props to slab i of the list (headers stay per document).
@@ -52,7 +59,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
   using Doc = fmt_mt::Doc<Ob, C, Rm>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
-  fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds) + wave;
+  fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds + wave * scratchBytes<C, Ob>());
   if (countDev != nullptr) count = __builtin_amdgcn_readfirstlane(*countDev);
   // Documents are dealt one at a time from a device counter (next != nullptr): a wave that finishes
   // early takes the next document, so the launch ends when the work does, not when the unluckiest
@@ -180,7 +187,7 @@ template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU>
 static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                              uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream,
                              const uint32_t* countDev = nullptr, uint32_t* next = nullptr) {
-  const size_t lds = sizeof(fmt_mt::Scratch<C>) * Waves;
+  const size_t lds = scratchBytes<C, Ob>() * Waves;
   // One resident wave of workgroups: every workgroup strides over the same number of documents,
   // so none waits behind the residency limit (VGPRs cap the small tier at 2 waves/SIMD).
   int blocksPerCU = 0;

@@ -16,6 +16,7 @@
 
 #include "../../include/fmt.h"
 #include "huge_engine.h"
+#include "jsnum.h"
 #include "kernels.h"
 
 namespace {
@@ -1147,6 +1148,9 @@ int fmt_internal_huge_profile(fmt_ctx* c, uint32_t doc, uint64_t* out) {
                        hipMemcpyDeviceToHost));
   return FMT_OK;
 }
+
+// Test hook (not part of fmt.h): the summary formatters' JSON.stringify of a number (jsnum.h).
+int fmt_internal_js_number(double x, char* out, int cap) { return out == nullptr || cap < 0 ? 0 : fmt_json::jsNumber(x, out, cap); }
 
 // Internal diagnostic (not part of fmt.h): per-phase cycle totals of a FMT_PROFILE=1 build.
 int fmt_internal_mt_profile(uint64_t* out, int n, int reset) {

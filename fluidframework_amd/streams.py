@@ -18,6 +18,7 @@ Semantics mirrored while packing:
 from __future__ import annotations
 
 import json
+from decimal import Decimal
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -138,13 +139,37 @@ def js_json(value) -> str:
         return js_quote(value)
     if isinstance(value, bool) or value is None:
         return json.dumps(value)
-    if isinstance(value, int):
-        return str(value)
+    if isinstance(value, int):  # JSON.parse reads every number as a double
+        return str(value) if abs(value) <= 2**53 else js_number(float(value))
     if isinstance(value, float):
-        if value.is_integer() and abs(value) < 1e21:
-            return str(int(value))
-        return repr(value)
+        return js_number(value)
     raise TypeError(f"not a JSON value: {value!r}")
+
+
+def js_number(x: float) -> str:
+    """JSON.stringify of a JS number: ECMAScript Number::toString (ECMA-262 §6.1.6.1.20) over the
+    shortest round-trip digits (which Python's repr also picks), "null" for NaN / ±Infinity
+    (SerializeJSONProperty), and "0" for -0."""
+    if x != x or x in (float("inf"), float("-inf")):
+        return "null"
+    if x == 0:
+        return "0"
+    if x < 0:
+        return "-" + js_number(-x)
+    sign, digits, exp = Decimal(repr(x)).as_tuple()
+    ds = "".join(map(str, digits)).rstrip("0")
+    exp += len(digits) - len(ds)  # x = int(ds) × 10^exp
+    k = len(ds)
+    n = k + exp  # x = 0.ds × 10^n
+    if k <= n <= 21:
+        return ds + "0" * (n - k)
+    if 0 < n <= 21:
+        return ds[:n] + "." + ds[n:]
+    if -6 < n <= 0:
+        return "0." + "0" * (-n) + ds
+    e = n - 1
+    es = ("+" if e >= 0 else "-") + str(abs(e))
+    return (ds if k == 1 else ds[0] + "." + ds[1:]) + "e" + es
 
 
 def utf16(text: str) -> np.ndarray:

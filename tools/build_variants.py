@@ -88,8 +88,12 @@ ROWS4 = [("mt_engine.h", "  static constexpr int kRows = 8;          // rows of 
 
 NOLOAD = ("mt_engine.h", "    if (in.loaded) loadSnapshot();", "    if (false) loadSnapshot();")
 
+CW3 = ("mergetree_compact.hip", "launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 4>",
+       "launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 3>")  # the round-2 occupancy
+
 VARIANTS = {
     "prof": [PROF],
+    "cw3": [CW3],
     "noload": [NOLOAD],
     "base": [],
     "cur": [],
