@@ -153,6 +153,7 @@ struct Scratch {
 // Leaf word fields (W0's packing is per tier, see Doc).
 // W4 = leaf id (23 bits) | Marker flag << 23 | insert client << 24
 constexpr uint32_t kW4Marker = 1u << 23;
+constexpr uint32_t kIdLimit = 1u << 23;  // leaf ids are 23-bit: a document allocating more fails (FMT_E_CAPACITY)
 FMT_DEV uint32_t fId(uint32_t w4) { return w4 & 0x7FFFFFu; }
 FMT_DEV bool fMarker(uint32_t w4) { return (w4 & kW4Marker) != 0; }
 FMT_DEV int32_t fClient(uint32_t w4) { return static_cast<int32_t>(static_cast<int8_t>(w4 >> 24)); }
@@ -1241,6 +1242,7 @@ class Doc {
   // splitLeafSegment (mergeTree.ts:1768-1796) of leaf j at `offset` (0 < offset < len): the right
   // part becomes leaf j + 1 of the same block, with a fresh id and the same stamps and props.
   FMT_DEV bool splitLeafAt(int j, int offset) {
+    if (nextId >= kIdLimit) return fail(kCapFinal);
     LeafRec rec;
     const uint32_t w0 = readField(j, 0);
     const uint32_t w4 = readField(j, 4);
@@ -1382,6 +1384,10 @@ class Doc {
     }
     if (nChars + len > kCapChars) {
       fail(FMT_E_CAPACITY);
+      return -1;
+    }
+    if (nextId >= kIdLimit) {
+      fail(kCapFinal);
       return -1;
     }
     const int cpos = static_cast<int>(charOffsetOf(insIdx));
@@ -1611,7 +1617,8 @@ class Doc {
   // posFromRelativePos (mergeTree.ts:1462-1483): the marker whose "markerId" property holds the id
   // (idToMarker: markers stay findable until zamboni unlinks them; with ids unique per document that
   // is every marker leaf still in the tree), its start in the op's perspective, then the side and
-  // offset. Returns -1 when no marker holds the id.
+  // offset. Returns -1 when no marker holds the id, or when it is removed (getMarkerFromId,
+  // mergeTree.ts:1450-1453, returns undefined for a marker with a remove stamp).
   FMT_DEV int posFromRelativePos(uint32_t idx, int refSeq, int client) {
     const uint32_t mid = uni(loadCoherent(&in.relpos[idx].marker_id));
     const int offset = static_cast<int>(uni(loadCoherent(reinterpret_cast<const uint32_t*>(&in.relpos[idx].offset))));
@@ -1648,7 +1655,7 @@ class Doc {
         j = k;
       }
     }
-    if (j < 0) return -1;
+    if (j < 0 || static_cast<int32_t>(readField(j, 2)) != kNotRemoved) return -1;
     Lane<VR> vis, st;
     visLengths(refSeq, client, vis, nr);
     scanRows(vis, st, nr);

@@ -53,6 +53,7 @@ struct fmt_ctx {
   std::string err;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the run's (first) launch
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // around a second launch (large-tier replay), if any
+  hipEvent_t evS0 = nullptr, evS1 = nullptr;  // around the bulk summary kernel (fmt_mt_summarize_legacy)
   bool timed = false, timed2 = false;
   fmt_stats stats{};
 
@@ -184,6 +185,8 @@ int fmt_open(const fmt_config* cfg, fmt_ctx** out) {
   FMT_HIP(c, hipEventCreate(&c->ev1));
   FMT_HIP(c, hipEventCreate(&c->ev2));
   FMT_HIP(c, hipEventCreate(&c->ev3));
+  FMT_HIP(c, hipEventCreate(&c->evS0));
+  FMT_HIP(c, hipEventCreate(&c->evS1));
   FMT_HIP(c, c->errWord.reserve(1));
   return FMT_OK;
 }
@@ -238,6 +241,8 @@ void fmt_close(fmt_ctx* c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
   if (c->ev3) (void)hipEventDestroy(c->ev3);
+  if (c->evS0) (void)hipEventDestroy(c->evS0);
+  if (c->evS1) (void)hipEventDestroy(c->evS1);
   if (c->ownStream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1023,13 +1028,13 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
   FMT_HIP(c, c->sumDocs.reserve(nd));
   FMT_HIP(c, hipMemcpyAsync(c->sumViews.p, views.data(), nd * sizeof(fmt_kernels::SumView), hipMemcpyHostToDevice, c->stream));
   FMT_HIP(c, hipMemsetAsync(c->sumCursors.p, 0, 2 * sizeof(unsigned long long), c->stream));
-  FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
+  FMT_HIP(c, hipEventRecord(c->evS0, c->stream));  // (own events: fmt_get_stats keeps reporting the replay)
   FMT_HIP(c, fmt_kernels::launchSummaryRuns(c->mtHdr.p, c->sumViews.p, nd, c->sumRuns.p, c->sumText.p, c->sumCursors.p,
                                             c->sumDocs.p, c->numCUs, c->stream));
-  FMT_HIP(c, hipEventRecord(c->ev3, c->stream));
+  FMT_HIP(c, hipEventRecord(c->evS1, c->stream));
   FMT_HIP(c, hipStreamSynchronize(c->stream));
   float kms = 0.f;
-  FMT_HIP(c, hipEventElapsedTime(&kms, c->ev2, c->ev3));
+  FMT_HIP(c, hipEventElapsedTime(&kms, c->evS0, c->evS1));
   // fetch: per-document spans, runs, text and the prop sets the runs name
   const auto t0 = clk::now();
   unsigned long long cur[2];
@@ -1079,9 +1084,19 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
           c->sumStatus[d] = static_cast<int32_t>(o.status);
           continue;
         }
+        // every prop set a run names, and every key / value id in it, within the tables passed in
         bool bad = false;
-        for (uint32_t i = 0; i < o.n_runs; i++)
-          if (runs[o.run_off + i].props != 0xFFFFu && runs[o.run_off + i].props >= hdr[d].n_props) bad = true;
+        for (uint32_t i = 0; i < o.n_runs && !bad; i++) {
+          const uint32_t p = runs[o.run_off + i].props;
+          if (p == 0xFFFFu) continue;
+          if (p >= hdr[d].n_props || propsHost[d][p].n > FMT_MT_PROPS_MAX) {
+            bad = true;
+            break;
+          }
+          const fmt_mt_propset& ps = propsHost[d][p];
+          for (uint32_t k = 0; k < ps.n; k++)
+            if ((ps.kv[k] >> 16) >= nKeys || (ps.kv[k] & 0xFFFFu) >= nValues) bad = true;
+        }
         if (bad) {
           c->sumStatus[d] = FMT_E_DATA;
           continue;

@@ -133,6 +133,33 @@ class MergeTreeDocBuilder {
 		this.clientNames = [observer];
 		this.nOps = 0;
 		this.messages = []; // {message, firstOp, count} when the builder keeps messages
+		// idToMarker history (streams.py _DocBuilder): exact while every marker id names one marker
+		// and no annotate rewrites an id
+		this.markerIds = new Set();
+		this.markerAmbiguous = false;
+		this.usesRelpos = false;
+	}
+	noteMarkerId(props) {
+		const mid = props ? props[MARKER_ID_KEY] : undefined;
+		if (mid) {
+			const k = JSON.stringify(mid);
+			if (this.markerIds.has(k)) this.markerAmbiguous = true;
+			this.markerIds.add(k);
+			this.checkMarkers();
+		}
+	}
+	checkMarkers() {
+		if (this.usesRelpos && this.markerAmbiguous) {
+			throw new UnsupportedOp("relative positions in a document whose marker ids repeat or are re-annotated");
+		}
+	}
+	noteOp(op) {
+		if (op === null) return;
+		if (op.type === MT_INSERT && markerRefType(op.seg) !== null) this.noteMarkerId(op.seg.props);
+		if (op.type === MT_ANNOTATE && op.props && Object.prototype.hasOwnProperty.call(op.props, MARKER_ID_KEY)) this.markerAmbiguous = true;
+		const none = (v) => v === undefined || v === null;
+		if ((none(op.pos1) && !none(op.relativePos1)) || (none(op.pos2) && !none(op.relativePos2))) this.usesRelpos = true;
+		this.checkMarkers();
 	}
 	shortClient(longId) {
 		const id = longId === null || longId === undefined ? "server" : longId;
@@ -156,6 +183,7 @@ class MergeTreeDocBuilder {
 		if (members.length === 0) members = [null]; // empty group: only advances the window
 		if (this.owner.keepMessages) this.messages.push({ message: msg, firstOp: this.nOps, count: members.length });
 		members.forEach((op, k) => {
+			this.noteOp(op);
 			this.owner.packOp(op, msg.sequenceNumber, msg.referenceSequenceNumber,
 				msg.minimumSequenceNumber, client, k > 0 ? FMT_MT_F_GROUP_CONT : 0);
 			this.nOps++;
@@ -290,6 +318,7 @@ class MergeTreeStreamBuilder {
 					info = this.mergeInfo(spec, d);
 					spec = spec.json;
 				}
+				if (markerRefType(spec) !== null) d.noteMarkerId(spec.props); // loaded markers register their ids too
 				this.specToSeg(spec);
 				this.snapshotInfo.push(info);
 			}

@@ -228,6 +228,37 @@ class _DocBuilder:
         self.client_names = [observer]
         self.ops: list[tuple] = []
         self.messages: list[tuple] = []
+        # idToMarker history (mergeTree.ts:675, 1614-1620, 2835-2840; zamboni.ts:202-204): the engine
+        # finds a relative position's marker by the "markerId" its leaf holds now, which is the
+        # reference's map as long as every id names one marker and no annotate rewrites an id
+        self.marker_ids: set = set()
+        self.marker_ambiguous = False
+        self.uses_relpos = False
+
+    def note_marker_id(self, props) -> None:
+        mid = (props or {}).get(MARKER_ID_KEY)
+        if mid:
+            k = js_json(mid)
+            self.marker_ambiguous |= k in self.marker_ids
+            self.marker_ids.add(k)
+            self._check_markers()
+
+    def _check_markers(self) -> None:
+        if self.uses_relpos and self.marker_ambiguous:
+            raise UnsupportedOp("relative positions in a document whose marker ids repeat or are re-annotated")
+
+    def _note_op(self, op) -> None:
+        if op is None:
+            return
+        t = op.get("type")
+        if t == MT_INSERT and marker_ref_type(op.get("seg")) is not None:
+            self.note_marker_id(op["seg"].get("props"))
+        if t == MT_ANNOTATE and MARKER_ID_KEY in (op.get("props") or {}):
+            self.marker_ambiguous = True
+        if ((op.get("pos1") is None and op.get("relativePos1") is not None)
+                or (op.get("pos2") is None and op.get("relativePos2") is not None)):
+            self.uses_relpos = True
+        self._check_markers()
 
     @property
     def n_ops(self) -> int:
@@ -257,12 +288,14 @@ class _DocBuilder:
         if self.owner.keep_messages:
             self.messages.append((msg, len(self.ops), len(members)))
         for k, op in enumerate(members):
+            self._note_op(op)
             rec = self.owner._pack(op, seq, ref, msn, client)
             if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
                 rec = rec[:-1] + (rec[-1] | 1,)
             self.ops.append(rec)
 
     def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
+        self._note_op(op)
         self.ops.append(self.owner._pack(op, seq, ref_seq, min_seq, client))
 
 
@@ -439,6 +472,8 @@ class MergeTreeStreamBuilder:
                         raise UnsupportedOp("SnapshotV1 body-chunk segments with merge info")
                     info = self._merge_info(spec, d)
                     spec = spec["json"]
+                if marker_ref_type(spec) is not None:  # loaded markers register their ids too
+                    d.note_marker_id(spec.get("props"))
                 self.snapshot_segs.append(self._spec(spec))
                 self.snapshot_info.append(info)
         n_header = len(specs(h))

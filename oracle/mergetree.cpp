@@ -700,7 +700,8 @@ void MergeTree::unlinkMarker(const Seg* s) {
 
 int MergeTree::posFromRelativePos(const fmt_mt_relpos& rp, const Perspective& p) const {
   const auto it = rp.marker_id == FMT_MT_NO_MARKER ? idToMarker.end() : idToMarker.find(rp.marker_id);
-  if (it == idToMarker.end()) return -1;
+  // getMarkerFromId (mergeTree.ts:1450-1453): a removed marker is not found
+  if (it == idToMarker.end() || it->second->removed()) return -1;
   int pos = getPosition(it->second, p);
   if (rp.flags & FMT_MT_REL_BEFORE) pos -= rp.offset;
   else pos += it->second->len() + rp.offset;  // cachedLength (1 for a marker)

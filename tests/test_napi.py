@@ -119,6 +119,25 @@ def test_js_packer_sided_obliterate_matches_python(addon):
     assert [int(f) for f in py.ops["flags"]] == [16, 0, 8 | 1]
 
 
+def test_js_packer_refuses_ambiguous_marker_ids(addon):
+    """Mirror of test_relative_pos.py::test_ambiguous_marker_ids_are_refused in the JS packer."""
+    msgs = [
+        {"clientId": "B", "sequenceNumber": 1, "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+         "contents": {"type": 0, "pos1": 1, "seg": {"marker": {"refType": 1}, "props": {"markerId": "m"}}}},
+        {"clientId": "B", "sequenceNumber": 2, "referenceSequenceNumber": 1, "minimumSequenceNumber": 0,
+         "contents": {"type": 2, "pos1": 1, "pos2": 2, "props": {"markerId": "n"}}},
+        {"clientId": "C", "sequenceNumber": 3, "referenceSequenceNumber": 2, "minimumSequenceNumber": 0,
+         "contents": {"type": 0, "relativePos1": {"id": "n"}, "seg": "X"}},
+    ]
+    js = (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          "const b=new fmt.MergeTreeStreamBuilder();const d=b.beginDoc('abc','A');"
+          f"const m={json.dumps(msgs)};d.addMessage(m[0]);d.addMessage(m[1]);"
+          "try{d.addMessage(m[2]);console.log('packed')}catch(e){console.log(e.name+':'+(e instanceof fmt.UnsupportedOp))}")
+    r = _node("-e", js)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().endswith(":true"), r.stdout
+
+
 def test_js_map_packer_orders_bunches(addon):
     """Messages of one bunch share a sequenceNumber; the packer keeps their order via the ordinal."""
     r = _node("-e", """
