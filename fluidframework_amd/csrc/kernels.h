@@ -5,6 +5,10 @@
 
 #include "../../include/fmt.h"
 
+namespace fmt_mt {
+struct AdjustTables;  // mt_engine.h
+}
+
 namespace fmt_kernels {
 
 // ---- SharedMap LWW (map_lww.hip)
@@ -39,6 +43,7 @@ struct MtDeviceBatch {
   const fmt_mt_relpos* relpos;     // relative positions (FMT_MT_F_REL1/REL2 ops), or nullptr
   uint32_t nRelpos;
   uint32_t markerKey;              // key id of "markerId", FMT_MT_NO_MARKER if none
+  const fmt_mt::AdjustTables* adj;  // annotate-adjust tables (device memory), nullptr when none
 };
 
 struct MtDeviceOut {
@@ -86,15 +91,16 @@ MtCaps mergeTreeCaps(bool large);
 // nullptr. A plain batch (no obliterates, no remove order) with esc2 != nullptr starts in the compact
 // tier and lists its overflow in esc2 (count + 1 entries) for the small tier. esc[0] and esc2[0] must
 // be zero before the call. sched: 3 zeroed device counters (compact, small, large) from which the
-// tiers deal documents to waves dynamically (nullptr: static grid-stride shares).
+// tiers deal documents to waves dynamically (nullptr: static grid-stride shares). adjust: the batch
+// holds annotate-adjust entries (the Adj engine variants, small tier first, no checkpoints).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
-                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched);
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                 uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
-                                uint32_t* next);
+                                uint32_t* next, bool adjust);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

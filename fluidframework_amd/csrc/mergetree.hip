@@ -86,9 +86,14 @@ __global__ __launch_bounds__(1024) void orderByRemainingKernel(const uint32_t* _
 // Variants: obliterates (Ob) and/or the remove-order recording of SnapshotV1 batches (Rm).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
-                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched) {
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust) {
   using S = fmt_mt::SmallTier;
   uint32_t* n1 = sched ? sched + 1 : nullptr;
+  if (adjust) {  // annotate-adjust batches: the Adj variants, small tier over every document (no checkpoints)
+    if (removeOrder)
+      return launchTier<true, S, true, kMtWaves, 2, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
+    return launchTier<true, S, false, kMtWaves, 2, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
+  }
   if (obliterate && removeOrder)
     return launchTier<true, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   if (obliterate && (esc == nullptr || esc2 == nullptr))

@@ -10,8 +10,12 @@ int mergeTreeProfileLarge(uint64_t* out, int n, bool reset) { return addTuProfil
 
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                 uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
-                                uint32_t* next) {
+                                uint32_t* next, bool adjust) {
   using G = fmt_mt::LargeTier;
+  if (adjust && removeOrder)
+    return launchTier<true, G, true, kMtWavesLarge, 1, true>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
+  if (adjust)
+    return launchTier<true, G, false, kMtWavesLarge, 1, true>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (obliterate && removeOrder)
     return launchTier<true, G, true, kMtWavesLarge, 1>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (obliterate)

@@ -163,6 +163,8 @@ struct LeafRec {
   uint32_t w[7];  // W0..W4, and W5, W6 in the large tier
 };
 
+struct AdjustTables;
+
 struct DocInputs {
   const fmt_mt_op* ops;
   uint64_t begin, end;
@@ -180,6 +182,27 @@ struct DocInputs {
   const fmt_mt_relpos* relpos;  // FMT_MT_F_REL1/REL2 ops index it (nullptr: none in the batch)
   uint32_t nRelpos;
   uint32_t markerKey;           // key id of "markerId"
+  // annotate-adjust (nullptr: none in the batch), see Doc::adjustValue; read on demand, so the rare
+  // path keeps no registers across the op loop
+  const AdjustTables* adj;
+  uint32_t doc;                 // this document's index (its number slab and count)
+};
+
+// Annotate-adjust tables of a batch (device memory): the rows, the number of each host value id
+// (NaN: not a number), the host's numbers ascending with their value ids, and per document a slab
+// of computed numbers (numOffsets) with its count (numCount, kept in memory across tiers).
+struct AdjustTables {
+  const fmt_mt_adjust* adjusts;
+  uint32_t nAdjusts;
+  uint32_t nValues;
+  const double* valueNum;
+  const double* numSorted;
+  const uint32_t* numSortedId;
+  uint32_t nNumSorted;
+  uint32_t pad;
+  double* nums;
+  const uint64_t* numOffsets;  // nDocs + 1
+  uint32_t* numCount;          // nDocs
 };
 
 struct DocOutputs {
@@ -212,11 +235,79 @@ enum ProfCat {
   kPfInsChars, kPfInsShift, kPfZFind, kPfZChars, kPfZSerial, kPfZDelete, kPfZPack, kPfCount
 };
 
+// ------------------------------------------------------------------ annotate-adjust
+// computePropertyValue for one adjust change (segmentPropertiesManager.ts:54-78): the current value's
+// number (typeof "number", else 0) + delta, then max clamps, else min, in IEEE double. A change's
+// current value is always the running fold of the key's changes in seq order (every remote change
+// folds into properties[key] when it applies, :199-235), so the replay state needs no per-segment
+// change lists. Returns the result's value id (0: null, the key is deleted) or a kAdjFail* code.
+// Compiled only into the Doc<..., Adj = true> variants (batches with adjusts): inlined into the op
+// loop it costs the register allocation of every other variant (measured: ~1000 VGPR spills).
+constexpr uint32_t kAdjFailData = 0xFFFFFFFFu, kAdjFailCap = 0xFFFFFFFEu;
+
+FMT_DEV double adjNumberOf(const AdjustTables* A, uint32_t doc, uint32_t id) {  // NaN: not a number
+  if (id >= FMT_MT_VALUE_COMPUTED) {
+    const uint32_t k = id - FMT_MT_VALUE_COMPUTED;
+    const uint32_t cnt = uni(loadCoherent(A->numCount + doc));
+    return k < cnt ? uniD(loadCoherentD(A->nums + A->numOffsets[doc] + k)) : __builtin_nan("");
+  }
+  return id < A->nValues ? uniD(A->valueNum[id]) : __builtin_nan("");
+}
+
+// The value id of a number: the host's id of an equal number (binary search of its sorted numbers),
+// else the document table's entry (lane-parallel search), else a new entry. -0 is +0 (=== equal, and
+// JSON.stringify writes both as 0).
+FMT_DEV uint32_t adjNumberId(const AdjustTables* A, uint32_t doc, double x) {
+  if (x == 0.0) x = 0.0;
+  const int ns = static_cast<int>(uni(A->nNumSorted));
+  int lo = 0, hi = ns;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (uniD(A->numSorted[mid]) < x) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < ns && uniD(A->numSorted[lo]) == x) return uni(A->numSortedId[lo]);
+  double* nums = A->nums + A->numOffsets[doc];
+  const uint32_t cap = static_cast<uint32_t>(A->numOffsets[doc + 1] - A->numOffsets[doc]);
+  const uint32_t cnt = uni(loadCoherent(A->numCount + doc));
+  for (uint32_t base = 0; base < cnt; base += 64) {
+    Lane<bool> eq;
+    FOR_LANES(l) { LANE(eq) = base + l < cnt && loadCoherentD(nums + base + l) == x; }
+    const uint64_t m = ballot(eq);
+    if (m != 0) return FMT_MT_VALUE_COMPUTED + base + static_cast<uint32_t>(ctz64(m));
+  }
+  if (cnt >= cap) return kAdjFailCap;
+  FOR_LANES(l) {
+    if (l == 0) {
+      storeGlobal(nums + cnt, x);
+      storeGlobal(A->numCount + doc, cnt + 1);
+    }
+  }
+  return FMT_MT_VALUE_COMPUTED + cnt;
+}
+
+FMT_DEV uint32_t adjustFold(const AdjustTables* A, uint32_t doc, uint32_t cur, uint32_t row) {
+  if (A == nullptr || row >= A->nAdjusts) return kAdjFailData;
+  const fmt_mt_adjust* R = A->adjusts + row;
+  const double delta = uniD(R->delta), mn = uniD(R->min), mx = uniD(R->max);
+  const uint32_t fl = uni(R->flags);
+  const double c = adjNumberOf(A, doc, cur);
+  const double adjusted = (c == c ? c : 0.0) + delta;
+  // `adjusted > adjust.max` with a null max compares against 0 and assigns null
+  if ((fl & FMT_MT_ADJ_MAX) != 0 && adjusted > ((fl & FMT_MT_ADJ_MAX_NULL) ? 0.0 : mx))
+    return (fl & FMT_MT_ADJ_MAX_NULL) ? 0u : adjNumberId(A, doc, mx);
+  if ((fl & FMT_MT_ADJ_MIN) != 0 && adjusted < ((fl & FMT_MT_ADJ_MIN_NULL) ? 0.0 : mn))
+    return (fl & FMT_MT_ADJ_MIN_NULL) ? 0u : adjNumberId(A, doc, mn);
+  return adjNumberId(A, doc, adjusted);
+}
+
 // Ob: the engine variant that also replays obliterates (f1). Without obliterates in a batch the
 // runtime launches Doc<false>, whose code is exactly the obliterate-free engine.
 // Rm: the variant that records the remove order for SnapshotV1 summaries (FMT_MT_F_RMORDER ops);
 // batches without such ops run the Rm = false code, which has none of it.
-template <bool Ob, class C = SmallTier, bool Rm = false>
+// Adj: the variant that folds annotate-adjust entries (batches with adjusts; always with Ob, whose
+// runtime path restarts overflowing documents in the next tier instead of checkpointing them).
+template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false>
 class Doc {
  public:
   using VR = typename C::VR;
@@ -1026,6 +1117,8 @@ class Doc {
 
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
   // The working set lives in LDS (kvWork, lane k = key slot k), so the sets' width costs no registers.
+  // (AdjSite: the annotate call site, the only one whose props ops can hold annotate-adjust entries)
+  template <bool AdjSite = false>
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
     uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
     FOR_LANES(l) {
@@ -1034,12 +1127,32 @@ class Doc {
     waveSync();
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
     for (uint32_t t = a; t < b; t++) {
-      const uint32_t e = uni(in.propsKv[t]);
+      uint32_t e = uni(in.propsKv[t]);
       const uint32_t key = e >> 16;
       Lane<bool> hit;
       FOR_LANES(l) { LANE(hit) = l < static_cast<int>(cnt) && (s->kvWork[l] >> 16) == key; }
       const uint64_t m = ballot(hit);
       const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
+      if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {  // annotate-adjust: fold into the current value
+        // (an insert's or a loaded segment's props hold raw values only; batches with adjusts run the
+        // Adj variant)
+        if constexpr (AdjSite && Adj) {
+          if (++t >= b) {
+            fail(FMT_E_DATA);
+            return 0;
+          }
+          const uint32_t cur = pos < cnt ? uni(s->kvWork[pos]) & 0xFFFFu : 0u;  // absent: null
+          const uint32_t v = adjustFold(in.adj, in.doc, cur, uni(in.propsKv[t]));
+          if (v == kAdjFailData || v == kAdjFailCap) {
+            fail(v == kAdjFailData ? FMT_E_DATA : kCapFinal);
+            return 0;
+          }
+          e = (key << 16) | v;
+        } else {
+          fail(AdjSite ? FMT_E_UNSUPPORTED : FMT_E_DATA);
+          return 0;
+        }
+      }
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
         if (pos < cnt) {
           Lane<uint32_t> v;
@@ -1090,6 +1203,12 @@ class Doc {
     return static_cast<uint32_t>(nProps++);
   }
 
+  // ------------------------------------------------------------------ annotate-adjust
+  // computePropertyValue for one adjust change (segmentPropertiesManager.ts:54-78): the current
+  // value's number (typeof "number", else 0) + delta, then max clamps, else min, in IEEE double.
+  // A change's current value is always the running fold of the key's changes in seq order (every
+  // remote change folds into properties[key] when it applies, :199-235), so the replay state needs
+  // no per-segment change lists. Returns the result's value id (0: null, the key is deleted).
   // ------------------------------------------------------------------ catch-up ranges
   // The ranges of the op's sequenceDelta event, merged as createOpsFromDelta merges them
   // (sequence/src/sequence.ts:395-452) and recorded for the legacy summary's catch-up ops. `delta`
@@ -1824,7 +1943,7 @@ class Doc {
         const int j = firstSet(todo, nr);
         if (j < 0) break;
         const uint32_t old = propsAt(j);
-        const uint32_t nw = applyProps(old, op.payload);
+        const uint32_t nw = applyProps<true>(old, op.payload);
         if (status != FMT_OK) return false;
         FOR_ROWS(r, 0, nr) {
           FOR_LANES(l) {
@@ -1862,9 +1981,12 @@ class Doc {
     // all leaves, at their char offsets from a scan of the block's lengths)
     const int r0 = first >> 6, r1 = (first + cnt - 1) >> 6;
     Lane<uint32_t> pk0, pk1;
+    Lane<uint32_t> pp0, pp1;  // (large tier: prop-set ids of up to 1024 sets beside the packed words)
     FOR_LANES(l) {
       LANE(pk0) = 0u;
       LANE(pk1) = 0u;
+      LANE(pp0) = 0u;
+      LANE(pp1) = 0u;
     }
     uint32_t cs = charOffsetOf(first);  // running char offset of leaf first + k
     uint32_t rowBase = cs;
@@ -1882,11 +2004,15 @@ class Doc {
         const uint32_t bl = LANE(blen);
         const bool nl = bl > 0 && chRead(static_cast<int>(rowBase + LANE(ex) + bl - 1)) == 10u;
         const uint32_t pr = propsL(l, r);
-        const uint32_t p = fLen(w0) | ((kPW ? (pr == kPropsUndef ? 0x7Fu : pr) : pr) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
+        const uint32_t p = fLen(w0) | ((kPW ? 0u : pr) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
                            (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u) | (nl ? 1u << 27 : 0u) |
                            (fMarker(LANE(W[4])[r]) ? 1u << 28 : 0u);
         if (r == r0) LANE(pk0) = p;
         else LANE(pk1) = p;
+        if constexpr (kPW) {
+          if (r == r0) LANE(pp0) = pr;
+          else LANE(pp1) = pr;
+        }
       }
       rowBase += tot;
     }
@@ -1900,8 +2026,9 @@ class Doc {
     for (int k = 0; k < cnt; k++) {
       const int j = first + k;
       const uint32_t p = (j >> 6) == r0 ? readlane(pk0, j & 63) : readlane(pk1, j & 63);
-      const uint32_t len = p & kLenMask, pp = (p >> C::kLenBits) & (kPW ? 0x7Fu : kPropsUndef);
-      const uint32_t props = kPW && pp == 0x7Fu ? kPropsUndef : pp;
+      const uint32_t len = p & kLenMask;
+      uint32_t props = (p >> C::kLenBits) & kPropsUndef;
+      if constexpr (kPW) props = (j >> 6) == r0 ? readlane(pp0, j & 63) : readlane(pp1, j & 63);
       s->tmp[k] = cs;  // char offset and length, for the deletions below
       s->tmp[kMaxNodes + k] = len;
       if (((p >> 24) & 1u) == 0) {
@@ -2583,6 +2710,7 @@ class Doc {
     cuOut = out.catchup;
     cuCap = out.catchup ? out.catchupCap : 0u;
     cuN = 0;
+
     rmOut = out.rmOrder;
     rmCap = out.rmOrder ? out.rmOrderCap : 0u;
     rmN = 0;
@@ -2593,10 +2721,15 @@ class Doc {
     bigCkpt = out.bigCkpt;
     bigCkptChars = out.bigCkptChars;
     if (kResumesCkpt && ckpt != nullptr && out.ckptResume) {
-      first = restoreCkpt();
+      first = restoreCkpt();  // (computed numbers: the slab and its count stay in memory)
     } else if (kResumesBig && bigCkpt != nullptr && out.ckptResume) {
       first = restoreBig();
     } else {
+      if (in.adj != nullptr) {  // a fresh replay (also a restart in the next tier) starts an empty table
+        FOR_LANES(l) {
+          if (l == 0) storeGlobal(in.adj->numCount + in.doc, 0u);
+        }
+      }
       if (in.loaded) loadSnapshot();
       else loadInitial();
     }

@@ -17,6 +17,7 @@
 #include "../../include/fmt.h"
 #include "huge_engine.h"
 #include "jsnum.h"
+#include "mt_engine.h"  // fmt_mt::AdjustTables
 #include "kernels.h"
 
 namespace {
@@ -126,6 +127,17 @@ struct fmt_ctx {
   std::vector<std::string> sumBlobs;          // per document: header, then body
   std::vector<uint32_t> sumSplit;             // per document: header length in sumBlobs[d]
   std::vector<int32_t> sumStatus;
+  // annotate-adjust: rows, numbers of host value ids, host numbers sorted for number → id lookups,
+  // per-document computed-number slabs and their counts
+  DevBuf<fmt_mt_adjust> mtAdjusts;
+  DevBuf<double> mtValueNum, mtNumSorted, mtNums;
+  DevBuf<uint32_t> mtNumSortedId, mtNumCount;
+  DevBuf<uint64_t> mtNumOffs;
+  DevBuf<fmt_mt::AdjustTables> mtAdjTab;      // the pointers above, for the kernels
+  std::vector<uint64_t> mtNumOffsHost;
+  std::vector<int32_t> mtAdjLastSeq;          // per doc: last seq of an annotate of an adjusted key (0: none)
+  bool mtHasAdjust = false;
+  uint32_t mtNAdjusts = 0, mtNValues = 0, mtNNumSorted = 0;
   DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
   uint32_t mtNSmall = 0;
   DevBuf<fmt_huge::HugeState> hugeStates;
@@ -512,6 +524,36 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       initChars += b->doc_init[2 * d + 1];
     }
   }
+  // Annotate-adjust entries (FMT_MT_VALUE_ADJUST + row index) in the props ops: validated here; per
+  // document they size its computed-number slab and decide whether its legacy summary is exact.
+  const uint32_t nKvAll = b->props_off ? b->props_off[b->n_props_ops] : 0;
+  std::vector<uint32_t> adjCount(b->n_props_ops, 0);  // adjust entries per props op
+  bool anyAdjust = false;
+  for (uint32_t op = 0; b->props_off && op < b->n_props_ops; op++) {
+    const uint32_t a = b->props_off[op], e = b->props_off[op + 1];
+    if (a > e || e > nKvAll) return setErr(c, FMT_E_USAGE, "props_off is not ascending");
+    for (uint32_t t = a; t < e; t++) {
+      const uint32_t v = b->props_kv[t] & 0xFFFFu;
+      if (v == FMT_MT_VALUE_ADJUST) {
+        if (t + 1 >= e || b->adjusts == nullptr || b->props_kv[t + 1] >= b->n_adjusts)
+          return setErr(c, FMT_E_DATA, "annotate-adjust entry without a valid adjust row");
+        adjCount[op]++;
+        anyAdjust = true;
+        t++;
+      }
+    }
+  }
+  if (anyAdjust) {
+    if (b->value_num == nullptr && b->n_values > 0) return setErr(c, FMT_E_USAGE, "adjusts need value_num");
+    for (uint32_t t = 0; t < nKvAll; t++) {
+      const uint32_t v = b->props_kv[t] & 0xFFFFu;
+      if (v == FMT_MT_VALUE_ADJUST) {
+        t++;
+      } else if (v >= FMT_MT_VALUE_COMPUTED) {
+        return setErr(c, FMT_E_USAGE, "host value ids must stay below FMT_MT_VALUE_COMPUTED in a batch with adjusts");
+      }
+    }
+  }
   const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(false);
   FMT_HIP(c, hipSetDevice(c->device));
   FMT_HIP(c, c->mtOps.reserve(b->n_ops));
@@ -563,6 +605,80 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
   };
+  // Computed-number slabs: 8 per adjust entry of the document's annotates + 16 (at most 0x7fff,
+  // the computed id range); a document that computes more distinct numbers reports FMT_E_CAPACITY.
+  c->mtHasAdjust = anyAdjust;
+  c->mtAdjLastSeq.assign(n, 0);
+  if (anyAdjust) {
+    c->mtNumOffsHost.assign(n + 1ull, 0);
+    for (uint32_t d = 0; d < n; d++) {
+      uint64_t f = 0;
+      std::vector<uint32_t> adjKeys;  // keys some annotate of this document adjusts
+      for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+        const fmt_mt_op& op = b->ops[i];
+        if (op.type != FMT_MT_ANNOTATE || adjCount[op.payload] == 0) continue;
+        f += adjCount[op.payload];
+        for (uint32_t t = b->props_off[op.payload]; t < b->props_off[op.payload + 1]; t++)
+          if ((b->props_kv[t] & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
+            adjKeys.push_back(b->props_kv[t] >> 16);
+            t++;
+          }
+      }
+      c->mtNumOffsHost[d + 1] = c->mtNumOffsHost[d] + (f ? std::min<uint64_t>(8 * f + 16, 0x7FFF) : 0);
+      if (adjKeys.empty()) continue;
+      // legacy getAtSeq(minSeq) is exact unless an adjusted key is annotated above the final minSeq
+      for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+        const fmt_mt_op& op = b->ops[i];
+        if (op.type != FMT_MT_ANNOTATE) continue;
+        for (uint32_t t = b->props_off[op.payload]; t < b->props_off[op.payload + 1]; t++) {
+          if (std::find(adjKeys.begin(), adjKeys.end(), b->props_kv[t] >> 16) != adjKeys.end())
+            c->mtAdjLastSeq[d] = std::max(c->mtAdjLastSeq[d], op.seq);
+          if ((b->props_kv[t] & 0xFFFFu) == FMT_MT_VALUE_ADJUST) t++;
+        }
+      }
+    }
+    std::vector<std::pair<double, uint32_t>> nums;
+    for (uint32_t i = 0; b->value_num && i < b->n_values; i++)
+      if (b->value_num[i] == b->value_num[i]) nums.emplace_back(b->value_num[i] == 0.0 ? 0.0 : b->value_num[i], i);
+    std::stable_sort(nums.begin(), nums.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    std::vector<double> sv;
+    std::vector<uint32_t> si;
+    for (const auto& [x, i] : nums) {
+      if (!sv.empty() && sv.back() == x) continue;  // (one text per number: the first id)
+      sv.push_back(x);
+      si.push_back(i);
+    }
+    c->mtNAdjusts = b->n_adjusts;
+    c->mtNValues = b->value_num ? b->n_values : 0u;
+    c->mtNNumSorted = static_cast<uint32_t>(sv.size());
+    FMT_HIP(c, c->mtAdjusts.reserve(b->n_adjusts));
+    FMT_HIP(c, c->mtValueNum.reserve(c->mtNValues));
+    FMT_HIP(c, c->mtNumSorted.reserve(sv.size()));
+    FMT_HIP(c, c->mtNumSortedId.reserve(si.size()));
+    FMT_HIP(c, c->mtNumOffs.reserve(n + 1ull));
+    FMT_HIP(c, c->mtNums.reserve(c->mtNumOffsHost[n]));
+    FMT_HIP(c, c->mtNumCount.reserve(n));
+    FMT_HIP(c, cp(c->mtAdjusts.p, b->adjusts, b->n_adjusts * sizeof(fmt_mt_adjust)));
+    FMT_HIP(c, cp(c->mtValueNum.p, b->value_num, c->mtNValues * sizeof(double)));
+    FMT_HIP(c, cp(c->mtNumSorted.p, sv.data(), sv.size() * sizeof(double)));
+    FMT_HIP(c, cp(c->mtNumSortedId.p, si.data(), si.size() * sizeof(uint32_t)));
+    FMT_HIP(c, cp(c->mtNumOffs.p, c->mtNumOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
+    FMT_HIP(c, hipMemsetAsync(c->mtNumCount.p, 0, n * sizeof(uint32_t), c->stream));
+    fmt_mt::AdjustTables T{};
+    T.adjusts = c->mtAdjusts.p;
+    T.nAdjusts = b->n_adjusts;
+    T.nValues = c->mtNValues;
+    T.valueNum = c->mtValueNum.p;
+    T.numSorted = c->mtNumSorted.p;
+    T.numSortedId = c->mtNumSortedId.p;
+    T.nNumSorted = c->mtNNumSorted;
+    T.nums = c->mtNums.p;
+    T.numOffsets = c->mtNumOffs.p;
+    T.numCount = c->mtNumCount.p;
+    FMT_HIP(c, c->mtAdjTab.reserve(1));
+    FMT_HIP(c, cp(c->mtAdjTab.p, &T, sizeof T));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));  // (sv / si / T are about to go out of scope)
+  }
   FMT_HIP(c, cp(c->mtOps.p, b->ops, b->n_ops * sizeof(fmt_mt_op)));
   FMT_HIP(c, cp(c->mtOffs.p, b->doc_op_offsets, (n + 1ull) * sizeof(uint64_t)));
   FMT_HIP(c, cp(c->mtText.p, b->text, b->text_len * sizeof(uint16_t)));
@@ -638,10 +754,13 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
           if (b->snapshot_info[k].ins_seq != 0 || b->snapshot_info[k].rm_count != 0)
             return setErr(c, FMT_E_UNSUPPORTED, "SnapshotV1 merge info in a document beyond the large tier");
       }
-      for (uint64_t i = o0; i < o1; i++)
+      for (uint64_t i = o0; i < o1; i++) {
         if (b->ops[i].flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2))
           return setErr(c, FMT_E_UNSUPPORTED,
                         "catch-up / remove-order recording or relative positions in a document beyond the large tier");
+        if (b->ops[i].type == FMT_MT_ANNOTATE && adjCount[b->ops[i].payload] > 0)
+          return setErr(c, FMT_E_UNSUPPORTED, "annotate-adjust in a document beyond the large tier");
+      }
       c->mtHugeSlot[d] = static_cast<int32_t>(c->huge.size());
       c->huge.emplace_back();
       auto& H = c->huge.back();
@@ -741,10 +860,11 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasRmOrder ? c->mtRmOffs.p : nullptr,
                                 c->mtHasSnapInfo ? c->mtSnapInfo.p : nullptr, c->mtHasSnapInfo ? c->mtSnapStamps.p : nullptr,
                                 c->mtNRelpos ? c->mtRelpos.p : nullptr,
-                                c->mtNRelpos, c->mtMarkerKey};
+                                c->mtNRelpos, c->mtMarkerKey,
+                                c->mtHasAdjust ? c->mtAdjTab.p : nullptr};
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
-                                !c->mtHasRmOrder && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
+                                !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
@@ -754,7 +874,7 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,
                                             c->mtObliterate,
-                                            c->mtHasRmOrder, c->mtSched.p));
+                                            c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust));
   if (hasHuge)
     FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p,
                                            static_cast<uint32_t>(c->huge.size()), c->stream));
@@ -772,11 +892,11 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
                                   c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
-                                  c->mtObliterate && !c->mtHasRmOrder && c->mtCkptOk ? c->mtCkpt.p : nullptr,
+                                  c->mtObliterate && !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr,
                                   !c->mtHasRmOrder ? c->mtLeaves.p : nullptr, !c->mtHasRmOrder ? c->mtChars.p : nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
-                                                 c->mtHasRmOrder, c->mtSched.p + 2));
+                                                 c->mtHasRmOrder, c->mtSched.p + 2, c->mtHasAdjust));
     FMT_HIP(c, hipEventRecord(c->ev3, c->stream));
     c->timed2 = true;
     std::vector<uint32_t> list(nEsc);
@@ -914,7 +1034,7 @@ struct SumDict {
 
 // A prop set as a JSON object in JS own-property order: array-index keys ascending, then the
 // others in insertion order (properties' key order, snapshotChunks.ts via JSON.stringify).
-void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D) {
+void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D, const std::vector<double>* nums) {
   const uint32_t n = ps.n < FMT_MT_PROPS_MAX ? ps.n : FMT_MT_PROPS_MAX;
   uint32_t order[FMT_MT_PROPS_MAX];
   uint32_t m = 0;
@@ -929,7 +1049,11 @@ void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D) {
     const uint32_t kv = ps.kv[order[j]];
     o += D.keys[kv >> 16];
     o.push_back(':');
-    o += D.values[kv & 0xFFFFu];
+    const uint32_t v = kv & 0xFFFFu;
+    if (nums != nullptr && v >= FMT_MT_VALUE_COMPUTED)  // an annotate-adjust result
+      o += fmt_json::jsNumber((*nums)[v - FMT_MT_VALUE_COMPUTED]);
+    else
+      o += D.values[v];
   }
   o.push_back('}');
 }
@@ -938,7 +1062,7 @@ void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D) {
 // the header chunk (runs until >= chunk units) and, when runs remain, the body chunk.
 void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* runs, uint32_t nRuns,
                  const uint16_t* text, const fmt_mt_propset* props, int32_t minSeq, uint32_t chunk,
-                 const SumDict& D) {
+                 const SumDict& D, const std::vector<double>* nums) {
   uint64_t total = 0;
   for (uint32_t i = 0; i < nRuns; i++) total += runs[i].len;
   std::vector<uint64_t> start(nRuns + 1, 0);
@@ -959,14 +1083,14 @@ void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* r
         out += "{\"marker\":{\"refType\":" + std::to_string(text[start[i]]) + "}";
         if (hasProps) {
           out += ",\"props\":";
-          propsObject(out, props[r.props], D);
+          propsObject(out, props[r.props], D, nums);
         }
         out.push_back('}');
       } else if (hasProps) {
         out += "{\"text\":";
         jsonQuote16(out, text + start[i], r.len);
         out += ",\"props\":";
-        propsObject(out, props[r.props], D);
+        propsObject(out, props[r.props], D, nums);
         out.push_back('}');
       } else {
         jsonQuote16(out, text + start[i], r.len);
@@ -1063,6 +1187,19 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
                               hipMemcpyDeviceToHost, c->stream));
     propsHost[d] = otherProps.back().data();
   }
+  // computed annotate-adjust numbers of the documents that have any
+  std::vector<std::vector<double>> docNums(c->mtHasAdjust ? nd : 0);
+  if (c->mtHasAdjust) {
+    std::vector<uint32_t> cnt(nd);
+    FMT_HIP(c, hipMemcpyAsync(cnt.data(), c->mtNumCount.p, nd * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t d = 0; d < nd; d++) {
+      docNums[d].resize(cnt[d]);
+      if (cnt[d])
+        FMT_HIP(c, hipMemcpyAsync(docNums[d].data(), c->mtNums.p + c->mtNumOffsHost[d], cnt[d] * sizeof(double),
+                                  hipMemcpyDeviceToHost, c->stream));
+    }
+  }
   FMT_HIP(c, hipStreamSynchronize(c->stream));
   const auto t1 = clk::now();
   // format on host threads
@@ -1084,6 +1221,12 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
           c->sumStatus[d] = static_cast<int32_t>(o.status);
           continue;
         }
+        // getAtSeq(minSeq) would fold only part of a segment's pending adjust history
+        if (c->mtHasAdjust && c->mtAdjLastSeq[d] > hdr[d].min_seq) {
+          c->sumStatus[d] = FMT_E_UNSUPPORTED;
+          continue;
+        }
+        const std::vector<double>* nums = c->mtHasAdjust ? &docNums[d] : nullptr;
         // every prop set a run names, and every key / value id in it, within the tables passed in
         bool bad = false;
         for (uint32_t i = 0; i < o.n_runs && !bad; i++) {
@@ -1094,8 +1237,11 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
             break;
           }
           const fmt_mt_propset& ps = propsHost[d][p];
-          for (uint32_t k = 0; k < ps.n; k++)
-            if ((ps.kv[k] >> 16) >= nKeys || (ps.kv[k] & 0xFFFFu) >= nValues) bad = true;
+          for (uint32_t k = 0; k < ps.n; k++) {
+            const uint32_t v = ps.kv[k] & 0xFFFFu;
+            const bool computed = nums != nullptr && v >= FMT_MT_VALUE_COMPUTED && v - FMT_MT_VALUE_COMPUTED < nums->size();
+            if ((ps.kv[k] >> 16) >= nKeys || (v >= nValues && !computed)) bad = true;
+          }
         }
         if (bad) {
           c->sumStatus[d] = FMT_E_DATA;
@@ -1103,7 +1249,7 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
         }
         c->sumBlobs[d].reserve(o.n_units + 64ull * o.n_runs + 256);
         legacyBlobs(c->sumBlobs[d], &c->sumSplit[d], runs.data() + o.run_off, o.n_runs, text.data() + o.text_off,
-                    propsHost[d], hdr[d].min_seq, chunk ? chunk : 10000u, D);
+                    propsHost[d], hdr[d].min_seq, chunk ? chunk : 10000u, D, nums);
       }
     });
   for (auto& th : pool) th.join();
@@ -1152,6 +1298,17 @@ int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
   const uint32_t m = h.n_rm_order < cap ? h.n_rm_order : cap;
   if (m) FMT_HIP(c, hipMemcpy(out, c->mtRmOrder.p + c->mtRmOffsHost[doc], m * sizeof(fmt_mt_remove_order), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_numbers(fmt_ctx* c, uint32_t doc, double* out, uint32_t cap, uint32_t* nOut) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_numbers: bad arguments");
+  uint32_t n = 0;
+  if (c->mtHasAdjust) FMT_HIP(c, hipMemcpy(&n, c->mtNumCount.p + doc, sizeof n, hipMemcpyDeviceToHost));
+  if (nOut) *nOut = n;
+  const uint32_t m = n < cap ? n : cap;
+  if (m) FMT_HIP(c, hipMemcpy(out, c->mtNums.p + c->mtNumOffsHost[doc], m * sizeof(double), hipMemcpyDeviceToHost));
   return FMT_OK;
 }
 

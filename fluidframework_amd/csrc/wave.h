@@ -60,6 +60,17 @@ FMT_DEV uint32_t loadCoherent(const uint32_t* p) {
 FMT_DEV int32_t loadCoherent(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A store to a global buffer whose pointer was loaded from memory (so the compiler cannot infer its
+// address space): written as a global store, a flat store could alias the wave's private arrays and
+// would force them out of registers around it.
+template <class T>
+FMT_DEV void storeGlobal(T* p, T v) {
+  *reinterpret_cast<__attribute__((address_space(1))) T*>(reinterpret_cast<uintptr_t>(p)) = v;
+}
+FMT_DEV double loadCoherentD(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
 // A global value this workgroup wrote: a workgroup-scope atomic load is a plain vector load (served by
 // the CU's L1, which this CU's own stores keep current) that the compiler never turns into a scalar
 // (K$) load, whose cache vector stores do not update.
@@ -72,6 +83,11 @@ FMT_DEV void atomicAddLds(int32_t* p, int v) { atomicAdd(p, v); }
 // Make a wave-uniform value provably uniform (lives in an SGPR afterwards).
 FMT_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 FMT_DEV uint32_t uni(uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x))); }
+FMT_DEV double uniD(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const uint64_t u = uni(static_cast<uint32_t>(b)) | (static_cast<uint64_t>(uni(static_cast<uint32_t>(b >> 32))) << 32);
+  return __builtin_bit_cast(double, u);
+}
 
 FMT_DEV uint64_t ballot(const Lane<bool>& p) { return __ballot(p.v); }
 
@@ -224,6 +240,10 @@ inline void launder(T&) {}
 inline uint32_t loadCoherent(const uint16_t* p) { return *p; }
 inline uint32_t loadCoherent(const uint32_t* p) { return *p; }
 inline int32_t loadCoherent(const int32_t* p) { return *p; }
+inline double loadCoherentD(const double* p) { return *p; }
+template <class T>
+inline void storeGlobal(T* p, T v) { *p = v; }
+inline double uniD(double x) { return x; }
 inline uint32_t loadWg(const uint32_t* p) { return *p; }
 inline int32_t loadWg(const int32_t* p) { return *p; }
 inline uint32_t loadWg(const uint16_t* p) { return *p; }

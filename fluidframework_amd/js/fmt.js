@@ -26,6 +26,9 @@ const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER =
 // legacy relativePos1/2 (ops.ts IRelativePosition): pos1/pos2 index the relpos table (fmt_mt_relpos, 16 B)
 const FMT_MT_F_REL1 = 64, FMT_MT_F_REL2 = 128, FMT_MT_NO_MARKER = 0xffffffff, FMT_MT_REL_BEFORE = 1;
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
+// annotate-adjust (fmt.h): props_kv escape, computed value ids, fmt_mt_adjust flags
+const FMT_MT_VALUE_ADJUST = 0xffff, FMT_MT_VALUE_COMPUTED = 0x8000;
+const FMT_MT_ADJ_MIN = 1, FMT_MT_ADJ_MIN_NULL = 2, FMT_MT_ADJ_MAX = 4, FMT_MT_ADJ_MAX_NULL = 8;
 const FMT_NON_COLLAB_CLIENT = -2; // fmt.h: the insert client of a segment without merge info
 
 /** The refType of a Marker spec {marker: {refType}, props?} (IJSONMarkerSegment), or null. */
@@ -231,6 +234,8 @@ class MergeTreeStreamBuilder {
 		this.snapshotInfo = []; // per snapshot segment: [insSeq, insClient, rmFirst, rmCount] (V1 merge info)
 		this.snapshotStamps = []; // [seq, client, kind]
 		this.hasMergeInfo = false;
+		this.adjusts = []; // fmt_mt_adjust rows [delta, min, max, flags]
+		this.adjustRows = new Map();
 		this.current = null;
 	}
 	beginDoc(initialText, observer) {
@@ -344,14 +349,49 @@ class MergeTreeStreamBuilder {
 		}
 		return d;
 	}
-	propsOp(props) {
+	/** An AdjustParams {delta, min?, max?} (ops.ts:191-208) as an fmt_mt_adjust row (streams.py _adjust_row). */
+	adjustRow(params) {
+		if (!params || typeof params !== "object" || !("delta" in params)) throw new UnsupportedOp("adjust without a delta");
+		const num = (v) => {
+			if (v === null) return null;
+			if (typeof v !== "number") throw new UnsupportedOp("non-numeric adjust parameter");
+			return v;
+		};
+		const delta = num(params.delta);
+		let flags = 0, lo = 0, hi = 0;
+		if ("min" in params) {
+			flags |= FMT_MT_ADJ_MIN | (params.min === null ? FMT_MT_ADJ_MIN_NULL : 0);
+			lo = num(params.min) || 0;
+		}
+		if ("max" in params) {
+			flags |= FMT_MT_ADJ_MAX | (params.max === null ? FMT_MT_ADJ_MAX_NULL : 0);
+			hi = num(params.max) || 0;
+		}
+		const row = [delta === null ? 0 : delta, lo, hi, flags];
+		const k = row.join(",");
+		let i = this.adjustRows.get(k);
+		if (i === undefined) {
+			i = this.adjusts.length;
+			this.adjustRows.set(k, i);
+			this.adjusts.push(row);
+		}
+		return i;
+	}
+	/** Raw (key, value) changes in key order, then adjust changes as (key, FMT_MT_VALUE_ADJUST) + row
+	 * index (opToChanges, segmentPropertiesManager.ts:86-95). */
+	propsOp(props, adjust) {
 		const kv = [];
 		for (const k of jsKeyOrder(props)) {
 			const v = props[k];
 			const keyId = this.keys.intern(k);
 			const valId = v === null ? 0 : this.values.intern(JSON.stringify(v));
-			if (keyId > 0xffff || valId > 0xffff) throw new UnsupportedOp("props dictionary exceeds 65535 entries");
+			if (keyId > 0xffff || valId >= FMT_MT_VALUE_ADJUST) throw new UnsupportedOp("props dictionary exceeds 65535 entries");
 			kv.push(((keyId << 16) | valId) >>> 0);
+		}
+		for (const k of jsKeyOrder(adjust || {})) {
+			const keyId = this.keys.intern(k);
+			if (keyId > 0xffff) throw new UnsupportedOp("props dictionary exceeds 65535 entries");
+			kv.push(((keyId << 16) | FMT_MT_VALUE_ADJUST) >>> 0, this.adjustRow(adjust[k]));
 		}
 		const t = kv.join(",");
 		let i = this.propsOps.get(t);
@@ -421,11 +461,10 @@ class MergeTreeStreamBuilder {
 			} else if (type === MT_OBLITERATE_SIDED) {
 				pos1 = op.pos1.pos; pos2 = op.pos2.pos;
 				flags |= (op.pos1.before ? FMT_MT_F_START_BEFORE : 0) | (op.pos2.before ? FMT_MT_F_END_BEFORE : 0);
-			} else if (type === MT_ANNOTATE) {
-				if (op.adjust !== undefined && op.adjust !== null) throw new UnsupportedOp("annotate adjust");
+			} else if (type === MT_ANNOTATE) { // props (IMergeTreeAnnotateMsg) and/or adjust (IMergeTreeAnnotateAdjustMsg)
 				const rp = this.positions(op, true);
 				pos1 = rp[0]; pos2 = rp[1]; flags |= rp[2];
-				payload = this.propsOp(op.props || {});
+				payload = this.propsOp(op.props || {}, op.adjust);
 			} else {
 				throw new UnsupportedOp(`merge-tree op type ${type}`);
 			}
@@ -517,6 +556,9 @@ class MergeTreeStreamBuilder {
 			});
 			snapshotSegs = Uint32Array.from([].concat(...this.snapshotSegs));
 		}
+		if (this.adjusts.length && this.values.items.length > FMT_MT_VALUE_COMPUTED) {
+			throw new UnsupportedOp(`more than ${FMT_MT_VALUE_COMPUTED} distinct values in a batch with annotate adjusts`);
+		}
 		return {
 			ops: this.ops.bytes(),
 			docOpOffsets: offs,
@@ -535,7 +577,32 @@ class MergeTreeStreamBuilder {
 			snapshotInfo: this.hasMergeInfo ? Uint32Array.from([].concat(...this.snapshotInfo.map((r) => [r[0] >>> 0, r[1] >>> 0, r[2], r[3]]))) : undefined,
 			snapshotStamps: this.hasMergeInfo ? Uint32Array.from([].concat(...this.snapshotStamps.map((r) => [r[0] >>> 0, r[1] >>> 0, r[2], 0]))) : undefined,
 			markerIdKey: this.relpos.length && this.keys.ids.has(MARKER_ID_KEY) ? this.keys.ids.get(MARKER_ID_KEY) : FMT_MT_NO_MARKER,
+			adjusts: this.adjusts.length ? adjustBytes(this.adjusts) : undefined,
+			valueNum: this.adjusts.length ? Float64Array.from(this.values.items, valueNumber) : undefined,
 		};
+	}
+}
+
+/** fmt_mt_adjust rows (32 bytes: f64 delta, min, max, u32 flags, pad) as bytes. */
+function adjustBytes(rows) {
+	const b = new ArrayBuffer(32 * rows.length);
+	const v = new DataView(b);
+	rows.forEach((r, i) => {
+		v.setFloat64(32 * i, r[0], true);
+		v.setFloat64(32 * i + 8, r[1], true);
+		v.setFloat64(32 * i + 16, r[2], true);
+		v.setUint32(32 * i + 24, r[3], true);
+	});
+	return new Uint8Array(b);
+}
+
+/** The number a value's JSON text holds (typeof "number" after JSON.parse), else NaN. */
+function valueNumber(text) {
+	try {
+		const v = JSON.parse(text);
+		return typeof v === "number" ? v : NaN;
+	} catch (e) {
+		return NaN;
 	}
 }
 
@@ -659,6 +726,46 @@ class MergeTreeReplay {
 	header(doc) {
 		return readHeader(this.headerView, doc);
 	}
+	/** The document's computed annotate-adjust numbers (value ids FMT_MT_VALUE_COMPUTED + k). */
+	numbers(doc) {
+		return this.batch.adjusts ? native().fetchNumbers(this.engine.ctx, doc) : new Float64Array(0);
+	}
+	/** The value texts the document's prop sets index: the batch's, then its computed numbers. */
+	valuesOf(doc) {
+		const nums = this.numbers(doc);
+		if (nums.length === 0) return this.batch.values;
+		const vals = this.batch.values.slice();
+		nums.forEach((x, k) => { vals[FMT_MT_VALUE_COMPUTED + k] = JSON.stringify(x); });
+		return vals;
+	}
+	/**
+	 * The last seq of an annotate touching a key some annotate of the document adjusts (0: none).
+	 * Legacy summaries read getAtSeq(minSeq), exact without per-segment change history unless that
+	 * seq is above minSeq (segmentPropertiesManager.ts:213-221, 328-344; summary.py check_legacy_adjust).
+	 */
+	adjustLastSeq(doc) {
+		if (!this.batch.adjusts) return 0;
+		const ops = new DataView(this.batch.ops.buffer, this.batch.ops.byteOffset, this.batch.ops.byteLength);
+		const changes = (pid) => {
+			const out = [];
+			for (let t = this.batch.propsOff[pid]; t < this.batch.propsOff[pid + 1]; t++) {
+				const adj = (this.batch.propsKv[t] & 0xffff) === FMT_MT_VALUE_ADJUST;
+				out.push([this.batch.propsKv[t] >>> 16, adj]);
+				if (adj) t++;
+			}
+			return out;
+		};
+		const ann = [];
+		for (let i = Number(this.batch.docOpOffsets[doc]); i < Number(this.batch.docOpOffsets[doc + 1]); i++) {
+			if (ops.getUint8(i * MT_OP_BYTES + 27) !== MT_ANNOTATE) continue;
+			ann.push([ops.getInt32(i * MT_OP_BYTES, true), changes(ops.getUint32(i * MT_OP_BYTES + 20, true))]);
+		}
+		const adjusted = new Set();
+		for (const [, ch] of ann) for (const [k, adj] of ch) if (adj) adjusted.add(k);
+		let last = 0;
+		for (const [seq, ch] of ann) if (ch.some(([k]) => adjusted.has(k))) last = Math.max(last, seq);
+		return last;
+	}
 	/** Leaves (segments, tombstones included), UTF-16 chars and prop sets of one document. */
 	segments(doc) {
 		const h = this.header(doc);
@@ -670,6 +777,7 @@ class MergeTreeReplay {
 		const r = native().fetchDoc(this.engine.ctx, doc, h.nLeaves, h.nChars, h.nProps);
 		const lv = new DataView(r.leaves), pv = new DataView(r.props);
 		const chars = new Uint16Array(r.chars);
+		const nums = this.numbers(doc);
 		const props = [];
 		for (let p = 0; p < h.nProps; p++) {
 			const n = pv.getUint32(p * PROPSET_BYTES, true);
@@ -677,7 +785,10 @@ class MergeTreeReplay {
 			for (let k = 0; k < n && k < PROPS_MAX; k++) {
 				const kv = pv.getUint32(p * PROPSET_BYTES + 4 + 4 * k, true);
 				const val = kv & 0xffff;
-				if (val !== 0) obj[this.batch.keys[kv >>> 16]] = JSON.parse(this.batch.values[val]);
+				if (val !== 0) {
+					obj[this.batch.keys[kv >>> 16]] = val >= FMT_MT_VALUE_COMPUTED && this.batch.adjusts
+						? nums[val - FMT_MT_VALUE_COMPUTED] : JSON.parse(this.batch.values[val]);
+				}
 			}
 			props.push(obj);
 		}
@@ -734,7 +845,12 @@ class MergeTreeReplay {
 			kv: s.kv,
 			refType: s.refType,
 		}));
-		const out = summary.legacySummary(segs, h.minSeq, this.batch.keys, this.batch.values);
+		if (this.adjustLastSeq(doc) > h.minSeq) {
+			const e = new UnsupportedOp("legacy summary of a document with annotate-adjust history above minSeq");
+			e.code = "FMT_E_UNSUPPORTED";
+			throw e;
+		}
+		const out = summary.legacySummary(segs, h.minSeq, this.batch.keys, this.valuesOf(doc));
 		const msgs = this.batch.messages && this.batch.messages[doc];
 		if (msgs && msgs.length) {
 			const cu = summary.catchupMessages(msgs, this.catchupRanges(doc), h.minSeq);
@@ -794,7 +910,22 @@ class MergeTreeReplay {
 			kv: s.kv,
 			refType: s.refType,
 		}));
-		return summary.v1Summary(v1, h.minSeq, h.curSeq, this.batch.keys, this.batch.values, this.batch.clients[doc], rem);
+		return summary.v1Summary(v1, h.minSeq, h.curSeq, this.batch.keys, this.valuesOf(doc), this.batch.clients[doc], rem);
+	}
+	/**
+	 * Legacy summaries of every document at once on the device (fmt_mt_summarize_legacy: the
+	 * extractSync merge in one launch, JSON on host threads). Resolves to the timing; read each
+	 * document's blobs with legacyBlobs(doc). Catch-up ops are not part of this path (summarize(doc)
+	 * builds them).
+	 */
+	async summarizeAllLegacy(options) {
+		const o = options || {};
+		return native().summarizeLegacy(this.engine.ctx, this.batch.keys.map((k) => JSON.stringify(k)), this.batch.values,
+			o.chunkSize || 10000, o.threads || 0);
+	}
+	/** {header, body?} of document doc from the last summarizeAllLegacy (throws with its status). */
+	legacyBlobs(doc) {
+		return native().summaryBlobs(this.engine.ctx, doc);
 	}
 	/** MergeTreeTextHelper.getText from the local perspective (MergeTreeTextHelper.ts:28-87). */
 	getText(doc) {
@@ -847,6 +978,39 @@ class MapReplay {
 	}
 }
 
+/** Converged SharedMap state from the sparse path (key pools of any size): live entries per
+ * document in JS Map insertion order (fmt_map_entry records). */
+class SparseMapReplay {
+	constructor(batch, counts, entries) {
+		this.batch = batch;
+		this.counts = new Uint32Array(counts);
+		this.view = new DataView(entries);
+		this.first = new Float64Array(this.counts.length + 1);
+		for (let d = 0; d < this.counts.length; d++) this.first[d + 1] = this.first[d] + this.counts[d];
+	}
+	/** [[key id, value id, birth seq], ...] of document doc in birth order. */
+	rawEntries(doc) {
+		const out = [];
+		for (let i = this.first[doc]; i < this.first[doc + 1]; i++) {
+			const o = i * 12;
+			out.push([this.view.getUint32(o, true), this.view.getUint32(o + 4, true), this.view.getUint32(o + 8, true)]);
+		}
+		return out;
+	}
+	entries(doc) {
+		return this.rawEntries(doc).map(([k, v]) => [this.batch.keys[k],
+			v === MAP_VALUE_UNDEFINED ? undefined : JSON.parse(this.batch.values[v])]);
+	}
+	summarize(doc) {
+		return summary.mapSummary(this.rawEntries(doc).map(([k, v]) => [this.batch.keys[k],
+			v === MAP_VALUE_UNDEFINED ? undefined : this.batch.values[v]]));
+	}
+	get(doc, key) {
+		const e = this.rawEntries(doc).find(([k]) => this.batch.keys[k] === key);
+		return e === undefined || e[1] === MAP_VALUE_UNDEFINED ? undefined : JSON.parse(this.batch.values[e[1]]);
+	}
+}
+
 /** One engine context on one GPU (fmt_open). */
 class Engine {
 	constructor(device) {
@@ -866,6 +1030,11 @@ class Engine {
 		const slots = await native().replayMap(this.ctx, batch);
 		return new MapReplay(batch, slots);
 	}
+	/** The sparse LWW path (fmt_map_*_sparse): any key pool size, live entries only. */
+	async replayMapSparse(batch) {
+		const r = await native().replayMapSparse(this.ctx, batch);
+		return new SparseMapReplay(batch, r.counts, r.entries);
+	}
 	close() {
 		native().close(this.ctx);
 	}
@@ -878,6 +1047,7 @@ module.exports = {
 	MapStreamBuilder,
 	MergeTreeReplay,
 	MapReplay,
+	SparseMapReplay,
 	UnsupportedOp,
 	summary,
 	constants: { MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MAP_SET, MAP_DELETE, MAP_CLEAR,

@@ -19,7 +19,11 @@
 //   fetchDoc(ctx, doc, nLeaves, nChars, nProps) -> {leaves, chars, props}   fmt_mt_fetch_doc
 //   fetchCatchup(ctx, doc, n) -> ArrayBuffer                         fmt_mt_fetch_catchup
 //   fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer                     fmt_mt_fetch_remove_order
+//   fetchNumbers(ctx, doc) -> Float64Array                           fmt_mt_fetch_numbers
 //   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
+//   replayMapSparse(ctx, batch) -> Promise<{counts, entries}>        fmt_map_load_sparse + run + fetch
+//   summarizeLegacy(ctx, quotedKeys, values, chunk, threads) -> Promise<timing>   fmt_mt_summarize_legacy
+//   summaryBlobs(ctx, doc) -> {header, body?}                        fmt_mt_summary_blobs
 //   stats(ctx) -> {kernelMs, totalMs, ops, docs, bytesRead, bytesWritten, launches}
 //   sizes: {mtOp, mapOp, leaf, docResult, propset, mapSlot}          struct sizes for the JS views
 #include <node_api.h>
@@ -247,13 +251,18 @@ struct Job {
   Ctx* c = nullptr;
   napi_ref ctx_ref = nullptr;
   std::vector<napi_ref> keep;  // input arrays stay alive (and unmoved) until Complete
-  bool is_map = false;
+  enum Kind { kMergeTree, kMap, kMapSparse, kSummarize } kind = kMergeTree;
   fmt_mt_batch mt;
   const fmt_map_op* map_ops = nullptr;
   uint64_t map_n_ops = 0;
   const uint64_t* map_offs = nullptr;
   uint32_t n_docs = 0, key_bound = 0;
-  std::vector<uint8_t> out;  // headers or map slots
+  std::vector<uint8_t> out;  // headers, map slots, sparse counts
+  std::vector<uint8_t> out2; // sparse entries
+  // summarizeLegacy: JSON-quoted keys and value texts (copied on the JS thread), chunk, threads
+  std::vector<std::string> keys, values;
+  uint32_t chunk = 0, threads = 0;
+  fmt_summary_timing timing{};
   int rc = FMT_OK;
   std::string err;
 };
@@ -261,13 +270,31 @@ struct Job {
 void Execute(napi_env, void* p) {  // libuv worker thread: no N-API calls here
   auto* j = static_cast<Job*>(p);
   fmt_ctx* ctx = j->c->ctx;
-  if (j->is_map) {
+  if (j->kind == Job::kMap) {
     j->rc = fmt_map_load(ctx, j->map_ops, j->map_n_ops, j->map_offs, j->n_docs, j->key_bound);
     if (j->rc == FMT_OK) j->rc = fmt_map_run(ctx);
     if (j->rc == FMT_OK) {
       j->out.resize(size_t(j->n_docs) * j->key_bound * sizeof(fmt_map_slot));
       j->rc = fmt_map_fetch(ctx, reinterpret_cast<fmt_map_slot*>(j->out.data()));
     }
+  } else if (j->kind == Job::kMapSparse) {
+    j->rc = fmt_map_load_sparse(ctx, j->map_ops, j->map_n_ops, j->map_offs, j->n_docs, j->key_bound);
+    if (j->rc == FMT_OK) j->rc = fmt_map_run_sparse(ctx);
+    uint64_t n = 0;
+    j->out.resize(size_t(j->n_docs) * sizeof(uint32_t));
+    if (j->rc == FMT_OK)  // sizes first (counts + total), then the packed entries
+      j->rc = fmt_map_fetch_sparse(ctx, reinterpret_cast<uint32_t*>(j->out.data()), nullptr, 0, &n);
+    if (j->rc == FMT_OK) {
+      j->out2.resize(size_t(n) * sizeof(fmt_map_entry));
+      j->rc = fmt_map_fetch_sparse(ctx, reinterpret_cast<uint32_t*>(j->out.data()),
+                                   reinterpret_cast<fmt_map_entry*>(j->out2.data()), n, &n);
+    }
+  } else if (j->kind == Job::kSummarize) {
+    std::vector<const char*> k, v;
+    for (const auto& x : j->keys) k.push_back(x.c_str());
+    for (const auto& x : j->values) v.push_back(x.c_str());
+    j->rc = fmt_mt_summarize_legacy(ctx, k.data(), uint32_t(k.size()), v.data(), uint32_t(v.size()), j->chunk,
+                                    j->threads, &j->timing);
   } else {
     j->rc = fmt_mt_load(ctx, &j->mt);
     if (j->rc == FMT_OK) j->rc = fmt_mt_run(ctx);
@@ -282,14 +309,36 @@ void Execute(napi_env, void* p) {  // libuv worker thread: no N-API calls here
 void Complete(napi_env env, napi_status, void* p) {  // JS thread
   auto* j = static_cast<Job*>(p);
   j->c->busy = false;
-  if (j->rc != FMT_OK) {
-    napi_reject_deferred(env, j->deferred, make_error(env, j->rc, j->err));
-  } else {
+  auto buffer = [&](const std::vector<uint8_t>& bytes) {
     void* data = nullptr;
     napi_value ab;
-    napi_create_arraybuffer(env, j->out.size(), &data, &ab);
-    if (!j->out.empty()) std::memcpy(data, j->out.data(), j->out.size());
-    napi_resolve_deferred(env, j->deferred, ab);
+    napi_create_arraybuffer(env, bytes.size(), &data, &ab);
+    if (!bytes.empty()) std::memcpy(data, bytes.data(), bytes.size());
+    return ab;
+  };
+  if (j->rc != FMT_OK) {
+    napi_reject_deferred(env, j->deferred, make_error(env, j->rc, j->err));
+  } else if (j->kind == Job::kMapSparse) {
+    napi_value o;
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "counts", buffer(j->out));
+    napi_set_named_property(env, o, "entries", buffer(j->out2));
+    napi_resolve_deferred(env, j->deferred, o);
+  } else if (j->kind == Job::kSummarize) {
+    napi_value o, v;
+    napi_create_object(env, &o);
+    auto num = [&](const char* k, double x) {
+      napi_create_double(env, x, &v);
+      napi_set_named_property(env, o, k, v);
+    };
+    num("kernelMs", j->timing.kernel_ms);
+    num("fetchMs", j->timing.fetch_ms);
+    num("formatMs", j->timing.format_ms);
+    num("bytes", double(j->timing.bytes));
+    num("threads", double(j->timing.threads));
+    napi_resolve_deferred(env, j->deferred, o);
+  } else {
+    napi_resolve_deferred(env, j->deferred, buffer(j->out));
   }
   for (napi_ref r : j->keep) napi_delete_reference(env, r);
   napi_delete_reference(env, j->ctx_ref);
@@ -398,6 +447,27 @@ napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
       if (st != nullptr) keep_array(env, j, prop(env, b, "snapshotStamps"));
     }
   }
+  // optional annotate-adjust: adjusts (fmt_mt_adjust rows) + valueNum (one double per value id)
+  void *adj, *vn;
+  size_t nadj, nvn;
+  if (!get_bytes(env, prop(env, b, "adjusts"), "adjusts", &adj, &nadj) ||
+      !get_bytes(env, prop(env, b, "valueNum"), "valueNum", &vn, &nvn)) {
+    delete j;
+    return nullptr;
+  }
+  if (adj != nullptr) {
+    if (nadj % sizeof(fmt_mt_adjust) || vn == nullptr || nvn % sizeof(double)) {
+      delete j;
+      throw_fmt(env, FMT_E_USAGE, "replayMergeTree: adjusts must hold fmt_mt_adjust rows, valueNum one double per value");
+      return nullptr;
+    }
+    j->mt.adjusts = static_cast<const fmt_mt_adjust*>(adj);
+    j->mt.n_adjusts = uint32_t(nadj / sizeof(fmt_mt_adjust));
+    j->mt.value_num = static_cast<const double*>(vn);
+    j->mt.n_values = uint32_t(nvn / sizeof(double));
+    keep_array(env, j, prop(env, b, "adjusts"));
+    keep_array(env, j, prop(env, b, "valueNum"));
+  }
   // optional legacy relative positions: relpos (fmt_mt_relpos rows) + markerIdKey
   void* rp;
   size_t nrp;
@@ -448,7 +518,7 @@ napi_value ReplayMap(napi_env env, napi_callback_info info) {
   }
   auto* j = new Job;
   j->c = c;
-  j->is_map = true;
+  j->kind = Job::kMap;
   j->map_ops = static_cast<const fmt_map_op*>(ops);
   j->map_n_ops = n_ops_b / sizeof(fmt_map_op);
   j->map_offs = static_cast<const uint64_t*>(offs);
@@ -457,6 +527,114 @@ napi_value ReplayMap(napi_env env, napi_callback_info info) {
   keep_array(env, j, prop(env, b, "ops"));
   keep_array(env, j, prop(env, b, "docOpOffsets"));
   return queue(env, j, argv[0], "fmtReplayMap");
+}
+
+// replayMapSparse(ctx, {ops, docOpOffsets, keyBound}) -> Promise<{counts, entries}>: the sparse LWW path
+// (key pools of any size): counts = n_docs u32 live-entry counts, entries = fmt_map_entry records of
+// all documents packed in document order, each document's in JS Map insertion order.
+napi_value ReplayMapSparse(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 2 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "replayMapSparse: a replay is already running on this context");
+    return nullptr;
+  }
+  napi_value b = argv[1];
+  void *ops, *offs;
+  size_t n_ops_b, n_offs_b;
+  uint32_t key_bound;
+  if (!get_bytes(env, prop(env, b, "ops"), "ops", &ops, &n_ops_b)) return nullptr;
+  if (!get_bytes(env, prop(env, b, "docOpOffsets"), "docOpOffsets", &offs, &n_offs_b)) return nullptr;
+  if (!get_u32(env, prop(env, b, "keyBound"), "keyBound", &key_bound)) return nullptr;
+  if (n_ops_b % sizeof(fmt_map_op) || n_offs_b < 8 || n_offs_b % 8 || key_bound == 0) {
+    throw_fmt(env, FMT_E_USAGE, "replayMapSparse: buffer sizes do not match the fmt_map_* record layouts");
+    return nullptr;
+  }
+  auto* j = new Job;
+  j->c = c;
+  j->kind = Job::kMapSparse;
+  j->map_ops = static_cast<const fmt_map_op*>(ops);
+  j->map_n_ops = n_ops_b / sizeof(fmt_map_op);
+  j->map_offs = static_cast<const uint64_t*>(offs);
+  j->n_docs = uint32_t(n_offs_b / 8 - 1);
+  j->key_bound = key_bound;
+  keep_array(env, j, prop(env, b, "ops"));
+  keep_array(env, j, prop(env, b, "docOpOffsets"));
+  return queue(env, j, argv[0], "fmtReplayMapSparse");
+}
+
+bool get_strings(napi_env env, napi_value arr, const char* what, std::vector<std::string>* out) {
+  bool is = false;
+  uint32_t n = 0;
+  if (napi_is_array(env, arr, &is) != napi_ok || !is || napi_get_array_length(env, arr, &n) != napi_ok)
+    return throw_fmt(env, FMT_E_USAGE, std::string(what) + ": expected an array of strings");
+  out->resize(n);
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value v;
+    size_t len = 0;
+    napi_get_element(env, arr, i, &v);
+    if (napi_get_value_string_utf8(env, v, nullptr, 0, &len) != napi_ok)
+      return throw_fmt(env, FMT_E_USAGE, std::string(what) + ": expected an array of strings");
+    (*out)[i].resize(len + 1);
+    napi_get_value_string_utf8(env, v, &(*out)[i][0], len + 1, &len);
+    (*out)[i].resize(len);
+  }
+  return true;
+}
+
+// summarizeLegacy(ctx, quotedKeys, values, chunk, threads) -> Promise<timing>: legacy summaries of every
+// document of the last merge-tree replay (fmt_mt_summarize_legacy: device merge, host JSON threads);
+// read them with summaryBlobs.
+napi_value SummarizeLegacy(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 5 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "summarizeLegacy: a replay is running on this context");
+    return nullptr;
+  }
+  auto* j = new Job;
+  j->c = c;
+  j->kind = Job::kSummarize;
+  if (!get_strings(env, argv[1], "keys", &j->keys) || !get_strings(env, argv[2], "values", &j->values) ||
+      !get_u32(env, argv[3], "chunk", &j->chunk) || !get_u32(env, argv[4], "threads", &j->threads)) {
+    delete j;
+    return nullptr;
+  }
+  return queue(env, j, argv[0], "fmtSummarizeLegacy");
+}
+
+// summaryBlobs(ctx, doc) -> {header, body?}: document doc's blobs of the last summarizeLegacy
+// (throws with the document's replay status, or FMT_E_UNSUPPORTED, when it has none).
+napi_value SummaryBlobs(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 2 || !get_ctx(env, argv[0], &c)) return nullptr;
+  uint32_t doc;
+  if (!get_u32(env, argv[1], "doc", &doc)) return nullptr;
+  const char *h = nullptr, *b = nullptr;
+  size_t hl = 0, bl = 0;
+  int rc = fmt_mt_summary_blobs(c->ctx, doc, &h, &hl, &b, &bl);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  napi_value o, v;
+  napi_create_object(env, &o);
+  CHECK_NAPI(env, napi_create_string_utf8(env, h, hl, &v));
+  napi_set_named_property(env, o, "header", v);
+  if (bl) {
+    CHECK_NAPI(env, napi_create_string_utf8(env, b, bl, &v));
+    napi_set_named_property(env, o, "body", v);
+  }
+  return o;
 }
 
 // fetchDoc(ctx, doc, nLeaves, nChars, nProps) -> {leaves: ArrayBuffer, chars: ArrayBuffer, props: ArrayBuffer}
@@ -540,6 +718,33 @@ napi_value FetchRemoveOrder(napi_env env, napi_callback_info info) {
   return ab;
 }
 
+// fetchNumbers(ctx, doc) -> Float64Array of the document's computed annotate-adjust numbers
+// (value ids FMT_MT_VALUE_COMPUTED + index)
+napi_value FetchNumbers(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 2 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchNumbers: a replay is running on this context");
+    return nullptr;
+  }
+  uint32_t doc, n = 0;
+  if (!get_u32(env, argv[1], "doc", &doc)) return nullptr;
+  int rc = fmt_mt_fetch_numbers(c->ctx, doc, nullptr, 0, &n);
+  void* p;
+  napi_value ab, arr;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(n) * sizeof(double), &p, &ab));
+  if (rc == FMT_OK && n) rc = fmt_mt_fetch_numbers(c->ctx, doc, static_cast<double*>(p), n, &n);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  CHECK_NAPI(env, napi_create_typedarray(env, napi_float64_array, n, ab, 0, &arr));
+  return arr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor fns[] = {
       {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
@@ -552,6 +757,10 @@ napi_value Init(napi_env env, napi_value exports) {
       {"fetchDoc", nullptr, FetchDoc, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchCatchup", nullptr, FetchCatchup, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchRemoveOrder", nullptr, FetchRemoveOrder, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchNumbers", nullptr, FetchNumbers, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"replayMapSparse", nullptr, ReplayMapSparse, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"summarizeLegacy", nullptr, SummarizeLegacy, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"summaryBlobs", nullptr, SummaryBlobs, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
   };
   napi_define_properties(env, exports, sizeof fns / sizeof fns[0], fns);
   napi_value sizes, v;
@@ -567,6 +776,8 @@ napi_value Init(napi_env env, napi_value exports) {
   sz("propset", sizeof(fmt_mt_propset));
   sz("mapSlot", sizeof(fmt_map_slot));
   sz("catchupRange", sizeof(fmt_mt_catchup_range));
+  sz("mapEntry", sizeof(fmt_map_entry));
+  sz("adjust", sizeof(fmt_mt_adjust));
   napi_set_named_property(env, exports, "sizes", sizes);
   return exports;
 }

@@ -89,7 +89,16 @@ class FmtMtBatch(ctypes.Structure):
         ("snapshot_info", ctypes.c_void_p),
         ("snapshot_stamps", ctypes.c_void_p),
         ("n_snapshot_stamps", ctypes.c_uint64),
+        ("adjusts", ctypes.c_void_p),
+        ("n_adjusts", ctypes.c_uint32),
+        ("n_values", ctypes.c_uint32),
+        ("value_num", ctypes.c_void_p),
     ]
+
+
+from .streams import ADJUST_DTYPE  # noqa: E402  (include/fmt.h fmt_mt_adjust, 32 bytes)
+
+assert ADJUST_DTYPE.itemsize == 32
 
 
 class FmtStats(ctypes.Structure):
@@ -153,6 +162,12 @@ def batch_struct(batch):
         b.snapshot_info, b.snapshot_stamps = _ptr(inf), _ptr(stp)
         b.n_snapshot_stamps = 0 if st is None else len(st)
         keep += [inf, stp]
+    adj = getattr(batch, "adjusts", None)
+    if adj is not None and len(adj):
+        a = np.ascontiguousarray(adj, dtype=ADJUST_DTYPE)
+        vn = np.ascontiguousarray(batch.value_num, dtype=np.float64)
+        b.adjusts, b.n_adjusts, b.value_num, b.n_values = _ptr(a), len(a), _ptr(vn), len(vn)
+        keep += [a, vn]
     return b, keep
 
 
@@ -206,6 +221,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_doc.argtypes = [P, U32, P, U32, P, U32, P, U32]
         L.fmt_mt_fetch_catchup.argtypes = [P, U32, P, U32]
         L.fmt_mt_fetch_remove_order.argtypes = [P, U32, P, U32]
+        L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         _libs[path] = L
     return _libs[path]
@@ -217,7 +233,7 @@ EXPORTED_SYMBOLS = [
     "fmt_map_load_sparse", "fmt_map_run_sparse", "fmt_map_fetch_sparse",
     "fmt_mt_summarize_legacy", "fmt_mt_summary_blobs",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
-    "fmt_mt_fetch_remove_order", "fmt_mt_capacity",
+    "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
 ]
 
 
@@ -383,6 +399,15 @@ class Engine:
         out = np.zeros(max(n, 1), dtype=RM_ORDER_DTYPE)
         self._check(self.L.fmt_mt_fetch_remove_order(self.h, doc, _ptr(out), n))
         return out[:n]
+
+    def mt_numbers(self, doc: int) -> np.ndarray:
+        """The document's computed annotate-adjust numbers (value ids FMT_MT_VALUE_COMPUTED + index)."""
+        n = ctypes.c_uint32(0)
+        self._check(self.L.fmt_mt_fetch_numbers(self.h, doc, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=np.float64)
+        if n.value:
+            self._check(self.L.fmt_mt_fetch_numbers(self.h, doc, _ptr(out), n.value, ctypes.byref(n)))
+        return out[: n.value]
 
     def mt_catchup(self, doc: int, hdr=None) -> np.ndarray:
         """The document's catch-up ranges (fmt_mt_catchup_range) of its FMT_MT_F_CATCHUP ops."""

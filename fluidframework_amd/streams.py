@@ -66,6 +66,23 @@ NO_MARKER = 0xFFFFFFFF  # fmt.h FMT_MT_NO_MARKER
 REL_BEFORE = 1  # fmt.h FMT_MT_REL_BEFORE
 MARKER_ID_KEY = "markerId"  # reservedMarkerIdKey (merge-tree/src/ops.ts)
 MT_SEG_MARKER = 0x80000000  # fmt.h FMT_MT_SEG_MARKER (snapshot segment len flag)
+# annotate-adjust (fmt.h): props_kv escape, computed value ids, fmt_mt_adjust rows and their flags
+VALUE_ADJUST, VALUE_COMPUTED = 0xFFFF, 0x8000
+ADJ_MIN, ADJ_MIN_NULL, ADJ_MAX, ADJ_MAX_NULL = 1, 2, 4, 8
+ADJUST_DTYPE = np.dtype([("delta", "<f8"), ("min", "<f8"), ("max", "<f8"), ("flags", "<u4"), ("pad", "<u4")])
+
+
+def value_numbers(values) -> np.ndarray:
+    """Per value JSON text: its number (JSON.parse gives typeof "number"), else NaN."""
+    out = np.full(len(values), np.nan)
+    for i, t in enumerate(values):
+        try:
+            v = json.loads(t)
+        except ValueError:
+            continue
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            out[i] = float(v)
+    return out
 MT_LEAF_MARKER = 0x8000  # fmt.h FMT_MT_LEAF_MARKER (fmt_mt_leaf.pad flag)
 
 
@@ -215,6 +232,9 @@ class MergeTreeBatch:
     # optional (SnapshotV1 merge info): per snapshot segment SNAPSHOT_INFO_DTYPE, and the stamps
     snapshot_info: np.ndarray | None = None
     snapshot_stamps: np.ndarray | None = None
+    # optional (annotate-adjust): ADJUST_DTYPE rows and, per value id, the number its text holds (NaN)
+    adjusts: np.ndarray | None = None
+    value_num: np.ndarray | None = None
 
     @property
     def n_docs(self) -> int:
@@ -318,6 +338,8 @@ class MergeTreeStreamBuilder:
         self.snapshot_info: list[tuple] = []  # per snapshot segment: (ins_seq, ins_client, rm_first, rm_count)
         self.snapshot_stamps: list[tuple] = []  # (seq, client, kind, 0)
         self.has_merge_info = False
+        self.adjusts: list[tuple] = []  # fmt_mt_adjust rows (delta, min, max, flags, 0)
+        self.adjust_rows: dict = {}
 
     def _relpos(self, rp: dict) -> int:
         """An IRelativePosition {id?, before?, offset?}: its row in the relpos table. The id is looked
@@ -357,15 +379,52 @@ class MergeTreeStreamBuilder:
         self.text_len += 1
         return off
 
-    def _props_op(self, props: dict) -> int:
+    def _adjust_row(self, params) -> int:
+        """An AdjustParams {delta, min?, max?} (ops.ts:191-208) as an fmt_mt_adjust row. JSON null
+        delta adds 0 (number + null); a null min / max is present (!== undefined) and compares as 0."""
+        if not isinstance(params, dict) or "delta" not in params:
+            raise UnsupportedOp("adjust without a delta")
+
+        def num(v):
+            if v is None:
+                return None
+            if isinstance(v, bool) or not isinstance(v, (int, float)):
+                raise UnsupportedOp("non-numeric adjust parameter")
+            return float(v)
+
+        delta = num(params["delta"])
+        flags, lo, hi = 0, 0.0, 0.0
+        if "min" in params:
+            flags |= ADJ_MIN | (ADJ_MIN_NULL if params["min"] is None else 0)
+            lo = num(params["min"]) or 0.0
+        if "max" in params:
+            flags |= ADJ_MAX | (ADJ_MAX_NULL if params["max"] is None else 0)
+            hi = num(params["max"]) or 0.0
+        row = (0.0 if delta is None else delta, lo, hi, flags, 0)
+        i = self.adjust_rows.get(row)
+        if i is None:
+            i = len(self.adjusts)
+            self.adjust_rows[row] = i
+            self.adjusts.append(row)
+        return i
+
+    def _props_op(self, props: dict, adjust: dict | None = None) -> int:
+        """A props op: the raw (key, value) changes in JS key order, then the adjust changes
+        (segmentPropertiesManager.ts:86-95 opToChanges), each adjust as (key, FMT_MT_VALUE_ADJUST)
+        followed by its row index."""
         kv = []
         for k in js_key_order(list(props)):
             v = props[k]
             key_id = self.keys.intern(k)
             val_id = 0 if v is None else self.values.intern(js_json(v))
-            if key_id > 0xFFFF or val_id > 0xFFFF:
+            if key_id > 0xFFFF or val_id >= VALUE_ADJUST:
                 raise UnsupportedOp("props dictionary exceeds 65535 entries")
             kv.append((key_id << 16) | val_id)
+        for k in js_key_order(list(adjust or {})):
+            key_id = self.keys.intern(k)
+            if key_id > 0xFFFF:
+                raise UnsupportedOp("props dictionary exceeds 65535 entries")
+            kv += [(key_id << 16) | VALUE_ADJUST, self._adjust_row(adjust[k])]
         t = tuple(kv)
         i = self.props_ops.get(t)
         if i is None:
@@ -408,11 +467,9 @@ class MergeTreeStreamBuilder:
             p1, p2 = op["pos1"], op["pos2"]
             flags = (MT_F_START_BEFORE if p1["before"] else 0) | (MT_F_END_BEFORE if p2["before"] else 0)
             return (seq, ref, msn, int(p1["pos"]), int(p2["pos"]), 0, 0, client, MT_OBLITERATE_SIDED, flags)
-        if t == MT_ANNOTATE:
-            if op.get("adjust") is not None:
-                raise UnsupportedOp("annotate adjust")
+        if t == MT_ANNOTATE:  # IMergeTreeAnnotateMsg props and/or IMergeTreeAnnotateAdjustMsg adjust
             p1, p2, rel = self._positions(op)
-            pid = self._props_op(op.get("props") or {})
+            pid = self._props_op(op.get("props") or {}, op.get("adjust"))
             return (seq, ref, msn, p1, p2, pid, 0, client, MT_ANNOTATE, rel)
         raise UnsupportedOp(f"merge-tree op type {t}")
 
@@ -539,6 +596,8 @@ class MergeTreeStreamBuilder:
         if remove_order:
             flag_remove_order(ops, offs)
         text = np.concatenate(self.text) if self.text else np.zeros(0, dtype="<u2")
+        if self.adjusts and len(self.values.items) > VALUE_COMPUTED:
+            raise UnsupportedOp(f"more than {VALUE_COMPUTED} distinct values in a batch with annotate adjusts")
         props_off = np.zeros(len(self.props_list) + 1, dtype=np.uint32)
         kv = []
         for j, t in enumerate(self.props_list):
@@ -561,6 +620,8 @@ class MergeTreeStreamBuilder:
             snapshot_info=np.array(self.snapshot_info, dtype=SNAPSHOT_INFO_DTYPE) if self.has_merge_info else None,
             snapshot_stamps=np.array(self.snapshot_stamps, dtype=STAMP_DTYPE) if self.has_merge_info else None,
             marker_id_key=self.keys.ids.get(MARKER_ID_KEY, NO_MARKER) if self.relpos else NO_MARKER,
+            adjusts=np.array(self.adjusts, dtype=ADJUST_DTYPE) if self.adjusts else None,
+            value_num=value_numbers(self.values.items) if self.adjusts else None,
         )
 
 

@@ -14,9 +14,9 @@ from __future__ import annotations
 
 import json
 
-from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_GROUP, MT_INSERT, MT_LEAF_MARKER, MT_OBLITERATE,
-                      MT_OBLITERATE_SIDED, MT_REMOVE,
-                      is_array_index_key, js_json, js_key_order, js_quote, marker_ref_type)
+from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_ANNOTATE, MT_GROUP, MT_INSERT, MT_LEAF_MARKER,
+                      MT_OBLITERATE, MT_OBLITERATE_SIDED, MT_REMOVE, VALUE_ADJUST, VALUE_COMPUTED, UnsupportedOp,
+                      is_array_index_key, js_json, js_key_order, js_number, js_quote, marker_ref_type)
 
 NOT_REMOVED = 0x7FFFFFFF
 TEXT_GRANULARITY = 256          # textSegment.ts:21
@@ -71,6 +71,47 @@ def map_summary(slots, keys, values):
 
 
 # ------------------------------------------------------------------------------------- merge-tree
+def values_with_numbers(values, numbers):
+    """The value texts a document's prop sets index: the host dictionary, then the document's
+    computed annotate-adjust numbers at FMT_MT_VALUE_COMPUTED + k, written as JSON.stringify writes
+    them (ECMAScript Number::toString)."""
+    if numbers is None or len(numbers) == 0:
+        return values
+    return list(values) + [""] * (VALUE_COMPUTED - len(values)) + [js_number(float(x)) for x in numbers]
+
+
+def adjust_last_seq(batch, doc: int) -> int:
+    """The last seq of an annotate that touches a key some annotate of the document adjusts (0: the
+    document has no adjusts). Mirrors fmt_mt_load's per-document value."""
+    if getattr(batch, "adjusts", None) is None:
+        return 0
+    a, b = int(batch.doc_op_offsets[doc]), int(batch.doc_op_offsets[doc + 1])
+    ops = batch.ops[a:b]
+
+    def changes(pid):
+        kv = batch.props_kv[int(batch.props_off[pid]): int(batch.props_off[pid + 1])]
+        out, i = [], 0
+        while i < len(kv):
+            adj = (int(kv[i]) & 0xFFFF) == VALUE_ADJUST
+            out.append((int(kv[i]) >> 16, adj))
+            i += 2 if adj else 1
+        return out
+
+    ann = [(int(op["seq"]), changes(int(op["payload"]))) for op in ops if int(op["type"]) == MT_ANNOTATE]
+    adjusted = {k for _, ch in ann for k, adj in ch if adj}
+    return max([seq for seq, ch in ann if any(k in adjusted for k, _ in ch)], default=0)
+
+
+def check_legacy_adjust(batch, doc: int, min_seq: int) -> None:
+    """The legacy summary reads getAtSeq(minSeq) (snapshotlegacy.ts:211-212), which folds only the
+    pending remote changes of each segment at or below minSeq (segmentPropertiesManager.ts:328-344);
+    a raw change folds into the consensus early only while the segment's remote list is empty
+    (:213-221), which depends on per-segment msn updates. The state is exact without that history
+    unless an adjusted key is annotated above minSeq: such a document's legacy summary is refused."""
+    if adjust_last_seq(batch, doc) > min_seq:
+        raise UnsupportedOp("legacy summary of a document with annotate-adjust history above minSeq")
+
+
 def _props_obj(kv, keys, values):
     pairs = [(keys[x >> 16], values[x & 0xFFFF]) for x in kv]
     names = [k for k, _ in pairs]

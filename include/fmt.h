@@ -193,6 +193,30 @@ typedef struct fmt_mt_stamp {
   uint32_t pad;
 } fmt_mt_stamp;
 
+/* Annotate-adjust (IMergeTreeAnnotateAdjustMsg.adjust, merge-tree/src/ops.ts:187-222): in props_kv an
+ * entry (key_id << 16) | FMT_MT_VALUE_ADJUST is followed by one word, the index of its fmt_mt_adjust
+ * row. The change folds into the key's current value as computePropertyValue does
+ * (segmentPropertiesManager.ts:54-78), in IEEE double: (current is a number ? current : 0) + delta,
+ * then max (if present) clamps, else min. A computed number gets a value id: the host dictionary's id
+ * of an equal number when there is one (matchProperties compares with ===, properties.ts:32-61),
+ * else FMT_MT_VALUE_COMPUTED + its index in the document's number table (fmt_mt_fetch_numbers),
+ * first-computed order, one entry per distinct number. Batches with adjusts therefore keep host
+ * value ids below FMT_MT_VALUE_COMPUTED. A null min / max (JSON null, !== undefined) compares as 0
+ * and yields null: the key is deleted (segmentPropertiesManager.ts:112-115). 32 bytes. */
+#define FMT_MT_VALUE_ADJUST 0xffffu
+#define FMT_MT_VALUE_COMPUTED 0x8000u
+#define FMT_MT_ADJ_MIN 1u      /* min present */
+#define FMT_MT_ADJ_MIN_NULL 2u /* min present and null */
+#define FMT_MT_ADJ_MAX 4u
+#define FMT_MT_ADJ_MAX_NULL 8u
+typedef struct fmt_mt_adjust {
+  double delta; /* AdjustParams.delta (a JSON null delta adds 0) */
+  double min;
+  double max;
+  uint32_t flags; /* FMT_MT_ADJ_* */
+  uint32_t pad;
+} fmt_mt_adjust;
+
 /* A batch of merge-tree documents. Pointers are HOST pointers for fmt_mt_load(). */
 typedef struct fmt_mt_batch {
   const fmt_mt_op* ops;           /* all ops, documents contiguous and in seq order */
@@ -215,6 +239,11 @@ typedef struct fmt_mt_batch {
   const fmt_mt_snapshot_info* snapshot_info; /* optional: n_snapshot_segs entries (V1 merge info), or NULL */
   const fmt_mt_stamp* snapshot_stamps;
   uint64_t n_snapshot_stamps;
+  const fmt_mt_adjust* adjusts;   /* optional: the rows FMT_MT_VALUE_ADJUST entries index, or NULL */
+  uint32_t n_adjusts;
+  uint32_t n_values;              /* entries of value_num */
+  const double* value_num;        /* with adjusts: per value id, the number its JSON text parses to, NaN
+                                     for a non-number (typeof !== "number") */
 } fmt_mt_batch;
 
 /* ---------------------------------------------------------------------------------------------
@@ -336,7 +365,12 @@ int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
  * SharedString.summarizeCore → SnapshotLegacy.extractSync + emit, snapshotlegacy.ts:74-262 and
  * snapshotChunks.ts:85-204, for all documents at once; catch-up ops are not included): the segment
  * merge runs on the device (one wave per document), the JSON on `threads` host threads (0 = up to
- * 16). keys: the batch's key strings JSON-quoted; values: the value JSON texts (UTF-8). */
+ * 16). keys: the batch's key strings JSON-quoted; values: the value JSON texts (UTF-8). Computed
+ * annotate-adjust numbers are written as JSON.stringify writes them. A document whose legacy summary
+ * depends on per-segment pending adjust history gets FMT_E_UNSUPPORTED: one with an adjust on a key
+ * and an annotate of that key above its final minSeq (getAtSeq(minSeq) then folds only part of the
+ * segment's remote changes, segmentPropertiesManager.ts:213-221, 328-344; SnapshotV1 and the replay
+ * state stay exact). */
 typedef struct fmt_summary_timing {
   double kernel_ms;   /* device merge (events) */
   double fetch_ms;    /* device -> host of runs, text and prop sets */
@@ -430,6 +464,9 @@ int fmt_mt_fetch_catchup(fmt_ctx* ctx, uint32_t doc, fmt_mt_catchup_range* out, 
 /* One document's remove-order entries (header n_rm_order entries, at most cap), in recording order:
  * with the first remover they give SnapshotV1's removedClientIds (snapshotV1.ts:235-250). */
 int fmt_mt_fetch_remove_order(fmt_ctx* ctx, uint32_t doc, fmt_mt_remove_order* out, uint32_t cap);
+/* One document's computed numbers (annotate-adjust results, FMT_MT_VALUE_COMPUTED + index): *n_out
+ * = their count, the first min(count, cap) copied to out. */
+int fmt_mt_fetch_numbers(fmt_ctx* ctx, uint32_t doc, double* out, uint32_t cap, uint32_t* n_out);
 /* Per-document capacities of this engine build (leaves, chars, prop sets): the large tier's, which
  * is where a document that outgrows the small tier ends up. */
 int fmt_mt_capacity(uint32_t* max_leaves, uint32_t* max_chars, uint32_t* max_props);

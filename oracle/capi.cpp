@@ -2,7 +2,10 @@
 //
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
 // Result layouts are the product's (include/fmt.h) so tests compare GPU and oracle field by field.
+#include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <mutex>
 #include <chrono>
 #include <cstring>
 #include <exception>
@@ -183,6 +186,7 @@ int orc_mt_dump(void* h, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint32_t c
 }
 
 // Legacy summary blobs (header, then body); returns the byte count needed for header+body.
+// (orc_mt_replay_summary: the same for document d of a batch after its replay)
 int orc_mt_summary(void* h, const char* const* keys, int nKeys, const char* const* values,
                    int nValues, int chunkSize, char* out, int cap, int* headerLen, int* bodyLen) {
   std::vector<std::string> k(keys, keys + nKeys), v(values, values + nValues);
@@ -196,12 +200,32 @@ int orc_mt_summary(void* h, const char* const* keys, int nKeys, const char* cons
 
 std::atomic<int> g_indexed{0};  // orc_set_index: replays use the remote-length index (BlockIdx)
 
+// The host's numbers of a batch (value ids whose JSON text is a number), sorted, the first id of
+// each number (annotate-adjust results equal to one of them take its id).
+std::vector<std::pair<double, uint32_t>> hostNumbers(const fmt_mt_batch* b) {
+  std::vector<std::pair<double, uint32_t>> v, uniq;
+  for (uint32_t i = 0; b->adjusts && b->value_num && i < b->n_values; i++)
+    if (!std::isnan(b->value_num[i])) v.emplace_back(b->value_num[i] == 0 ? 0.0 : b->value_num[i], i);
+  std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  for (const auto& e : v)
+    if (uniq.empty() || uniq.back().first != e.first) uniq.push_back(e);
+  return uniq;
+}
+
 // The document's initial state: a loaded summary (f3) or its initial text, then collaboration.
-void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d) {
+void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d,
+              const std::vector<std::pair<double, uint32_t>>* hostNums = nullptr) {
   if (g_indexed.load()) mt.enableIndex();
   mt.relpos = b->relpos;
   mt.nRelpos = b->relpos ? b->n_relpos : 0;
   mt.markerIdKey = b->marker_id_key;
+  if (b->adjusts != nullptr) {  // annotate-adjust: rows, host numbers (sorted once per batch)
+    mt.adjusts = b->adjusts;
+    mt.nAdjusts = b->n_adjusts;
+    mt.valueNum = b->value_num;
+    mt.nValues = b->value_num ? b->n_values : 0u;
+    mt.hostNumbers = hostNums;
+  }
   if (b->snapshots != nullptr && b->snapshots[d].loaded) {
     const fmt_mt_snapshot_doc& sd = b->snapshots[d];
     std::vector<MergeTree::LoadedSeg> head, body;
@@ -242,15 +266,16 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
                         uint32_t nThreads, fmt_mt_doc_result* hdrs, fmt_mt_leaf* leaves,
                         uint32_t capLeaves, uint16_t* chars, uint32_t capChars,
                         fmt_mt_propset* props, uint32_t capProps, fmt_mt_catchup_range* catchup,
-                        uint32_t capCatchup, double* seconds) {
+                        uint32_t capCatchup, double* seconds, double* nums, uint32_t capNums, uint32_t* nNums) {
   const auto t0 = std::chrono::steady_clock::now();
   std::atomic<int> status{FMT_OK};
+  const auto hn = hostNumbers(b);
   parallelFor(docBegin, docEnd, nThreads, [&](uint32_t d) {
     MergeTree mt;
     const size_t i = d - docBegin;
     int32_t failSeq = 0;
     int st = FMT_OK;
-    startDoc(mt, b, d);
+    startDoc(mt, b, d, &hn);
     const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
     std::vector<fmt_mt_catchup_range> cu;
     st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq,
@@ -270,6 +295,9 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
     }
     if (catchup)
       for (size_t k = 0; k < cu.size() && k < capCatchup; k++) catchup[i * capCatchup + k] = cu[k];
+    if (nNums) nNums[i] = static_cast<uint32_t>(mt.numbers.size());
+    if (nums)
+      for (size_t k = 0; k < mt.numbers.size() && k < capNums; k++) nums[i * capNums + k] = mt.numbers[k];
   });
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return status.load();
@@ -282,8 +310,9 @@ int orc_mt_replay_timed(const fmt_mt_batch* b, uint32_t d, uint64_t maxOps, doub
                         uint32_t capLeaves, uint16_t* chars, uint32_t capChars, fmt_mt_propset* props,
                         uint32_t capProps) {
   MergeTree mt;
+  const auto hn = hostNumbers(b);
   const auto t0 = std::chrono::steady_clock::now();
-  startDoc(mt, b, d);
+  startDoc(mt, b, d, &hn);
   const auto t1 = std::chrono::steady_clock::now();
   const uint64_t o0 = b->doc_op_offsets[d];
   uint64_t n = b->doc_op_offsets[d + 1] - o0;
@@ -312,9 +341,24 @@ void orc_set_index(int on) { g_indexed = on; }
 // Every remove stamp of every final leaf of document d, in stamp order: (leaf index, client, seq,
 // kind) quads into out[4 * k] (kind 0 = setRemove, 1 = sliceRemove), at most cap quads. Returns the
 // number of quads, or a negative FMT_E_* code.
+// Document d of a batch replayed, then its legacy summary (orc_mt_summary's layout and return value;
+// a negative FMT_E_* code when the replay fails).
+int orc_mt_replay_summary(const fmt_mt_batch* b, uint32_t d, const char* const* keys, int nKeys,
+                          const char* const* values, int nValues, int chunkSize, char* out, int cap,
+                          int* headerLen, int* bodyLen) {
+  MergeTree mt;
+  const auto hn = hostNumbers(b);
+  startDoc(mt, b, d, &hn);
+  const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
+  const int st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, nullptr);
+  if (st != FMT_OK) return st;
+  return orc_mt_summary(&mt, keys, nKeys, values, nValues, chunkSize, out, cap, headerLen, bodyLen);
+}
+
 int orc_mt_removers(const fmt_mt_batch* b, uint32_t d, int32_t* out, uint32_t cap) {
   MergeTree mt;
-  startDoc(mt, b, d);
+  const auto hn = hostNumbers(b);
+  startDoc(mt, b, d, &hn);
   const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
   const int st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, nullptr);
   if (st != FMT_OK) return st;

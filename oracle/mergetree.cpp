@@ -2,6 +2,9 @@
 #include "mergetree.hpp"
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.hpp"
@@ -630,21 +633,61 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
   if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
 }
 
-// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238 (raw values: for an
-// observer a remote raw change folds straight into msnConsensus, so the value is plain LWW; null
-// deletes the key; `seg.properties ??= createMap()` runs even if nothing changes).
-void MergeTree::annotateRange(int start, int end,
-                              const std::vector<std::pair<uint16_t, uint16_t>>& props,
-                              const Perspective& p, Stamp stamp) {
+// segmentPropertiesManager.ts:54-78 computePropertyValue for one adjust change onto the current value
+// `cur` (0: null / absent): (typeof number ? value : 0) + delta, then `adjusted > max` (a JSON null
+// max compares as 0 and is assigned: null), else `adjusted < min`. Returns the result's value id.
+double MergeTree::numberOfValue(uint16_t id) const {
+  if (id >= FMT_MT_VALUE_COMPUTED) return numbers.at(id - FMT_MT_VALUE_COMPUTED);
+  return valueNum != nullptr && id < nValues ? valueNum[id] : std::nan("");
+}
+
+// A number's value id: the host's id of a === number, else this document's computed entry (new
+// entries appended in first-computed order). -0 === 0.
+uint16_t MergeTree::valueOfNumber(double x) {
+  if (x == 0) x = 0;
+  if (hostNumbers != nullptr) {
+    auto it = std::lower_bound(hostNumbers->begin(), hostNumbers->end(), x,
+                               [](const std::pair<double, uint32_t>& e, double v) { return e.first < v; });
+    if (it != hostNumbers->end() && it->first == x) return static_cast<uint16_t>(it->second);
+  }
+  for (size_t k = 0; k < numbers.size(); k++)
+    if (numbers[k] == x) return static_cast<uint16_t>(FMT_MT_VALUE_COMPUTED + k);
+  if (numbers.size() >= 0x7FFF) throw DataError("more computed numbers than value ids");
+  numbers.push_back(x);
+  return static_cast<uint16_t>(FMT_MT_VALUE_COMPUTED + numbers.size() - 1);
+}
+
+uint16_t MergeTree::adjustedValue(uint16_t cur, const fmt_mt_adjust& a) {
+  const double c = numberOfValue(cur);  // (absent: null → not a number)
+  const double adjusted = (std::isnan(c) ? 0.0 : c) + a.delta;
+  if ((a.flags & FMT_MT_ADJ_MAX) && adjusted > ((a.flags & FMT_MT_ADJ_MAX_NULL) ? 0.0 : a.max))
+    return (a.flags & FMT_MT_ADJ_MAX_NULL) ? 0 : valueOfNumber(a.max);
+  if ((a.flags & FMT_MT_ADJ_MIN) && adjusted < ((a.flags & FMT_MT_ADJ_MIN_NULL) ? 0.0 : a.min))
+    return (a.flags & FMT_MT_ADJ_MIN_NULL) ? 0 : valueOfNumber(a.min);
+  return valueOfNumber(adjusted);
+}
+
+// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238. For an observer every
+// change is remote, and properties[key] = computePropertyValue(msnConsensus, remote) after each, which
+// is the running fold of the key's changes in seq order: a raw value replaces it, an adjust folds
+// onto it; null deletes the key; `seg.properties ??= createMap()` runs even if nothing changes.
+void MergeTree::annotateRange(int start, int end, const std::vector<PropChange>& props, const Perspective& p,
+                              Stamp stamp) {
   ensureIntervalBoundary(start, p);
   ensureIntervalBoundary(end, p);
   std::vector<Seg*> hit;
   nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
   for (Seg* s : hit) {
     s->props.defined = true;
-    for (const auto& [key, value] : props) {
+    for (const PropChange& ch : props) {
+      const uint16_t key = ch.key;
       auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(),
                              [&](const auto& e) { return e.first == key; });
+      uint16_t value = ch.value;
+      if (ch.adjust >= 0) {
+        if (adjusts == nullptr || static_cast<uint32_t>(ch.adjust) >= nAdjusts) throw DataError("adjust row out of range");
+        value = adjustedValue(it != s->props.kv.end() ? it->second : 0, adjusts[ch.adjust]);
+      }
       if (value == 0) {  // null → delete
         if (it != s->props.kv.end()) s->props.kv.erase(it);
       } else if (it != s->props.kv.end()) {
@@ -757,7 +800,9 @@ void MergeTree::insertLocal(int pos, const std::u16string& text) {
 
 void MergeTree::annotateLocal(int start, int end,
                               const std::vector<std::pair<uint16_t, uint16_t>>& props) {
-  annotateRange(start, end, props, localPerspective(),
+  std::vector<PropChange> ch;
+  for (const auto& [k, v] : props) ch.push_back(PropChange{k, v, -1});
+  annotateRange(start, end, ch, localPerspective(),
                 Stamp{collaborating ? kUnassignedSeq : 0, clientId});
 }
 
@@ -880,9 +925,16 @@ void MergeTree::applyRemote(const fmt_mt_op& opIn, const uint16_t* arena, const 
                       (op.flags & FMT_MT_F_END_BEFORE) != 0, p, stamp);
       break;
     case FMT_MT_ANNOTATE: {
-      std::vector<std::pair<uint16_t, uint16_t>> kv;
-      for (uint32_t i = propsOff[op.payload]; i < propsOff[op.payload + 1]; i++)
-        kv.emplace_back(static_cast<uint16_t>(propsKv[i] >> 16), static_cast<uint16_t>(propsKv[i] & 0xffff));
+      std::vector<PropChange> kv;
+      for (uint32_t i = propsOff[op.payload]; i < propsOff[op.payload + 1]; i++) {
+        const uint16_t key = static_cast<uint16_t>(propsKv[i] >> 16), value = static_cast<uint16_t>(propsKv[i] & 0xffff);
+        if (value == FMT_MT_VALUE_ADJUST) {  // (key, adjust row in the next word)
+          if (i + 1 >= propsOff[op.payload + 1]) throw DataError("adjust entry without its row");
+          kv.push_back(PropChange{key, 0, static_cast<int32_t>(propsKv[++i])});
+        } else {
+          kv.push_back(PropChange{key, value, -1});
+        }
+      }
       annotateRange(op.pos1, op.pos2, kv, p, stamp);
       break;
     }
@@ -1218,9 +1270,34 @@ void MergeTree::collectLeaves(std::vector<const Seg*>& out, std::vector<int>& bl
   *depth = maxDepth;
 }
 
-// JSON object of a property map: array-index keys first ascending, then insertion order.
+// JSON.stringify of a number (ECMA-262 Number::toString): the shortest %.*e digits that read back
+// as x, laid out in decimal for 1e-7 <= |x| < 1e21, else with an unpadded exponent; NaN / Infinity
+// are null, -0 is 0. (The oracle's own restatement; csrc/jsnum.h is the product's.)
+std::string jsNumberText(double x) {
+  if (std::isnan(x) || std::isinf(x)) return "null";
+  if (x == 0) return "0";
+  if (x < 0) return "-" + jsNumberText(-x);
+  char buf[64];
+  for (int prec = 1; prec <= 17; prec++) {
+    std::snprintf(buf, sizeof buf, "%.*e", prec - 1, x);
+    if (std::strtod(buf, nullptr) == x) break;
+  }
+  std::string mant, exps(std::strchr(buf, 'e') + 1);
+  for (const char* q = buf; *q != 'e'; q++)
+    if (*q >= '0' && *q <= '9') mant.push_back(*q);
+  while (mant.size() > 1 && mant.back() == '0') mant.pop_back();
+  const int k = static_cast<int>(mant.size()), n = std::atoi(exps.c_str()) + 1;
+  if (k <= n && n <= 21) return mant + std::string(n - k, '0');
+  if (0 < n && n <= 21) return mant.substr(0, n) + "." + mant.substr(n);
+  if (-6 < n && n <= 0) return "0." + std::string(-n, '0') + mant;
+  return mant.substr(0, 1) + (k > 1 ? "." + mant.substr(1) : "") + "e" + (n - 1 >= 0 ? "+" : "-") +
+         std::to_string(std::abs(n - 1));
+}
+
+// JSON object of a property map: array-index keys first ascending, then insertion order. Computed
+// annotate-adjust values (ids from FMT_MT_VALUE_COMPUTED) are numbers of `numbers`.
 static void emitProps(std::string& out, const PropMap& pm, const std::vector<std::string>& keys,
-                      const std::vector<std::string>& values) {
+                      const std::vector<std::string>& values, const std::vector<double>& numbers) {
   std::vector<std::pair<uint64_t, size_t>> idx;
   std::vector<size_t> rest;
   for (size_t i = 0; i < pm.kv.size(); i++) {
@@ -1236,7 +1313,11 @@ static void emitProps(std::string& out, const PropMap& pm, const std::vector<std
     first = false;
     jsonQuoteUtf8(out, keys.at(pm.kv[i].first));
     out.push_back(':');
-    out += values.at(pm.kv[i].second);
+    const uint16_t v = pm.kv[i].second;
+    if (v >= FMT_MT_VALUE_COMPUTED && v - FMT_MT_VALUE_COMPUTED < numbers.size())
+      out += jsNumberText(numbers[v - FMT_MT_VALUE_COMPUTED]);
+    else
+      out += values.at(v);
   };
   for (auto& e : idx) one(e.second);
   for (size_t i : rest) one(i);
@@ -1306,14 +1387,14 @@ Summary MergeTree::summarize(const std::vector<std::string>& keys,
         j += "}";
         if (o.props.defined) {
           j += ",\"props\":";
-          emitProps(j, o.props, keys, values);
+          emitProps(j, o.props, keys, values, numbers);
         }
         j.push_back('}');
       } else if (o.props.defined) {
         j += "{\"text\":";
         jsonQuoteUtf16(j, o.text.data(), o.text.size());
         j += ",\"props\":";
-        emitProps(j, o.props, keys, values);
+        emitProps(j, o.props, keys, values, numbers);
         j.push_back('}');
       } else {
         jsonQuoteUtf16(j, o.text.data(), o.text.size());

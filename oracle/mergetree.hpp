@@ -215,6 +215,22 @@ class MergeTree {
   // (sequence.ts:395-452), tagged with catchupOp.
   std::vector<fmt_mt_catchup_range>* catchupOut = nullptr;
   uint32_t catchupOp = 0;
+  // Annotate-adjust (IMergeTreeAnnotateAdjustMsg, ops.ts:187-222): the batch's adjust rows, the
+  // number of each host value id (NaN: not a number), the host's numbers with their ids, and this
+  // document's computed numbers (value ids FMT_MT_VALUE_COMPUTED + index, first-computed order).
+  const fmt_mt_adjust* adjusts = nullptr;
+  uint32_t nAdjusts = 0;
+  const double* valueNum = nullptr;
+  uint32_t nValues = 0;
+  const std::vector<std::pair<double, uint32_t>>* hostNumbers = nullptr;  // sorted by number
+  std::vector<double> numbers;
+  // One change of an annotate op, in opToChanges order (segmentPropertiesManager.ts:86-95): a raw
+  // value id (0 = null), or an adjust row (adjust >= 0).
+  struct PropChange {
+    uint16_t key;
+    uint16_t value;
+    int32_t adjust;
+  };
   // Legacy relative positions (FMT_MT_F_REL1/REL2): the batch's table and the "markerId" key id.
   const fmt_mt_relpos* relpos = nullptr;
   uint32_t nRelpos = 0;
@@ -299,7 +315,10 @@ class MergeTree {
   void attachRef(LRef* ref, Seg* seg, int offset);
   static void detachRef(LRef* ref);
   std::pair<Seg*, int> getContainingSegment(int pos, const Perspective& p) const;
-  void annotateRange(int start, int end, const std::vector<std::pair<uint16_t, uint16_t>>& props,
+  uint16_t adjustedValue(uint16_t cur, const fmt_mt_adjust& a);  // computePropertyValue for one adjust
+  double numberOfValue(uint16_t id) const;
+  uint16_t valueOfNumber(double x);
+  void annotateRange(int start, int end, const std::vector<PropChange>& props,
                      const Perspective& p, Stamp stamp);
   void addToLRUSet(Seg* leaf, int seq);
   void setMinSeq(int min);

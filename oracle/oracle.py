@@ -43,7 +43,9 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_removers.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_mt_replay_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P,
                                           ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P,
-                                          ctypes.c_uint32, P]
+                                          ctypes.c_uint32, P, P, ctypes.c_uint32, P]
+        L.orc_mt_replay_summary.argtypes = [P, ctypes.c_uint32, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P,
+                                            ctypes.c_int, P, P]
         L.orc_mt_replay_timed.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P, ctypes.c_uint32, P,
                                           ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_set_index.argtypes = [ctypes.c_int]
@@ -139,11 +141,13 @@ class MergeTreeDoc:
 
 
 def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096, cap_chars=1 << 16,
-                    cap_props=64, outputs=True, cap_catchup=0):
+                    cap_props=64, outputs=True, cap_catchup=0, numbers=None):
     """Replay a MergeTreeBatch; returns (rc, headers, leaves, chars, props, seconds).
 
     With cap_catchup > 0 the catch-up ranges of FMT_MT_F_CATCHUP ops are recorded too and returned
     as a 7th element, shape (n_docs, cap_catchup) of CATCHUP_DTYPE (headers' n_catchup counts them).
+    With a list `numbers`, each document's computed annotate-adjust numbers (value ids
+    FMT_MT_VALUE_COMPUTED + index) are appended to it as a float64 array.
     """
     from fluidframework_amd.native import (CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE,
                                            batch_struct)
@@ -156,11 +160,18 @@ def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096
     props = np.zeros(n * cap_props, dtype=PROPSET_DTYPE) if outputs else None
     catchup = np.zeros(n * cap_catchup, dtype=CATCHUP_DTYPE) if cap_catchup else None
     secs = ctypes.c_double(0)
+    cap_nums = 4096 if numbers is not None else 0
+    nums = np.zeros(n * cap_nums, dtype=np.float64) if cap_nums else None
+    n_nums = np.zeros(n, dtype=np.uint32) if cap_nums else None
     b, keep = batch_struct(batch)
     rc = lib().orc_mt_replay_batch(ctypes.byref(b), doc_begin, doc_end, threads, _ptr(hdrs),
                                    _ptr(leaves), cap_leaves, _ptr(chars), cap_chars, _ptr(props),
-                                   cap_props, _ptr(catchup), cap_catchup, ctypes.byref(secs))
+                                   cap_props, _ptr(catchup), cap_catchup, ctypes.byref(secs),
+                                   _ptr(nums), cap_nums, _ptr(n_nums))
     del keep
+    if numbers is not None:
+        for i in range(n):
+            numbers.append(nums[i * cap_nums: i * cap_nums + min(int(n_nums[i]), cap_nums)].copy())
     if outputs:
         leaves = leaves.reshape(n, cap_leaves)
         chars = chars.reshape(n, cap_chars)
@@ -168,6 +179,26 @@ def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096
     if cap_catchup:
         return rc, hdrs, leaves, chars, props, secs.value, catchup.reshape(n, cap_catchup)
     return rc, hdrs, leaves, chars, props, secs.value
+
+
+def mt_replay_summary(batch, doc: int, keys, values, chunk_size: int = 10000):
+    """Document `doc` of a batch replayed by the oracle, then its legacy summary (header, body) from
+    the oracle's own SnapshotLegacy restatement; raises on a replay failure."""
+    from fluidframework_amd.native import batch_struct
+
+    kk, vv = _cstrs(keys), _cstrs(values)
+    b, keep = batch_struct(batch)
+    hl, bl = ctypes.c_int(0), ctypes.c_int(0)
+    n = lib().orc_mt_replay_summary(ctypes.byref(b), doc, kk, len(keys), vv, len(values), chunk_size, None, 0,
+                                    ctypes.byref(hl), ctypes.byref(bl))
+    if n < 0:
+        raise RuntimeError(f"oracle replay failed ({n}): {lib().orc_last_error().decode()}")
+    buf = ctypes.create_string_buffer(n)
+    lib().orc_mt_replay_summary(ctypes.byref(b), doc, kk, len(keys), vv, len(values), chunk_size, buf, n,
+                                ctypes.byref(hl), ctypes.byref(bl))
+    del keep
+    raw = buf.raw[:n]
+    return raw[: hl.value].decode("utf-8"), (raw[hl.value:].decode("utf-8") if bl.value else None)
 
 
 def set_index(on: bool):

@@ -32,6 +32,7 @@ def emu_lib():
         L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
                                                               ctypes.c_void_p, ctypes.c_uint32]
         L.emu_mt_capacity.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint32)] * 3
+        L.emu_mt_numbers.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
         _emu = L
     return _emu
 
@@ -114,6 +115,13 @@ def emu_replay(batch, cap_catchup=0, force_ob=False, large=False, cap_rm=0):
     if cap_rm:
         out = out + (rm.reshape(n, cap_rm),)
     return out
+
+
+def emu_numbers(doc: int) -> np.ndarray:
+    """Document `doc`'s computed annotate-adjust numbers after the last emu_replay."""
+    out = np.zeros(4096, dtype=np.float64)
+    n = emu_lib().emu_mt_numbers(doc, _p(out), 4096)
+    return out[:n]
 
 
 def resolve_props(pid, table):

@@ -323,3 +323,27 @@ def test_inserts_with_props_match_oracle(orc, n_clients):
         hdr, leaves, chars, props = small if int(small[0]["status"][d]) == 0 else large
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
         assert not diffs, f"doc {d}: {diffs[:5]}"
+
+
+def test_large_tier_zamboni_matches_props_beyond_127_sets(orc):
+    """Documents with hundreds of distinct prop sets (annotate values cycling over 400 texts): the
+    large tier's zamboni compares prop-set ids of up to 1024 sets when it decides appends
+    (matchProperties), not a 7-bit packing of them; bit-exact vs the oracle."""
+    import copy
+
+    batch = copy.copy(workloads.conflict_farm(6, n_clients=8, ops_per_doc=2000, seed=23))
+    ann = np.nonzero(batch.ops["type"] == 2)[0]
+    batch.ops = batch.ops.copy()
+    batch.ops["payload"][ann] = np.arange(len(ann), dtype=np.uint32)
+    batch.props_off = np.arange(len(ann) + 1, dtype=np.uint32)
+    batch.props_kv = (1 + np.arange(len(ann), dtype=np.uint32) % 400)
+    batch.values = ["null"] + [f'"v{i}"' for i in range(400)]
+    batch.keys = ["k"]
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+    assert rc == 0
+    hdr, leaves, chars, props = emu_replay(batch, large=True)
+    assert (hdr["status"] == 0).all() and hdr["n_props"].max() > 127
+    for d in range(batch.n_docs):
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (hdr[d], leaves[d], chars[d], props[d]))
+        assert not diffs, f"doc {d}: {diffs[:5]}"

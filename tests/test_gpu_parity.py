@@ -616,3 +616,60 @@ def test_mt_v1_merge_info_load_on_gpu(orc, engine):
     for d, want in enumerate(expected):
         leaves, chars, _ = engine.mt_doc(d, hdrs[d])
         assert visible_text(hdrs[d], leaves, chars) == want, d
+
+
+@pytest.mark.parametrize("narrow", [True, False])
+def test_mt_annotate_adjust_farms_on_gpu(orc, engine, narrow):
+    """Annotate-adjust (computePropertyValue, segmentPropertiesManager.ts:54-78) on the GPU: the
+    reference's conflict-farm fixtures with annotates rewritten into adjusts (test_annotate_adjust.py),
+    cycled to 120 documents; engine == oracle bit for bit incl. the computed-number tables, final
+    texts == the fixtures' resultText. narrow: values stay in the small tier; wide: hundreds of prop
+    sets, documents escalate to the large tier."""
+    import copy
+
+    from test_annotate_adjust import adjust_fixture_batch
+
+    base, finals = adjust_fixture_batch(narrow=narrow)
+    reps = 20
+    batch = copy.copy(base)
+    n = int(base.doc_op_offsets[-1])
+    batch.ops = np.concatenate([base.ops] * reps)
+    batch.doc_op_offsets = np.concatenate([base.doc_op_offsets[:-1] + r * n for r in range(reps)] + [[reps * n]]).astype(np.uint64)
+    batch.doc_init = np.concatenate([base.doc_init] * reps)
+    hdrs = _gpu_mt(engine, batch)
+    cl, cc, cp = native.capacity()
+    nums = []
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(base, threads=16, cap_leaves=cl, cap_chars=cc, cap_props=max(cp, 256),
+                                                numbers=nums)
+    assert rc == 0
+    computed = 0
+    for d in range(batch.n_docs):
+        k = d % base.n_docs
+        leaves, chars, props = engine.mt_doc(d, hdrs[d])
+        diffs = compare_doc((oh[k], ol[k], oc[k], op[k]), (hdrs[d], leaves, chars, props))
+        assert not diffs, f"doc {d}: {diffs[:5]}"
+        assert np.array_equal(engine.mt_numbers(d), nums[k]), d
+        assert visible_text(hdrs[d], leaves, chars) == finals[k]
+        computed += len(nums[k])
+    assert computed > 0
+
+
+def test_mt_bulk_legacy_summaries_with_adjusts(orc, engine):
+    """fmt_mt_summarize_legacy with computed numbers: documents whose adjusted keys are last annotated
+    at or below minSeq give the oracle's own SnapshotLegacy bytes (C++ JSON.stringify of the numbers);
+    the others report FMT_E_UNSUPPORTED for that document only."""
+    from fluidframework_amd.native import EngineError
+    from fluidframework_amd.summary import adjust_last_seq
+    from test_annotate_adjust import adjust_fixture_batch
+
+    for exact_tail in (True, False):
+        batch, _ = adjust_fixture_batch(exact_tail)
+        hdrs = _gpu_mt(engine, batch)
+        engine.mt_summarize_legacy(batch.keys, batch.values)
+        for d in range(batch.n_docs):
+            if adjust_last_seq(batch, d) > int(hdrs[d]["min_seq"]):
+                with pytest.raises(EngineError) as ei:
+                    engine.mt_summary(d)
+                assert ei.value.code == -5
+            else:
+                assert engine.mt_summary(d) == orc.mt_replay_summary(batch, d, batch.keys, batch.values), d

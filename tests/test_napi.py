@@ -45,10 +45,10 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
-                               "fetchRemoveOrder",
-                               "replayMap", "fetchDoc", "sizes"])
+                               "fetchRemoveOrder", "fetchNumbers", "replayMapSparse", "summarizeLegacy",
+                               "summaryBlobs", "replayMap", "fetchDoc", "sizes"])
     assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
-                        "catchupRange": 16}
+                        "catchupRange": 16, "mapEntry": 12, "adjust": 32}
     assert out["c"]["leaves"] >= 512
 
 
@@ -329,3 +329,109 @@ def test_js_v1_merge_info_load_on_gpu(addon, tmp_path):
     r = _node(str(script), timeout=300)
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout) == [want for _, _, want in cases]
+
+
+def _adjust_js(docs, body):
+    return (f"const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});"
+            "const b=new fmt.MergeTreeStreamBuilder();"
+            f"for(const x of {json.dumps(docs)}){{const d=b.beginDoc(x[0],'A');for(const m of x[1]) d.addMessage(m);}}" + body)
+
+
+def test_js_packer_annotate_adjust_matches_python(addon, tmp_path):
+    """Annotate-adjust packs identically in the JS and Python packers: the props ops with their
+    (key, FMT_MT_VALUE_ADJUST) + row entries, the fmt_mt_adjust rows, and each value's number."""
+    from test_annotate_adjust import adjust_fixture_batch
+
+    docs = adjust_fixture_batch(messages=True)
+    script = tmp_path / "adj_pack.js"
+    script.write_text(_adjust_js(docs, (
+        "const r=b.finish();const hex=(a)=>Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
+        "process.stdout.write(JSON.stringify({ops:hex(r.ops),off:hex(r.propsOff),kv:hex(r.propsKv),adj:hex(r.adjusts),"
+        "num:hex(r.valueNum),values:r.values}))")))
+    r = _node(str(script))
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    py, _ = adjust_fixture_batch()
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert bytes.fromhex(out["off"]) == py.props_off.tobytes() and bytes.fromhex(out["kv"]) == py.props_kv.tobytes()
+    assert bytes.fromhex(out["adj"]) == py.adjusts.tobytes()
+    assert bytes.fromhex(out["num"]) == py.value_num.tobytes()
+    assert out["values"] == py.values
+
+
+@pytest.mark.gpu
+def test_js_annotate_adjust_summaries_on_gpu(addon, tmp_path, orc):
+    """Through the addon: getText equals the fixtures' resultText; summarizeV1 (computed numbers as
+    JSON.stringify writes them) equals the Python host over the GPU state; the legacy summary of an
+    exact-tail document equals the oracle's SnapshotLegacy restatement, and the others are refused
+    with FMT_E_UNSUPPORTED."""
+    from fluidframework_amd import native
+    from fluidframework_amd.summary import v1_summary, values_with_numbers, removers_from_engine
+    from test_annotate_adjust import adjust_fixture_batch
+
+    for exact_tail in (True, False):
+        docs = adjust_fixture_batch(exact_tail=exact_tail, messages=True)
+        script = tmp_path / f"adj_gpu_{exact_tail}.js"
+        script.write_text("(async()=>{" + _adjust_js(docs, (
+            "const e=new fmt.Engine(0);const r=await e.replayMergeTree(b.finish());const out=[];"
+            f"for(let i=0;i<{len(docs)};i++){{let leg=null;try{{leg=r.summarize(i)}}catch(x){{leg=x.code}}"
+            "out.push({text:r.getText(i),v1:r.summarizeV1(i),legacy:leg});}"
+            "e.close();process.stdout.write(JSON.stringify(out));})().catch((e)=>{console.error(e);process.exit(1);});")))
+        r = _node(str(script), timeout=300)
+        assert r.returncode == 0, r.stderr
+        out = json.loads(r.stdout)
+        batch, finals = adjust_fixture_batch(exact_tail)
+        for d, o in enumerate(out):
+            assert o["text"] == finals[d]
+            if isinstance(o["legacy"], str):
+                assert not exact_tail and o["legacy"] == "FMT_E_UNSUPPORTED"
+            else:
+                want = orc.mt_replay_summary(batch, d, batch.keys, batch.values)
+                assert [o["legacy"]["header"], o["legacy"].get("body")] == list(want), d
+        assert not exact_tail or all(not isinstance(o["legacy"], str) for o in out)
+        e = native.Engine(0)
+        try:
+            e.mt_load(batch)
+            e.mt_run()
+            hdrs = e.mt_headers()
+            for d, o in enumerate(out):
+                lv, ch, pr = e.mt_doc(d, hdrs[d])
+                vals = values_with_numbers(batch.values, e.mt_numbers(d))
+                a, bb = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+                rem = removers_from_engine(lv, int(hdrs[d]["n_leaves"]), e.mt_remove_order(d, hdrs[d]), batch.ops[a:bb])
+                head, bodies = v1_summary(hdrs[d], lv, ch, pr, batch.keys, vals, batch.clients[d], rem)
+                assert [o["v1"]["header"], o["v1"]["bodies"]] == [head, bodies], d
+        finally:
+            e.close()
+
+
+@pytest.mark.gpu
+def test_js_sparse_map_and_bulk_summaries_on_gpu(addon, tmp_path):
+    """The addon's sparse map path (replayMapSparse, key pools of any size) gives the dense path's live
+    entries and summaries; the bulk legacy summaries (summarizeAllLegacy: device merge + C++ JSON)
+    equal the JS host's per-document summarize() on the reference's replay fixtures."""
+    js = f"""const fmt=require({json.dumps(os.path.join(REPO, 'fluidframework_amd', 'js', 'fmt.js'))});
+const zlib=require('zlib');const fs=require('fs');
+(async()=>{{
+const mb=new fmt.MapStreamBuilder();let x=12345;const rnd=(n)=>{{x=(x*1103515245+12345)%2147483648;return x%n;}};
+for(let d=0;d<64;d++){{const doc=mb.beginDoc();for(let s=1;s<=600;s++){{const r=rnd(41);
+ const c=r<20?{{type:'set',key:'k'+rnd(3000),value:{{type:'Plain',value:rnd(50)}}}}:(r<40?{{type:'delete',key:'k'+rnd(3000)}}:{{type:'clear'}});
+ mb.addMessage(doc,s,c);}}}}
+const mbatch=mb.finish();const e=new fmt.Engine(0);
+const dense=await e.replayMap(mbatch);const sparse=await e.replayMapSparse(mbatch);
+const out={{map:[]}};
+for(let d=0;d<64;d++) out.map.push([JSON.stringify(dense.entries(d))===JSON.stringify(sparse.entries(d)),
+  JSON.stringify(dense.summarize(d))===JSON.stringify(sparse.summarize(d)), sparse.entries(d).length]);
+const fx=JSON.parse(zlib.gunzipSync(fs.readFileSync({json.dumps(GOLDEN)})).toString());
+const b=new fmt.MergeTreeStreamBuilder();
+for(const f of fx){{const d=b.beginDoc(f.groups[0].initialText,'A');for(const g of f.groups) for(const m of g.msgs) d.addMessage(m);}}
+const r=await e.replayMergeTree(b.finish());const t=await r.summarizeAllLegacy();out.bytes=t.bytes;out.legacy=[];
+for(let d=0;d<fx.length;d++){{const a=r.legacyBlobs(d),h=r.summarize(d);out.legacy.push(a.header===h.header&&a.body===h.body);}}
+e.close();process.stdout.write(JSON.stringify(out));}})().catch((e)=>{{console.error(e);process.exit(1);}});"""
+    script = tmp_path / "sparse_bulk.js"
+    script.write_text(js)
+    r = _node(str(script), timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert all(a and b for a, b, _ in out["map"]) and sum(n for _, _, n in out["map"]) > 1000
+    assert out["bytes"] > 0 and all(out["legacy"])

@@ -35,4 +35,4 @@ def test_oracle_and_engine_source_under_asan_ubsan():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("tier")]
-    assert len(lines) == 5 and all(l.endswith(": 0 mismatches") for l in lines), r.stdout
+    assert len(lines) == 7 and all(l.endswith(": 0 mismatches") for l in lines), r.stdout
