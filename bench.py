@@ -473,15 +473,25 @@ def _issue_record(traffic):
     if not rec:
         return None
     split = rec.get("wave_cycle_split", {})
+    counters = rec.get("counters", {})
+    cycles, simds = rec.get("kernel_cycles"), 1024
+
+    def busy(pipe, name):  # per-pipe fraction of SIMD issue slots (tools/pmc_issue.py), each <= 1
+        if rec.get(f"{pipe}_busy") is not None:
+            return rec[f"{pipe}_busy"]
+        return 4.0 * counters[name] / (cycles * simds) if cycles and name in counters else None
+
     return {
         "insts_per_op": rec.get("insts_per_op"),
-        "valu_busy": rec.get("valu_busy"),
-        "issue_busy": rec.get("issue_busy"),
+        "valu_busy": busy("valu", "SQ_ACTIVE_INST_VALU"),
+        "salu_busy": busy("salu", "SQ_ACTIVE_INST_SCA"),
+        "lds_busy": busy("lds", "SQ_ACTIVE_INST_LDS"),
         "wave_cycles_active": split.get("active_inst_any"),
         "wave_cycles_waitcnt": split.get("wait_any"),
         "wave_cycles_issue_stall": split.get("wait_inst_any"),
         "source": rec["source"][0].rsplit("/", 2)[0],
-        "note": "VALU busy = 4*SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); wave-cycle split from "
+        "note": "<pipe>_busy = 4*SQ_ACTIVE_INST_<pipe> / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs), per pipe (they issue "
+                "in parallel, so they do not sum to one); wave-cycle split from "
                 "SQ_WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_ANY (waitcnt) + WAIT_INST_ANY (issue stall)",
     }
 

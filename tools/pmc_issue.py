@@ -60,10 +60,14 @@ def main():
     if grbm:
         cycles = grbm[0] / 8.0
         rec["kernel_cycles"] = cycles
-        if "SQ_ACTIVE_INST_VALU" in c:
-            rec["valu_busy"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / (cycles * simds)
-        if "SQ_ACTIVE_INST_ANY" in c:
-            rec["issue_busy"] = 4.0 * c["SQ_ACTIVE_INST_ANY"] / (cycles * simds)
+        # Per-pipe busy fractions, each <= 1: a SIMD gets one issue slot per pipe every 4 cycles
+        # (the sequencer visits the 4 SIMDs of a CU round-robin), and ACTIVE_INST_<pipe> counts the
+        # quad-cycles in which that pipe held an instruction of this kernel. The pipes issue in
+        # parallel, so the fractions do not add up to one "issue busy" figure.
+        for pipe, n in (("valu", "SQ_ACTIVE_INST_VALU"), ("salu", "SQ_ACTIVE_INST_SCA"),
+                        ("lds", "SQ_ACTIVE_INST_LDS")):
+            if n in c:
+                rec[f"{pipe}_busy"] = 4.0 * c[n] / (cycles * simds)
         if "SQ_BUSY_CYCLES" in c:
             rec["sq_busy_cycles"] = c["SQ_BUSY_CYCLES"]
     db = json.load(open(out)) if os.path.exists(out) else {}
