@@ -260,15 +260,14 @@ def main():
     achieved = bytes_per_launch / (avg_kernel_ms / 1e3) / 1e9
 
     cpu = cpu_js = None
-    # (the sparse map line has none: the oracle's dense per-(doc, key) output would dominate its time)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not t2 and not args.sparse:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not t2:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # CPU baseline only ("port" of the reference path)
 
         hc = host_cpus()
         threads = args.cpu_threads or hc["usable"]
         # bounded sample: consecutive chunks of the same batch until >= --cpu-seconds of CPU work
-        chunk = args.cpu_sample_docs or (min(docs, 4 * threads * 80) if mt else min(docs, 200_000))
+        chunk = args.cpu_sample_docs or (min(docs, 4 * threads * 80) if mt else min(docs, 50_000 if args.sparse else 200_000))
         secs, sample_ops, sample_docs, lo = 0.0, 0, 0, 0
         while secs < args.cpu_seconds:
             hi = min(lo + chunk, docs)
@@ -278,7 +277,10 @@ def main():
                 o0, o1 = int(batch.doc_op_offsets[lo]), int(batch.doc_op_offsets[hi])
                 sub = batch.__class__(batch.ops[o0:o1], batch.doc_op_offsets[lo : hi + 1] - o0,
                                       batch.key_bound, batch.keys, batch.values)
-                _, s_ = oracle.map_replay(sub, threads=threads)
+                if args.sparse:  # hash map per document (the dense table would be key_bound x 8 B per doc)
+                    _, _, s_ = oracle.map_replay_sparse(sub, threads=threads)
+                else:
+                    _, s_ = oracle.map_replay(sub, threads=threads)
             secs += s_
             sample_ops += int(batch.doc_op_offsets[hi] - batch.doc_op_offsets[lo])
             sample_docs += hi - lo
@@ -290,12 +292,13 @@ def main():
             "kind": "port",
             "seconds": secs,
             "sample": f"{sample_docs} documents ({sample_ops} ops) of the same workload in chunks of {chunk}, "
-                      f"C++ oracle -O3, one document per task on {threads} std::threads",
+                      f"C++ oracle -O3{' (sparse: std::unordered_map key index per document)' if args.sparse else ''}, "
+                      f"one document per task on {threads} std::threads",
             "cpu_model": hc["model"],
             "host_cpus": {k: hc[k] for k in ("cpu_count", "affinity", "cgroup_quota_cpus")},
         }
         log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
-        if not args.no_js_baseline and not ob:
+        if not args.no_js_baseline and not ob and not args.sparse:
             cpu_js = (_js_mt_baseline if mt else _js_map_baseline)(oracle, batch, docs, threads, args.cpu_seconds / 2)
             if cpu_js is not None:
                 log(rank, f"[bench] JS baseline {cpu_js['value']:.3g} ops/s on {threads} worker_threads")
@@ -304,6 +307,7 @@ def main():
     # (tools/pmc_traffic.py; gfx950 FETCH_SIZE correction applied there), or null.
     traffic = None
     tkey = (f"{args.workload}:{docs}x{opd}" + ("" if mt or args.key_pool == 20 else f"k{args.key_pool}")
+            + ("s" if args.sparse else "")
             + (f"m{args.min_length}" if mt and args.min_length else ""))
     tpath = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(tpath):
@@ -356,6 +360,9 @@ def main():
                                                          if args.key_pool <= 2560 else "mapLwwHbmKernel+mapLwwFinishKernel"),
                 "limiter": ("per-document dependent op chain: VALU issue + LDS/readlane latency of one wave per "
                             "document (HBM fraction is reported for the contract; see DESIGN.md)") if mt
+                           else ("per-document LDS hash reduce-by-key (ds_cmpswap claims, dependent LDS "
+                                 "round trips) at the occupancy the 16 KiB table allows; HBM streaming of 16-byte op "
+                                 "records is the bound it is measured against") if args.sparse
                            else "HBM streaming of 16-byte op records",
                 "bytes_per_launch": bytes_per_launch,
                 "avg_kernel_ms": avg_kernel_ms,

@@ -42,6 +42,7 @@ function markerRefType(spec) {
 	return r;
 }
 const MAX_CLIENTS = 63;
+const RECYCLE_FROM = 32; // fresh short ids up to the small tier's 31 writers, then recycled (streams.py)
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 36;
 const CATCHUP_BYTES = 16, SNAPSHOT_DOC_BYTES = 32;
@@ -134,6 +135,8 @@ class MergeTreeDocBuilder {
 		this.index = index;
 		this.clientIds = new Map([[observer, 0]]);
 		this.clientNames = [observer];
+		this.lastStamp = [null]; // per short id: the current holder's latest stamp seq
+		this.minSeq = 0; // the engine's minSeq when the next message applies
 		this.nOps = 0;
 		this.messages = []; // {message, firstOp, count} when the builder keeps messages
 		// idToMarker history (streams.py _DocBuilder): exact while every marker id names one marker
@@ -164,15 +167,36 @@ class MergeTreeDocBuilder {
 		if ((none(op.pos1) && !none(op.relativePos1)) || (none(op.pos2) && !none(op.relativePos2))) this.usesRelpos = true;
 		this.checkMarkers();
 	}
-	shortClient(longId) {
+	/**
+	 * getOrAddShortClientId (client.ts:831-855) with recycling (mirrors streams.py short_client): a
+	 * new client takes, past RECYCLE_FROM - 1 ids, the id of a client whose every stamp is at or
+	 * below the engine's minSeq; `seq` notes a stamp of the client.
+	 */
+	shortClient(longId, seq) {
 		const id = longId === null || longId === undefined ? "server" : longId;
 		let i = this.clientIds.get(id);
 		if (i === undefined) {
 			i = this.clientNames.length;
-			if (i > MAX_CLIENTS) throw new UnsupportedOp(`more than ${MAX_CLIENTS} clients in one document`);
+			if (i >= RECYCLE_FROM) {
+				for (let j = 1; j < this.clientNames.length; j++) {
+					const st = this.lastStamp[j];
+					if (st === null || st <= this.minSeq) {
+						this.clientIds.delete(this.clientNames[j]);
+						this.clientNames[j] = id;
+						this.lastStamp[j] = null;
+						i = j;
+						break;
+					}
+				}
+			}
+			if (i === this.clientNames.length) {
+				if (i > MAX_CLIENTS) throw new UnsupportedOp(`more than ${MAX_CLIENTS} clients with stamps above minSeq in one document`);
+				this.clientNames.push(id);
+				this.lastStamp.push(null);
+			}
 			this.clientIds.set(id, i);
-			this.clientNames.push(id);
 		}
+		if (seq !== undefined && (this.lastStamp[i] === null || seq > this.lastStamp[i])) this.lastStamp[i] = seq;
 		return i;
 	}
 	/** One ISequencedDocumentMessage with merge-tree contents (client.applyMsg, client.ts:1358). */
@@ -180,7 +204,7 @@ class MergeTreeDocBuilder {
 		if (this.owner.current !== this) {
 			throw new UnsupportedOp("documents must be packed contiguously (finish one before the next)");
 		}
-		const client = this.shortClient(msg.clientId);
+		const client = this.shortClient(msg.clientId, msg.sequenceNumber);
 		const contents = msg.contents;
 		let members = contents.type === MT_GROUP ? contents.ops : [contents];
 		if (members.length === 0) members = [null]; // empty group: only advances the window
@@ -191,6 +215,7 @@ class MergeTreeDocBuilder {
 				msg.minimumSequenceNumber, client, k > 0 ? FMT_MT_F_GROUP_CONT : 0);
 			this.nOps++;
 		});
+		if (msg.minimumSequenceNumber > this.minSeq) this.minSeq = msg.minimumSequenceNumber; // updateSeqNumbers
 	}
 	/** SharedObjectCore.processMessagesCore shape: a bunch sharing one envelope (sequence.ts:873-919). */
 	processMessagesCore(messagesCollection) {
@@ -278,18 +303,18 @@ class MergeTreeStreamBuilder {
 	mergeInfo(spec, d) {
 		this.hasMergeInfo = true;
 		const insSeq = spec.seq === undefined ? 0 : spec.seq;
-		const insClient = spec.client === undefined || spec.client === null ? FMT_NON_COLLAB_CLIENT : d.shortClient(spec.client);
+		const insClient = spec.client === undefined || spec.client === null ? FMT_NON_COLLAB_CLIENT : d.shortClient(spec.client, insSeq);
 		const stamps = [];
 		if (spec.removedSeq !== undefined) {
 			let ids = spec.removedClientIds;
 			if (ids === undefined && spec.removedClient !== undefined) ids = [spec.removedClient];
 			if (ids === undefined) throw new Error("must have removedClient ids");
-			for (const c of ids) stamps.push([spec.removedSeq, d.shortClient(c), 0]);
+			for (const c of ids) stamps.push([spec.removedSeq, d.shortClient(c, spec.removedSeq), 0]);
 		}
 		if (spec.movedSeq !== undefined) {
 			const seqs = spec.movedSeqs, ids = spec.movedClientIds;
 			if (seqs === undefined || ids === undefined || seqs.length !== ids.length) throw new Error("must have movedIds ids");
-			seqs.forEach((s, i) => stamps.push([s, d.shortClient(ids[i]), 1]));
+			seqs.forEach((s, i) => stamps.push([s, d.shortClient(ids[i], s), 1]));
 		}
 		const sorted = stamps.map((x, i) => [x, i]).sort((a, b) => a[0][0] - b[0][0] || a[1] - b[1]).map((x) => x[0]);
 		const first = this.snapshotStamps.length;
@@ -314,6 +339,7 @@ class MergeTreeStreamBuilder {
 		}
 		const specsOf = (c) => (c.version === "1" ? c.segments : c.segmentTexts);
 		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "snapshot" : observer);
+		d.minSeq = md.minSequenceNumber === undefined ? md.sequenceNumber : md.minSequenceNumber;
 		const first = this.snapshotSegs.length;
 		chunks.forEach((c, ci) => {
 			for (let spec of specsOf(c)) {

@@ -105,6 +105,9 @@ MAP_KIND_SHIFT = 30
 MAP_VALUE_UNDEFINED = 0x3FFFFFFF
 MAP_ABSENT = 0xFFFFFFFF
 MAX_CLIENTS = 63  # short ids 1..63 (the observer is 0); remove-client sets are 64-bit masks
+# Short ids up to 31 (the small tier's writers) are handed out fresh; past that a new client takes the
+# id of a client whose every stamp is at or below the engine's minSeq (see _DocBuilder.short_client).
+RECYCLE_FROM = 32
 
 
 class UnsupportedOp(NotImplementedError):
@@ -246,6 +249,8 @@ class _DocBuilder:
         self.owner = owner
         self.client_ids = {observer: 0}
         self.client_names = [observer]
+        self.last_stamp = [None]  # per short id: the current holder's latest stamp seq (None: none yet)
+        self.min_seq = 0          # the engine's minSeq when the next message applies
         self.ops: list[tuple] = []
         self.messages: list[tuple] = []
         # idToMarker history (mergeTree.ts:675, 1614-1620, 2835-2840; zamboni.ts:202-204): the engine
@@ -284,23 +289,46 @@ class _DocBuilder:
     def n_ops(self) -> int:
         return len(self.ops)
 
-    def short_client(self, long_id) -> int:
+    def short_client(self, long_id, seq=None) -> int:
+        """The short id of a long client id (getOrAddShortClientId, client.ts:831-855), noting a
+        stamp at `seq`. The reference never forgets a long id; here ids are recycled, because every
+        reconnect brings a new clientId and the engine's remove-client sets hold 31 (small tier) or
+        63 (large tier) writers. A short id matters only through stamps above minSeq: a perspective
+        (refSeq >= minSeq, client) sees a stamp at or below minSeq by its seq whoever made it, and
+        merge info (SnapshotV1, catch-up) is written only for stamps above the final minSeq. So once
+        every stamp of a client is at or below the engine's minSeq, its id can pass to a new client
+        (a returning client just gets a new id). Ids stay fresh up to RECYCLE_FROM - 1; the oldest
+        free-able id is taken before a fresh one past that. After the last op, client_names[id] is
+        the name of every stamp above the final minSeq that carries the id."""
         long_id = "server" if long_id is None else long_id
         i = self.client_ids.get(long_id)
         if i is None:
             i = len(self.client_names)
-            if i > MAX_CLIENTS:
-                raise UnsupportedOp(f"more than {MAX_CLIENTS} clients in one document")
+            if i >= RECYCLE_FROM:
+                for j in range(1, len(self.client_names)):
+                    st = self.last_stamp[j]
+                    if st is None or st <= self.min_seq:
+                        del self.client_ids[self.client_names[j]]
+                        self.client_names[j] = long_id
+                        self.last_stamp[j] = None
+                        i = j
+                        break
+            if i == len(self.client_names):
+                if i > MAX_CLIENTS:
+                    raise UnsupportedOp(f"more than {MAX_CLIENTS} clients with stamps above minSeq in one document")
+                self.client_names.append(long_id)
+                self.last_stamp.append(None)
             self.client_ids[long_id] = i
-            self.client_names.append(long_id)
+        if seq is not None and (self.last_stamp[i] is None or seq > self.last_stamp[i]):
+            self.last_stamp[i] = seq
         return i
 
     def add_message(self, msg: dict) -> None:
         """Append one ISequencedDocumentMessage (type "op") with merge-tree contents."""
-        client = self.short_client(msg.get("clientId"))
         seq = int(msg["sequenceNumber"])
         ref = int(msg["referenceSequenceNumber"])
         msn = int(msg["minimumSequenceNumber"])
+        client = self.short_client(msg.get("clientId"), seq)
         contents = msg["contents"]
         members = contents["ops"] if contents["type"] == MT_GROUP else [contents]
         if not members:
@@ -313,10 +341,14 @@ class _DocBuilder:
             if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
                 rec = rec[:-1] + (rec[-1] | 1,)
             self.ops.append(rec)
+        self.min_seq = max(self.min_seq, msn)  # updateSeqNumbers after the message (client.ts:1381-1391)
 
     def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
         self._note_op(op)
         self.ops.append(self.owner._pack(op, seq, ref_seq, min_seq, client))
+        if 0 < client < len(self.last_stamp):
+            self.last_stamp[client] = max(self.last_stamp[client] or seq, seq)
+        self.min_seq = max(self.min_seq, min_seq)
 
 
 class MergeTreeStreamBuilder:
@@ -519,7 +551,10 @@ class MergeTreeStreamBuilder:
         def specs(c):
             return c["segments"] if c.get("version") == "1" else c["segmentTexts"]
 
+        seq = int(md["sequenceNumber"])
+        min_seq = int(md.get("minSequenceNumber", seq))
         d = _DocBuilder(self, observer)
+        d.min_seq = min_seq  # the loaded tree's minSeq (loadCore → MergeTree.startCollaboration)
         first = len(self.snapshot_segs)
         for ci, c in enumerate(chunks):
             for spec in specs(c):
@@ -537,8 +572,6 @@ class MergeTreeStreamBuilder:
         n_body = len(self.snapshot_segs) - first - n_header
         if n_header + n_body != md["totalSegmentCount"]:
             raise ValueError("Mismatch in totalSegmentCount")  # snapshotLoader.ts:272-275
-        seq = int(md["sequenceNumber"])
-        min_seq = int(md.get("minSequenceNumber", seq))
         self.docs.append(d)
         self.doc_init.append((0, 0))
         self.snapshots.append((first, n_header, n_body, min_seq, seq, 1))
@@ -559,7 +592,7 @@ class MergeTreeStreamBuilder:
         (opstampUtils.compare; Array.prototype.sort is stable)."""
         self.has_merge_info = True
         ins_seq = int(spec.get("seq", 0))
-        ins_client = d.short_client(spec["client"]) if spec.get("client") is not None else NON_COLLAB_CLIENT
+        ins_client = d.short_client(spec["client"], ins_seq) if spec.get("client") is not None else NON_COLLAB_CLIENT
         stamps = []
         if spec.get("removedSeq") is not None:
             ids = spec.get("removedClientIds")
@@ -567,12 +600,12 @@ class MergeTreeStreamBuilder:
                 ids = [spec["removedClient"]]
             if ids is None:
                 raise ValueError("must have removedClient ids")  # 0xaac
-            stamps += [(int(spec["removedSeq"]), d.short_client(c), 0) for c in ids]
+            stamps += [(int(spec["removedSeq"]), d.short_client(c, int(spec["removedSeq"])), 0) for c in ids]
         if spec.get("movedSeq") is not None:
             seqs, ids = spec.get("movedSeqs"), spec.get("movedClientIds")
             if seqs is None or ids is None or len(seqs) != len(ids):
                 raise ValueError("must have movedIds ids")  # 0xaa5 / 0xb5f
-            stamps += [(int(s), d.short_client(c), 1) for s, c in zip(seqs, ids)]
+            stamps += [(int(s), d.short_client(c, int(s)), 1) for s, c in zip(seqs, ids)]
         stamps.sort(key=lambda x: x[0])
         first = len(self.snapshot_stamps)
         self.snapshot_stamps += [(s, c, k, 0) for s, c, k in stamps]

@@ -405,6 +405,32 @@ int orc_map_replay(const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, 
   return status.load();
 }
 
+// The sparse path's oracle (any key pool): per document its live entries in Map order, written at
+// the document's op offset (entries[offs[d] ..], counts[d] of them) as fmt_map_entry does on the GPU
+// before packing.
+int orc_map_replay_sparse(const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, uint32_t keyBound,
+                          uint32_t* counts, fmt_map_entry* entries, uint32_t nThreads, double* seconds) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::atomic<int> status{FMT_OK};
+  parallelFor(0, nDocs, nThreads, [&](uint32_t d) {
+    orc::MapState m(keyBound, true);
+    for (uint64_t i = offs[d]; i < offs[d + 1]; i++) {
+      const fmt_map_op& op = ops[i];
+      const uint32_t kind = op.kind_value >> FMT_MAP_KIND_SHIFT;
+      if (kind == FMT_MAP_CLEAR) m.clear();
+      else if (op.key >= keyBound) status = FMT_E_DATA;
+      else if (kind == FMT_MAP_DELETE) m.del(op.key);
+      else m.set(op.key, op.kind_value & FMT_MAP_VALUE_MASK, op.seq);
+    }
+    const auto es = m.entries();
+    counts[d] = static_cast<uint32_t>(es.size());
+    if (entries)
+      for (size_t j = 0; j < es.size(); j++) entries[offs[d] + j] = {es[j].key, es[j].value, es[j].birth};
+  });
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return status.load();
+}
+
 // Summary of one document: header then each blobN, NUL-separated; returns bytes needed.
 int orc_map_summary(const fmt_map_op* ops, uint64_t begin, uint64_t end, uint32_t keyBound,
                     const char* const* keys, int nKeys, const char* const* values, int nValues,

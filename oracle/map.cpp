@@ -2,30 +2,44 @@
 #include "map.hpp"
 
 #include <algorithm>
+#include <stdexcept>
 
 #include "common.hpp"
 
 namespace orc {
 
+int MapState::slotOf(uint32_t key) const {
+  if (!sparse_) return slot_.at(key);
+  if (key >= keyBound_) throw std::out_of_range("key id >= key_bound");
+  const auto it = map_.find(key);
+  return it == map_.end() ? -1 : it->second;
+}
+
+void MapState::setSlot(uint32_t key, int s) {
+  if (!sparse_) slot_[key] = s;
+  else if (s < 0) map_.erase(key);
+  else map_[key] = s;
+}
+
 void MapState::set(uint32_t key, uint32_t value, uint32_t seq) {
-  const int s = slot_.at(key);
+  const int s = slotOf(key);
   if (s >= 0 && items_[static_cast<size_t>(s)].live) {
     items_[static_cast<size_t>(s)].value = value;  // existing key keeps its position
     return;
   }
-  slot_[key] = static_cast<int>(items_.size());
+  setSlot(key, static_cast<int>(items_.size()));
   items_.push_back({key, value, seq, true});
 }
 
 void MapState::del(uint32_t key) {
-  const int s = slot_.at(key);
+  const int s = slotOf(key);
   if (s >= 0) items_[static_cast<size_t>(s)].live = false;
-  slot_[key] = -1;
+  setSlot(key, -1);
 }
 
 void MapState::clear() {
   for (auto& it : items_) {
-    if (it.live) slot_[it.key] = -1;
+    if (it.live) setSlot(it.key, -1);
     it.live = false;
   }
   items_.clear();

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../include/fmt.h"
@@ -16,7 +17,10 @@ namespace orc {
 // existing key, delete/clear drop it, a later set re-appends it (ECMAScript Map insertion order).
 class MapState {
  public:
-  explicit MapState(uint32_t keyBound) : slot_(keyBound, -1) {}
+  // sparse: key -> item index in a hash map (any key pool, the sparse path's oracle) instead of a
+  // dense table of key_bound entries
+  explicit MapState(uint32_t keyBound, bool sparse = false)
+      : slot_(sparse ? 0 : keyBound, -1), keyBound_(keyBound), sparse_(sparse) {}
   // mapKernel.ts:802-850 "set" remote branch: sequencedData.set(key, {value}).
   void set(uint32_t key, uint32_t value, uint32_t seq);
   // mapKernel.ts:761-801 "delete" remote branch: sequencedData.delete(key).
@@ -35,7 +39,12 @@ class MapState {
     uint32_t key, value, birth;
     bool live;
   };
-  std::vector<int> slot_;   // key → index in items_, -1 if absent
+  int slotOf(uint32_t key) const;
+  void setSlot(uint32_t key, int s);
+  std::vector<int> slot_;   // key → index in items_, -1 if absent (dense)
+  std::unordered_map<uint32_t, int> map_;  // the same, sparse
+  uint32_t keyBound_;
+  bool sparse_;
   std::vector<Item> items_; // append-only with tombstones; order = Map insertion order
 };
 

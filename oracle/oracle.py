@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_set_index.argtypes = [ctypes.c_int]
         L.orc_map_replay.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.c_uint32, P]
+        L.orc_map_replay_sparse.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_uint32, P]
         L.orc_map_summary.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P,
                                       ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P]
         L.orc_xsadd_uint32.argtypes = [P, ctypes.c_int, P, ctypes.c_int]
@@ -237,6 +238,26 @@ def map_replay(batch, threads=1):
     if rc != 0:
         raise OracleError("map replay failed")
     return out.reshape(batch.n_docs, batch.key_bound), secs.value
+
+
+def map_replay_sparse(batch, threads=1):
+    """Replay a MapBatch keeping only live entries (any key pool): returns (counts[n_docs], entries
+    packed in document order, each document's in Map order, seconds) — the sparse path's layout."""
+    from fluidframework_amd.native import MAP_ENTRY_DTYPE
+
+    counts = np.zeros(batch.n_docs, dtype=np.uint32)
+    ent = np.zeros(max(len(batch.ops), 1), dtype=MAP_ENTRY_DTYPE)
+    secs = ctypes.c_double(0)
+    ops = np.ascontiguousarray(batch.ops)
+    offs = np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64)
+    rc = lib().orc_map_replay_sparse(_ptr(ops), _ptr(offs), batch.n_docs, batch.key_bound, _ptr(counts), _ptr(ent),
+                                     threads, ctypes.byref(secs))
+    if rc != 0:
+        raise OracleError("map replay failed")
+    c = counts.astype(np.int64)
+    first = np.cumsum(c) - c  # packed index of each document's first entry
+    take = np.arange(int(c.sum()), dtype=np.int64) + np.repeat(offs[:-1].astype(np.int64) - first, c)
+    return counts, ent[take], secs.value
 
 
 def map_summary(batch, doc: int):

@@ -130,6 +130,45 @@ def test_map_sparse_matches_oracle(orc, engine, n_docs, n_ops, key_pool):
     assert np.array_equal(c2, counts) and np.array_equal(e2, entries)
 
 
+def _check_sparse(orc, engine, batch):
+    engine.map_load_sparse(batch)
+    engine.map_run_sparse()
+    counts, entries = engine.map_fetch_sparse()
+    wc, we, _ = orc.map_replay_sparse(batch, threads=16)
+    assert np.array_equal(counts, wc)
+    assert np.array_equal(entries, we)
+    return counts
+
+
+def test_map_sparse_m2_shape_matches_sparse_oracle(orc, engine):
+    """The benchmarked shape (1000 ops per document, keys U[0, 2^20)) on 20k documents against the
+    sparse oracle, every entry equal; and a 2^20 pool with 200-op documents (smaller tables)."""
+    counts = _check_sparse(orc, engine, workloads.map_stream(20000, 1000, key_pool=1 << 20, seed=5))
+    assert counts.sum() > 20000
+    _check_sparse(orc, engine, workloads.map_stream(5000, 200, key_pool=1 << 20, seed=6))
+
+
+def test_map_sparse_ragged_documents(orc, engine):
+    """Document lengths around every path boundary (0, 1, 63/64/65, 1023/1024/1025 — the register /
+    streaming switch — 2048, 4097 and the 16384 maximum) in one batch, small and 2^20 key pools."""
+    from fluidframework_amd.streams import MapBatch
+
+    lens = [0, 1, 63, 64, 65, 511, 512, 513, 1023, 1024, 1025, 2048, 4097, 16384, 3, 0, 1000]
+    for pool in (20, 3000, 1 << 20):
+        src = workloads.map_stream(len(lens), 16384, key_pool=pool, seed=11)
+        parts, offs = [], [0]
+        for d, n in enumerate(lens):
+            o0 = int(src.doc_op_offsets[d])
+            parts.append(src.ops[o0 : o0 + n])
+            offs.append(offs[-1] + n)
+        ops = np.concatenate(parts)
+        for d in range(len(lens)):
+            ops["doc"][offs[d] : offs[d + 1]] = d
+            if lens[d] > 2000:  # at most 2048 distinct keys per document (the table): 1900, spread over the pool
+                ops["key"][offs[d] : offs[d + 1]] = ops["key"][offs[d] : offs[d + 1]] % 1900 * max(1, pool // 2000)
+        _check_sparse(orc, engine, MapBatch(ops, np.array(offs, dtype=np.uint64), pool, src.keys, src.values))
+
+
 def test_map_sparse_limits(engine):
     """A key id >= key_bound is FMT_E_DATA; a document with more distinct keys than the table holds
     is FMT_E_CAPACITY (its count 0), the other documents unaffected."""
@@ -142,6 +181,19 @@ def test_map_sparse_limits(engine):
     with pytest.raises(native.EngineError) as ei:
         engine.map_fetch_sparse()
     assert ei.value.code == native.FMT_E_DATA
+    # one bad key id before the document's last clear is still FMT_E_DATA (the kernel skips those
+    # ops' effects, not their checks): streaming (3000 ops) and register (500 ops) documents
+    for n_ops in (3000, 500):
+        b2 = workloads.map_stream(4, n_ops, key_pool=1000, seed=44)
+        ops = b2.ops.copy()
+        ops["kind_value"][10] = 5
+        ops["key"][10] = 5000
+        ops["kind_value"][20] = 2 << 30
+        engine.map_load_sparse(MapBatch(ops, b2.doc_op_offsets, 1000, b2.keys, b2.values))
+        engine.map_run_sparse()
+        with pytest.raises(native.EngineError) as ei:
+            engine.map_fetch_sparse()
+        assert ei.value.code == native.FMT_E_DATA
     ops = src.ops.copy()
     o0, o1 = int(src.doc_op_offsets[1]), int(src.doc_op_offsets[2])
     ops["kind_value"][o0:o1] = ops["kind_value"][o0:o1] & 0x3FFFFFFF  # all sets

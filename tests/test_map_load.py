@@ -87,3 +87,19 @@ def test_split_replay_through_summary_equals_full_replay(orc):
     full, resumed = split_replay_batches(orc)
     for d in range(full.n_docs):
         assert orc.map_summary(resumed, d) == orc.map_summary(full, d), d
+
+
+@pytest.mark.parametrize("n_docs,n_ops,key_pool", [(64, 1000, 20), (32, 1000, 5000), (16, 1500, 1 << 20)])
+def test_sparse_oracle_equals_dense_oracle(orc, n_docs, n_ops, key_pool):
+    """The sparse path's oracle (hash-map key index, entries in Map order) equals the dense oracle's
+    live slots in birth order: the checker of mapSparseKernel at key pools the dense table cannot hold."""
+    batch = workloads.map_stream(n_docs, n_ops, key_pool=key_pool, seed=7)
+    exp, _ = orc.map_replay(batch, threads=4)
+    counts, entries, _ = orc.map_replay_sparse(batch, threads=4)
+    o = 0
+    for d in range(n_docs):
+        live = np.nonzero(exp["value"][d] != 0xFFFFFFFF)[0]
+        want = sorted((int(exp["birth_seq"][d][k]), int(k), int(exp["value"][d][k])) for k in live)
+        got = [(int(e["birth_seq"]), int(e["key"]), int(e["value"])) for e in entries[o : o + int(counts[d])]]
+        o += int(counts[d])
+        assert got == want, d
