@@ -86,6 +86,8 @@ def main():
     ap.add_argument("--key-pool", type=int, default=20, help="map: key ids per document (> 2560 takes the HBM-table path)")
     ap.add_argument("--no-summaries", action="store_true",
                     help="mt: skip the bulk legacy summaries of every document after the timed steps")
+    ap.add_argument("--catchup-sample", type=int, default=200,
+                    help="T1 summaries: build the catchupOps blob for this many documents (0: skip)")
     ap.add_argument("--sparse", action="store_true",
                     help="map: the sparse path (LDS hash reduce-by-key, one entry per live key; any key pool)")
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
@@ -250,7 +252,10 @@ def main():
         summaries = {"docs": docs, "summaries_per_s": docs / (total_ms / 1e3), **tm, "total_ms": total_ms,
                      "checked_vs_python": checked,
                      "what": "legacy SharedString summary (header + body chunk) of every document: extractSync "
-                             "merge on the GPU (summaryRunsKernel), JSON on host threads; catch-up ops not included"}
+                             "merge on the GPU (summaryRunsKernel), JSON on host threads; the catchupOps blob is "
+                             "the 'catchup' record"}
+        if args.catchup_sample > 0:
+            summaries["catchup"] = _bench_catchup(eng, batch, hdrs, docs, args.catchup_sample)
         log(rank, f"[bench] summaries: {summaries['summaries_per_s']:.3g}/s ({total_ms:.1f} ms: kernel "
                   f"{tm['kernel_ms']:.1f}, fetch {tm['fetch_ms']:.1f}, format {tm['format_ms']:.1f} on {tm['threads']} threads)")
     elapsed = float(stats["elapsed_s"].max())
@@ -472,6 +477,51 @@ def _check_obliterate_farms(eng, hdrs, fixtures, docs):
                        if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000)
         if text != fixtures[d][4][-1]:
             raise SystemExit(f"obliterate farm {fixtures[d][0]}: final text differs from the reference's")
+
+
+def _bench_catchup(eng, batch, hdrs, docs, sample):
+    """The legacy summary's catchupOps blob (sequence.ts:949-964, snapshotlegacy.ts:178-190) for the
+    T1 documents: one more replay of the same batch with the catch-up window's ops flagged
+    (FMT_MT_F_CATCHUP: the kernel records their delta ranges; the state must equal the timed
+    replay's), every document's ranges in one copy (fmt_mt_fetch_catchup_all), and the messages
+    rebuilt on the Python host for a sample of documents (their generated streams carry op records,
+    so each message is the single-op ISequencedDocumentMessage streams.op_messages renders)."""
+    from dataclasses import replace
+
+    import numpy as np
+
+    from fluidframework_amd import shard, streams, summary, workloads
+
+    cb = replace(batch, ops=batch.ops.copy())
+    streams.flag_catchup(cb.ops, cb.doc_op_offsets)
+    eng.mt_load(cb)
+    t = time.perf_counter()
+    eng.mt_run()
+    eng.sync()
+    replay_ms = (time.perf_counter() - t) * 1e3
+    h2 = eng.mt_headers()
+    if shard.state_checksum(h2, 0) != shard.state_checksum(hdrs, 0):
+        raise SystemExit("catch-up recording changed the replayed state")
+    t = time.perf_counter()
+    offs, ranges = eng.mt_catchup_all()
+    fetch_ms = (time.perf_counter() - t) * 1e3
+    step = max(1, docs // sample)
+    t = time.perf_counter()
+    n_docs = n_msgs = n_bytes = 0
+    for d in range(0, docs, step):
+        ms = int(h2[d]["min_seq"])
+        msgs = streams.op_messages(batch, d, ms, workloads.CLIENT_NAMES)
+        blob = summary.catchup_blob(summary.catchup_messages(msgs, ranges[int(offs[d]):int(offs[d + 1])], ms))
+        n_docs += 1
+        n_msgs += len(msgs)
+        n_bytes += len(blob.encode("utf-8")) if blob else 0
+    fmt_ms = (time.perf_counter() - t) * 1e3
+    return {"ranges": int(offs[-1]), "ranges_per_doc": float(offs[-1]) / docs, "replay_ms": replay_ms, "fetch_ms": fetch_ms,
+            "sample_docs": n_docs, "sample_messages": n_msgs, "sample_bytes": n_bytes,
+            "python_ms_per_doc": fmt_ms / max(n_docs, 1),
+            "what": "catchupOps of the same documents: the replay again with the catch-up window's ops flagged (the "
+                    "kernel records their delta ranges; state equal to the timed replay), every document's ranges in "
+                    "one fmt_mt_fetch_catchup_all copy, messages rebuilt on the Python host for a sample of documents"}
 
 
 def _issue_record(traffic):

@@ -69,6 +69,8 @@ FMT_DEV uint32_t wFirstRm(uint32_t m) { return (m >> 8) & 0xFFu; }
 constexpr uint32_t kWMetaMask = 0x1FFFFu;
 constexpr int kWGroupShift = 17;
 constexpr int kWinList = 1024;  // LDS list of one group's visible window entries (slot pass)
+constexpr int kGlCap = 2048;    // LDS list of the visible window entries of one group pass
+constexpr int kGlEntBits = 21;  // entry index bits in glEnt (the group id above them)
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));
 typedef uint32_t u32x2 __attribute__((vector_size(8)));
@@ -152,6 +154,12 @@ struct HugeLds {
   int32_t cmd[8];                // pass command from wave 0 to the helper waves (HugeDoc::PassCmd)
   uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
   int32_t wlVis[kWinList];
+  // group pass: every window entry of positive view length in the pass's perspective, (entry |
+  // group << 21, view length), kGlPerWave per wave; the slot passes of the same find read these
+  // instead of the window table (glN[w] < 0: that wave's part overflowed)
+  uint32_t glEnt[kGlCap];
+  int32_t glVis[kGlCap];
+  int32_t glN[4];
 };
 
 struct HugeInputs {
@@ -216,6 +224,7 @@ class HugeDoc {
   bool corrValid = false;    // gCorr holds the current op's perspective
   uint32_t epoch = 0;        // bumped by every change of the index (window table, slots, stable sums)
   uint32_t slotCacheG = kNone, slotCacheEpoch = 0;  // sLen / sBlk hold group slotCacheG at that epoch
+  uint32_t glEpoch = ~0u;    // the epoch whose group pass filled L->glEnt / glVis
   FMT_DEV void invalidate() {
     corrValid = false;
     epoch++;
@@ -550,9 +559,10 @@ class HugeDoc {
   struct PassCmd {
     int op, r, c;
     uint32_t g, nWin;
+    int useList;  // slot pass: take group g's entries from the group pass' LDS lists
   };
-  FMT_DEV void runPass(int op, int r, int c, uint32_t g) {
-    const PassCmd cmd{op, r, c, g, nWin};
+  FMT_DEV void runPass(int op, int r, int c, uint32_t g, int useList = 0) {
+    const PassCmd cmd{op, r, c, g, nWin, useList};
     FOR_LANES(l) {
       if (l == 0) {
         L->cmd[0] = op;
@@ -560,6 +570,7 @@ class HugeDoc {
         L->cmd[2] = c;
         L->cmd[3] = static_cast<int32_t>(g);
         L->cmd[4] = static_cast<int32_t>(nWin);
+        L->cmd[5] = useList;
       }
     }
     waveSync();
@@ -585,7 +596,7 @@ class HugeDoc {
     for (;;) {
       groupBarrier();
       const PassCmd cmd{uni(L->cmd[0]), uni(L->cmd[1]), uni(L->cmd[2]), static_cast<uint32_t>(uni(L->cmd[3])),
-                        static_cast<uint32_t>(uni(L->cmd[4]))};
+                        static_cast<uint32_t>(uni(L->cmd[4])), uni(L->cmd[5])};
       if (cmd.op == kCmdExit) return;
       if (cmd.op == kCmdSlots) {
         slotShare(cmd, wave);
@@ -651,6 +662,7 @@ class HugeDoc {
   // to sLen[slot of its block] — those entries are first listed in this wave's part of the LDS list,
   // then their blocks' slots are loaded for the whole list at once.
   static constexpr int kPassU = 16;
+  static constexpr int kGlPerWave = kGlCap / kWaves;
   FMT_DEV void windowShare(const PassCmd& cmd, int wave) {
     const int r = cmd.r, c = cmd.c;
     const uint32_t n = cmd.nWin;
@@ -659,6 +671,40 @@ class HugeDoc {
     uint32_t* lEnt = L->wlEnt + wave * kListPerWave;
     int32_t* lVis = L->wlVis + wave * kListPerWave;
     int nList = 0;
+    if (bySlot && cmd.useList) {  // group g's visible entries, from this wave's group-pass list
+      const int gn = L->glN[wave];
+      const uint32_t* gE = L->glEnt + wave * kGlPerWave;
+      const int32_t* gV = L->glVis + wave * kGlPerWave;
+      for (int base = 0; base < gn; base += 64) {
+        Lane<bool> hit;
+        Lane<uint32_t> ent;
+        FOR_LANES(l) {
+          const uint32_t e = base + l < gn ? gE[base + l] : kNone;
+          LANE(ent) = e;
+          LANE(hit) = base + l < gn && (e >> kGlEntBits) == only;
+        }
+        const uint64_t m = ballot(hit);
+        if (!m) continue;
+        if (nList + 64 > kListPerWave) {
+          flushSlotList(lEnt, lVis, nList);
+          nList = 0;
+        }
+        FOR_LANES(l) {
+          if ((m >> l) & 1ull) {
+            const int at = nList + __builtin_popcountll(m & ((1ull << l) - 1));
+            lEnt[at] = LANE(ent) & ((1u << kGlEntBits) - 1);
+            lVis[at] = gV[base + l];
+          }
+        }
+        nList += __builtin_popcountll(m);
+      }
+      if (nList) flushSlotList(lEnt, lVis, nList);
+      waveSync();
+      return;
+    }
+    int glN = 0;  // group pass: this wave's list of visible entries
+    uint32_t* gE = L->glEnt + wave * kGlPerWave;
+    int32_t* gV = L->glVis + wave * kGlPerWave;
     // 64-record pieces dealt round-robin to the waves: piece (u * kWaves + wave) of each step
     for (uint32_t base = 0; base < n; base += kWaves * 64 * kPassU) {
       Lane<u32x4> rec[kPassU];
@@ -696,6 +742,28 @@ class HugeDoc {
           LANE(vis[u]) = v;
         }
       }
+      if (!bySlot && glN >= 0) {
+#pragma unroll
+        for (int u = 0; u < kPassU; u++) {
+          Lane<bool> hit;
+          FOR_LANES(l) { LANE(hit) = u < nu && LANE(vis[u]) != 0; }
+          const uint64_t m = ballot(hit);
+          if (!m || glN < 0) continue;
+          if (glN + __builtin_popcountll(m) > kGlPerWave || base + static_cast<uint32_t>((u * kWaves + wave + 1) * 64) > (1u << kGlEntBits)) {
+            glN = -1;
+            continue;
+          }
+          FOR_LANES(l) {
+            if ((m >> l) & 1ull) {
+              const int at = glN + __builtin_popcountll(m & ((1ull << l) - 1));
+              const uint32_t w = base + static_cast<uint32_t>(u * kWaves + wave) * 64 + l;
+              gE[at] = w | ((LANE(rec[u])[3] >> kWGroupShift) << kGlEntBits);
+              gV[at] = static_cast<int32_t>(LANE(vis[u]));
+            }
+          }
+          glN += __builtin_popcountll(m);
+        }
+      }
       if (bySlot) {
 #pragma unroll
         for (int u = 0; u < kPassU; u++) {
@@ -719,6 +787,11 @@ class HugeDoc {
       }
     }
     if (bySlot && nList) flushSlotList(lEnt, lVis, nList);
+    if (!bySlot) {
+      FOR_LANES(l) {
+        if (l == 0) L->glN[wave] = glN;
+      }
+    }
     waveSync();
   }
   // sLen[slot of the block of listed entry i] += its view length, for the n listed entries.
@@ -743,6 +816,7 @@ class HugeDoc {
     prof[19] += static_cast<uint64_t>(nGroups);
     runPass(kCmdGroups, r, c, kNone);
     corrValid = true;
+    glEpoch = epoch;
   }
 
   // View length of the groups at positions [k0, k0 + 64) (lane l: position k0 + l; 0 past the end).
@@ -776,7 +850,9 @@ class HugeDoc {
     slotCacheEpoch = epoch;
     ProfScope ps_(prof[2]);
     prof[17]++;
-    runPass(kCmdSlots, r, c, g);
+    bool lists = corrValid && glEpoch == epoch;
+    for (int w = 0; w < kWaves && lists; w++) lists = uni(L->glN[w]) >= 0;
+    runPass(kCmdSlots, r, c, g, lists ? 1 : 0);
   }
 
   // ------------------------------------------------------------------ the hierarchical search
@@ -791,19 +867,49 @@ class HugeDoc {
     // stopping at the chunk that holds it)
     int k = -1, base = 0;
     {
+      // two levels: lane l sums the groups at positions [l*C, l*C + C) (C = ceil(nGroups / 64)), one
+      // wave scan finds the first run whose end reaches p, a second scans that run's groups
       ProfScope psScan_(prof[21]);
-      for (int k0 = 0; k0 < nGroups && k < 0; k0 += 64) {
-        const Lane<uint32_t> len = groupLens(k0);
-        uint32_t tot;
-        const Lane<uint32_t> ex = waveExclusiveSum(len, &tot);
-        Lane<bool> q;
-        FOR_LANES(l) { LANE(q) = k0 + l < nGroups && base + static_cast<int>(LANE(ex) + LANE(len)) >= p; }
-        const uint64_t m = ballot(q);
-        if (m) {
-          k = k0 + ctz64(m);
-          base += static_cast<int>(readlane(ex, ctz64(m)));
-        } else {
-          base += static_cast<int>(tot);
+      const int C = (nGroups + 63) / 64;
+      Lane<uint32_t> run;
+      FOR_LANES(l) {
+        uint32_t x = 0;
+        for (int j = 0; j < C; j++) {
+          const int kk = l * C + j;
+          if (kk < nGroups) {
+            const uint32_t g = L->gOrder[kk];
+            x += static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
+          }
+        }
+        LANE(run) = x;
+      }
+      uint32_t tot;
+      const Lane<uint32_t> ex = waveExclusiveSum(run, &tot);
+      Lane<bool> q;
+      FOR_LANES(l) { LANE(q) = l * C < nGroups && static_cast<int>(LANE(ex) + LANE(run)) >= p; }
+      const uint64_t m = ballot(q);
+      if (m) {
+        const int lr = ctz64(m);
+        base = static_cast<int>(readlane(ex, lr));
+        const int k0 = lr * C;
+        Lane<uint32_t> len;
+        FOR_LANES(l) {
+          const int kk = k0 + l;
+          uint32_t x = 0;
+          if (l < C && kk < nGroups) {
+            const uint32_t g = L->gOrder[kk];
+            x = static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
+          }
+          LANE(len) = x;
+        }
+        uint32_t t2;
+        const Lane<uint32_t> ex2 = waveExclusiveSum(len, &t2);
+        Lane<bool> q2;
+        FOR_LANES(l) { LANE(q2) = l < C && k0 + l < nGroups && base + static_cast<int>(LANE(ex2) + LANE(len)) >= p; }
+        const uint64_t m2 = ballot(q2);
+        if (m2) {  // (always: the run's end reaches p)
+          k = k0 + ctz64(m2);
+          base += static_cast<int>(readlane(ex2, ctz64(m2)));
         }
       }
     }

@@ -1290,6 +1290,34 @@ int fmt_mt_fetch_catchup(fmt_ctx* c, uint32_t doc, fmt_mt_catchup_range* out, ui
   return FMT_OK;
 }
 
+int fmt_mt_fetch_catchup_all(fmt_ctx* c, uint64_t* offsets, fmt_mt_catchup_range* out, uint64_t cap) {
+  if (c == nullptr || !c->mtLoaded || offsets == nullptr)
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_catchup_all: bad arguments");
+  FMT_HIP(c, hipSetDevice(c->device));
+  const uint32_t nd = c->mtDocs;
+  offsets[0] = 0;
+  if (!c->mtHasCatchup) {
+    for (uint32_t d = 0; d < nd; d++) offsets[d + 1] = 0;
+    return FMT_OK;
+  }
+  std::vector<fmt_mt_doc_result> hdr(nd);
+  FMT_HIP(c, hipMemcpy(hdr.data(), c->mtHdr.p, nd * sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost));
+  for (uint32_t d = 0; d < nd; d++) {
+    const uint64_t slab = c->mtCuOffsHost[d + 1] - c->mtCuOffsHost[d];
+    offsets[d + 1] = offsets[d] + std::min<uint64_t>(hdr[d].n_catchup, slab);
+  }
+  if (out == nullptr) return FMT_OK;
+  if (cap < offsets[nd]) return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_catchup_all: cap below the ranges recorded");
+  // one copy of the whole slab region, then each document's recorded prefix packed on the host
+  std::vector<fmt_mt_catchup_range> slab(c->mtCuOffsHost[nd] ? c->mtCuOffsHost[nd] : 1);
+  if (c->mtCuOffsHost[nd])
+    FMT_HIP(c, hipMemcpy(slab.data(), c->mtCatchup.p, c->mtCuOffsHost[nd] * sizeof(fmt_mt_catchup_range), hipMemcpyDeviceToHost));
+  for (uint32_t d = 0; d < nd; d++)
+    if (offsets[d + 1] > offsets[d])
+      std::memcpy(out + offsets[d], slab.data() + c->mtCuOffsHost[d], (offsets[d + 1] - offsets[d]) * sizeof(fmt_mt_catchup_range));
+  return FMT_OK;
+}
+
 int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out, uint32_t cap) {
   if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
     return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_remove_order: bad arguments");

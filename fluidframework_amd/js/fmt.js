@@ -946,12 +946,38 @@ class MergeTreeReplay {
 	 */
 	async summarizeAllLegacy(options) {
 		const o = options || {};
-		return native().summarizeLegacy(this.engine.ctx, this.batch.keys.map((k) => JSON.stringify(k)), this.batch.values,
+		const t = await native().summarizeLegacy(this.engine.ctx, this.batch.keys.map((k) => JSON.stringify(k)), this.batch.values,
 			o.chunkSize || 10000, o.threads || 0);
+		// the catchupOps blobs (snapshotlegacy.ts:178-190): every document's catch-up ranges in one copy
+		// (fmt_mt_fetch_catchup_all), messages rebuilt here from the kept messages
+		this.bulkCatchup = null;
+		if (this.batch.messages && this.batch.messages.some((m) => m && m.length)) {
+			const t0 = Date.now();
+			const all = native().fetchCatchupAll(this.engine.ctx, this.batch.nDocs);
+			this.bulkCatchup = { offsets: all.offsets, dv: new DataView(all.ranges) };
+			t.catchupFetchMs = Date.now() - t0;
+		}
+		return t;
 	}
-	/** {header, body?} of document doc from the last summarizeAllLegacy (throws with its status). */
+	/**
+	 * {header, body?, catchupOps?} of document doc from the last summarizeAllLegacy (throws with its
+	 * status). catchupOps needs a batch built with keepMessages and finish({catchup: true}).
+	 */
 	legacyBlobs(doc) {
-		return native().summaryBlobs(this.engine.ctx, doc);
+		const out = native().summaryBlobs(this.engine.ctx, doc);
+		const msgs = this.batch.messages && this.batch.messages[doc];
+		if (this.bulkCatchup && msgs && msgs.length) {
+			const { offsets, dv } = this.bulkCatchup;
+			const ranges = [];
+			for (let i = offsets[doc]; i < offsets[doc + 1]; i++) {
+				const o = i * CATCHUP_BYTES;
+				ranges.push({ op: dv.getUint32(o, true), pos1: dv.getInt32(o + 4, true), pos2: dv.getInt32(o + 8, true),
+					type: dv.getUint32(o + 12, true) });
+			}
+			const cu = summary.catchupMessages(msgs, ranges, this.header(doc).minSeq);
+			if (cu.length) out.catchupOps = JSON.stringify(cu);
+		}
+		return out;
 	}
 	/** MergeTreeTextHelper.getText from the local perspective (MergeTreeTextHelper.ts:28-87). */
 	getText(doc) {

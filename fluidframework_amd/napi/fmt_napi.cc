@@ -18,6 +18,7 @@
 //   replayMergeTree(ctx, batch) -> Promise<ArrayBuffer headers>     fmt_mt_load + fmt_mt_run + fetch
 //   fetchDoc(ctx, doc, nLeaves, nChars, nProps) -> {leaves, chars, props}   fmt_mt_fetch_doc
 //   fetchCatchup(ctx, doc, n) -> ArrayBuffer                         fmt_mt_fetch_catchup
+//   fetchCatchupAll(ctx, nDocs) -> {offsets, ranges}                 fmt_mt_fetch_catchup_all
 //   fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer                     fmt_mt_fetch_remove_order
 //   fetchNumbers(ctx, doc) -> Float64Array                           fmt_mt_fetch_numbers
 //   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
@@ -694,6 +695,43 @@ napi_value FetchCatchup(napi_env env, napi_callback_info info) {
   return ab;
 }
 
+// fetchCatchupAll(ctx, nDocs) -> {offsets: Float64Array(nDocs + 1), ranges: ArrayBuffer}
+// (fmt_mt_fetch_catchup_all; nDocs = the loaded batch's document count)
+napi_value FetchCatchupAll(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  uint32_t nd;
+  if (argc < 2 || !get_ctx(env, argv[0], &c) || !get_u32(env, argv[1], "nDocs", &nd)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchCatchupAll: a replay is running on this context");
+    return nullptr;
+  }
+  std::vector<uint64_t> offs(size_t(nd) + 1);
+  int rc = fmt_mt_fetch_catchup_all(c->ctx, offs.data(), nullptr, 0);
+  void* p = nullptr;
+  napi_value ab;
+  if (rc == FMT_OK) {
+    CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(offs[nd]) * sizeof(fmt_mt_catchup_range), &p, &ab));
+    rc = fmt_mt_fetch_catchup_all(c->ctx, offs.data(), static_cast<fmt_mt_catchup_range*>(p), offs[nd]);
+  }
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  void* q;
+  napi_value ob, oa;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, (size_t(nd) + 1) * sizeof(double), &q, &ob));
+  for (size_t d = 0; d <= nd; d++) static_cast<double*>(q)[d] = static_cast<double>(offs[d]);
+  CHECK_NAPI(env, napi_create_typedarray(env, napi_float64_array, size_t(nd) + 1, ob, 0, &oa));
+  napi_value o;
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "offsets", oa);
+  napi_set_named_property(env, o, "ranges", ab);
+  return o;
+}
+
 // fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer of n fmt_mt_remove_order records (SnapshotV1)
 napi_value FetchRemoveOrder(napi_env env, napi_callback_info info) {
   size_t argc = 3;
@@ -756,6 +794,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"replayMap", nullptr, ReplayMap, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchDoc", nullptr, FetchDoc, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchCatchup", nullptr, FetchCatchup, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchCatchupAll", nullptr, FetchCatchupAll, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchRemoveOrder", nullptr, FetchRemoveOrder, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchNumbers", nullptr, FetchNumbers, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"replayMapSparse", nullptr, ReplayMapSparse, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

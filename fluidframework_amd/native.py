@@ -220,6 +220,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_headers.argtypes = [P, P]
         L.fmt_mt_fetch_doc.argtypes = [P, U32, P, U32, P, U32, P, U32]
         L.fmt_mt_fetch_catchup.argtypes = [P, U32, P, U32]
+        L.fmt_mt_fetch_catchup_all.argtypes = [P, P, P, U64]
         L.fmt_mt_fetch_remove_order.argtypes = [P, U32, P, U32]
         L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
@@ -233,7 +234,7 @@ EXPORTED_SYMBOLS = [
     "fmt_map_load_sparse", "fmt_map_run_sparse", "fmt_map_fetch_sparse",
     "fmt_mt_summarize_legacy", "fmt_mt_summary_blobs",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
-    "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
+    "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
 ]
 
 
@@ -417,3 +418,12 @@ class Engine:
         out = np.zeros(max(n, 1), dtype=CATCHUP_DTYPE)
         self._check(self.L.fmt_mt_fetch_catchup(self.h, doc, _ptr(out), n))
         return out[:n]
+
+    def mt_catchup_all(self):
+        """Every document's catch-up ranges in one copy (fmt_mt_fetch_catchup_all): (offsets[n_docs + 1],
+        ranges), document d's at ranges[offsets[d]:offsets[d + 1]]."""
+        offs = np.zeros(self._mt_docs + 1, dtype=np.uint64)
+        self._check(self.L.fmt_mt_fetch_catchup_all(self.h, _ptr(offs), None, 0))
+        out = np.zeros(max(int(offs[-1]), 1), dtype=CATCHUP_DTYPE)
+        self._check(self.L.fmt_mt_fetch_catchup_all(self.h, _ptr(offs), _ptr(out), int(offs[-1])))
+        return offs, out[: int(offs[-1])]

@@ -672,14 +672,45 @@ def flag_catchup(ops: np.ndarray, offs: np.ndarray) -> None:
     summary's catch-up blob with regenerated contents: seq above the document's final minSeq
     (processMinSequenceNumberChanged at summarize, sequence.ts:949-963, 1008-1018) and
     refSeq != seq - 1 (needsTransformation, sequence.ts:978)."""
-    for d in range(len(offs) - 1):
-        a, b = int(offs[d]), int(offs[d + 1])
-        if a == b:
-            continue
-        seg = ops[a:b]
-        final_msn = int(seg["min_seq"][-1])
-        sel = (seg["seq"] > final_msn) & (seg["ref_seq"] != seg["seq"] - 1)
-        seg["flags"][sel] |= MT_F_CATCHUP
+    offs = np.asarray(offs, dtype=np.int64)
+    n = np.diff(offs)
+    if not len(ops):
+        return
+    last = np.maximum(offs[1:] - 1, 0)
+    final_msn = np.repeat(ops["min_seq"][last], n)  # each op's document's final minSeq
+    sel = (ops["seq"] > final_msn) & (ops["ref_seq"] != ops["seq"] - 1)
+    ops["flags"][sel] |= MT_F_CATCHUP
+
+
+def op_messages(batch, d: int, above_seq: int, names) -> list:
+    """[(message, first op, 1)] for the ops of document d with seq > above_seq, as the
+    ISequencedDocumentMessage a single-op-per-message stream (the generated farms) carries:
+    {clientId, sequenceNumber, referenceSequenceNumber, minimumSequenceNumber, type, contents} with the
+    op rebuilt from its record (insert text / {text, props}, remove, annotate props). The catch-up
+    window of a generated document, for the legacy summary's catchupOps blob."""
+    a, b = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+    recs = batch.ops[a:b]
+    out = []
+    for k in np.nonzero(recs["seq"] > above_seq)[0]:
+        r = recs[int(k)]
+        t = int(r["type"])
+        if int(r["flags"]) & MT_F_GROUP_CONT:
+            raise UnsupportedOp("GROUP messages need the original messages")
+        if t == MT_INSERT:
+            off, ln = int(r["payload"]), int(r["len"])
+            op = {"pos1": int(r["pos1"]), "seg": batch.text[off : off + ln].tobytes().decode("utf-16-le", "surrogatepass"),
+                  "type": t}
+        elif t == MT_ANNOTATE:
+            pid = int(r["payload"])
+            kv = batch.props_kv[int(batch.props_off[pid]) : int(batch.props_off[pid + 1])]
+            op = {"pos1": int(r["pos1"]), "pos2": int(r["pos2"]),
+                  "props": {batch.keys[int(x) >> 16]: json.loads(batch.values[int(x) & 0xFFFF]) for x in kv}, "type": t}
+        else:
+            op = {"pos1": int(r["pos1"]), "pos2": int(r["pos2"]), "type": t}
+        out.append(({"clientId": names[int(r["client"])], "sequenceNumber": int(r["seq"]),
+                     "referenceSequenceNumber": int(r["ref_seq"]), "minimumSequenceNumber": int(r["min_seq"]),
+                     "type": "op", "contents": op}, int(k), 1))
+    return out
 
 
 def flag_remove_order(ops: np.ndarray, offs: np.ndarray) -> None:

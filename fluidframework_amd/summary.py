@@ -388,6 +388,20 @@ def catchup_blob(msgs):
     return js_json(msgs)
 
 
+def bulk_catchup_blobs(messages, min_seqs, offsets, ranges):
+    """The catchupOps blob (or None) of every document from one bulk fetch of the catch-up ranges
+    (Engine.mt_catchup_all: offsets[n_docs + 1], ranges): what summarizeMergeTree emits for each
+    string (sequence.ts:949-964, snapshotlegacy.ts:178-190). messages[d]: the batch's kept messages."""
+    out = []
+    for d, msgs in enumerate(messages):
+        if not msgs:
+            out.append(None)
+            continue
+        r = ranges[int(offsets[d]) : int(offsets[d + 1])]
+        out.append(catchup_blob(catchup_messages(msgs, r, int(min_seqs[d]))))
+    return out
+
+
 def summary_tree(header_blob, body_blob, catchup=None):
     """convertSummaryTreeToITree shape of SharedString.summarizeCore's content subtree (blobs in
     SnapshotLegacy.emit order: header, body, catchupOps)."""

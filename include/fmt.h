@@ -461,6 +461,12 @@ int fmt_mt_fetch_doc(fmt_ctx* ctx, uint32_t doc, fmt_mt_leaf* leaves, uint32_t c
  * messagesSinceMSNChange contents SharedSegmentSequence stashes for the legacy summary's catchupOps
  * blob (sequence.ts:949-1018, snapshotlegacy.ts:178-190). */
 int fmt_mt_fetch_catchup(fmt_ctx* ctx, uint32_t doc, fmt_mt_catchup_range* out, uint32_t cap);
+/* Every document's catch-up ranges in one device -> host copy, for the bulk summary path (what
+ * summarizeMergeTree hands SnapshotLegacy for each string, sequence.ts:949-964, emitted as the
+ * catchupOps blob, snapshotlegacy.ts:178-190): offsets[n_docs + 1] (packed prefix of the headers'
+ * n_catchup) and, when out is not NULL, the ranges of document d at out[offsets[d] .. offsets[d+1]).
+ * FMT_E_USAGE when cap < offsets[n_docs]. */
+int fmt_mt_fetch_catchup_all(fmt_ctx* ctx, uint64_t* offsets, fmt_mt_catchup_range* out, uint64_t cap);
 /* One document's remove-order entries (header n_rm_order entries, at most cap), in recording order:
  * with the first remover they give SnapshotV1's removedClientIds (snapshotV1.ts:235-250). */
 int fmt_mt_fetch_remove_order(fmt_ctx* ctx, uint32_t doc, fmt_mt_remove_order* out, uint32_t cap);

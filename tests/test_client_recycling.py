@@ -143,3 +143,37 @@ def test_js_packer_recycles_like_python(tmp_path):
     out = json.loads(r.stdout)
     assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
     assert out["clients"] == py.clients
+
+
+@pytest.mark.gpu
+def test_recycled_churn_farm_on_gpu(orc):
+    """On the GPU: 500+ clientIds per document recycled into <= 31 short ids replay in the compact /
+    small tiers only (two launches, no large-tier pass), engine == oracle bit for bit, and the V1
+    summaries from GPU state name the same clients as the oracle's (plain and remove-order batches)."""
+    from fluidframework_amd import native
+
+    orig, chd, counts = churned_farm(n_docs=16, ops_per_doc=3000, seed=5, remove_order=False)
+    assert min(counts) >= 500
+    _, chd_rm, _ = churned_farm(n_docs=16, ops_per_doc=3000, seed=5, remove_order=True)
+    eng = native.Engine(0)
+    try:
+        for batch, rm in ((chd, False), (chd_rm, True)):
+            eng.mt_load(batch)
+            eng.mt_run()
+            hdrs = eng.mt_headers()
+            assert (hdrs["status"] == 0).all()
+            if not rm:
+                assert eng.stats().launches == 2  # compact tier + small tier, no large-tier replay
+            oh, ol, oc, op = _oracle(orc, batch)
+            for d in range(batch.n_docs):
+                lv, ch, pr = eng.mt_doc(d, hdrs[d])
+                assert not compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], lv, ch, pr)), d
+                if rm:
+                    o0, o1 = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+                    got = summary.removers_from_engine(lv, int(hdrs[d]["n_leaves"]), eng.mt_remove_order(d, hdrs[d]),
+                                                       batch.ops[o0:o1])
+                    want = orc.mt_removers(batch, d)
+                    assert summary.v1_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values, batch.clients[d], got) == \
+                        summary.v1_summary(oh[d], ol[d], oc[d], op[d], batch.keys, batch.values, batch.clients[d], want), d
+    finally:
+        eng.close()

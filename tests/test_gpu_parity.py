@@ -205,6 +205,35 @@ def test_map_sparse_limits(engine):
     assert ei.value.code == native.FMT_E_CAPACITY
 
 
+def test_mt_bulk_summaries_with_catchup_match_per_document_path(orc, engine):
+    """The bulk summary path with catch-up: fmt_mt_summarize_legacy's header/body plus the catchupOps
+    blobs from one fmt_mt_fetch_catchup_all copy equal, for every reference replay fixture, the
+    per-document path (fetch_doc + Python legacy_summary + fetch_catchup) and the oracle's ranges."""
+    from fluidframework_amd import summary
+    from test_catchup import fixture_batch
+
+    batch, _ = fixture_batch()
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert (hdrs["status"] == 0).all()
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    offs, ranges = engine.mt_catchup_all()
+    blobs = summary.bulk_catchup_blobs(batch.messages, hdrs["min_seq"], offs, ranges)
+    rc, oh, _, _, _, _, ocu = orc.mt_replay_batch(batch, cap_catchup=4096)
+    assert rc == 0
+    seen = 0
+    for d in range(batch.n_docs):
+        lv, ch, pr = engine.mt_doc(d, hdrs[d])
+        assert engine.mt_summary(d) == legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values), d
+        one = engine.mt_catchup(d, hdrs[d])
+        assert np.array_equal(ranges[int(offs[d]) : int(offs[d + 1])], one), d
+        assert np.array_equal(one, ocu[d][: int(oh[d]["n_catchup"])]), d
+        assert blobs[d] == summary.catchup_blob(summary.catchup_messages(batch.messages[d], one, int(hdrs[d]["min_seq"]))), d
+        seen += blobs[d] is not None
+    assert seen > 0
+
+
 def test_map_lww_ragged_documents(orc, engine):
     """Document lengths straddle the register-held path (≤1024 ops) and the streaming path, with
     empty and one-op documents in between."""

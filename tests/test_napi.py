@@ -45,7 +45,7 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
-                               "fetchRemoveOrder", "fetchNumbers", "replayMapSparse", "summarizeLegacy",
+                               "fetchRemoveOrder", "fetchNumbers", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
                                "summaryBlobs", "replayMap", "fetchDoc", "sizes"])
     assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
                         "catchupRange": 16, "mapEntry": 12, "adjust": 32}
@@ -423,10 +423,11 @@ const out={{map:[]}};
 for(let d=0;d<64;d++) out.map.push([JSON.stringify(dense.entries(d))===JSON.stringify(sparse.entries(d)),
   JSON.stringify(dense.summarize(d))===JSON.stringify(sparse.summarize(d)), sparse.entries(d).length]);
 const fx=JSON.parse(zlib.gunzipSync(fs.readFileSync({json.dumps(GOLDEN)})).toString());
-const b=new fmt.MergeTreeStreamBuilder();
+const b=new fmt.MergeTreeStreamBuilder({{keepMessages:true}});
 for(const f of fx){{const d=b.beginDoc(f.groups[0].initialText,'A');for(const g of f.groups) for(const m of g.msgs) d.addMessage(m);}}
-const r=await e.replayMergeTree(b.finish());const t=await r.summarizeAllLegacy();out.bytes=t.bytes;out.legacy=[];
-for(let d=0;d<fx.length;d++){{const a=r.legacyBlobs(d),h=r.summarize(d);out.legacy.push(a.header===h.header&&a.body===h.body);}}
+const r=await e.replayMergeTree(b.finish({{catchup:true}}));const t=await r.summarizeAllLegacy();out.bytes=t.bytes;out.legacy=[];out.cu=0;
+for(let d=0;d<fx.length;d++){{const a=r.legacyBlobs(d),h=r.summarize(d);out.cu+=a.catchupOps!==undefined;
+ out.legacy.push(a.header===h.header&&a.body===h.body&&a.catchupOps===h.catchupOps);}}
 e.close();process.stdout.write(JSON.stringify(out));}})().catch((e)=>{{console.error(e);process.exit(1);}});"""
     script = tmp_path / "sparse_bulk.js"
     script.write_text(js)
@@ -434,4 +435,4 @@ e.close();process.stdout.write(JSON.stringify(out));}})().catch((e)=>{{console.e
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert all(a and b for a, b, _ in out["map"]) and sum(n for _, _, n in out["map"]) > 1000
-    assert out["bytes"] > 0 and all(out["legacy"])
+    assert out["bytes"] > 0 and all(out["legacy"]) and out["cu"] > 0  # catchupOps from the bulk copy too
