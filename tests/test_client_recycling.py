@@ -152,9 +152,9 @@ def test_recycled_churn_farm_on_gpu(orc):
     summaries from GPU state name the same clients as the oracle's (plain and remove-order batches)."""
     from fluidframework_amd import native
 
-    orig, chd, counts = churned_farm(n_docs=16, ops_per_doc=3000, seed=5, remove_order=False)
+    orig, chd, counts = churned_farm(n_docs=16, ops_per_doc=3500, seed=5, remove_order=False)
     assert min(counts) >= 500
-    _, chd_rm, _ = churned_farm(n_docs=16, ops_per_doc=3000, seed=5, remove_order=True)
+    _, chd_rm, _ = churned_farm(n_docs=16, ops_per_doc=3500, seed=5, remove_order=True)
     eng = native.Engine(0)
     try:
         for batch, rm in ((chd, False), (chd_rm, True)):
