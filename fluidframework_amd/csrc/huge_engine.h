@@ -171,6 +171,10 @@ struct HugeInputs {
   const fmt_mt_snapshot_seg* segs;  // loaded header chunk
   uint32_t nSegs;
   int32_t snapMinSeq, snapSeq;
+  // client of the loaded segments' insert stamp: FMT_NON_COLLAB_CLIENT for a summary's segments
+  // (specToSegment, snapshotLoader.ts:180-186), FMT_LOCAL_CLIENT for a document's initial text (the
+  // replay harness inserts it locally before collaborating, client.replay.spec.ts:30-33)
+  int32_t initClient;
 };
 
 // A leaf found by the hierarchical search.
@@ -1439,9 +1443,20 @@ class HugeDoc {
         fail(FMT_E_DATA);
         return;
       }
-      if (lastBlk == kNone) {  // empty document: the empty root becomes a leaf block
-        fail(FMT_E_UNSUPPORTED);
-        return;
+      if (lastBlk == kNone) {
+        // empty document: the root, childless, takes the segment (insertRecursive's `_pos === 0`
+        // leaf, mergeTree.ts:1935-1943) and becomes a leaf block, the first slot of the first group
+        const uint32_t rb = static_cast<uint32_t>(root);
+        if (ldu(S.bCount + rb) != 0 || L->gCount[L->gOrder[0]] != 0) {
+          fail(FMT_E_DATA);
+          return;
+        }
+        FOR_LANES(l) {
+          if (l == 0) S.bLeaf[rb] = 1;
+        }
+        waveSync();
+        if (!slotInsert(L->gOrder[0], 0, rb, 0)) return;
+        lastBlk = rb;
       }
       b = lastBlk;
       k = -1;
@@ -2199,8 +2214,35 @@ class HugeDoc {
     ProfScope ps_(prof[5]);
     const uint32_t N = in.nSegs;
     const uint32_t nLeafBlk = (N + 6) / 7;
-    if (N == 0 || nLeafBlk > S.blockCap || N + 1 > S.idCap) {
-      fail(N == 0 ? FMT_E_UNSUPPORTED : FMT_E_CAPACITY);
+    if (N == 0) {  // an empty document: the root block alone, no leaf block listed yet (insertText)
+      if (S.blockCap < 1) {
+        fail(FMT_E_CAPACITY);
+        return;
+      }
+      FOR_LANES(l) {
+        if (l == 0) {
+          S.bCount[0] = 0;
+          S.bLeaf[0] = 0;
+          S.bScour[0] = -1;
+          S.bParent[0] = kNone;
+        }
+      }
+      L->gOrder[0] = 0;
+      L->gStable[0] = 0;
+      L->gCount[0] = 0;
+      L->gCorr[0] = 0;
+      waveSync();
+      nGroups = 1;
+      root = 0;
+      nextBlock = 1;
+      nextId = 1;
+      lastBlk = kNone;
+      minSeq = in.snapMinSeq;
+      curSeq = in.snapSeq;
+      return;
+    }
+    if (nLeafBlk > S.blockCap || N + 1 > S.idCap) {
+      fail(FMT_E_CAPACITY);
       return;
     }
     for (uint32_t base = 0; base < N; base += 64) {
@@ -2217,7 +2259,7 @@ class HugeDoc {
           S.lMhi[i] = 0;
           S.lId[i] = j + 1;
           S.lText[i] = sg.text;
-          S.lMeta[i] = mkMeta(FMT_NON_COLLAB_CLIENT, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
+          S.lMeta[i] = mkMeta(in.initClient, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
           S.leafBlk[j + 1] = b;
           S.winIdx[j + 1] = kNone;
         }

@@ -118,6 +118,21 @@ struct fmt_ctx {
   };
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
+  // documents that outgrow the large tier replay again, from their start, in the huge tier when
+  // they hold nothing it does not (mtHugeOk: no obliterate, catch-up / remove-order recording,
+  // relative positions, annotate-adjust or SnapshotV1 merge info; no body chunk); their starts
+  std::vector<uint8_t> mtHugeOk;
+  std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
+  std::vector<fmt_mt_snapshot_seg> mtStartSeg;  // per document: its initial text as one segment (len 0: none)
+  uint32_t mtHugeLoaded = 0;                 // huge documents routed at load (the rest were escalated)
+  uint32_t mtGrown = 0;                      // documents the last run escalated into the huge tier
+  uint32_t mtNPropsOps = 0;
+  std::vector<uint64_t> mtOffsHost;          // host copies of doc_op_offsets and the snapshot docs
+  std::vector<fmt_mt_snapshot_doc> mtSnapHost;
+  DevBuf<fmt_mt_snapshot_seg> mtStartSegDev;
+  DevBuf<fmt_huge::HugeState> hugeStates2;
+  DevBuf<fmt_huge::HugeInputs> hugeInputs2;
+  DevBuf<fmt_kernels::HugeOut> hugeOuts2;
   // bulk legacy summaries (fmt_mt_summarize_legacy): device runs / text, host blobs
   DevBuf<fmt_kernels::SumView> sumViews;
   DevBuf<fmt_kernels::SumRun> sumRuns;
@@ -473,6 +488,75 @@ int fmt_mt_capacity(uint32_t* maxLeaves, uint32_t* maxChars, uint32_t* maxProps)
   return FMT_OK;
 }
 
+// One huge-tier document (huge_engine.h): its HBM state sized from its op count and start, inputs
+// (ops [o0, o1) of the staged batch, nSegs start segments at segsDev) and output buffers; header d.
+// textPerOp bounds the merge area (zamboni appends build their text there).
+static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32_t d, uint64_t o0,
+                        uint64_t o1, const fmt_mt_snapshot_seg* segsDev, uint64_t N, int32_t minSeq, int32_t seq,
+                        int32_t initClient, uint64_t textPerOp, uint64_t docChars) {
+  const uint64_t nOps = o1 - o0;
+  c->mtHugeSlot[d] = static_cast<int32_t>(c->huge.size());
+  c->huge.emplace_back();
+  auto& H = c->huge.back();
+  auto alloc = [&](size_t bytes, void** out) -> hipError_t {
+    hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+    if (e == hipSuccess) H.allocs.push_back(*out);
+    return e;
+  };
+  fmt_huge::HugeState& S = H.state;
+  S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
+  S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
+  S.winCap = S.idCap;  // every leaf can be in the window (a wide remove puts many there)
+  const uint64_t textCap = std::min<uint64_t>(textLen + textPerOp * nOps + 65536, 0xFFFFFFF0ull);
+  const size_t nl = static_cast<size_t>(S.blockCap) * 8, nb = S.blockCap;
+  void* p;
+#define FMT_ALLOC(field, T, count)                        \
+  FMT_HIP(c, alloc((count) * sizeof(T), &p));              \
+  S.field = static_cast<T*>(p);
+  FMT_ALLOC(lLen, uint32_t, nl) FMT_ALLOC(lIns, int32_t, nl) FMT_ALLOC(lRm, int32_t, nl)
+  FMT_ALLOC(lMlo, uint32_t, nl) FMT_ALLOC(lMhi, uint32_t, nl) FMT_ALLOC(lId, uint32_t, nl)
+  FMT_ALLOC(lText, uint32_t, nl) FMT_ALLOC(lMeta, uint32_t, nl)
+  FMT_ALLOC(bCount, uint32_t, nb) FMT_ALLOC(bParent, uint32_t, nb) FMT_ALLOC(bLeaf, uint32_t, nb)
+  FMT_ALLOC(bScour, int32_t, nb) FMT_ALLOC(bChild, uint32_t, nb * 8) FMT_ALLOC(bGroup, uint32_t, nb)
+  FMT_ALLOC(bSlot, uint32_t, nb) FMT_ALLOC(freeBlk, uint32_t, nb)
+  FMT_ALLOC(gSlotBlk, uint32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
+  FMT_ALLOC(gSlotStable, int32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
+  FMT_ALLOC(leafBlk, uint32_t, S.idCap) FMT_ALLOC(winIdx, uint32_t, S.idCap)
+  FMT_ALLOC(wRec, uint32_t, static_cast<size_t>(S.winCap) * 4) FMT_ALLOC(wMask, uint32_t, static_cast<size_t>(S.winCap) * 2)
+  FMT_ALLOC(wBlk, uint32_t, S.winCap)
+  FMT_ALLOC(wLeaf, uint32_t, S.winCap)
+  FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * fmt_huge::kPropWords)
+#undef FMT_ALLOC
+  S.textLen = textLen;
+  S.textCap = textCap;
+  FMT_HIP(c, hipMemcpyAsync(S.text, c->mtText.p, textLen * sizeof(uint16_t), hipMemcpyDeviceToDevice, c->stream));
+  fmt_huge::HugeInputs& I = H.in;
+  I.ops = c->mtOps.p;
+  I.begin = o0;
+  I.end = o1;
+  I.propsOff = c->mtPropsOff.p;
+  I.propsKv = c->mtPropsKv.p;
+  I.nPropsOps = nPropsOps;
+  I.segs = segsDev;
+  I.nSegs = static_cast<uint32_t>(N);
+  I.snapMinSeq = minSeq;
+  I.snapSeq = seq;
+  I.initClient = initClient;
+  fmt_kernels::HugeOut& O = H.out;
+  O.header = c->mtHdr.p + d;
+  O.capLeaves = N + 3 * nOps + 8;
+  O.capChars = docChars + 8;  // (every unit the document can hold: its start plus its inserts)
+  FMT_HIP(c, alloc(O.capLeaves * sizeof(fmt_mt_leaf), &p));
+  O.leaves = static_cast<fmt_mt_leaf*>(p);
+  FMT_HIP(c, alloc(O.capChars * sizeof(uint16_t), &p));
+  O.chars = static_cast<uint16_t*>(p);
+  FMT_HIP(c, alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p));
+  O.props = static_cast<fmt_mt_propset*>(p);
+  FMT_HIP(c, alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p));
+  O.prof = static_cast<unsigned long long*>(p);
+  return FMT_OK;
+}
+
 int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   if (c == nullptr || b == nullptr || b->doc_op_offsets == nullptr || (b->n_ops && b->ops == nullptr))
     return setErr(c, FMT_E_USAGE, "fmt_mt_load: bad arguments");
@@ -715,6 +799,10 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtNOps = b->n_ops;
   c->mtDocs = n;
   c->mtTextLen = b->text_len;
+  c->mtNPropsOps = b->n_props_ops;
+  c->mtOffsHost.assign(b->doc_op_offsets, b->doc_op_offsets + n + 1);
+  if (b->snapshots) c->mtSnapHost.assign(b->snapshots, b->snapshots + n);
+  else c->mtSnapHost.clear();
   c->mtNProps = b->n_props_ops;
   c->mtHasInit = b->doc_init != nullptr;
   c->mtObliterate = obliterates;
@@ -737,6 +825,34 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     for (void* p : h.allocs) (void)hipFree(p);
   c->huge.clear();
   c->mtHugeSlot.assign(n, -1);
+  c->mtHugeOk.assign(n, 1);
+  c->mtDocChars.assign(n, 0);
+  c->mtStartSeg.assign(n, fmt_mt_snapshot_seg{0, 0, FMT_MT_NO_PROPS});
+  for (uint32_t d = 0; d < n; d++) {
+    uint8_t ok = 1;
+    uint64_t chars = 0;
+    for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+      const fmt_mt_op& op = b->ops[i];
+      if (op.type == FMT_MT_INSERT) chars += op.len;
+      if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2)) ||
+          op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED ||
+          (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
+        ok = 0;
+    }
+    if (b->snapshots && b->snapshots[d].loaded) {
+      const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+      if (sd.n_body != 0) ok = 0;
+      for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
+        chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
+      for (uint64_t k = sd.first_seg; b->snapshot_info != nullptr && k < sd.first_seg + sd.n_header; k++)
+        if (b->snapshot_info[k].ins_seq != 0 || b->snapshot_info[k].rm_count != 0) ok = 0;
+    } else if (b->doc_init && b->doc_init[2 * d + 1] > 0) {
+      c->mtStartSeg[d] = fmt_mt_snapshot_seg{b->doc_init[2 * d], b->doc_init[2 * d + 1], FMT_MT_NO_PROPS};
+      chars += b->doc_init[2 * d + 1];
+    }
+    c->mtHugeOk[d] = ok;
+    c->mtDocChars[d] = chars;
+  }
   if (b->snapshots) {
     const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true);
     for (uint32_t d = 0; d < n; d++) {
@@ -748,7 +864,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
       if (sd.n_body != 0)
         return setErr(c, FMT_E_UNSUPPORTED, "a document beyond the large tier must load from one header chunk (n_body = 0)");
-      const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1], nOps = o1 - o0;
+      const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
       if (b->snapshot_info != nullptr) {
         for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header; k++)
           if (b->snapshot_info[k].ins_seq != 0 || b->snapshot_info[k].rm_count != 0)
@@ -761,67 +877,13 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
         if (b->ops[i].type == FMT_MT_ANNOTATE && adjCount[b->ops[i].payload] > 0)
           return setErr(c, FMT_E_UNSUPPORTED, "annotate-adjust in a document beyond the large tier");
       }
-      c->mtHugeSlot[d] = static_cast<int32_t>(c->huge.size());
-      c->huge.emplace_back();
-      auto& H = c->huge.back();
-      auto alloc = [&](size_t bytes, void** out) -> hipError_t {
-        hipError_t e = hipMalloc(out, bytes ? bytes : 1);
-        if (e == hipSuccess) H.allocs.push_back(*out);
-        return e;
-      };
-      const uint64_t N = sd.n_header;
-      fmt_huge::HugeState& S = H.state;
-      S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
-      S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
-      S.winCap = S.idCap;  // every leaf can be in the window (a wide remove puts many there)
-      const uint64_t textCap = std::min<uint64_t>(b->text_len + 256 * nOps + 65536, 0xFFFFFFF0ull);
-      const size_t nl = static_cast<size_t>(S.blockCap) * 8, nb = S.blockCap;
-      void* p;
-#define FMT_ALLOC(field, T, count)                        \
-  FMT_HIP(c, alloc((count) * sizeof(T), &p));              \
-  S.field = static_cast<T*>(p);
-      FMT_ALLOC(lLen, uint32_t, nl) FMT_ALLOC(lIns, int32_t, nl) FMT_ALLOC(lRm, int32_t, nl)
-      FMT_ALLOC(lMlo, uint32_t, nl) FMT_ALLOC(lMhi, uint32_t, nl) FMT_ALLOC(lId, uint32_t, nl)
-      FMT_ALLOC(lText, uint32_t, nl) FMT_ALLOC(lMeta, uint32_t, nl)
-      FMT_ALLOC(bCount, uint32_t, nb) FMT_ALLOC(bParent, uint32_t, nb) FMT_ALLOC(bLeaf, uint32_t, nb)
-      FMT_ALLOC(bScour, int32_t, nb) FMT_ALLOC(bChild, uint32_t, nb * 8) FMT_ALLOC(bGroup, uint32_t, nb)
-      FMT_ALLOC(bSlot, uint32_t, nb) FMT_ALLOC(freeBlk, uint32_t, nb)
-      FMT_ALLOC(gSlotBlk, uint32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
-      FMT_ALLOC(gSlotStable, int32_t, static_cast<size_t>(fmt_huge::kGroupCap) * fmt_huge::kSlotCap)
-      FMT_ALLOC(leafBlk, uint32_t, S.idCap) FMT_ALLOC(winIdx, uint32_t, S.idCap)
-      FMT_ALLOC(wRec, uint32_t, static_cast<size_t>(S.winCap) * 4) FMT_ALLOC(wMask, uint32_t, static_cast<size_t>(S.winCap) * 2)
-      FMT_ALLOC(wBlk, uint32_t, S.winCap)
-      FMT_ALLOC(wLeaf, uint32_t, S.winCap)
-      FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * fmt_huge::kPropWords)
-#undef FMT_ALLOC
-      S.textLen = b->text_len;
-      S.textCap = textCap;
-      FMT_HIP(c, hipMemcpyAsync(S.text, b->text, b->text_len * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
-      fmt_huge::HugeInputs& I = H.in;
-      I.ops = c->mtOps.p;
-      I.begin = o0;
-      I.end = o1;
-      I.propsOff = c->mtPropsOff.p;
-      I.propsKv = c->mtPropsKv.p;
-      I.nPropsOps = b->n_props_ops;
-      I.segs = c->mtSnapSegs.p + sd.first_seg;
-      I.nSegs = static_cast<uint32_t>(N);
-      I.snapMinSeq = sd.min_seq;
-      I.snapSeq = sd.seq;
-      fmt_kernels::HugeOut& O = H.out;
-      O.header = c->mtHdr.p + d;
-      O.capLeaves = N + 3 * nOps + 8;
-      O.capChars = b->text_len + 8;
-      FMT_HIP(c, alloc(O.capLeaves * sizeof(fmt_mt_leaf), &p));
-      O.leaves = static_cast<fmt_mt_leaf*>(p);
-      FMT_HIP(c, alloc(O.capChars * sizeof(uint16_t), &p));
-      O.chars = static_cast<uint16_t*>(p);
-      FMT_HIP(c, alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p));
-      O.props = static_cast<fmt_mt_propset*>(p);
-      FMT_HIP(c, alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p));
-      O.prof = static_cast<unsigned long long*>(p);
+      const int rc = setupHugeDoc(c, b->text_len, b->n_props_ops, d, b->doc_op_offsets[d], b->doc_op_offsets[d + 1],
+                                  c->mtSnapSegs.p + sd.first_seg, sd.n_header, sd.min_seq, sd.seq, FMT_NON_COLLAB_CLIENT, 256,
+                                  c->mtDocChars[d]);
+      if (rc != FMT_OK) return rc;
     }
   }
+  c->mtHugeLoaded = static_cast<uint32_t>(c->huge.size());
   if (!c->huge.empty()) {
     const size_t nh = c->huge.size();
     std::vector<uint32_t> small;
@@ -882,6 +944,7 @@ int fmt_mt_run(fmt_ctx* c) {
   c->timed2 = false;
   // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
   uint32_t nEsc = 0;
+  c->mtGrown = 0;
   FMT_HIP(c, hipMemcpyAsync(&nEsc, c->mtEsc.p, sizeof nEsc, hipMemcpyDeviceToHost, c->stream));
   FMT_HIP(c, hipStreamSynchronize(c->stream));
   c->mtBigSlot.assign(c->mtDocs, -1);
@@ -903,6 +966,64 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, hipMemcpyAsync(list.data(), c->mtEsc.p + 1, nEsc * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     FMT_HIP(c, hipStreamSynchronize(c->stream));
     for (uint32_t i = 0; i < nEsc; i++) c->mtBigSlot[list[i]] = static_cast<int32_t>(i);
+    // Documents the large tier could not hold (FMT_E_CAPACITY: leaves, text, blocks, prop sets)
+    // replay again from their start in the huge tier, which has no such limit but device memory —
+    // the reference grows a tree without bound (insertSegments, mergeTree.ts:1484-1517).
+    std::vector<fmt_mt_doc_result> hb(nEsc);
+    std::vector<uint32_t> grow;
+    for (uint32_t i = 0; i < nEsc; i++) {
+      FMT_HIP(c, hipMemcpyAsync(&hb[i], c->mtHdr.p + list[i], sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost, c->stream));
+    }
+    FMT_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < nEsc; i++)
+      if (hb[i].status == FMT_E_CAPACITY && c->mtHugeOk[list[i]] && c->mtHugeSlot[list[i]] < 0) grow.push_back(list[i]);
+    // (escalated documents of an earlier run of this load are released first)
+    for (size_t h = c->mtHugeLoaded; h < c->huge.size(); h++)
+      for (void* q : c->huge[h].allocs) (void)hipFree(q);
+    for (uint32_t d = 0; d < c->mtDocs; d++)
+      if (c->mtHugeSlot[d] >= static_cast<int32_t>(c->mtHugeLoaded)) c->mtHugeSlot[d] = -1;
+    c->huge.resize(c->mtHugeLoaded);
+    if (!grow.empty()) {
+      FMT_HIP(c, c->mtStartSegDev.reserve(grow.size()));
+      std::vector<fmt_mt_snapshot_seg> starts(grow.size());
+      for (size_t i = 0; i < grow.size(); i++) starts[i] = c->mtStartSeg[grow[i]];
+      FMT_HIP(c, hipMemcpyAsync(c->mtStartSegDev.p, starts.data(), grow.size() * sizeof(fmt_mt_snapshot_seg),
+                                hipMemcpyHostToDevice, c->stream));
+      for (size_t i = 0; i < grow.size(); i++) {
+        const uint32_t d = grow[i];
+        const uint64_t o0 = c->mtOffsHost[d], o1 = c->mtOffsHost[d + 1];
+        int rc;
+        if (c->mtSnapHost.size() > d && c->mtSnapHost[d].loaded) {
+          const fmt_mt_snapshot_doc& sd = c->mtSnapHost[d];
+          rc = setupHugeDoc(c, c->mtTextLen, c->mtNPropsOps, d, o0, o1, c->mtSnapSegs.p + sd.first_seg, sd.n_header,
+                            sd.min_seq, sd.seq, FMT_NON_COLLAB_CLIENT, 1024, c->mtDocChars[d]);
+        } else {
+          rc = setupHugeDoc(c, c->mtTextLen, c->mtNPropsOps, d, o0, o1, c->mtStartSegDev.p + i, starts[i].len > 0 ? 1 : 0,
+                            0, 0, FMT_LOCAL_CLIENT, 1024, c->mtDocChars[d]);
+        }
+        if (rc != FMT_OK) return rc;
+      }
+      const size_t ng = grow.size();
+      FMT_HIP(c, c->hugeStates2.reserve(ng));
+      FMT_HIP(c, c->hugeInputs2.reserve(ng));
+      FMT_HIP(c, c->hugeOuts2.reserve(ng));
+      std::vector<fmt_huge::HugeState> hs(ng);
+      std::vector<fmt_huge::HugeInputs> hi(ng);
+      std::vector<fmt_kernels::HugeOut> ho(ng);
+      for (size_t i = 0; i < ng; i++) {
+        const auto& H = c->huge[c->mtHugeLoaded + i];
+        hs[i] = H.state;
+        hi[i] = H.in;
+        ho[i] = H.out;
+      }
+      FMT_HIP(c, hipMemcpyAsync(c->hugeStates2.p, hs.data(), ng * sizeof(fmt_huge::HugeState), hipMemcpyHostToDevice, c->stream));
+      FMT_HIP(c, hipMemcpyAsync(c->hugeInputs2.p, hi.data(), ng * sizeof(fmt_huge::HugeInputs), hipMemcpyHostToDevice, c->stream));
+      FMT_HIP(c, hipMemcpyAsync(c->hugeOuts2.p, ho.data(), ng * sizeof(fmt_kernels::HugeOut), hipMemcpyHostToDevice, c->stream));
+      FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates2.p, c->hugeInputs2.p, c->hugeOuts2.p, static_cast<uint32_t>(ng),
+                                             c->stream));
+      FMT_HIP(c, hipStreamSynchronize(c->stream));
+      c->mtGrown = static_cast<uint32_t>(ng);
+    }
   }
   c->timed = true;
   c->stats = fmt_stats{};
@@ -914,7 +1035,8 @@ int fmt_mt_run(fmt_ctx* c) {
                         (c->mtDocs + 1ull) * sizeof(uint64_t);
   c->stats.bytes_written = static_cast<uint64_t>(c->mtDocs) * sizeof(fmt_mt_doc_result);
   // compact + small tier (no remove-order recording) or small tier alone, then the large tier when it ran
-  c->stats.launches = (!c->mtHasRmOrder ? 2 : 1) + (nEsc > 0 ? 1 : 0);
+  // (+1: the huge-tier pass over documents that outgrew the large tier, after the timed events)
+  c->stats.launches = (!c->mtHasRmOrder ? 2 : 1) + (nEsc > 0 ? 1 : 0) + (c->mtGrown > 0 ? 1 : 0);
   return FMT_OK;
 }
 

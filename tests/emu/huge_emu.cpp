@@ -19,16 +19,26 @@ extern "C" {
 
 // Replays document d of the batch (a summary-loaded document, header chunk only) into the caller's
 // output arrays (fmt_mt_fetch_doc layout). Returns the document status.
+// A document that does not start from a summary starts from its initial text (one segment stamped
+// {0, FMT_LOCAL_CLIENT}) or empty, as the runtime replays documents that outgrow the large tier.
 int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
                     uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
-  const fmt_mt_snapshot_doc& sd = b->snapshots[d];
+  const bool loaded = b->snapshots != nullptr && b->snapshots[d].loaded;
+  fmt_mt_snapshot_doc sd{};
+  fmt_mt_snapshot_seg initSeg{};
+  if (loaded) sd = b->snapshots[d];
+  else if (b->doc_init != nullptr && b->doc_init[2 * d + 1] > 0) {
+    initSeg = {b->doc_init[2 * d], b->doc_init[2 * d + 1], FMT_MT_NO_PROPS};
+    sd.n_header = 1;
+  }
   const uint64_t nOps = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
   const uint32_t N = sd.n_header;
   HugeState S{};
   S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
   S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
   S.winCap = S.idCap;  // every leaf can be in the window (wide removes)
-  const uint64_t textCap = b->text_len + 256 * nOps + 65536;
+  uint64_t textCap = b->text_len + (loaded ? 256 : 1024) * nOps + 65536;  // (runtime.cpp setupHugeDoc)
+  if (const char* e = std::getenv("FMT_EMU_TEXTCAP")) textCap = std::strtoull(e, nullptr, 10);
   std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6);
   std::vector<int32_t> i32(static_cast<size_t>(S.blockCap) * 8 * 2);
   size_t o = 0, oi = 0;
@@ -66,12 +76,14 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   in.propsOff = b->props_off;
   in.propsKv = b->props_kv;
   in.nPropsOps = b->n_props_ops;
-  in.segs = b->snapshot_segs + sd.first_seg;
+  in.segs = loaded ? b->snapshot_segs + sd.first_seg : &initSeg;
   in.nSegs = N;
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
+  in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
   doc->run(in);
   doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props);
+  if (std::getenv("FMT_EMU_TEXTCAP")) std::fprintf(stderr, "textTop %llu of %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap);
   return hdr->status;
 }
 

@@ -1,10 +1,11 @@
 #!/bin/bash
-# GPU parity tests only (incl. the JavaScript driver), with a per-test time limit.
+# The GPU parity suite alone (OUTDIR under gpurun_out/), time-limited.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+OUT=gpurun_out/${OUTDIR:-tests}
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider ${K:+-k "$K"} > $OUT/pytest_gpu.log 2>&1
 rc=$?
-tail -5 gpurun_out/pytest_gpu.log
+tail -3 $OUT/pytest_gpu.log
 exit $rc
