@@ -878,12 +878,16 @@ class HugeDoc {
       Lane<uint32_t> run;
       FOR_LANES(l) {
         uint32_t x = 0;
-        for (int j = 0; j < C; j++) {
-          const int kk = l * C + j;
-          if (kk < nGroups) {
-            const uint32_t g = L->gOrder[kk];
-            x += static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
+        for (int j0 = 0; j0 < C; j0 += 8) {  // 8 group ids, then their 16 sums, in flight together
+          uint32_t g[8];
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const int kk = l * C + j0 + j;
+            g[j] = j0 + j < C && kk < nGroups ? static_cast<uint32_t>(L->gOrder[kk]) : kNone;
           }
+#pragma unroll
+          for (int j = 0; j < 8; j++)
+            if (g[j] != kNone) x += static_cast<uint32_t>(L->gStable[g[j]] + L->gCorr[g[j]]);
         }
         LANE(run) = x;
       }

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
   using Doc = fmt_mt::Doc<Ob, C, Rm, Adj>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
-  fmt_mt::Scratch<C>* scratch = reinterpret_cast<fmt_mt::Scratch<C>*>(lds + wave * scratchBytes<C, Ob>());
+  FMT_LDS fmt_mt::Scratch<C>* scratch = (FMT_LDS fmt_mt::Scratch<C>*)(lds + wave * scratchBytes<C, Ob>());
   if (countDev != nullptr) count = __builtin_amdgcn_readfirstlane(*countDev);
   // Documents are dealt one at a time from a device counter (next != nullptr): a wave that finishes
   // early takes the next document, so the launch ends when the work does, not when the unluckiest

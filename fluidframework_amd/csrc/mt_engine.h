@@ -35,6 +35,12 @@
 #include <cstddef>
 #include <type_traits>
 
+#if FMT_GPU
+#define FMT_LDS __attribute__((address_space(3)))
+#else
+#define FMT_LDS
+#endif
+
 namespace fmt_mt {
 
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
@@ -352,7 +358,7 @@ class Doc {
   static constexpr int kWords = C::kWords;
   static constexpr int kMaxClient = C::kMaxClient;
   Lane<VR> W[kWords];  // W[f] element r of lane l = field f of leaf 64 r + l
-  Scratch<C>* s;
+  FMT_LDS Scratch<C>* s;  // (an LDS-space pointer: per-lane LDS addresses stay 32-bit)
   uint16_t* gch = nullptr;  // large tier: the document's text, in its HBM output slab
   int n = 0;          // leaves
   int nChars = 0;
@@ -451,7 +457,7 @@ class Doc {
       }
     }
     if constexpr (Ob) {
-      const uint32_t* obw = reinterpret_cast<const uint32_t*>(s->ob);
+      const uint32_t* obw = reinterpret_cast<const FMT_LDS uint32_t*>(s->ob);
       FOR_LANES(l) {
         for (int t = l; t < kCkptObWords; t += 64) ckpt[kCkptObOff + t] = obw[t];
       }
@@ -493,7 +499,7 @@ class Doc {
       obSeqN = static_cast<int>(c13 & 0xFFFFu);
       obStartN = static_cast<int>(c13 >> 16);
       obUsed = uni(ck[14]) | (static_cast<uint64_t>(uni(ck[15])) << 32);
-      uint32_t* obw = reinterpret_cast<uint32_t*>(s->ob);
+      uint32_t* obw = reinterpret_cast<FMT_LDS uint32_t*>(s->ob);
       FOR_LANES(l) {
         for (int t = l; t < kCkptObWords; t += 64) obw[t] = ckpt[kCkptObOff + t];
       }
@@ -583,7 +589,7 @@ class Doc {
       }
     }
     waveSync();  // every LDS write of the op stream has landed
-    const uint32_t* chars = reinterpret_cast<const uint32_t*>(s->chars);
+    const uint32_t* chars = reinterpret_cast<const FMT_LDS uint32_t*>(s->chars);
     const uint32_t* rest = reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(s) + offsetof(Scratch<C>, blk));
     uint32_t* dst = ck + kCkptHead + 5 * kCkptRows * 64;
     const int charWords = (nChars + 1) / 2;
@@ -592,7 +598,7 @@ class Doc {
       for (int t = l; t < kCkptRestWords; t += 64) dst[kCkptCharWords + t] = rest[t];
     }
     if constexpr (Ob) {
-      const uint32_t* obw = reinterpret_cast<const uint32_t*>(s->ob);
+      const uint32_t* obw = reinterpret_cast<const FMT_LDS uint32_t*>(s->ob);
       FOR_LANES(l) {
         for (int t = l; t < kCkptObWords; t += 64) dst[kCkptCharWords + kCkptRestWords + t] = obw[t];
       }
@@ -631,7 +637,7 @@ class Doc {
       }
     }
     const uint32_t* src = ck + kCkptHead + 5 * kCkptRows * 64;
-    uint32_t* chars = reinterpret_cast<uint32_t*>(s->chars);
+    uint32_t* chars = reinterpret_cast<FMT_LDS uint32_t*>(s->chars);
     uint32_t* rest = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(s) + offsetof(Scratch<C>, blk));
     const int charWords = (nChars + 1) / 2;
     FOR_LANES(l) {
@@ -639,7 +645,7 @@ class Doc {
       for (int t = l; t < kCkptRestWords; t += 64) rest[t] = src[kCkptCharWords + t];
     }
     if constexpr (Ob) {
-      uint32_t* obw = reinterpret_cast<uint32_t*>(s->ob);
+      uint32_t* obw = reinterpret_cast<FMT_LDS uint32_t*>(s->ob);
       FOR_LANES(l) {
         for (int t = l; t < kCkptObWords; t += 64) obw[t] = src[kCkptCharWords + kCkptRestWords + t];
       }
@@ -2395,7 +2401,7 @@ class Doc {
     // Every loaded leaf in one row pass (lengths staged through the still-unused char area); slots
     // past N stay all-zero. Header leaf j belongs to leaf block j / 7, body leaves get theirs below.
     // (the large tier reads the lengths straight from the segment records)
-    uint32_t* stage = reinterpret_cast<uint32_t*>(s->chars);
+    uint32_t* stage = reinterpret_cast<FMT_LDS uint32_t*>(s->chars);
     if constexpr (!C::kHbmChars) {
       FOR_LANES(l) {
         for (int j = l; j < N; j += 64) stage[j] = in.snapSegs[j].len;  // (with FMT_MT_SEG_MARKER)

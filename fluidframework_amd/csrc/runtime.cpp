@@ -915,6 +915,14 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
 int fmt_mt_run(fmt_ctx* c) {
   if (c == nullptr || !c->mtLoaded) return setErr(c, FMT_E_USAGE, "fmt_mt_run before fmt_mt_load");
   FMT_HIP(c, hipSetDevice(c->device));
+  // documents an earlier run of this load escalated into the huge tier start over: their state is
+  // released, and only the load-time huge documents (c->mtHugeLoaded) run with the small tiers
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  for (size_t h = c->mtHugeLoaded; h < c->huge.size(); h++)
+    for (void* q : c->huge[h].allocs) (void)hipFree(q);
+  for (uint32_t d = 0; d < c->mtDocs; d++)
+    if (c->mtHugeSlot[d] >= static_cast<int32_t>(c->mtHugeLoaded)) c->mtHugeSlot[d] = -1;
+  c->huge.resize(c->mtHugeLoaded);
   fmt_kernels::MtDeviceBatch db{c->mtOps.p, c->mtOffs.p, c->mtDocs, c->mtText.p,
                                 c->mtHasInit ? c->mtInit.p : nullptr, c->mtPropsOff.p, c->mtPropsKv.p, c->mtNProps,
                                 c->mtHasCatchup ? c->mtCuOffs.p : nullptr,
@@ -931,15 +939,14 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
-  const bool hasHuge = !c->huge.empty();
+  const bool hasHuge = c->mtHugeLoaded > 0;
   if (!hasHuge || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,
                                             c->mtObliterate,
                                             c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust));
   if (hasHuge)
-    FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p,
-                                           static_cast<uint32_t>(c->huge.size()), c->stream));
+    FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p, c->mtHugeLoaded, c->stream));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));  // device time excludes the host read-back below
   c->timed2 = false;
   // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
@@ -977,12 +984,6 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, hipStreamSynchronize(c->stream));
     for (uint32_t i = 0; i < nEsc; i++)
       if (hb[i].status == FMT_E_CAPACITY && c->mtHugeOk[list[i]] && c->mtHugeSlot[list[i]] < 0) grow.push_back(list[i]);
-    // (escalated documents of an earlier run of this load are released first)
-    for (size_t h = c->mtHugeLoaded; h < c->huge.size(); h++)
-      for (void* q : c->huge[h].allocs) (void)hipFree(q);
-    for (uint32_t d = 0; d < c->mtDocs; d++)
-      if (c->mtHugeSlot[d] >= static_cast<int32_t>(c->mtHugeLoaded)) c->mtHugeSlot[d] = -1;
-    c->huge.resize(c->mtHugeLoaded);
     if (!grow.empty()) {
       FMT_HIP(c, c->mtStartSegDev.reserve(grow.size()));
       std::vector<fmt_mt_snapshot_seg> starts(grow.size());
