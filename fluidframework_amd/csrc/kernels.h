@@ -40,6 +40,7 @@ struct MtDeviceBatch {
   const uint64_t* rmOrderOffsets;  // per-doc remove-order slab offsets (nDocs + 1), or nullptr
   const fmt_mt_snapshot_info* snapshotInfo;  // SnapshotV1 merge info per snapshot segment, or nullptr
   const fmt_mt_stamp* snapshotStamps;
+  uint64_t nSnapshotInfo;
   const fmt_mt_relpos* relpos;     // relative positions (FMT_MT_F_REL1/REL2 ops), or nullptr
   uint32_t nRelpos;
   uint32_t markerKey;              // key id of "markerId", FMT_MT_NO_MARKER if none

@@ -88,6 +88,9 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     in.markerKey = batch.markerKey;
     in.adj = batch.adj;
     in.doc = d;
+    in.infoAll = batch.snapshotInfo;
+    in.stampsAll = batch.snapshotStamps;
+    in.nInfoAll = batch.snapshotInfo ? batch.nSnapshotInfo : 0u;
     if (batch.snapshots && batch.snapshots[d].loaded) {
       const fmt_mt_snapshot_doc sd = batch.snapshots[d];
       in.snapSegs = batch.snapshotSegs + sd.first_seg;

@@ -185,6 +185,10 @@ struct DocInputs {
   uint32_t loaded;
   const fmt_mt_snapshot_info* snapInfo;  // SnapshotV1 merge info parallel to snapSegs, or nullptr
   const fmt_mt_stamp* snapStamps;
+  // the batch's whole merge-info table (FMT_MT_F_LOADSEG ops name rows of it), or nullptr
+  const fmt_mt_snapshot_info* infoAll;
+  const fmt_mt_stamp* stampsAll;
+  uint64_t nInfoAll;
   const fmt_mt_relpos* relpos;  // FMT_MT_F_REL1/REL2 ops index it (nullptr: none in the batch)
   uint32_t nRelpos;
   uint32_t markerKey;           // key id of "markerId"
@@ -814,6 +818,7 @@ class Doc {
   // Whether `client` holds a remove stamp on leaf 64 r + l (the remove-client set: W3, plus W5 for
   // ids 32..63 in the large tier).
   FMT_DEV bool removedBy(int l, int r, int client) const {
+    if (client < 0) return false;  // NonCollabClient / LocalClientId never hold a remove stamp here
     if constexpr (kWords > 5) {
       if (client >= 32) return ((LANE(W[5])[r] >> (client - 32)) & 1u) != 0;
     }
@@ -1457,8 +1462,8 @@ class Doc {
   // first leaf whose view prefix equals pos, leaves removed at/below minSeq skipped except the very
   // last leaf (mergeTree.ts:1862-1875); past the end it is appended to the last leaf's block.
   // Returns the new leaf's index, or -1 (nothing inserted, or failure).
-  FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
-    const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
+  FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0, int clientArg = 0x7fff, bool boundary = true) {
+    const int refSeq = op.ref_seq, client = clientArg != 0x7fff ? clientArg : op.client, seq = op.seq;
     const int pos = op.pos1, len = op.len;
     const int nr = rows();
     Lane<VR> vis, st;
@@ -1469,7 +1474,7 @@ class Doc {
     // the right part (view start pos) is then the first leaf at pos.
     int sp = 0;
     const int js = containing(vis, st, pos, nr, &sp);
-    if (js >= 0 && !splitLeafAt(js, pos - sp)) return -1;
+    if (boundary && js >= 0 && !splitLeafAt(js, pos - sp)) return -1;
     if (len <= 0) return -1;
     // seg {text, props}: the new segment's properties = clone(props) (textSegment.ts:41-52,
     // mergeTreeNodes.ts:343-347): raw LWW of the props op onto an empty set
@@ -1482,7 +1487,9 @@ class Doc {
       insProps = applyProps(kPropsUndef, static_cast<uint32_t>(op.pos2 - 1));
       if (status != FMT_OK) return -1;
     }
-    int insIdx = js >= 0 ? js + 1 : -1;
+    // (without the boundary — a loader batch's later segment — the walk stops at the leaf holding
+    // pos and inserts before it, mergeTree.ts:1876-1882)
+    int insIdx = js >= 0 ? (boundary ? js + 1 : js) : -1;
     FOR_ROWS(r, 0, nr) {
       if (insIdx < 0) {
         Lane<bool> p;
@@ -1809,6 +1816,51 @@ class Doc {
   }
 
   // One member op of a remote message (client.ts:1291-1327).
+  // SnapshotLoader.loadBody's append of one body-chunk segment (FMT_MT_F_LOADSEG,
+  // snapshotLoader.ts:287-309): insertSegments at the local length (every acked, not removed leaf)
+  // from PriorPerspective(UniversalSequenceNumber, client) with stamp {seq, client}; the segment keeps
+  // specToSegment's remove stamps (snapshot_info row op.pos1).
+  FMT_DEV void loadBodySegment(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
+    if (in.infoAll == nullptr || op.pos1 < 0 || static_cast<uint64_t>(op.pos1) >= in.nInfoAll) {
+      fail(FMT_E_DATA);
+      return;
+    }
+    const int client = op.client == FMT_MT_CLIENT_NONCOLLAB ? FMT_NON_COLLAB_CLIENT : static_cast<int>(op.client);
+    const int nr = rows();
+    Lane<uint32_t> acc;
+    FOR_LANES(l) { LANE(acc) = 0u; }
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        if (static_cast<int32_t>(LANE(W[2])[r]) == kNotRemoved) LANE(acc) += fLen(LANE(W[0])[r]);
+      }
+    }
+    uint32_t local;
+    waveExclusiveSum(acc, &local);
+    fmt_mt_op o = op;
+    o.pos1 = static_cast<int32_t>(local);
+    o.ref_seq = 0;
+    const int k = insertText(o, text0, client, (op.flags & FMT_MT_F_GROUP_CONT) == 0);
+    if (k < 0 || status != FMT_OK) return;
+    const fmt_mt_snapshot_info inf = in.infoAll[op.pos1];
+    int32_t rm = kNotRemoved;
+    uint64_t mask = 0;
+    for (uint32_t t = 0; t < inf.rm_count; t++) {
+      const fmt_mt_stamp st = in.stampsAll[inf.rm_first + t];
+      rm = uni(st.seq) < rm ? uni(st.seq) : rm;
+      const int c = uni(st.client);
+      if (c < 0 || c > kMaxClient) {
+        fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
+        return;
+      }
+      mask |= 1ull << c;
+    }
+    if (inf.rm_count) {
+      writeField(k, 2, static_cast<uint32_t>(rm));
+      writeField(k, 3, static_cast<uint32_t>(mask));
+      if constexpr (kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
+    }
+  }
+
   FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
     const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
     Lane<uint32_t> delta;  // catch-up: the segments of the op's delta event (row bitmask per lane)
@@ -2553,9 +2605,10 @@ class Doc {
         // writer set of this tier
         // (the small tier also stops near its block and prop-set limits, which the large tier's
         // 1023 / 1024 lift: an op's splits allocate a few blocks, an annotate a few sets)
+        const bool loaderNonCollab = (op.flags & FMT_MT_F_LOADSEG) != 0 && op.client == FMT_MT_CLIENT_NONCOLLAB;
         if (canSave &&
             (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(op.len) > kCapChars) ||
-             (kSavesBig && (op.client > kMaxClient ||
+             (kSavesBig && ((op.client > kMaxClient && !loaderNonCollab) ||
                             // (margins: plain batches only — obliterate documents near them mostly
                             // finish in this tier, measured on the obliterate farms)
                             (!Ob && (nFree < 16 || ((op.type == FMT_MT_ANNOTATE || op.type == FMT_MT_INSERT) &&
@@ -2579,7 +2632,11 @@ class Doc {
       rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
       opIdx = static_cast<uint32_t>(i - in.begin);
-      if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63
+      const bool loader = (op.flags & FMT_MT_F_LOADSEG) != 0;
+      if (loader) {
+        if (op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient) loadBodySegment(op, text);
+        else fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
+      } else if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63
         fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
       else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);
@@ -2589,7 +2646,9 @@ class Doc {
         if (rmPendN > 0 || rmHitsSet)
           rmFlush(op.client, op.seq, op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE);
       }
-      const bool lastMember = i + 1 == in.end || (recWord(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
+      // (a loader segment updates no collab window; a batch of them is no GROUP message)
+      const bool lastMember = !loader && (i + 1 == in.end || (recWord(rec0, 7) & (FMT_MT_F_GROUP_CONT | FMT_MT_F_LOADSEG)) !=
+                                                                 FMT_MT_F_GROUP_CONT);
       // zamboni once inside the op (mergeTree.ts:1510-1516, 2074-2080, 2376-2382), then, after the
       // message's last member, updateSeqNumbers (client.ts:1381-1391) → setMinSeq
       // (mergeTree.ts:1147-1166), which runs zamboni again only if minSeq advanced.

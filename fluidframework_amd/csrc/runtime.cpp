@@ -98,6 +98,7 @@ struct fmt_ctx {
   DevBuf<fmt_mt_snapshot_info> mtSnapInfo;   // SnapshotV1 merge info of loaded segments
   DevBuf<fmt_mt_stamp> mtSnapStamps;
   bool mtHasSnapInfo = false;
+  uint64_t mtNSnapSegs = 0;
   uint32_t mtNRelpos = 0, mtMarkerKey = FMT_MT_NO_MARKER;
   bool mtHasSnap = false;
   bool mtObliterate = false;                 // batch holds obliterates: launch the Doc<true> kernel
@@ -569,6 +570,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     const fmt_mt_op& op = b->ops[i];
     if (op.flags & FMT_MT_F_CATCHUP) catchupOps++;
     if (op.flags & FMT_MT_F_RMORDER) rmOrderOps++;
+    if (op.flags & FMT_MT_F_LOADSEG) {  // a SnapshotV1 body segment: its merge info row in range
+      if (op.type != FMT_MT_INSERT || b->snapshot_info == nullptr || op.pos1 < 0 ||
+          static_cast<uint64_t>(op.pos1) >= b->n_snapshot_segs ||
+          b->snapshot_info[op.pos1].rm_first + static_cast<uint64_t>(b->snapshot_info[op.pos1].rm_count) > b->n_snapshot_stamps)
+        return setErr(c, FMT_E_DATA, "a loader segment (FMT_MT_F_LOADSEG) without a valid merge-info row");
+    }
     if (op.type == FMT_MT_INSERT) {
       if (static_cast<uint64_t>(op.payload) + op.len > b->text_len)
         return setErr(c, FMT_E_DATA, "insert payload outside the text arena");
@@ -775,6 +782,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg)));
   }
   c->mtHasSnapInfo = c->mtHasSnap && b->snapshot_info != nullptr;
+  c->mtNSnapSegs = b->n_snapshot_segs;
   if (c->mtHasSnapInfo) {
     FMT_HIP(c, c->mtSnapInfo.reserve(b->n_snapshot_segs));
     FMT_HIP(c, c->mtSnapStamps.reserve(b->n_snapshot_stamps));
@@ -834,7 +842,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
       const fmt_mt_op& op = b->ops[i];
       if (op.type == FMT_MT_INSERT) chars += op.len;
-      if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2)) ||
+      if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) ||
           op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED ||
           (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
         ok = 0;
@@ -929,6 +937,7 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasSnap ? c->mtSnap.p : nullptr, c->mtHasSnap ? c->mtSnapSegs.p : nullptr,
                                 c->mtHasRmOrder ? c->mtRmOffs.p : nullptr,
                                 c->mtHasSnapInfo ? c->mtSnapInfo.p : nullptr, c->mtHasSnapInfo ? c->mtSnapStamps.p : nullptr,
+                                c->mtHasSnapInfo ? c->mtNSnapSegs : 0u,
                                 c->mtNRelpos ? c->mtRelpos.p : nullptr,
                                 c->mtNRelpos, c->mtMarkerKey,
                                 c->mtHasAdjust ? c->mtAdjTab.p : nullptr};

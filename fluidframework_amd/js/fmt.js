@@ -24,6 +24,7 @@ const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
 const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate places (client.ts:680-700)
 const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER = 0x8000; // Marker segments
 // legacy relativePos1/2 (ops.ts IRelativePosition): pos1/pos2 index the relpos table (fmt_mt_relpos, 16 B)
+const FMT_MT_F_LOADSEG = 256, FMT_MT_CLIENT_NONCOLLAB = 0xfe; // SnapshotV1 body segments with merge info
 const FMT_MT_F_REL1 = 64, FMT_MT_F_REL2 = 128, FMT_MT_NO_MARKER = 0xffffffff, FMT_MT_REL_BEFORE = 1;
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 // annotate-adjust (fmt.h): props_kv escape, computed value ids, fmt_mt_adjust flags
@@ -326,7 +327,9 @@ class MergeTreeStreamBuilder {
 	 * a legacy header + optional body, or SnapshotV1's header + body_0, body_1, ... (pass the bodies
 	 * as an array), and optionally the legacy catchupOps blob, whose messages become the first ops
 	 * after loadCore's validation (sequence.ts:818-863). V1 header segments with merge info keep
-	 * their stamps; body-chunk segments with merge info are not supported (mirrors streams.py).
+	 * their stamps; when any segment has merge info, the body-chunk segments become
+	 * FMT_MT_F_LOADSEG inserts ahead of the messages (loadBody appends each through insertSegments
+	 * at the local length, snapshotLoader.ts:254-309; mirrors streams.py).
 	 */
 	beginDocFromSummary(header, body, catchupOps, observer) {
 		const h = JSON.parse(header);
@@ -341,11 +344,12 @@ class MergeTreeStreamBuilder {
 		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "snapshot" : observer);
 		d.minSeq = md.minSequenceNumber === undefined ? md.sequenceNumber : md.minSequenceNumber;
 		const first = this.snapshotSegs.length;
-		chunks.forEach((c, ci) => {
+		let anyInfo = false;
+		chunks.forEach((c) => {
 			for (let spec of specsOf(c)) {
 				let info = [0, FMT_NON_COLLAB_CLIENT, 0, 0];
 				if (spec && typeof spec === "object" && "json" in spec) { // hasMergeInfo
-					if (ci > 0) throw new UnsupportedOp("SnapshotV1 body-chunk segments with merge info");
+					anyInfo = true;
 					info = this.mergeInfo(spec, d);
 					spec = spec.json;
 				}
@@ -354,14 +358,44 @@ class MergeTreeStreamBuilder {
 				this.snapshotInfo.push(info);
 			}
 		});
-		const nHeader = specsOf(h).length, nBody = this.snapshotSegs.length - first - nHeader;
+		const nHeader = specsOf(h).length;
+		let nBody = this.snapshotSegs.length - first - nHeader;
 		if (nHeader + nBody !== md.totalSegmentCount) throw new Error("Mismatch in totalSegmentCount");
 		const seq = md.sequenceNumber;
 		const minSeq = md.minSequenceNumber === undefined ? seq : md.minSequenceNumber;
 		this.docs.push(d);
 		this.docInit.push([0, 0]);
-		this.snapshots.push([first, nHeader, nBody, minSeq, seq]);
 		this.current = d;
+		if (anyInfo && nBody > 0) {
+			// each body segment: an insert at the local length from PriorPerspective(0, its client), a run
+			// of segments without merge info in one insertSegments call (FMT_MT_F_GROUP_CONT)
+			let prevUniversal = false;
+			for (let k = first + nHeader; k < first + nHeader + nBody; k++) {
+				const [off, ln, pid] = this.snapshotSegs[k];
+				const [insSeq, insClient] = this.snapshotInfo[k];
+				const universal = insClient === FMT_NON_COLLAB_CLIENT && insSeq === 0;
+				let flags = FMT_MT_F_LOADSEG | ((ln & FMT_MT_SEG_MARKER) ? FMT_MT_F_MARKER : 0);
+				if (universal && prevUniversal) flags |= FMT_MT_F_GROUP_CONT;
+				prevUniversal = universal;
+				const nUnits = (ln & ~FMT_MT_SEG_MARKER) >>> 0;
+				if (nUnits > 0xffff) throw new UnsupportedOp("a SnapshotV1 body segment with merge info longer than 65535 UTF-16 units");
+				const o = this.ops.next();
+				const v = this.ops.view;
+				v.setInt32(o + 0, insSeq, true);
+				v.setInt32(o + 4, 0, true);
+				v.setInt32(o + 8, minSeq, true);
+				v.setInt32(o + 12, k, true);
+				v.setInt32(o + 16, pid !== NO_PROPS ? pid + 1 : 0, true);
+				v.setUint32(o + 20, off, true);
+				v.setUint16(o + 24, nUnits, true);
+				v.setUint8(o + 26, insClient === FMT_NON_COLLAB_CLIENT ? FMT_MT_CLIENT_NONCOLLAB : insClient);
+				v.setUint8(o + 27, MT_INSERT);
+				v.setUint32(o + 28, flags, true);
+				d.nOps++;
+			}
+			nBody = 0; // the document loads its header alone
+		}
+		this.snapshots.push([first, nHeader, nBody, minSeq, seq]);
 		if (catchupOps !== undefined && catchupOps !== null) {
 			let cur = seq;
 			for (const m of JSON.parse(catchupOps)) {
@@ -533,7 +567,8 @@ class MergeTreeStreamBuilder {
 					for (let o = a * MT_OP_BYTES; o < b * MT_OP_BYTES; o += MT_OP_BYTES) anyOb = anyOb || isOb(v.getUint8(o + 27));
 					for (let o = a * MT_OP_BYTES; o < b * MT_OP_BYTES; o += MT_OP_BYTES) {
 						const t = v.getUint8(o + 27);
-						if (v.getInt32(o, true) > finalMsn && (t === MT_REMOVE || isOb(t) || (anyOb && t === MT_INSERT)))
+						if ((v.getUint32(o + 28, true) & FMT_MT_F_LOADSEG) === 0 && v.getInt32(o, true) > finalMsn &&
+							(t === MT_REMOVE || isOb(t) || (anyOb && t === MT_INSERT)))
 							v.setUint32(o + 28, v.getUint32(o + 28, true) | FMT_MT_F_RMORDER, true);
 					}
 				}

@@ -60,6 +60,8 @@ MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED 
 MT_F_START_BEFORE, MT_F_END_BEFORE = 8, 16  # fmt.h FMT_MT_F_START_BEFORE / FMT_MT_F_END_BEFORE
 MT_F_MARKER = 32  # fmt.h FMT_MT_F_MARKER: insert of a Marker segment
 MT_F_REL1, MT_F_REL2 = 64, 128  # fmt.h FMT_MT_F_REL1/REL2: pos1/pos2 index the relpos table
+MT_F_LOADSEG = 256  # fmt.h FMT_MT_F_LOADSEG: a SnapshotV1 body segment the loader appends
+CLIENT_NONCOLLAB_OP = 0xFE  # fmt.h FMT_MT_CLIENT_NONCOLLAB
 # fmt_mt_relpos: an IRelativePosition {id, before, offset} (ops.ts IRelativePosition)
 RELPOS_DTYPE = np.dtype([("marker_id", "<u4"), ("offset", "<i4"), ("flags", "<u4"), ("pad", "<u4")])
 NO_MARKER = 0xFFFFFFFF  # fmt.h FMT_MT_NO_MARKER
@@ -538,7 +540,7 @@ class MergeTreeStreamBuilder:
         SharedSegmentSequence.loadCore does (sequence.ts:818-863). The loading client is `observer`
         (short id 0). V1 header-chunk segments that carry merge info (seq/client/removed and moved
         stamps above minSeq) load with their stamps as specToSegment builds them
-        (snapshotLoader.ts:105-175); body-chunk segments with merge info are not supported."""
+        (snapshotLoader.ts:105-175); body-chunk segments then load as FMT_MT_F_LOADSEG inserts (below)."""
         h = json.loads(header)
         md = h.get("headerMetadata")
         if md is None:
@@ -556,14 +558,14 @@ class MergeTreeStreamBuilder:
         d = _DocBuilder(self, observer)
         d.min_seq = min_seq  # the loaded tree's minSeq (loadCore → MergeTree.startCollaboration)
         first = len(self.snapshot_segs)
+        any_info = False
         for ci, c in enumerate(chunks):
             for spec in specs(c):
                 info = (0, NON_COLLAB_CLIENT, 0, 0)
                 if isinstance(spec, dict) and "json" in spec:  # hasMergeInfo
-                    if ci > 0:
-                        raise UnsupportedOp("SnapshotV1 body-chunk segments with merge info")
                     info = self._merge_info(spec, d)
                     spec = spec["json"]
+                    any_info = True
                 if marker_ref_type(spec) is not None:  # loaded markers register their ids too
                     d.note_marker_id(spec.get("props"))
                 self.snapshot_segs.append(self._spec(spec))
@@ -574,6 +576,28 @@ class MergeTreeStreamBuilder:
             raise ValueError("Mismatch in totalSegmentCount")  # snapshotLoader.ts:272-275
         self.docs.append(d)
         self.doc_init.append((0, 0))
+        if any_info and n_body:
+            # loadBody with merge info (snapshotLoader.ts:254-309): each body segment is appended through
+            # insertSegments at the local length from PriorPerspective(0, its client) — a batch of
+            # segments without merge info in one call — so they become FMT_MT_F_LOADSEG inserts ahead of
+            # the messages (their specs and merge info rows stay in the tables; the document loads its
+            # header alone)
+            prev_universal = False
+            for k in range(first + n_header, first + n_header + n_body):
+                off, ln, pid = self.snapshot_segs[k]
+                ins_seq, ins_client = self.snapshot_info[k][0], self.snapshot_info[k][1]
+                universal = ins_client == NON_COLLAB_CLIENT and ins_seq == 0
+                flags = MT_F_LOADSEG | (MT_F_MARKER if ln & MT_SEG_MARKER else 0)
+                if universal and prev_universal:
+                    flags |= MT_F_GROUP_CONT
+                prev_universal = universal
+                n_units = ln & ~MT_SEG_MARKER
+                if n_units > 0xFFFF:
+                    raise UnsupportedOp("a SnapshotV1 body segment with merge info longer than 65535 UTF-16 units")
+                client = CLIENT_NONCOLLAB_OP if ins_client == NON_COLLAB_CLIENT else ins_client
+                d.ops.append((ins_seq, 0, min_seq, k, pid + 1 if pid != NO_PROPS else 0, off, n_units, client,
+                              MT_INSERT, flags))
+            n_body = 0
         self.snapshots.append((first, n_header, n_body, min_seq, seq, 1))
         if catchup_ops is not None:
             cur = seq
@@ -678,7 +702,7 @@ def flag_catchup(ops: np.ndarray, offs: np.ndarray) -> None:
         return
     last = np.maximum(offs[1:] - 1, 0)
     final_msn = np.repeat(ops["min_seq"][last], n)  # each op's document's final minSeq
-    sel = (ops["seq"] > final_msn) & (ops["ref_seq"] != ops["seq"] - 1)
+    sel = (ops["seq"] > final_msn) & (ops["ref_seq"] != ops["seq"] - 1) & ((ops["flags"] & MT_F_LOADSEG) == 0)
     ops["flags"][sel] |= MT_F_CATCHUP
 
 
@@ -728,7 +752,7 @@ def flag_remove_order(ops: np.ndarray, offs: np.ndarray) -> None:
         t = seg["type"]
         ob = (t == MT_OBLITERATE) | (t == MT_OBLITERATE_SIDED)
         kinds = (t == MT_REMOVE) | ob | ((t == MT_INSERT) & bool(ob.any()))
-        sel = (seg["seq"] > final_msn) & kinds
+        sel = (seg["seq"] > final_msn) & kinds & ((seg["flags"] & MT_F_LOADSEG) == 0)
         seg["flags"][sel] |= MT_F_RMORDER
 
 

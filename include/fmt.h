@@ -107,6 +107,15 @@ extern "C" {
  * (mergeTree.ts:1462-1483, via client.ts:760-767 getValidOpRange). */
 #define FMT_MT_F_REL1 64u
 #define FMT_MT_F_REL2 128u
+/* A SnapshotV1 body-chunk segment the loader appends (snapshotLoader.ts:254-309), an INSERT placed
+ * before the document's messages: insertSegments at the local length (root.cachedLength; the op's
+ * pos1 is ignored for it) from PriorPerspective(UniversalSequenceNumber, client) with stamp {seq,
+ * client}, the segment's remove stamps (fmt_mt_snapshot_info row pos1 of the batch) kept, and no
+ * collab-window update. client FMT_MT_CLIENT_NONCOLLAB: NonCollabClient (a segment without merge
+ * info). With FMT_MT_F_GROUP_CONT it continues the previous one's insertSegments call (a batch of
+ * segments without merge info): no interval boundary is made at its position. */
+#define FMT_MT_F_LOADSEG 256u
+#define FMT_MT_CLIENT_NONCOLLAB 0xFEu
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */

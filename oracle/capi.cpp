@@ -39,7 +39,10 @@ int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* ar
       mt->catchupOp = static_cast<uint32_t>(i);
       mt->applyRemote(op, arena, propsOff, propsKv);
       mt->catchupOut = nullptr;
-      if (i + 1 == n || (ops[i + 1].flags & FMT_MT_F_GROUP_CONT) == 0) mt->updateSeqNumbers(op.min_seq, op.seq);
+      // (loader segments: no collab-window update; a batch of them is not a GROUP message)
+      if ((op.flags & FMT_MT_F_LOADSEG) == 0 &&
+          (i + 1 == n || (ops[i + 1].flags & (FMT_MT_F_GROUP_CONT | FMT_MT_F_LOADSEG)) != FMT_MT_F_GROUP_CONT))
+        mt->updateSeqNumbers(op.min_seq, op.seq);
     } catch (const std::exception& e) {
       if (failSeq) *failSeq = op.seq;
       return fail(e.what());
@@ -226,6 +229,9 @@ void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d,
     mt.nValues = b->value_num ? b->n_values : 0u;
     mt.hostNumbers = hostNums;
   }
+  mt.snapInfo = b->snapshot_info;
+  mt.snapStamps = b->snapshot_stamps;
+  mt.nSnapInfo = b->snapshot_info ? b->n_snapshot_segs : 0;
   if (b->snapshots != nullptr && b->snapshots[d].loaded) {
     const fmt_mt_snapshot_doc& sd = b->snapshots[d];
     std::vector<MergeTree::LoadedSeg> head, body;

@@ -584,8 +584,8 @@ void MergeTree::addToLRUSet(Seg* leaf, int seq) {
 }
 
 // mergeTree.ts:1484-1517 insertSegments + :1555-1750 blockInsert (no obliterates in scope).
-void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp) {
-  ensureIntervalBoundary(pos, p);
+void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp, bool boundary) {
+  if (boundary) ensureIntervalBoundary(pos, p);
   if (seg->len() > 0) {
     seg->ins = stamp;
     InsertCtx ctx{true, seg};
@@ -911,6 +911,22 @@ void MergeTree::applyRemote(const fmt_mt_op& opIn, const uint16_t* arena, const 
         }
       }
       if (s->marker) registerMarker(s);  // idToMarker.set (mergeTree.ts:1614-1620)
+      if (op.flags & FMT_MT_F_LOADSEG) {
+        // SnapshotLoader.loadBody's append (snapshotLoader.ts:287-309): insertSegments at
+        // root.cachedLength from PriorPerspective(UniversalSequenceNumber, clientId) with stamp
+        // {seq, clientId}; specToSegment's remove stamps stay on the segment (:105-175)
+        const int client = op.client == FMT_MT_CLIENT_NONCOLLAB ? kNonCollabClient : static_cast<int>(op.client);
+        if (snapInfo == nullptr || op.pos1 < 0 || static_cast<uint64_t>(op.pos1) >= nSnapInfo)
+          throw DataError("loader segment without its merge info");
+        const fmt_mt_snapshot_info& inf = snapInfo[op.pos1];
+        for (uint32_t t = 0; t < inf.rm_count; t++) {
+          const fmt_mt_stamp& st = snapStamps[inf.rm_first + t];
+          s->removes.push_back(Stamp{st.seq, st.client, static_cast<int>(st.kind)});
+        }
+        insertSegments(getLocalLength(), s, Perspective{false, 0, client}, Stamp{op.seq, client},
+                       (op.flags & FMT_MT_F_GROUP_CONT) == 0);
+        break;
+      }
       insertSegments(op.pos1, s, p, stamp);
       break;
     }

@@ -219,6 +219,10 @@ class MergeTree {
   // number of each host value id (NaN: not a number), the host's numbers with their ids, and this
   // document's computed numbers (value ids FMT_MT_VALUE_COMPUTED + index, first-computed order).
   const fmt_mt_adjust* adjusts = nullptr;
+  // SnapshotV1 merge info of the batch (FMT_MT_F_LOADSEG body segments name their row)
+  const fmt_mt_snapshot_info* snapInfo = nullptr;
+  const fmt_mt_stamp* snapStamps = nullptr;
+  uint64_t nSnapInfo = 0;
   uint32_t nAdjusts = 0;
   const double* valueNum = nullptr;
   uint32_t nValues = 0;
@@ -297,7 +301,7 @@ class MergeTree {
   template <class F>
   void nodeMap(const Perspective& p, int start, int end, F&& leafFn) const;
 
-  void insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp);
+  void insertSegments(int pos, Seg* seg, const Perspective& p, Stamp stamp, bool boundary = true);
   void markRangeRemoved(int start, int end, const Perspective& p, Stamp stamp);
   // obliterateRange (mergeTree.ts:2262-2290) → obliterateRangeSided (:2083-2260) with
   // start {pos1, Before} and end {pos2 - 1, After}.

@@ -70,6 +70,9 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     in.markerKey = b->marker_id_key;
     in.adj = g_nums.empty() ? nullptr : &g_adj;
     in.doc = d;
+    in.infoAll = b->snapshot_info;
+    in.stampsAll = b->snapshot_stamps;
+    in.nInfoAll = b->snapshot_info ? b->n_snapshot_segs : 0u;
     if (b->snapshots && b->snapshots[d].loaded) {
       const fmt_mt_snapshot_doc sd = b->snapshots[d];
       in.snapSegs = b->snapshot_segs + sd.first_seg;

@@ -325,12 +325,24 @@ def test_v1_merge_info_load_then_replay_matches_reference_text():
         assert not diffs, f"doc {d}: {diffs[:5]}"
 
 
-def test_v1_body_chunk_merge_info_is_rejected():
+def test_v1_body_chunk_merge_info_loads():
+    """A body segment with merge info appends at the local length from its own perspective
+    (snapshotLoader.ts:254-309): after a universal header it lands at the end, keeping its stamp."""
+    import oracle as orc
+
     head = json.dumps({"version": "1", "segmentCount": 1, "length": 2, "segments": ["ab"], "startIndex": 0,
                        "headerMetadata": {"minSequenceNumber": 0, "sequenceNumber": 5, "totalLength": 3,
                                           "totalSegmentCount": 2,
                                           "orderedChunkMetadata": [{"id": "header"}, {"id": "body_0"}]}})
     body = json.dumps({"version": "1", "segmentCount": 1, "length": 1, "startIndex": 1,
                        "segments": [{"json": "c", "seq": 3, "client": "B"}]})
-    with pytest.raises(UnsupportedOp):
-        MergeTreeStreamBuilder().begin_doc_from_summary(head, [body])
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc_from_summary(head, [body])
+    d.add_message({"clientId": "B", "sequenceNumber": 6, "referenceSequenceNumber": 2, "minimumSequenceNumber": 0,
+                   "type": "op", "contents": {"pos1": 2, "seg": "x", "type": 0}})
+    batch = b.finish()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=512, cap_chars=2048, cap_props=1024)
+    assert rc == 0 and int(oh[0]["status"]) == 0
+    assert visible_text(oh[0], ol[0], oc[0]) == "abxc"  # B saw its own "c" (seq 3) at refSeq 2
+    eh, el, ec, ep = emu_replay(batch)
+    assert not compare_doc((oh[0], ol[0], oc[0], op[0]), (eh[0], el[0], ec[0], ep[0]))

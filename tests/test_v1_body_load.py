@@ -1,0 +1,171 @@
+"""SnapshotV1 body-chunk segments with merge info (snapshotLoader.ts:221-309).
+
+loadBody appends each body segment through insertSegments at root.cachedLength (the local length)
+from PriorPerspective(UniversalSequenceNumber, the segment's client) with its stamp, a run of
+segments without merge info in one call. The hosts pack them as FMT_MT_F_LOADSEG inserts ahead of the
+messages (the header alone is reloaded); the oracle and the engine apply them as the reference does.
+
+What the reference does with them: a body segment whose perspective misses an earlier segment that
+the local length counts (inserted above seq 0 by another client) cannot reach that position, and the
+load throws "MergeTree insert failed" — which is what happens to V1 summaries of collaborative
+documents with merge info before a body segment. A document whose body merge info comes from one
+writer after a universal header loads, and replaying the rest of its stream reaches the original's
+text. Both outcomes are checked: oracle status and text, and engine == oracle bit for bit (emulated
+here, on the GPU in -m gpu).
+"""
+import json
+import os
+import random
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from churn import farm_messages
+from fluidframework_amd import summary, workloads
+from fluidframework_amd.streams import MergeTreeStreamBuilder
+from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
+
+
+def _source_docs():
+    src = workloads.conflict_farm(3, n_clients=8, ops_per_doc=1500, seed=3)
+    docs = []
+    for d in range(3):  # collaborative: the farm runs after a 12,000-unit prefix (the header chunk)
+        init, msgs = farm_messages(src, d)
+        for m in msgs:
+            c = m["contents"]
+            c["pos1"] += 12000
+            if "pos2" in c:
+                c["pos2"] += 12000
+        docs.append(("Z" * 12000 + init, msgs))
+    for seed in (1, 2):  # one writer appending after the prefix (some of it removed again)
+        rnd, msgs, length = random.Random(seed), [], 12000
+        for seq in range(1, 300):
+            if rnd.random() < 0.2 and length > 12010:
+                a = rnd.randint(12000, length - 3)
+                op = {"pos1": a, "pos2": a + 2, "type": 1}
+                length -= 2
+            else:
+                n = rnd.randint(1, 5)
+                op = {"pos1": length, "seg": "q" * n, "type": 0}
+                length += n
+            msgs.append({"clientId": "solo", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+                         "minimumSequenceNumber": max(0, seq - 30), "type": "op", "contents": op})
+        docs.append(("Z" * 12000, msgs))
+    return docs
+
+
+def _cut(docs, at):
+    """V1 summaries of every document after its first `at` messages (oracle state), the rest of its
+    messages, and the text of the whole stream."""
+    import oracle as orc
+
+    b = MergeTreeStreamBuilder(keep_messages=True)
+    for init, msgs in docs:
+        d = b.begin_doc(init, observer="observer")
+        for m in msgs[:at]:
+            d.add_message(m)
+    cut = b.finish(remove_order=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(cut, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    assert rc == 0
+    out = []
+    for d, (init, msgs) in enumerate(docs):
+        head, bodies = summary.v1_summary(oh[d], ol[d], oc[d], op[d], cut.keys, cut.values, cut.clients[d],
+                                          orc.mt_removers(cut, d))
+        assert bodies and any("json" in s for bd in bodies for s in json.loads(bd)["segments"] if isinstance(s, dict))
+        out.append((head, bodies, msgs[at:]))
+    return out
+
+
+@pytest.fixture(scope="module")
+def reload_batch():
+    docs = _source_docs()
+    cuts = _cut(docs, 200)
+    b = MergeTreeStreamBuilder()
+    for head, bodies, rest in cuts:
+        d = b.begin_doc_from_summary(head, bodies)
+        for m in rest:
+            d.add_message(m)
+    return b.finish(), docs, cuts
+
+
+def test_loader_segments_follow_the_reference(orc, reload_batch):
+    batch, docs, _ = reload_batch
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    st = [int(x) for x in oh["status"]]
+    assert st[:3] == [-2, -2, -2]  # DataProcessingError: "MergeTree insert failed" while loading
+    assert st[3:] == [0, 0]
+    whole = MergeTreeStreamBuilder()
+    for init, msgs in docs[3:]:
+        d = whole.begin_doc(init, observer="observer")
+        for m in msgs:
+            d.add_message(m)
+    wb = whole.finish()
+    rc2, wh, wl, wc, _, _ = orc.mt_replay_batch(wb, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    for k in range(2):
+        assert visible_text(oh[3 + k], ol[3 + k], oc[3 + k]) == visible_text(wh[k], wl[k], wc[k])
+
+
+def test_emulated_engine_matches_oracle_on_loader_segments(orc, reload_batch):
+    batch, _, _ = reload_batch
+    cl, cc, cp = emu_caps(large=True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=cl, cap_chars=cc, cap_props=cp)
+    eh, el, ec, ep = emu_replay(batch, large=True)
+    for d in range(batch.n_docs):
+        assert int(eh[d]["status"]) == int(oh[d]["status"]) and int(eh[d]["fail_seq"]) == int(oh[d]["fail_seq"]), d
+        if int(oh[d]["status"]) == 0:
+            assert not compare_doc((oh[d], ol[d], oc[d], op[d]), (eh[d], el[d], ec[d], ep[d])), d
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node is not installed")
+def test_js_packer_matches_python_on_loader_segments(reload_batch, tmp_path):
+    """js/fmt.js packs the body segments as the same FMT_MT_F_LOADSEG ops as streams.py."""
+    batch, _, cuts = reload_batch
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    (tmp_path / "cuts.json").write_text(json.dumps([[h, b, r] for h, b, r in cuts]))
+    js = (f"const fmt=require({json.dumps(os.path.join(repo, 'fluidframework_amd', 'js', 'fmt.js'))});"
+          f"const cuts=JSON.parse(require('fs').readFileSync({json.dumps(str(tmp_path / 'cuts.json'))},'utf8'));"
+          "const b=new fmt.MergeTreeStreamBuilder();"
+          "for(const [h,bodies,rest] of cuts){const d=b.beginDocFromSummary(h,bodies,null,'observer');"
+          "for(const m of rest) d.addMessage(m);}"
+          "const r=b.finish();const hex=(a)=>Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
+          "process.stdout.write(JSON.stringify({ops:hex(r.ops),segs:hex(r.snapshotSegs),info:hex(r.snapshotInfo),"
+          "stamps:hex(r.snapshotStamps),snaps:hex(new Uint8Array(r.snapshots))}))")
+    script = tmp_path / "load.js"
+    script.write_text(js)
+    r = subprocess.run(["node", str(script)], capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    loader = (batch.ops["flags"] & 256) != 0
+    assert loader.sum() > 100
+    assert bytes.fromhex(out["ops"]) == batch.ops.tobytes()
+    assert bytes.fromhex(out["segs"]) == batch.snapshot_segs.tobytes()
+    assert bytes.fromhex(out["info"]) == batch.snapshot_info.tobytes()
+    assert bytes.fromhex(out["stamps"]) == batch.snapshot_stamps.tobytes()
+    assert bytes.fromhex(out["snaps"]) == batch.snapshots.tobytes()
+
+
+@pytest.mark.gpu
+def test_loader_segments_on_gpu(orc, reload_batch):
+    import ctypes
+
+    from fluidframework_amd import native
+
+    batch, _, _ = reload_batch
+    cl, cc, cp = native.capacity()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    eng = native.Engine(0)
+    try:
+        eng.mt_load(batch)
+        eng.mt_run()
+        eng.sync()
+        hdrs = np.zeros(batch.n_docs, dtype=native.DOC_RESULT_DTYPE)  # fmt_mt_fetch_headers reports the failures
+        native.lib().fmt_mt_fetch_headers(eng.h, hdrs.ctypes.data_as(ctypes.c_void_p))
+        for d in range(batch.n_docs):
+            assert int(hdrs[d]["status"]) == int(oh[d]["status"]) and int(hdrs[d]["fail_seq"]) == int(oh[d]["fail_seq"]), d
+            if int(oh[d]["status"]) == 0:
+                lv, ch, pr = eng.mt_doc(d, hdrs[d])
+                assert not compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], lv, ch, pr)), d
+    finally:
+        eng.close()
