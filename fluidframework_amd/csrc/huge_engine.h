@@ -71,6 +71,18 @@ constexpr int kWGroupShift = 17;
 constexpr int kWinList = 1024;  // LDS list of one group's visible window entries (slot pass)
 constexpr int kGlCap = 2048;    // LDS list of the visible window entries of one group pass
 constexpr int kGlEntBits = 21;  // entry index bits in glEnt (the group id above them)
+constexpr int kObCap = 128;     // live obliterates (seq above minSeq)
+
+// One live obliterate (mergeTree.ts ObliterateInfo): its endpoint references as (leaf id, offset) —
+// id 0 once the reference is removed — and its stamp.
+struct ObEnt {
+  uint32_t startId;
+  int32_t startOff;
+  uint32_t endId;
+  int32_t endOff;
+  int32_t seq;
+  int32_t client;
+};
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));
 typedef uint32_t u32x2 __attribute__((vector_size(8)));
@@ -144,7 +156,7 @@ struct HugeState {
 struct HugeLds {
   uint16_t gOrder[kGroupCap];    // group ids in document order
   int32_t gStable[kGroupCap];    // by group id: Σ stable lengths of its slots
-  uint32_t gCount[kGroupCap];    // by group id: slots
+  uint16_t gCount[kGroupCap];    // by group id: slots (<= kSlotCap)
   int32_t gCorr[kGroupCap];      // by group id: window correction of the current perspective
   int32_t sLen[kSlotCap];        // the group being searched: view length per slot
   uint32_t sBlk[kSlotCap];
@@ -160,6 +172,11 @@ struct HugeLds {
   uint32_t glEnt[kGlCap];
   int32_t glVis[kGlCap];
   int32_t glN[4];
+  // live obliterates: slots, slot in use, Obliterates.seqOrdered / startOrdered (slot lists)
+  ObEnt ob[kObCap];
+  uint8_t obUsed[kObCap];
+  uint8_t obSeq[kObCap];
+  uint8_t obStart[kObCap];
 };
 
 struct HugeInputs {
@@ -204,6 +221,7 @@ class HugeDoc {
   int curSeq = 0, minSeq = 0;
   int status = FMT_OK, failSeq = 0;
   uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
+  int obLive = 0, obSeqN = 0, obStartN = 0;  // live obliterates: slots in use, seqOrdered / startOrdered lengths
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
@@ -439,7 +457,7 @@ class HugeDoc {
         S.bGroup[nb] = g;
       }
     }
-    L->gCount[g] = static_cast<uint32_t>(cnt + 1);
+    L->gCount[g] = static_cast<uint16_t>(cnt + 1);
     L->gStable[g] += st;
     waveSync();
     return true;
@@ -485,7 +503,7 @@ class HugeDoc {
       }
       waveSync();
     }
-    L->gCount[g] = static_cast<uint32_t>(cnt - n);
+    L->gCount[g] = static_cast<uint16_t>(cnt - n);
     L->gStable[g] -= removed;
     waveSync();
   }
@@ -527,8 +545,8 @@ class HugeDoc {
       L->gOrder[k] = v;
     }
     L->gOrder[gp + 1] = static_cast<uint16_t>(g2);
-    L->gCount[g] = static_cast<uint32_t>(half);
-    L->gCount[g2] = static_cast<uint32_t>(moved);
+    L->gCount[g] = static_cast<uint16_t>(half);
+    L->gCount[g2] = static_cast<uint16_t>(moved);
     L->gStable[g] -= static_cast<int32_t>(tot);
     L->gStable[g2] = static_cast<int32_t>(tot);
     L->gCorr[g2] = 0;
@@ -1389,6 +1407,7 @@ class HugeDoc {
     setLane(R.f[0], k, x.len);
     regsInsert(R, k + 1, y, wy);
     st1(S.leafBlk + y.id, b);
+    obRefsMove(x.id, y.id, o, -o);  // the right part takes the references at/after the split
     const uint32_t nb = commitBlock(R);
     if (nb != kNone && k + 1 >= kMaxNodes / 2) {
       *rb = nb;
@@ -1493,6 +1512,8 @@ class HugeDoc {
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);
     const uint32_t nb = commitBlock(R);
+    if (status != FMT_OK) return;
+    if (obStartN > 0) obliterateOnInsert(x.id, r, c);
     if (status != FMT_OK) return;
     lru(nb != kNone && k >= kMaxNodes / 2 ? nb : b, x.id, op.seq);
   }
@@ -1668,6 +1689,318 @@ class HugeDoc {
     putLeaf(b, j, x);
   }
 
+  // ------------------------------------------------------------------ obliterates (f1)
+  // Obliterates (mergeTree.ts:515-635, 2083-2290), the same rules as mt_engine.h. A reference's
+  // "ordinal" is its leaf's document order — (group position, slot, index in block) here — or ""
+  // (smallest, -1) once the leaf is gone from the tree or the reference was removed.
+  FMT_DEV int64_t ordOf(uint32_t id) const {
+    if (id == 0) return -1;
+    if (ldu(S.leafBlk + id) == kNone) return -1;
+    uint32_t b;
+    int k;
+    locate(id, &b, &k);
+    if (k < 0) return -1;
+    return (static_cast<int64_t>(groupPos(ldu(S.bGroup + b))) << 16) | (static_cast<int64_t>(ldu(S.bSlot + b)) << 3) | k;
+  }
+  FMT_DEV static int ordinalCompare(int64_t a, int64_t b) {
+    if (a < 0 || b < 0) return (a < 0) == (b < 0) ? 0 : (a < 0 ? -1 : 1);
+    return a < b ? -1 : (a > b ? 1 : 0);
+  }
+  FMT_DEV int obU(uint8_t* p, int i) const { return uni(static_cast<int>(p[i])); }
+  FMT_DEV int startCompare(int a, int b) const {  // SortedSegmentSet.compare on start references
+    const int c = ordinalCompare(ordOf(uni(L->ob[a].startId)), ordOf(uni(L->ob[b].startId)));
+    return c != 0 ? c : uni(L->ob[a].startOff) - uni(L->ob[b].startOff);
+  }
+  // SortedSet.findItemPosition + SortedSegmentSet.onFindEquivalent, verbatim: the array is only as
+  // sorted as the ordinals were at insertion.
+  FMT_DEV int findStart(int slot, bool* exists) const {
+    *exists = false;
+    if (obStartN == 0) return 0;
+    int start = 0, end = obStartN - 1, index = -1;
+    while (start <= end) {
+      index = start + (end - start) / 2;
+      const int at = obU(L->obStart, index);
+      const int c = startCompare(slot, at);
+      if (c < 0) {
+        if (start == index) return index;
+        end = index - 1;
+      } else if (c > 0) {
+        if (index == end) return index + 1;
+        start = index + 1;
+      } else {
+        if (at == slot) {
+          *exists = true;
+          return index;
+        }
+        for (int b = index - 1; b >= 0 && startCompare(slot, obU(L->obStart, b)) == 0; b--)
+          if (obU(L->obStart, b) == slot) {
+            *exists = true;
+            return b;
+          }
+        for (; index < obStartN && startCompare(slot, obU(L->obStart, index)) == 0; index++)
+          if (obU(L->obStart, index) == slot) {
+            *exists = true;
+            return index;
+          }
+        return index;
+      }
+    }
+    return index;
+  }
+
+  // References on leaf `from` at offset >= minOff move to leaf `to`, offset += add (split: the right
+  // part; zamboni append: every reference of the appended leaf). Lane l takes slots l, l + 64.
+  FMT_DEV void obRefsMove(uint32_t from, uint32_t to, int minOff, int add) {
+    if (obLive == 0) return;
+    FOR_LANES(l) {
+      for (int k = l; k < kObCap; k += 64) {
+        if (L->obUsed[k]) {
+          ObEnt& e = L->ob[k];
+          if (e.startId == from && e.startOff >= minOff) {
+            e.startId = to;
+            e.startOff += add;
+          }
+          if (e.endId == from && e.endOff >= minOff) {
+            e.endId = to;
+            e.endOff += add;
+          }
+        }
+      }
+    }
+    waveSync();
+  }
+
+  FMT_DEV bool obAdd(uint32_t sId, int sOff, uint32_t eId, int eOff, int seq, int client) {
+    int slot = -1;
+    for (int base = 0; base < kObCap && slot < 0; base += 64) {
+      Lane<bool> q;
+      FOR_LANES(l) { LANE(q) = L->obUsed[base + l] == 0; }
+      const uint64_t m = ballot(q);
+      if (m) slot = base + ctz64(m);
+    }
+    if (slot < 0) return fail(FMT_E_CAPACITY);
+    FOR_LANES(l) {
+      if (l == 0) {
+        L->obUsed[slot] = 1;
+        ObEnt& e = L->ob[slot];
+        e.startId = sId;
+        e.startOff = sOff;
+        e.endId = eId;
+        e.endOff = eOff;
+        e.seq = seq;
+        e.client = client;
+        L->obSeq[obSeqN] = static_cast<uint8_t>(slot);
+      }
+    }
+    waveSync();
+    obLive++;
+    obSeqN++;
+    bool exists;
+    const int at = findStart(slot, &exists);
+    if (!exists) {
+      if (obStartN >= kObCap) return fail(FMT_E_CAPACITY);
+      for (int i = obStartN; i > at; i--) {
+        const uint8_t v = static_cast<uint8_t>(obU(L->obStart, i - 1));
+        waveSync();
+        L->obStart[i] = v;
+      }
+      L->obStart[at] = static_cast<uint8_t>(slot);
+      waveSync();
+      obStartN++;
+    }
+    return true;
+  }
+
+  // Obliterates.setMinSeq (mergeTree.ts:537-545): drop obliterates at/below minSeq from both lists
+  // and remove their references.
+  FMT_DEV void obSetMinSeq() {
+    int k = 0;
+    for (; k < obSeqN && uni(L->ob[obU(L->obSeq, k)].seq) <= minSeq; k++) {
+      const int slot = obU(L->obSeq, k);
+      bool exists;
+      const int at = findStart(slot, &exists);
+      if (exists) {
+        for (int i = at; i + 1 < obStartN; i++) {
+          const uint8_t v = static_cast<uint8_t>(obU(L->obStart, i + 1));
+          waveSync();
+          L->obStart[i] = v;
+        }
+        waveSync();
+        obStartN--;
+      }
+      L->ob[slot].startId = 0;  // removeLocalReferencePosition
+      L->ob[slot].endId = 0;
+      waveSync();
+      if (!exists) continue;  // still listed in startOrdered: its slot stays taken
+      L->obUsed[slot] = 0;
+      waveSync();
+      obLive--;
+    }
+    if (k > 0) {
+      for (int i = 0; i + k < obSeqN; i++) {
+        const uint8_t v = static_cast<uint8_t>(obU(L->obSeq, i + k));
+        waveSync();
+        L->obSeq[i] = v;
+      }
+      waveSync();
+      obSeqN -= k;
+    }
+  }
+
+  // blockInsert's obliterate branch (mergeTree.ts:1642-1746) for the new leaf `id`: every overlapping
+  // obliterate the inserter had not seen (seq > refSeq); when one is from another client and the
+  // newest is not the inserter's own, the leaf starts out removed by those other clients' ones.
+  FMT_DEV void obliterateOnInsert(uint32_t id, int refSeq, int client) {
+    const int64_t k = ordOf(id);
+    int minSeqOther = kNotRemoved, newestSeq = -1, newestClient = -1, firstCl = 0;
+    uint32_t mlo = 0, mhi = 0;
+    bool any = false;
+    for (int i = 0; i < obStartN; i++) {  // Obliterates.findOverlapping (:566-582)
+      const int slot = obU(L->obStart, i);
+      const int64_t si = ordOf(uni(L->ob[slot].startId));
+      if (!(si >= 0 && si <= k)) break;
+      const int64_t ei = ordOf(uni(L->ob[slot].endId));
+      if (!(ei >= 0 && ei >= k)) continue;
+      const int oseq = uni(L->ob[slot].seq), ocl = uni(L->ob[slot].client);
+      if (oseq <= refSeq) continue;
+      if (ocl != client) {
+        any = true;
+        if (ocl < 32) mlo |= 1u << ocl;
+        else mhi |= 1u << (ocl - 32);
+        if (oseq < minSeqOther) {
+          minSeqOther = oseq;
+          firstCl = ocl;
+        }
+      }
+      if (oseq > newestSeq) {
+        newestSeq = oseq;
+        newestClient = ocl;
+      }
+    }
+    if (!(any && newestClient != client)) return;
+    uint32_t b;
+    int kk;
+    locate(id, &b, &kk);
+    const size_t i = li(b, kk);
+    st1(S.lRm + i, static_cast<int32_t>(minSeqOther));
+    st1(S.lMlo + i, mlo);
+    st1(S.lMhi + i, mhi);
+    const uint32_t w = ldu(S.winIdx + id);  // (a new leaf: always a window entry)
+    const bool more = __builtin_popcount(mlo) + __builtin_popcount(mhi) > 1;
+    st1(wWord(w, 1), static_cast<uint32_t>(minSeqOther));
+    st1(wWord3(w), (ldu(wWord3(w)) & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(firstCl) << 8) | (more ? 1u << 16 : 0u));
+    st1(S.wMask + 2 * w, mlo);
+    st1(S.wMask + 2 * w + 1, mhi);
+    invalidate();
+  }
+
+  // ensureIntervalBoundary (mergeTree.ts:1798-1808): split the leaf that strictly contains pos in
+  // the op's view.
+  FMT_DEV bool splitAt(int pos, int r, int c) {
+    const Hit h = find(pos, r, c);
+    if (!h.found || h.st >= pos) return status == FMT_OK;
+    BlockRegs R;
+    uint32_t rb;
+    int rk;
+    return splitLeaf(R, h.blk, h.k, pos - h.st, nullptr, &rb, &rk);
+  }
+
+  // obliterateRangeSided (mergeTree.ts:2083-2260). Places {pos, before?}: a non-sided op is
+  // {pos1, Before} .. {pos2 - 1, After} (:2282-2286); a sided one carries its sides in flags. The
+  // boundaries are the places' Before edges (:2090-2091). nodeMap(start.pos, end.pos + 1) under
+  // RemoteObliteratePerspective visits a leaf when it has length in the op's view or is not removed
+  // at all (so concurrent inserts strictly inside are caught): st < end.pos + 1, start.pos < st + vis;
+  // markRemoved skips the exclusive endpoints (:2145-2152). Endpoint references go to the leaves
+  // holding start.pos and end.pos in the op's view (getContainingSegment, :858-886).
+  FMT_DEV void applyObliterate(const fmt_mt_op& op) {
+    ProfScope ps_(prof[13]);
+    const int r = op.ref_seq, c = op.client, seq = op.seq;
+    const bool sided = op.type == FMT_MT_OBLITERATE_SIDED;
+    const bool sB = !sided || (op.flags & FMT_MT_F_START_BEFORE) != 0;
+    const bool eB = sided && (op.flags & FMT_MT_F_END_BEFORE) != 0;
+    const int sPl = op.pos1, ePl = sided ? op.pos2 : op.pos2 - 1;
+    const int startPos = sB ? sPl : sPl + 1, endPos = eB ? ePl : ePl + 1, endW = ePl + 1;
+    if (!splitAt(startPos, r, c) || !splitAt(endPos, r, c)) return;
+    const Hit h = find(sPl, r, c);  // every leaf before it ends at or before sPl: no hit
+    if (!h.found) {
+      fail(FMT_E_DATA);  // "segments cannot be undefined"
+      return;
+    }
+    uint32_t sId = 0, eId = 0;
+    int sOff = 0, eOff = 0;
+    uint32_t b = h.blk;
+    int k = h.k, pos = h.st;
+    while (b != kNone && pos < endW) {
+      const uint32_t cnt = ldu(S.bCount + b);
+      const uint32_t g = ldu(S.bGroup + b), s = ldu(S.bSlot + b);
+      bool scour = ldi(S.bScour + b) == 1;
+      Lane<uint32_t> f[8], wi, vis;
+      FOR_LANES(l) {
+        const size_t i = li(b, l < static_cast<int>(cnt) ? l : 0);
+        LANE(f[0]) = rd(S.lLen + i);
+        LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
+        LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
+        LANE(f[3]) = rd(S.lMlo + i);
+        LANE(f[4]) = rd(S.lMhi + i);
+        LANE(f[5]) = rd(S.lId + i);
+        LANE(f[6]) = rd(S.lText + i);
+        LANE(f[7]) = rd(S.lMeta + i);
+      }
+      FOR_LANES(l) {
+        LANE(wi) = rd(S.winIdx + LANE(f[5]));
+        LANE(vis) = l < static_cast<int>(cnt)
+                        ? static_cast<uint32_t>(visOf(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
+                                                      LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c))
+                        : 0u;
+      }
+      int stableDelta = 0;
+      for (; k < static_cast<int>(cnt) && pos < endW; k++) {
+        const int v = static_cast<int>(readlane(vis, k));
+        const uint32_t len = readlane(f[0], k);
+        const bool removed = static_cast<int32_t>(readlane(f[2], k)) != kNotRemoved;
+        if (v > 0 && sId == 0 && pos <= sPl && sPl < pos + v) {
+          sId = readlane(f[5], k);
+          sOff = sPl - pos;
+        }
+        if (v > 0 && eId == 0 && pos <= ePl && ePl < pos + v) {
+          eId = readlane(f[5], k);
+          eOff = ePl - pos;
+        }
+        const bool excl = (!sB && startPos == pos + static_cast<int>(len)) || (eB && endPos == pos && v > 0);
+        if (!(v == 0 && removed) && !excl && sPl < pos + v) {
+          Leaf x;
+          x.len = len;
+          x.ins = static_cast<int32_t>(readlane(f[1], k));
+          x.rm = static_cast<int32_t>(readlane(f[2], k));
+          x.mlo = readlane(f[3], k);
+          x.mhi = readlane(f[4], k);
+          x.id = readlane(f[5], k);
+          x.text = readlane(f[6], k);
+          x.meta = readlane(f[7], k);
+          stableDelta += removeLeaf(b, k, x, seq, c, readlane(wi, k), g);
+          if (status != FMT_OK) return;
+          if (!scour && seq > curSeq) {  // addToLRUSet (mergeTree.ts:812-822), once per block
+            st1(S.bScour + b, 1);
+            heapAdd(seq, x.id);
+            scour = true;
+            if (status != FMT_OK) return;
+          }
+        }
+        pos += v;
+      }
+      if (stableDelta) addStableAt(g, s, stableDelta);
+      if (pos < endW) {
+        b = nextBlockAt(g, s);
+        k = 0;
+      }
+    }
+    if (sId == 0 || eId == 0) {
+      fail(FMT_E_DATA);
+      return;
+    }
+    obAdd(sId, sOff, eId, eOff, seq, c);
+  }
+
   // ------------------------------------------------------------------ minSeq
   // Window entries whose insert and first remove are both at/below minSeq graduate into the stable
   // sums (mergeTree.ts:1147-1166 moves the window; their length is now the same for every view).
@@ -1733,6 +2066,33 @@ class HugeDoc {
     int total;
     uint32_t mergeBase;
   };
+
+  // LocalReferenceCollection.append (localReference.ts:233-251) for a scour plan: the references of a
+  // leaf appended onto its run head move to the head, offset by the run's length before the leaf.
+  FMT_DEV void obRefsFromPlan(const ScourPlan& P, const Lane<uint32_t>* f) {
+    if (obLive == 0 || P.heads == 0) return;
+    Lane<uint32_t> srcU;
+    Lane<int> dd;
+    FOR_LANES(l) {
+      LANE(srcU) = static_cast<uint32_t>(LANE(P.srcOf));
+      LANE(dd) = LANE(P.dst) < 0 ? 0 : LANE(P.dst);
+    }
+    const Lane<uint32_t> headSrc = gather(srcU, dd);
+    Lane<int> hs;
+    Lane<bool> mv;
+    FOR_LANES(l) {
+      LANE(hs) = static_cast<int>(LANE(headSrc));
+      const int d = LANE(P.dst);
+      LANE(mv) = d >= 0 && ((P.heads >> d) & 1ull) != 0 && LANE(headSrc) != static_cast<uint32_t>(l);
+    }
+    const Lane<uint32_t> headId = gather(f[5], hs), headFlat = gather(P.flat, hs);
+    uint64_t m = ballot(mv);
+    while (m) {
+      const int s = ctz64(m);
+      m &= m - 1;
+      obRefsMove(readlane(f[5], s), readlane(headId, s), 0, static_cast<int>(readlane(P.flat, s) - readlane(headFlat, s)));
+    }
+  }
   FMT_DEV bool scourPlan(const Lane<uint32_t>* f, const Lane<uint32_t>& lastCh, const Lane<int>& cntL, int nBlk, ScourPlan& P) {
     if (!scourDecideWide(f, lastCh, cntL, P)) scourDecideSerial(f, lastCh, cntL, nBlk, P);
     return scourText(f, P);
@@ -1920,6 +2280,7 @@ class HugeDoc {
     ScourPlan P;
     if (!scourPlan(f, lastCh, cntL, 1, P)) return cnt;
     if (P.total == cnt) return cnt;  // nothing dropped or appended
+    obRefsFromPlan(P, f);
     Lane<uint32_t> g8[8];
 #pragma unroll
     for (int x = 0; x < 8; x++) g8[x] = gather(f[x], P.srcOf);
@@ -1971,6 +2332,7 @@ class HugeDoc {
     loadOctets(chl, cntL, f, lastCh);
     ScourPlan P;
     if (!scourPlan(f, lastCh, cntL, pc, P)) return;
+    obRefsFromPlan(P, f);
     const int total = P.total;
     const uint64_t heads = P.heads;
     const Lane<int>& srcOf = P.srcOf;
@@ -2310,7 +2672,7 @@ class HugeDoc {
       waveExclusiveSum(acc, &tot);
       L->gOrder[g] = static_cast<uint16_t>(g);
       L->gStable[g] = static_cast<int32_t>(tot);
-      L->gCount[g] = hi - lo;
+      L->gCount[g] = static_cast<uint16_t>(hi - lo);
       L->gCorr[g] = 0;
       waveSync();
     }
@@ -2394,8 +2756,10 @@ class HugeDoc {
       else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
         if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
         else applyRange(op);
+      } else if (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED) {
+        applyObliterate(op);
       } else {
-        fail(FMT_E_UNSUPPORTED);  // obliterate: the small / large tiers only
+        fail(FMT_E_UNSUPPORTED);
       }
       if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER)) != 0) fail(FMT_E_UNSUPPORTED);
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
@@ -2410,6 +2774,7 @@ class HugeDoc {
           if (op.min_seq <= minSeq) break;
           minSeq = op.min_seq;
           graduate();
+          if (obSeqN > 0) obSetMinSeq();
         }
         zamboni();
       }
@@ -2619,6 +2984,11 @@ class HugeDoc {
     nProps = 0;
     textTop = S.textLen;
     status = FMT_OK;
+    obLive = obSeqN = obStartN = 0;
+    FOR_LANES(l) {
+      for (int k = l; k < kObCap; k += 64) L->obUsed[k] = 0;
+    }
+    waveSync();
     load();
     if (status == FMT_OK) replay();
   }

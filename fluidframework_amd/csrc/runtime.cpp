@@ -120,7 +120,7 @@ struct fmt_ctx {
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
   // documents that outgrow the large tier replay again, from their start, in the huge tier when
-  // they hold nothing it does not (mtHugeOk: no obliterate, catch-up / remove-order recording,
+  // they hold nothing it does not (mtHugeOk: no catch-up / remove-order recording,
   // relative positions, annotate-adjust or SnapshotV1 merge info; no body chunk); their starts
   std::vector<uint8_t> mtHugeOk;
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
@@ -828,7 +828,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->mtInitChars = initChars;
   // Huge documents: a summary-loaded document with more segments or text than the large tier holds
   // is replayed by the huge-document engine (huge_engine.h: one wave, state in HBM). It loads from
-  // one header chunk; catch-up / remove-order recording and obliterates stay with the other tiers.
+  // one header chunk; catch-up / remove-order recording stays with the other tiers.
   for (auto& h : c->huge)
     for (void* p : h.allocs) (void)hipFree(p);
   c->huge.clear();
@@ -843,7 +843,6 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       const fmt_mt_op& op = b->ops[i];
       if (op.type == FMT_MT_INSERT) chars += op.len;
       if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) ||
-          op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED ||
           (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
         ok = 0;
     }
