@@ -148,7 +148,7 @@ struct HugeState {
   // text arena (batch text, then the merge area) and prop sets
   uint16_t* text;
   uint64_t textLen;   // batch text (read-only part)
-  uint64_t textCap;
+  uint64_t textCap;   // end of the merge area: two halves of (textCap - textLen) / 2 units, one in use
   uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
 };
 
@@ -221,13 +221,14 @@ class HugeDoc {
   int curSeq = 0, minSeq = 0;
   int status = FMT_OK, failSeq = 0;
   uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
-  int obLive = 0, obSeqN = 0, obStartN = 0;  // live obliterates: slots in use, seqOrdered / startOrdered lengths
+  int obLive = 0, obSeqN = 0, obStartN = 0;
+  uint64_t mergeLo = 0, mergeHi = 0;  // the merge-area half in use  // live obliterates: slots in use, seqOrdered / startOrdered lengths
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
   // 12 insert, 13 range ops, 14 leaf split, 15 interior pack; counts: 16 group passes, 17 slot
   // passes, 18 Σ window entries at group passes, 19 Σ groups at group passes; 20 wave 0's window
-  // share time, 21 group scan time
+  // share time, 21 group scan time, 22 merge-area compactions, 23 merge-area units in use
   static constexpr int kProf = 24;
   uint64_t prof[kProf] = {};
   struct ProfScope {
@@ -252,7 +253,12 @@ class HugeDoc {
     epoch++;
   }
 
-  FMT_DEV bool fail(int code) {
+  FMT_DEV bool fail(int code, int line = __builtin_LINE()) {
+#ifdef FMT_HUGE_CHECK
+    if (status == FMT_OK && std::getenv("FMT_HUGE_TRACE")) std::fprintf(stderr, "huge_engine.h:%d fails %d\n", line, code);
+#else
+    (void)line;
+#endif
     if (status == FMT_OK) status = code;
     return false;
   }
@@ -2206,6 +2212,88 @@ class HugeDoc {
     }
   }
 
+  // Room in the merge area for the loaded octets' text (every merged run is at most all of it).
+  FMT_DEV bool textRoom(const Lane<uint32_t>* f, const Lane<int>& cntL) const {
+    Lane<uint32_t> len;
+    FOR_LANES(l) { LANE(len) = (l & 7) < LANE(cntL) ? LANE(f[0]) : 0u; }
+    uint32_t total;
+    waveExclusiveSum(len, &total);
+    return textTop + total <= mergeHi;
+  }
+
+  // The merge area's half is full: copy the text of every leaf in the tree that lives in it, in
+  // document order, into the other half (zamboni appends copy whole runs, so a long run that keeps
+  // absorbing short acked leaves would otherwise fill any fixed arena). Eight blocks per step.
+  FMT_DEV bool compactText() {
+    const uint64_t half = (S.textCap - S.textLen) / 2;
+    const uint64_t lo = mergeLo == S.textLen ? S.textLen + half : S.textLen;
+    uint64_t top = lo;
+    prof[22]++;
+    for (int k = 0; k < nGroups && status == FMT_OK; k++) {
+      const uint32_t g = L->gOrder[k];
+      const int cnt = static_cast<int>(L->gCount[g]);
+      const uint32_t* sb = slotBlkPtr(g);
+      for (int s0 = 0; s0 < cnt; s0 += 8) {
+        Lane<uint32_t> mv, tx;
+        Lane<size_t> idx;
+        FOR_LANES(l) {
+          const int s = s0 + l / 8, j = l % 8;
+          uint32_t n = 0, t = 0;
+          size_t i = 0;
+          if (s < cnt) {
+            const uint32_t b = rd(sb + s);
+            if (j < static_cast<int>(rd(S.bCount + b))) {
+              i = li(b, j);
+              t = rd(S.lText + i);
+              if (t >= mergeLo && t < mergeHi) n = rd(S.lLen + i);
+            }
+          }
+          LANE(mv) = n;
+          LANE(tx) = t;
+          LANE(idx) = i;
+        }
+        uint32_t total;
+        const Lane<uint32_t> ex = waveExclusiveSum(mv, &total);
+        if (top + total > lo + half) {
+          fail(FMT_E_CAPACITY);
+          break;
+        }
+        FOR_LANES(l) {
+          if (LANE(mv)) S.lText[LANE(idx)] = static_cast<uint32_t>(top + LANE(ex));
+        }
+        // unit t of this step comes from the last lane whose start ex <= t (gathers, as scourText)
+        for (uint32_t base = 0; base < total; base += 64) {
+          Lane<int> pos;
+          FOR_LANES(l) { LANE(pos) = 0; }
+          for (int step = 32; step >= 1; step >>= 1) {
+            Lane<int> cand;
+            FOR_LANES(l) { LANE(cand) = LANE(pos) + step; }
+            const Lane<uint32_t> v = gather(ex, cand);
+            FOR_LANES(l) {
+              if (LANE(v) <= base + static_cast<uint32_t>(l)) LANE(pos) = LANE(cand);
+            }
+          }
+          const Lane<uint32_t> st = gather(ex, pos), sx = gather(tx, pos);
+          Lane<uint32_t> v;
+          FOR_LANES(l) {
+            const uint32_t t = base + l;
+            LANE(v) = t < total ? loadWg(S.text + LANE(sx) + (t - LANE(st))) : 0u;
+          }
+          FOR_LANES(l) {
+            const uint32_t t = base + l;
+            if (t < total) S.text[top + t] = static_cast<uint16_t>(LANE(v));
+          }
+        }
+        waveSync();
+        top += total;
+      }
+    }
+    mergeLo = lo;
+    mergeHi = lo + half;
+    textTop = top;
+    return status == FMT_OK;
+  }
+
   // The merged runs' text, concatenated in lane order, into the merge area.
   FMT_DEV bool scourText(const Lane<uint32_t>* f, ScourPlan& P) {
     Lane<uint32_t> member;
@@ -2217,7 +2305,7 @@ class HugeDoc {
     P.flat = waveExclusiveSum(member, &need);
     P.mergeBase = static_cast<uint32_t>(textTop);
     if (!need) return true;
-    if (textTop + need > S.textCap) return fail(FMT_E_CAPACITY);
+    if (textTop + need > mergeHi) return fail(FMT_E_CAPACITY);
     for (uint32_t base = 0; base < need; base += 64) {
       // source lane of unit t: the last lane whose flat start is <= t (binary search by gathers;
       // flat is non-decreasing over lanes)
@@ -2277,6 +2365,10 @@ class HugeDoc {
       LANE(cntL) = l < 8 ? cnt : 0;
     }
     loadOctets(blk, cntL, f, lastCh);
+    if (!textRoom(f, cntL)) {
+      if (!compactText()) return cnt;
+      loadOctets(blk, cntL, f, lastCh);
+    }
     ScourPlan P;
     if (!scourPlan(f, lastCh, cntL, 1, P)) return cnt;
     if (P.total == cnt) return cnt;  // nothing dropped or appended
@@ -2330,6 +2422,10 @@ class HugeDoc {
     FOR_LANES(l) { LANE(chl) = (l >> 3) < pc ? rd(S.bChild + (static_cast<size_t>(p) * 8 + (l >> 3))) : 0u; }
     FOR_LANES(l) { LANE(cntL) = (l >> 3) < pc ? static_cast<int>(rd(S.bCount + LANE(chl))) : 0; }
     loadOctets(chl, cntL, f, lastCh);
+    if (!textRoom(f, cntL)) {
+      if (!compactText()) return;
+      loadOctets(chl, cntL, f, lastCh);
+    }
     ScourPlan P;
     if (!scourPlan(f, lastCh, cntL, pc, P)) return;
     obRefsFromPlan(P, f);
@@ -2983,6 +3079,8 @@ class HugeDoc {
     nFree = 0;
     nProps = 0;
     textTop = S.textLen;
+    mergeLo = S.textLen;
+    mergeHi = S.textLen + (S.textCap - S.textLen) / 2;
     status = FMT_OK;
     obLive = obSeqN = obStartN = 0;
     FOR_LANES(l) {

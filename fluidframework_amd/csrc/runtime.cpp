@@ -508,7 +508,10 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
   S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
   S.winCap = S.idCap;  // every leaf can be in the window (a wide remove puts many there)
-  const uint64_t textCap = std::min<uint64_t>(textLen + textPerOp * nOps + 65536, 0xFFFFFFF0ull);
+  // the merge area: two halves (huge_engine.h compactText), each able to hold the document's whole
+  // text twice over (its live merged text plus one run as long as the document)
+  const uint64_t merge = std::max<uint64_t>(textPerOp * nOps + 65536, 4 * docChars + 131072);
+  const uint64_t textCap = std::min<uint64_t>(textLen + merge, 0xFFFFFFF0ull);
   const size_t nl = static_cast<size_t>(S.blockCap) * 8, nb = S.blockCap;
   void* p;
 #define FMT_ALLOC(field, T, count)                        \

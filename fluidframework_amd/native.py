@@ -389,7 +389,7 @@ class Engine:
         names = ["replay", "window_groups", "window_slots", "zamboni", "graduate", "load", "output", "find",
                  "scour", "pack_leaf_parent", "slot_shift", "heap", "insert", "range", "split", "pack_interior",
                  "n_group_passes", "n_slot_passes", "sum_window_entries", "sum_groups", "window_share_w0", "group_scan",
-                 "unused22", "unused23"]
+                 "text_compactions", "merge_units_in_use"]
         return dict(zip(names, (int(x) for x in out)))
 
     def mt_remove_order(self, doc: int, hdr=None) -> np.ndarray:

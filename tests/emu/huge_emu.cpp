@@ -3,6 +3,7 @@
 // its logic against the oracle without a GPU. Never loaded by the product.
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -37,7 +38,12 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
   S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
   S.winCap = S.idCap;  // every leaf can be in the window (wide removes)
-  uint64_t textCap = b->text_len + (loaded ? 256 : 1024) * nOps + 65536;  // (runtime.cpp setupHugeDoc)
+  uint64_t docChars = initSeg.len;  // (runtime.cpp setupHugeDoc; the snapshot's text counts below)
+  for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
+    if (b->ops[i].type == FMT_MT_INSERT) docChars += b->ops[i].len;
+  if (loaded)
+    for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header; k++) docChars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
+  uint64_t textCap = b->text_len + std::max<uint64_t>((loaded ? 256 : 1024) * nOps + 65536, 4 * docChars + 131072);
   if (const char* e = std::getenv("FMT_EMU_TEXTCAP")) textCap = std::strtoull(e, nullptr, 10);
   std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6);
   std::vector<int32_t> i32(static_cast<size_t>(S.blockCap) * 8 * 2);
@@ -83,7 +89,9 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
   doc->run(in);
   doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props);
-  if (std::getenv("FMT_EMU_TEXTCAP")) std::fprintf(stderr, "textTop %llu of %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap);
+  if (std::getenv("FMT_EMU_TEXTCAP"))
+    std::fprintf(stderr, "textTop %llu of %llu, compactions %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap,
+                 (unsigned long long)doc->prof[22]);
   return hdr->status;
 }
 

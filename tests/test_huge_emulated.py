@@ -93,3 +93,19 @@ def test_huge_engine_loaded_markers(orc):
     assert int(got[0]["status"]) == 0
     assert compare_doc(exp, got) == []
     assert int((exp[1]["pad"] & MT_LEAF_MARKER != 0).sum()) > 50
+
+
+def test_huge_engine_merge_area_compaction(orc, monkeypatch, capfd):
+    """A tight merge area (4x the document's text) on a T3-shaped document with 16-slot groups: the
+    merge area compacts into its other half, walking every group, and the state still == oracle."""
+    import re
+
+    batch = workloads.t3_stream(3000, 6000, n_clients=31, max_lag=500, max_range=8, seed=5)
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    doc_chars = int(batch.snapshot_segs["len"].sum()) + int(batch.ops["len"][batch.ops["type"] == 0].sum())
+    monkeypatch.setenv("FMT_EMU_TEXTCAP", str(len(batch.text) + 4 * doc_chars + 64))
+    got = emu_huge_replay(batch, tiny_groups=True)
+    assert int(re.search(r"compactions (\d+)", capfd.readouterr().err).group(1)) >= 1
+    assert int(got[0]["status"]) == 0
+    assert compare_doc(exp, got) == []

@@ -49,16 +49,38 @@ def test_emulated_huge_tier_sided_obliterates(orc, seed):
         assert compare_doc(exp, got) == [], name
 
 
-def test_emulated_huge_tier_scaled_obliterate_farm(orc):
-    """One farm on a 135,000-unit initial text (past the large tier): emulated huge engine == oracle."""
+def _one(batch, d):
     from dataclasses import replace
 
-    batch = long_obliterate_farms(extra=135000)
-    one = replace(batch, ops=batch.ops[: int(batch.doc_op_offsets[1])], doc_op_offsets=batch.doc_op_offsets[:2].copy(),
-                  doc_init=batch.doc_init[:1].copy())
+    o0, o1 = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
+    return replace(batch, ops=batch.ops[o0:o1], doc_op_offsets=np.array([0, o1 - o0], np.uint64),
+                   doc_init=batch.doc_init[d : d + 1].copy())
+
+
+@pytest.mark.parametrize("doc", [0, 3, 4, 5])
+def test_emulated_huge_tier_scaled_obliterate_farm(orc, doc):
+    """A farm on a 135,000-unit initial text (past the large tier): emulated huge engine == oracle.
+    (Farms 3-5 keep appending short acked leaves onto the long initial run: zamboni recopies the run
+    each time, which the merge area absorbs by compacting into its other half.)"""
+    one = _one(long_obliterate_farms(extra=135000), doc)
     exp = _oracle(orc, one)
     got = emu_huge_replay(one, 0)
     assert int(got[0]["status"]) == 0 and int(got[0]["visible_len"]) > 131071
+    assert compare_doc(exp, got) == []
+
+
+def test_emulated_merge_area_compaction(orc, monkeypatch, capfd):
+    """A merge area of 4x the document's text forces compactions: the state still == oracle."""
+    import re
+
+    one = _one(long_obliterate_farms(extra=135000), 3)
+    exp = _oracle(orc, one)
+    doc_chars = int(one.doc_init[0][1]) + int(one.ops["len"][one.ops["type"] == 0].sum())
+    monkeypatch.setenv("FMT_EMU_TEXTCAP", str(len(one.text) + 4 * doc_chars + 64))
+    got = emu_huge_replay(one, 0)
+    n = int(re.search(r"compactions (\d+)", capfd.readouterr().err).group(1))
+    assert n >= 3
+    assert int(got[0]["status"]) == 0
     assert compare_doc(exp, got) == []
 
 
