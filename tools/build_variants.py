@@ -24,7 +24,7 @@ def _export_rev(rev, root):
             open(dst, "wb").write(data)
 
 
-def build(name, edits, rev=None):
+def build(name, edits, rev=None, flags=()):
     root = os.path.join(REPO, "build", "variants", name)
     csrc = os.path.join(root, "fluidframework_amd", "csrc")
     shutil.rmtree(root, ignore_errors=True)
@@ -44,16 +44,16 @@ def build(name, edits, rev=None):
     for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip"]:
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
-               "-x", "hip", "-c", "-o", o, os.path.join(csrc, f)]
+               *flags, "-x", "hip", "-c", "-o", o, os.path.join(csrc, f)]
         subprocess.run(cmd, check=True)
         objs.append(o)
     out = os.path.join(root, "libfmt.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", out] + objs, check=True)
-    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-variable",
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-variable", *flags,
                         "-c", "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage",
                         os.path.join(csrc, "mergetree_compact.hip")], capture_output=True, text=True)
     info = [l.split("remark:")[1].strip() for l in r.stderr.splitlines()
-            if "remark" in l and any(k in l for k in ("VGPRs:", "AGPRs", "Scratch", "Occupancy"))]
+            if "remark" in l and any(k in l for k in ("VGPRs:", "AGPRs", "Scratch", "Occupancy", "Spill"))]
     print(name, "|", "; ".join(info))
     return out
 
@@ -118,6 +118,14 @@ VARIANTS = {
     "map_nt_w16": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 16;")],
     "map_nt_w1": [MAP_NT, ("map_lww.hip", "constexpr int kWaves = 4;", "constexpr int kWaves = 1;")],
 }
+# compiler-flag variants (scheduler strategies) of the current sources
+FLAGS = {
+    "trk": ["-mllvm", "-amdgpu-use-amdgpu-trackers"],
+    "ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "mclause": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+    "bias100": ["-mllvm", "-amdgpu-schedule-metric-bias=100"],
+    "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
+}
 REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD"}  # committed engines to A/B against
 
 
@@ -126,5 +134,7 @@ if __name__ == "__main__":
     for n in names:
         if n in REVS:
             build(n, [], rev=REVS[n])
+        elif n in FLAGS:
+            build(n, [], flags=FLAGS[n])
         else:
             build(n, VARIANTS[n])
