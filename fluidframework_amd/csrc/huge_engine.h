@@ -1490,7 +1490,8 @@ class HugeDoc {
       b = lastBlk;
       k = -1;
     }
-    if (op.len == 0) return;
+    const uint32_t opLen = op.len | (op.flags & FMT_MT_F_LEN_HI_MASK);
+    if (opLen == 0) return;
     if (nextId >= S.idCap) {
       fail(FMT_E_CAPACITY);
       return;
@@ -1507,7 +1508,7 @@ class HugeDoc {
     if (R.b != b) loadBlock(b, R);  // (after a split without overflow the block is still in registers)
     if (k < 0) k = R.cnt;
     Leaf x;
-    x.len = op.len;
+    x.len = opLen;
     x.ins = op.seq;
     x.rm = kNotRemoved;
     x.mlo = x.mhi = 0;

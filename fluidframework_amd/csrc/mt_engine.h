@@ -1464,7 +1464,7 @@ class Doc {
   // Returns the new leaf's index, or -1 (nothing inserted, or failure).
   FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0, int clientArg = 0x7fff, bool boundary = true) {
     const int refSeq = op.ref_seq, client = clientArg != 0x7fff ? clientArg : op.client, seq = op.seq;
-    const int pos = op.pos1, len = op.len;
+    const int pos = op.pos1, len = static_cast<int>(opLen(op));
     const int nr = rows();
     Lane<VR> vis, st;
     visLengths(refSeq, client, vis, nr);
@@ -2567,6 +2567,7 @@ class Doc {
   FMT_DEV static uint32_t recWord(const OpRec& r, int k) { return readlane(r, k); }
 #endif
 
+  FMT_DEV static uint32_t opLen(const fmt_mt_op& op) { return op.len | (op.flags & FMT_MT_F_LEN_HI_MASK); }
   FMT_DEV static fmt_mt_op decodeOp(const OpRec& rec) {
     fmt_mt_op op;
     op.seq = static_cast<int32_t>(recWord(rec, 0));
@@ -2585,7 +2586,7 @@ class Doc {
 
   FMT_DEV Lane<uint32_t> fetchText(const OpRec& rec) const {
     const uint32_t lct = recWord(rec, 6);
-    const int len = (lct >> 24) == FMT_MT_INSERT ? static_cast<int>(lct & 0xFFFF) : 0;
+    const int len = (lct >> 24) == FMT_MT_INSERT ? static_cast<int>((lct & 0xFFFF) | (recWord(rec, 7) & FMT_MT_F_LEN_HI_MASK)) : 0;
     const uint32_t payload = recWord(rec, 5);
     Lane<uint32_t> x;
     FOR_LANES(l) { LANE(x) = l < len ? static_cast<uint32_t>(in.text[payload + l]) : 0u; }
@@ -2607,7 +2608,7 @@ class Doc {
         // 1023 / 1024 lift: an op's splits allocate a few blocks, an annotate a few sets)
         const bool loaderNonCollab = (op.flags & FMT_MT_F_LOADSEG) != 0 && op.client == FMT_MT_CLIENT_NONCOLLAB;
         if (canSave &&
-            (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(op.len) > kCapChars) ||
+            (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(opLen(op)) > kCapChars) ||
              (kSavesBig && ((op.client > kMaxClient && !loaderNonCollab) ||
                             // (margins: plain batches only — obliterate documents near them mostly
                             // finish in this tier, measured on the obliterate farms)

@@ -580,9 +580,9 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
         return setErr(c, FMT_E_DATA, "a loader segment (FMT_MT_F_LOADSEG) without a valid merge-info row");
     }
     if (op.type == FMT_MT_INSERT) {
-      if (static_cast<uint64_t>(op.payload) + op.len > b->text_len)
+      if (static_cast<uint64_t>(op.payload) + fmt_mt_op_len(&op) > b->text_len)
         return setErr(c, FMT_E_DATA, "insert payload outside the text arena");
-      insertChars += op.len;
+      insertChars += fmt_mt_op_len(&op);
     } else if (op.type == FMT_MT_ANNOTATE) {
       if (op.payload >= b->n_props_ops) return setErr(c, FMT_E_DATA, "annotate props op id out of range");
     } else if (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED) {
@@ -844,7 +844,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     uint64_t chars = 0;
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
       const fmt_mt_op& op = b->ops[i];
-      if (op.type == FMT_MT_INSERT) chars += op.len;
+      if (op.type == FMT_MT_INSERT) chars += fmt_mt_op_len(&op);
       if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) ||
           (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
         ok = 0;

@@ -25,6 +25,7 @@ const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate p
 const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER = 0x8000; // Marker segments
 // legacy relativePos1/2 (ops.ts IRelativePosition): pos1/pos2 index the relpos table (fmt_mt_relpos, 16 B)
 const FMT_MT_F_LOADSEG = 256, FMT_MT_CLIENT_NONCOLLAB = 0xfe; // SnapshotV1 body segments with merge info
+const FMT_MT_F_LEN_HI_MASK = 0x00ff0000; // insert length bits 16..23 (fmt.h FMT_MT_F_LEN_HI_SHIFT)
 const FMT_MT_F_REL1 = 64, FMT_MT_F_REL2 = 128, FMT_MT_NO_MARKER = 0xffffffff, FMT_MT_REL_BEFORE = 1;
 const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 // annotate-adjust (fmt.h): props_kv escape, computed value ids, fmt_mt_adjust flags
@@ -509,9 +510,10 @@ class MergeTreeStreamBuilder {
 						}
 					}
 					const r = this.text.push(seg);
-					if (r[1] > 0xffff) throw new UnsupportedOp("insert longer than 65535 UTF-16 units");
+					if (r[1] > 0xffffff) throw new UnsupportedOp("insert longer than 2^24 - 1 UTF-16 units");
 					// pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
-					pos1 = rp[0]; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1];
+					pos1 = rp[0]; pos2 = props === null ? -1 : this.propsOp(props) + 1; payload = r[0]; len = r[1] & 0xffff;
+					flags |= r[1] & FMT_MT_F_LEN_HI_MASK; // length bits 16..23 (fmt.h FMT_MT_F_LEN_HI_SHIFT)
 				}
 			} else if (type === MT_REMOVE) {
 				const rp = this.positions(op, true);

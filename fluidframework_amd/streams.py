@@ -61,6 +61,13 @@ MT_F_START_BEFORE, MT_F_END_BEFORE = 8, 16  # fmt.h FMT_MT_F_START_BEFORE / FMT_
 MT_F_MARKER = 32  # fmt.h FMT_MT_F_MARKER: insert of a Marker segment
 MT_F_REL1, MT_F_REL2 = 64, 128  # fmt.h FMT_MT_F_REL1/REL2: pos1/pos2 index the relpos table
 MT_F_LOADSEG = 256  # fmt.h FMT_MT_F_LOADSEG: a SnapshotV1 body segment the loader appends
+MT_F_LEN_HI_SHIFT, MT_F_LEN_HI_MASK = 16, 0x00FF0000  # fmt.h: bits 16..23 of an insert's length
+MAX_INSERT_UNITS = (1 << 24) - 1
+
+
+def op_len(rec) -> int:
+    """The full length of a packed INSERT record (fmt.h fmt_mt_op_len)."""
+    return int(rec["len"]) | (int(rec["flags"]) & MT_F_LEN_HI_MASK)
 CLIENT_NONCOLLAB_OP = 0xFE  # fmt.h FMT_MT_CLIENT_NONCOLLAB
 # fmt_mt_relpos: an IRelativePosition {id, before, offset} (ops.ts IRelativePosition)
 RELPOS_DTYPE = np.dtype([("marker_id", "<u4"), ("offset", "<i4"), ("flags", "<u4"), ("pad", "<u4")])
@@ -487,11 +494,12 @@ class MergeTreeStreamBuilder:
                 else:
                     raise UnsupportedOp("segment spec")
             off, n = self._text(seg)
-            if n > 0xFFFF:
-                raise UnsupportedOp("insert longer than 65535 UTF-16 units")
+            if n > MAX_INSERT_UNITS:
+                raise UnsupportedOp("insert longer than 2^24 - 1 UTF-16 units")
             # pos2: the segment's props-op id + 1 (TextSegment.make(text, props)); -1: a plain string
             pos2 = -1 if props is None else self._props_op(props) + 1
-            return (seq, ref, msn, p1, pos2, off, n, client, MT_INSERT, rel)
+            # a length past 16 bits keeps its bits 16..23 in flags (FMT_MT_F_LEN_HI_SHIFT)
+            return (seq, ref, msn, p1, pos2, off, n & 0xFFFF, client, MT_INSERT, rel | (n & MT_F_LEN_HI_MASK))
         if t == MT_REMOVE:
             p1, p2, rel = self._positions(op)
             return (seq, ref, msn, p1, p2, 0, 0, client, MT_REMOVE, rel)
@@ -721,7 +729,7 @@ def op_messages(batch, d: int, above_seq: int, names) -> list:
         if int(r["flags"]) & MT_F_GROUP_CONT:
             raise UnsupportedOp("GROUP messages need the original messages")
         if t == MT_INSERT:
-            off, ln = int(r["payload"]), int(r["len"])
+            off, ln = int(r["payload"]), op_len(r)
             op = {"pos1": int(r["pos1"]), "seg": batch.text[off : off + ln].tobytes().decode("utf-16-le", "surrogatepass"),
                   "type": t}
         elif t == MT_ANNOTATE:

@@ -116,6 +116,10 @@ extern "C" {
  * segments without merge info): no interval boundary is made at its position. */
 #define FMT_MT_F_LOADSEG 256u
 #define FMT_MT_CLIENT_NONCOLLAB 0xFEu
+/* INSERT longer than 65535 UTF-16 units (a large paste): flags bits 16..23 hold bits 16..23 of the
+ * length, `len` its low 16 bits (inserts up to 2^24 - 1 units; fmt_mt_op_len). */
+#define FMT_MT_F_LEN_HI_SHIFT 16
+#define FMT_MT_F_LEN_HI_MASK 0x00FF0000u
 typedef struct fmt_mt_op {
   int32_t seq;      /* sequenceNumber */
   int32_t ref_seq;  /* referenceSequenceNumber */
@@ -123,11 +127,15 @@ typedef struct fmt_mt_op {
   int32_t pos1;     /* op.pos1 */
   int32_t pos2;     /* op.pos2; INSERT: props-op id + 1 of a {text, props} segment, <= 0 for a string */
   uint32_t payload; /* INSERT: offset of the text in the UTF-16 arena; ANNOTATE: props-op id */
-  uint16_t len;     /* INSERT: text length in UTF-16 units (> 0) */
+  uint16_t len;     /* INSERT: text length in UTF-16 units (> 0), low 16 bits (FMT_MT_F_LEN_HI_SHIFT) */
   uint8_t client;   /* short client id (client.ts:831-855): 1..63 in order of first appearance */
   uint8_t type;     /* FMT_MT_* */
   uint32_t flags;   /* FMT_MT_F_* */
 } fmt_mt_op;
+/* The full length of an INSERT record (len plus the FMT_MT_F_LEN_HI bits). */
+static inline uint32_t fmt_mt_op_len(const fmt_mt_op* op) {
+  return (uint32_t)op->len | (op->flags & FMT_MT_F_LEN_HI_MASK);
+}
 
 /* An IRelativePosition {id, before, offset}: `marker_id` is the value id (props_kv dictionary) of the
  * marker's id string, i.e. the value its "markerId" property holds (FMT_MT_NO_MARKER when the

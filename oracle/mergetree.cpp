@@ -890,7 +890,7 @@ void MergeTree::applyRemote(const fmt_mt_op& opIn, const uint16_t* arena, const 
   switch (op.type) {
     case FMT_MT_INSERT: {
       Seg* s = makeSeg();
-      s->text.assign(reinterpret_cast<const char16_t*>(arena + op.payload), op.len);
+      s->text.assign(reinterpret_cast<const char16_t*>(arena + op.payload), fmt_mt_op_len(&op));
       s->marker = (op.flags & FMT_MT_F_MARKER) != 0;  // Marker.make(refType, props)
       // seg {text, props}: TextSegment.make(text, props) → BaseSegment's `properties = clone(props)`
       // (textSegment.ts:41-52, mergeTreeNodes.ts:343-347; clone = extend({}, props): null values

@@ -40,7 +40,7 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   S.winCap = S.idCap;  // every leaf can be in the window (wide removes)
   uint64_t docChars = initSeg.len;  // (runtime.cpp setupHugeDoc; the snapshot's text counts below)
   for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
-    if (b->ops[i].type == FMT_MT_INSERT) docChars += b->ops[i].len;
+    if (b->ops[i].type == FMT_MT_INSERT) docChars += fmt_mt_op_len(&b->ops[i]);
   if (loaded)
     for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header; k++) docChars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
   uint64_t textCap = b->text_len + std::max<uint64_t>((loaded ? 256 : 1024) * nOps + 65536, 4 * docChars + 131072);
