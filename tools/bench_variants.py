@@ -22,7 +22,9 @@ def main():
     ap.add_argument("--docs", type=int, default=20000)
     ap.add_argument("--unique", type=int, default=2000)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--workload", choices=["mt", "map"], default="mt")
+    ap.add_argument("--workload", choices=["mt", "map", "t3"], default="mt")
+    ap.add_argument("--segments", type=int, default=2_000_000, help="t3: segments of the loaded document")
+    ap.add_argument("--t3-ops", type=int, default=200_000, help="t3: ops replayed")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     paths = {os.path.basename(os.path.dirname(p)): p for p in glob.glob(os.path.join(REPO, "build/variants/*/libfmt.so"))}
@@ -30,7 +32,10 @@ def main():
         paths = {k: v for k, v in paths.items() if k in a.variants}
     if a.workload == "map":
         return bench_map(a, paths)
-    batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
+    if a.workload == "t3":
+        batch = workloads.t3_stream(a.segments, a.t3_ops)
+    else:
+        batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
     ref = native.Engine(0)
     ref.mt_load(batch)
     ref.mt_run()

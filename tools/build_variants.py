@@ -40,8 +40,8 @@ def build(name, edits, rev=None, flags=()):
         assert old in s, (name, fname, old[:50])
         open(p, "w").write(s.replace(old, new))
     # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc)
-    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o", "hugedoc.o")]
-    for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip"]:
+    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o")]
+    for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip", "hugedoc.hip"]:
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
                *flags, "-x", "hip", "-c", "-o", o, os.path.join(csrc, f)]
@@ -91,7 +91,11 @@ NOLOAD = ("mt_engine.h", "    if (in.loaded) loadSnapshot();", "    if (false) l
 CW3 = ("mergetree_compact.hip", "launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 4>",
        "launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 3>")  # the round-2 occupancy
 
+HW8 = [("huge_engine.h", "  static constexpr int kWaves = 4;", "  static constexpr int kWaves = 8;"),
+       ("huge_engine.h", "  int32_t glN[4];", "  int32_t glN[8];")]
+
 VARIANTS = {
+    "hw8": HW8,
     "prof": [PROF],
     "cw3": [CW3],
     "noload": [NOLOAD],
