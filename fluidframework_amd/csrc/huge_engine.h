@@ -222,7 +222,8 @@ class HugeDoc {
   int status = FMT_OK, failSeq = 0;
   uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
   int obLive = 0, obSeqN = 0, obStartN = 0;
-  uint64_t mergeLo = 0, mergeHi = 0;  // the merge-area half in use  // live obliterates: slots in use, seqOrdered / startOrdered lengths
+  uint64_t mergeLo = 0, mergeHi = 0;  // the merge-area half in use
+  bool textFull = false;              // a scour plan's runs did not fit the merge area's half  // live obliterates: slots in use, seqOrdered / startOrdered lengths
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
@@ -2104,6 +2105,15 @@ class HugeDoc {
     if (!scourDecideWide(f, lastCh, cntL, P)) scourDecideSerial(f, lastCh, cntL, nBlk, P);
     return scourText(f, P);
   }
+  // The same plan once the merge area was compacted: a run that still does not fit is a capacity
+  // failure (the half holds twice the document's text, so only an undersized arena gets here).
+  FMT_DEV bool scourPlanAfterCompaction(const Lane<uint32_t>* f, const Lane<uint32_t>& lastCh, const Lane<int>& cntL, int nBlk,
+                                        ScourPlan& P) {
+    textFull = false;
+    if (scourPlan(f, lastCh, cntL, nBlk, P)) return true;
+    textFull = false;
+    return fail(FMT_E_CAPACITY);
+  }
 
   // The decisions lane-parallel. Leaf s appends onto its run iff it and leaf s-1 (same block) are
   // acked, not removed and non-empty, s-1 does not end in '\n', their props match, and (s's length
@@ -2213,15 +2223,6 @@ class HugeDoc {
     }
   }
 
-  // Room in the merge area for the loaded octets' text (every merged run is at most all of it).
-  FMT_DEV bool textRoom(const Lane<uint32_t>* f, const Lane<int>& cntL) const {
-    Lane<uint32_t> len;
-    FOR_LANES(l) { LANE(len) = (l & 7) < LANE(cntL) ? LANE(f[0]) : 0u; }
-    uint32_t total;
-    waveExclusiveSum(len, &total);
-    return textTop + total <= mergeHi;
-  }
-
   // The merge area's half is full: copy the text of every leaf in the tree that lives in it, in
   // document order, into the other half (zamboni appends copy whole runs, so a long run that keeps
   // absorbing short acked leaves would otherwise fill any fixed arena). Eight blocks per step.
@@ -2306,7 +2307,10 @@ class HugeDoc {
     P.flat = waveExclusiveSum(member, &need);
     P.mergeBase = static_cast<uint32_t>(textTop);
     if (!need) return true;
-    if (textTop + need > mergeHi) return fail(FMT_E_CAPACITY);
+    if (textTop + need > mergeHi) {  // the caller compacts the merge area and plans again
+      textFull = true;
+      return false;
+    }
     for (uint32_t base = 0; base < need; base += 64) {
       // source lane of unit t: the last lane whose flat start is <= t (binary search by gathers;
       // flat is non-decreasing over lanes)
@@ -2366,12 +2370,12 @@ class HugeDoc {
       LANE(cntL) = l < 8 ? cnt : 0;
     }
     loadOctets(blk, cntL, f, lastCh);
-    if (!textRoom(f, cntL)) {
-      if (!compactText()) return cnt;
-      loadOctets(blk, cntL, f, lastCh);
-    }
     ScourPlan P;
-    if (!scourPlan(f, lastCh, cntL, 1, P)) return cnt;
+    if (!scourPlan(f, lastCh, cntL, 1, P)) {
+      if (!textFull || !compactText()) return cnt;  // (compaction moved the octets' text: reload)
+      loadOctets(blk, cntL, f, lastCh);
+      if (!scourPlanAfterCompaction(f, lastCh, cntL, 1, P)) return cnt;
+    }
     if (P.total == cnt) return cnt;  // nothing dropped or appended
     obRefsFromPlan(P, f);
     Lane<uint32_t> g8[8];
@@ -2423,12 +2427,12 @@ class HugeDoc {
     FOR_LANES(l) { LANE(chl) = (l >> 3) < pc ? rd(S.bChild + (static_cast<size_t>(p) * 8 + (l >> 3))) : 0u; }
     FOR_LANES(l) { LANE(cntL) = (l >> 3) < pc ? static_cast<int>(rd(S.bCount + LANE(chl))) : 0; }
     loadOctets(chl, cntL, f, lastCh);
-    if (!textRoom(f, cntL)) {
-      if (!compactText()) return;
-      loadOctets(chl, cntL, f, lastCh);
-    }
     ScourPlan P;
-    if (!scourPlan(f, lastCh, cntL, pc, P)) return;
+    if (!scourPlan(f, lastCh, cntL, pc, P)) {
+      if (!textFull || !compactText()) return;
+      loadOctets(chl, cntL, f, lastCh);
+      if (!scourPlanAfterCompaction(f, lastCh, cntL, pc, P)) return;
+    }
     obRefsFromPlan(P, f);
     const int total = P.total;
     const uint64_t heads = P.heads;

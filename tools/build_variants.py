@@ -130,7 +130,7 @@ FLAGS = {
     "bias100": ["-mllvm", "-amdgpu-schedule-metric-bias=100"],
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
 }
-REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD"}  # committed engines to A/B against
+REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08"}  # committed engines to A/B against
 
 
 if __name__ == "__main__":
