@@ -91,7 +91,10 @@ def main():
     ap.add_argument("--sparse", action="store_true",
                     help="map: the sparse path (LDS hash reduce-by-key, one entry per live key; any key pool)")
     ap.add_argument("--cpu-sample-docs", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=25.0,
+                    help="CPU baseline sample length (the sample stops early once every document was replayed)")
+    ap.add_argument("--t2-check-docs", type=int, default=1024,
+                    help="t2: documents of every shard replayed by the oracle and compared by state digest")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-js-baseline", action="store_true", help="skip the JS worker_threads baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline pool (0 = every usable host core)")
@@ -204,17 +207,33 @@ def main():
     rec["rank"], rec["doc_lo"], rec["doc_hi"] = rank, doc_base, doc_base + docs
     rec["ops"], rec["elapsed_s"], rec["bytes"] = n_ops, elapsed, bytes_per_launch
     rec["kernel_ms"] = sum(kernel_ms) / len(kernel_ms)
+    digests = None
+    t2_check = None
     if mt:
         hdrs = eng.mt_headers()
         rec["status_bad"] = int((hdrs["status"] != 0).sum())
         rec["checksum"] = shard.state_checksum(hdrs, doc_base)
+        # every document's content digest (fmt_mt_state_digest: leaves, props by value, text, header)
+        t = time.perf_counter()
+        digests = eng.mt_digests()
+        digest_ms = (time.perf_counter() - t) * 1e3
         if ob:
             _check_obliterate_farms(eng, hdrs, fixtures, docs)
+        if t2 and args.t2_check_docs > 0:
+            t2_check = _t2_oracle_check(batch, digests, docs, doc_base, args.t2_check_docs, world)
     elif args.sparse:
         rec["checksum"] = shard.map_sparse_checksum(*eng.map_fetch_sparse(), doc_base)
     else:
         rec["checksum"] = shard.map_checksum(eng.map_fetch(), doc_base)
     stats = shard.gather_stats(rec, dist, device="cuda") if dist is not None else rec
+    content = None
+    if digests is not None:  # whole-job content digest: Σ over ranks of Σ_d mix(global d, digest_d)
+        part = shard.digest_checksum(digests, doc_base)
+        content = shard.gather_u64(part, dist, device="cuda") if dist is not None else [part]
+        if t2_check is not None:  # every rank checked a sample of its own shard
+            n_chk = shard.gather_u64(t2_check["docs"], dist, device="cuda") if dist is not None else [t2_check["docs"]]
+            n_bad = shard.gather_u64(t2_check["mismatches"], dist, device="cuda") if dist is not None else [t2_check["mismatches"]]
+            t2_check = {**t2_check, "docs_all_ranks": sum(n_chk), "mismatches_all_ranks": sum(n_bad)}
     gathered = None
     if t2 and args.gather_docs > 0:
         from fluidframework_amd.summary import legacy_summary
@@ -271,25 +290,46 @@ def main():
 
         hc = host_cpus()
         threads = args.cpu_threads or hc["usable"]
-        # bounded sample: consecutive chunks of the same batch until >= --cpu-seconds of CPU work
+        # bounded sample: consecutive chunks of the same batch until >= --cpu-seconds of CPU work or
+        # every document replayed once. The oracle's result of every sampled document is compared
+        # with the GPU's (merge-tree: state digests; map: the result slots / entries), untimed.
         chunk = args.cpu_sample_docs or (min(docs, 4 * threads * 80) if mt else min(docs, 50_000 if args.sparse else 200_000))
         secs, sample_ops, sample_docs, lo = 0.0, 0, 0, 0
-        while secs < args.cpu_seconds:
+        checked = mismatched = 0
+        first_bad = None
+        gpu_map = None
+        if not mt:
+            gpu_map = eng.map_fetch_sparse() if args.sparse else eng.map_fetch()
+            if args.sparse:
+                gpu_first = np.concatenate([[0], np.cumsum(gpu_map[0].astype(np.int64))])
+        while secs < args.cpu_seconds and sample_docs < docs:
             hi = min(lo + chunk, docs)
             if mt:
-                _, _, _, _, _, s_ = oracle.mt_replay_batch(batch, lo, hi, threads=threads, outputs=False)
+                rc_, dig_, _, s_ = oracle.mt_replay_digest(batch, lo, hi, threads=threads)
+                bad = np.nonzero(dig_ != digests[lo:hi])[0]
             else:
                 o0, o1 = int(batch.doc_op_offsets[lo]), int(batch.doc_op_offsets[hi])
                 sub = batch.__class__(batch.ops[o0:o1], batch.doc_op_offsets[lo : hi + 1] - o0,
                                       batch.key_bound, batch.keys, batch.values)
                 if args.sparse:  # hash map per document (the dense table would be key_bound x 8 B per doc)
-                    _, _, s_ = oracle.map_replay_sparse(sub, threads=threads)
+                    cnt_, ent_, s_ = oracle.map_replay_sparse(sub, threads=threads)
+                    g_cnt = gpu_map[0][lo:hi]
+                    g_ent = gpu_map[1][int(gpu_first[lo]):int(gpu_first[hi])]
+                    bad = np.zeros(0, dtype=np.int64) if np.array_equal(cnt_, g_cnt) and np.array_equal(ent_, g_ent) else \
+                        np.nonzero(cnt_ != g_cnt)[0] if not np.array_equal(cnt_, g_cnt) else np.array([0])
                 else:
-                    _, s_ = oracle.map_replay(sub, threads=threads)
+                    slots_, s_ = oracle.map_replay(sub, threads=threads)
+                    bad = np.nonzero((slots_ != gpu_map[lo:hi]).any(axis=1))[0]
+            if len(bad) and first_bad is None:
+                first_bad = lo + int(bad[0])
+            mismatched += len(bad)
+            checked += hi - lo
             secs += s_
             sample_ops += int(batch.doc_op_offsets[hi] - batch.doc_op_offsets[lo])
             sample_docs += hi - lo
             lo = hi % docs
+        if mismatched:
+            raise SystemExit(f"{mismatched} of {checked} documents differ from the oracle (first: document {first_bad})")
         cpu = {
             "value": sample_ops / secs,
             "unit": "ops/s",
@@ -301,8 +341,13 @@ def main():
                       f"one document per task on {threads} std::threads",
             "cpu_model": hc["model"],
             "host_cpus": {k: hc[k] for k in ("cpu_count", "affinity", "cgroup_quota_cpus")},
+            "checked_vs_oracle_docs": checked,
+            "checked_how": ("per-document state digest (fmt_mt_state_digest vs the oracle's digest of its own replay: "
+                            "every leaf field, props by value, text, header)" if mt else
+                            "result entries equal" if args.sparse else "result slots equal"),
         }
-        log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s)")
+        log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s); "
+                  f"{checked} documents equal to the oracle's")
         if not args.no_js_baseline and not ob and not args.sparse:
             cpu_js = (_js_mt_baseline if mt else _js_map_baseline)(oracle, batch, docs, threads, args.cpu_seconds / 2)
             if cpu_js is not None:
@@ -380,6 +425,11 @@ def main():
             # secondary: the plain-JS observer restatement on worker_threads
             **({"cpu_baseline_js": cpu_js} if cpu_js is not None else {}),
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
+            "content_digest": f"{sum(content) & 0xFFFFFFFFFFFFFFFF:016x}" if content is not None else None,
+            "checked_vs_oracle_docs": (cpu or {}).get("checked_vs_oracle_docs", 0) + (
+                t2_check["docs_all_ranks"] if t2_check else 0),
+            **({"t2_oracle_check": t2_check} if t2_check else {}),
+            **({"digest_ms": digest_ms} if digests is not None else {}),
             "summary_gather": gathered,
             "summaries": summaries,
             "failed_docs": int(stats["status_bad"].sum()),
@@ -389,6 +439,38 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _t2_oracle_check(batch, digests, docs, doc_base, n_check, world):
+    """T2: this rank's shard checked against the oracle — n_check of its documents spread over the
+    shard, replayed by the oracle and compared by state digest. Raises on a mismatch."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # parity checker only
+
+    threads = max(1, host_cpus()["usable"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world))))
+    n = min(n_check, docs)
+    step = max(1, docs // n)
+    t = time.perf_counter()
+    checked = bad = 0
+    first = None
+    for lo in range(0, docs, step * 64):  # runs of 64 consecutive documents, spread over the shard
+        hi = min(lo + 64, docs)
+        rc, dig, _, _ = oracle.mt_replay_digest(batch, lo, hi, threads=threads)
+        diff = np.nonzero(dig != digests[lo:hi])[0]
+        if len(diff) and first is None:
+            first = doc_base + lo + int(diff[0])
+        bad += len(diff)
+        checked += hi - lo
+        if checked >= n:
+            break
+    if bad:
+        raise SystemExit(f"t2: {bad} of {checked} documents of shard [{doc_base}, {doc_base + docs}) differ from the "
+                         f"oracle (first: document {first})")
+    return {"docs": checked, "mismatches": bad, "seconds": time.perf_counter() - t, "threads": threads,
+            "what": "per rank: runs of 64 documents spread over its shard replayed by the C++ oracle, compared by "
+                    "per-document state digest (fmt_mt_state_digest)"}
 
 
 def _js_map_baseline(oracle, batch, docs, workers, seconds):

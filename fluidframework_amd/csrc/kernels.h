@@ -81,6 +81,9 @@ struct SumDocOut {
 hipError_t launchSummaryRuns(const fmt_mt_doc_result* hdrs, const SumView* views, uint32_t nDocs, SumRun* runs,
                              uint16_t* text, unsigned long long* cursors, SumDocOut* docOut, int numCUs,
                              hipStream_t stream);
+// Per-document content digest of the converged state (digest.hip).
+hipError_t launchStateDigest(const fmt_mt_doc_result* hdrs, const SumView* views, uint32_t nDocs, uint64_t* out,
+                             int numCUs, hipStream_t stream);
 
 struct MtCaps {
   uint32_t leaves, chars, props;

@@ -140,6 +140,7 @@ struct fmt_ctx {
   DevBuf<uint16_t> sumText;
   DevBuf<unsigned long long> sumCursors;
   DevBuf<fmt_kernels::SumDocOut> sumDocs;
+  DevBuf<uint64_t> digests;                   // fmt_mt_state_digest output
   std::vector<std::string> sumBlobs;          // per document: header, then body
   std::vector<uint32_t> sumSplit;             // per document: header length in sumBlobs[d]
   std::vector<int32_t> sumStatus;
@@ -1246,22 +1247,11 @@ void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* r
   if (n1 < nRuns) emit(n1, total, false, &n2);
 }
 
-}  // namespace
-
-int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys, const char* const* values,
-                            uint32_t nValues, uint32_t chunk, uint32_t threads, fmt_summary_timing* timing) {
-  if (c == nullptr || !c->mtLoaded || (nKeys && keys == nullptr) || (nValues && values == nullptr))
-    return setErr(c, FMT_E_USAGE, "fmt_mt_summarize_legacy: bad arguments");
-  using clk = std::chrono::steady_clock;
-  FMT_HIP(c, hipSetDevice(c->device));
+// Where each document's converged state lives: the small tier's slabs, a large-tier slab, or a
+// huge document's own buffers.
+void docViews(const fmt_ctx* c, std::vector<fmt_kernels::SumView>& views) {
   const uint32_t nd = c->mtDocs;
-  std::vector<fmt_mt_doc_result> hdr(nd);
-  FMT_HIP(c, hipMemcpyAsync(hdr.data(), c->mtHdr.p, nd * sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost, c->stream));
-  FMT_HIP(c, hipStreamSynchronize(c->stream));
-  // every document's result buffers (small tier, large-tier slab, or huge tier)
-  std::vector<fmt_kernels::SumView> views(nd);
-  std::vector<fmt_mt_propset*> propsDev(nd);
-  uint64_t capRuns = 0, capText = 0;
+  views.resize(nd);
   for (uint32_t d = 0; d < nd; d++) {
     const int32_t hs = d < c->mtHugeSlot.size() ? c->mtHugeSlot[d] : -1;
     if (hs >= 0) {
@@ -1275,6 +1265,42 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
                   (slot >= 0 ? c->mtBigChars.p : c->mtChars.p) + at * caps.chars,
                   (slot >= 0 ? c->mtBigProps.p : c->mtProps.p) + at * caps.props};
     }
+  }
+}
+
+}  // namespace
+
+int fmt_mt_state_digest(fmt_ctx* c, uint64_t* out) {
+  if (c == nullptr || out == nullptr || !c->mtLoaded) return setErr(c, FMT_E_USAGE, "fmt_mt_state_digest: nothing loaded");
+  FMT_HIP(c, hipSetDevice(c->device));
+  const uint32_t nd = c->mtDocs;
+  std::vector<fmt_kernels::SumView> views;
+  docViews(c, views);
+  FMT_HIP(c, c->sumViews.reserve(nd));
+  FMT_HIP(c, c->digests.reserve(nd));
+  FMT_HIP(c, hipMemcpyAsync(c->sumViews.p, views.data(), nd * sizeof(fmt_kernels::SumView), hipMemcpyHostToDevice, c->stream));
+  FMT_HIP(c, fmt_kernels::launchStateDigest(c->mtHdr.p, c->sumViews.p, nd, c->digests.p, c->numCUs, c->stream));
+  FMT_HIP(c, hipMemcpyAsync(out, c->digests.p, nd * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  return FMT_OK;
+}
+
+int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys, const char* const* values,
+                            uint32_t nValues, uint32_t chunk, uint32_t threads, fmt_summary_timing* timing) {
+  if (c == nullptr || !c->mtLoaded || (nKeys && keys == nullptr) || (nValues && values == nullptr))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_summarize_legacy: bad arguments");
+  using clk = std::chrono::steady_clock;
+  FMT_HIP(c, hipSetDevice(c->device));
+  const uint32_t nd = c->mtDocs;
+  std::vector<fmt_mt_doc_result> hdr(nd);
+  FMT_HIP(c, hipMemcpyAsync(hdr.data(), c->mtHdr.p, nd * sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  // every document's result buffers (small tier, large-tier slab, or huge tier)
+  std::vector<fmt_kernels::SumView> views;
+  docViews(c, views);
+  std::vector<fmt_mt_propset*> propsDev(nd);
+  uint64_t capRuns = 0, capText = 0;
+  for (uint32_t d = 0; d < nd; d++) {
     propsDev[d] = const_cast<fmt_mt_propset*>(views[d].props);
     capRuns += hdr[d].n_leaves;
     capText += hdr[d].n_chars;

@@ -224,6 +224,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_remove_order.argtypes = [P, U32, P, U32]
         L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
+        L.fmt_mt_state_digest.argtypes = [P, P]
         _libs[path] = L
     return _libs[path]
 
@@ -235,6 +236,7 @@ EXPORTED_SYMBOLS = [
     "fmt_mt_summarize_legacy", "fmt_mt_summary_blobs",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
+    "fmt_mt_state_digest",
 ]
 
 
@@ -364,9 +366,13 @@ class Engine:
     def mt_run(self):
         self._check(self.L.fmt_mt_run(self.h))
 
-    def mt_headers(self) -> np.ndarray:
+    def mt_headers(self, raise_on_failed_docs: bool = True) -> np.ndarray:
+        """Every document's result header; by default raises EngineError when a document failed
+        (fmt_mt_fetch_headers returns the first failure), else returns them all."""
         out = np.zeros(self._mt_docs, dtype=DOC_RESULT_DTYPE)
-        self._check(self.L.fmt_mt_fetch_headers(self.h, _ptr(out)))
+        rc = self.L.fmt_mt_fetch_headers(self.h, _ptr(out))
+        if raise_on_failed_docs or rc not in (FMT_OK, FMT_E_DATA, FMT_E_CAPACITY, FMT_E_UNSUPPORTED):
+            self._check(rc)
         return out
 
     def mt_doc(self, doc: int, hdr=None):
@@ -378,6 +384,12 @@ class Engine:
         props = np.zeros(max(npp, 1), dtype=PROPSET_DTYPE)
         self._check(self.L.fmt_mt_fetch_doc(self.h, doc, _ptr(leaves), nl, _ptr(chars), nc, _ptr(props), npp))
         return leaves[:nl], chars[:nc], props[:npp]
+
+    def mt_digests(self) -> np.ndarray:
+        """fmt_mt_state_digest: every document's 64-bit content digest."""
+        out = np.zeros(self._mt_docs, dtype=np.uint64)
+        self._check(self.L.fmt_mt_state_digest(self.h, _ptr(out)))
+        return out
 
     def huge_profile(self, doc: int):
         """Diagnostics: shader-clock totals per phase of a huge document's last replay

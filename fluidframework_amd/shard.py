@@ -135,6 +135,30 @@ def gather_stats(rec: np.ndarray, dist, device=None) -> np.ndarray:
     return np.frombuffer(out.tobytes(), dtype=STATS_DTYPE)
 
 
+def digest_checksum(digests: np.ndarray, doc_lo: int = 0) -> int:
+    """Order-independent fold of per-document content digests (fmt_mt_state_digest): Σ_d mix(d,
+    digest_d) mod 2^64 with d the global document index, so shard sums add up to the unsharded one."""
+    d = np.arange(doc_lo, doc_lo + len(digests), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = (d + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15) ^ np.asarray(digests, dtype=np.uint64)
+        h *= np.uint64(0xBF58476D1CE4E5B9)
+        h ^= h >> np.uint64(31)
+        return int(h.sum(dtype=np.uint64))
+
+
+def gather_u64(value: int, dist, device=None) -> list[int]:
+    """All-gather one unsigned 64-bit value per rank (rank order)."""
+    import torch
+
+    v = int(value) & 0xFFFFFFFFFFFFFFFF
+    t = torch.tensor([v - (1 << 64) if v >= 1 << 63 else v], dtype=torch.int64)  # (two's complement bits)
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [int(p.cpu().item()) & 0xFFFFFFFFFFFFFFFF for p in parts]
+
+
 def combine_checksums(stats: np.ndarray) -> int:
     """Whole-job state checksum = Σ shard checksums mod 2^64."""
     return int(stats["checksum"].astype(np.uint64).sum(dtype=np.uint64))

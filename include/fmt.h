@@ -490,6 +490,15 @@ int fmt_mt_fetch_remove_order(fmt_ctx* ctx, uint32_t doc, fmt_mt_remove_order* o
 /* One document's computed numbers (annotate-adjust results, FMT_MT_VALUE_COMPUTED + index): *n_out
  * = their count, the first min(count, cap) copied to out. */
 int fmt_mt_fetch_numbers(fmt_ctx* ctx, uint32_t doc, double* out, uint32_t cap, uint32_t* n_out);
+/* Per-document 64-bit content digest of the converged state of the last fmt_mt_run (n_docs entries):
+ * everything the reference's getText / summarize read back (MergeTreeTextHelper.ts:28-87,
+ * snapshotlegacy.ts:195-262) — every leaf in document order with its stamps, remove-client set, length,
+ * parent block ordinal and marker bit, its properties by value, the text — plus the header's collab
+ * window, counts, depth and visible length; a failed document digests its status and fail_seq only.
+ * Definition: mix(Σ elem(tag, index, word) mod 2^64), mix = the splitmix64 finalizer.
+ * No reference counterpart: it lets a host check a whole batch against another replay (a replica, a
+ * CPU client) without copying the state back. Synchronizes the ctx stream. */
+int fmt_mt_state_digest(fmt_ctx* ctx, uint64_t* out);
 /* Per-document capacities of this engine build (leaves, chars, prop sets): the large tier's, which
  * is where a document that outgrows the small tier ends up. */
 int fmt_mt_capacity(uint32_t* max_leaves, uint32_t* max_chars, uint32_t* max_props);

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <memory>
 #include <mutex>
 #include <chrono>
 #include <cstring>
@@ -108,6 +109,41 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
     hdr->depth = static_cast<uint32_t>(depth);
     hdr->visible_len = static_cast<uint32_t>(mt->getLocalLength());
   }
+}
+
+// The state digest of DESIGN.md §2 (what fmt_mt_state_digest computes on the device), restated over
+// the oracle's dumped state: mix(Σ elem(tag, index, word) mod 2^64), mix = the splitmix64 finalizer.
+uint64_t dgMix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t dgElem(uint64_t tag, uint64_t i, uint64_t w) { return dgMix(dgMix((tag << 56) ^ i) ^ w); }
+
+uint64_t digestOf(const fmt_mt_doc_result& h, const fmt_mt_leaf* leaves, const uint16_t* chars, const fmt_mt_propset* props) {
+  uint64_t acc = 0;
+  if (h.status != FMT_OK)
+    return dgMix(dgElem(1, 0, static_cast<uint32_t>(h.status)) + dgElem(1, 1, static_cast<uint32_t>(h.fail_seq)));
+  const uint32_t f[8] = {static_cast<uint32_t>(h.status), static_cast<uint32_t>(h.cur_seq), static_cast<uint32_t>(h.min_seq),
+                         h.n_leaves, h.n_chars, h.n_blocks, h.depth, h.visible_len};
+  for (uint32_t k = 0; k < 8; k++) acc += dgElem(1, k, f[k]);
+  for (uint32_t i = 0; i < h.n_leaves; i++) {
+    const fmt_mt_leaf& L = leaves[i];
+    acc += dgElem(2, i, static_cast<uint32_t>(L.ins_seq) | static_cast<uint64_t>(static_cast<uint32_t>(L.rm_seq)) << 32);
+    acc += dgElem(3, i, L.rm_clients);
+    acc += dgElem(4, i, L.char_off | static_cast<uint64_t>(L.len) << 32);
+    acc += dgElem(5, i, static_cast<uint16_t>(L.ins_client) | static_cast<uint64_t>(L.block) << 16 |
+                            static_cast<uint64_t>(L.pad) << 32);
+    if (L.props == 0xFFFFu) {
+      acc += dgElem(6, i, ~0ull);
+    } else {
+      const fmt_mt_propset& P = props[L.props];
+      acc += dgElem(6, i, P.n);
+      for (uint32_t k = 0; k < P.n && k < FMT_MT_PROPS_MAX; k++) acc += dgElem(7, static_cast<uint64_t>(i) * 8 + k, P.kv[k]);
+    }
+  }
+  for (uint32_t u = 0; u < h.n_chars; u++) acc += dgElem(8, u, chars[u]);
+  return dgMix(acc);
 }
 
 template <class F>
@@ -307,6 +343,54 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
   });
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return status.load();
+}
+
+// Replays documents [docBegin, docEnd) like orc_mt_replay_batch, keeping every tree, then digests
+// each one into digests[d - docBegin]. *seconds times the replays only (the first
+// pass); the digest pass runs after it, so the bench's CPU baseline doubles as its parity check.
+int orc_mt_replay_digest(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEnd, uint32_t nThreads,
+                         uint64_t* digests, int32_t* statuses, double* seconds) {
+  const auto hn = hostNumbers(b);
+  const uint32_t n = docEnd - docBegin;
+  std::vector<std::unique_ptr<MergeTree>> trees(n);
+  std::vector<int32_t> st(n, FMT_OK), fs(n, 0);
+  std::atomic<int> status{FMT_OK};
+  const auto t0 = std::chrono::steady_clock::now();
+  parallelFor(docBegin, docEnd, nThreads, [&](uint32_t d) {
+    const size_t i = d - docBegin;
+    trees[i].reset(new MergeTree());
+    startDoc(*trees[i], b, d, &hn);
+    const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
+    st[i] = applyOps(trees[i].get(), b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &fs[i]);
+    if (st[i] != FMT_OK) status = st[i];
+  });
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  parallelFor(0, n, nThreads, [&](uint32_t i) {
+    fmt_mt_doc_result h{};
+    std::vector<const orc::Seg*> segs;
+    std::vector<int> blockOf;
+    int nb = 0, dp = 0;
+    trees[i]->collectLeaves(segs, blockOf, &nb, &dp);
+    std::vector<fmt_mt_leaf> lv(segs.size() + 1);
+    size_t units = 0;
+    for (const orc::Seg* s : segs) units += static_cast<size_t>(s->len());
+    std::vector<uint16_t> ch(units + 1);
+    std::vector<fmt_mt_propset> pr(segs.size() + 1);
+    dumpDoc(trees[i].get(), &h, lv.data(), static_cast<uint32_t>(lv.size()), ch.data(), static_cast<uint32_t>(ch.size()),
+            pr.data(), static_cast<uint32_t>(pr.size()));
+    h.status = st[i];
+    h.fail_seq = fs[i];
+    if (statuses) statuses[i] = st[i];
+    digests[i] = digestOf(h, lv.data(), ch.data(), pr.data());
+    trees[i].reset();
+  });
+  return status.load();
+}
+
+// The state digest of one dumped document: a test hook pinning the definition.
+uint64_t orc_state_digest(const fmt_mt_doc_result* h, const fmt_mt_leaf* leaves, const uint16_t* chars,
+                          const fmt_mt_propset* props) {
+  return digestOf(*h, leaves, chars, props);
 }
 
 // Replays ONE document: its initial state, then at most maxOps of its ops (all with maxOps = 0), timing

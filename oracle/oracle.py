@@ -49,6 +49,9 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_replay_timed.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P, ctypes.c_uint32, P,
                                           ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_set_index.argtypes = [ctypes.c_int]
+        L.orc_mt_replay_digest.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P, P]
+        L.orc_state_digest.argtypes = [P, P, P, P]
+        L.orc_state_digest.restype = ctypes.c_uint64
         L.orc_map_replay.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, ctypes.c_uint32, P]
         L.orc_map_replay_sparse.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_uint32, P]
         L.orc_map_summary.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P,
@@ -180,6 +183,34 @@ def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096
     if cap_catchup:
         return rc, hdrs, leaves, chars, props, secs.value, catchup.reshape(n, cap_catchup)
     return rc, hdrs, leaves, chars, props, secs.value
+
+
+def mt_replay_digest(batch, doc_begin=0, doc_end=None, threads=1):
+    """Replay documents [doc_begin, doc_end) and return (rc, digests uint64[n], statuses int32[n],
+    replay seconds): each document's state digest (what fmt_mt_state_digest computes on
+    the device); the seconds time the replays alone, the digests are taken afterwards."""
+    from fluidframework_amd.native import batch_struct
+
+    doc_end = batch.n_docs if doc_end is None else doc_end
+    n = doc_end - doc_begin
+    dig = np.zeros(max(n, 1), dtype=np.uint64)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    secs = ctypes.c_double(0)
+    b, keep = batch_struct(batch)
+    rc = lib().orc_mt_replay_digest(ctypes.byref(b), doc_begin, doc_end, threads, _ptr(dig), _ptr(st), ctypes.byref(secs))
+    del keep
+    return rc, dig[:n], st[:n], secs.value
+
+
+def state_digest(hdr, leaves, chars, props) -> int:
+    """The state digest of one dumped document (the oracle's restatement of the definition)."""
+    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE
+
+    h = np.ascontiguousarray(np.asarray(hdr).reshape(1), dtype=DOC_RESULT_DTYPE)
+    lv = np.ascontiguousarray(leaves, dtype=LEAF_DTYPE) if len(leaves) else np.zeros(1, LEAF_DTYPE)
+    ch = np.ascontiguousarray(chars, dtype="<u2") if len(chars) else np.zeros(1, "<u2")
+    pr = np.ascontiguousarray(props, dtype=PROPSET_DTYPE) if len(props) else np.zeros(1, PROPSET_DTYPE)
+    return int(lib().orc_state_digest(_ptr(h), _ptr(lv), _ptr(ch), _ptr(pr)))
 
 
 def mt_replay_summary(batch, doc: int, keys, values, chunk_size: int = 10000):

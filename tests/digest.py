@@ -1,0 +1,57 @@
+"""The state digest restated in numpy: the definition both fmt_mt_state_digest (device,
+csrc/digest.hip) and the oracle (oracle/capi.cpp digestOf) implement. Test-only."""
+import numpy as np
+
+M64 = (1 << 64) - 1
+
+
+def _mix(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _elems(tag, idx, w):
+    idx = np.asarray(idx, dtype=np.uint64)
+    w = np.asarray(w, dtype=np.uint64)
+    return _mix(_mix((np.uint64(tag) << np.uint64(56)) ^ idx) ^ w)
+
+
+def _sum(a):
+    return int(np.asarray(a, dtype=np.uint64).sum(dtype=np.uint64)) if np.size(a) else 0
+
+
+def state_digest(hdr, leaves, chars, props) -> int:
+    """Digest of one document from its header, leaves[:n_leaves], chars[:n_chars] and prop sets."""
+    u32 = lambda v: int(v) & 0xFFFFFFFF  # noqa: E731
+    if int(hdr["status"]) != 0:
+        acc = (_sum(_elems(1, [0], [u32(hdr["status"])])) + _sum(_elems(1, [1], [u32(hdr["fail_seq"])]))) & M64
+        return int(_mix(np.uint64(acc)))
+    f = [u32(hdr[k]) for k in ("status", "cur_seq", "min_seq", "n_leaves", "n_chars", "n_blocks", "depth", "visible_len")]
+    acc = _sum(_elems(1, np.arange(8), f))
+    n = int(hdr["n_leaves"])
+    L = leaves[:n]
+    i = np.arange(n, dtype=np.uint64)
+    w2 = L["ins_seq"].astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    w2 |= (L["rm_seq"].astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF)) << np.uint64(32)
+    acc += _sum(_elems(2, i, w2))
+    acc += _sum(_elems(3, i, L["rm_clients"]))
+    acc += _sum(_elems(4, i, L["char_off"].astype(np.uint64) | (L["len"].astype(np.uint64) << np.uint64(32))))
+    w5 = (L["ins_client"].astype(np.int64).astype(np.uint64) & np.uint64(0xFFFF)) | (L["block"].astype(np.uint64) << np.uint64(16))
+    w5 |= L["pad"].astype(np.uint64) << np.uint64(32)
+    acc += _sum(_elems(5, i, w5))
+    for k in range(n):
+        p = int(L["props"][k])
+        if p == 0xFFFF:
+            acc += _sum(_elems(6, [k], [M64]))
+        else:
+            ps = props[p]
+            m = int(ps["n"])
+            acc += _sum(_elems(6, [k], [m]))
+            if m:
+                acc += _sum(_elems(7, np.arange(m) + 8 * k, ps["kv"][:m]))
+    nc = int(hdr["n_chars"])
+    acc += _sum(_elems(8, np.arange(nc), chars[:nc]))
+    return int(_mix(np.uint64(acc & M64)))

@@ -144,3 +144,29 @@ def test_gloo_gather_blobs_world3(tmp_path):
         got.append(raw[o + 8 : o + 8 + n])
         o += 8 + n
     assert got == [b"a", b"bc" * 1000, b"", "é€😀".encode(), b"\0x"]
+
+
+def _u64_main(rank, world, port, out_path):
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+
+    from fluidframework_amd import shard as sh
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    vals = [0xFFFFFFFFFFFFFFFF, 0x8000000000000000, 12345]
+    got = sh.gather_u64(vals[rank], dist)
+    if rank == 0:
+        np.save(out_path, np.array(got, dtype=np.uint64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_u64_world3_and_digest_fold(tmp_path):
+    """The whole-job content digest: per-rank folds of the per-document digests, all-gathered as
+    unsigned 64-bit values, add up to the unsharded fold."""
+    out = str(tmp_path / "u64.npy")
+    mp.start_processes(_u64_main, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
+    assert [int(x) for x in np.load(out)] == [0xFFFFFFFFFFFFFFFF, 0x8000000000000000, 12345]
+    dig = np.random.default_rng(3).integers(0, 2**63, 50, dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    parts = [shard.digest_checksum(dig[lo:hi], lo) for lo, hi in shard.plan_shards(np.arange(51, dtype=np.uint64), 4)]
+    assert sum(parts) & 0xFFFFFFFFFFFFFFFF == shard.digest_checksum(dig)
