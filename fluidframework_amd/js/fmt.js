@@ -370,16 +370,29 @@ class MergeTreeStreamBuilder {
 		if (anyInfo && nBody > 0) {
 			// each body segment: an insert at the local length from PriorPerspective(0, its client), a run
 			// of segments without merge info in one insertSegments call (FMT_MT_F_GROUP_CONT)
+			// flushBatch (snapshotLoader.ts:291-296) never clears its batch: a segment without merge info
+			// before one with merge info gets inserted again by every later flush, so that shape is refused
+			let universalSeen = false;
+			for (let k = first + nHeader; k < first + nHeader + nBody; k++) {
+				const [insSeq, insClient] = this.snapshotInfo[k];
+				const universal = insClient === FMT_NON_COLLAB_CLIENT && insSeq === 0;
+				if (universalSeen && !universal) {
+					throw new UnsupportedOp("a SnapshotV1 body where a segment without merge info precedes one with " +
+						"merge info (the reference's loadBody re-inserts the batched segments)");
+				}
+				universalSeen = universalSeen || universal;
+			}
 			let prevUniversal = false;
 			for (let k = first + nHeader; k < first + nHeader + nBody; k++) {
 				const [off, ln, pid] = this.snapshotSegs[k];
 				const [insSeq, insClient] = this.snapshotInfo[k];
 				const universal = insClient === FMT_NON_COLLAB_CLIENT && insSeq === 0;
-				let flags = FMT_MT_F_LOADSEG | ((ln & FMT_MT_SEG_MARKER) ? FMT_MT_F_MARKER : 0);
+				const nUnits = (ln & ~FMT_MT_SEG_MARKER) >>> 0;
+				let flags = FMT_MT_F_LOADSEG | ((ln & FMT_MT_SEG_MARKER) ? FMT_MT_F_MARKER : 0) |
+					(nUnits & FMT_MT_F_LEN_HI_MASK);
 				if (universal && prevUniversal) flags |= FMT_MT_F_GROUP_CONT;
 				prevUniversal = universal;
-				const nUnits = (ln & ~FMT_MT_SEG_MARKER) >>> 0;
-				if (nUnits > 0xffff) throw new UnsupportedOp("a SnapshotV1 body segment with merge info longer than 65535 UTF-16 units");
+				if (nUnits > 0xffffff) throw new UnsupportedOp("a SnapshotV1 body segment longer than 2^24 - 1 UTF-16 units");
 				const o = this.ops.next();
 				const v = this.ops.view;
 				v.setInt32(o + 0, insSeq, true);
@@ -388,7 +401,7 @@ class MergeTreeStreamBuilder {
 				v.setInt32(o + 12, k, true);
 				v.setInt32(o + 16, pid !== NO_PROPS ? pid + 1 : 0, true);
 				v.setUint32(o + 20, off, true);
-				v.setUint16(o + 24, nUnits, true);
+				v.setUint16(o + 24, nUnits & 0xffff, true);
 				v.setUint8(o + 26, insClient === FMT_NON_COLLAB_CLIENT ? FMT_MT_CLIENT_NONCOLLAB : insClient);
 				v.setUint8(o + 27, MT_INSERT);
 				v.setUint32(o + 28, flags, true);

@@ -590,20 +590,33 @@ class MergeTreeStreamBuilder:
             # segments without merge info in one call — so they become FMT_MT_F_LOADSEG inserts ahead of
             # the messages (their specs and merge info rows stay in the tables; the document loads its
             # header alone)
+            # The reference's flushBatch (snapshotLoader.ts:291-296) never clears `batch`: once a segment
+            # without merge info precedes one with merge info, every later flush inserts the batched
+            # segment objects AGAIN (overwriteInfo + insertingWalk on segments already in the tree,
+            # mergeTree.ts:1609-1626), aliasing them in two blocks. That state has no consistent
+            # segment list to reproduce, so such a body is refused rather than loaded differently.
+            universal_seen = False
+            for k in range(first + n_header, first + n_header + n_body):
+                ins_seq, ins_client = self.snapshot_info[k][0], self.snapshot_info[k][1]
+                universal = ins_client == NON_COLLAB_CLIENT and ins_seq == 0
+                if universal_seen and not universal:
+                    raise UnsupportedOp("a SnapshotV1 body where a segment without merge info precedes one with "
+                                        "merge info (the reference's loadBody re-inserts the batched segments)")
+                universal_seen = universal_seen or universal
             prev_universal = False
             for k in range(first + n_header, first + n_header + n_body):
                 off, ln, pid = self.snapshot_segs[k]
                 ins_seq, ins_client = self.snapshot_info[k][0], self.snapshot_info[k][1]
                 universal = ins_client == NON_COLLAB_CLIENT and ins_seq == 0
-                flags = MT_F_LOADSEG | (MT_F_MARKER if ln & MT_SEG_MARKER else 0)
+                n_units = ln & ~MT_SEG_MARKER
+                flags = MT_F_LOADSEG | (MT_F_MARKER if ln & MT_SEG_MARKER else 0) | (n_units & MT_F_LEN_HI_MASK)
                 if universal and prev_universal:
                     flags |= MT_F_GROUP_CONT
                 prev_universal = universal
-                n_units = ln & ~MT_SEG_MARKER
-                if n_units > 0xFFFF:
-                    raise UnsupportedOp("a SnapshotV1 body segment with merge info longer than 65535 UTF-16 units")
+                if n_units > 0xFFFFFF:
+                    raise UnsupportedOp("a SnapshotV1 body segment longer than 2^24 - 1 UTF-16 units")
                 client = CLIENT_NONCOLLAB_OP if ins_client == NON_COLLAB_CLIENT else ins_client
-                d.ops.append((ins_seq, 0, min_seq, k, pid + 1 if pid != NO_PROPS else 0, off, n_units, client,
+                d.ops.append((ins_seq, 0, min_seq, k, pid + 1 if pid != NO_PROPS else 0, off, n_units & 0xFFFF, client,
                               MT_INSERT, flags))
             n_body = 0
         self.snapshots.append((first, n_header, n_body, min_seq, seq, 1))

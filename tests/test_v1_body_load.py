@@ -1,17 +1,22 @@
 """SnapshotV1 body-chunk segments with merge info (snapshotLoader.ts:221-309).
 
 loadBody appends each body segment through insertSegments at root.cachedLength (the local length)
-from PriorPerspective(UniversalSequenceNumber, the segment's client) with its stamp, a run of
-segments without merge info in one call. The hosts pack them as FMT_MT_F_LOADSEG inserts ahead of the
-messages (the header alone is reloaded); the oracle and the engine apply them as the reference does.
+from PriorPerspective(UniversalSequenceNumber, the segment's client) with its stamp, and batches
+segments without merge info into one call. The hosts pack them as FMT_MT_F_LOADSEG inserts ahead of
+the messages (the header alone is reloaded); the oracle and the engine apply them as the reference
+does.
 
-What the reference does with them: a body segment whose perspective misses an earlier segment that
-the local length counts (inserted above seq 0 by another client) cannot reach that position, and the
-load throws "MergeTree insert failed" — which is what happens to V1 summaries of collaborative
-documents with merge info before a body segment. A document whose body merge info comes from one
-writer after a universal header loads, and replaying the rest of its stream reaches the original's
-text. Both outcomes are checked: oracle status and text, and engine == oracle bit for bit (emulated
-here, on the GPU in -m gpu).
+What the reference does with them:
+- a body segment whose perspective misses an earlier segment that the local length counts (inserted
+  above seq 0 by another client) cannot reach that position, and the load throws "MergeTree insert
+  failed" — V1 summaries of collaborative documents with merge info in the body;
+- a body whose merge-info segments come from one writer, followed by old text, loads, and replaying
+  the rest of the stream reaches the original's text;
+- flushBatch never clears its batch (snapshotLoader.ts:291-296): when a segment without merge info
+  precedes one with merge info, every later flush inserts the batched segment objects again, aliasing
+  them in the tree. The hosts refuse that shape (UnsupportedOp) instead of loading something else.
+The first two are checked by oracle status and text and engine == oracle bit for bit (emulated here,
+on the GPU in -m gpu), the third by both packers refusing.
 """
 import json
 import os
@@ -28,7 +33,30 @@ from fluidframework_amd.streams import MergeTreeStreamBuilder
 from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
 
 
-def _source_docs():
+def _solo(seed, at_end, msn_lag):
+    """One writer after a 12,000-unit prefix: appending at the end (at_end), or editing inside
+    [11000, 11000 + its text), i.e. between the header chunk and the prefix's last 1000 units."""
+    rnd, msgs, added = random.Random(seed), [], 0
+    base = 12000 if at_end else 11000
+    for seq in range(1, 300):
+        if rnd.random() < 0.2 and added > 10:
+            a = base + rnd.randint(0, added - 3)
+            op = {"pos1": a, "pos2": a + 2, "type": 1}
+            added -= 2
+        else:
+            n = rnd.randint(1, 5)
+            op = {"pos1": base + (added if at_end else rnd.randint(0, added)), "seg": "q" * n, "type": 0}
+            added += n
+        msn = 0 if msn_lag is None else max(0, seq - msn_lag)
+        msgs.append({"clientId": "solo", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+                     "minimumSequenceNumber": msn, "type": "op", "contents": op})
+    return "Z" * 12000, msgs
+
+
+def _source_docs(msn_lag=None):
+    """Collaborative farms after a 12,000-unit prefix (3), one writer appending after it (2), one
+    writer editing before the prefix's tail (2). msn_lag None: the minSeq stays 0, so every segment
+    inserted or removed since carries merge info; otherwise msn = seq - msn_lag."""
     src = workloads.conflict_farm(3, n_clients=8, ops_per_doc=1500, seed=3)
     docs = []
     for d in range(3):  # collaborative: the farm runs after a 12,000-unit prefix (the header chunk)
@@ -38,21 +66,11 @@ def _source_docs():
             c["pos1"] += 12000
             if "pos2" in c:
                 c["pos2"] += 12000
+            if msn_lag is None:
+                m["minimumSequenceNumber"] = 0
         docs.append(("Z" * 12000 + init, msgs))
-    for seed in (1, 2):  # one writer appending after the prefix (some of it removed again)
-        rnd, msgs, length = random.Random(seed), [], 12000
-        for seq in range(1, 300):
-            if rnd.random() < 0.2 and length > 12010:
-                a = rnd.randint(12000, length - 3)
-                op = {"pos1": a, "pos2": a + 2, "type": 1}
-                length -= 2
-            else:
-                n = rnd.randint(1, 5)
-                op = {"pos1": length, "seg": "q" * n, "type": 0}
-                length += n
-            msgs.append({"clientId": "solo", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
-                         "minimumSequenceNumber": max(0, seq - 30), "type": "op", "contents": op})
-        docs.append(("Z" * 12000, msgs))
+    docs += [_solo(seed, True, msn_lag) for seed in (1, 2)]
+    docs += [_solo(seed, False, msn_lag) for seed in (3, 4)]
     return docs
 
 
@@ -90,14 +108,40 @@ def reload_batch():
     return b.finish(), docs, cuts
 
 
+def test_body_with_universal_run_before_merge_info_is_refused(orc):
+    """msn advancing: the older writer segments lose their merge info, so a run without merge info
+    precedes segments with it and both packers refuse the body (the reference would re-insert it)."""
+    from fluidframework_amd.streams import UnsupportedOp
+
+    cuts = _cut(_source_docs(msn_lag=30)[3:5], 200)
+    refused = 0
+    for head, bodies, rest in cuts:
+        b = MergeTreeStreamBuilder()
+        segs = [s for bd in bodies for s in json.loads(bd)["segments"]]
+        # a segment goes into the batch when its insert stamp is {UniversalSequenceNumber, NonCollabClient}
+        stamped = [isinstance(s, dict) and "json" in s and (s.get("client") is not None or s.get("seq", 0) != 0)
+                   for s in segs]
+        shape_bad = any(not a and b_ for k, a in enumerate(stamped) for b_ in stamped[k + 1:])
+        if shape_bad:
+            with pytest.raises(UnsupportedOp):
+                b.begin_doc_from_summary(head, bodies)
+            refused += 1
+        else:
+            b.begin_doc_from_summary(head, bodies)
+    assert refused == 2
+
+
 def test_loader_segments_follow_the_reference(orc, reload_batch):
     batch, docs, _ = reload_batch
     rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
     st = [int(x) for x in oh["status"]]
-    assert st[:3] == [-2, -2, -2]  # DataProcessingError: "MergeTree insert failed" while loading
-    assert st[3:] == [0, 0]
+    # DataProcessingError "MergeTree insert failed" while loading: a farm segment whose perspective
+    # misses the other writers' appended segments; the prefix's tail (a batch without merge info,
+    # PriorPerspective(0, NonCollabClient)) after the writer's segments. The appending writer loads.
+    assert st == [-2, -2, -2, 0, 0, -2, -2]
+    assert [int(x) for x in oh["fail_seq"][5:]] == [0, 0]  # (the tail's stamp seq)
     whole = MergeTreeStreamBuilder()
-    for init, msgs in docs[3:]:
+    for init, msgs in docs[3:5]:
         d = whole.begin_doc(init, observer="observer")
         for m in msgs:
             d.add_message(m)
