@@ -58,6 +58,9 @@ struct MtDeviceOut {
   // large tier over a plain batch: the small tier's result slabs, where it left its checkpoints
   const fmt_mt_leaf* smallLeaves;
   const uint16_t* smallChars;
+  // annotate-adjust batches: per leaf the prop set of getAtSeq(minSeq) (legacy summaries), at the
+  // leaves slab's stride; nullptr otherwise
+  uint16_t* legacyProps;
 };
 // Bytes of one document's tier checkpoint (mt_engine.h Doc::kCkptWords).
 size_t mergeTreeCheckpointBytes();
@@ -68,6 +71,7 @@ struct SumView {
   const fmt_mt_leaf* leaves;
   const uint16_t* chars;
   const fmt_mt_propset* props;
+  const uint16_t* legacyProps;  // per leaf: the prop set the legacy summary reads, or nullptr (leaf.props)
 };
 struct SumRun {
   uint32_t len;    // UTF-16 units of the merged segment
@@ -81,6 +85,13 @@ struct SumDocOut {
 hipError_t launchSummaryRuns(const fmt_mt_doc_result* hdrs, const SumView* views, uint32_t nDocs, SumRun* runs,
                              uint16_t* text, unsigned long long* cursors, SumDocOut* docOut, int numCUs,
                              hipStream_t stream);
+// Packing before a D2H copy (transfer.hip): span i's `words` dwords from src to dst + dstWord.
+struct GatherSpan {
+  const uint32_t* src;
+  uint64_t dstWord;
+  uint32_t words, pad;
+};
+hipError_t launchGatherSpans(const GatherSpan* spans, uint32_t n, uint32_t* dst, int numCUs, hipStream_t stream);
 // Per-document content digest of the converged state (digest.hip).
 hipError_t launchStateDigest(const fmt_mt_doc_result* hdrs, const SumView* views, uint32_t nDocs, uint64_t* out,
                              int numCUs, hipStream_t stream);
@@ -96,10 +107,12 @@ MtCaps mergeTreeCaps(bool large);
 // tier and lists its overflow in esc2 (count + 1 entries) for the small tier. esc[0] and esc2[0] must
 // be zero before the call. sched: 3 zeroed device counters (compact, small, large) from which the
 // tiers deal documents to waves dynamically (nullptr: static grid-stride shares). adjust: the batch
-// holds annotate-adjust entries (the Adj engine variants, small tier first, no checkpoints).
+// holds annotate-adjust entries (the Adj engine variants, small tier first, no checkpoints). lean: no
+// op of the batch has FMT_MT_F_CATCHUP / REL1 / REL2 / LOADSEG (the Lean variants of the plain path).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
-                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust);
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust,
+                           bool lean);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,

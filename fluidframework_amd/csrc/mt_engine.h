@@ -213,6 +213,9 @@ struct AdjustTables {
   double* nums;
   const uint64_t* numOffsets;  // nDocs + 1
   uint32_t* numCount;          // nDocs
+  // per document: its leaves' PropertiesManager records (Doc::pm*), 4 words each, at pmOffsets[doc]
+  uint32_t* pm;
+  const uint64_t* pmOffsets;   // nDocs + 1, in records
 };
 
 struct DocOutputs {
@@ -230,6 +233,9 @@ struct DocOutputs {
   // head, leaf words, scratch; chars slab: the text), where the large tier reads it
   uint32_t* bigCkpt;              // small tier: its leaves slab; large tier: the small slab to read
   uint16_t* bigCkptChars;
+  // annotate-adjust batches: per leaf, the prop-set id of getAtSeq(properties, minSeq), what the legacy
+  // summary reads (snapshotlegacy.ts:211-212); nullptr otherwise
+  uint16_t* legacyProps;
 };
 
 // Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
@@ -317,7 +323,10 @@ FMT_DEV uint32_t adjustFold(const AdjustTables* A, uint32_t doc, uint32_t cur, u
 // batches without such ops run the Rm = false code, which has none of it.
 // Adj: the variant that folds annotate-adjust entries (batches with adjusts; always with Ob, whose
 // runtime path restarts overflowing documents in the next tier instead of checkpointing them).
-template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false>
+// Lean: the variant for batches without catch-up recording, relative positions or loader segments
+// (no FMT_MT_F_CATCHUP / REL1 / REL2 / LOADSEG op): those paths, and the pointers they keep live
+// across the op loop, are compiled out, which frees scalar registers for the hot path.
+template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false, bool Lean = false>
 class Doc {
  public:
   using VR = typename C::VR;
@@ -1190,6 +1199,12 @@ class Doc {
       }
       waveSync();
     }
+    return internWork(cnt);
+  }
+
+  // The prop set s->kvWork[0 .. cnt) (key order kept) as an interned set id: an equal set already in
+  // the table, else a new one.
+  FMT_DEV uint32_t internWork(uint32_t cnt) {
     for (int base = 0; base < nProps; base += 64) {  // interned already? lane p checks prop set base + p
       Lane<bool> same;
       FOR_LANES(l) {
@@ -1212,6 +1227,290 @@ class Doc {
     }
     waveSync();
     return static_cast<uint32_t>(nProps++);
+  }
+
+  // ------------------------------------------------------------------ property managers (Adj)
+  // segment.propertyManager (segmentPropertiesManager.ts:140-345) of every leaf, kept for the legacy
+  // summary's getAtSeq(properties, minSeq) (snapshotlegacy.ts:211-212), as records in the document's
+  // HBM slab, in creation order: a head {leaf id, key, kind 0, value = msnConsensus} per (leaf, key)
+  // that has pending remote changes (the manager's Map order), and the pending changes {leaf id, key,
+  // kind 1, seq, value after the change}. A change's value after it is all a later fold needs: the
+  // fold of msnConsensus with a prefix of the list equals the value the last change of that prefix
+  // produced when it applied. A raw change folds straight into msnConsensus while its key has nothing
+  // pending (:213-221); updateMsn(msn) (:275-291) folds the changes at or below msn and drops a key
+  // left with none. Record words: leaf id (0: deleted), key | kind << 16, seq, value.
+  int pmN = 0;  // records in use (deleted ones included)
+  FMT_DEV uint32_t* pmBase() const { return in.adj->pm + 4 * in.adj->pmOffsets[in.doc]; }
+  FMT_DEV int pmCap() const { return static_cast<int>(in.adj->pmOffsets[in.doc + 1] - in.adj->pmOffsets[in.doc]); }
+  FMT_DEV uint32_t pmWord(int i, int w) const { return uni(loadCoherent(pmBase() + 4 * i + w)); }
+
+  // First record at or after `from` whose (leaf id, key | kind) match (~0u: any key / kind), or -1.
+  FMT_DEV int pmFind(uint32_t leaf, uint32_t keyKind, uint32_t mask, int from = 0) const {
+    const uint32_t* R = pmBase();
+    for (int base = from; base < pmN; base += 64) {
+      Lane<bool> p;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(p) = i < pmN && loadCoherent(R + 4 * i) == leaf && (loadCoherent(R + 4 * i + 1) & mask) == (keyKind & mask);
+      }
+      const uint64_t m = ballot(p);
+      if (m != 0) return base + ctz64(m);
+    }
+    return -1;
+  }
+
+  // Drops deleted records, keeping the order (a wave stream compaction in place).
+  FMT_DEV void pmCompact() {
+    uint32_t* R = pmBase();
+    int out = 0;
+    for (int base = 0; base < pmN; base += 64) {
+      Lane<uint32_t> w0, w1, w2, w3;
+      Lane<bool> live;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(w0) = i < pmN ? loadCoherent(R + 4 * i) : 0u;
+        LANE(w1) = i < pmN ? loadCoherent(R + 4 * i + 1) : 0u;
+        LANE(w2) = i < pmN ? loadCoherent(R + 4 * i + 2) : 0u;
+        LANE(w3) = i < pmN ? loadCoherent(R + 4 * i + 3) : 0u;
+        LANE(live) = LANE(w0) != 0u;
+      }
+      const uint64_t m = ballot(live);
+      FOR_LANES(l) {
+        if (LANE(live)) {
+          const int at = out + __builtin_popcountll(m & ((1ull << l) - 1ull));
+          storeGlobal(R + 4 * at, LANE(w0));
+          storeGlobal(R + 4 * at + 1, LANE(w1));
+          storeGlobal(R + 4 * at + 2, LANE(w2));
+          storeGlobal(R + 4 * at + 3, LANE(w3));
+        }
+      }
+      out += __builtin_popcountll(m);
+    }
+    pmN = out;
+  }
+
+  FMT_DEV bool pmAppend(uint32_t leaf, uint32_t keyKind, int seq, uint32_t value) {
+    if (pmN >= pmCap()) pmCompact();
+    if (pmN >= pmCap()) return fail(kCapFinal);
+    uint32_t* R = pmBase() + 4 * pmN;
+    FOR_LANES(l) {
+      if (l < 4) storeGlobal(R + l, l == 0 ? leaf : l == 1 ? keyKind : l == 2 ? static_cast<uint32_t>(seq) : value);
+    }
+    pmN++;
+    return true;
+  }
+
+  FMT_DEV void pmSet(int i, int w, uint32_t v) {
+    uint32_t* R = pmBase() + 4 * i + w;
+    FOR_LANES(l) {
+      if (l == 0) storeGlobal(R, v);
+    }
+  }
+
+  // updateMsn(msn) on the manager of leaf `leaf`.
+  FMT_DEV void pmUpdateMsn(uint32_t leaf, int msn) {
+    for (int h = pmFind(leaf, 0u, 0x10000u); h >= 0 && status == FMT_OK; h = pmFind(leaf, 0u, 0x10000u, h + 1)) {
+      const uint32_t key = pmWord(h, 1) & 0xFFFFu;
+      const uint32_t* R = pmBase();
+      int last = -1;
+      bool pending = false;
+      for (int base = h + 1; base < pmN; base += 64) {  // (a head precedes its key's changes)
+        Lane<bool> fold, keep;
+        FOR_LANES(l) {
+          const int i = base + l;
+          const bool mine = i < pmN && loadCoherent(R + 4 * i) == leaf && loadCoherent(R + 4 * i + 1) == (key | 0x10000u);
+          const int sq = mine ? static_cast<int>(loadCoherent(R + 4 * i + 2)) : 0;
+          LANE(fold) = mine && sq <= msn;
+          LANE(keep) = mine && sq > msn;
+        }
+        const uint64_t mf = ballot(fold), mk = ballot(keep);
+        if (mf != 0) last = base + 63 - __builtin_clzll(mf);
+        pending = pending || mk != 0;
+        FOR_LANES(l) {
+          if (LANE(fold)) storeGlobal(pmBase() + 4 * (base + l), 0u);  // folded: deleted
+        }
+      }
+      if (last >= 0) pmSet(h, 3, pmWord(last, 3));  // (a deleted record keeps its value word)
+      if (!pending) pmSet(h, 0, 0u);
+    }
+  }
+
+  // copyTo (segmentPropertiesManager.ts:300-316): a split's right part gets the left's records.
+  FMT_DEV void pmCopy(uint32_t from, uint32_t to) {
+    if (pmFind(from, 0u, 0u) < 0) return;
+    pmCompact();  // (no compaction while copying: record indices stay put)
+    const int end = pmN;
+    for (int i = pmFind(from, 0u, 0u); i >= 0 && i < end && status == FMT_OK; i = pmFind(from, 0u, 0u, i + 1)) {
+      if (pmN >= pmCap()) {
+        fail(kCapFinal);
+        return;
+      }
+      pmAppend(to, pmWord(i, 1), static_cast<int>(pmWord(i, 2)), pmWord(i, 3));
+    }
+  }
+
+  FMT_DEV void pmDropLeaf(uint32_t leaf) {  // the leaf left the tree (zamboni): its manager is unreachable
+    const uint32_t* R = pmBase();
+    for (int base = 0; base < pmN; base += 64) {
+      FOR_LANES(l) {
+        const int i = base + l;
+        if (i < pmN && loadCoherent(R + 4 * i) == leaf) storeGlobal(pmBase() + 4 * i, 0u);
+      }
+    }
+  }
+
+  // handleProperties (segmentPropertiesManager.ts:188-238) of an annotate op on leaf j, before the
+  // leaf's prop set changes: every change of the op in opToChanges order, then updateMsn(minSeq).
+  FMT_DEV void pmAnnotate(int j, uint32_t opId, int seq) {
+    const uint32_t leaf = fId(readField(j, 4));
+    const uint32_t old = propsAt(j);
+    uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
+    FOR_LANES(l) {
+      if (l < FMT_MT_PROPS_MAX) s->kvWork[l] = (old != kPropsUndef && l < static_cast<int>(cnt)) ? s->props[old].kv[l] : 0u;
+    }
+    waveSync();
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+      const uint32_t e = uni(in.propsKv[t]);
+      const uint32_t key = e >> 16;
+      const bool adjust = (e & 0xFFFFu) == FMT_MT_VALUE_ADJUST;
+      uint32_t pos = cnt;
+      for (uint32_t k = 0; k < cnt; k++)
+        if ((uni(s->kvWork[k]) >> 16) == key) pos = k;
+      const uint32_t before = pos < cnt ? uni(s->kvWork[pos]) & 0xFFFFu : 0u;
+      uint32_t after = e & 0xFFFFu;
+      if (adjust) {
+        if (++t >= b) {
+          fail(FMT_E_DATA);
+          return;
+        }
+        after = adjustFold(in.adj, in.doc, before, uni(in.propsKv[t]));
+        if (after == kAdjFailData || after == kAdjFailCap) {
+          fail(after == kAdjFailData ? FMT_E_DATA : kCapFinal);
+          return;
+        }
+      }
+      int h = pmFind(leaf, key, 0x1FFFFu);
+      if (h < 0) {
+        if (!pmAppend(leaf, key, 0, before)) return;
+        h = pmN - 1;
+      }
+      if (!adjust && pmFind(leaf, key | 0x10000u, 0x1FFFFu, h + 1) < 0) pmSet(h, 3, after);
+      else if (!pmAppend(leaf, key | 0x10000u, seq, after)) return;
+      // the working set follows the change (null deletes the key)
+      if (after == 0u) {
+        if (pos < cnt) {
+          for (uint32_t k = pos; k + 1 < cnt; k++) {
+            const uint32_t v = uni(s->kvWork[k + 1]);
+            waveSync();
+            FOR_LANES(l) {
+              if (l == 0) s->kvWork[k] = v;
+            }
+          }
+          cnt--;
+        }
+      } else if (pos < cnt) {
+        FOR_LANES(l) {
+          if (l == 0) s->kvWork[pos] = (key << 16) | after;
+        }
+      } else if (cnt < FMT_MT_PROPS_MAX) {
+        FOR_LANES(l) {
+          if (l == 0) s->kvWork[cnt] = (key << 16) | after;
+        }
+        cnt++;
+      }
+      waveSync();
+    }
+    pmUpdateMsn(leaf, minSeq);
+  }
+
+  // getAtSeq(properties, minSeq) of every leaf (segmentPropertiesManager.ts:328-344): leaves with a
+  // pending key get the interned set of their current properties with each pending key set to the
+  // value its changes at or below minSeq leave (null: deleted; a key the properties lack goes last, in
+  // the manager's key order); the others keep their set.
+  FMT_DEV void pmLegacyProps(uint16_t* out) {
+    const int nr = rows();
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const int idx = r * 64 + l;
+        if (idx < n) {
+          const uint32_t pid = propsL(l, r);
+          out[idx] = pid == kPropsUndef ? 0xFFFFu : static_cast<uint16_t>(pid);
+        }
+      }
+    }
+    const uint32_t* R = pmBase();
+    for (int h0 = 0; h0 < pmN && status == FMT_OK;) {
+      // the next head of a leaf not handled yet (a handled head's seq word gets bit 31)
+      int h = -1;
+      for (int base = h0; base < pmN && h < 0; base += 64) {
+        Lane<bool> p;
+        FOR_LANES(l) {
+          const int i = base + l;
+          LANE(p) = i < pmN && loadCoherent(R + 4 * i) != 0u && (loadCoherent(R + 4 * i + 1) & 0x10000u) == 0u &&
+                    (loadCoherent(R + 4 * i + 2) & 0x80000000u) == 0u;
+        }
+        const uint64_t m = ballot(p);
+        if (m != 0) h = base + ctz64(m);
+      }
+      if (h < 0) break;
+      const uint32_t leaf = pmWord(h, 0);
+      const int j = findLeafById(leaf);
+      uint32_t cnt = 0;
+      if (j >= 0) {
+        const uint32_t old = propsAt(j);
+        cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
+        FOR_LANES(l) {
+          if (l < FMT_MT_PROPS_MAX) s->kvWork[l] = (old != kPropsUndef && l < static_cast<int>(cnt)) ? s->props[old].kv[l] : 0u;
+        }
+        waveSync();
+      }
+      for (int g = h; g >= 0 && status == FMT_OK; g = pmFind(leaf, 0u, 0x10000u, g + 1)) {
+        pmSet(g, 2, 0x80000000u);  // (done: a head's seq word is otherwise unused)
+        if (j < 0) continue;
+        const uint32_t key = pmWord(g, 1) & 0xFFFFu;
+        uint32_t v = pmWord(g, 3);
+        for (int c = pmFind(leaf, key | 0x10000u, 0x1FFFFu, g + 1); c >= 0; c = pmFind(leaf, key | 0x10000u, 0x1FFFFu, c + 1)) {
+          if (static_cast<int>(pmWord(c, 2)) > minSeq) break;  // (a key's changes are in seq order)
+          v = pmWord(c, 3);
+        }
+        uint32_t pos = cnt;
+        for (uint32_t k = 0; k < cnt; k++)
+          if ((uni(s->kvWork[k]) >> 16) == key) pos = k;
+        if (v == 0u) {
+          if (pos < cnt) {
+            for (uint32_t k = pos; k + 1 < cnt; k++) {
+              const uint32_t x = uni(s->kvWork[k + 1]);
+              waveSync();
+              FOR_LANES(l) {
+                if (l == 0) s->kvWork[k] = x;
+              }
+            }
+            cnt--;
+          }
+        } else if (pos < cnt) {
+          FOR_LANES(l) {
+            if (l == 0) s->kvWork[pos] = (key << 16) | v;
+          }
+        } else if (cnt < FMT_MT_PROPS_MAX) {
+          FOR_LANES(l) {
+            if (l == 0) s->kvWork[cnt] = (key << 16) | v;
+          }
+          cnt++;
+        } else {
+          fail(kCapFinal);
+        }
+        waveSync();
+      }
+      if (j >= 0 && status == FMT_OK) {
+        const uint32_t id = internWork(cnt);
+        if (status != FMT_OK) break;
+        FOR_LANES(l) {
+          if (l == 0) out[j] = static_cast<uint16_t>(id);
+        }
+      }
+      h0 = h + 1;
+    }
   }
 
   // ------------------------------------------------------------------ annotate-adjust
@@ -1397,6 +1696,9 @@ class Doc {
         }
         rmPendN++;
       }
+    }
+    if constexpr (Adj) {  // copyPropertiesAndManager (mergeTree.ts:1784)
+      if (pmN > 0) pmCopy(fId(w4), fId(rec.w[4]));
     }
     writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0)));
     if (!insertLeafAt(j + 1, rec)) return false;
@@ -1862,7 +2164,7 @@ class Doc {
   }
 
   FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
-    const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
+    const bool catchup = !Lean && (op.flags & FMT_MT_F_CATCHUP) != 0;
     Lane<uint32_t> delta;  // catch-up: the segments of the op's delta event (row bitmask per lane)
     if (op.type == FMT_MT_INSERT) {
       const int k = insertText(op, text0);
@@ -1875,14 +2177,14 @@ class Doc {
       if (!applyRange(op, delta)) return;
     }
     // one call site: the recording is inlined once; a sided obliterate raises OBLITERATE (:2249-2253)
-    recordCatchup(delta, op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
+    if constexpr (!Lean) recordCatchup(delta, op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
   }
 
   // Remove / annotate (after their boundary splits); fills `delta` for catch-up ops. Returns true
   // when a catch-up recording should follow.
   FMT_DEV bool applyRange(const fmt_mt_op& op, Lane<uint32_t>& delta) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
-    const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
+    const bool catchup = !Lean && (op.flags & FMT_MT_F_CATCHUP) != 0;
     bool obliterate = false;
     if constexpr (Ob) obliterate = op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED;
     const int start = op.pos1, end = op.pos2;
@@ -1996,6 +2298,17 @@ class Doc {
       }
     } else {
       // annotateRange (mergeTree.ts:2009-2081): one prop-set transition per distinct old set
+      if constexpr (Adj) {  // each hit leaf's PropertiesManager, in nodeMap order
+        for (Lane<uint32_t> t = hits;;) {
+          const int j = firstSet(t, nr);
+          if (j < 0 || status != FMT_OK) break;
+          FOR_LANES(l) {
+            if (l == (j & 63)) LANE(t) &= ~(1u << (j >> 6));
+          }
+          pmAnnotate(j, op.payload, seq);
+        }
+        if (status != FMT_OK) return false;
+      }
       Lane<uint32_t> todo = hits;
       for (;;) {
         const int j = firstSet(todo, nr);
@@ -2161,6 +2474,9 @@ class Doc {
       }
       nChars = newChars;
     }
+    if constexpr (Adj) {  // appended and unlinked leaves take their managers with them
+      for (uint32_t m = pmN > 0 ? (mergeMask | dropMask) : 0u; m != 0; m &= m - 1) pmDropLeaf(fId(readField(first + ctz32(m), 4)));
+    }
     deleteLeaves(first, cnt, mergeMask | dropMask);
     stamp(kPfZDelete);
     return kept;
@@ -2216,6 +2532,9 @@ class Doc {
   FMT_DEV void zamboni() {
     for (int i = 0; i < 2; i++) {
       if (heapN == 0) break;
+      if constexpr (Adj) {  // segmentToScour?.segment?.propertyManager?.updateMsn(minSeq) (zamboni.ts:44)
+        if (pmN > 0) pmUpdateMsn(uni(s->heap[1].leafId), minSeq);
+      }
       if (heapSeq(1) > minSeq) break;
       const HeapEnt ent = heapGet();
       const int j = findLeafById(ent.leafId);
@@ -2632,9 +2951,11 @@ class Doc {
       txt0 = fetchText(rec0);
       rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
-      opIdx = static_cast<uint32_t>(i - in.begin);
-      const bool loader = (op.flags & FMT_MT_F_LOADSEG) != 0;
-      if (loader) {
+      if constexpr (!Lean) opIdx = static_cast<uint32_t>(i - in.begin);
+      const bool loader = !Lean && (op.flags & FMT_MT_F_LOADSEG) != 0;
+      if (Lean && (op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) != 0) {
+        fail(FMT_E_USAGE);  // (the runtime picks the Lean variant only for batches without them)
+      } else if (loader) {
         if (op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient) loadBodySegment(op, text);
         else fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
       } else if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63
@@ -2642,7 +2963,7 @@ class Doc {
       else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
-      else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
+      else if (Lean || (op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
       if constexpr (Rm) {
         if (rmPendN > 0 || rmHitsSet)
           rmFlush(op.client, op.seq, op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE);
@@ -2676,6 +2997,9 @@ class Doc {
   }
 
   FMT_DEV void writeOutputs(const DocOutputs& out) {
+    if constexpr (Adj) {
+      if (out.legacyProps != nullptr && status == FMT_OK) pmLegacyProps(out.legacyProps);
+    }
     const int nr = rows();
     // char offsets and leaf-block ordinals
     Lane<VR> cst;
@@ -2796,6 +3120,7 @@ class Doc {
           if (l == 0) storeGlobal(in.adj->numCount + in.doc, 0u);
         }
       }
+      pmN = 0;
       if (in.loaded) loadSnapshot();
       else loadInitial();
     }

@@ -43,6 +43,35 @@ struct DevBuf {
   }
 };
 
+// Large host <-> device copies through pinned staging. The caller's arrays are pageable (numpy, JS
+// ArrayBuffers), which the DMA engines reach only through the runtime's own small bounce buffer
+// (measured: 4.3 GB/s H2D for T1's 7.3 GB, 0.18 GB/s for the catch-up fetch). Here kStageWorkers
+// host threads each own two pinned chunks and a stream, and move every kStageWorkers-th chunk of
+// the copy: one chunk's host memcpy overlaps the DMA of the chunk before it.
+constexpr size_t kStageChunk = 8u << 20;
+constexpr int kStageWorkers = 8;
+constexpr size_t kStageMin = 16u << 20;  // smaller copies go straight through hipMemcpy
+
+struct Stager {
+  bool ready = false;
+  void* buf[kStageWorkers][2] = {};
+  hipStream_t st[kStageWorkers] = {};
+  hipEvent_t ev[kStageWorkers][2] = {};
+  void release() {
+    for (int w = 0; w < kStageWorkers; w++) {
+      for (int k = 0; k < 2; k++) {
+        if (buf[w][k]) (void)hipHostFree(buf[w][k]);
+        if (ev[w][k]) (void)hipEventDestroy(ev[w][k]);
+        buf[w][k] = nullptr;
+        ev[w][k] = nullptr;
+      }
+      if (st[w]) (void)hipStreamDestroy(st[w]);
+      st[w] = nullptr;
+    }
+    ready = false;
+  }
+};
+
 }  // namespace
 
 struct fmt_ctx {
@@ -106,6 +135,7 @@ struct fmt_ctx {
   DevBuf<fmt_mt_catchup_range> mtCatchup;    // catch-up range slabs
   std::vector<uint64_t> mtCuOffsHost;
   bool mtHasCatchup = false;
+  bool mtLean = false;                       // no catch-up / relative-position / loader-segment op (Lean kernels)
   DevBuf<uint64_t> mtRmOffs;                 // per-doc remove-order slab offsets (n_docs + 1)
   DevBuf<fmt_mt_remove_order> mtRmOrder;     // remove-order slabs (FMT_MT_F_RMORDER ops)
   std::vector<uint64_t> mtRmOffsHost;
@@ -141,9 +171,16 @@ struct fmt_ctx {
   DevBuf<unsigned long long> sumCursors;
   DevBuf<fmt_kernels::SumDocOut> sumDocs;
   DevBuf<uint64_t> digests;                   // fmt_mt_state_digest output
+  Stager stage;                               // pinned staging of large host <-> device copies
+  DevBuf<fmt_kernels::GatherSpan> spans;      // packing before a D2H copy
+  DevBuf<uint32_t> packed;
   std::vector<std::string> sumBlobs;          // per document: header, then body
   std::vector<uint32_t> sumSplit;             // per document: header length in sumBlobs[d]
   std::vector<int32_t> sumStatus;
+  std::vector<fmt_kernels::SumDocOut> sumHostDocs;  // host copies of the device runs / text / prop sets
+  std::vector<fmt_kernels::SumRun> sumHostRuns;
+  std::vector<uint16_t> sumHostText;
+  std::vector<fmt_mt_propset> sumHostProps;
   // annotate-adjust: rows, numbers of host value ids, host numbers sorted for number → id lookups,
   // per-document computed-number slabs and their counts
   DevBuf<fmt_mt_adjust> mtAdjusts;
@@ -152,7 +189,10 @@ struct fmt_ctx {
   DevBuf<uint64_t> mtNumOffs;
   DevBuf<fmt_mt::AdjustTables> mtAdjTab;      // the pointers above, for the kernels
   std::vector<uint64_t> mtNumOffsHost;
-  std::vector<int32_t> mtAdjLastSeq;          // per doc: last seq of an annotate of an adjusted key (0: none)
+  DevBuf<uint32_t> mtPm;                      // PropertiesManager records (4 words each) per document
+  DevBuf<uint64_t> mtPmOffs;
+  std::vector<uint64_t> mtPmOffsHost;
+  DevBuf<uint16_t> mtLegacy, mtBigLegacy;     // per leaf: the getAtSeq(minSeq) prop set (small / large slabs)
   bool mtHasAdjust = false;
   uint32_t mtNAdjusts = 0, mtNValues = 0, mtNNumSorted = 0;
   DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
@@ -181,6 +221,82 @@ int hipErr(fmt_ctx* c, hipError_t e, const char* what) {
     hipError_t e_ = (expr);                                \
     if (e_ != hipSuccess) return hipErr((ctx), e_, #expr); \
   } while (0)
+
+hipError_t stageInit(fmt_ctx* c) {
+  Stager& S = c->stage;
+  if (S.ready) return hipSuccess;
+  for (int w = 0; w < kStageWorkers; w++) {
+    for (int k = 0; k < 2; k++) {
+      hipError_t e = hipHostMalloc(&S.buf[w][k], kStageChunk, hipHostMallocDefault);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&S.ev[w][k], hipEventDisableTiming);
+      if (e != hipSuccess) {
+        S.release();
+        return e;
+      }
+    }
+    const hipError_t e = hipStreamCreateWithFlags(&S.st[w], hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      S.release();
+      return e;
+    }
+  }
+  S.ready = true;
+  return hipSuccess;
+}
+
+// Copies `bytes` between pageable host memory and the device, synchronously with respect to the
+// ctx stream (it waits for the work already queued there first). toDevice: dst is device memory.
+hipError_t stagedCopy(fmt_ctx* c, void* dst, const void* src, size_t bytes, bool toDevice) {
+  if (bytes == 0) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return e;
+  if (bytes < kStageMin || stageInit(c) != hipSuccess)  // (no pinned memory: the runtime's own path)
+    return hipMemcpy(dst, src, bytes, toDevice ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost);
+  const size_t nChunks = (bytes + kStageChunk - 1) / kStageChunk;
+  const int workers = static_cast<int>(std::min<size_t>(kStageWorkers, nChunks));
+  std::vector<hipError_t> errs(workers, hipSuccess);
+  std::vector<std::thread> pool;
+  for (int w = 0; w < workers; w++)
+    pool.emplace_back([&, w] {
+      Stager& S = c->stage;
+      hipError_t err = hipSetDevice(c->device);
+      auto span = [&](size_t k) { return std::min(kStageChunk, bytes - k * kStageChunk); };
+      if (toDevice) {
+        int slot = 0;
+        for (size_t k = w; k < nChunks && err == hipSuccess; k += workers, slot ^= 1) {
+          err = hipEventSynchronize(S.ev[w][slot]);  // the DMA that last read this chunk is done
+          if (err != hipSuccess) break;
+          std::memcpy(S.buf[w][slot], static_cast<const char*>(src) + k * kStageChunk, span(k));
+          err = hipMemcpyAsync(static_cast<char*>(dst) + k * kStageChunk, S.buf[w][slot], span(k), hipMemcpyHostToDevice,
+                               S.st[w]);
+          if (err == hipSuccess) err = hipEventRecord(S.ev[w][slot], S.st[w]);
+        }
+      } else {
+        // two chunks in flight: issue both, then drain one and refill it while the other lands
+        auto issue = [&](size_t k, int slot) {
+          hipError_t r = hipMemcpyAsync(S.buf[w][slot], static_cast<const char*>(src) + k * kStageChunk, span(k),
+                                        hipMemcpyDeviceToHost, S.st[w]);
+          return r == hipSuccess ? hipEventRecord(S.ev[w][slot], S.st[w]) : r;
+        };
+        size_t k0 = w, k1 = w + workers;
+        if (k0 < nChunks) err = issue(k0, 0);
+        if (err == hipSuccess && k1 < nChunks) err = issue(k1, 1);
+        int slot = 0;
+        for (size_t k = k0; k < nChunks && err == hipSuccess; k += workers, slot ^= 1) {
+          err = hipEventSynchronize(S.ev[w][slot]);
+          if (err != hipSuccess) break;
+          std::memcpy(static_cast<char*>(dst) + k * kStageChunk, S.buf[w][slot], span(k));
+          if (k + 2 * workers < nChunks) err = issue(k + 2 * workers, slot);
+        }
+      }
+      const hipError_t e2 = hipStreamSynchronize(S.st[w]);
+      errs[w] = err != hipSuccess ? err : e2;
+    });
+  for (auto& t : pool) t.join();
+  for (hipError_t x : errs)
+    if (x != hipSuccess) return x;
+  return hipSuccess;
+}
 
 }  // namespace
 
@@ -266,6 +382,14 @@ void fmt_close(fmt_ctx* c) {
   c->hugeStates.release();
   c->hugeInputs.release();
   c->hugeOuts.release();
+  c->stage.release();
+  c->mtPm.release();
+  c->mtPmOffs.release();
+  c->mtLegacy.release();
+  c->mtBigLegacy.release();
+  c->spans.release();
+  c->packed.release();
+  c->digests.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -341,7 +465,7 @@ static int mapStage(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint
   } else {
     FMT_HIP(c, c->mapOut.reserve(static_cast<size_t>(nDocs) * keyBound));
   }
-  if (nOps) FMT_HIP(c, hipMemcpyAsync(c->mapOps.p, ops, nOps * sizeof(fmt_map_op), hipMemcpyHostToDevice, c->stream));
+  if (nOps) FMT_HIP(c, stagedCopy(c, c->mapOps.p, ops, nOps * sizeof(fmt_map_op), true));
   FMT_HIP(c, hipMemcpyAsync(c->mapOffs.p, offs, (nDocs + 1ull) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   FMT_HIP(c, hipStreamSynchronize(c->stream));
   c->mapNOps = nOps;
@@ -570,10 +694,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
   uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
   bool obliterates = false;
+  uint32_t rareFlags = 0;
   for (uint64_t i = 0; i < b->n_ops; i++) {
     const fmt_mt_op& op = b->ops[i];
     if (op.flags & FMT_MT_F_CATCHUP) catchupOps++;
     if (op.flags & FMT_MT_F_RMORDER) rmOrderOps++;
+    rareFlags |= op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG);
     if (op.flags & FMT_MT_F_LOADSEG) {  // a SnapshotV1 body segment: its merge info row in range
       if (op.type != FMT_MT_INSERT || b->snapshot_info == nullptr || op.pos1 < 0 ||
           static_cast<uint64_t>(op.pos1) >= b->n_snapshot_segs ||
@@ -670,6 +796,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
   // any; a document that needs more reports FMT_E_CAPACITY.
   c->mtHasCatchup = catchupOps > 0;
+  c->mtLean = rareFlags == 0;
   if (c->mtHasCatchup) {
     constexpr uint64_t kCatchupPerOp = 16, kCatchupPerDoc = 16;
     c->mtCuOffsHost.assign(n + 1ull, 0);
@@ -700,37 +827,24 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) : hipSuccess;
   };
-  // Computed-number slabs: 8 per adjust entry of the document's annotates + 16 (at most 0x7fff,
-  // the computed id range); a document that computes more distinct numbers reports FMT_E_CAPACITY.
+  // Computed-number slabs: 64 per adjust entry of the document's annotates + 64 (at most 0x7fff, the
+  // computed id range: one adjust over a range can compute a new number per leaf it hits); a document
+  // that computes more distinct numbers reports FMT_E_CAPACITY. PropertiesManager record slabs
+  // (mt_engine.h Doc::pm*): 32 per change of the document's annotates + 256 records.
   c->mtHasAdjust = anyAdjust;
-  c->mtAdjLastSeq.assign(n, 0);
   if (anyAdjust) {
     c->mtNumOffsHost.assign(n + 1ull, 0);
+    c->mtPmOffsHost.assign(n + 1ull, 0);
     for (uint32_t d = 0; d < n; d++) {
-      uint64_t f = 0;
-      std::vector<uint32_t> adjKeys;  // keys some annotate of this document adjusts
-      for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
-        const fmt_mt_op& op = b->ops[i];
-        if (op.type != FMT_MT_ANNOTATE || adjCount[op.payload] == 0) continue;
-        f += adjCount[op.payload];
-        for (uint32_t t = b->props_off[op.payload]; t < b->props_off[op.payload + 1]; t++)
-          if ((b->props_kv[t] & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
-            adjKeys.push_back(b->props_kv[t] >> 16);
-            t++;
-          }
-      }
-      c->mtNumOffsHost[d + 1] = c->mtNumOffsHost[d] + (f ? std::min<uint64_t>(8 * f + 16, 0x7FFF) : 0);
-      if (adjKeys.empty()) continue;
-      // legacy getAtSeq(minSeq) is exact unless an adjusted key is annotated above the final minSeq
+      uint64_t f = 0, g = 0;
       for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
         const fmt_mt_op& op = b->ops[i];
         if (op.type != FMT_MT_ANNOTATE) continue;
-        for (uint32_t t = b->props_off[op.payload]; t < b->props_off[op.payload + 1]; t++) {
-          if (std::find(adjKeys.begin(), adjKeys.end(), b->props_kv[t] >> 16) != adjKeys.end())
-            c->mtAdjLastSeq[d] = std::max(c->mtAdjLastSeq[d], op.seq);
-          if ((b->props_kv[t] & 0xFFFFu) == FMT_MT_VALUE_ADJUST) t++;
-        }
+        f += adjCount[op.payload];
+        g += b->props_off[op.payload + 1] - b->props_off[op.payload];
       }
+      c->mtNumOffsHost[d + 1] = c->mtNumOffsHost[d] + (f ? std::min<uint64_t>(64 * f + 64, 0x7FFF) : 0);
+      c->mtPmOffsHost[d + 1] = c->mtPmOffsHost[d] + (g ? std::min<uint64_t>(32 * g + 256, 1u << 20) : 0);
     }
     std::vector<std::pair<double, uint32_t>> nums;
     for (uint32_t i = 0; b->value_num && i < b->n_values; i++)
@@ -753,6 +867,10 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, c->mtNumOffs.reserve(n + 1ull));
     FMT_HIP(c, c->mtNums.reserve(c->mtNumOffsHost[n]));
     FMT_HIP(c, c->mtNumCount.reserve(n));
+    FMT_HIP(c, c->mtPmOffs.reserve(n + 1ull));
+    FMT_HIP(c, c->mtPm.reserve(4 * c->mtPmOffsHost[n]));
+    FMT_HIP(c, c->mtLegacy.reserve(static_cast<size_t>(n) * caps.leaves));
+    FMT_HIP(c, cp(c->mtPmOffs.p, c->mtPmOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
     FMT_HIP(c, cp(c->mtAdjusts.p, b->adjusts, b->n_adjusts * sizeof(fmt_mt_adjust)));
     FMT_HIP(c, cp(c->mtValueNum.p, b->value_num, c->mtNValues * sizeof(double)));
     FMT_HIP(c, cp(c->mtNumSorted.p, sv.data(), sv.size() * sizeof(double)));
@@ -770,20 +888,22 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     T.nums = c->mtNums.p;
     T.numOffsets = c->mtNumOffs.p;
     T.numCount = c->mtNumCount.p;
+    T.pm = c->mtPm.p;
+    T.pmOffsets = c->mtPmOffs.p;
     FMT_HIP(c, c->mtAdjTab.reserve(1));
     FMT_HIP(c, cp(c->mtAdjTab.p, &T, sizeof T));
     FMT_HIP(c, hipStreamSynchronize(c->stream));  // (sv / si / T are about to go out of scope)
   }
-  FMT_HIP(c, cp(c->mtOps.p, b->ops, b->n_ops * sizeof(fmt_mt_op)));
+  FMT_HIP(c, stagedCopy(c, c->mtOps.p, b->ops, b->n_ops * sizeof(fmt_mt_op), true));
   FMT_HIP(c, cp(c->mtOffs.p, b->doc_op_offsets, (n + 1ull) * sizeof(uint64_t)));
-  FMT_HIP(c, cp(c->mtText.p, b->text, b->text_len * sizeof(uint16_t)));
+  FMT_HIP(c, stagedCopy(c, c->mtText.p, b->text, b->text_len * sizeof(uint16_t), true));
   if (b->doc_init) FMT_HIP(c, cp(c->mtInit.p, b->doc_init, 2ull * n * sizeof(uint32_t)));
   c->mtHasSnap = b->snapshots != nullptr;
   if (c->mtHasSnap) {
     FMT_HIP(c, c->mtSnap.reserve(n));
     FMT_HIP(c, c->mtSnapSegs.reserve(b->n_snapshot_segs));
     FMT_HIP(c, cp(c->mtSnap.p, b->snapshots, n * sizeof(fmt_mt_snapshot_doc)));
-    FMT_HIP(c, cp(c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg)));
+    FMT_HIP(c, stagedCopy(c, c->mtSnapSegs.p, b->snapshot_segs, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_seg), true));
   }
   c->mtHasSnapInfo = c->mtHasSnap && b->snapshot_info != nullptr;
   c->mtNSnapSegs = b->n_snapshot_segs;
@@ -946,7 +1066,8 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasAdjust ? c->mtAdjTab.p : nullptr};
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
-                                !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr};
+                                !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr,
+                                c->mtHasAdjust ? c->mtLegacy.p : nullptr};
   FMT_HIP(c, hipMemsetAsync(c->mtEsc.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
@@ -956,7 +1077,7 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,
                                             c->mtObliterate,
-                                            c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust));
+                                            c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust, c->mtLean));
   if (hasHuge)
     FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p, c->mtHugeLoaded, c->stream));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));  // device time excludes the host read-back below
@@ -972,10 +1093,12 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigLeaves.reserve(static_cast<size_t>(nEsc) * big.leaves));
     FMT_HIP(c, c->mtBigChars.reserve(static_cast<size_t>(nEsc) * big.chars));
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
+    if (c->mtHasAdjust) FMT_HIP(c, c->mtBigLegacy.reserve(static_cast<size_t>(nEsc) * big.leaves));
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
                                   c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
                                   c->mtObliterate && !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr,
-                                  !c->mtHasRmOrder ? c->mtLeaves.p : nullptr, !c->mtHasRmOrder ? c->mtChars.p : nullptr};
+                                  !c->mtHasRmOrder ? c->mtLeaves.p : nullptr, !c->mtHasRmOrder ? c->mtChars.p : nullptr,
+                                  c->mtHasAdjust ? c->mtBigLegacy.p : nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
                                                  c->mtHasRmOrder, c->mtSched.p + 2, c->mtHasAdjust));
@@ -1256,14 +1379,15 @@ void docViews(const fmt_ctx* c, std::vector<fmt_kernels::SumView>& views) {
     const int32_t hs = d < c->mtHugeSlot.size() ? c->mtHugeSlot[d] : -1;
     if (hs >= 0) {
       const fmt_kernels::HugeOut& O = c->huge[static_cast<size_t>(hs)].out;
-      views[d] = {O.leaves, O.chars, O.props};
+      views[d] = {O.leaves, O.chars, O.props, nullptr};
     } else {
       const int32_t slot = d < c->mtBigSlot.size() ? c->mtBigSlot[d] : -1;
       const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(slot >= 0);
       const size_t at = slot >= 0 ? static_cast<size_t>(slot) : d;
       views[d] = {(slot >= 0 ? c->mtBigLeaves.p : c->mtLeaves.p) + at * caps.leaves,
                   (slot >= 0 ? c->mtBigChars.p : c->mtChars.p) + at * caps.chars,
-                  (slot >= 0 ? c->mtBigProps.p : c->mtProps.p) + at * caps.props};
+                  (slot >= 0 ? c->mtBigProps.p : c->mtProps.p) + at * caps.props,
+                  c->mtHasAdjust ? (slot >= 0 ? c->mtBigLegacy.p : c->mtLegacy.p) + at * caps.leaves : nullptr};
     }
   }
 }
@@ -1319,34 +1443,39 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
   FMT_HIP(c, hipStreamSynchronize(c->stream));
   float kms = 0.f;
   FMT_HIP(c, hipEventElapsedTime(&kms, c->evS0, c->evS1));
-  // fetch: per-document spans, runs, text and the prop sets the runs name
+  // fetch: per-document spans, runs, text and every document's prop sets (packed on the device:
+  // only the sets a document has, not its tier's whole table), staged into host buffers the ctx keeps
   const auto t0 = clk::now();
   unsigned long long cur[2];
   FMT_HIP(c, hipMemcpy(cur, c->sumCursors.p, sizeof cur, hipMemcpyDeviceToHost));
-  std::vector<fmt_kernels::SumDocOut> docs(nd);
-  std::vector<fmt_kernels::SumRun> runs(cur[0] ? cur[0] : 1);
-  std::vector<uint16_t> text(cur[1] ? cur[1] : 1);
-  FMT_HIP(c, hipMemcpyAsync(docs.data(), c->sumDocs.p, nd * sizeof(fmt_kernels::SumDocOut), hipMemcpyDeviceToHost, c->stream));
-  if (cur[0]) FMT_HIP(c, hipMemcpyAsync(runs.data(), c->sumRuns.p, cur[0] * sizeof(fmt_kernels::SumRun), hipMemcpyDeviceToHost, c->stream));
-  if (cur[1]) FMT_HIP(c, hipMemcpyAsync(text.data(), c->sumText.p, cur[1] * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
-  // prop sets: the small tier's slab in one copy, the other documents' tables one by one
-  const uint32_t smallCap = fmt_kernels::mergeTreeCaps(false).props;
-  std::vector<fmt_mt_propset> smallProps(static_cast<size_t>(nd) * smallCap + 1);
-  FMT_HIP(c, hipMemcpyAsync(smallProps.data(), c->mtProps.p, static_cast<size_t>(nd) * smallCap * sizeof(fmt_mt_propset),
-                            hipMemcpyDeviceToHost, c->stream));
-  std::vector<const fmt_mt_propset*> propsHost(nd);
-  std::vector<std::vector<fmt_mt_propset>> otherProps;
+  constexpr uint32_t kPW = sizeof(fmt_mt_propset) / 4;
+  std::vector<uint64_t> propOff(nd + 1ull, 0);
+  std::vector<fmt_kernels::GatherSpan> sp;
   for (uint32_t d = 0; d < nd; d++) {
-    const bool small = !((d < c->mtHugeSlot.size() && c->mtHugeSlot[d] >= 0) || (d < c->mtBigSlot.size() && c->mtBigSlot[d] >= 0));
-    if (small || hdr[d].n_props == 0) {
-      propsHost[d] = smallProps.data() + static_cast<size_t>(d) * smallCap;
-      continue;
-    }
-    otherProps.emplace_back(hdr[d].n_props);
-    FMT_HIP(c, hipMemcpyAsync(otherProps.back().data(), propsDev[d], hdr[d].n_props * sizeof(fmt_mt_propset),
-                              hipMemcpyDeviceToHost, c->stream));
-    propsHost[d] = otherProps.back().data();
+    propOff[d + 1] = propOff[d] + hdr[d].n_props;
+    if (hdr[d].n_props)
+      sp.push_back({reinterpret_cast<const uint32_t*>(propsDev[d]), propOff[d] * kPW, hdr[d].n_props * kPW, 0u});
   }
+  if (!sp.empty()) {
+    FMT_HIP(c, c->spans.reserve(sp.size()));
+    FMT_HIP(c, c->packed.reserve(propOff[nd] * kPW));
+    FMT_HIP(c, hipMemcpyAsync(c->spans.p, sp.data(), sp.size() * sizeof(fmt_kernels::GatherSpan), hipMemcpyHostToDevice,
+                              c->stream));
+    FMT_HIP(c, fmt_kernels::launchGatherSpans(c->spans.p, static_cast<uint32_t>(sp.size()), c->packed.p, c->numCUs, c->stream));
+  }
+  if (c->sumHostDocs.size() < nd) c->sumHostDocs.resize(nd);
+  if (c->sumHostRuns.size() < cur[0]) c->sumHostRuns.resize(cur[0]);
+  if (c->sumHostText.size() < cur[1]) c->sumHostText.resize(cur[1]);
+  if (c->sumHostProps.size() < propOff[nd] + 1) c->sumHostProps.resize(propOff[nd] + 1);
+  FMT_HIP(c, stagedCopy(c, c->sumHostDocs.data(), c->sumDocs.p, nd * sizeof(fmt_kernels::SumDocOut), false));
+  FMT_HIP(c, stagedCopy(c, c->sumHostRuns.data(), c->sumRuns.p, cur[0] * sizeof(fmt_kernels::SumRun), false));
+  FMT_HIP(c, stagedCopy(c, c->sumHostText.data(), c->sumText.p, cur[1] * sizeof(uint16_t), false));
+  if (propOff[nd]) FMT_HIP(c, stagedCopy(c, c->sumHostProps.data(), c->packed.p, propOff[nd] * sizeof(fmt_mt_propset), false));
+  const fmt_kernels::SumDocOut* docs = c->sumHostDocs.data();
+  const fmt_kernels::SumRun* runs = c->sumHostRuns.data();
+  const uint16_t* text = c->sumHostText.data();
+  std::vector<const fmt_mt_propset*> propsHost(nd);
+  for (uint32_t d = 0; d < nd; d++) propsHost[d] = c->sumHostProps.data() + propOff[d];
   // computed annotate-adjust numbers of the documents that have any
   std::vector<std::vector<double>> docNums(c->mtHasAdjust ? nd : 0);
   if (c->mtHasAdjust) {
@@ -1381,11 +1510,6 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
           c->sumStatus[d] = static_cast<int32_t>(o.status);
           continue;
         }
-        // getAtSeq(minSeq) would fold only part of a segment's pending adjust history
-        if (c->mtHasAdjust && c->mtAdjLastSeq[d] > hdr[d].min_seq) {
-          c->sumStatus[d] = FMT_E_UNSUPPORTED;
-          continue;
-        }
         const std::vector<double>* nums = c->mtHasAdjust ? &docNums[d] : nullptr;
         // every prop set a run names, and every key / value id in it, within the tables passed in
         bool bad = false;
@@ -1408,7 +1532,7 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
           continue;
         }
         c->sumBlobs[d].reserve(o.n_units + 64ull * o.n_runs + 256);
-        legacyBlobs(c->sumBlobs[d], &c->sumSplit[d], runs.data() + o.run_off, o.n_runs, text.data() + o.text_off,
+        legacyBlobs(c->sumBlobs[d], &c->sumSplit[d], runs + o.run_off, o.n_runs, text + o.text_off,
                     propsHost[d], hdr[d].min_seq, chunk ? chunk : 10000u, D, nums);
       }
     });
@@ -1468,13 +1592,22 @@ int fmt_mt_fetch_catchup_all(fmt_ctx* c, uint64_t* offsets, fmt_mt_catchup_range
   }
   if (out == nullptr) return FMT_OK;
   if (cap < offsets[nd]) return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_catchup_all: cap below the ranges recorded");
-  // one copy of the whole slab region, then each document's recorded prefix packed on the host
-  std::vector<fmt_mt_catchup_range> slab(c->mtCuOffsHost[nd] ? c->mtCuOffsHost[nd] : 1);
-  if (c->mtCuOffsHost[nd])
-    FMT_HIP(c, hipMemcpy(slab.data(), c->mtCatchup.p, c->mtCuOffsHost[nd] * sizeof(fmt_mt_catchup_range), hipMemcpyDeviceToHost));
+  // each document's recorded prefix packed on the device (gatherSpansKernel), then one staged copy of
+  // exactly the recorded ranges
+  constexpr uint32_t kW = sizeof(fmt_mt_catchup_range) / 4;
+  std::vector<fmt_kernels::GatherSpan> sp;
+  sp.reserve(nd);
   for (uint32_t d = 0; d < nd; d++)
     if (offsets[d + 1] > offsets[d])
-      std::memcpy(out + offsets[d], slab.data() + c->mtCuOffsHost[d], (offsets[d + 1] - offsets[d]) * sizeof(fmt_mt_catchup_range));
+      sp.push_back({reinterpret_cast<const uint32_t*>(c->mtCatchup.p + c->mtCuOffsHost[d]), offsets[d] * kW,
+                    static_cast<uint32_t>(offsets[d + 1] - offsets[d]) * kW, 0u});
+  if (offsets[nd] == 0) return FMT_OK;
+  FMT_HIP(c, c->spans.reserve(sp.size()));
+  FMT_HIP(c, c->packed.reserve(offsets[nd] * kW));
+  FMT_HIP(c, hipMemcpyAsync(c->spans.p, sp.data(), sp.size() * sizeof(fmt_kernels::GatherSpan), hipMemcpyHostToDevice,
+                            c->stream));
+  FMT_HIP(c, fmt_kernels::launchGatherSpans(c->spans.p, static_cast<uint32_t>(sp.size()), c->packed.p, c->numCUs, c->stream));
+  FMT_HIP(c, stagedCopy(c, out, c->packed.p, offsets[nd] * sizeof(fmt_mt_catchup_range), false));
   return FMT_OK;
 }
 
@@ -1486,6 +1619,25 @@ int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
   const uint32_t m = h.n_rm_order < cap ? h.n_rm_order : cap;
   if (m) FMT_HIP(c, hipMemcpy(out, c->mtRmOrder.p + c->mtRmOffsHost[doc], m * sizeof(fmt_mt_remove_order), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_legacy_props(fmt_ctx* c, uint32_t doc, uint16_t* out, uint32_t cap) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_legacy_props: bad arguments");
+  fmt_mt_doc_result h;
+  FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
+  const uint32_t m = h.n_leaves < cap ? h.n_leaves : cap;
+  if (m == 0) return FMT_OK;
+  std::vector<fmt_kernels::SumView> views;
+  docViews(c, views);
+  if (views[doc].legacyProps != nullptr) {
+    FMT_HIP(c, hipMemcpy(out, views[doc].legacyProps, m * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    return FMT_OK;
+  }
+  std::vector<fmt_mt_leaf> lv(m);  // (no annotate-adjust in the batch: getAtSeq is the current properties)
+  FMT_HIP(c, hipMemcpy(lv.data(), views[doc].leaves, m * sizeof(fmt_mt_leaf), hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < m; i++) out[i] = lv[i].props;
   return FMT_OK;
 }
 

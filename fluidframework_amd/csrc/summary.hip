@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64 * kSumWaves) void summaryRunsKernel(const fmt_mt
         pres = L.ins_seq <= minSeq && !(L.rm_seq <= minSeq);
         if (pres) {
           len = L.len;
-          props = L.props;
+          props = V.legacyProps != nullptr ? V.legacyProps[i] : L.props;  // getAtSeq(minSeq) (adjust batches)
           off = L.char_off;
           marker = (L.pad & FMT_MT_LEAF_MARKER) != 0 ? 1u : 0u;
           last = len > 0 ? V.chars[off + len - 1] : 0u;

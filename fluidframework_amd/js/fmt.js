@@ -814,34 +814,6 @@ class MergeTreeReplay {
 		nums.forEach((x, k) => { vals[FMT_MT_VALUE_COMPUTED + k] = JSON.stringify(x); });
 		return vals;
 	}
-	/**
-	 * The last seq of an annotate touching a key some annotate of the document adjusts (0: none).
-	 * Legacy summaries read getAtSeq(minSeq), exact without per-segment change history unless that
-	 * seq is above minSeq (segmentPropertiesManager.ts:213-221, 328-344; summary.py check_legacy_adjust).
-	 */
-	adjustLastSeq(doc) {
-		if (!this.batch.adjusts) return 0;
-		const ops = new DataView(this.batch.ops.buffer, this.batch.ops.byteOffset, this.batch.ops.byteLength);
-		const changes = (pid) => {
-			const out = [];
-			for (let t = this.batch.propsOff[pid]; t < this.batch.propsOff[pid + 1]; t++) {
-				const adj = (this.batch.propsKv[t] & 0xffff) === FMT_MT_VALUE_ADJUST;
-				out.push([this.batch.propsKv[t] >>> 16, adj]);
-				if (adj) t++;
-			}
-			return out;
-		};
-		const ann = [];
-		for (let i = Number(this.batch.docOpOffsets[doc]); i < Number(this.batch.docOpOffsets[doc + 1]); i++) {
-			if (ops.getUint8(i * MT_OP_BYTES + 27) !== MT_ANNOTATE) continue;
-			ann.push([ops.getInt32(i * MT_OP_BYTES, true), changes(ops.getUint32(i * MT_OP_BYTES + 20, true))]);
-		}
-		const adjusted = new Set();
-		for (const [, ch] of ann) for (const [k, adj] of ch) if (adj) adjusted.add(k);
-		let last = 0;
-		for (const [seq, ch] of ann) if (ch.some(([k]) => adjusted.has(k))) last = Math.max(last, seq);
-		return last;
-	}
 	/** Leaves (segments, tombstones included), UTF-16 chars and prop sets of one document. */
 	segments(doc) {
 		const h = this.header(doc);
@@ -876,6 +848,7 @@ class MergeTreeReplay {
 			kvs.push(kv);
 		}
 		const segs = [];
+		segs.kvs = kvs; // every prop set's (key, value) ids, by set id
 		for (let i = 0; i < h.nLeaves; i++) {
 			const o = i * LEAF_BYTES;
 			const off = lv.getUint32(o + 16, true), len = lv.getUint32(o + 20, true);
@@ -914,18 +887,17 @@ class MergeTreeReplay {
 	 */
 	summarize(doc) {
 		const h = this.header(doc);
-		const segs = this.segments(doc).map((s) => ({
+		const all = this.segments(doc);
+		// getAtSeq(properties, minSeq) (snapshotlegacy.ts:211-212): with annotate-adjust the engine's
+		// per-leaf prop sets of each segment's PropertiesManager at minSeq
+		const legacy = this.batch.adjusts ? native().fetchLegacyProps(this.engine.ctx, doc, h.nLeaves) : null;
+		const segs = all.map((s, i) => ({
 			insertSeq: s.insertSeq,
 			removedSeq: s.removedSeq === undefined ? NOT_REMOVED : s.removedSeq,
 			text: s.text,
-			kv: s.kv,
+			kv: legacy ? (legacy[i] === 0xffff ? null : all.kvs[legacy[i]]) : s.kv,
 			refType: s.refType,
 		}));
-		if (this.adjustLastSeq(doc) > h.minSeq) {
-			const e = new UnsupportedOp("legacy summary of a document with annotate-adjust history above minSeq");
-			e.code = "FMT_E_UNSUPPORTED";
-			throw e;
-		}
 		const out = summary.legacySummary(segs, h.minSeq, this.batch.keys, this.valuesOf(doc));
 		const msgs = this.batch.messages && this.batch.messages[doc];
 		if (msgs && msgs.length) {

@@ -21,6 +21,7 @@
 //   fetchCatchupAll(ctx, nDocs) -> {offsets, ranges}                 fmt_mt_fetch_catchup_all
 //   fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer                     fmt_mt_fetch_remove_order
 //   fetchNumbers(ctx, doc) -> Float64Array                           fmt_mt_fetch_numbers
+//   fetchLegacyProps(ctx, doc, nLeaves) -> Uint16Array               fmt_mt_fetch_legacy_props
 //   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
 //   replayMapSparse(ctx, batch) -> Promise<{counts, entries}>        fmt_map_load_sparse + run + fetch
 //   summarizeLegacy(ctx, quotedKeys, values, chunk, threads) -> Promise<timing>   fmt_mt_summarize_legacy
@@ -783,6 +784,31 @@ napi_value FetchNumbers(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+// fetchLegacyProps(ctx, doc, nLeaves) -> Uint16Array: per leaf, the prop-set id of getAtSeq(minSeq)
+napi_value FetchLegacyProps(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 3 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchLegacyProps: a replay is running on this context");
+    return nullptr;
+  }
+  uint32_t doc, n;
+  if (!get_u32(env, argv[1], "doc", &doc) || !get_u32(env, argv[2], "nLeaves", &n)) return nullptr;
+  void* p;
+  napi_value ab, arr;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(n) * sizeof(uint16_t), &p, &ab));
+  const int rc = n ? fmt_mt_fetch_legacy_props(c->ctx, doc, static_cast<uint16_t*>(p), n) : FMT_OK;
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  CHECK_NAPI(env, napi_create_typedarray(env, napi_uint16_array, n, ab, 0, &arr));
+  return arr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor fns[] = {
       {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
@@ -797,6 +823,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"fetchCatchupAll", nullptr, FetchCatchupAll, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchRemoveOrder", nullptr, FetchRemoveOrder, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchNumbers", nullptr, FetchNumbers, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchLegacyProps", nullptr, FetchLegacyProps, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"replayMapSparse", nullptr, ReplayMapSparse, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"summarizeLegacy", nullptr, SummarizeLegacy, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"summaryBlobs", nullptr, SummaryBlobs, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -225,6 +225,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         L.fmt_mt_state_digest.argtypes = [P, P]
+        L.fmt_mt_fetch_legacy_props.argtypes = [P, U32, P, U32]
         _libs[path] = L
     return _libs[path]
 
@@ -236,7 +237,7 @@ EXPORTED_SYMBOLS = [
     "fmt_mt_summarize_legacy", "fmt_mt_summary_blobs",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
-    "fmt_mt_state_digest",
+    "fmt_mt_state_digest", "fmt_mt_fetch_legacy_props",
 ]
 
 
@@ -411,6 +412,15 @@ class Engine:
         n = int(hdr["n_rm_order"])
         out = np.zeros(max(n, 1), dtype=RM_ORDER_DTYPE)
         self._check(self.L.fmt_mt_fetch_remove_order(self.h, doc, _ptr(out), n))
+        return out[:n]
+
+    def mt_legacy_props(self, doc: int, hdr=None) -> np.ndarray:
+        """Per leaf, the prop-set id of getAtSeq(properties, minSeq) (what the legacy summary reads)."""
+        if hdr is None:
+            hdr = self.mt_headers(raise_on_failed_docs=False)[doc]
+        n = int(hdr["n_leaves"])
+        out = np.zeros(max(n, 1), dtype=np.uint16)
+        self._check(self.L.fmt_mt_fetch_legacy_props(self.h, doc, _ptr(out), n))
         return out[:n]
 
     def mt_numbers(self, doc: int) -> np.ndarray:

@@ -80,38 +80,6 @@ def values_with_numbers(values, numbers):
     return list(values) + [""] * (VALUE_COMPUTED - len(values)) + [js_number(float(x)) for x in numbers]
 
 
-def adjust_last_seq(batch, doc: int) -> int:
-    """The last seq of an annotate that touches a key some annotate of the document adjusts (0: the
-    document has no adjusts). Mirrors fmt_mt_load's per-document value."""
-    if getattr(batch, "adjusts", None) is None:
-        return 0
-    a, b = int(batch.doc_op_offsets[doc]), int(batch.doc_op_offsets[doc + 1])
-    ops = batch.ops[a:b]
-
-    def changes(pid):
-        kv = batch.props_kv[int(batch.props_off[pid]): int(batch.props_off[pid + 1])]
-        out, i = [], 0
-        while i < len(kv):
-            adj = (int(kv[i]) & 0xFFFF) == VALUE_ADJUST
-            out.append((int(kv[i]) >> 16, adj))
-            i += 2 if adj else 1
-        return out
-
-    ann = [(int(op["seq"]), changes(int(op["payload"]))) for op in ops if int(op["type"]) == MT_ANNOTATE]
-    adjusted = {k for _, ch in ann for k, adj in ch if adj}
-    return max([seq for seq, ch in ann if any(k in adjusted for k, _ in ch)], default=0)
-
-
-def check_legacy_adjust(batch, doc: int, min_seq: int) -> None:
-    """The legacy summary reads getAtSeq(minSeq) (snapshotlegacy.ts:211-212), which folds only the
-    pending remote changes of each segment at or below minSeq (segmentPropertiesManager.ts:328-344);
-    a raw change folds into the consensus early only while the segment's remote list is empty
-    (:213-221), which depends on per-segment msn updates. The state is exact without that history
-    unless an adjusted key is annotated above minSeq: such a document's legacy summary is refused."""
-    if adjust_last_seq(batch, doc) > min_seq:
-        raise UnsupportedOp("legacy summary of a document with annotate-adjust history above minSeq")
-
-
 def _props_obj(kv, keys, values):
     pairs = [(keys[x >> 16], values[x & 0xFFFF]) for x in kv]
     names = [k for k, _ in pairs]
@@ -142,18 +110,20 @@ def _props_match(a, b):
     return all(bd.get(x >> 16) == x for x in a)
 
 
-def legacy_segments(header, leaves, chars, propsets, min_seq):
+def legacy_segments(header, leaves, chars, propsets, min_seq, legacy_props=None):
     """extractSync: leaves present at PriorPerspective(minSeq, NonCollabClient), merged greedily
-    (prev.canAppend(seg): both TextSegments; a Marker never appends, mergeTreeNodes.ts:557-559)."""
+    (prev.canAppend(seg): both TextSegments; a Marker never appends, mergeTreeNodes.ts:557-559). Each
+    leaf's properties are getAtSeq(properties, minSeq) (snapshotlegacy.ts:211-212): for batches with
+    annotate-adjust the engine's per-leaf legacy prop sets (legacy_props), else the current ones."""
     segs = []  # [text, props kv tuple or None, marker]
-    for L in leaves[: int(header["n_leaves"])]:
+    for i, L in enumerate(leaves[: int(header["n_leaves"])]):
         ins, rm = int(L["ins_seq"]), int(L["rm_seq"])
         if not (ins <= min_seq) or rm <= min_seq:
             continue
         o, n = int(L["char_off"]), int(L["len"])
         text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
         marker = (int(L["pad"]) & MT_LEAF_MARKER) != 0
-        pid = int(L["props"])
+        pid = int(L["props"]) if legacy_props is None else int(legacy_props[i])
         props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
         if segs:
             prev = segs[-1]
@@ -169,10 +139,11 @@ def legacy_segments(header, leaves, chars, propsets, min_seq):
     return segs
 
 
-def legacy_summary(header, leaves, chars, propsets, keys, values, chunk_size=SIZE_OF_FIRST_CHUNK):
-    """(header_blob, body_blob or None) of the legacy SharedString summary at the doc's minSeq."""
+def legacy_summary(header, leaves, chars, propsets, keys, values, chunk_size=SIZE_OF_FIRST_CHUNK, legacy_props=None):
+    """(header_blob, body_blob or None) of the legacy SharedString summary at the doc's minSeq
+    (legacy_props: the engine's getAtSeq prop set per leaf, batches with annotate-adjust)."""
     min_seq = int(header["min_seq"])
-    segs = legacy_segments(header, leaves, chars, propsets, min_seq)
+    segs = legacy_segments(header, leaves, chars, propsets, min_seq, legacy_props)
     total_len = sum(_utf16_len(t) for t, _, _ in segs)
 
     def chunk(start, approx, is_header):

@@ -383,11 +383,11 @@ int fmt_device_info(fmt_ctx* ctx, char* buf, size_t cap);
  * snapshotChunks.ts:85-204, for all documents at once; catch-up ops are not included): the segment
  * merge runs on the device (one wave per document), the JSON on `threads` host threads (0 = up to
  * 16). keys: the batch's key strings JSON-quoted; values: the value JSON texts (UTF-8). Computed
- * annotate-adjust numbers are written as JSON.stringify writes them. A document whose legacy summary
- * depends on per-segment pending adjust history gets FMT_E_UNSUPPORTED: one with an adjust on a key
- * and an annotate of that key above its final minSeq (getAtSeq(minSeq) then folds only part of the
- * segment's remote changes, segmentPropertiesManager.ts:213-221, 328-344; SnapshotV1 and the replay
- * state stay exact). */
+ * annotate-adjust numbers are written as JSON.stringify writes them. Segment properties are
+ * getAtSeq(properties, minSeq) (snapshotlegacy.ts:211-212): in batches with annotate-adjust the engine
+ * keeps every segment's PropertiesManager (msnConsensus and pending remote changes,
+ * segmentPropertiesManager.ts:140-345) and evaluates it at the end of the replay
+ * (fmt_mt_fetch_legacy_props). */
 typedef struct fmt_summary_timing {
   double kernel_ms;   /* device merge (events) */
   double fetch_ms;    /* device -> host of runs, text and prop sets */
@@ -490,6 +490,10 @@ int fmt_mt_fetch_remove_order(fmt_ctx* ctx, uint32_t doc, fmt_mt_remove_order* o
 /* One document's computed numbers (annotate-adjust results, FMT_MT_VALUE_COMPUTED + index): *n_out
  * = their count, the first min(count, cap) copied to out. */
 int fmt_mt_fetch_numbers(fmt_ctx* ctx, uint32_t doc, double* out, uint32_t cap, uint32_t* n_out);
+/* One document's per-leaf prop-set ids of getAtSeq(properties, minSeq) (segmentPropertiesManager.ts:328-344),
+ * what the legacy summary reads (snapshotlegacy.ts:211-212); the first min(n_leaves, cap). Without
+ * annotate-adjust in the batch they are the leaves' own props. */
+int fmt_mt_fetch_legacy_props(fmt_ctx* ctx, uint32_t doc, uint16_t* out, uint32_t cap);
 /* Per-document 64-bit content digest of the converged state of the last fmt_mt_run (n_docs entries):
  * everything the reference's getText / summarize read back (MergeTreeTextHelper.ts:28-87,
  * snapshotlegacy.ts:195-262) — every leaf in document order with its stamps, remove-client set, length,

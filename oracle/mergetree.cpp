@@ -286,7 +286,10 @@ Seg* MergeTree::splitAt(Seg* seg, int pos) {
   seg->text.resize(static_cast<size_t>(pos));
   next->ins = seg->ins;
   next->removes = seg->removes;
-  if (seg->props.defined) next->props = seg->props;
+  if (seg->props.defined) {  // copyPropertiesAndManager (segmentPropertiesManager.ts:24-42, copyTo :300-316)
+    next->props = seg->props;
+    if (seg->pm) next->pm = std::make_unique<PropManager>(*seg->pm);
+  }
   // LocalReferenceCollection.split (localReference.ts:464-483): refs at offset >= pos move over
   std::vector<LRef*> keep;
   for (LRef* r : seg->refs) {
@@ -667,10 +670,63 @@ uint16_t MergeTree::adjustedValue(uint16_t cur, const fmt_mt_adjust& a) {
   return valueOfNumber(adjusted);
 }
 
-// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238. For an observer every
-// change is remote, and properties[key] = computePropertyValue(msnConsensus, remote) after each, which
-// is the running fold of the key's changes in seq order: a raw value replaces it, an adjust folds
-// onto it; null deletes the key; `seg.properties ??= createMap()` runs even if nothing changes.
+uint16_t MergeTree::foldChanges(uint16_t consensus, const std::vector<PropChangeRec>& changes, size_t n) {
+  uint16_t v = consensus;
+  for (size_t i = 0; i < n && i < changes.size(); i++) {
+    const PropChangeRec& c = changes[i];
+    if (!c.adjust) {
+      v = c.value;
+    } else {
+      if (adjusts == nullptr || static_cast<uint32_t>(c.row) >= nAdjusts) throw DataError("adjust row out of range");
+      v = adjustedValue(v, adjusts[c.row]);
+    }
+  }
+  return v;
+}
+
+// segmentPropertiesManager.ts:275-291: every key folds its remote changes at or below msn into
+// msnConsensus; a key left with no pending change loses its entry.
+void MergeTree::updateMsn(PropManager& pm, int msn) {
+  for (size_t k = 0; k < pm.changes.size();) {
+    PropPending& e = pm.changes[k];
+    size_t n = 0;
+    while (n < e.remote.size() && e.remote[n].seq <= msn) n++;
+    e.msnConsensus = foldChanges(e.msnConsensus, e.remote, n);
+    e.remote.erase(e.remote.begin(), e.remote.begin() + static_cast<std::ptrdiff_t>(n));
+    if (e.remote.empty()) pm.changes.erase(pm.changes.begin() + static_cast<std::ptrdiff_t>(k));
+    else k++;
+  }
+}
+
+// segmentPropertiesManager.ts:328-344 getAtSeq: the current properties with every pending key set to
+// its msnConsensus folded with the remote changes at or below seq (null: deleted; a key the current
+// properties lack goes last, in the manager's key order).
+PropMap MergeTree::getAtSeq(const Seg* s, int seq) {
+  PropMap out;
+  out.defined = true;  // ({...oldProps}: an object even when the properties are undefined)
+  out.kv = s->props.kv;
+  for (const PropPending& e : s->pm->changes) {
+    size_t n = 0;
+    while (n < e.remote.size() && e.remote[n].seq <= seq) n++;
+    const uint16_t v = foldChanges(e.msnConsensus, e.remote, n);
+    auto it = std::find_if(out.kv.begin(), out.kv.end(), [&](const auto& x) { return x.first == e.key; });
+    if (v == 0) {
+      if (it != out.kv.end()) out.kv.erase(it);
+    } else if (it != out.kv.end()) {
+      it->second = v;
+    } else {
+      out.kv.emplace_back(e.key, v);
+    }
+  }
+  return out;
+}
+
+// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238 handleProperties. For an
+// observer every change is remote: a key's entry starts at its current value (null when absent), a
+// raw change folds into msnConsensus while the key has no remote change pending and is queued
+// otherwise (an adjust always is), and properties[key] = computePropertyValue(msnConsensus, remote);
+// null deletes the key; `seg.properties ??= createMap()` runs even if nothing changes. Then
+// updateMsn(collabWindow.minSeq).
 void MergeTree::annotateRange(int start, int end, const std::vector<PropChange>& props, const Perspective& p,
                               Stamp stamp) {
   ensureIntervalBoundary(start, p);
@@ -679,15 +735,22 @@ void MergeTree::annotateRange(int start, int end, const std::vector<PropChange>&
   nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
   for (Seg* s : hit) {
     s->props.defined = true;
+    if (!s->pm) s->pm = std::make_unique<PropManager>();
+    PropManager& pm = *s->pm;
     for (const PropChange& ch : props) {
       const uint16_t key = ch.key;
       auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(),
                              [&](const auto& e) { return e.first == key; });
-      uint16_t value = ch.value;
-      if (ch.adjust >= 0) {
-        if (adjusts == nullptr || static_cast<uint32_t>(ch.adjust) >= nAdjusts) throw DataError("adjust row out of range");
-        value = adjustedValue(it != s->props.kv.end() ? it->second : 0, adjusts[ch.adjust]);
+      const uint16_t previous = it != s->props.kv.end() ? it->second : 0;
+      auto pe = std::find_if(pm.changes.begin(), pm.changes.end(), [&](const PropPending& e) { return e.key == key; });
+      if (pe == pm.changes.end()) {
+        pm.changes.push_back(PropPending{key, previous, {}});
+        pe = pm.changes.end() - 1;
       }
+      const PropChangeRec rec{stamp.seq, ch.adjust >= 0, ch.value, ch.adjust};
+      if (!rec.adjust && pe->remote.empty()) pe->msnConsensus = rec.value;
+      else pe->remote.push_back(rec);
+      const uint16_t value = foldChanges(pe->msnConsensus, pe->remote, pe->remote.size());
       if (value == 0) {  // null → delete
         if (it != s->props.kv.end()) s->props.kv.erase(it);
       } else if (it != s->props.kv.end()) {
@@ -696,6 +759,7 @@ void MergeTree::annotateRange(int start, int end, const std::vector<PropChange>&
         s->props.kv.emplace_back(key, value);
       }
     }
+    updateMsn(pm, minSeq);
     if (collaborating && stamp.seq != kUnassignedSeq) addToLRUSet(s, stamp.seq);
   }
   if (catchupOut) {  // deltaSegments: annotated segments not removed (mergeTree.ts:2045-2047, 2068-2073)
@@ -973,6 +1037,8 @@ void MergeTree::zamboniSegments() {
   if (!collaborating) return;
   for (int i = 0; i < kZamboniMax; i++) {
     if (heap_.count() == 0) break;
+    // segmentToScour?.segment?.propertyManager?.updateMsn(minSeq) on the peeked entry (zamboni.ts:44)
+    if (heap_.peek().seg->pm) updateMsn(*heap_.peek().seg->pm, minSeq);
     if (heap_.peek().maxSeq > minSeq) break;
     LruHeap::Entry e = heap_.get();
     Block* block = e.seg->parent;
@@ -1341,7 +1407,7 @@ static void emitProps(std::string& out, const PropMap& pm, const std::vector<std
 }
 
 Summary MergeTree::summarize(const std::vector<std::string>& keys,
-                             const std::vector<std::string>& values, int chunkSize) const {
+                             const std::vector<std::string>& values, int chunkSize) {
   // extractSync: leaves present at PriorPerspective(minSeq, NonCollabClient), merged while
   // prev.canAppend(seg) && matchProperties (props for raw-only annotations = current props).
   struct Out {
@@ -1355,17 +1421,19 @@ Summary MergeTree::summarize(const std::vector<std::string>& keys,
   const int total = rootLen == kUndefinedLen ? 0 : rootLen;
   nodeMap(mp, 0, total, [&](Seg* s) {
     if (!isPresent(s, mp)) return;
+    // segment.propertyManager?.getAtSeq(segment.properties, minSeq) ?? segment.properties (:211-212)
+    const PropMap props = s->pm ? getAtSeq(s, minSeq) : s->props;
     if (!segs.empty()) {
       Out& prev = segs.back();
       const bool endsNl = !prev.text.empty() && prev.text.back() == u'\n';
       const bool sizeOk = static_cast<int>(prev.text.size()) <= kTextGranularity ||
                           s->len() <= kTextGranularity;
-      if (!prev.marker && !s->marker && !endsNl && sizeOk && matchProperties(prev.props, s->props)) {
+      if (!prev.marker && !s->marker && !endsNl && sizeOk && matchProperties(prev.props, props)) {
         prev.text += s->text;
         return;
       }
     }
-    segs.push_back({s->text, s->props, s->marker});
+    segs.push_back({s->text, props, s->marker});
   });
   long long totalLen = 0;
   for (auto& o : segs) {

@@ -77,6 +77,25 @@ struct PropMap {
 };
 bool matchProperties(const PropMap& a, const PropMap& b);  // properties.ts:32-61
 
+// PropertiesManager (segmentPropertiesManager.ts:140-345) of a segment, for an observer: per key (in
+// the order its entry was created, a JS Map) the msnConsensus value and the remote changes not yet
+// folded into it. Only adjusts make the list grow: a raw change folds straight into msnConsensus
+// while the list is empty (:213-221). Values are value ids (0 = null).
+struct PropChangeRec {
+  int seq;
+  bool adjust;
+  uint16_t value;  // raw value id
+  int32_t row;     // adjust row
+};
+struct PropPending {
+  uint16_t key;
+  uint16_t msnConsensus;
+  std::vector<PropChangeRec> remote;
+};
+struct PropManager {
+  std::vector<PropPending> changes;
+};
+
 struct Block;
 struct Node {
   explicit Node(bool leaf) : isLeaf(leaf) {}
@@ -93,6 +112,7 @@ struct Seg : Node {
   Stamp ins{0, 0};
   std::vector<Stamp> removes;  // sorted by stamps.compare (spliceIntoList)
   PropMap props;
+  std::unique_ptr<PropManager> pm;  // segment.propertyManager (created by the first annotate)
   std::vector<LRef*> refs;     // local references on this segment (localReference.ts)
   int len() const { return static_cast<int>(text.size()); }
   bool removed() const { return !removes.empty(); }
@@ -246,8 +266,9 @@ class MergeTree {
   void collectLeaves(std::vector<const Seg*>& out, std::vector<int>& blockOfLeaf,
                      int* nLeafBlocks, int* depth) const;
   // snapshotlegacy.ts:195-262 extractSync + :126-193 emit (header/body blob contents).
+  // (not const: getAtSeq may look up computed numbers, and the answer never differs from a replay's)
   Summary summarize(const std::vector<std::string>& keyNames,
-                    const std::vector<std::string>& valueJson, int chunkSize = 10000) const;
+                    const std::vector<std::string>& valueJson, int chunkSize = 10000);
 
  private:
   struct InsertCtx {
@@ -320,6 +341,10 @@ class MergeTree {
   static void detachRef(LRef* ref);
   std::pair<Seg*, int> getContainingSegment(int pos, const Perspective& p) const;
   uint16_t adjustedValue(uint16_t cur, const fmt_mt_adjust& a);  // computePropertyValue for one adjust
+  // computePropertyValue(consensus, changes[0 .. n)) (segmentPropertiesManager.ts:54-78)
+  uint16_t foldChanges(uint16_t consensus, const std::vector<PropChangeRec>& changes, size_t n);
+  void updateMsn(PropManager& pm, int msn);                             // :275-291
+  PropMap getAtSeq(const Seg* s, int seq);                              // :328-344
   double numberOfValue(uint16_t id) const;
   uint16_t valueOfNumber(double x);
   void annotateRange(int start, int end, const std::vector<PropChange>& props,

@@ -15,6 +15,12 @@ static std::vector<double> g_numSorted, g_nums;
 static std::vector<uint32_t> g_numSortedId, g_numCount;
 static std::vector<uint64_t> g_numOffs;
 static fmt_mt::AdjustTables g_adj;
+// property-manager records (Doc::pm*) and the per-leaf legacy prop sets of the last replay
+constexpr uint32_t kEmuPmCap = 1 << 14;
+static std::vector<uint32_t> g_pm;
+static std::vector<uint64_t> g_pmOffs;
+static std::vector<uint16_t> g_legacy;
+static size_t g_legacyStride = 0;
 
 static void prepareNumbers(const fmt_mt_batch* b) {
   g_numSorted.clear();
@@ -34,9 +40,12 @@ static void prepareNumbers(const fmt_mt_batch* b) {
   g_nums.assign(static_cast<size_t>(b->n_docs) * kEmuNumCap, 0.0);
   g_numOffs.resize(b->n_docs + 1ull);
   for (uint32_t d = 0; d <= b->n_docs; d++) g_numOffs[d] = static_cast<uint64_t>(d) * kEmuNumCap;
+  g_pm.assign(static_cast<size_t>(b->n_docs) * kEmuPmCap * 4, 0u);
+  g_pmOffs.resize(b->n_docs + 1ull);
+  for (uint32_t d = 0; d <= b->n_docs; d++) g_pmOffs[d] = static_cast<uint64_t>(d) * kEmuPmCap;
   g_adj = fmt_mt::AdjustTables{b->adjusts, b->n_adjusts, b->value_num ? b->n_values : 0u, b->value_num,
                                g_numSorted.data(), g_numSortedId.data(), static_cast<uint32_t>(g_numSorted.size()), 0,
-                               g_nums.data(), g_numOffs.data(), g_numCount.data()};
+                               g_nums.data(), g_numOffs.data(), g_numCount.data(), g_pm.data(), g_pmOffs.data()};
 }
 
 // ckpt (plain batches): per-document tier checkpoints; the compact tier saves, the small tier resumes
@@ -47,7 +56,8 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
                      fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
                      fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* ckpt = nullptr,
                      bool onlyEscalated = false, size_t leafStride = 0, size_t charStride = 0,
-                     const fmt_mt_leaf* smallLeaves = nullptr, const uint16_t* smallChars = nullptr) {
+                     const fmt_mt_leaf* smallLeaves = nullptr, const uint16_t* smallChars = nullptr,
+                     uint16_t* legacy = nullptr) {
   using Doc = fmt_mt::Doc<Ob, C, Rm, Adj>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
@@ -105,6 +115,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     o.ckptResume = o.ckpt != nullptr && Doc::kResumesCkpt && headers[d].status == fmt_mt::kCkptEscalate;
     o.bigCkpt = nullptr;
     o.bigCkptChars = nullptr;
+    o.legacyProps = legacy ? legacy + static_cast<size_t>(d) * (leafStride ? leafStride : Doc::kCapLeaves) : nullptr;
     if (Doc::kSavesBig && ckpt != nullptr) {  // the small tier of a cascade: its own slabs
       o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);
       o.bigCkptChars = o.chars;
@@ -177,8 +188,12 @@ static int adjustCascade(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_
   using S = fmt_mt::SmallTier;
   using G = fmt_mt::LargeTier;
   if (large == 0 || large == 3) {
-    return rm ? replayAll<true, S, true, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm)
-              : replayAll<true, S, false, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+    g_legacyStride = fmt_mt::Doc<true, S>::kCapLeaves;
+    g_legacy.assign(b->n_docs * g_legacyStride, 0xFFFFu);
+    return rm ? replayAll<true, S, true, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm,
+                                               nullptr, false, 0, 0, nullptr, nullptr, g_legacy.data())
+              : replayAll<true, S, false, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm,
+                                                nullptr, false, 0, 0, nullptr, nullptr, g_legacy.data());
   }
   using DS = fmt_mt::Doc<true, S, false, true>;
   using DL = fmt_mt::Doc<true, G, false, true>;
@@ -186,17 +201,25 @@ static int adjustCascade(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_
   std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
   std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
   std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
-  if (rm) replayAll<true, S, true, true>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm);
-  else replayAll<true, S, false, true>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm);
+  std::vector<uint16_t> smallLegacy(n * DS::kCapLeaves, 0xFFFFu);
+  if (rm) replayAll<true, S, true, true>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm,
+                                         nullptr, false, 0, 0, nullptr, nullptr, smallLegacy.data());
+  else replayAll<true, S, false, true>(b, headers, sl.get(), sc.get(), sp.get(), catchup, capCatchup, rmOrder, capRm,
+                                       nullptr, false, 0, 0, nullptr, nullptr, smallLegacy.data());
+  g_legacyStride = DL::kCapLeaves;
+  g_legacy.assign(n * g_legacyStride, 0xFFFFu);
   for (size_t d = 0; d < n; d++) {
     const fmt_mt_doc_result& h = headers[d];
     if (h.status == FMT_E_CAPACITY) continue;
     std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));
     std::memcpy(chars + d * G::kCapChars, sc.get() + d * S::kCapChars, h.n_chars * sizeof(uint16_t));
     std::memcpy(props + d * G::kPropCap, sp.get() + d * S::kPropCap, h.n_props * sizeof(fmt_mt_propset));
+    std::memcpy(g_legacy.data() + d * DL::kCapLeaves, smallLegacy.data() + d * DS::kCapLeaves, h.n_leaves * sizeof(uint16_t));
   }
-  return rm ? replayAll<true, G, true, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr, true)
-            : replayAll<true, G, false, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr, true);
+  return rm ? replayAll<true, G, true, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr,
+                                             true, 0, 0, nullptr, nullptr, g_legacy.data())
+            : replayAll<true, G, false, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm, nullptr,
+                                              true, 0, 0, nullptr, nullptr, g_legacy.data());
 }
 
 extern "C" {
@@ -231,6 +254,7 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
                   fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, int forceOb, int large,
                   fmt_mt_remove_order* rmOrder, uint32_t capRm) {
   prepareNumbers(b);
+  g_legacyStride = 0;
   if (b->adjusts != nullptr) {  // the runtime's annotate-adjust path: Adj variants, no checkpoints
     bool rmA = false;
     for (uint64_t i = 0; i < b->n_ops && !rmA; i++) rmA = (b->ops[i].flags & FMT_MT_F_RMORDER) != 0;
@@ -261,6 +285,14 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   if (ob) return replayAll<true, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (rm) return replayAll<false, S, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+}
+
+// Document d's legacy prop sets (getAtSeq at minSeq, per leaf) after the last emu_mt_replay of a batch
+// with adjusts: copies <= cap, returns the count (0 without adjusts).
+int emu_mt_legacy_props(uint32_t d, uint16_t* out, uint32_t cap) {
+  if (g_legacyStride == 0 || (d + 1) * g_legacyStride > g_legacy.size()) return 0;
+  for (uint32_t k = 0; k < cap && k < g_legacyStride; k++) out[k] = g_legacy[d * g_legacyStride + k];
+  return static_cast<int>(g_legacyStride);
 }
 
 // Document d's computed numbers after the last emu_mt_replay: returns their count, copies <= cap.

@@ -33,6 +33,7 @@ def emu_lib():
                                                               ctypes.c_void_p, ctypes.c_uint32]
         L.emu_mt_capacity.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.emu_mt_numbers.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+        L.emu_mt_legacy_props.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
         _emu = L
     return _emu
 
@@ -115,6 +116,14 @@ def emu_replay(batch, cap_catchup=0, force_ob=False, large=False, cap_rm=0):
     if cap_rm:
         out = out + (rm.reshape(n, cap_rm),)
     return out
+
+
+def emu_legacy_props(doc: int):
+    """Document `doc`'s per-leaf getAtSeq(minSeq) prop sets after the last emu_replay of a batch with
+    annotate-adjust (None otherwise)."""
+    out = np.zeros(4096, dtype=np.uint16)
+    n = emu_lib().emu_mt_legacy_props(doc, _p(out), 4096)
+    return out[:n] if n else None
 
 
 def emu_numbers(doc: int) -> np.ndarray:

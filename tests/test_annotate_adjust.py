@@ -8,10 +8,10 @@ The reference's fixtures hold no adjust op, so parity is anchored three ways:
     adjusts and raw numbers on the same keys: the final texts still equal the fixtures' resultText,
     and the emulated engine (small tier, and the large tier the runtime escalates to) equals the
     oracle restatement bit for bit, computed-number tables included;
-  - legacy summaries where getAtSeq(minSeq) is exact without per-segment change history (no adjusted
-    key annotated above minSeq): the Python host over engine state equals the oracle's own
-    SnapshotLegacy restatement byte for byte; every other adjusted document's legacy summary is
-    refused (UnsupportedOp), while its SnapshotV1 summary (current properties) is produced.
+  - legacy summaries read getAtSeq(minSeq), which the oracle restates with each segment's
+    PropertiesManager (msnConsensus + pending remote changes, updateMsn at handleProperties and at
+    zamboni's peek, copyTo on splits) and the engine keeps as per-leaf records: the Python host over
+    the engine's legacy prop sets equals the oracle's SnapshotLegacy restatement byte for byte.
 """
 import gzip
 import json
@@ -23,7 +23,7 @@ import pytest
 
 from fluidframework_amd import summary
 from fluidframework_amd.streams import VALUE_COMPUTED, MergeTreeStreamBuilder, UnsupportedOp, js_number
-from mt_compare import compare_doc, emu_caps, emu_numbers, emu_replay, visible_text
+from mt_compare import compare_doc, emu_caps, emu_legacy_props, emu_numbers, emu_replay, visible_text
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "replay_msgs_0.40.json.gz")
 
@@ -230,28 +230,90 @@ def test_engine_adjust_farms_match_oracle(orc, large):
     assert computed > (50 if large else 3)
 
 
-def test_legacy_summaries_exact_or_refused(orc):
-    """Exact tail: summary.py over engine state == the oracle's SnapshotLegacy restatement (its own
-    number formatting); documents with adjusts above minSeq are refused, their V1 summary is not."""
+def test_legacy_summaries_match_oracle(orc):
+    """getAtSeq(minSeq) (segmentPropertiesManager.ts:328-344, via snapshotlegacy.ts:211-212): every
+    adjusted document's legacy summary from the engine's per-leaf legacy prop sets (the emulated
+    PropertiesManager records) equals the oracle's SnapshotLegacy restatement over its own managers,
+    with adjusts above the final minSeq (the common case) and without."""
+    differs = 0
     for exact_tail in (True, False):
         batch, _ = adjust_fixture_batch(exact_tail)
-        cl, cc, cp = emu_caps(True)
         hdr, leaves, chars, props = emu_replay(batch, large=4)
-        refused = 0
         for d in range(batch.n_docs):
             h = hdr[d]
+            assert int(h["status"]) == 0, d
             vals = summary.values_with_numbers(batch.values, emu_numbers(d))
-            if summary.adjust_last_seq(batch, d) > int(h["min_seq"]):
-                assert not exact_tail
-                with pytest.raises(UnsupportedOp):
-                    summary.check_legacy_adjust(batch, d, int(h["min_seq"]))
-                refused += 1
-                continue
-            summary.check_legacy_adjust(batch, d, int(h["min_seq"]))
-            got = summary.legacy_summary(h, leaves[d], chars[d], props[d], batch.keys, vals)
+            legacy = emu_legacy_props(d)
+            assert legacy is not None
+            got = summary.legacy_summary(h, leaves[d], chars[d], props[d], batch.keys, vals, legacy_props=legacy)
             want = orc.mt_replay_summary(batch, d, batch.keys, batch.values)
             assert got == want, d
-        assert (refused > 0) != exact_tail
+            now = summary.legacy_summary(h, leaves[d], chars[d], props[d], batch.keys, vals)
+            differs += now != got
+    assert differs > 0  # pending changes above minSeq make getAtSeq differ from the current properties
+
+
+def test_legacy_summaries_match_oracle_small_tier(orc):
+    """The same through the small tier alone (narrow deltas: documents fit its 32 prop sets), and with
+    the legacy prop sets the getAtSeq evaluation interns at the end of the replay."""
+    batch, _ = adjust_fixture_batch(narrow=True)
+    hdr, leaves, chars, props = emu_replay(batch)
+    checked = 0
+    for d in range(batch.n_docs):
+        h = hdr[d]
+        if int(h["status"]) != 0:
+            continue  # (outgrew the small tier: the large tier replays it)
+        vals = summary.values_with_numbers(batch.values, emu_numbers(d))
+        got = summary.legacy_summary(h, leaves[d], chars[d], props[d], batch.keys, vals, legacy_props=emu_legacy_props(d))
+        assert got == orc.mt_replay_summary(batch, d, batch.keys, batch.values), d
+        checked += 1
+    assert checked > 3
+
+
+def getatseq_cases():
+    """(initial text, messages, expected legacy segmentTexts) worked out by hand from
+    segmentPropertiesManager.ts (handleProperties :188-238, updateMsn :275-291, getAtSeq :328-344) and
+    zamboni.ts:44 (updateMsn on the peeked segment when minSeq advances)."""
+    ins = lambda p, t: {"type": 0, "pos1": p, "seg": t}  # noqa: E731
+    return [
+        # a raw change that arrives while an adjust is pending is queued: at minSeq 1 the adjust's
+        # result shows, not the later raw value
+        ("ab", [_msg("B", 1, 0, _ann(0, 2, adjust={"n": {"delta": 1}})), _msg("B", 2, 1, _ann(0, 2, props={"n": 5})),
+                _msg("C", 3, 2, ins(2, "x"), msn=1)],
+         [{"text": "ab", "props": {"n": 1}}]),
+        # the adjust was folded (zamboni's updateMsn when minSeq reached it) before the raw change came:
+        # the raw change folds straight into msnConsensus, so it shows although its seq is above minSeq
+        ("ab", [_msg("B", 1, 0, _ann(0, 2, adjust={"n": {"delta": 1}})), _msg("C", 2, 1, ins(2, "x"), msn=1),
+                _msg("B", 3, 2, _ann(0, 2, props={"n": 5}), msn=1)],
+         [{"text": "ab", "props": {"n": 5}}]),
+        # a key deleted now (null queued behind an adjust) but alive at minSeq goes last
+        ("ab", [_msg("B", 1, 0, _ann(0, 2, props={"n": 2, "a": 1})), _msg("B", 2, 1, _ann(0, 2, adjust={"n": {"delta": 1}})),
+                _msg("B", 3, 2, _ann(0, 2, props={"n": None})), _msg("C", 4, 3, ins(2, "x"), msn=2)],
+         [{"text": "ab", "props": {"a": 1, "n": 3}}]),
+        # a split copies the manager (copyTo): both halves keep the pending adjust
+        ("abcd", [_msg("B", 1, 0, _ann(0, 4, adjust={"n": {"delta": 2}})), _msg("B", 2, 1, _ann(2, 4, props={"n": 9})),
+                  _msg("C", 3, 2, ins(4, "x"), msn=1)],
+         [{"text": "abcd", "props": {"n": 2}}]),
+    ]
+
+
+def test_getatseq_hand_cases(orc):
+    cases = getatseq_cases()
+    b = MergeTreeStreamBuilder()
+    for init, msgs, _ in cases:
+        d = b.begin_doc(init, observer="A")
+        for m in msgs:
+            d.add_message(m)
+    batch = b.finish()
+    hdr, leaves, chars, props = emu_replay(batch)
+    for d, (_, _, want) in enumerate(cases):
+        head, body = orc.mt_replay_summary(batch, d, batch.keys, batch.values)
+        assert body is None and json.loads(head)["segmentTexts"] == want, (d, head)
+        vals = summary.values_with_numbers(batch.values, emu_numbers(d))
+        got = summary.legacy_summary(hdr[d], leaves[d], chars[d], props[d], batch.keys, vals, legacy_props=emu_legacy_props(d))
+        assert got == (head, body), d
+        assert json.loads(got[0])["segmentTexts"] == want  # (JSON key order too: json.loads keeps it)
+        assert list(json.loads(got[0])["segmentTexts"][0]["props"]) == list(want[0]["props"])
 
 
 def test_computed_numbers_format_like_json_stringify():

@@ -737,21 +737,35 @@ def test_mt_annotate_adjust_farms_on_gpu(orc, engine, narrow):
 
 
 def test_mt_bulk_legacy_summaries_with_adjusts(orc, engine):
-    """fmt_mt_summarize_legacy with computed numbers: documents whose adjusted keys are last annotated
-    at or below minSeq give the oracle's own SnapshotLegacy bytes (C++ JSON.stringify of the numbers);
-    the others report FMT_E_UNSUPPORTED for that document only."""
-    from fluidframework_amd.native import EngineError
-    from fluidframework_amd.summary import adjust_last_seq
-    from test_annotate_adjust import adjust_fixture_batch
+    """fmt_mt_summarize_legacy with computed numbers and getAtSeq(minSeq) (the engine's per-leaf
+    PropertiesManager records): every document, adjusts above its final minSeq or not, gives the
+    oracle's own SnapshotLegacy bytes (C++ JSON.stringify of the numbers); the Python host over
+    fmt_mt_fetch_legacy_props agrees; the hand-worked getAtSeq cases give their stated segments."""
+    import json
+
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+    from fluidframework_amd.summary import legacy_summary, values_with_numbers
+    from test_annotate_adjust import adjust_fixture_batch, getatseq_cases
 
     for exact_tail in (True, False):
         batch, _ = adjust_fixture_batch(exact_tail)
         hdrs = _gpu_mt(engine, batch)
         engine.mt_summarize_legacy(batch.keys, batch.values)
         for d in range(batch.n_docs):
-            if adjust_last_seq(batch, d) > int(hdrs[d]["min_seq"]):
-                with pytest.raises(EngineError) as ei:
-                    engine.mt_summary(d)
-                assert ei.value.code == -5
-            else:
-                assert engine.mt_summary(d) == orc.mt_replay_summary(batch, d, batch.keys, batch.values), d
+            want = orc.mt_replay_summary(batch, d, batch.keys, batch.values)
+            assert engine.mt_summary(d) == want, d
+            lv, ch, pr = engine.mt_doc(d, hdrs[d])
+            vals = values_with_numbers(batch.values, engine.mt_numbers(d))
+            got = legacy_summary(hdrs[d], lv, ch, pr, batch.keys, vals, legacy_props=engine.mt_legacy_props(d, hdrs[d]))
+            assert got == want, d
+    cases = getatseq_cases()
+    b = MergeTreeStreamBuilder()
+    for init, msgs, _ in cases:
+        d = b.begin_doc(init, observer="A")
+        for m in msgs:
+            d.add_message(m)
+    batch = b.finish()
+    _gpu_mt(engine, batch)
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    for d, (_, _, want) in enumerate(cases):
+        assert json.loads(engine.mt_summary(d)[0])["segmentTexts"] == want, d

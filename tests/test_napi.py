@@ -45,7 +45,7 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
-                               "fetchRemoveOrder", "fetchNumbers", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
+                               "fetchRemoveOrder", "fetchNumbers", "fetchLegacyProps", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
                                "summaryBlobs", "replayMap", "fetchDoc", "sizes"])
     assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
                         "catchupRange": 16, "mapEntry": 12, "adjust": 32}
@@ -362,9 +362,8 @@ def test_js_packer_annotate_adjust_matches_python(addon, tmp_path):
 @pytest.mark.gpu
 def test_js_annotate_adjust_summaries_on_gpu(addon, tmp_path, orc):
     """Through the addon: getText equals the fixtures' resultText; summarizeV1 (computed numbers as
-    JSON.stringify writes them) equals the Python host over the GPU state; the legacy summary of an
-    exact-tail document equals the oracle's SnapshotLegacy restatement, and the others are refused
-    with FMT_E_UNSUPPORTED."""
+    JSON.stringify writes them) equals the Python host over the GPU state; every legacy summary
+    (getAtSeq(minSeq) from fetchLegacyProps) equals the oracle's SnapshotLegacy restatement."""
     from fluidframework_amd import native
     from fluidframework_amd.summary import v1_summary, values_with_numbers, removers_from_engine
     from test_annotate_adjust import adjust_fixture_batch
@@ -383,12 +382,9 @@ def test_js_annotate_adjust_summaries_on_gpu(addon, tmp_path, orc):
         batch, finals = adjust_fixture_batch(exact_tail)
         for d, o in enumerate(out):
             assert o["text"] == finals[d]
-            if isinstance(o["legacy"], str):
-                assert not exact_tail and o["legacy"] == "FMT_E_UNSUPPORTED"
-            else:
-                want = orc.mt_replay_summary(batch, d, batch.keys, batch.values)
-                assert [o["legacy"]["header"], o["legacy"].get("body")] == list(want), d
-        assert not exact_tail or all(not isinstance(o["legacy"], str) for o in out)
+            assert not isinstance(o["legacy"], str), (d, o["legacy"])
+            want = orc.mt_replay_summary(batch, d, batch.keys, batch.values)
+            assert [o["legacy"]["header"], o["legacy"].get("body")] == list(want), d
         e = native.Engine(0)
         try:
             e.mt_load(batch)

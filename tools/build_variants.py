@@ -40,7 +40,7 @@ def build(name, edits, rev=None, flags=()):
         assert old in s, (name, fname, old[:50])
         open(p, "w").write(s.replace(old, new))
     # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc)
-    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o")]
+    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o", "digest.o", "transfer.o")]
     for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip", "hugedoc.hip"]:
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
