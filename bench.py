@@ -71,6 +71,10 @@ def main():
                          "ob: the reference's 30 obliterate conflict farms replicated to --docs documents")
     ap.add_argument("--segments", type=int, default=10_000_000, help="t3: segments of the loaded document")
     ap.add_argument("--t3-ops", type=int, default=10_000_000, help="t3: sequenced ops replayed")
+    ap.add_argument("--t3-summary", choices=["legacy", "header"], default="legacy",
+                    help="t3: the loaded summary's shape: legacy = SnapshotLegacy.emit's header chunk (~10,000 "
+                         "units) + body chunk; header = every segment in one header chunk")
+    ap.add_argument("--t3-range", type=int, default=8, help="t3: max range length of removes/annotates")
     ap.add_argument("--cpu-ops", type=int, default=200_000, help="t3: ops of the CPU baseline sample")
     ap.add_argument("--docs", type=int, default=None,
                     help="documents per GPU (mt, map) or in the whole batch (t2)")
@@ -666,7 +670,10 @@ def bench_t3(args, rank, world, local_rank, dist):
     from fluidframework_amd import native, shard, workloads
 
     t = time.time()
-    batch = workloads.t3_stream(args.segments, args.t3_ops, n_clients=63, max_lag=4096, max_range=8, seed=args.seed)
+    batch = workloads.t3_stream(args.segments, args.t3_ops, n_clients=63, max_lag=4096, max_range=args.t3_range,
+                                seed=args.seed)
+    if args.t3_summary == "legacy":
+        batch = workloads.as_legacy_load(batch)
     n_ops = len(batch.ops)
     log(rank, f"[bench] t3: generated {args.segments} segments + {n_ops} ops in {time.time() - t:.1f}s")
     eng = native.Engine(local_rank)
@@ -737,7 +744,9 @@ def bench_t3(args, rank, world, local_rank, dist):
             "data": "synthetic (one SharedString loaded from a summary of U[1,8]-char segments, then conflict-farm "
                     "op kinds from 63 writers with refSeq lag U[0,4096) and local edit ranges, reference XSadd PRNG)",
             "config": {"workload": "T3 single huge SharedString replay (load + replay + output in the timed launch)",
-                       "segments": args.segments, "ops": n_ops, "clients": 63, "max_lag": 4096, "max_range": 8,
+                       "segments": args.segments, "ops": n_ops, "clients": 63, "max_lag": 4096, "max_range": args.t3_range,
+                       "summary": {"shape": args.t3_summary, "header_segments": int(batch.snapshots[0]["n_header"]),
+                                   "body_segments": int(batch.snapshots[0]["n_body"])},
                        "parallelism": f"replicas x{world} (one dependency chain per document)"},
             "roofline": {"bound": "hbm", "achieved": bytes_per_launch / (avg_kernel_ms / 1e3) / 1e9,
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -38,6 +38,9 @@
 #include "../../include/fmt.h"
 #include "wave.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace fmt_huge {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -145,7 +148,10 @@ struct HugeState {
   uint32_t* wBlk;
   uint32_t* wLeaf;
   uint32_t winCap;
-  // text arena (batch text, then the merge area) and prop sets
+  // text arena, one offset space: [0, textLen) is the batch's shared text (read in place through
+  // base, never copied per document); [textLen, textCap) is this document's merge area, addressed
+  // through text (its allocation minus textLen units, so text + off is valid for off >= textLen)
+  const uint16_t* base;
   uint16_t* text;
   uint64_t textLen;   // batch text (read-only part)
   uint64_t textCap;   // end of the merge area: two halves of (textCap - textLen) / 2 units, one in use
@@ -185,14 +191,62 @@ struct HugeInputs {
   const uint32_t* propsOff;
   const uint32_t* propsKv;
   uint32_t nPropsOps;
-  const fmt_mt_snapshot_seg* segs;  // loaded header chunk
+  const fmt_mt_snapshot_seg* segs;  // loaded segments: the header chunk, then the body chunk(s)
   uint32_t nSegs;
+  // Tree shape of the loaded segments when a body follows the header (nullptr: the header alone,
+  // reloaded 7 wide): [L, n_0 .. n_{L-1}, then per level its n_l nodes as (start, count)] —
+  // level 0 the leaf blocks (start: first segment), level l > 0 interior blocks (start: first
+  // child on level l - 1), level L - 1 the root. Built on the host by loadShape below.
+  const uint32_t* shape;
   int32_t snapMinSeq, snapSeq;
   // client of the loaded segments' insert stamp: FMT_NON_COLLAB_CLIENT for a summary's segments
   // (specToSegment, snapshotLoader.ts:180-186), FMT_LOCAL_CLIENT for a document's initial text (the
   // replay harness inserts it locally before collaborating, client.replay.spec.ts:30-33)
   int32_t initClient;
+  uint32_t segProps;  // some loaded segment has properties
 };
+
+// The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
+// header — 7 leaves per block, 7 blocks per interior block up to one root (mergeTree.ts:751-800) —
+// then loadBody's appends (snapshotLoader.ts:277-309), each into the last leaf block, a full block
+// (MaxNodesInBlock) splitting 4 / 4 and the split climbing the right edge, a new root above a split
+// root (mergeTree.ts:1946-1987; an empty root first becomes the leaf block). Only the right edge
+// changes, so this tracks node counts per level. (Host code: the runtime and the emulation tests.)
+inline void loadShape(uint64_t nHeader, uint64_t nBody, std::vector<uint32_t>& out) {
+  std::vector<std::vector<uint32_t>> lv;
+  if (nHeader > 0) {
+    uint64_t below = nHeader;
+    do {
+      std::vector<uint32_t> level;
+      for (uint64_t q = 0; q * 7 < below; q++) level.push_back(static_cast<uint32_t>(std::min<uint64_t>(7, below - 7 * q)));
+      below = level.size();
+      lv.push_back(std::move(level));
+    } while (below > 1);
+  }
+  for (uint64_t i = 0; i < nBody; i++) {
+    if (lv.empty()) lv.push_back({0});
+    lv[0].back()++;
+    for (size_t l = 0; lv[l].back() == kMaxNodes; l++) {
+      lv[l].back() = kMaxNodes / 2;
+      lv[l].push_back(kMaxNodes / 2);
+      if (l + 1 == lv.size()) {
+        lv.push_back({2});
+        break;
+      }
+      lv[l + 1].back()++;
+    }
+  }
+  out.assign(1, static_cast<uint32_t>(lv.size()));
+  for (const auto& level : lv) out.push_back(static_cast<uint32_t>(level.size()));
+  for (const auto& level : lv) {
+    uint32_t st = 0;
+    for (uint32_t cnt : level) {
+      out.push_back(st);
+      out.push_back(cnt);
+      st += cnt;
+    }
+  }
+}
 
 // A leaf found by the hierarchical search.
 struct Hit {
@@ -272,6 +326,10 @@ class HugeDoc {
   FMT_DEV static int32_t rd(const int32_t* p) { return loadWg(p); }
   FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(loadWg(p)); }
   FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadWg(p)); }
+  // one text unit at arena offset off (batch text below textLen, the merge area above)
+  FMT_DEV uint32_t textAt(uint64_t off) const {
+    return loadWg((off < S.textLen ? S.base : static_cast<const uint16_t*>(S.text)) + off);
+  }
   // one lane stores a wave-uniform value
   template <class T>
   FMT_DEV static void st1(T* p, T v) {
@@ -2059,7 +2117,7 @@ class HugeDoc {
       LANE(f[6]) = rd(S.lText + i);
       LANE(f[7]) = rd(S.lMeta + i);
       const uint32_t ln = LANE(f[0]);
-      LANE(lastCh) = ln > 0 ? loadWg(S.text + LANE(f[6]) + ln - 1) : 0u;
+      LANE(lastCh) = ln > 0 ? textAt(LANE(f[6]) + ln - 1) : 0u;
     }
   }
 
@@ -2279,7 +2337,7 @@ class HugeDoc {
           Lane<uint32_t> v;
           FOR_LANES(l) {
             const uint32_t t = base + l;
-            LANE(v) = t < total ? loadWg(S.text + LANE(sx) + (t - LANE(st))) : 0u;
+            LANE(v) = t < total ? textAt(LANE(sx) + (t - LANE(st))) : 0u;
           }
           FOR_LANES(l) {
             const uint32_t t = base + l;
@@ -2328,7 +2386,7 @@ class HugeDoc {
       Lane<uint32_t> v;
       FOR_LANES(l) {
         const uint32_t t = base + l;
-        LANE(v) = t < need ? loadWg(S.text + LANE(tx) + (t - LANE(st))) : 0u;
+        LANE(v) = t < need ? textAt(LANE(tx) + (t - LANE(st))) : 0u;
       }
       waveSync();
       FOR_LANES(l) {
@@ -2552,8 +2610,10 @@ class HugeDoc {
       }
       i += run - 1;
     }
+    // (a parent left childless stays; packParent empties it, zamboni.ts:129-132. When that is the
+    // root, no leaf block is listed any more, and the next insert makes the root a leaf block again
+    // as in an empty document, insertText)
     st1(S.bCount + p, static_cast<uint32_t>(nb));
-    if (nb == 0 && static_cast<int>(p) == root) fail(FMT_E_UNSUPPORTED);  // document emptied by zamboni
     if (lastBlk != kNone) updateLastBlk();
     invalidate();
   }
@@ -2673,14 +2733,40 @@ class HugeDoc {
     }
   }
 
-  // ------------------------------------------------------------------ load (f3, header chunk only)
-  // reloadFromSegments (mergeTree.ts:751-800): 7 leaves per block, layer by layer; every loaded
-  // segment stamped {UniversalSequenceNumber, NonCollabClient} (snapshotLoader.ts:180-186).
-  // Blocks are numbered leaf level first; groups take kFill leaf blocks each.
+  // ------------------------------------------------------------------ load (f3)
+  // reloadFromSegments (mergeTree.ts:751-800) of the header chunk: 7 leaves per block, layer by
+  // layer; then SnapshotLoader.loadBody's appends of the body chunk (snapshotLoader.ts:277-309), each
+  // through the inserting walk at the end — the last leaf's block, split 4 / 4 at MaxNodesInBlock
+  // (mergeTree.ts:1946-1987) — whose resulting shape the runtime passes in in.shape. Every loaded
+  // segment is stamped {UniversalSequenceNumber, NonCollabClient} (snapshotLoader.ts:180-186) and
+  // keeps its spec's properties (a clone, as TextSegment.fromJSONObject does). Blocks are numbered
+  // leaf level first; groups take kFill leaf blocks each.
+  FMT_DEV uint32_t shapeLevels() const {
+    if (in.shape != nullptr) return ldu(in.shape);
+    uint32_t L = 1;
+    for (uint32_t n = (in.nSegs + 6) / 7; n > 1; n = (n + 6) / 7) L++;
+    return L;
+  }
+  FMT_DEV uint32_t shapeCount(uint32_t lvl) const {
+    if (in.shape != nullptr) return ldu(in.shape + 1 + lvl);
+    uint32_t n = (in.nSegs + 6) / 7;
+    for (uint32_t l = 0; l < lvl; l++) n = (n + 6) / 7;
+    return n;
+  }
+  // node q of a level (pairs: that level's first (start, count) record; below: the level's size)
+  FMT_DEV void shapeNode(const uint32_t* pairs, uint32_t below, uint32_t q, uint32_t* st, uint32_t* c) const {
+    if (pairs != nullptr) {
+      *st = rd(pairs + 2 * static_cast<size_t>(q));
+      *c = rd(pairs + 2 * static_cast<size_t>(q) + 1);
+    } else {
+      *st = 7 * q;
+      *c = below - 7 * q < 7 ? below - 7 * q : 7;
+    }
+  }
+
   FMT_DEV void load() {
     ProfScope ps_(prof[5]);
     const uint32_t N = in.nSegs;
-    const uint32_t nLeafBlk = (N + 6) / 7;
     if (N == 0) {  // an empty document: the root block alone, no leaf block listed yet (insertText)
       if (S.blockCap < 1) {
         fail(FMT_E_CAPACITY);
@@ -2708,58 +2794,59 @@ class HugeDoc {
       curSeq = in.snapSeq;
       return;
     }
+    const uint32_t nLv = shapeLevels();
+    const uint32_t nLeafBlk = shapeCount(0);
+    const uint32_t* pairs = in.shape != nullptr ? in.shape + 1 + nLv : nullptr;
     if (nLeafBlk > S.blockCap || N + 1 > S.idCap) {
       fail(FMT_E_CAPACITY);
       return;
     }
-    for (uint32_t base = 0; base < N; base += 64) {
-      FOR_LANES(l) {
-        const uint32_t j = base + l;
-        if (j < N) {
-          const uint32_t b = j / 7, k = j % 7;
-          const size_t i = static_cast<size_t>(b) * 8 + k;
-          const fmt_mt_snapshot_seg sg = in.segs[j];
-          S.lLen[i] = sg.len & ~FMT_MT_SEG_MARKER;
-          S.lIns[i] = 0;
-          S.lRm[i] = kNotRemoved;
-          S.lMlo[i] = 0;
-          S.lMhi[i] = 0;
-          S.lId[i] = j + 1;
-          S.lText[i] = sg.text;
-          S.lMeta[i] = mkMeta(in.initClient, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
-          S.leafBlk[j + 1] = b;
-          S.winIdx[j + 1] = kNone;
-        }
-      }
-    }
-    nextId = N + 1;
-    // leaf blocks: count, parent later; stable sums; group lists
-    uint32_t cntL = nLeafBlk;
     nGroups = static_cast<int>((nLeafBlk + kFill - 1) / kFill);
     if (nGroups > kGroupCap) {
       fail(FMT_E_CAPACITY);
       return;
     }
+    // leaf blocks (lane = block): their leaves, count, stable sum, group slot
     for (uint32_t base = 0; base < nLeafBlk; base += 64) {
       FOR_LANES(l) {
         const uint32_t b = base + l;
         if (b < nLeafBlk) {
-          const uint32_t c = (N - 7 * b) < 7 ? N - 7 * b : 7;
+          uint32_t st, c;
+          shapeNode(pairs, N, b, &st, &c);
+          int sum = 0;
+          for (uint32_t k = 0; k < c; k++) {
+            const uint32_t j = st + k;
+            const size_t i = static_cast<size_t>(b) * 8 + k;
+            const fmt_mt_snapshot_seg sg = in.segs[j];
+            const uint32_t len = sg.len & ~FMT_MT_SEG_MARKER;
+            S.lLen[i] = len;
+            S.lIns[i] = 0;
+            S.lRm[i] = kNotRemoved;
+            S.lMlo[i] = 0;
+            S.lMhi[i] = 0;
+            S.lId[i] = j + 1;
+            S.lText[i] = sg.text;
+            S.lMeta[i] = mkMeta(in.initClient, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
+            S.leafBlk[j + 1] = b;
+            S.winIdx[j + 1] = kNone;
+            sum += static_cast<int>(len);
+          }
           S.bCount[b] = c;
           S.bLeaf[b] = 1;
           S.bScour[b] = -1;
           S.bParent[b] = kNone;
-          int st = 0;
-          for (uint32_t k = 0; k < c; k++) st += static_cast<int>(rd(S.lLen + (static_cast<size_t>(b) * 8 + k)));
           const uint32_t g = b / kFill, s = b % kFill;
           S.bGroup[b] = g;
           S.bSlot[b] = s;
           S.gSlotBlk[static_cast<size_t>(g) * kSlotCap + s] = b;
-          S.gSlotStable[static_cast<size_t>(g) * kSlotCap + s] = st;
+          S.gSlotStable[static_cast<size_t>(g) * kSlotCap + s] = sum;
         }
       }
     }
+    nextId = N + 1;
     waveSync();
+    loadProps(nLeafBlk, pairs);
+    if (status != FMT_OK) return;
     for (int g = 0; g < nGroups; g++) {
       const uint32_t lo = static_cast<uint32_t>(g) * kFill, hi = lo + kFill < nLeafBlk ? lo + kFill : nLeafBlk;
       Lane<uint32_t> acc;
@@ -2777,10 +2864,12 @@ class HugeDoc {
       L->gCorr[g] = 0;
       waveSync();
     }
-    // interior levels, 7 children per block
-    uint32_t lo = 0, next = nLeafBlk;
-    while (cntL > 1) {
-      const uint32_t nb = (cntL + 6) / 7;
+    // interior levels (lane = block)
+    uint32_t lo = 0, next = nLeafBlk, below = nLeafBlk;
+    const uint32_t* lvPairs = pairs;
+    for (uint32_t lvl = 1; lvl < nLv; lvl++) {
+      const uint32_t nb = shapeCount(lvl);
+      if (lvPairs != nullptr) lvPairs += 2 * static_cast<size_t>(below);
       if (next + nb > S.blockCap) {
         fail(FMT_E_CAPACITY);
         return;
@@ -2789,15 +2878,16 @@ class HugeDoc {
         FOR_LANES(l) {
           const uint32_t q = base + l;
           if (q < nb) {
+            uint32_t st, c;
+            shapeNode(lvPairs, below, q, &st, &c);
             const uint32_t id = next + q;
-            const uint32_t c = cntL - 7 * q < 7 ? cntL - 7 * q : 7;
             S.bCount[id] = c;
             S.bLeaf[id] = 0;
             S.bScour[id] = -1;
             S.bParent[id] = kNone;
             for (uint32_t k = 0; k < c; k++) {
-              S.bChild[static_cast<size_t>(id) * 8 + k] = lo + 7 * q + k;
-              S.bParent[lo + 7 * q + k] = id;
+              S.bChild[static_cast<size_t>(id) * 8 + k] = lo + st + k;
+              S.bParent[lo + st + k] = id;
             }
           }
         }
@@ -2805,13 +2895,58 @@ class HugeDoc {
       waveSync();
       lo = next;
       next += nb;
-      cntL = nb;
+      below = nb;
     }
     root = static_cast<int>(lo);
     nextBlock = next;
     lastBlk = nLeafBlk - 1;
     minSeq = in.snapMinSeq;
     curSeq = in.snapSeq;
+  }
+
+  // The loaded segments' properties (IJSONTextSegment.props: the segment's properties are a clone of
+  // them, textSegment.ts:41-52): interned once per distinct props op, 64 segments a step.
+  FMT_DEV void loadProps(uint32_t nLeafBlk, const uint32_t* pairs) {
+    if (!in.segProps) return;
+    uint32_t lastOp = kNone, lastSet = kNoProps;
+    for (uint32_t base = 0; base < nLeafBlk * 8; base += 64) {
+      Lane<uint32_t> op;
+      FOR_LANES(l) {
+        const uint32_t x = base + l, b = x >> 3, k = x & 7;
+        uint32_t v = FMT_MT_NO_PROPS;
+        if (b < nLeafBlk) {
+          uint32_t st, c;
+          shapeNode(pairs, in.nSegs, b, &st, &c);
+          if (k < c) v = in.segs[st + k].props;
+        }
+        LANE(op) = v;
+      }
+      for (;;) {
+        Lane<bool> p;
+        FOR_LANES(l) { LANE(p) = LANE(op) != FMT_MT_NO_PROPS; }
+        const uint64_t m = ballot(p);
+        if (m == 0) break;
+        const uint32_t id = readlane(op, ctz64(m));
+        if (id >= in.nPropsOps) {
+          fail(FMT_E_DATA);
+          return;
+        }
+        if (id != lastOp) {
+          lastSet = applyProps(kNoProps, id);
+          if (status != FMT_OK) return;
+          lastOp = id;
+        }
+        FOR_LANES(l) {
+          if (LANE(op) == id) {
+            const uint32_t x = base + l;
+            const size_t i = li(x >> 3, static_cast<int>(x & 7));
+            S.lMeta[i] = mkMeta(in.initClient, lastSet) | (rd(S.lMeta + i) & kMetaMarker);
+            LANE(op) = FMT_MT_NO_PROPS;
+          }
+        }
+      }
+    }
+    waveSync();
   }
 
   // ------------------------------------------------------------------ driver
@@ -3033,7 +3168,7 @@ class HugeDoc {
             x.pad = static_cast<uint16_t>((blk >> 16) | (mMarker(m) ? FMT_MT_LEAF_MARKER : 0u));
             outLeaves[o] = x;
             const uint32_t t = rd(S.lText + i);
-            for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(loadWg(S.text + t + c));
+            for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(textAt(t + c));
           }
         }
         nLeaves += tv;

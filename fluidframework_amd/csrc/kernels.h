@@ -107,12 +107,10 @@ MtCaps mergeTreeCaps(bool large);
 // tier and lists its overflow in esc2 (count + 1 entries) for the small tier. esc[0] and esc2[0] must
 // be zero before the call. sched: 3 zeroed device counters (compact, small, large) from which the
 // tiers deal documents to waves dynamically (nullptr: static grid-stride shares). adjust: the batch
-// holds annotate-adjust entries (the Adj engine variants, small tier first, no checkpoints). lean: no
-// op of the batch has FMT_MT_F_CATCHUP / REL1 / REL2 / LOADSEG (the Lean variants of the plain path).
+// holds annotate-adjust entries (the Adj engine variants, small tier first, no checkpoints).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
-                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust,
-                           bool lean);
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust);
 
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,

@@ -35,7 +35,7 @@ size_t mergeTreeCheckpointBytes() { return sizeof(uint32_t) * fmt_mt::Doc<false,
 
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                   uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next,
-                                  bool obliterate, bool lean);
+                                  bool obliterate);
 
 // The compact tier's overflow list in[0] = n, in[1..n] reordered into out by remaining ops,
 // longest first (64 buckets between 0 and the largest remainder): with documents dealt to waves
@@ -86,8 +86,7 @@ __global__ __launch_bounds__(1024) void orderByRemainingKernel(const uint32_t* _
 // Variants: obliterates (Ob) and/or the remove-order recording of SnapshotV1 batches (Rm).
 hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                            uint32_t count, uint32_t* esc, uint32_t* esc2, uint32_t* esc3, int numCUs,
-                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust,
-                           bool lean) {
+                           hipStream_t stream, bool obliterate, bool removeOrder, uint32_t* sched, bool adjust) {
   using S = fmt_mt::SmallTier;
   uint32_t* n1 = sched ? sched + 1 : nullptr;
   if (adjust) {  // annotate-adjust batches: the Adj variants, small tier over every document (no checkpoints)
@@ -104,7 +103,7 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
   if (esc == nullptr || esc2 == nullptr)
     return launchTier<false, S, false, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   // compact tier over everything → overflow list esc2 → this tier over that list → overflow list esc
-  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream, sched, obliterate, lean);
+  hipError_t e = launchMergeTreeCompact(batch, out, docList, count, esc2, numCUs, stream, sched, obliterate);
   if (e != hipSuccess) return e;
   if (esc3 != nullptr && out.ckpt != nullptr) {  // longest remaining streams first
     hipLaunchKernelGGL(orderByRemainingKernel, dim3(1), dim3(1024), 0, stream, esc2, esc3, out.headers,
@@ -114,8 +113,6 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
   }
   if (obliterate)
     return launchTier<true, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
-  if (lean)
-    return launchTier<false, S, false, kMtWaves, 2, false, true>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
   return launchTier<false, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);
 }
 

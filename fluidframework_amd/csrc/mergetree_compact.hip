@@ -12,13 +12,10 @@ int mergeTreeProfileCompact(uint64_t* out, int n, bool reset) { return addTuProf
 
 hipError_t launchMergeTreeCompact(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                   uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream, uint32_t* next,
-                                  bool obliterate, bool lean) {
+                                  bool obliterate) {
   if (obliterate)  // Doc<true>: the same 4 rows plus the live-obliterate table (163 VGPRs)
     return launchTier<true, fmt_mt::CompactTier, false, kMtWavesCompact, 3>(batch, out, docList, count, esc, numCUs,
                                                                            stream, nullptr, next);
-  if (lean)  // no catch-up / relative-position / loader-segment ops in the batch
-    return launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 4, false, true>(batch, out, docList, count, esc,
-                                                                                        numCUs, stream, nullptr, next);
   return launchTier<false, fmt_mt::CompactTier, false, kMtWavesCompact, 4>(batch, out, docList, count, esc, numCUs,
                                                                           stream, nullptr, next);
 }

@@ -323,10 +323,7 @@ FMT_DEV uint32_t adjustFold(const AdjustTables* A, uint32_t doc, uint32_t cur, u
 // batches without such ops run the Rm = false code, which has none of it.
 // Adj: the variant that folds annotate-adjust entries (batches with adjusts; always with Ob, whose
 // runtime path restarts overflowing documents in the next tier instead of checkpointing them).
-// Lean: the variant for batches without catch-up recording, relative positions or loader segments
-// (no FMT_MT_F_CATCHUP / REL1 / REL2 / LOADSEG op): those paths, and the pointers they keep live
-// across the op loop, are compiled out, which frees scalar registers for the hot path.
-template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false, bool Lean = false>
+template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false>
 class Doc {
  public:
   using VR = typename C::VR;
@@ -2164,7 +2161,7 @@ class Doc {
   }
 
   FMT_DEV void applyOp(const fmt_mt_op& op, const Lane<uint32_t>& text0) {
-    const bool catchup = !Lean && (op.flags & FMT_MT_F_CATCHUP) != 0;
+    const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
     Lane<uint32_t> delta;  // catch-up: the segments of the op's delta event (row bitmask per lane)
     if (op.type == FMT_MT_INSERT) {
       const int k = insertText(op, text0);
@@ -2177,14 +2174,14 @@ class Doc {
       if (!applyRange(op, delta)) return;
     }
     // one call site: the recording is inlined once; a sided obliterate raises OBLITERATE (:2249-2253)
-    if constexpr (!Lean) recordCatchup(delta, op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
+    recordCatchup(delta, op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
   }
 
   // Remove / annotate (after their boundary splits); fills `delta` for catch-up ops. Returns true
   // when a catch-up recording should follow.
   FMT_DEV bool applyRange(const fmt_mt_op& op, Lane<uint32_t>& delta) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
-    const bool catchup = !Lean && (op.flags & FMT_MT_F_CATCHUP) != 0;
+    const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
     bool obliterate = false;
     if constexpr (Ob) obliterate = op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED;
     const int start = op.pos1, end = op.pos2;
@@ -2951,11 +2948,9 @@ class Doc {
       txt0 = fetchText(rec0);
       rec1 = fetchOp(i + 2);
       stamp(kPfOpLoad);
-      if constexpr (!Lean) opIdx = static_cast<uint32_t>(i - in.begin);
-      const bool loader = !Lean && (op.flags & FMT_MT_F_LOADSEG) != 0;
-      if (Lean && (op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) != 0) {
-        fail(FMT_E_USAGE);  // (the runtime picks the Lean variant only for batches without them)
-      } else if (loader) {
+      opIdx = static_cast<uint32_t>(i - in.begin);
+      const bool loader = (op.flags & FMT_MT_F_LOADSEG) != 0;
+      if (loader) {
         if (op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient) loadBodySegment(op, text);
         else fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
       } else if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63
@@ -2963,7 +2958,7 @@ class Doc {
       else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
-      else if (Lean || (op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
+      else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
       if constexpr (Rm) {
         if (rmPendN > 0 || rmHitsSet)
           rmFlush(op.client, op.seq, op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE);

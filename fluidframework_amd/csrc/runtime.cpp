@@ -135,7 +135,6 @@ struct fmt_ctx {
   DevBuf<fmt_mt_catchup_range> mtCatchup;    // catch-up range slabs
   std::vector<uint64_t> mtCuOffsHost;
   bool mtHasCatchup = false;
-  bool mtLean = false;                       // no catch-up / relative-position / loader-segment op (Lean kernels)
   DevBuf<uint64_t> mtRmOffs;                 // per-doc remove-order slab offsets (n_docs + 1)
   DevBuf<fmt_mt_remove_order> mtRmOrder;     // remove-order slabs (FMT_MT_F_RMORDER ops)
   std::vector<uint64_t> mtRmOffsHost;
@@ -146,16 +145,22 @@ struct fmt_ctx {
     fmt_huge::HugeState state{};
     fmt_huge::HugeInputs in{};
     fmt_kernels::HugeOut out{};
+    std::vector<uint32_t> shape;             // host copy of in.shape (kept until the load completes)
   };
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
   // documents that outgrow the large tier replay again, from their start, in the huge tier when
   // they hold nothing it does not (mtHugeOk: no catch-up / remove-order recording,
-  // relative positions, annotate-adjust or SnapshotV1 merge info; no body chunk); their starts
+  // relative positions, annotate-adjust or SnapshotV1 merge info); their starts
   std::vector<uint8_t> mtHugeOk;
+  std::vector<uint8_t> mtSegProps;           // per document: a loaded segment has properties
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
   std::vector<fmt_mt_snapshot_seg> mtStartSeg;  // per document: its initial text as one segment (len 0: none)
   uint32_t mtHugeLoaded = 0;                 // huge documents routed at load (the rest were escalated)
+  // documents refused at load (a feature the huge tier lacks, or no device memory for its state):
+  // their headers are written at load and no tier runs them; the rest of the batch is unaffected
+  std::vector<uint32_t> mtRefused;
+  bool mtUseList = false;                    // the small tiers run mtSmallList (huge or refused docs)
   uint32_t mtGrown = 0;                      // documents the last run escalated into the huge tier
   uint32_t mtNPropsOps = 0;
   std::vector<uint64_t> mtOffsHost;          // host copies of doc_op_offsets and the snapshot docs
@@ -221,6 +226,22 @@ int hipErr(fmt_ctx* c, hipError_t e, const char* what) {
     hipError_t e_ = (expr);                                \
     if (e_ != hipSuccess) return hipErr((ctx), e_, #expr); \
   } while (0)
+
+// Host threads for the runtime's own passes over a batch (validation, per-document sizing).
+unsigned hostWorkers() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+
+// fn(begin, end, worker) over hostWorkers() contiguous shares of [0, n) (one share below 2^16 items).
+template <class F>
+void parallelChunks(uint64_t n, F&& fn) {
+  const unsigned T = n < (1u << 16) ? 1u : hostWorkers();
+  if (T == 1) {
+    fn(0, n, 0u);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (unsigned t = 0; t < T; t++) pool.emplace_back([&, t] { fn(n * t / T, n * (t + 1) / T, t); });
+  for (auto& th : pool) th.join();
+}
 
 hipError_t stageInit(fmt_ctx* c) {
   Stager& S = c->stage;
@@ -618,9 +639,9 @@ int fmt_mt_capacity(uint32_t* maxLeaves, uint32_t* maxChars, uint32_t* maxProps)
 // (ops [o0, o1) of the staged batch, nSegs start segments at segsDev) and output buffers; header d.
 // textPerOp bounds the merge area (zamboni appends build their text there).
 static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32_t d, uint64_t o0,
-                        uint64_t o1, const fmt_mt_snapshot_seg* segsDev, uint64_t N, int32_t minSeq, int32_t seq,
-                        int32_t initClient, uint64_t textPerOp, uint64_t docChars) {
-  const uint64_t nOps = o1 - o0;
+                        uint64_t o1, const fmt_mt_snapshot_seg* segsDev, uint64_t nHeader, uint64_t nBody, int32_t minSeq,
+                        int32_t seq, int32_t initClient, uint64_t textPerOp, uint64_t docChars) {
+  const uint64_t nOps = o1 - o0, N = nHeader + nBody;
   c->mtHugeSlot[d] = static_cast<int32_t>(c->huge.size());
   c->huge.emplace_back();
   auto& H = c->huge.back();
@@ -629,18 +650,39 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
     if (e == hipSuccess) H.allocs.push_back(*out);
     return e;
   };
+  // a document whose state does not fit in device memory fails alone (FMT_E_CAPACITY): what it
+  // allocated is released and it leaves the huge tier
+  auto drop = [&](hipError_t e) -> int {
+    for (void* q : H.allocs) (void)hipFree(q);
+    c->huge.pop_back();
+    c->mtHugeSlot[d] = -1;
+    if (e == hipErrorOutOfMemory) {
+      (void)hipGetLastError();
+      return FMT_E_CAPACITY;
+    }
+    return hipErr(c, e, "setupHugeDoc");
+  };
   fmt_huge::HugeState& S = H.state;
-  S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
+  uint64_t shapeBlocks = 0;
+  if (nBody > 0) {
+    fmt_huge::loadShape(nHeader, nBody, H.shape);
+    for (uint32_t l = 0; l < H.shape[0]; l++) shapeBlocks += H.shape[1 + l];
+  }
+  const uint64_t blockCap = shapeBlocks + 2 * (N / 7 + 1) + 2 * nOps + 1024;
+  if (blockCap > 0xFFFFFFF0ull || N + 3 * nOps + 16 > 0xFFFFFFF0ull) return drop(hipErrorOutOfMemory);
+  S.blockCap = static_cast<uint32_t>(blockCap);
   S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
   S.winCap = S.idCap;  // every leaf can be in the window (a wide remove puts many there)
   // the merge area: two halves (huge_engine.h compactText), each able to hold the document's whole
   // text twice over (its live merged text plus one run as long as the document)
   const uint64_t merge = std::max<uint64_t>(textPerOp * nOps + 65536, 4 * docChars + 131072);
   const uint64_t textCap = std::min<uint64_t>(textLen + merge, 0xFFFFFFF0ull);
+  if (textCap <= textLen) return drop(hipErrorOutOfMemory);  // (offsets are 32-bit)
   const size_t nl = static_cast<size_t>(S.blockCap) * 8, nb = S.blockCap;
   void* p;
-#define FMT_ALLOC(field, T, count)                        \
-  FMT_HIP(c, alloc((count) * sizeof(T), &p));              \
+  hipError_t e;
+#define FMT_ALLOC(field, T, count)                                      \
+  if ((e = alloc((count) * sizeof(T), &p)) != hipSuccess) return drop(e); \
   S.field = static_cast<T*>(p);
   FMT_ALLOC(lLen, uint32_t, nl) FMT_ALLOC(lIns, int32_t, nl) FMT_ALLOC(lRm, int32_t, nl)
   FMT_ALLOC(lMlo, uint32_t, nl) FMT_ALLOC(lMhi, uint32_t, nl) FMT_ALLOC(lId, uint32_t, nl)
@@ -654,11 +696,13 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   FMT_ALLOC(wRec, uint32_t, static_cast<size_t>(S.winCap) * 4) FMT_ALLOC(wMask, uint32_t, static_cast<size_t>(S.winCap) * 2)
   FMT_ALLOC(wBlk, uint32_t, S.winCap)
   FMT_ALLOC(wLeaf, uint32_t, S.winCap)
-  FMT_ALLOC(text, uint16_t, textCap) FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * fmt_huge::kPropWords)
-#undef FMT_ALLOC
+  // the merge area only; the batch text is read in place (huge_engine.h HugeState::base)
+  FMT_ALLOC(text, uint16_t, textCap - textLen)
+  FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * fmt_huge::kPropWords)
+  S.text -= textLen;
+  S.base = c->mtText.p;
   S.textLen = textLen;
   S.textCap = textCap;
-  FMT_HIP(c, hipMemcpyAsync(S.text, c->mtText.p, textLen * sizeof(uint16_t), hipMemcpyDeviceToDevice, c->stream));
   fmt_huge::HugeInputs& I = H.in;
   I.ops = c->mtOps.p;
   I.begin = o0;
@@ -668,6 +712,13 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   I.nPropsOps = nPropsOps;
   I.segs = segsDev;
   I.nSegs = static_cast<uint32_t>(N);
+  I.segProps = c->mtSegProps.empty() ? 0u : c->mtSegProps[d];
+  I.shape = nullptr;
+  if (!H.shape.empty()) {
+    if ((e = alloc(H.shape.size() * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    FMT_HIP(c, hipMemcpyAsync(p, H.shape.data(), H.shape.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    I.shape = static_cast<const uint32_t*>(p);
+  }
   I.snapMinSeq = minSeq;
   I.snapSeq = seq;
   I.initClient = initClient;
@@ -675,13 +726,13 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   O.header = c->mtHdr.p + d;
   O.capLeaves = N + 3 * nOps + 8;
   O.capChars = docChars + 8;  // (every unit the document can hold: its start plus its inserts)
-  FMT_HIP(c, alloc(O.capLeaves * sizeof(fmt_mt_leaf), &p));
+  if ((e = alloc(O.capLeaves * sizeof(fmt_mt_leaf), &p)) != hipSuccess) return drop(e);
   O.leaves = static_cast<fmt_mt_leaf*>(p);
-  FMT_HIP(c, alloc(O.capChars * sizeof(uint16_t), &p));
+  if ((e = alloc(O.capChars * sizeof(uint16_t), &p)) != hipSuccess) return drop(e);
   O.chars = static_cast<uint16_t*>(p);
-  FMT_HIP(c, alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p));
+  if ((e = alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p)) != hipSuccess) return drop(e);
   O.props = static_cast<fmt_mt_propset*>(p);
-  FMT_HIP(c, alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p));
+  if ((e = alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p)) != hipSuccess) return drop(e);
   O.prof = static_cast<unsigned long long*>(p);
   return FMT_OK;
 }
@@ -692,32 +743,64 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   const uint32_t n = b->n_docs;
   if (b->doc_op_offsets[0] != 0 || b->doc_op_offsets[n] != b->n_ops)
     return setErr(c, FMT_E_USAGE, "doc_op_offsets do not cover ops");
+  // one pass over the op records on host threads: counts, and the first invalid record
+  struct OpScan {
+    uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
+    bool obliterates = false;
+    uint64_t errAt = ~0ull;
+    int errCode = FMT_OK;
+    const char* err = nullptr;
+  };
+  std::vector<OpScan> scans(hostWorkers());
+  parallelChunks(b->n_ops, [&](uint64_t lo, uint64_t hi, unsigned t) {
+    OpScan& S = scans[t];
+    auto bad = [&](uint64_t i, int code, const char* what) {
+      S.errAt = i;
+      S.errCode = code;
+      S.err = what;
+    };
+    for (uint64_t i = lo; i < hi; i++) {
+      const fmt_mt_op& op = b->ops[i];
+      if (op.flags & FMT_MT_F_CATCHUP) S.catchupOps++;
+      if (op.flags & FMT_MT_F_RMORDER) S.rmOrderOps++;
+      if (op.flags & FMT_MT_F_LOADSEG) {  // a SnapshotV1 body segment: its merge info row in range
+        if (op.type != FMT_MT_INSERT || b->snapshot_info == nullptr || op.pos1 < 0 ||
+            static_cast<uint64_t>(op.pos1) >= b->n_snapshot_segs ||
+            b->snapshot_info[op.pos1].rm_first + static_cast<uint64_t>(b->snapshot_info[op.pos1].rm_count) > b->n_snapshot_stamps) {
+          bad(i, FMT_E_DATA, "a loader segment (FMT_MT_F_LOADSEG) without a valid merge-info row");
+          return;
+        }
+      }
+      if (op.type == FMT_MT_INSERT) {
+        if (static_cast<uint64_t>(op.payload) + fmt_mt_op_len(&op) > b->text_len) {
+          bad(i, FMT_E_DATA, "insert payload outside the text arena");
+          return;
+        }
+        S.insertChars += fmt_mt_op_len(&op);
+      } else if (op.type == FMT_MT_ANNOTATE) {
+        if (op.payload >= b->n_props_ops) {
+          bad(i, FMT_E_DATA, "annotate props op id out of range");
+          return;
+        }
+      } else if (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED) {
+        S.obliterates = true;
+      } else if (op.type != FMT_MT_REMOVE) {
+        bad(i, FMT_E_UNSUPPORTED, "op type not supported by this engine build");
+        return;
+      }
+    }
+  });
   uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
   bool obliterates = false;
-  uint32_t rareFlags = 0;
-  for (uint64_t i = 0; i < b->n_ops; i++) {
-    const fmt_mt_op& op = b->ops[i];
-    if (op.flags & FMT_MT_F_CATCHUP) catchupOps++;
-    if (op.flags & FMT_MT_F_RMORDER) rmOrderOps++;
-    rareFlags |= op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG);
-    if (op.flags & FMT_MT_F_LOADSEG) {  // a SnapshotV1 body segment: its merge info row in range
-      if (op.type != FMT_MT_INSERT || b->snapshot_info == nullptr || op.pos1 < 0 ||
-          static_cast<uint64_t>(op.pos1) >= b->n_snapshot_segs ||
-          b->snapshot_info[op.pos1].rm_first + static_cast<uint64_t>(b->snapshot_info[op.pos1].rm_count) > b->n_snapshot_stamps)
-        return setErr(c, FMT_E_DATA, "a loader segment (FMT_MT_F_LOADSEG) without a valid merge-info row");
-    }
-    if (op.type == FMT_MT_INSERT) {
-      if (static_cast<uint64_t>(op.payload) + fmt_mt_op_len(&op) > b->text_len)
-        return setErr(c, FMT_E_DATA, "insert payload outside the text arena");
-      insertChars += fmt_mt_op_len(&op);
-    } else if (op.type == FMT_MT_ANNOTATE) {
-      if (op.payload >= b->n_props_ops) return setErr(c, FMT_E_DATA, "annotate props op id out of range");
-    } else if (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED) {
-      obliterates = true;
-    } else if (op.type != FMT_MT_REMOVE) {
-      return setErr(c, FMT_E_UNSUPPORTED, "op type not supported by this engine build");
-    }
+  const OpScan* firstBad = nullptr;
+  for (const OpScan& S : scans) {
+    insertChars += S.insertChars;
+    catchupOps += S.catchupOps;
+    rmOrderOps += S.rmOrderOps;
+    obliterates = obliterates || S.obliterates;
+    if (S.err != nullptr && (firstBad == nullptr || S.errAt < firstBad->errAt)) firstBad = &S;
   }
+  if (firstBad != nullptr) return setErr(c, firstBad->errCode, firstBad->err);
   if (b->snapshots) {
     for (uint32_t d = 0; d < n; d++) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
@@ -796,7 +879,6 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   // Catch-up slabs: kCatchupPerOp ranges per flagged op plus kCatchupPerDoc per document that has
   // any; a document that needs more reports FMT_E_CAPACITY.
   c->mtHasCatchup = catchupOps > 0;
-  c->mtLean = rareFlags == 0;
   if (c->mtHasCatchup) {
     constexpr uint64_t kCatchupPerOp = 16, kCatchupPerDoc = 16;
     c->mtCuOffsHost.assign(n + 1ull, 0);
@@ -958,9 +1040,11 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->huge.clear();
   c->mtHugeSlot.assign(n, -1);
   c->mtHugeOk.assign(n, 1);
+  c->mtSegProps.assign(n, 0);
   c->mtDocChars.assign(n, 0);
   c->mtStartSeg.assign(n, fmt_mt_snapshot_seg{0, 0, FMT_MT_NO_PROPS});
-  for (uint32_t d = 0; d < n; d++) {
+  parallelChunks(n, [&](uint64_t d0, uint64_t d1, unsigned) {
+  for (uint64_t d = d0; d < d1; d++) {
     uint8_t ok = 1;
     uint64_t chars = 0;
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
@@ -972,7 +1056,11 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     }
     if (b->snapshots && b->snapshots[d].loaded) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
-      if (sd.n_body != 0) ok = 0;
+      for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
+        if (b->snapshot_segs[k].props != FMT_MT_NO_PROPS) {
+          c->mtSegProps[d] = 1;
+          break;
+        }
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       for (uint64_t k = sd.first_seg; b->snapshot_info != nullptr && k < sd.first_seg + sd.n_header; k++)
@@ -984,6 +1072,21 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     c->mtHugeOk[d] = ok;
     c->mtDocChars[d] = chars;
   }
+  });
+  // Summary-loaded documents past the large tier go to the huge tier; one that holds a feature the
+  // huge tier lacks, or whose state does not fit in device memory, fails alone at load (its header
+  // says why) and the rest of the batch replays.
+  c->mtRefused.clear();
+  std::vector<fmt_mt_doc_result> refusedHdr;
+  auto refuse = [&](uint32_t d, int status) {
+    fmt_mt_doc_result h{};
+    h.status = status;
+    h.fail_seq = b->snapshots[d].seq;
+    h.cur_seq = b->snapshots[d].seq;
+    h.min_seq = b->snapshots[d].min_seq;
+    c->mtRefused.push_back(d);
+    refusedHdr.push_back(h);
+  };
   if (b->snapshots) {
     const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true);
     for (uint32_t d = 0; d < n; d++) {
@@ -993,35 +1096,35 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (sd.n_body != 0)
-        return setErr(c, FMT_E_UNSUPPORTED, "a document beyond the large tier must load from one header chunk (n_body = 0)");
-      const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
-      if (b->snapshot_info != nullptr) {
-        for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header; k++)
-          if (b->snapshot_info[k].ins_seq != 0 || b->snapshot_info[k].rm_count != 0)
-            return setErr(c, FMT_E_UNSUPPORTED, "SnapshotV1 merge info in a document beyond the large tier");
-      }
-      for (uint64_t i = o0; i < o1; i++) {
-        if (b->ops[i].flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2))
-          return setErr(c, FMT_E_UNSUPPORTED,
-                        "catch-up / remove-order recording or relative positions in a document beyond the large tier");
-        if (b->ops[i].type == FMT_MT_ANNOTATE && adjCount[b->ops[i].payload] > 0)
-          return setErr(c, FMT_E_UNSUPPORTED, "annotate-adjust in a document beyond the large tier");
+      if (!c->mtHugeOk[d]) {  // (V1 merge info, recording, relative positions, annotate-adjust)
+        refuse(d, FMT_E_UNSUPPORTED);
+        continue;
       }
       const int rc = setupHugeDoc(c, b->text_len, b->n_props_ops, d, b->doc_op_offsets[d], b->doc_op_offsets[d + 1],
-                                  c->mtSnapSegs.p + sd.first_seg, sd.n_header, sd.min_seq, sd.seq, FMT_NON_COLLAB_CLIENT, 256,
+                                  c->mtSnapSegs.p + sd.first_seg, sd.n_header, sd.n_body, sd.min_seq, sd.seq,
+                                  FMT_NON_COLLAB_CLIENT, 256,
                                   c->mtDocChars[d]);
-      if (rc != FMT_OK) return rc;
+      if (rc == FMT_E_CAPACITY) refuse(d, FMT_E_CAPACITY);
+      else if (rc != FMT_OK) return rc;
     }
   }
+  for (size_t i = 0; i < c->mtRefused.size(); i++)
+    FMT_HIP(c, hipMemcpyAsync(c->mtHdr.p + c->mtRefused[i], &refusedHdr[i], sizeof(fmt_mt_doc_result), hipMemcpyHostToDevice,
+                              c->stream));
   c->mtHugeLoaded = static_cast<uint32_t>(c->huge.size());
-  if (!c->huge.empty()) {
-    const size_t nh = c->huge.size();
+  c->mtUseList = !c->huge.empty() || !c->mtRefused.empty();
+  if (c->mtUseList) {
+    std::vector<uint8_t> skip(n, 0);
+    for (uint32_t d : c->mtRefused) skip[d] = 1;
     std::vector<uint32_t> small;
     for (uint32_t d = 0; d < n; d++)
-      if (c->mtHugeSlot[d] < 0) small.push_back(d);
+      if (c->mtHugeSlot[d] < 0 && !skip[d]) small.push_back(d);
     c->mtNSmall = static_cast<uint32_t>(small.size());
     FMT_HIP(c, c->mtSmallList.reserve(small.size()));
+    FMT_HIP(c, cp(c->mtSmallList.p, small.data(), small.size() * sizeof(uint32_t)));
+  }
+  if (!c->huge.empty()) {
+    const size_t nh = c->huge.size();
     FMT_HIP(c, c->hugeStates.reserve(nh));
     FMT_HIP(c, c->hugeInputs.reserve(nh));
     FMT_HIP(c, c->hugeOuts.reserve(nh));
@@ -1033,12 +1136,11 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       hi[i] = c->huge[i].in;
       ho[i] = c->huge[i].out;
     }
-    FMT_HIP(c, cp(c->mtSmallList.p, small.data(), small.size() * sizeof(uint32_t)));
     FMT_HIP(c, cp(c->hugeStates.p, hs.data(), nh * sizeof(fmt_huge::HugeState)));
     FMT_HIP(c, cp(c->hugeInputs.p, hi.data(), nh * sizeof(fmt_huge::HugeInputs)));
     FMT_HIP(c, cp(c->hugeOuts.p, ho.data(), nh * sizeof(fmt_kernels::HugeOut)));
-    FMT_HIP(c, hipStreamSynchronize(c->stream));
   }
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
   c->mtLoaded = true;
   return FMT_OK;
 }
@@ -1072,12 +1174,12 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipMemsetAsync(c->mtEsc2.p, 0, sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
-  const bool hasHuge = c->mtHugeLoaded > 0;
-  if (!hasHuge || c->mtNSmall > 0)
-    FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, hasHuge ? c->mtSmallList.p : nullptr, hasHuge ? c->mtNSmall : c->mtDocs,
+  const bool hasHuge = c->mtHugeLoaded > 0, list = c->mtUseList;
+  if (!list || c->mtNSmall > 0)
+    FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,
                                             c->mtObliterate,
-                                            c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust, c->mtLean));
+                                            c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust));
   if (hasHuge)
     FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p, c->mtHugeLoaded, c->stream));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));  // device time excludes the host read-back below
@@ -1125,6 +1227,8 @@ int fmt_mt_run(fmt_ctx* c) {
       for (size_t i = 0; i < grow.size(); i++) starts[i] = c->mtStartSeg[grow[i]];
       FMT_HIP(c, hipMemcpyAsync(c->mtStartSegDev.p, starts.data(), grow.size() * sizeof(fmt_mt_snapshot_seg),
                                 hipMemcpyHostToDevice, c->stream));
+      // (a document whose huge-tier state does not fit in device memory keeps the large tier's
+      // FMT_E_CAPACITY header)
       for (size_t i = 0; i < grow.size(); i++) {
         const uint32_t d = grow[i];
         const uint64_t o0 = c->mtOffsHost[d], o1 = c->mtOffsHost[d + 1];
@@ -1132,14 +1236,15 @@ int fmt_mt_run(fmt_ctx* c) {
         if (c->mtSnapHost.size() > d && c->mtSnapHost[d].loaded) {
           const fmt_mt_snapshot_doc& sd = c->mtSnapHost[d];
           rc = setupHugeDoc(c, c->mtTextLen, c->mtNPropsOps, d, o0, o1, c->mtSnapSegs.p + sd.first_seg, sd.n_header,
-                            sd.min_seq, sd.seq, FMT_NON_COLLAB_CLIENT, 1024, c->mtDocChars[d]);
+                            sd.n_body, sd.min_seq, sd.seq, FMT_NON_COLLAB_CLIENT, 1024, c->mtDocChars[d]);
         } else {
           rc = setupHugeDoc(c, c->mtTextLen, c->mtNPropsOps, d, o0, o1, c->mtStartSegDev.p + i, starts[i].len > 0 ? 1 : 0,
-                            0, 0, FMT_LOCAL_CLIENT, 1024, c->mtDocChars[d]);
+                            0, 0, 0, FMT_LOCAL_CLIENT, 1024, c->mtDocChars[d]);
         }
-        if (rc != FMT_OK) return rc;
+        if (rc != FMT_OK && rc != FMT_E_CAPACITY) return rc;
       }
-      const size_t ng = grow.size();
+      const size_t ng = c->huge.size() - c->mtHugeLoaded;
+      if (ng > 0) {
       FMT_HIP(c, c->hugeStates2.reserve(ng));
       FMT_HIP(c, c->hugeInputs2.reserve(ng));
       FMT_HIP(c, c->hugeOuts2.reserve(ng));
@@ -1158,6 +1263,7 @@ int fmt_mt_run(fmt_ctx* c) {
       FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates2.p, c->hugeInputs2.p, c->hugeOuts2.p, static_cast<uint32_t>(ng),
                                              c->stream));
       FMT_HIP(c, hipStreamSynchronize(c->stream));
+      }
       c->mtGrown = static_cast<uint32_t>(ng);
     }
   }

@@ -224,8 +224,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_remove_order.argtypes = [P, U32, P, U32]
         L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
-        L.fmt_mt_state_digest.argtypes = [P, P]
-        L.fmt_mt_fetch_legacy_props.argtypes = [P, U32, P, U32]
+        for name, args in (("fmt_mt_state_digest", [P, P]), ("fmt_mt_fetch_legacy_props", [P, U32, P, U32])):
+            if path == LIB_PATH or hasattr(L, name):  # (older experimental builds may lack them)
+                getattr(L, name).argtypes = args
         _libs[path] = L
     return _libs[path]
 

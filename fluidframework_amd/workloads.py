@@ -11,7 +11,7 @@ import subprocess
 
 import numpy as np
 
-from .streams import (MAP_OP_DTYPE, MT_ANNOTATE, MT_INSERT, MT_OP_DTYPE, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
+from .streams import (MAP_OP_DTYPE, MT_ANNOTATE, MT_INSERT, MT_OP_DTYPE, MT_REMOVE, MT_SEG_MARKER, NO_PROPS, SNAPSHOT_DOC_DTYPE, SNAPSHOT_SEG_DTYPE, MapBatch,
                       MergeTreeBatch, js_json)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -146,6 +146,53 @@ def t3_stream(n_segments: int = 10_000_000, n_ops: int = 10_000_000, n_clients: 
         snapshots=snaps,
         snapshot_segs=segs,
     )
+
+
+def as_legacy_load(batch: MergeTreeBatch, header_chars: int = 10000, props_every: int = 0) -> MergeTreeBatch:
+    """A copy of a one-document summary-loaded batch (t3_stream) whose summary has the shape
+    SnapshotLegacy.emit writes (snapshotlegacy.ts:55, 126-193; summary.py legacy_summary): a header
+    chunk of the first segments up to header_chars UTF-16 units, the rest in the body chunk (loaded
+    by loadBody's appends, snapshotLoader.ts:277-309). props_every > 0: every props_every-th segment
+    spec carries props {"client": <name>} (props op (k // props_every) % n)."""
+    import dataclasses
+
+    lens = (batch.snapshot_segs["len"] & ~np.uint32(MT_SEG_MARKER)).astype(np.int64)
+    n = len(lens)
+    n_header = min(n, int(np.searchsorted(np.cumsum(lens), header_chars)) + 1)  # while length < header_chars
+    snaps = batch.snapshots.copy()
+    snaps["n_header"], snaps["n_body"] = n_header, n - n_header
+    segs = batch.snapshot_segs.copy()
+    if props_every:
+        k = np.arange(n)
+        pick = (k % props_every) == 0
+        segs["props"] = np.where(pick, (k // props_every) % (len(batch.props_off) - 1), segs["props"]).astype(np.uint32)
+    return dataclasses.replace(batch, snapshots=snaps, snapshot_segs=segs)
+
+
+def emptying_stream(n_segments: int = 3000, pairs: int = 600, seed: int = 1) -> MergeTreeBatch:
+    """A summary-loaded document (n_segments segments, beyond the large tier) that one remove
+    empties; then `pairs` insert/remove pairs, minSeq trailing by one, so zamboni scours every block
+    and packParent leaves the root childless (zamboni.ts:83-139); a final insert then grows the
+    document from its empty root again."""
+    import dataclasses
+
+    base = t3_stream(n_segments, 1, n_clients=2, max_lag=1, seed=seed)
+    total = int((base.snapshot_segs["len"] & ~np.uint32(MT_SEG_MARKER)).sum())
+    text = list(base.text.tolist())
+    ab = len(text)
+    text += [ord("a"), ord("b")]
+    hello = len(text)
+    text += [ord(c) for c in "hello"]
+    ops = np.zeros(2 * pairs + 2, dtype=MT_OP_DTYPE)
+    ops[0] = (1, 0, 0, 0, total, 0, 0, 1, MT_REMOVE, 0)
+    seq = 2
+    for i in range(pairs):
+        ops[1 + 2 * i] = (seq, seq - 1, seq - 1, 0, 0, ab, 2, 2, MT_INSERT, 0)
+        ops[2 + 2 * i] = (seq + 1, seq, seq, 0, 2, 0, 0, 3, MT_REMOVE, 0)
+        seq += 2
+    ops[-1] = (seq, seq - 1, seq - 1, 0, 0, hello, 5, 2, MT_INSERT, 0)
+    return dataclasses.replace(base, ops=ops, doc_op_offsets=np.array([0, len(ops)], dtype=np.uint64),
+                               text=np.asarray(text, dtype="<u2"))
 
 
 def with_insert_props(batch: MergeTreeBatch, every: int = 3) -> MergeTreeBatch:

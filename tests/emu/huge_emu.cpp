@@ -33,16 +33,25 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
     sd.n_header = 1;
   }
   const uint64_t nOps = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
-  const uint32_t N = sd.n_header;
+  const uint32_t N = sd.n_header + (loaded ? sd.n_body : 0);
+  std::vector<uint32_t> shape;  // (runtime.cpp setupHugeDoc)
+  uint64_t shapeBlocks = 0;
+  if (loaded && sd.n_body > 0) {
+    loadShape(sd.n_header, sd.n_body, shape);
+    for (uint32_t l = 0; l < shape[0]; l++) shapeBlocks += shape[1 + l];
+  }
+  bool segProps = false;
+  if (loaded)
+    for (uint64_t k = sd.first_seg; k < sd.first_seg + N; k++) segProps = segProps || b->snapshot_segs[k].props != FMT_MT_NO_PROPS;
   HugeState S{};
-  S.blockCap = static_cast<uint32_t>(2 * (N / 7 + 1) + 2 * nOps + 1024);
+  S.blockCap = static_cast<uint32_t>(shapeBlocks + 2 * (N / 7 + 1) + 2 * nOps + 1024);
   S.idCap = static_cast<uint32_t>(N + 3 * nOps + 16);
   S.winCap = S.idCap;  // every leaf can be in the window (wide removes)
   uint64_t docChars = initSeg.len;  // (runtime.cpp setupHugeDoc; the snapshot's text counts below)
   for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
     if (b->ops[i].type == FMT_MT_INSERT) docChars += fmt_mt_op_len(&b->ops[i]);
   if (loaded)
-    for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header; k++) docChars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
+    for (uint64_t k = sd.first_seg; k < sd.first_seg + N; k++) docChars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
   uint64_t textCap = b->text_len + std::max<uint64_t>((loaded ? 256 : 1024) * nOps + 65536, 4 * docChars + 131072);
   if (const char* e = std::getenv("FMT_EMU_TEXTCAP")) textCap = std::strtoull(e, nullptr, 10);
   std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6);
@@ -65,9 +74,10 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   S.leafBlk = ids.data(); S.winIdx = ids.data() + S.idCap;
   std::vector<uint32_t> wu(8ull * S.winCap);
   S.wRec = wu.data(); S.wMask = S.wRec + 4ull * S.winCap; S.wBlk = S.wMask + 2ull * S.winCap; S.wLeaf = S.wBlk + S.winCap;
-  std::vector<uint16_t> text(textCap);
-  std::memcpy(text.data(), b->text, b->text_len * 2);
-  S.text = text.data(); S.textLen = b->text_len; S.textCap = textCap;
+  // the merge area only: the batch text is read in place (runtime.cpp setupHugeDoc)
+  std::vector<uint16_t> text(textCap - b->text_len);
+  S.base = b->text;
+  S.text = text.data() - b->text_len; S.textLen = b->text_len; S.textCap = textCap;
   std::vector<uint32_t> pr(static_cast<size_t>(kPropCap) * kPropWords);
   S.props = pr.data();
   auto lds = std::make_unique<HugeLds>();
@@ -84,6 +94,8 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   in.nPropsOps = b->n_props_ops;
   in.segs = loaded ? b->snapshot_segs + sd.first_seg : &initSeg;
   in.nSegs = N;
+  in.shape = shape.empty() ? nullptr : shape.data();
+  in.segProps = segProps ? 1u : 0u;
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;

@@ -66,7 +66,8 @@ def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=F
     """(header, leaves, chars, props) of document `doc` replayed by the emulated huge engine."""
     from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
 
-    segs = int(batch.snapshots[doc]["n_header"]) if batch.snapshots is not None and batch.snapshots[doc]["loaded"] else 1
+    sd = batch.snapshots[doc] if batch.snapshots is not None else None
+    segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 1
     nops = int(batch.doc_op_offsets[doc + 1] - batch.doc_op_offsets[doc])
     cap_leaves = cap_leaves or segs + 3 * nops + 8
     cap_chars = cap_chars or len(batch.text) + 8

@@ -23,7 +23,8 @@ def _oracle(orc, batch, doc=0):
     orc.set_index(True)
     try:
         sub = _one_doc(batch, doc)
-        segs = int(sub.snapshots[0]["n_header"]) if sub.snapshots is not None and sub.snapshots[0]["loaded"] else 0
+        sd = sub.snapshots[0] if sub.snapshots is not None else None
+        segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 0
         nops = len(sub.ops)
         rc, h, lv, ch, pr, *_ = orc.mt_replay_timed(sub, 0, 0, cap_leaves=segs + 3 * nops + 4096,
                                                     cap_chars=len(sub.text) + 8, cap_props=4096)
@@ -156,3 +157,67 @@ def test_huge_loaded_markers(orc, engine):
     assert rc == 0
     leaves, chars, props = engine.mt_doc(0, hdrs[0])
     assert compare_doc(exp, (hdrs[0], leaves, chars, props)) == []
+
+
+def test_unsupported_huge_document_fails_alone(orc, engine):
+    """A summary-loaded document past the large tier that asks for something the huge tier does not
+    record (here remove-order recording) fails alone, with FMT_E_UNSUPPORTED in its own header: the
+    ordinary and huge documents beside it replay as in a batch without it."""
+    from fluidframework_amd.streams import MT_F_RMORDER
+    farm = workloads.conflict_farm(24, n_clients=8, ops_per_doc=600, seed=8)
+    t3a = workloads.t3_stream(3000, 4000, n_clients=31, max_lag=700, seed=9)
+    bad = workloads.t3_stream(9000, 6000, n_clients=63, max_lag=4096, max_range=20, seed=10)
+    bad.ops["flags"][bad.ops["type"] == 1] |= MT_F_RMORDER
+    batch = _concat([farm, t3a, bad, farm])
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers(raise_on_failed_docs=False)
+    bad_doc = farm.n_docs + 1
+    assert int(hdrs[bad_doc]["status"]) == native.FMT_E_UNSUPPORTED
+    for d in range(batch.n_docs):
+        if d == bad_doc:
+            continue
+        assert int(hdrs[d]["status"]) == 0, d
+        rc, exp = _oracle(orc, _strip_rmorder(batch), d)
+        assert rc == 0
+        lv, ch, pr = engine.mt_doc(d, hdrs[d])
+        assert compare_doc(exp, (hdrs[d], lv, ch, pr)) == [], d
+
+
+def _strip_rmorder(batch):
+    from fluidframework_amd.streams import MT_F_RMORDER
+    b = copy.copy(batch)
+    b.ops = batch.ops.copy()
+    b.ops["flags"] &= ~np.uint32(MT_F_RMORDER)
+    return b
+
+
+@pytest.mark.parametrize("segs,ops,props_every,seed", [
+    (30000, 20000, 0, 21),
+    (1_000_000, 100_000, 5, 22),
+])
+def test_huge_legacy_header_and_body_on_gpu(orc, engine, segs, ops, props_every, seed):
+    """T3 from a summary in SnapshotLegacy.emit's shape (header chunk ~10,000 units, body chunk
+    appended by loadBody) with props on some segment specs == oracle on the GPU."""
+    batch = workloads.as_legacy_load(workloads.t3_stream(segs, ops, n_clients=63, max_lag=4096, seed=seed),
+                                     props_every=props_every)
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+
+
+def test_huge_zamboni_empties_the_root_on_gpu(orc, engine):
+    batch = workloads.emptying_stream(3000, 600, seed=4)
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []

@@ -10,7 +10,7 @@ from mt_compare import compare_doc, emu_huge_replay
 def _oracle_doc(orc, batch):
     orc.set_index(True)
     try:
-        segs = int(batch.snapshots[0]["n_header"])
+        segs = int(batch.snapshots[0]["n_header"]) + int(batch.snapshots[0]["n_body"])
         nops = len(batch.ops)
         rc, h, lv, ch, pr, *_ = orc.mt_replay_timed(batch, 0, 0, cap_leaves=segs + 3 * nops + 8,
                                                     cap_chars=len(batch.text) + 8, cap_props=4096)
@@ -109,3 +109,53 @@ def test_huge_engine_merge_area_compaction(orc, monkeypatch, capfd):
     assert int(re.search(r"compactions (\d+)", capfd.readouterr().err).group(1)) >= 1
     assert int(got[0]["status"]) == 0
     assert compare_doc(exp, got) == []
+
+
+@pytest.mark.parametrize("segs,ops,props_every,tiny,seed", [
+    (3000, 4000, 0, False, 11),
+    (6000, 8000, 3, True, 12),
+    (20000, 6000, 7, False, 13),
+])
+def test_huge_engine_legacy_header_and_body(orc, segs, ops, props_every, tiny, seed):
+    """A summary in SnapshotLegacy.emit's shape — a header chunk of ~10,000 units, the rest in the
+    body chunk appended by loadBody (snapshotLoader.ts:277-309) — with props on some segment specs:
+    the tree the appends build (4 / 4 splits up the right edge) and every replayed op == oracle."""
+    batch = workloads.as_legacy_load(workloads.t3_stream(segs, ops, n_clients=16, max_lag=300, max_range=8, seed=seed),
+                                     props_every=props_every)
+    assert int(batch.snapshots[0]["n_body"]) > 0
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=tiny)
+    assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+    assert compare_doc(exp, got) == []
+
+
+def test_huge_engine_body_only_load_and_shape(orc):
+    """The loaded tree alone (no ops) for header+body splits at several sizes, including an empty
+    header (the body's first append makes the empty root the leaf block): block ordinals and depth."""
+    import dataclasses
+
+    import numpy as np
+    base = workloads.t3_stream(5000, 1, n_clients=2, max_lag=1, seed=3)
+    for n_header in (0, 1, 7, 8, 49, 50, 343, 344, 2222):
+        snaps = base.snapshots.copy()
+        snaps["n_header"], snaps["n_body"] = n_header, 5000 - n_header
+        batch = dataclasses.replace(base, snapshots=snaps, ops=base.ops[:0],
+                                    doc_op_offsets=np.array([0, 0], dtype=np.uint64))
+        rc, exp = _oracle_doc(orc, batch)
+        assert rc == 0
+        got = emu_huge_replay(batch)
+        assert int(got[0]["status"]) == 0
+        assert compare_doc(exp, got) == [], n_header
+
+
+def test_huge_engine_zamboni_empties_the_root(orc):
+    """Zamboni scours every block of a document one remove emptied; packParent leaves the root
+    childless (zamboni.ts:129-132) and the next insert makes it the leaf block again."""
+    batch = workloads.emptying_stream(3000, 600, seed=4)
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    for tiny in (False, True):
+        got = emu_huge_replay(batch, tiny_groups=tiny)
+        assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+        assert compare_doc(exp, got) == []
