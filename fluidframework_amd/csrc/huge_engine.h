@@ -156,6 +156,7 @@ struct HugeState {
   uint64_t textLen;   // batch text (read-only part)
   uint64_t textCap;   // end of the merge area: two halves of (textCap - textLen) / 2 units, one in use
   uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
+  uint32_t* cuIds;    // [idCap]: the current catch-up op's delta leaves in document order (or nullptr)
 };
 
 // LDS state of the wave.
@@ -204,6 +205,9 @@ struct HugeInputs {
   // replay harness inserts it locally before collaborating, client.replay.spec.ts:30-33)
   int32_t initClient;
   uint32_t segProps;  // some loaded segment has properties
+  // catch-up ranges of FMT_MT_F_CATCHUP ops (the document's slab; nullptr: the batch records none)
+  fmt_mt_catchup_range* catchup;
+  uint32_t catchupCap;
 };
 
 // The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
@@ -277,7 +281,10 @@ class HugeDoc {
   uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
   int obLive = 0, obSeqN = 0, obStartN = 0;
   uint64_t mergeLo = 0, mergeHi = 0;  // the merge-area half in use
-  bool textFull = false;              // a scour plan's runs did not fit the merge area's half  // live obliterates: slots in use, seqOrdered / startOrdered lengths
+  bool textFull = false;              // a scour plan's runs did not fit the merge area's half
+  // catch-up recording (FMT_MT_F_CATCHUP ops): ranges written, the op's delta leaves, its index
+  uint32_t cuN = 0, cuIdN = 0, opIdx = 0;
+  bool cuRec = false;
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
@@ -1582,6 +1589,12 @@ class HugeDoc {
     if (obStartN > 0) obliterateOnInsert(x.id, r, c);
     if (status != FMT_OK) return;
     lru(nb != kNone && k >= kMaxNodes / 2 ? nb : b, x.id, op.seq);
+    if (cuRec) {  // the new segment, unless obliterated on arrival (mergeTree.ts:1497-1508)
+      uint32_t xb;
+      int xk;
+      locate(x.id, &xb, &xk);
+      if (ldi(S.lRm + li(xb, xk)) == kNotRemoved) cuPush(x.id);
+    }
   }
 
   // View lengths of the leaves of block b (lane k = leaf k) from PriorPerspective(r, c).
@@ -1704,8 +1717,12 @@ class HugeDoc {
           x.id = readlane(f[5], k);
           x.text = readlane(f[6], k);
           x.meta = readlane(f[7], k);
-          if (op.type == FMT_MT_REMOVE) stableDelta += removeLeaf(b, k, x, seq, c, readlane(wi, k), g);
-          else annotateLeaf(b, k, x, op.payload);
+          if (op.type == FMT_MT_REMOVE) {
+            stableDelta += removeLeaf(b, k, x, seq, c, readlane(wi, k), g);
+          } else {
+            annotateLeaf(b, k, x, op.payload);
+            if (cuRec && x.rm == kNotRemoved) cuPush(x.id);  // deltaSegments: annotated, not removed (:2045-2047)
+          }
           if (status != FMT_OK) return;
           if (!scour && seq > curSeq) {  // addToLRUSet (mergeTree.ts:812-822), once per block
             st1(S.bScour + b, 1);
@@ -1727,7 +1744,10 @@ class HugeDoc {
   // Remove leaf (b, j) (window entry w, block group g); returns the change of b's stable sum.
   FMT_DEV int removeLeaf(uint32_t b, int j, Leaf& x, int seq, int c, uint32_t w, uint32_t g) {
     const bool was = x.rm != kNotRemoved;
-    if (!was) x.rm = seq;
+    if (!was) {
+      x.rm = seq;
+      if (cuRec) cuPush(x.id);  // removedSegments: hits not removed before this op (mergeTree.ts:2314-2321)
+    }
     if (c < 32) x.mlo |= 1u << c;
     else x.mhi |= 1u << (c - 32);
     putLeaf(b, j, x);
@@ -2065,6 +2085,112 @@ class HugeDoc {
       return;
     }
     obAdd(sId, sOff, eId, eOff, seq, c);
+  }
+
+  // ------------------------------------------------------------------ catch-up ranges
+  // The delta event of an FMT_MT_F_CATCHUP op regenerated as position ranges (sequence.ts:395-452),
+  // positions in the local view right after the op, before its zamboni pass (Client.getPosition):
+  // INSERT [pos, pos + len) of the new leaf; REMOVE / OBLITERATE the newly removed leaves, merged
+  // while they start at the same position; ANNOTATE the annotated leaves not removed, merged while
+  // contiguous. The local view counts every leaf not removed: perspective (kLocalSeq, any client).
+  static constexpr int kLocalSeq = 0x7FFFFFFE;
+  FMT_DEV void cuPush(uint32_t id) {
+    if (cuIdN >= S.idCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    st1(S.cuIds + cuIdN, id);
+    cuIdN++;
+  }
+  FMT_DEV void cuEmit(int p1, int p2, int type) {
+    if (cuN >= in.catchupCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    FOR_LANES(l) {
+      if (l == 0) {
+        fmt_mt_catchup_range r;
+        r.op = opIdx;
+        r.pos1 = p1;
+        r.pos2 = p2;
+        r.type = static_cast<uint32_t>(type);
+        in.catchup[cuN] = r;
+      }
+    }
+    cuN++;
+  }
+  FMT_DEV void recordCatchup(int type) {
+    if (cuIdN == 0) return;
+    waveSync();
+    invalidate();
+    groupCorrections(kLocalSeq, 0);
+    uint32_t b;
+    int k0;
+    locate(ldu(S.cuIds), &b, &k0);
+    if (k0 < 0) {
+      fail(FMT_E_DATA);
+      return;
+    }
+    // local start of block b: the groups before its group, then the slots before its slot
+    const uint32_t g = ldu(S.bGroup + b), s = ldu(S.bSlot + b);
+    const int gp = groupPos(g);
+    int base = 0;
+    for (int k = 0; k < gp; k += 64) {
+      const Lane<uint32_t> len = groupLens(k);
+      Lane<uint32_t> part;
+      FOR_LANES(l) { LANE(part) = k + l < gp ? LANE(len) : 0u; }
+      uint32_t tot;
+      waveExclusiveSum(part, &tot);
+      base += static_cast<int>(tot);
+    }
+    slotLengths(g, kLocalSeq, 0);
+    for (uint32_t q = 0; q < s; q += 64) {
+      Lane<uint32_t> part;
+      FOR_LANES(l) { LANE(part) = q + l < s ? static_cast<uint32_t>(L->sLen[q + l]) : 0u; }
+      uint32_t tot;
+      waveExclusiveSum(part, &tot);
+      base += static_cast<int>(tot);
+    }
+    int p1 = 0, p2 = 0;
+    bool open = false;
+    uint32_t q = 0;
+    while (q < cuIdN) {
+      if (b == kNone) {
+        fail(FMT_E_DATA);
+        return;
+      }
+      const int cnt = static_cast<int>(ldu(S.bCount + b));
+      Lane<uint32_t> loc, ids;
+      FOR_LANES(l) {
+        const size_t i = li(b, l < cnt ? l : 0);
+        LANE(ids) = l < cnt ? rd(S.lId + i) : 0u;
+        LANE(loc) = l < cnt && rd(S.lRm + i) == kNotRemoved ? rd(S.lLen + i) : 0u;
+      }
+      uint32_t tot;
+      const Lane<uint32_t> ex = waveExclusiveSum(loc, &tot);
+      for (; q < cuIdN; q++) {
+        const uint32_t id = ldu(S.cuIds + q);
+        Lane<bool> hit;
+        FOR_LANES(l) { LANE(hit) = l < cnt && LANE(ids) == id; }
+        const uint64_t m = ballot(hit);
+        if (m == 0) break;
+        const int lane = ctz64(m);
+        const int pos = base + static_cast<int>(readlane(ex, lane));
+        const int len = static_cast<int>(ldu(S.lLen + li(b, lane)));
+        if (open && (((type == FMT_MT_REMOVE || type == FMT_MT_OBLITERATE) && p1 == pos) || (type == FMT_MT_ANNOTATE && p2 == pos))) {
+          p2 += len;
+          continue;
+        }
+        if (open) cuEmit(p1, p2, type);
+        p1 = pos;
+        p2 = pos + len;
+        open = true;
+      }
+      base += static_cast<int>(tot);
+      if (q < cuIdN) b = nextBlockOf(b);
+    }
+    if (open) cuEmit(p1, p2, type);
+    invalidate();
   }
 
   // ------------------------------------------------------------------ minSeq
@@ -2987,6 +3113,9 @@ class HugeDoc {
 #ifdef FMT_HUGE_CHECK
       checkPerspective(op.seq, op.ref_seq, op.client);
 #endif
+      cuRec = (op.flags & FMT_MT_F_CATCHUP) != 0 && in.catchup != nullptr && S.cuIds != nullptr;
+      cuIdN = 0;
+      opIdx = static_cast<uint32_t>(i - in.begin);
       if (op.client > 63) fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_INSERT) insertText(op);
       else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
@@ -2997,7 +3126,9 @@ class HugeDoc {
       } else {
         fail(FMT_E_UNSUPPORTED);
       }
-      if ((op.flags & (FMT_MT_F_CATCHUP | FMT_MT_F_RMORDER)) != 0) fail(FMT_E_UNSUPPORTED);
+      if ((op.flags & FMT_MT_F_RMORDER) != 0 || ((op.flags & FMT_MT_F_CATCHUP) != 0 && !cuRec)) fail(FMT_E_UNSUPPORTED);
+      if (cuRec && status == FMT_OK) recordCatchup(op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
+      cuRec = false;
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       for (int z = 0; z < 2 && status == FMT_OK; z++) {
         if (z == 1) {
@@ -3199,7 +3330,7 @@ class HugeDoc {
         h.n_blocks = nBlocks;
         h.depth = static_cast<uint32_t>(d);
         h.visible_len = static_cast<uint32_t>(visible);
-        h.n_catchup = 0;
+        h.n_catchup = cuN;
         h.n_rm_order = 0;
         *hdr = h;
       }
@@ -3216,6 +3347,8 @@ class HugeDoc {
     in = inputs;
     heapN = 0;
     nWin = 0;
+    cuN = cuIdN = 0;
+    cuRec = false;
     nFree = 0;
     nProps = 0;
     textTop = S.textLen;

@@ -22,8 +22,10 @@ extern "C" {
 // output arrays (fmt_mt_fetch_doc layout). Returns the document status.
 // A document that does not start from a summary starts from its initial text (one segment stamped
 // {0, FMT_LOCAL_CLIENT}) or empty, as the runtime replays documents that outgrow the large tier.
-int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
-                    uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
+// With catchup != nullptr the catch-up ranges of FMT_MT_F_CATCHUP ops go there (capCatchup ranges).
+int emu_huge_replay_cu(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+                       uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, fmt_mt_catchup_range* catchup,
+                       uint32_t capCatchup) {
   const bool loaded = b->snapshots != nullptr && b->snapshots[d].loaded;
   fmt_mt_snapshot_doc sd{};
   fmt_mt_snapshot_seg initSeg{};
@@ -80,6 +82,8 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   S.text = text.data() - b->text_len; S.textLen = b->text_len; S.textCap = textCap;
   std::vector<uint32_t> pr(static_cast<size_t>(kPropCap) * kPropWords);
   S.props = pr.data();
+  std::vector<uint32_t> cuIds(catchup != nullptr ? S.idCap : 0);
+  S.cuIds = catchup != nullptr ? cuIds.data() : nullptr;
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));
   auto doc = std::make_unique<HugeDoc>();
@@ -96,6 +100,8 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
   in.nSegs = N;
   in.shape = shape.empty() ? nullptr : shape.data();
   in.segProps = segProps ? 1u : 0u;
+  in.catchup = catchup;
+  in.catchupCap = capCatchup;
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
@@ -105,6 +111,11 @@ int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, f
     std::fprintf(stderr, "textTop %llu of %llu, compactions %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap,
                  (unsigned long long)doc->prof[22]);
   return hdr->status;
+}
+
+int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+                    uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
+  return emu_huge_replay_cu(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0);
 }
 
 }  // extern "C"

@@ -221,3 +221,45 @@ def test_huge_zamboni_empties_the_root_on_gpu(orc, engine):
     assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
     lv, ch, pr = engine.mt_doc(0, hdrs[0])
     assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+
+
+def test_huge_legacy_summary_with_catchup_on_gpu(orc, engine):
+    """The whole legacy summary of a huge document loaded from a SnapshotLegacy-shaped summary —
+    header and body blobs at its minSeq plus the catchupOps blob regenerated from the catch-up
+    ranges the huge engine records (sequence.ts:949-1018, snapshotlegacy.ts:126-193) — equals the
+    one built from the oracle's state and ranges."""
+    from fluidframework_amd import summary
+    from fluidframework_amd.streams import MT_F_CATCHUP, flag_catchup, op_messages
+    from fluidframework_amd.summary import legacy_summary
+    batch = workloads.as_legacy_load(workloads.t3_stream(60000, 30000, n_clients=63, max_lag=4096, max_range=40, seed=27),
+                                     props_every=6)
+    flag_catchup(batch.ops, batch.doc_op_offsets)
+    n_flag = int(((batch.ops["flags"] & MT_F_CATCHUP) != 0).sum())
+    assert n_flag > 1000
+    cap = 16 * n_flag + 16
+    n_segs = int(batch.snapshots[0]["n_header"]) + int(batch.snapshots[0]["n_body"])
+    orc.set_index(True)
+    try:
+        rc, oh, olv, och, opr, _, ocu = orc.mt_replay_batch(batch, cap_leaves=n_segs + 3 * len(batch.ops) + 8,
+                                                           cap_chars=len(batch.text) + 8, cap_props=4096, cap_catchup=cap)
+    finally:
+        orc.set_index(False)
+    assert rc == 0
+    h = oh[0]
+    exp = (h, olv[0][: int(h["n_leaves"])], och[0][: int(h["n_chars"])], opr[0][: int(h["n_props"])])
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+    cu = engine.mt_catchup(0, hdrs[0])
+    assert np.array_equal(cu, ocu[0][: int(h["n_catchup"])])
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    names = [f"client-{k}" for k in range(64)]
+    msgs = op_messages(batch, 0, int(h["min_seq"]), names)
+    got = (*engine.mt_summary(0), summary.catchup_blob(summary.catchup_messages(msgs, cu, int(hdrs[0]["min_seq"]))))
+    want = (*legacy_summary(*exp, batch.keys, batch.values),
+            summary.catchup_blob(summary.catchup_messages(msgs, ocu[0][: int(h["n_catchup"])], int(h["min_seq"]))))
+    assert got == want
+    assert got[1] is not None and got[2] is not None

@@ -159,3 +159,37 @@ def test_huge_engine_zamboni_empties_the_root(orc):
         got = emu_huge_replay(batch, tiny_groups=tiny)
         assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
         assert compare_doc(exp, got) == []
+
+
+@pytest.mark.parametrize("segs,ops,rng,tiny,seed,legacy", [
+    (3000, 6000, 8, True, 31, False),
+    (8000, 8000, 200, False, 32, True),
+])
+def test_huge_engine_catchup_ranges(orc, segs, ops, rng, tiny, seed, legacy):
+    """Catch-up ranges (sequence.ts:395-452) of the ops a legacy summary keeps (seq above the final
+    minSeq, refSeq != seq - 1: streams.flag_catchup), recorded by the huge engine == oracle."""
+    import numpy as np
+
+    from fluidframework_amd.streams import MT_F_CATCHUP, flag_catchup
+    batch = workloads.t3_stream(segs, ops, n_clients=31, max_lag=1500, max_range=rng, seed=seed)
+    if legacy:
+        batch = workloads.as_legacy_load(batch, props_every=4)
+    flag_catchup(batch.ops, batch.doc_op_offsets)
+    n_flag = int(((batch.ops["flags"] & MT_F_CATCHUP) != 0).sum())
+    assert n_flag > 100
+    cap = 16 * n_flag + 16
+    n_segs = int(batch.snapshots[0]["n_header"]) + int(batch.snapshots[0]["n_body"])
+    orc.set_index(True)
+    try:
+        rc, oh, olv, och, opr, _, ocu = orc.mt_replay_batch(batch, cap_leaves=n_segs + 3 * ops + 8, cap_chars=len(batch.text) + 8,
+                                                           cap_props=4096, cap_catchup=cap)
+    finally:
+        orc.set_index(False)
+    assert rc == 0
+    h = oh[0]
+    exp = (h, olv[0][: int(h["n_leaves"])], och[0][: int(h["n_chars"])], opr[0][: int(h["n_props"])])
+    *got, cu = emu_huge_replay(batch, tiny_groups=tiny, cap_catchup=cap)
+    assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+    assert compare_doc(exp, tuple(got)) == []
+    assert int(h["n_catchup"]) > n_flag // 2
+    assert np.array_equal(cu, ocu[0][: int(h["n_catchup"])])
