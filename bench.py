@@ -246,7 +246,7 @@ def main():
         blobs = []
         for d in range(min(args.gather_docs, docs)):
             lv, ch, pr = eng.mt_doc(d, hdrs[d])
-            head, body = legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values)
+            head, body = legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.doc_values(d))
             blobs.append(head.encode("utf-8", "surrogatepass") + b"\0" + (body or "").encode("utf-8", "surrogatepass"))
         build_s = time.perf_counter() - t
         t = time.perf_counter()
@@ -269,7 +269,7 @@ def main():
         checked = 0
         for d in range(0, docs, max(1, docs // 16)):
             lv, ch, pr = eng.mt_doc(d, hdrs[d])
-            if eng.mt_summary(d) != legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.values):
+            if eng.mt_summary(d) != legacy_summary(hdrs[d], lv, ch, pr, batch.keys, batch.doc_values(d)):
                 raise SystemExit(f"bulk summary of document {d} differs from the Python host's")
             checked += 1
         summaries = {"docs": docs, "summaries_per_s": docs / (total_ms / 1e3), **tm, "total_ms": total_ms,

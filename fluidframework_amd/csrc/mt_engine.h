@@ -210,6 +210,11 @@ struct AdjustTables {
   const uint32_t* numSortedId;
   uint32_t nNumSorted;
   uint32_t pad;
+  // document-local value ids (fmt_mt_batch.doc_value_base): per document its value base (nDocs + 1),
+  // and its own host numbers numSorted[numSortedOffs[doc] .. numSortedOffs[doc + 1]) with local ids;
+  // nullptr: batch-global ids, one sorted list
+  const uint32_t* valueBase;
+  const uint32_t* numSortedOffs;
   double* nums;
   const uint64_t* numOffsets;  // nDocs + 1
   uint32_t* numCount;          // nDocs
@@ -267,6 +272,10 @@ FMT_DEV double adjNumberOf(const AdjustTables* A, uint32_t doc, uint32_t id) {  
     const uint32_t cnt = uni(loadCoherent(A->numCount + doc));
     return k < cnt ? uniD(loadCoherentD(A->nums + A->numOffsets[doc] + k)) : __builtin_nan("");
   }
+  if (A->valueBase != nullptr) {
+    const uint32_t b0 = uni(A->valueBase[doc]), cnt = uni(A->valueBase[doc + 1]) - b0;
+    return id >= 1 && id <= cnt ? uniD(A->valueNum[b0 + id]) : __builtin_nan("");
+  }
   return id < A->nValues ? uniD(A->valueNum[id]) : __builtin_nan("");
 }
 
@@ -275,8 +284,8 @@ FMT_DEV double adjNumberOf(const AdjustTables* A, uint32_t doc, uint32_t id) {  
 // JSON.stringify writes both as 0).
 FMT_DEV uint32_t adjNumberId(const AdjustTables* A, uint32_t doc, double x) {
   if (x == 0.0) x = 0.0;
-  const int ns = static_cast<int>(uni(A->nNumSorted));
-  int lo = 0, hi = ns;
+  const int ns = static_cast<int>(A->numSortedOffs != nullptr ? uni(A->numSortedOffs[doc + 1]) : uni(A->nNumSorted));
+  int lo = A->numSortedOffs != nullptr ? static_cast<int>(uni(A->numSortedOffs[doc])) : 0, hi = ns;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (uniD(A->numSorted[mid]) < x) lo = mid + 1;

@@ -191,6 +191,8 @@ struct fmt_ctx {
   DevBuf<fmt_mt_adjust> mtAdjusts;
   DevBuf<double> mtValueNum, mtNumSorted, mtNums;
   DevBuf<uint32_t> mtNumSortedId, mtNumCount;
+  DevBuf<uint32_t> mtValueBase, mtNumSortedOffs;  // document-local value ids (doc_value_base)
+  std::vector<uint32_t> mtValueBaseHost;         // empty: batch-global value ids
   DevBuf<uint64_t> mtNumOffs;
   DevBuf<fmt_mt::AdjustTables> mtAdjTab;      // the pointers above, for the kernels
   std::vector<uint64_t> mtNumOffsHost;
@@ -857,6 +859,16 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       }
     }
   }
+  if (b->doc_value_base != nullptr) {
+    for (uint32_t d = 0; d < n; d++)
+      if (b->doc_value_base[d + 1] < b->doc_value_base[d])
+        return setErr(c, FMT_E_USAGE, "doc_value_base is not ascending");
+    if (b->value_num != nullptr && b->doc_value_base[n] >= b->n_values)
+      return setErr(c, FMT_E_USAGE, "doc_value_base reaches past value_num");
+    c->mtValueBaseHost.assign(b->doc_value_base, b->doc_value_base + n + 1);
+  } else {
+    c->mtValueBaseHost.clear();
+  }
   if (anyAdjust) {
     if (b->value_num == nullptr && b->n_values > 0) return setErr(c, FMT_E_USAGE, "adjusts need value_num");
     for (uint32_t t = 0; t < nKvAll; t++) {
@@ -938,16 +950,31 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       c->mtNumOffsHost[d + 1] = c->mtNumOffsHost[d] + (f ? std::min<uint64_t>(64 * f + 64, 0x7FFF) : 0);
       c->mtPmOffsHost[d + 1] = c->mtPmOffsHost[d] + (g ? std::min<uint64_t>(32 * g + 256, 1u << 20) : 0);
     }
-    std::vector<std::pair<double, uint32_t>> nums;
-    for (uint32_t i = 0; b->value_num && i < b->n_values; i++)
-      if (b->value_num[i] == b->value_num[i]) nums.emplace_back(b->value_num[i] == 0.0 ? 0.0 : b->value_num[i], i);
-    std::stable_sort(nums.begin(), nums.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    // the host's numbers, ascending, each with the first value id that holds it: one list for the
+    // batch, or per document with its local ids (doc_value_base)
     std::vector<double> sv;
-    std::vector<uint32_t> si;
-    for (const auto& [x, i] : nums) {
-      if (!sv.empty() && sv.back() == x) continue;  // (one text per number: the first id)
-      sv.push_back(x);
-      si.push_back(i);
+    std::vector<uint32_t> si, so;
+    auto sortNumbers = [&](uint32_t lo, uint32_t hi, uint32_t base) {
+      std::vector<std::pair<double, uint32_t>> nums;
+      for (uint32_t i = lo; b->value_num && i < hi; i++)
+        if (b->value_num[base + i] == b->value_num[base + i])
+          nums.emplace_back(b->value_num[base + i] == 0.0 ? 0.0 : b->value_num[base + i], i);
+      std::stable_sort(nums.begin(), nums.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      const size_t first = sv.size();
+      for (const auto& [x, i] : nums) {
+        if (sv.size() > first && sv.back() == x) continue;  // (one text per number: the first id)
+        sv.push_back(x);
+        si.push_back(i);
+      }
+    };
+    if (b->doc_value_base != nullptr) {
+      so.assign(1, 0);
+      for (uint32_t d = 0; d < n; d++) {
+        sortNumbers(1, b->doc_value_base[d + 1] - b->doc_value_base[d] + 1, b->doc_value_base[d]);
+        so.push_back(static_cast<uint32_t>(sv.size()));
+      }
+    } else {
+      sortNumbers(0, b->n_values, 0);
     }
     c->mtNAdjusts = b->n_adjusts;
     c->mtNValues = b->value_num ? b->n_values : 0u;
@@ -967,6 +994,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtValueNum.p, b->value_num, c->mtNValues * sizeof(double)));
     FMT_HIP(c, cp(c->mtNumSorted.p, sv.data(), sv.size() * sizeof(double)));
     FMT_HIP(c, cp(c->mtNumSortedId.p, si.data(), si.size() * sizeof(uint32_t)));
+    if (b->doc_value_base != nullptr) {
+      FMT_HIP(c, c->mtValueBase.reserve(n + 1ull));
+      FMT_HIP(c, c->mtNumSortedOffs.reserve(n + 1ull));
+      FMT_HIP(c, cp(c->mtValueBase.p, b->doc_value_base, (n + 1ull) * sizeof(uint32_t)));
+      FMT_HIP(c, cp(c->mtNumSortedOffs.p, so.data(), (n + 1ull) * sizeof(uint32_t)));
+    }
     FMT_HIP(c, cp(c->mtNumOffs.p, c->mtNumOffsHost.data(), (n + 1ull) * sizeof(uint64_t)));
     FMT_HIP(c, hipMemsetAsync(c->mtNumCount.p, 0, n * sizeof(uint32_t), c->stream));
     fmt_mt::AdjustTables T{};
@@ -976,6 +1009,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     T.valueNum = c->mtValueNum.p;
     T.numSorted = c->mtNumSorted.p;
     T.numSortedId = c->mtNumSortedId.p;
+    T.valueBase = b->doc_value_base != nullptr ? c->mtValueBase.p : nullptr;
+    T.numSortedOffs = b->doc_value_base != nullptr ? c->mtNumSortedOffs.p : nullptr;
     T.nNumSorted = c->mtNNumSorted;
     T.nums = c->mtNums.p;
     T.numOffsets = c->mtNumOffs.p;
@@ -1408,7 +1443,8 @@ struct SumDict {
 
 // A prop set as a JSON object in JS own-property order: array-index keys ascending, then the
 // others in insertion order (properties' key order, snapshotChunks.ts via JSON.stringify).
-void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D, const std::vector<double>* nums) {
+void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D, const std::vector<double>* nums,
+                 uint32_t valueBase) {
   const uint32_t n = ps.n < FMT_MT_PROPS_MAX ? ps.n : FMT_MT_PROPS_MAX;
   uint32_t order[FMT_MT_PROPS_MAX];
   uint32_t m = 0;
@@ -1427,7 +1463,7 @@ void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D, con
     if (nums != nullptr && v >= FMT_MT_VALUE_COMPUTED)  // an annotate-adjust result
       o += fmt_json::jsNumber((*nums)[v - FMT_MT_VALUE_COMPUTED]);
     else
-      o += D.values[v];
+      o += D.values[valueBase + v];
   }
   o.push_back('}');
 }
@@ -1436,7 +1472,7 @@ void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D, con
 // the header chunk (runs until >= chunk units) and, when runs remain, the body chunk.
 void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* runs, uint32_t nRuns,
                  const uint16_t* text, const fmt_mt_propset* props, int32_t minSeq, uint32_t chunk,
-                 const SumDict& D, const std::vector<double>* nums) {
+                 const SumDict& D, const std::vector<double>* nums, uint32_t valueBase) {
   uint64_t total = 0;
   for (uint32_t i = 0; i < nRuns; i++) total += runs[i].len;
   std::vector<uint64_t> start(nRuns + 1, 0);
@@ -1457,14 +1493,14 @@ void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* r
         out += "{\"marker\":{\"refType\":" + std::to_string(text[start[i]]) + "}";
         if (hasProps) {
           out += ",\"props\":";
-          propsObject(out, props[r.props], D, nums);
+          propsObject(out, props[r.props], D, nums, valueBase);
         }
         out.push_back('}');
       } else if (hasProps) {
         out += "{\"text\":";
         jsonQuote16(out, text + start[i], r.len);
         out += ",\"props\":";
-        propsObject(out, props[r.props], D, nums);
+        propsObject(out, props[r.props], D, nums, valueBase);
         out.push_back('}');
       } else {
         jsonQuote16(out, text + start[i], r.len);
@@ -1627,6 +1663,9 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
           continue;
         }
         const std::vector<double>* nums = c->mtHasAdjust ? &docNums[d] : nullptr;
+        // value id v names values[vBase + v] (document-local ids: v <= vCount)
+        const uint32_t vBase = c->mtValueBaseHost.empty() ? 0u : c->mtValueBaseHost[d];
+        const uint64_t vEnd = c->mtValueBaseHost.empty() ? nValues : std::min<uint64_t>(nValues, c->mtValueBaseHost[d + 1] + 1ull);
         // every prop set a run names, and every key / value id in it, within the tables passed in
         bool bad = false;
         for (uint32_t i = 0; i < o.n_runs && !bad; i++) {
@@ -1640,7 +1679,7 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
           for (uint32_t k = 0; k < ps.n; k++) {
             const uint32_t v = ps.kv[k] & 0xFFFFu;
             const bool computed = nums != nullptr && v >= FMT_MT_VALUE_COMPUTED && v - FMT_MT_VALUE_COMPUTED < nums->size();
-            if ((ps.kv[k] >> 16) >= nKeys || (v >= nValues && !computed)) bad = true;
+            if ((ps.kv[k] >> 16) >= nKeys || (vBase + static_cast<uint64_t>(v) >= vEnd && !computed)) bad = true;
           }
         }
         if (bad) {
@@ -1649,7 +1688,7 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
         }
         c->sumBlobs[d].reserve(o.n_units + 64ull * o.n_runs + 256);
         legacyBlobs(c->sumBlobs[d], &c->sumSplit[d], runs + o.run_off, o.n_runs, text + o.text_off,
-                    propsHost[d], hdr[d].min_seq, chunk ? chunk : 10000u, D, nums);
+                    propsHost[d], hdr[d].min_seq, chunk ? chunk : 10000u, D, nums, vBase);
       }
     });
   for (auto& th : pool) th.join();

@@ -93,6 +93,7 @@ class FmtMtBatch(ctypes.Structure):
         ("n_adjusts", ctypes.c_uint32),
         ("n_values", ctypes.c_uint32),
         ("value_num", ctypes.c_void_p),
+        ("doc_value_base", ctypes.c_void_p),
     ]
 
 
@@ -168,6 +169,11 @@ def batch_struct(batch):
         vn = np.ascontiguousarray(batch.value_num, dtype=np.float64)
         b.adjusts, b.n_adjusts, b.value_num, b.n_values = _ptr(a), len(a), _ptr(vn), len(vn)
         keep += [a, vn]
+    vb = getattr(batch, "value_base", None)
+    if vb is not None:
+        vba = np.ascontiguousarray(vb, dtype=np.uint32)
+        b.doc_value_base = _ptr(vba)
+        keep.append(vba)
     return b, keep
 
 

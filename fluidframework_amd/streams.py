@@ -247,10 +247,20 @@ class MergeTreeBatch:
     # optional (annotate-adjust): ADJUST_DTYPE rows and, per value id, the number its text holds (NaN)
     adjusts: np.ndarray | None = None
     value_num: np.ndarray | None = None
+    # optional (fmt.h doc_value_base): document-local value ids — value id v >= 1 of document d names
+    # values[value_base[d] + v]; None: ids are batch-global
+    value_base: np.ndarray | None = None
 
     @property
     def n_docs(self) -> int:
         return len(self.doc_op_offsets) - 1
+
+    def doc_values(self, d: int):
+        """Document d's value table: its value id → JSON text (the batch's table when ids are global)."""
+        if self.value_base is None:
+            return self.values
+        b0, b1 = int(self.value_base[d]), int(self.value_base[d + 1])
+        return ["null"] + self.values[b0 + 1 : b1 + 1]
 
 
 class _DocBuilder:
@@ -375,6 +385,7 @@ class MergeTreeStreamBuilder:
         self.doc_init: list[tuple] = []
         self.snapshots: list[tuple] = []  # per doc: (first_seg, n_header, n_body, min_seq, seq, loaded)
         self.snapshot_segs: list[tuple] = []
+        self.seg_doc: list[int] = []  # per snapshot segment: its document
         self.relpos: list[tuple] = []  # (marker value id, offset, flags, 0)
         self.snapshot_info: list[tuple] = []  # per snapshot segment: (ins_seq, ins_client, rm_first, rm_count)
         self.snapshot_stamps: list[tuple] = []  # (seq, client, kind, 0)
@@ -451,21 +462,22 @@ class MergeTreeStreamBuilder:
 
     def _props_op(self, props: dict, adjust: dict | None = None) -> int:
         """A props op: the raw (key, value) changes in JS key order, then the adjust changes
-        (segmentPropertiesManager.ts:86-95 opToChanges), each adjust as (key, FMT_MT_VALUE_ADJUST)
-        followed by its row index."""
+        (segmentPropertiesManager.ts:86-95 opToChanges). Held as entries (key, value id) and
+        (key, -1, adjust row) over the builder's batch-wide value dictionary; finish() packs them as
+        (key << 16) | value words, each adjust as (key, FMT_MT_VALUE_ADJUST) followed by its row index,
+        with batch-global or document-local value ids."""
         kv = []
         for k in js_key_order(list(props)):
             v = props[k]
             key_id = self.keys.intern(k)
-            val_id = 0 if v is None else self.values.intern(js_json(v))
-            if key_id > 0xFFFF or val_id >= VALUE_ADJUST:
-                raise UnsupportedOp("props dictionary exceeds 65535 entries")
-            kv.append((key_id << 16) | val_id)
+            if key_id > 0xFFFF:
+                raise UnsupportedOp("more than 65536 distinct property keys in a batch")
+            kv.append((key_id, 0 if v is None else self.values.intern(js_json(v))))
         for k in js_key_order(list(adjust or {})):
             key_id = self.keys.intern(k)
             if key_id > 0xFFFF:
-                raise UnsupportedOp("props dictionary exceeds 65535 entries")
-            kv += [(key_id << 16) | VALUE_ADJUST, self._adjust_row(adjust[k])]
+                raise UnsupportedOp("more than 65536 distinct property keys in a batch")
+            kv.append((key_id, -1, self._adjust_row(adjust[k])))
         t = tuple(kv)
         i = self.props_ops.get(t)
         if i is None:
@@ -578,6 +590,7 @@ class MergeTreeStreamBuilder:
                     d.note_marker_id(spec.get("props"))
                 self.snapshot_segs.append(self._spec(spec))
                 self.snapshot_info.append(info)
+        self.seg_doc.extend([len(self.docs)] * (len(self.snapshot_segs) - first))
         n_header = len(specs(h))
         n_body = len(self.snapshot_segs) - first - n_header
         if n_header + n_body != md["totalSegmentCount"]:
@@ -674,12 +687,21 @@ class MergeTreeStreamBuilder:
         if remove_order:
             flag_remove_order(ops, offs)
         text = np.concatenate(self.text) if self.text else np.zeros(0, dtype="<u2")
-        if self.adjusts and len(self.values.items) > VALUE_COMPUTED:
-            raise UnsupportedOp(f"more than {VALUE_COMPUTED} distinct values in a batch with annotate adjusts")
-        props_off = np.zeros(len(self.props_list) + 1, dtype=np.uint32)
+        segs = np.array(self.snapshot_segs, dtype=SNAPSHOT_SEG_DTYPE)
+        relpos = np.array(self.relpos, dtype=RELPOS_DTYPE) if self.relpos else None
+        # value ids: batch-global while the batch's distinct values fit below the id limit
+        # (FMT_MT_VALUE_COMPUTED with adjusts, else FMT_MT_VALUE_ADJUST), else document-local
+        # (fmt.h doc_value_base): every document gets its own dictionary and props ops
+        limit = VALUE_COMPUTED if self.adjusts else VALUE_ADJUST
+        if len(self.values.items) <= limit:
+            props_list, values, value_base = self.props_list, list(self.values.items), None
+        else:
+            props_list, values, value_base = self._localize_values(ops, offs, segs, relpos, limit)
+        props_off = np.zeros(len(props_list) + 1, dtype=np.uint32)
         kv = []
-        for j, t in enumerate(self.props_list):
-            kv.extend(t)
+        for j, t in enumerate(props_list):
+            for e in t:
+                kv += [(e[0] << 16) | e[1]] if len(e) == 2 else [(e[0] << 16) | VALUE_ADJUST, e[2]]
             props_off[j + 1] = len(kv)
         return MergeTreeBatch(
             ops=ops,
@@ -689,18 +711,70 @@ class MergeTreeStreamBuilder:
             props_off=props_off,
             props_kv=np.asarray(kv, dtype=np.uint32),
             keys=list(self.keys.items),
-            values=list(self.values.items),
+            values=values,
             clients=[list(d.client_names) for d in self.docs],
             messages=[list(d.messages) for d in self.docs] if self.keep_messages else [],
             snapshots=_snapshot_array(self.snapshots),
-            snapshot_segs=np.array(self.snapshot_segs, dtype=SNAPSHOT_SEG_DTYPE),
-            relpos=np.array(self.relpos, dtype=RELPOS_DTYPE) if self.relpos else None,
+            snapshot_segs=segs,
+            relpos=relpos,
             snapshot_info=np.array(self.snapshot_info, dtype=SNAPSHOT_INFO_DTYPE) if self.has_merge_info else None,
             snapshot_stamps=np.array(self.snapshot_stamps, dtype=STAMP_DTYPE) if self.has_merge_info else None,
             marker_id_key=self.keys.ids.get(MARKER_ID_KEY, NO_MARKER) if self.relpos else NO_MARKER,
             adjusts=np.array(self.adjusts, dtype=ADJUST_DTYPE) if self.adjusts else None,
-            value_num=value_numbers(self.values.items) if self.adjusts else None,
+            value_num=value_numbers(values) if self.adjusts else None,
+            value_base=value_base,
         )
+
+    def _localize_values(self, ops, offs, segs, relpos, limit):
+        """Document-local value ids: every props op a document references (annotate payloads, insert
+        props pos2 - 1, its summary segments' props) becomes a props op of that document alone whose
+        values are numbered 1.. in the document's own dictionary, and its relative positions' marker
+        ids follow. Rewrites ops / segs / relpos in place; returns (props ops, values, value_base)."""
+        n_docs = len(offs) - 1
+        doc_of = np.repeat(np.arange(n_docs, dtype=np.int64), np.diff(offs.astype(np.int64)))
+        t = ops["type"]
+        ann = np.nonzero(t == MT_ANNOTATE)[0]
+        ins = np.nonzero((t == MT_INSERT) & (ops["pos2"] > 0))[0]
+        seg_doc = np.asarray(self.seg_doc, dtype=np.int64)
+        sgp = np.nonzero(segs["props"] != NO_PROPS)[0] if len(segs) else np.zeros(0, np.int64)
+        n_p = max(1, len(self.props_list))
+        keys = np.concatenate([doc_of[ann] * n_p + ops["payload"][ann].astype(np.int64),
+                               doc_of[ins] * n_p + (ops["pos2"][ins].astype(np.int64) - 1),
+                               seg_doc[sgp] * n_p + segs["props"][sgp].astype(np.int64)])
+        uniq, inv = np.unique(keys, return_inverse=True)
+        na, ni = len(ann), len(ins)
+        ops["payload"][ann] = inv[:na].astype(np.uint32)
+        ops["pos2"][ins] = (inv[na : na + ni] + 1).astype(np.int32)
+        if len(sgp):
+            segs["props"][sgp] = inv[na + ni :].astype(np.uint32)
+        local: list[dict] = [dict() for _ in range(n_docs)]  # per document: batch value id → local id
+
+        def lid(d, g):
+            m = local[d]
+            v = m.get(g)
+            if v is None:
+                v = m[g] = len(m) + 1
+            return v
+
+        props_list = []
+        for u in uniq.tolist():
+            d, pid = divmod(u, n_p)
+            props_list.append(tuple((e[0], 0 if e[1] == 0 else lid(d, e[1])) if len(e) == 2 else e
+                                    for e in self.props_list[pid]))
+        if relpos is not None:
+            for flag, field in ((MT_F_REL1, "pos1"), (MT_F_REL2, "pos2")):
+                for i in np.nonzero(ops["flags"] & flag)[0].tolist():
+                    row = int(ops[field][i])
+                    if relpos["marker_id"][row] != NO_MARKER:
+                        relpos["marker_id"][row] = lid(int(doc_of[i]), int(relpos["marker_id"][row]))
+        values, base = ["null"], np.zeros(n_docs + 1, dtype=np.uint32)
+        for d in range(n_docs):
+            if len(local[d]) >= limit:
+                raise UnsupportedOp(f"more than {limit - 1} distinct property values in one document")
+            base[d] = len(values) - 1
+            values += [self.values.items[g] for g in local[d]]  # (dicts keep insertion order)
+        base[n_docs] = len(values) - 1
+        return props_list, values, base
 
 
 def _snapshot_array(rows) -> np.ndarray | None:
@@ -735,6 +809,7 @@ def op_messages(batch, d: int, above_seq: int, names) -> list:
     window of a generated document, for the legacy summary's catchupOps blob."""
     a, b = int(batch.doc_op_offsets[d]), int(batch.doc_op_offsets[d + 1])
     recs = batch.ops[a:b]
+    vals = batch.doc_values(d) if hasattr(batch, "doc_values") else batch.values
     out = []
     for k in np.nonzero(recs["seq"] > above_seq)[0]:
         r = recs[int(k)]
@@ -749,7 +824,7 @@ def op_messages(batch, d: int, above_seq: int, names) -> list:
             pid = int(r["payload"])
             kv = batch.props_kv[int(batch.props_off[pid]) : int(batch.props_off[pid + 1])]
             op = {"pos1": int(r["pos1"]), "pos2": int(r["pos2"]),
-                  "props": {batch.keys[int(x) >> 16]: json.loads(batch.values[int(x) & 0xFFFF]) for x in kv}, "type": t}
+                  "props": {batch.keys[int(x) >> 16]: json.loads(vals[int(x) & 0xFFFF]) for x in kv}, "type": t}
         else:
             op = {"pos1": int(r["pos1"]), "pos2": int(r["pos2"]), "type": t}
         out.append(({"clientId": names[int(r["client"])], "sequenceNumber": int(r["seq"]),

@@ -261,6 +261,14 @@ typedef struct fmt_mt_batch {
   uint32_t n_values;              /* entries of value_num */
   const double* value_num;        /* with adjusts: per value id, the number its JSON text parses to, NaN
                                      for a non-number (typeof !== "number") */
+  const uint32_t* doc_value_base; /* optional: n_docs + 1 entries, or NULL. Non-NULL: value ids are
+                                     document-local — value id v >= 1 of document d's props ops and
+                                     relative positions names the batch's value v + doc_value_base[d]
+                                     (value_num, fmt_mt_summarize_legacy's values), and
+                                     v <= doc_value_base[d + 1] - doc_value_base[d]. A batch then holds
+                                     any number of distinct values, each document below the id limits
+                                     (FMT_MT_VALUE_COMPUTED with adjusts, else FMT_MT_VALUE_ADJUST). NULL:
+                                     value ids are batch-global. Id 0 is null either way. */
 } fmt_mt_batch;
 
 /* ---------------------------------------------------------------------------------------------

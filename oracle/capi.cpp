@@ -264,6 +264,21 @@ void startDoc(MergeTree& mt, const fmt_mt_batch* b, uint32_t d,
     mt.valueNum = b->value_num;
     mt.nValues = b->value_num ? b->n_values : 0u;
     mt.hostNumbers = hostNums;
+    if (b->doc_value_base != nullptr && b->value_num != nullptr) {
+      // document-local value ids (fmt.h doc_value_base): id v names value v + base; the host numbers
+      // are this document's own, with local ids
+      const uint32_t base = b->doc_value_base[d], cnt = b->doc_value_base[d + 1] - base;
+      mt.valueNum = b->value_num + base;
+      mt.nValues = cnt + 1;
+      std::vector<std::pair<double, uint32_t>> v;
+      for (uint32_t i = 1; i <= cnt; i++)
+        if (!std::isnan(mt.valueNum[i])) v.emplace_back(mt.valueNum[i] == 0 ? 0.0 : mt.valueNum[i], i);
+      std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      mt.docNumbers.clear();
+      for (const auto& e : v)
+        if (mt.docNumbers.empty() || mt.docNumbers.back().first != e.first) mt.docNumbers.push_back(e);
+      mt.hostNumbers = &mt.docNumbers;
+    }
   }
   mt.snapInfo = b->snapshot_info;
   mt.snapStamps = b->snapshot_stamps;

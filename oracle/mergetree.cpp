@@ -641,7 +641,7 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
 // max compares as 0 and is assigned: null), else `adjusted < min`. Returns the result's value id.
 double MergeTree::numberOfValue(uint16_t id) const {
   if (id >= FMT_MT_VALUE_COMPUTED) return numbers.at(id - FMT_MT_VALUE_COMPUTED);
-  return valueNum != nullptr && id < nValues ? valueNum[id] : std::nan("");
+  return valueNum != nullptr && id != 0 && id < nValues ? valueNum[id] : std::nan("");  // (0: null)
 }
 
 // A number's value id: the host's id of a === number, else this document's computed entry (new

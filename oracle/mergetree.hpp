@@ -247,6 +247,7 @@ class MergeTree {
   const double* valueNum = nullptr;
   uint32_t nValues = 0;
   const std::vector<std::pair<double, uint32_t>>* hostNumbers = nullptr;  // sorted by number
+  std::vector<std::pair<double, uint32_t>> docNumbers;  // hostNumbers' storage with document-local value ids
   std::vector<double> numbers;
   // One change of an annotate op, in opToChanges order (segmentPropertiesManager.ts:86-95): a raw
   // value id (0 = null), or an adjust row (adjust >= 0).

@@ -22,20 +22,37 @@ static std::vector<uint64_t> g_pmOffs;
 static std::vector<uint16_t> g_legacy;
 static size_t g_legacyStride = 0;
 
+static std::vector<uint32_t> g_numSortedOffs;
+
 static void prepareNumbers(const fmt_mt_batch* b) {
   g_numSorted.clear();
   g_numSortedId.clear();
+  g_numSortedOffs.clear();
   g_nums.clear();
   g_numCount.assign(b->n_docs, 0u);
   if (b->adjusts == nullptr || b->value_num == nullptr) return;
-  std::vector<std::pair<double, uint32_t>> v;
-  for (uint32_t i = 0; i < b->n_values; i++)
-    if (b->value_num[i] == b->value_num[i]) v.emplace_back(b->value_num[i] == 0.0 ? 0.0 : b->value_num[i], i);
-  std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-  for (const auto& [x, i] : v) {
-    if (!g_numSorted.empty() && g_numSorted.back() == x) continue;  // the first id of an equal number
-    g_numSorted.push_back(x);
-    g_numSortedId.push_back(i);
+  // the host numbers ascending with their first value id (runtime.cpp fmt_mt_load): one list, or per
+  // document with local ids when value ids are document-local (doc_value_base)
+  auto sortNumbers = [&](uint32_t lo, uint32_t hi, uint32_t base) {
+    std::vector<std::pair<double, uint32_t>> v;
+    for (uint32_t i = lo; i < hi; i++)
+      if (b->value_num[base + i] == b->value_num[base + i]) v.emplace_back(b->value_num[base + i] == 0.0 ? 0.0 : b->value_num[base + i], i);
+    std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    const size_t first = g_numSorted.size();
+    for (const auto& [x, i] : v) {
+      if (g_numSorted.size() > first && g_numSorted.back() == x) continue;  // the first id of an equal number
+      g_numSorted.push_back(x);
+      g_numSortedId.push_back(i);
+    }
+  };
+  if (b->doc_value_base != nullptr) {
+    g_numSortedOffs.assign(1, 0u);
+    for (uint32_t d = 0; d < b->n_docs; d++) {
+      sortNumbers(1, b->doc_value_base[d + 1] - b->doc_value_base[d] + 1, b->doc_value_base[d]);
+      g_numSortedOffs.push_back(static_cast<uint32_t>(g_numSorted.size()));
+    }
+  } else {
+    sortNumbers(0, b->n_values, 0);
   }
   g_nums.assign(static_cast<size_t>(b->n_docs) * kEmuNumCap, 0.0);
   g_numOffs.resize(b->n_docs + 1ull);
@@ -43,9 +60,21 @@ static void prepareNumbers(const fmt_mt_batch* b) {
   g_pm.assign(static_cast<size_t>(b->n_docs) * kEmuPmCap * 4, 0u);
   g_pmOffs.resize(b->n_docs + 1ull);
   for (uint32_t d = 0; d <= b->n_docs; d++) g_pmOffs[d] = static_cast<uint64_t>(d) * kEmuPmCap;
-  g_adj = fmt_mt::AdjustTables{b->adjusts, b->n_adjusts, b->value_num ? b->n_values : 0u, b->value_num,
-                               g_numSorted.data(), g_numSortedId.data(), static_cast<uint32_t>(g_numSorted.size()), 0,
-                               g_nums.data(), g_numOffs.data(), g_numCount.data(), g_pm.data(), g_pmOffs.data()};
+  g_adj = fmt_mt::AdjustTables{};
+  g_adj.adjusts = b->adjusts;
+  g_adj.nAdjusts = b->n_adjusts;
+  g_adj.nValues = b->value_num ? b->n_values : 0u;
+  g_adj.valueNum = b->value_num;
+  g_adj.numSorted = g_numSorted.data();
+  g_adj.numSortedId = g_numSortedId.data();
+  g_adj.nNumSorted = static_cast<uint32_t>(g_numSorted.size());
+  g_adj.valueBase = b->doc_value_base;
+  g_adj.numSortedOffs = b->doc_value_base != nullptr ? g_numSortedOffs.data() : nullptr;
+  g_adj.nums = g_nums.data();
+  g_adj.numOffsets = g_numOffs.data();
+  g_adj.numCount = g_numCount.data();
+  g_adj.pm = g_pm.data();
+  g_adj.pmOffsets = g_pmOffs.data();
 }
 
 // ckpt (plain batches): per-document tier checkpoints; the compact tier saves, the small tier resumes

@@ -769,3 +769,25 @@ def test_mt_bulk_legacy_summaries_with_adjusts(orc, engine):
     engine.mt_summarize_legacy(batch.keys, batch.values)
     for d, (_, _, want) in enumerate(cases):
         assert json.loads(engine.mt_summary(d)[0])["segmentTexts"] == want, d
+
+
+@pytest.mark.parametrize("adjust", [False, True])
+def test_mt_document_local_value_ids_on_gpu(orc, engine, adjust):
+    """A batch whose documents hold more distinct property values than batch-global 16-bit ids name
+    (each Marker's own markerId; fmt.h doc_value_base): the engine's state == oracle for every
+    document, and the runtime's legacy summaries (values looked up per document) == the oracle's."""
+    from marker_docs import marker_batch
+
+    batch = marker_batch(200, 1200, seed=3) if not adjust else marker_batch(120, 900, seed=5, adjust=True)
+    assert batch.value_base is not None
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert (hdrs["status"] == 0).all()
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    assert rc == 0
+    for d in range(0, batch.n_docs, 7):
+        lv, ch, pr = engine.mt_doc(d, hdrs[d])
+        assert compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], lv, ch, pr)) == [], d
+        assert engine.mt_summary(d) == orc.mt_replay_summary(batch, d, batch.keys, batch.doc_values(d)), d
