@@ -257,6 +257,7 @@ class MergeTreeStreamBuilder {
 		this.docInit = [];
 		this.snapshots = []; // per doc: null or [firstSeg, nHeader, nBody, minSeq, seq]
 		this.snapshotSegs = []; // [textOff, len, propsOp]
+		this.segDoc = []; // per snapshot segment: its document
 		this.relpos = []; // [marker value id, offset, flags]
 		this.snapshotInfo = []; // per snapshot segment: [insSeq, insClient, rmFirst, rmCount] (V1 merge info)
 		this.snapshotStamps = []; // [seq, client, kind]
@@ -281,6 +282,7 @@ class MergeTreeStreamBuilder {
 			const [off] = this.text.push(String.fromCharCode(rtype));
 			const p = spec.props;
 			this.snapshotSegs.push([off, (1 | FMT_MT_SEG_MARKER) >>> 0, p && Object.keys(p).length ? this.propsOp(p) : NO_PROPS]);
+			this.segDoc.push(this.docs.length);
 			return;
 		}
 		if (typeof spec === "string") {
@@ -295,6 +297,7 @@ class MergeTreeStreamBuilder {
 		if (text.length === 0) throw new Error("empty segment in a summary chunk");
 		const [off, len] = this.text.push(text);
 		this.snapshotSegs.push([off, len, props && Object.keys(props).length ? this.propsOp(props) : NO_PROPS]);
+		this.segDoc.push(this.docs.length);
 	}
 	/**
 	 * specToSegment's stamps for a V1 segment with merge info (snapshotLoader.ts:105-175): insert
@@ -451,23 +454,24 @@ class MergeTreeStreamBuilder {
 		}
 		return i;
 	}
-	/** Raw (key, value) changes in key order, then adjust changes as (key, FMT_MT_VALUE_ADJUST) + row
-	 * index (opToChanges, segmentPropertiesManager.ts:86-95). */
+	/** Raw (key, value) changes in key order, then adjust changes (opToChanges,
+	 * segmentPropertiesManager.ts:86-95), held as [key, value id] / [key, -1, adjust row] over the
+	 * batch-wide value dictionary; finish() packs them with batch-global or document-local value ids
+	 * (streams.py _props_op). */
 	propsOp(props, adjust) {
 		const kv = [];
 		for (const k of jsKeyOrder(props)) {
 			const v = props[k];
 			const keyId = this.keys.intern(k);
-			const valId = v === null ? 0 : this.values.intern(JSON.stringify(v));
-			if (keyId > 0xffff || valId >= FMT_MT_VALUE_ADJUST) throw new UnsupportedOp("props dictionary exceeds 65535 entries");
-			kv.push(((keyId << 16) | valId) >>> 0);
+			if (keyId > 0xffff) throw new UnsupportedOp("more than 65536 distinct property keys in a batch");
+			kv.push([keyId, v === null ? 0 : this.values.intern(JSON.stringify(v))]);
 		}
 		for (const k of jsKeyOrder(adjust || {})) {
 			const keyId = this.keys.intern(k);
-			if (keyId > 0xffff) throw new UnsupportedOp("props dictionary exceeds 65535 entries");
-			kv.push(((keyId << 16) | FMT_MT_VALUE_ADJUST) >>> 0, this.adjustRow(adjust[k]));
+			if (keyId > 0xffff) throw new UnsupportedOp("more than 65536 distinct property keys in a batch");
+			kv.push([keyId, -1, this.adjustRow(adjust[k])]);
 		}
-		const t = kv.join(",");
+		const t = kv.map((e) => e.join(":")).join(",");
 		let i = this.propsOps.get(t);
 		if (i === undefined) {
 			i = this.propsList.length;
@@ -605,10 +609,18 @@ class MergeTreeStreamBuilder {
 				a = b;
 			}
 		}
-		const propsOff = new Uint32Array(this.propsList.length + 1);
+		// value ids: batch-global while the distinct values fit below the id limit, else document-local
+		// (fmt.h doc_value_base; streams.py _localize_values)
+		const limit = this.adjusts.length ? FMT_MT_VALUE_COMPUTED : FMT_MT_VALUE_ADJUST;
+		let propsList = this.propsList, values = this.values.items.slice(), valueBase;
+		if (this.values.items.length > limit) [propsList, values, valueBase] = this.localizeValues(limit);
+		const propsOff = new Uint32Array(propsList.length + 1);
 		const kv = [];
-		this.propsList.forEach((t, j) => {
-			kv.push(...t);
+		propsList.forEach((t, j) => {
+			for (const e of t) {
+				if (e.length === 2) kv.push(((e[0] << 16) | e[1]) >>> 0);
+				else kv.push(((e[0] << 16) | FMT_MT_VALUE_ADJUST) >>> 0, e[2]);
+			}
 			propsOff[j + 1] = kv.length;
 		});
 		const docInit = new Uint32Array(this.docs.length * 2);
@@ -632,9 +644,6 @@ class MergeTreeStreamBuilder {
 			});
 			snapshotSegs = Uint32Array.from([].concat(...this.snapshotSegs));
 		}
-		if (this.adjusts.length && this.values.items.length > FMT_MT_VALUE_COMPUTED) {
-			throw new UnsupportedOp(`more than ${FMT_MT_VALUE_COMPUTED} distinct values in a batch with annotate adjusts`);
-		}
 		return {
 			ops: this.ops.bytes(),
 			docOpOffsets: offs,
@@ -645,7 +654,8 @@ class MergeTreeStreamBuilder {
 			propsOff,
 			propsKv: Uint32Array.from(kv),
 			keys: this.keys.items.slice(),
-			values: this.values.items.slice(),
+			values,
+			docValueBase: valueBase,
 			clients: this.docs.map((d) => d.clientNames.slice()),
 			messages: this.docs.map((d) => d.messages),
 			nDocs: this.docs.length,
@@ -654,9 +664,82 @@ class MergeTreeStreamBuilder {
 			snapshotStamps: this.hasMergeInfo ? Uint32Array.from([].concat(...this.snapshotStamps.map((r) => [r[0] >>> 0, r[1] >>> 0, r[2], 0]))) : undefined,
 			markerIdKey: this.relpos.length && this.keys.ids.has(MARKER_ID_KEY) ? this.keys.ids.get(MARKER_ID_KEY) : FMT_MT_NO_MARKER,
 			adjusts: this.adjusts.length ? adjustBytes(this.adjusts) : undefined,
-			valueNum: this.adjusts.length ? Float64Array.from(this.values.items, valueNumber) : undefined,
+			valueNum: this.adjusts.length ? Float64Array.from(values, valueNumber) : undefined,
 		};
 	}
+	/**
+	 * Document-local value ids: every props op a document references (annotate payloads, insert props
+	 * pos2 - 1, its summary segments' props) becomes a props op of that document alone whose values
+	 * are numbered 1.. in the document's own dictionary; its relative positions' marker ids follow.
+	 * Rewrites the op records and segment / relpos rows in place. Mirrors streams.py _localize_values.
+	 */
+	localizeValues(limit) {
+		const v = this.ops.view;
+		const pairs = new Map(); // "doc:pid" -> new props op id
+		const list = [];
+		const local = this.docs.map(() => new Map()); // per document: batch value id -> local id
+		const lid = (d, g) => {
+			const m = local[d];
+			let x = m.get(g);
+			if (x === undefined) {
+				x = m.size + 1;
+				m.set(g, x);
+			}
+			return x;
+		};
+		const refs = []; // [doc, pid, apply(newPid)]
+		let a = 0;
+		this.docs.forEach((doc, d) => {
+			for (let i = a; i < a + doc.nOps; i++) {
+				const o = i * MT_OP_BYTES, t = v.getUint8(o + 27);
+				if (t === MT_ANNOTATE) refs.push([d, v.getUint32(o + 20, true), (p) => v.setUint32(o + 20, p, true)]);
+				else if (t === MT_INSERT && v.getInt32(o + 16, true) > 0)
+					refs.push([d, v.getInt32(o + 16, true) - 1, (p) => v.setInt32(o + 16, p + 1, true)]);
+			}
+			a += doc.nOps;
+		});
+		this.snapshotSegs.forEach((sg, k) => {
+			if (sg[2] !== NO_PROPS) refs.push([this.segDoc[k], sg[2], (p) => { sg[2] = p; }]);
+		});
+		refs.sort((x, y) => x[0] - y[0] || x[1] - y[1]);
+		for (const [d, pid, apply] of refs) {
+			const key = `${d}:${pid}`;
+			let np = pairs.get(key);
+			if (np === undefined) {
+				np = list.length;
+				pairs.set(key, np);
+				list.push(this.propsList[pid].map((e) => (e.length === 2 ? [e[0], e[1] === 0 ? 0 : lid(d, e[1])] : e)));
+			}
+			apply(np);
+		}
+		a = 0;
+		this.docs.forEach((doc, d) => {
+			for (let i = a; i < a + doc.nOps; i++) {
+				const o = i * MT_OP_BYTES, f = v.getUint32(o + 28, true);
+				for (const [flag, at] of [[FMT_MT_F_REL1, 12], [FMT_MT_F_REL2, 16]]) {
+					if ((f & flag) === 0) continue;
+					const row = this.relpos[v.getInt32(o + at, true)];
+					if (row[0] !== FMT_MT_NO_MARKER) row[0] = lid(d, row[0]);
+				}
+			}
+			a += doc.nOps;
+		});
+		const values = ["null"], base = new Uint32Array(this.docs.length + 1);
+		local.forEach((m, d) => {
+			if (m.size >= limit) throw new UnsupportedOp(`more than ${limit - 1} distinct property values in one document`);
+			base[d] = values.length - 1;
+			for (const g of m.keys()) values.push(this.values.items[g]);
+		});
+		base[this.docs.length] = values.length - 1;
+		return [list, values, base];
+	}
+}
+
+/** Document d's value table (value id -> JSON text): the batch's, or its own slice when the batch
+ * has document-local value ids (docValueBase, fmt.h doc_value_base). */
+function docValues(batch, d) {
+	if (!batch.docValueBase) return batch.values;
+	return ["null"].concat(batch.values.slice(batch.docValueBase[d] + 1, batch.docValueBase[d + 1] + 1));
 }
 
 /** fmt_mt_adjust rows (32 bytes: f64 delta, min, max, u32 flags, pad) as bytes. */
@@ -809,8 +892,9 @@ class MergeTreeReplay {
 	/** The value texts the document's prop sets index: the batch's, then its computed numbers. */
 	valuesOf(doc) {
 		const nums = this.numbers(doc);
-		if (nums.length === 0) return this.batch.values;
-		const vals = this.batch.values.slice();
+		const own = docValues(this.batch, doc);
+		if (nums.length === 0) return own;
+		const vals = own.slice();
 		nums.forEach((x, k) => { vals[FMT_MT_VALUE_COMPUTED + k] = JSON.stringify(x); });
 		return vals;
 	}
@@ -826,6 +910,7 @@ class MergeTreeReplay {
 		const lv = new DataView(r.leaves), pv = new DataView(r.props);
 		const chars = new Uint16Array(r.chars);
 		const nums = this.numbers(doc);
+		const vals = docValues(this.batch, doc);
 		const props = [];
 		for (let p = 0; p < h.nProps; p++) {
 			const n = pv.getUint32(p * PROPSET_BYTES, true);
@@ -835,7 +920,7 @@ class MergeTreeReplay {
 				const val = kv & 0xffff;
 				if (val !== 0) {
 					obj[this.batch.keys[kv >>> 16]] = val >= FMT_MT_VALUE_COMPUTED && this.batch.adjusts
-						? nums[val - FMT_MT_VALUE_COMPUTED] : JSON.parse(this.batch.values[val]);
+						? nums[val - FMT_MT_VALUE_COMPUTED] : JSON.parse(vals[val]);
 				}
 			}
 			props.push(obj);

@@ -470,6 +470,22 @@ napi_value ReplayMergeTree(napi_env env, napi_callback_info info) {
     keep_array(env, j, prop(env, b, "adjusts"));
     keep_array(env, j, prop(env, b, "valueNum"));
   }
+  // optional document-local value ids: docValueBase (n_docs + 1 uint32, fmt.h doc_value_base)
+  void* vb;
+  size_t nvb;
+  if (!get_bytes(env, prop(env, b, "docValueBase"), "docValueBase", &vb, &nvb)) {
+    delete j;
+    return nullptr;
+  }
+  if (vb != nullptr) {
+    if (nvb != (static_cast<size_t>(j->mt.n_docs) + 1) * sizeof(uint32_t)) {
+      delete j;
+      throw_fmt(env, FMT_E_USAGE, "replayMergeTree: docValueBase must hold n_docs + 1 uint32 entries");
+      return nullptr;
+    }
+    j->mt.doc_value_base = static_cast<const uint32_t*>(vb);
+    keep_array(env, j, prop(env, b, "docValueBase"));
+  }
   // optional legacy relative positions: relpos (fmt_mt_relpos rows) + markerIdKey
   void* rp;
   size_t nrp;

@@ -432,3 +432,37 @@ e.close();process.stdout.write(JSON.stringify(out));}})().catch((e)=>{{console.e
     out = json.loads(r.stdout)
     assert all(a and b for a, b, _ in out["map"]) and sum(n for _, _, n in out["map"]) > 1000
     assert out["bytes"] > 0 and all(out["legacy"]) and out["cu"] > 0  # catchupOps from the bulk copy too
+
+
+def test_js_packer_document_local_values_match_python(addon, tmp_path):
+    """A batch with more distinct property values than 16-bit batch-global ids (each Marker's own
+    markerId): the JS packer switches to document-local ids (docValueBase, fmt.h doc_value_base)
+    exactly as streams.py does — the same op records, props tables, values and bases."""
+    import marker_docs
+
+    docs = [marker_docs.doc_messages(d, 1200, 3) for d in range(200)]
+    (tmp_path / "docs.json").write_text(json.dumps([{"init": i, "msgs": m} for i, m in docs]))
+    script = (
+        "const f=require('./fluidframework_amd/js/fmt.js');const fs=require('fs');"
+        f"const out={json.dumps(str(tmp_path))};"
+        "const docs=JSON.parse(fs.readFileSync(out+'/docs.json','utf8'));"
+        "const b=new f.MergeTreeStreamBuilder();"
+        "for(const x of docs){const d=b.beginDoc(x.init);for(const m of x.msgs)d.addMessage(m);}"
+        "const r=b.finish();"
+        "fs.writeFileSync(out+'/ops.bin',Buffer.from(r.ops.buffer,r.ops.byteOffset,r.ops.byteLength));"
+        "fs.writeFileSync(out+'/props_off.bin',Buffer.from(r.propsOff.buffer));"
+        "fs.writeFileSync(out+'/props_kv.bin',Buffer.from(r.propsKv.buffer));"
+        "fs.writeFileSync(out+'/relpos.bin',Buffer.from(r.relpos.buffer));"
+        "fs.writeFileSync(out+'/base.bin',Buffer.from(r.docValueBase.buffer));"
+        "fs.writeFileSync(out+'/meta.json',JSON.stringify({values:r.values}));")
+    r = _node("-e", script, timeout=600)
+    assert r.returncode == 0, r.stderr
+    py = marker_docs.marker_batch(200, 1200, seed=3)
+    assert py.value_base is not None
+    rd = lambda n, dt: np.fromfile(tmp_path / n, dtype=dt)  # noqa: E731
+    assert rd("ops.bin", np.uint8).tobytes() == py.ops.tobytes()
+    assert np.array_equal(rd("props_off.bin", np.uint32), py.props_off)
+    assert np.array_equal(rd("props_kv.bin", np.uint32), py.props_kv)
+    assert rd("relpos.bin", np.uint8).tobytes() == py.relpos.tobytes()
+    assert np.array_equal(rd("base.bin", np.uint32), py.value_base)
+    assert json.load(open(tmp_path / "meta.json"))["values"] == py.values
