@@ -62,7 +62,11 @@ __global__ __launch_bounds__(64 * kDigWaves) void stateDigestKernel(const fmt_mt
           const fmt_mt_propset& P = V.props[L.props];
           const uint32_t n = P.n;
           acc += digElem(6, i, n);
-          for (uint32_t k = 0; k < n && k < FMT_MT_PROPS_MAX; k++) acc += digElem(7, static_cast<uint64_t>(i) * 8 + k, P.kv[k]);
+          // (a wide set continues in the following records: tag 9 for entries 8 and up)
+          for (uint32_t k = 0; k < n && k < FMT_MT_PROPS_KEYS_MAX && L.props + k / FMT_MT_PROPS_MAX < h.n_props; k++) {
+            const uint32_t w = V.props[L.props + k / FMT_MT_PROPS_MAX].kv[k % FMT_MT_PROPS_MAX];
+            acc += k < FMT_MT_PROPS_MAX ? digElem(7, static_cast<uint64_t>(i) * 8 + k, w) : digElem(9, static_cast<uint64_t>(i) * 64 + k, w);
+          }
         }
       }
       for (uint32_t u = lane; u < h.n_chars; u += 64) acc += digElem(8, u, V.chars[u]);

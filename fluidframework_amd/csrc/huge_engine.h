@@ -170,6 +170,7 @@ struct HugeLds {
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
   uint32_t tmp[256];
   uint16_t pClass[kPropCap];     // prop set id -> its match class (the first set with the same content)
+  uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (lane k = entry k)
   int32_t cmd[8];                // pass command from wave 0 to the helper waves (HugeDoc::PassCmd)
   uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
   int32_t wlVis[kWinList];
@@ -1376,47 +1377,63 @@ class HugeDoc {
   FMT_DEV uint32_t propClass(uint32_t a) const { return a == kNoProps ? 0xFFFFu : L->pClass[a]; }
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || uni(propClass(a)) == uni(propClass(b)); }
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
+  // The working set lives in LDS (kvWork, lane k = entry k); a set wider than FMT_MT_PROPS_MAX entries
+  // takes consecutive records (fmt.h fmt_mt_propset).
+  FMT_DEV uint32_t setKv(uint32_t p, uint32_t k) const {
+    return rd(S.props + ((static_cast<size_t>(p) + k / FMT_MT_PROPS_MAX) * kPropWords + 1 + k % FMT_MT_PROPS_MAX));
+  }
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
-    uint32_t kv[FMT_MT_PROPS_MAX] = {};
-    uint32_t cnt = 0;
-    if (old != kNoProps) {
-      cnt = ldu(S.props + old * kPropWords);
-      for (uint32_t i = 0; i < cnt; i++) kv[i] = ldu(S.props + old * kPropWords + 1 + i);
-    }
+    constexpr int kKeysMax = FMT_MT_PROPS_KEYS_MAX;
+    uint32_t cnt = old != kNoProps ? ldu(S.props + old * kPropWords) : 0u;
+    FOR_LANES(l) { L->kvWork[l] = l < static_cast<int>(cnt) ? setKv(old, static_cast<uint32_t>(l)) : 0u; }
+    waveSync();
     const uint32_t a = ldu(in.propsOff + opId), b = ldu(in.propsOff + opId + 1);
     for (uint32_t t = a; t < b; t++) {
       const uint32_t e = ldu(in.propsKv + t);
-      uint32_t pos = cnt;
-      for (uint32_t i = 0; i < cnt; i++)
-        if ((kv[i] >> 16) == (e >> 16)) pos = i;
-      if ((e & 0xFFFFu) == 0) {
+      Lane<bool> hit;
+      FOR_LANES(l) { LANE(hit) = l < static_cast<int>(cnt) && (L->kvWork[l] >> 16) == (e >> 16); }
+      const uint64_t m = ballot(hit);
+      const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
+      if ((e & 0xFFFFu) == 0) {  // null: delete the key
         if (pos < cnt) {
-          for (uint32_t i = pos; i + 1 < cnt; i++) kv[i] = kv[i + 1];
+          Lane<uint32_t> v;
+          FOR_LANES(l) { LANE(v) = (l < kKeysMax - 1 && l >= static_cast<int>(pos)) ? L->kvWork[l + 1] : 0u; }
+          waveSync();
+          FOR_LANES(l) {
+            if (l >= static_cast<int>(pos) && l + 1 < static_cast<int>(cnt)) L->kvWork[l] = LANE(v);
+            if (l + 1 == static_cast<int>(cnt)) L->kvWork[l] = 0u;
+          }
           cnt--;
         }
       } else if (pos < cnt) {
-        kv[pos] = e;
+        FOR_LANES(l) {
+          if (l == static_cast<int>(pos)) L->kvWork[l] = e;
+        }
       } else {
-        if (cnt >= FMT_MT_PROPS_MAX) {
+        if (cnt >= static_cast<uint32_t>(kKeysMax)) {
           fail(FMT_E_CAPACITY);
           return kNoProps;
         }
-        kv[cnt++] = e;
+        FOR_LANES(l) {
+          if (l == static_cast<int>(cnt)) L->kvWork[l] = e;
+        }
+        cnt++;
       }
+      waveSync();
     }
     for (int base = 0; base < nProps; base += 64) {  // interned already?
       Lane<bool> same;
       FOR_LANES(l) {
         const int p = base + l;
         bool eq = p < nProps && rd(S.props + (p * kPropWords)) == cnt;
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++)
-          if (i < cnt) eq = eq && rd(S.props + (p * kPropWords + 1 + i)) == kv[i];
+        for (uint32_t i = 0; eq && i < cnt; i++) eq = setKv(static_cast<uint32_t>(p), i) == L->kvWork[i];
         LANE(same) = eq;
       }
       const uint64_t m = ballot(same);
       if (m) return static_cast<uint32_t>(base + ctz64(m));
     }
-    if (nProps >= kPropCap) {
+    const int rec = cnt > FMT_MT_PROPS_MAX ? static_cast<int>((cnt + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1;
+    if (nProps + rec > kPropCap) {
       fail(FMT_E_CAPACITY);
       return kNoProps;
     }
@@ -1427,28 +1444,31 @@ class HugeDoc {
       FOR_LANES(l) {
         const int p = base + l;
         bool eq = p < nProps && rd(S.props + (p * kPropWords)) == cnt;
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) {
-          if (i < cnt) {
-            bool found = false;
-            for (uint32_t j = 0; j < FMT_MT_PROPS_MAX; j++)
-              if (j < cnt && rd(S.props + (p * kPropWords + 1 + j)) == kv[i]) found = true;
-            eq = eq && found;
-          }
+        for (uint32_t i = 0; eq && i < cnt; i++) {
+          const uint32_t x = L->kvWork[i];
+          bool found = false;
+          for (uint32_t j = 0; j < cnt; j++)
+            if (setKv(static_cast<uint32_t>(p), j) == x) found = true;
+          eq = found;
         }
         LANE(same) = eq;
       }
       const uint64_t m = ballot(same);
       if (m) cls = static_cast<uint32_t>(base + ctz64(m));
     }
-    nProps++;
     FOR_LANES(l) {
-      if (l == 0) {
-        S.props[id * kPropWords] = cnt;
-        for (uint32_t i = 0; i < FMT_MT_PROPS_MAX; i++) S.props[id * kPropWords + 1 + i] = kv[i];
-        L->pClass[id] = static_cast<uint16_t>(cls);
+      const int q = l / FMT_MT_PROPS_MAX, k = l % FMT_MT_PROPS_MAX;
+      if (q < rec) {
+        const size_t r = static_cast<size_t>(id + q) * kPropWords;
+        if (k == 0) {
+          S.props[r] = q == 0 ? cnt : FMT_MT_PROPS_CONT;
+          L->pClass[id + q] = static_cast<uint16_t>(q == 0 ? cls : 0xFFFEu);
+        }
+        S.props[r + 1 + k] = L->kvWork[l];
       }
     }
     waveSync();
+    nProps += rec;
     return id;
   }
 

@@ -46,6 +46,7 @@ namespace fmt_mt {
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
 constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:21)
 constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
+constexpr int kKeysMax = FMT_MT_PROPS_KEYS_MAX;  // keys of one prop set (one working-set lane each)
 constexpr int32_t kNotRemoved = 0x7fffffff;
 constexpr int kCapacityFinal = -33;  // internal status (small tier only), never leaves the runtime
 constexpr int kCkptEscalate = -34;   // internal status: the compact tier stopped at a checkpoint (Doc::saveCkpt)
@@ -148,7 +149,7 @@ struct Scratch {
   HeapEnt heap[C::kHeapCap + 1];  // 1-based
   PropSet props[C::kPropCap];
   uint16_t propCls[C::kPropCap];  // match class: the first interned set with the same content (empty: 0xFFFF)
-  uint32_t kvWork[FMT_MT_PROPS_MAX];  // applyProps' working set (wave-uniform)
+  uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (lane k = entry k)
   typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
@@ -1126,7 +1127,7 @@ class Doc {
           const uint32_t x = s->kvWork[i];
           bool found = false;
           for (uint32_t k = 0; k < cnt; k++)
-            if ((s->props[p].kv[k] >> 16) == (x >> 16)) found = s->props[p].kv[k] == x;
+            if ((setKv(p, k) >> 16) == (x >> 16)) found = setKv(p, k) == x;
           m = found;
         }
         LANE(eq) = m;
@@ -1146,11 +1147,7 @@ class Doc {
   // (AdjSite: the annotate call site, the only one whose props ops can hold annotate-adjust entries)
   template <bool AdjSite = false>
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
-    uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
-    FOR_LANES(l) {
-      if (l < FMT_MT_PROPS_MAX) s->kvWork[l] = (old != kPropsUndef && l < static_cast<int>(cnt)) ? s->props[old].kv[l] : 0u;
-    }
-    waveSync();
+    uint32_t cnt = loadWork(old);
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
     for (uint32_t t = a; t < b; t++) {
       uint32_t e = uni(in.propsKv[t]);
@@ -1182,7 +1179,7 @@ class Doc {
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
         if (pos < cnt) {
           Lane<uint32_t> v;
-          FOR_LANES(l) { LANE(v) = (l < FMT_MT_PROPS_MAX - 1 && l >= static_cast<int>(pos)) ? s->kvWork[l + 1] : 0u; }
+          FOR_LANES(l) { LANE(v) = (l < kKeysMax - 1 && l >= static_cast<int>(pos)) ? s->kvWork[l + 1] : 0u; }
           waveSync();
           FOR_LANES(l) {
             if (l >= static_cast<int>(pos) && l + 1 < static_cast<int>(cnt)) s->kvWork[l] = LANE(v);
@@ -1194,7 +1191,7 @@ class Doc {
           if (l == static_cast<int>(pos)) s->kvWork[l] = e;
         }
       } else {
-        if (cnt >= FMT_MT_PROPS_MAX) {
+        if (cnt >= static_cast<uint32_t>(kKeysMax)) {
           fail(kCapFinal);
           return 0;
         }
@@ -1210,29 +1207,46 @@ class Doc {
 
   // The prop set s->kvWork[0 .. cnt) (key order kept) as an interned set id: an equal set already in
   // the table, else a new one.
+  // (a set wider than FMT_MT_PROPS_MAX takes consecutive records, fmt.h fmt_mt_propset)
   FMT_DEV uint32_t internWork(uint32_t cnt) {
     for (int base = 0; base < nProps; base += 64) {  // interned already? lane p checks prop set base + p
       Lane<bool> same;
       FOR_LANES(l) {
         const int p = base + l;
         bool eq = p < nProps && s->props[p].n == cnt;
-        for (uint32_t i = 0; eq && i < cnt; i++) eq = s->props[p].kv[i] == s->kvWork[i];
+        for (uint32_t i = 0; eq && i < cnt; i++) eq = setKv(p, i) == s->kvWork[i];
         LANE(same) = eq;
       }
       const uint64_t m = ballot(same);
       if (m != 0) return static_cast<uint32_t>(base + ctz64(m));
     }
-    if (nProps >= kPropCap) {
+    const int rec = cnt > FMT_MT_PROPS_MAX ? static_cast<int>((cnt + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1;
+    if (nProps + rec > kPropCap) {
       fail(FMT_E_CAPACITY);
       return 0;
     }
     propsIndex(nProps, cnt);
     FOR_LANES(l) {
-      if (l == 0) s->props[nProps].n = cnt;
-      if (l < FMT_MT_PROPS_MAX) s->props[nProps].kv[l] = s->kvWork[l];
+      const int q = l / FMT_MT_PROPS_MAX, k = l % FMT_MT_PROPS_MAX;
+      if (q < rec) {
+        if (k == 0) s->props[nProps + q].n = q == 0 ? cnt : FMT_MT_PROPS_CONT;
+        s->props[nProps + q].kv[k] = s->kvWork[l];
+        if (k == 0 && q > 0) s->propCls[nProps + q] = 0xFFFEu;  // (a continuation: no leaf names it)
+      }
     }
     waveSync();
-    return static_cast<uint32_t>(nProps++);
+    const int id = nProps;
+    nProps += rec;
+    return static_cast<uint32_t>(id);
+  }
+  // entry k of the prop set whose first record is p
+  FMT_DEV uint32_t setKv(int p, uint32_t k) const { return s->props[p + static_cast<int>(k / FMT_MT_PROPS_MAX)].kv[k % FMT_MT_PROPS_MAX]; }
+  // the working set = the entries of set `old` (kPropsUndef: none); returns their count
+  FMT_DEV uint32_t loadWork(uint32_t old) {
+    const uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
+    FOR_LANES(l) { s->kvWork[l] = l < static_cast<int>(cnt) ? setKv(static_cast<int>(old), static_cast<uint32_t>(l)) : 0u; }
+    waveSync();
+    return cnt;
   }
 
   // ------------------------------------------------------------------ property managers (Adj)
@@ -1370,11 +1384,7 @@ class Doc {
   FMT_DEV void pmAnnotate(int j, uint32_t opId, int seq) {
     const uint32_t leaf = fId(readField(j, 4));
     const uint32_t old = propsAt(j);
-    uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
-    FOR_LANES(l) {
-      if (l < FMT_MT_PROPS_MAX) s->kvWork[l] = (old != kPropsUndef && l < static_cast<int>(cnt)) ? s->props[old].kv[l] : 0u;
-    }
-    waveSync();
+    uint32_t cnt = loadWork(old);
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
     for (uint32_t t = a; t < b && status == FMT_OK; t++) {
       const uint32_t e = uni(in.propsKv[t]);
@@ -1419,7 +1429,7 @@ class Doc {
         FOR_LANES(l) {
           if (l == 0) s->kvWork[pos] = (key << 16) | after;
         }
-      } else if (cnt < FMT_MT_PROPS_MAX) {
+      } else if (cnt < static_cast<uint32_t>(kKeysMax)) {
         FOR_LANES(l) {
           if (l == 0) s->kvWork[cnt] = (key << 16) | after;
         }
@@ -1464,12 +1474,7 @@ class Doc {
       const int j = findLeafById(leaf);
       uint32_t cnt = 0;
       if (j >= 0) {
-        const uint32_t old = propsAt(j);
-        cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
-        FOR_LANES(l) {
-          if (l < FMT_MT_PROPS_MAX) s->kvWork[l] = (old != kPropsUndef && l < static_cast<int>(cnt)) ? s->props[old].kv[l] : 0u;
-        }
-        waveSync();
+        cnt = loadWork(propsAt(j));
       }
       for (int g = h; g >= 0 && status == FMT_OK; g = pmFind(leaf, 0u, 0x10000u, g + 1)) {
         pmSet(g, 2, 0x80000000u);  // (done: a head's seq word is otherwise unused)
@@ -1498,7 +1503,7 @@ class Doc {
           FOR_LANES(l) {
             if (l == 0) s->kvWork[pos] = (key << 16) | v;
           }
-        } else if (cnt < FMT_MT_PROPS_MAX) {
+        } else if (cnt < static_cast<uint32_t>(kKeysMax)) {
           FOR_LANES(l) {
             if (l == 0) s->kvWork[cnt] = (key << 16) | v;
           }
@@ -2074,7 +2079,7 @@ class Doc {
         if (r * 64 + l < n && fMarker(LANE(W[4])[r]) && pid != kPropsUndef && mid <= 0xFFFFu) {
           const uint32_t cnt = s->props[pid].n;
           bool f = false;
-          for (uint32_t k = 0; k < cnt && k < FMT_MT_PROPS_MAX; k++) f = f || s->props[pid].kv[k] == want;
+          for (uint32_t k = 0; k < cnt && k < static_cast<uint32_t>(kKeysMax); k++) f = f || setKv(static_cast<int>(pid), k) == want;
           if (f) m |= 1u << r;
         }
       }

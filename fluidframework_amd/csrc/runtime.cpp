@@ -1443,20 +1443,22 @@ struct SumDict {
 
 // A prop set as a JSON object in JS own-property order: array-index keys ascending, then the
 // others in insertion order (properties' key order, snapshotChunks.ts via JSON.stringify).
-void propsObject(std::string& o, const fmt_mt_propset& ps, const SumDict& D, const std::vector<double>* nums,
+// (ps: the set's first record; a set wider than FMT_MT_PROPS_MAX continues in the next records)
+void propsObject(std::string& o, const fmt_mt_propset* ps, const SumDict& D, const std::vector<double>* nums,
                  uint32_t valueBase) {
-  const uint32_t n = ps.n < FMT_MT_PROPS_MAX ? ps.n : FMT_MT_PROPS_MAX;
-  uint32_t order[FMT_MT_PROPS_MAX];
+  const uint32_t n = ps->n < FMT_MT_PROPS_KEYS_MAX ? ps->n : FMT_MT_PROPS_KEYS_MAX;
+  uint32_t kvs[FMT_MT_PROPS_KEYS_MAX], order[FMT_MT_PROPS_KEYS_MAX];
+  for (uint32_t i = 0; i < n; i++) kvs[i] = ps[i / FMT_MT_PROPS_MAX].kv[i % FMT_MT_PROPS_MAX];
   uint32_t m = 0;
   for (uint32_t i = 0; i < n; i++)
-    if (D.keyIndex[ps.kv[i] >> 16] >= 0) order[m++] = i;
-  std::sort(order, order + m, [&](uint32_t a, uint32_t b) { return D.keyIndex[ps.kv[a] >> 16] < D.keyIndex[ps.kv[b] >> 16]; });
+    if (D.keyIndex[kvs[i] >> 16] >= 0) order[m++] = i;
+  std::sort(order, order + m, [&](uint32_t a, uint32_t b) { return D.keyIndex[kvs[a] >> 16] < D.keyIndex[kvs[b] >> 16]; });
   for (uint32_t i = 0; i < n; i++)
-    if (D.keyIndex[ps.kv[i] >> 16] < 0) order[m++] = i;
+    if (D.keyIndex[kvs[i] >> 16] < 0) order[m++] = i;
   o.push_back('{');
   for (uint32_t j = 0; j < m; j++) {
     if (j) o.push_back(',');
-    const uint32_t kv = ps.kv[order[j]];
+    const uint32_t kv = kvs[order[j]];
     o += D.keys[kv >> 16];
     o.push_back(':');
     const uint32_t v = kv & 0xFFFFu;
@@ -1493,14 +1495,14 @@ void legacyBlobs(std::string& out, uint32_t* split, const fmt_kernels::SumRun* r
         out += "{\"marker\":{\"refType\":" + std::to_string(text[start[i]]) + "}";
         if (hasProps) {
           out += ",\"props\":";
-          propsObject(out, props[r.props], D, nums, valueBase);
+          propsObject(out, props + r.props, D, nums, valueBase);
         }
         out.push_back('}');
       } else if (hasProps) {
         out += "{\"text\":";
         jsonQuote16(out, text + start[i], r.len);
         out += ",\"props\":";
-        propsObject(out, props[r.props], D, nums, valueBase);
+        propsObject(out, props + r.props, D, nums, valueBase);
         out.push_back('}');
       } else {
         jsonQuote16(out, text + start[i], r.len);
@@ -1671,15 +1673,16 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
         for (uint32_t i = 0; i < o.n_runs && !bad; i++) {
           const uint32_t p = runs[o.run_off + i].props;
           if (p == 0xFFFFu) continue;
-          if (p >= hdr[d].n_props || propsHost[d][p].n > FMT_MT_PROPS_MAX) {
+          const uint32_t pn = p < hdr[d].n_props ? propsHost[d][p].n : 0u;
+          if (p >= hdr[d].n_props || pn > FMT_MT_PROPS_KEYS_MAX || (pn > 0 && p + (pn - 1) / FMT_MT_PROPS_MAX >= hdr[d].n_props)) {
             bad = true;
             break;
           }
-          const fmt_mt_propset& ps = propsHost[d][p];
-          for (uint32_t k = 0; k < ps.n; k++) {
-            const uint32_t v = ps.kv[k] & 0xFFFFu;
+          for (uint32_t k = 0; k < pn; k++) {
+            const uint32_t kv = propsHost[d][p + k / FMT_MT_PROPS_MAX].kv[k % FMT_MT_PROPS_MAX];
+            const uint32_t v = kv & 0xFFFFu;
             const bool computed = nums != nullptr && v >= FMT_MT_VALUE_COMPUTED && v - FMT_MT_VALUE_COMPUTED < nums->size();
-            if ((ps.kv[k] >> 16) >= nKeys || (vBase + static_cast<uint64_t>(v) >= vEnd && !computed)) bad = true;
+            if ((kv >> 16) >= nKeys || (vBase + static_cast<uint64_t>(v) >= vEnd && !computed)) bad = true;
           }
         }
         if (bad) {

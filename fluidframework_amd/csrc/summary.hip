@@ -31,12 +31,20 @@ __device__ __forceinline__ uint32_t sumLane(uint32_t v, int lane) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), lane));
 }
 
-// Same (key, value) pairs, any order.
-__device__ __forceinline__ bool sumSameSet(const fmt_mt_propset& a, const fmt_mt_propset& b) {
-  if (a.n != b.n) return false;
-  for (uint32_t i = 0; i < a.n && i < FMT_MT_PROPS_MAX; i++) {
+// Entry k of the prop set whose first record is p (fmt.h: wide sets take consecutive records).
+__device__ __forceinline__ uint32_t sumKv(const fmt_mt_propset* T, uint32_t p, uint32_t k) {
+  return T[p + k / FMT_MT_PROPS_MAX].kv[k % FMT_MT_PROPS_MAX];
+}
+
+// Sets p and q (first records, np records in all) hold the same (key, value) pairs, any order.
+__device__ __forceinline__ bool sumSameSet(const fmt_mt_propset* T, uint32_t p, uint32_t q, uint32_t np) {
+  const uint32_t n = T[p].n;
+  if (n != T[q].n || n == FMT_MT_PROPS_CONT || n > FMT_MT_PROPS_KEYS_MAX) return false;
+  if (p + (n ? (n - 1) / FMT_MT_PROPS_MAX : 0) >= np || q + (n ? (n - 1) / FMT_MT_PROPS_MAX : 0) >= np) return false;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t x = sumKv(T, p, i);
     bool found = false;
-    for (uint32_t j = 0; j < b.n && j < FMT_MT_PROPS_MAX; j++) found = found || b.kv[j] == a.kv[i];
+    for (uint32_t j = 0; j < n; j++) found = found || sumKv(T, q, j) == x;
     if (!found) return false;
   }
   return true;
@@ -65,11 +73,11 @@ __global__ __launch_bounds__(64 * kSumWaves) void summaryRunsKernel(const fmt_mt
     const int32_t minSeq = h.min_seq;
     // match classes: the first prop set with the same content (empty sets: undefined's class)
     for (uint32_t p = lane; p < np; p += 64) {
-      const fmt_mt_propset a = V.props[p];
-      uint16_t c = a.n == 0 ? 0xFFFFu : static_cast<uint16_t>(p);
-      if (a.n != 0)
+      const uint32_t an = V.props[p].n;
+      uint16_t c = an == 0 ? 0xFFFFu : static_cast<uint16_t>(p);
+      if (an != 0 && an != FMT_MT_PROPS_CONT)  // (continuation records: no leaf names them)
         for (uint32_t q = 0; q < p; q++)
-          if (sumSameSet(V.props[q], a)) {
+          if (sumSameSet(V.props, q, p, np)) {
             c = static_cast<uint16_t>(q);
             break;
           }

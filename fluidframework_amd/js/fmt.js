@@ -49,7 +49,7 @@ const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 36;
 const CATCHUP_BYTES = 16, SNAPSHOT_DOC_BYTES = 32;
 const NO_PROPS = 0xffffffff;
-const PROPS_MAX = 8;
+const PROPS_MAX = 8, FMT_MT_PROPS_CONT = 0xffffffff; // fmt.h: entries per prop-set record; n of a continuation record
 
 let addon = null;
 /** The native addon; throws if it was not built (there is no JavaScript fallback engine). */
@@ -911,12 +911,19 @@ class MergeTreeReplay {
 		const chars = new Uint16Array(r.chars);
 		const nums = this.numbers(doc);
 		const vals = docValues(this.batch, doc);
+		// entry k of the set whose first record is p (a set wider than PROPS_MAX continues in the next
+		// records, fmt.h fmt_mt_propset; continuation records have n = FMT_MT_PROPS_CONT)
+		const entry = (p, k) => pv.getUint32((p + Math.floor(k / PROPS_MAX)) * PROPSET_BYTES + 4 + 4 * (k % PROPS_MAX), true);
+		const width = (p) => {
+			const n = pv.getUint32(p * PROPSET_BYTES, true);
+			return n === FMT_MT_PROPS_CONT || p + Math.floor((n - 1) / PROPS_MAX) >= h.nProps ? 0 : n;
+		};
 		const props = [];
 		for (let p = 0; p < h.nProps; p++) {
-			const n = pv.getUint32(p * PROPSET_BYTES, true);
+			const n = width(p);
 			const obj = {};
-			for (let k = 0; k < n && k < PROPS_MAX; k++) {
-				const kv = pv.getUint32(p * PROPSET_BYTES + 4 + 4 * k, true);
+			for (let k = 0; k < n; k++) {
+				const kv = entry(p, k);
 				const val = kv & 0xffff;
 				if (val !== 0) {
 					obj[this.batch.keys[kv >>> 16]] = val >= FMT_MT_VALUE_COMPUTED && this.batch.adjusts
@@ -927,9 +934,9 @@ class MergeTreeReplay {
 		}
 		const kvs = [];
 		for (let p = 0; p < h.nProps; p++) {
-			const n = Math.min(pv.getUint32(p * PROPSET_BYTES, true), PROPS_MAX);
+			const n = width(p);
 			const kv = [];
-			for (let k = 0; k < n; k++) kv.push(pv.getUint32(p * PROPSET_BYTES + 4 + 4 * k, true));
+			for (let k = 0; k < n; k++) kv.push(entry(p, k));
 			kvs.push(kv);
 		}
 		const segs = [];

@@ -60,8 +60,20 @@ CATCHUP_DTYPE = np.dtype([("op", "<u4"), ("pos1", "<i4"), ("pos2", "<i4"), ("typ
 from .streams import (NO_MARKER, RELPOS_DTYPE, SNAPSHOT_DOC_DTYPE, SNAPSHOT_INFO_DTYPE, SNAPSHOT_SEG_DTYPE,  # noqa: E402
                       STAMP_DTYPE)  # (include/fmt.h layouts)
 
-PROPS_MAX = 8
+PROPS_MAX = 8        # fmt.h FMT_MT_PROPS_MAX: entries per prop-set record
+PROPS_KEYS_MAX = 64  # fmt.h FMT_MT_PROPS_KEYS_MAX: entries per prop set
+PROPS_CONT = 0xFFFFFFFF  # fmt.h FMT_MT_PROPS_CONT: n of a continuation record
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])
+
+
+def propset_entries(table, pid: int) -> tuple:
+    """The (key << 16 | value) entries of the prop set whose first record is table[pid]; a set wider
+    than PROPS_MAX continues in the following records (fmt.h fmt_mt_propset)."""
+    n = int(table[pid]["n"])
+    if n <= PROPS_MAX:
+        return tuple(int(x) for x in table[pid]["kv"][:n])
+    rec = table[pid : pid + (n + PROPS_MAX - 1) // PROPS_MAX]["kv"].reshape(-1)
+    return tuple(int(x) for x in rec[:n])
 assert PROPSET_DTYPE.itemsize == 36
 
 MAP_SLOT_DTYPE = np.dtype([("value", "<u4"), ("birth_seq", "<u4")])

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import json
 
+from .native import propset_entries
+
 from .streams import (MAP_ABSENT, MAP_VALUE_UNDEFINED, MT_ANNOTATE, MT_GROUP, MT_INSERT, MT_LEAF_MARKER,
                       MT_OBLITERATE, MT_OBLITERATE_SIDED, MT_REMOVE, VALUE_ADJUST, VALUE_COMPUTED, UnsupportedOp,
                       is_array_index_key, js_json, js_key_order, js_number, js_quote, marker_ref_type)
@@ -124,7 +126,7 @@ def legacy_segments(header, leaves, chars, propsets, min_seq, legacy_props=None)
         text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
         marker = (int(L["pad"]) & MT_LEAF_MARKER) != 0
         pid = int(L["props"]) if legacy_props is None else int(legacy_props[i])
-        props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
+        props = None if pid == 0xFFFF else propset_entries(propsets, pid)
         if segs:
             prev = segs[-1]
             if (not prev[2] and not marker and not prev[0].endswith("\n")
@@ -226,7 +228,7 @@ def v1_segments(header, leaves, chars, propsets, keys, values, client_names, rem
         text = chars[o : o + n].tobytes().decode("utf-16-le", "surrogatepass")
         marker = (int(L["pad"]) & MT_LEAF_MARKER) != 0
         pid = int(L["props"])
-        props = None if pid == 0xFFFF else tuple(int(x) for x in propsets[pid]["kv"][: propsets[pid]["n"]])
+        props = None if pid == 0xFFFF else propset_entries(propsets, pid)
         if ins <= min_seq and not removed:
             if prev is None:
                 prev = [text, props, marker]

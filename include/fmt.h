@@ -333,8 +333,14 @@ typedef struct fmt_mt_remove_order {
   uint32_t kind;  /* FMT_MT_RM_SET / FMT_MT_RM_SLICE */
 } fmt_mt_remove_order;
 
-/* A document-local prop set: up to FMT_MT_PROPS_MAX (key_id, value_id) pairs in JS insertion order. */
+/* A document-local prop set: n (key_id, value_id) pairs in JS insertion order, n <=
+ * FMT_MT_PROPS_KEYS_MAX. A record holds FMT_MT_PROPS_MAX of them; a set with more takes
+ * ceil(n / FMT_MT_PROPS_MAX) consecutive records: the first holds n and entries 0..7, each following
+ * one n = FMT_MT_PROPS_CONT and the next 8 entries (unused entries 0). Leaf prop-set ids name first
+ * records; fmt_mt_doc_result.n_props counts records. */
 #define FMT_MT_PROPS_MAX 8
+#define FMT_MT_PROPS_KEYS_MAX 64
+#define FMT_MT_PROPS_CONT 0xffffffffu
 typedef struct fmt_mt_propset {
   uint32_t n;
   uint32_t kv[FMT_MT_PROPS_MAX]; /* (key_id << 16) | value_id */

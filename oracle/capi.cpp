@@ -59,6 +59,8 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
   int nBlocks = 0, depth = 0;
   mt->collectLeaves(segs, blockOf, &nBlocks, &depth);
   std::vector<const orc::PropMap*> sets;
+  std::vector<uint32_t> setRec;  // first record of each set (a set wider than 8 entries takes several)
+  uint32_t nRec = 0;
   uint32_t charOff = 0;
   for (size_t i = 0; i < segs.size(); i++) {
     const orc::Seg* s = segs[i];
@@ -67,8 +69,13 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
       size_t j = 0;
       for (; j < sets.size(); j++)
         if (sets[j]->kv == s->props.kv) break;
-      if (j == sets.size()) sets.push_back(&s->props);
-      pid = static_cast<uint16_t>(j);
+      if (j == sets.size()) {
+        sets.push_back(&s->props);
+        setRec.push_back(nRec);
+        const size_t n = s->props.kv.size();
+        nRec += n > FMT_MT_PROPS_MAX ? static_cast<uint32_t>((n + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1u;
+      }
+      pid = static_cast<uint16_t>(setRec[j]);
     }
     if (leaves && i < capLeaves) {
       fmt_mt_leaf& L = leaves[i];
@@ -92,11 +99,18 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
     charOff += static_cast<uint32_t>(s->len());
   }
   if (props) {
-    for (size_t j = 0; j < sets.size() && j < capProps; j++) {
-      std::memset(&props[j], 0, sizeof(props[j]));
-      props[j].n = static_cast<uint32_t>(sets[j]->kv.size());
-      for (size_t k = 0; k < sets[j]->kv.size() && k < FMT_MT_PROPS_MAX; k++)
-        props[j].kv[k] = (static_cast<uint32_t>(sets[j]->kv[k].first) << 16) | sets[j]->kv[k].second;
+    for (size_t j = 0; j < sets.size(); j++) {
+      const size_t n = sets[j]->kv.size();
+      const size_t rec = n > FMT_MT_PROPS_MAX ? (n + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX : 1;
+      for (size_t q = 0; q < rec && setRec[j] + q < capProps; q++) {
+        fmt_mt_propset& P = props[setRec[j] + q];
+        std::memset(&P, 0, sizeof(P));
+        P.n = q == 0 ? static_cast<uint32_t>(n) : FMT_MT_PROPS_CONT;
+        for (size_t k = 0; k < FMT_MT_PROPS_MAX && q * FMT_MT_PROPS_MAX + k < n; k++) {
+          const auto& e = sets[j]->kv[q * FMT_MT_PROPS_MAX + k];
+          P.kv[k] = (static_cast<uint32_t>(e.first) << 16) | e.second;
+        }
+      }
     }
   }
   if (hdr) {
@@ -104,7 +118,7 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
     hdr->min_seq = mt->minSeq;
     hdr->n_leaves = static_cast<uint32_t>(segs.size());
     hdr->n_chars = charOff;
-    hdr->n_props = static_cast<uint32_t>(sets.size());
+    hdr->n_props = nRec;
     hdr->n_blocks = static_cast<uint32_t>(nBlocks);
     hdr->depth = static_cast<uint32_t>(depth);
     hdr->visible_len = static_cast<uint32_t>(mt->getLocalLength());
@@ -139,7 +153,10 @@ uint64_t digestOf(const fmt_mt_doc_result& h, const fmt_mt_leaf* leaves, const u
     } else {
       const fmt_mt_propset& P = props[L.props];
       acc += dgElem(6, i, P.n);
-      for (uint32_t k = 0; k < P.n && k < FMT_MT_PROPS_MAX; k++) acc += dgElem(7, static_cast<uint64_t>(i) * 8 + k, P.kv[k]);
+      for (uint32_t k = 0; k < P.n && k < FMT_MT_PROPS_KEYS_MAX && L.props + k / FMT_MT_PROPS_MAX < h.n_props; k++) {
+        const uint32_t w = props[L.props + k / FMT_MT_PROPS_MAX].kv[k % FMT_MT_PROPS_MAX];
+        acc += k < FMT_MT_PROPS_MAX ? dgElem(7, static_cast<uint64_t>(i) * 8 + k, w) : dgElem(9, static_cast<uint64_t>(i) * 64 + k, w);
+      }
     }
   }
   for (uint32_t u = 0; u < h.n_chars; u++) acc += dgElem(8, u, chars[u]);
@@ -390,7 +407,7 @@ int orc_mt_replay_digest(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docE
     size_t units = 0;
     for (const orc::Seg* s : segs) units += static_cast<size_t>(s->len());
     std::vector<uint16_t> ch(units + 1);
-    std::vector<fmt_mt_propset> pr(segs.size() + 1);
+    std::vector<fmt_mt_propset> pr(segs.size() * (FMT_MT_PROPS_KEYS_MAX / FMT_MT_PROPS_MAX) + 1);  // (wide sets: several records)
     dumpDoc(&mt, &h, lv.data(), static_cast<uint32_t>(lv.size()), ch.data(), static_cast<uint32_t>(ch.size()), pr.data(),
             static_cast<uint32_t>(pr.size()));
     h.status = st;

@@ -2,6 +2,8 @@
 csrc/digest.hip) and the oracle (oracle/capi.cpp digestOf) implement. Test-only."""
 import numpy as np
 
+from fluidframework_amd.native import propset_entries
+
 M64 = (1 << 64) - 1
 
 
@@ -47,11 +49,13 @@ def state_digest(hdr, leaves, chars, props) -> int:
         if p == 0xFFFF:
             acc += _sum(_elems(6, [k], [M64]))
         else:
-            ps = props[p]
-            m = int(ps["n"])
+            m = int(props[p]["n"])
             acc += _sum(_elems(6, [k], [m]))
-            if m:
-                acc += _sum(_elems(7, np.arange(m) + 8 * k, ps["kv"][:m]))
+            kv = np.array(propset_entries(props, p), dtype=np.uint64)
+            if m:  # entries 8.. of a wide set (several records) under tag 9
+                acc += _sum(_elems(7, np.arange(min(m, 8)) + 8 * k, kv[:8]))
+            if m > 8:
+                acc += _sum(_elems(9, np.arange(8, m) + 64 * k, kv[8:]))
     nc = int(hdr["n_chars"])
     acc += _sum(_elems(8, np.arange(nc), chars[:nc]))
     return int(_mix(np.uint64(acc & M64)))

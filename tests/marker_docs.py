@@ -12,7 +12,7 @@ def _msg(client, seq, ref, contents, msn):
             "contents": contents}
 
 
-def doc_messages(d: int, n_ops: int, seed: int, adjust: bool = False):
+def doc_messages(d: int, n_ops: int, seed: int, adjust: bool = False, wide: int = 0):
     """(initial text, messages) of document d: one writer per message, refSeq = seq - 1, minSeq
     trailing by up to 8, so every position is in the op's own view."""
     rnd = random.Random(seed * 1_000_003 + d)
@@ -35,6 +35,10 @@ def doc_messages(d: int, n_ops: int, seed: int, adjust: bool = False):
             p = rnd.randint(0, length - 2)
             if adjust and rnd.random() < 0.5:
                 op = {"type": 2, "pos1": p, "pos2": p + 2, "adjust": {"weight": {"delta": rnd.randint(-3, 3)}}}
+            elif wide:  # a formatting run: `wide` keys at once, some of them deleted (null)
+                keys = rnd.sample(range(wide + 6), wide)
+                op = {"type": 2, "pos1": p, "pos2": p + 2,
+                      "props": {f"k{k}": (None if rnd.random() < 0.1 else rnd.randint(0, 3)) for k in keys}}
             else:
                 op = {"type": 2, "pos1": p, "pos2": p + 2, "props": {"color": f"c{d}-{rnd.randint(0, 40)}",
                                                                     "n": rnd.randint(0, 5000)}}
@@ -45,11 +49,12 @@ def doc_messages(d: int, n_ops: int, seed: int, adjust: bool = False):
     return init, msgs
 
 
-def marker_batch(n_docs: int, n_ops: int, seed: int = 1, adjust: bool = False, docs=None, keep_messages=False):
+def marker_batch(n_docs: int, n_ops: int, seed: int = 1, adjust: bool = False, docs=None, keep_messages=False,
+                 wide: int = 0):
     """A batch of the generated documents (docs: the document indices to include, default all)."""
     b = MergeTreeStreamBuilder(keep_messages=keep_messages)
     for d in (range(n_docs) if docs is None else docs):
-        init, msgs = doc_messages(d, n_ops, seed, adjust)
+        init, msgs = doc_messages(d, n_ops, seed, adjust, wide)
         doc = b.begin_doc(init)
         for m in msgs:
             doc.add_message(m)

@@ -141,10 +141,11 @@ def emu_numbers(doc: int) -> np.ndarray:
 
 
 def resolve_props(pid, table):
+    from fluidframework_amd.native import propset_entries
+
     if pid == 0xFFFF:
         return None
-    ps = table[pid]
-    return tuple(int(x) for x in ps["kv"][: ps["n"]])
+    return propset_entries(table, pid)
 
 
 HEADER_FIELDS = ["status", "cur_seq", "min_seq", "n_leaves", "n_chars", "n_blocks", "depth", "visible_len"]

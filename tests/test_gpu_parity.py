@@ -791,3 +791,25 @@ def test_mt_document_local_value_ids_on_gpu(orc, engine, adjust):
         lv, ch, pr = engine.mt_doc(d, hdrs[d])
         assert compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], lv, ch, pr)) == [], d
         assert engine.mt_summary(d) == orc.mt_replay_summary(batch, d, batch.keys, batch.doc_values(d)), d
+
+
+def test_mt_wide_prop_sets_on_gpu(orc, engine):
+    """20-key formatting runs (prop sets over several records, fmt.h FMT_MT_PROPS_KEYS_MAX) through the
+    whole tier cascade == oracle, with their legacy summaries and state digests."""
+    from marker_docs import marker_batch
+
+    batch = marker_batch(300, 400, seed=21, wide=20)
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert (hdrs["status"] == 0).all()
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=8192, cap_chars=1 << 17, cap_props=2048)
+    assert rc == 0
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    for d in range(0, batch.n_docs, 5):
+        lv, ch, pr = engine.mt_doc(d, hdrs[d])
+        assert compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], lv, ch, pr)) == [], d
+        assert engine.mt_summary(d) == orc.mt_replay_summary(batch, d, batch.keys, batch.doc_values(d)), d
+    rc, odig, _, _ = orc.mt_replay_digest(batch, threads=8)
+    assert rc == 0
+    assert np.array_equal(engine.mt_digests(), odig)

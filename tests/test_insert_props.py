@@ -17,6 +17,8 @@ import subprocess
 import numpy as np
 import pytest
 
+from fluidframework_amd.native import PROPS_CONT
+
 from fluidframework_amd import streams, summary
 from fluidframework_amd.streams import MergeTreeStreamBuilder
 from mt_compare import compare_doc, emu_caps, emu_replay
@@ -151,8 +153,8 @@ def _wide_messages(n_keys):
     return m
 
 
-@pytest.mark.parametrize("n_keys", [5, 8])
-def test_prop_sets_up_to_eight_keys_match_oracle(orc, n_keys):
+@pytest.mark.parametrize("n_keys", [5, 8, 9, 17, 40, 64])
+def test_prop_sets_up_to_64_keys_match_oracle(orc, n_keys):
     b = MergeTreeStreamBuilder()
     d = b.begin_doc("", observer="A")
     for msg in _wide_messages(n_keys):
@@ -168,16 +170,16 @@ def test_prop_sets_up_to_eight_keys_match_oracle(orc, n_keys):
             continue  # more prop sets than the small tier holds: the runtime escalates to the large tier
         assert int(hdr[0]["status"]) == 0
         assert compare_doc((oh[0], ol[0], oc[0], op[0]), (hdr[0], leaves[0], chars[0], props[0])) == []
-        assert max(int(p["n"]) for p in op[0][: int(oh[0]["n_props"])]) == n_keys
+        assert max(int(p["n"]) for p in op[0][: int(oh[0]["n_props"])] if int(p["n"]) != PROPS_CONT) == n_keys
 
 
-def test_prop_set_beyond_eight_keys_is_a_capacity_error():
+def test_prop_set_beyond_64_keys_is_a_capacity_error():
     b = MergeTreeStreamBuilder()
     d = b.begin_doc("", observer="A")
-    for msg in _wide_messages(9):
+    for msg in _wide_messages(65):
         d.add_message(msg)
     hdr, *_ = emu_replay(b.finish(), large=True)
-    assert int(hdr[0]["status"]) == -3  # FMT_E_CAPACITY (include/fmt.h FMT_MT_PROPS_MAX)
+    assert int(hdr[0]["status"]) == -3  # FMT_E_CAPACITY (include/fmt.h FMT_MT_PROPS_KEYS_MAX)
 
 
 def _marker_messages():
