@@ -926,7 +926,15 @@ void MergeTree::loadSnapshot(const std::vector<LoadedSeg>& header, const std::ve
   root_->parent = nullptr;
   startCollaboration(0, minSeqArg, seqArg);  // loadHeader (snapshotLoader.ts:204-216)
   const Perspective p{false, 0, kNonCollabClient};
-  for (const LoadedSeg& l : body) insertSegments(getLocalLength(), make(l), p, Stamp{0, kNonCollabClient});
+  // (the local length grows by each appended segment: every loaded segment is present, so it is
+  // summed once rather than walked per append)
+  int localLen = getLocalLength();
+  for (const LoadedSeg& l : body) {
+    Seg* s = make(l);
+    const int len = s->len();
+    insertSegments(localLen, s, p, Stamp{0, kNonCollabClient});
+    localLen += len;
+  }
 }
 
 void MergeTree::startCollaboration(int localClientId, int minSeqArg, int currentSeqArg) {
