@@ -2947,7 +2947,16 @@ class HugeDoc {
       fail(FMT_E_CAPACITY);
       return;
     }
-    nGroups = static_cast<int>((nLeafBlk + kFill - 1) / kFill);
+    // kFill leaf blocks per group, more when that would take over 3/4 of the groups (a body appended
+    // 4 per block: 10M segments make 2.5M leaf blocks), leaving room for group splits either way
+    uint32_t fill = kFill;
+    if (nLeafBlk > static_cast<uint32_t>(kGroupCap / 4 * 3) * kFill)
+      fill = (nLeafBlk + kGroupCap / 4 * 3 - 1) / (kGroupCap / 4 * 3);
+    if (fill > static_cast<uint32_t>(kSlotCap) / 8 * 7) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    nGroups = static_cast<int>((nLeafBlk + fill - 1) / fill);
     if (nGroups > kGroupCap) {
       fail(FMT_E_CAPACITY);
       return;
@@ -2981,7 +2990,7 @@ class HugeDoc {
           S.bLeaf[b] = 1;
           S.bScour[b] = -1;
           S.bParent[b] = kNone;
-          const uint32_t g = b / kFill, s = b % kFill;
+          const uint32_t g = b / fill, s = b % fill;
           S.bGroup[b] = g;
           S.bSlot[b] = s;
           S.gSlotBlk[static_cast<size_t>(g) * kSlotCap + s] = b;
@@ -2994,7 +3003,7 @@ class HugeDoc {
     loadProps(nLeafBlk, pairs);
     if (status != FMT_OK) return;
     for (int g = 0; g < nGroups; g++) {
-      const uint32_t lo = static_cast<uint32_t>(g) * kFill, hi = lo + kFill < nLeafBlk ? lo + kFill : nLeafBlk;
+      const uint32_t lo = static_cast<uint32_t>(g) * fill, hi = lo + fill < nLeafBlk ? lo + fill : nLeafBlk;
       Lane<uint32_t> acc;
       FOR_LANES(l) { LANE(acc) = 0; }
       for (uint32_t base = lo; base < hi; base += 64) {
