@@ -75,6 +75,9 @@ def main():
                     help="t3: the loaded summary's shape: legacy = SnapshotLegacy.emit's header chunk (~10,000 "
                          "units) + body chunk; header = every segment in one header chunk")
     ap.add_argument("--t3-range", type=int, default=8, help="t3: max range length of removes/annotates")
+    ap.add_argument("--t3-check", action="store_true",
+                    help="t3: replay the whole document through the oracle too (one core, minutes at full size) "
+                         "and compare its state digest with the GPU's")
     ap.add_argument("--cpu-ops", type=int, default=200_000, help="t3: ops of the CPU baseline sample")
     ap.add_argument("--docs", type=int, default=None,
                     help="documents per GPU (mt, map) or in the whole batch (t2)")
@@ -735,6 +738,33 @@ def bench_t3(args, rank, world, local_rank, dist):
                          f"(BlockIdx), one thread (a single document's ops are one dependency chain)",
                "cpu_model": hc["model"]}
         log(rank, f"[bench] t3 cpu baseline {cpu['value']:.3g} ops/s ({done} ops in {ops_s:.1f}s)")
+    t3_check = None
+    if rank == 0 and args.t3_check:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # parity at full size (test infrastructure; after the timed region)
+
+        gpu_dig = eng.mt_digests()
+        oracle.set_index(True)
+        t = time.time()
+        import threading
+
+        res = {}
+        th = threading.Thread(target=lambda: res.update(r=oracle.mt_replay_digest(batch, threads=1)))
+        th.start()
+        while th.is_alive():  # (ctypes releases the GIL; progress lines keep the job runner from calling it hung)
+            th.join(30.0)
+            if th.is_alive():
+                log(rank, f"[bench] t3 oracle check: still running after {time.time() - t:.0f}s")
+        rc, odig, ost, _ = res["r"]
+        oracle.set_index(False)
+        t3_check = {"equal": bool(rc == 0 and int(odig[0]) == int(gpu_dig[0])), "oracle_rc": int(rc),
+                    "gpu_digest": f"{int(gpu_dig[0]):016x}", "oracle_digest": f"{int(odig[0]):016x}",
+                    "oracle_s": time.time() - t,
+                    "what": "state digest (every leaf field, props by value, text, header; DESIGN.md §2) of the whole "
+                            "replayed document, GPU vs the oracle's own full replay"}
+        log(rank, f"[bench] t3 oracle check: {t3_check}")
+        if not t3_check["equal"]:
+            raise SystemExit(f"t3: GPU state differs from the oracle's: {t3_check}")
     if rank == 0:
         h = hdrs[0]
         out = {
@@ -757,6 +787,7 @@ def bench_t3(args, rank, world, local_rank, dist):
                                     "block/heap updates; bandwidth is idle by construction",
                          "bytes_per_launch": bytes_per_launch, "avg_kernel_ms": avg_kernel_ms},
             "cpu_baseline": cpu,
+            "t3_oracle_check": t3_check,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
             "phase_clocks_per_op": {k: v / n_ops for k, v in prof.items() if k not in ("text_compactions", "merge_units_in_use")},
             "merge_area": {"compactions": prof.get("text_compactions"), "units_in_use": prof.get("merge_units_in_use")},

@@ -90,9 +90,11 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
   using S = fmt_mt::SmallTier;
   uint32_t* n1 = sched ? sched + 1 : nullptr;
   if (adjust) {  // annotate-adjust batches: the Adj variants, small tier over every document (no checkpoints)
+    // (1 wave/SIMD: 512 registers a wave; at 2 the property-manager code spilled 3710 VGPRs to scratch,
+    // at 1 the overflow lives in AGPRs)
     if (removeOrder)
-      return launchTier<true, S, true, kMtWaves, 2, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
-    return launchTier<true, S, false, kMtWaves, 2, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
+      return launchTier<true, S, true, kMtWaves, 1, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
+    return launchTier<true, S, false, kMtWaves, 1, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   }
   if (obliterate && removeOrder)
     return launchTier<true, S, true, kMtWaves, 2>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);

@@ -52,6 +52,30 @@ constexpr size_t kStageChunk = 8u << 20;
 constexpr int kStageWorkers = 8;
 constexpr size_t kStageMin = 16u << 20;  // smaller copies go straight through hipMemcpy
 
+// Pinned host memory the ctx keeps across calls (hipHostMalloc'd, grown on demand): DMA lands in it
+// directly, no staging copy.
+template <class T>
+struct PinnedBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    release();
+    void* q = nullptr;
+    const hipError_t e = hipHostMalloc(&q, (n ? n : 1) * sizeof(T), hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    p = static_cast<T*>(q);
+    cap = n;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  ~PinnedBuf() { release(); }
+};
+
 struct Stager {
   bool ready = false;
   void* buf[kStageWorkers][2] = {};
@@ -182,10 +206,10 @@ struct fmt_ctx {
   std::vector<std::string> sumBlobs;          // per document: header, then body
   std::vector<uint32_t> sumSplit;             // per document: header length in sumBlobs[d]
   std::vector<int32_t> sumStatus;
-  std::vector<fmt_kernels::SumDocOut> sumHostDocs;  // host copies of the device runs / text / prop sets
-  std::vector<fmt_kernels::SumRun> sumHostRuns;
-  std::vector<uint16_t> sumHostText;
-  std::vector<fmt_mt_propset> sumHostProps;
+  PinnedBuf<fmt_kernels::SumDocOut> sumHostDocs;  // host copies of the device runs / text / prop sets
+  PinnedBuf<fmt_kernels::SumRun> sumHostRuns;
+  PinnedBuf<uint16_t> sumHostText;
+  PinnedBuf<fmt_mt_propset> sumHostProps;
   // annotate-adjust: rows, numbers of host value ids, host numbers sorted for number → id lookups,
   // per-document computed-number slabs and their counts
   DevBuf<fmt_mt_adjust> mtAdjusts;
@@ -1617,19 +1641,24 @@ int fmt_mt_summarize_legacy(fmt_ctx* c, const char* const* keys, uint32_t nKeys,
                               c->stream));
     FMT_HIP(c, fmt_kernels::launchGatherSpans(c->spans.p, static_cast<uint32_t>(sp.size()), c->packed.p, c->numCUs, c->stream));
   }
-  if (c->sumHostDocs.size() < nd) c->sumHostDocs.resize(nd);
-  if (c->sumHostRuns.size() < cur[0]) c->sumHostRuns.resize(cur[0]);
-  if (c->sumHostText.size() < cur[1]) c->sumHostText.resize(cur[1]);
-  if (c->sumHostProps.size() < propOff[nd] + 1) c->sumHostProps.resize(propOff[nd] + 1);
-  FMT_HIP(c, stagedCopy(c, c->sumHostDocs.data(), c->sumDocs.p, nd * sizeof(fmt_kernels::SumDocOut), false));
-  FMT_HIP(c, stagedCopy(c, c->sumHostRuns.data(), c->sumRuns.p, cur[0] * sizeof(fmt_kernels::SumRun), false));
-  FMT_HIP(c, stagedCopy(c, c->sumHostText.data(), c->sumText.p, cur[1] * sizeof(uint16_t), false));
-  if (propOff[nd]) FMT_HIP(c, stagedCopy(c, c->sumHostProps.data(), c->packed.p, propOff[nd] * sizeof(fmt_mt_propset), false));
-  const fmt_kernels::SumDocOut* docs = c->sumHostDocs.data();
-  const fmt_kernels::SumRun* runs = c->sumHostRuns.data();
-  const uint16_t* text = c->sumHostText.data();
+  // (pinned destinations the ctx keeps: four DMAs back to back on the stream, one wait)
+  FMT_HIP(c, c->sumHostDocs.reserve(nd));
+  FMT_HIP(c, c->sumHostRuns.reserve(cur[0]));
+  FMT_HIP(c, c->sumHostText.reserve(cur[1]));
+  FMT_HIP(c, c->sumHostProps.reserve(propOff[nd] + 1));
+  FMT_HIP(c, hipMemcpyAsync(c->sumHostDocs.p, c->sumDocs.p, nd * sizeof(fmt_kernels::SumDocOut), hipMemcpyDeviceToHost, c->stream));
+  if (cur[0])
+    FMT_HIP(c, hipMemcpyAsync(c->sumHostRuns.p, c->sumRuns.p, cur[0] * sizeof(fmt_kernels::SumRun), hipMemcpyDeviceToHost, c->stream));
+  if (cur[1])
+    FMT_HIP(c, hipMemcpyAsync(c->sumHostText.p, c->sumText.p, cur[1] * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+  if (propOff[nd])
+    FMT_HIP(c, hipMemcpyAsync(c->sumHostProps.p, c->packed.p, propOff[nd] * sizeof(fmt_mt_propset), hipMemcpyDeviceToHost,
+                              c->stream));
+  const fmt_kernels::SumDocOut* docs = c->sumHostDocs.p;
+  const fmt_kernels::SumRun* runs = c->sumHostRuns.p;
+  const uint16_t* text = c->sumHostText.p;
   std::vector<const fmt_mt_propset*> propsHost(nd);
-  for (uint32_t d = 0; d < nd; d++) propsHost[d] = c->sumHostProps.data() + propOff[d];
+  for (uint32_t d = 0; d < nd; d++) propsHost[d] = c->sumHostProps.p + propOff[d];
   // computed annotate-adjust numbers of the documents that have any
   std::vector<std::vector<double>> docNums(c->mtHasAdjust ? nd : 0);
   if (c->mtHasAdjust) {

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--docs", type=int, default=20000)
     ap.add_argument("--unique", type=int, default=2000)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--workload", choices=["mt", "map", "t3"], default="mt")
+    ap.add_argument("--workload", choices=["mt", "map", "t3", "ob"], default="mt")
     ap.add_argument("--segments", type=int, default=2_000_000, help="t3: segments of the loaded document")
     ap.add_argument("--t3-ops", type=int, default=200_000, help="t3: ops replayed")
     ap.add_argument("variants", nargs="*")
@@ -34,6 +34,11 @@ def main():
         return bench_map(a, paths)
     if a.workload == "t3":
         batch = workloads.t3_stream(a.segments, a.t3_ops)
+    elif a.workload == "ob":  # the reference's obliterate farms cycled to --docs documents (bench.py ob)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from golden_data import replay_fixtures
+
+        batch = workloads.replicate_batches([f[1] for f in replay_fixtures("replay_obliterate_2.3.0.npz")], a.docs)
     else:
         batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
     ref = native.Engine(0)

@@ -94,7 +94,31 @@ CW3 = ("mergetree_compact.hip", "launchTier<false, fmt_mt::CompactTier, false, k
 HW8 = [("huge_engine.h", "  static constexpr int kWaves = 4;", "  static constexpr int kWaves = 8;"),
        ("huge_engine.h", "  int32_t glN[4];", "  int32_t glN[8];")]
 
+# the small tier's obliterate variant (escalated obliterate documents) at 1 wave/SIMD: 512 registers a
+# wave, so its 32 spilled VGPRs go to AGPRs instead of scratch memory
+OB_S1 = ("mergetree.hip", "    return launchTier<true, S, false, kMtWaves, 2>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);",
+         "    return launchTier<true, S, false, kMtWaves, 1>(batch, out, esc2 + 1, count, esc, numCUs, stream, esc2, n1);")
+
+# op records and insert text through a wave-uniform base (SGPRs) plus a small lane offset, so the
+# loads take the saddr form and neither the loop index nor the arena pointers live in VGPRs (the
+# compact kernel kept `in.ops` as a VGPR pair, spilled it, and its reload's vmcnt(0) waited for the
+# next op's text prefetch every op)
+FETCH_UNI = [("mt_engine.h", """    if (i < in.end) {
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(in.ops + i);
+      FOR_LANES(l) { LANE(x) = l < 8 ? p[l] : 0u; }
+    } else {""", """    if (i < in.end) {
+      const uint32_t k = uni(static_cast<uint32_t>(i - in.begin));  // (documents below 2^32 ops)
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(in.ops + in.begin) + static_cast<uint64_t>(k) * 8u;
+      FOR_LANES(l) { LANE(x) = l < 8 ? p[l] : 0u; }
+    } else {"""),
+             ("mt_engine.h", """    FOR_LANES(l) { LANE(x) = l < len ? static_cast<uint32_t>(in.text[payload + l]) : 0u; }
+    return x;""", """    const uint16_t* t = in.text + uni(payload);
+    FOR_LANES(l) { LANE(x) = l < len ? static_cast<uint32_t>(t[l]) : 0u; }
+    return x;""")]
+
 VARIANTS = {
+    "fetch_uni": FETCH_UNI,
+    "ob_s1": [OB_S1],
     "hw8": HW8,
     "prof": [PROF],
     "cw3": [CW3],
