@@ -157,6 +157,8 @@ struct HugeState {
   uint64_t textCap;   // end of the merge area: two halves of (textCap - textLen) / 2 units, one in use
   uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
   uint32_t* cuIds;    // [idCap]: the current catch-up op's delta leaves in document order (or nullptr)
+  uint32_t* rmIds;    // [idCap]: the current remove-order op's already-removed hits; at output, leaf id ->
+                      // output index (or nullptr: no remove-order recording)
 };
 
 // LDS state of the wave.
@@ -209,6 +211,9 @@ struct HugeInputs {
   // catch-up ranges of FMT_MT_F_CATCHUP ops (the document's slab; nullptr: the batch records none)
   fmt_mt_catchup_range* catchup;
   uint32_t catchupCap;
+  // remove-order entries of FMT_MT_F_RMORDER ops (the document's slab; nullptr: none recorded)
+  fmt_mt_remove_order* rmOrder;
+  uint32_t rmOrderCap;
 };
 
 // The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
@@ -286,6 +291,13 @@ class HugeDoc {
   // catch-up recording (FMT_MT_F_CATCHUP ops): ranges written, the op's delta leaves, its index
   uint32_t cuN = 0, cuIdN = 0, opIdx = 0;
   bool cuRec = false;
+  // remove-order recording (FMT_MT_F_RMORDER ops, SnapshotV1): entries written, the op's hits on
+  // leaves already removed, split copies pending (at most two splits per op), the op's stamp kind
+  uint32_t rmN = 0, rmHitN = 0;
+  bool rmRec = false;
+  int rmPendN = 0;
+  uint32_t rmPendFrom[2] = {0, 0}, rmPendTo[2] = {0, 0};
+  uint32_t rmKind = FMT_MT_RM_SET;
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
@@ -1500,6 +1512,11 @@ class HugeDoc {
     regsInsert(R, k + 1, y, wy);
     st1(S.leafBlk + y.id, b);
     obRefsMove(x.id, y.id, o, -o);  // the right part takes the references at/after the split
+    if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
+      rmPendFrom[rmPendN] = x.id;
+      rmPendTo[rmPendN] = y.id;
+      rmPendN++;
+    }
     const uint32_t nb = commitBlock(R);
     if (nb != kNone && k + 1 >= kMaxNodes / 2) {
       *rb = nb;
@@ -1767,6 +1784,8 @@ class HugeDoc {
     if (!was) {
       x.rm = seq;
       if (cuRec) cuPush(x.id);  // removedSegments: hits not removed before this op (mergeTree.ts:2314-2321)
+    } else if (rmRec) {
+      rmPushHit(x.id);  // a later remove stamp (stamps.ts:144-158), recorded in rmFlush
     }
     if (c < 32) x.mlo |= 1u << c;
     else x.mhi |= 1u << (c - 32);
@@ -1984,6 +2003,23 @@ class HugeDoc {
       }
     }
     if (!(any && newestClient != client)) return;
+    if (rmRec) {  // SnapshotV1: every stamp but the first (rm_seq) is a remove-order entry (mergeTree.ts:1715-1725)
+      bool firstSkipped = false;
+      for (int i = 0; i < obStartN && status == FMT_OK; i++) {
+        const int slot = obU(L->obStart, i);
+        const int64_t si = ordOf(uni(L->ob[slot].startId));
+        if (!(si >= 0 && si <= k)) break;
+        const int64_t ei = ordOf(uni(L->ob[slot].endId));
+        if (!(ei >= 0 && ei >= k)) continue;
+        const int oseq = uni(L->ob[slot].seq), ocl = uni(L->ob[slot].client);
+        if (oseq <= refSeq || ocl == client) continue;
+        if (!firstSkipped && oseq == minSeqOther) {
+          firstSkipped = true;
+          continue;
+        }
+        rmAppend(id, ocl, oseq, FMT_MT_RM_SLICE);
+      }
+    }
     uint32_t b;
     int kk;
     locate(id, &b, &kk);
@@ -2105,6 +2141,51 @@ class HugeDoc {
       return;
     }
     obAdd(sId, sOff, eId, eOff, seq, c);
+  }
+
+  // ------------------------------------------------------------------ remove order (SnapshotV1)
+  // As mt_engine.h rmAppend / rmFlush: an FMT_MT_F_RMORDER REMOVE or obliterate that hits an
+  // already-removed leaf adds the op's stamp to it; the right part of a split leaf inherits the left
+  // part's entries; obliterate-on-insert adds every overlapping stamp past the first. Entries hold
+  // leaf ids until writeOutputs turns them into output indices (FMT_MT_LEAF_GONE once dropped).
+  FMT_DEV void rmAppend(uint32_t id, int client, int seq, uint32_t kind) {
+    if (in.rmOrder == nullptr || rmN >= in.rmOrderCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    FOR_LANES(l) {
+      if (l == 0) {
+        fmt_mt_remove_order e;
+        e.leaf = id;
+        e.client = client;
+        e.seq = seq;
+        e.kind = kind;
+        in.rmOrder[rmN] = e;
+      }
+    }
+    waveSync();
+    rmN++;
+  }
+  FMT_DEV void rmPushHit(uint32_t id) {
+    if (rmHitN >= S.idCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    st1(S.rmIds + rmHitN, id);
+    rmHitN++;
+  }
+  FMT_DEV void rmFlush(int client, int seq) {
+    for (int q = 0; q < rmPendN && status == FMT_OK; q++) {
+      const uint32_t n0 = rmN;
+      for (uint32_t k = 0; k < n0 && status == FMT_OK; k++) {
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(in.rmOrder + k);
+        if (ldu(e) == rmPendFrom[q]) rmAppend(rmPendTo[q], ldi(reinterpret_cast<const int32_t*>(e + 1)),
+                                             ldi(reinterpret_cast<const int32_t*>(e + 2)), ldu(e + 3));
+      }
+    }
+    rmPendN = 0;
+    for (uint32_t q = 0; q < rmHitN && status == FMT_OK; q++) rmAppend(ldu(S.rmIds + q), client, seq, rmKind);
+    rmHitN = 0;
   }
 
   // ------------------------------------------------------------------ catch-up ranges
@@ -3144,6 +3225,9 @@ class HugeDoc {
 #endif
       cuRec = (op.flags & FMT_MT_F_CATCHUP) != 0 && in.catchup != nullptr && S.cuIds != nullptr;
       cuIdN = 0;
+      rmRec = (op.flags & FMT_MT_F_RMORDER) != 0 && in.rmOrder != nullptr && S.rmIds != nullptr;
+      rmKind = op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE;
+      rmHitN = 0;
       opIdx = static_cast<uint32_t>(i - in.begin);
       if (op.client > 63) fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_INSERT) insertText(op);
@@ -3155,9 +3239,10 @@ class HugeDoc {
       } else {
         fail(FMT_E_UNSUPPORTED);
       }
-      if ((op.flags & FMT_MT_F_RMORDER) != 0 || ((op.flags & FMT_MT_F_CATCHUP) != 0 && !cuRec)) fail(FMT_E_UNSUPPORTED);
+      if (((op.flags & FMT_MT_F_RMORDER) != 0 && !rmRec) || ((op.flags & FMT_MT_F_CATCHUP) != 0 && !cuRec)) fail(FMT_E_UNSUPPORTED);
       if (cuRec && status == FMT_OK) recordCatchup(op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
-      cuRec = false;
+      if ((rmPendN > 0 || rmHitN > 0) && status == FMT_OK) rmFlush(op.client, op.seq);
+      cuRec = rmRec = false;
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       for (int z = 0; z < 2 && status == FMT_OK; z++) {
         if (z == 1) {
@@ -3327,6 +3412,7 @@ class HugeDoc {
             x.block = static_cast<uint16_t>(blk & 0xFFFFu);
             x.pad = static_cast<uint16_t>((blk >> 16) | (mMarker(m) ? FMT_MT_LEAF_MARKER : 0u));
             outLeaves[o] = x;
+            if (S.rmIds != nullptr) S.rmIds[rd(S.lId + i)] = static_cast<uint32_t>(o);  // (remove-order entries)
             const uint32_t t = rd(S.lText + i);
             for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(textAt(t + c));
           }
@@ -3345,6 +3431,18 @@ class HugeDoc {
         outProps[p] = ps;
       }
     }
+    waveSync();
+    // remove-order entries: leaf id -> output index, FMT_MT_LEAF_GONE once zamboni dropped the leaf
+    for (uint32_t base = 0; status == FMT_OK && S.rmIds != nullptr && base < rmN; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t k = base + l;
+        if (k < rmN) {
+          uint32_t* e = reinterpret_cast<uint32_t*>(in.rmOrder + k);
+          const uint32_t id = rd(e);
+          e[0] = rd(S.leafBlk + id) == kNone ? FMT_MT_LEAF_GONE : rd(S.rmIds + id);
+        }
+      }
+    }
     const int d = status == FMT_OK ? depth() : 0;
     FOR_LANES(l) {
       if (l == 0) {
@@ -3360,7 +3458,7 @@ class HugeDoc {
         h.depth = static_cast<uint32_t>(d);
         h.visible_len = static_cast<uint32_t>(visible);
         h.n_catchup = cuN;
-        h.n_rm_order = 0;
+        h.n_rm_order = rmN;
         *hdr = h;
       }
     }
@@ -3378,6 +3476,9 @@ class HugeDoc {
     nWin = 0;
     cuN = cuIdN = 0;
     cuRec = false;
+    rmN = rmHitN = 0;
+    rmRec = false;
+    rmPendN = 0;
     nFree = 0;
     nProps = 0;
     textTop = S.textLen;

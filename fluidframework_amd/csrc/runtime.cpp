@@ -174,8 +174,8 @@ struct fmt_ctx {
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
   // documents that outgrow the large tier replay again, from their start, in the huge tier when
-  // they hold nothing it does not (mtHugeOk: no remove-order recording, relative positions,
-  // annotate-adjust or SnapshotV1 merge info); their starts
+  // they hold nothing it does not (mtHugeOk: no relative positions, annotate-adjust or SnapshotV1
+  // merge info); their starts
   std::vector<uint8_t> mtHugeOk;
   std::vector<uint8_t> mtSegProps;           // per document: a loaded segment has properties
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
@@ -749,6 +749,16 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
     if ((e = alloc(static_cast<size_t>(S.idCap) * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
     S.cuIds = static_cast<uint32_t*>(p);
   }
+  // remove-order entries (SnapshotV1) go to the document's slab too
+  I.rmOrder = nullptr;
+  I.rmOrderCap = 0;
+  S.rmIds = nullptr;
+  if (c->mtHasRmOrder && c->mtRmOffsHost[d + 1] > c->mtRmOffsHost[d]) {
+    I.rmOrder = c->mtRmOrder.p + c->mtRmOffsHost[d];
+    I.rmOrderCap = static_cast<uint32_t>(std::min<uint64_t>(c->mtRmOffsHost[d + 1] - c->mtRmOffsHost[d], 0xFFFFFFFFull));
+    if ((e = alloc(static_cast<size_t>(S.idCap) * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    S.rmIds = static_cast<uint32_t*>(p);
+  }
   I.shape = nullptr;
   if (!H.shape.empty()) {
     if ((e = alloc(H.shape.size() * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
@@ -1119,7 +1129,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
       const fmt_mt_op& op = b->ops[i];
       if (op.type == FMT_MT_INSERT) chars += fmt_mt_op_len(&op);
-      if ((op.flags & (FMT_MT_F_RMORDER | FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) ||
+      if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) ||
           (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
         ok = 0;
     }
@@ -1165,7 +1175,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (!c->mtHugeOk[d]) {  // (V1 merge info, remove order, relative positions, annotate-adjust)
+      if (!c->mtHugeOk[d]) {  // (V1 merge info, relative positions, annotate-adjust)
         refuse(d, FMT_E_UNSUPPORTED);
         continue;
       }

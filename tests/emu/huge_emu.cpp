@@ -23,9 +23,9 @@ extern "C" {
 // A document that does not start from a summary starts from its initial text (one segment stamped
 // {0, FMT_LOCAL_CLIENT}) or empty, as the runtime replays documents that outgrow the large tier.
 // With catchup != nullptr the catch-up ranges of FMT_MT_F_CATCHUP ops go there (capCatchup ranges).
-int emu_huge_replay_cu(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
-                       uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, fmt_mt_catchup_range* catchup,
-                       uint32_t capCatchup) {
+int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+                        uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, fmt_mt_catchup_range* catchup,
+                        uint32_t capCatchup, fmt_mt_remove_order* rmOrder, uint32_t capRm) {
   const bool loaded = b->snapshots != nullptr && b->snapshots[d].loaded;
   fmt_mt_snapshot_doc sd{};
   fmt_mt_snapshot_seg initSeg{};
@@ -84,6 +84,8 @@ int emu_huge_replay_cu(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr
   S.props = pr.data();
   std::vector<uint32_t> cuIds(catchup != nullptr ? S.idCap : 0);
   S.cuIds = catchup != nullptr ? cuIds.data() : nullptr;
+  std::vector<uint32_t> rmIds(rmOrder != nullptr ? S.idCap : 0);
+  S.rmIds = rmOrder != nullptr ? rmIds.data() : nullptr;
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));
   auto doc = std::make_unique<HugeDoc>();
@@ -102,6 +104,8 @@ int emu_huge_replay_cu(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr
   in.segProps = segProps ? 1u : 0u;
   in.catchup = catchup;
   in.catchupCap = capCatchup;
+  in.rmOrder = rmOrder;
+  in.rmOrderCap = capRm;
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
@@ -115,7 +119,7 @@ int emu_huge_replay_cu(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr
 
 int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
                     uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
-  return emu_huge_replay_cu(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0);
+  return emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0, nullptr, 0);
 }
 
 }  // extern "C"

@@ -58,15 +58,18 @@ def huge_emu_lib(tiny_groups=False):
         L = ctypes.CDLL(path)
         L.emu_huge_replay.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
-        L.emu_huge_replay_cu.argtypes = L.emu_huge_replay.argtypes + [ctypes.c_void_p, ctypes.c_uint32]
+        L.emu_huge_replay_rec.argtypes = L.emu_huge_replay.argtypes + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                                      ctypes.c_uint32]
         _huge[tiny_groups] = L
     return _huge[tiny_groups]
 
 
-def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=False, cap_catchup=0):
+def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=False, cap_catchup=0, cap_rm=0):
     """(header, leaves, chars, props) of document `doc` replayed by the emulated huge engine, plus its
-    catch-up ranges (header n_catchup of them) when cap_catchup > 0."""
-    from fluidframework_amd.native import CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+    catch-up ranges (header n_catchup of them) when cap_catchup > 0, then its remove-order entries
+    (header n_rm_order of them) when cap_rm > 0."""
+    from fluidframework_amd.native import (CATCHUP_DTYPE, DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, RM_ORDER_DTYPE,
+                                           batch_struct)
 
     sd = batch.snapshots[doc] if batch.snapshots is not None else None
     segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 1
@@ -79,13 +82,17 @@ def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=F
     props = np.zeros(4096, dtype=PROPSET_DTYPE)
     b, keep = batch_struct(batch)
     cu = np.zeros(max(cap_catchup, 1), dtype=CATCHUP_DTYPE)
-    huge_emu_lib(tiny_groups).emu_huge_replay_cu(ctypes.addressof(b), doc, _p(hdr), _p(leaves), cap_leaves, _p(chars), cap_chars,
-                                      _p(props), _p(cu) if cap_catchup else None, cap_catchup)
+    rm = np.zeros(max(cap_rm, 1), dtype=RM_ORDER_DTYPE)
+    huge_emu_lib(tiny_groups).emu_huge_replay_rec(ctypes.addressof(b), doc, _p(hdr), _p(leaves), cap_leaves, _p(chars),
+                                                  cap_chars, _p(props), _p(cu) if cap_catchup else None, cap_catchup,
+                                                  _p(rm) if cap_rm else None, cap_rm)
     del keep
     h = hdr[0]
     out = h, leaves[: int(h["n_leaves"])], chars[: int(h["n_chars"])], props[: int(h["n_props"])]
     if cap_catchup:
-        return out + (cu[: int(h["n_catchup"])],)
+        out = out + (cu[: int(h["n_catchup"])],)
+    if cap_rm:
+        out = out + (rm[: int(h["n_rm_order"])],)
     return out
 
 

@@ -161,14 +161,19 @@ def test_huge_loaded_markers(orc, engine):
 
 def test_unsupported_huge_document_fails_alone(orc, engine):
     """A summary-loaded document past the large tier that asks for something the huge tier does not
-    record (here remove-order recording) fails alone, with FMT_E_UNSUPPORTED in its own header: the
+    resolve (here a relative position) fails alone, with FMT_E_UNSUPPORTED in its own header: the
     ordinary and huge documents beside it replay as in a batch without it."""
-    from fluidframework_amd.streams import MT_F_RMORDER
+    import dataclasses
+
+    from fluidframework_amd.streams import MT_F_REL1, NO_MARKER, RELPOS_DTYPE
     farm = workloads.conflict_farm(24, n_clients=8, ops_per_doc=600, seed=8)
     t3a = workloads.t3_stream(3000, 4000, n_clients=31, max_lag=700, seed=9)
     bad = workloads.t3_stream(9000, 6000, n_clients=63, max_lag=4096, max_range=20, seed=10)
-    bad.ops["flags"][bad.ops["type"] == 1] |= MT_F_RMORDER
+    first_insert = int(np.nonzero(bad.ops["type"] == 0)[0][0])
+    bad.ops["flags"][first_insert] |= MT_F_REL1
+    bad.ops["pos1"][first_insert] = 0  # (row 0 of the relpos table below)
     batch = _concat([farm, t3a, bad, farm])
+    batch = dataclasses.replace(batch, relpos=np.array([(NO_MARKER, 0, 0, 0)], dtype=RELPOS_DTYPE))
     engine.mt_load(batch)
     engine.mt_run()
     hdrs = engine.mt_headers(raise_on_failed_docs=False)
@@ -178,18 +183,10 @@ def test_unsupported_huge_document_fails_alone(orc, engine):
         if d == bad_doc:
             continue
         assert int(hdrs[d]["status"]) == 0, d
-        rc, exp = _oracle(orc, _strip_rmorder(batch), d)
+        rc, exp = _oracle(orc, batch, d)
         assert rc == 0
         lv, ch, pr = engine.mt_doc(d, hdrs[d])
         assert compare_doc(exp, (hdrs[d], lv, ch, pr)) == [], d
-
-
-def _strip_rmorder(batch):
-    from fluidframework_amd.streams import MT_F_RMORDER
-    b = copy.copy(batch)
-    b.ops = batch.ops.copy()
-    b.ops["flags"] &= ~np.uint32(MT_F_RMORDER)
-    return b
 
 
 @pytest.mark.parametrize("segs,ops,props_every,seed", [
@@ -263,3 +260,35 @@ def test_huge_legacy_summary_with_catchup_on_gpu(orc, engine):
             summary.catchup_blob(summary.catchup_messages(msgs, ocu[0][: int(h["n_catchup"])], int(h["min_seq"]))))
     assert got == want
     assert got[1] is not None and got[2] is not None
+
+
+def test_huge_remove_order_on_gpu(orc, engine):
+    """SnapshotV1 remove order from a huge document (header + body summary, overlapping removes of
+    lagging writers): each leaf's remove stamps == the oracle's, and its V1 summary from GPU state ==
+    the one from the oracle's stamp lists."""
+    from fluidframework_amd import summary
+    from fluidframework_amd.streams import flag_remove_order
+    batch = workloads.as_legacy_load(workloads.t3_stream(40000, 20000, n_clients=63, max_lag=2000, max_range=60, seed=43))
+    flag_remove_order(batch.ops, batch.doc_op_offsets)
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+    rm = engine.mt_remove_order(0, hdrs[0])
+    assert len(rm) > 0
+    want = orc.mt_removers(batch, 0)
+    got = summary.removers_from_engine(lv, int(hdrs[0]["n_leaves"]), rm, batch.ops)
+    ms, multi = int(hdrs[0]["min_seq"]), 0
+    for i in range(int(hdrs[0]["n_leaves"])):
+        r = int(lv[i]["rm_seq"])
+        if r != summary.NOT_REMOVED and r > ms:
+            assert got.get(i) == want.get(i), i
+            multi += len(want[i]) > 1
+    assert multi > 0
+    names = [f"client-{k}" for k in range(64)]
+    assert summary.v1_summary(hdrs[0], lv, ch, pr, batch.keys, batch.values, names, got) == \
+        summary.v1_summary(hdrs[0], lv, ch, pr, batch.keys, batch.values, names, want)

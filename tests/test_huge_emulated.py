@@ -193,3 +193,52 @@ def test_huge_engine_catchup_ranges(orc, segs, ops, rng, tiny, seed, legacy):
     assert compare_doc(exp, tuple(got)) == []
     assert int(h["n_catchup"]) > n_flag // 2
     assert np.array_equal(cu, ocu[0][: int(h["n_catchup"])])
+
+
+def _removers_match(orc, batch, got, rm):
+    import sys
+
+    from fluidframework_amd import summary
+
+    h, lv = got[0], got[1]
+    want = orc.mt_removers(batch, 0)
+    ops = batch.ops[int(batch.doc_op_offsets[0]) : int(batch.doc_op_offsets[1])]
+    mine = summary.removers_from_engine(lv, int(h["n_leaves"]), rm, ops)
+    ms, multi = int(h["min_seq"]), 0
+    for i in range(int(h["n_leaves"])):
+        r = int(lv[i]["rm_seq"])
+        if r != summary.NOT_REMOVED and r > ms:
+            assert mine.get(i) == want.get(i), (i, mine.get(i), want.get(i))
+            multi += len(want[i]) > 1
+    return multi
+
+
+@pytest.mark.parametrize("tiny", [False, True])
+def test_huge_engine_remove_order(orc, tiny):
+    """Remove-order entries (SnapshotV1's removedClientIds order, snapshotV1.ts:207-265) recorded by
+    the huge engine for the REMOVEs above the final minSeq: every leaf's stamp list == the oracle's."""
+    from fluidframework_amd.streams import flag_remove_order
+    batch = workloads.t3_stream(3000, 8000, n_clients=31, max_lag=600, max_range=60, seed=41)
+    flag_remove_order(batch.ops, batch.doc_op_offsets)
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=tiny, cap_rm=1 << 16)
+    assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+    assert compare_doc(exp, got[:4]) == []
+    assert int(got[0]["n_rm_order"]) > 0
+    assert _removers_match(orc, batch, got, got[4]) > 0
+
+
+def test_huge_engine_remove_order_with_obliterates(orc):
+    """The same with obliterates (sliceRemove stamps, obliterate-on-insert) on a farm past the large
+    tier (135,000-unit initial text)."""
+    from test_huge_obliterate import _one
+    from test_obliterate import long_obliterate_farms
+
+    from fluidframework_amd.streams import flag_remove_order
+    for doc in (0, 4):
+        one = _one(long_obliterate_farms(extra=135000), doc)
+        flag_remove_order(one.ops, one.doc_op_offsets)
+        got = emu_huge_replay(one, 0, cap_rm=1 << 16)
+        assert int(got[0]["status"]) == 0, doc
+        _removers_match(orc, one, got, got[4])
