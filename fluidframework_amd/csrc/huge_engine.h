@@ -208,6 +208,10 @@ struct HugeInputs {
   // replay harness inserts it locally before collaborating, client.replay.spec.ts:30-33)
   int32_t initClient;
   uint32_t segProps;  // some loaded segment has properties
+  // SnapshotV1 merge info of the loaded segments (aligned with segs; nullptr: none) and the batch's
+  // remove stamps its rows index (specToSegment, snapshotLoader.ts:105-175)
+  const fmt_mt_snapshot_info* info;
+  const fmt_mt_stamp* stamps;
   // catch-up ranges of FMT_MT_F_CATCHUP ops (the document's slab; nullptr: the batch records none)
   fmt_mt_catchup_range* catchup;
   uint32_t catchupCap;
@@ -3043,6 +3047,11 @@ class HugeDoc {
       return;
     }
     // leaf blocks (lane = block): their leaves, count, stable sum, group slot
+    Lane<bool> winL, wideL;  // some leaf stamped above minSeq; a writer past 63 (merge info)
+    FOR_LANES(l) {
+      LANE(winL) = false;
+      LANE(wideL) = false;
+    }
     for (uint32_t base = 0; base < nLeafBlk; base += 64) {
       FOR_LANES(l) {
         const uint32_t b = base + l;
@@ -3055,17 +3064,34 @@ class HugeDoc {
             const size_t i = static_cast<size_t>(b) * 8 + k;
             const fmt_mt_snapshot_seg sg = in.segs[j];
             const uint32_t len = sg.len & ~FMT_MT_SEG_MARKER;
+            int32_t ins = 0, rm = kNotRemoved, client = in.initClient;
+            uint64_t mask = 0;
+            if (in.info != nullptr) {  // merge info: the insert stamp, the remove stamps folded
+              const fmt_mt_snapshot_info inf = in.info[j];
+              ins = inf.ins_seq;
+              client = inf.ins_client;
+              for (uint32_t t = 0; t < inf.rm_count; t++) {
+                const fmt_mt_stamp st = in.stamps[inf.rm_first + t];
+                rm = st.seq < rm ? st.seq : rm;
+                if (st.client < 0 || st.client > 63) LANE(wideL) = true;
+                else mask |= 1ull << st.client;
+              }
+              if (client > 63) LANE(wideL) = true;
+            }
             S.lLen[i] = len;
-            S.lIns[i] = 0;
-            S.lRm[i] = kNotRemoved;
-            S.lMlo[i] = 0;
-            S.lMhi[i] = 0;
+            S.lIns[i] = ins;
+            S.lRm[i] = rm;
+            S.lMlo[i] = static_cast<uint32_t>(mask);
+            S.lMhi[i] = static_cast<uint32_t>(mask >> 32);
             S.lId[i] = j + 1;
             S.lText[i] = sg.text;
-            S.lMeta[i] = mkMeta(in.initClient, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
+            S.lMeta[i] = mkMeta(client, kNoProps) | ((sg.len & FMT_MT_SEG_MARKER) != 0 ? kMetaMarker : 0u);
             S.leafBlk[j + 1] = b;
             S.winIdx[j + 1] = kNone;
-            sum += static_cast<int>(len);
+            // (a leaf stamped above minSeq is a window entry, added below; a removed one counts nowhere)
+            const bool win = ins > in.snapMinSeq || (rm != kNotRemoved && rm > in.snapMinSeq);
+            if (win) LANE(winL) = true;
+            else if (rm == kNotRemoved) sum += static_cast<int>(len);
           }
           S.bCount[b] = c;
           S.bLeaf[b] = 1;
@@ -3081,6 +3107,11 @@ class HugeDoc {
     }
     nextId = N + 1;
     waveSync();
+    if (ballot(wideL) != 0) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    const bool anyWin = ballot(winL) != 0;
     loadProps(nLeafBlk, pairs);
     if (status != FMT_OK) return;
     for (int g = 0; g < nGroups; g++) {
@@ -3138,6 +3169,46 @@ class HugeDoc {
     lastBlk = nLeafBlk - 1;
     minSeq = in.snapMinSeq;
     curSeq = in.snapSeq;
+    if (anyWin) loadWindow(nLeafBlk);
+  }
+
+  // Loaded leaves whose merge info is above minSeq enter the window table (their lengths differ
+  // between perspectives), in document order; the stable sums above left them out.
+  FMT_DEV void loadWindow(uint32_t nLeafBlk) {
+    for (uint32_t base = 0; base < nLeafBlk * 8 && status == FMT_OK; base += 64) {
+      Lane<bool> w;
+      FOR_LANES(l) {
+        const uint32_t x = base + l, b = x >> 3, k = x & 7;
+        bool v = false;
+        if (b < nLeafBlk && k < rd(S.bCount + b)) {
+          const size_t i = li(b, static_cast<int>(k));
+          const int32_t ins = rd(S.lIns + i), rm = rd(S.lRm + i);
+          v = ins > minSeq || (rm != kNotRemoved && rm > minSeq);
+        }
+        LANE(w) = v;
+      }
+      for (uint64_t m = ballot(w); m != 0 && status == FMT_OK; m &= m - 1) {
+        const uint32_t x = base + static_cast<uint32_t>(ctz64(m)), b = x >> 3;
+        const Leaf y = getLeaf(b, static_cast<int>(x & 7));
+        const uint64_t mask = static_cast<uint64_t>(y.mlo) | (static_cast<uint64_t>(y.mhi) << 32);
+        // window meta: insert client | first remover << 8 | more removers << 16 (as removeLeaf leaves it)
+        uint32_t first = 0;
+        if (y.rm != kNotRemoved) {
+          const fmt_mt_snapshot_info inf = in.info[y.id - 1];
+          for (uint32_t t = 0; t < inf.rm_count; t++) {
+            const fmt_mt_stamp st = in.stamps[inf.rm_first + t];
+            if (st.seq == y.rm) {
+              first = static_cast<uint32_t>(st.client);
+              break;
+            }
+          }
+        }
+        const uint32_t meta = (static_cast<uint32_t>(mClient(y.meta)) & 0xFFu) | (first << 8) |
+                              (__builtin_popcountll(mask) > 1 ? 1u << 16 : 0u);
+        winAdd(y.id, y.ins, y.rm, y.len, meta, ldu(S.bGroup + b), b, y.mlo, y.mhi);
+      }
+    }
+    invalidate();
   }
 
   // The loaded segments' properties (IJSONTextSegment.props: the segment's properties are a clone of

@@ -175,7 +175,7 @@ struct fmt_ctx {
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
   // documents that outgrow the large tier replay again, from their start, in the huge tier when
   // they hold nothing it does not (mtHugeOk: no relative positions, annotate-adjust or SnapshotV1
-  // merge info); their starts
+  // body segments with merge info, FMT_MT_F_LOADSEG); their starts
   std::vector<uint8_t> mtHugeOk;
   std::vector<uint8_t> mtSegProps;           // per document: a loaded segment has properties
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
@@ -739,6 +739,13 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   I.segs = segsDev;
   I.nSegs = static_cast<uint32_t>(N);
   I.segProps = c->mtSegProps.empty() ? 0u : c->mtSegProps[d];
+  // SnapshotV1 merge info of a summary-loaded document's segments (header chunk)
+  I.info = nullptr;
+  I.stamps = nullptr;
+  if (c->mtHasSnapInfo && c->mtSnapHost.size() > d && c->mtSnapHost[d].loaded) {
+    I.info = c->mtSnapInfo.p + c->mtSnapHost[d].first_seg;
+    I.stamps = c->mtSnapStamps.p;
+  }
   // catch-up ranges go to the document's slab, as in the other tiers
   I.catchup = nullptr;
   I.catchupCap = 0;
@@ -1142,8 +1149,6 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
         }
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
-      for (uint64_t k = sd.first_seg; b->snapshot_info != nullptr && k < sd.first_seg + sd.n_header; k++)
-        if (b->snapshot_info[k].ins_seq != 0 || b->snapshot_info[k].rm_count != 0) ok = 0;
     } else if (b->doc_init && b->doc_init[2 * d + 1] > 0) {
       c->mtStartSeg[d] = fmt_mt_snapshot_seg{b->doc_init[2 * d], b->doc_init[2 * d + 1], FMT_MT_NO_PROPS};
       chars += b->doc_init[2 * d + 1];
@@ -1175,7 +1180,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (!c->mtHugeOk[d]) {  // (V1 merge info, relative positions, annotate-adjust)
+      if (!c->mtHugeOk[d]) {  // (V1 body segments with merge info, relative positions, annotate-adjust)
         refuse(d, FMT_E_UNSUPPORTED);
         continue;
       }

@@ -102,6 +102,8 @@ int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   in.nSegs = N;
   in.shape = shape.empty() ? nullptr : shape.data();
   in.segProps = segProps ? 1u : 0u;
+  in.info = loaded && b->snapshot_info != nullptr ? b->snapshot_info + sd.first_seg : nullptr;
+  in.stamps = b->snapshot_stamps;
   in.catchup = catchup;
   in.catchupCap = capCatchup;
   in.rmOrder = rmOrder;

@@ -292,3 +292,18 @@ def test_huge_remove_order_on_gpu(orc, engine):
     names = [f"client-{k}" for k in range(64)]
     assert summary.v1_summary(hdrs[0], lv, ch, pr, batch.keys, batch.values, names, got) == \
         summary.v1_summary(hdrs[0], lv, ch, pr, batch.keys, batch.values, names, want)
+
+
+def test_huge_v1_merge_info_load_on_gpu(orc, engine):
+    """A huge document loaded from a SnapshotV1 summary whose header segments carry merge info above
+    minSeq (inserted by writers, removed by one to three of them): == oracle on the GPU."""
+    from v1_huge import with_v1_merge_info
+    batch = with_v1_merge_info(workloads.t3_stream(30000, 20000, n_clients=31, max_lag=800, max_range=8, seed=52))
+    rc, exp = _oracle(orc, batch)
+    assert rc == 0
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []

@@ -242,3 +242,17 @@ def test_huge_engine_remove_order_with_obliterates(orc):
         got = emu_huge_replay(one, 0, cap_rm=1 << 16)
         assert int(got[0]["status"]) == 0, doc
         _removers_match(orc, one, got, got[4])
+
+
+@pytest.mark.parametrize("tiny", [False, True])
+def test_huge_engine_v1_merge_info_load(orc, tiny):
+    """A huge document loaded from a SnapshotV1 summary whose header segments carry merge info above
+    minSeq (specToSegment's insert and remove stamps, snapshotLoader.ts:105-175): those leaves enter
+    the window table at load, and the replay == oracle."""
+    from v1_huge import with_v1_merge_info
+    batch = with_v1_merge_info(workloads.t3_stream(4000, 6000, n_clients=31, max_lag=800, max_range=8, seed=51))
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=tiny)
+    assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+    assert compare_doc(exp, got) == []
