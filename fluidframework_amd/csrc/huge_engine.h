@@ -54,7 +54,9 @@ constexpr int32_t kNotRemoved = 0x7fffffff;
 constexpr int kSlotCap = FMT_HUGE_SLOTCAP;  // leaf blocks listed per group
 constexpr int kGroupCap = 2048;       // groups
 constexpr int kHeapCap = 10240;       // LRU heap entries (≈ blocks registered in one window)
-constexpr int kPropCap = 4096;        // interned prop sets per document
+constexpr int kPropCap = 65534;       // interned prop sets per document (ids fit the meta word's 16 bits)
+constexpr int kPropLds = 4096;        // match classes of the first sets cached in LDS
+constexpr uint32_t kPropHash = 1u << 17;  // buckets per prop-set hash table (exact content, match class)
 constexpr int kPropWords = 1 + FMT_MT_PROPS_MAX;  // a prop set in HBM: n, kv[]
 constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
 
@@ -65,6 +67,13 @@ FMT_DEV uint32_t mkMeta(int32_t client, uint32_t props) { return (static_cast<ui
 constexpr uint32_t kMetaMarker = 1u << 24;  // the leaf is a Marker (mergeTreeNodes.ts:495-564)
 FMT_DEV bool mMarker(uint32_t m) { return (m & kMetaMarker) != 0; }
 constexpr uint32_t kNoProps = 0xFFFFu;
+FMT_DEV uint32_t mix32(uint32_t x) {  // (a 32-bit finalizer: prop-set hashes)
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  return x ^ (x >> 16);
+}
 
 // Window meta word: insert client (int8) | first remover (u8) << 8 | "more removers" << 16; the
 // record's word 3 adds the entry's group << 17
@@ -156,9 +165,14 @@ struct HugeState {
   uint64_t textLen;   // batch text (read-only part)
   uint64_t textCap;   // end of the merge area: two halves of (textCap - textLen) / 2 units, one in use
   uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
+  uint32_t* pClass;   // [kPropCap]: prop set id -> its match class (the first set with the same content)
+  uint32_t* pHead;    // [2 * kPropHash]: bucket heads (set id + 1, 0 = empty), exact content then class
+  uint32_t* pNext;    // [2 * kPropCap]: per set, the next set of its exact-content / class bucket
   uint32_t* cuIds;    // [idCap]: the current catch-up op's delta leaves in document order (or nullptr)
   uint32_t* rmIds;    // [idCap]: the current remove-order op's already-removed hits; at output, leaf id ->
                       // output index (or nullptr: no remove-order recording)
+  uint32_t* mkIds;    // [mkCap]: every marker leaf ever in the document, in insertion order (relative
+  uint32_t mkCap;     //   positions; nullptr: the batch has none)
 };
 
 // LDS state of the wave.
@@ -171,7 +185,7 @@ struct HugeLds {
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
   uint32_t tmp[256];
-  uint16_t pClass[kPropCap];     // prop set id -> its match class (the first set with the same content)
+  uint16_t pClass[kPropLds];     // S.pClass of the first kPropLds sets
   uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (lane k = entry k)
   int32_t cmd[8];                // pass command from wave 0 to the helper waves (HugeDoc::PassCmd)
   uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
@@ -218,6 +232,10 @@ struct HugeInputs {
   // remove-order entries of FMT_MT_F_RMORDER ops (the document's slab; nullptr: none recorded)
   fmt_mt_remove_order* rmOrder;
   uint32_t rmOrderCap;
+  // legacy relative positions (FMT_MT_F_REL1/REL2 ops index the table; nullptr: none in the batch)
+  const fmt_mt_relpos* relpos;
+  uint32_t nRelpos;
+  uint32_t markerKey;  // key id of "markerId"
 };
 
 // The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
@@ -302,6 +320,7 @@ class HugeDoc {
   int rmPendN = 0;
   uint32_t rmPendFrom[2] = {0, 0}, rmPendTo[2] = {0, 0};
   uint32_t rmKind = FMT_MT_RM_SET;
+  uint32_t mkN = 0;  // markers listed in S.mkIds
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
@@ -1390,7 +1409,9 @@ class HugeDoc {
   // ------------------------------------------------------------------ props
   // matchProperties (properties.ts:32-61, undefined ≡ {}) as equality of match classes: interned
   // sets with the same (key, value) content in any key order share the class of the first of them.
-  FMT_DEV uint32_t propClass(uint32_t a) const { return a == kNoProps ? 0xFFFFu : L->pClass[a]; }
+  FMT_DEV uint32_t propClass(uint32_t a) const {
+    return a == kNoProps ? 0xFFFFu : a < static_cast<uint32_t>(kPropLds) ? L->pClass[a] : rd(S.pClass + a);
+  }
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || uni(propClass(a)) == uni(propClass(b)); }
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
   // The working set lives in LDS (kvWork, lane k = entry k); a set wider than FMT_MT_PROPS_MAX entries
@@ -1437,16 +1458,26 @@ class HugeDoc {
       }
       waveSync();
     }
-    for (int base = 0; base < nProps; base += 64) {  // interned already?
-      Lane<bool> same;
-      FOR_LANES(l) {
-        const int p = base + l;
-        bool eq = p < nProps && rd(S.props + (p * kPropWords)) == cnt;
-        for (uint32_t i = 0; eq && i < cnt; i++) eq = setKv(static_cast<uint32_t>(p), i) == L->kvWork[i];
-        LANE(same) = eq;
-      }
-      const uint64_t m = ballot(same);
-      if (m) return static_cast<uint32_t>(base + ctz64(m));
+    // Interned already? Sets are found through two hash tables in HBM: one keyed by the ordered
+    // entries (the same set), one by the entries in any order (its match class).
+    Lane<uint32_t> ho, hu;
+    FOR_LANES(l) {
+      const bool on = l < static_cast<int>(cnt);
+      const uint32_t e = on ? L->kvWork[l] : 0u;
+      LANE(ho) = on ? mix32(e ^ (0x9E3779B9u * static_cast<uint32_t>(l + 1))) : 0u;
+      LANE(hu) = on ? mix32(e) : 0u;
+    }
+    uint32_t so, su;
+    waveExclusiveSum(ho, &so);
+    waveExclusiveSum(hu, &su);
+    const uint32_t bo = mix32(so + cnt) & (kPropHash - 1);
+    const uint32_t bu = kPropHash + (mix32(su ^ (cnt * 0x85EBCA6Bu)) & (kPropHash - 1));
+    for (uint32_t p = ldu(S.pHead + bo); p != 0; p = ldu(S.pNext + 2 * (p - 1))) {
+      const uint32_t q = p - 1;
+      if (ldu(S.props + q * kPropWords) != cnt) continue;
+      Lane<bool> diff;
+      FOR_LANES(l) { LANE(diff) = l < static_cast<int>(cnt) && setKv(q, static_cast<uint32_t>(l)) != L->kvWork[l]; }
+      if (ballot(diff) == 0) return q;
     }
     const int rec = cnt > FMT_MT_PROPS_MAX ? static_cast<int>((cnt + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1;
     if (nProps + rec > kPropCap) {
@@ -1454,33 +1485,38 @@ class HugeDoc {
       return kNoProps;
     }
     const uint32_t id = static_cast<uint32_t>(nProps);
-    uint32_t cls = cnt == 0 ? 0xFFFFu : id;
-    for (int base = 0; cnt > 0 && base < nProps && cls == id; base += 64) {  // same content, other key order?
-      Lane<bool> same;
+    uint32_t cls = cnt == 0 ? 0xFFFFu : id;  // same content, other key order? (the class bucket lists
+    for (uint32_t p = cnt > 0 ? ldu(S.pHead + bu) : 0u; p != 0 && cls == id; p = ldu(S.pNext + 2 * (p - 1) + 1)) {
+      const uint32_t q = p - 1;                //  only the first set of each class)
+      if (ldu(S.props + q * kPropWords) != cnt) continue;
+      Lane<bool> miss;
       FOR_LANES(l) {
-        const int p = base + l;
-        bool eq = p < nProps && rd(S.props + (p * kPropWords)) == cnt;
-        for (uint32_t i = 0; eq && i < cnt; i++) {
-          const uint32_t x = L->kvWork[i];
-          bool found = false;
-          for (uint32_t j = 0; j < cnt; j++)
-            if (setKv(static_cast<uint32_t>(p), j) == x) found = true;
-          eq = found;
-        }
-        LANE(same) = eq;
+        bool found = l >= static_cast<int>(cnt);
+        for (uint32_t j = 0; !found && j < cnt; j++) found = setKv(q, j) == L->kvWork[l];
+        LANE(miss) = !found;
       }
-      const uint64_t m = ballot(same);
-      if (m) cls = static_cast<uint32_t>(base + ctz64(m));
+      if (ballot(miss) == 0) cls = q;
     }
+    const uint32_t headO = ldu(S.pHead + bo), headU = ldu(S.pHead + bu);
     FOR_LANES(l) {
       const int q = l / FMT_MT_PROPS_MAX, k = l % FMT_MT_PROPS_MAX;
       if (q < rec) {
         const size_t r = static_cast<size_t>(id + q) * kPropWords;
         if (k == 0) {
+          const uint32_t c = q == 0 ? cls : 0xFFFEu;
           S.props[r] = q == 0 ? cnt : FMT_MT_PROPS_CONT;
-          L->pClass[id + q] = static_cast<uint16_t>(q == 0 ? cls : 0xFFFEu);
+          S.pClass[id + q] = c;
+          if (id + q < static_cast<uint32_t>(kPropLds)) L->pClass[id + q] = static_cast<uint16_t>(c);
         }
         S.props[r + 1 + k] = L->kvWork[l];
+      }
+      if (l == 0) {
+        S.pNext[2 * id] = headO;
+        S.pHead[bo] = id + 1;
+        if (cls == id) {
+          S.pNext[2 * id + 1] = headU;
+          S.pHead[bu] = id + 1;
+        }
       }
     }
     waveSync();
@@ -1623,6 +1659,7 @@ class HugeDoc {
     x.text = op.payload;
     x.meta = mkMeta(c, insProps) | ((op.flags & FMT_MT_F_MARKER) != 0 ? kMetaMarker : 0u);
     const uint32_t wx = winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, R.g, b);
+    if ((op.flags & FMT_MT_F_MARKER) != 0) markerAdd(x.id);
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);
     const uint32_t nb = commitBlock(R);
@@ -2190,6 +2227,132 @@ class HugeDoc {
     rmPendN = 0;
     for (uint32_t q = 0; q < rmHitN && status == FMT_OK; q++) rmAppend(ldu(S.rmIds + q), client, seq, rmKind);
     rmHitN = 0;
+  }
+
+  // ------------------------------------------------------------------ relative positions
+  // posFromRelativePos (mergeTree.ts:1462-1483), as mt_engine.h: the marker whose "markerId" holds
+  // the id (the last inserted one when several do), -1 when none does or it is removed; else its start
+  // in the op's perspective, then the side and offset. Markers are found through the document's
+  // marker list (every marker leaf inserted or loaded, dropped ones skipped), positioned through the
+  // group / slot index as the catch-up ranges are.
+  FMT_DEV void markerAdd(uint32_t id) {
+    if (S.mkIds == nullptr) return;
+    if (mkN >= S.mkCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    st1(S.mkIds + mkN, id);
+    mkN++;
+  }
+  FMT_DEV bool setHas(uint32_t p, uint32_t want) const {  // (lane-level) prop set p holds entry want
+    if (p == kNoProps) return false;
+    const uint32_t n = rd(S.props + p * kPropWords);
+    bool f = false;
+    for (uint32_t k = 0; k < n && k < FMT_MT_PROPS_KEYS_MAX; k++) f = f || setKv(p, k) == want;
+    return f;
+  }
+  // View start of leaf `id` from PriorPerspective(r, c)
+  FMT_DEV int viewStart(uint32_t id, int r, int c) {
+    uint32_t b;
+    int k;
+    locate(id, &b, &k);
+    invalidate();
+    groupCorrections(r, c);
+    const uint32_t g = ldu(S.bGroup + b), s = ldu(S.bSlot + b);
+    const int gp = groupPos(g);
+    int base = 0;
+    for (int q = 0; q < gp; q += 64) {
+      const Lane<uint32_t> len = groupLens(q);
+      Lane<uint32_t> part;
+      FOR_LANES(l) { LANE(part) = q + l < gp ? LANE(len) : 0u; }
+      uint32_t tot;
+      waveExclusiveSum(part, &tot);
+      base += static_cast<int>(tot);
+    }
+    slotLengths(g, r, c);
+    for (uint32_t q = 0; q < s; q += 64) {
+      Lane<uint32_t> part;
+      FOR_LANES(l) { LANE(part) = q + l < s ? static_cast<uint32_t>(L->sLen[q + l]) : 0u; }
+      uint32_t tot;
+      waveExclusiveSum(part, &tot);
+      base += static_cast<int>(tot);
+    }
+    const Lane<uint32_t> vis = blockVis(b, ldu(S.bCount + b), r, c);
+    Lane<uint32_t> part;
+    FOR_LANES(l) { LANE(part) = l < k ? LANE(vis) : 0u; }
+    uint32_t tot;
+    waveExclusiveSum(part, &tot);
+    invalidate();
+    return base + static_cast<int>(tot);
+  }
+  FMT_DEV int posFromRelativePos(uint32_t idx, int r, int c) {
+    const uint32_t mid = ldu(&in.relpos[idx].marker_id);
+    const int offset = ldi(reinterpret_cast<const int32_t*>(&in.relpos[idx].offset));
+    const bool before = (ldu(&in.relpos[idx].flags) & FMT_MT_REL_BEFORE) != 0;
+    if (mid == FMT_MT_NO_MARKER || in.markerKey == FMT_MT_NO_MARKER || mid > 0xFFFFu || S.mkIds == nullptr) return -1;
+    const uint32_t want = (in.markerKey << 16) | mid;
+    uint32_t best = kNone;
+    int bestIns = -1;
+    int64_t bestOrd = -1;
+    for (uint32_t base = 0; base < mkN; base += 64) {
+      Lane<bool> hit;
+      Lane<uint32_t> ids;
+      FOR_LANES(l) {
+        bool h = false;
+        uint32_t id = 0;
+        if (base + l < mkN) {
+          id = rd(S.mkIds + base + l);
+          const uint32_t b = rd(S.leafBlk + id);
+          if (b != kNone) {
+            const uint32_t cnt = rd(S.bCount + b);
+            for (uint32_t k = 0; k < cnt && k < static_cast<uint32_t>(kMaxNodes); k++)
+              if (rd(S.lId + li(b, static_cast<int>(k))) == id) h = setHas(mProps(rd(S.lMeta + li(b, static_cast<int>(k)))), want);
+          }
+        }
+        LANE(hit) = h;
+        LANE(ids) = id;
+      }
+      for (uint64_t m = ballot(hit); m != 0; m &= m - 1) {  // the last inserted (ties: the later in the document)
+        const uint32_t id = readlane(ids, ctz64(m));
+        uint32_t b;
+        int k;
+        locate(id, &b, &k);
+        const int ins = ldi(S.lIns + li(b, k));
+        const int64_t ord = ordOf(id);
+        if (ins > bestIns || (ins == bestIns && ord > bestOrd)) {
+          best = id;
+          bestIns = ins;
+          bestOrd = ord;
+        }
+      }
+    }
+    if (best == kNone) return -1;
+    uint32_t b;
+    int k;
+    locate(best, &b, &k);
+    if (ldi(S.lRm + li(b, k)) != kNotRemoved) return -1;
+    int pos = viewStart(best, r, c);
+    if (before) pos -= offset;
+    else pos += static_cast<int>(ldu(S.lLen + li(b, k))) + offset;
+    return pos;
+  }
+  // getValidOpRange (client.ts:758-767): an undefined pos1 / pos2 comes from relativePos1 / 2.
+  FMT_DEV bool resolveRelative(fmt_mt_op& op) {
+    for (int k = 0; k < 2; k++) {
+      if ((op.flags & (k == 0 ? FMT_MT_F_REL1 : FMT_MT_F_REL2)) == 0) continue;
+      const int32_t idx = k == 0 ? op.pos1 : op.pos2;
+      const int pos = idx >= 0 && static_cast<uint32_t>(idx) < in.nRelpos && in.relpos != nullptr
+                          ? posFromRelativePos(static_cast<uint32_t>(idx), op.ref_seq, op.client)
+                          : -1;
+      if (pos < 0) {
+        fail(FMT_E_DATA);
+        return false;
+      }
+      if (k == 0) op.pos1 = pos;
+      else op.pos2 = pos;
+    }
+    invalidate();
+    return true;
   }
 
   // ------------------------------------------------------------------ catch-up ranges
@@ -3170,6 +3333,28 @@ class HugeDoc {
     minSeq = in.snapMinSeq;
     curSeq = in.snapSeq;
     if (anyWin) loadWindow(nLeafBlk);
+    if (S.mkIds != nullptr) loadMarkers(nLeafBlk);
+  }
+
+  // Loaded Markers join the marker list (relative positions), in document order.
+  FMT_DEV void loadMarkers(uint32_t nLeafBlk) {
+    for (uint32_t base = 0; base < nLeafBlk * 8 && status == FMT_OK; base += 64) {
+      Lane<bool> mk;
+      Lane<uint32_t> ids;
+      FOR_LANES(l) {
+        const uint32_t x = base + l, b = x >> 3, k = x & 7;
+        bool v = false;
+        uint32_t id = 0;
+        if (b < nLeafBlk && k < rd(S.bCount + b)) {
+          const size_t i = li(b, static_cast<int>(k));
+          v = mMarker(rd(S.lMeta + i));
+          id = rd(S.lId + i);
+        }
+        LANE(mk) = v;
+        LANE(ids) = id;
+      }
+      for (uint64_t m = ballot(mk); m != 0 && status == FMT_OK; m &= m - 1) markerAdd(readlane(ids, ctz64(m)));
+    }
   }
 
   // Loaded leaves whose merge info is above minSeq enter the window table (their lengths differ
@@ -3287,7 +3472,7 @@ class HugeDoc {
     ProfScope ps_(prof[0]);
     Lane<uint32_t> rec0 = fetchOp(in.begin), rec1 = fetchOp(in.begin + 1);
     for (uint64_t i = in.begin; i < in.end; i++) {
-      const fmt_mt_op op = decodeOp(rec0);
+      fmt_mt_op op = decodeOp(rec0);
       rec0 = rec1;
       rec1 = fetchOp(i + 2);
       invalidate();
@@ -3301,7 +3486,8 @@ class HugeDoc {
       rmHitN = 0;
       opIdx = static_cast<uint32_t>(i - in.begin);
       if (op.client > 63) fail(FMT_E_UNSUPPORTED);
-      else if (op.type == FMT_MT_INSERT) insertText(op);
+      else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) != 0 && !resolveRelative(op)) {
+      } else if (op.type == FMT_MT_INSERT) insertText(op);
       else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
         if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
         else applyRange(op);
@@ -3550,8 +3736,15 @@ class HugeDoc {
     rmN = rmHitN = 0;
     rmRec = false;
     rmPendN = 0;
+    mkN = 0;
     nFree = 0;
     nProps = 0;
+    if (inputs.nPropsOps > 0 || inputs.segProps != 0) {  // (empty prop-set hash tables)
+      FOR_LANES(l) {
+        for (uint32_t k = static_cast<uint32_t>(l); k < 2 * kPropHash; k += 64) S.pHead[k] = 0u;
+      }
+      waveSync();
+    }
     textTop = S.textLen;
     mergeLo = S.textLen;
     mergeHi = S.textLen + (S.textCap - S.textLen) / 2;

@@ -174,8 +174,8 @@ struct fmt_ctx {
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
   // documents that outgrow the large tier replay again, from their start, in the huge tier when
-  // they hold nothing it does not (mtHugeOk: no relative positions, annotate-adjust or SnapshotV1
-  // body segments with merge info, FMT_MT_F_LOADSEG); their starts
+  // they hold nothing it does not (mtHugeOk: no annotate-adjust or SnapshotV1 body segments with
+  // merge info, FMT_MT_F_LOADSEG); their starts
   std::vector<uint8_t> mtHugeOk;
   std::vector<uint8_t> mtSegProps;           // per document: a loaded segment has properties
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
@@ -725,6 +725,9 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   // the merge area only; the batch text is read in place (huge_engine.h HugeState::base)
   FMT_ALLOC(text, uint16_t, textCap - textLen)
   FMT_ALLOC(props, uint32_t, static_cast<size_t>(fmt_huge::kPropCap) * fmt_huge::kPropWords)
+  FMT_ALLOC(pClass, uint32_t, fmt_huge::kPropCap)
+  FMT_ALLOC(pHead, uint32_t, 2ull * fmt_huge::kPropHash)
+  FMT_ALLOC(pNext, uint32_t, 2ull * fmt_huge::kPropCap)
   S.text -= textLen;
   S.base = c->mtText.p;
   S.textLen = textLen;
@@ -755,6 +758,17 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
     I.catchupCap = static_cast<uint32_t>(std::min<uint64_t>(c->mtCuOffsHost[d + 1] - c->mtCuOffsHost[d], 0xFFFFFFFFull));
     if ((e = alloc(static_cast<size_t>(S.idCap) * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
     S.cuIds = static_cast<uint32_t*>(p);
+  }
+  // relative positions: the batch's table, and the document's marker list
+  I.relpos = c->mtNRelpos ? c->mtRelpos.p : nullptr;
+  I.nRelpos = c->mtNRelpos;
+  I.markerKey = c->mtMarkerKey;
+  S.mkIds = nullptr;
+  S.mkCap = 0;
+  if (c->mtNRelpos) {
+    if ((e = alloc(static_cast<size_t>(S.idCap) * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    S.mkIds = static_cast<uint32_t*>(p);
+    S.mkCap = S.idCap;
   }
   // remove-order entries (SnapshotV1) go to the document's slab too
   I.rmOrder = nullptr;
@@ -1136,7 +1150,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
       const fmt_mt_op& op = b->ops[i];
       if (op.type == FMT_MT_INSERT) chars += fmt_mt_op_len(&op);
-      if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2 | FMT_MT_F_LOADSEG)) ||
+      if ((op.flags & FMT_MT_F_LOADSEG) ||
           (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
         ok = 0;
     }
@@ -1180,7 +1194,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (!c->mtHugeOk[d]) {  // (V1 body segments with merge info, relative positions, annotate-adjust)
+      if (!c->mtHugeOk[d]) {  // (V1 body segments with merge info, annotate-adjust)
         refuse(d, FMT_E_UNSUPPORTED);
         continue;
       }

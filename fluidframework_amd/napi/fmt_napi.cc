@@ -30,7 +30,12 @@
 //   sizes: {mtOp, mapOp, leaf, docResult, propset, mapSlot}          struct sizes for the JS views
 #include <node_api.h>
 
+#include <execinfo.h>
+#include <unistd.h>
+
+#include <csignal>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -62,6 +67,11 @@ const char* status_name(int rc) {
 struct Ctx {
   fmt_ctx* ctx = nullptr;
   bool busy = false;  // one async replay at a time per ctx (the C ABI is one-thread-per-ctx)
+  // A strong reference to the ctx's own external, never released: the external is never collected
+  // while node runs, so its finalizer only runs at environment teardown. (This image's node, v12,
+  // can run the second-pass finalizer of an external collected just before exit after teardown has
+  // freed its reference record: a SIGSEGV at exit. close() is what frees the device context.)
+  napi_ref self = nullptr;
 };
 
 void finalize_ctx(napi_env, void* data, void*) {
@@ -165,6 +175,7 @@ napi_value Open(napi_env env, napi_callback_info info) {
   c->ctx = ctx;
   napi_value ext;
   CHECK_NAPI(env, napi_create_external(env, c, finalize_ctx, nullptr, &ext));
+  CHECK_NAPI(env, napi_create_reference(env, ext, 1, &c->self));
   return ext;
 }
 
@@ -825,7 +836,18 @@ napi_value FetchLegacyProps(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+// FMT_NAPI_BACKTRACE=1: a SIGSEGV prints the native stack to stderr before the default action
+// (diagnostics for crashes inside the addon or the HIP runtime under node).
+void segvTrace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  std::signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 napi_value Init(napi_env env, napi_value exports) {
+  if (std::getenv("FMT_NAPI_BACKTRACE") != nullptr) std::signal(SIGSEGV, segvTrace);
   napi_property_descriptor fns[] = {
       {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -82,6 +82,10 @@ int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   S.text = text.data() - b->text_len; S.textLen = b->text_len; S.textCap = textCap;
   std::vector<uint32_t> pr(static_cast<size_t>(kPropCap) * kPropWords);
   S.props = pr.data();
+  std::vector<uint32_t> pcl(kPropCap), phead(2ull * kPropHash), pnext(2ull * kPropCap);
+  S.pClass = pcl.data();
+  S.pHead = phead.data();
+  S.pNext = pnext.data();
   std::vector<uint32_t> cuIds(catchup != nullptr ? S.idCap : 0);
   S.cuIds = catchup != nullptr ? cuIds.data() : nullptr;
   std::vector<uint32_t> rmIds(rmOrder != nullptr ? S.idCap : 0);
@@ -108,6 +112,12 @@ int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   in.catchupCap = capCatchup;
   in.rmOrder = rmOrder;
   in.rmOrderCap = capRm;
+  in.relpos = b->relpos;
+  in.nRelpos = b->relpos ? b->n_relpos : 0;
+  in.markerKey = b->marker_id_key;
+  std::vector<uint32_t> mkIds(b->relpos != nullptr ? S.idCap : 0);
+  doc->S.mkIds = b->relpos != nullptr ? mkIds.data() : nullptr;
+  doc->S.mkCap = S.idCap;
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;

@@ -64,7 +64,8 @@ def huge_emu_lib(tiny_groups=False):
     return _huge[tiny_groups]
 
 
-def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=False, cap_catchup=0, cap_rm=0):
+def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=False, cap_catchup=0, cap_rm=0,
+                    cap_props=65534):
     """(header, leaves, chars, props) of document `doc` replayed by the emulated huge engine, plus its
     catch-up ranges (header n_catchup of them) when cap_catchup > 0, then its remove-order entries
     (header n_rm_order of them) when cap_rm > 0."""
@@ -79,7 +80,7 @@ def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=F
     hdr = np.zeros(1, dtype=DOC_RESULT_DTYPE)
     leaves = np.zeros(cap_leaves, dtype=LEAF_DTYPE)
     chars = np.zeros(cap_chars, dtype="<u2")
-    props = np.zeros(4096, dtype=PROPSET_DTYPE)
+    props = np.zeros(cap_props, dtype=PROPSET_DTYPE)
     b, keep = batch_struct(batch)
     cu = np.zeros(max(cap_catchup, 1), dtype=CATCHUP_DTYPE)
     rm = np.zeros(max(cap_rm, 1), dtype=RM_ORDER_DTYPE)

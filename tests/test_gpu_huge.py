@@ -19,7 +19,7 @@ def engine():
     e.close()
 
 
-def _oracle(orc, batch, doc=0):
+def _oracle(orc, batch, doc=0, cap_props=4096):
     orc.set_index(True)
     try:
         sub = _one_doc(batch, doc)
@@ -27,7 +27,7 @@ def _oracle(orc, batch, doc=0):
         segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 0
         nops = len(sub.ops)
         rc, h, lv, ch, pr, *_ = orc.mt_replay_timed(sub, 0, 0, cap_leaves=segs + 3 * nops + 4096,
-                                                    cap_chars=len(sub.text) + 8, cap_props=4096)
+                                                    cap_chars=len(sub.text) + 8, cap_props=cap_props)
     finally:
         orc.set_index(False)
     return rc, (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
@@ -161,19 +161,26 @@ def test_huge_loaded_markers(orc, engine):
 
 def test_unsupported_huge_document_fails_alone(orc, engine):
     """A summary-loaded document past the large tier that asks for something the huge tier does not
-    resolve (here a relative position) fails alone, with FMT_E_UNSUPPORTED in its own header: the
+    replay (here an annotate-adjust) fails alone, with FMT_E_UNSUPPORTED in its own header: the
     ordinary and huge documents beside it replay as in a batch without it."""
     import dataclasses
 
-    from fluidframework_amd.streams import MT_F_REL1, NO_MARKER, RELPOS_DTYPE
+    from fluidframework_amd.streams import ADJUST_DTYPE, value_numbers
     farm = workloads.conflict_farm(24, n_clients=8, ops_per_doc=600, seed=8)
     t3a = workloads.t3_stream(3000, 4000, n_clients=31, max_lag=700, seed=9)
     bad = workloads.t3_stream(9000, 6000, n_clients=63, max_lag=4096, max_range=20, seed=10)
-    first_insert = int(np.nonzero(bad.ops["type"] == 0)[0][0])
-    bad.ops["flags"][first_insert] |= MT_F_REL1
-    bad.ops["pos1"][first_insert] = 0  # (row 0 of the relpos table below)
     batch = _concat([farm, t3a, bad, farm])
-    batch = dataclasses.replace(batch, relpos=np.array([(NO_MARKER, 0, 0, 0)], dtype=RELPOS_DTYPE))
+    n_props = len(batch.props_off) - 1
+    o0 = int(batch.doc_op_offsets[farm.n_docs + 1])
+    first_annotate = o0 + int(np.nonzero(bad.ops["type"] == 2)[0][0])
+    ops = batch.ops.copy()
+    ops["payload"][first_annotate] = n_props  # (the props op appended below: one adjust entry)
+    adjusts = np.zeros(1, dtype=ADJUST_DTYPE)
+    adjusts["delta"] = 1.0
+    batch = dataclasses.replace(
+        batch, ops=ops, props_off=np.append(batch.props_off, batch.props_off[-1] + 2).astype(np.uint32),
+        props_kv=np.append(batch.props_kv, [0xFFFF, 0]).astype(np.uint32), adjusts=adjusts,
+        value_num=value_numbers(batch.values))
     engine.mt_load(batch)
     engine.mt_run()
     hdrs = engine.mt_headers(raise_on_failed_docs=False)
@@ -187,6 +194,25 @@ def test_unsupported_huge_document_fails_alone(orc, engine):
         assert rc == 0
         lv, ch, pr = engine.mt_doc(d, hdrs[d])
         assert compare_doc(exp, (hdrs[d], lv, ch, pr)) == [], d
+
+
+@pytest.mark.parametrize("n_ops,split,seed", [(6000, 0, 2), (12000, 9000, 4)])
+def test_huge_relative_positions_on_gpu(orc, engine, n_ops, split, seed):
+    """Legacy relativePos1 inserts in documents past the large tier: one grown from its start (the
+    large tier runs out of leaves and prop sets), one loaded from a summary holding its first
+    `split` messages' Markers; == oracle."""
+    from marker_docs import marker_batch
+    from test_huge_emulated import marker_reload
+    batch = marker_batch(1, n_ops, seed=seed) if split == 0 else marker_reload(orc, n_ops, split, seed)
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    assert int(hdrs[0]["n_leaves"]) > 2048  # (past the large tier)
+    rc, exp = _oracle(orc, batch, cap_props=1 << 15)
+    assert rc == 0
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
 
 
 @pytest.mark.parametrize("segs,ops,props_every,seed", [

@@ -7,13 +7,14 @@ from fluidframework_amd import workloads
 from mt_compare import compare_doc, emu_huge_replay
 
 
-def _oracle_doc(orc, batch):
+def _oracle_doc(orc, batch, cap_props=4096):
     orc.set_index(True)
     try:
-        segs = int(batch.snapshots[0]["n_header"]) + int(batch.snapshots[0]["n_body"])
+        sd = batch.snapshots[0] if batch.snapshots is not None else None
+        segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None else 1
         nops = len(batch.ops)
         rc, h, lv, ch, pr, *_ = orc.mt_replay_timed(batch, 0, 0, cap_leaves=segs + 3 * nops + 8,
-                                                    cap_chars=len(batch.text) + 8, cap_props=4096)
+                                                    cap_chars=len(batch.text) + 8, cap_props=cap_props)
     finally:
         orc.set_index(False)
     return rc, (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
@@ -256,3 +257,51 @@ def test_huge_engine_v1_merge_info_load(orc, tiny):
     got = emu_huge_replay(batch, tiny_groups=tiny)
     assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
     assert compare_doc(exp, got) == []
+
+
+def marker_reload(orc, n_ops, split, seed):
+    """A marker-rich document (marker_docs) summarized by the oracle after `split` messages (legacy
+    header/body + catch-up blob) and reloaded, the rest of its messages after it: relative positions
+    then name Markers loaded from the summary as well as inserted ones."""
+    from marker_docs import doc_messages
+
+    from fluidframework_amd import summary
+    from fluidframework_amd.streams import MergeTreeStreamBuilder
+    init, msgs = doc_messages(0, n_ops, seed)
+    b = MergeTreeStreamBuilder(keep_messages=True)
+    doc = b.begin_doc(init)
+    for m in msgs[:split]:
+        doc.add_message(m)
+    first = b.finish(catchup=True)
+    rc, h, lv, ch, pr, _, cu = orc.mt_replay_batch(first, cap_leaves=4 * split + 64, cap_chars=len(first.text) + 8,
+                                                 cap_props=1 << 14, cap_catchup=4 * split + 64)
+    assert rc == 0
+    head, body = summary.legacy_summary(h[0], lv[0], ch[0], pr[0], first.keys, first.values, chunk_size=200)
+    blob = summary.catchup_blob(summary.catchup_messages(first.messages[0], cu[0][: h[0]["n_catchup"]],
+                                                         int(h[0]["min_seq"])))
+    b2 = MergeTreeStreamBuilder()
+    doc = b2.begin_doc_from_summary(head, body, blob)
+    for m in msgs[split:]:
+        doc.add_message(m)
+    return b2.finish()
+
+
+@pytest.mark.parametrize("n_ops,split,seed,tiny", [(3000, 0, 1, True), (6000, 0, 2, False), (5000, 2500, 3, True),
+                                                   (8000, 6000, 4, False), (12000, 0, 5, False)])
+def test_huge_engine_relative_positions(orc, n_ops, split, seed, tiny):
+    """Legacy relativePos1 inserts (getValidOpRange, client.ts:758-767) in a huge document: the
+    marker named by markerId found through the document's marker list (inserted Markers, and with a
+    split the ones loaded from the summary), positioned in the op's view (posFromRelativePos,
+    mergeTree.ts:1462-1483). The longest document interns more than 4096 prop sets (every Marker's
+    markerId is its own set: the hash-table interning, past the LDS class cache)."""
+    from marker_docs import marker_batch
+    from fluidframework_amd.streams import MT_F_REL1
+    batch = marker_batch(1, n_ops, seed=seed) if split == 0 else marker_reload(orc, n_ops, split, seed)
+    assert int((batch.ops["flags"] & MT_F_REL1 != 0).sum()) > 100
+    rc, exp = _oracle_doc(orc, batch, cap_props=1 << 15)
+    assert rc == 0
+    got = emu_huge_replay(batch, tiny_groups=tiny)
+    assert int(got[0]["status"]) == 0, f"engine status {int(got[0]['status'])} at seq {int(got[0]['fail_seq'])}"
+    assert compare_doc(exp, got) == []
+    if n_ops >= 12000:
+        assert int(got[0]["n_props"]) > 4096
