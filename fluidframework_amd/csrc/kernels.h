@@ -21,6 +21,12 @@ hipError_t launchMapSparse(const fmt_map_op* ops, const uint64_t* offsets, uint3
                            fmt_map_entry* out, uint32_t* counts, int* error, int numCUs, hipStream_t stream);
 hipError_t launchMapSparsePack(const fmt_map_entry* in, const uint64_t* offsets, const uint32_t* counts,
                                const uint64_t* packedOff, uint32_t nDocs, fmt_map_entry* packed, hipStream_t stream);
+// ---- SharedMap local-client pending state (map_pending.hip)
+size_t mapPendingScratchBytes(uint64_t nEvents);
+hipError_t launchMapPending(const fmt_map_local_op* events, const uint64_t* evOffs, const fmt_map_entry* seqEntries,
+                            const uint64_t* seqOffs, const uint32_t* seqCounts, uint32_t nDocs, void* scratch,
+                            const uint64_t* outBase, fmt_map_entry* out, uint32_t* outCounts, int32_t* outStatus,
+                            hipStream_t stream);
 hipError_t launchMapLww(const fmt_map_op* ops, const uint64_t* offsets, uint32_t nDocs, uint32_t keyBound,
                         fmt_map_slot* out, int* error, int numCUs, hipStream_t stream, uint32_t* scratch);
 

@@ -125,6 +125,17 @@ struct fmt_ctx {
   DevBuf<uint32_t> mapCounts;
   DevBuf<uint64_t> mapPackedOff;
   bool mapSparse = false;
+  bool mapSparseRan = false;
+  std::vector<uint64_t> mapOffsHost;  // the staged batch's doc_op_offsets
+  // SharedMap local-client pending state (fmt_map_pending_run): events, per-event scratch, the
+  // optimistic entries at mapPendBase[d] = op offset + event offset of the document
+  DevBuf<fmt_map_local_op> mapEv;
+  DevBuf<uint64_t> mapEvOffs, mapPendBase;
+  DevBuf<uint8_t> mapPendScratch;
+  DevBuf<fmt_map_entry> mapPendOut;
+  DevBuf<uint32_t> mapPendCounts;
+  DevBuf<int32_t> mapPendStatus;
+  bool mapPendRan = false;
 
   // merge-tree
   DevBuf<fmt_mt_op> mtOps;
@@ -392,6 +403,13 @@ void fmt_close(fmt_ctx* c) {
   c->mapScratch.release();
   c->mapEntries.release();
   c->mapPacked.release();
+  c->mapEv.release();
+  c->mapEvOffs.release();
+  c->mapPendBase.release();
+  c->mapPendScratch.release();
+  c->mapPendOut.release();
+  c->mapPendCounts.release();
+  c->mapPendStatus.release();
   c->mapCounts.release();
   c->mapPackedOff.release();
   c->errWord.release();
@@ -520,6 +538,9 @@ static int mapStage(fmt_ctx* c, const fmt_map_op* ops, uint64_t nOps, const uint
   c->mapKeyBound = keyBound;
   c->mapLoaded = true;
   c->mapSparse = sparse;
+  c->mapSparseRan = false;
+  c->mapPendRan = false;
+  c->mapOffsHost.assign(offs, offs + nDocs + 1ull);
   return FMT_OK;
 }
 
@@ -551,6 +572,8 @@ int fmt_map_run_sparse(fmt_ctx* c) {
   c->stats.bytes_read = c->mapNOps * sizeof(fmt_map_op) + (c->mapDocs + 1ull) * sizeof(uint64_t);
   c->stats.bytes_written = static_cast<uint64_t>(c->mapDocs) * sizeof(uint32_t);  // + entries, at fetch
   c->stats.launches = 1;
+  c->mapSparseRan = true;
+  c->mapPendRan = false;
   return FMT_OK;
 }
 
@@ -580,6 +603,82 @@ int fmt_map_fetch_sparse(fmt_ctx* c, uint32_t* counts, fmt_map_entry* entries, u
   }
   if (errWord & 1) return setErr(c, FMT_E_DATA, "an op referenced a key id >= key_bound");
   if (errWord & 2) return setErr(c, FMT_E_CAPACITY, "a document exceeded the sparse path's keys or ops per document");
+  return FMT_OK;
+}
+
+int fmt_map_pending_run(fmt_ctx* c, const fmt_map_local_op* events, uint64_t nEvents, const uint64_t* evOffs) {
+  if (c == nullptr || !c->mapLoaded || !c->mapSparse || !c->mapSparseRan)
+    return setErr(c, FMT_E_USAGE, "fmt_map_pending_run needs a sparse map run (fmt_map_run_sparse) first");
+  if ((nEvents > 0 && events == nullptr) || evOffs == nullptr)
+    return setErr(c, FMT_E_USAGE, "fmt_map_pending_run: null events or offsets");
+  if (nEvents >= 0xFFFFFFFFull) return setErr(c, FMT_E_USAGE, "fmt_map_pending_run: too many events");
+  const uint32_t n = c->mapDocs;
+  if (evOffs[0] != 0 || evOffs[n] != nEvents) return setErr(c, FMT_E_USAGE, "doc_event_offsets must span [0, n_events)");
+  std::vector<uint64_t> base(n);
+  for (uint32_t d = 0; d < n; d++) {
+    if (evOffs[d + 1] < evOffs[d]) return setErr(c, FMT_E_USAGE, "doc_event_offsets is not ascending");
+    for (uint64_t i = evOffs[d]; i < evOffs[d + 1]; i++) {
+      const fmt_map_local_op& e = events[i];
+      const uint32_t kind = e.kind_value >> FMT_MAP_KIND_SHIFT;
+      if (e.doc != d || e.event > FMT_MAP_EV_ROLLBACK || kind > FMT_MAP_CLEAR ||
+          (kind != FMT_MAP_CLEAR && e.key >= c->mapKeyBound))
+        return setErr(c, FMT_E_DATA, "a local event with a bad document, event, kind or key id");
+    }
+    base[d] = c->mapOffsHost[d] + evOffs[d];  // room for the sequenced entries plus one per event
+  }
+  FMT_HIP(c, hipSetDevice(c->device));
+  FMT_HIP(c, c->mapEv.reserve(nEvents));
+  FMT_HIP(c, c->mapEvOffs.reserve(n + 1ull));
+  FMT_HIP(c, c->mapPendBase.reserve(n));
+  FMT_HIP(c, c->mapPendScratch.reserve(fmt_kernels::mapPendingScratchBytes(nEvents)));
+  FMT_HIP(c, c->mapPendOut.reserve(c->mapNOps + nEvents));
+  FMT_HIP(c, c->mapPendCounts.reserve(n));
+  FMT_HIP(c, c->mapPendStatus.reserve(n));
+  if (nEvents) FMT_HIP(c, stagedCopy(c, c->mapEv.p, events, nEvents * sizeof(fmt_map_local_op), true));
+  FMT_HIP(c, hipMemcpyAsync(c->mapEvOffs.p, evOffs, (n + 1ull) * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  FMT_HIP(c, hipMemcpyAsync(c->mapPendBase.p, base.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
+  FMT_HIP(c, fmt_kernels::launchMapPending(c->mapEv.p, c->mapEvOffs.p, c->mapEntries.p, c->mapOffs.p, c->mapCounts.p, n,
+                                           c->mapPendScratch.p, c->mapPendBase.p, c->mapPendOut.p, c->mapPendCounts.p,
+                                           c->mapPendStatus.p, c->stream));
+  FMT_HIP(c, hipEventRecord(c->ev1, c->stream));
+  // (the host arrays above are read by the copies before the call returns: synchronize)
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  c->timed = true;
+  c->timed2 = false;
+  c->stats = fmt_stats{};
+  c->stats.ops = nEvents;
+  c->stats.docs = n;
+  c->stats.bytes_read = nEvents * sizeof(fmt_map_local_op) + c->mapNOps * sizeof(fmt_map_entry);
+  c->stats.launches = 1;
+  c->mapPendRan = true;
+  return FMT_OK;
+}
+
+int fmt_map_pending_fetch(fmt_ctx* c, uint32_t* counts, int32_t* status, fmt_map_entry* entries, uint64_t capEntries,
+                          uint64_t* nEntries) {
+  if (c == nullptr || counts == nullptr || !c->mapPendRan)
+    return setErr(c, FMT_E_USAGE, "fmt_map_pending_fetch before fmt_map_pending_run");
+  const uint32_t n = c->mapDocs;
+  FMT_HIP(c, hipSetDevice(c->device));
+  FMT_HIP(c, hipMemcpyAsync(counts, c->mapPendCounts.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  if (status) FMT_HIP(c, hipMemcpyAsync(status, c->mapPendStatus.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  FMT_HIP(c, hipStreamSynchronize(c->stream));
+  std::vector<uint64_t> packedOff(n + 1ull, 0);
+  for (uint32_t d = 0; d < n; d++) packedOff[d + 1] = packedOff[d] + counts[d];
+  const uint64_t total = packedOff[n];
+  if (nEntries) *nEntries = total;
+  if (entries != nullptr) {
+    if (capEntries < total) return setErr(c, FMT_E_USAGE, "fmt_map_pending_fetch: cap_entries below the entries");
+    FMT_HIP(c, c->mapPackedOff.reserve(n + 1ull));
+    FMT_HIP(c, c->mapPacked.reserve(total));
+    FMT_HIP(c, hipMemcpyAsync(c->mapPackedOff.p, packedOff.data(), (n + 1ull) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                              c->stream));
+    FMT_HIP(c, fmt_kernels::launchMapSparsePack(c->mapPendOut.p, c->mapPendBase.p, c->mapPendCounts.p, c->mapPackedOff.p,
+                                                n, c->mapPacked.p, c->stream));
+    FMT_HIP(c, hipMemcpyAsync(entries, c->mapPacked.p, total * sizeof(fmt_map_entry), hipMemcpyDeviceToHost, c->stream));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));
+  }
   return FMT_OK;
 }
 

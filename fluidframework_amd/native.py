@@ -242,7 +242,9 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_remove_order.argtypes = [P, U32, P, U32]
         L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
-        for name, args in (("fmt_mt_state_digest", [P, P]), ("fmt_mt_fetch_legacy_props", [P, U32, P, U32])):
+        for name, args in (("fmt_mt_state_digest", [P, P]), ("fmt_mt_fetch_legacy_props", [P, U32, P, U32]),
+                           ("fmt_map_pending_run", [P, P, U64, P]),
+                           ("fmt_map_pending_fetch", [P, P, P, P, U64, ctypes.POINTER(U64)])):
             if path == LIB_PATH or hasattr(L, name):  # (older experimental builds may lack them)
                 getattr(L, name).argtypes = args
         _libs[path] = L
@@ -256,7 +258,7 @@ EXPORTED_SYMBOLS = [
     "fmt_mt_summarize_legacy", "fmt_mt_summary_blobs",
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
-    "fmt_mt_state_digest", "fmt_mt_fetch_legacy_props",
+    "fmt_mt_state_digest", "fmt_mt_fetch_legacy_props", "fmt_map_pending_run", "fmt_map_pending_fetch",
 ]
 
 
@@ -352,6 +354,22 @@ class Engine:
         entries = np.zeros(max(n.value, 1), dtype=MAP_ENTRY_DTYPE)
         self._check(self.L.fmt_map_fetch_sparse(self.h, _ptr(counts), _ptr(entries), n.value, ctypes.byref(n)))
         return counts, entries[: n.value]
+
+    def map_pending(self, batch):
+        """fmt_map_pending_run + fetch over the last sparse run: the local client's optimistic view of
+        every document of `batch` (its local_ops / local_offsets, streams.MapStreamBuilder.local_*).
+        Returns (counts[n_docs], status[n_docs], entries[sum(counts)]) with MAP_ENTRY_DTYPE."""
+        ev = np.ascontiguousarray(batch.local_ops)
+        eo = np.ascontiguousarray(batch.local_offsets, dtype=np.uint64)
+        self._check(self.L.fmt_map_pending_run(self.h, _ptr(ev), len(ev), _ptr(eo)))
+        counts = np.zeros(self._map_shape[0], dtype=np.uint32)
+        status = np.zeros(self._map_shape[0], dtype=np.int32)
+        n = ctypes.c_uint64()
+        self._check(self.L.fmt_map_pending_fetch(self.h, _ptr(counts), _ptr(status), None, 0, ctypes.byref(n)))
+        entries = np.zeros(max(n.value, 1), dtype=MAP_ENTRY_DTYPE)
+        self._check(self.L.fmt_map_pending_fetch(self.h, _ptr(counts), _ptr(status), _ptr(entries), n.value,
+                                                 ctypes.byref(n)))
+        return counts, status, entries[: n.value]
 
     # ---- bulk legacy summaries of the last merge-tree run
     def mt_summarize_legacy(self, keys, values, chunk: int = 10000, threads: int = 0) -> dict:

@@ -54,6 +54,10 @@ NO_PROPS = 0xFFFFFFFF
 
 # include/fmt.h fmt_map_op (16 bytes)
 MAP_OP_DTYPE = np.dtype([("doc", "<u4"), ("key", "<u4"), ("seq", "<u4"), ("kind_value", "<u4")])
+# fmt.h fmt_map_local_op: one event of a document's local client (FMT_MAP_EV_*)
+MAP_LOCAL_OP_DTYPE = np.dtype([("doc", "<u4"), ("key", "<u4"), ("event", "<u4"), ("kind_value", "<u4")])
+MAP_EV_SUBMIT, MAP_EV_ACK, MAP_EV_ROLLBACK = 0, 1, 2
+MAP_PENDING_BIRTH = 0x80000000
 assert MAP_OP_DTYPE.itemsize == 16
 
 MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MT_OBLITERATE, MT_OBLITERATE_SIDED = range(6)
@@ -859,6 +863,8 @@ class MapBatch:
     key_bound: int
     keys: list                  # key id → key string
     values: list                # value id → JSON text
+    local_ops: np.ndarray = None      # MAP_LOCAL_OP_DTYPE: the local client's events (fmt_map_pending_run)
+    local_offsets: np.ndarray = None  # uint64, n_docs + 1
 
     @property
     def n_docs(self) -> int:
@@ -873,10 +879,64 @@ class MapStreamBuilder:
         self.values = Dictionary()
         self.docs: list[list[tuple]] = []
         self._last_seq: dict[int, int] = {}
+        self.local: list[list[tuple]] = []     # per document, its local client's events
+        self._unacked: list[list[tuple]] = []  # per document, (key, kind_value) of unacknowledged submissions
 
     def begin_doc(self) -> int:
         self.docs.append([])
+        self.local.append([])
+        self._unacked.append([])
         return len(self.docs) - 1
+
+    def _record(self, doc: int, contents: dict):
+        """(key id, kind_value) of a set / delete / clear op's contents."""
+        t = contents["type"]
+        if t == "clear":
+            return 0, MAP_CLEAR << MAP_KIND_SHIFT
+        key = self.keys.intern(contents["key"])
+        if t == "delete":
+            return key, MAP_DELETE << MAP_KIND_SHIFT
+        if t != "set":
+            raise UnsupportedOp(f"map op type {t}")
+        sv = contents["value"]
+        if sv.get("type") != "Plain":
+            raise UnsupportedOp("legacy Shared value type")
+        if "value" in sv and sv["value"] is not _MISSING:
+            vid = self.values.intern(js_json(sv["value"]))
+            if vid >= MAP_VALUE_UNDEFINED:
+                raise UnsupportedOp("value dictionary overflow")
+        else:
+            vid = MAP_VALUE_UNDEFINED
+        return key, (MAP_SET << MAP_KIND_SHIFT) | vid
+
+    # ---- the document's local client (MapKernel pendingData, mapKernel.ts:132-139, 388-538, 633-853)
+    def local_submit(self, doc: int, contents: dict) -> None:
+        """MapKernel.set / delete / clear on the attached map: the op enters pendingData (it is not
+        sequenced until local_ack)."""
+        key, kv = self._record(doc, contents)
+        self.local[doc].append((doc, key, MAP_EV_SUBMIT, kv))
+        self._unacked[doc].append((key, kv))
+
+    def local_ack(self, doc: int, seq: int) -> None:
+        """The oldest unacknowledged local op comes back sequenced: it is appended to the document's
+        sequenced stream like any message and leaves pendingData (the handlers' local branches)."""
+        if not self._unacked[doc]:
+            raise ValueError("local_ack with no unacknowledged local op")
+        key, kv = self._unacked[doc].pop(0)
+        ops = self.docs[doc]
+        last = self._last_seq.get(doc, 0)
+        if seq < last:
+            raise ValueError(f"map message seq {seq} after {last}: messages must arrive in seq order")
+        self._last_seq[doc] = seq
+        ops.append((doc, key, len(ops) + 1, kv))
+        self.local[doc].append((doc, key, MAP_EV_ACK, kv))
+
+    def local_rollback(self, doc: int) -> None:
+        """MapKernel.rollback of the newest unacknowledged local op (mapKernel.ts:633-700)."""
+        if not self._unacked[doc]:
+            raise ValueError("local_rollback with no unacknowledged local op")
+        key, kv = self._unacked[doc].pop()
+        self.local[doc].append((doc, key, MAP_EV_ROLLBACK, kv))
 
     def add_message(self, doc: int, seq: int, contents: dict) -> None:
         """One sequenced map message. Messages of one runtime bunch share their envelope's
@@ -937,7 +997,14 @@ class MapStreamBuilder:
                 ops[i : i + len(d)] = np.array(d, dtype=MAP_OP_DTYPE)
             i += len(d)
             offs[di + 1] = i
-        return MapBatch(ops, offs, max(1, len(self.keys.items)), list(self.keys.items), list(self.values.items))
+        lo, loff = None, None
+        if any(self.local):
+            ev = [e for d in self.local for e in d]
+            lo = np.array(ev, dtype=MAP_LOCAL_OP_DTYPE) if ev else np.zeros(0, dtype=MAP_LOCAL_OP_DTYPE)
+            loff = np.zeros(len(self.docs) + 1, dtype=np.uint64)
+            loff[1:] = np.cumsum([len(d) for d in self.local])
+        return MapBatch(ops, offs, max(1, len(self.keys.items)), list(self.keys.items), list(self.values.items),
+                        lo, loff)
 
 
 class _Missing:

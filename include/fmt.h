@@ -465,6 +465,39 @@ int fmt_map_run_sparse(fmt_ctx* ctx);
 int fmt_map_fetch_sparse(fmt_ctx* ctx, uint32_t* counts, fmt_map_entry* entries, uint64_t cap_entries,
                          uint64_t* n_entries);
 
+/* Local-client pending state (the optimistic view of a client with unacknowledged local ops):
+ * MapKernel.pendingData (mapKernel.ts:132-139) built by set / delete / clear (:388-538), emptied
+ * by the local branches of the message handlers (:706-853) and by rollback (:633-700); read by
+ * get / has (:374-392) and the iterator (:176-240). Each document's local-client events, in the
+ * order they happened (the sequenced stream itself, local ops included, stays the document's
+ * fmt_map_op records): */
+#define FMT_MAP_EV_SUBMIT 0u   /* set / delete / clear of an attached map: the op enters pendingData */
+#define FMT_MAP_EV_ACK 1u      /* the oldest unacknowledged submission came back sequenced
+                                  (tryProcessMessage with local = true) and leaves pendingData */
+#define FMT_MAP_EV_ROLLBACK 2u /* rollback of the newest unacknowledged submission */
+typedef struct fmt_map_local_op {
+  uint32_t doc;
+  uint32_t key;        /* key id (set / delete); 0 for clear */
+  uint32_t event;      /* FMT_MAP_EV_* */
+  uint32_t kind_value; /* (kind << 30) | value id, as fmt_map_op. ACK / ROLLBACK repeat the op they
+                          resolve, which must be the oldest / newest unacknowledged submission (the
+                          reference asserts 0xbf2-0xbf9), else the document fails with FMT_E_DATA */
+} fmt_map_local_op;
+/* birth_seq of an optimistic entry that comes from a pending set lifetime: this bit | the index,
+ * within the document's events, of the submission that created the lifetime */
+#define FMT_MAP_PENDING_BIRTH 0x80000000u
+/* Every document's optimistic view over the sequenced entries of the last fmt_map_run_sparse and
+ * the documents' local events (document d's at events[doc_event_offsets[d] .. [d + 1])), one
+ * device thread per document. Asynchronous on the ctx stream. */
+int fmt_map_pending_run(fmt_ctx* ctx, const fmt_map_local_op* events, uint64_t n_events,
+                        const uint64_t* doc_event_offsets);
+/* counts[d] = optimistic entries of document d; entries packed in document order, each document's
+ * in internalIterator order (key, optimistic value, birth_seq: the sequenced birth, or
+ * FMT_MAP_PENDING_BIRTH | creating submission); status[d] (may be NULL): FMT_OK, or FMT_E_DATA for
+ * a document whose ACK / ROLLBACK events do not match its pending ops (no entries). Synchronizes. */
+int fmt_map_pending_fetch(fmt_ctx* ctx, uint32_t* counts, int32_t* status, fmt_map_entry* entries,
+                          uint64_t cap_entries, uint64_t* n_entries);
+
 /* ---------------------------------------------------------------------------------------------
  * merge-tree / SharedString (Client.applyMsg observer path + zamboni, client.ts:1358-1391)
  * ------------------------------------------------------------------------------------------- */

@@ -2,6 +2,7 @@
 //
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
 // Result layouts are the product's (include/fmt.h) so tests compare GPU and oracle field by field.
+#include <deque>
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -554,6 +555,61 @@ int orc_map_replay_sparse(const fmt_map_op* ops, const uint64_t* offs, uint32_t 
   });
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return status.load();
+}
+
+// The local-client pending state's oracle: each document's sequenced entries (as the sparse path),
+// then its local events through PendingMap; the optimistic entries at offs[d] + evOffs[d] (counts,
+// status per document) as fmt_map_pending_run writes them before packing. Submissions are named by
+// their index within the document's events; ACK resolves the oldest unacknowledged one, ROLLBACK
+// the newest (PendingStateManager's order), and the event must repeat that submission's op.
+int orc_map_pending(const fmt_map_op* ops, const uint64_t* offs, uint32_t nDocs, uint32_t keyBound,
+                    const fmt_map_local_op* events, const uint64_t* evOffs, uint32_t* counts, int32_t* status,
+                    fmt_map_entry* entries) {
+  for (uint32_t d = 0; d < nDocs; d++) {
+    orc::MapState m(keyBound, true);
+    for (uint64_t i = offs[d]; i < offs[d + 1]; i++) {
+      const uint32_t kind = ops[i].kind_value >> FMT_MAP_KIND_SHIFT;
+      if (kind == FMT_MAP_CLEAR) m.clear();
+      else if (kind == FMT_MAP_DELETE) m.del(ops[i].key);
+      else m.set(ops[i].key, ops[i].kind_value & FMT_MAP_VALUE_MASK, ops[i].seq);
+    }
+    orc::PendingMap p;
+    std::deque<uint32_t> unacked;
+    bool ok = true;
+    for (uint64_t i = evOffs[d]; i < evOffs[d + 1] && ok; i++) {
+      const fmt_map_local_op& e = events[i];
+      const uint32_t sub = static_cast<uint32_t>(i - evOffs[d]);
+      const uint32_t kind = e.kind_value >> FMT_MAP_KIND_SHIFT;
+      if (e.event == FMT_MAP_EV_SUBMIT) {
+        unacked.push_back(static_cast<uint32_t>(i));
+        if (kind == FMT_MAP_SET) p.set(e.key, e.kind_value & FMT_MAP_VALUE_MASK, sub);
+        else if (kind == FMT_MAP_DELETE) p.del(e.key, sub);
+        else p.clear(sub);
+        continue;
+      }
+      if (unacked.empty()) {
+        ok = false;
+        break;
+      }
+      const uint32_t s = e.event == FMT_MAP_EV_ACK ? unacked.front() : unacked.back();
+      if (e.event == FMT_MAP_EV_ACK) unacked.pop_front();
+      else unacked.pop_back();
+      const fmt_map_local_op& so = events[s];
+      if (so.kind_value != e.kind_value || (kind != FMT_MAP_CLEAR && so.key != e.key)) {
+        ok = false;
+        break;
+      }
+      const uint32_t ssub = static_cast<uint32_t>(s - evOffs[d]);
+      ok = e.event == FMT_MAP_EV_ACK ? p.ack(kind, so.key, ssub) : p.rollback(kind, so.key, ssub);
+    }
+    status[d] = ok ? FMT_OK : FMT_E_DATA;
+    counts[d] = 0;
+    if (!ok) continue;
+    const auto es = p.iterate(m.entries());
+    counts[d] = static_cast<uint32_t>(es.size());
+    for (size_t j = 0; j < es.size(); j++) entries[offs[d] + evOffs[d] + j] = {es[j].key, es[j].value, es[j].birth};
+  }
+  return FMT_OK;
 }
 
 // Summary of one document: header then each blobN, NUL-separated; returns bytes needed.

@@ -58,6 +58,94 @@ void MapState::toSlots(fmt_map_slot* out, uint32_t keyBound) const {
     if (it.live) out[it.key] = {it.value, it.birth};
 }
 
+// ---------------------------------------------------------------- local-client pending state
+void PendingMap::set(uint32_t key, uint32_t value, uint32_t sub) {
+  // latestPendingEntry = findLast(pendingData, clear || entry.key === key) (:427-430)
+  int latest = -1;
+  for (int i = static_cast<int>(pending_.size()) - 1; i >= 0 && latest < 0; i--)
+    if (pending_[i].type == kClear || pending_[i].key == key) latest = i;
+  if (latest < 0 || pending_[latest].type != kLifetime) {  // a new lifetime (:431-437)
+    pending_.push_back({kLifetime, key, {}, sub});
+    latest = static_cast<int>(pending_.size()) - 1;
+  }
+  pending_[latest].keySets.push_back({value, sub});
+}
+
+void PendingMap::del(uint32_t key, uint32_t sub) { pending_.push_back({kDelete, key, {}, sub}); }
+
+void PendingMap::clear(uint32_t sub) { pending_.push_back({kClear, 0, {}, sub}); }
+
+bool PendingMap::ack(uint32_t kind, uint32_t key, uint32_t sub) {
+  if (kind == FMT_MAP_CLEAR) {  // pendingData.shift() must be this clear (:714-723)
+    if (pending_.empty() || pending_.front().type != kClear || pending_.front().sub != sub) return false;
+    pending_.erase(pending_.begin());
+    return true;
+  }
+  // findIndex(entry.type !== "clear" && entry.key === key) (:771-787, :812-835)
+  size_t i = 0;
+  while (i < pending_.size() && !(pending_[i].type != kClear && pending_[i].key == key)) i++;
+  if (i == pending_.size()) return false;
+  Entry& e = pending_[i];
+  if (kind == FMT_MAP_DELETE) {
+    if (e.type != kDelete || e.sub != sub) return false;
+    pending_.erase(pending_.begin() + static_cast<long>(i));
+    return true;
+  }
+  if (e.type != kLifetime || e.keySets.empty() || e.keySets.front().sub != sub) return false;
+  e.keySets.erase(e.keySets.begin());  // keySets.shift()
+  if (e.keySets.empty()) pending_.erase(pending_.begin() + static_cast<long>(i));
+  return true;
+}
+
+bool PendingMap::rollback(uint32_t kind, uint32_t key, uint32_t sub) {
+  if (kind == FMT_MAP_CLEAR) {  // pendingData.pop() must be this clear (:637-646)
+    if (pending_.empty() || pending_.back().type != kClear || pending_.back().sub != sub) return false;
+    pending_.pop_back();
+    return true;
+  }
+  // findLastIndex(entry.type !== "clear" && entry.key === key) (:659-663)
+  int i = static_cast<int>(pending_.size()) - 1;
+  while (i >= 0 && !(pending_[i].type != kClear && pending_[i].key == key)) i--;
+  if (i < 0) return false;
+  Entry& e = pending_[i];
+  if (e.type == kDelete) {
+    if (kind != FMT_MAP_DELETE || e.sub != sub) return false;
+    pending_.erase(pending_.begin() + i);
+    return true;
+  }
+  if (kind != FMT_MAP_SET || e.keySets.empty() || e.keySets.back().sub != sub) return false;
+  e.keySets.pop_back();
+  if (e.keySets.empty()) pending_.erase(pending_.begin() + i);
+  return true;
+}
+
+std::vector<MapState::Entry> PendingMap::iterate(const std::vector<MapState::Entry>& sequenced) const {
+  std::vector<MapState::Entry> out;
+  // getOptimisticLocalValue (:374-392) of a sequenced key with no pending delete / clear
+  for (const auto& x : sequenced) {
+    bool hidden = false;  // pendingData.some(clear || (delete && key === key)) (:190-195)
+    for (const auto& e : pending_) hidden = hidden || e.type == kClear || (e.type == kDelete && e.key == x.key);
+    if (hidden) continue;
+    const Entry* latest = nullptr;
+    for (const auto& e : pending_)
+      if (e.type == kClear || e.key == x.key) latest = &e;
+    out.push_back({x.key, latest == nullptr ? x.value : latest->keySets.back().value, x.birth});
+  }
+  for (size_t i = 0; i < pending_.size(); i++) {  // the pending lifetimes (:209-234)
+    const Entry& e = pending_[i];
+    if (e.type != kLifetime) continue;
+    int lastDC = -1;  // findLastIndex(clear || (delete && key === e.key))
+    for (size_t j = 0; j < pending_.size(); j++)
+      if (pending_[j].type == kClear || (pending_[j].type == kDelete && pending_[j].key == e.key)) lastDC = static_cast<int>(j);
+    if (static_cast<int>(i) <= lastDC) continue;
+    bool inSeq = false;
+    for (const auto& x : sequenced) inSeq = inSeq || x.key == e.key;
+    if (inSeq && lastDC == -1) continue;
+    out.push_back({e.key, e.keySets.back().value, FMT_MAP_PENDING_BIRTH | e.sub});
+  }
+  return out;
+}
+
 // String.prototype.length of a UTF-8 encoded text (UTF-16 code units).
 static size_t utf16Length(const std::string& s) {
   size_t n = 0;

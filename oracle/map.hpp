@@ -48,6 +48,37 @@ class MapState {
   std::vector<Item> items_; // append-only with tombstones; order = Map insertion order
 };
 
+// MapKernel's local-client pending state (mapKernel.ts:132-139) with the reference's own shapes: an
+// ordered list of entries (a set "lifetime" holding its pending keySets, a delete, a clear), built by
+// set / delete / clear (:388-538), emptied by the local branches of the message handlers (:706-853)
+// and by rollback (:633-700). A submission is named by its event index (the localOpMetadata
+// identity); the reference's asserts become a false return.
+class PendingMap {
+ public:
+  enum Type : uint32_t { kLifetime = 0, kDelete = 1, kClear = 2 };
+  struct KeySet {
+    uint32_t value, sub;
+  };
+  struct Entry {
+    uint32_t type, key;
+    std::vector<KeySet> keySets;  // lifetimes
+    uint32_t sub;                 // the submission that created the entry
+  };
+  void set(uint32_t key, uint32_t value, uint32_t sub);  // :402-447
+  void del(uint32_t key, uint32_t sub);                  // :453-490
+  void clear(uint32_t sub);                              // :495-538
+  // process(op, local = true, metadata = sub): the handlers' local branches (:714-723, :771-787, :812-835)
+  bool ack(uint32_t kind, uint32_t key, uint32_t sub);
+  // rollback(op, metadata = sub) (:633-700)
+  bool rollback(uint32_t kind, uint32_t key, uint32_t sub);
+  // internalIterator (:176-240) over the sequenced entries (Map order) and the pending entries:
+  // (key, optimistic value, sequenced birth or FMT_MAP_PENDING_BIRTH | creating submission)
+  std::vector<MapState::Entry> iterate(const std::vector<MapState::Entry>& sequenced) const;
+
+ private:
+  std::vector<Entry> pending_;
+};
+
 // map.ts:176-246: header blob {"blobs":[...],"content":{...}} plus blobN for values ≥ 8 KiB and
 // for each 16 KiB flush; object keys enumerate array indices first (OrdinaryOwnPropertyKeys).
 struct MapSummary {

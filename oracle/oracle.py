@@ -291,6 +291,28 @@ def map_replay_sparse(batch, threads=1):
     return counts, ent[take], secs.value
 
 
+def map_pending(batch):
+    """The local client's optimistic view of every document (MapKernel pendingData over the sequenced
+    entries, oracle/map.cpp PendingMap): (counts[n_docs], status[n_docs], entries packed in document
+    order) — the layout of fmt_map_pending_fetch."""
+    from fluidframework_amd.native import MAP_ENTRY_DTYPE
+
+    ops = np.ascontiguousarray(batch.ops)
+    offs = np.ascontiguousarray(batch.doc_op_offsets, dtype=np.uint64)
+    ev = np.ascontiguousarray(batch.local_ops)
+    eo = np.ascontiguousarray(batch.local_offsets, dtype=np.uint64)
+    counts = np.zeros(batch.n_docs, dtype=np.uint32)
+    status = np.zeros(batch.n_docs, dtype=np.int32)
+    ent = np.zeros(max(len(ops) + len(ev), 1), dtype=MAP_ENTRY_DTYPE)
+    lib().orc_map_pending(_ptr(ops), _ptr(offs), ctypes.c_uint32(batch.n_docs), ctypes.c_uint32(batch.key_bound),
+                          _ptr(ev), _ptr(eo), _ptr(counts), _ptr(status), _ptr(ent))
+    c = counts.astype(np.int64)
+    first = np.cumsum(c) - c
+    base = offs[:-1].astype(np.int64) + eo[:-1].astype(np.int64)
+    take = np.arange(int(c.sum()), dtype=np.int64) + np.repeat(base - first, c)
+    return counts, status, ent[take]
+
+
 def map_summary(batch, doc: int):
     ops = np.ascontiguousarray(batch.ops)
     b, e = int(batch.doc_op_offsets[doc]), int(batch.doc_op_offsets[doc + 1])
