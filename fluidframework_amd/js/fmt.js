@@ -20,6 +20,7 @@ const summary = require("./summary.js");
 const MT_INSERT = 0, MT_REMOVE = 1, MT_ANNOTATE = 2, MT_GROUP = 3, MT_OBLITERATE = 4, MT_OBLITERATE_SIDED = 5; // ops.ts:61-71
 const MAP_SET = 0, MAP_DELETE = 1, MAP_CLEAR = 2, MAP_KIND_SHIFT = 30;
 const MAP_VALUE_UNDEFINED = 0x3fffffff, MAP_ABSENT = 0xffffffff;
+const MAP_EV_SUBMIT = 0, MAP_EV_ACK = 1, MAP_EV_ROLLBACK = 2;  // fmt.h FMT_MAP_EV_*
 const FMT_MT_F_GROUP_CONT = 1, FMT_MT_F_CATCHUP = 2, FMT_MT_F_RMORDER = 4;
 const FMT_MT_F_START_BEFORE = 8, FMT_MT_F_END_BEFORE = 16; // sided obliterate places (client.ts:680-700)
 const FMT_MT_F_MARKER = 32, FMT_MT_SEG_MARKER = 0x80000000, FMT_MT_LEAF_MARKER = 0x8000; // Marker segments
@@ -772,11 +773,71 @@ class MapStreamBuilder {
 		this.values = new Dictionary();
 		this.ops = new RecordBuffer(MAP_OP_BYTES);
 		this.docOps = [];
+		this.events = new RecordBuffer(MAP_OP_BYTES);  // fmt_map_local_op records (same 16-byte shape)
+		this.docEvents = [];
+		this.unacked = [];
 	}
 	beginDoc() {
 		this.docOps.push(0);
+		this.docEvents.push(0);
+		this.unacked = [];
 		this.lastSeq = 0;
 		return this.docOps.length - 1;
+	}
+	/** (key id, kind_value) of a set / delete / clear op's contents. */
+	record(contents) {
+		if (contents.type === "clear") return [0, (MAP_CLEAR << MAP_KIND_SHIFT) >>> 0];
+		if (contents.type !== "set" && contents.type !== "delete") throw new UnsupportedOp(`map op type ${contents.type}`);
+		const key = this.keys.intern(contents.key);
+		if (contents.type === "delete") return [key, (MAP_DELETE << MAP_KIND_SHIFT) >>> 0];
+		const sv = contents.value;
+		if (sv.type !== "Plain") throw new UnsupportedOp("legacy Shared value type");
+		let vid = MAP_VALUE_UNDEFINED;
+		if ("value" in sv && sv.value !== undefined) {
+			vid = this.values.intern(JSON.stringify(sv.value));
+			if (vid >= MAP_VALUE_UNDEFINED) throw new UnsupportedOp("value dictionary overflow");
+		}
+		return [key, ((MAP_SET << MAP_KIND_SHIFT) | vid) >>> 0];
+	}
+	pushEvent(doc, key, event, kv) {
+		const o = this.events.next();
+		const v = this.events.view;
+		v.setUint32(o, doc, true);
+		v.setUint32(o + 4, key, true);
+		v.setUint32(o + 8, event, true);
+		v.setUint32(o + 12, kv, true);
+		this.docEvents[doc]++;
+	}
+	/**
+	 * The document's local client (MapKernel pendingData, mapKernel.ts:132-139): set / delete / clear
+	 * on the attached map enters pendingData (:388-538) until its ack; rollback drops the newest
+	 * (:633-700).
+	 */
+	localSubmit(doc, contents) {
+		if (doc !== this.docOps.length - 1) throw new UnsupportedOp("documents must be packed contiguously");
+		const [key, kv] = this.record(contents);
+		this.pushEvent(doc, key, MAP_EV_SUBMIT, kv);
+		this.unacked.push([key, kv]);
+	}
+	/** The oldest pending local op comes back sequenced (the handlers' local branches, :706-853). */
+	localAck(doc, seq) {
+		if (this.unacked.length === 0) throw new Error("localAck with no unacknowledged local op");
+		if (seq < this.lastSeq) throw new Error(`map message seq ${seq} after ${this.lastSeq}: messages must arrive in seq order`);
+		this.lastSeq = seq;
+		const [key, kv] = this.unacked.shift();
+		const o = this.ops.next();
+		const v = this.ops.view;
+		v.setUint32(o, doc, true);
+		v.setUint32(o + 4, key, true);
+		v.setUint32(o + 8, this.docOps[doc] + 1, true);
+		v.setUint32(o + 12, kv, true);
+		this.docOps[doc]++;
+		this.pushEvent(doc, key, MAP_EV_ACK, kv);
+	}
+	localRollback(doc) {
+		if (this.unacked.length === 0) throw new Error("localRollback with no unacknowledged local op");
+		const [key, kv] = this.unacked.pop();
+		this.pushEvent(doc, key, MAP_EV_ROLLBACK, kv);
 	}
 	/**
 	 * One sequenced map message. Messages of one bunch share their envelope's sequenceNumber
@@ -846,7 +907,7 @@ class MapStreamBuilder {
 			i += n;
 			offs[k + 1] = BigInt(i);
 		});
-		return {
+		const out = {
 			ops: this.ops.bytes(),
 			docOpOffsets: offs,
 			keyBound: Math.max(1, this.keys.items.length),
@@ -854,6 +915,17 @@ class MapStreamBuilder {
 			values: this.values.items.slice(),
 			nDocs: this.docOps.length,
 		};
+		if (this.docEvents.some((n) => n > 0)) {
+			const eo = new BigUint64Array(this.docEvents.length + 1);
+			let e = 0;
+			this.docEvents.forEach((n, k) => {
+				e += n;
+				eo[k + 1] = BigInt(e);
+			});
+			out.localOps = this.events.bytes();
+			out.localOffsets = eo;
+		}
+		return out;
 	}
 }
 
@@ -1147,12 +1219,42 @@ class MapReplay {
 /** Converged SharedMap state from the sparse path (key pools of any size): live entries per
  * document in JS Map insertion order (fmt_map_entry records). */
 class SparseMapReplay {
-	constructor(batch, counts, entries) {
+	constructor(batch, counts, entries, pending) {
 		this.batch = batch;
 		this.counts = new Uint32Array(counts);
 		this.view = new DataView(entries);
 		this.first = new Float64Array(this.counts.length + 1);
 		for (let d = 0; d < this.counts.length; d++) this.first[d + 1] = this.first[d] + this.counts[d];
+		if (pending !== undefined) {  // the local client's optimistic view (fmt_map_pending_*)
+			this.pCounts = new Uint32Array(pending.counts);
+			this.pStatus = new Int32Array(pending.status);
+			this.pView = new DataView(pending.entries);
+			this.pFirst = new Float64Array(this.pCounts.length + 1);
+			for (let d = 0; d < this.pCounts.length; d++) this.pFirst[d + 1] = this.pFirst[d] + this.pCounts[d];
+		}
+	}
+	/**
+	 * The local client's view of document doc (MapKernel's internalIterator over sequencedData and
+	 * pendingData, mapKernel.ts:176-240): [[key, value], ...] in its iteration order.
+	 */
+	optimisticEntries(doc) {
+		if (this.pCounts === undefined) return this.entries(doc);
+		if (this.pStatus[doc] !== 0) {
+			const e = new Error(`document ${doc}: local events do not match its pending ops`);
+			e.code = "FMT_E_DATA";
+			throw e;
+		}
+		const out = [];
+		for (let i = this.pFirst[doc]; i < this.pFirst[doc + 1]; i++) {
+			const k = this.pView.getUint32(i * 12, true), v = this.pView.getUint32(i * 12 + 4, true);
+			out.push([this.batch.keys[k], v === MAP_VALUE_UNDEFINED ? undefined : JSON.parse(this.batch.values[v])]);
+		}
+		return out;
+	}
+	/** MapKernel.get (:374-392): the optimistic value. */
+	optimisticGet(doc, key) {
+		const e = this.optimisticEntries(doc).find(([k]) => k === key);
+		return e === undefined ? undefined : e[1];
 	}
 	/** [[key id, value id, birth seq], ...] of document doc in birth order. */
 	rawEntries(doc) {
@@ -1199,7 +1301,7 @@ class Engine {
 	/** The sparse LWW path (fmt_map_*_sparse): any key pool size, live entries only. */
 	async replayMapSparse(batch) {
 		const r = await native().replayMapSparse(this.ctx, batch);
-		return new SparseMapReplay(batch, r.counts, r.entries);
+		return new SparseMapReplay(batch, r.counts, r.entries, r.pending);
 	}
 	close() {
 		native().close(this.ctx);

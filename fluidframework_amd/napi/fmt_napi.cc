@@ -272,6 +272,11 @@ struct Job {
   uint32_t n_docs = 0, key_bound = 0;
   std::vector<uint8_t> out;  // headers, map slots, sparse counts
   std::vector<uint8_t> out2; // sparse entries
+  // sparse map with the local client's events (fmt_map_pending_*): events, offsets, results
+  const fmt_map_local_op* ev = nullptr;
+  uint64_t n_ev = 0;
+  const uint64_t* ev_offs = nullptr;
+  std::vector<uint8_t> pcounts, pstatus, pentries;
   // summarizeLegacy: JSON-quoted keys and value texts (copied on the JS thread), chunk, threads
   std::vector<std::string> keys, values;
   uint32_t chunk = 0, threads = 0;
@@ -301,6 +306,19 @@ void Execute(napi_env, void* p) {  // libuv worker thread: no N-API calls here
       j->out2.resize(size_t(n) * sizeof(fmt_map_entry));
       j->rc = fmt_map_fetch_sparse(ctx, reinterpret_cast<uint32_t*>(j->out.data()),
                                    reinterpret_cast<fmt_map_entry*>(j->out2.data()), n, &n);
+    }
+    if (j->rc == FMT_OK && j->ev_offs != nullptr) {  // the local client's optimistic view
+      j->rc = fmt_map_pending_run(ctx, j->ev, j->n_ev, j->ev_offs);
+      uint64_t np = 0;
+      j->pcounts.resize(size_t(j->n_docs) * sizeof(uint32_t));
+      j->pstatus.resize(size_t(j->n_docs) * sizeof(int32_t));
+      auto* pc = reinterpret_cast<uint32_t*>(j->pcounts.data());
+      auto* ps = reinterpret_cast<int32_t*>(j->pstatus.data());
+      if (j->rc == FMT_OK) j->rc = fmt_map_pending_fetch(ctx, pc, ps, nullptr, 0, &np);
+      if (j->rc == FMT_OK) {
+        j->pentries.resize(size_t(np) * sizeof(fmt_map_entry));
+        j->rc = fmt_map_pending_fetch(ctx, pc, ps, reinterpret_cast<fmt_map_entry*>(j->pentries.data()), np, &np);
+      }
     }
   } else if (j->kind == Job::kSummarize) {
     std::vector<const char*> k, v;
@@ -336,6 +354,14 @@ void Complete(napi_env env, napi_status, void* p) {  // JS thread
     napi_create_object(env, &o);
     napi_set_named_property(env, o, "counts", buffer(j->out));
     napi_set_named_property(env, o, "entries", buffer(j->out2));
+    if (j->ev_offs != nullptr) {
+      napi_value p;
+      napi_create_object(env, &p);
+      napi_set_named_property(env, p, "counts", buffer(j->pcounts));
+      napi_set_named_property(env, p, "status", buffer(j->pstatus));
+      napi_set_named_property(env, p, "entries", buffer(j->pentries));
+      napi_set_named_property(env, o, "pending", p);
+    }
     napi_resolve_deferred(env, j->deferred, o);
   } else if (j->kind == Job::kSummarize) {
     napi_value o, v;
@@ -558,9 +584,11 @@ napi_value ReplayMap(napi_env env, napi_callback_info info) {
   return queue(env, j, argv[0], "fmtReplayMap");
 }
 
-// replayMapSparse(ctx, {ops, docOpOffsets, keyBound}) -> Promise<{counts, entries}>: the sparse LWW path
-// (key pools of any size): counts = n_docs u32 live-entry counts, entries = fmt_map_entry records of
-// all documents packed in document order, each document's in JS Map insertion order.
+// replayMapSparse(ctx, {ops, docOpOffsets, keyBound, localOps?, localOffsets?}) -> Promise<{counts,
+// entries, pending?}>: the sparse LWW path (key pools of any size): counts = n_docs u32 live-entry
+// counts, entries = fmt_map_entry records of all documents packed in document order, each
+// document's in JS Map insertion order; with the local client's events, pending = {counts, status,
+// entries} of the optimistic view (fmt_map_pending_run / fetch).
 napi_value ReplayMapSparse(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -590,6 +618,26 @@ napi_value ReplayMapSparse(napi_env env, napi_callback_info info) {
   j->map_offs = static_cast<const uint64_t*>(offs);
   j->n_docs = uint32_t(n_offs_b / 8 - 1);
   j->key_bound = key_bound;
+  // optional: the local client's events (localOps: fmt_map_local_op records, localOffsets: n_docs + 1)
+  void *ev, *eo;
+  size_t n_ev_b, n_eo_b;
+  if (!get_bytes(env, prop(env, b, "localOps"), "localOps", &ev, &n_ev_b) ||
+      !get_bytes(env, prop(env, b, "localOffsets"), "localOffsets", &eo, &n_eo_b)) {
+    delete j;
+    return nullptr;
+  }
+  if (eo != nullptr) {
+    if (n_ev_b % sizeof(fmt_map_local_op) || n_eo_b != (size_t(j->n_docs) + 1) * 8) {
+      delete j;
+      throw_fmt(env, FMT_E_USAGE, "replayMapSparse: localOps / localOffsets do not match the fmt_map_local_op layout");
+      return nullptr;
+    }
+    j->ev = static_cast<const fmt_map_local_op*>(ev);
+    j->n_ev = n_ev_b / sizeof(fmt_map_local_op);
+    j->ev_offs = static_cast<const uint64_t*>(eo);
+    keep_array(env, j, prop(env, b, "localOps"));
+    keep_array(env, j, prop(env, b, "localOffsets"));
+  }
   keep_array(env, j, prop(env, b, "ops"));
   keep_array(env, j, prop(env, b, "docOpOffsets"));
   return queue(env, j, argv[0], "fmtReplayMapSparse");

@@ -466,3 +466,59 @@ def test_js_packer_document_local_values_match_python(addon, tmp_path):
     assert rd("relpos.bin", np.uint8).tobytes() == py.relpos.tobytes()
     assert np.array_equal(rd("base.bin", np.uint32), py.value_base)
     assert json.load(open(tmp_path / "meta.json"))["values"] == py.values
+
+
+def _pending_js(body):
+    """A JS program that rebuilds the map pending scenarios (tests/golden/map_pending_cases.json) with
+    fmt.js's MapStreamBuilder, one document per assertion as test_map_pending.golden_checkpoints does."""
+    gold = os.path.join(REPO, "tests", "golden", "map_pending_cases.json")
+    return (f"const fmt=require({json.dumps(os.path.join(PKG, 'js', 'fmt.js'))});"
+            f"const cases=JSON.parse(require('fs').readFileSync({json.dumps(gold)},'utf8')).cases;"
+            "const plain=(o)=>o.type!=='set'?o:{type:'set',key:o.key,value:{type:'Plain',value:o.value}};"
+            "const b=new fmt.MapStreamBuilder();const checks=[];"
+            "for(const c of cases){c.steps.forEach((st,si)=>{if(!st[0].startsWith('expect'))return;"
+            "const d=b.beginDoc();let seq=0;for(const s of c.steps.slice(0,si)){"
+            "if(s[0]==='local')b.localSubmit(d,plain(s[1]));"
+            "else if(s[0]==='flush'){while(b.unacked.length)b.localAck(d,++seq);}"
+            "else if(s[0]==='remote')b.addMessage(d,++seq,plain(s[1]));"
+            "else if(s[0]==='rollback_all'){while(b.unacked.length)b.localRollback(d);}}"
+            "checks.push([d,st]);});}const batch=b.finish();" + body)
+
+
+def test_js_map_pending_packing_matches_python(addon, tmp_path):
+    """fmt.js packs the local client's events (localSubmit / localAck / localRollback) into the same
+    fmt_map_local_op records and sequenced ops as the Python host."""
+    from test_map_pending import golden_checkpoints
+
+    script = tmp_path / "pending_pack.js"
+    script.write_text(_pending_js(
+        "const hex=(a)=>Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
+        "process.stdout.write(JSON.stringify({ops:hex(batch.ops),ev:hex(batch.localOps),"
+        "eo:Array.from(batch.localOffsets,Number),keys:batch.keys,values:batch.values}));"))
+    r = _node(str(script))
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    py = golden_checkpoints()[0].finish()
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert bytes.fromhex(out["ev"]) == py.local_ops.tobytes()
+    assert out["eo"] == py.local_offsets.tolist()
+    assert out["keys"] == py.keys and out["values"] == py.values
+
+
+@pytest.mark.gpu
+def test_js_map_pending_view_on_gpu(addon, tmp_path):
+    """The JS driver's optimistic view (replayMapSparse with localOps, SparseMapReplay
+    .optimisticEntries) reaches what the reference's rollback / iteration tests assert."""
+    from test_map_pending import _check_assertion, golden_checkpoints
+
+    script = tmp_path / "pending_gpu.js"
+    script.write_text("(async()=>{" + _pending_js(
+        "const e=new fmt.Engine(0);const r=await e.replayMapSparse(batch);"
+        "const out=checks.map(([d,st])=>[r.optimisticEntries(d),st]);e.close();"
+        "process.stdout.write(JSON.stringify(out));") + "})().catch((e)=>{console.error(e);process.exit(1);});")
+    r = _node(str(script), timeout=300)
+    assert r.returncode == 0, r.stderr
+    checks = json.loads(r.stdout)
+    assert len(checks) == len(golden_checkpoints()[1])
+    for view, step in checks:
+        _check_assertion([tuple(x) for x in view], step)
