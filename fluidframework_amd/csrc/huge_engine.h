@@ -37,6 +37,7 @@
 
 #include "../../include/fmt.h"
 #include "wave.h"
+#include "adjust.h"
 
 #include <algorithm>
 #include <vector>
@@ -173,6 +174,7 @@ struct HugeState {
                       // output index (or nullptr: no remove-order recording)
   uint32_t* mkIds;    // [mkCap]: every marker leaf ever in the document, in insertion order (relative
   uint32_t mkCap;     //   positions; nullptr: the batch has none)
+  uint32_t* outIdx;   // [idCap]: at output, leaf id -> output index (annotate-adjust batches; else nullptr)
 };
 
 // LDS state of the wave.
@@ -236,6 +238,10 @@ struct HugeInputs {
   const fmt_mt_relpos* relpos;
   uint32_t nRelpos;
   uint32_t markerKey;  // key id of "markerId"
+  // annotate-adjust (nullptr: none in the batch): the batch's tables (adjust.h), this document's
+  // index into their per-document slabs (computed numbers, PropertiesManager records)
+  const fmt_mt::AdjustTables* adj;
+  uint32_t doc;
 };
 
 // The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
@@ -321,6 +327,7 @@ class HugeDoc {
   uint32_t rmPendFrom[2] = {0, 0}, rmPendTo[2] = {0, 0};
   uint32_t rmKind = FMT_MT_RM_SET;
   uint32_t mkN = 0;  // markers listed in S.mkIds
+  int pmN = 0;       // PropertiesManager records in use (deleted ones included), annotate-adjust batches
   // shader-clock totals per phase (diagnostics, written to HugeOut::prof; inclusive, so nested phases
   // overlap): 0 replay, 1 window pass (groups), 2 window pass (slots), 3 zamboni, 4 graduation,
   // 5 load, 6 output, 7 finds, 8 scour, 9 leaf-parent pack, 10 slot insert/remove, 11 heap,
@@ -1419,18 +1426,37 @@ class HugeDoc {
   FMT_DEV uint32_t setKv(uint32_t p, uint32_t k) const {
     return rd(S.props + ((static_cast<size_t>(p) + k / FMT_MT_PROPS_MAX) * kPropWords + 1 + k % FMT_MT_PROPS_MAX));
   }
-  FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
-    constexpr int kKeysMax = FMT_MT_PROPS_KEYS_MAX;
-    uint32_t cnt = old != kNoProps ? ldu(S.props + old * kPropWords) : 0u;
+  FMT_DEV uint32_t loadWork(uint32_t old) {
+    const uint32_t cnt = old != kNoProps ? ldu(S.props + old * kPropWords) : 0u;
     FOR_LANES(l) { L->kvWork[l] = l < static_cast<int>(cnt) ? setKv(old, static_cast<uint32_t>(l)) : 0u; }
     waveSync();
+    return cnt;
+  }
+  // adjSite: the annotate call site, the only one whose props ops may hold annotate-adjust entries
+  // ((key, FMT_MT_VALUE_ADJUST) then the adjust row; computePropertyValue folds into the current value)
+  FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId, bool adjSite = false) {
+    constexpr int kKeysMax = FMT_MT_PROPS_KEYS_MAX;
+    uint32_t cnt = loadWork(old);
     const uint32_t a = ldu(in.propsOff + opId), b = ldu(in.propsOff + opId + 1);
     for (uint32_t t = a; t < b; t++) {
-      const uint32_t e = ldu(in.propsKv + t);
+      uint32_t e = ldu(in.propsKv + t);
       Lane<bool> hit;
       FOR_LANES(l) { LANE(hit) = l < static_cast<int>(cnt) && (L->kvWork[l] >> 16) == (e >> 16); }
       const uint64_t m = ballot(hit);
       const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
+      if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
+        if (!adjSite || in.adj == nullptr || ++t >= b) {
+          fail(FMT_E_DATA);
+          return kNoProps;
+        }
+        const uint32_t cur = pos < cnt ? uni(L->kvWork[pos]) & 0xFFFFu : 0u;  // absent: null
+        const uint32_t v = fmt_mt::adjustFold(in.adj, in.doc, cur, ldu(in.propsKv + t));
+        if (v == fmt_mt::kAdjFailData || v == fmt_mt::kAdjFailCap) {
+          fail(v == fmt_mt::kAdjFailData ? FMT_E_DATA : FMT_E_CAPACITY);
+          return kNoProps;
+        }
+        e = (e & 0xFFFF0000u) | v;
+      }
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
         if (pos < cnt) {
           Lane<uint32_t> v;
@@ -1458,6 +1484,10 @@ class HugeDoc {
       }
       waveSync();
     }
+    return internWork(cnt);
+  }
+  // The interned id of the working set (kvWork[0 .. cnt)), a new set if none has its entries.
+  FMT_DEV uint32_t internWork(uint32_t cnt) {
     // Interned already? Sets are found through two hash tables in HBM: one keyed by the ordered
     // entries (the same set), one by the entries in any order (its match class).
     Lane<uint32_t> ho, hu;
@@ -1524,6 +1554,195 @@ class HugeDoc {
     return id;
   }
 
+  // ------------------------------------------------------------------ PropertiesManager (annotate-adjust)
+  // Per leaf, the remote changes a legacy summary's getAtSeq(properties, minSeq) needs
+  // (segmentPropertiesManager.ts:140-345), as mt_engine.h keeps them: records of 4 words in the
+  // document's HBM slab (AdjustTables::pm), in creation order — a head {leaf id, key, kind 0, value =
+  // msnConsensus} per (leaf, key) with pending changes (the manager's Map order) and the changes
+  // {leaf id, key | 1 << 16, seq, value after the change}. Leaf id 0 marks a deleted record.
+  FMT_DEV uint32_t* pmBase() const { return in.adj->pm + 4 * in.adj->pmOffsets[in.doc]; }
+  FMT_DEV int pmCap() const { return static_cast<int>(in.adj->pmOffsets[in.doc + 1] - in.adj->pmOffsets[in.doc]); }
+  FMT_DEV uint32_t pmWord(int i, int w) const { return ldu(pmBase() + 4 * i + w); }
+  FMT_DEV void pmSet(int i, int w, uint32_t v) { st1(pmBase() + 4 * i + w, v); }
+  // First record at or after `from` whose (leaf id, key | kind) match under `mask`, or -1.
+  FMT_DEV int pmFind(uint32_t leaf, uint32_t keyKind, uint32_t mask, int from = 0) const {
+    const uint32_t* R = pmBase();
+    for (int base = from; base < pmN; base += 64) {
+      Lane<bool> p;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(p) = i < pmN && rd(R + 4 * i) == leaf && (rd(R + 4 * i + 1) & mask) == (keyKind & mask);
+      }
+      const uint64_t m = ballot(p);
+      if (m != 0) return base + ctz64(m);
+    }
+    return -1;
+  }
+  FMT_DEV void pmCompact() {  // drops deleted records, keeping the order
+    uint32_t* R = pmBase();
+    int out = 0;
+    for (int base = 0; base < pmN; base += 64) {
+      Lane<uint32_t> w0, w1, w2, w3;
+      Lane<bool> live;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(w0) = i < pmN ? rd(R + 4 * i) : 0u;
+        LANE(w1) = i < pmN ? rd(R + 4 * i + 1) : 0u;
+        LANE(w2) = i < pmN ? rd(R + 4 * i + 2) : 0u;
+        LANE(w3) = i < pmN ? rd(R + 4 * i + 3) : 0u;
+        LANE(live) = LANE(w0) != 0u;
+      }
+      const uint64_t m = ballot(live);
+      waveSync();
+      FOR_LANES(l) {
+        if (LANE(live)) {
+          const int at = out + __builtin_popcountll(m & ((1ull << l) - 1ull));
+          R[4 * at] = LANE(w0);
+          R[4 * at + 1] = LANE(w1);
+          R[4 * at + 2] = LANE(w2);
+          R[4 * at + 3] = LANE(w3);
+        }
+      }
+      waveSync();
+      out += __builtin_popcountll(m);
+    }
+    pmN = out;
+  }
+  FMT_DEV bool pmAppend(uint32_t leaf, uint32_t keyKind, int seq, uint32_t value) {
+    if (pmN >= pmCap()) pmCompact();
+    if (pmN >= pmCap()) return fail(FMT_E_CAPACITY);
+    uint32_t* R = pmBase() + 4 * pmN;
+    FOR_LANES(l) {
+      if (l < 4) R[l] = l == 0 ? leaf : l == 1 ? keyKind : l == 2 ? static_cast<uint32_t>(seq) : value;
+    }
+    waveSync();
+    pmN++;
+    return true;
+  }
+  // updateMsn(msn) (:275-291) on the manager of `leaf`: changes at or below msn fold into
+  // msnConsensus; a key left with none leaves the manager.
+  FMT_DEV void pmUpdateMsn(uint32_t leaf, int msn) {
+    for (int h = pmFind(leaf, 0u, 0x10000u); h >= 0 && status == FMT_OK; h = pmFind(leaf, 0u, 0x10000u, h + 1)) {
+      const uint32_t key = pmWord(h, 1) & 0xFFFFu;
+      uint32_t* R = pmBase();
+      int last = -1;
+      bool pending = false;
+      for (int base = h + 1; base < pmN; base += 64) {  // (a head precedes its key's changes)
+        Lane<bool> fold, keep;
+        FOR_LANES(l) {
+          const int i = base + l;
+          const bool mine = i < pmN && rd(R + 4 * i) == leaf && rd(R + 4 * i + 1) == (key | 0x10000u);
+          const int sq = mine ? static_cast<int>(rd(R + 4 * i + 2)) : 0;
+          LANE(fold) = mine && sq <= msn;
+          LANE(keep) = mine && sq > msn;
+        }
+        const uint64_t mf = ballot(fold), mk = ballot(keep);
+        if (mf != 0) last = base + 63 - __builtin_clzll(mf);
+        pending = pending || mk != 0;
+        waveSync();
+        FOR_LANES(l) {
+          if (LANE(fold)) R[4 * (base + l)] = 0u;  // folded: deleted (its value word stays readable)
+        }
+        waveSync();
+      }
+      if (last >= 0) pmSet(h, 3, pmWord(last, 3));
+      if (!pending) pmSet(h, 0, 0u);
+    }
+  }
+  FMT_DEV void pmCopy(uint32_t from, uint32_t to) {
+    if (pmFind(from, 0u, 0u) < 0) return;
+    pmCompact();  // (no compaction while copying: record indices stay put)
+    const int end = pmN;
+    for (int i = pmFind(from, 0u, 0u); i >= 0 && i < end && status == FMT_OK; i = pmFind(from, 0u, 0u, i + 1)) {
+      if (pmN >= pmCap()) {
+        fail(FMT_E_CAPACITY);
+        return;
+      }
+      pmAppend(to, pmWord(i, 1), static_cast<int>(pmWord(i, 2)), pmWord(i, 3));
+    }
+  }
+  FMT_DEV void pmDropLeaf(uint32_t leaf) {
+    uint32_t* R = pmBase();
+    for (int base = 0; base < pmN; base += 64) {
+      Lane<bool> mine;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(mine) = i < pmN && rd(R + 4 * i) == leaf;
+      }
+      waveSync();
+      FOR_LANES(l) {
+        if (LANE(mine)) R[4 * (base + l)] = 0u;
+      }
+      waveSync();
+    }
+  }
+  // Working-set edit: key set to v (v == 0: deleted), in kvWork[0 .. cnt).
+  FMT_DEV uint32_t workSet(uint32_t cnt, uint32_t key, uint32_t v) {
+    uint32_t pos = cnt;
+    for (uint32_t k = 0; k < cnt; k++)
+      if ((uni(L->kvWork[k]) >> 16) == key) pos = k;
+    if (v == 0u) {
+      if (pos < cnt) {
+        for (uint32_t k = pos; k + 1 < cnt; k++) {
+          const uint32_t x = uni(L->kvWork[k + 1]);
+          waveSync();
+          FOR_LANES(l) {
+            if (l == 0) L->kvWork[k] = x;
+          }
+        }
+        cnt--;
+      }
+    } else if (pos < cnt) {
+      FOR_LANES(l) {
+        if (l == 0) L->kvWork[pos] = (key << 16) | v;
+      }
+    } else if (cnt < static_cast<uint32_t>(FMT_MT_PROPS_KEYS_MAX)) {
+      FOR_LANES(l) {
+        if (l == 0) L->kvWork[cnt] = (key << 16) | v;
+      }
+      cnt++;
+    }
+    waveSync();
+    return cnt;
+  }
+  // handleProperties (:188-238) of an annotate op on one leaf, before its prop set changes: every
+  // change in opToChanges order (a raw change folds into msnConsensus while its key has nothing
+  // pending), then updateMsn(minSeq).
+  FMT_DEV void pmAnnotate(uint32_t leaf, uint32_t old, uint32_t opId, int seq) {
+    uint32_t cnt = loadWork(old);
+    const uint32_t a = ldu(in.propsOff + opId), b = ldu(in.propsOff + opId + 1);
+    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+      const uint32_t e = ldu(in.propsKv + t);
+      const uint32_t key = e >> 16;
+      const bool adjust = (e & 0xFFFFu) == FMT_MT_VALUE_ADJUST;
+      uint32_t pos = cnt;
+      for (uint32_t k = 0; k < cnt; k++)
+        if ((uni(L->kvWork[k]) >> 16) == key) pos = k;
+      const uint32_t before = pos < cnt ? uni(L->kvWork[pos]) & 0xFFFFu : 0u;
+      uint32_t after = e & 0xFFFFu;
+      if (adjust) {
+        if (++t >= b) {
+          fail(FMT_E_DATA);
+          return;
+        }
+        after = fmt_mt::adjustFold(in.adj, in.doc, before, ldu(in.propsKv + t));
+        if (after == fmt_mt::kAdjFailData || after == fmt_mt::kAdjFailCap) {
+          fail(after == fmt_mt::kAdjFailData ? FMT_E_DATA : FMT_E_CAPACITY);
+          return;
+        }
+      }
+      int h = pmFind(leaf, key, 0x1FFFFu);
+      if (h < 0) {
+        if (!pmAppend(leaf, key, 0, before)) return;
+        h = pmN - 1;
+      }
+      if (!adjust && pmFind(leaf, key | 0x10000u, 0x1FFFFu, h + 1) < 0) pmSet(h, 3, after);
+      else if (!pmAppend(leaf, key | 0x10000u, seq, after)) return;
+      cnt = workSet(cnt, key, after);  // the working set follows the change
+    }
+    pmUpdateMsn(leaf, minSeq);
+  }
+
   // ------------------------------------------------------------------ op pieces
   // splitLeafSegment (mergeTree.ts:1768-1796) of leaf (b, k) at offset o (0 < o < len): the right part
   // follows it in the same block, with a fresh id; a window leaf's right part joins the window table.
@@ -1552,6 +1771,7 @@ class HugeDoc {
     regsInsert(R, k + 1, y, wy);
     st1(S.leafBlk + y.id, b);
     obRefsMove(x.id, y.id, o, -o);  // the right part takes the references at/after the split
+    if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
     if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
       rmPendFrom[rmPendN] = x.id;
       rmPendTo[rmPendN] = y.id;
@@ -1798,7 +2018,7 @@ class HugeDoc {
           if (op.type == FMT_MT_REMOVE) {
             stableDelta += removeLeaf(b, k, x, seq, c, readlane(wi, k), g);
           } else {
-            annotateLeaf(b, k, x, op.payload);
+            annotateLeaf(b, k, x, op.payload, seq);
             if (cuRec && x.rm == kNotRemoved) cuPush(x.id);  // deltaSegments: annotated, not removed (:2045-2047)
           }
           if (status != FMT_OK) return;
@@ -1848,8 +2068,12 @@ class HugeDoc {
     return 0;
   }
 
-  FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId) {
-    const uint32_t np = applyProps(mProps(x.meta), opId);
+  FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId, int seq) {
+    if (in.adj != nullptr) {  // the leaf's PropertiesManager first (handleProperties, :188-238)
+      pmAnnotate(x.id, mProps(x.meta), opId, seq);
+      if (status != FMT_OK) return;
+    }
+    const uint32_t np = applyProps(mProps(x.meta), opId, true);
     if (status != FMT_OK) return;
     x.meta = (x.meta & ~(0xFFFFu << 8)) | (np << 8);
     putLeaf(b, j, x);
@@ -2803,9 +3027,15 @@ class HugeDoc {
       LANE(dd) = LANE(P.dst) < 0 ? 0 : LANE(P.dst);
     }
     const Lane<uint32_t> headSrc = gather(srcU, dd);
+    Lane<bool> gone;
     FOR_LANES(l) {
       const bool valid = (l & 7) < LANE(cntL);
-      if (valid && (LANE(P.dst) < 0 || LANE(headSrc) != static_cast<uint32_t>(l))) S.leafBlk[LANE(f[5])] = kNone;
+      LANE(gone) = valid && (LANE(P.dst) < 0 || LANE(headSrc) != static_cast<uint32_t>(l));
+      if (LANE(gone)) S.leafBlk[LANE(f[5])] = kNone;
+    }
+    if (pmN > 0) {  // appended and unlinked leaves take their managers with them
+      waveSync();
+      for (uint64_t m = ballot(gone); m != 0 && status == FMT_OK; m &= m - 1) pmDropLeaf(readlane(f[5], ctz64(m)));
     }
   }
 
@@ -3102,6 +3332,8 @@ class HugeDoc {
     ProfScope ps_(prof[3]);
     for (int i = 0; i < 2; i++) {
       if (heapN == 0) break;
+      // segmentToScour?.segment?.propertyManager?.updateMsn(minSeq) (zamboni.ts:44)
+      if (pmN > 0) pmUpdateMsn(uni(L->heap[1].leafId), minSeq);
       if (heapSeq(1) > minSeq) break;
       const HeapEnt e = heapGet();
       const uint32_t b = ldu(S.leafBlk + e.leafId);
@@ -3610,8 +3842,59 @@ class HugeDoc {
   // Converged state in document order: fmt_mt_leaf records (block = leaf-block ordinal, low 16 bits,
   // pad = high 16 bits), the text of every leaf (tombstones included), the prop sets, the header.
   // Eight leaf blocks per wave step: lane l handles slot l % 8 of block l / 8.
+  // getAtSeq(properties, minSeq) (segmentPropertiesManager.ts:328-344) of every leaf with a manager,
+  // as mt_engine.h: its current properties with each pending key set to the value its changes at or
+  // below minSeq leave (null: deleted; a key the properties lack goes last, in the manager's key
+  // order), interned; outLegacy[output index] already holds every leaf's current set.
+  FMT_DEV void pmLegacyProps(uint16_t* outLegacy) {
+    const uint32_t* R = pmBase();
+    for (;;) {
+      if (status != FMT_OK) return;
+      int h = -1;  // the next head of a leaf not handled yet (a handled head's seq word gets bit 31)
+      for (int base = 0; base < pmN && h < 0; base += 64) {
+        Lane<bool> p;
+        FOR_LANES(l) {
+          const int i = base + l;
+          LANE(p) = i < pmN && rd(R + 4 * i) != 0u && (rd(R + 4 * i + 1) & 0x10000u) == 0u &&
+                    (rd(R + 4 * i + 2) & 0x80000000u) == 0u;
+        }
+        const uint64_t m = ballot(p);
+        if (m != 0) h = base + ctz64(m);
+      }
+      if (h < 0) return;
+      const uint32_t leaf = pmWord(h, 0);
+      int j = -1;
+      uint32_t cnt = 0;
+      if (ldu(S.leafBlk + leaf) != kNone) {
+        uint32_t b;
+        int k;
+        locate(leaf, &b, &k);
+        if (k >= 0) {
+          j = static_cast<int>(ldu(S.outIdx + leaf));
+          cnt = loadWork(mProps(ldu(S.lMeta + li(b, k))));
+        }
+      }
+      for (int g = h; g >= 0 && status == FMT_OK; g = pmFind(leaf, 0u, 0x10000u, g + 1)) {
+        pmSet(g, 2, 0x80000000u);  // (done: a head's seq word is otherwise unused)
+        if (j < 0) continue;
+        const uint32_t key = pmWord(g, 1) & 0xFFFFu;
+        uint32_t v = pmWord(g, 3);
+        for (int c = pmFind(leaf, key | 0x10000u, 0x1FFFFu, g + 1); c >= 0; c = pmFind(leaf, key | 0x10000u, 0x1FFFFu, c + 1)) {
+          if (static_cast<int>(pmWord(c, 2)) > minSeq) break;  // (a key's changes are in seq order)
+          v = pmWord(c, 3);
+        }
+        cnt = workSet(cnt, key, v);
+      }
+      if (j >= 0 && status == FMT_OK) {
+        const uint32_t id = internWork(cnt);
+        if (status != FMT_OK) return;
+        st1(outLegacy + j, static_cast<uint16_t>(id));
+      }
+    }
+  }
+
   FMT_DEV void writeOutputs(fmt_mt_doc_result* hdr, fmt_mt_leaf* outLeaves, uint64_t capLeaves, uint16_t* outChars,
-                            uint64_t capChars, fmt_mt_propset* outProps) {
+                            uint64_t capChars, fmt_mt_propset* outProps, uint16_t* outLegacy = nullptr) {
     uint64_t nLeaves = 0, nChars = 0, visible = 0;
     uint32_t nBlocks = 0;
     for (int k = 0; k < nGroups && status == FMT_OK; k++) {
@@ -3670,6 +3953,10 @@ class HugeDoc {
             x.pad = static_cast<uint16_t>((blk >> 16) | (mMarker(m) ? FMT_MT_LEAF_MARKER : 0u));
             outLeaves[o] = x;
             if (S.rmIds != nullptr) S.rmIds[rd(S.lId + i)] = static_cast<uint32_t>(o);  // (remove-order entries)
+            if (outLegacy != nullptr) {  // (annotate-adjust: getAtSeq below)
+              S.outIdx[rd(S.lId + i)] = static_cast<uint32_t>(o);
+              outLegacy[o] = static_cast<uint16_t>(mProps(m));
+            }
             const uint32_t t = rd(S.lText + i);
             for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(textAt(t + c));
           }
@@ -3679,6 +3966,10 @@ class HugeDoc {
         visible += tvl;
         nBlocks += tb;
       }
+    }
+    if (outLegacy != nullptr && S.outIdx != nullptr && status == FMT_OK) {
+      waveSync();
+      if (pmN > 0) pmLegacyProps(outLegacy);
     }
     FOR_LANES(l) {
       for (int p = l; p < nProps; p += 64) {
@@ -3737,6 +4028,7 @@ class HugeDoc {
     rmRec = false;
     rmPendN = 0;
     mkN = 0;
+    pmN = 0;
     nFree = 0;
     nProps = 0;
     if (inputs.nPropsOps > 0 || inputs.segProps != 0) {  // (empty prop-set hash tables)

@@ -78,6 +78,8 @@ struct SumView {
   const uint16_t* chars;
   const fmt_mt_propset* props;
   const uint16_t* legacyProps;  // per leaf: the prop set the legacy summary reads, or nullptr (leaf.props)
+  const uint32_t* cls;          // per prop set its match class as the engine interned it (huge documents,
+                                // up to 65534 sets), or nullptr: the summary kernel derives it in LDS
 };
 struct SumRun {
   uint32_t len;    // UTF-16 units of the merged segment
@@ -143,6 +145,8 @@ struct HugeOut {
   uint16_t* chars;
   uint64_t capChars;
   fmt_mt_propset* props;
+  uint16_t* legacy;          // annotate-adjust batches: per leaf the getAtSeq(minSeq) prop set, else nullptr
+  const uint32_t* cls;       // the engine's match class per prop set (HugeState::pClass)
   unsigned long long* prof;  // [24] shader-clock totals per phase (huge_engine.h HugeDoc::prof)
 };
 size_t hugeLdsBytes();

@@ -185,8 +185,8 @@ struct fmt_ctx {
   std::vector<HugeDocBufs> huge;             // per huge document
   std::vector<int32_t> mtHugeSlot;           // doc -> index in huge, or -1
   // documents that outgrow the large tier replay again, from their start, in the huge tier when
-  // they hold nothing it does not (mtHugeOk: no annotate-adjust or SnapshotV1 body segments with
-  // merge info, FMT_MT_F_LOADSEG); their starts
+  // they hold nothing it does not (mtHugeOk: no SnapshotV1 body segments with merge info,
+  // FMT_MT_F_LOADSEG); their starts
   std::vector<uint8_t> mtHugeOk;
   std::vector<uint8_t> mtSegProps;           // per document: a loaded segment has properties
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
@@ -862,6 +862,15 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   I.relpos = c->mtNRelpos ? c->mtRelpos.p : nullptr;
   I.nRelpos = c->mtNRelpos;
   I.markerKey = c->mtMarkerKey;
+  // annotate-adjust: the batch's tables (computed numbers, PropertiesManager records), the leaf id ->
+  // output index map of the getAtSeq output
+  I.adj = c->mtHasAdjust ? c->mtAdjTab.p : nullptr;
+  I.doc = d;
+  S.outIdx = nullptr;
+  if (c->mtHasAdjust) {
+    if ((e = alloc(static_cast<size_t>(S.idCap) * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    S.outIdx = static_cast<uint32_t*>(p);
+  }
   S.mkIds = nullptr;
   S.mkCap = 0;
   if (c->mtNRelpos) {
@@ -898,6 +907,12 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   O.chars = static_cast<uint16_t*>(p);
   if ((e = alloc(fmt_huge::kPropCap * sizeof(fmt_mt_propset), &p)) != hipSuccess) return drop(e);
   O.props = static_cast<fmt_mt_propset*>(p);
+  O.cls = S.pClass;
+  O.legacy = nullptr;  // annotate-adjust batches: per leaf the getAtSeq(minSeq) prop set
+  if (c->mtHasAdjust) {
+    if ((e = alloc(O.capLeaves * sizeof(uint16_t), &p)) != hipSuccess) return drop(e);
+    O.legacy = static_cast<uint16_t*>(p);
+  }
   if ((e = alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p)) != hipSuccess) return drop(e);
   O.prof = static_cast<unsigned long long*>(p);
   return FMT_OK;
@@ -1249,9 +1264,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
       const fmt_mt_op& op = b->ops[i];
       if (op.type == FMT_MT_INSERT) chars += fmt_mt_op_len(&op);
-      if ((op.flags & FMT_MT_F_LOADSEG) ||
-          (op.type == FMT_MT_ANNOTATE && adjCount[op.payload] > 0))
-        ok = 0;
+      if (op.flags & FMT_MT_F_LOADSEG) ok = 0;
     }
     if (b->snapshots && b->snapshots[d].loaded) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
@@ -1293,7 +1306,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (!c->mtHugeOk[d]) {  // (V1 body segments with merge info, annotate-adjust)
+      if (!c->mtHugeOk[d]) {  // (V1 body segments with merge info)
         refuse(d, FMT_E_UNSUPPORTED);
         continue;
       }
@@ -1685,7 +1698,7 @@ void docViews(const fmt_ctx* c, std::vector<fmt_kernels::SumView>& views) {
     const int32_t hs = d < c->mtHugeSlot.size() ? c->mtHugeSlot[d] : -1;
     if (hs >= 0) {
       const fmt_kernels::HugeOut& O = c->huge[static_cast<size_t>(hs)].out;
-      views[d] = {O.leaves, O.chars, O.props, nullptr};
+      views[d] = {O.leaves, O.chars, O.props, c->mtHasAdjust ? O.legacy : nullptr, O.cls};
     } else {
       const int32_t slot = d < c->mtBigSlot.size() ? c->mtBigSlot[d] : -1;
       const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(slot >= 0);

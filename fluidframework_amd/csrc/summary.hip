@@ -63,16 +63,16 @@ __global__ __launch_bounds__(64 * kSumWaves) void summaryRunsKernel(const fmt_mt
     const fmt_mt_doc_result h = hdrs[d];
     SumDocOut od{};
     od.status = static_cast<uint32_t>(h.status);
-    if (h.status != FMT_OK || h.n_props > static_cast<uint32_t>(kSumMaxProps)) {
+    const SumView V = views[d];
+    if (h.status != FMT_OK || (V.cls == nullptr && h.n_props > static_cast<uint32_t>(kSumMaxProps))) {
       if (h.status == FMT_OK) od.status = static_cast<uint32_t>(FMT_E_CAPACITY);
       if (lane == 0) docOut[d] = od;
       continue;
     }
-    const SumView V = views[d];
     const uint32_t n = h.n_leaves, np = h.n_props;
     const int32_t minSeq = h.min_seq;
     // match classes: the first prop set with the same content (empty sets: undefined's class)
-    for (uint32_t p = lane; p < np; p += 64) {
+    for (uint32_t p = lane; p < np && V.cls == nullptr; p += 64) {  // (huge documents: the engine's classes)
       const uint32_t an = V.props[p].n;
       uint16_t c = an == 0 ? 0xFFFFu : static_cast<uint16_t>(p);
       if (an != 0 && an != FMT_MT_PROPS_CONT)  // (continuation records: no leaf names them)
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64 * kSumWaves) void summaryRunsKernel(const fmt_mt
         m &= m - 1;
         const uint32_t l = sumLane(len, k), p = sumLane(props, k), lc = sumLane(last, k);
         const bool mk = sumLane(marker, k) != 0;
-        const uint32_t c = p == 0xFFFFu ? 0xFFFFu : static_cast<uint32_t>(cls[p]);
+        const uint32_t c = p == 0xFFFFu ? 0xFFFFu : V.cls != nullptr ? (V.cls[p] & 0xFFFFu) : static_cast<uint32_t>(cls[p]);
         const bool append = have && !runMarker && !mk && runLast != 10u &&
                             (runLen <= 256u || l <= 256u) && runCls == c;
         if (append) {

@@ -16,6 +16,64 @@
 
 using namespace fmt_huge;
 
+// Annotate-adjust tables of the last replay (runtime.cpp fmt_mt_load's, one document's slabs here):
+// the host numbers ascending with their first value id, the computed-number slab and the
+// PropertiesManager records.
+namespace {
+constexpr uint32_t kEmuNumCap = 1 << 16;
+constexpr uint32_t kEmuPmCap = 1 << 20;
+std::vector<double> g_numSorted, g_nums;
+std::vector<uint32_t> g_numSortedId, g_numSortedOffs, g_numCount, g_pm;
+std::vector<uint64_t> g_numOffs, g_pmOffs;
+fmt_mt::AdjustTables g_adj;
+
+const fmt_mt::AdjustTables* prepareNumbers(const fmt_mt_batch* b) {
+  g_numSorted.clear();
+  g_numSortedId.clear();
+  g_numSortedOffs.clear();
+  if (b->adjusts == nullptr || b->value_num == nullptr) return nullptr;
+  auto sortNumbers = [&](uint32_t lo, uint32_t hi, uint32_t base) {
+    std::vector<std::pair<double, uint32_t>> v;
+    for (uint32_t i = lo; i < hi; i++)
+      if (b->value_num[base + i] == b->value_num[base + i]) v.emplace_back(b->value_num[base + i] == 0.0 ? 0.0 : b->value_num[base + i], i);
+    std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    const size_t first = g_numSorted.size();
+    for (const auto& [x, i] : v) {
+      if (g_numSorted.size() > first && g_numSorted.back() == x) continue;
+      g_numSorted.push_back(x);
+      g_numSortedId.push_back(i);
+    }
+  };
+  if (b->doc_value_base != nullptr) {
+    g_numSortedOffs.assign(1, 0u);
+    for (uint32_t d = 0; d < b->n_docs; d++) {
+      sortNumbers(1, b->doc_value_base[d + 1] - b->doc_value_base[d] + 1, b->doc_value_base[d]);
+      g_numSortedOffs.push_back(static_cast<uint32_t>(g_numSorted.size()));
+    }
+  } else {
+    sortNumbers(0, b->n_values, 0);
+  }
+  // every document indexes its own slabs; only the replayed one gets room
+  g_nums.assign(kEmuNumCap, 0.0);
+  g_numCount.assign(b->n_docs, 0u);
+  g_pm.assign(static_cast<size_t>(kEmuPmCap) * 4, 0u);
+  g_adj = fmt_mt::AdjustTables{};
+  g_adj.adjusts = b->adjusts;
+  g_adj.nAdjusts = b->n_adjusts;
+  g_adj.nValues = b->n_values;
+  g_adj.valueNum = b->value_num;
+  g_adj.numSorted = g_numSorted.data();
+  g_adj.numSortedId = g_numSortedId.data();
+  g_adj.nNumSorted = static_cast<uint32_t>(g_numSorted.size());
+  g_adj.valueBase = b->doc_value_base;
+  g_adj.numSortedOffs = b->doc_value_base != nullptr ? g_numSortedOffs.data() : nullptr;
+  g_adj.nums = g_nums.data();
+  g_adj.numCount = g_numCount.data();
+  g_adj.pm = g_pm.data();
+  return &g_adj;
+}
+}  // namespace
+
 extern "C" {
 
 // Replays document d of the batch (a summary-loaded document, header chunk only) into the caller's
@@ -23,9 +81,12 @@ extern "C" {
 // A document that does not start from a summary starts from its initial text (one segment stamped
 // {0, FMT_LOCAL_CLIENT}) or empty, as the runtime replays documents that outgrow the large tier.
 // With catchup != nullptr the catch-up ranges of FMT_MT_F_CATCHUP ops go there (capCatchup ranges).
-int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+// With an annotate-adjust batch, legacy (one entry per output leaf) receives the getAtSeq(minSeq) prop
+// sets and nums / *nNums the document's computed numbers.
+int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
                         uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, fmt_mt_catchup_range* catchup,
-                        uint32_t capCatchup, fmt_mt_remove_order* rmOrder, uint32_t capRm) {
+                        uint32_t capCatchup, fmt_mt_remove_order* rmOrder, uint32_t capRm, uint16_t* legacy, double* nums,
+                        uint32_t capNums, uint32_t* nNums) {
   const bool loaded = b->snapshots != nullptr && b->snapshots[d].loaded;
   fmt_mt_snapshot_doc sd{};
   fmt_mt_snapshot_seg initSeg{};
@@ -118,15 +179,33 @@ int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   std::vector<uint32_t> mkIds(b->relpos != nullptr ? S.idCap : 0);
   doc->S.mkIds = b->relpos != nullptr ? mkIds.data() : nullptr;
   doc->S.mkCap = S.idCap;
+  const fmt_mt::AdjustTables* adj = prepareNumbers(b);
+  std::vector<uint64_t> numOffs(b->n_docs + 1ull, kEmuNumCap), pmOffs(b->n_docs + 1ull, kEmuPmCap);
+  for (uint32_t k = 0; k <= d && k <= b->n_docs; k++) numOffs[k] = pmOffs[k] = 0;  // (document d: [0, cap))
+  g_adj.numOffsets = numOffs.data();
+  g_adj.pmOffsets = pmOffs.data();
+  in.adj = adj;
+  in.doc = d;
+  std::vector<uint32_t> outIdx(adj != nullptr ? S.idCap : 0);
+  doc->S.outIdx = adj != nullptr ? outIdx.data() : nullptr;
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
   doc->run(in);
-  doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props);
+  doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props, adj != nullptr ? legacy : nullptr);
+  if (nNums) *nNums = adj != nullptr ? g_numCount[d] : 0u;
+  for (uint32_t k = 0; adj != nullptr && nums != nullptr && k < g_numCount[d] && k < capNums; k++) nums[k] = g_nums[k];
   if (std::getenv("FMT_EMU_TEXTCAP"))
     std::fprintf(stderr, "textTop %llu of %llu, compactions %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap,
                  (unsigned long long)doc->prof[22]);
   return hdr->status;
+}
+
+int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+                        uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, fmt_mt_catchup_range* catchup,
+                        uint32_t capCatchup, fmt_mt_remove_order* rmOrder, uint32_t capRm) {
+  return emu_huge_replay_adj(b, d, hdr, leaves, capLeaves, chars, capChars, props, catchup, capCatchup, rmOrder, capRm,
+                             nullptr, nullptr, 0, nullptr);
 }
 
 int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,

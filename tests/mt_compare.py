@@ -49,7 +49,7 @@ def huge_emu_lib(tiny_groups=False):
         name = "libhuge_emu_tiny.so" if tiny_groups else "libhuge_emu.so"
         path = os.path.join(HERE, "_build", name)
         src = os.path.join(HERE, "emu", "huge_emu.cpp")
-        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("huge_engine.h", "wave.h")]
+        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("huge_engine.h", "wave.h", "adjust.h")]
         if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(d) for d in deps):
             os.makedirs(os.path.dirname(path), exist_ok=True)
             extra = ["-DFMT_HUGE_SLOTCAP=16", "-DFMT_HUGE_FILL=8"] if tiny_groups else []
@@ -60,8 +60,36 @@ def huge_emu_lib(tiny_groups=False):
                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         L.emu_huge_replay_rec.argtypes = L.emu_huge_replay.argtypes + [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                                                       ctypes.c_uint32]
+        L.emu_huge_replay_adj.argtypes = L.emu_huge_replay_rec.argtypes + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                                          ctypes.c_void_p]
         _huge[tiny_groups] = L
     return _huge[tiny_groups]
+
+
+def emu_huge_replay_adjust(batch, doc=0, tiny_groups=False, cap_props=65534):
+    """(header, leaves, chars, props, legacy prop sets per leaf, computed numbers) of document `doc`
+    of an annotate-adjust batch replayed by the emulated huge engine."""
+    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+
+    sd = batch.snapshots[doc] if batch.snapshots is not None else None
+    segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 1
+    nops = int(batch.doc_op_offsets[doc + 1] - batch.doc_op_offsets[doc])
+    cap_leaves, cap_chars = segs + 3 * nops + 8, len(batch.text) + 8
+    hdr = np.zeros(1, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(cap_leaves, dtype=LEAF_DTYPE)
+    chars = np.zeros(cap_chars, dtype="<u2")
+    props = np.zeros(cap_props, dtype=PROPSET_DTYPE)
+    legacy = np.zeros(cap_leaves, dtype="<u2")
+    nums = np.zeros(1 << 16, dtype=np.float64)
+    nn = ctypes.c_uint32()
+    b, keep = batch_struct(batch)
+    huge_emu_lib(tiny_groups).emu_huge_replay_adj(ctypes.addressof(b), doc, _p(hdr), _p(leaves), cap_leaves, _p(chars),
+                                                  cap_chars, _p(props), None, 0, None, 0, _p(legacy), _p(nums),
+                                                  len(nums), ctypes.byref(nn))
+    del keep
+    h = hdr[0]
+    n = int(h["n_leaves"])
+    return h, leaves[:n], chars[: int(h["n_chars"])], props[: int(h["n_props"])], legacy[:n], nums[: nn.value]
 
 
 def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=False, cap_catchup=0, cap_rm=0,

@@ -161,26 +161,24 @@ def test_huge_loaded_markers(orc, engine):
 
 def test_unsupported_huge_document_fails_alone(orc, engine):
     """A summary-loaded document past the large tier that asks for something the huge tier does not
-    replay (here an annotate-adjust) fails alone, with FMT_E_UNSUPPORTED in its own header: the
-    ordinary and huge documents beside it replay as in a batch without it."""
+    replay (here a SnapshotV1 body-chunk segment with merge info, FMT_MT_F_LOADSEG) fails alone, with
+    FMT_E_UNSUPPORTED in its own header: the ordinary and huge documents beside it replay as in a
+    batch without it."""
     import dataclasses
 
-    from fluidframework_amd.streams import ADJUST_DTYPE, value_numbers
+    from fluidframework_amd.streams import MT_F_LOADSEG, NON_COLLAB_CLIENT, SNAPSHOT_INFO_DTYPE, STAMP_DTYPE
     farm = workloads.conflict_farm(24, n_clients=8, ops_per_doc=600, seed=8)
     t3a = workloads.t3_stream(3000, 4000, n_clients=31, max_lag=700, seed=9)
     bad = workloads.t3_stream(9000, 6000, n_clients=63, max_lag=4096, max_range=20, seed=10)
     batch = _concat([farm, t3a, bad, farm])
-    n_props = len(batch.props_off) - 1
+    info = np.zeros(len(batch.snapshot_segs), dtype=SNAPSHOT_INFO_DTYPE)
+    info["ins_client"] = NON_COLLAB_CLIENT  # (rows without merge info: the loads are unchanged)
     o0 = int(batch.doc_op_offsets[farm.n_docs + 1])
-    first_annotate = o0 + int(np.nonzero(bad.ops["type"] == 2)[0][0])
+    first_insert = o0 + int(np.nonzero(bad.ops["type"] == 0)[0][0])
     ops = batch.ops.copy()
-    ops["payload"][first_annotate] = n_props  # (the props op appended below: one adjust entry)
-    adjusts = np.zeros(1, dtype=ADJUST_DTYPE)
-    adjusts["delta"] = 1.0
-    batch = dataclasses.replace(
-        batch, ops=ops, props_off=np.append(batch.props_off, batch.props_off[-1] + 2).astype(np.uint32),
-        props_kv=np.append(batch.props_kv, [0xFFFF, 0]).astype(np.uint32), adjusts=adjusts,
-        value_num=value_numbers(batch.values))
+    ops["flags"][first_insert] |= MT_F_LOADSEG
+    ops["pos1"][first_insert] = 0  # (merge-info row 0)
+    batch = dataclasses.replace(batch, ops=ops, snapshot_info=info, snapshot_stamps=np.zeros(1, dtype=STAMP_DTYPE))
     engine.mt_load(batch)
     engine.mt_run()
     hdrs = engine.mt_headers(raise_on_failed_docs=False)
@@ -194,6 +192,41 @@ def test_unsupported_huge_document_fails_alone(orc, engine):
         assert rc == 0
         lv, ch, pr = engine.mt_doc(d, hdrs[d])
         assert compare_doc(exp, (hdrs[d], lv, ch, pr)) == [], d
+
+
+@pytest.mark.parametrize("n_ops,seed", [(6000, 5), (9000, 6)])
+def test_huge_annotate_adjust_on_gpu(orc, engine, n_ops, seed):
+    """Annotate-adjust in documents past the large tier (grown from their start: marker-rich streams
+    whose annotates adjust "weight"): state, computed numbers and the legacy summary with
+    getAtSeq(minSeq) props (the huge tier's PropertiesManager records) == oracle."""
+    from marker_docs import marker_batch
+
+    from fluidframework_amd.summary import legacy_summary, values_with_numbers
+    batch = marker_batch(1, n_ops, seed=seed, adjust=True)
+    assert batch.adjusts is not None
+    engine.mt_load(batch)
+    engine.mt_run()
+    hdrs = engine.mt_headers()
+    assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
+    assert int(hdrs[0]["n_leaves"]) > 2048  # (past the large tier)
+    nums = []
+    orc.set_index(True)
+    try:
+        rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=4 * n_ops + 64, cap_chars=len(batch.text) + 8,
+                                                    cap_props=1 << 15, numbers=nums)
+    finally:
+        orc.set_index(False)
+    assert rc == 0
+    exp = (oh[0], ol[0][: int(oh[0]["n_leaves"])], oc[0][: int(oh[0]["n_chars"])], op[0][: int(oh[0]["n_props"])])
+    lv, ch, pr = engine.mt_doc(0, hdrs[0])
+    assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+    got_nums = engine.mt_numbers(0)
+    assert np.array_equal(got_nums, nums[0])
+    want = orc.mt_replay_summary(batch, 0, batch.keys, batch.values)
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    assert engine.mt_summary(0) == want
+    vals = values_with_numbers(batch.values, got_nums)
+    assert legacy_summary(hdrs[0], lv, ch, pr, batch.keys, vals, legacy_props=engine.mt_legacy_props(0, hdrs[0])) == want
 
 
 @pytest.mark.parametrize("n_ops,split,seed", [(6000, 0, 2), (12000, 9000, 4)])
@@ -213,6 +246,11 @@ def test_huge_relative_positions_on_gpu(orc, engine, n_ops, split, seed):
     assert rc == 0
     lv, ch, pr = engine.mt_doc(0, hdrs[0])
     assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+    # the bulk legacy summary (summaryRunsKernel with the engine's match classes: > 4096 prop sets)
+    engine.mt_summarize_legacy(batch.keys, batch.values)
+    assert engine.mt_summary(0) == orc.mt_replay_summary(batch, 0, batch.keys, batch.values)
+    if split:
+        assert int(hdrs[0]["n_props"]) > 4096
 
 
 @pytest.mark.parametrize("segs,ops,props_every,seed", [

@@ -1,6 +1,7 @@
 """The huge-document engine (csrc/huge_engine.h: paged leaf blocks, group lists, window table —
 the T3 path, BASELINE config 5) under host emulation, bit-exact against the oracle on T3-shaped
 documents: every leaf field, the text, the prop sets and the header."""
+import numpy as np
 import pytest
 
 from fluidframework_amd import workloads
@@ -305,3 +306,33 @@ def test_huge_engine_relative_positions(orc, n_ops, split, seed, tiny):
     assert compare_doc(exp, got) == []
     if n_ops >= 12000:
         assert int(got[0]["n_props"]) > 4096
+
+
+@pytest.mark.parametrize("exact_tail,tiny", [(False, True), (True, False), (False, False)])
+def test_huge_engine_annotate_adjust(orc, exact_tail, tiny):
+    """Annotate-adjust in the huge tier (computePropertyValue, segmentPropertiesManager.ts:54-78, with
+    the batch's number tables, adjust.h) and its PropertiesManager records: every document of the
+    reference's conflict farms with adjusts, replayed by the emulated huge engine, equals the oracle
+    (state and computed numbers), and its legacy summary from the engine's getAtSeq(minSeq) prop
+    sets equals the oracle's SnapshotLegacy restatement."""
+    from test_annotate_adjust import adjust_fixture_batch
+
+    from fluidframework_amd import summary
+    from mt_compare import emu_huge_replay_adjust
+    batch, finals = adjust_fixture_batch(exact_tail)
+    nums = []
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=4096, cap_chars=1 << 16, cap_props=4096,
+                                                numbers=nums)
+    assert rc == 0
+    differs = 0
+    for d in range(batch.n_docs):
+        h, lv, ch, pr, legacy, got_nums = emu_huge_replay_adjust(batch, d, tiny_groups=tiny)
+        assert int(h["status"]) == 0, (d, int(h["status"]), int(h["fail_seq"]))
+        assert compare_doc((oh[d], ol[d], oc[d], op[d]), (h, lv, ch, pr)) == [], d
+        assert np.array_equal(got_nums, nums[d]), d
+        vals = summary.values_with_numbers(batch.values, got_nums)
+        got = summary.legacy_summary(h, lv, ch, pr, batch.keys, vals, legacy_props=legacy)
+        assert got == orc.mt_replay_summary(batch, d, batch.keys, batch.values), d
+        differs += got != summary.legacy_summary(h, lv, ch, pr, batch.keys, vals)
+    if not exact_tail:
+        assert differs > 0
