@@ -40,7 +40,7 @@ def build(name, edits, rev=None, flags=()):
         assert old in s, (name, fname, old[:50])
         open(p, "w").write(s.replace(old, new))
     # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc)
-    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "summary.o", "digest.o", "transfer.o")]
+    objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "map_pending.o", "summary.o", "digest.o", "transfer.o")]
     for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip", "hugedoc.hip"]:
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
@@ -154,7 +154,8 @@ FLAGS = {
     "bias100": ["-mllvm", "-amdgpu-schedule-metric-bias=100"],
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
 }
-REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08"}  # committed engines to A/B against
+REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
+        "r4pend": "4831c1d"}  # committed engines to A/B against
 
 
 if __name__ == "__main__":
