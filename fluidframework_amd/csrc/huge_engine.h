@@ -297,7 +297,10 @@ struct Hit {
   int vis;         // view length of the leaf
 };
 
-class HugeDoc {
+// Adj: the variant for batches with annotate-adjust (the fold and the PropertiesManager records);
+// batches without run the Adj = false code, which has none of it in its op loop.
+template <bool Adj = false>
+class HugeDocT {
  public:
   HugeState S;
   HugeLds* L;
@@ -1445,17 +1448,22 @@ class HugeDoc {
       const uint64_t m = ballot(hit);
       const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
       if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
-        if (!adjSite || in.adj == nullptr || ++t >= b) {
-          fail(FMT_E_DATA);
+        if constexpr (Adj) {
+          if (!adjSite || in.adj == nullptr || ++t >= b) {
+            fail(FMT_E_DATA);
+            return kNoProps;
+          }
+          const uint32_t cur = pos < cnt ? uni(L->kvWork[pos]) & 0xFFFFu : 0u;  // absent: null
+          const uint32_t v = fmt_mt::adjustFold(in.adj, in.doc, cur, ldu(in.propsKv + t));
+          if (v == fmt_mt::kAdjFailData || v == fmt_mt::kAdjFailCap) {
+            fail(v == fmt_mt::kAdjFailData ? FMT_E_DATA : FMT_E_CAPACITY);
+            return kNoProps;
+          }
+          e = (e & 0xFFFF0000u) | v;
+        } else {
+          fail(FMT_E_DATA);  // (the runtime launches the Adj variant for batches with adjusts)
           return kNoProps;
         }
-        const uint32_t cur = pos < cnt ? uni(L->kvWork[pos]) & 0xFFFFu : 0u;  // absent: null
-        const uint32_t v = fmt_mt::adjustFold(in.adj, in.doc, cur, ldu(in.propsKv + t));
-        if (v == fmt_mt::kAdjFailData || v == fmt_mt::kAdjFailCap) {
-          fail(v == fmt_mt::kAdjFailData ? FMT_E_DATA : FMT_E_CAPACITY);
-          return kNoProps;
-        }
-        e = (e & 0xFFFF0000u) | v;
       }
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
         if (pos < cnt) {
@@ -1771,7 +1779,9 @@ class HugeDoc {
     regsInsert(R, k + 1, y, wy);
     st1(S.leafBlk + y.id, b);
     obRefsMove(x.id, y.id, o, -o);  // the right part takes the references at/after the split
-    if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
+    if constexpr (Adj) {
+      if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
+    }
     if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
       rmPendFrom[rmPendN] = x.id;
       rmPendTo[rmPendN] = y.id;
@@ -2069,9 +2079,11 @@ class HugeDoc {
   }
 
   FMT_DEV void annotateLeaf(uint32_t b, int j, Leaf& x, uint32_t opId, int seq) {
-    if (in.adj != nullptr) {  // the leaf's PropertiesManager first (handleProperties, :188-238)
-      pmAnnotate(x.id, mProps(x.meta), opId, seq);
-      if (status != FMT_OK) return;
+    if constexpr (Adj) {  // the leaf's PropertiesManager first (handleProperties, :188-238)
+      if (in.adj != nullptr) {
+        pmAnnotate(x.id, mProps(x.meta), opId, seq);
+        if (status != FMT_OK) return;
+      }
     }
     const uint32_t np = applyProps(mProps(x.meta), opId, true);
     if (status != FMT_OK) return;
@@ -3033,9 +3045,11 @@ class HugeDoc {
       LANE(gone) = valid && (LANE(P.dst) < 0 || LANE(headSrc) != static_cast<uint32_t>(l));
       if (LANE(gone)) S.leafBlk[LANE(f[5])] = kNone;
     }
-    if (pmN > 0) {  // appended and unlinked leaves take their managers with them
-      waveSync();
-      for (uint64_t m = ballot(gone); m != 0 && status == FMT_OK; m &= m - 1) pmDropLeaf(readlane(f[5], ctz64(m)));
+    if constexpr (Adj) {
+      if (pmN > 0) {  // appended and unlinked leaves take their managers with them
+        waveSync();
+        for (uint64_t m = ballot(gone); m != 0 && status == FMT_OK; m &= m - 1) pmDropLeaf(readlane(f[5], ctz64(m)));
+      }
     }
   }
 
@@ -3332,8 +3346,9 @@ class HugeDoc {
     ProfScope ps_(prof[3]);
     for (int i = 0; i < 2; i++) {
       if (heapN == 0) break;
-      // segmentToScour?.segment?.propertyManager?.updateMsn(minSeq) (zamboni.ts:44)
-      if (pmN > 0) pmUpdateMsn(uni(L->heap[1].leafId), minSeq);
+      if constexpr (Adj) {  // segmentToScour?.segment?.propertyManager?.updateMsn(minSeq) (zamboni.ts:44)
+        if (pmN > 0) pmUpdateMsn(uni(L->heap[1].leafId), minSeq);
+      }
       if (heapSeq(1) > minSeq) break;
       const HeapEnt e = heapGet();
       const uint32_t b = ldu(S.leafBlk + e.leafId);
@@ -3953,9 +3968,11 @@ class HugeDoc {
             x.pad = static_cast<uint16_t>((blk >> 16) | (mMarker(m) ? FMT_MT_LEAF_MARKER : 0u));
             outLeaves[o] = x;
             if (S.rmIds != nullptr) S.rmIds[rd(S.lId + i)] = static_cast<uint32_t>(o);  // (remove-order entries)
-            if (outLegacy != nullptr) {  // (annotate-adjust: getAtSeq below)
-              S.outIdx[rd(S.lId + i)] = static_cast<uint32_t>(o);
-              outLegacy[o] = static_cast<uint16_t>(mProps(m));
+            if constexpr (Adj) {
+              if (outLegacy != nullptr) {  // (annotate-adjust: getAtSeq below)
+                S.outIdx[rd(S.lId + i)] = static_cast<uint32_t>(o);
+                outLegacy[o] = static_cast<uint16_t>(mProps(m));
+              }
             }
             const uint32_t t = rd(S.lText + i);
             for (uint32_t c = 0; c < LANE(len); c++) outChars[co + c] = static_cast<uint16_t>(textAt(t + c));
@@ -3967,9 +3984,11 @@ class HugeDoc {
         nBlocks += tb;
       }
     }
-    if (outLegacy != nullptr && S.outIdx != nullptr && status == FMT_OK) {
-      waveSync();
-      if (pmN > 0) pmLegacyProps(outLegacy);
+    if constexpr (Adj) {
+      if (outLegacy != nullptr && S.outIdx != nullptr && status == FMT_OK) {
+        waveSync();
+        if (pmN > 0) pmLegacyProps(outLegacy);
+      }
     }
     FOR_LANES(l) {
       for (int p = l; p < nProps; p += 64) {
@@ -4050,5 +4069,7 @@ class HugeDoc {
     if (status == FMT_OK) replay();
   }
 };
+
+using HugeDoc = HugeDocT<false>;
 
 }  // namespace fmt_huge

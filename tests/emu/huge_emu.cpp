@@ -153,7 +153,8 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   S.rmIds = rmOrder != nullptr ? rmIds.data() : nullptr;
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));
-  auto doc = std::make_unique<HugeDoc>();
+  const fmt_mt::AdjustTables* adj = prepareNumbers(b);
+  auto replay = [&](auto* doc) {  // (HugeDocT<true> for annotate-adjust batches, as the runtime launches)
   doc->S = S;
   doc->L = lds.get();
   HugeInputs in;
@@ -179,7 +180,6 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   std::vector<uint32_t> mkIds(b->relpos != nullptr ? S.idCap : 0);
   doc->S.mkIds = b->relpos != nullptr ? mkIds.data() : nullptr;
   doc->S.mkCap = S.idCap;
-  const fmt_mt::AdjustTables* adj = prepareNumbers(b);
   std::vector<uint64_t> numOffs(b->n_docs + 1ull, kEmuNumCap), pmOffs(b->n_docs + 1ull, kEmuPmCap);
   for (uint32_t k = 0; k <= d && k <= b->n_docs; k++) numOffs[k] = pmOffs[k] = 0;  // (document d: [0, cap))
   g_adj.numOffsets = numOffs.data();
@@ -198,6 +198,9 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   if (std::getenv("FMT_EMU_TEXTCAP"))
     std::fprintf(stderr, "textTop %llu of %llu, compactions %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap,
                  (unsigned long long)doc->prof[22]);
+  };
+  if (adj != nullptr) replay(std::make_unique<HugeDocT<true>>().get());
+  else replay(std::make_unique<HugeDocT<false>>().get());
   return hdr->status;
 }
 

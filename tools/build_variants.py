@@ -116,7 +116,18 @@ FETCH_UNI = [("mt_engine.h", """    if (i < in.end) {
     FOR_LANES(l) { LANE(x) = l < len ? static_cast<uint32_t>(t[l]) : 0u; }
     return x;""")]
 
+# the huge engine's rare paths (PropertiesManager records, remove order, relative positions, catch-up
+# ranges) as out-of-line calls instead of force-inlined into the op loop
+_COLD_FNS = ["void pmCompact(", "void pmUpdateMsn(", "void pmCopy(", "void pmDropLeaf(", "void pmAnnotate(",
+             "void rmAppend(", "void rmFlush(", "int viewStart(", "int posFromRelativePos(", "bool resolveRelative(",
+             "void recordCatchup(", "void pmLegacyProps("]
+COLD = [("wave.h", "#define FMT_DEV __device__ __forceinline__",
+         "#define FMT_DEV __device__ __forceinline__\n#define FMT_COLD __device__ __attribute__((noinline))"),
+        ("wave.h", "#define FMT_DEV inline\n", "#define FMT_DEV inline\n#define FMT_COLD inline\n")] + \
+       [("huge_engine.h", "  FMT_DEV " + f, "  FMT_COLD " + f) for f in _COLD_FNS]
+
 VARIANTS = {
+    "cold": COLD,
     "fetch_uni": FETCH_UNI,
     "ob_s1": [OB_S1],
     "hw8": HW8,
