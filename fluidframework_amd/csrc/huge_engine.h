@@ -298,8 +298,10 @@ struct Hit {
 };
 
 // Adj: the variant for batches with annotate-adjust (the fold and the PropertiesManager records);
-// batches without run the Adj = false code, which has none of it in its op loop.
-template <bool Adj = false>
+// Rm: the variant for batches that record the SnapshotV1 remove order (FMT_MT_F_RMORDER ops).
+// Batches without them run code that has none of it in its op loop (the remove-order hooks alone
+// cost a T3 slice 39%: 6.55 s -> 9.12 s, profiles/r4/ab_t3_bisect.json).
+template <bool Adj = false, bool Rm = false>
 class HugeDocT {
  public:
   HugeState S;
@@ -1782,10 +1784,12 @@ class HugeDocT {
     if constexpr (Adj) {
       if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
     }
-    if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
-      rmPendFrom[rmPendN] = x.id;
-      rmPendTo[rmPendN] = y.id;
-      rmPendN++;
+    if constexpr (Rm) {
+      if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
+        rmPendFrom[rmPendN] = x.id;
+        rmPendTo[rmPendN] = y.id;
+        rmPendN++;
+      }
     }
     const uint32_t nb = commitBlock(R);
     if (nb != kNone && k + 1 >= kMaxNodes / 2) {
@@ -2055,8 +2059,8 @@ class HugeDocT {
     if (!was) {
       x.rm = seq;
       if (cuRec) cuPush(x.id);  // removedSegments: hits not removed before this op (mergeTree.ts:2314-2321)
-    } else if (rmRec) {
-      rmPushHit(x.id);  // a later remove stamp (stamps.ts:144-158), recorded in rmFlush
+    } else if constexpr (Rm) {
+      if (rmRec) rmPushHit(x.id);  // a later remove stamp (stamps.ts:144-158), recorded in rmFlush
     }
     if (c < 32) x.mlo |= 1u << c;
     else x.mhi |= 1u << (c - 32);
@@ -2280,6 +2284,7 @@ class HugeDocT {
       }
     }
     if (!(any && newestClient != client)) return;
+    if constexpr (Rm) {
     if (rmRec) {  // SnapshotV1: every stamp but the first (rm_seq) is a remove-order entry (mergeTree.ts:1715-1725)
       bool firstSkipped = false;
       for (int i = 0; i < obStartN && status == FMT_OK; i++) {
@@ -2296,6 +2301,7 @@ class HugeDocT {
         }
         rmAppend(id, ocl, oseq, FMT_MT_RM_SLICE);
       }
+    }
     }
     uint32_t b;
     int kk;
@@ -3728,7 +3734,7 @@ class HugeDocT {
 #endif
       cuRec = (op.flags & FMT_MT_F_CATCHUP) != 0 && in.catchup != nullptr && S.cuIds != nullptr;
       cuIdN = 0;
-      rmRec = (op.flags & FMT_MT_F_RMORDER) != 0 && in.rmOrder != nullptr && S.rmIds != nullptr;
+      if constexpr (Rm) rmRec = (op.flags & FMT_MT_F_RMORDER) != 0 && in.rmOrder != nullptr && S.rmIds != nullptr;
       rmKind = op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE;
       rmHitN = 0;
       opIdx = static_cast<uint32_t>(i - in.begin);
@@ -3745,7 +3751,9 @@ class HugeDocT {
       }
       if (((op.flags & FMT_MT_F_RMORDER) != 0 && !rmRec) || ((op.flags & FMT_MT_F_CATCHUP) != 0 && !cuRec)) fail(FMT_E_UNSUPPORTED);
       if (cuRec && status == FMT_OK) recordCatchup(op.type == FMT_MT_OBLITERATE_SIDED ? FMT_MT_OBLITERATE : op.type);
-      if ((rmPendN > 0 || rmHitN > 0) && status == FMT_OK) rmFlush(op.client, op.seq);
+      if constexpr (Rm) {
+        if ((rmPendN > 0 || rmHitN > 0) && status == FMT_OK) rmFlush(op.client, op.seq);
+      }
       cuRec = rmRec = false;
       const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
       for (int z = 0; z < 2 && status == FMT_OK; z++) {
@@ -3967,7 +3975,9 @@ class HugeDocT {
             x.block = static_cast<uint16_t>(blk & 0xFFFFu);
             x.pad = static_cast<uint16_t>((blk >> 16) | (mMarker(m) ? FMT_MT_LEAF_MARKER : 0u));
             outLeaves[o] = x;
-            if (S.rmIds != nullptr) S.rmIds[rd(S.lId + i)] = static_cast<uint32_t>(o);  // (remove-order entries)
+            if constexpr (Rm) {
+              if (S.rmIds != nullptr) S.rmIds[rd(S.lId + i)] = static_cast<uint32_t>(o);  // (remove-order entries)
+            }
             if constexpr (Adj) {
               if (outLegacy != nullptr) {  // (annotate-adjust: getAtSeq below)
                 S.outIdx[rd(S.lId + i)] = static_cast<uint32_t>(o);
@@ -4000,7 +4010,7 @@ class HugeDocT {
     }
     waveSync();
     // remove-order entries: leaf id -> output index, FMT_MT_LEAF_GONE once zamboni dropped the leaf
-    for (uint32_t base = 0; status == FMT_OK && S.rmIds != nullptr && base < rmN; base += 64) {
+    for (uint32_t base = 0; Rm && status == FMT_OK && S.rmIds != nullptr && base < rmN; base += 64) {
       FOR_LANES(l) {
         const uint32_t k = base + l;
         if (k < rmN) {

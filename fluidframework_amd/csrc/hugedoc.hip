@@ -16,14 +16,14 @@ static_assert(sizeof(fmt_huge::HugeLds) <= 160 * 1024, "the huge-document LDS st
 
 // kWaves waves per workgroup: wave 0 replays; the others serve its window/slot passes. Adj: batches
 // with annotate-adjust (huge_engine.h HugeDocT).
-template <bool Adj>
+template <bool Adj, bool Rm>
 __global__ __launch_bounds__(64 * fmt_huge::HugeDoc::kWaves) void hugeDocKernel(const fmt_huge::HugeState* __restrict__ states,
                                                                             const fmt_huge::HugeInputs* __restrict__ inputs,
                                                                             const HugeOut* __restrict__ outs, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (scalar branch below)
   for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
-    fmt_huge::HugeDocT<Adj> doc;
+    fmt_huge::HugeDocT<Adj, Rm> doc;
     doc.S = states[i];
     doc.L = reinterpret_cast<fmt_huge::HugeLds*>(lds);
     if (wave != 0) {
@@ -45,14 +45,14 @@ __global__ __launch_bounds__(64 * fmt_huge::HugeDoc::kWaves) void hugeDocKernel(
 size_t hugeLdsBytes() { return sizeof(fmt_huge::HugeLds); }
 
 hipError_t launchHugeDocs(const fmt_huge::HugeState* states, const fmt_huge::HugeInputs* inputs, const HugeOut* outs,
-                          uint32_t count, bool adjust, hipStream_t stream) {
+                          uint32_t count, bool adjust, bool rmOrder, hipStream_t stream) {
   if (count == 0) return hipSuccess;
-  if (adjust)
-    hipLaunchKernelGGL(hugeDocKernel<true>, dim3(count), dim3(64 * fmt_huge::HugeDoc::kWaves), sizeof(fmt_huge::HugeLds), stream,
-                       states, inputs, outs, count);
-  else
-    hipLaunchKernelGGL(hugeDocKernel<false>, dim3(count), dim3(64 * fmt_huge::HugeDoc::kWaves), sizeof(fmt_huge::HugeLds), stream,
-                       states, inputs, outs, count);
+  const dim3 grid(count), block(64 * fmt_huge::HugeDoc::kWaves);
+  const size_t lds = sizeof(fmt_huge::HugeLds);
+  if (adjust && rmOrder) hipLaunchKernelGGL((hugeDocKernel<true, true>), grid, block, lds, stream, states, inputs, outs, count);
+  else if (adjust) hipLaunchKernelGGL((hugeDocKernel<true, false>), grid, block, lds, stream, states, inputs, outs, count);
+  else if (rmOrder) hipLaunchKernelGGL((hugeDocKernel<false, true>), grid, block, lds, stream, states, inputs, outs, count);
+  else hipLaunchKernelGGL((hugeDocKernel<false, false>), grid, block, lds, stream, states, inputs, outs, count);
   return hipGetLastError();
 }
 

@@ -151,6 +151,6 @@ struct HugeOut {
 };
 size_t hugeLdsBytes();
 hipError_t launchHugeDocs(const fmt_huge::HugeState* states, const fmt_huge::HugeInputs* inputs, const HugeOut* outs,
-                          uint32_t count, bool adjust, hipStream_t stream);
+                          uint32_t count, bool adjust, bool rmOrder, hipStream_t stream);
 
 }  // namespace fmt_kernels

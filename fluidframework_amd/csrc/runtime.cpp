@@ -1391,7 +1391,7 @@ int fmt_mt_run(fmt_ctx* c) {
                                             c->mtObliterate,
                                             c->mtHasRmOrder, c->mtSched.p, c->mtHasAdjust));
   if (hasHuge)
-    FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p, c->mtHugeLoaded, c->mtHasAdjust, c->stream));
+    FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates.p, c->hugeInputs.p, c->hugeOuts.p, c->mtHugeLoaded, c->mtHasAdjust, c->mtHasRmOrder, c->stream));
   FMT_HIP(c, hipEventRecord(c->ev1, c->stream));  // device time excludes the host read-back below
   c->timed2 = false;
   // Documents that overflowed the small tier replay again, from their inputs, in the large tier.
@@ -1471,7 +1471,7 @@ int fmt_mt_run(fmt_ctx* c) {
       FMT_HIP(c, hipMemcpyAsync(c->hugeInputs2.p, hi.data(), ng * sizeof(fmt_huge::HugeInputs), hipMemcpyHostToDevice, c->stream));
       FMT_HIP(c, hipMemcpyAsync(c->hugeOuts2.p, ho.data(), ng * sizeof(fmt_kernels::HugeOut), hipMemcpyHostToDevice, c->stream));
       FMT_HIP(c, fmt_kernels::launchHugeDocs(c->hugeStates2.p, c->hugeInputs2.p, c->hugeOuts2.p, static_cast<uint32_t>(ng),
-                                             c->mtHasAdjust, c->stream));
+                                             c->mtHasAdjust, c->mtHasRmOrder, c->stream));
       FMT_HIP(c, hipStreamSynchronize(c->stream));
       }
       c->mtGrown = static_cast<uint32_t>(ng);

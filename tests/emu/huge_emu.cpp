@@ -199,8 +199,11 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
     std::fprintf(stderr, "textTop %llu of %llu, compactions %llu\n", (unsigned long long)doc->textTop, (unsigned long long)textCap,
                  (unsigned long long)doc->prof[22]);
   };
-  if (adj != nullptr) replay(std::make_unique<HugeDocT<true>>().get());
-  else replay(std::make_unique<HugeDocT<false>>().get());
+  const bool rm = rmOrder != nullptr;  // (the runtime launches the Rm variant for batches that record)
+  if (adj != nullptr && rm) replay(std::make_unique<HugeDocT<true, true>>().get());
+  else if (adj != nullptr) replay(std::make_unique<HugeDocT<true, false>>().get());
+  else if (rm) replay(std::make_unique<HugeDocT<false, true>>().get());
+  else replay(std::make_unique<HugeDocT<false, false>>().get());
   return hdr->status;
 }
 

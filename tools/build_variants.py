@@ -135,6 +135,7 @@ VARIANTS = {
     "cw3": [CW3],
     "noload": [NOLOAD],
     "base": [],
+    "rmt": [],
     "cur": [],
     "sops": [("mt_engine.h", "#define FMT_SCALAR_OPS 0", "#define FMT_SCALAR_OPS 1")],
     "cw2": [("mergetree_compact.hip", "constexpr int kMtWavesCompact = 4;", "constexpr int kMtWavesCompact = 2;")],
@@ -166,7 +167,7 @@ FLAGS = {
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
 }
 REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
-        "r4pend": "4831c1d"}  # committed engines to A/B against
+        "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
 
 
 if __name__ == "__main__":
