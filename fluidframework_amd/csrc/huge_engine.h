@@ -329,7 +329,9 @@ class HugeDocT {
   uint32_t rmN = 0, rmHitN = 0;
   bool rmRec = false;
   int rmPendN = 0;
-  uint32_t rmPendFrom[2] = {0, 0}, rmPendTo[2] = {0, 0};
+  // (named scalars, not arrays: an array member indexed by a counter sends the whole engine object to
+  // scratch memory)
+  uint32_t rmPendFrom0 = 0, rmPendTo0 = 0, rmPendFrom1 = 0, rmPendTo1 = 0;
   uint32_t rmKind = FMT_MT_RM_SET;
   uint32_t mkN = 0;  // markers listed in S.mkIds
   int pmN = 0;       // PropertiesManager records in use (deleted ones included), annotate-adjust batches
@@ -1786,8 +1788,13 @@ class HugeDocT {
     }
     if constexpr (Rm) {
       if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
-        rmPendFrom[rmPendN] = x.id;
-        rmPendTo[rmPendN] = y.id;
+        if (rmPendN == 0) {
+          rmPendFrom0 = x.id;
+          rmPendTo0 = y.id;
+        } else {
+          rmPendFrom1 = x.id;
+          rmPendTo1 = y.id;
+        }
         rmPendN++;
       }
     }
@@ -2459,11 +2466,12 @@ class HugeDocT {
   }
   FMT_DEV void rmFlush(int client, int seq) {
     for (int q = 0; q < rmPendN && status == FMT_OK; q++) {
+      const uint32_t from = q == 0 ? rmPendFrom0 : rmPendFrom1, to = q == 0 ? rmPendTo0 : rmPendTo1;
       const uint32_t n0 = rmN;
       for (uint32_t k = 0; k < n0 && status == FMT_OK; k++) {
         const uint32_t* e = reinterpret_cast<const uint32_t*>(in.rmOrder + k);
-        if (ldu(e) == rmPendFrom[q]) rmAppend(rmPendTo[q], ldi(reinterpret_cast<const int32_t*>(e + 1)),
-                                             ldi(reinterpret_cast<const int32_t*>(e + 2)), ldu(e + 3));
+        if (ldu(e) == from) rmAppend(to, ldi(reinterpret_cast<const int32_t*>(e + 1)),
+                                     ldi(reinterpret_cast<const int32_t*>(e + 2)), ldu(e + 3));
       }
     }
     rmPendN = 0;

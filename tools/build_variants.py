@@ -136,6 +136,7 @@ VARIANTS = {
     "noload": [NOLOAD],
     "base": [],
     "rmt": [],
+    "rmt_cold": COLD,
     "cur": [],
     "sops": [("mt_engine.h", "#define FMT_SCALAR_OPS 0", "#define FMT_SCALAR_OPS 1")],
     "cw2": [("mergetree_compact.hip", "constexpr int kMtWavesCompact = 4;", "constexpr int kMtWavesCompact = 2;")],
