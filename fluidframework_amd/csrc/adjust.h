@@ -8,6 +8,10 @@
 
 namespace fmt_mt {
 
+// legacyProps entry (every leaf of the document) when the getAtSeq view of an annotate-adjust document
+// did not fit its prop-set table: the replay state stands, its legacy summary reports FMT_E_CAPACITY
+constexpr uint16_t kLegacyUnavailable = 0xFFFEu;
+
 // Annotate-adjust tables of a batch (device memory): the rows, the number of each host value id
 // (NaN: not a number), the host's numbers ascending with their value ids, and per document a slab
 // of computed numbers (numOffsets) with its count (numCount, kept in memory across tiers).

@@ -1787,7 +1787,8 @@ class HugeDocT {
       if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
     }
     if constexpr (Rm) {
-      if (rmN > 0 && y.rm != kNotRemoved && rmPendN < 2) {  // its remove-order entries, copied in rmFlush
+      if (rmN > 0 && y.rm != kNotRemoved) {  // its remove-order entries, copied in rmFlush
+        if (rmPendN >= 2) return fail(FMT_E_DATA);  // an op splits at most twice (its two boundaries)
         if (rmPendN == 0) {
           rmPendFrom0 = x.id;
           rmPendTo0 = y.id;
@@ -4006,6 +4007,18 @@ class HugeDocT {
       if (outLegacy != nullptr && S.outIdx != nullptr && status == FMT_OK) {
         waveSync();
         if (pmN > 0) pmLegacyProps(outLegacy);
+        if (status != FMT_OK) {
+          // the legacy getAtSeq view did not fit the prop-set table: the replay state stands, only
+          // its legacy summary is unavailable (kLegacyUnavailable: summaryRunsKernel and
+          // fmt_mt_fetch_legacy_props report FMT_E_CAPACITY for this document)
+          status = FMT_OK;
+          for (uint64_t base = 0; base < nLeaves; base += 64) {
+            FOR_LANES(l) {
+              if (base + l < nLeaves) outLegacy[base + l] = fmt_mt::kLegacyUnavailable;
+            }
+          }
+          waveSync();
+        }
       }
     }
     FOR_LANES(l) {

@@ -38,6 +38,11 @@ __global__ void __launch_bounds__(256) mapPendingKernel(const fmt_map_local_op* 
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= nDocs) return;
   const uint64_t e0 = evOffs[d], e1 = evOffs[d + 1];
+  if (e1 - e0 > FMT_MAP_PENDING_MAX_EVENTS) {  // one lane's dependent list walks: bounded per document
+    outCounts[d] = 0;
+    outStatus[d] = FMT_E_CAPACITY;
+    return;
+  }
   uint32_t eHead = kNil, eTail = kNil, uHead = kNil, uTail = kNil;
   bool bad = false;
   auto keyOf = [&](uint32_t i) { return ev[i].key; };

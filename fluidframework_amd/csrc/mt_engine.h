@@ -1604,6 +1604,7 @@ class Doc {
     }
     if constexpr (Rm) {
       if (rmN > 0 && static_cast<int32_t>(rec.w[2]) != kNotRemoved) {  // its entries, if any: copied in rmFlush
+        if (rmPendN >= 2) return fail(FMT_E_DATA);  // an op splits at most twice: a broken invariant
         if (rmPendN == 0) {
           rmPendFrom0 = fId(w4);
           rmPendTo0 = fId(rec.w[4]);
@@ -2913,7 +2914,24 @@ class Doc {
 
   FMT_DEV void writeOutputs(const DocOutputs& out) {
     if constexpr (Adj) {
-      if (out.legacyProps != nullptr && status == FMT_OK) pmLegacyProps(out.legacyProps);
+      if (out.legacyProps != nullptr && status == FMT_OK) {
+        pmLegacyProps(out.legacyProps);
+        if (status != FMT_OK) {
+          // the legacy getAtSeq view did not fit the prop-set table. Small tier: escalate (the large
+          // tier holds 1024 sets). Large tier: the replay state stands and only the legacy summary is
+          // unavailable (kLegacyUnavailable: summaryRunsKernel and fmt_mt_fetch_legacy_props report
+          // FMT_E_CAPACITY for this document).
+          if constexpr (C::kHbmChars) {
+            status = FMT_OK;
+            FOR_LANES(l) {
+              for (int t = l; t < n; t += 64) out.legacyProps[t] = kLegacyUnavailable;
+            }
+            waveSync();
+          } else {
+            status = FMT_E_CAPACITY;
+          }
+        }
+      }
     }
     const int nr = rows();
     // char offsets and leaf-block ordinals

@@ -1961,6 +1961,8 @@ int fmt_mt_fetch_legacy_props(fmt_ctx* c, uint32_t doc, uint16_t* out, uint32_t 
   docViews(c, views);
   if (views[doc].legacyProps != nullptr) {
     FMT_HIP(c, hipMemcpy(out, views[doc].legacyProps, m * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    if (out[0] == fmt_mt::kLegacyUnavailable)  // (the engine marks every leaf)
+      return setErr(c, FMT_E_CAPACITY, "fmt_mt_fetch_legacy_props: the document's getAtSeq view did not fit its prop-set table");
     return FMT_OK;
   }
   std::vector<fmt_mt_leaf> lv(m);  // (no annotate-adjust in the batch: getAtSeq is the current properties)

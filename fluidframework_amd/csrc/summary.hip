@@ -14,6 +14,7 @@
 
 #include "../../include/fmt.h"
 #include "kernels.h"
+#include "adjust.h"
 
 namespace fmt_kernels {
 
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(64 * kSumWaves) void summaryRunsKernel(const fmt_mt
     }
     // present leaves and their units: the spans reserved for this document
     uint32_t nPresent = 0, nUnits = 0;
+    bool unavailable = false;  // the engine could not intern this document's getAtSeq view
     for (uint32_t b = 0; b < n; b += 64) {
       const uint32_t i = b + lane;
       bool pres = false;
@@ -93,10 +95,16 @@ __global__ __launch_bounds__(64 * kSumWaves) void summaryRunsKernel(const fmt_mt
         const fmt_mt_leaf L = V.leaves[i];
         pres = L.ins_seq <= minSeq && !(L.rm_seq <= minSeq);
         len = pres ? L.len : 0u;
+        if (V.legacyProps != nullptr && V.legacyProps[i] == fmt_mt::kLegacyUnavailable) unavailable = true;
       }
       nPresent += static_cast<uint32_t>(__popcll(__ballot(pres)));
       for (int off = 32; off > 0; off >>= 1) len += static_cast<uint32_t>(__shfl_xor(static_cast<int>(len), off));
       nUnits += len;
+    }
+    if (__ballot(unavailable) != 0) {
+      od.status = static_cast<uint32_t>(FMT_E_CAPACITY);
+      if (lane == 0) docOut[d] = od;
+      continue;
     }
     unsigned long long runBase = 0, textBase = 0;
     if (lane == 0) {

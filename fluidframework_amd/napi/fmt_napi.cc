@@ -12,7 +12,8 @@
 //
 // Exports:
 //   open(device) -> ctx                        fmt_open
-//   close(ctx)                                 fmt_close (also run by the ctx finalizer)
+//   close(ctx)                                 fmt_close (contexts still open at exit: an env cleanup hook)
+//   openContexts() -> number                   contexts open in this process
 //   deviceInfo(ctx) -> string                  fmt_device_info
 //   capacity() -> {leaves, chars, props}       fmt_mt_capacity
 //   replayMergeTree(ctx, batch) -> Promise<ArrayBuffer headers>     fmt_mt_load + fmt_mt_run + fetch
@@ -67,17 +68,56 @@ const char* status_name(int rc) {
 struct Ctx {
   fmt_ctx* ctx = nullptr;
   bool busy = false;  // one async replay at a time per ctx (the C ABI is one-thread-per-ctx)
-  // A strong reference to the ctx's own external, never released: the external is never collected
-  // while node runs, so its finalizer only runs at environment teardown. (This image's node, v12,
-  // can run the second-pass finalizer of an external collected just before exit after teardown has
-  // freed its reference record: a SIGSEGV at exit. close() is what frees the device context.)
-  napi_ref self = nullptr;
 };
 
-void finalize_ctx(napi_env, void* data, void*) {
-  auto* c = static_cast<Ctx*>(data);
-  if (c->ctx) fmt_close(c->ctx);
-  delete c;
+// Context lifetime without N-API finalizers. A finalizer makes node create a weak v8impl::Reference
+// for the external; node v12 (this image's) frees every such Reference when the environment is torn
+// down even if GC already ran its first weak pass, and the queued second pass then calls through
+// the freed object: the SIGSEGV at exit of round 4 (libnode.so.72 +0x878a80, the second-pass
+// callback, loading the vtable of a freed Reference, reached from InvokeSecondPassPhantomCallbacks
+// during FreeEnvironment's CleanupHandles; the addon frame in that backtrace was the diagnostic
+// handler itself). So the externals carry no finalizer and no reference: each holds a handle
+// (slot + 1 | generation << 32) into this table. close() frees the slot and its device context at
+// once; a stale handle (closed, or from a reused slot) is detected, never dereferenced. Contexts
+// still open when the environment is torn down are closed by an env cleanup hook, before node
+// deletes the napi_env and while the HIP runtime is alive. Open contexts are capped
+// (FMT_NAPI_MAX_CONTEXTS, default 64): a caller that drops contexts without close() gets
+// FMT_E_CAPACITY instead of device memory that grows without bound.
+struct Slot {
+  Ctx* c = nullptr;
+  uint32_t gen = 0;
+};
+std::vector<Slot>& slots() {
+  static std::vector<Slot>* s = new std::vector<Slot>();
+  return *s;
+}
+uint32_t max_contexts() {
+  const char* e = std::getenv("FMT_NAPI_MAX_CONTEXTS");
+  const long v = e ? std::strtol(e, nullptr, 10) : 0;
+  return v > 0 ? static_cast<uint32_t>(v) : 64u;
+}
+uint32_t live_contexts() {
+  uint32_t n = 0;
+  for (const Slot& s : slots()) n += s.c != nullptr;
+  return n;
+}
+
+void close_all_at_teardown(void*) {
+  for (Slot& s : slots()) {
+    if (s.c == nullptr || s.c->busy) continue;  // (a replay still on a worker: left to process exit)
+    if (s.c->ctx) fmt_close(s.c->ctx);
+    delete s.c;
+    s.c = nullptr;
+    s.gen++;
+  }
+}
+
+Ctx* ctx_of_handle(void* p) {
+  const uint64_t h = reinterpret_cast<uintptr_t>(p);
+  const uint32_t slot = static_cast<uint32_t>(h & 0xffffffffu), gen = static_cast<uint32_t>(h >> 32);
+  if (slot == 0 || slot > slots().size()) return nullptr;
+  const Slot& s = slots()[slot - 1];
+  return s.gen == gen ? s.c : nullptr;
 }
 
 napi_value make_error(napi_env env, int rc, const std::string& msg) {
@@ -100,8 +140,8 @@ bool get_ctx(napi_env env, napi_value v, Ctx** out) {
   void* p = nullptr;
   if (napi_get_value_external(env, v, &p) != napi_ok || p == nullptr)
     return throw_fmt(env, FMT_E_USAGE, "expected an engine context from open()");
-  *out = static_cast<Ctx*>(p);
-  if ((*out)->ctx == nullptr) return throw_fmt(env, FMT_E_USAGE, "engine context is closed");
+  *out = ctx_of_handle(p);
+  if (*out == nullptr || (*out)->ctx == nullptr) return throw_fmt(env, FMT_E_USAGE, "engine context is closed");
   return true;
 }
 
@@ -160,6 +200,11 @@ napi_value Open(napi_env env, napi_callback_info info) {
   CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   int32_t device = 0;
   if (argc >= 1) napi_get_value_int32(env, argv[0], &device);
+  if (live_contexts() >= max_contexts()) {
+    throw_fmt(env, FMT_E_CAPACITY,
+              "open: " + std::to_string(max_contexts()) + " engine contexts are open (close() the ones no longer used)");
+    return nullptr;
+  }
   fmt_config cfg;
   std::memset(&cfg, 0, sizeof cfg);
   cfg.device = device;
@@ -173,9 +218,14 @@ napi_value Open(napi_env env, napi_callback_info info) {
   }
   auto* c = new Ctx;
   c->ctx = ctx;
+  std::vector<Slot>& t = slots();
+  size_t k = 0;
+  while (k < t.size() && t[k].c != nullptr) k++;
+  if (k == t.size()) t.emplace_back();
+  t[k].c = c;
+  const uint64_t h = static_cast<uint64_t>(k + 1) | (static_cast<uint64_t>(t[k].gen) << 32);
   napi_value ext;
-  CHECK_NAPI(env, napi_create_external(env, c, finalize_ctx, nullptr, &ext));
-  CHECK_NAPI(env, napi_create_reference(env, ext, 1, &c->self));
+  CHECK_NAPI(env, napi_create_external(env, reinterpret_cast<void*>(static_cast<uintptr_t>(h)), nullptr, nullptr, &ext));
   return ext;
 }
 
@@ -188,14 +238,26 @@ napi_value Close(napi_env env, napi_callback_info info) {
     throw_fmt(env, FMT_E_USAGE, "close: expected an engine context");
     return nullptr;
   }
-  auto* c = static_cast<Ctx*>(p);
+  Ctx* c = ctx_of_handle(p);
+  if (c == nullptr) return nullptr;  // already closed: a no-op, as before
   if (c->busy) {
     throw_fmt(env, FMT_E_USAGE, "close: a replay is still running on this context");
     return nullptr;
   }
+  const uint64_t h = reinterpret_cast<uintptr_t>(p);
+  Slot& s = slots()[static_cast<uint32_t>(h & 0xffffffffu) - 1];
   if (c->ctx) fmt_close(c->ctx);
-  c->ctx = nullptr;
+  delete c;
+  s.c = nullptr;
+  s.gen++;
   return nullptr;
+}
+
+// openContexts() -> number of engine contexts open in this process (diagnostics and tests)
+napi_value OpenContexts(napi_env env, napi_callback_info) {
+  napi_value v;
+  CHECK_NAPI(env, napi_create_uint32(env, live_contexts(), &v));
+  return v;
 }
 
 napi_value DeviceInfo(napi_env env, napi_callback_info info) {
@@ -885,20 +947,40 @@ napi_value FetchLegacyProps(napi_env env, napi_callback_info info) {
 }
 
 // FMT_NAPI_BACKTRACE=1: a SIGSEGV prints the native stack to stderr before the default action
-// (diagnostics for crashes inside the addon or the HIP runtime under node).
+// (diagnostics for crashes inside the addon or the HIP runtime under node). backtrace() is called
+// once before the handler is installed (it loads libgcc's unwinder, which allocates), the handler
+// runs on its own stack (a fault from a stack overflow still reports) and is reset on entry.
 void segvTrace(int sig) {
   void* frames[64];
   const int n = backtrace(frames, 64);
   backtrace_symbols_fd(frames, n, 2);
-  std::signal(sig, SIG_DFL);
-  raise(sig);
+  raise(sig);  // SA_RESETHAND: the default action now
+}
+
+void install_segv_trace() {
+  void* warm[2];
+  backtrace(warm, 2);
+  static std::vector<char>* alt = new std::vector<char>(1 << 16);
+  stack_t ss;
+  std::memset(&ss, 0, sizeof ss);
+  ss.ss_sp = alt->data();
+  ss.ss_size = alt->size();
+  sigaltstack(&ss, nullptr);
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof sa);
+  sa.sa_handler = segvTrace;
+  sa.sa_flags = SA_RESETHAND | SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, nullptr);
 }
 
 napi_value Init(napi_env env, napi_value exports) {
-  if (std::getenv("FMT_NAPI_BACKTRACE") != nullptr) std::signal(SIGSEGV, segvTrace);
+  if (std::getenv("FMT_NAPI_BACKTRACE") != nullptr) install_segv_trace();
+  napi_add_env_cleanup_hook(env, close_all_at_teardown, nullptr);
   napi_property_descriptor fns[] = {
       {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"openContexts", nullptr, OpenContexts, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"deviceInfo", nullptr, DeviceInfo, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"capacity", nullptr, Capacity, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"stats", nullptr, Stats, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

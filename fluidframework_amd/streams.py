@@ -66,6 +66,11 @@ MT_F_MARKER = 32  # fmt.h FMT_MT_F_MARKER: insert of a Marker segment
 MT_F_REL1, MT_F_REL2 = 64, 128  # fmt.h FMT_MT_F_REL1/REL2: pos1/pos2 index the relpos table
 MT_F_LOADSEG = 256  # fmt.h FMT_MT_F_LOADSEG: a SnapshotV1 body segment the loader appends
 MT_F_LEN_HI_SHIFT, MT_F_LEN_HI_MASK = 16, 0x00FF0000  # fmt.h: bits 16..23 of an insert's length
+# fmt.h f4, the local client: a submission, the ack of the oldest pending op, rollback of the newest,
+# reconnect (regeneratePendingOp for every pending op)
+MT_F_LOCAL, MT_F_ACK, MT_F_ROLLBACK, MT_F_REGEN = 512, 1024, 2048, 4096
+MT_F_LOCAL_ANY = MT_F_LOCAL | MT_F_ACK | MT_F_ROLLBACK | MT_F_REGEN
+LOCAL_SEQ_BASE = 0x40000000  # fmt.h FMT_MT_LOCAL_SEQ_BASE: ins_seq / rm_seq of a stamp pending its ack
 MAX_INSERT_UNITS = (1 << 24) - 1
 
 
@@ -282,6 +287,11 @@ class _DocBuilder:
         self.marker_ids: set = set()
         self.marker_ambiguous = False
         self.uses_relpos = False
+        # f4: the local client (the observer name is its long id, short id 0). pending: its
+        # unacknowledged ops in submission order, each (record type, payload) — what ACK and
+        # ROLLBACK records must repeat (mergeTree.ts:1325-1408, 2388-2514)
+        self.local = False
+        self.pending: list[tuple] = []
 
     def note_marker_id(self, props) -> None:
         mid = (props or {}).get(MARKER_ID_KEY)
@@ -347,7 +357,9 @@ class _DocBuilder:
         return i
 
     def add_message(self, msg: dict) -> None:
-        """Append one ISequencedDocumentMessage (type "op") with merge-tree contents."""
+        """Append one ISequencedDocumentMessage (type "op") with merge-tree contents. In a document
+        with local events (f4), a message of the local client itself acknowledges its oldest pending
+        ops, one per member (client.ts:1367-1368 ackPendingSegment)."""
         seq = int(msg["sequenceNumber"])
         ref = int(msg["referenceSequenceNumber"])
         msn = int(msg["minimumSequenceNumber"])
@@ -356,6 +368,7 @@ class _DocBuilder:
         members = contents["ops"] if contents["type"] == MT_GROUP else [contents]
         if not members:
             members = [None]
+        ack = self.local and client == 0
         if self.owner.keep_messages:
             self.messages.append((msg, len(self.ops), len(members)))
         for k, op in enumerate(members):
@@ -363,8 +376,55 @@ class _DocBuilder:
             rec = self.owner._pack(op, seq, ref, msn, client)
             if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
                 rec = rec[:-1] + (rec[-1] | 1,)
+            if ack:
+                if op is None or not self.pending or self.pending[0][0] != rec[8]:
+                    raise ValueError("an ack that is not the oldest pending local op")  # mergeTree.ts:1331-1340
+                self.pending.pop(0)
+                rec = rec[:-1] + (rec[-1] | MT_F_ACK,)
             self.ops.append(rec)
         self.min_seq = max(self.min_seq, msn)  # updateSeqNumbers after the message (client.ts:1381-1391)
+
+    # ---- f4: the local client's own events (the document's observer is that client) ----
+    def local_op(self, op: dict) -> None:
+        """A local submission (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
+        client.ts:273-355): op contents with positions in the local view. A GROUP op (localTransaction,
+        client.ts:1600-1629) submits its members one by one."""
+        members = op["ops"] if op["type"] == MT_GROUP else [op]
+        for m in members:
+            if m["type"] not in (MT_INSERT, MT_REMOVE, MT_ANNOTATE):
+                raise UnsupportedOp("local obliterate")
+            self._note_op(m)
+            rec = self.owner._pack(m, 0, 0, 0, 0)
+            if rec[9] & (MT_F_REL1 | MT_F_REL2):
+                raise UnsupportedOp("local op with relative positions")
+            self.local = True
+            self.pending.append((rec[8], rec[5]))
+            self.ops.append(rec[:-1] + (rec[-1] | MT_F_LOCAL,))
+
+    def local_rollback(self) -> None:
+        """Rollback of the newest pending op (client.ts:554; a GROUP op: call once per member)."""
+        if not self.pending:
+            raise ValueError("rollback without a pending local op")
+        t, payload = self.pending.pop()
+        self.ops.append((0, 0, 0, 0, 0, payload, 0, 0, t, MT_F_ROLLBACK))
+
+    def local_regen(self, new_ops: list | None = None) -> None:
+        """Reconnect: regeneratePendingOp for every pending op (client.ts:1452-1542). The ops it
+        returns (one per segment of each pending op, in order: what fmt_mt_fetch_regen returns)
+        become the pending ops, whose acks follow as the local client's messages: pass them here, or
+        to regen_pending once known."""
+        self.local = True
+        self.ops.append((0, 0, 0, 0, 0, 0, 0, 0, 0, MT_F_REGEN))
+        self.pending = []
+        if new_ops is not None:
+            self.regen_pending(new_ops)
+
+    def regen_pending(self, new_ops: list) -> None:
+        self.pending = []
+        for op in new_ops:
+            t = op["type"]
+            payload = self.owner._props_op(op.get("props") or {}, op.get("adjust")) if t == MT_ANNOTATE else 0
+            self.pending.append((t, payload))
 
     def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
         self._note_op(op)

@@ -118,6 +118,36 @@ extern "C" {
 #define FMT_MT_CLIENT_NONCOLLAB 0xFEu
 /* INSERT longer than 65535 UTF-16 units (a large paste): flags bits 16..23 hold bits 16..23 of the
  * length, `len` its low 16 bits (inserts up to 2^24 - 1 units; fmt_mt_op_len). */
+/* f4 — the local client (a Client whose own ops apply before they are sequenced). A document with
+ * these records is replayed from the perspective of its own client, short client id 0 (it never
+ * appears as a remote client of that document). Each flag below makes the record a local event
+ * instead of a remote message:
+ * FMT_MT_F_LOCAL: a submission (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
+ *   client.ts:273-355): INSERT / REMOVE / ANNOTATE with positions in the local view
+ *   (LocalDefaultPerspective, perspective.ts:174-184), stamped {UnassignedSequenceNumber, 0,
+ *   localSeq = ++localSeq}; its segments form a pending segment group (mergeTree.ts:1410-1447). No
+ *   collab-window update, no zamboni; seq / ref_seq / min_seq are not read. An invalid range is
+ *   FMT_E_USAGE (client.ts:797-810).
+ * FMT_MT_F_ACK: a sequenced message of the local client (client.ts:1367-1368 ackPendingSegment →
+ *   mergeTree.ts:1325-1408 ackOp): acknowledges the OLDEST pending group with {seq, 0}; type (and an
+ *   ANNOTATE's props op, whose keys PropertiesManager.ack shifts, segmentPropertiesManager.ts:248-267)
+ *   must be the group's, else FMT_E_DATA; then the collab window advances like any message (a
+ *   GROUP message: one ACK per member, FMT_MT_F_GROUP_CONT).
+ * FMT_MT_F_ROLLBACK: rollback of the NEWEST pending group (client.ts:554 → mergeTree.ts:2388-2514;
+ *   a GROUP op's members newest first); type must match.
+ * FMT_MT_F_REGEN: reconnect — regeneratePendingOp for every pending group in order
+ *   (client.ts:1452-1542, squash false): segments normalized (mergeTree.ts:2734-2766), then one new
+ *   op per segment at its position in LocalReconnectingPerspective(currentSeq, 0, localSeq)
+ *   (resetPendingDeltaToOps, client.ts:1160-1289); the new ops replace the pending groups and are
+ *   returned by fmt_mt_fetch_regen. */
+#define FMT_MT_F_LOCAL 512u
+#define FMT_MT_F_ACK 1024u
+#define FMT_MT_F_ROLLBACK 2048u
+#define FMT_MT_F_REGEN 4096u
+#define FMT_MT_F_LOCAL_ANY (FMT_MT_F_LOCAL | FMT_MT_F_ACK | FMT_MT_F_ROLLBACK | FMT_MT_F_REGEN)
+/* fmt_mt_leaf.ins_seq / rm_seq of a stamp still pending its ack: this | its localSeq (stamps.ts:47;
+ * above every sequence number, below FMT_NOT_REMOVED). Sequence numbers stay below it. */
+#define FMT_MT_LOCAL_SEQ_BASE 0x40000000
 #define FMT_MT_F_LEN_HI_SHIFT 16
 #define FMT_MT_F_LEN_HI_MASK 0x00FF0000u
 typedef struct fmt_mt_op {
@@ -486,6 +516,10 @@ typedef struct fmt_map_local_op {
 /* birth_seq of an optimistic entry that comes from a pending set lifetime: this bit | the index,
  * within the document's events, of the submission that created the lifetime */
 #define FMT_MAP_PENDING_BIRTH 0x80000000u
+/* Local events per document: one device thread walks a document's pending lists (a submit's
+ * findLast and the iterator's scans are linear in the pending list), so a longer event list gets
+ * status FMT_E_CAPACITY and no entries instead of stalling the launch. */
+#define FMT_MAP_PENDING_MAX_EVENTS 16384
 /* Every document's optimistic view over the sequenced entries of the last fmt_map_run_sparse and
  * the documents' local events (document d's at events[doc_event_offsets[d] .. [d + 1])), one
  * device thread per document. Asynchronous on the ctx stream. */
@@ -493,8 +527,9 @@ int fmt_map_pending_run(fmt_ctx* ctx, const fmt_map_local_op* events, uint64_t n
                         const uint64_t* doc_event_offsets);
 /* counts[d] = optimistic entries of document d; entries packed in document order, each document's
  * in internalIterator order (key, optimistic value, birth_seq: the sequenced birth, or
- * FMT_MAP_PENDING_BIRTH | creating submission); status[d] (may be NULL): FMT_OK, or FMT_E_DATA for
- * a document whose ACK / ROLLBACK events do not match its pending ops (no entries). Synchronizes. */
+ * FMT_MAP_PENDING_BIRTH | creating submission); status[d] (may be NULL): FMT_OK, FMT_E_DATA for
+ * a document whose ACK / ROLLBACK events do not match its pending ops, or FMT_E_CAPACITY for one
+ * with more than FMT_MAP_PENDING_MAX_EVENTS events (no entries). Synchronizes. */
 int fmt_map_pending_fetch(fmt_ctx* ctx, uint32_t* counts, int32_t* status, fmt_map_entry* entries,
                           uint64_t cap_entries, uint64_t* n_entries);
 

@@ -31,20 +31,34 @@ int fail(const char* what) {
 }
 
 // Applies ops[0..n): a record flagged FMT_MT_F_GROUP_CONT continues the previous message.
+// f4 (FMT_MT_F_LOCAL / ACK / ROLLBACK / REGEN): the local client's events; REGEN appends its new ops
+// (and their insert text) to *regen / *regenText.
 int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* arena,
              const uint32_t* propsOff, const uint32_t* propsKv, int32_t* failSeq,
-             std::vector<fmt_mt_catchup_range>* catchup = nullptr) {
+             std::vector<fmt_mt_catchup_range>* catchup = nullptr, std::vector<fmt_mt_op>* regen = nullptr,
+             std::u16string* regenText = nullptr) {
   for (uint64_t i = 0; i < n; i++) {
     const fmt_mt_op& op = ops[i];
     try {
+      if (op.flags & (FMT_MT_F_LOCAL | FMT_MT_F_ROLLBACK | FMT_MT_F_REGEN)) {  // no collab-window update
+        if (op.flags & FMT_MT_F_LOCAL) mt->applyLocal(op, arena, propsOff, propsKv);
+        else if (op.flags & FMT_MT_F_ROLLBACK) mt->rollback(op);
+        else mt->regeneratePending(regen ? regen : &mt->regenOps, regenText ? regenText : &mt->regenText);
+        continue;
+      }
       mt->catchupOut = (catchup && (op.flags & FMT_MT_F_CATCHUP)) ? catchup : nullptr;
       mt->catchupOp = static_cast<uint32_t>(i);
-      mt->applyRemote(op, arena, propsOff, propsKv);
+      if (op.flags & FMT_MT_F_ACK) mt->ackOp(op, propsOff, propsKv);
+      else mt->applyRemote(op, arena, propsOff, propsKv);
       mt->catchupOut = nullptr;
       // (loader segments: no collab-window update; a batch of them is not a GROUP message)
       if ((op.flags & FMT_MT_F_LOADSEG) == 0 &&
           (i + 1 == n || (ops[i + 1].flags & (FMT_MT_F_GROUP_CONT | FMT_MT_F_LOADSEG)) != FMT_MT_F_GROUP_CONT))
         mt->updateSeqNumbers(op.min_seq, op.seq);
+    } catch (const orc::UsageError& e) {
+      if (failSeq) *failSeq = op.seq;
+      fail(e.what());
+      return FMT_E_USAGE;
     } catch (const std::exception& e) {
       if (failSeq) *failSeq = op.seq;
       return fail(e.what());
@@ -81,9 +95,11 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
     if (leaves && i < capLeaves) {
       fmt_mt_leaf& L = leaves[i];
       std::memset(&L, 0, sizeof(L));
-      L.ins_seq = s->ins.seq;
+      // (a stamp pending its ack: FMT_MT_LOCAL_SEQ_BASE | localSeq, the engine's encoding)
+      auto seqOf = [](const orc::Stamp& st) { return orc::isLocal(st) ? FMT_MT_LOCAL_SEQ_BASE | st.localSeq : st.seq; };
+      L.ins_seq = seqOf(s->ins);
       L.ins_client = static_cast<int16_t>(s->ins.client);
-      L.rm_seq = s->removed() ? s->removes[0].seq : FMT_NOT_REMOVED;
+      L.rm_seq = s->removed() ? seqOf(s->removes[0]) : FMT_NOT_REMOVED;
       uint64_t mask = 0;
       for (const auto& r : s->removes)
         if (r.client >= 0 && r.client < 64) mask |= 1ull << r.client;
@@ -230,6 +246,24 @@ int orc_mt_apply_ops(void* h, const fmt_mt_op* ops, uint64_t n, const uint16_t* 
 }
 
 // Returns the text length; copies min(len, cap) UTF-16 units.
+// f4: the local length (getLength, client.ts:1696) and the ops REGEN events produced since the last
+// take (their insert text in `text`, payloads relative to it); *nOps / *nText are the full counts. With
+// out and text both NULL only the counts are reported; otherwise the buffers are handed over and cleared.
+int orc_mt_local_length(void* h) { return static_cast<MergeTree*>(h)->getLocalLength(); }
+int orc_mt_pending_groups(void* h) { return static_cast<int>(static_cast<MergeTree*>(h)->pendingGroups()); }
+int orc_mt_regen_take(void* h, fmt_mt_op* out, uint32_t cap, uint16_t* text, uint32_t textCap, uint32_t* nOps,
+                      uint32_t* nText) {
+  MergeTree* mt = static_cast<MergeTree*>(h);
+  *nOps = static_cast<uint32_t>(mt->regenOps.size());
+  *nText = static_cast<uint32_t>(mt->regenText.size());
+  if (out == nullptr && text == nullptr) return FMT_OK;  // (counts only)
+  for (uint32_t i = 0; i < *nOps && i < cap; i++) out[i] = mt->regenOps[i];
+  for (uint32_t i = 0; i < *nText && i < textCap; i++) text[i] = static_cast<uint16_t>(mt->regenText[i]);
+  mt->regenOps.clear();
+  mt->regenText.clear();
+  return FMT_OK;
+}
+
 int orc_mt_text(void* h, uint16_t* buf, int cap) {
   const std::u16string t = static_cast<MergeTree*>(h)->getText();
   for (int i = 0; i < static_cast<int>(t.size()) && i < cap; i++) buf[i] = static_cast<uint16_t>(t[i]);
@@ -376,6 +410,24 @@ int orc_mt_replay_batch(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docEn
   });
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return status.load();
+}
+
+// f4: document d of a batch replayed; its REGEN events' ops (fmt_mt_fetch_regen's layout: insert
+// payloads index `text`). Returns the replay status.
+int orc_mt_replay_regen(const fmt_mt_batch* b, uint32_t d, fmt_mt_op* out, uint32_t cap, uint16_t* text,
+                        uint32_t textCap, uint32_t* nOps, uint32_t* nText) {
+  MergeTree mt;
+  startDoc(mt, b, d);
+  int32_t failSeq = 0;
+  std::vector<fmt_mt_op> ops;
+  std::u16string t;
+  const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
+  const int st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &failSeq, nullptr, &ops, &t);
+  *nOps = static_cast<uint32_t>(ops.size());
+  *nText = static_cast<uint32_t>(t.size());
+  for (uint32_t i = 0; i < *nOps && i < cap; i++) out[i] = ops[i];
+  for (uint32_t i = 0; i < *nText && i < textCap; i++) text[i] = static_cast<uint16_t>(t[i]);
+  return st;
 }
 
 // Replays documents [docBegin, docEnd) like orc_mt_replay_batch and digests each final state

@@ -2,6 +2,8 @@
 #include "mergetree.hpp"
 
 #include <algorithm>
+#include <list>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -286,6 +288,22 @@ Seg* MergeTree::splitAt(Seg* seg, int pos) {
   seg->text.resize(static_cast<size_t>(pos));
   next->ins = seg->ins;
   next->removes = seg->removes;
+  // SegmentGroupCollection.copyTo (segmentGroupCollection.ts:47-59, splitLeafSegment mergeTree.ts:1779-1782):
+  // the right part joins every pending group of the left, in the left's queue order
+  for (SegmentGroup* g : seg->groups) {
+    next->groups.push_back(g);
+    if (g->hasPrevious) {
+      const size_t idx = static_cast<size_t>(std::find(g->segments.begin(), g->segments.end(), seg) - g->segments.begin());
+      const bool found = idx < g->segments.size();
+      g->segments.push_back(next);
+      if (found) {
+        auto copy = g->previousProps.at(idx);  // (push_back may reallocate)
+        g->previousProps.push_back(std::move(copy));
+      }
+    } else {
+      g->segments.push_back(next);
+    }
+  }
   if (seg->props.defined) {  // copyPropertiesAndManager (segmentPropertiesManager.ts:24-42, copyTo :300-316)
     next->props = seg->props;
     if (seg->pm) next->pm = std::make_unique<PropManager>(*seg->pm);
@@ -598,10 +616,10 @@ void MergeTree::insertSegments(int pos, Seg* seg, const Perspective& p, Stamp st
     if (indexed_) idxOnNewLeaf(seg);
     // delta callback precedes zamboni (:1497-1516); an insert obliterated on arrival raises none
     if (catchupOut && !seg->removed()) recordDelta(FMT_MT_INSERT, {seg});
-    if (collaborating) {
-      const bool isLocal = stamp.seq == kUnassignedSeq;
-      if (!(isLocal && stamp.client == clientId) &&
-          stampGreater(seg->ins, Stamp{minSeq, kNonCollabClient}))
+    if (collaborating) {  // saveIfLocal (mergeTree.ts:1573-1591)
+      if (isLocal(seg->ins) && stamp.client == clientId)
+        addToPendingList(seg, nullptr, stamp.localSeq);
+      else if (stampGreater(seg->ins, Stamp{minSeq, kNonCollabClient}))
         addToLRUSet(seg, seg->ins.seq);
     }
   }
@@ -615,6 +633,7 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
   std::vector<Seg*> hit;
   nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
   std::vector<Seg*> newlyRemoved;  // removedSegments: the REMOVE delta (mergeTree.ts:2314-2321)
+  SegmentGroup* group = nullptr;
   for (Seg* s : hit) {
     const bool wasRemoved = s->removed();
     if (!s->removed() || stamp.seq == kUnassignedSeq) {
@@ -627,9 +646,9 @@ void MergeTree::markRangeRemoved(int start, int end, const Perspective& p, Stamp
       s->removes.insert(s->removes.begin() + (i + 1), stamp);
     }
     if (indexed_) idxOnRemove(s, stamp.client, wasRemoved);
-    if (collaborating) {
-      const bool localPending = s->removes[0].seq == kUnassignedSeq && stamp.client == clientId;
-      if (!localPending) addToLRUSet(s, stamp.seq);
+    if (collaborating) {  // mergeTree.ts:2335-2347
+      if (isLocal(s->removes[0]) && stamp.client == clientId) group = addToPendingList(s, group, stamp.localSeq);
+      else addToLRUSet(s, stamp.seq);
     }
   }
   if (catchupOut) recordDelta(FMT_MT_REMOVE, newlyRemoved);  // mergeTree.ts:2363-2368
@@ -693,7 +712,7 @@ void MergeTree::updateMsn(PropManager& pm, int msn) {
     while (n < e.remote.size() && e.remote[n].seq <= msn) n++;
     e.msnConsensus = foldChanges(e.msnConsensus, e.remote, n);
     e.remote.erase(e.remote.begin(), e.remote.begin() + static_cast<std::ptrdiff_t>(n));
-    if (e.remote.empty()) pm.changes.erase(pm.changes.begin() + static_cast<std::ptrdiff_t>(k));
+    if (e.remote.empty() && e.local.empty()) pm.changes.erase(pm.changes.begin() + static_cast<std::ptrdiff_t>(k));
     else k++;
   }
 }
@@ -721,46 +740,65 @@ PropMap MergeTree::getAtSeq(const Seg* s, int seq) {
   return out;
 }
 
-// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238 handleProperties. For an
-// observer every change is remote: a key's entry starts at its current value (null when absent), a
-// raw change folds into msnConsensus while the key has no remote change pending and is queued
-// otherwise (an adjust always is), and properties[key] = computePropertyValue(msnConsensus, remote);
-// null deletes the key; `seg.properties ??= createMap()` runs even if nothing changes. Then
-// updateMsn(collabWindow.minSeq).
+// mergeTree.ts:2009-2081 annotateRange + segmentPropertiesManager.ts:188-238 handleProperties: a
+// key's entry starts at its current value (null when absent); a local change joins its local list, a
+// raw remote change folds into msnConsensus while the key has no remote change pending and is queued
+// otherwise (an adjust always is); properties[key] = computePropertyValue(msnConsensus, remote,
+// local); null deletes the key; `seg.properties ??= createMap()` runs even if nothing changes. Then
+// updateMsn(collabWindow.minSeq). A local op's segments join its pending group with their
+// propertyDeltas (the keys' previous values, for rollback); rollbackOp: rollbackProperties instead
+// (handleProperties' rollback branch, :196-198).
 void MergeTree::annotateRange(int start, int end, const std::vector<PropChange>& props, const Perspective& p,
-                              Stamp stamp) {
+                              Stamp stamp, bool rollbackOp) {
   ensureIntervalBoundary(start, p);
   ensureIntervalBoundary(end, p);
   std::vector<Seg*> hit;
   nodeMap(p, start, end, [&](Seg* s) { hit.push_back(s); });
+  SegmentGroup* group = nullptr;
+  const bool local = isLocal(stamp);
   for (Seg* s : hit) {
     s->props.defined = true;
     if (!s->pm) s->pm = std::make_unique<PropManager>();
     PropManager& pm = *s->pm;
-    for (const PropChange& ch : props) {
-      const uint16_t key = ch.key;
-      auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(),
-                             [&](const auto& e) { return e.first == key; });
-      const uint16_t previous = it != s->props.kv.end() ? it->second : 0;
-      auto pe = std::find_if(pm.changes.begin(), pm.changes.end(), [&](const PropPending& e) { return e.key == key; });
-      if (pe == pm.changes.end()) {
-        pm.changes.push_back(PropPending{key, previous, {}});
-        pe = pm.changes.end() - 1;
+    if (rollbackOp) {
+      std::vector<std::pair<uint16_t, uint16_t>> kv;
+      for (const PropChange& ch : props) kv.emplace_back(ch.key, ch.value);
+      rollbackProperties(s, kv);
+    } else {
+      std::vector<std::pair<uint16_t, uint16_t>> deltas;  // propertyDeltas: key -> previous value
+      for (const PropChange& ch : props) {
+        const uint16_t key = ch.key;
+        auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(),
+                               [&](const auto& e) { return e.first == key; });
+        const uint16_t previous = it != s->props.kv.end() ? it->second : 0;
+        auto pe = std::find_if(pm.changes.begin(), pm.changes.end(), [&](const PropPending& e) { return e.key == key; });
+        if (pe == pm.changes.end()) {
+          pm.changes.push_back(PropPending{key, previous, {}, {}});
+          pe = pm.changes.end() - 1;
+        }
+        const PropChangeRec rec{stamp.seq, ch.adjust >= 0, ch.value, ch.adjust};
+        if (local) pe->local.push_back(rec);
+        else if (!rec.adjust && pe->remote.empty()) pe->msnConsensus = rec.value;
+        else pe->remote.push_back(rec);
+        const uint16_t afterRemote = foldChanges(pe->msnConsensus, pe->remote, pe->remote.size());
+        const uint16_t value = foldChanges(afterRemote, pe->local, pe->local.size());
+        if (local || pe->local.empty() || value != previous) {
+          auto d = std::find_if(deltas.begin(), deltas.end(), [&](const auto& e) { return e.first == key; });
+          if (d == deltas.end()) deltas.emplace_back(key, previous);
+          else d->second = previous;
+        }
+        if (value == 0) {  // null → delete
+          if (it != s->props.kv.end()) s->props.kv.erase(it);
+        } else if (it != s->props.kv.end()) {
+          it->second = value;
+        } else {
+          s->props.kv.emplace_back(key, value);
+        }
       }
-      const PropChangeRec rec{stamp.seq, ch.adjust >= 0, ch.value, ch.adjust};
-      if (!rec.adjust && pe->remote.empty()) pe->msnConsensus = rec.value;
-      else pe->remote.push_back(rec);
-      const uint16_t value = foldChanges(pe->msnConsensus, pe->remote, pe->remote.size());
-      if (value == 0) {  // null → delete
-        if (it != s->props.kv.end()) s->props.kv.erase(it);
-      } else if (it != s->props.kv.end()) {
-        it->second = value;
-      } else {
-        s->props.kv.emplace_back(key, value);
-      }
+      updateMsn(pm, minSeq);
+      if (collaborating && local) group = addToPendingList(s, group, stamp.localSeq, &deltas);
     }
-    updateMsn(pm, minSeq);
-    if (collaborating && stamp.seq != kUnassignedSeq) addToLRUSet(s, stamp.seq);
+    if (collaborating && !local) addToLRUSet(s, stamp.seq);
   }
   if (catchupOut) {  // deltaSegments: annotated segments not removed (mergeTree.ts:2045-2047, 2068-2073)
     std::vector<Seg*> delta;
@@ -768,7 +806,32 @@ void MergeTree::annotateRange(int start, int end, const std::vector<PropChange>&
       if (!s->removed()) delta.push_back(s);
     recordDelta(FMT_MT_ANNOTATE, delta);
   }
-  if (collaborating && stamp.seq != kUnassignedSeq) zamboniSegments();
+  if (collaborating && !local) zamboniSegments();
+}
+
+// segmentPropertiesManager.ts:140-173 (collaborating): each key of the op (its previous values are
+// not read) drops its newest local change and takes computePropertyValue(msnConsensus, remote, local)
+// again; a key left with no change loses its entry; null deletes the key.
+void MergeTree::rollbackProperties(Seg* s, const std::vector<std::pair<uint16_t, uint16_t>>& props) {
+  s->props.defined = true;  // applyChanges: seg.properties ??= createMap()
+  if (!s->pm) s->pm = std::make_unique<PropManager>();
+  PropManager& pm = *s->pm;
+  for (const auto& [key, prev] : props) {
+    (void)prev;
+    auto pe = std::find_if(pm.changes.begin(), pm.changes.end(), [&](const PropPending& e) { return e.key == key; });
+    if (pe == pm.changes.end()) throw DataError("Pending changes must exist for rollback when collaborating");  // 0xa6f
+    if (!pe->local.empty()) pe->local.pop_back();
+    const uint16_t value = foldChanges(foldChanges(pe->msnConsensus, pe->remote, pe->remote.size()), pe->local, pe->local.size());
+    if (pe->local.empty() && pe->remote.empty()) pm.changes.erase(pe);
+    auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(), [&](const auto& e) { return e.first == key; });
+    if (value == 0) {
+      if (it != s->props.kv.end()) s->props.kv.erase(it);
+    } else if (it != s->props.kv.end()) {
+      it->second = value;
+    } else {
+      s->props.kv.emplace_back(key, value);
+    }
+  }
 }
 
 // mergeTree.ts:835-856 getPosition: lengths of everything before the node, walking up the parents.
@@ -873,6 +936,360 @@ void MergeTree::annotateLocal(int start, int end,
 void MergeTree::removeLocal(int start, int end) {
   markRangeRemoved(start, end, localPerspective(),
                    Stamp{collaborating ? kUnassignedSeq : 0, clientId});
+}
+
+// ------------------------------------------------------------------------------------------------
+// f4: the local client
+// ------------------------------------------------------------------------------------------------
+// mergeTree.ts:1410-1447 addToPendingList + segmentGroupCollection.ts:25-28 enqueue.
+SegmentGroup* MergeTree::addToPendingList(Seg* seg, SegmentGroup* group, int localSeqArg,
+                                          const std::vector<std::pair<uint16_t, uint16_t>>* previousProps) {
+  if (group == nullptr) {
+    if (localSeqArg <= 0) throw DataError("Local seq should be passed when creating new segment group");  // 0xb72
+    groupPool_.push_back(std::make_unique<SegmentGroup>());
+    group = groupPool_.back().get();
+    group->localSeq = localSeqArg;
+    group->refSeq = currentSeq;
+    group->hasPrevious = previousProps != nullptr;
+    pendingSegments_.push_back(group);
+  }
+  if (group->hasPrevious != (previousProps != nullptr)) throw DataError("All segments in group should have previousProps or none");
+  if (previousProps) group->previousProps.push_back(*previousProps);
+  seg->groups.push_back(group);
+  group->segments.push_back(seg);
+  return group;
+}
+
+namespace {
+std::vector<MergeTree::PropChange> opChanges(const fmt_mt_op& op, const uint32_t* propsOff, const uint32_t* propsKv) {
+  std::vector<MergeTree::PropChange> kv;
+  for (uint32_t i = propsOff[op.payload]; i < propsOff[op.payload + 1]; i++) {
+    const uint16_t key = static_cast<uint16_t>(propsKv[i] >> 16), value = static_cast<uint16_t>(propsKv[i] & 0xffff);
+    if (value == FMT_MT_VALUE_ADJUST) {
+      if (i + 1 >= propsOff[op.payload + 1]) throw DataError("adjust entry without its row");
+      kv.push_back(MergeTree::PropChange{key, 0, static_cast<int32_t>(propsKv[++i])});
+    } else {
+      kv.push_back(MergeTree::PropChange{key, value, -1});
+    }
+  }
+  return kv;
+}
+}  // namespace
+
+void MergeTree::applyLocal(const fmt_mt_op& op, const uint16_t* arena, const uint32_t* propsOff, const uint32_t* propsKv) {
+  if (!collaborating) throw DataError("local op before collaboration");
+  const Perspective lp = localPerspective();
+  // getValidOpRange (client.ts:749-815), local branch: positions against the local length
+  const int length = getLocalLength();
+  const int start = op.pos1, end = op.pos2;
+  if (op.type == FMT_MT_INSERT) {
+    if (start < 0 || start > length) throw UsageError("RangeOutOfBounds");
+  } else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
+    if (start < 0 || start >= length || end <= start) throw UsageError("RangeOutOfBounds");
+  } else {
+    throw DataError("unsupported local op type");
+  }
+  const size_t groupsBefore = pendingSegments_.size();
+  Stamp stamp{kUnassignedSeq, clientId, 0, 0};
+  if (op.type == FMT_MT_INSERT) {
+    const uint32_t len = fmt_mt_op_len(&op);
+    if (len == 0) return;  // insertSegmentLocal: nothing to insert, no op (client.ts:348-351)
+    stamp.localSeq = ++localSeq;  // mintNextLocalOperationStamp (mergeTreeNodes.ts:685-695)
+    Seg* s = makeSeg();
+    s->text.assign(reinterpret_cast<const char16_t*>(arena + op.payload), len);
+    s->marker = (op.flags & FMT_MT_F_MARKER) != 0;
+    if (op.pos2 > 0) {
+      const uint32_t id = static_cast<uint32_t>(op.pos2 - 1);
+      s->props.defined = true;
+      for (uint32_t i = propsOff[id]; i < propsOff[id + 1]; i++) {
+        const uint16_t key = static_cast<uint16_t>(propsKv[i] >> 16), value = static_cast<uint16_t>(propsKv[i] & 0xffff);
+        auto it = std::find_if(s->props.kv.begin(), s->props.kv.end(), [&](const auto& e) { return e.first == key; });
+        if (value == 0) {
+          if (it != s->props.kv.end()) s->props.kv.erase(it);
+        } else if (it != s->props.kv.end()) {
+          it->second = value;
+        } else {
+          s->props.kv.emplace_back(key, value);
+        }
+      }
+    }
+    if (s->marker) registerMarker(s);
+    insertSegments(start, s, lp, stamp);
+  } else if (op.type == FMT_MT_REMOVE) {
+    stamp.localSeq = ++localSeq;
+    markRangeRemoved(start, end, lp, stamp);
+  } else {
+    stamp.localSeq = ++localSeq;
+    annotateRange(start, end, opChanges(op, propsOff, propsKv), lp, stamp);
+  }
+  if (pendingSegments_.size() != groupsBefore + 1) throw DataError("local op created no segment group");
+  SegmentGroup* g = pendingSegments_.back();
+  g->type = op.type;
+  g->payload = static_cast<int32_t>(op.payload);
+  g->pos2 = op.type == FMT_MT_INSERT ? op.pos2 : 0;
+  g->flags = op.flags & FMT_MT_F_MARKER;
+}
+
+// mergeTree.ts:149-215 ackSegment + :1325-1408 ackOp.
+void MergeTree::ackOp(const fmt_mt_op& op, const uint32_t* propsOff, const uint32_t* propsKv) {
+  if (pendingSegments_.empty()) throw DataError("ack without a pending local op");
+  SegmentGroup* g = pendingSegments_.front();
+  if (g->type != op.type) throw DataError("ack of a different op type than the oldest pending op");
+  pendingSegments_.erase(pendingSegments_.begin());
+  const Stamp stamp{op.seq, clientId};
+  std::vector<PropChange> changes;
+  if (op.type == FMT_MT_ANNOTATE) changes = opChanges(op, propsOff, propsKv);
+  for (Seg* seg : g->segments) {
+    if (seg->groups.empty() || seg->groups.front() != g) throw DataError("On ack, unexpected segmentGroup!");  // 0x043
+    seg->groups.erase(seg->groups.begin());
+    switch (op.type) {
+      case FMT_MT_ANNOTATE: {  // PropertiesManager.ack (segmentPropertiesManager.ts:248-267)
+        if (!seg->pm) throw DataError("On annotate ack, missing segment property manager!");  // 0x044
+        for (const PropChange& ch : changes) {
+          auto pe = std::find_if(seg->pm->changes.begin(), seg->pm->changes.end(),
+                                 [&](const PropPending& e) { return e.key == ch.key; });
+          if (pe == seg->pm->changes.end() || pe->local.empty()) throw DataError("must have local change to ack");  // 0xa71
+          pe->local.erase(pe->local.begin());
+          const PropChangeRec rec{op.seq, ch.adjust >= 0, ch.value, ch.adjust};
+          if (!rec.adjust && pe->remote.empty()) pe->msnConsensus = rec.value;
+          else pe->remote.push_back(rec);
+        }
+        updateMsn(*seg->pm, op.min_seq);  // (the acked message's minimumSequenceNumber)
+        break;
+      }
+      case FMT_MT_INSERT:
+        if (!isLocal(seg->ins)) throw DataError("On insert, seq number already assigned!");  // 0x045
+        seg->ins = stamp;
+        break;
+      case FMT_MT_REMOVE: {
+        if (!seg->removed() || !isLocal(seg->removes.back())) throw DataError("Expected last remove to be unacked");  // 0xb5d
+        if (seg->removes.size() > 1 && isLocal(seg->removes[seg->removes.size() - 2]))
+          throw DataError("Expected prior remove to be acked");  // 0xb5e
+        seg->removes.back() = Stamp{op.seq, clientId, 0, 0};
+        break;
+      }
+      default:
+        throw DataError("unsupported ack op type");
+    }
+    addToLRUSet(seg, op.seq);
+  }
+  zamboniSegments();
+}
+
+// mergeTree.ts:2519-2536: the lengths of the not-removed segments before it.
+int MergeTree::findRollbackPosition(const Seg* seg) const {
+  int pos = 0;
+  bool found = false;
+  auto walk = [&](auto&& self, const Block* b) -> void {
+    for (int i = 0; i < b->childCount && !found; i++) {
+      const Node* n = b->children[i];
+      if (!n->isLeaf) {
+        self(self, static_cast<const Block*>(n));
+        continue;
+      }
+      const Seg* s = static_cast<const Seg*>(n);
+      if (s == seg) {
+        found = true;
+        return;
+      }
+      if (!s->removed()) pos += s->len();
+    }
+  };
+  walk(walk, root_);
+  return pos;
+}
+
+// mergeTree.ts:2388-2514 rollback (one op; GROUP members are rolled back last first by the caller).
+void MergeTree::rollback(const fmt_mt_op& op) {
+  if (pendingSegments_.empty()) throw DataError("Rollback op doesn't match last edit");
+  SegmentGroup* g = pendingSegments_.back();
+  if (g->type != op.type || (op.type == FMT_MT_ANNOTATE && !g->hasPrevious))
+    throw DataError("Rollback op doesn't match last edit");
+  pendingSegments_.pop_back();
+  const Stamp rollbackStamp{kTreeMaintSeq, kNonCollabClient};
+  if (op.type == FMT_MT_REMOVE) {
+    for (Seg* seg : g->segments) {
+      if (seg->groups.empty() || seg->groups.back() != g) throw DataError("Unexpected segmentGroup in segment");  // 0x3ee
+      seg->groups.pop_back();
+      if (!seg->removed() || seg->removes[0].kind != 0) throw DataError("Rollback segment removedClientId does not match local client");  // 0x39d
+      // a peer's concurrent remove keeps the segment removed
+      if (seg->removes[0].client == clientId) seg->removes.clear();  // removeRemovalInfo
+    }
+    return;
+  }
+  if (op.type != FMT_MT_INSERT && op.type != FMT_MT_ANNOTATE) throw DataError("Unsupported op type for rollback");
+  size_t i = 0;
+  for (Seg* seg : g->segments) {
+    if (seg->groups.empty() || seg->groups.back() != g) throw DataError("Unexpected segmentGroup in segment");  // 0x3ef
+    seg->groups.pop_back();
+    const int start = findRollbackPosition(seg);
+    if (op.type == FMT_MT_INSERT) {
+      seg->ins = rollbackStamp;
+      markRangeRemoved(start, start + seg->len(), localPerspective(), rollbackStamp);
+    } else {
+      const auto& props = g->previousProps.at(i);
+      if (seg->removed()) {
+        rollbackProperties(seg, props);
+      } else {
+        std::vector<PropChange> ch;
+        for (const auto& [k, v] : props) ch.push_back(PropChange{k, v, -1});
+        annotateRange(start, start + seg->len(), ch, localPerspective(), rollbackStamp, true);
+      }
+      i++;
+    }
+  }
+}
+
+// mergeTree.ts:2613-2712 normalizeAdjacentSegments over one run of adjacent removed / locally
+// inserted segments: segments removed by others slide after the last segment the local client
+// affected, locally removed ones past the local inserts made after their removal; the new order
+// takes the run's slots (parent, index) in order.
+void MergeTree::normalizeAdjacentSegments(std::vector<Seg*>& range) {
+  std::vector<std::pair<Block*, int>> slots;
+  for (Seg* s : range) slots.emplace_back(s->parent, s->index);
+  std::list<Seg*> list(range.begin(), range.end());
+  auto lastLocal = list.end();
+  for (auto it = list.end(); it != list.begin();) {
+    --it;
+    if (!isRemovedAndAcked(*it)) {
+      lastLocal = it;
+      break;
+    }
+  }
+  if (lastLocal == list.end()) return;
+  auto slide = lastLocal;
+  for (;;) {
+    const bool hasNearer = slide != list.begin();
+    const auto nearer = hasNearer ? std::prev(slide) : list.end();
+    Seg* seg = *slide;
+    if (isRemovedAndAcked(seg)) {
+      list.erase(slide);
+      list.insert(std::next(lastLocal), seg);
+    } else if (seg->removed()) {
+      auto cur = slide;
+      for (auto scan = std::next(cur); scan != list.end() && !isRemovedAndAcked(*scan) && (*scan)->ins.localSeq > 0 &&
+                                       stampGreater((*scan)->ins, seg->removes[0]);
+           ++scan)
+        cur = scan;
+      if (cur != slide) {
+        list.erase(slide);
+        list.insert(std::next(cur), seg);
+      }
+    }
+    if (!hasNearer) break;
+    slide = nearer;
+  }
+  size_t k = 0;
+  for (Seg* s : list) {
+    assignChild(slots[k].first, s, slots[k].second);
+    k++;
+  }
+}
+
+// mergeTree.ts:2734-2766: runs of adjacent segments that are removed or locally inserted, normalized
+// when a run holds both a local insert and a segment removed by an acked op.
+void MergeTree::normalizeSegmentsOnRebase() {
+  std::vector<Seg*> range;
+  bool hasLocal = false, hasRemote = false;
+  auto flush = [&]() {
+    if (hasLocal && hasRemote && range.size() > 1) normalizeAdjacentSegments(range);
+    range.clear();
+    hasLocal = hasRemote = false;
+  };
+  std::vector<const Seg*> leaves;
+  std::vector<int> blockOf;
+  int nb = 0, depth = 0;
+  collectLeaves(leaves, blockOf, &nb, &depth);
+  for (const Seg* cs : leaves) {
+    Seg* s = const_cast<Seg*>(cs);
+    if (s->removed() || isLocal(s->ins)) {
+      if (isRemovedAndAcked(s)) hasRemote = true;
+      if (isLocal(s->ins)) hasLocal = true;
+      range.push_back(s);
+    } else {
+      flush();
+    }
+  }
+  flush();
+}
+
+void MergeTree::regeneratePending(std::vector<fmt_mt_op>* out, std::u16string* text) {
+  if (pendingSegments_.empty()) return;
+  std::vector<SegmentGroup*> rebase;
+  rebase.swap(pendingSegments_);  // pendingRebase = pendingSegments.splice(first) (client.ts:1470-1477)
+  if (!lastNormSet_ || currentSeq != lastNormRefSeq_ || localSeq != lastNormLocalSeq_) {
+    normalizeSegmentsOnRebase();
+    lastNormSet_ = true;
+    lastNormRefSeq_ = currentSeq;
+    lastNormLocalSeq_ = localSeq;
+  }
+  // document order of every leaf (the segments' ordinals)
+  std::vector<const Seg*> leaves;
+  std::vector<int> blockOf;
+  int nb = 0, depth = 0;
+  collectLeaves(leaves, blockOf, &nb, &depth);
+  std::map<const Seg*, size_t> ordinal;
+  for (size_t k = 0; k < leaves.size(); k++) ordinal[leaves[k]] = k;
+  for (SegmentGroup* g : rebase) {  // resetPendingDeltaToOps (client.ts:963-1289), non-obliterate ops
+    std::vector<Seg*> segs = g->segments;
+    std::sort(segs.begin(), segs.end(), [&](const Seg* a, const Seg* b) { return ordinal.at(a) < ordinal.at(b); });
+    const Perspective rp{false, currentSeq, clientId, g->localSeq};
+    for (Seg* seg : segs) {
+      auto it = std::find(seg->groups.begin(), seg->groups.end(), g);
+      if (it == seg->groups.end()) throw DataError("Segment group not in segment pending queue");  // 0xb6c
+      seg->groups.erase(it);
+      const int pos = getPosition(seg, rp);  // findReconnectionPosition (client.ts:866-877)
+      fmt_mt_op o;
+      std::memset(&o, 0, sizeof o);
+      o.seq = g->localSeq;
+      o.ref_seq = currentSeq;
+      o.client = 0;
+      o.type = static_cast<uint8_t>(g->type);
+      bool emit = false;
+      if (g->type == FMT_MT_ANNOTATE) {
+        if (!isRemovedAndAcked(seg)) {
+          o.pos1 = pos;
+          o.pos2 = pos + seg->len();
+          o.payload = static_cast<uint32_t>(g->payload);
+          emit = true;
+        }
+      } else if (g->type == FMT_MT_INSERT) {
+        if (!isLocal(seg->ins)) throw DataError("Segment already has assigned sequence number");  // 0x037
+        if (seg->removed() && !isLocal(seg->removes[0])) throw DataError("obliterated local insert (obliterate reconnect unsupported)");
+        o.pos1 = pos;
+        o.pos2 = g->pos2;  // the original op's seg props (client.ts:1246-1252)
+        o.payload = static_cast<uint32_t>(text->size());
+        const uint32_t len = static_cast<uint32_t>(seg->len());
+        o.len = static_cast<uint16_t>(len & 0xFFFFu);
+        o.flags = (len & FMT_MT_F_LEN_HI_MASK) | (seg->marker ? FMT_MT_F_MARKER : 0u);
+        text->append(seg->text);
+        emit = true;
+      } else if (g->type == FMT_MT_REMOVE) {
+        if (seg->removed() && isLocal(seg->removes[0])) {
+          o.pos1 = pos;
+          o.pos2 = pos + seg->len();
+          emit = true;
+        }
+      } else {
+        throw DataError("Invalid op type");
+      }
+      if (!emit) continue;
+      groupPool_.push_back(std::make_unique<SegmentGroup>());
+      SegmentGroup* ng = groupPool_.back().get();
+      ng->localSeq = g->localSeq;
+      ng->refSeq = currentSeq;
+      ng->hasPrevious = g->hasPrevious;
+      ng->previousProps = g->previousProps;
+      ng->type = g->type;
+      ng->payload = g->payload;
+      ng->pos2 = g->pos2;
+      ng->flags = g->flags;
+      seg->groups.push_back(ng);
+      ng->segments.push_back(seg);
+      pendingSegments_.push_back(ng);
+      out->push_back(o);
+    }
+  }
 }
 
 void MergeTree::loadSnapshot(const std::vector<LoadedSeg>& header, const std::vector<LoadedSeg>& body,
@@ -1072,7 +1489,7 @@ void MergeTree::scourNode(Block* node, std::vector<Node*>& hold) {
   const Perspective lp = localPerspective();
   for (int k = 0; k < node->childCount; k++) {
     Node* child = node->children[k];
-    if (!child->isLeaf) {
+    if (!child->isLeaf || !static_cast<Seg*>(child)->groups.empty()) {  // pending local ops hold a leaf (zamboni.ts:148)
       hold.push_back(child);
       prev = nullptr;
       continue;

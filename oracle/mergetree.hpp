@@ -42,31 +42,48 @@ constexpr int kZamboniMax = 2;         // zamboni.ts:25
 struct DataError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// A local op whose range is invalid in the local view (client.ts:797-810 "RangeOutOfBounds",
+// thrown with usageError: true): FMT_E_USAGE.
+struct UsageError : DataError {
+  using DataError::DataError;
+};
 
 // A remove stamp's kind (stamps.ts RemoveOperationStamp.type): 0 = "setRemove" (markRangeRemoved),
 // 1 = "sliceRemove" (obliterate, incl. obliterate-on-insert). Insert stamps leave it 0.
+// localSeq (stamps.ts:47): defined (> 0) iff the stamp is a local op pending its ack (seq -1).
 struct Stamp {
   int seq;
   int client;
   int kind = 0;
+  int localSeq = 0;
 };
 
-// stamps.ts:101-113 (the oracle never holds two unassigned stamps, so localSeq never decides).
+// stamps.ts:87-121 (lessThan / greaterThan / lte): acked before unacked; unacked by localSeq.
 inline bool stampGreater(const Stamp& a, const Stamp& b) {
-  if (a.seq == kUnassignedSeq) return b.seq != kUnassignedSeq;
+  if (a.seq == kUnassignedSeq) return b.seq != kUnassignedSeq || a.localSeq > b.localSeq;
   if (b.seq == kUnassignedSeq) return false;
   return a.seq > b.seq;
 }
+inline bool stampLess(const Stamp& a, const Stamp& b) {
+  if (a.seq == kUnassignedSeq) return b.seq == kUnassignedSeq && a.localSeq < b.localSeq;
+  if (b.seq == kUnassignedSeq) return true;
+  return a.seq < b.seq;
+}
 inline bool stampLte(const Stamp& a, const Stamp& b) { return !stampGreater(a, b); }
+inline bool isLocal(const Stamp& a) { return a.seq == kUnassignedSeq; }  // stamps.ts:125-127
 
-// perspective.ts:80-93 (PriorPerspective) and :174-184 (LocalDefaultPerspective).
+// perspective.ts:80-93 (PriorPerspective), :103-118 (LocalReconnectingPerspective) and :174-184
+// (LocalDefaultPerspective). mergeTreeNodes.ts:325-327 seqLTE excludes UnassignedSequenceNumber.
 struct Perspective {
   bool everything;  // LocalDefaultPerspective: every op has occurred
   int refSeq;
   int client;
+  int localSeq = 0;  // > 0: LocalReconnectingPerspective(refSeq, client, localSeq)
   bool hasOccurred(const Stamp& s) const {
     if (everything) return true;
-    return (s.seq != kUnassignedSeq && s.seq <= refSeq) || s.client == client;
+    const bool viaRefSeq = s.seq != kUnassignedSeq && s.seq <= refSeq;
+    if (localSeq > 0) return viaRefSeq || (s.localSeq > 0 && s.localSeq <= localSeq);
+    return viaRefSeq || s.client == client;
   }
 };
 
@@ -91,6 +108,7 @@ struct PropPending {
   uint16_t key;
   uint16_t msnConsensus;
   std::vector<PropChangeRec> remote;
+  std::vector<PropChangeRec> local;  // the local client's unacked changes (segmentPropertiesManager.ts:209-211)
 };
 struct PropManager {
   std::vector<PropPending> changes;
@@ -105,6 +123,23 @@ struct Node {
 };
 
 struct LRef;
+struct Seg;
+// mergeTreeNodes.ts:234-240 SegmentGroup: the segments one local op touched, pending its ack. `type`
+// and `payload` are the op's (FMT_MT_* and its props-op id / insert props-op id + 1, what ackOp and
+// regeneratePendingOp read from the op they are handed); previousProps (annotate: the keys' values
+// before the op, null = 0) parallel to segments.
+struct SegmentGroup {
+  std::vector<Seg*> segments;
+  bool hasPrevious = false;
+  std::vector<std::vector<std::pair<uint16_t, uint16_t>>> previousProps;
+  int localSeq = 0;
+  int refSeq = 0;
+  uint32_t type = 0;
+  int32_t payload = 0;
+  int32_t pos2 = 0;      // (insert: props-op id + 1 of the original op's seg props)
+  uint32_t flags = 0;    // (insert: FMT_MT_F_MARKER)
+};
+
 struct Seg : Node {
   Seg() : Node(true) {}
   std::u16string text;  // a Marker's one unit is its refType
@@ -114,6 +149,7 @@ struct Seg : Node {
   PropMap props;
   std::unique_ptr<PropManager> pm;  // segment.propertyManager (created by the first annotate)
   std::vector<LRef*> refs;     // local references on this segment (localReference.ts)
+  std::vector<SegmentGroup*> groups;  // segmentGroups (segmentGroupCollection.ts): pending local ops
   int len() const { return static_cast<int>(text.size()); }
   bool removed() const { return !removes.empty(); }
 };
@@ -224,6 +260,30 @@ class MergeTree {
   // client.ts:1381-1391 updateSeqNumbers, after the last member of a message.
   void updateSeqNumbers(int min, int seq);
 
+  // --- f4: the local client (a Client whose own ops apply before they are
+  // sequenced). Its short id is clientId (startCollaboration); every other client is remote. ---
+  int localSeq = 0;  // collabWindow.localSeq (mergeTreeNodes.ts:685-695 mintNextLocalOperationStamp)
+  // insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:273-355): the op's positions
+  // are in the local view (LocalDefaultPerspective), its stamp {UnassignedSequenceNumber, clientId,
+  // ++localSeq}, its segments a new pending SegmentGroup (mergeTree.ts:1410-1447).
+  void applyLocal(const fmt_mt_op& op, const uint16_t* arena, const uint32_t* propsOff, const uint32_t* propsKv);
+  // The local client's own op came back sequenced (client.ts:1367-1368 ackPendingSegment →
+  // mergeTree.ts:1325-1408 ackOp): the oldest pending group takes the stamp {seq, clientId}.
+  void ackOp(const fmt_mt_op& op, const uint32_t* propsOff, const uint32_t* propsKv);
+  // client.ts:554 → mergeTree.ts:2388-2514: undo the newest pending op.
+  void rollback(const fmt_mt_op& op);
+  // Reconnect (client.ts:1452-1542 regeneratePendingOp, called for every pending op in order): the
+  // segments are normalized once (mergeTree.ts:2602-2818), then every pending group becomes one new
+  // op per segment (resetPendingDeltaToOps, client.ts:1160-1289) at positions from
+  // LocalReconnectingPerspective(currentSeq, clientId, group localSeq). The new ops are appended to
+  // *out (fmt_mt_op records: seq = localSeq, ref_seq = currentSeq, insert text appended to *text
+  // with payload = its offset there); squash is false (IDeltaHandler.reSubmit's default path).
+  void regeneratePending(std::vector<fmt_mt_op>* out, std::u16string* text);
+  size_t pendingGroups() const { return pendingSegments_.size(); }
+  // REGEN events applied without an explicit output (orc_mt_apply_ops) collect their ops here
+  std::vector<fmt_mt_op> regenOps;
+  std::u16string regenText;
+
   // Maintain the per-block remote length index (BlockIdx) instead of summing leaf lengths over the
   // subtree on every query: O(log window + the querying client's window leaves) per block, which
   // makes a 10M-segment document (BASELINE config 5, T3) replayable. Results are identical; only
@@ -286,6 +346,19 @@ class MergeTree {
   static void assignChild(Block* parent, Node* child, int index);
 
   Perspective localPerspective() const { return {true, 0x7fffffff, clientId}; }
+  // f4 internals
+  std::vector<std::unique_ptr<SegmentGroup>> groupPool_;
+  std::vector<SegmentGroup*> pendingSegments_;  // mergeTree.ts:657 pendingSegments (front = oldest)
+  bool lastNormSet_ = false;                    // client.ts:1414 lastNormalization
+  int lastNormRefSeq_ = 0, lastNormLocalSeq_ = 0;
+  SegmentGroup* addToPendingList(Seg* seg, SegmentGroup* group, int localSeqArg,
+                                 const std::vector<std::pair<uint16_t, uint16_t>>* previousProps = nullptr);
+  int findRollbackPosition(const Seg* seg) const;  // mergeTree.ts:2519-2536
+  void normalizeSegmentsOnRebase();                // mergeTree.ts:2734-2766
+  void normalizeAdjacentSegments(std::vector<Seg*>& range);  // mergeTree.ts:2613-2712
+  // segmentPropertiesManager.ts:140-173 rollbackProperties (collaborating)
+  void rollbackProperties(Seg* s, const std::vector<std::pair<uint16_t, uint16_t>>& props);
+  static bool isRemovedAndAcked(const Seg* s) { return s->removed() && !isLocal(s->removes[0]); }
   bool minSeqHasOccurred(const Stamp& s) const {
     return (s.seq != kUnassignedSeq && s.seq <= minSeq) || s.client == kNonCollabClient;
   }
@@ -294,8 +367,10 @@ class MergeTree {
   int localBlockLength(const Block* b) const;                    // blockUpdate cachedLength
   int remoteBlockLength(const Block* b, const Perspective& p) const;  // const_cast inside when indexed
   int nodeLength(const Node* n, const Perspective& p) const;     // mergeTree.ts:1116-1145
+  // mergeTree.ts:1123-1135: a local perspective that sees every local edit reads the cached lengths
   bool isLocalPerspective(const Perspective& p) const {
-    return !collaborating || clientId == p.client;
+    return (!collaborating || clientId == p.client) &&
+           (p.localSeq == 0 || (p.localSeq == localSeq && p.refSeq >= currentSeq));
   }
 
   void insertingWalk(int pos, const Perspective& p, Stamp stamp, InsertCtx& ctx);
@@ -349,7 +424,7 @@ class MergeTree {
   double numberOfValue(uint16_t id) const;
   uint16_t valueOfNumber(double x);
   void annotateRange(int start, int end, const std::vector<PropChange>& props,
-                     const Perspective& p, Stamp stamp);
+                     const Perspective& p, Stamp stamp, bool rollbackOp = false);
   void addToLRUSet(Seg* leaf, int seq);
   void setMinSeq(int min);
 

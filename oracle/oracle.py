@@ -58,6 +58,10 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int, P]
         L.orc_xsadd_uint32.argtypes = [P, ctypes.c_int, P, ctypes.c_int]
         L.orc_xsadd_mixed.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int]
+        L.orc_mt_local_length.argtypes = [P]
+        L.orc_mt_pending_groups.argtypes = [P]
+        L.orc_mt_regen_take.argtypes = [P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P]
+        L.orc_mt_replay_regen.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P]
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -112,6 +116,23 @@ class MergeTreeDoc:
         self._check(lib().orc_mt_apply_ops(self.h, _ptr(ops), len(ops), _ptr(arena), _ptr(props_off),
                                            _ptr(props_kv)))
 
+    def local_length(self) -> int:
+        """getLength() from the local perspective (client.ts:1696)."""
+        return int(lib().orc_mt_local_length(self.h))
+
+    def pending_groups(self) -> int:
+        return int(lib().orc_mt_pending_groups(self.h))
+
+    def regen_take(self):
+        """The ops REGEN events produced since the last call: (MT_OP_DTYPE records, their text)."""
+        from fluidframework_amd.streams import MT_OP_DTYPE
+        n, nt = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        lib().orc_mt_regen_take(self.h, None, 0, None, 0, ctypes.byref(n), ctypes.byref(nt))
+        ops = np.zeros(max(1, n.value), dtype=MT_OP_DTYPE)
+        text = np.zeros(max(1, nt.value), dtype="<u2")
+        lib().orc_mt_regen_take(self.h, _ptr(ops), n.value, _ptr(text), nt.value, ctypes.byref(n), ctypes.byref(nt))
+        return ops[: n.value], text[: nt.value]
+
     def text(self) -> str:
         n = lib().orc_mt_text(self.h, None, 0)
         buf = np.zeros(max(n, 1), dtype="<u2")
@@ -142,6 +163,22 @@ class MergeTreeDoc:
         header = raw[: hl.value].decode("utf-8")
         body = raw[hl.value : hl.value + bl.value].decode("utf-8") if bl.value else None
         return header, body
+
+
+def mt_replay_regen(batch, doc: int):
+    """f4: document `doc` replayed; (status, regenerated ops (MT_OP_DTYPE), their text) — the layout of
+    fmt_mt_fetch_regen."""
+    from fluidframework_amd.native import batch_struct
+    from fluidframework_amd.streams import MT_OP_DTYPE
+    b, keep = batch_struct(batch)
+    n, nt = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    lib().orc_mt_replay_regen(ctypes.byref(b), doc, None, 0, None, 0, ctypes.byref(n), ctypes.byref(nt))
+    ops = np.zeros(max(1, n.value), dtype=MT_OP_DTYPE)
+    text = np.zeros(max(1, nt.value), dtype="<u2")
+    rc = lib().orc_mt_replay_regen(ctypes.byref(b), doc, _ptr(ops), n.value, _ptr(text), nt.value,
+                                   ctypes.byref(n), ctypes.byref(nt))
+    del keep
+    return rc, ops[: n.value], text[: nt.value]
 
 
 def mt_replay_batch(batch, doc_begin=0, doc_end=None, threads=1, cap_leaves=4096, cap_chars=1 << 16,

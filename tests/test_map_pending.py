@@ -168,3 +168,38 @@ def test_pending_view_on_gpu_matches_oracle_and_reference_scenarios(orc):
                     _check_assertion(views[d], step)
     finally:
         e.close()
+
+
+@pytest.mark.gpu
+def test_pending_event_cap_per_document(orc):
+    """FMT_MAP_PENDING_MAX_EVENTS: a document with exactly the cap of local events replays (its view
+    equals the oracle's); one past it gets FMT_E_CAPACITY and no entries, its neighbours unaffected."""
+    from fluidframework_amd import native
+    cap = native.MAP_PENDING_MAX_EVENTS
+    b = MapStreamBuilder()
+    for n in (cap, cap + 1, 10):
+        d = b.begin_doc()
+        seq = 0
+        for i in range(n):
+            if i % 2 == 0 or not b._unacked[d]:
+                b.local_submit(d, _plain({"type": "set", "key": f"k{i % 5}", "value": i % 50}))
+            else:
+                seq += 1
+                b.local_ack(d, seq)
+    bt = b.finish()
+    assert list(np.diff(bt.local_offsets)) == [cap, cap + 1, 10]
+    e = native.Engine(0)
+    try:
+        e.map_load_sparse(bt)
+        e.map_run_sparse()
+        counts, status, entries = e.map_pending(bt)
+    finally:
+        e.close()
+    exp = orc.map_pending(bt)
+    assert list(status) == [0, -3, 0]
+    assert counts[1] == 0
+    assert counts[0] == exp[0][0] and counts[2] == exp[0][2]
+    off = np.concatenate([[0], np.cumsum(counts)])
+    eoff = np.concatenate([[0], np.cumsum(exp[0])])
+    for d in (0, 2):
+        assert np.array_equal(entries[off[d]:off[d + 1]], exp[2][eoff[d]:eoff[d + 1]])

@@ -44,7 +44,7 @@ def test_addon_exports(addon):
                     "console.log(JSON.stringify({k:Object.keys(a).sort(),s:a.sizes,c:a.capacity()}))")
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
-    assert out["k"] == sorted(["open", "close", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
+    assert out["k"] == sorted(["open", "close", "openContexts", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
                                "fetchRemoveOrder", "fetchNumbers", "fetchLegacyProps", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
                                "summaryBlobs", "replayMap", "fetchDoc", "sizes"])
     assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
@@ -58,6 +58,28 @@ def test_open_without_gpu_rejects(addon):
                     "try{new f.Engine(0);console.log('opened')}catch(e){console.log(e.code)}")
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "FMT_E_DEVICE"
+
+
+@pytest.mark.gpu
+def test_contexts_open_close_churn_and_cap(addon):
+    """Context lifetime (fmt_napi.cc, no N-API finalizers): 200 open/close cycles leave no context
+    open (the slot table is reused); contexts dropped without close() count against the cap
+    (FMT_NAPI_MAX_CONTEXTS) so device memory cannot grow without bound, close() of a stale handle is
+    a no-op and using it throws; the env cleanup hook closes what is still open and node exits 0."""
+    js = (f"const a=require({json.dumps(addon)});"
+          "for(let i=0;i<200;i++){const c=a.open(0);a.close(c);}"
+          "const n0=a.openContexts();"
+          "let capped='';const held=[];"
+          "try{for(let i=0;i<8;i++) held.push(a.open(0));}catch(e){capped=e.code;}"
+          "const n1=a.openContexts();"
+          "a.close(held[0]);a.close(held[0]);let stale='';"
+          "try{a.deviceInfo(held[0]);}catch(e){stale=e.code;}"
+          "process.stdout.write(JSON.stringify({n0,n1,capped,stale,n2:a.openContexts()}));")
+    env = dict(os.environ, FMT_NAPI_MAX_CONTEXTS="5")
+    r = subprocess.run([NODE, "-e", js], capture_output=True, text=True, timeout=120, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out == {"n0": 0, "n1": 5, "capped": "FMT_E_CAPACITY", "stale": "FMT_E_USAGE", "n2": 4}
 
 
 def _python_pack(stride):
