@@ -7,6 +7,7 @@
 
 namespace fmt_mt {
 struct AdjustTables;  // mt_engine.h
+struct LocalTables;   // mt_engine.h (f4)
 }
 
 namespace fmt_kernels {
@@ -51,6 +52,7 @@ struct MtDeviceBatch {
   uint32_t nRelpos;
   uint32_t markerKey;              // key id of "markerId", FMT_MT_NO_MARKER if none
   const fmt_mt::AdjustTables* adj;  // annotate-adjust tables (device memory), nullptr when none
+  const fmt_mt::LocalTables* loc = nullptr;  // f4 local-client slabs (device memory), nullptr when none
 };
 
 struct MtDeviceOut {
@@ -123,7 +125,7 @@ hipError_t launchMergeTree(const MtDeviceBatch& batch, const MtDeviceOut& out, c
 // Large tier over docList[0..count): out.leaves/chars/props are slabs indexed by list position.
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                 uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
-                                uint32_t* next, bool adjust);
+                                uint32_t* next, bool adjust, bool local = false);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

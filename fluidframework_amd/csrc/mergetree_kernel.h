@@ -51,12 +51,12 @@ constexpr size_t scratchBytes() {
 // A tier over all documents (docList == nullptr) or a list of countDev[0] (when countDev is set:
 // the overflow list a previous launch built on the device) or `count` documents. The large tier
 // writes leaves/chars/props to slab i of the list (headers stay per document).
-template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU, bool Adj = false>
+template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU, bool Adj = false, bool Loc = false>
 __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDeviceBatch batch, MtDeviceOut out,
                                                                       const uint32_t* __restrict__ docList,
                                                                       uint32_t count, const uint32_t* countDev,
                                                                       uint32_t* next) {
-  using Doc = fmt_mt::Doc<Ob, C, Rm, Adj>;
+  using Doc = fmt_mt::Doc<Ob, C, Rm, Adj, Loc>;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // wave-uniform
   FMT_LDS fmt_mt::Scratch<C>* scratch = (FMT_LDS fmt_mt::Scratch<C>*)(lds + wave * scratchBytes<C, Ob>());
@@ -87,6 +87,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     in.nRelpos = batch.relpos ? batch.nRelpos : 0u;
     in.markerKey = batch.markerKey;
     in.adj = batch.adj;
+    in.loc = Loc ? batch.loc : nullptr;
     in.doc = d;
     in.infoAll = batch.snapshotInfo;
     in.stampsAll = batch.snapshotStamps;
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(256) void collectOverflowKernel(fmt_mt_doc_result* 
 #endif
 
 // countDev: the list length lives on the device (an overflow list); `count` then bounds it (grid size).
-template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU, bool Adj = false>
+template <bool Ob, class C, bool Rm, int Waves, int WavesPerEU, bool Adj = false, bool Loc = false>
 static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                              uint32_t count, uint32_t* esc, int numCUs, hipStream_t stream,
                              const uint32_t* countDev = nullptr, uint32_t* next = nullptr) {
@@ -198,12 +199,12 @@ static hipError_t launchTier(const MtDeviceBatch& batch, const MtDeviceOut& out,
   // so none waits behind the residency limit (VGPRs cap the small tier at 2 waves/SIMD).
   int blocksPerCU = 0;
   const hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU, Adj>, 64 * Waves, lds);
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocksPerCU, mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU, Adj, Loc>, 64 * Waves, lds);
   if (e != hipSuccess) return e;
   const uint32_t wanted = (count + Waves - 1) / Waves;
   const uint32_t cap = static_cast<uint32_t>(numCUs * (blocksPerCU > 0 ? blocksPerCU : 1));
   const uint32_t grid = wanted < cap ? (wanted > 0 ? wanted : 1) : cap;
-  hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU, Adj>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
+  hipLaunchKernelGGL((mergeTreeKernel<Ob, C, Rm, Waves, WavesPerEU, Adj, Loc>), dim3(grid), dim3(64 * Waves), lds, stream, batch, out,
                      docList, count, countDev, next);
   if (esc != nullptr) {  // over the documents this launch replayed
     const uint32_t g = (count + 255) / 256;

@@ -10,8 +10,10 @@ int mergeTreeProfileLarge(uint64_t* out, int n, bool reset) { return addTuProfil
 
 hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                 uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
-                                uint32_t* next, bool adjust) {
+                                uint32_t* next, bool adjust, bool local) {
   using G = fmt_mt::LargeTier;
+  if (local)  // f4: the local client's submissions, acks, rollbacks and reconnects (plain ops otherwise)
+    return launchTier<false, G, false, kMtWavesLarge, 1, false, true>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (adjust && removeOrder)
     return launchTier<true, G, true, kMtWavesLarge, 1, true>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (adjust)

@@ -168,10 +168,35 @@ FMT_DEV int32_t fClient(uint32_t w4) { return static_cast<int32_t>(static_cast<i
 FMT_DEV uint32_t mkW4(uint32_t id, int32_t client) { return (id & 0x7FFFFFu) | (static_cast<uint32_t>(client & 0xFF) << 24); }
 
 struct LeafRec {
-  uint32_t w[7];  // W0..W4, and W5, W6 in the large tier
+  uint32_t w[8];  // W0..W4, and W5, W6 in the large tier; W7: the local variant's pending-group count
 };
 
 struct AdjustTables;
+
+// f4: the local client's per-document slabs (device memory), each at its offset table's entry for the
+// document (nDocs + 1 entries, in records): the pending segment groups (4 words: localSeq, type |
+// marker flag << 8, payload, pos2 — the op's, what acks, rollbacks and regeneration read), the group
+// records (2 words: leaf id, group serial; a SegmentGroup's segments in order, a segment's groups in
+// order), PropertiesManager records (4 words, Doc::pm*), the regenerated ops and their text, and a
+// scratch area for segment normalization (leaf records + text of the runs it reorders).
+// f4 (Doc<..., Loc = true>): per-document slabs of the local client's state, each document's at
+// xOffs[doc] .. xOffs[doc + 1] (units: groups of 8 words, records of 2 words, PropertiesManager records of
+// 4 words, ops, UTF-16 units, words).
+struct LocalTables {
+  uint32_t* groups;  // pending SegmentGroups, in queue order (Doc::groupPush)
+  const uint64_t* groupOffs;
+  uint32_t* recs;    // (leaf id, group serial): the segments of each group in the order they joined
+  const uint64_t* recOffs;
+  uint32_t* pm;
+  const uint64_t* pmOffs;
+  fmt_mt_op* regen;
+  const uint64_t* regenOffs;
+  uint16_t* regenText;
+  const uint64_t* regenTextOffs;
+  uint32_t* regenCount;  // per document: regenerated ops, their text units
+  uint32_t* scratch;
+  const uint64_t* scratchOffs;
+};
 
 struct DocInputs {
   const fmt_mt_op* ops;
@@ -198,6 +223,7 @@ struct DocInputs {
   // path keeps no registers across the op loop
   const AdjustTables* adj;
   uint32_t doc;                 // this document's index (its number slab and count)
+  const LocalTables* loc = nullptr;  // f4 slabs (Loc variants only)
 };
 
 struct DocOutputs {
@@ -239,7 +265,9 @@ enum ProfCat {
 // batches without such ops run the Rm = false code, which has none of it.
 // Adj: the variant that folds annotate-adjust entries (batches with adjusts; always with Ob, whose
 // runtime path restarts overflowing documents in the next tier instead of checkpointing them).
-template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false>
+// Loc: the local-client variant (f4, batches with FMT_MT_F_LOCAL / ACK / ROLLBACK / REGEN records):
+// local stamps, pending segment groups, acks, rollbacks and regeneration (large tier only).
+template <bool Ob, class C = SmallTier, bool Rm = false, bool Adj = false, bool Loc = false>
 class Doc {
  public:
   using VR = typename C::VR;
@@ -281,7 +309,11 @@ class Doc {
 #else
   FMT_DEV void stamp(int) {}
 #endif
-  static constexpr int kWords = C::kWords;
+  // Loc (f4): one more leaf word, W[kPendW] = the number of the local client's pending segment groups
+  // holding the leaf (segmentGroupCollection.ts); the prop-set word stays W[kPropW]
+  static constexpr int kWords = C::kWords + (Loc ? 1 : 0);
+  static constexpr int kPropW = C::kWords - 1;
+  static constexpr int kPendW = C::kWords;
   static constexpr int kMaxClient = C::kMaxClient;
   Lane<VR> W[kWords];  // W[f] element r of lane l = field f of leaf 64 r + l
   FMT_LDS Scratch<C>* s;  // (an LDS-space pointer: per-lane LDS addresses stay 32-bit)
@@ -320,8 +352,8 @@ class Doc {
   // in its HBM checkpoint: the scalars, the leaf words of the compact rows and the LDS scratch (same
   // layout in both tiers). The small tier resumes it from that op instead of replaying it from its
   // first op.
-  static constexpr bool kSavesCkpt = !C::kHbmChars && C::kRows < SmallTier::kRows && !Rm;
-  static constexpr bool kResumesCkpt = !C::kHbmChars && C::kRows == SmallTier::kRows && !Rm;
+  static constexpr bool kSavesCkpt = !C::kHbmChars && C::kRows < SmallTier::kRows && !Rm && !Loc;
+  static constexpr bool kResumesCkpt = !C::kHbmChars && C::kRows == SmallTier::kRows && !Rm && !Loc;
   // layout: 16 head words | leaf words of the compact rows | the compact tier's chars | the rest of
   // the scratch (blk .. tmp: the same fields in both tiers; only the chars array differs in size) |
   // the live obliterates (ob .. obStart; Ob only, head words 13..15 hold their counts and bitmap)
@@ -347,8 +379,8 @@ class Doc {
   // (W0 packing and 8-bit block ids of the small tier, text into the HBM slab).
   // (Ob: the live-obliterate table goes to the end of the document's compact checkpoint slot, free
   // once the small tier has resumed from it; head words 13..15 of the slab hold its counts and bitmap)
-  static constexpr bool kSavesBig = !C::kHbmChars && C::kRows == SmallTier::kRows && !Rm;
-  static constexpr bool kResumesBig = C::kHbmChars && !Rm;
+  static constexpr bool kSavesBig = !C::kHbmChars && C::kRows == SmallTier::kRows && !Rm && !Loc;
+  static constexpr bool kResumesBig = C::kHbmChars && !Rm && !Loc;
   static constexpr int kCkptObOff = kCkptWords - kCkptObWords;
   static constexpr int kBigRows = SmallTier::kRows;
   static constexpr int kBigRestWords =
@@ -445,9 +477,9 @@ class Doc {
         LANE(W[2])[r] = w[2];
         LANE(W[3])[r] = w[3];
         LANE(W[4])[r] = w[4];
-        if constexpr (kWords > 5) {
+        if constexpr (C::kWords > 5) {
           LANE(W[5])[r] = 0u;
-          LANE(W[kWords - 1])[r] = live ? (sp == kSmallNoProps ? kPropsUndef : sp) : 0u;
+          LANE(W[kPropW])[r] = live ? (sp == kSmallNoProps ? kPropsUndef : sp) : 0u;
         }
       }
     }
@@ -610,16 +642,16 @@ class Doc {
 
   // Prop-set id of leaf j / of leaf 64 r + l inside a FOR_LANES body, and setting it.
   FMT_DEV uint32_t propsAt(int j) const {
-    if constexpr (kPW) return readField(j, kWords - 1);
+    if constexpr (kPW) return readField(j, kPropW);
     else return fProps(readField(j, 0));
   }
   FMT_DEV uint32_t propsL(int l, int r) const {
-    if constexpr (kPW) return LANE(W[kWords - 1])[r];
+    if constexpr (kPW) return LANE(W[kPropW])[r];
     else return fProps(LANE(W[0])[r]);
   }
   FMT_DEV void setPropsL(int l, int r, uint32_t p) {
     if constexpr (kPW) {
-      LANE(W[kWords - 1])[r] = p;
+      LANE(W[kPropW])[r] = p;
     } else {
       const uint32_t w0 = LANE(W[0])[r];
       LANE(W[0])[r] = mkW0(fLen(w0), fBlk(w0), p);
@@ -741,7 +773,7 @@ class Doc {
   // ids 32..63 in the large tier).
   FMT_DEV bool removedBy(int l, int r, int client) const {
     if (client < 0) return false;  // NonCollabClient / LocalClientId never hold a remove stamp here
-    if constexpr (kWords > 5) {
+    if constexpr (C::kWords > 5) {
       if (client >= 32) return ((LANE(W[5])[r] >> (client - 32)) & 1u) != 0;
     }
     return ((LANE(W[3])[r] >> client) & 1u) != 0;
@@ -1166,8 +1198,16 @@ class Doc {
   // pending (:213-221); updateMsn(msn) (:275-291) folds the changes at or below msn and drops a key
   // left with none. Record words: leaf id (0: deleted), key | kind << 16, seq, value.
   int pmN = 0;  // records in use (deleted ones included)
-  FMT_DEV uint32_t* pmBase() const { return in.adj->pm + 4 * in.adj->pmOffsets[in.doc]; }
-  FMT_DEV int pmCap() const { return static_cast<int>(in.adj->pmOffsets[in.doc + 1] - in.adj->pmOffsets[in.doc]); }
+  // (Loc: the local client's managers, in its own slab: heads {leaf, key, 0, msnConsensus} and local
+  // changes {leaf, key | 0x20000, group serial, value}, segmentPropertiesManager.ts:48-52 `local`)
+  FMT_DEV uint32_t* pmBase() const {
+    if constexpr (Loc) return in.loc->pm + 4 * in.loc->pmOffs[in.doc];
+    else return in.adj->pm + 4 * in.adj->pmOffsets[in.doc];
+  }
+  FMT_DEV int pmCap() const {
+    if constexpr (Loc) return static_cast<int>(in.loc->pmOffs[in.doc + 1] - in.loc->pmOffs[in.doc]);
+    else return static_cast<int>(in.adj->pmOffsets[in.doc + 1] - in.adj->pmOffsets[in.doc]);
+  }
   FMT_DEV uint32_t pmWord(int i, int w) const { return uni(loadCoherent(pmBase() + 4 * i + w)); }
 
   // First record at or after `from` whose (leaf id, key | kind) match (~0u: any key / kind), or -1.
@@ -1597,8 +1637,13 @@ class Doc {
     rec.w[2] = readField(j, 2);
     rec.w[3] = readField(j, 3);
     rec.w[4] = mkW4(nextId++, fClient(w4));
-    rec.w[5] = kWords > 5 ? readField(j, 5) : 0u;
-    rec.w[6] = kPW ? readField(j, kWords - 1) : 0u;
+    rec.w[5] = C::kWords > 5 ? readField(j, 5) : 0u;
+    rec.w[6] = kPW ? readField(j, kPropW) : 0u;
+    rec.w[7] = 0u;
+    if constexpr (Loc) {  // SegmentGroupCollection.copyTo (splitLeafSegment, mergeTree.ts:1779-1782)
+      rec.w[kPendW] = readField(j, kPendW);
+      if (rec.w[kPendW] != 0u) recCopy(fId(w4), fId(rec.w[4]));
+    }
     if constexpr (Ob) {  // LocalReferenceCollection.split (localReference.ts:464-483)
       if (obUsed != 0) obRefsMove(fId(w4), fId(rec.w[4]), offset, -offset);
     }
@@ -1615,7 +1660,7 @@ class Doc {
         rmPendN++;
       }
     }
-    if constexpr (Adj) {  // copyPropertiesAndManager (mergeTree.ts:1784)
+    if constexpr (Adj || Loc) {  // copyPropertiesAndManager (mergeTree.ts:1784)
       if (pmN > 0) pmCopy(fId(w4), fId(rec.w[4]));
     }
     writeField(j, 0, mkW0(static_cast<uint32_t>(offset), fBlk(w0), fProps(w0)));
@@ -1682,7 +1727,9 @@ class Doc {
   // first leaf whose view prefix equals pos, leaves removed at/below minSeq skipped except the very
   // last leaf (mergeTree.ts:1862-1875); past the end it is appended to the last leaf's block.
   // Returns the new leaf's index, or -1 (nothing inserted, or failure).
-  FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0, int clientArg = 0x7fff, bool boundary = true) {
+  // (localOp, Loc: the local client's submission — local perspective, local stamp, no LRU entry)
+  FMT_DEV int insertText(const fmt_mt_op& op, const Lane<uint32_t>& text0, int clientArg = 0x7fff, bool boundary = true,
+                         bool localOp = false) {
     const int refSeq = op.ref_seq, client = clientArg != 0x7fff ? clientArg : op.client, seq = op.seq;
     const int pos = op.pos1, len = static_cast<int>(opLen(op));
     const int nr = rows();
@@ -1717,7 +1764,10 @@ class Doc {
           const int idx = r * 64 + l;
           const bool undefinedLen = static_cast<int32_t>(LANE(W[2])[r]) <= minSeq;
           const bool skipped = undefinedLen && idx != n - 1;
-          LANE(p) = idx < n && !skipped && static_cast<int>(LANE(st)[r]) == pos;
+          // breakTie (mergeTree.ts:1811-1826) of a remote insert against a leaf the local client
+          // inserted and has not had acked: the remote stamp is older, so the walk passes it
+          const bool tie = !Loc || localOp || LANE(vis)[r] > 0u || static_cast<int32_t>(LANE(W[1])[r]) < FMT_MT_LOCAL_SEQ_BASE;
+          LANE(p) = idx < n && !skipped && tie && static_cast<int>(LANE(st)[r]) == pos;
         }
         const uint64_t m = ballot(p);
         if (m != 0) insIdx = r * 64 + ctz64(m);
@@ -1759,6 +1809,7 @@ class Doc {
     rec.w[4] = mkW4(nextId++, client) | ((op.flags & FMT_MT_F_MARKER) != 0 ? kW4Marker : 0u);  // Marker.make
     rec.w[5] = 0;
     rec.w[6] = insProps;
+    rec.w[7] = 0;
     if (uni(static_cast<int>(s->blk[blk].count)) == 0) {
       s->blk[blk].leaf = 1;  // an empty root becomes a leaf block
       waveSync();
@@ -1771,7 +1822,7 @@ class Doc {
     if constexpr (Ob) {
       if (obStartN > 0) obliterateOnInsert(insIdx, refSeq, client, Rm && (op.flags & FMT_MT_F_RMORDER) != 0);
     }
-    lruForLeaf(insIdx, static_cast<int>(fBlk(readField(insIdx, 0))), seq);
+    if (!localOp) lruForLeaf(insIdx, static_cast<int>(fBlk(readField(insIdx, 0))), seq);
     stamp(kPfLru);
     return status == FMT_OK ? insIdx : -1;
   }
@@ -1939,7 +1990,7 @@ class Doc {
     if (any && newestClient != client) {
       writeField(k, 2, static_cast<uint32_t>(minSeqOther));
       writeField(k, 3, static_cast<uint32_t>(mask));
-      if constexpr (kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
+      if constexpr (C::kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
       // SnapshotV1: the leaf's stamps are overlappingAcked sorted by seq (:1715-1725); the first is
       // rm_seq, every other one is a remove-order entry (the host sorts a leaf's entries by seq)
       if constexpr (Rm) {
@@ -2077,7 +2128,7 @@ class Doc {
     if (inf.rm_count) {
       writeField(k, 2, static_cast<uint32_t>(rm));
       writeField(k, 3, static_cast<uint32_t>(mask));
-      if constexpr (kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
+      if constexpr (C::kWords > 5) writeField(k, 5, static_cast<uint32_t>(mask >> 32));
     }
   }
 
@@ -2100,7 +2151,8 @@ class Doc {
 
   // Remove / annotate (after their boundary splits); fills `delta` for catch-up ops. Returns true
   // when a catch-up recording should follow.
-  FMT_DEV bool applyRange(const fmt_mt_op& op, Lane<uint32_t>& delta) {
+  // (localOp, Loc: the local client's submission, its segments joining pending group `group`)
+  FMT_DEV bool applyRange(const fmt_mt_op& op, Lane<uint32_t>& delta, bool localOp = false, uint32_t group = 0) {
     const int refSeq = op.ref_seq, client = op.client, seq = op.seq;
     const bool catchup = (op.flags & FMT_MT_F_CATCHUP) != 0;
     bool obliterate = false;
@@ -2209,7 +2261,7 @@ class Doc {
             const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);
             if (rm == kNotRemoved) LANE(delta) |= 1u << r;
             LANE(W[2])[r] = static_cast<uint32_t>(rm < seq ? rm : seq);
-            if (kWords > 5 && client >= 32) LANE(W[kWords > 5 ? 5 : 3])[r] |= 1u << (client - 32);
+            if (C::kWords > 5 && client >= 32) LANE(W[C::kWords > 5 ? 5 : 3])[r] |= 1u << (client - 32);
             else LANE(W[3])[r] |= 1u << client;
           }
         }
@@ -2228,6 +2280,40 @@ class Doc {
         if (status != FMT_OK) return false;
       }
       Lane<uint32_t> todo = hits;
+      if constexpr (Loc) {
+        if (localOp) {  // each hit leaf's manager records the local change (segmentPropertiesManager.ts:209-211)
+          for (Lane<uint32_t> t = hits;;) {
+            const int j = firstSet(t, nr);
+            if (j < 0 || status != FMT_OK) break;
+            FOR_LANES(l) {
+              if (l == (j & 63)) LANE(t) &= ~(1u << (j >> 6));
+            }
+            locPmLocal(j, op.payload, group);
+          }
+          if (status != FMT_OK) return false;
+        } else if (pmN > 0) {  // leaves whose managers hold local changes keep those keys' local values
+          for (Lane<uint32_t> t = hits;;) {
+            const int j = firstSet(t, nr);
+            if (j < 0 || status != FMT_OK) break;
+            FOR_LANES(l) {
+              if (l == (j & 63)) LANE(t) &= ~(1u << (j >> 6));
+            }
+            if (pmFind(fId(readField(j, 4)), 0u, 0x30000u) < 0) continue;  // (no head: the shared path)
+            const uint32_t nw = locRemoteAnnotate(j, op.payload);
+            if (status != FMT_OK) return false;
+            const int rj = j >> 6, lane = j & 63;
+            FOR_ROWS(r, rj, rj + 1) {
+              FOR_LANES(l) {
+                if (l == lane) {
+                  setPropsL(l, r, nw);
+                  LANE(todo) &= ~(1u << r);
+                }
+              }
+            }
+          }
+          if (status != FMT_OK) return false;
+        }
+      }
       for (;;) {
         const int j = firstSet(todo, nr);
         if (j < 0) break;
@@ -2252,9 +2338,768 @@ class Doc {
       }
     }
     stamp(kPfRange);
+    if constexpr (Loc) {
+      if (localOp) {  // addToPendingList for every hit leaf, in nodeMap order (mergeTree.ts:2048-2055, 2336-2341)
+        for (Lane<uint32_t> t = hits; status == FMT_OK;) {
+          const int j = firstSet(t, nr);
+          if (j < 0) break;
+          FOR_LANES(l) {
+            if (l == (j & 63)) LANE(t) &= ~(1u << (j >> 6));
+          }
+          pendAdd(j, 1);
+          recAppend(fId(readField(j, 4)), group);
+        }
+        return false;
+      }
+    }
     lruForHits(hits, seq, nr);
     stamp(kPfLru);
     return catchup && status == FMT_OK;
+  }
+
+
+  // ------------------------------------------------------------------ f4: the local client (Loc)
+  // The document is replayed from the perspective of its own client, short id 0. Its submissions are
+  // stamped {UnassignedSequenceNumber, 0, localSeq}: W1 / W2 hold FMT_MT_LOCAL_SEQ_BASE | localSeq,
+  // above every sequence number, so PriorPerspective(refSeq, c) of any remote client sees neither
+  // a pending insert nor a pending remove (perspective.ts:80-93), LocalReconnectingPerspective(seq,
+  // 0, k) is visLengths(LOCAL_SEQ_BASE | k, none) (perspective.ts:103-118), and the local view is
+  // visLengths(kLocalView, 0). A pending op's segments are a SegmentGroup (mergeTree.ts:1410-1447):
+  // a queue entry in the group slab plus one record per segment in the record slab, in the order the
+  // segments joined (splits append the right part, segmentGroupCollection.ts:25-59); W[kPendW]
+  // counts the groups holding a leaf, which zamboni must not touch (zamboni.ts:148).
+  static constexpr int32_t kLocalView = 0x7FFFFFFE;  // every stamp has occurred
+  static constexpr int kGW = 8;                        // words per pending group (LocalTables::groups)
+  uint32_t locSeq = 0;        // collabWindow.localSeq
+  int gHead = 0, gTail = 0;   // the pending queue: group serials [gHead, gTail) of the group slab
+  int recN = 0;               // group records in use (deleted ones included)
+  bool recFrozen = false;     // (regeneration iterates records by index: no compaction meanwhile)
+  uint32_t regenN = 0, regenTextN = 0;
+  bool normSet = false;       // client.ts:1414 lastNormalization
+  int normRef = 0;
+  uint32_t normLocal = 0;
+
+  FMT_DEV static bool isLocalSeq(uint32_t w) { return static_cast<int32_t>(w) >= FMT_MT_LOCAL_SEQ_BASE && static_cast<int32_t>(w) != kNotRemoved; }
+  FMT_DEV uint32_t* gBase() const { return in.loc->groups + kGW * in.loc->groupOffs[in.doc]; }
+  FMT_DEV int gCap() const { return static_cast<int>(in.loc->groupOffs[in.doc + 1] - in.loc->groupOffs[in.doc]); }
+  FMT_DEV uint32_t gWord(int g, int w) const { return uni(loadCoherent(gBase() + kGW * g + w)); }
+  FMT_DEV uint32_t* rBase() const { return in.loc->recs + 2 * in.loc->recOffs[in.doc]; }
+  FMT_DEV int rCap() const { return static_cast<int>(in.loc->recOffs[in.doc + 1] - in.loc->recOffs[in.doc]); }
+  FMT_DEV uint32_t rWord(int i, int w) const { return uni(loadCoherent(rBase() + 2 * i + w)); }
+  FMT_DEV void rSet(int i, int w, uint32_t v) {
+    uint32_t* R = rBase() + 2 * i + w;
+    FOR_LANES(l) {
+      if (l == 0) storeGlobal(R, v);
+    }
+  }
+
+  // Drops deleted group records (leaf id 0), keeping the order.
+  FMT_DEV void recCompact() {
+    uint32_t* R = rBase();
+    int out = 0;
+    for (int base = 0; base < recN; base += 64) {
+      Lane<uint32_t> w0, w1;
+      Lane<bool> live;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(w0) = i < recN ? loadCoherent(R + 2 * i) : 0u;
+        LANE(w1) = i < recN ? loadCoherent(R + 2 * i + 1) : 0u;
+        LANE(live) = LANE(w0) != 0u;
+      }
+      const uint64_t m = ballot(live);
+      waveSync();
+      FOR_LANES(l) {
+        if (LANE(live)) {
+          const int at = out + __builtin_popcountll(m & ((1ull << l) - 1ull));
+          storeGlobal(R + 2 * at, LANE(w0));
+          storeGlobal(R + 2 * at + 1, LANE(w1));
+        }
+      }
+      waveSync();
+      out += __builtin_popcountll(m);
+    }
+    recN = out;
+  }
+
+  FMT_DEV bool recAppend(uint32_t leaf, uint32_t g) {
+    if (recN >= rCap() && !recFrozen) recCompact();
+    if (recN >= rCap()) return fail(FMT_E_CAPACITY);
+    uint32_t* R = rBase() + 2 * recN;
+    FOR_LANES(l) {
+      if (l < 2) storeGlobal(R + l, l == 0 ? leaf : g);
+    }
+    waveSync();
+    recN++;
+    return true;
+  }
+
+  // First live record at or after `from` of group g (leaf == 0: any leaf), or -1.
+  FMT_DEV int recFind(uint32_t g, int from, uint32_t leaf = 0u) const {
+    const uint32_t* R = rBase();
+    for (int base = from; base < recN; base += 64) {
+      Lane<bool> p;
+      FOR_LANES(l) {
+        const int i = base + l;
+        const uint32_t lf = i < recN ? loadCoherent(R + 2 * i) : 0u;
+        LANE(p) = i < recN && lf != 0u && loadCoherent(R + 2 * i + 1) == g && (leaf == 0u || lf == leaf);
+      }
+      const uint64_t m = ballot(p);
+      if (m != 0) return base + ctz64(m);
+    }
+    return -1;
+  }
+
+  // SegmentGroupCollection.copyTo: the split's right part joins every group of the left, in order.
+  FMT_DEV void recCopy(uint32_t from, uint32_t to) {
+    if (!recFrozen) recCompact();  // (records keep their indices while appending)
+    const int end = recN;
+    for (int base = 0; base < end && status == FMT_OK; base += 64) {
+      Lane<bool> p;
+      Lane<uint32_t> g;
+      FOR_LANES(l) {
+        const int i = base + l;
+        LANE(p) = i < end && loadCoherent(rBase() + 2 * i) == from;
+        LANE(g) = i < end ? loadCoherent(rBase() + 2 * i + 1) : 0u;
+      }
+      for (uint64_t m = ballot(p); m != 0 && status == FMT_OK; m &= m - 1) recAppend(to, readlane(g, ctz64(m)));
+    }
+  }
+
+  // A new pending group at the queue's tail; its serial, or -1. Group words: localSeq, type | marker
+  // << 8, payload, pos2, the refSeq its op was submitted at (in flight: sequence.ts:468-499).
+  FMT_DEV int groupPush(uint32_t localSeq, uint32_t typeFlags, uint32_t payload, int32_t pos2, int32_t inflightRef) {
+    if (gTail >= gCap() && gHead > 0 && !recFrozen) groupCompact();
+    if (gTail >= gCap()) {
+      fail(FMT_E_CAPACITY);
+      return -1;
+    }
+    uint32_t* G = gBase() + kGW * gTail;
+    FOR_LANES(l) {
+      if (l < kGW)
+        storeGlobal(G + l, l == 0 ? localSeq : l == 1 ? typeFlags : l == 2 ? payload : l == 3 ? static_cast<uint32_t>(pos2)
+                                                                         : l == 4 ? static_cast<uint32_t>(inflightRef) : 0u);
+    }
+    waveSync();
+    return gTail++;
+  }
+
+  // The queue back to serial 0 (records renumbered).
+  FMT_DEV void groupCompact() {
+    const int cnt = gTail - gHead;
+    uint32_t* G = gBase();
+    for (int base = 0; base < kGW * cnt; base += 64) {
+      Lane<uint32_t> v;
+      FOR_LANES(l) { LANE(v) = base + l < kGW * cnt ? loadCoherent(G + kGW * gHead + base + l) : 0u; }
+      waveSync();
+      FOR_LANES(l) {
+        if (base + l < kGW * cnt) storeGlobal(G + base + l, LANE(v));
+      }
+      waveSync();
+    }
+    uint32_t* R = rBase();
+    for (int base = 0; base < recN; base += 64) {
+      FOR_LANES(l) {
+        const int i = base + l;
+        if (i < recN && loadCoherent(R + 2 * i) != 0u) storeGlobal(R + 2 * i + 1, loadCoherent(R + 2 * i + 1) - static_cast<uint32_t>(gHead));
+      }
+    }
+    waveSync();
+    gTail = cnt;
+    gHead = 0;
+  }
+
+  FMT_DEV void pendAdd(int j, int d) {
+    if constexpr (!Loc) return;
+    const int rj = j >> 6, lane = j & 63;
+    FOR_ROWS(r, rj, rj + 1) {
+      FOR_LANES(l) {
+        if (l == lane) LANE(W[kPendW])[r] = static_cast<uint32_t>(static_cast<int>(LANE(W[kPendW])[r]) + d);
+      }
+    }
+  }
+
+  // getLength() from the local perspective: every leaf not removed.
+  FMT_DEV int localLength() const {
+    const int nr = rows();
+    Lane<uint32_t> acc;
+    FOR_LANES(l) { LANE(acc) = 0u; }
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        if (static_cast<int32_t>(LANE(W[2])[r]) == kNotRemoved) LANE(acc) += fLen(LANE(W[0])[r]);
+      }
+    }
+    uint32_t total;
+    waveExclusiveSum(acc, &total);
+    return static_cast<int>(total);
+  }
+
+  // --- the local client's PropertiesManager records (raw values; adjusts are refused at load)
+  FMT_DEV int locHead(uint32_t leaf, uint32_t key) const { return pmFind(leaf, key, 0x3FFFFu); }
+  FMT_DEV int locLocalFirst(uint32_t leaf, uint32_t key) const { return pmFind(leaf, key | 0x20000u, 0x3FFFFu); }
+  FMT_DEV int locLocalLast(uint32_t leaf, uint32_t key) const {
+    int last = -1;
+    for (int i = locLocalFirst(leaf, key); i >= 0; i = pmFind(leaf, key | 0x20000u, 0x3FFFFu, i + 1)) last = i;
+    return last;
+  }
+  // The leaf's current value of `key` (0: absent) from its prop set.
+  FMT_DEV uint32_t keyValue(uint32_t props, uint32_t key) const {
+    if (props == kPropsUndef) return 0u;
+    const uint32_t cnt = uni(s->props[props].n);
+    uint32_t v = 0u;
+    for (uint32_t k = 0; k < cnt && k < static_cast<uint32_t>(kKeysMax); k++) {
+      const uint32_t e = uni(setKv(static_cast<int>(props), k));
+      if ((e >> 16) == key) v = e & 0xFFFFu;
+    }
+    return v;
+  }
+  // The working set with `key` set to v (0: deleted; a new key goes last); returns the count.
+  FMT_DEV uint32_t workSetKey(uint32_t cnt, uint32_t key, uint32_t v) {
+    uint32_t pos = cnt;
+    for (uint32_t k = 0; k < cnt; k++)
+      if ((uni(s->kvWork[k]) >> 16) == key) pos = k;
+    if (v == 0u) {
+      if (pos < cnt) {
+        for (uint32_t k = pos; k + 1 < cnt; k++) {
+          const uint32_t x = uni(s->kvWork[k + 1]);
+          waveSync();
+          FOR_LANES(l) {
+            if (l == 0) s->kvWork[k] = x;
+          }
+        }
+        cnt--;
+      }
+    } else if (pos < cnt) {
+      FOR_LANES(l) {
+        if (l == 0) s->kvWork[pos] = (key << 16) | v;
+      }
+    } else if (cnt < static_cast<uint32_t>(kKeysMax)) {
+      FOR_LANES(l) {
+        if (l == 0) s->kvWork[cnt] = (key << 16) | v;
+      }
+      cnt++;
+    } else {
+      fail(kCapFinal);
+    }
+    waveSync();
+    return cnt;
+  }
+
+  // handleProperties for a local change (segmentPropertiesManager.ts:199-211): a key's entry starts at
+  // its current value, the change joins its local list. (The visible set follows the op's values,
+  // applied by the caller.)
+  FMT_DEV void locPmLocal(int j, uint32_t opId, uint32_t g) {
+    const uint32_t leaf = fId(readField(j, 4));
+    const uint32_t props = propsAt(j);
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+      const uint32_t e = uni(in.propsKv[t]);
+      const uint32_t key = e >> 16;
+      if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
+        fail(FMT_E_UNSUPPORTED);
+        return;
+      }
+      if (locHead(leaf, key) < 0 && !pmAppend(leaf, key, 0, keyValue(props, key))) return;
+      if (!pmAppend(leaf, key | 0x20000u, static_cast<int>(g), e & 0xFFFFu)) return;
+    }
+  }
+
+  // A remote annotate on a leaf whose manager has local changes (segmentPropertiesManager.ts:213-227):
+  // a key with local changes keeps its local value and folds the remote one into msnConsensus;
+  // the others change as for any leaf. Returns the leaf's new prop set.
+  FMT_DEV uint32_t locRemoteAnnotate(int j, uint32_t opId) {
+    const uint32_t leaf = fId(readField(j, 4));
+    uint32_t cnt = loadWork(propsAt(j));
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+      const uint32_t e = uni(in.propsKv[t]);
+      const uint32_t key = e >> 16;
+      if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
+        fail(FMT_E_UNSUPPORTED);
+        return 0;
+      }
+      const int h = locHead(leaf, key);
+      if (h >= 0) pmSet(h, 3, e & 0xFFFFu);
+      else cnt = workSetKey(cnt, key, e & 0xFFFFu);
+    }
+    return status == FMT_OK ? internWork(cnt) : 0u;
+  }
+
+  // PropertiesManager.ack (segmentPropertiesManager.ts:248-267) + updateMsn: each key's oldest local
+  // change leaves, msnConsensus takes the acknowledged value; a key left without changes loses its entry.
+  FMT_DEV void locPmAck(uint32_t leaf, uint32_t opId) {
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+      const uint32_t e = uni(in.propsKv[t]);
+      const uint32_t key = e >> 16;
+      const int c = locLocalFirst(leaf, key), h = locHead(leaf, key);
+      if (c < 0 || h < 0) {  // "must have local change to ack" (0xa71)
+        fail(FMT_E_DATA);
+        return;
+      }
+      pmSet(c, 0, 0u);
+      pmSet(h, 3, e & 0xFFFFu);
+      waveSync();
+      if (locLocalFirst(leaf, key) < 0) pmSet(h, 0, 0u);
+      waveSync();
+    }
+  }
+
+  // rollbackProperties (segmentPropertiesManager.ts:140-173, collaborating): each key of the op drops
+  // its newest local change and takes the newest one left, else msnConsensus; a key left without
+  // changes loses its entry. Sets the leaf's prop set.
+  FMT_DEV void locPmRollback(int j, uint32_t opId) {
+    const uint32_t leaf = fId(readField(j, 4));
+    uint32_t cnt = loadWork(propsAt(j));  // (`seg.properties ??= {}`: a set even if empty)
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+      const uint32_t key = uni(in.propsKv[t]) >> 16;
+      const int h = locHead(leaf, key);
+      if (h < 0) {  // "Pending changes must exist for rollback when collaborating" (0xa6f)
+        fail(FMT_E_DATA);
+        return;
+      }
+      const int c = locLocalLast(leaf, key);
+      if (c >= 0) pmSet(c, 0, 0u);
+      waveSync();
+      const int c2 = locLocalLast(leaf, key);
+      const uint32_t v = c2 >= 0 ? pmWord(c2, 3) : pmWord(h, 3);
+      if (c2 < 0) pmSet(h, 0, 0u);
+      waveSync();
+      cnt = workSetKey(cnt, key, v);
+    }
+    if (status != FMT_OK) return;
+    const uint32_t id = internWork(cnt);
+    if (status != FMT_OK) return;
+    const int rj = j >> 6, lane = j & 63;
+    FOR_ROWS(r, rj, rj + 1) {
+      FOR_LANES(l) {
+        if (l == lane) setPropsL(l, r, id);
+      }
+    }
+  }
+
+  // insertSegmentLocal / removeRangeLocal / annotateRangeLocal (client.ts:273-355) after
+  // getValidOpRange's local checks (client.ts:769-811: FMT_E_USAGE).
+  FMT_DEV void applyLocal(const fmt_mt_op& op0, const Lane<uint32_t>& text0) {
+    fmt_mt_op op = op0;
+    const int length = localLength();
+    if (op.type == FMT_MT_INSERT) {
+      if (op.pos1 < 0 || op.pos1 > length) {
+        fail(FMT_E_USAGE);
+        return;
+      }
+      if (opLen(op) == 0) return;  // insertSegmentLocal: no segment, no op (client.ts:348-351)
+    } else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
+      if (op.pos1 < 0 || op.pos1 >= length || op.pos2 <= op.pos1) {
+        fail(FMT_E_USAGE);
+        return;
+      }
+    } else {
+      fail(FMT_E_UNSUPPORTED);
+      return;
+    }
+    const uint32_t ls = ++locSeq;  // mintNextLocalOperationStamp (mergeTreeNodes.ts:685-695)
+    const uint32_t marker = (op.flags & FMT_MT_F_MARKER) != 0 ? 1u : 0u;
+    const int g = groupPush(ls, static_cast<uint32_t>(op.type) | (marker << 8), op.payload,
+                            op.type == FMT_MT_INSERT ? op.pos2 : 0, op0.ref_seq);
+    if (g < 0) return;
+    op.ref_seq = kLocalView;
+    op.client = 0;
+    op.seq = static_cast<int32_t>(FMT_MT_LOCAL_SEQ_BASE | ls);
+    if (op.type == FMT_MT_INSERT) {
+      const int k = insertText(op, text0, 0, true, true);
+      if (k < 0 || status != FMT_OK) return;
+      pendAdd(k, 1);
+      recAppend(fId(readField(k, 4)), static_cast<uint32_t>(g));
+    } else {
+      Lane<uint32_t> delta;
+      applyRange(op, delta, true, static_cast<uint32_t>(g));
+    }
+  }
+
+  // ackOp (mergeTree.ts:1325-1408 + ackSegment :149-215): the oldest pending group takes {seq, 0};
+  // each of its segments enters the LRU set in the group's order. (Zamboni follows in replay.)
+  FMT_DEV void ackOp(const fmt_mt_op& op) {
+    if (gHead == gTail || static_cast<int>(gWord(gHead, 1) & 0xFFu) != op.type) {
+      fail(FMT_E_DATA);
+      return;
+    }
+    const uint32_t g = static_cast<uint32_t>(gHead++);
+    for (int i = recFind(g, 0); i >= 0 && status == FMT_OK; i = recFind(g, i + 1)) {
+      const uint32_t leaf = rWord(i, 0);
+      const int j = findLeafById(leaf);
+      if (j < 0) {
+        fail(FMT_E_DATA);
+        return;
+      }
+      rSet(i, 0, 0u);
+      waveSync();
+      if (op.type == FMT_MT_INSERT) {
+        if (!isLocalSeq(readField(j, 1))) {  // "On insert, seq number already assigned!" (0x045)
+          fail(FMT_E_DATA);
+          return;
+        }
+        writeField(j, 1, static_cast<uint32_t>(op.seq));
+      } else if (op.type == FMT_MT_REMOVE) {
+        const uint32_t rm = readField(j, 2);
+        if (isLocalSeq(rm)) writeField(j, 2, static_cast<uint32_t>(op.seq));  // (an earlier acked remove stays first)
+        else if (rm == static_cast<uint32_t>(kNotRemoved)) {
+          fail(FMT_E_DATA);
+          return;
+        }
+      } else {
+        locPmAck(leaf, op.payload);
+      }
+      pendAdd(j, -1);
+      lruForLeaf(j, static_cast<int>(fBlk(readField(j, 0))), op.seq);
+    }
+  }
+
+  // rollback (mergeTree.ts:2388-2514) of the newest pending group.
+  FMT_DEV void rollbackOp(const fmt_mt_op& op) {
+    if (gHead == gTail || static_cast<int>(gWord(gTail - 1, 1) & 0xFFu) != op.type) {  // "Rollback op doesn't match last edit"
+      fail(FMT_E_DATA);
+      return;
+    }
+    const uint32_t g = static_cast<uint32_t>(--gTail);
+    const uint32_t payload = gWord(static_cast<int>(g), 2);
+    for (int i = recFind(g, 0); i >= 0 && status == FMT_OK; i = recFind(g, i + 1)) {
+      const uint32_t leaf = rWord(i, 0);
+      const int j = findLeafById(leaf);
+      if (j < 0) {
+        fail(FMT_E_DATA);
+        return;
+      }
+      rSet(i, 0, 0u);
+      waveSync();
+      pendAdd(j, -1);
+      if (op.type == FMT_MT_REMOVE) {
+        // a peer's concurrent remove keeps the segment removed; otherwise removeRemovalInfo
+        if (isLocalSeq(readField(j, 2))) {
+          writeField(j, 2, static_cast<uint32_t>(kNotRemoved));
+          writeField(j, 3, 0u);
+          if constexpr (C::kWords > 5) writeField(j, 5, 0u);
+        }
+      } else if (op.type == FMT_MT_INSERT) {
+        // insert = {TreeMaintenanceSequenceNumber, NonCollabClient}, then markRangeRemoved over exactly
+        // the segment's span in the local view with that stamp (rollback's position,
+        // findRollbackPosition :2519-2536), then zamboni
+        if (readField(j, 2) != static_cast<uint32_t>(kNotRemoved)) {
+          fail(FMT_E_DATA);
+          return;
+        }
+        writeField(j, 1, static_cast<uint32_t>(-2));
+        writeField(j, 2, static_cast<uint32_t>(-2));
+        const uint32_t w4 = readField(j, 4);
+        writeField(j, 4, mkW4(fId(w4), FMT_NON_COLLAB_CLIENT) | (w4 & kW4Marker));
+        zamboni();
+      } else {
+        // removed: rollbackProperties directly; else annotateRange(rollback) over its span, then zamboni
+        const bool removed = readField(j, 2) != static_cast<uint32_t>(kNotRemoved);
+        locPmRollback(j, payload);
+        if (!removed && status == FMT_OK) zamboni();
+      }
+    }
+  }
+
+  // normalizeSegmentsOnRebase (mergeTree.ts:2734-2766) + normalizeAdjacentSegments (:2613-2712): runs of
+  // adjacent segments that are removed or locally inserted, holding both a local insert and a
+  // segment removed by an acked op, are reordered — acked-removed segments after the last segment the
+  // local client affected, locally removed ones past the local inserts made after their removal —
+  // and the new order takes the run's slots (leaf blocks stay; the text moves with its segments).
+  // Serial over the document's leaves (reconnects are rare), state in the document's scratch slab.
+  FMT_DEV void normalizeOnRebase() {
+    uint32_t* S = in.loc->scratch + in.loc->scratchOffs[in.doc];
+    const uint64_t cap = in.loc->scratchOffs[in.doc + 1] - in.loc->scratchOffs[in.doc];
+    if (cap < 5ull * static_cast<uint64_t>(n) + 16ull) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    // scratch: A[j] = W1, B[j] = W2 of every leaf, a run's list links (nxt, prv) and new order (perm),
+    // then permuteRun's copies
+    // A[j] = W1, B[j] = W2 of every leaf
+    const int nr = rows();
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        if (j < n) {
+          storeGlobal(S + j, LANE(W[1])[r]);
+          storeGlobal(S + n + j, LANE(W[2])[r]);
+        }
+      }
+    }
+    waveSync();
+    uint32_t* nxt = S + 2 * n;  // list links of one run (members 0..m-1)
+    uint32_t* prv = S + 3 * n;
+    const uint32_t kNil = 0xFFFFFFFFu;
+    auto ins = [&](int j) { return uni(loadCoherent(S + j)); };
+    auto rm = [&](int j) { return uni(loadCoherent(S + n + j)); };
+    auto inRun = [&](int j) { return rm(j) != static_cast<uint32_t>(kNotRemoved) || isLocalSeq(ins(j)); };
+    auto ackedRm = [&](int j) { return rm(j) != static_cast<uint32_t>(kNotRemoved) && !isLocalSeq(rm(j)); };
+    auto put = [&](uint32_t* p, uint32_t v) {
+      FOR_LANES(l) {
+        if (l == 0) storeGlobal(p, v);
+      }
+      waveSync();
+    };
+    auto get = [&](const uint32_t* p) { return uni(loadCoherent(p)); };
+    for (int a = 0; a < n && status == FMT_OK;) {
+      if (!inRun(a)) {
+        a++;
+        continue;
+      }
+      int b = a;
+      bool hasLocal = false, hasRemote = false;
+      while (b < n && inRun(b)) {
+        hasLocal = hasLocal || isLocalSeq(ins(b));
+        hasRemote = hasRemote || ackedRm(b);
+        b++;
+      }
+      const int m = b - a;
+      if (hasLocal && hasRemote && m > 1) {
+        for (int k = 0; k < m; k++) {
+          put(nxt + k, k + 1 < m ? static_cast<uint32_t>(k + 1) : kNil);
+          put(prv + k, k > 0 ? static_cast<uint32_t>(k - 1) : kNil);
+        }
+        uint32_t head = 0, tail = static_cast<uint32_t>(m - 1);
+        auto unlink = [&](uint32_t x) {
+          const uint32_t p = get(prv + x), q = get(nxt + x);
+          if (p != kNil) put(nxt + p, q);
+          else head = q;
+          if (q != kNil) put(prv + q, p);
+          else tail = p;
+        };
+        auto insertAfter = [&](uint32_t at, uint32_t x) {
+          const uint32_t q = get(nxt + at);
+          put(nxt + x, q);
+          put(prv + x, at);
+          put(nxt + at, x);
+          if (q != kNil) put(prv + q, x);
+          else tail = x;
+        };
+        uint32_t lastLocal = kNil;
+        for (uint32_t x = tail; x != kNil; x = get(prv + x))
+          if (!ackedRm(a + static_cast<int>(x))) {
+            lastLocal = x;
+            break;
+          }
+        if (lastLocal != kNil) {
+          for (uint32_t slide = lastLocal;;) {
+            const uint32_t nearer = get(prv + slide);
+            const int sj = a + static_cast<int>(slide);
+            if (ackedRm(sj)) {
+              unlink(slide);
+              insertAfter(lastLocal, slide);
+            } else if (rm(sj) != static_cast<uint32_t>(kNotRemoved)) {
+              uint32_t cur = slide;
+              for (uint32_t scan = get(nxt + cur); scan != kNil; scan = get(nxt + scan)) {
+                const int qj = a + static_cast<int>(scan);
+                if (ackedRm(qj) || !isLocalSeq(ins(qj)) || ins(qj) <= rm(sj)) break;
+                cur = scan;
+              }
+              if (cur != slide) {
+                unlink(slide);
+                insertAfter(cur, slide);
+              }
+            }
+            if (nearer == kNil) break;
+            slide = nearer;
+          }
+          // the new order: perm[k] = the member that takes slot a + k
+          uint32_t* perm = S + 4 * n;
+          bool identity = true;
+          int k = 0;
+          for (uint32_t x = head; x != kNil; x = get(nxt + x), k++) {
+            identity = identity && x == static_cast<uint32_t>(k);
+            put(perm + k, x);
+          }
+          if (!identity) permuteRun(a, m, perm, S + 5 * n, cap - 5ull * static_cast<uint64_t>(n));
+        }
+      }
+      a = b;
+    }
+  }
+
+  // The run of leaves [a, a + m) takes the order perm (perm[k]: the member now in slot a + k): leaf
+  // words and text move with their segment, each slot keeps its leaf block (assignChild(parent, seg,
+  // index), mergeTree.ts:2680-2685).
+  FMT_DEV void permuteRun(int a, int m, const uint32_t* perm, uint32_t* area, uint64_t areaCap) {
+    const int b = a + m;
+    const uint32_t ca = charOffsetOf(a), cb = charOffsetOf(b);
+    const uint64_t need = static_cast<uint64_t>(kWords) * m + static_cast<uint64_t>(m) + (cb - ca + 1) / 2 + 1;
+    if (need > areaCap) {
+      fail(FMT_E_CAPACITY);
+      return;
+    }
+    uint32_t* R = area;                                  // kWords words per member
+    uint32_t* co = area + static_cast<size_t>(kWords) * m;  // members' char offsets in the run (original order)
+    uint16_t* T = reinterpret_cast<uint16_t*>(co + m);   // the run's text
+    const int r0 = a >> 6, r1 = ((b - 1) >> 6) + 1;
+    FOR_ROWS(r, r0, r1) {
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        if (j >= a && j < b)
+          for (int f = 0; f < kWords; f++) storeGlobal(R + static_cast<size_t>(j - a) * kWords + f, LANE(W[f])[r]);
+      }
+    }
+    FOR_LANES(l) {
+      for (uint32_t t = l; t < cb - ca; t += 64) storeGlobal(T + t, static_cast<uint16_t>(chRead(static_cast<int>(ca + t))));
+    }
+    waveSync();
+    uint32_t off = 0;
+    for (int k = 0; k < m; k++) {  // (serial: runs are short, reconnects rare)
+      const uint32_t len = fLen(uni(loadCoherent(R + static_cast<size_t>(k) * kWords)));
+      FOR_LANES(l) {
+        if (l == 0) storeGlobal(co + k, off);
+      }
+      off += len;
+    }
+    waveSync();
+    FOR_ROWS(r, r0, r1) {
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        if (j >= a && j < b) {
+          const uint32_t src = loadCoherent(perm + (j - a));
+          const uint32_t blk = fBlk(LANE(W[0])[r]);
+          for (int f = 0; f < kWords; f++) {
+            uint32_t v = loadCoherent(R + static_cast<size_t>(src) * kWords + f);
+            if (f == 0) v = mkW0(fLen(v), blk, fProps(v));
+            LANE(W[f])[r] = v;
+          }
+        }
+      }
+    }
+    uint32_t dst = ca;
+    for (int k = 0; k < m; k++) {
+      const uint32_t src = uni(loadCoherent(perm + k));
+      const uint32_t so = uni(loadCoherent(co + src));
+      const uint32_t len = fLen(uni(loadCoherent(R + static_cast<size_t>(src) * kWords)));
+      FOR_LANES(l) {
+        for (uint32_t t = l; t < len; t += 64) chWrite(static_cast<int>(dst + t), loadCoherent(T + so + t));
+      }
+      dst += len;
+    }
+    waveSync();
+  }
+
+  // regeneratePendingOp for every pending op in order (client.ts:1452-1542, squash false): segments
+  // normalized once per (currentSeq, localSeq) (:1480-1507); each pending group, its segments in
+  // document order, becomes one op per segment at its position in LocalReconnectingPerspective(
+  // currentSeq, 0, localSeq) (resetPendingDeltaToOps :1160-1289) — an annotate unless the segment was
+  // removed by an acked op, an insert of its current text with the original op's props, a remove
+  // while its first remove is still the local one — and a new pending group. The ops go to the
+  // document's regen slab.
+  FMT_DEV void regenerate() {
+    if (gHead == gTail) return;
+    if (!normSet || curSeq != normRef || locSeq != normLocal) {
+      normalizeOnRebase();
+      if (status != FMT_OK) return;
+      normSet = true;
+      normRef = curSeq;
+      normLocal = locSeq;
+    }
+    if (gHead > 0) groupCompact();
+    recCompact();
+    recFrozen = true;
+    const int g1 = gTail;
+    fmt_mt_op* outOps = in.loc->regen + in.loc->regenOffs[in.doc];
+    const uint32_t opCap = static_cast<uint32_t>(in.loc->regenOffs[in.doc + 1] - in.loc->regenOffs[in.doc]);
+    uint16_t* outText = in.loc->regenText + in.loc->regenTextOffs[in.doc];
+    const uint64_t textCap = in.loc->regenTextOffs[in.doc + 1] - in.loc->regenTextOffs[in.doc];
+    for (int g = gHead; g < g1 && status == FMT_OK; g++) {
+      const uint32_t ls = gWord(g, 0), tf = gWord(g, 1), payload = gWord(g, 2);
+      const int32_t pos2 = static_cast<int32_t>(gWord(g, 3)), inflightRef = static_cast<int32_t>(gWord(g, 4));
+      const int type = static_cast<int>(tf & 0xFFu);
+      // the group's segments as a row bitmask (document order), its records released
+      const int nr = rows();
+      Lane<uint32_t> segs;
+      FOR_LANES(l) { LANE(segs) = 0u; }
+      for (int i = recFind(static_cast<uint32_t>(g), 0); i >= 0 && status == FMT_OK; i = recFind(static_cast<uint32_t>(g), i + 1)) {
+        const int j = findLeafById(rWord(i, 0));
+        if (j < 0) {
+          fail(FMT_E_DATA);
+          break;
+        }
+        rSet(i, 0, 0u);
+        FOR_LANES(l) {
+          if (l == (j & 63)) LANE(segs) |= 1u << (j >> 6);
+        }
+      }
+      waveSync();
+      if (status != FMT_OK) break;
+      Lane<VR> vis, st;
+      visLengths(static_cast<int>(FMT_MT_LOCAL_SEQ_BASE | ls), -5, vis, nr);  // findReconnectionPosition
+      scanRows(vis, st, nr);
+      for (Lane<uint32_t> todo = segs; status == FMT_OK;) {
+        const int j = firstSet(todo, nr);
+        if (j < 0) break;
+        FOR_LANES(l) {
+          if (l == (j & 63)) LANE(todo) &= ~(1u << (j >> 6));
+        }
+        const uint32_t w1 = readField(j, 1), w2 = readField(j, 2), w4 = readField(j, 4);
+        const uint32_t len = fLen(readField(j, 0));
+        const int pos = static_cast<int>(readlane(selectRow(st, j >> 6), j & 63));
+        const bool removed = w2 != static_cast<uint32_t>(kNotRemoved);
+        bool emit = false;
+        fmt_mt_op o;
+        o.seq = static_cast<int32_t>(ls);
+        o.ref_seq = curSeq;
+        o.min_seq = 0;
+        o.pos1 = pos;
+        o.pos2 = pos + static_cast<int32_t>(len);
+        o.payload = payload;
+        o.len = 0;
+        o.client = 0;
+        o.type = static_cast<uint8_t>(type);
+        o.flags = 0;
+        if (type == FMT_MT_ANNOTATE) {
+          emit = !(removed && !isLocalSeq(w2));  // not isRemovedAndAcked
+        } else if (type == FMT_MT_INSERT) {
+          if (!isLocalSeq(w1)) {  // "Segment already has assigned sequence number" (0x037)
+            fail(FMT_E_DATA);
+            break;
+          }
+          if (removed && !isLocalSeq(w2)) {  // obliterated on arrival: obliterate reconnect is not in this build
+            fail(FMT_E_UNSUPPORTED);
+            break;
+          }
+          if (regenTextN + len > textCap) {
+            fail(FMT_E_CAPACITY);
+            break;
+          }
+          const uint32_t c0 = charOffsetOf(j);
+          FOR_LANES(l) {
+            for (uint32_t t = l; t < len; t += 64) storeGlobal(outText + regenTextN + t, static_cast<uint16_t>(chRead(static_cast<int>(c0 + t))));
+          }
+          o.pos2 = pos2;
+          o.payload = regenTextN;
+          o.len = static_cast<uint16_t>(len & 0xFFFFu);
+          o.flags = (len & FMT_MT_F_LEN_HI_MASK) | (fMarker(w4) ? FMT_MT_F_MARKER : 0u);
+          regenTextN += len;
+          emit = true;
+        } else {
+          emit = removed && isLocalSeq(w2);  // nobody else removed it meanwhile
+        }
+        if (emit) {
+          if (regenN >= opCap) {
+            fail(FMT_E_CAPACITY);
+            break;
+          }
+          FOR_LANES(l) {
+            if (l == 0) outOps[regenN] = o;
+          }
+          regenN++;
+          const int ng = groupPush(ls, tf, payload, pos2, inflightRef);
+          if (ng < 0) break;
+          recAppend(fId(w4), static_cast<uint32_t>(ng));
+        } else {
+          pendAdd(j, -1);
+        }
+      }
+    }
+    waveSync();
+    gHead = g1;  // (the old groups are replaced by the new ones, [g1, gTail))
+    recFrozen = false;
   }
 
   // ------------------------------------------------------------------ zamboni (zamboni.ts)
@@ -2293,9 +3138,11 @@ class Doc {
         const uint32_t bl = LANE(blen);
         const bool nl = bl > 0 && chRead(static_cast<int>(rowBase + LANE(ex) + bl - 1)) == 10u;
         const uint32_t pr = propsL(l, r);
+        bool held = false;  // (Loc) a leaf with pending local ops (zamboni.ts:148)
+        if constexpr (Loc) held = LANE(W[kPendW])[r] != 0u;
         const uint32_t p = fLen(w0) | ((kPW ? 0u : pr) << C::kLenBits) | (rm != kNotRemoved ? 1u << 24 : 0u) |
                            (rm <= minSeq ? 1u << 25 : 0u) | (ins <= minSeq ? 1u << 26 : 0u) | (nl ? 1u << 27 : 0u) |
-                           (fMarker(LANE(W[4])[r]) ? 1u << 28 : 0u);
+                           (fMarker(LANE(W[4])[r]) ? 1u << 28 : 0u) | (held ? 1u << 29 : 0u);
         if (r == r0) LANE(pk0) = p;
         else LANE(pk1) = p;
         if constexpr (kPW) {
@@ -2320,7 +3167,10 @@ class Doc {
       if constexpr (kPW) props = (j >> 6) == r0 ? readlane(pp0, j & 63) : readlane(pp1, j & 63);
       s->tmp[k] = cs;  // char offset and length, for the deletions below
       s->tmp[kMaxNodes + k] = len;
-      if (((p >> 24) & 1u) == 0) {
+      if ((p >> 29) & 1u) {  // held: kept as it is, and nothing appends onto it
+        prev = -1;
+        kept++;
+      } else if (((p >> 24) & 1u) == 0) {
         if ((p >> 26) & 1u) {
           const bool lastNl = ((p >> 27) & 1u) != 0;
           const bool marker = ((p >> 28) & 1u) != 0;  // Marker: never appends, nothing appends onto it
@@ -2392,7 +3242,7 @@ class Doc {
       }
       nChars = newChars;
     }
-    if constexpr (Adj) {  // appended and unlinked leaves take their managers with them
+    if constexpr (Adj || Loc) {  // appended and unlinked leaves take their managers with them
       for (uint32_t m = pmN > 0 ? (mergeMask | dropMask) : 0u; m != 0; m &= m - 1) pmDropLeaf(fId(readField(first + ctz32(m), 4)));
     }
     deleteLeaves(first, cnt, mergeMask | dropMask);
@@ -2531,11 +3381,12 @@ class Doc {
       LANE(W[1]) = z;
       LANE(W[2]) = z;
       LANE(W[3]) = z;
-      if constexpr (kWords > 5) {
+      if constexpr (C::kWords > 5) {
         LANE(W[5]) = z;
-        LANE(W[kWords - 1]) = z;
+        LANE(W[kPropW]) = z;
       }
       LANE(W[4]) = z;
+      if constexpr (Loc) LANE(W[kPendW]) = z;
     }
     FOR_LANES(l) {
       for (int i = l; i < kMaxBlocks; i += 64) s->freeList[i] = static_cast<BId>(kMaxBlocks - 1 - i);
@@ -2569,7 +3420,7 @@ class Doc {
         LANE(W[2])[0] = static_cast<uint32_t>(kNotRemoved);
         LANE(W[3])[0] = 0u;
         LANE(W[4])[0] = w4;
-        if constexpr (kPW) LANE(W[kWords - 1])[0] = kPropsUndef;
+        if constexpr (kPW) LANE(W[kPropW])[0] = kPropsUndef;
       }
     }
     n = 1;
@@ -2651,7 +3502,7 @@ class Doc {
           LANE(W[1])[r] = static_cast<uint32_t>(inf.ins_seq);
           LANE(W[2])[r] = static_cast<uint32_t>(rm);
           LANE(W[3])[r] = static_cast<uint32_t>(mask);
-          if constexpr (kWords > 5) LANE(W[5])[r] = static_cast<uint32_t>(mask >> 32);
+          if constexpr (C::kWords > 5) LANE(W[5])[r] = static_cast<uint32_t>(mask >> 32);
           const uint32_t w4 = LANE(W[4])[r];
           LANE(W[4])[r] = mkW4(fId(w4), inf.ins_client) | (w4 & kW4Marker);
         }
@@ -2707,7 +3558,7 @@ class Doc {
         LANE(W[0])[r] = live ? mkW0(len, static_cast<uint32_t>(j < H ? j / 7 : 0), kPropsUndef) : 0u;
         LANE(W[2])[r] = live ? static_cast<uint32_t>(kNotRemoved) : 0u;
         LANE(W[4])[r] = live ? mkW4(static_cast<uint32_t>(j + 1), FMT_NON_COLLAB_CLIENT) | ((lenF & FMT_MT_SEG_MARKER) != 0 ? kW4Marker : 0u) : 0u;
-        if constexpr (kPW) LANE(W[kWords - 1])[r] = live ? kPropsUndef : 0u;
+        if constexpr (kPW) LANE(W[kPropW])[r] = live ? kPropsUndef : 0u;
       }
     }
     waveSync();
@@ -2871,6 +3722,20 @@ class Doc {
       stamp(kPfOpLoad);
       opIdx = static_cast<uint32_t>(i - in.begin);
       const bool loader = (op.flags & FMT_MT_F_LOADSEG) != 0;
+      if constexpr (Loc) {
+        // the local client's own events: a submission, a rollback or a reconnect changes no collab
+        // window and runs no window zamboni (an ACK is a sequenced message: below)
+        if (op.flags & (FMT_MT_F_LOCAL | FMT_MT_F_ROLLBACK | FMT_MT_F_REGEN)) {
+          if (op.flags & FMT_MT_F_LOCAL) applyLocal(op, text);
+          else if (op.flags & FMT_MT_F_ROLLBACK) rollbackOp(op);
+          else regenerate();
+          if (status != FMT_OK) {
+            failSeq = op.seq;
+            break;
+          }
+          continue;
+        }
+      }
       if (loader) {
         if (op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient) loadBodySegment(op, text);
         else fail(kMaxClient < 63 ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
@@ -2879,6 +3744,7 @@ class Doc {
       else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);
       else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
+      else if (Loc && (op.flags & FMT_MT_F_ACK)) ackOp(op);
       else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
       if constexpr (Rm) {
         if (rmPendN > 0 || rmHitsSet)
@@ -2898,8 +3764,12 @@ class Doc {
             break;
           }
           curSeq = op.seq;
-          if (op.min_seq <= minSeq) break;
-          minSeq = op.min_seq;
+          int eff = op.min_seq;
+          if constexpr (Loc) {  // bounded by the oldest in-flight op's refSeq (client.ts:1374-1378, sequence.ts:499)
+            if (gHead < gTail && static_cast<int32_t>(gWord(gHead, 4)) < eff) eff = static_cast<int32_t>(gWord(gHead, 4));
+          }
+          if (eff <= minSeq) break;
+          minSeq = eff;
           if constexpr (Ob) obSetMinSeq();
         }
         zamboni();
@@ -2913,6 +3783,11 @@ class Doc {
   }
 
   FMT_DEV void writeOutputs(const DocOutputs& out) {
+    if constexpr (Loc) {
+      FOR_LANES(l) {
+        if (l < 2) storeGlobal(in.loc->regenCount + 2 * in.doc + l, l == 0 ? regenN : regenTextN);
+      }
+    }
     if constexpr (Adj) {
       if (out.legacyProps != nullptr && status == FMT_OK) {
         pmLegacyProps(out.legacyProps);
@@ -2969,7 +3844,7 @@ class Doc {
           L.ins_seq = static_cast<int32_t>(LANE(W[1])[r]);
           L.rm_seq = static_cast<int32_t>(LANE(W[2])[r]);
           L.rm_clients = LANE(W[3])[r];
-          if constexpr (kWords > 5) L.rm_clients |= static_cast<uint64_t>(LANE(W[5])[r]) << 32;
+          if constexpr (C::kWords > 5) L.rm_clients |= static_cast<uint64_t>(LANE(W[5])[r]) << 32;
           L.char_off = LANE(cst)[r];
           L.len = fLen(w0);
           L.ins_client = static_cast<int16_t>(fClient(LANE(W[4])[r]));
@@ -3054,6 +3929,14 @@ class Doc {
         }
       }
       pmN = 0;
+      if constexpr (Loc) {
+        locSeq = 0;
+        gHead = gTail = 0;
+        recN = 0;
+        recFrozen = false;
+        regenN = regenTextN = 0;
+        normSet = false;
+      }
       if (in.loaded) loadSnapshot();
       else loadInitial();
     }

@@ -238,6 +238,17 @@ struct fmt_ctx {
   bool mtHasAdjust = false;
   uint32_t mtNAdjusts = 0, mtNValues = 0, mtNNumSorted = 0;
   DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
+  // f4 (local-client records): every document replays in the large tier's Loc variant; its pending
+  // groups, group records, PropertiesManager records, regenerated ops / text and normalization
+  // scratch live in per-document slabs (mt_engine.h LocalTables)
+  bool mtLocal = false;
+  DevBuf<uint32_t> mtLocGroups, mtLocRecs, mtLocPm, mtLocScratch, mtLocRegenCount;
+  DevBuf<uint64_t> mtLocOffs;                // 6 offset arrays of n + 1: groups, recs, pm, regen, text, scratch
+  DevBuf<fmt_mt_op> mtLocRegen;
+  DevBuf<uint16_t> mtLocRegenText;
+  DevBuf<fmt_mt::LocalTables> mtLocTab;
+  std::vector<uint64_t> mtLocRegenOffsHost, mtLocRegenTextOffsHost;
+  std::vector<uint32_t> mtLocIds;            // [n, 0, 1, .. n-1]: the large tier's document list
   uint32_t mtNSmall = 0;
   DevBuf<fmt_huge::HugeState> hugeStates;
   DevBuf<fmt_huge::HugeInputs> hugeInputs;
@@ -452,6 +463,11 @@ void fmt_close(fmt_ctx* c) {
   c->mtPmOffs.release();
   c->mtLegacy.release();
   c->mtBigLegacy.release();
+  for (auto* q : {&c->mtLocGroups, &c->mtLocRecs, &c->mtLocPm, &c->mtLocScratch, &c->mtLocRegenCount}) q->release();
+  c->mtLocOffs.release();
+  c->mtLocRegen.release();
+  c->mtLocRegenText.release();
+  c->mtLocTab.release();
   c->spans.release();
   c->packed.release();
   c->digests.release();
@@ -927,7 +943,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   // one pass over the op records on host threads: counts, and the first invalid record
   struct OpScan {
     uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
-    bool obliterates = false;
+    bool obliterates = false, local = false;
     uint64_t errAt = ~0ull;
     int errCode = FMT_OK;
     const char* err = nullptr;
@@ -944,6 +960,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       const fmt_mt_op& op = b->ops[i];
       if (op.flags & FMT_MT_F_CATCHUP) S.catchupOps++;
       if (op.flags & FMT_MT_F_RMORDER) S.rmOrderOps++;
+      if (op.flags & FMT_MT_F_LOCAL_ANY) S.local = true;
       if (op.flags & FMT_MT_F_LOADSEG) {  // a SnapshotV1 body segment: its merge info row in range
         if (op.type != FMT_MT_INSERT || b->snapshot_info == nullptr || op.pos1 < 0 ||
             static_cast<uint64_t>(op.pos1) >= b->n_snapshot_segs ||
@@ -972,16 +989,23 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     }
   });
   uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
-  bool obliterates = false;
+  bool obliterates = false, local = false;
   const OpScan* firstBad = nullptr;
   for (const OpScan& S : scans) {
     insertChars += S.insertChars;
     catchupOps += S.catchupOps;
     rmOrderOps += S.rmOrderOps;
     obliterates = obliterates || S.obliterates;
+    local = local || S.local;
     if (S.err != nullptr && (firstBad == nullptr || S.errAt < firstBad->errAt)) firstBad = &S;
   }
   if (firstBad != nullptr) return setErr(c, firstBad->errCode, firstBad->err);
+  // f4 batches run the large tier's Loc variant alone: features it does not combine with are refused
+  if (local && (obliterates || catchupOps || rmOrderOps || b->relpos != nullptr || b->adjusts != nullptr ||
+                b->snapshot_info != nullptr))
+    return setErr(c, FMT_E_UNSUPPORTED,
+                  "local-client records (FMT_MT_F_LOCAL_ANY) do not combine with obliterate, catch-up, remove order, "
+                  "relative positions, annotate-adjust or SnapshotV1 merge info");
   if (b->snapshots) {
     for (uint32_t d = 0; d < n; d++) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
@@ -1190,6 +1214,57 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtAdjTab.p, &T, sizeof T));
     FMT_HIP(c, hipStreamSynchronize(c->stream));  // (sv / si / T are about to go out of scope)
   }
+  c->mtLocal = local;
+  if (local) {
+    // Per-document slabs, sized from the document's local records (a document that needs more reports
+    // FMT_E_CAPACITY): 4 + 2 pending groups per submission (a reconnect replaces a group by one per
+    // segment), 32 group records per submission (hits and split copies; deleted ones compact away),
+    // 64 PropertiesManager records per key of a local annotate, regenerated ops / text per reconnect,
+    // and normalization scratch for a document that reconnects.
+    const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true);
+    std::vector<uint64_t> offs(6 * (n + 1ull), 0);
+    for (uint32_t d = 0; d < n; d++) {
+      uint64_t sub = 0, keys = 0, regens = 0, text = 0;
+      for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+        const fmt_mt_op& op = b->ops[i];
+        if (op.flags & FMT_MT_F_REGEN) regens++;
+        if (!(op.flags & FMT_MT_F_LOCAL)) continue;
+        sub++;
+        if (op.type == FMT_MT_INSERT) text += fmt_mt_op_len(&op);
+        if (op.type == FMT_MT_ANNOTATE) keys += b->props_off[op.payload + 1] - b->props_off[op.payload];
+      }
+      const uint64_t cap[6] = {sub ? std::min<uint64_t>(6 * sub + 64 + (regens ? big.leaves : 0), 1u << 22) : 0,
+                               sub ? std::min<uint64_t>(32 * sub + 1024, 1u << 24) : 0,
+                               keys ? std::min<uint64_t>(64 * keys + 512, 1u << 22) : 0,
+                               regens ? std::min<uint64_t>(regens * std::min<uint64_t>(8 * sub + 64, big.leaves), 1u << 22) : 0,
+                               regens ? std::min<uint64_t>(regens * std::min<uint64_t>(text, big.chars) + 64, 1u << 26) : 0,
+                               regens ? 15ull * big.leaves + big.chars / 2 + 64 : 0};
+      for (int k = 0; k < 6; k++) offs[k * (n + 1ull) + d + 1] = offs[k * (n + 1ull) + d] + cap[k];
+    }
+    auto total = [&](int k) { return offs[k * (n + 1ull) + n]; };
+    FMT_HIP(c, c->mtLocOffs.reserve(6 * (n + 1ull)));
+    FMT_HIP(c, c->mtLocGroups.reserve(8 * total(0)));
+    FMT_HIP(c, c->mtLocRecs.reserve(2 * total(1)));
+    FMT_HIP(c, c->mtLocPm.reserve(4 * total(2)));
+    FMT_HIP(c, c->mtLocRegen.reserve(total(3)));
+    FMT_HIP(c, c->mtLocRegenText.reserve(total(4)));
+    FMT_HIP(c, c->mtLocScratch.reserve(total(5)));
+    FMT_HIP(c, c->mtLocRegenCount.reserve(2ull * n));
+    FMT_HIP(c, c->mtLocTab.reserve(1));
+    FMT_HIP(c, cp(c->mtLocOffs.p, offs.data(), offs.size() * sizeof(uint64_t)));
+    FMT_HIP(c, hipMemsetAsync(c->mtLocRegenCount.p, 0, 2ull * n * sizeof(uint32_t), c->stream));
+    const uint64_t* O = c->mtLocOffs.p;
+    fmt_mt::LocalTables T{c->mtLocGroups.p, O, c->mtLocRecs.p, O + (n + 1ull), c->mtLocPm.p, O + 2 * (n + 1ull),
+                          c->mtLocRegen.p, O + 3 * (n + 1ull), c->mtLocRegenText.p, O + 4 * (n + 1ull),
+                          c->mtLocRegenCount.p, c->mtLocScratch.p, O + 5 * (n + 1ull)};
+    FMT_HIP(c, cp(c->mtLocTab.p, &T, sizeof T));
+    c->mtLocRegenOffsHost.assign(offs.begin() + 3 * (n + 1ull), offs.begin() + 4 * (n + 1ull));
+    c->mtLocRegenTextOffsHost.assign(offs.begin() + 4 * (n + 1ull), offs.begin() + 5 * (n + 1ull));
+    c->mtLocIds.resize(n + 1ull);
+    c->mtLocIds[0] = n;
+    for (uint32_t d = 0; d < n; d++) c->mtLocIds[d + 1] = d;
+    FMT_HIP(c, hipStreamSynchronize(c->stream));  // (offs / T are about to go out of scope)
+  }
   FMT_HIP(c, stagedCopy(c, c->mtOps.p, b->ops, b->n_ops * sizeof(fmt_mt_op), true));
   FMT_HIP(c, cp(c->mtOffs.p, b->doc_op_offsets, (n + 1ull) * sizeof(uint64_t)));
   FMT_HIP(c, stagedCopy(c, c->mtText.p, b->text, b->text_len * sizeof(uint16_t), true));
@@ -1306,7 +1381,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
       if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (!c->mtHugeOk[d]) {  // (V1 body segments with merge info)
+      if (!c->mtHugeOk[d] || local) {  // (V1 body segments with merge info; local-client records)
         refuse(d, FMT_E_UNSUPPORTED);
         continue;
       }
@@ -1375,7 +1450,8 @@ int fmt_mt_run(fmt_ctx* c) {
                                 c->mtHasSnapInfo ? c->mtNSnapSegs : 0u,
                                 c->mtNRelpos ? c->mtRelpos.p : nullptr,
                                 c->mtNRelpos, c->mtMarkerKey,
-                                c->mtHasAdjust ? c->mtAdjTab.p : nullptr};
+                                c->mtHasAdjust ? c->mtAdjTab.p : nullptr,
+                                c->mtLocal ? c->mtLocTab.p : nullptr};
   fmt_kernels::MtDeviceOut dout{c->mtHdr.p, c->mtLeaves.p, c->mtChars.p, c->mtProps.p,
                                 c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
                                 !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr, nullptr, nullptr,
@@ -1385,7 +1461,20 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   const bool hasHuge = c->mtHugeLoaded > 0, list = c->mtUseList;
-  if (!list || c->mtNSmall > 0)
+  if (c->mtLocal) {  // every document goes straight to the large tier's Loc variant
+    std::vector<uint32_t> ids;
+    if (list) {
+      ids.push_back(c->mtNSmall);
+      std::vector<uint8_t> skip(c->mtDocs, 0);
+      for (uint32_t d : c->mtRefused) skip[d] = 1;
+      for (uint32_t d = 0; d < c->mtDocs; d++)
+        if (!skip[d]) ids.push_back(d);
+      ids[0] = static_cast<uint32_t>(ids.size() - 1);
+    }
+    const std::vector<uint32_t>& L = list ? ids : c->mtLocIds;
+    FMT_HIP(c, hipMemcpyAsync(c->mtEsc.p, L.data(), L.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    FMT_HIP(c, hipStreamSynchronize(c->stream));  // (ids goes out of scope)
+  } else if (!list || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,
                                             c->mtObliterate,
@@ -1413,7 +1502,7 @@ int fmt_mt_run(fmt_ctx* c) {
                                   c->mtHasAdjust ? c->mtBigLegacy.p : nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
-                                                 c->mtHasRmOrder, c->mtSched.p + 2, c->mtHasAdjust));
+                                                 c->mtHasRmOrder, c->mtSched.p + 2, c->mtHasAdjust, c->mtLocal));
     FMT_HIP(c, hipEventRecord(c->ev3, c->stream));
     c->timed2 = true;
     std::vector<uint32_t> list(nEsc);
@@ -1430,7 +1519,8 @@ int fmt_mt_run(fmt_ctx* c) {
     }
     FMT_HIP(c, hipStreamSynchronize(c->stream));
     for (uint32_t i = 0; i < nEsc; i++)
-      if (hb[i].status == FMT_E_CAPACITY && c->mtHugeOk[list[i]] && c->mtHugeSlot[list[i]] < 0) grow.push_back(list[i]);
+      if (hb[i].status == FMT_E_CAPACITY && c->mtHugeOk[list[i]] && c->mtHugeSlot[list[i]] < 0 && !c->mtLocal)
+        grow.push_back(list[i]);
     if (!grow.empty()) {
       FMT_HIP(c, c->mtStartSegDev.reserve(grow.size()));
       std::vector<fmt_mt_snapshot_seg> starts(grow.size());
@@ -1979,6 +2069,20 @@ int fmt_mt_fetch_numbers(fmt_ctx* c, uint32_t doc, double* out, uint32_t cap, ui
   if (nOut) *nOut = n;
   const uint32_t m = n < cap ? n : cap;
   if (m) FMT_HIP(c, hipMemcpy(out, c->mtNums.p + c->mtNumOffsHost[doc], m * sizeof(double), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_regen(fmt_ctx* c, uint32_t doc, fmt_mt_op* ops, uint32_t capOps, uint16_t* text, uint32_t capText,
+                       uint32_t* nOps, uint32_t* nText) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (ops == nullptr && capOps > 0) || (text == nullptr && capText > 0))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_regen: bad arguments");
+  uint32_t cnt[2] = {0, 0};
+  if (c->mtLocal) FMT_HIP(c, hipMemcpy(cnt, c->mtLocRegenCount.p + 2ull * doc, sizeof cnt, hipMemcpyDeviceToHost));
+  if (nOps) *nOps = cnt[0];
+  if (nText) *nText = cnt[1];
+  const uint32_t m = cnt[0] < capOps ? cnt[0] : capOps, t = cnt[1] < capText ? cnt[1] : capText;
+  if (m) FMT_HIP(c, hipMemcpy(ops, c->mtLocRegen.p + c->mtLocRegenOffsHost[doc], m * sizeof(fmt_mt_op), hipMemcpyDeviceToHost));
+  if (t) FMT_HIP(c, hipMemcpy(text, c->mtLocRegenText.p + c->mtLocRegenTextOffsHost[doc], t * sizeof(uint16_t), hipMemcpyDeviceToHost));
   return FMT_OK;
 }
 

@@ -33,6 +33,9 @@ const MARKER_ID_KEY = "markerId"; // reservedMarkerIdKey
 const FMT_MT_VALUE_ADJUST = 0xffff, FMT_MT_VALUE_COMPUTED = 0x8000;
 const FMT_MT_ADJ_MIN = 1, FMT_MT_ADJ_MIN_NULL = 2, FMT_MT_ADJ_MAX = 4, FMT_MT_ADJ_MAX_NULL = 8;
 const FMT_NON_COLLAB_CLIENT = -2; // fmt.h: the insert client of a segment without merge info
+// f4, the local client (fmt.h): a submission, the ack of the oldest pending op, rollback of the newest,
+// reconnect (regeneratePendingOp for every pending op)
+const FMT_MT_F_LOCAL = 512, FMT_MT_F_ACK = 1024, FMT_MT_F_ROLLBACK = 2048, FMT_MT_F_REGEN = 4096;
 
 /** The refType of a Marker spec {marker: {refType}, props?} (IJSONMarkerSegment), or null. */
 function markerRefType(spec) {
@@ -147,6 +150,10 @@ class MergeTreeDocBuilder {
 		this.markerIds = new Set();
 		this.markerAmbiguous = false;
 		this.usesRelpos = false;
+		// f4: the document's observer is a local client with events of its own (streams.py _DocBuilder)
+		this.local = false;
+		this.pending = []; // [type, payload] of each pending local op, oldest first
+		this.curSeq = 0; // the last message's seq: a local op's refSeq (sequence.ts:666 currentRefSeq)
 	}
 	noteMarkerId(props) {
 		const mid = props ? props[MARKER_ID_KEY] : undefined;
@@ -211,20 +218,79 @@ class MergeTreeDocBuilder {
 		const contents = msg.contents;
 		let members = contents.type === MT_GROUP ? contents.ops : [contents];
 		if (members.length === 0) members = [null]; // empty group: only advances the window
+		// a message of the local client itself acknowledges its oldest pending ops, one per member
+		// (client.ts:1367-1368 ackPendingSegment)
+		const ack = this.local && client === 0;
 		if (this.owner.keepMessages) this.messages.push({ message: msg, firstOp: this.nOps, count: members.length });
 		members.forEach((op, k) => {
 			this.noteOp(op);
+			let flags = k > 0 ? FMT_MT_F_GROUP_CONT : 0;
+			if (ack) {
+				if (op === null || this.pending.length === 0 || this.pending[0][0] !== op.type) {
+					throw new Error("an ack that is not the oldest pending local op"); // mergeTree.ts:1331-1340
+				}
+				this.pending.shift();
+				flags |= FMT_MT_F_ACK;
+			}
 			this.owner.packOp(op, msg.sequenceNumber, msg.referenceSequenceNumber,
-				msg.minimumSequenceNumber, client, k > 0 ? FMT_MT_F_GROUP_CONT : 0);
+				msg.minimumSequenceNumber, client, flags);
 			this.nOps++;
 		});
 		if (msg.minimumSequenceNumber > this.minSeq) this.minSeq = msg.minimumSequenceNumber; // updateSeqNumbers
+		this.curSeq = msg.sequenceNumber;
 	}
-	/** SharedObjectCore.processMessagesCore shape: a bunch sharing one envelope (sequence.ts:873-919). */
+	/**
+	 * A local submission (insertSegmentLocal / removeRangeLocal / annotateRangeLocal,
+	 * client.ts:273-355): op contents with positions in the local view; a GROUP op
+	 * (localTransaction, client.ts:1600-1629) submits its members one by one. Mirrors streams.py.
+	 */
+	localOp(op) {
+		if (this.owner.current !== this) throw new UnsupportedOp("documents must be packed contiguously (finish one before the next)");
+		const members = op.type === MT_GROUP ? op.ops : [op];
+		for (const m of members) {
+			if (m.type !== MT_INSERT && m.type !== MT_REMOVE && m.type !== MT_ANNOTATE) throw new UnsupportedOp("local obliterate");
+			const none = (v) => v === undefined || v === null;
+			if ((none(m.pos1) && !none(m.relativePos1)) || (m.type !== MT_INSERT && none(m.pos2) && !none(m.relativePos2))) {
+				throw new UnsupportedOp("local op with relative positions");
+			}
+			this.noteOp(m);
+			this.owner.packOp(m, 0, this.curSeq, 0, 0, FMT_MT_F_LOCAL);
+			const o = (this.owner.ops.n - 1) * MT_OP_BYTES;
+			this.local = true;
+			this.pending.push([m.type, this.owner.ops.view.getUint32(o + 20, true)]);
+			this.nOps++;
+		}
+	}
+	/** Rollback of the newest pending op (client.ts:554; a GROUP op: once per member). */
+	localRollback() {
+		if (this.pending.length === 0) throw new Error("rollback without a pending local op");
+		const [t, payload] = this.pending.pop();
+		this.owner.rawOp(0, 0, 0, 0, 0, payload, 0, 0, t, FMT_MT_F_ROLLBACK);
+		this.nOps++;
+	}
+	/**
+	 * Reconnect: regeneratePendingOp for every pending op (client.ts:1452-1542). The ops it returns
+	 * (MergeTreeReplay.regenerated) become the pending ops whose acks follow: pass them here or to
+	 * regenPending once known.
+	 */
+	localRegen(newOps) {
+		this.local = true;
+		this.owner.rawOp(0, 0, 0, 0, 0, 0, 0, 0, 0, FMT_MT_F_REGEN);
+		this.nOps++;
+		this.pending = [];
+		if (newOps) this.regenPending(newOps);
+	}
+	regenPending(newOps) {
+		this.pending = newOps.map((op) => [op.type, op.type === MT_ANNOTATE ? this.owner.propsOp(op.props || {}, op.adjust) : 0]);
+	}
+	/**
+	 * SharedObjectCore.processMessagesCore shape: a bunch sharing one envelope (sequence.ts:873-919).
+	 * A local bunch (the client's own messages coming back sequenced) acknowledges its pending ops.
+	 */
 	processMessagesCore(messagesCollection) {
 		const { envelope, messagesContent } = messagesCollection;
-		if (messagesCollection.local) {
-			throw new UnsupportedOp("local (pending) ops are outside the batch replay path");
+		if (messagesCollection.local && (!this.local || this.clientIds.get(envelope.clientId) !== 0)) {
+			throw new UnsupportedOp("a local bunch from a client other than the document's observer, or with no pending local ops");
 		}
 		for (const mc of messagesContent) {
 			this.addMessage(Object.assign({}, envelope, {
@@ -348,6 +414,7 @@ class MergeTreeStreamBuilder {
 		const specsOf = (c) => (c.version === "1" ? c.segments : c.segmentTexts);
 		const d = new MergeTreeDocBuilder(this, this.docs.length, observer === undefined ? "snapshot" : observer);
 		d.minSeq = md.minSequenceNumber === undefined ? md.sequenceNumber : md.minSequenceNumber;
+		d.curSeq = md.sequenceNumber;
 		const first = this.snapshotSegs.length;
 		let anyInfo = false;
 		chunks.forEach((c) => {
@@ -501,6 +568,21 @@ class MergeTreeStreamBuilder {
 			f |= FMT_MT_F_REL2;
 		}
 		return [p1, p2, f];
+	}
+	/** One raw fmt_mt_op record (the local client's rollback / reconnect records). */
+	rawOp(seq, ref, msn, pos1, pos2, payload, len, client, type, flags) {
+		const o = this.ops.next();
+		const v = this.ops.view;
+		v.setInt32(o + 0, seq, true);
+		v.setInt32(o + 4, ref, true);
+		v.setInt32(o + 8, msn, true);
+		v.setInt32(o + 12, pos1, true);
+		v.setInt32(o + 16, pos2, true);
+		v.setUint32(o + 20, payload, true);
+		v.setUint16(o + 24, len, true);
+		v.setUint8(o + 26, client);
+		v.setUint8(o + 27, type);
+		v.setUint32(o + 28, flags, true);
 	}
 	packOp(op, seq, ref, msn, client, flags) {
 		const o = this.ops.next();
@@ -1032,6 +1114,51 @@ class MergeTreeReplay {
 		}
 		return segs;
 	}
+	/** Props op `id` of the batch as the object it was packed from (null values: deletions). */
+	propsOf(doc, id) {
+		const vals = docValues(this.batch, doc);
+		const out = {};
+		for (let t = this.batch.propsOff[id]; t < this.batch.propsOff[id + 1]; t++) {
+			const kv = this.batch.propsKv[t], val = kv & 0xffff;
+			out[this.batch.keys[kv >>> 16]] = val === 0 ? null : JSON.parse(vals[val]);
+		}
+		return out;
+	}
+	/**
+	 * f4: what regeneratePendingOp returned at each reconnect record of the document
+	 * (client.ts:1452-1542, one op per segment of each pending op, in order), as
+	 * [{localSeq, refSeq, op}] with op an IMergeTreeInsertMsg / RemoveMsg / AnnotateMsg in the
+	 * reconnect view — the ops to resubmit (fmt_mt_fetch_regen).
+	 */
+	regenerated(doc) {
+		const r = native().fetchRegen(this.engine.ctx, doc);
+		const dv = new DataView(r.ops);
+		const out = [];
+		for (let o = 0; o < r.ops.byteLength; o += MT_OP_BYTES) {
+			const type = dv.getUint8(o + 27), flags = dv.getUint32(o + 28, true);
+			const pos1 = dv.getInt32(o + 12, true), pos2 = dv.getInt32(o + 16, true), payload = dv.getUint32(o + 20, true);
+			let op;
+			if (type === MT_INSERT) {
+				const n = dv.getUint16(o + 24, true) + (flags & FMT_MT_F_LEN_HI_MASK);
+				const props = pos2 > 0 ? this.propsOf(doc, pos2 - 1) : undefined;
+				let seg;
+				if (flags & FMT_MT_F_MARKER) {
+					seg = { marker: { refType: r.text[payload] } };
+					if (props) seg.props = props;
+				} else {
+					const text = String.fromCharCode.apply(null, r.text.subarray(payload, payload + n));
+					seg = props ? { text, props } : text;
+				}
+				op = { type, pos1, seg };
+			} else if (type === MT_REMOVE) {
+				op = { type, pos1, pos2 };
+			} else {
+				op = { type, pos1, pos2, props: this.propsOf(doc, payload) };
+			}
+			out.push({ localSeq: dv.getInt32(o, true), refSeq: dv.getInt32(o + 4, true), op });
+		}
+		return out;
+	}
 	/** The document's catch-up ranges (ops flagged by finish({catchup: true})). */
 	catchupRanges(doc) {
 		const n = this.header(doc).nCatchup;
@@ -1319,5 +1446,6 @@ module.exports = {
 	UnsupportedOp,
 	summary,
 	constants: { MT_INSERT, MT_REMOVE, MT_ANNOTATE, MT_GROUP, MAP_SET, MAP_DELETE, MAP_CLEAR,
-		MAP_VALUE_UNDEFINED, MAP_ABSENT, FMT_MT_F_GROUP_CONT, FMT_MT_F_CATCHUP, NOT_REMOVED },
+		MAP_VALUE_UNDEFINED, MAP_ABSENT, FMT_MT_F_GROUP_CONT, FMT_MT_F_CATCHUP, NOT_REMOVED,
+		FMT_MT_F_LOCAL, FMT_MT_F_ACK, FMT_MT_F_ROLLBACK, FMT_MT_F_REGEN, FMT_MT_LOCAL_SEQ_BASE: 0x40000000 },
 };

@@ -23,6 +23,7 @@
 //   fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer                     fmt_mt_fetch_remove_order
 //   fetchNumbers(ctx, doc) -> Float64Array                           fmt_mt_fetch_numbers
 //   fetchLegacyProps(ctx, doc, nLeaves) -> Uint16Array               fmt_mt_fetch_legacy_props
+//   fetchRegen(ctx, doc) -> {ops: ArrayBuffer, text: Uint16Array}     fmt_mt_fetch_regen (f4 reconnects)
 //   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
 //   replayMapSparse(ctx, batch) -> Promise<{counts, entries}>        fmt_map_load_sparse + run + fetch
 //   summarizeLegacy(ctx, quotedKeys, values, chunk, threads) -> Promise<timing>   fmt_mt_summarize_legacy
@@ -946,6 +947,37 @@ napi_value FetchLegacyProps(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+napi_value FetchRegen(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 2 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchRegen: a replay is running on this context");
+    return nullptr;
+  }
+  uint32_t doc;
+  if (!get_u32(env, argv[1], "doc", &doc)) return nullptr;
+  uint32_t n = 0, nt = 0;
+  int rc = fmt_mt_fetch_regen(c->ctx, doc, nullptr, 0, nullptr, 0, &n, &nt);
+  void *po, *pt;
+  napi_value abo, abt, arr, out;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(n) * sizeof(fmt_mt_op), &po, &abo));
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(nt) * sizeof(uint16_t), &pt, &abt));
+  if (rc == FMT_OK && (n || nt))
+    rc = fmt_mt_fetch_regen(c->ctx, doc, static_cast<fmt_mt_op*>(po), n, static_cast<uint16_t*>(pt), nt, &n, &nt);
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  CHECK_NAPI(env, napi_create_typedarray(env, napi_uint16_array, nt, abt, 0, &arr));
+  CHECK_NAPI(env, napi_create_object(env, &out));
+  CHECK_NAPI(env, napi_set_named_property(env, out, "ops", abo));
+  CHECK_NAPI(env, napi_set_named_property(env, out, "text", arr));
+  return out;
+}
+
 // FMT_NAPI_BACKTRACE=1: a SIGSEGV prints the native stack to stderr before the default action
 // (diagnostics for crashes inside the addon or the HIP runtime under node). backtrace() is called
 // once before the handler is installed (it loads libgcc's unwinder, which allocates), the handler
@@ -992,6 +1024,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"fetchRemoveOrder", nullptr, FetchRemoveOrder, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchNumbers", nullptr, FetchNumbers, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchLegacyProps", nullptr, FetchLegacyProps, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchRegen", nullptr, FetchRegen, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"replayMapSparse", nullptr, ReplayMapSparse, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"summarizeLegacy", nullptr, SummarizeLegacy, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"summaryBlobs", nullptr, SummaryBlobs, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -245,6 +245,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         for name, args in (("fmt_mt_state_digest", [P, P]), ("fmt_mt_fetch_legacy_props", [P, U32, P, U32]),
                            ("fmt_map_pending_run", [P, P, U64, P]),
+                           ("fmt_mt_fetch_regen", [P, U32, P, U32, P, U32, ctypes.POINTER(U32), ctypes.POINTER(U32)]),
                            ("fmt_map_pending_fetch", [P, P, P, P, U64, ctypes.POINTER(U64)])):
             if path == LIB_PATH or hasattr(L, name):  # (older experimental builds may lack them)
                 getattr(L, name).argtypes = args
@@ -260,6 +261,7 @@ EXPORTED_SYMBOLS = [
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
     "fmt_mt_state_digest", "fmt_mt_fetch_legacy_props", "fmt_map_pending_run", "fmt_map_pending_fetch",
+    "fmt_mt_fetch_regen",
 ]
 
 
@@ -469,6 +471,20 @@ class Engine:
         if n.value:
             self._check(self.L.fmt_mt_fetch_numbers(self.h, doc, _ptr(out), n.value, ctypes.byref(n)))
         return out[: n.value]
+
+    def mt_regen(self, doc: int):
+        """f4: the document's regenerated ops (MT_OP_DTYPE) and their text after the last run
+        (fmt_mt_fetch_regen; regeneratePendingOp at each reconnect record, client.ts:1452-1542)."""
+        from .streams import MT_OP_DTYPE
+
+        n, nt = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self._check(self.L.fmt_mt_fetch_regen(self.h, doc, None, 0, None, 0, ctypes.byref(n), ctypes.byref(nt)))
+        ops = np.zeros(max(n.value, 1), dtype=MT_OP_DTYPE)
+        text = np.zeros(max(nt.value, 1), dtype="<u2")
+        if n.value or nt.value:
+            self._check(self.L.fmt_mt_fetch_regen(self.h, doc, _ptr(ops), n.value, _ptr(text), nt.value, ctypes.byref(n),
+                                                  ctypes.byref(nt)))
+        return ops[: n.value], text[: nt.value]
 
     def mt_catchup(self, doc: int, hdr=None) -> np.ndarray:
         """The document's catch-up ranges (fmt_mt_catchup_range) of its FMT_MT_F_CATCHUP ops."""

@@ -292,6 +292,7 @@ class _DocBuilder:
         # ROLLBACK records must repeat (mergeTree.ts:1325-1408, 2388-2514)
         self.local = False
         self.pending: list[tuple] = []
+        self.cur_seq = 0  # the last message's seq: a local op's refSeq (sequence.ts:666 currentRefSeq)
 
     def note_marker_id(self, props) -> None:
         mid = (props or {}).get(MARKER_ID_KEY)
@@ -383,6 +384,7 @@ class _DocBuilder:
                 rec = rec[:-1] + (rec[-1] | MT_F_ACK,)
             self.ops.append(rec)
         self.min_seq = max(self.min_seq, msn)  # updateSeqNumbers after the message (client.ts:1381-1391)
+        self.cur_seq = seq
 
     # ---- f4: the local client's own events (the document's observer is that client) ----
     def local_op(self, op: dict) -> None:
@@ -394,7 +396,7 @@ class _DocBuilder:
             if m["type"] not in (MT_INSERT, MT_REMOVE, MT_ANNOTATE):
                 raise UnsupportedOp("local obliterate")
             self._note_op(m)
-            rec = self.owner._pack(m, 0, 0, 0, 0)
+            rec = self.owner._pack(m, 0, self.cur_seq, 0, 0)
             if rec[9] & (MT_F_REL1 | MT_F_REL2):
                 raise UnsupportedOp("local op with relative positions")
             self.local = True
@@ -641,6 +643,7 @@ class MergeTreeStreamBuilder:
         min_seq = int(md.get("minSequenceNumber", seq))
         d = _DocBuilder(self, observer)
         d.min_seq = min_seq  # the loaded tree's minSeq (loadCore → MergeTree.startCollaboration)
+        d.cur_seq = seq
         first = len(self.snapshot_segs)
         any_info = False
         for ci, c in enumerate(chunks):

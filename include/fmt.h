@@ -126,8 +126,11 @@ extern "C" {
  *   client.ts:273-355): INSERT / REMOVE / ANNOTATE with positions in the local view
  *   (LocalDefaultPerspective, perspective.ts:174-184), stamped {UnassignedSequenceNumber, 0,
  *   localSeq = ++localSeq}; its segments form a pending segment group (mergeTree.ts:1410-1447). No
- *   collab-window update, no zamboni; seq / ref_seq / min_seq are not read. An invalid range is
- *   FMT_E_USAGE (client.ts:797-810).
+ *   collab-window update, no zamboni; seq / min_seq are not read. ref_seq: the refSeq the op was
+ *   submitted at (SharedSegmentSequence.inFlightRefSeqs, sequence.ts:468-499, 666): while the op is
+ *   pending, every collab-window update of the document takes min(message minSeq, the oldest
+ *   pending op's ref_seq) (getMinInFlightRefSeq, client.ts:1374-1378); a regenerated op keeps the
+ *   original's (sequence.ts:782-790). An invalid range is FMT_E_USAGE (client.ts:797-810).
  * FMT_MT_F_ACK: a sequenced message of the local client (client.ts:1367-1368 ackPendingSegment →
  *   mergeTree.ts:1325-1408 ackOp): acknowledges the OLDEST pending group with {seq, 0}; type (and an
  *   ANNOTATE's props op, whose keys PropertiesManager.ack shifts, segmentPropertiesManager.ts:248-267)
@@ -576,6 +579,15 @@ int fmt_mt_fetch_numbers(fmt_ctx* ctx, uint32_t doc, double* out, uint32_t cap, 
  * what the legacy summary reads (snapshotlegacy.ts:211-212); the first min(n_leaves, cap). Without
  * annotate-adjust in the batch they are the leaves' own props. */
 int fmt_mt_fetch_legacy_props(fmt_ctx* ctx, uint32_t doc, uint16_t* out, uint32_t cap);
+/* f4: one document's regenerated ops after the last fmt_mt_run, what regeneratePendingOp returned at
+ * each FMT_MT_F_REGEN record in order (client.ts:1452-1542; replaces Client.regeneratePendingOp as the
+ * host's resubmit source). Each op: type, pos1 / pos2 in the reconnect view, seq = the pending op's
+ * localSeq, ref_seq = the document's currentSeq at the reconnect; an INSERT's payload / length (len +
+ * FMT_MT_F_LEN_HI bits) address `text`, its pos2 and FMT_MT_F_MARKER flag are the original op's; an
+ * ANNOTATE's payload is the original props op. *n_ops / *n_text = the counts, the first min(count,
+ * cap) copied. Zero without local records. */
+int fmt_mt_fetch_regen(fmt_ctx* ctx, uint32_t doc, fmt_mt_op* ops, uint32_t cap_ops, uint16_t* text, uint32_t cap_text,
+                       uint32_t* n_ops, uint32_t* n_text);
 /* Per-document 64-bit content digest of the converged state of the last fmt_mt_run (n_docs entries):
  * everything the reference's getText / summarize read back (MergeTreeTextHelper.ts:28-87,
  * snapshotlegacy.ts:195-262) — every leaf in document order with its stamps, remove-client set, length,

@@ -54,7 +54,7 @@ int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* ar
       // (loader segments: no collab-window update; a batch of them is not a GROUP message)
       if ((op.flags & FMT_MT_F_LOADSEG) == 0 &&
           (i + 1 == n || (ops[i + 1].flags & (FMT_MT_F_GROUP_CONT | FMT_MT_F_LOADSEG)) != FMT_MT_F_GROUP_CONT))
-        mt->updateSeqNumbers(op.min_seq, op.seq);
+        mt->updateSeqNumbers(std::min(op.min_seq, mt->minInflightRef()), op.seq);
     } catch (const orc::UsageError& e) {
       if (failSeq) *failSeq = op.seq;
       fail(e.what());

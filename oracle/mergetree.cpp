@@ -1028,6 +1028,7 @@ void MergeTree::applyLocal(const fmt_mt_op& op, const uint16_t* arena, const uin
   g->payload = static_cast<int32_t>(op.payload);
   g->pos2 = op.type == FMT_MT_INSERT ? op.pos2 : 0;
   g->flags = op.flags & FMT_MT_F_MARKER;
+  g->inflightRef = op.ref_seq;  // (the record's ref_seq: the refSeq it was submitted at)
 }
 
 // mergeTree.ts:149-215 ackSegment + :1325-1408 ackOp.
@@ -1284,6 +1285,7 @@ void MergeTree::regeneratePending(std::vector<fmt_mt_op>* out, std::u16string* t
       ng->payload = g->payload;
       ng->pos2 = g->pos2;
       ng->flags = g->flags;
+      ng->inflightRef = g->inflightRef;
       seg->groups.push_back(ng);
       ng->segments.push_back(seg);
       pendingSegments_.push_back(ng);

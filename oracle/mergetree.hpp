@@ -138,6 +138,9 @@ struct SegmentGroup {
   int32_t payload = 0;
   int32_t pos2 = 0;      // (insert: props-op id + 1 of the original op's seg props)
   uint32_t flags = 0;    // (insert: FMT_MT_F_MARKER)
+  // the refSeq its op was submitted at (SharedSegmentSequence.inFlightRefSeqs, sequence.ts:468-499,
+  // 666; a resubmitted op keeps its original one, :782-790)
+  int inflightRef = 0;
 };
 
 struct Seg : Node {
@@ -280,6 +283,9 @@ class MergeTree {
   // with payload = its offset there); squash is false (IDeltaHandler.reSubmit's default path).
   void regeneratePending(std::vector<fmt_mt_op>* out, std::u16string* text);
   size_t pendingGroups() const { return pendingSegments_.size(); }
+  // the oldest in-flight op's refSeq (none: INT_MAX): SharedSegmentSequence bounds every window update
+  // by it (getMinInFlightRefSeq, sequence.ts:499 → client.ts:1374-1378)
+  int minInflightRef() const { return pendingSegments_.empty() ? 0x7FFFFFFF : pendingSegments_.front()->inflightRef; }
   // REGEN events applied without an explicit output (orc_mt_apply_ops) collect their ops here
   std::vector<fmt_mt_op> regenOps;
   std::u16string regenText;

@@ -80,14 +80,47 @@ static void prepareNumbers(const fmt_mt_batch* b) {
 // ckpt (plain batches): per-document tier checkpoints; the compact tier saves, the small tier resumes
 // the documents whose header says kCkptEscalate and, with onlyEscalated, replays only those and the
 // documents that overflowed (the runtime's cascade over the overflow list).
-template <bool Ob, class C, bool Rm = false, bool Adj = false>
+// f4 (the local client): per-document slabs of the last emu_mt_replay_local (fixed capacities)
+constexpr uint32_t kEmuGroupCap = 4096, kEmuRecCap = 16384, kEmuRegenCap = 4096, kEmuRegenTextCap = 1 << 16,
+                   kEmuScratchCap = 1 << 16;
+static std::vector<uint32_t> g_lgroups, g_lrecs, g_lpm, g_lscratch, g_lregenCount;
+static std::vector<uint64_t> g_lgroupOffs, g_lrecOffs, g_lpmOffs, g_lscratchOffs, g_lregenOffs, g_lregenTextOffs;
+static std::vector<fmt_mt_op> g_lregen;
+static std::vector<uint16_t> g_lregenText;
+static fmt_mt::LocalTables g_loc;
+
+static void prepareLocal(uint32_t nDocs) {
+  auto offs = [&](std::vector<uint64_t>& v, uint64_t cap) {
+    v.resize(nDocs + 1ull);
+    for (uint32_t d = 0; d <= nDocs; d++) v[d] = static_cast<uint64_t>(d) * cap;
+  };
+  g_lgroups.assign(static_cast<size_t>(nDocs) * kEmuGroupCap * 8, 0u);
+  g_lrecs.assign(static_cast<size_t>(nDocs) * kEmuRecCap * 2, 0u);
+  g_lpm.assign(static_cast<size_t>(nDocs) * kEmuPmCap * 4, 0u);
+  g_lscratch.assign(static_cast<size_t>(nDocs) * kEmuScratchCap, 0u);
+  g_lregen.assign(static_cast<size_t>(nDocs) * kEmuRegenCap, fmt_mt_op{});
+  g_lregenText.assign(static_cast<size_t>(nDocs) * kEmuRegenTextCap, 0u);
+  g_lregenCount.assign(2ull * nDocs, 0u);
+  offs(g_lgroupOffs, kEmuGroupCap);
+  offs(g_lrecOffs, kEmuRecCap);
+  offs(g_lpmOffs, kEmuPmCap);
+  offs(g_lscratchOffs, kEmuScratchCap);
+  offs(g_lregenOffs, kEmuRegenCap);
+  offs(g_lregenTextOffs, kEmuRegenTextCap);
+  g_loc = fmt_mt::LocalTables{g_lgroups.data(), g_lgroupOffs.data(), g_lrecs.data(), g_lrecOffs.data(),
+                              g_lpm.data(), g_lpmOffs.data(), g_lregen.data(), g_lregenOffs.data(),
+                              g_lregenText.data(), g_lregenTextOffs.data(), g_lregenCount.data(),
+                              g_lscratch.data(), g_lscratchOffs.data()};
+}
+
+template <bool Ob, class C, bool Rm = false, bool Adj = false, bool Loc = false>
 static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                      fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup,
                      fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* ckpt = nullptr,
                      bool onlyEscalated = false, size_t leafStride = 0, size_t charStride = 0,
                      const fmt_mt_leaf* smallLeaves = nullptr, const uint16_t* smallChars = nullptr,
                      uint16_t* legacy = nullptr) {
-  using Doc = fmt_mt::Doc<Ob, C, Rm, Adj>;
+  using Doc = fmt_mt::Doc<Ob, C, Rm, Adj, Loc>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
   int status = FMT_OK;
@@ -109,6 +142,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     in.markerKey = b->marker_id_key;
     in.adj = g_nums.empty() ? nullptr : &g_adj;
     in.doc = d;
+    in.loc = Loc ? &g_loc : nullptr;
     in.infoAll = b->snapshot_info;
     in.stampsAll = b->snapshot_stamps;
     in.nInfoAll = b->snapshot_info ? b->n_snapshot_segs : 0u;
@@ -314,6 +348,27 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   if (ob) return replayAll<true, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   if (rm) return replayAll<false, S, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
+}
+
+// f4 batches (local submissions, acks, rollbacks, reconnects): the large tier's Loc variant over every
+// document, as the runtime runs them (results at large strides).
+int emu_mt_replay_local(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                        fmt_mt_propset* props) {
+  g_nums.clear();
+  g_legacyStride = 0;
+  prepareLocal(b->n_docs);
+  return replayAll<false, fmt_mt::LargeTier, false, false, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0);
+}
+
+// Document d's regenerated ops (and their text) after the last emu_mt_replay_local: copies <= the
+// caps, returns the op count; *nText = the text units.
+int emu_mt_regen(uint32_t d, fmt_mt_op* ops, uint32_t capOps, uint16_t* text, uint32_t capText, uint32_t* nText) {
+  if (2ull * d + 1 >= g_lregenCount.size()) return -1;
+  const uint32_t n = g_lregenCount[2 * d], t = g_lregenCount[2 * d + 1];
+  for (uint32_t k = 0; k < n && k < capOps; k++) ops[k] = g_lregen[static_cast<size_t>(d) * kEmuRegenCap + k];
+  for (uint32_t k = 0; k < t && k < capText; k++) text[k] = g_lregenText[static_cast<size_t>(d) * kEmuRegenTextCap + k];
+  *nText = t;
+  return static_cast<int>(n);
 }
 
 // Document d's legacy prop sets (getAtSeq at minSeq, per leaf) after the last emu_mt_replay of a batch

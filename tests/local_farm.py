@@ -65,10 +65,12 @@ def fixture_local_batch(stride=8, max_fixtures=None, clients=None):
 
 class _Participant:
     def __init__(self, farm: "LocalFarm", name: str):
-        from oracle.oracle import MergeTreeDoc
+        from oracle import MergeTreeDoc  # (oracle/oracle.py: tests put oracle/ on sys.path)
 
         self.farm = farm
         self.name = name
+        self.index = len(farm.b.docs)
+        farm.log.append((self.index, "begin", farm.initial, name))
         self.doc = farm.b.begin_doc(initial_text=farm.initial, observer=name)
         self.orc = MergeTreeDoc()
         if farm.initial:
@@ -107,6 +109,8 @@ class LocalFarm:
         self.seq = 0
         self.msn = 0
         self.inflight: list = []  # sent, not yet sequenced: [participant, op, ref, localSeq]
+        # every builder call, (doc index, method, args...): replayable per document (replay_log)
+        self.log: list = []
         self.parts = [_Participant(self, chr(ord("A") + i)) for i in range(n_clients)]
         self._arena_n = 0
         self._arena = np.zeros(0, dtype="<u2")
@@ -153,6 +157,7 @@ class LocalFarm:
 
     def submit(self, p: _Participant):
         op = self._gen_op(p)
+        self.log.append((p.index, "local_op", op))
         p.doc.local_op(op)
         p.local_seq += 1
         p.by_local_seq[p.local_seq] = op
@@ -169,6 +174,7 @@ class LocalFarm:
         msg = {"clientId": p.name, "sequenceNumber": self.seq, "referenceSequenceNumber": ref,
                "minimumSequenceNumber": self.msn, "type": "op", "contents": op}
         for q in self.parts:
+            self.log.append((q.index, "add_message", msg))
             q.doc.add_message(msg)
             q.cur_seq = self.seq
         p.pending.pop(0)
@@ -183,6 +189,7 @@ class LocalFarm:
             return False
         self.inflight.pop()
         p.pending.pop()
+        self.log.append((p.index, "local_rollback"))
         p.doc.local_rollback()
         self.rollbacks += 1
         return True
@@ -198,10 +205,12 @@ class LocalFarm:
         self.inflight = [e for e in self.inflight if e[0] is not p]
         while self.inflight:
             self.sequence_one()
+        self.log.append((p.index, "local_regen"))
         p.doc.local_regen()  # (the REGEN record; the pending ops follow once the oracle made them)
         p.sync()
         recs, text = p.orc.regen_take()
         new_ops = [self._regen_op(p, r, text) for r in recs]
+        self.log.append((p.index, "regen_pending", new_ops))
         p.doc.regen_pending(new_ops)
         p.pending = []
         for r, op in zip(recs, new_ops):
@@ -254,6 +263,25 @@ class LocalFarm:
             p.sync()
             out.append(p.orc.text())
         return out
+
+
+def farm_log(farms) -> list:
+    """The builder calls of the farms, document by document (each document's own calls in order):
+    what a packer that writes documents contiguously (js/fmt.js) replays."""
+    log = [e for f in farms for e in f.log]
+    return sorted(log, key=lambda e: e[0])  # (stable: each document keeps its order)
+
+
+def replay_log(log, builder=None) -> MergeTreeStreamBuilder:
+    """The calls of farm_log on a (fresh) Python builder."""
+    b = builder if builder is not None else MergeTreeStreamBuilder()
+    docs = {}
+    for e in log:
+        if e[1] == "begin":
+            docs[e[0]] = b.begin_doc(initial_text=e[2], observer=e[3])
+        else:
+            getattr(docs[e[0]], e[1])(*e[2:])
+    return b
 
 
 def local_farm_batch(seeds, steps=300, **kw):

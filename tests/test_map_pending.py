@@ -199,7 +199,7 @@ def test_pending_event_cap_per_document(orc):
     assert list(status) == [0, -3, 0]
     assert counts[1] == 0
     assert counts[0] == exp[0][0] and counts[2] == exp[0][2]
-    off = np.concatenate([[0], np.cumsum(counts)])
-    eoff = np.concatenate([[0], np.cumsum(exp[0])])
+    off = np.concatenate([[0], np.cumsum(counts, dtype=np.int64)])
+    eoff = np.concatenate([[0], np.cumsum(exp[0], dtype=np.int64)])
     for d in (0, 2):
         assert np.array_equal(entries[off[d]:off[d + 1]], exp[2][eoff[d]:eoff[d + 1]])

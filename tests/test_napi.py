@@ -45,7 +45,7 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert out["k"] == sorted(["open", "close", "openContexts", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
-                               "fetchRemoveOrder", "fetchNumbers", "fetchLegacyProps", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
+                               "fetchRemoveOrder", "fetchNumbers", "fetchLegacyProps", "fetchRegen", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
                                "summaryBlobs", "replayMap", "fetchDoc", "sizes"])
     assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
                         "catchupRange": 16, "mapEntry": 12, "adjust": 32}
@@ -544,3 +544,88 @@ def test_js_map_pending_view_on_gpu(addon, tmp_path):
     assert len(checks) == len(golden_checkpoints()[1])
     for view, step in checks:
         _check_assertion([tuple(x) for x in view], step)
+
+
+# ---- f4: the merge-tree local client (submissions, acks, rollbacks, reconnects) from JavaScript --
+
+_LOCAL_JS = (
+    "const fs=require('fs');const fmt=require(%s);const log=JSON.parse(fs.readFileSync(%s,'utf8'));"
+    "const b=new fmt.MergeTreeStreamBuilder();const docs={};"
+    "for(const e of log){const d=docs[e[0]];"
+    "if(e[1]==='begin')docs[e[0]]=b.beginDoc(e[2],e[3]);"
+    "else if(e[1]==='local_op')d.localOp(e[2]);else if(e[1]==='add_message')d.addMessage(e[2]);"
+    "else if(e[1]==='local_rollback')d.localRollback();else if(e[1]==='local_regen')d.localRegen();"
+    "else if(e[1]==='regen_pending')d.regenPending(e[2]);else throw new Error(e[1]);}"
+    "const batch=b.finish();")
+
+
+def _local_log(tmp_path, seeds=(3, 4), steps=300):
+    from local_farm import farm_log, local_farm_batch
+
+    _, farms = local_farm_batch(seeds, steps=steps)
+    log = farm_log(farms)
+    path = tmp_path / "local_log.json"
+    path.write_text(json.dumps(log))
+    return log, path
+
+
+def test_js_packer_local_client_matches_python(addon, tmp_path):
+    """fmt.js packs the local client's events (localOp / acks / localRollback / localRegen) into the
+    same records as streams.py (tests/local_farm.py farms, documents written contiguously)."""
+    from local_farm import replay_log
+
+    log, path = _local_log(tmp_path)
+    script = tmp_path / "local_pack.js"
+    script.write_text(_LOCAL_JS % (json.dumps(os.path.join(PKG, "js", "fmt.js")), json.dumps(str(path))) +
+                      "const hex=(a)=>Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
+                      "process.stdout.write(JSON.stringify({ops:hex(batch.ops),text:hex(batch.text),"
+                      "po:Array.from(batch.propsOff),kv:Array.from(batch.propsKv),keys:batch.keys,values:batch.values}));")
+    r = _node(str(script))
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    py = replay_log(log).finish()
+    from fluidframework_amd.streams import MT_F_ACK, MT_F_REGEN, MT_F_ROLLBACK
+
+    f = py.ops["flags"]
+    assert ((f & MT_F_ACK) != 0).sum() > 50 and ((f & MT_F_ROLLBACK) != 0).any() and ((f & MT_F_REGEN) != 0).any()
+    assert bytes.fromhex(out["ops"]) == py.ops.tobytes()
+    assert bytes.fromhex(out["text"]) == py.text.tobytes()
+    assert out["po"] == py.props_off.tolist() and out["kv"] == py.props_kv.tolist()
+    assert out["keys"] == py.keys and out["values"] == py.values
+
+
+@pytest.mark.gpu
+def test_js_local_client_replay_and_regenerated_ops_on_gpu(addon, orc, tmp_path):
+    """The JS driver replays the local farms on the GPU: every participant's local view equals the
+    oracle's, and MergeTreeReplay.regenerated(doc) gives the ops the farm resubmitted (the oracle's
+    regeneratePendingOp restatement) as IMergeTree*Msg objects."""
+    from local_farm import replay_log
+    from mt_compare import emu_caps, visible_text
+
+    log, path = _local_log(tmp_path)
+    script = tmp_path / "local_gpu.js"
+    script.write_text("(async()=>{" + _LOCAL_JS % (json.dumps(os.path.join(PKG, "js", "fmt.js")), json.dumps(str(path))) +
+                      "const e=new fmt.Engine(0);const r=await e.replayMergeTree(batch);const out=[];"
+                      "for(let d=0;d<batch.nDocs;d++){const h=r.header(d);const segs=h.status===0?r.segments(d):[];"
+                      "out.push({status:h.status,text:segs.filter((s)=>s.removedSeq===undefined&&!s.marker)"
+                      ".map((s)=>s.text).join(''),regen:r.regenerated(d)});}"
+                      "e.close();process.stdout.write(JSON.stringify(out));"
+                      "})().catch((e)=>{console.error(e);process.exit(1);});")
+    r = _node(str(script), timeout=300)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    py = replay_log(log).finish()
+    cl, cc, cp = emu_caps(True)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(py, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
+    assert rc == 0 and len(got) == py.n_docs
+    regen = {}
+    for e in log:
+        if e[1] == "regen_pending":
+            regen.setdefault(e[0], []).extend(e[2])
+    n = 0
+    for d, g in enumerate(got):
+        assert g["status"] == 0, f"doc {d}"
+        assert g["text"] == visible_text(oh[d], ol[d], oc[d]), f"doc {d}"
+        assert [x["op"] for x in g["regen"]] == regen.get(d, []), f"doc {d}"
+        n += len(g["regen"])
+    assert n > 10
