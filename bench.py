@@ -677,6 +677,11 @@ def bench_t3(args, rank, world, local_rank, dist):
                                 seed=args.seed)
     if args.t3_summary == "legacy":
         batch = workloads.as_legacy_load(batch)
+    from fluidframework_amd.streams import MT_F_CATCHUP, flag_catchup
+
+    # the summary's catchupOps blob: the engine records the delta ranges of the ops above the final
+    # minSeq whose refSeq trails (sequence.ts:949-1018); only the last window's ops are flagged
+    flag_catchup(batch.ops, batch.doc_op_offsets)
     n_ops = len(batch.ops)
     log(rank, f"[bench] t3: generated {args.segments} segments + {n_ops} ops in {time.time() - t:.1f}s")
     eng = native.Engine(local_rank)
@@ -724,6 +729,32 @@ def bench_t3(args, rank, world, local_rank, dist):
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     prof = eng.huge_profile(0)
     log(rank, f"[bench] t3 phase clocks per op: " + ", ".join(f"{k} {v / n_ops:.0f}" for k, v in prof.items()))
+    # Summary emission of the replayed document (SharedString.summarizeCore, legacy format:
+    # snapshotlegacy.ts:126-193 + the catchupOps blob, sequence.ts:949-964), timed on its own:
+    # the device merge of the segment runs, host JSON, the catch-up ranges' fetch and their messages.
+    import hashlib
+
+    from fluidframework_amd import summary as fsum
+    from fluidframework_amd.streams import op_messages
+
+    names = batch.clients[0] if batch.clients else [f"client-{k}" for k in range(64)]
+    min_seq = int(hdrs[0]["min_seq"])
+    t = time.perf_counter()
+    stiming = eng.mt_summarize_legacy(batch.keys, batch.values)
+    head, body = eng.mt_summary(0)
+    cu = eng.mt_catchup(0, hdrs[0])
+    msgs = op_messages(batch, 0, min_seq, names)
+    cblob = fsum.catchup_blob(fsum.catchup_messages(msgs, cu, min_seq))
+    sum_s = time.perf_counter() - t
+    blob_hash = hashlib.sha256("\x00".join([head, body or "", cblob or ""]).encode("utf-8")).hexdigest()[:16]
+    t3_summary = {"seconds": sum_s, "kernel_ms": stiming["kernel_ms"], "fetch_ms": stiming["fetch_ms"],
+                  "format_ms": stiming["format_ms"], "header_bytes": len(head), "body_bytes": len(body or ""),
+                  "catchup_bytes": len(cblob or ""), "catchup_ops": int(((batch.ops["flags"] & MT_F_CATCHUP) != 0).sum()),
+                  "catchup_ranges": int(len(cu)), "sha16": blob_hash,
+                  "what": "legacy summary (header + body at minSeq, snapshotlegacy.ts:126-193) + catchupOps "
+                          "(sequence.ts:949-1018) of the 10M-segment document, after the timed replay"}
+    log(rank, f"[bench] t3 summary: {sum_s:.2f}s, header {len(head)} B, body {len(body or '')} B, "
+              f"catchup {len(cblob or '')} B ({len(cu)} ranges), sha {blob_hash}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -749,19 +780,32 @@ def bench_t3(args, rank, world, local_rank, dist):
         import threading
 
         res = {}
-        th = threading.Thread(target=lambda: res.update(r=oracle.mt_replay_digest(batch, threads=1)))
+
+        def full():
+            try:
+                res["r"] = oracle.mt_replay_full(batch, 0, batch.keys, batch.values)
+            except Exception as e:  # (reported below)
+                res["e"] = e
+        th = threading.Thread(target=full)
         th.start()
         while th.is_alive():  # (ctypes releases the GIL; progress lines keep the job runner from calling it hung)
             th.join(30.0)
             if th.is_alive():
                 log(rank, f"[bench] t3 oracle check: still running after {time.time() - t:.0f}s")
-        rc, odig, ost, _ = res["r"]
         oracle.set_index(False)
-        t3_check = {"equal": bool(rc == 0 and int(odig[0]) == int(gpu_dig[0])), "oracle_rc": int(rc),
-                    "gpu_digest": f"{int(gpu_dig[0]):016x}", "oracle_digest": f"{int(odig[0]):016x}",
+        if "e" in res:
+            raise SystemExit(f"t3: oracle replay failed: {res['e']}")
+        odig, ohead, obody, ocu = res["r"]
+        oblob = fsum.catchup_blob(fsum.catchup_messages(msgs, ocu, min_seq))
+        t3_check = {"equal": bool(int(odig) == int(gpu_dig[0])), "oracle_rc": 0,
+                    "gpu_digest": f"{int(gpu_dig[0]):016x}", "oracle_digest": f"{int(odig):016x}",
+                    "summary_equal": bool(ohead == head and obody == body and oblob == cblob),
+                    "catchup_ranges_equal": bool(len(ocu) == len(cu) and (len(cu) == 0 or bool((ocu == cu).all()))),
                     "oracle_s": time.time() - t,
                     "what": "state digest (every leaf field, props by value, text, header; DESIGN.md §2) of the whole "
-                            "replayed document, GPU vs the oracle's own full replay"}
+                            "replayed document and its legacy summary + catchupOps blobs, GPU vs the oracle's own "
+                            "full replay (one replay) and its SnapshotLegacy restatement"}
+        t3_check["equal"] = t3_check["equal"] and t3_check["summary_equal"] and t3_check["catchup_ranges_equal"]
         log(rank, f"[bench] t3 oracle check: {t3_check}")
         if not t3_check["equal"]:
             raise SystemExit(f"t3: GPU state differs from the oracle's: {t3_check}")
@@ -788,6 +832,7 @@ def bench_t3(args, rank, world, local_rank, dist):
                          "bytes_per_launch": bytes_per_launch, "avg_kernel_ms": avg_kernel_ms},
             "cpu_baseline": cpu,
             "t3_oracle_check": t3_check,
+            "t3_summary": t3_summary,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
             "phase_clocks_per_op": {k: v / n_ops for k, v in prof.items() if k not in ("text_compactions", "merge_units_in_use")},
             "merge_area": {"compactions": prof.get("text_compactions"), "units_in_use": prof.get("merge_units_in_use")},

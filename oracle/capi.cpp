@@ -533,6 +533,67 @@ int orc_mt_replay_summary(const fmt_mt_batch* b, uint32_t d, const char* const* 
   return orc_mt_summary(&mt, keys, nKeys, values, nValues, chunkSize, out, cap, headerLen, bodyLen);
 }
 
+// Document d of a batch replayed ONCE (a T3 document takes minutes): its state digest, legacy
+// summary blobs and catch-up ranges, kept until the next call and read with orc_mt_full_take.
+namespace {
+struct FullResult {
+  std::string blobs;
+  int headerLen = 0, bodyLen = 0;
+  std::vector<fmt_mt_catchup_range> cu;
+  uint64_t digest = 0;
+  int32_t minSeq = 0;
+};
+FullResult g_full;
+}  // namespace
+
+int orc_mt_replay_full(const fmt_mt_batch* b, uint32_t d, const char* const* keys, int nKeys, const char* const* values,
+                       int nValues, int chunkSize, uint64_t* digest, int* headerLen, int* bodyLen, uint32_t* nCatchup) {
+  g_full = FullResult{};
+  MergeTree mt;
+  const auto hn = hostNumbers(b);
+  startDoc(mt, b, d, &hn);
+  const uint64_t o0 = b->doc_op_offsets[d], o1 = b->doc_op_offsets[d + 1];
+  int32_t fs = 0;
+  const int st = applyOps(&mt, b->ops + o0, o1 - o0, b->text, b->props_off, b->props_kv, &fs, &g_full.cu);
+  if (st != FMT_OK) return st;
+  {
+    fmt_mt_doc_result h{};
+    std::vector<const orc::Seg*> segs;
+    std::vector<int> blockOf;
+    int nb = 0, dp = 0;
+    mt.collectLeaves(segs, blockOf, &nb, &dp);
+    std::vector<fmt_mt_leaf> lv(segs.size() + 1);
+    size_t units = 0;
+    for (const orc::Seg* s : segs) units += static_cast<size_t>(s->len());
+    std::vector<uint16_t> ch(units + 1);
+    std::vector<fmt_mt_propset> pr(segs.size() * (FMT_MT_PROPS_KEYS_MAX / FMT_MT_PROPS_MAX) + 1);
+    dumpDoc(&mt, &h, lv.data(), static_cast<uint32_t>(lv.size()), ch.data(), static_cast<uint32_t>(ch.size()), pr.data(),
+            static_cast<uint32_t>(pr.size()));
+    h.status = st;
+    h.fail_seq = fs;
+    g_full.digest = digestOf(h, lv.data(), ch.data(), pr.data());
+    g_full.minSeq = h.min_seq;
+  }
+  int hl = 0, bl = 0;
+  const int n = orc_mt_summary(&mt, keys, nKeys, values, nValues, chunkSize, nullptr, 0, &hl, &bl);
+  if (n < 0) return n;
+  g_full.blobs.resize(static_cast<size_t>(n));
+  orc_mt_summary(&mt, keys, nKeys, values, nValues, chunkSize, g_full.blobs.data(), n, &hl, &bl);
+  g_full.headerLen = hl;
+  g_full.bodyLen = bl;
+  if (digest) *digest = g_full.digest;
+  if (headerLen) *headerLen = hl;
+  if (bodyLen) *bodyLen = bl;
+  if (nCatchup) *nCatchup = static_cast<uint32_t>(g_full.cu.size());
+  return FMT_OK;
+}
+
+// The blobs (header then body) and catch-up ranges of the last orc_mt_replay_full.
+void orc_mt_full_take(char* blobs, fmt_mt_catchup_range* cu) {
+  if (blobs) std::memcpy(blobs, g_full.blobs.data(), g_full.blobs.size());
+  if (cu && !g_full.cu.empty()) std::memcpy(cu, g_full.cu.data(), g_full.cu.size() * sizeof(fmt_mt_catchup_range));
+}
+
 int orc_mt_removers(const fmt_mt_batch* b, uint32_t d, int32_t* out, uint32_t cap) {
   MergeTree mt;
   const auto hn = hostNumbers(b);

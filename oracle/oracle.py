@@ -49,6 +49,8 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_replay_timed.argtypes = [P, ctypes.c_uint32, ctypes.c_uint64, P, P, P, P, P, ctypes.c_uint32, P,
                                           ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_set_index.argtypes = [ctypes.c_int]
+        L.orc_mt_replay_full.argtypes = [P, ctypes.c_uint32, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, P, P, P]
+        L.orc_mt_full_take.argtypes = [P, P]
         L.orc_mt_replay_digest.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P, P, P]
         L.orc_state_digest.argtypes = [P, P, P, P]
         L.orc_state_digest.restype = ctypes.c_uint64
@@ -268,6 +270,28 @@ def mt_replay_summary(batch, doc: int, keys, values, chunk_size: int = 10000):
     del keep
     raw = buf.raw[:n]
     return raw[: hl.value].decode("utf-8"), (raw[hl.value:].decode("utf-8") if bl.value else None)
+
+
+def mt_replay_full(batch, doc: int, keys, values, chunk_size: int = 10000):
+    """Document `doc` replayed ONCE by the oracle: (state digest, legacy header, body or None, catch-up
+    ranges of its FMT_MT_F_CATCHUP ops, final minSeq is in the digest's header). Raises on failure."""
+    from fluidframework_amd.native import CATCHUP_DTYPE, batch_struct
+
+    kk, vv = _cstrs(keys), _cstrs(values)
+    b, keep = batch_struct(batch)
+    dig = ctypes.c_uint64(0)
+    hl, bl, ncu = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_uint32(0)
+    rc = lib().orc_mt_replay_full(ctypes.byref(b), doc, kk, len(keys), vv, len(values), chunk_size, ctypes.byref(dig),
+                                  ctypes.byref(hl), ctypes.byref(bl), ctypes.byref(ncu))
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"oracle replay failed ({rc}): {lib().orc_last_error().decode()}")
+    buf = ctypes.create_string_buffer(hl.value + bl.value + 1)
+    cu = np.zeros(max(ncu.value, 1), dtype=CATCHUP_DTYPE)
+    lib().orc_mt_full_take(buf, _ptr(cu))
+    raw = buf.raw[: hl.value + bl.value]
+    return (int(dig.value), raw[: hl.value].decode("utf-8"), raw[hl.value:].decode("utf-8") if bl.value else None,
+            cu[: ncu.value])
 
 
 def set_index(on: bool):
