@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--t2-check-docs", type=int, default=1024,
                     help="t2: documents of every shard replayed by the oracle and compared by state digest")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed (nccl = RCCL) even at one rank, so the gathers go over RCCL")
     ap.add_argument("--no-js-baseline", action="store_true", help="skip the JS worker_threads baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline pool (0 = every usable host core)")
     args = ap.parse_args()
@@ -116,7 +118,7 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:  # (--dist: the RCCL path at one rank too, e.g. on a one-GPU box)
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))

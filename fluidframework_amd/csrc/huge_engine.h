@@ -228,6 +228,10 @@ struct HugeInputs {
   // remove stamps its rows index (specToSegment, snapshotLoader.ts:105-175)
   const fmt_mt_snapshot_info* info;
   const fmt_mt_stamp* stamps;
+  // the batch's whole merge-info table: V1 body-chunk segments with merge info arrive as
+  // FMT_MT_F_LOADSEG insert ops naming a row of it (nullptr: none in the batch)
+  const fmt_mt_snapshot_info* infoAll;
+  uint64_t nInfoAll;
   // catch-up ranges of FMT_MT_F_CATCHUP ops (the document's slab; nullptr: the batch records none)
   fmt_mt_catchup_range* catchup;
   uint32_t catchupCap;
@@ -1837,16 +1841,28 @@ class HugeDocT {
   // insertSegments (mergeTree.ts:1484-1517): ensureIntervalBoundary(p) then the inserting walk, both
   // from one search: the new leaf goes before the first qualifying leaf at p, or before the right part
   // of the leaf that strictly contained p.
-  FMT_DEV void insertText(const fmt_mt_op& op) {
+  // A body-chunk segment's stamps (loadBodySegment): its insert client, whether its insertSegments
+  // call splits at the position (the first of a batch), and specToSegment's remove stamps folded.
+  struct LoadStamp {
+    int client;
+    bool boundary;
+    int32_t rm;
+    uint32_t mlo, mhi, firstRm;
+    bool moreRm;
+  };
+  FMT_DEV void insertText(const fmt_mt_op& op, const LoadStamp* ld = nullptr) {
     ProfScope ps_(prof[12]);
-    const int r = op.ref_seq, c = op.client, p = op.pos1;
+    const int r = op.ref_seq, c = ld ? ld->client : op.client, p = op.pos1;
     const Hit h = find(p, r, c);
     uint32_t b;
     int k;
     BlockRegs R;
     R.b = kNone;
     if (h.found) {
-      if (h.st < p) {
+      if (h.st < p && ld != nullptr && !ld->boundary) {  // (a loader batch's later segment: before the leaf holding p)
+        b = h.blk;
+        k = h.k;
+      } else if (h.st < p) {
         if (!splitLeaf(R, h.blk, h.k, p - h.st, nullptr, &b, &k)) return;
       } else {
         b = h.blk;
@@ -1895,17 +1911,29 @@ class HugeDocT {
     Leaf x;
     x.len = opLen;
     x.ins = op.seq;
-    x.rm = kNotRemoved;
-    x.mlo = x.mhi = 0;
+    x.rm = ld ? ld->rm : kNotRemoved;
+    x.mlo = ld ? ld->mlo : 0u;
+    x.mhi = ld ? ld->mhi : 0u;
     x.id = nextId++;
     x.text = op.payload;
     x.meta = mkMeta(c, insProps) | ((op.flags & FMT_MT_F_MARKER) != 0 ? kMetaMarker : 0u);
-    const uint32_t wx = winAdd(x.id, x.ins, x.rm, x.len, mkMeta(c, 0) & 0xFFu, R.g, b);
+    // a window entry unless every stamp is at or below minSeq (a loaded segment can be: its length
+    // is then the same in every perspective and goes to the stable sums)
+    const bool win = x.ins > minSeq || (x.rm != kNotRemoved && x.rm > minSeq);
+    uint32_t wx = kNone;
+    if (win) {
+      const uint32_t wm = (mkMeta(c, 0) & 0xFFu) | (ld ? (ld->firstRm << 8) | (ld->moreRm ? 1u << 16 : 0u) : 0u);
+      wx = winAdd(x.id, x.ins, x.rm, x.len, wm, R.g, b, x.mlo, x.mhi);
+    } else {
+      st1(S.winIdx + x.id, kNone);
+    }
     if ((op.flags & FMT_MT_F_MARKER) != 0) markerAdd(x.id);
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);
     const uint32_t nb = commitBlock(R);
     if (status != FMT_OK) return;
+    // (a block split recounts both halves' stable sums from the registers)
+    if (!win && nb == kNone && x.rm == kNotRemoved) addStable(b, static_cast<int>(x.len));
     if (obStartN > 0) obliterateOnInsert(x.id, r, c);
     if (status != FMT_OK) return;
     lru(nb != kNone && k >= kMaxNodes / 2 ? nb : b, x.id, op.seq);
@@ -1915,6 +1943,49 @@ class HugeDocT {
       locate(x.id, &xb, &xk);
       if (ldi(S.lRm + li(xb, xk)) == kNotRemoved) cuPush(x.id);
     }
+  }
+
+  // SnapshotLoader.loadBody's append of one body-chunk segment (FMT_MT_F_LOADSEG,
+  // snapshotLoader.ts:277-309; mt_engine.h loadBodySegment): insertSegments at the local length
+  // (every leaf not removed) from PriorPerspective(UniversalSequenceNumber, client) with stamp
+  // {seq, client}, a batch of universal segments splitting only at its first; the segment keeps
+  // specToSegment's remove stamps (the batch's merge-info row op.pos1, snapshotLoader.ts:105-175).
+  FMT_DEV void loadBodySegment(const fmt_mt_op& op) {
+    if (in.infoAll == nullptr || in.stamps == nullptr || op.pos1 < 0 || static_cast<uint64_t>(op.pos1) >= in.nInfoAll) {
+      fail(FMT_E_DATA);
+      return;
+    }
+    LoadStamp ld;
+    ld.client = op.client == FMT_MT_CLIENT_NONCOLLAB ? FMT_NON_COLLAB_CLIENT : static_cast<int>(op.client);
+    ld.boundary = (op.flags & FMT_MT_F_GROUP_CONT) == 0;
+    ld.rm = kNotRemoved;
+    ld.firstRm = 0;
+    uint64_t mask = 0;
+    const fmt_mt_snapshot_info inf = in.infoAll[op.pos1];
+    for (uint32_t t = 0; t < inf.rm_count; t++) {
+      const fmt_mt_stamp st = in.stamps[inf.rm_first + t];
+      const int sc = uni(st.client);
+      if (sc < 0 || sc > 63) {
+        fail(FMT_E_UNSUPPORTED);
+        return;
+      }
+      if (uni(st.seq) < ld.rm) {
+        ld.rm = uni(st.seq);
+        ld.firstRm = static_cast<uint32_t>(sc);
+      }
+      mask |= 1ull << sc;
+    }
+    ld.mlo = static_cast<uint32_t>(mask);
+    ld.mhi = static_cast<uint32_t>(mask >> 32);
+    ld.moreRm = __builtin_popcountll(mask) > 1;
+    invalidate();
+    groupCorrections(kLocalSeq, ld.client);  // the local length: every leaf not removed
+    const int local = totalView();
+    invalidate();
+    fmt_mt_op o = op;
+    o.pos1 = local;
+    o.ref_seq = 0;
+    insertText(o, &ld);
   }
 
   // View lengths of the leaves of block b (lane k = leaf k) from PriorPerspective(r, c).
@@ -3694,7 +3765,7 @@ class HugeDocT {
           if (LANE(op) == id) {
             const uint32_t x = base + l;
             const size_t i = li(x >> 3, static_cast<int>(x & 7));
-            S.lMeta[i] = mkMeta(in.initClient, lastSet) | (rd(S.lMeta + i) & kMetaMarker);
+            S.lMeta[i] = (rd(S.lMeta + i) & (0xFFu | kMetaMarker)) | (lastSet << 8);  // (the insert client stays)
             LANE(op) = FMT_MT_NO_PROPS;
           }
         }
@@ -3747,7 +3818,11 @@ class HugeDocT {
       rmKind = op.type == FMT_MT_REMOVE ? FMT_MT_RM_SET : FMT_MT_RM_SLICE;
       rmHitN = 0;
       opIdx = static_cast<uint32_t>(i - in.begin);
-      if (op.client > 63) fail(FMT_E_UNSUPPORTED);
+      const bool loader = (op.flags & FMT_MT_F_LOADSEG) != 0;
+      if (loader) {
+        if (op.type != FMT_MT_INSERT || (op.client > 63 && op.client != FMT_MT_CLIENT_NONCOLLAB)) fail(FMT_E_UNSUPPORTED);
+        else loadBodySegment(op);
+      } else if (op.client > 63) fail(FMT_E_UNSUPPORTED);
       else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) != 0 && !resolveRelative(op)) {
       } else if (op.type == FMT_MT_INSERT) insertText(op);
       else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
@@ -3764,7 +3839,9 @@ class HugeDocT {
         if ((rmPendN > 0 || rmHitN > 0) && status == FMT_OK) rmFlush(op.client, op.seq);
       }
       cuRec = rmRec = false;
-      const bool lastMember = i + 1 == in.end || (readlane(rec0, 7) & FMT_MT_F_GROUP_CONT) == 0;
+      // (a loader segment updates no collab window; a batch of them is no GROUP message)
+      const bool lastMember =
+          !loader && (i + 1 == in.end || (readlane(rec0, 7) & (FMT_MT_F_GROUP_CONT | FMT_MT_F_LOADSEG)) != FMT_MT_F_GROUP_CONT);
       for (int z = 0; z < 2 && status == FMT_OK; z++) {
         if (z == 1) {
           if (!lastMember) break;

@@ -188,6 +188,7 @@ struct fmt_ctx {
   // they hold nothing it does not (mtHugeOk: no SnapshotV1 body segments with merge info,
   // FMT_MT_F_LOADSEG); their starts
   std::vector<uint8_t> mtHugeOk;
+  std::vector<uint32_t> mtLoadSegs;          // per document: its FMT_MT_F_LOADSEG ops (V1 body segments)
   std::vector<uint8_t> mtSegProps;           // per document: a loaded segment has properties
   std::vector<uint64_t> mtDocChars;          // per document: start units + inserted units (its most text)
   std::vector<fmt_mt_snapshot_seg> mtStartSeg;  // per document: its initial text as one segment (len 0: none)
@@ -859,11 +860,11 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   I.segProps = c->mtSegProps.empty() ? 0u : c->mtSegProps[d];
   // SnapshotV1 merge info of a summary-loaded document's segments (header chunk)
   I.info = nullptr;
-  I.stamps = nullptr;
-  if (c->mtHasSnapInfo && c->mtSnapHost.size() > d && c->mtSnapHost[d].loaded) {
-    I.info = c->mtSnapInfo.p + c->mtSnapHost[d].first_seg;
-    I.stamps = c->mtSnapStamps.p;
-  }
+  I.stamps = c->mtHasSnapInfo ? c->mtSnapStamps.p : nullptr;
+  if (c->mtHasSnapInfo && c->mtSnapHost.size() > d && c->mtSnapHost[d].loaded) I.info = c->mtSnapInfo.p + c->mtSnapHost[d].first_seg;
+  // V1 body-chunk segments with merge info (FMT_MT_F_LOADSEG ops) name rows of the batch's table
+  I.infoAll = c->mtHasSnapInfo ? c->mtSnapInfo.p : nullptr;
+  I.nInfoAll = c->mtHasSnapInfo ? c->mtNSnapSegs : 0;
   // catch-up ranges go to the document's slab, as in the other tiers
   I.catchup = nullptr;
   I.catchupCap = 0;
@@ -1329,18 +1330,21 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   c->huge.clear();
   c->mtHugeSlot.assign(n, -1);
   c->mtHugeOk.assign(n, 1);
+  c->mtLoadSegs.assign(n, 0);
   c->mtSegProps.assign(n, 0);
   c->mtDocChars.assign(n, 0);
   c->mtStartSeg.assign(n, fmt_mt_snapshot_seg{0, 0, FMT_MT_NO_PROPS});
   parallelChunks(n, [&](uint64_t d0, uint64_t d1, unsigned) {
   for (uint64_t d = d0; d < d1; d++) {
-    uint8_t ok = 1;
+    uint8_t ok = 1;  // (the huge tier replays every feature a document of the other tiers may hold)
     uint64_t chars = 0;
+    uint32_t loadSegs = 0;
     for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
       const fmt_mt_op& op = b->ops[i];
       if (op.type == FMT_MT_INSERT) chars += fmt_mt_op_len(&op);
-      if (op.flags & FMT_MT_F_LOADSEG) ok = 0;
+      if (op.flags & FMT_MT_F_LOADSEG) loadSegs++;
     }
+    c->mtLoadSegs[d] = loadSegs;
     if (b->snapshots && b->snapshots[d].loaded) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
@@ -1380,8 +1384,11 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       uint64_t chars = 0;
       for (uint64_t k = sd.first_seg; k < sd.first_seg + sd.n_header + sd.n_body; k++)
         chars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
-      if (sd.n_header + sd.n_body <= big.leaves && chars <= big.chars) continue;
-      if (!c->mtHugeOk[d] || local) {  // (V1 body segments with merge info; local-client records)
+      // (a V1 summary with merge info brings its body as loader-segment ops: they count as loaded)
+      const uint64_t loaded = sd.n_header + sd.n_body + c->mtLoadSegs[d];
+      if (c->mtLoadSegs[d] > 0) chars = c->mtDocChars[d];
+      if (loaded <= big.leaves && chars <= big.chars) continue;
+      if (!c->mtHugeOk[d] || local) {  // (local-client records)
         refuse(d, FMT_E_UNSUPPORTED);
         continue;
       }

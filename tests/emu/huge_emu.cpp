@@ -170,6 +170,8 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   in.segProps = segProps ? 1u : 0u;
   in.info = loaded && b->snapshot_info != nullptr ? b->snapshot_info + sd.first_seg : nullptr;
   in.stamps = b->snapshot_stamps;
+  in.infoAll = b->snapshot_info;
+  in.nInfoAll = b->snapshot_info != nullptr ? b->n_snapshot_segs : 0;
   in.catchup = catchup;
   in.catchupCap = capCatchup;
   in.rmOrder = rmOrder;

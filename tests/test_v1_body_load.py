@@ -30,7 +30,7 @@ import pytest
 from churn import farm_messages
 from fluidframework_amd import summary, workloads
 from fluidframework_amd.streams import MergeTreeStreamBuilder
-from mt_compare import compare_doc, emu_caps, emu_replay, visible_text
+from mt_compare import compare_doc, emu_caps, emu_huge_replay, emu_replay, visible_text
 
 
 def _solo(seed, at_end, msn_lag):
@@ -211,5 +211,92 @@ def test_loader_segments_on_gpu(orc, reload_batch):
             if int(oh[d]["status"]) == 0:
                 lv, ch, pr = eng.mt_doc(d, hdrs[d])
                 assert not compare_doc((oh[d], ol[d], oc[d], op[d]), (hdrs[d], lv, ch, pr)), d
+    finally:
+        eng.close()
+
+
+def test_emulated_huge_tier_matches_oracle_on_loader_segments(orc, reload_batch):
+    """The huge tier (round 5) takes loader segments as the other tiers do: insertSegments at the local
+    length from PriorPerspective(UniversalSequenceNumber, client), the segment keeping its remove stamps
+    (huge_engine.h loadBodySegment). Emulated with its index invariants checked after every op, normal
+    and 16-slot groups: status, fail seq and state == the oracle's."""
+    batch, _, _ = reload_batch
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    for tiny in (False, True):
+        for d in range(batch.n_docs):
+            h, lv, ch, pr = emu_huge_replay(batch, d, tiny_groups=tiny)
+            assert int(h["status"]) == int(oh[d]["status"]) and int(h["fail_seq"]) == int(oh[d]["fail_seq"]), (tiny, d)
+            if int(oh[d]["status"]) == 0:
+                assert not compare_doc((oh[d], ol[d], oc[d], op[d]), (h, lv, ch, pr)), (tiny, d)
+
+
+def _many_segments(n, seed, rest=300):
+    """One writer appends n one-unit segments after a 12,000-unit prefix (minSeq 0: none merges, every
+    one keeps its merge info), then edits inside them: the V1 summary after the appends has a body of
+    about n segments with merge info, the messages after it continue the stream."""
+    rnd, msgs = random.Random(seed), []
+    for k in range(n):
+        msgs.append({"clientId": "solo", "sequenceNumber": k + 1, "referenceSequenceNumber": k,
+                     "minimumSequenceNumber": 0, "type": "op", "contents": {"pos1": 12000 + k, "seg": "abcdefgh"[k % 8], "type": 0}})
+    length = 12000 + n
+    for j in range(rest):
+        seq = n + j + 1
+        if rnd.random() < 0.3:
+            a = rnd.randint(12000, length - 3)
+            op = {"pos1": a, "pos2": a + 2, "type": 1}
+            length -= 2
+        else:
+            op = {"pos1": rnd.randint(12000, length), "seg": "x" * rnd.randint(1, 4), "type": 0}
+            length += len(op["seg"])
+        msgs.append({"clientId": "solo", "sequenceNumber": seq, "referenceSequenceNumber": seq - 1,
+                     "minimumSequenceNumber": 0, "type": "op", "contents": op})
+    return "Z" * 12000, msgs
+
+
+def _many_segments_batch(n, seed=31):
+    init, msgs = _many_segments(n, seed)
+    (head, bodies, rest), = _cut([(init, msgs)], n)
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc_from_summary(head, bodies)
+    for m in rest:
+        d.add_message(m)
+    batch = b.finish()
+    assert ((batch.ops["flags"] & 256) != 0).sum() > n // 2
+    return batch, init, msgs
+
+
+def test_emulated_huge_tier_loads_a_long_v1_body(orc):
+    """A V1 body of 2,500 segments with merge info, loaded and edited in the huge tier (emulated) ==
+    the oracle, whose text equals the unsummarized stream's."""
+    batch, init, msgs = _many_segments_batch(2500)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=16384, cap_chars=1 << 17, cap_props=1024)
+    assert rc == 0
+    h, lv, ch, pr = emu_huge_replay(batch, 0)
+    assert not compare_doc((oh[0], ol[0], oc[0], op[0]), (h, lv, ch, pr))
+    whole = MergeTreeStreamBuilder()
+    d = whole.begin_doc(init, observer="observer")
+    for m in msgs:
+        d.add_message(m)
+    rc2, wh, wl, wc, _, _ = orc.mt_replay_batch(whole.finish(), cap_leaves=16384, cap_chars=1 << 17, cap_props=1024)
+    assert visible_text(oh[0], ol[0], oc[0]) == visible_text(wh[0], wl[0], wc[0])
+
+
+@pytest.mark.gpu
+def test_long_v1_body_loads_in_the_huge_tier_on_gpu(orc):
+    """A V1 summary whose body holds 20,000 segments with merge info: past the large tier at load, so
+    the runtime routes it to the huge tier, whose loader segments replay it == the oracle."""
+    from fluidframework_amd import native
+
+    batch, _, _ = _many_segments_batch(20000)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, cap_leaves=65536, cap_chars=1 << 18, cap_props=1024)
+    assert rc == 0
+    eng = native.Engine(0)
+    try:
+        eng.mt_load(batch)
+        eng.mt_run()
+        hdrs = eng.mt_headers()
+        lv, ch, pr = eng.mt_doc(0, hdrs[0])
+        assert not compare_doc((oh[0], ol[0], oc[0], op[0]), (hdrs[0], lv, ch, pr))
+        assert eng.huge_profile(0)["replay"] > 0  # (it ran in the huge tier)
     finally:
         eng.close()
