@@ -166,6 +166,7 @@ FLAGS = {
     "mclause": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
     "bias100": ["-mllvm", "-amdgpu-schedule-metric-bias=100"],
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
+    "lines": ["-gline-tables-only"],  # (line tables only: the same code, for PC-sample attribution)
 }
 REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
         "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
