@@ -2,7 +2,8 @@
 //
 // A 64-bit fingerprint of everything the parity tests compare field by field (tests/mt_compare.py):
 // the header (status, collab window, counts, depth, visible length), every leaf in document order
-// (stamps, remove-client set, char offset, length, insert client, parent block ordinal, marker bit),
+// (stamps, remove-client set — tag 10 for short ids 64..127, only on leaves that have one — char
+// offset, length, insert client, parent block ordinal, marker bit),
 // each leaf's properties BY VALUE (document-local prop-set ids are not part of it) and the text. The
 // definition is an order-sensitive sum of mixed elements, so one wave per document
 // folds its leaves and units lane-parallel and reduces once:
@@ -67,6 +68,12 @@ __global__ __launch_bounds__(64 * kDigWaves) void stateDigestKernel(const fmt_mt
             const uint32_t w = V.props[L.props + k / FMT_MT_PROPS_MAX].kv[k % FMT_MT_PROPS_MAX];
             acc += k < FMT_MT_PROPS_MAX ? digElem(7, static_cast<uint64_t>(i) * 8 + k, w) : digElem(9, static_cast<uint64_t>(i) * 64 + k, w);
           }
+        }
+      }
+      if (V.rmHi != nullptr) {  // remove clients 64..127: leaves that have any
+        for (uint32_t i = lane; i < h.n_leaves; i += 64) {
+          const uint64_t hi = V.rmHi[i];
+          if (hi != 0) acc += digElem(10, i, hi);
         }
       }
       for (uint32_t u = lane; u < h.n_chars; u += 64) acc += digElem(8, u, V.chars[u]);

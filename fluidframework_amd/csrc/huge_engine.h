@@ -60,6 +60,7 @@ constexpr int kPropLds = 4096;        // match classes of the first sets cached 
 constexpr uint32_t kPropHash = 1u << 17;  // buckets per prop-set hash table (exact content, match class)
 constexpr int kPropWords = 1 + FMT_MT_PROPS_MAX;  // a prop set in HBM: n, kv[]
 constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
+constexpr int kMaxClient = 127;       // short client ids 0..127 (remove-client sets: two mask words + HugeState::hiMask)
 
 // Leaf meta word: insert client (int8) | prop set id << 8 (0xFFFF = properties undefined)
 FMT_DEV int32_t mClient(uint32_t m) { return static_cast<int32_t>(static_cast<int8_t>(m & 0xFFu)); }
@@ -175,6 +176,9 @@ struct HugeState {
   uint32_t* mkIds;    // [mkCap]: every marker leaf ever in the document, in insertion order (relative
   uint32_t mkCap;     //   positions; nullptr: the batch has none)
   uint32_t* outIdx;   // [idCap]: at output, leaf id -> output index (annotate-adjust batches; else nullptr)
+  // [idCap * 2]: per leaf id, the remove clients with short ids 64..127 (bit c - 64), beyond the two
+  // mask words every leaf and window entry carry (nullptr: the batch has no such client; zeroed)
+  uint32_t* hiMask;
 };
 
 // LDS state of the wave.
@@ -401,10 +405,42 @@ class HugeDocT {
   FMT_DEV static bool removedBy(uint32_t mlo, uint32_t mhi, int c) {
     return c < 32 ? ((mlo >> c) & 1u) != 0 : ((mhi >> (c - 32)) & 1u) != 0;
   }
-  // leaf length from PriorPerspective(r, c) (perspective.ts:80-93)
+  // leaf length from PriorPerspective(r, c) (perspective.ts:80-93), c < 64
   FMT_DEV static int visOf(uint32_t len, int32_t ins, int32_t rm, uint32_t mlo, uint32_t mhi, int32_t ic, int r, int c) {
     const bool present = (ins <= r || ic == c) && !(rm <= r || removedBy(mlo, mhi, c));
     return present ? static_cast<int>(len) : 0;
+  }
+  // ---- remove clients 64..127 (getOrAddShortClientId interns without bound, client.ts:831-855): a
+  // per-leaf-id side table; a perspective of such a client (wave-uniform c) reads it, others never do
+  FMT_DEV bool hiRemovedBy(uint32_t id, int c) const {
+    const uint32_t b = static_cast<uint32_t>(c - 64);
+    return ((rd(S.hiMask + 2 * static_cast<size_t>(id) + (b >> 5)) >> (b & 31u)) & 1u) != 0;
+  }
+  // PriorPerspective(r, c) of leaf `id` for any c (the mask words for c < 64, the side table above)
+  FMT_DEV int visAny(uint32_t len, int32_t ins, int32_t rm, uint32_t mlo, uint32_t mhi, int32_t ic, int r, int c,
+                     uint32_t id) const {
+    if (c < 64) return visOf(len, ins, rm, mlo, mhi, ic, r, c);
+    const bool present = (ins <= r || ic == c) && !(rm <= r || (S.hiMask != nullptr && hiRemovedBy(id, c)));
+    return present ? static_cast<int>(len) : 0;
+  }
+  FMT_DEV void hiSet(uint32_t id, int c) {  // (c in 64..127, S.hiMask present)
+    const uint32_t b = static_cast<uint32_t>(c - 64);
+    uint32_t* p = S.hiMask + 2 * static_cast<size_t>(id) + (b >> 5);
+    const uint32_t v = ldu(p) | (1u << (b & 31u));
+    st1(p, v);
+  }
+  FMT_DEV void hiPut(uint32_t id, uint32_t lo, uint32_t hi) {
+    FOR_LANES(l) {
+      if (l == 0) {
+        S.hiMask[2 * static_cast<size_t>(id)] = lo;
+        S.hiMask[2 * static_cast<size_t>(id) + 1] = hi;
+      }
+    }
+  }
+  FMT_DEV int hiCount(uint32_t id) const {
+    return S.hiMask == nullptr ? 0
+                               : __builtin_popcount(ldu(S.hiMask + 2 * static_cast<size_t>(id))) +
+                                     __builtin_popcount(ldu(S.hiMask + 2 * static_cast<size_t>(id) + 1));
   }
 
   FMT_DEV uint32_t allocBlk(uint32_t leaf) {
@@ -883,7 +919,9 @@ class HugeDocT {
             const uint32_t grp = x[3] >> kWGroupShift;
             if (only == kNone || grp == only) {
               const u32x2 mk = LANE(msk[u]);
-              v = static_cast<uint32_t>(winVis(static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, mk[0], mk[1], r, c));
+              v = c < 64 ? static_cast<uint32_t>(winVis(static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, mk[0], mk[1], r, c))
+                         : static_cast<uint32_t>(visAny(x[2], static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), 0u, 0u,
+                                                        mClient(x[3]), r, c, rd(S.wLeaf + w)));
               if (v && !bySlot) atomicAddLds(&L->gCorr[grp], static_cast<int>(v));
             }
           }
@@ -1108,7 +1146,8 @@ class HugeDocT {
       if (l < static_cast<int>(cnt)) {
         const size_t i = static_cast<size_t>(b) * 8 + l;
         const int32_t rm = rd(S.lRm + i);
-        v = static_cast<uint32_t>(visOf(rd(S.lLen + i), rd(S.lIns + i), rm, rd(S.lMlo + i), rd(S.lMhi + i), mClient(rd(S.lMeta + i)), r, c));
+        v = static_cast<uint32_t>(visAny(rd(S.lLen + i), rd(S.lIns + i), rm, rd(S.lMlo + i), rd(S.lMhi + i), mClient(rd(S.lMeta + i)), r, c,
+                                         c < 64 ? 0u : rd(S.lId + i)));
         sk = rm <= minSeq && !(b == lastBlk && l == static_cast<int>(cnt) - 1);
       }
       LANE(vis) = v;
@@ -1787,6 +1826,7 @@ class HugeDocT {
     regsInsert(R, k + 1, y, wy);
     st1(S.leafBlk + y.id, b);
     obRefsMove(x.id, y.id, o, -o);  // the right part takes the references at/after the split
+    if (S.hiMask != nullptr) hiPut(y.id, ldu(S.hiMask + 2 * static_cast<size_t>(x.id)), ldu(S.hiMask + 2 * static_cast<size_t>(x.id) + 1));
     if constexpr (Adj) {
       if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
     }
@@ -1847,7 +1887,7 @@ class HugeDocT {
     int client;
     bool boundary;
     int32_t rm;
-    uint32_t mlo, mhi, firstRm;
+    uint32_t mlo, mhi, hlo, hhi, firstRm;  // (hlo, hhi: remove clients 64..127)
     bool moreRm;
   };
   FMT_DEV void insertText(const fmt_mt_op& op, const LoadStamp* ld = nullptr) {
@@ -1928,6 +1968,7 @@ class HugeDocT {
       st1(S.winIdx + x.id, kNone);
     }
     if ((op.flags & FMT_MT_F_MARKER) != 0) markerAdd(x.id);
+    if (S.hiMask != nullptr) hiPut(x.id, ld ? ld->hlo : 0u, ld ? ld->hhi : 0u);
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);
     const uint32_t nb = commitBlock(R);
@@ -1960,12 +2001,12 @@ class HugeDocT {
     ld.boundary = (op.flags & FMT_MT_F_GROUP_CONT) == 0;
     ld.rm = kNotRemoved;
     ld.firstRm = 0;
-    uint64_t mask = 0;
+    uint64_t mask = 0, hmask = 0;
     const fmt_mt_snapshot_info inf = in.infoAll[op.pos1];
     for (uint32_t t = 0; t < inf.rm_count; t++) {
       const fmt_mt_stamp st = in.stamps[inf.rm_first + t];
       const int sc = uni(st.client);
-      if (sc < 0 || sc > 63) {
+      if (sc < 0 || sc > kMaxClient || (sc > 63 && S.hiMask == nullptr)) {
         fail(FMT_E_UNSUPPORTED);
         return;
       }
@@ -1973,11 +2014,14 @@ class HugeDocT {
         ld.rm = uni(st.seq);
         ld.firstRm = static_cast<uint32_t>(sc);
       }
-      mask |= 1ull << sc;
+      if (sc < 64) mask |= 1ull << sc;
+      else hmask |= 1ull << (sc - 64);
     }
     ld.mlo = static_cast<uint32_t>(mask);
     ld.mhi = static_cast<uint32_t>(mask >> 32);
-    ld.moreRm = __builtin_popcountll(mask) > 1;
+    ld.hlo = static_cast<uint32_t>(hmask);
+    ld.hhi = static_cast<uint32_t>(hmask >> 32);
+    ld.moreRm = __builtin_popcountll(mask) + __builtin_popcountll(hmask) > 1;
     invalidate();
     groupCorrections(kLocalSeq, ld.client);  // the local length: every leaf not removed
     const int local = totalView();
@@ -1995,8 +2039,8 @@ class HugeDocT {
       uint32_t v = 0;
       if (l < static_cast<int>(cnt)) {
         const size_t i = li(b, l);
-        v = static_cast<uint32_t>(visOf(rd(S.lLen + i), rd(S.lIns + i), rd(S.lRm + i), rd(S.lMlo + i), rd(S.lMhi + i),
-                                        mClient(rd(S.lMeta + i)), r, c));
+        v = static_cast<uint32_t>(visAny(rd(S.lLen + i), rd(S.lIns + i), rd(S.lRm + i), rd(S.lMlo + i), rd(S.lMhi + i),
+                                         mClient(rd(S.lMeta + i)), r, c, c < 64 ? 0u : rd(S.lId + i)));
       }
       LANE(vis) = v;
     }
@@ -2091,8 +2135,8 @@ class HugeDocT {
       FOR_LANES(l) {
         LANE(wi) = rd(S.winIdx + LANE(f[5]));
         LANE(vis) = l < static_cast<int>(cnt)
-                        ? static_cast<uint32_t>(visOf(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
-                                                      LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c))
+                        ? static_cast<uint32_t>(visAny(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
+                                                       LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c, LANE(f[5])))
                         : 0u;
       }
       int stableDelta = 0;
@@ -2142,7 +2186,8 @@ class HugeDocT {
       if (rmRec) rmPushHit(x.id);  // a later remove stamp (stamps.ts:144-158), recorded in rmFlush
     }
     if (c < 32) x.mlo |= 1u << c;
-    else x.mhi |= 1u << (c - 32);
+    else if (c < 64) x.mhi |= 1u << (c - 32);
+    else hiSet(x.id, c);
     putLeaf(b, j, x);
     invalidate();
     if (w == kNone) {  // a stable leaf enters the window: its length leaves the stable sums
@@ -2338,7 +2383,7 @@ class HugeDocT {
   FMT_DEV void obliterateOnInsert(uint32_t id, int refSeq, int client) {
     const int64_t k = ordOf(id);
     int minSeqOther = kNotRemoved, newestSeq = -1, newestClient = -1, firstCl = 0;
-    uint32_t mlo = 0, mhi = 0;
+    uint32_t mlo = 0, mhi = 0, hlo = 0, hhi = 0;
     bool any = false;
     for (int i = 0; i < obStartN; i++) {  // Obliterates.findOverlapping (:566-582)
       const int slot = obU(L->obStart, i);
@@ -2351,7 +2396,9 @@ class HugeDocT {
       if (ocl != client) {
         any = true;
         if (ocl < 32) mlo |= 1u << ocl;
-        else mhi |= 1u << (ocl - 32);
+        else if (ocl < 64) mhi |= 1u << (ocl - 32);
+        else if (ocl < 96) hlo |= 1u << (ocl - 64);
+        else hhi |= 1u << (ocl - 96);
         if (oseq < minSeqOther) {
           minSeqOther = oseq;
           firstCl = ocl;
@@ -2389,8 +2436,9 @@ class HugeDocT {
     st1(S.lRm + i, static_cast<int32_t>(minSeqOther));
     st1(S.lMlo + i, mlo);
     st1(S.lMhi + i, mhi);
+    if (S.hiMask != nullptr) hiPut(id, hlo, hhi);
     const uint32_t w = ldu(S.winIdx + id);  // (a new leaf: always a window entry)
-    const bool more = __builtin_popcount(mlo) + __builtin_popcount(mhi) > 1;
+    const bool more = __builtin_popcount(mlo) + __builtin_popcount(mhi) + __builtin_popcount(hlo) + __builtin_popcount(hhi) > 1;
     st1(wWord(w, 1), static_cast<uint32_t>(minSeqOther));
     st1(wWord3(w), (ldu(wWord3(w)) & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(firstCl) << 8) | (more ? 1u << 16 : 0u));
     st1(S.wMask + 2 * w, mlo);
@@ -2453,8 +2501,8 @@ class HugeDocT {
       FOR_LANES(l) {
         LANE(wi) = rd(S.winIdx + LANE(f[5]));
         LANE(vis) = l < static_cast<int>(cnt)
-                        ? static_cast<uint32_t>(visOf(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
-                                                      LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c))
+                        ? static_cast<uint32_t>(visAny(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
+                                                       LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c, LANE(f[5])))
                         : 0u;
       }
       int stableDelta = 0;
@@ -3561,7 +3609,7 @@ class HugeDocT {
             const fmt_mt_snapshot_seg sg = in.segs[j];
             const uint32_t len = sg.len & ~FMT_MT_SEG_MARKER;
             int32_t ins = 0, rm = kNotRemoved, client = in.initClient;
-            uint64_t mask = 0;
+            uint64_t mask = 0, hmask = 0;
             if (in.info != nullptr) {  // merge info: the insert stamp, the remove stamps folded
               const fmt_mt_snapshot_info inf = in.info[j];
               ins = inf.ins_seq;
@@ -3569,10 +3617,15 @@ class HugeDocT {
               for (uint32_t t = 0; t < inf.rm_count; t++) {
                 const fmt_mt_stamp st = in.stamps[inf.rm_first + t];
                 rm = st.seq < rm ? st.seq : rm;
-                if (st.client < 0 || st.client > 63) LANE(wideL) = true;
-                else mask |= 1ull << st.client;
+                if (st.client < 0 || st.client > kMaxClient || (st.client > 63 && S.hiMask == nullptr)) LANE(wideL) = true;
+                else if (st.client < 64) mask |= 1ull << st.client;
+                else hmask |= 1ull << (st.client - 64);
               }
-              if (client > 63) LANE(wideL) = true;
+              if (client > kMaxClient) LANE(wideL) = true;
+            }
+            if (S.hiMask != nullptr) {
+              S.hiMask[2 * static_cast<size_t>(j + 1)] = static_cast<uint32_t>(hmask);
+              S.hiMask[2 * static_cast<size_t>(j + 1) + 1] = static_cast<uint32_t>(hmask >> 32);
             }
             S.lLen[i] = len;
             S.lIns[i] = ins;
@@ -3722,7 +3775,7 @@ class HugeDocT {
           }
         }
         const uint32_t meta = (static_cast<uint32_t>(mClient(y.meta)) & 0xFFu) | (first << 8) |
-                              (__builtin_popcountll(mask) > 1 ? 1u << 16 : 0u);
+                              (__builtin_popcountll(mask) + hiCount(y.id) > 1 ? 1u << 16 : 0u);
         winAdd(y.id, y.ins, y.rm, y.len, meta, ldu(S.bGroup + b), b, y.mlo, y.mhi);
       }
     }
@@ -3820,9 +3873,9 @@ class HugeDocT {
       opIdx = static_cast<uint32_t>(i - in.begin);
       const bool loader = (op.flags & FMT_MT_F_LOADSEG) != 0;
       if (loader) {
-        if (op.type != FMT_MT_INSERT || (op.client > 63 && op.client != FMT_MT_CLIENT_NONCOLLAB)) fail(FMT_E_UNSUPPORTED);
+        if (op.type != FMT_MT_INSERT || (op.client > kMaxClient && op.client != FMT_MT_CLIENT_NONCOLLAB)) fail(FMT_E_UNSUPPORTED);
         else loadBodySegment(op);
-      } else if (op.client > 63) fail(FMT_E_UNSUPPORTED);
+      } else if (op.client > kMaxClient || (op.client > 63 && S.hiMask == nullptr)) fail(FMT_E_UNSUPPORTED);
       else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) != 0 && !resolveRelative(op)) {
       } else if (op.type == FMT_MT_INSERT) insertText(op);
       else if (op.type == FMT_MT_REMOVE || op.type == FMT_MT_ANNOTATE) {
@@ -3880,7 +3933,7 @@ class HugeDocT {
         long bl = 0;
         for (uint32_t j = 0; j < S.bCount[b]; j++) {
           const size_t i = li(b, static_cast<int>(j));
-          bl += visOf(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c);
+          bl += visAny(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c, S.lId[i]);
         }
         if (bl != L->sLen[s]) {
           std::fprintf(stderr, "seq %d: slot %u of group %u (block %u) view %ld, index %d (stable %d) r=%d c=%d minSeq=%d\n", seq, s, g, b, bl,
@@ -3890,7 +3943,7 @@ class HugeDocT {
             const uint32_t w = S.winIdx[S.lId[i]];
             std::fprintf(stderr, "  leaf id %u len %u ins %d rm %d mask %x:%x ic %d vis %d win %d", S.lId[i], S.lLen[i], S.lIns[i], S.lRm[i],
                          S.lMhi[i], S.lMlo[i], mClient(S.lMeta[i]),
-                         visOf(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c), w == kNone ? -1 : (int)w);
+                         visAny(S.lLen[i], S.lIns[i], S.lRm[i], S.lMlo[i], S.lMhi[i], mClient(S.lMeta[i]), r, c, S.lId[i]), w == kNone ? -1 : (int)w);
             if (w != kNone) std::fprintf(stderr, " | w ins %d rm %d len %u meta %x grp %u blk %u", S.wRec[4 * w], S.wRec[4 * w + 1], S.wRec[4 * w + 2], S.wRec[4 * w + 3] & kWMetaMask, S.wRec[4 * w + 3] >> kWGroupShift, S.wBlk[w]);
             std::fprintf(stderr, "\n");
           }
@@ -4003,7 +4056,8 @@ class HugeDocT {
   }
 
   FMT_DEV void writeOutputs(fmt_mt_doc_result* hdr, fmt_mt_leaf* outLeaves, uint64_t capLeaves, uint16_t* outChars,
-                            uint64_t capChars, fmt_mt_propset* outProps, uint16_t* outLegacy = nullptr) {
+                            uint64_t capChars, fmt_mt_propset* outProps, uint16_t* outLegacy = nullptr,
+                            uint64_t* outHi = nullptr) {
     uint64_t nLeaves = 0, nChars = 0, visible = 0;
     uint32_t nBlocks = 0;
     for (int k = 0; k < nGroups && status == FMT_OK; k++) {
@@ -4053,6 +4107,10 @@ class HugeDocT {
             x.ins_seq = rd(S.lIns + i);
             x.rm_seq = rd(S.lRm + i);
             x.rm_clients = static_cast<uint64_t>(rd(S.lMlo + i)) | (static_cast<uint64_t>(rd(S.lMhi + i)) << 32);
+            if (outHi != nullptr) {  // (remove clients 64..127)
+              const size_t q = 2 * static_cast<size_t>(rd(S.lId + i));
+              outHi[o] = static_cast<uint64_t>(rd(S.hiMask + q)) | (static_cast<uint64_t>(rd(S.hiMask + q + 1)) << 32);
+            }
             x.char_off = static_cast<uint32_t>(co);
             x.len = LANE(len);
             const uint32_t m = rd(S.lMeta + i);

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(64 * fmt_huge::HugeDoc::kWaves) void hugeDocKernel(
     doc.postExit();
     const HugeOut o = outs[i];
     const uint64_t t0 = fmt_huge::HugeDoc::clk();
-    doc.writeOutputs(o.header, o.leaves, o.capLeaves, o.chars, o.capChars, o.props, o.legacy);
+    doc.writeOutputs(o.header, o.leaves, o.capLeaves, o.chars, o.capChars, o.props, o.legacy, o.leavesHi);
     doc.prof[6] += fmt_huge::HugeDoc::clk() - t0;
     doc.prof[23] = doc.textTop - doc.mergeLo;
     if ((threadIdx.x & 63) == 0)

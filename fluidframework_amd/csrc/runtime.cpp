@@ -243,6 +243,7 @@ struct fmt_ctx {
   // groups, group records, PropertiesManager records, regenerated ops / text and normalization
   // scratch live in per-document slabs (mt_engine.h LocalTables)
   bool mtLocal = false;
+  bool mtHiClients = false;  // some op or merge-info stamp names a short client id 64..127 (huge tier only)
   DevBuf<uint32_t> mtLocGroups, mtLocRecs, mtLocPm, mtLocScratch, mtLocRegenCount;
   DevBuf<uint64_t> mtLocOffs;                // 6 offset arrays of n + 1: groups, recs, pm, regen, text, scratch
   DevBuf<fmt_mt_op> mtLocRegen;
@@ -932,6 +933,16 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   }
   if ((e = alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p)) != hipSuccess) return drop(e);
   O.prof = static_cast<unsigned long long*>(p);
+  // remove clients 64..127: the per-leaf-id side table (zeroed) and its per-leaf output
+  S.hiMask = nullptr;
+  O.leavesHi = nullptr;
+  if (c->mtHiClients) {
+    if ((e = alloc(2ull * S.idCap * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    FMT_HIP(c, hipMemsetAsync(p, 0, 2ull * S.idCap * sizeof(uint32_t), c->stream));
+    S.hiMask = static_cast<uint32_t*>(p);
+    if ((e = alloc(O.capLeaves * sizeof(uint64_t), &p)) != hipSuccess) return drop(e);
+    O.leavesHi = static_cast<uint64_t*>(p);
+  }
   return FMT_OK;
 }
 
@@ -944,7 +955,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
   // one pass over the op records on host threads: counts, and the first invalid record
   struct OpScan {
     uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
-    bool obliterates = false, local = false;
+    bool obliterates = false, local = false, hiClients = false;
     uint64_t errAt = ~0ull;
     int errCode = FMT_OK;
     const char* err = nullptr;
@@ -962,6 +973,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       if (op.flags & FMT_MT_F_CATCHUP) S.catchupOps++;
       if (op.flags & FMT_MT_F_RMORDER) S.rmOrderOps++;
       if (op.flags & FMT_MT_F_LOCAL_ANY) S.local = true;
+      if (op.client > 63 && op.client != FMT_MT_CLIENT_NONCOLLAB) S.hiClients = true;
       if (op.flags & FMT_MT_F_LOADSEG) {  // a SnapshotV1 body segment: its merge info row in range
         if (op.type != FMT_MT_INSERT || b->snapshot_info == nullptr || op.pos1 < 0 ||
             static_cast<uint64_t>(op.pos1) >= b->n_snapshot_segs ||
@@ -990,7 +1002,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     }
   });
   uint64_t insertChars = 0, catchupOps = 0, rmOrderOps = 0;
-  bool obliterates = false, local = false;
+  bool obliterates = false, local = false, hiClients = false;
   const OpScan* firstBad = nullptr;
   for (const OpScan& S : scans) {
     insertChars += S.insertChars;
@@ -998,6 +1010,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     rmOrderOps += S.rmOrderOps;
     obliterates = obliterates || S.obliterates;
     local = local || S.local;
+    hiClients = hiClients || S.hiClients;
     if (S.err != nullptr && (firstBad == nullptr || S.errAt < firstBad->errAt)) firstBad = &S;
   }
   if (firstBad != nullptr) return setErr(c, firstBad->errCode, firstBad->err);
@@ -1216,6 +1229,7 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, hipStreamSynchronize(c->stream));  // (sv / si / T are about to go out of scope)
   }
   c->mtLocal = local;
+  c->mtHiClients = hiClients;
   if (local) {
     // Per-document slabs, sized from the document's local records (a document that needs more reports
     // FMT_E_CAPACITY): 4 + 2 pending groups per submission (a reconnect replaces a group by one per
@@ -1284,6 +1298,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, c->mtSnapStamps.reserve(b->n_snapshot_stamps));
     FMT_HIP(c, cp(c->mtSnapInfo.p, b->snapshot_info, b->n_snapshot_segs * sizeof(fmt_mt_snapshot_info)));
     FMT_HIP(c, cp(c->mtSnapStamps.p, b->snapshot_stamps, b->n_snapshot_stamps * sizeof(fmt_mt_stamp)));
+    for (uint64_t k = 0; k < b->n_snapshot_stamps && !c->mtHiClients; k++) c->mtHiClients = b->snapshot_stamps[k].client > 63;
+    for (uint64_t k = 0; k < b->n_snapshot_segs && !c->mtHiClients; k++) c->mtHiClients = b->snapshot_info[k].ins_client > 63;
   }
   c->mtNRelpos = b->relpos ? b->n_relpos : 0u;
   c->mtMarkerKey = b->marker_id_key;
@@ -1795,7 +1811,7 @@ void docViews(const fmt_ctx* c, std::vector<fmt_kernels::SumView>& views) {
     const int32_t hs = d < c->mtHugeSlot.size() ? c->mtHugeSlot[d] : -1;
     if (hs >= 0) {
       const fmt_kernels::HugeOut& O = c->huge[static_cast<size_t>(hs)].out;
-      views[d] = {O.leaves, O.chars, O.props, c->mtHasAdjust ? O.legacy : nullptr, O.cls};
+      views[d] = {O.leaves, O.chars, O.props, c->mtHasAdjust ? O.legacy : nullptr, O.cls, O.leavesHi};
     } else {
       const int32_t slot = d < c->mtBigSlot.size() ? c->mtBigSlot[d] : -1;
       const fmt_kernels::MtCaps caps = fmt_kernels::mergeTreeCaps(slot >= 0);
@@ -2044,6 +2060,19 @@ int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
   const uint32_t m = h.n_rm_order < cap ? h.n_rm_order : cap;
   if (m) FMT_HIP(c, hipMemcpy(out, c->mtRmOrder.p + c->mtRmOffsHost[doc], m * sizeof(fmt_mt_remove_order), hipMemcpyDeviceToHost));
+  return FMT_OK;
+}
+
+int fmt_mt_fetch_rm_clients_hi(fmt_ctx* c, uint32_t doc, uint64_t* out, uint32_t cap) {
+  if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
+    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_rm_clients_hi: bad arguments");
+  fmt_mt_doc_result h;
+  FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
+  const uint32_t m = h.n_leaves < cap ? h.n_leaves : cap;
+  const int32_t hs = doc < c->mtHugeSlot.size() ? c->mtHugeSlot[doc] : -1;
+  const uint64_t* src = hs >= 0 ? c->huge[static_cast<size_t>(hs)].out.leavesHi : nullptr;
+  if (src != nullptr && m) FMT_HIP(c, hipMemcpy(out, src, m * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  else if (m) std::memset(out, 0, m * sizeof(uint64_t));  // (the other tiers hold ids 0..63 only)
   return FMT_OK;
 }
 

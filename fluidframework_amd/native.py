@@ -244,6 +244,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_fetch_numbers.argtypes = [P, U32, P, U32, ctypes.POINTER(U32)]
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         for name, args in (("fmt_mt_state_digest", [P, P]), ("fmt_mt_fetch_legacy_props", [P, U32, P, U32]),
+                           ("fmt_mt_fetch_rm_clients_hi", [P, U32, P, U32]),
                            ("fmt_map_pending_run", [P, P, U64, P]),
                            ("fmt_mt_fetch_regen", [P, U32, P, U32, P, U32, ctypes.POINTER(U32), ctypes.POINTER(U32)]),
                            ("fmt_map_pending_fetch", [P, P, P, P, U64, ctypes.POINTER(U64)])):
@@ -261,7 +262,7 @@ EXPORTED_SYMBOLS = [
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
     "fmt_mt_state_digest", "fmt_mt_fetch_legacy_props", "fmt_map_pending_run", "fmt_map_pending_fetch",
-    "fmt_mt_fetch_regen",
+    "fmt_mt_fetch_regen", "fmt_mt_fetch_rm_clients_hi",
 ]
 
 
@@ -461,6 +462,15 @@ class Engine:
         n = int(hdr["n_leaves"])
         out = np.zeros(max(n, 1), dtype=np.uint16)
         self._check(self.L.fmt_mt_fetch_legacy_props(self.h, doc, _ptr(out), n))
+        return out[:n]
+
+    def mt_rm_clients_hi(self, doc: int, hdr=None) -> np.ndarray:
+        """Per leaf, its remove clients with short ids 64..127 (bit c - 64; zero for most documents)."""
+        if hdr is None:
+            hdr = self.mt_headers(raise_on_failed_docs=False)[doc]
+        n = int(hdr["n_leaves"])
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        self._check(self.L.fmt_mt_fetch_rm_clients_hi(self.h, doc, _ptr(out), n))
         return out[:n]
 
     def mt_numbers(self, doc: int) -> np.ndarray:

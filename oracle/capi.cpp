@@ -67,12 +67,15 @@ int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* ar
   return FMT_OK;
 }
 
+// rmHi (optional): per leaf, its remove clients with short ids 64..127 (fmt_mt_fetch_rm_clients_hi).
 void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint32_t capLeaves,
-             uint16_t* chars, uint32_t capChars, fmt_mt_propset* props, uint32_t capProps) {
+             uint16_t* chars, uint32_t capChars, fmt_mt_propset* props, uint32_t capProps,
+             std::vector<uint64_t>* rmHi = nullptr) {
   std::vector<const orc::Seg*> segs;
   std::vector<int> blockOf;
   int nBlocks = 0, depth = 0;
   mt->collectLeaves(segs, blockOf, &nBlocks, &depth);
+  if (rmHi) rmHi->assign(segs.size(), 0);
   std::vector<const orc::PropMap*> sets;
   std::vector<uint32_t> setRec;  // first record of each set (a set wider than 8 entries takes several)
   uint32_t nRec = 0;
@@ -101,8 +104,10 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
       L.ins_client = static_cast<int16_t>(s->ins.client);
       L.rm_seq = s->removed() ? seqOf(s->removes[0]) : FMT_NOT_REMOVED;
       uint64_t mask = 0;
-      for (const auto& r : s->removes)
+      for (const auto& r : s->removes) {
         if (r.client >= 0 && r.client < 64) mask |= 1ull << r.client;
+        else if (r.client >= 64 && r.client < 128 && rmHi) (*rmHi)[i] |= 1ull << (r.client - 64);
+      }
       L.rm_clients = mask;
       L.char_off = charOff;
       L.len = static_cast<uint32_t>(s->len());
@@ -151,7 +156,8 @@ uint64_t dgMix(uint64_t z) {
 }
 uint64_t dgElem(uint64_t tag, uint64_t i, uint64_t w) { return dgMix(dgMix((tag << 56) ^ i) ^ w); }
 
-uint64_t digestOf(const fmt_mt_doc_result& h, const fmt_mt_leaf* leaves, const uint16_t* chars, const fmt_mt_propset* props) {
+uint64_t digestOf(const fmt_mt_doc_result& h, const fmt_mt_leaf* leaves, const uint16_t* chars, const fmt_mt_propset* props,
+                  const std::vector<uint64_t>* rmHi = nullptr) {
   uint64_t acc = 0;
   if (h.status != FMT_OK)
     return dgMix(dgElem(1, 0, static_cast<uint32_t>(h.status)) + dgElem(1, 1, static_cast<uint32_t>(h.fail_seq)));
@@ -176,6 +182,9 @@ uint64_t digestOf(const fmt_mt_doc_result& h, const fmt_mt_leaf* leaves, const u
       }
     }
   }
+  if (rmHi)  // remove clients 64..127, on the leaves that have any
+    for (uint32_t i = 0; i < h.n_leaves && i < rmHi->size(); i++)
+      if ((*rmHi)[i] != 0) acc += dgElem(10, i, (*rmHi)[i]);
   for (uint32_t u = 0; u < h.n_chars; u++) acc += dgElem(8, u, chars[u]);
   return dgMix(acc);
 }
@@ -461,12 +470,13 @@ int orc_mt_replay_digest(const fmt_mt_batch* b, uint32_t docBegin, uint32_t docE
     for (const orc::Seg* s : segs) units += static_cast<size_t>(s->len());
     std::vector<uint16_t> ch(units + 1);
     std::vector<fmt_mt_propset> pr(segs.size() * (FMT_MT_PROPS_KEYS_MAX / FMT_MT_PROPS_MAX) + 1);  // (wide sets: several records)
+    std::vector<uint64_t> hi;
     dumpDoc(&mt, &h, lv.data(), static_cast<uint32_t>(lv.size()), ch.data(), static_cast<uint32_t>(ch.size()), pr.data(),
-            static_cast<uint32_t>(pr.size()));
+            static_cast<uint32_t>(pr.size()), &hi);
     h.status = st;
     h.fail_seq = fs;
     if (statuses) statuses[i] = st;
-    digests[i] = digestOf(h, lv.data(), ch.data(), pr.data());
+    digests[i] = digestOf(h, lv.data(), ch.data(), pr.data(), &hi);
     digestNs += std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - td).count();
   });
   const double wall = std::chrono::duration<double>(clk::now() - t0).count();
@@ -567,11 +577,12 @@ int orc_mt_replay_full(const fmt_mt_batch* b, uint32_t d, const char* const* key
     for (const orc::Seg* s : segs) units += static_cast<size_t>(s->len());
     std::vector<uint16_t> ch(units + 1);
     std::vector<fmt_mt_propset> pr(segs.size() * (FMT_MT_PROPS_KEYS_MAX / FMT_MT_PROPS_MAX) + 1);
+    std::vector<uint64_t> hi;
     dumpDoc(&mt, &h, lv.data(), static_cast<uint32_t>(lv.size()), ch.data(), static_cast<uint32_t>(ch.size()), pr.data(),
-            static_cast<uint32_t>(pr.size()));
+            static_cast<uint32_t>(pr.size()), &hi);
     h.status = st;
     h.fail_seq = fs;
-    g_full.digest = digestOf(h, lv.data(), ch.data(), pr.data());
+    g_full.digest = digestOf(h, lv.data(), ch.data(), pr.data(), &hi);
     g_full.minSeq = h.min_seq;
   }
   int hl = 0, bl = 0;

@@ -25,7 +25,7 @@ def _sum(a):
     return int(np.asarray(a, dtype=np.uint64).sum(dtype=np.uint64)) if np.size(a) else 0
 
 
-def state_digest(hdr, leaves, chars, props) -> int:
+def state_digest(hdr, leaves, chars, props, rm_hi=None) -> int:
     """Digest of one document from its header, leaves[:n_leaves], chars[:n_chars] and prop sets."""
     u32 = lambda v: int(v) & 0xFFFFFFFF  # noqa: E731
     if int(hdr["status"]) != 0:
@@ -56,6 +56,11 @@ def state_digest(hdr, leaves, chars, props) -> int:
                 acc += _sum(_elems(7, np.arange(min(m, 8)) + 8 * k, kv[:8]))
             if m > 8:
                 acc += _sum(_elems(9, np.arange(8, m) + 64 * k, kv[8:]))
+    if rm_hi is not None:  # remove clients 64..127 (tag 10), on the leaves that have any
+        hi = np.asarray(rm_hi[:n], dtype=np.uint64)
+        at = np.nonzero(hi)[0]
+        if len(at):
+            acc += _sum(_elems(10, at.astype(np.uint64), hi[at]))
     nc = int(hdr["n_chars"])
     acc += _sum(_elems(8, np.arange(nc), chars[:nc]))
     return int(_mix(np.uint64(acc & M64)))

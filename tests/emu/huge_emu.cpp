@@ -72,6 +72,8 @@ const fmt_mt::AdjustTables* prepareNumbers(const fmt_mt_batch* b) {
   g_adj.pm = g_pm.data();
   return &g_adj;
 }
+// emu_huge_replay_hi: the per-leaf output of remove clients 64..127 for the next replay (or nullptr)
+uint64_t* g_hiOut = nullptr;
 }  // namespace
 
 extern "C" {
@@ -151,6 +153,8 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   S.cuIds = catchup != nullptr ? cuIds.data() : nullptr;
   std::vector<uint32_t> rmIds(rmOrder != nullptr ? S.idCap : 0);
   S.rmIds = rmOrder != nullptr ? rmIds.data() : nullptr;
+  std::vector<uint32_t> hiMask(g_hiOut != nullptr ? 2ull * S.idCap : 0, 0u);  // (runtime.cpp: zeroed)
+  S.hiMask = g_hiOut != nullptr ? hiMask.data() : nullptr;
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));
   const fmt_mt::AdjustTables* adj = prepareNumbers(b);
@@ -194,7 +198,7 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
   doc->run(in);
-  doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props, adj != nullptr ? legacy : nullptr);
+  doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props, adj != nullptr ? legacy : nullptr, g_hiOut);
   if (nNums) *nNums = adj != nullptr ? g_numCount[d] : 0u;
   for (uint32_t k = 0; adj != nullptr && nums != nullptr && k < g_numCount[d] && k < capNums; k++) nums[k] = g_nums[k];
   if (std::getenv("FMT_EMU_TEXTCAP"))
@@ -219,6 +223,16 @@ int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
 int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
                     uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
   return emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0, nullptr, 0);
+}
+
+// As emu_huge_replay, with the remove-client side table for short ids 64..127 (the runtime allocates
+// it for batches that name such clients): hi[capLeaves] receives each leaf's ids 64..127.
+int emu_huge_replay_hi(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
+                       uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, uint64_t* hi) {
+  g_hiOut = hi;
+  const int st = emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0, nullptr, 0);
+  g_hiOut = nullptr;
+  return st;
 }
 
 }  // extern "C"

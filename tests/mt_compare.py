@@ -65,6 +65,7 @@ def huge_emu_lib(tiny_groups=False):
                                                                       ctypes.c_uint32]
         L.emu_huge_replay_adj.argtypes = L.emu_huge_replay_rec.argtypes + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                                           ctypes.c_void_p]
+        L.emu_huge_replay_hi.argtypes = L.emu_huge_replay.argtypes + [ctypes.c_void_p]
         _huge[tiny_groups] = L
     return _huge[tiny_groups]
 
@@ -126,6 +127,41 @@ def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=F
     if cap_rm:
         out = out + (rm[: int(h["n_rm_order"])],)
     return out
+
+
+def emu_huge_replay_hi(batch, doc=0, tiny_groups=False, cap_props=65534):
+    """(header, leaves, chars, props, remove clients 64..127 per leaf) of document `doc` replayed by
+    the emulated huge engine with its side table for short ids 64..127."""
+    from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
+
+    sd = batch.snapshots[doc] if batch.snapshots is not None else None
+    segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 1
+    nops = int(batch.doc_op_offsets[doc + 1] - batch.doc_op_offsets[doc])
+    cap_leaves, cap_chars = segs + 3 * nops + 8, len(batch.text) + 8
+    hdr = np.zeros(1, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(cap_leaves, dtype=LEAF_DTYPE)
+    chars = np.zeros(cap_chars, dtype="<u2")
+    props = np.zeros(cap_props, dtype=PROPSET_DTYPE)
+    hi = np.zeros(cap_leaves, dtype=np.uint64)
+    b, keep = batch_struct(batch)
+    huge_emu_lib(tiny_groups).emu_huge_replay_hi(ctypes.addressof(b), doc, _p(hdr), _p(leaves), cap_leaves, _p(chars),
+                                                 cap_chars, _p(props), _p(hi))
+    del keep
+    h = hdr[0]
+    n = int(h["n_leaves"])
+    return h, leaves[:n], chars[: int(h["n_chars"])], props[: int(h["n_props"])], hi[:n]
+
+
+def oracle_rm_clients_hi(batch, doc, n_leaves):
+    """The oracle's remove clients 64..127 per final leaf (from every remove stamp, oracle.mt_removers)."""
+    import oracle
+
+    hi = np.zeros(n_leaves, dtype=np.uint64)
+    for leaf, stamps in oracle.mt_removers(batch, doc).items():
+        for client, _, _ in stamps:
+            if 64 <= client < 128:
+                hi[leaf] |= np.uint64(1) << np.uint64(client - 64)
+    return hi
 
 
 def emu_caps(large=False):

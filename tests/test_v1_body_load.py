@@ -85,7 +85,7 @@ def _cut(docs, at):
         for m in msgs[:at]:
             d.add_message(m)
     cut = b.finish(remove_order=True)
-    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(cut, cap_leaves=8192, cap_chars=1 << 17, cap_props=1024)
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(cut, cap_leaves=max(8192, 2 * at + 1024), cap_chars=1 << 17, cap_props=1024)
     assert rc == 0
     out = []
     for d, (init, msgs) in enumerate(docs):
