@@ -23,6 +23,7 @@
 //   fetchRemoveOrder(ctx, doc, n) -> ArrayBuffer                     fmt_mt_fetch_remove_order
 //   fetchNumbers(ctx, doc) -> Float64Array                           fmt_mt_fetch_numbers
 //   fetchLegacyProps(ctx, doc, nLeaves) -> Uint16Array               fmt_mt_fetch_legacy_props
+//   fetchRmClientsHi(ctx, doc, nLeaves) -> BigUint64Array            fmt_mt_fetch_rm_clients_hi (ids 64..127)
 //   fetchRegen(ctx, doc) -> {ops: ArrayBuffer, text: Uint16Array}     fmt_mt_fetch_regen (f4 reconnects)
 //   replayMap(ctx, batch) -> Promise<ArrayBuffer slots>              fmt_map_load + run + fetch
 //   replayMapSparse(ctx, batch) -> Promise<{counts, entries}>        fmt_map_load_sparse + run + fetch
@@ -947,6 +948,31 @@ napi_value FetchLegacyProps(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+// fetchRmClientsHi(ctx, doc, nLeaves) -> BigUint64Array: per leaf, its remove clients 64..127 (bit c - 64)
+napi_value FetchRmClientsHi(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c;
+  if (argc < 3 || !get_ctx(env, argv[0], &c)) return nullptr;
+  if (c->busy) {
+    throw_fmt(env, FMT_E_USAGE, "fetchRmClientsHi: a replay is running on this context");
+    return nullptr;
+  }
+  uint32_t doc, n;
+  if (!get_u32(env, argv[1], "doc", &doc) || !get_u32(env, argv[2], "nLeaves", &n)) return nullptr;
+  void* p;
+  napi_value ab, arr;
+  CHECK_NAPI(env, napi_create_arraybuffer(env, size_t(n) * sizeof(uint64_t), &p, &ab));
+  const int rc = n ? fmt_mt_fetch_rm_clients_hi(c->ctx, doc, static_cast<uint64_t*>(p), n) : FMT_OK;
+  if (rc != FMT_OK) {
+    throw_fmt(env, rc, fmt_last_error(c->ctx));
+    return nullptr;
+  }
+  CHECK_NAPI(env, napi_create_typedarray(env, napi_biguint64_array, n, ab, 0, &arr));
+  return arr;
+}
+
 napi_value FetchRegen(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
@@ -1024,6 +1050,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"fetchRemoveOrder", nullptr, FetchRemoveOrder, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchNumbers", nullptr, FetchNumbers, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchLegacyProps", nullptr, FetchLegacyProps, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+      {"fetchRmClientsHi", nullptr, FetchRmClientsHi, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"fetchRegen", nullptr, FetchRegen, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"replayMapSparse", nullptr, ReplayMapSparse, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"summarizeLegacy", nullptr, SummarizeLegacy, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -45,7 +45,7 @@ def test_addon_exports(addon):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert out["k"] == sorted(["open", "close", "openContexts", "deviceInfo", "capacity", "stats", "replayMergeTree", "fetchCatchup",
-                               "fetchRemoveOrder", "fetchNumbers", "fetchLegacyProps", "fetchRegen", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
+                               "fetchRemoveOrder", "fetchNumbers", "fetchLegacyProps", "fetchRmClientsHi", "fetchRegen", "replayMapSparse", "summarizeLegacy", "fetchCatchupAll",
                                "summaryBlobs", "replayMap", "fetchDoc", "sizes"])
     assert out["s"] == {"mtOp": 32, "mapOp": 16, "leaf": 32, "docResult": 48, "propset": 36, "mapSlot": 8,
                         "catchupRange": 16, "mapEntry": 12, "adjust": 32}

@@ -5,7 +5,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5_pcs
-K="huge or loader or v1_body or writer" OUTDIR=r5_huge bash tools/gpu_tests.sh || exit $?
+K="huge or loader or v1_body or writer" OUTDIR=r5_huge bash tools/gpu_tests.sh
+rc=$?
+# (failed tests go on to the profiles; a time limit, abort or fault ends the call)
+case $rc in 0|1) ;; *) exit $rc ;; esac
 timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
   --pc-sampling-interval 1 --output-format csv -d gpurun_out/r5_pcs/host_trap -o run -- \
   python3 tools/pcs_driver.py --docs 20000 --runs 1 > gpurun_out/r5_pcs/host_trap.log 2>&1
