@@ -836,7 +836,7 @@ def bench_t3(args, rank, world, local_rank, dist):
             "t3_oracle_check": t3_check,
             "t3_summary": t3_summary,
             "state_checksum": f"{shard.combine_checksums(stats):016x}",
-            "phase_clocks_per_op": {k: v / n_ops for k, v in prof.items() if k not in ("text_compactions", "merge_units_in_use")},
+            "phase_clocks_per_op": {k: v / n_ops for k, v in prof.items() if k not in ("text_compactions", "merge_units_in_use", "resumed_at")},
             "merge_area": {"compactions": prof.get("text_compactions"), "units_in_use": prof.get("merge_units_in_use")},
             "final_state": {"leaves": int(h["n_leaves"]), "chars": int(h["n_chars"]), "visible": int(h["visible_len"]),
                             "blocks": int(h["n_blocks"]), "depth": int(h["depth"]), "min_seq": int(h["min_seq"])},

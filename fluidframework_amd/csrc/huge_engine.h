@@ -38,6 +38,7 @@
 #include "../../include/fmt.h"
 #include "wave.h"
 #include "adjust.h"
+#include "huge_ckpt.h"
 
 #include <algorithm>
 #include <vector>
@@ -85,18 +86,9 @@ constexpr int kWGroupShift = 17;
 constexpr int kWinList = 1024;  // LDS list of one group's visible window entries (slot pass)
 constexpr int kGlCap = 2048;    // LDS list of the visible window entries of one group pass
 constexpr int kGlEntBits = 21;  // entry index bits in glEnt (the group id above them)
-constexpr int kObCap = 128;     // live obliterates (seq above minSeq)
 
-// One live obliterate (mergeTree.ts ObliterateInfo): its endpoint references as (leaf id, offset) —
-// id 0 once the reference is removed — and its stamp.
-struct ObEnt {
-  uint32_t startId;
-  int32_t startOff;
-  uint32_t endId;
-  int32_t endOff;
-  int32_t seq;
-  int32_t client;
-};
+// One live obliterate (mergeTree.ts ObliterateInfo) is a 6-word record of HugeState::obRec: its
+// endpoint references as (leaf id, offset) — id 0 once the reference is removed — and its stamp.
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));
 typedef uint32_t u32x2 __attribute__((vector_size(8)));
@@ -179,6 +171,15 @@ struct HugeState {
   // [idCap * 2]: per leaf id, the remove clients with short ids 64..127 (bit c - 64), beyond the two
   // mask words every leaf and window entry carry (nullptr: the batch has no such client; zeroed)
   uint32_t* hiMask;
+  // live obliterates (Obliterates, mergeTree.ts:515-635), [obCap] each: per slot its record
+  // {startId, startOff, endId, endOff, seq, client} (obRec, 6 words) and whether it is in use, and the
+  // two ordered slot lists seqOrdered / startOrdered (nullptr / 0: the document has no obliterate;
+  // obCap = its obliterate ops, the most that can be live at once)
+  uint32_t* obRec;
+  uint32_t* obUsed;
+  uint32_t* obSeq;
+  uint32_t* obStart;
+  uint32_t obCap;
 };
 
 // LDS state of the wave.
@@ -202,11 +203,6 @@ struct HugeLds {
   uint32_t glEnt[kGlCap];
   int32_t glVis[kGlCap];
   int32_t glN[4];
-  // live obliterates: slots, slot in use, Obliterates.seqOrdered / startOrdered (slot lists)
-  ObEnt ob[kObCap];
-  uint8_t obUsed[kObCap];
-  uint8_t obSeq[kObCap];
-  uint8_t obStart[kObCap];
 };
 
 struct HugeInputs {
@@ -250,6 +246,12 @@ struct HugeInputs {
   // index into their per-document slabs (computed numbers, PropertiesManager records)
   const fmt_mt::AdjustTables* adj;
   uint32_t doc;
+  // large → huge checkpoint (huge_ckpt.h; nullptr: load from the segments above): the large tier's
+  // record and its result slabs for this document at the op it stopped before
+  const uint32_t* ck = nullptr;
+  const fmt_mt_leaf* ckLeaves = nullptr;
+  const uint16_t* ckChars = nullptr;
+  const fmt_mt_propset* ckProps = nullptr;
 };
 
 // The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
@@ -326,7 +328,7 @@ class HugeDocT {
   int curSeq = 0, minSeq = 0;
   int status = FMT_OK, failSeq = 0;
   uint32_t lastBlk = kNone;  // the last leaf block in document order (kNone: document empty)
-  int obLive = 0, obSeqN = 0, obStartN = 0;
+  int obLive = 0, obSeqN = 0, obStartN = 0, obSlotsHi = 0;
   uint64_t mergeLo = 0, mergeHi = 0;  // the merge-area half in use
   bool textFull = false;              // a scour plan's runs did not fit the merge area's half
   // catch-up recording (FMT_MT_F_CATCHUP ops): ranges written, the op's delta leaves, its index
@@ -349,7 +351,7 @@ class HugeDocT {
   // 12 insert, 13 range ops, 14 leaf split, 15 interior pack; counts: 16 group passes, 17 slot
   // passes, 18 Σ window entries at group passes, 19 Σ groups at group passes; 20 wave 0's window
   // share time, 21 group scan time, 22 merge-area compactions, 23 merge-area units in use
-  static constexpr int kProf = 24;
+  static constexpr int kProf = 25;  // [24]: the op a large → huge checkpoint resumed at
   uint64_t prof[kProf] = {};
   struct ProfScope {
     uint64_t& a;
@@ -2236,10 +2238,39 @@ class HugeDocT {
     if (a < 0 || b < 0) return (a < 0) == (b < 0) ? 0 : (a < 0 ? -1 : 1);
     return a < b ? -1 : (a > b ? 1 : 0);
   }
-  FMT_DEV int obU(uint8_t* p, int i) const { return uni(static_cast<int>(p[i])); }
+  // ---- the live-obliterate table in HBM (HugeState::obRec ...): fields of slot `slot`
+  enum : int { kObStartId = 0, kObStartOff = 1, kObEndId = 2, kObEndOff = 3, kObSeq = 4, kObClient = 5 };
+  FMT_DEV uint32_t obF(int slot, int f) const { return ldu(S.obRec + 6 * static_cast<size_t>(slot) + f); }
+  FMT_DEV int obU(const uint32_t* p, int i) const { return static_cast<int>(ldu(p + i)); }
+  // p[at + 1 .. n] = p[at .. n - 1] (one entry opens at `at`), 64 entries per step from the top
+  FMT_DEV void listOpen(uint32_t* p, int at, int n) {
+    for (int hi = n; hi > at; hi -= 64) {
+      const int lo = hi - 64 > at ? hi - 64 : at;  // destinations (lo, hi]
+      Lane<uint32_t> v;
+      FOR_LANES(l) { LANE(v) = lo + 1 + l <= hi ? rd(p + lo + l) : 0u; }
+      waveSync();
+      FOR_LANES(l) {
+        if (lo + 1 + l <= hi) p[lo + 1 + l] = LANE(v);
+      }
+      waveSync();
+    }
+  }
+  // p[at .. n - 2] = p[at + 1 .. n - 1] (entry `at` closes), 64 entries per step from the bottom
+  FMT_DEV void listClose(uint32_t* p, int at, int n) {
+    for (int lo = at; lo + 1 < n; lo += 64) {
+      const int hi = lo + 64 < n - 1 ? lo + 64 : n - 1;  // destinations [lo, hi)
+      Lane<uint32_t> v;
+      FOR_LANES(l) { LANE(v) = lo + l < hi ? rd(p + lo + l + 1) : 0u; }
+      waveSync();
+      FOR_LANES(l) {
+        if (lo + l < hi) p[lo + l] = LANE(v);
+      }
+      waveSync();
+    }
+  }
   FMT_DEV int startCompare(int a, int b) const {  // SortedSegmentSet.compare on start references
-    const int c = ordinalCompare(ordOf(uni(L->ob[a].startId)), ordOf(uni(L->ob[b].startId)));
-    return c != 0 ? c : uni(L->ob[a].startOff) - uni(L->ob[b].startOff);
+    const int c = ordinalCompare(ordOf(obF(a, kObStartId)), ordOf(obF(b, kObStartId)));
+    return c != 0 ? c : static_cast<int>(obF(a, kObStartOff)) - static_cast<int>(obF(b, kObStartOff));
   }
   // SortedSet.findItemPosition + SortedSegmentSet.onFindEquivalent, verbatim: the array is only as
   // sorted as the ordinals were at insertion.
@@ -2249,7 +2280,7 @@ class HugeDocT {
     int start = 0, end = obStartN - 1, index = -1;
     while (start <= end) {
       index = start + (end - start) / 2;
-      const int at = obU(L->obStart, index);
+      const int at = obU(S.obStart, index);
       const int c = startCompare(slot, at);
       if (c < 0) {
         if (start == index) return index;
@@ -2262,13 +2293,13 @@ class HugeDocT {
           *exists = true;
           return index;
         }
-        for (int b = index - 1; b >= 0 && startCompare(slot, obU(L->obStart, b)) == 0; b--)
-          if (obU(L->obStart, b) == slot) {
+        for (int b = index - 1; b >= 0 && startCompare(slot, obU(S.obStart, b)) == 0; b--)
+          if (obU(S.obStart, b) == slot) {
             *exists = true;
             return b;
           }
-        for (; index < obStartN && startCompare(slot, obU(L->obStart, index)) == 0; index++)
-          if (obU(L->obStart, index) == slot) {
+        for (; index < obStartN && startCompare(slot, obU(S.obStart, index)) == 0; index++)
+          if (obU(S.obStart, index) == slot) {
             *exists = true;
             return index;
           }
@@ -2279,20 +2310,24 @@ class HugeDocT {
   }
 
   // References on leaf `from` at offset >= minOff move to leaf `to`, offset += add (split: the right
-  // part; zamboni append: every reference of the appended leaf). Lane l takes slots l, l + 64.
+  // part; zamboni append: every reference of the appended leaf). Lane l takes slots l, l + 64, ...
+  // up to the highest slot ever taken.
   FMT_DEV void obRefsMove(uint32_t from, uint32_t to, int minOff, int add) {
     if (obLive == 0) return;
-    FOR_LANES(l) {
-      for (int k = l; k < kObCap; k += 64) {
-        if (L->obUsed[k]) {
-          ObEnt& e = L->ob[k];
-          if (e.startId == from && e.startOff >= minOff) {
-            e.startId = to;
-            e.startOff += add;
+    for (int base = 0; base < obSlotsHi; base += 64) {
+      FOR_LANES(l) {
+        const int k = base + l;
+        if (k < obSlotsHi && rd(S.obUsed + k) != 0u) {
+          uint32_t* e = S.obRec + 6 * static_cast<size_t>(k);
+          const uint32_t sId = rd(e + kObStartId), eId = rd(e + kObEndId);
+          const int sOff = static_cast<int>(rd(e + kObStartOff)), eOff = static_cast<int>(rd(e + kObEndOff));
+          if (sId == from && sOff >= minOff) {
+            e[kObStartId] = to;
+            e[kObStartOff] = static_cast<uint32_t>(sOff + add);
           }
-          if (e.endId == from && e.endOff >= minOff) {
-            e.endId = to;
-            e.endOff += add;
+          if (eId == from && eOff >= minOff) {
+            e[kObEndId] = to;
+            e[kObEndOff] = static_cast<uint32_t>(eOff + add);
           }
         }
       }
@@ -2302,39 +2337,37 @@ class HugeDocT {
 
   FMT_DEV bool obAdd(uint32_t sId, int sOff, uint32_t eId, int eOff, int seq, int client) {
     int slot = -1;
-    for (int base = 0; base < kObCap && slot < 0; base += 64) {
+    const int cap = static_cast<int>(S.obCap);
+    for (int base = 0; base < cap && slot < 0; base += 64) {
       Lane<bool> q;
-      FOR_LANES(l) { LANE(q) = L->obUsed[base + l] == 0; }
+      FOR_LANES(l) { LANE(q) = base + l < cap && rd(S.obUsed + base + l) == 0u; }
       const uint64_t m = ballot(q);
       if (m) slot = base + ctz64(m);
     }
-    if (slot < 0) return fail(FMT_E_CAPACITY);
+    if (slot < 0 || obSeqN >= cap) return fail(FMT_E_CAPACITY);
     FOR_LANES(l) {
       if (l == 0) {
-        L->obUsed[slot] = 1;
-        ObEnt& e = L->ob[slot];
-        e.startId = sId;
-        e.startOff = sOff;
-        e.endId = eId;
-        e.endOff = eOff;
-        e.seq = seq;
-        e.client = client;
-        L->obSeq[obSeqN] = static_cast<uint8_t>(slot);
+        S.obUsed[slot] = 1u;
+        uint32_t* e = S.obRec + 6 * static_cast<size_t>(slot);
+        e[kObStartId] = sId;
+        e[kObStartOff] = static_cast<uint32_t>(sOff);
+        e[kObEndId] = eId;
+        e[kObEndOff] = static_cast<uint32_t>(eOff);
+        e[kObSeq] = static_cast<uint32_t>(seq);
+        e[kObClient] = static_cast<uint32_t>(client);
+        S.obSeq[obSeqN] = static_cast<uint32_t>(slot);
       }
     }
     waveSync();
+    if (slot + 1 > obSlotsHi) obSlotsHi = slot + 1;
     obLive++;
     obSeqN++;
     bool exists;
     const int at = findStart(slot, &exists);
     if (!exists) {
-      if (obStartN >= kObCap) return fail(FMT_E_CAPACITY);
-      for (int i = obStartN; i > at; i--) {
-        const uint8_t v = static_cast<uint8_t>(obU(L->obStart, i - 1));
-        waveSync();
-        L->obStart[i] = v;
-      }
-      L->obStart[at] = static_cast<uint8_t>(slot);
+      if (obStartN >= cap) return fail(FMT_E_CAPACITY);
+      listOpen(S.obStart, at, obStartN);
+      st1(S.obStart + at, static_cast<uint32_t>(slot));
       waveSync();
       obStartN++;
     }
@@ -2345,34 +2378,28 @@ class HugeDocT {
   // and remove their references.
   FMT_DEV void obSetMinSeq() {
     int k = 0;
-    for (; k < obSeqN && uni(L->ob[obU(L->obSeq, k)].seq) <= minSeq; k++) {
-      const int slot = obU(L->obSeq, k);
+    for (; k < obSeqN && static_cast<int>(obF(obU(S.obSeq, k), kObSeq)) <= minSeq; k++) {
+      const int slot = obU(S.obSeq, k);
       bool exists;
       const int at = findStart(slot, &exists);
       if (exists) {
-        for (int i = at; i + 1 < obStartN; i++) {
-          const uint8_t v = static_cast<uint8_t>(obU(L->obStart, i + 1));
-          waveSync();
-          L->obStart[i] = v;
-        }
-        waveSync();
+        listClose(S.obStart, at, obStartN);
         obStartN--;
       }
-      L->ob[slot].startId = 0;  // removeLocalReferencePosition
-      L->ob[slot].endId = 0;
+      FOR_LANES(l) {  // removeLocalReferencePosition
+        if (l == 0) {
+          S.obRec[6 * static_cast<size_t>(slot) + kObStartId] = 0u;
+          S.obRec[6 * static_cast<size_t>(slot) + kObEndId] = 0u;
+        }
+      }
       waveSync();
       if (!exists) continue;  // still listed in startOrdered: its slot stays taken
-      L->obUsed[slot] = 0;
+      st1(S.obUsed + slot, 0u);
       waveSync();
       obLive--;
     }
     if (k > 0) {
-      for (int i = 0; i + k < obSeqN; i++) {
-        const uint8_t v = static_cast<uint8_t>(obU(L->obSeq, i + k));
-        waveSync();
-        L->obSeq[i] = v;
-      }
-      waveSync();
+      for (int i = 0; i < k; i++) listClose(S.obSeq, 0, obSeqN - i);  // (k is almost always 1)
       obSeqN -= k;
     }
   }
@@ -2386,12 +2413,12 @@ class HugeDocT {
     uint32_t mlo = 0, mhi = 0, hlo = 0, hhi = 0;
     bool any = false;
     for (int i = 0; i < obStartN; i++) {  // Obliterates.findOverlapping (:566-582)
-      const int slot = obU(L->obStart, i);
-      const int64_t si = ordOf(uni(L->ob[slot].startId));
+      const int slot = obU(S.obStart, i);
+      const int64_t si = ordOf(obF(slot, kObStartId));
       if (!(si >= 0 && si <= k)) break;
-      const int64_t ei = ordOf(uni(L->ob[slot].endId));
+      const int64_t ei = ordOf(obF(slot, kObEndId));
       if (!(ei >= 0 && ei >= k)) continue;
-      const int oseq = uni(L->ob[slot].seq), ocl = uni(L->ob[slot].client);
+      const int oseq = static_cast<int>(obF(slot, kObSeq)), ocl = static_cast<int>(obF(slot, kObClient));
       if (oseq <= refSeq) continue;
       if (ocl != client) {
         any = true;
@@ -2414,12 +2441,12 @@ class HugeDocT {
     if (rmRec) {  // SnapshotV1: every stamp but the first (rm_seq) is a remove-order entry (mergeTree.ts:1715-1725)
       bool firstSkipped = false;
       for (int i = 0; i < obStartN && status == FMT_OK; i++) {
-        const int slot = obU(L->obStart, i);
-        const int64_t si = ordOf(uni(L->ob[slot].startId));
+        const int slot = obU(S.obStart, i);
+        const int64_t si = ordOf(obF(slot, kObStartId));
         if (!(si >= 0 && si <= k)) break;
-        const int64_t ei = ordOf(uni(L->ob[slot].endId));
+        const int64_t ei = ordOf(obF(slot, kObEndId));
         if (!(ei >= 0 && ei >= k)) continue;
-        const int oseq = uni(L->ob[slot].seq), ocl = uni(L->ob[slot].client);
+        const int oseq = static_cast<int>(obF(slot, kObSeq)), ocl = static_cast<int>(obF(slot, kObClient));
         if (oseq <= refSeq || ocl == client) continue;
         if (!firstSkipped && oseq == minSeqOther) {
           firstSkipped = true;
@@ -3722,6 +3749,237 @@ class HugeDocT {
     if (S.mkIds != nullptr) loadMarkers(nLeafBlk);
   }
 
+  // The large tier's state at its checkpoint (huge_ckpt.h) in the paged layout: the same B+tree —
+  // block ids kept, leaf blocks listed in document order kFill per group as a load lists them (a
+  // large document has at most 1023 blocks: one group) —, the same leaf ids, the LRU heap in its array order, the free-block
+  // list, the collab window and the live obliterates; its prop sets are interned again in their id
+  // order and its text goes to the merge area. Returns the op (batch index) to resume at.
+  FMT_DEV uint64_t loadFromLarge() {
+    namespace K = fmt_ckpt;
+    ProfScope ps_(prof[5]);
+    const uint32_t* ck = in.ck;
+    const uint64_t next = ldu(ck + K::kNextLo) | (static_cast<uint64_t>(ldu(ck + K::kNextHi)) << 32);
+    const int n = static_cast<int>(ldu(ck + K::kN));
+    const uint32_t nChars = ldu(ck + K::kNChars);
+    const int nPropsL = static_cast<int>(ldu(ck + K::kNProps));
+    const int heapL = static_cast<int>(ldu(ck + K::kHeapN));
+    const uint32_t nextIdL = ldu(ck + K::kNextId);
+    if (n <= 0 || static_cast<uint32_t>(K::kBlocks) > S.blockCap || nextIdL > S.idCap || heapL > kHeapCap ||
+        nChars > (S.textCap - S.textLen) / 2) {
+      fail(FMT_E_CAPACITY);
+      return 0;
+    }
+    // prop sets, in id order (a wide set spans records: FMT_MT_PROPS_CONT), their new ids in sBlk
+    uint32_t* pmap = L->sBlk;
+    for (int p = 0; p < nPropsL && status == FMT_OK;) {
+      const uint32_t cnt = ldu(&in.ckProps[p].n);
+      if (cnt == FMT_MT_PROPS_CONT || cnt > static_cast<uint32_t>(FMT_MT_PROPS_KEYS_MAX) || p >= kSlotCap) {
+        fail(FMT_E_DATA);
+        return 0;
+      }
+      FOR_LANES(l) {
+        if (l < static_cast<int>(cnt)) L->kvWork[l] = rd(&in.ckProps[p + l / FMT_MT_PROPS_MAX].kv[l % FMT_MT_PROPS_MAX]);
+      }
+      waveSync();
+      const uint32_t id = internWork(cnt);
+      FOR_LANES(l) {
+        if (l == 0) pmap[p] = id;
+      }
+      waveSync();
+      p += cnt > FMT_MT_PROPS_MAX ? static_cast<int>((cnt + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1;
+    }
+    if (status != FMT_OK) return 0;
+    minSeq = static_cast<int>(ldu(ck + K::kMinSeq));
+    curSeq = static_cast<int>(ldu(ck + K::kCurSeq));
+    // the text, into the merge area
+    const uint64_t tb = textTop;
+    FOR_LANES(l) {
+      for (uint32_t t = static_cast<uint32_t>(l); t < nChars; t += 64) S.text[tb + t] = static_cast<uint16_t>(loadWg(in.ckChars + t));
+    }
+    textTop = tb + nChars;
+    // every block's tree fields (free ones too: nothing reaches them)
+    FOR_LANES(l) {
+      for (int b = l; b < K::kBlocks; b += 64) {
+        const uint32_t* o = ck + K::kBlk + K::kBlkWords * b;
+        const uint32_t w0 = rd(o), par = rd(o + 1);
+        const uint32_t cnt = w0 & 0xFFu;
+        S.bCount[b] = cnt;
+        S.bLeaf[b] = (w0 >> 8) & 0xFFu;
+        S.bScour[b] = static_cast<int32_t>(static_cast<int8_t>((w0 >> 16) & 0xFFu));
+        S.bParent[b] = par == K::kNoParent ? kNone : par;
+        if (((w0 >> 8) & 0xFFu) == 0)
+          for (uint32_t c = 0; c < cnt && c < 8; c++) S.bChild[static_cast<size_t>(b) * 8 + c] = rd(o + 2 + c);
+      }
+    }
+    waveSync();
+    // leaf blocks in document order (a run of leaves per block), kFill per group as a load fills
+    // them: ordinal o is slot o % kFill of group o / kFill; the run's first leaf is parked in the
+    // slot's stable-sum word until the leaves are placed
+    const auto slotOf = [](uint32_t o) -> size_t { return static_cast<size_t>(o / kFill) * kSlotCap + o % kFill; };
+    uint32_t nLeafBlk = 0;
+    for (int base = 0; base < n; base += 64) {
+      FOR_LANES(l) {
+        const int j = base + l;
+        if (j < n) {
+          const uint32_t b = rd(ck + K::kLeafBlk + j);
+          if (j == 0 || rd(ck + K::kLeafBlk + j - 1) != b) {
+            const fmt_mt_leaf x = in.ckLeaves[j];
+            const uint32_t o = static_cast<uint32_t>(x.block) | (static_cast<uint32_t>(x.pad & 0x7FFFu) << 16);
+            S.gSlotBlk[slotOf(o)] = b;
+            S.gSlotStable[slotOf(o)] = j;
+          }
+        }
+      }
+    }
+    {
+      const fmt_mt_leaf x = in.ckLeaves[n - 1];
+      nLeafBlk = uni(static_cast<uint32_t>(x.block) | (static_cast<uint32_t>(x.pad & 0x7FFFu) << 16)) + 1u;
+    }
+    nGroups = static_cast<int>((nLeafBlk + kFill - 1) / kFill);
+    if (nGroups > kGroupCap) {
+      fail(FMT_E_CAPACITY);
+      return 0;
+    }
+    waveSync();
+    Lane<bool> winL;
+    FOR_LANES(l) { LANE(winL) = false; }
+    for (uint32_t base = 0; base < nLeafBlk; base += 64) {
+      FOR_LANES(l) {
+        const uint32_t o = base + l;
+        if (o < nLeafBlk) {
+          const uint32_t b = rd(S.gSlotBlk + slotOf(o));
+          const int start = rd(S.gSlotStable + slotOf(o));
+          const uint32_t c = rd(S.bCount + b);
+          int sum = 0;
+          for (uint32_t k = 0; k < c && k < 8; k++) {
+            const int j = start + static_cast<int>(k);
+            const fmt_mt_leaf x = in.ckLeaves[j];
+            const uint32_t w4 = rd(ck + K::kLeafW4 + j);
+            const uint32_t id = w4 & 0x7FFFFFu;
+            const size_t i = li(b, static_cast<int>(k));
+            const uint32_t props = x.props == 0xFFFFu ? kNoProps : L->sBlk[x.props];
+            S.lLen[i] = x.len;
+            S.lIns[i] = x.ins_seq;
+            S.lRm[i] = x.rm_seq;
+            S.lMlo[i] = static_cast<uint32_t>(x.rm_clients);
+            S.lMhi[i] = static_cast<uint32_t>(x.rm_clients >> 32);
+            S.lId[i] = id;
+            S.lText[i] = static_cast<uint32_t>(tb + x.char_off);
+            S.lMeta[i] = mkMeta(x.ins_client, props) | ((w4 & (1u << 23)) != 0 ? kMetaMarker : 0u);
+            S.leafBlk[id] = b;
+            S.winIdx[id] = kNone;
+            if (S.hiMask != nullptr) {
+              S.hiMask[2 * static_cast<size_t>(id)] = 0u;
+              S.hiMask[2 * static_cast<size_t>(id) + 1] = 0u;
+            }
+            const bool win = x.ins_seq > minSeq || (x.rm_seq != kNotRemoved && x.rm_seq > minSeq);
+            if (win) LANE(winL) = true;
+            else if (x.rm_seq == kNotRemoved) sum += static_cast<int>(x.len);
+          }
+          S.bGroup[b] = o / kFill;
+          S.bSlot[b] = o % kFill;
+          S.gSlotStable[slotOf(o)] = sum;
+        }
+      }
+    }
+    waveSync();
+    for (int g = 0; g < nGroups; g++) {
+      const uint32_t lo = static_cast<uint32_t>(g) * kFill, hi = lo + kFill < nLeafBlk ? lo + kFill : nLeafBlk;
+      Lane<uint32_t> acc;
+      FOR_LANES(l) { LANE(acc) = 0; }
+      for (uint32_t base = lo; base < hi; base += 64) {
+        FOR_LANES(l) {
+          if (base + l < hi) LANE(acc) += static_cast<uint32_t>(rd(S.gSlotStable + slotOf(base + l)));
+        }
+      }
+      uint32_t tot;
+      waveExclusiveSum(acc, &tot);
+      L->gOrder[g] = static_cast<uint16_t>(g);
+      L->gStable[g] = static_cast<int32_t>(tot);
+      L->gCount[g] = static_cast<uint16_t>(hi - lo);
+      L->gCorr[g] = 0;
+      waveSync();
+    }
+    root = static_cast<int>(ldu(ck + K::kRoot));
+    nextBlock = K::kBlocks;
+    nFree = static_cast<uint32_t>(ldu(ck + K::kNFree));
+    FOR_LANES(l) {
+      for (uint32_t k = static_cast<uint32_t>(l); k < nFree; k += 64) S.freeBlk[k] = rd(ck + K::kFree + k);
+      for (int k = l; k <= heapL; k += 64) {
+        HeapEnt e;
+        e.maxSeq = static_cast<int32_t>(rd(ck + K::kHeapOff + 2 * k));
+        e.leafId = rd(ck + K::kHeapOff + 2 * k + 1);
+        L->heap[k] = e;
+      }
+    }
+    waveSync();
+    heapN = heapL;
+    lastBlk = ldu(S.gSlotBlk + slotOf(nLeafBlk - 1));
+    nextId = nextIdL;
+    cuN = ldu(ck + K::kCuN);
+    // the window: leaves stamped above minSeq, in document order
+    if (ballot(winL) != 0) {
+      for (uint32_t base = 0; base < nLeafBlk * 8 && status == FMT_OK; base += 64) {
+        Lane<bool> w;
+        FOR_LANES(l) {
+          const uint32_t x = base + l, o = x >> 3, k = x & 7;
+          bool v = false;
+          if (o < nLeafBlk) {
+            const uint32_t b = rd(S.gSlotBlk + slotOf(o));
+            if (k < rd(S.bCount + b)) {
+              const size_t i = li(b, static_cast<int>(k));
+              const int32_t ins = rd(S.lIns + i), rm = rd(S.lRm + i);
+              v = ins > minSeq || (rm != kNotRemoved && rm > minSeq);
+            }
+          }
+          LANE(w) = v;
+        }
+        for (uint64_t m = ballot(w); m != 0 && status == FMT_OK; m &= m - 1) {
+          const uint32_t x = base + static_cast<uint32_t>(ctz64(m));
+          const uint32_t b = ldu(S.gSlotBlk + slotOf(x >> 3));
+          const Leaf y = getLeaf(b, static_cast<int>(x & 7));
+          const uint64_t mask = static_cast<uint64_t>(y.mlo) | (static_cast<uint64_t>(y.mhi) << 32);
+          // window meta: insert client | first remover << 8 | more removers << 16 (the large tier keeps
+          // the set, not which remover came first: the lowest id stands in; the passes read neither)
+          const uint32_t first = mask != 0 ? static_cast<uint32_t>(__builtin_ctzll(mask)) : 0u;
+          const uint32_t meta = (static_cast<uint32_t>(mClient(y.meta)) & 0xFFu) | (first << 8) |
+                                (__builtin_popcountll(mask) > 1 ? 1u << 16 : 0u);
+          winAdd(y.id, y.ins, y.rm, y.len, meta, (x >> 3) / kFill, b, y.mlo, y.mhi);
+        }
+      }
+    }
+    // live obliterates (same slots)
+    const uint32_t obc = ldu(ck + K::kObCounts);
+    const uint64_t used = ldu(ck + K::kObUsedLo) | (static_cast<uint64_t>(ldu(ck + K::kObUsedHi)) << 32);
+    if (used != 0 || obc != 0) {
+      if (S.obCap < static_cast<uint32_t>(K::kObSlots)) {
+        fail(FMT_E_CAPACITY);
+        return 0;
+      }
+      obSeqN = static_cast<int>(obc & 0xFFFFu);
+      obStartN = static_cast<int>(obc >> 16);
+      obLive = __builtin_popcountll(used);
+      obSlotsHi = K::kObSlots;
+      FOR_LANES(l) {
+        const int k = l;  // (kObSlots == 64: one slot per lane)
+        const uint32_t* o = ck + K::kOb + 6 * k;
+        uint32_t* e = S.obRec + 6 * static_cast<size_t>(k);
+        e[kObStartId] = rd(o);
+        e[kObEndId] = rd(o + 1);
+        e[kObStartOff] = rd(o + 2);
+        e[kObEndOff] = rd(o + 3);
+        e[kObSeq] = rd(o + 4);
+        e[kObClient] = rd(o + 5);
+        S.obUsed[k] = static_cast<uint32_t>((used >> k) & 1u);
+        S.obSeq[k] = rd(ck + K::kObSeq + k);
+        S.obStart[k] = rd(ck + K::kObStart + k);
+      }
+      waveSync();
+    }
+    invalidate();
+    return next;
+  }
+
   // Loaded Markers join the marker list (relative positions), in document order.
   FMT_DEV void loadMarkers(uint32_t nLeafBlk) {
     for (uint32_t base = 0; base < nLeafBlk * 8 && status == FMT_OK; base += 64) {
@@ -3854,10 +4112,10 @@ class HugeDocT {
     return op;
   }
 
-  FMT_DEV void replay() {
+  FMT_DEV void replay(uint64_t first) {
     ProfScope ps_(prof[0]);
-    Lane<uint32_t> rec0 = fetchOp(in.begin), rec1 = fetchOp(in.begin + 1);
-    for (uint64_t i = in.begin; i < in.end; i++) {
+    Lane<uint32_t> rec0 = fetchOp(first), rec1 = fetchOp(first + 1);
+    for (uint64_t i = first; i < in.end; i++) {
       fmt_mt_op op = decodeOp(rec0);
       rec0 = rec1;
       rec1 = fetchOp(i + 2);
@@ -4226,13 +4484,21 @@ class HugeDocT {
     mergeLo = S.textLen;
     mergeHi = S.textLen + (S.textCap - S.textLen) / 2;
     status = FMT_OK;
-    obLive = obSeqN = obStartN = 0;
-    FOR_LANES(l) {
-      for (int k = l; k < kObCap; k += 64) L->obUsed[k] = 0;
+    obLive = obSeqN = obStartN = obSlotsHi = 0;
+    for (uint32_t base = 0; base < S.obCap; base += 64) {
+      FOR_LANES(l) {
+        if (base + l < S.obCap) S.obUsed[base + l] = 0u;
+      }
     }
     waveSync();
-    load();
-    if (status == FMT_OK) replay();
+    uint64_t first = in.begin;
+    if (in.ck != nullptr) {
+      first = loadFromLarge();  // (an index into the batch's ops, as in.begin)
+      prof[24] = first - in.begin;
+    } else {
+      load();
+    }
+    if (status == FMT_OK) replay(first);
   }
 };
 

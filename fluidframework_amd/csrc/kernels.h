@@ -69,6 +69,9 @@ struct MtDeviceOut {
   // annotate-adjust batches: per leaf the prop set of getAtSeq(minSeq) (legacy summaries), at the
   // leaves slab's stride; nullptr otherwise
   uint16_t* legacyProps;
+  // large tier over a plain batch: per large-tier slot, its large → huge checkpoint record
+  // (huge_ckpt.h, fmt_ckpt::kWords words), or nullptr
+  uint32_t* hugeCkpt = nullptr;
 };
 // Bytes of one document's tier checkpoint (mt_engine.h Doc::kCkptWords).
 size_t mergeTreeCheckpointBytes();

@@ -142,6 +142,7 @@ __global__ __launch_bounds__(64 * Waves, WavesPerEU) void mergeTreeKernel(MtDevi
     o.bigCkpt = nullptr;
     o.bigCkptChars = nullptr;
     o.legacyProps = out.legacyProps ? out.legacyProps + slot * Slab<C>::kLeaves : nullptr;
+    o.hugeCkpt = Doc::kSavesHuge && out.hugeCkpt != nullptr ? out.hugeCkpt + slot * static_cast<size_t>(fmt_ckpt::kWords) : nullptr;
     if constexpr (Doc::kSavesBig) {  // batches without remove order (out.ckpt set): the small tier's own slabs
       if (out.ckpt != nullptr) {
         o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);

@@ -32,6 +32,7 @@
 #include "../../include/fmt.h"
 #include "wave.h"
 #include "adjust.h"
+#include "huge_ckpt.h"
 
 #include <cstddef>
 #include <type_traits>
@@ -244,6 +245,8 @@ struct DocOutputs {
   // annotate-adjust batches: per leaf, the prop-set id of getAtSeq(properties, minSeq), what the legacy
   // summary reads (snapshotlegacy.ts:211-212); nullptr otherwise
   uint16_t* legacyProps;
+  // large tier, plain batches: the document's large → huge checkpoint record (huge_ckpt.h), or nullptr
+  uint32_t* hugeCkpt = nullptr;
 };
 
 // Diagnostic build only (FMT_PROFILE=1): per-phase shader-clock totals, see stamp().
@@ -390,6 +393,77 @@ class Doc {
                 "the small tier's checkpoint fits its leaves slab");
   uint32_t* bigCkpt = nullptr;
   uint16_t* bigCkptChars = nullptr;
+
+  // large → huge (round 5; huge_ckpt.h): a plain document the large tier is about to outgrow stops
+  // before the op, writes its result slabs and the checkpoint record, and the huge tier replays on
+  // from that op with the same tree.
+  static constexpr bool kSavesHuge = C::kHbmChars && !Rm && !Loc && !Adj;
+  uint32_t* hugeCkpt = nullptr;
+  FMT_DEV void saveHuge(uint64_t next) {
+    namespace K = fmt_ckpt;
+    uint32_t* ck = hugeCkpt;
+    FOR_LANES(l) {
+      if (l == 0) {
+        ck[K::kNextLo] = static_cast<uint32_t>(next);
+        ck[K::kNextHi] = static_cast<uint32_t>(next >> 32);
+        ck[K::kN] = static_cast<uint32_t>(n);
+        ck[K::kNChars] = static_cast<uint32_t>(nChars);
+        ck[K::kRoot] = static_cast<uint32_t>(root);
+        ck[K::kNFree] = static_cast<uint32_t>(nFree);
+        ck[K::kHeapN] = static_cast<uint32_t>(heapN);
+        ck[K::kNProps] = static_cast<uint32_t>(nProps);
+        ck[K::kCurSeq] = static_cast<uint32_t>(curSeq);
+        ck[K::kMinSeq] = static_cast<uint32_t>(minSeq);
+        ck[K::kNextId] = nextId;
+        ck[K::kCuN] = cuN;
+        ck[K::kObCounts] = Ob ? static_cast<uint32_t>(obSeqN) | (static_cast<uint32_t>(obStartN) << 16) : 0u;
+        ck[K::kObUsedLo] = Ob ? static_cast<uint32_t>(obUsed) : 0u;
+        ck[K::kObUsedHi] = Ob ? static_cast<uint32_t>(obUsed >> 32) : 0u;
+      }
+    }
+    static_assert(!kSavesHuge || (kCapLeaves == K::kLeaves && kMaxBlocks == K::kBlocks && kHeapCap + 1 == K::kHeap &&
+                                  kObCap == K::kObSlots), "huge_ckpt.h layout");
+    const int nr = rows();
+    FOR_ROWS(r, 0, nr) {
+      FOR_LANES(l) {
+        const int j = r * 64 + l;
+        if (j < n) {
+          ck[K::kLeafW4 + j] = LANE(W[4])[r];
+          ck[K::kLeafBlk + j] = fBlk(LANE(W[0])[r]);
+        }
+      }
+    }
+    FOR_LANES(l) {
+      for (int b = l; b < kMaxBlocks; b += 64) {
+        const Blk<BId> k = s->blk[b];
+        uint32_t* o = ck + K::kBlk + K::kBlkWords * b;
+        o[0] = static_cast<uint32_t>(k.count) | (static_cast<uint32_t>(k.leaf) << 8) |
+               (static_cast<uint32_t>(static_cast<uint8_t>(k.needsScour)) << 16);
+        o[1] = static_cast<uint32_t>(k.parent) == kNoBlk ? K::kNoParent : static_cast<uint32_t>(k.parent);
+        for (int c = 0; c < kMaxNodes; c++) o[2 + c] = static_cast<uint32_t>(k.child[c]);
+      }
+      for (int k = l; k <= heapN; k += 64) {
+        ck[K::kHeapOff + 2 * k] = static_cast<uint32_t>(s->heap[k].maxSeq);
+        ck[K::kHeapOff + 2 * k + 1] = s->heap[k].leafId;
+      }
+      for (int k = l; k < nFree; k += 64) ck[K::kFree + k] = static_cast<uint32_t>(s->freeList[k]);
+      if constexpr (Ob) {
+        for (int k = l; k < kObCap; k += 64) {
+          const ObEnt e = s->ob[k];
+          uint32_t* o = ck + K::kOb + 6 * k;
+          o[0] = e.startId;
+          o[1] = e.endId;
+          o[2] = static_cast<uint32_t>(e.startOff);
+          o[3] = static_cast<uint32_t>(e.endOff);
+          o[4] = static_cast<uint32_t>(e.seq);
+          o[5] = static_cast<uint32_t>(e.client);
+          ck[K::kObSeq + k] = s->obSeq[k];
+          ck[K::kObStart + k] = s->obStart[k];
+        }
+      }
+    }
+    waveSync();
+  }
 
   FMT_DEV void saveBig(uint64_t next) {
     uint32_t* ck = bigCkpt;
@@ -1901,7 +1975,8 @@ class Doc {
   }
 
   FMT_DEV bool obAdd(uint32_t sId, int sOff, uint32_t eId, int eOff, int seq, int client) {
-    if (obUsed == ~0ull) return fail(kCapFinal);
+    // (more live obliterates than this table holds: the document grows, up to the huge tier's HBM table)
+    if (obUsed == ~0ull) return fail(FMT_E_CAPACITY);
     const int slot = ctz64(~obUsed);
     obUsed |= 1ull << slot;
     s->ob[slot].startId = sId;
@@ -1916,7 +1991,7 @@ class Doc {
     bool exists;
     const int at = findStart(slot, &exists);
     if (!exists) {
-      if (obStartN >= kObCap) return fail(kCapFinal);
+      if (obStartN >= kObCap) return fail(FMT_E_CAPACITY);
       for (int i = obStartN; i > at; i--) {
         const uint8_t v = s->obStart[i - 1];
         waveSync();
@@ -3690,6 +3765,19 @@ class Doc {
     const bool canSave = kSavesCkpt ? ckpt != nullptr : bigCkpt != nullptr && (!Ob || ckpt != nullptr);
     for (uint64_t i = first; i < in.end; i++) {
       fmt_mt_op op = decodeOp(rec0);
+      if constexpr (kSavesHuge) {
+        // large tier: the same limits — rows, text, blocks, prop sets, writers past 63 — stop the
+        // document for the huge tier (a document still empty restarts there instead)
+        const bool loaderNonCollab = (op.flags & FMT_MT_F_LOADSEG) != 0 && op.client == FMT_MT_CLIENT_NONCOLLAB;
+        if (hugeCkpt != nullptr && n > 0 &&
+            (n + 2 > kCapLeaves || (op.type == FMT_MT_INSERT && nChars + static_cast<int>(opLen(op)) > kCapChars) ||
+             (op.client > kMaxClient && !loaderNonCollab) || nFree < 16 ||
+             ((op.type == FMT_MT_ANNOTATE || op.type == FMT_MT_INSERT) && nProps > kPropCap - 4))) {
+          ckptNext = i;
+          status = kCkptEscalate;
+          return;
+        }
+      }
       if constexpr (kSavesCkpt || kSavesBig) {
         // the op could outgrow the rows (at most two new leaves), the text, or (small tier) the
         // writer set of this tier
@@ -3941,7 +4029,19 @@ class Doc {
       if (in.loaded) loadSnapshot();
       else loadInitial();
     }
+    hugeCkpt = out.hugeCkpt;
     if (status == FMT_OK) replay(first);
+    if constexpr (kSavesHuge) {
+      if (status == kCkptEscalate) {  // the huge tier resumes: the result slabs, then the record
+        status = FMT_OK;
+        writeOutputs(out);
+        saveHuge(ckptNext);
+        FOR_LANES(l) {
+          if (l == 0) out.header->status = fmt_ckpt::kStatusHuge;
+        }
+        return;
+      }
+    }
     if ((kSavesCkpt || kSavesBig) && status == kCkptEscalate) {  // the next tier writes everything else
       if constexpr (!Ob && kSavesCkpt) saveCkpt(ckptNext);
       else if constexpr (!Ob && kSavesBig) saveBig(ckptNext);

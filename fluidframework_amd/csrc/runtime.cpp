@@ -150,6 +150,7 @@ struct fmt_ctx {
   DevBuf<uint32_t> mtEsc2;                   // compact-tier overflow list (no remove order), same layout
   DevBuf<uint32_t> mtEsc3;                   // the same list, longest remaining streams first
   DevBuf<uint32_t> mtCkpt;                   // per-document compact → small tier checkpoints
+  DevBuf<uint32_t> mtHugeCk;                 // per large-tier slot: its large → huge checkpoint record (huge_ckpt.h)
   bool mtCkptOk = false;                     // allocated for this batch (else tiers replay overflow from op 0)
   DevBuf<uint32_t> mtSched;                  // per-tier document counters (dynamic dealing to waves)
   DevBuf<fmt_mt_leaf> mtBigLeaves;           // large-tier result slabs, one per escalated doc
@@ -441,6 +442,7 @@ void fmt_close(fmt_ctx* c) {
   c->mtEsc3.release();
   c->mtSched.release();
   c->mtCkpt.release();
+  c->mtHugeCk.release();
   c->mtBigLeaves.release();
   c->mtBigChars.release();
   c->mtBigProps.release();
@@ -933,6 +935,18 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
   }
   if ((e = alloc(fmt_huge::HugeDoc::kProf * sizeof(unsigned long long), &p)) != hipSuccess) return drop(e);
   O.prof = static_cast<unsigned long long*>(p);
+  // live obliterates: at most one per op of the document is alive at once (HBM; batches with obliterates)
+  S.obRec = S.obUsed = S.obSeq = S.obStart = nullptr;
+  S.obCap = 0;
+  if (c->mtObliterate && nOps > 0) {
+    if (nOps > 0x0FFFFFFFull) return drop(hipErrorOutOfMemory);
+    S.obCap = static_cast<uint32_t>(std::max<uint64_t>(nOps, fmt_ckpt::kObSlots));  // (a checkpoint keeps its slot ids)
+    if ((e = alloc(9ull * S.obCap * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    S.obRec = static_cast<uint32_t*>(p);
+    S.obUsed = S.obRec + 6ull * S.obCap;
+    S.obSeq = S.obUsed + S.obCap;
+    S.obStart = S.obSeq + S.obCap;
+  }
   // remove clients 64..127: the per-leaf-id side table (zeroed) and its per-leaf output
   S.hiMask = nullptr;
   O.leavesHi = nullptr;
@@ -1518,11 +1532,16 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigChars.reserve(static_cast<size_t>(nEsc) * big.chars));
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     if (c->mtHasAdjust) FMT_HIP(c, c->mtBigLegacy.reserve(static_cast<size_t>(nEsc) * big.leaves));
+    // plain batches: a document the large tier is about to outgrow leaves a checkpoint for the huge
+    // tier (huge_ckpt.h) instead of failing; without the slab it restarts there from its first op
+    const bool hugeCk = !c->mtHasRmOrder && !c->mtHasAdjust && c->mtNRelpos == 0 && !c->mtLocal &&
+                        c->mtHugeCk.reserve(static_cast<size_t>(nEsc) * fmt_ckpt::kWords) == hipSuccess;
+    if (!hugeCk) (void)hipGetLastError();
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,
                                   c->mtHasCatchup ? c->mtCatchup.p : nullptr, c->mtHasRmOrder ? c->mtRmOrder.p : nullptr,
                                   c->mtObliterate && !c->mtHasRmOrder && !c->mtHasAdjust && c->mtCkptOk ? c->mtCkpt.p : nullptr,
                                   !c->mtHasRmOrder ? c->mtLeaves.p : nullptr, !c->mtHasRmOrder ? c->mtChars.p : nullptr,
-                                  c->mtHasAdjust ? c->mtBigLegacy.p : nullptr};
+                                  c->mtHasAdjust ? c->mtBigLegacy.p : nullptr, hugeCk ? c->mtHugeCk.p : nullptr};
     FMT_HIP(c, hipEventRecord(c->ev2, c->stream));
     FMT_HIP(c, fmt_kernels::launchMergeTreeLarge(db, bout, c->mtEsc.p + 1, nEsc, c->numCUs, c->stream, c->mtObliterate,
                                                  c->mtHasRmOrder, c->mtSched.p + 2, c->mtHasAdjust, c->mtLocal));
@@ -1537,13 +1556,18 @@ int fmt_mt_run(fmt_ctx* c) {
     // the reference grows a tree without bound (insertSegments, mergeTree.ts:1484-1517).
     std::vector<fmt_mt_doc_result> hb(nEsc);
     std::vector<uint32_t> grow;
+    std::vector<int32_t> growSlot;  // the large-tier slot of a checkpointed document (-1: restart from op 0)
     for (uint32_t i = 0; i < nEsc; i++) {
       FMT_HIP(c, hipMemcpyAsync(&hb[i], c->mtHdr.p + list[i], sizeof(fmt_mt_doc_result), hipMemcpyDeviceToHost, c->stream));
     }
     FMT_HIP(c, hipStreamSynchronize(c->stream));
-    for (uint32_t i = 0; i < nEsc; i++)
-      if (hb[i].status == FMT_E_CAPACITY && c->mtHugeOk[list[i]] && c->mtHugeSlot[list[i]] < 0 && !c->mtLocal)
+    for (uint32_t i = 0; i < nEsc; i++) {
+      if ((hb[i].status == FMT_E_CAPACITY || hb[i].status == fmt_ckpt::kStatusHuge) && c->mtHugeOk[list[i]] &&
+          c->mtHugeSlot[list[i]] < 0 && !c->mtLocal) {
         grow.push_back(list[i]);
+        growSlot.push_back(hb[i].status == fmt_ckpt::kStatusHuge ? static_cast<int32_t>(i) : -1);
+      }
+    }
     if (!grow.empty()) {
       FMT_HIP(c, c->mtStartSegDev.reserve(grow.size()));
       std::vector<fmt_mt_snapshot_seg> starts(grow.size());
@@ -1565,6 +1589,20 @@ int fmt_mt_run(fmt_ctx* c) {
                             0, 0, 0, FMT_LOCAL_CLIENT, 1024, c->mtDocChars[d]);
         }
         if (rc != FMT_OK && rc != FMT_E_CAPACITY) return rc;
+        if (growSlot[i] >= 0) {
+          if (rc == FMT_OK) {  // resume from the large tier's checkpoint and result slabs
+            const size_t k = static_cast<size_t>(growSlot[i]);
+            fmt_huge::HugeInputs& I = c->huge.back().in;
+            I.ck = c->mtHugeCk.p + k * fmt_ckpt::kWords;
+            I.ckLeaves = c->mtBigLeaves.p + k * big.leaves;
+            I.ckChars = c->mtBigChars.p + k * big.chars;
+            I.ckProps = c->mtBigProps.p + k * big.props;
+          } else {  // (no room in device memory: the document reports FMT_E_CAPACITY)
+            const int32_t st = FMT_E_CAPACITY;
+            FMT_HIP(c, hipMemcpyAsync(&c->mtHdr.p[d].status, &st, sizeof st, hipMemcpyHostToDevice, c->stream));
+            FMT_HIP(c, hipStreamSynchronize(c->stream));
+          }
+        }
       }
       const size_t ng = c->huge.size() - c->mtHugeLoaded;
       if (ng > 0) {

@@ -436,14 +436,14 @@ class Engine:
     def huge_profile(self, doc: int):
         """Diagnostics: shader-clock totals per phase of a huge document's last replay
         (inclusive; nested phases overlap)."""
-        out = np.zeros(24, dtype=np.uint64)
+        out = np.zeros(25, dtype=np.uint64)
         f = self.L.fmt_internal_huge_profile
         f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
         self._check(f(self.h, doc, _ptr(out)))
         names = ["replay", "window_groups", "window_slots", "zamboni", "graduate", "load", "output", "find",
                  "scour", "pack_leaf_parent", "slot_shift", "heap", "insert", "range", "split", "pack_interior",
                  "n_group_passes", "n_slot_passes", "sum_window_entries", "sum_groups", "window_share_w0", "group_scan",
-                 "text_compactions", "merge_units_in_use"]
+                 "text_compactions", "merge_units_in_use", "resumed_at"]
         return dict(zip(names, (int(x) for x in out)))
 
     def mt_remove_order(self, doc: int, hdr=None) -> np.ndarray:

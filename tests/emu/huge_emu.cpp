@@ -74,6 +74,12 @@ const fmt_mt::AdjustTables* prepareNumbers(const fmt_mt_batch* b) {
 }
 // emu_huge_replay_hi: the per-leaf output of remove clients 64..127 for the next replay (or nullptr)
 uint64_t* g_hiOut = nullptr;
+// emu_huge_resume: the large tier's checkpoint record and result slabs for the next replay (or nullptr)
+const uint32_t* g_ck = nullptr;
+const fmt_mt_leaf* g_ckLeaves = nullptr;
+const uint16_t* g_ckChars = nullptr;
+const fmt_mt_propset* g_ckProps = nullptr;
+uint64_t g_resumedAt = 0;
 }  // namespace
 
 extern "C" {
@@ -153,6 +159,15 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   S.cuIds = catchup != nullptr ? cuIds.data() : nullptr;
   std::vector<uint32_t> rmIds(rmOrder != nullptr ? S.idCap : 0);
   S.rmIds = rmOrder != nullptr ? rmIds.data() : nullptr;
+  bool obl = false;  // (runtime.cpp: the live-obliterate table of batches with obliterates)
+  for (uint64_t i = 0; i < b->n_ops && !obl; i++) obl = b->ops[i].type == FMT_MT_OBLITERATE || b->ops[i].type == FMT_MT_OBLITERATE_SIDED;
+  const uint64_t obCap = std::max<uint64_t>(nOps, fmt_ckpt::kObSlots);  // (runtime.cpp setupHugeDoc)
+  std::vector<uint32_t> obTab(obl ? 9ull * obCap : 0, 0xCDCDCDCDu);
+  S.obCap = obl ? static_cast<uint32_t>(obCap) : 0u;
+  S.obRec = obl ? obTab.data() : nullptr;
+  S.obUsed = obl ? obTab.data() + 6ull * obCap : nullptr;
+  S.obSeq = obl ? S.obUsed + obCap : nullptr;
+  S.obStart = obl ? S.obSeq + obCap : nullptr;
   std::vector<uint32_t> hiMask(g_hiOut != nullptr ? 2ull * S.idCap : 0, 0u);  // (runtime.cpp: zeroed)
   S.hiMask = g_hiOut != nullptr ? hiMask.data() : nullptr;
   auto lds = std::make_unique<HugeLds>();
@@ -197,7 +212,12 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   in.snapMinSeq = sd.min_seq;
   in.snapSeq = sd.seq;
   in.initClient = loaded ? FMT_NON_COLLAB_CLIENT : FMT_LOCAL_CLIENT;
+  in.ck = g_ck;
+  in.ckLeaves = g_ckLeaves;
+  in.ckChars = g_ckChars;
+  in.ckProps = g_ckProps;
   doc->run(in);
+  g_resumedAt = doc->prof[24];
   doc->writeOutputs(hdr, leaves, capLeaves, chars, capChars, props, adj != nullptr ? legacy : nullptr, g_hiOut);
   if (nNums) *nNums = adj != nullptr ? g_numCount[d] : 0u;
   for (uint32_t k = 0; adj != nullptr && nums != nullptr && k < g_numCount[d] && k < capNums; k++) nums[k] = g_nums[k];
@@ -223,6 +243,27 @@ int emu_huge_replay_rec(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
 int emu_huge_replay(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
                     uint16_t* chars, uint64_t capChars, fmt_mt_propset* props) {
   return emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0, nullptr, 0);
+}
+
+// Document d resumed in the huge tier from the large tier's checkpoint (emu_mt_replay_large_ckpt: its
+// record ck and its result slabs at large strides, leaves / chars / props of document d). Returns the
+// status; *resumedAt = the op index within the document it resumed at.
+int emu_huge_resume(const fmt_mt_batch* b, uint32_t d, const uint32_t* ck, const fmt_mt_leaf* ckLeaves,
+                    const uint16_t* ckChars, const fmt_mt_propset* ckProps, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves,
+                    uint64_t capLeaves, uint16_t* chars, uint64_t capChars, fmt_mt_propset* props,
+                    fmt_mt_catchup_range* catchup, uint32_t capCatchup, uint64_t* resumedAt) {
+  g_ck = ck;
+  g_ckLeaves = ckLeaves;
+  g_ckChars = ckChars;
+  g_ckProps = ckProps;
+  g_resumedAt = 0;
+  const int st = emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, catchup, capCatchup, nullptr, 0);
+  g_ck = nullptr;
+  g_ckLeaves = nullptr;
+  g_ckChars = nullptr;
+  g_ckProps = nullptr;
+  if (resumedAt) *resumedAt = g_resumedAt;
+  return st;
 }
 
 // As emu_huge_replay, with the remove-client side table for short ids 64..127 (the runtime allocates

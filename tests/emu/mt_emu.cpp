@@ -119,7 +119,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
                      fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* ckpt = nullptr,
                      bool onlyEscalated = false, size_t leafStride = 0, size_t charStride = 0,
                      const fmt_mt_leaf* smallLeaves = nullptr, const uint16_t* smallChars = nullptr,
-                     uint16_t* legacy = nullptr) {
+                     uint16_t* legacy = nullptr, uint32_t* hugeCk = nullptr) {
   using Doc = fmt_mt::Doc<Ob, C, Rm, Adj, Loc>;
   auto scratch = std::make_unique<fmt_mt::Scratch<C>>();
   auto doc = std::make_unique<Doc>();
@@ -179,6 +179,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     o.bigCkpt = nullptr;
     o.bigCkptChars = nullptr;
     o.legacyProps = legacy ? legacy + static_cast<size_t>(d) * (leafStride ? leafStride : Doc::kCapLeaves) : nullptr;
+    o.hugeCkpt = Doc::kSavesHuge && hugeCk != nullptr ? hugeCk + static_cast<size_t>(d) * fmt_ckpt::kWords : nullptr;
     if (Doc::kSavesBig && ckpt != nullptr) {  // the small tier of a cascade: its own slabs
       o.bigCkpt = reinterpret_cast<uint32_t*>(o.leaves);
       o.bigCkptChars = o.chars;
@@ -193,6 +194,7 @@ static int replayAll(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_l
     doc->run(in, o);
     if (headers[d].status == fmt_mt::kCapacityFinal) headers[d].status = FMT_E_CAPACITY;  // as collectOverflowKernel
     if (headers[d].status == fmt_mt::kCkptEscalate) continue;  // the small tier resumes it
+    if (headers[d].status == fmt_ckpt::kStatusHuge) continue;  // the huge tier resumes it
     if (headers[d].status != FMT_OK && status == FMT_OK) status = headers[d].status;
   }
   return status;
@@ -349,6 +351,24 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
   if (rm) return replayAll<false, S, true>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
   return replayAll<false, S>(b, headers, leaves, chars, props, catchup, capCatchup, rmOrder, capRm);
 }
+
+// The large tier over every document from its first op, each document it is about to outgrow
+// stopping with its large → huge checkpoint (hugeCk: fmt_ckpt::kWords words per document; header
+// status fmt_ckpt::kStatusHuge) for emu_huge_resume (results at large strides).
+int emu_mt_replay_large_ckpt(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                             fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, uint32_t* hugeCk) {
+  g_nums.clear();
+  g_legacyStride = 0;
+  bool ob = false;
+  for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE || b->ops[i].type == FMT_MT_OBLITERATE_SIDED;
+  using G = fmt_mt::LargeTier;
+  return ob ? replayAll<true, G>(b, headers, leaves, chars, props, catchup, capCatchup, nullptr, 0, nullptr, false, 0, 0,
+                                 nullptr, nullptr, nullptr, hugeCk)
+            : replayAll<false, G>(b, headers, leaves, chars, props, catchup, capCatchup, nullptr, 0, nullptr, false, 0, 0,
+                                  nullptr, nullptr, nullptr, hugeCk);
+}
+
+uint32_t emu_huge_ckpt_words() { return fmt_ckpt::kWords; }
 
 // f4 batches (local submissions, acks, rollbacks, reconnects): the large tier's Loc variant over every
 // document, as the runtime runs them (results at large strides).

@@ -23,7 +23,7 @@ def emu_lib():
     global _emu
     if _emu is None:
         src = os.path.join(HERE, "emu", "mt_emu.cpp")
-        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("mt_engine.h", "wave.h")]
+        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("mt_engine.h", "wave.h", "huge_ckpt.h", "adjust.h")]
         if not os.path.exists(EMU_PATH) or os.path.getmtime(EMU_PATH) < max(os.path.getmtime(d) for d in deps):
             os.makedirs(os.path.dirname(EMU_PATH), exist_ok=True)
             subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas", "-o",
@@ -37,6 +37,8 @@ def emu_lib():
         L.emu_mt_replay_local.argtypes = [ctypes.c_void_p] * 5
         L.emu_mt_regen.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                    ctypes.POINTER(ctypes.c_uint32)]
+        L.emu_mt_replay_large_ckpt.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p]
+        L.emu_huge_ckpt_words.restype = ctypes.c_uint32
         _emu = L
     return _emu
 
@@ -52,7 +54,7 @@ def huge_emu_lib(tiny_groups=False):
         name = "libhuge_emu_tiny.so" if tiny_groups else "libhuge_emu.so"
         path = os.path.join(HERE, "_build", name)
         src = os.path.join(HERE, "emu", "huge_emu.cpp")
-        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("huge_engine.h", "wave.h", "adjust.h")]
+        deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("huge_engine.h", "wave.h", "adjust.h", "huge_ckpt.h")]
         if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(d) for d in deps):
             os.makedirs(os.path.dirname(path), exist_ok=True)
             extra = ["-DFMT_HUGE_SLOTCAP=16", "-DFMT_HUGE_FILL=8"] if tiny_groups else []
@@ -66,6 +68,9 @@ def huge_emu_lib(tiny_groups=False):
         L.emu_huge_replay_adj.argtypes = L.emu_huge_replay_rec.argtypes + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                                           ctypes.c_void_p]
         L.emu_huge_replay_hi.argtypes = L.emu_huge_replay.argtypes + [ctypes.c_void_p]
+        L.emu_huge_resume.argtypes = ([ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 6 +
+                                      [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)])
         _huge[tiny_groups] = L
     return _huge[tiny_groups]
 
@@ -150,6 +155,60 @@ def emu_huge_replay_hi(batch, doc=0, tiny_groups=False, cap_props=65534):
     h = hdr[0]
     n = int(h["n_leaves"])
     return h, leaves[:n], chars[: int(h["n_chars"])], props[: int(h["n_props"])], hi[:n]
+
+
+def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
+    """The runtime's large → huge path under host emulation: the large tier over every document from
+    its first op, each document it is about to outgrow stopping at its checkpoint (huge_ckpt.h), then
+    the huge tier resuming it from there. Returns per document (header, leaves, chars, props[, catch-up
+    ranges]) and the op index each resumed at (0: the large tier finished it)."""
+    cl, cc, cp = emu_caps(True)
+    n = batch.n_docs
+    hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
+    leaves = np.zeros(n * cl, dtype=LEAF_DTYPE)
+    chars = np.zeros(n * cc, dtype="<u2")
+    props = np.zeros(n * cp, dtype=PROPSET_DTYPE)
+    cu = np.zeros(max(n * cap_catchup, 1), dtype=CATCHUP_DTYPE)
+    L = emu_lib()
+    ck = np.zeros(n * int(L.emu_huge_ckpt_words()), dtype=np.uint32)
+    b, keep = batch_struct(batch)
+    L.emu_mt_replay_large_ckpt(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props),
+                               _p(cu) if cap_catchup else None, cap_catchup, _p(ck))
+    words = int(L.emu_huge_ckpt_words())
+    out, resumed = [], []
+    for d in range(n):
+        if int(hdr[d]["status"]) != -35:  # (fmt_ckpt::kStatusHuge)
+            h = hdr[d]
+            res = (h, leaves[d * cl: d * cl + int(h["n_leaves"])], chars[d * cc: d * cc + int(h["n_chars"])],
+                   props[d * cp: d * cp + int(h["n_props"])])
+            if cap_catchup:
+                res = res + (cu[d * cap_catchup: d * cap_catchup + int(h["n_catchup"])],)
+            out.append(res)
+            resumed.append(0)
+            continue
+        sd = batch.snapshots[d] if batch.snapshots is not None else None
+        segs = int(sd["n_header"]) + int(sd["n_body"]) if sd is not None and sd["loaded"] else 1
+        nops = int(batch.doc_op_offsets[d + 1] - batch.doc_op_offsets[d])
+        hcl, hcc = segs + 3 * nops + 8, len(batch.text) + 8 + int(batch.doc_init[d][1]) + cc
+        h1 = np.zeros(1, dtype=DOC_RESULT_DTYPE)
+        lv = np.zeros(hcl, dtype=LEAF_DTYPE)
+        ch = np.zeros(hcc, dtype="<u2")
+        pr = np.zeros(65534, dtype=PROPSET_DTYPE)
+        cud = np.zeros(max(cap_catchup, 1), dtype=CATCHUP_DTYPE)
+        if cap_catchup:
+            cud[:cap_catchup] = cu[d * cap_catchup: (d + 1) * cap_catchup]
+        at = ctypes.c_uint64(0)
+        huge_emu_lib(tiny_groups).emu_huge_resume(
+            ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
+            _p(h1), _p(lv), hcl, _p(ch), hcc, _p(pr), _p(cud) if cap_catchup else None, cap_catchup, ctypes.byref(at))
+        h = h1[0]
+        res = (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
+        if cap_catchup:
+            res = res + (cud[: int(h["n_catchup"])],)
+        out.append(res)
+        resumed.append(int(at.value))
+    del keep
+    return out, resumed
 
 
 def oracle_rm_clients_hi(batch, doc, n_leaves):
