@@ -39,14 +39,23 @@ def build(name, edits, rev=None, flags=()):
         s = open(p).read()
         assert old in s, (name, fname, old[:50])
         open(p, "w").write(s.replace(old, new))
-    # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc)
+    # kernels the variants do not touch link from the in-tree build (make -C fluidframework_amd/csrc);
+    # VARIANT_ONLY=a.hip,b.hip compiles only those of the rest (the others from the in-tree build too)
     objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "map_pending.o", "summary.o", "digest.o", "transfer.o")]
+    only = [x for x in os.environ.get("VARIANT_ONLY", "").split(",") if x]
+    procs = []
     for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip", "hugedoc.hip"]:
+        if only and f not in only:
+            objs.append(os.path.join(REPO, "build", "fmt", f.split(".")[0] + ".o"))
+            continue
         o = os.path.join(root, f + ".o")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-variable",
                *flags, "-x", "hip", "-c", "-o", o, os.path.join(csrc, f)]
-        subprocess.run(cmd, check=True)
+        procs.append(subprocess.Popen(cmd))
         objs.append(o)
+    for pr in procs:
+        if pr.wait() != 0:
+            raise SystemExit(f"{name}: compile failed")
     out = os.path.join(root, "libfmt.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", out] + objs, check=True)
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-variable", *flags,
@@ -126,7 +135,76 @@ COLD = [("wave.h", "#define FMT_DEV __device__ __forceinline__",
         ("wave.h", "#define FMT_DEV inline\n", "#define FMT_DEV inline\n#define FMT_COLD inline\n")] + \
        [("huge_engine.h", "  FMT_DEV " + f, "  FMT_COLD " + f) for f in _COLD_FNS]
 
+# chars moves 256 units per iteration (4 loads per lane in flight, one wave sync per 256) instead of 64
+SHIFT4 = [("mt_engine.h", """    const int count = nChars - from;
+    for (int top = count - 1; top >= 0; top -= 64) {
+      Lane<uint32_t> v;
+      FOR_LANES(l) {
+        const int t = top - l;
+        LANE(v) = t >= 0 ? chRead(from + t) : 0u;
+      }
+      waveSync();
+      FOR_LANES(l) {
+        const int t = top - l;
+        if (t >= 0) chWrite(from + t + by, LANE(v));
+      }
+      waveSync();
+    }""", """    const int count = nChars - from;
+    for (int top = count - 1; top >= 0; top -= 256) {
+      Lane<uint32_t> v[4];
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int t = top - l - 64 * u;
+          LANE(v[u]) = t >= 0 ? chRead(from + t) : 0u;
+        }
+      }
+      waveSync();
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int t = top - l - 64 * u;
+          if (t >= 0) chWrite(from + t + by, LANE(v[u]));
+        }
+      }
+      waveSync();
+    }"""),
+          ("mt_engine.h", """    for (int base = from; base < nChars; base += 64) {
+      Lane<uint32_t> v;
+      FOR_LANES(l) {
+        const int t = base + l;
+        LANE(v) = t < nChars ? chRead(t) : 0u;
+      }
+      waveSync();
+      FOR_LANES(l) {
+        const int t = base + l;
+        if (t < nChars) chWrite(t - by, LANE(v));
+      }
+      waveSync();
+    }""", """    for (int base = from; base < nChars; base += 256) {
+      Lane<uint32_t> v[4];
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int t = base + l + 64 * u;
+          LANE(v[u]) = t < nChars ? chRead(t) : 0u;
+        }
+      }
+      waveSync();
+      FOR_LANES(l) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int t = base + l + 64 * u;
+          if (t < nChars) chWrite(t - by, LANE(v[u]));
+        }
+      }
+      waveSync();
+    }""")]
+
 VARIANTS = {
+    "shift4": SHIFT4,
+    "pass8": [("huge_engine.h", "  static constexpr int kPassU = 16;", "  static constexpr int kPassU = 8;")],
+    "hcur": [],
     "cold": COLD,
     "fetch_uni": FETCH_UNI,
     "ob_s1": [OB_S1],
@@ -168,7 +246,7 @@ FLAGS = {
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
     "lines": ["-gline-tables-only"],  # (line tables only: the same code, for PC-sample attribution)
 }
-REVS = {"v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
+REVS = {"r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
         "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
 
 
