@@ -842,12 +842,12 @@ class HugeDocT {
     waveSync();
   }
 
-  // This wave's steps of one pass over the window table, 16 x 64 records per step with every load of
+  // This wave's steps of one pass over the window table, 8 x 64 records per step with every load of
   // a step in flight together (one 16-byte load per record): for each entry of positive view length,
   // add it to gCorr[group] (kCmdGroups); or (kCmdSlots) for each such entry of group cmd.g, add it
   // to sLen[slot of its block] — those entries are first listed in this wave's part of the LDS list,
   // then their blocks' slots are loaded for the whole list at once.
-  static constexpr int kPassU = 16;
+  static constexpr int kPassU = 8;
   static constexpr int kGlPerWave = kGlCap / kWaves;
   FMT_DEV void windowShare(const PassCmd& cmd, int wave) {
     const int r = cmd.r, c = cmd.c;
@@ -1434,68 +1434,25 @@ class HugeDocT {
     const int xs = uni(x.maxSeq);
     waveSync();
     heapN--;
-    const int n = heapN;
-    // heap.ts's sift-down, five levels per LDS round trip: the 62 entries of the five levels below
-    // the hole are loaded one per lane (level d at lanes 2^d - 2 ..), the hole's path (the smaller
-    // child, the left one on ties, while it is smaller than x) is walked in registers, and the
-    // entries on it move up one level in one write
     int k = 1;
-    bool done = false;
-    while (!done && (k << 1) <= n) {
-      Lane<int32_t> sq;
-      Lane<uint32_t> lid;
-      FOR_LANES(l) {
-        const int d = 31 - __builtin_clz(static_cast<unsigned>(l + 2));  // level of lane l below k
-        const long node = (static_cast<long>(k) << d) + (l + 2 - (1 << d));
-        const bool have = l < 62 && node <= n;
-        LANE(sq) = have ? L->heap[node].maxSeq : 0;
-        LANE(lid) = have ? L->heap[node].leafId : 0u;
+    while ((k << 1) <= heapN) {
+      int j = k << 1;
+      int js = heapSeq(j);
+      if (j < heapN) {
+        const int j2 = heapSeq(j + 1);
+        if (js - j2 > 0) {
+          j++;
+          js = j2;
+        }
       }
-      int cur = k, np = 0;
-      int from[5], to[5];
-      for (int d = 1; d <= 5; d++) {
-        const int j0 = cur << 1;
-        if (j0 > n) {
-          done = true;
-          break;
-        }
-        const int lane0 = (1 << d) - 2 + (j0 - (k << d));
-        int j = j0, lj = lane0;
-        int js = readlane(sq, lane0);
-        if (j0 < n) {
-          const int j2 = readlane(sq, lane0 + 1);
-          if (js - j2 > 0) {
-            j = j0 + 1;
-            lj = lane0 + 1;
-            js = j2;
-          }
-        }
-        if (xs - js <= 0) {
-          done = true;
-          break;
-        }
-        from[np] = lj;
-        to[np] = cur;
-        np++;
-        cur = j;
-      }
+      if (xs - js <= 0) break;
+      const HeapEnt c = L->heap[j];
       waveSync();
-      for (int t = 0; t < np; t++) {
-        HeapEnt e;
-        e.maxSeq = readlane(sq, from[t]);
-        e.leafId = readlane(lid, from[t]);
-        FOR_LANES(l) {
-          if (l == 0) L->heap[to[t]] = e;
-        }
-      }
-      k = cur;
+      L->heap[k] = c;
+      k = j;
     }
     waveSync();
-    if (heapN >= 1) {
-      FOR_LANES(l) {
-        if (l == 0) L->heap[k] = x;
-      }
-    }
+    if (heapN >= 1) L->heap[k] = x;
     waveSync();
     return top;
   }
