@@ -202,9 +202,11 @@ SHIFT4 = [("mt_engine.h", """    const int count = nChars - from;
     }""")]
 
 VARIANTS = {
-    "shift4": SHIFT4,
+    "chars4": SHIFT4,
     "pass8": [("huge_engine.h", "  static constexpr int kPassU = 16;", "  static constexpr int kPassU = 8;")],
     "pass4": [("huge_engine.h", "  static constexpr int kPassU = 8;", "  static constexpr int kPassU = 4;")],
+    "pass2": [("huge_engine.h", "  static constexpr int kPassU = 4;", "  static constexpr int kPassU = 2;")],
+    "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
     "cold": COLD,
