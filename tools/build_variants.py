@@ -209,6 +209,7 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    "cur2": [],
     "cold": COLD,
     "fetch_uni": FETCH_UNI,
     "ob_s1": [OB_S1],
