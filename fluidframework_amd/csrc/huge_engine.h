@@ -188,6 +188,10 @@ struct HugeLds {
   int32_t gStable[kGroupCap];    // by group id: Σ stable lengths of its slots
   uint16_t gCount[kGroupCap];    // by group id: slots (<= kSlotCap)
   int32_t gCorr[kGroupCap];      // by group id: window correction of the current perspective
+  // chunks of 32 group positions (document order): the group scan's first level
+  uint16_t gPos[kGroupCap];      // by group id: its position in gOrder
+  int32_t cStable[kGroupCap / 32];  // by chunk: Σ gStable of its groups
+  int32_t cCorr[kGroupCap / 32];    // by chunk: Σ gCorr of its groups (the current perspective)
   int32_t sLen[kSlotCap];        // the group being searched: view length per slot
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
@@ -529,6 +533,28 @@ class HugeDocT {
   }
 
   // ------------------------------------------------------------------ stable sums
+  // gStable[g] += delta, and its chunk's sum (wave-uniform: every lane stores the same value)
+  FMT_DEV void stableAdd(uint32_t g, int delta) {
+    L->gStable[g] += delta;
+    L->cStable[L->gPos[g] >> 5] += delta;
+  }
+  // Group positions and chunk sums from gOrder / gStable (at load, and after a group split moved
+  // the positions of the groups after it).
+  FMT_DEV void chunksRebuild() {
+    FOR_LANES(l) {
+      for (int k = l; k < nGroups; k += 64) L->gPos[L->gOrder[k]] = static_cast<uint16_t>(k);
+    }
+    waveSync();
+    FOR_LANES(l) {
+      if (l < kGroupCap / 32) {
+        int32_t sum = 0;
+        for (int k = l * 32; k < l * 32 + 32 && k < nGroups; k++) sum += L->gStable[L->gOrder[k]];
+        L->cStable[l] = sum;
+      }
+    }
+    waveSync();
+  }
+
   // Stable length of a leaf: its length for every perspective at/above minSeq (non-window leaves).
   FMT_DEV void addStable(uint32_t blk, int delta) {
     invalidate();
@@ -537,7 +563,7 @@ class HugeDocT {
     int32_t* p = S.gSlotStable + static_cast<size_t>(g) * kSlotCap + s;
     const int32_t v = ldi(p);
     st1(p, v + delta);
-    L->gStable[g] += delta;  // (uniform LDS store)
+    stableAdd(g, delta);  // (uniform LDS stores)
     waveSync();
   }
 
@@ -546,7 +572,7 @@ class HugeDocT {
     int32_t* p = S.gSlotStable + static_cast<size_t>(g) * kSlotCap + s;
     const int32_t v = ldi(p);
     st1(p, v + delta);
-    L->gStable[g] += delta;
+    stableAdd(g, delta);
     waveSync();
   }
 
@@ -622,7 +648,7 @@ class HugeDocT {
       }
     }
     L->gCount[g] = static_cast<uint16_t>(cnt + 1);
-    L->gStable[g] += st;
+    stableAdd(g, st);
     waveSync();
     return true;
   }
@@ -668,7 +694,7 @@ class HugeDocT {
       waveSync();
     }
     L->gCount[g] = static_cast<uint16_t>(cnt - n);
-    L->gStable[g] -= removed;
+    stableAdd(g, -removed);
     waveSync();
   }
 
@@ -716,6 +742,7 @@ class HugeDocT {
     L->gCorr[g2] = 0;
     waveSync();
     nGroups++;
+    chunksRebuild();
     // window entries follow their blocks
     for (uint32_t base = 0; base < nWin; base += 64) {
       FOR_LANES(l) {
@@ -924,7 +951,10 @@ class HugeDocT {
               v = c < 64 ? static_cast<uint32_t>(winVis(static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, mk[0], mk[1], r, c))
                          : static_cast<uint32_t>(visAny(x[2], static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), 0u, 0u,
                                                         mClient(x[3]), r, c, rd(S.wLeaf + w)));
-              if (v && !bySlot) atomicAddLds(&L->gCorr[grp], static_cast<int>(v));
+              if (v && !bySlot) {
+                atomicAddLds(&L->gCorr[grp], static_cast<int>(v));
+                atomicAddLds(&L->cCorr[L->gPos[grp] >> 5], static_cast<int>(v));
+              }
             }
           }
           LANE(vis[u]) = v;
@@ -997,6 +1027,7 @@ class HugeDocT {
     ProfScope ps_(prof[1]);
     FOR_LANES(l) {
       for (int g = l; g < nGroups; g += 64) L->gCorr[g] = 0;
+      if (l < kGroupCap / 32) L->cCorr[l] = 0;
     }
     waveSync();
     prof[16]++;
@@ -1055,40 +1086,27 @@ class HugeDocT {
     // stopping at the chunk that holds it)
     int k = -1, base = 0;
     {
-      // two levels: lane l sums the groups at positions [l*C, l*C + C) (C = ceil(nGroups / 64)), one
-      // wave scan finds the first run whose end reaches p, a second scans that run's groups
+      // two levels: lane l takes chunk l (group positions [32 l, 32 l + 32): its stable sum and its
+      // window correction, kept as the groups' change), one wave scan finds the first chunk whose end
+      // reaches p, a second scans that chunk's groups
       ProfScope psScan_(prof[21]);
-      const int C = (nGroups + 63) / 64;
+      const int nc = (nGroups + 31) / 32;
       Lane<uint32_t> run;
-      FOR_LANES(l) {
-        uint32_t x = 0;
-        for (int j0 = 0; j0 < C; j0 += 8) {  // 8 group ids, then their 16 sums, in flight together
-          uint32_t g[8];
-#pragma unroll
-          for (int j = 0; j < 8; j++) {
-            const int kk = l * C + j0 + j;
-            g[j] = j0 + j < C && kk < nGroups ? static_cast<uint32_t>(L->gOrder[kk]) : kNone;
-          }
-#pragma unroll
-          for (int j = 0; j < 8; j++)
-            if (g[j] != kNone) x += static_cast<uint32_t>(L->gStable[g[j]] + L->gCorr[g[j]]);
-        }
-        LANE(run) = x;
-      }
+      FOR_LANES(l) { LANE(run) = l < nc ? static_cast<uint32_t>(L->cStable[l] + L->cCorr[l]) : 0u; }
       uint32_t tot;
       const Lane<uint32_t> ex = waveExclusiveSum(run, &tot);
       Lane<bool> q;
-      FOR_LANES(l) { LANE(q) = l * C < nGroups && static_cast<int>(LANE(ex) + LANE(run)) >= p; }
+      FOR_LANES(l) { LANE(q) = l < nc && static_cast<int>(LANE(ex) + LANE(run)) >= p; }
       const uint64_t m = ballot(q);
       if (m) {
         const int lr = ctz64(m);
         base = static_cast<int>(readlane(ex, lr));
-        const int k0 = lr * C;
+        const int k0 = lr * 32;
         Lane<uint32_t> len;
         FOR_LANES(l) {
           const int kk = k0 + l;
           uint32_t x = 0;
-          if (l < C && kk < nGroups) {
+          if (l < 32 && kk < nGroups) {
             const uint32_t g = L->gOrder[kk];
             x = static_cast<uint32_t>(L->gStable[g] + L->gCorr[g]);
           }
@@ -1097,9 +1115,9 @@ class HugeDocT {
         uint32_t t2;
         const Lane<uint32_t> ex2 = waveExclusiveSum(len, &t2);
         Lane<bool> q2;
-        FOR_LANES(l) { LANE(q2) = l < C && k0 + l < nGroups && base + static_cast<int>(LANE(ex2) + LANE(len)) >= p; }
+        FOR_LANES(l) { LANE(q2) = l < 32 && k0 + l < nGroups && base + static_cast<int>(LANE(ex2) + LANE(len)) >= p; }
         const uint64_t m2 = ballot(q2);
-        if (m2) {  // (always: the run's end reaches p)
+        if (m2) {  // (always: the chunk's end reaches p)
           k = k0 + ctz64(m2);
           base += static_cast<int>(readlane(ex2, ctz64(m2)));
         }
@@ -1327,7 +1345,7 @@ class HugeDocT {
     int32_t* sp = slotStPtr(R.g) + R.s;
     const int32_t oldSt = ldi(sp);
     st1(sp, stB);
-    L->gStable[R.g] += stB - oldSt;
+    stableAdd(R.g, stB - oldSt);
     waveSync();
     invalidate();
     if (!slotInsert(R.g, static_cast<int>(R.s) + 1, nb, stN)) return kNone;
@@ -3391,6 +3409,7 @@ class HugeDocT {
         const int32_t old = rd(sp);
         *sp = stB;
         atomicAddLds(&L->gStable[g], stB - old);
+        atomicAddLds(&L->cStable[L->gPos[g] >> 5], stB - old);
       }
     }
     waveSync();
@@ -3594,6 +3613,7 @@ class HugeDocT {
       lastBlk = kNone;
       minSeq = in.snapMinSeq;
       curSeq = in.snapSeq;
+      chunksRebuild();
       return;
     }
     const uint32_t nLv = shapeLevels();
@@ -3743,6 +3763,7 @@ class HugeDocT {
     root = static_cast<int>(lo);
     nextBlock = next;
     lastBlk = nLeafBlk - 1;
+    chunksRebuild();
     minSeq = in.snapMinSeq;
     curSeq = in.snapSeq;
     if (anyWin) loadWindow(nLeafBlk);
@@ -3900,6 +3921,7 @@ class HugeDocT {
       L->gCorr[g] = 0;
       waveSync();
     }
+    chunksRebuild();
     root = static_cast<int>(ldu(ck + K::kRoot));
     nextBlock = K::kBlocks;
     nFree = static_cast<uint32_t>(ldu(ck + K::kNFree));
@@ -4256,6 +4278,14 @@ class HugeDocT {
       if (sum != L->gStable[g]) return bad("group stable", sum, L->gStable[g]);
     }
     if (nw != static_cast<long>(nWin)) bad("window count", nw, nWin);
+    for (int c = 0; c * 32 < nGroups; c++) {  // the group scan's chunk sums and positions
+      long sum = 0;
+      for (int k = c * 32; k < c * 32 + 32 && k < nGroups; k++) {
+        if (L->gPos[L->gOrder[k]] != k) return bad("group position", L->gOrder[k], k);
+        sum += L->gStable[L->gOrder[k]];
+      }
+      if (sum != L->cStable[c]) return bad("chunk stable", sum, L->cStable[c]);
+    }
   }
 #endif
 
