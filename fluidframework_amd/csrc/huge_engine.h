@@ -111,6 +111,17 @@ FMT_DEV u32x4 ld4(const uint32_t* p) {  // one 16-byte vector load (p 16-byte al
 #endif
 }
 
+// HugeState's / HugeInputs' buffers are global memory: typed so in the kernel (hugedoc.hip), every
+// access to them is a global load/store (SGPR base + lane offset) instead of a flat one, which would
+// also count against the LDS counter and make each LDS wait wait for the outstanding HBM loads (T3
+// slice 9.84 -> 9.72 s, profiles/r5/ab/ab_t3_chunks_global.json). Host code that fills the structs
+// sees plain pointers (same layout).
+#if FMT_GPU && defined(FMT_HUGE_KERNEL)
+#define FMT_HBM __attribute__((address_space(1)))
+#else
+#define FMT_HBM
+#endif
+
 struct HeapEnt {
   int32_t maxSeq;
   uint32_t leafId;
@@ -119,66 +130,66 @@ struct HeapEnt {
 // Device buffers of one huge document (all sized by the runtime from host-side bounds).
 struct HugeState {
   // leaf fields, [blockCap * 8]: slot k of leaf block b at b * 8 + k
-  uint32_t* lLen;
-  int32_t* lIns;
-  int32_t* lRm;
-  uint32_t* lMlo;
-  uint32_t* lMhi;
-  uint32_t* lId;
-  uint32_t* lText;
-  uint32_t* lMeta;
+  FMT_HBM uint32_t* lLen;
+  FMT_HBM int32_t* lIns;
+  FMT_HBM int32_t* lRm;
+  FMT_HBM uint32_t* lMlo;
+  FMT_HBM uint32_t* lMhi;
+  FMT_HBM uint32_t* lId;
+  FMT_HBM uint32_t* lText;
+  FMT_HBM uint32_t* lMeta;
   // blocks [blockCap]
-  uint32_t* bCount;
-  uint32_t* bParent;
-  uint32_t* bLeaf;
-  int32_t* bScour;
-  uint32_t* bChild;   // [blockCap * 8] (interior blocks)
-  uint32_t* bGroup;   // leaf blocks: group id
-  uint32_t* bSlot;    // leaf blocks: slot in the group
-  uint32_t* freeBlk;  // [blockCap] stack of freed block ids
+  FMT_HBM uint32_t* bCount;
+  FMT_HBM uint32_t* bParent;
+  FMT_HBM uint32_t* bLeaf;
+  FMT_HBM int32_t* bScour;
+  FMT_HBM uint32_t* bChild;   // [blockCap * 8] (interior blocks)
+  FMT_HBM uint32_t* bGroup;   // leaf blocks: group id
+  FMT_HBM uint32_t* bSlot;    // leaf blocks: slot in the group
+  FMT_HBM uint32_t* freeBlk;  // [blockCap] stack of freed block ids
   uint32_t blockCap;
   // groups [kGroupCap * kSlotCap]
-  uint32_t* gSlotBlk;
-  int32_t* gSlotStable;
+  FMT_HBM uint32_t* gSlotBlk;
+  FMT_HBM int32_t* gSlotStable;
   // leaf id → leaf block / window entry, [idCap]
-  uint32_t* leafBlk;
-  uint32_t* winIdx;
+  FMT_HBM uint32_t* leafBlk;
+  FMT_HBM uint32_t* winIdx;
   uint32_t idCap;
   // window table [winCap]: one 16-byte record per entry {ins, rm, len, meta | group << 17} (one
   // vector load per entry in the window passes), plus the entry's leaf block and leaf id
-  uint32_t* wRec;
-  uint32_t* wMask;  // [winCap * 2]: the leaf's remove-client set (lo, hi), loaded with the record
-  uint32_t* wBlk;
-  uint32_t* wLeaf;
+  FMT_HBM uint32_t* wRec;
+  FMT_HBM uint32_t* wMask;  // [winCap * 2]: the leaf's remove-client set (lo, hi), loaded with the record
+  FMT_HBM uint32_t* wBlk;
+  FMT_HBM uint32_t* wLeaf;
   uint32_t winCap;
   // text arena, one offset space: [0, textLen) is the batch's shared text (read in place through
   // base, never copied per document); [textLen, textCap) is this document's merge area, addressed
   // through text (its allocation minus textLen units, so text + off is valid for off >= textLen)
-  const uint16_t* base;
-  uint16_t* text;
+  const FMT_HBM uint16_t* base;
+  FMT_HBM uint16_t* text;
   uint64_t textLen;   // batch text (read-only part)
   uint64_t textCap;   // end of the merge area: two halves of (textCap - textLen) / 2 units, one in use
-  uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
-  uint32_t* pClass;   // [kPropCap]: prop set id -> its match class (the first set with the same content)
-  uint32_t* pHead;    // [2 * kPropHash]: bucket heads (set id + 1, 0 = empty), exact content then class
-  uint32_t* pNext;    // [2 * kPropCap]: per set, the next set of its exact-content / class bucket
-  uint32_t* cuIds;    // [idCap]: the current catch-up op's delta leaves in document order (or nullptr)
-  uint32_t* rmIds;    // [idCap]: the current remove-order op's already-removed hits; at output, leaf id ->
+  FMT_HBM uint32_t* props;    // [kPropCap * kPropWords]: n, kv[FMT_MT_PROPS_MAX]
+  FMT_HBM uint32_t* pClass;   // [kPropCap]: prop set id -> its match class (the first set with the same content)
+  FMT_HBM uint32_t* pHead;    // [2 * kPropHash]: bucket heads (set id + 1, 0 = empty), exact content then class
+  FMT_HBM uint32_t* pNext;    // [2 * kPropCap]: per set, the next set of its exact-content / class bucket
+  FMT_HBM uint32_t* cuIds;    // [idCap]: the current catch-up op's delta leaves in document order (or nullptr)
+  FMT_HBM uint32_t* rmIds;    // [idCap]: the current remove-order op's already-removed hits; at output, leaf id ->
                       // output index (or nullptr: no remove-order recording)
-  uint32_t* mkIds;    // [mkCap]: every marker leaf ever in the document, in insertion order (relative
+  FMT_HBM uint32_t* mkIds;    // [mkCap]: every marker leaf ever in the document, in insertion order (relative
   uint32_t mkCap;     //   positions; nullptr: the batch has none)
-  uint32_t* outIdx;   // [idCap]: at output, leaf id -> output index (annotate-adjust batches; else nullptr)
+  FMT_HBM uint32_t* outIdx;   // [idCap]: at output, leaf id -> output index (annotate-adjust batches; else nullptr)
   // [idCap * 2]: per leaf id, the remove clients with short ids 64..127 (bit c - 64), beyond the two
   // mask words every leaf and window entry carry (nullptr: the batch has no such client; zeroed)
-  uint32_t* hiMask;
+  FMT_HBM uint32_t* hiMask;
   // live obliterates (Obliterates, mergeTree.ts:515-635), [obCap] each: per slot its record
   // {startId, startOff, endId, endOff, seq, client} (obRec, 6 words) and whether it is in use, and the
   // two ordered slot lists seqOrdered / startOrdered (nullptr / 0: the document has no obliterate;
   // obCap = its obliterate ops, the most that can be live at once)
-  uint32_t* obRec;
-  uint32_t* obUsed;
-  uint32_t* obSeq;
-  uint32_t* obStart;
+  FMT_HBM uint32_t* obRec;
+  FMT_HBM uint32_t* obUsed;
+  FMT_HBM uint32_t* obSeq;
+  FMT_HBM uint32_t* obStart;
   uint32_t obCap;
 };
 
@@ -210,18 +221,18 @@ struct HugeLds {
 };
 
 struct HugeInputs {
-  const fmt_mt_op* ops;
+  const FMT_HBM fmt_mt_op* ops;
   uint64_t begin, end;
-  const uint32_t* propsOff;
-  const uint32_t* propsKv;
+  const FMT_HBM uint32_t* propsOff;
+  const FMT_HBM uint32_t* propsKv;
   uint32_t nPropsOps;
-  const fmt_mt_snapshot_seg* segs;  // loaded segments: the header chunk, then the body chunk(s)
+  const FMT_HBM fmt_mt_snapshot_seg* segs;  // loaded segments: the header chunk, then the body chunk(s)
   uint32_t nSegs;
   // Tree shape of the loaded segments when a body follows the header (nullptr: the header alone,
   // reloaded 7 wide): [L, n_0 .. n_{L-1}, then per level its n_l nodes as (start, count)] —
   // level 0 the leaf blocks (start: first segment), level l > 0 interior blocks (start: first
   // child on level l - 1), level L - 1 the root. Built on the host by loadShape below.
-  const uint32_t* shape;
+  const FMT_HBM uint32_t* shape;
   int32_t snapMinSeq, snapSeq;
   // client of the loaded segments' insert stamp: FMT_NON_COLLAB_CLIENT for a summary's segments
   // (specToSegment, snapshotLoader.ts:180-186), FMT_LOCAL_CLIENT for a document's initial text (the
@@ -230,32 +241,32 @@ struct HugeInputs {
   uint32_t segProps;  // some loaded segment has properties
   // SnapshotV1 merge info of the loaded segments (aligned with segs; nullptr: none) and the batch's
   // remove stamps its rows index (specToSegment, snapshotLoader.ts:105-175)
-  const fmt_mt_snapshot_info* info;
-  const fmt_mt_stamp* stamps;
+  const FMT_HBM fmt_mt_snapshot_info* info;
+  const FMT_HBM fmt_mt_stamp* stamps;
   // the batch's whole merge-info table: V1 body-chunk segments with merge info arrive as
   // FMT_MT_F_LOADSEG insert ops naming a row of it (nullptr: none in the batch)
-  const fmt_mt_snapshot_info* infoAll;
+  const FMT_HBM fmt_mt_snapshot_info* infoAll;
   uint64_t nInfoAll;
   // catch-up ranges of FMT_MT_F_CATCHUP ops (the document's slab; nullptr: the batch records none)
-  fmt_mt_catchup_range* catchup;
+  FMT_HBM fmt_mt_catchup_range* catchup;
   uint32_t catchupCap;
   // remove-order entries of FMT_MT_F_RMORDER ops (the document's slab; nullptr: none recorded)
-  fmt_mt_remove_order* rmOrder;
+  FMT_HBM fmt_mt_remove_order* rmOrder;
   uint32_t rmOrderCap;
   // legacy relative positions (FMT_MT_F_REL1/REL2 ops index the table; nullptr: none in the batch)
-  const fmt_mt_relpos* relpos;
+  const FMT_HBM fmt_mt_relpos* relpos;
   uint32_t nRelpos;
   uint32_t markerKey;  // key id of "markerId"
   // annotate-adjust (nullptr: none in the batch): the batch's tables (adjust.h), this document's
   // index into their per-document slabs (computed numbers, PropertiesManager records)
-  const fmt_mt::AdjustTables* adj;
+  const FMT_HBM fmt_mt::AdjustTables* adj;
   uint32_t doc;
   // large → huge checkpoint (huge_ckpt.h; nullptr: load from the segments above): the large tier's
   // record and its result slabs for this document at the op it stopped before
-  const uint32_t* ck = nullptr;
-  const fmt_mt_leaf* ckLeaves = nullptr;
-  const uint16_t* ckChars = nullptr;
-  const fmt_mt_propset* ckProps = nullptr;
+  const FMT_HBM uint32_t* ck = nullptr;
+  const FMT_HBM fmt_mt_leaf* ckLeaves = nullptr;
+  const FMT_HBM uint16_t* ckChars = nullptr;
+  const FMT_HBM fmt_mt_propset* ckProps = nullptr;
 };
 
 // The tree a legacy summary loads into (huge_engine.h HugeInputs::shape): reloadFromSegments of the
@@ -399,11 +410,11 @@ class HugeDocT {
   FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadWg(p)); }
   // one text unit at arena offset off (batch text below textLen, the merge area above)
   FMT_DEV uint32_t textAt(uint64_t off) const {
-    return loadWg((off < S.textLen ? S.base : static_cast<const uint16_t*>(S.text)) + off);
+    return loadWg((off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text)) + off);
   }
   // one lane stores a wave-uniform value
-  template <class T>
-  FMT_DEV static void st1(T* p, T v) {
+  template <class P, class T>
+  FMT_DEV static void st1(P* p, T v) {
     FOR_LANES(l) {
       if (l == 0) *p = v;
     }

@@ -7,6 +7,7 @@
 // block, the block/heap updates), not bandwidth.
 #include <hip/hip_runtime.h>
 
+#define FMT_HUGE_KERNEL 1  // (huge_engine.h: global-typed state pointers)
 #include "huge_engine.h"
 #include "kernels.h"
 

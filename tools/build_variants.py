@@ -212,6 +212,11 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    # obliterate cascade: the small tier at 1 wave/SIMD (512 registers a wave: the overflow in AGPRs)
+    "ob_o1": [("mergetree.hip", "  if (obliterate)\n    return launchTier<true, S, false, kMtWaves, 2>(batch, out, esc2 + 1,",
+               "  if (obliterate)\n    return launchTier<true, S, false, kMtWaves, 1>(batch, out, esc2 + 1,")],
+    "ob_base": [],
+    "gq": [],  # (working tree: HugeState / HugeInputs buffers typed as global memory)
     "cur2": [],
     "cold": COLD,
     "fetch_uni": FETCH_UNI,

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r5_ab4
 mkdir -p $OUT
-timeout -k 10 600 python3 tools/bench_variants.py --docs 20000 --unique 20000 --rounds 4 prev cur > $OUT/ab_t1.json 2> $OUT/ab_t1.err
+timeout -k 10 600 python3 tools/bench_variants.py --docs 20000 --unique 20000 --rounds 4 cur visbf > $OUT/ab_t1.json 2> $OUT/ab_t1.err
 rc=$?
 cat $OUT/ab_t1.json
 exit $rc
