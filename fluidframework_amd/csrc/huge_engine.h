@@ -1466,16 +1466,14 @@ class HugeDocT {
     int k = 1;
     while ((k << 1) <= heapN) {
       int j = k << 1;
-      int js = heapSeq(j);
-      if (j < heapN) {
-        const int j2 = heapSeq(j + 1);
-        if (js - j2 > 0) {
-          j++;
-          js = j2;
-        }
+      // both children in one LDS round trip (entry heapN + 1 is inside the array and never chosen)
+      const HeapEnt a = L->heap[j], b = L->heap[j + 1];
+      HeapEnt c = a;
+      if (j < heapN && uni(a.maxSeq) - uni(b.maxSeq) > 0) {
+        j++;
+        c = b;
       }
-      if (xs - js <= 0) break;
-      const HeapEnt c = L->heap[j];
+      if (xs - uni(c.maxSeq) <= 0) break;
       waveSync();
       L->heap[k] = c;
       k = j;

@@ -1077,47 +1077,56 @@ class Doc {
   }
 
   // ------------------------------------------------------------------ LRU heap (heap.ts)
-  FMT_DEV void heapSwap(int a, int b) {
-    const HeapEnt x = s->heap[a], y = s->heap[b];
-    waveSync();
-    s->heap[a] = y;
-    s->heap[b] = x;
-    waveSync();
-  }
-
   FMT_DEV int heapSeq(int k) const { return uni(s->heap[k].maxSeq); }
 
+  // heap.ts sift order (add: fixUp; get: swap root and last, fixDown), moving a hole instead of
+  // swapping entries: the same arrangement, with one LDS round trip per level (going down, both
+  // children are read together; entry heapN + 1 is inside the array and never chosen)
   FMT_DEV void heapAdd(int maxSeq, uint32_t leafId) {
     if (heapN >= kHeapCap) {
       fail(FMT_E_CAPACITY);
       return;
     }
-    heapN++;
-    s->heap[heapN].maxSeq = maxSeq;
-    s->heap[heapN].leafId = leafId;
-    waveSync();
-    int k = heapN;
-    while (k > 1 && heapSeq(k >> 1) - heapSeq(k) > 0) {
-      heapSwap(k, k >> 1);
+    int k = ++heapN;
+    while (k > 1) {
+      const HeapEnt up = s->heap[k >> 1];
+      if (!(uni(up.maxSeq) - maxSeq > 0)) break;
+      waveSync();
+      s->heap[k] = up;
       k >>= 1;
     }
+    waveSync();
+    s->heap[k].maxSeq = maxSeq;
+    s->heap[k].leafId = leafId;
+    waveSync();
   }
 
   FMT_DEV HeapEnt heapGet() {
-    heapSwap(1, heapN);
-    HeapEnt x;
-    x.maxSeq = uni(s->heap[heapN].maxSeq);
-    x.leafId = uni(s->heap[heapN].leafId);
+    HeapEnt top;
+    top.maxSeq = uni(s->heap[1].maxSeq);
+    top.leafId = uni(s->heap[1].leafId);
+    const HeapEnt y = s->heap[heapN];  // the last entry sifts down from the root
+    const int ys = uni(y.maxSeq);
+    waveSync();
     heapN--;
     int k = 1;
     while ((k << 1) <= heapN) {
       int j = k << 1;
-      if (j < heapN && heapSeq(j) - heapSeq(j + 1) > 0) j++;
-      if (heapSeq(k) - heapSeq(j) <= 0) break;
-      heapSwap(k, j);
+      const HeapEnt a = s->heap[j], b = s->heap[j + 1];
+      HeapEnt c = a;
+      if (j < heapN && uni(a.maxSeq) - uni(b.maxSeq) > 0) {
+        j++;
+        c = b;
+      }
+      if (ys - uni(c.maxSeq) <= 0) break;
+      waveSync();
+      s->heap[k] = c;
       k = j;
     }
-    return x;
+    waveSync();
+    if (heapN >= 1) s->heap[k] = y;
+    waveSync();
+    return top;
   }
 
   // ------------------------------------------------------------------ prop sets

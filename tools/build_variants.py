@@ -212,6 +212,7 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    "heap2": [],  # (working tree: hole-moving heap sifts, both children read together)
     # obliterate cascade: the small tier at 1 wave/SIMD (512 registers a wave: the overflow in AGPRs)
     "ob_o1": [("mergetree.hip", "  if (obliterate)\n    return launchTier<true, S, false, kMtWaves, 2>(batch, out, esc2 + 1,",
                "  if (obliterate)\n    return launchTier<true, S, false, kMtWaves, 1>(batch, out, esc2 + 1,")],
@@ -259,7 +260,7 @@ FLAGS = {
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
     "lines": ["-gline-tables-only"],  # (line tables only: the same code, for PC-sample attribution)
 }
-REVS = {"r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
+REVS = {"r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
         "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
 
 
