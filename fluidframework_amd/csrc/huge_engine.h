@@ -401,13 +401,17 @@ class HugeDocT {
   }
 
   // ------------------------------------------------------------------ small helpers
-  // Every read of HBM state goes through a workgroup-scope load: a vector load served by this CU's
-  // L1 (which the wave's own stores keep current; no other CU writes this document's state), never
-  // a scalar-cache load. rd() inside FOR_LANES bodies, ldu()/ldi() for wave-uniform values.
-  FMT_DEV static uint32_t rd(const uint32_t* p) { return loadWg(p); }
-  FMT_DEV static int32_t rd(const int32_t* p) { return loadWg(p); }
-  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(loadWg(p)); }
-  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadWg(p)); }
+  // Reads of HBM state: plain vector loads served by this CU's L1 (which the wave's own stores keep
+  // current; no other CU writes this document's state; the helper waves read after a workgroup
+  // barrier). They were workgroup-scope atomic loads until round 5: an atomic load is an ordered
+  // memory reference to the scheduler, so independent loads issued one round trip at a time (T3
+  // slice 9.69 -> 9.16 s as plain loads, profiles/r5/ab/ab_t3_plainrd.json; the kernel's scalar
+  // loads stay the 142 of its arguments: the compiler picks a scalar load only where no store of
+  // this kernel can reach it). rd() inside FOR_LANES bodies, ldu()/ldi() for wave-uniform values.
+  FMT_DEV static uint32_t rd(const uint32_t* p) { return *p; }
+  FMT_DEV static int32_t rd(const int32_t* p) { return *p; }
+  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(*p); }
+  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(*p); }
   // one text unit at arena offset off (batch text below textLen, the merge area above)
   FMT_DEV uint32_t textAt(uint64_t off) const {
     return loadWg((off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text)) + off);
