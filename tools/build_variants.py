@@ -212,6 +212,10 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    "ptext": [("huge_engine.h", "    return loadWg((off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text)) + off);",
+               "    return (off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text))[off];")],
+    "shift4b": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
+    "pass2b": [("huge_engine.h", "  static constexpr int kPassU = 4;", "  static constexpr int kPassU = 2;")],
     # huge tier: HBM state read with plain (unordered) loads instead of workgroup-scope atomic ones
     "plainrd": [("huge_engine.h", "  FMT_DEV static uint32_t rd(const uint32_t* p) { return loadWg(p); }\n  FMT_DEV static int32_t rd(const int32_t* p) { return loadWg(p); }\n  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(loadWg(p)); }\n  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(loadWg(p)); }",
                  "  FMT_DEV static uint32_t rd(const uint32_t* p) { return *p; }\n  FMT_DEV static int32_t rd(const int32_t* p) { return *p; }\n  FMT_DEV static uint32_t ldu(const uint32_t* p) { return uni(*p); }\n  FMT_DEV static int32_t ldi(const int32_t* p) { return uni(*p); }")],
@@ -263,7 +267,7 @@ FLAGS = {
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
     "lines": ["-gline-tables-only"],  # (line tables only: the same code, for PC-sample attribution)
 }
-REVS = {"r5heap": "2d9f706", "r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
+REVS = {"r5plain": "140dfb5", "r5heap": "2d9f706", "r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
         "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
 
 
