@@ -605,7 +605,7 @@ class HugeDocT {
     return -1;
   }
 
-  static constexpr int kShiftU = 8;  // slot-list passes: 8 x 64 slots per step
+  static constexpr int kShiftU = 4;  // slot-list passes: 4 x 64 slots per step
 
   // Insert leaf block nb into group g at slot `at` with stable length st (slots at/after shift up).
   // Splits the group first when it is full; returns false on failure.
@@ -884,12 +884,12 @@ class HugeDocT {
     waveSync();
   }
 
-  // This wave's steps of one pass over the window table, 4 x 64 records per step with every load of
+  // This wave's steps of one pass over the window table, 2 x 64 records per step with every load of
   // a step in flight together (one 16-byte load per record): for each entry of positive view length,
   // add it to gCorr[group] (kCmdGroups); or (kCmdSlots) for each such entry of group cmd.g, add it
   // to sLen[slot of its block] — those entries are first listed in this wave's part of the LDS list,
   // then their blocks' slots are loaded for the whole list at once.
-  static constexpr int kPassU = 4;
+  static constexpr int kPassU = 2;
   static constexpr int kGlPerWave = kGlCap / kWaves;
   FMT_DEV void windowShare(const PassCmd& cmd, int wave) {
     const int r = cmd.r, c = cmd.c;

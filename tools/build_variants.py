@@ -212,6 +212,7 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    "w2s4": [],  # (working tree: window pass 2 x 64, slot pass 4 x 64 records per wave step)
     "ptext": [("huge_engine.h", "    return loadWg((off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text)) + off);",
                "    return (off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text))[off];")],
     "shift4b": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
