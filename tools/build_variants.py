@@ -212,6 +212,9 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    # huge tier: 8 waves per workgroup (2 per SIMD) share the window / slot passes
+    "w8": [("huge_engine.h", "  int32_t glN[4];", "  int32_t glN[8];"),
+           ("huge_engine.h", "  static constexpr int kWaves = 4;", "  static constexpr int kWaves = 8;")],
     "w2s4": [],  # (working tree: window pass 2 x 64, slot pass 4 x 64 records per wave step)
     "ptext": [("huge_engine.h", "    return loadWg((off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text)) + off);",
                "    return (off < S.textLen ? S.base : static_cast<const FMT_HBM uint16_t*>(S.text))[off];")],
@@ -268,7 +271,7 @@ FLAGS = {
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
     "lines": ["-gline-tables-only"],  # (line tables only: the same code, for PC-sample attribution)
 }
-REVS = {"r5plain": "140dfb5", "r5heap": "2d9f706", "r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
+REVS = {"r5w2s4": "9cd02c8", "r5plain": "140dfb5", "r5heap": "2d9f706", "r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
         "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
 
 
