@@ -212,6 +212,11 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    # obliterate small tier: its small -> large checkpoint saved by run() after the op loop (as plain
+    # batches do), not inside it
+    "obsb": [("mt_engine.h", "          if constexpr (Ob) {\n            if constexpr (kSavesCkpt) saveCkpt(i);\n            else saveBig(i);\n          } else {\n            ckptNext = i;\n          }",
+              "          if constexpr (Ob && kSavesCkpt) {\n            saveCkpt(i);\n          } else {\n            ckptNext = i;\n          }"),
+             ("mt_engine.h", "      else if constexpr (!Ob && kSavesBig) saveBig(ckptNext);", "      else if constexpr (kSavesBig) saveBig(ckptNext);")],
     # huge tier: 8 waves per workgroup (2 per SIMD) share the window / slot passes
     "w8": [("huge_engine.h", "  int32_t glN[4];", "  int32_t glN[8];"),
            ("huge_engine.h", "  static constexpr int kWaves = 4;", "  static constexpr int kWaves = 8;")],
