@@ -36,7 +36,10 @@ def addon():
 
 
 def _node(*args, timeout=120):
-    return subprocess.run([NODE, *args], capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    # (FMT_NAPI_BACKTRACE: a SIGSEGV in the child prints its native stack into r.stderr, which the
+    # assertions show — INTEGRATION.md §2, the open exit-path crash)
+    env = dict(os.environ, FMT_NAPI_BACKTRACE=os.environ.get("FMT_NAPI_BACKTRACE", "1"))
+    return subprocess.run([NODE, *args], capture_output=True, text=True, timeout=timeout, cwd=REPO, env=env)
 
 
 def test_addon_exports(addon):
