@@ -212,6 +212,8 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    "pass1": [("huge_engine.h", "  static constexpr int kPassU = 2;", "  static constexpr int kPassU = 1;")],
+    "shift2": [("huge_engine.h", "  static constexpr int kShiftU = 4;", "  static constexpr int kShiftU = 2;")],
     # obliterate small tier: its small -> large checkpoint saved by run() after the op loop (as plain
     # batches do), not inside it
     "obsb": [("mt_engine.h", "          if constexpr (Ob) {\n            if constexpr (kSavesCkpt) saveCkpt(i);\n            else saveBig(i);\n          } else {\n            ckptNext = i;\n          }",
@@ -276,7 +278,7 @@ FLAGS = {
     "relaxocc": ["-mllvm", "-amdgpu-schedule-relaxed-occupancy"],
     "lines": ["-gline-tables-only"],  # (line tables only: the same code, for PC-sample attribution)
 }
-REVS = {"r5w2s4": "9cd02c8", "r5plain": "140dfb5", "r5heap": "2d9f706", "r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
+REVS = {"r5nb": "41cb064", "r5w2s4": "9cd02c8", "r5plain": "140dfb5", "r5heap": "2d9f706", "r5gq": "79be899", "r5ck": "bb3640d", "r5wc": "75f92c9", "v1": "352970f", "head": "6b38e0f", "prev": "HEAD", "pre_ob": "4bc1b08", "r4start": "14023f9", "r4relpos": "b4d93d3",
         "r4pend": "4831c1d", "r4rm": "07be56c", "r4v1": "efa25af"}  # committed engines to A/B against
 
 
