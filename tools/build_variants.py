@@ -212,6 +212,7 @@ VARIANTS = {
     "shift4": [("huge_engine.h", "  static constexpr int kShiftU = 8;", "  static constexpr int kShiftU = 4;")],
     "shift8": [("huge_engine.h", "  static constexpr int kShiftU = 16;", "  static constexpr int kShiftU = 8;")],
     "hcur": [],
+    "grad": [],  # (working tree: graduation masks from one batched pass, removals from the top)
     "pass1": [("huge_engine.h", "  static constexpr int kPassU = 2;", "  static constexpr int kPassU = 1;")],
     "shift2": [("huge_engine.h", "  static constexpr int kShiftU = 4;", "  static constexpr int kShiftU = 2;")],
     # obliterate small tier: its small -> large checkpoint saved by run() after the op loop (as plain
