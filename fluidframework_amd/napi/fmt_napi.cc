@@ -72,14 +72,14 @@ struct Ctx {
   bool busy = false;  // one async replay at a time per ctx (the C ABI is one-thread-per-ctx)
 };
 
-// Context lifetime without N-API finalizers. A finalizer makes node create a weak v8impl::Reference
-// for the external; node v12 (this image's) frees every such Reference when the environment is torn
-// down even if GC already ran its first weak pass, and the queued second pass then calls through
-// the freed object: the SIGSEGV at exit of round 4 (libnode.so.72 +0x878a80, the second-pass
-// callback, loading the vtable of a freed Reference, reached from InvokeSecondPassPhantomCallbacks
-// during FreeEnvironment's CleanupHandles; the addon frame in that backtrace was the diagnostic
-// handler itself). So the externals carry no finalizer and no reference: each holds a handle
-// (slot + 1 | generation << 32) into this table. close() frees the slot and its device context at
+// Context lifetime without N-API weak references. node v12 (this image's) frees every weak
+// v8impl::Reference when the environment is torn down even if GC already ran its first weak pass,
+// and the queued second pass then calls through the freed object: the SIGSEGV at exit (libnode.so.72
+// +0x878a80, the second-pass callback loading the vtable of a freed Reference, reached from
+// InvokeSecondPassPhantomCallbacks during FreeEnvironment's CleanupHandles). node v12's
+// napi_create_external makes such a Reference for every External, finalizer or not (round 5's
+// Externals without finalizers still crashed the same way, profiles/r5/last/), so a context handle
+// is a plain JS number: slot + 1 + (generation mod 2^20) * 2^32 into this table. close() frees the slot and its device context at
 // once; a stale handle (closed, or from a reused slot) is detected, never dereferenced. Contexts
 // still open when the environment is torn down are closed by an env cleanup hook, before node
 // deletes the napi_env and while the HIP runtime is alive. Open contexts are capped
@@ -114,12 +114,20 @@ void close_all_at_teardown(void*) {
   }
 }
 
-Ctx* ctx_of_handle(void* p) {
-  const uint64_t h = reinterpret_cast<uintptr_t>(p);
+// A handle is a plain JS number, slot + 1 + (generation mod 2^20) * 2^32 (exact in a double).
+constexpr uint32_t kGenMask = 0xFFFFFu;
+Ctx* ctx_of_handle(uint64_t h) {
   const uint32_t slot = static_cast<uint32_t>(h & 0xffffffffu), gen = static_cast<uint32_t>(h >> 32);
   if (slot == 0 || slot > slots().size()) return nullptr;
   const Slot& s = slots()[slot - 1];
-  return s.gen == gen ? s.c : nullptr;
+  return (s.gen & kGenMask) == gen ? s.c : nullptr;
+}
+// The handle in v (false: v is not a number an open() returned).
+bool handle_of(napi_env env, napi_value v, uint64_t* h) {
+  double d = 0;
+  if (napi_get_value_double(env, v, &d) != napi_ok || !(d >= 1.0) || d > 9007199254740991.0) return false;
+  *h = static_cast<uint64_t>(d);
+  return static_cast<double>(*h) == d;
 }
 
 napi_value make_error(napi_env env, int rc, const std::string& msg) {
@@ -139,10 +147,9 @@ bool throw_fmt(napi_env env, int rc, const std::string& msg) {
 }
 
 bool get_ctx(napi_env env, napi_value v, Ctx** out) {
-  void* p = nullptr;
-  if (napi_get_value_external(env, v, &p) != napi_ok || p == nullptr)
-    return throw_fmt(env, FMT_E_USAGE, "expected an engine context from open()");
-  *out = ctx_of_handle(p);
+  uint64_t h = 0;
+  if (!handle_of(env, v, &h)) return throw_fmt(env, FMT_E_USAGE, "expected an engine context from open()");
+  *out = ctx_of_handle(h);
   if (*out == nullptr || (*out)->ctx == nullptr) return throw_fmt(env, FMT_E_USAGE, "engine context is closed");
   return true;
 }
@@ -225,28 +232,27 @@ napi_value Open(napi_env env, napi_callback_info info) {
   while (k < t.size() && t[k].c != nullptr) k++;
   if (k == t.size()) t.emplace_back();
   t[k].c = c;
-  const uint64_t h = static_cast<uint64_t>(k + 1) | (static_cast<uint64_t>(t[k].gen) << 32);
-  napi_value ext;
-  CHECK_NAPI(env, napi_create_external(env, reinterpret_cast<void*>(static_cast<uintptr_t>(h)), nullptr, nullptr, &ext));
-  return ext;
+  const uint64_t h = static_cast<uint64_t>(k + 1) | (static_cast<uint64_t>(t[k].gen & kGenMask) << 32);
+  napi_value num;
+  CHECK_NAPI(env, napi_create_double(env, static_cast<double>(h), &num));
+  return num;
 }
 
 napi_value Close(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-  void* p = nullptr;
-  if (argc < 1 || napi_get_value_external(env, argv[0], &p) != napi_ok || !p) {
+  uint64_t h = 0;
+  if (argc < 1 || !handle_of(env, argv[0], &h)) {
     throw_fmt(env, FMT_E_USAGE, "close: expected an engine context");
     return nullptr;
   }
-  Ctx* c = ctx_of_handle(p);
+  Ctx* c = ctx_of_handle(h);
   if (c == nullptr) return nullptr;  // already closed: a no-op, as before
   if (c->busy) {
     throw_fmt(env, FMT_E_USAGE, "close: a replay is still running on this context");
     return nullptr;
   }
-  const uint64_t h = reinterpret_cast<uintptr_t>(p);
   Slot& s = slots()[static_cast<uint32_t>(h & 0xffffffffu) - 1];
   if (c->ctx) fmt_close(c->ctx);
   delete c;
