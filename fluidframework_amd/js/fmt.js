@@ -152,7 +152,8 @@ class MergeTreeDocBuilder {
 		this.usesRelpos = false;
 		// f4: the document's observer is a local client with events of its own (streams.py _DocBuilder)
 		this.local = false;
-		this.pending = []; // [type, payload] of each pending local op, oldest first
+		this.pending = []; // [type, payload, refSeq] of each pending local op, oldest first
+		this.regenRef = 0;
 		this.curSeq = 0; // the last message's seq: a local op's refSeq (sequence.ts:666 currentRefSeq)
 	}
 	noteMarkerId(props) {
@@ -188,9 +189,13 @@ class MergeTreeDocBuilder {
 		if (i === undefined) {
 			i = this.clientNames.length;
 			if (i >= RECYCLE_FROM) {
+				// the engine's minSeq: in a document with local events it is also bounded by the oldest
+				// pending op's refSeq (getMinInFlightRefSeq, client.ts:1374-1378)
+				let floor = this.minSeq;
+				for (const p of this.pending) if (p[2] < floor) floor = p[2];
 				for (let j = 1; j < this.clientNames.length; j++) {
 					const st = this.lastStamp[j];
-					if (st === null || st <= this.minSeq) {
+					if (st === null || st <= floor) {
 						this.clientIds.delete(this.clientNames[j]);
 						this.clientNames[j] = id;
 						this.lastStamp[j] = null;
@@ -257,14 +262,14 @@ class MergeTreeDocBuilder {
 			this.owner.packOp(m, 0, this.curSeq, 0, 0, FMT_MT_F_LOCAL);
 			const o = (this.owner.ops.n - 1) * MT_OP_BYTES;
 			this.local = true;
-			this.pending.push([m.type, this.owner.ops.view.getUint32(o + 20, true)]);
+			this.pending.push([m.type, this.owner.ops.view.getUint32(o + 20, true), this.curSeq]);
 			this.nOps++;
 		}
 	}
 	/** Rollback of the newest pending op (client.ts:554; a GROUP op: once per member). */
 	localRollback() {
 		if (this.pending.length === 0) throw new Error("rollback without a pending local op");
-		const [t, payload] = this.pending.pop();
+		const [t, payload] = this.pending.pop(); // (refSeq dropped)
 		this.owner.rawOp(0, 0, 0, 0, 0, payload, 0, 0, t, FMT_MT_F_ROLLBACK);
 		this.nOps++;
 	}
@@ -273,15 +278,28 @@ class MergeTreeDocBuilder {
 	 * (MergeTreeReplay.regenerated) become the pending ops whose acks follow: pass them here or to
 	 * regenPending once known.
 	 */
-	localRegen(newOps) {
+	localRegen(newOps, newClientId) {
+		// newClientId: the new connection's clientId keeps short id 0 (startOrUpdateCollaboration,
+		// client.ts:1719-1725; the old long id stays mapped too), so the resubmitted ops come back as acks
+		if (newClientId !== undefined && newClientId !== null) this.renameLocal(newClientId);
 		this.local = true;
 		this.owner.rawOp(0, 0, 0, 0, 0, 0, 0, 0, 0, FMT_MT_F_REGEN);
 		this.nOps++;
+		// a resubmitted op keeps its original refSeq (sequence.ts:782-790): the oldest of the old pending
+		// ops' refSeqs still bounds the engine's minSeq
+		this.regenRef = this.pending.reduce((m, p) => Math.min(m, p[2]), this.curSeq);
 		this.pending = [];
 		if (newOps) this.regenPending(newOps);
 	}
+	/** startOrUpdateCollaboration with a new long id (client.ts:1719-1725): it names short id 0 now. */
+	renameLocal(newClientId) {
+		const i = this.clientIds.get(newClientId);
+		if (i !== undefined && i !== 0) throw new UnsupportedOp("a reconnect clientId that already names another client");
+		this.clientIds.set(newClientId, 0);
+		this.clientNames[0] = newClientId;
+	}
 	regenPending(newOps) {
-		this.pending = newOps.map((op) => [op.type, op.type === MT_ANNOTATE ? this.owner.propsOp(op.props || {}, op.adjust) : 0]);
+		this.pending = newOps.map((op) => [op.type, op.type === MT_ANNOTATE ? this.owner.propsOp(op.props || {}, op.adjust) : 0, this.regenRef]);
 	}
 	/**
 	 * SharedObjectCore.processMessagesCore shape: a bunch sharing one envelope (sequence.ts:873-919).

@@ -40,6 +40,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -85,42 +86,73 @@ struct Ctx {
 // deletes the napi_env and while the HIP runtime is alive. Open contexts are capped
 // (FMT_NAPI_MAX_CONTEXTS, default 64): a caller that drops contexts without close() gets
 // FMT_E_CAPACITY instead of device memory that grows without bound.
+// The table is process-wide (a handle is only a number), but every slot belongs to the napi_env
+// (main thread or worker_thread) that opened it: only that env can use or close it, and its env
+// cleanup hook closes only its own slots, so one worker's teardown never closes another thread's
+// contexts. Slots are reached under one mutex (a worker's open() may grow the vector while another
+// thread looks a handle up); a Ctx itself is only ever touched by its owner's thread.
 struct Slot {
   Ctx* c = nullptr;
+  napi_env env = nullptr;  // the owner
   uint32_t gen = 0;
 };
 std::vector<Slot>& slots() {
   static std::vector<Slot>* s = new std::vector<Slot>();
   return *s;
 }
+std::mutex& slots_mu() {
+  static std::mutex* m = new std::mutex();
+  return *m;
+}
 uint32_t max_contexts() {
   const char* e = std::getenv("FMT_NAPI_MAX_CONTEXTS");
   const long v = e ? std::strtol(e, nullptr, 10) : 0;
   return v > 0 ? static_cast<uint32_t>(v) : 64u;
 }
-uint32_t live_contexts() {
+uint32_t live_contexts() {  // (caller holds slots_mu)
   uint32_t n = 0;
   for (const Slot& s : slots()) n += s.c != nullptr;
   return n;
 }
 
-void close_all_at_teardown(void*) {
-  for (Slot& s : slots()) {
-    if (s.c == nullptr || s.c->busy) continue;  // (a replay still on a worker: left to process exit)
-    if (s.c->ctx) fmt_close(s.c->ctx);
-    delete s.c;
-    s.c = nullptr;
-    s.gen++;
+// env cleanup hook (arg: the env it was registered for): closes that env's contexts only
+void close_env_at_teardown(void* arg) {
+  const napi_env env = static_cast<napi_env>(arg);
+  std::vector<Ctx*> mine;
+  {
+    std::lock_guard<std::mutex> lk(slots_mu());
+    for (Slot& s : slots()) {
+      if (s.c == nullptr || s.env != env || s.c->busy) continue;  // (a replay still on a worker: left to process exit)
+      mine.push_back(s.c);
+      s.c = nullptr;
+      s.env = nullptr;
+      s.gen++;
+    }
+  }
+  for (Ctx* c : mine) {
+    if (c->ctx) fmt_close(c->ctx);
+    delete c;
   }
 }
 
 // A handle is a plain JS number, slot + 1 + (generation mod 2^20) * 2^32 (exact in a double).
 constexpr uint32_t kGenMask = 0xFFFFFu;
-Ctx* ctx_of_handle(uint64_t h) {
+enum class Lookup { kOk, kStale, kForeign };
+// The open context handle h names, if it belongs to env (kForeign: another thread's context).
+Ctx* ctx_of_handle(napi_env env, uint64_t h, Lookup* why = nullptr) {
   const uint32_t slot = static_cast<uint32_t>(h & 0xffffffffu), gen = static_cast<uint32_t>(h >> 32);
-  if (slot == 0 || slot > slots().size()) return nullptr;
-  const Slot& s = slots()[slot - 1];
-  return (s.gen & kGenMask) == gen ? s.c : nullptr;
+  std::lock_guard<std::mutex> lk(slots_mu());
+  Lookup w = Lookup::kStale;
+  Ctx* c = nullptr;
+  if (slot != 0 && slot <= slots().size()) {
+    const Slot& s = slots()[slot - 1];
+    if ((s.gen & kGenMask) == gen && s.c != nullptr) {
+      w = s.env == env ? Lookup::kOk : Lookup::kForeign;
+      c = w == Lookup::kOk ? s.c : nullptr;
+    }
+  }
+  if (why) *why = w;
+  return c;
 }
 // The handle in v (false: v is not a number an open() returned).
 bool handle_of(napi_env env, napi_value v, uint64_t* h) {
@@ -149,7 +181,10 @@ bool throw_fmt(napi_env env, int rc, const std::string& msg) {
 bool get_ctx(napi_env env, napi_value v, Ctx** out) {
   uint64_t h = 0;
   if (!handle_of(env, v, &h)) return throw_fmt(env, FMT_E_USAGE, "expected an engine context from open()");
-  *out = ctx_of_handle(h);
+  Lookup why;
+  *out = ctx_of_handle(env, h, &why);
+  if (why == Lookup::kForeign)
+    return throw_fmt(env, FMT_E_USAGE, "engine context belongs to another thread (open one per worker)");
   if (*out == nullptr || (*out)->ctx == nullptr) return throw_fmt(env, FMT_E_USAGE, "engine context is closed");
   return true;
 }
@@ -209,10 +244,13 @@ napi_value Open(napi_env env, napi_callback_info info) {
   CHECK_NAPI(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
   int32_t device = 0;
   if (argc >= 1) napi_get_value_int32(env, argv[0], &device);
-  if (live_contexts() >= max_contexts()) {
-    throw_fmt(env, FMT_E_CAPACITY,
-              "open: " + std::to_string(max_contexts()) + " engine contexts are open (close() the ones no longer used)");
-    return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(slots_mu());
+    if (live_contexts() >= max_contexts()) {
+      throw_fmt(env, FMT_E_CAPACITY,
+                "open: " + std::to_string(max_contexts()) + " engine contexts are open (close() the ones no longer used)");
+      return nullptr;
+    }
   }
   fmt_config cfg;
   std::memset(&cfg, 0, sizeof cfg);
@@ -227,12 +265,17 @@ napi_value Open(napi_env env, napi_callback_info info) {
   }
   auto* c = new Ctx;
   c->ctx = ctx;
-  std::vector<Slot>& t = slots();
-  size_t k = 0;
-  while (k < t.size() && t[k].c != nullptr) k++;
-  if (k == t.size()) t.emplace_back();
-  t[k].c = c;
-  const uint64_t h = static_cast<uint64_t>(k + 1) | (static_cast<uint64_t>(t[k].gen & kGenMask) << 32);
+  uint64_t h;
+  {
+    std::lock_guard<std::mutex> lk(slots_mu());
+    std::vector<Slot>& t = slots();
+    size_t k = 0;
+    while (k < t.size() && t[k].c != nullptr) k++;
+    if (k == t.size()) t.emplace_back();
+    t[k].c = c;
+    t[k].env = env;
+    h = static_cast<uint64_t>(k + 1) | (static_cast<uint64_t>(t[k].gen & kGenMask) << 32);
+  }
   napi_value num;
   CHECK_NAPI(env, napi_create_double(env, static_cast<double>(h), &num));
   return num;
@@ -247,24 +290,38 @@ napi_value Close(napi_env env, napi_callback_info info) {
     throw_fmt(env, FMT_E_USAGE, "close: expected an engine context");
     return nullptr;
   }
-  Ctx* c = ctx_of_handle(h);
+  Lookup why;
+  Ctx* c = ctx_of_handle(env, h, &why);
+  if (why == Lookup::kForeign) {
+    throw_fmt(env, FMT_E_USAGE, "close: engine context belongs to another thread");
+    return nullptr;
+  }
   if (c == nullptr) return nullptr;  // already closed: a no-op, as before
   if (c->busy) {
     throw_fmt(env, FMT_E_USAGE, "close: a replay is still running on this context");
     return nullptr;
   }
-  Slot& s = slots()[static_cast<uint32_t>(h & 0xffffffffu) - 1];
+  {
+    std::lock_guard<std::mutex> lk(slots_mu());
+    Slot& s = slots()[static_cast<uint32_t>(h & 0xffffffffu) - 1];
+    s.c = nullptr;
+    s.env = nullptr;
+    s.gen++;
+  }
   if (c->ctx) fmt_close(c->ctx);
   delete c;
-  s.c = nullptr;
-  s.gen++;
   return nullptr;
 }
 
 // openContexts() -> number of engine contexts open in this process (diagnostics and tests)
 napi_value OpenContexts(napi_env env, napi_callback_info) {
   napi_value v;
-  CHECK_NAPI(env, napi_create_uint32(env, live_contexts(), &v));
+  uint32_t n;
+  {
+    std::lock_guard<std::mutex> lk(slots_mu());
+    n = live_contexts();
+  }
+  CHECK_NAPI(env, napi_create_uint32(env, n, &v));
   return v;
 }
 
@@ -332,7 +389,6 @@ struct Job {
   napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
   Ctx* c = nullptr;
-  napi_ref ctx_ref = nullptr;
   std::vector<napi_ref> keep;  // input arrays stay alive (and unmoved) until Complete
   enum Kind { kMergeTree, kMap, kMapSparse, kSummarize } kind = kMergeTree;
   fmt_mt_batch mt;
@@ -450,7 +506,6 @@ void Complete(napi_env env, napi_status, void* p) {  // JS thread
     napi_resolve_deferred(env, j->deferred, buffer(j->out));
   }
   for (napi_ref r : j->keep) napi_delete_reference(env, r);
-  napi_delete_reference(env, j->ctx_ref);
   napi_delete_async_work(env, j->work);
   delete j;
 }
@@ -465,9 +520,8 @@ bool keep_array(napi_env env, Job* j, napi_value v) {
   return true;
 }
 
-napi_value queue(napi_env env, Job* j, napi_value ctx_val, const char* name) {
+napi_value queue(napi_env env, Job* j, napi_value /*ctx: a number handle, kept alive by the slot table*/, const char* name) {
   napi_value promise, res_name;
-  napi_create_reference(env, ctx_val, 1, &j->ctx_ref);
   napi_create_promise(env, &j->deferred, &promise);
   napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res_name);
   napi_create_async_work(env, nullptr, res_name, Execute, Complete, j, &j->work);
@@ -1040,7 +1094,7 @@ void install_segv_trace() {
 
 napi_value Init(napi_env env, napi_value exports) {
   if (std::getenv("FMT_NAPI_BACKTRACE") != nullptr) install_segv_trace();
-  napi_add_env_cleanup_hook(env, close_all_at_teardown, nullptr);
+  napi_add_env_cleanup_hook(env, close_env_at_teardown, env);
   napi_property_descriptor fns[] = {
       {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
       {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

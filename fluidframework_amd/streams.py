@@ -292,7 +292,8 @@ class _DocBuilder:
         # unacknowledged ops in submission order, each (record type, payload) — what ACK and
         # ROLLBACK records must repeat (mergeTree.ts:1325-1408, 2388-2514)
         self.local = False
-        self.pending: list[tuple] = []
+        self.pending: list[tuple] = []  # (record type, payload, refSeq)
+        self.regen_ref = 0  # the oldest refSeq among the ops the last reconnect regenerated
         self.cur_seq = 0  # the last message's seq: a local op's refSeq (sequence.ts:666 currentRefSeq)
 
     def note_marker_id(self, props) -> None:
@@ -340,9 +341,12 @@ class _DocBuilder:
         if i is None:
             i = len(self.client_names)
             if i >= RECYCLE_FROM:
+                # the engine's minSeq: in a document with local events it is also bounded by the
+                # oldest pending op's refSeq (getMinInFlightRefSeq, client.ts:1374-1378)
+                floor = min([self.min_seq] + [p[2] for p in self.pending])
                 for j in range(1, len(self.client_names)):
                     st = self.last_stamp[j]
-                    if st is None or st <= self.min_seq:
+                    if st is None or st <= floor:
                         del self.client_ids[self.client_names[j]]
                         self.client_names[j] = long_id
                         self.last_stamp[j] = None
@@ -401,33 +405,49 @@ class _DocBuilder:
             if rec[9] & (MT_F_REL1 | MT_F_REL2):
                 raise UnsupportedOp("local op with relative positions")
             self.local = True
-            self.pending.append((rec[8], rec[5]))
+            self.pending.append((rec[8], rec[5], self.cur_seq))
             self.ops.append(rec[:-1] + (rec[-1] | MT_F_LOCAL,))
 
     def local_rollback(self) -> None:
         """Rollback of the newest pending op (client.ts:554; a GROUP op: call once per member)."""
         if not self.pending:
             raise ValueError("rollback without a pending local op")
-        t, payload = self.pending.pop()
+        t, payload, _ = self.pending.pop()
         self.ops.append((0, 0, 0, 0, 0, payload, 0, 0, t, MT_F_ROLLBACK))
 
-    def local_regen(self, new_ops: list | None = None) -> None:
+    def local_regen(self, new_ops: list | None = None, new_client_id: str | None = None) -> None:
         """Reconnect: regeneratePendingOp for every pending op (client.ts:1452-1542). The ops it
         returns (one per segment of each pending op, in order: what fmt_mt_fetch_regen returns)
         become the pending ops, whose acks follow as the local client's messages: pass them here, or
-        to regen_pending once known."""
+        to regen_pending once known. new_client_id: the clientId of the new connection, which keeps
+        the local client's short id 0 (startOrUpdateCollaboration, client.ts:1719-1725: the old long
+        id stays mapped too), so its resubmitted ops come back as acks, not as remote ops."""
+        if new_client_id is not None:
+            self.rename_local(new_client_id)
         self.local = True
         self.ops.append((0, 0, 0, 0, 0, 0, 0, 0, 0, MT_F_REGEN))
+        # a resubmitted op keeps its original refSeq (sequence.ts:782-790): the regenerated ops' refSeqs
+        # are the old pending ops', whose oldest bounds the engine's minSeq as before
+        self.regen_ref = min([p[2] for p in self.pending], default=self.cur_seq)
         self.pending = []
         if new_ops is not None:
             self.regen_pending(new_ops)
+
+    def rename_local(self, new_client_id: str) -> None:
+        """startOrUpdateCollaboration with a new long id (client.ts:1719-1725): it names short id 0
+        from now on; the old one keeps mapping to 0."""
+        i = self.client_ids.get(new_client_id)
+        if i is not None and i != 0:
+            raise UnsupportedOp("a reconnect clientId that already names another client")
+        self.client_ids[new_client_id] = 0
+        self.client_names[0] = new_client_id
 
     def regen_pending(self, new_ops: list) -> None:
         self.pending = []
         for op in new_ops:
             t = op["type"]
             payload = self.owner._props_op(op.get("props") or {}, op.get("adjust")) if t == MT_ANNOTATE else 0
-            self.pending.append((t, payload))
+            self.pending.append((t, payload, self.regen_ref))
 
     def add_op(self, seq, ref_seq, min_seq, client, op: dict) -> None:
         self._note_op(op)

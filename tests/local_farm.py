@@ -99,8 +99,11 @@ class LocalFarm:
     """A generated multi-client farm; every participant's own event stream is one document."""
 
     def __init__(self, seed, n_clients=4, initial="", min_length=8, keys=("a", "b", "c"), markers=True,
-                 builder: MergeTreeStreamBuilder | None = None):
+                 builder: MergeTreeStreamBuilder | None = None, new_ids=False):
         self.rnd = random.Random(seed)
+        # new_ids: every reconnect comes back under a new clientId (as a real reconnect does); the
+        # local client keeps its short id (startOrUpdateCollaboration, client.ts:1719-1725)
+        self.new_ids = new_ids
         self.b = builder if builder is not None else MergeTreeStreamBuilder()
         self.initial = initial
         self.min_length = min_length
@@ -205,8 +208,13 @@ class LocalFarm:
         self.inflight = [e for e in self.inflight if e[0] is not p]
         while self.inflight:
             self.sequence_one()
-        self.log.append((p.index, "local_regen"))
-        p.doc.local_regen()  # (the REGEN record; the pending ops follow once the oracle made them)
+        if self.new_ids:
+            p.name = f"{p.name.split('~')[0]}~{self.regens + 1}"
+            self.log.append((p.index, "local_regen", None, p.name))
+            p.doc.local_regen(None, p.name)
+        else:
+            self.log.append((p.index, "local_regen"))
+            p.doc.local_regen()  # (the REGEN record; the pending ops follow once the oracle made them)
         p.sync()
         recs, text = p.orc.regen_take()
         new_ops = [self._regen_op(p, r, text) for r in recs]

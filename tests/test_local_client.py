@@ -34,6 +34,16 @@ def farms_local():
     return batch, farms
 
 
+@pytest.fixture(scope="module")
+def farms_new_ids():
+    """Farms whose every reconnect comes back under a new clientId: the packer keeps the
+    local client's short id 0 for it (startOrUpdateCollaboration, client.ts:1719-1725), so the
+    resubmitted ops are acked, not applied a second time as remote ops."""
+    batch, farms = local_farm_batch(range(10, 14), steps=500, n_clients=5, min_length=120, new_ids=True)
+    assert sum(f.regens for f in farms) >= 10
+    return batch, farms
+
+
 def _oracle(orc, batch, large=True):
     cl, cc, cp = emu_caps(large)
     rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024)
@@ -57,6 +67,18 @@ def test_oracle_local_farms_converge(orc, farms_local):
     for f in farms:
         texts = f.texts()
         assert all(t == texts[0] for t in texts), texts
+
+
+def test_oracle_local_farms_with_new_client_ids_converge(orc, farms_new_ids):
+    from fluidframework_amd.streams import MT_F_ACK
+
+    batch, farms = farms_new_ids
+    for f in farms:
+        texts = f.texts()
+        assert all(t == texts[0] for t in texts), texts
+        # every participant's sequenced op came back to its author as an ack, reconnects included
+        assert len({p.name for p in f.parts}) == len(f.parts) and any("~" in p.name for p in f.parts)
+    assert ((batch.ops["flags"] & MT_F_ACK) != 0).sum() > 200
 
 
 def _check_engine_vs_oracle(orc, batch, got, regen_of, expected=None):
@@ -87,6 +109,11 @@ def test_emulated_engine_local_fixtures_match_oracle(orc, fixtures_local):
 def test_emulated_engine_local_farms_match_oracle(orc, farms_local):
     batch, _ = farms_local
     assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen) > 50
+
+
+def test_emulated_engine_local_farms_with_new_client_ids_match_oracle(orc, farms_new_ids):
+    batch, _ = farms_new_ids
+    assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen) > 20
 
 
 def test_emulated_engine_local_usage_and_data_errors(orc):
@@ -155,6 +182,12 @@ def test_gpu_local_fixtures_match_oracle(orc, engine, fixtures_local):
 def test_gpu_local_farms_match_oracle_and_regenerate_the_same_ops(orc, engine, farms_local):
     batch, _ = farms_local
     assert _check_engine_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen) > 50
+
+
+@pytest.mark.gpu
+def test_gpu_local_farms_with_new_client_ids_match_oracle(orc, engine, farms_new_ids):
+    batch, _ = farms_new_ids
+    assert _check_engine_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen) > 20
 
 
 @pytest.mark.gpu

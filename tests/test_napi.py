@@ -557,27 +557,29 @@ _LOCAL_JS = (
     "for(const e of log){const d=docs[e[0]];"
     "if(e[1]==='begin')docs[e[0]]=b.beginDoc(e[2],e[3]);"
     "else if(e[1]==='local_op')d.localOp(e[2]);else if(e[1]==='add_message')d.addMessage(e[2]);"
-    "else if(e[1]==='local_rollback')d.localRollback();else if(e[1]==='local_regen')d.localRegen();"
+    "else if(e[1]==='local_rollback')d.localRollback();else if(e[1]==='local_regen')d.localRegen(e[2]||undefined,e[3]);"
     "else if(e[1]==='regen_pending')d.regenPending(e[2]);else throw new Error(e[1]);}"
     "const batch=b.finish();")
 
 
-def _local_log(tmp_path, seeds=(3, 4), steps=300):
+def _local_log(tmp_path, seeds=(3, 4), steps=300, **kw):
     from local_farm import farm_log, local_farm_batch
 
-    _, farms = local_farm_batch(seeds, steps=steps)
+    _, farms = local_farm_batch(seeds, steps=steps, **kw)
     log = farm_log(farms)
     path = tmp_path / "local_log.json"
     path.write_text(json.dumps(log))
     return log, path
 
 
-def test_js_packer_local_client_matches_python(addon, tmp_path):
+@pytest.mark.parametrize("new_ids", [False, True])
+def test_js_packer_local_client_matches_python(addon, tmp_path, new_ids):
     """fmt.js packs the local client's events (localOp / acks / localRollback / localRegen) into the
-    same records as streams.py (tests/local_farm.py farms, documents written contiguously)."""
+    same records as streams.py (tests/local_farm.py farms, documents written contiguously; new_ids:
+    every reconnect under a new clientId, which keeps short id 0)."""
     from local_farm import replay_log
 
-    log, path = _local_log(tmp_path)
+    log, path = _local_log(tmp_path, new_ids=new_ids)
     script = tmp_path / "local_pack.js"
     script.write_text(_LOCAL_JS % (json.dumps(os.path.join(PKG, "js", "fmt.js")), json.dumps(str(path))) +
                       "const hex=(a)=>Buffer.from(a.buffer,a.byteOffset,a.byteLength).toString('hex');"
