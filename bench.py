@@ -65,7 +65,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["mt", "t2", "t3", "map", "ob"], default="mt",
+    ap.add_argument("--workload", choices=["mt", "t2", "t3", "map", "ob", "local"], default="mt",
                     help="mt: T1 (per-GPU shard of 100k docs); t2: one 1M-doc batch partitioned over the ranks "
                          "(the default for mt when --gpus > 1); t3: one SharedString of 10M segments; map: M2; "
                          "ob: the reference's 30 obliterate conflict farms replicated to --docs documents")
@@ -128,7 +128,8 @@ def main():
     if args.workload == "t3":
         return bench_t3(args, rank, world, local_rank, dist)
     ob = args.workload == "ob"
-    mt = args.workload in ("mt", "t2", "ob")
+    loc = args.workload == "local"
+    mt = args.workload in ("mt", "t2", "ob", "local")
     t2 = args.workload == "t2" or (args.workload == "mt" and world > 1)
     opd = 2040 if ob else args.ops_per_doc or (2000 if mt else 1000)
     if t2:
@@ -138,7 +139,7 @@ def main():
         lo, hi = shard.plan_shards(np.arange(total_docs + 1, dtype=np.uint64) * np.uint64(opd), world)[rank]
         docs, doc_base = hi - lo, lo
     else:
-        docs = args.docs or (100_000 if mt else 1_000_000)
+        docs = args.docs or (100_000 if mt else 1_000_000)  # (local: pass --docs for a shorter run)
         total_docs, doc_base = docs * world, rank * docs  # weak scaling: every rank its own docs
     seed = args.seed if mt else args.seed + 1000 * rank
 
@@ -153,6 +154,17 @@ def main():
         fixtures = list(replay_fixtures("replay_obliterate_2.3.0.npz"))
         uniq = len(fixtures)
         batch = workloads.replicate_batches([f[1] for f in fixtures], docs)
+    elif loc:
+        # f4 local client: each writing client's own view of the reference's 0.40 conflict
+        # farms (its ops of a round submitted locally, then the round's messages, its own acking them;
+        # tests/local_farm.py), 28 (fixture, writer) streams cycled to `docs` documents
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from local_farm import fixture_local_docs
+
+        fixtures = fixture_local_docs()
+        uniq = len(fixtures)
+        batch = workloads.replicate_batches([f[1] for f in fixtures], docs)
+        opd = int(round(len(batch.ops) / docs))
     elif mt:
         uniq = min(args.unique_docs or docs, docs)
         if docs % uniq:
@@ -228,6 +240,8 @@ def main():
         digest_ms = (time.perf_counter() - t) * 1e3
         if ob:
             _check_obliterate_farms(eng, hdrs, fixtures, docs)
+        if loc:
+            _check_local_farms(eng, hdrs, fixtures, docs)
         if t2 and args.t2_check_docs > 0:
             t2_check = _t2_oracle_check(batch, digests, docs, doc_base, args.t2_check_docs, world)
     elif args.sparse:
@@ -263,7 +277,7 @@ def main():
                         "what": f"legacy summaries (header, body) of the first {args.gather_docs} documents of every "
                                 "shard, gathered to rank 0 (all-gather of byte counts + grouped send/recv)"}
     summaries = None
-    if mt and not t2 and not ob and not args.no_summaries:
+    if mt and not t2 and not ob and not loc and not args.no_summaries:
         # every document's legacy summary from the converged state (device merge + host JSON on the
         # usable cores), timed apart from the replay; a sample checked against the Python host
         from fluidframework_amd.summary import legacy_summary
@@ -357,7 +371,7 @@ def main():
         }
         log(rank, f"[bench] cpu baseline {cpu['value']:.3g} ops/s on {threads} threads ({secs:.1f}s); "
                   f"{checked} documents equal to the oracle's")
-        if not args.no_js_baseline and not ob and not args.sparse:
+        if not args.no_js_baseline and not ob and not loc and not args.sparse:
             cpu_js = (_js_mt_baseline if mt else _js_map_baseline)(oracle, batch, docs, threads, args.cpu_seconds / 2)
             if cpu_js is not None:
                 log(rank, f"[bench] JS baseline {cpu_js['value']:.3g} ops/s on {threads} worker_threads")
@@ -387,12 +401,15 @@ def main():
             "dtype": "int32",
             "data": (f"reference fixtures: the 30 obliterate conflict farms (merge-tree 2.3.0 results), cycled to "
                      f"{docs} docs per GPU" if ob else
+                     f"reference fixtures: each writing client's local view of the 0.40 conflict farms ({uniq} streams: "
+                     f"local submissions, acks), cycled to {docs} docs per GPU" if loc else
                      f"synthetic ({'conflict-farm' if mt else 'map fuzz'} shape, reference XSadd PRNG; "
                      + (f"one {total_docs}-doc batch partitioned by shard.plan_shards)" if t2
                         else f"{docs} distinct docs per GPU)" if not mt or uniq == docs
                         else f"{uniq} distinct docs per GPU replicated to {docs})")),
             "config": {
                 "workload": ("merge-tree conflict farms with obliterate (reference fixtures) replay" if ob
+                             else "f4 local-client replay (writer views of the reference conflict farms)" if loc
                              else f"T2 merge-tree conflict-farm replay, {total_docs} docs doc-sharded over {world} GPU(s)" if t2
                              else (f"merge-tree conflict-farm replay, documents kept >= {args.min_length} UTF-16 units"
                                    if args.min_length else "T1 merge-tree conflict-farm replay") if mt
@@ -568,6 +585,18 @@ def _check_obliterate_farms(eng, hdrs, fixtures, docs):
                        if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000)
         if text != fixtures[d][4][-1]:
             raise SystemExit(f"obliterate farm {fixtures[d][0]}: final text differs from the reference's")
+
+
+def _check_local_farms(eng, hdrs, fixtures, docs):
+    """The first copy of every writer-view stream reaches the fixture's final resultText (the
+    reference's own recorded result); the oracle digest check covers every sampled copy."""
+    for d in range(min(len(fixtures), docs)):
+        lv, ch, _ = eng.mt_doc(d, hdrs[d])
+        text = "".join(ch[int(L["char_off"]):int(L["char_off"]) + int(L["len"])].tobytes().decode("utf-16-le", "surrogatepass")
+                       for L in lv[:int(hdrs[d]["n_leaves"])]
+                       if int(L["rm_seq"]) == 0x7FFFFFFF and not int(L["pad"]) & 0x8000)
+        if text != fixtures[d][2]:
+            raise SystemExit(f"local document {d} ({fixtures[d][0]}) does not reach the fixture's resultText")
 
 
 def _bench_catchup(eng, batch, hdrs, docs, sample):

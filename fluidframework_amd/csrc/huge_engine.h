@@ -80,6 +80,10 @@ FMT_DEV uint32_t mix32(uint32_t x) {  // (a 32-bit finalizer: prop-set hashes)
 
 // Window meta word: insert client (int8) | first remover (u8) << 8 | "more removers" << 16; the
 // record's word 3 adds the entry's group << 17
+// NOT reliable after a large → huge checkpoint (loadFromLarge): the large tier keeps the remove-client
+// set, not which remover came first, so the lowest id stands in there. Nothing reads it today (the
+// passes use the set; SnapshotV1's removedClientIds come from the remove-order slab, which checkpointed
+// batches never carry); a future reader must carry the first remover through huge_ckpt.h first.
 FMT_DEV uint32_t wFirstRm(uint32_t m) { return (m >> 8) & 0xFFu; }
 constexpr uint32_t kWMetaMask = 0x1FFFFu;
 constexpr int kWGroupShift = 17;

@@ -63,6 +63,26 @@ def fixture_local_batch(stride=8, max_fixtures=None, clients=None):
     return b.finish(), expected, where
 
 
+def fixture_local_docs(max_fixtures=None):
+    """Every writing client's whole local stream of each 0.40 fixture (all 64 rounds) as its own
+    single-document batch, with the fixture's final resultText: the `bench.py --workload local`
+    sources (cycled to the bench's document count by workloads.replicate_batches)."""
+    out = []
+    for fx in load_fixture_msgs()[:max_fixtures]:
+        groups = fx["groups"]
+        for x in sorted({m["clientId"] for g in groups for m in g["msgs"]}):
+            b = MergeTreeStreamBuilder()
+            d = b.begin_doc(initial_text=groups[0]["initialText"], observer=x)
+            for g in groups:
+                for m in g["msgs"]:
+                    if m["clientId"] == x:
+                        d.local_op(m["contents"])
+                for m in g["msgs"]:
+                    d.add_message(m)
+            out.append((f"{fx['name']}/{x}", b.finish(), groups[-1]["resultText"]))
+    return out
+
+
 class _Participant:
     def __init__(self, farm: "LocalFarm", name: str):
         from oracle import MergeTreeDoc  # (oracle/oracle.py: tests put oracle/ on sys.path)

@@ -204,6 +204,8 @@ SHIFT4 = [("mt_engine.h", """    const int count = nChars - from;
 VISBF = [("mt_engine.h", '  FMT_DEV void visLengths(int refSeq, int client, Lane<VR>& vis, int nr) const {\n    FOR_ROWS(r, 0, nr) {\n      FOR_LANES(l) {\n        const uint32_t w0 = LANE(W[0])[r];\n        const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]);\n        const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);\n        const int32_t ic = fClient(LANE(W[4])[r]);\n        const bool present = (ins <= refSeq || ic == client) && !(rm <= refSeq || removedBy(l, r, client));\n        LANE(vis)[r] = present ? fLen(w0) : 0u;\n      }\n    }\n  }', '  FMT_DEV void visLengths(int refSeq, int client, Lane<VR>& vis, int nr) const {\n    // branch-free: every term is a 0/1 word in a VGPR (shifts of differences, which cannot overflow:\n    // stamps are in [0, 2^31)), so no lane masks are combined in scalar registers\n    const bool hiW = C::kWords > 5 && client >= 32;\n    const uint32_t sh = client < 0 ? 0u : static_cast<uint32_t>(client & 31);\n    const uint32_t cm = client < 0 ? 0u : 1u;\n    const uint32_t cl8 = static_cast<uint32_t>(client) & 0xFFu;\n    FOR_ROWS(r, 0, nr) {\n      FOR_LANES(l) {\n        const uint32_t w0 = LANE(W[0])[r];\n        const uint32_t ins = LANE(W[1])[r];\n        const uint32_t rm = LANE(W[2])[r];\n        const uint32_t insLE = ((static_cast<uint32_t>(refSeq) - ins) >> 31) ^ 1u;\n        const uint32_t rmLE = ((static_cast<uint32_t>(refSeq) - rm) >> 31) ^ 1u;\n        const uint32_t icEq = (((LANE(W[4])[r] >> 24) ^ cl8) - 1u) >> 31;\n        const uint32_t rmb = ((hiW ? LANE(W[C::kWords > 5 ? 5 : 3])[r] : LANE(W[3])[r]) >> sh) & cm;\n        const uint32_t present = (insLE | icEq) & ((rmLE | rmb) ^ 1u);\n        LANE(vis)[r] = fLen(w0) * present;\n      }\n    }\n  }')]
 
 VARIANTS = {
+    # huge tier without its per-phase shader-clock reads (ProfScope's s_memtime pairs)
+    "t3noclk": [("huge_engine.h", "    return __builtin_amdgcn_s_memtime();", "    return 0;")],
     "visbf": VISBF,
     "chars4": SHIFT4,
     "pass8": [("huge_engine.h", "  static constexpr int kPassU = 16;", "  static constexpr int kPassU = 8;")],

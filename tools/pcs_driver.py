@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One T1-shaped replay through a given libfmt.so (a PC-sampling target: run under rocprofv3
+"""One T1-shaped (or --workload t3: T3-slice) replay through a given libfmt.so (a PC-sampling target: run under rocprofv3
 --pc-sampling-*; tools/pcs_attribute.py maps the samples to source lines)."""
 import argparse
 import os
@@ -17,8 +17,14 @@ def main():
     ap.add_argument("--docs", type=int, default=20000)
     ap.add_argument("--unique", type=int, default=2000)
     ap.add_argument("--runs", type=int, default=2)
+    ap.add_argument("--workload", choices=["mt", "t3"], default="mt")
+    ap.add_argument("--segments", type=int, default=2_000_000, help="t3: segments of the loaded document")
+    ap.add_argument("--t3-ops", type=int, default=200_000, help="t3: ops replayed")
     a = ap.parse_args()
-    batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
+    if a.workload == "t3":
+        batch = workloads.t3_stream(a.segments, a.t3_ops)
+    else:
+        batch = workloads.conflict_farm(a.unique, n_clients=8, ops_per_doc=2000, seed=5, replicas=a.docs // a.unique)
     e = native.Engine(0, lib_path=a.lib)
     e.mt_load(batch)
     for k in range(a.runs):
