@@ -57,7 +57,7 @@ constexpr int kSlotCap = FMT_HUGE_SLOTCAP;  // leaf blocks listed per group
 constexpr int kGroupCap = 2048;       // groups
 constexpr int kHeapCap = 10240;       // LRU heap entries (≈ blocks registered in one window)
 constexpr int kPropCap = 65534;       // interned prop sets per document (ids fit the meta word's 16 bits)
-constexpr int kPropLds = 4096;        // match classes of the first sets cached in LDS
+constexpr int kPropLds = 2048;        // match classes of the first sets cached in LDS
 constexpr uint32_t kPropHash = 1u << 17;  // buckets per prop-set hash table (exact content, match class)
 constexpr int kPropWords = 1 + FMT_MT_PROPS_MAX;  // a prop set in HBM: n, kv[]
 constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
@@ -87,9 +87,10 @@ FMT_DEV uint32_t mix32(uint32_t x) {  // (a 32-bit finalizer: prop-set hashes)
 FMT_DEV uint32_t wFirstRm(uint32_t m) { return (m >> 8) & 0xFFu; }
 constexpr uint32_t kWMetaMask = 0x1FFFFu;
 constexpr int kWGroupShift = 17;
-constexpr int kWinList = 1024;  // LDS list of one group's visible window entries (slot pass)
-constexpr int kGlCap = 2048;    // LDS list of the visible window entries of one group pass
-constexpr int kGlEntBits = 21;  // entry index bits in glEnt (the group id above them)
+// The first kWinLds window entries are mirrored in LDS (HugeLds::wRecL / wMaskL; HBM stays the
+// authoritative copy and every write updates both): the per-op window passes read them there instead
+// of issuing L2 round trips (round 6). T3 keeps about 1.2k entries in its window.
+constexpr uint32_t kWinLds = 1280;
 
 // One live obliterate (mergeTree.ts ObliterateInfo) is a 6-word record of HugeState::obRec: its
 // endpoint references as (leaf id, offset) — id 0 once the reference is removed — and its stamp.
@@ -199,6 +200,9 @@ struct HugeState {
 
 // LDS state of the wave.
 struct HugeLds {
+  // window entries [0, kWinLds): their 16-byte records and remove-client masks (HugeState::wRec / wMask)
+  alignas(16) uint32_t wRecL[kWinLds * 4];
+  alignas(16) uint32_t wMaskL[kWinLds * 2];
   uint16_t gOrder[kGroupCap];    // group ids in document order
   int32_t gStable[kGroupCap];    // by group id: Σ stable lengths of its slots
   uint16_t gCount[kGroupCap];    // by group id: slots (<= kSlotCap)
@@ -214,14 +218,6 @@ struct HugeLds {
   uint16_t pClass[kPropLds];     // S.pClass of the first kPropLds sets
   uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (lane k = entry k)
   int32_t cmd[8];                // pass command from wave 0 to the helper waves (HugeDoc::PassCmd)
-  uint32_t wlEnt[kWinList];      // slot pass: listed window entries and their view lengths
-  int32_t wlVis[kWinList];
-  // group pass: every window entry of positive view length in the pass's perspective, (entry |
-  // group << 21, view length), kGlPerWave per wave; the slot passes of the same find read these
-  // instead of the window table (glN[w] < 0: that wave's part overflowed)
-  uint32_t glEnt[kGlCap];
-  int32_t glVis[kGlCap];
-  int32_t glN[4];
 };
 
 struct HugeInputs {
@@ -388,7 +384,6 @@ class HugeDocT {
   bool corrValid = false;    // gCorr holds the current op's perspective
   uint32_t epoch = 0;        // bumped by every change of the index (window table, slots, stable sums)
   uint32_t slotCacheG = kNone, slotCacheEpoch = 0;  // sLen / sBlk hold group slotCacheG at that epoch
-  uint32_t glEpoch = ~0u;    // the epoch whose group pass filled L->glEnt / glVis
   FMT_DEV void invalidate() {
     corrValid = false;
     epoch++;
@@ -513,6 +508,14 @@ class HugeDocT {
         S.winIdx[id] = w;
       }
     }
+    if (w < kWinLds) {  // (uniform LDS stores)
+      L->wRecL[4 * w] = static_cast<uint32_t>(ins);
+      L->wRecL[4 * w + 1] = static_cast<uint32_t>(rm);
+      L->wRecL[4 * w + 2] = len;
+      L->wRecL[4 * w + 3] = (meta & kWMetaMask) | (grp << kWGroupShift);
+      L->wMaskL[2 * w] = mlo;
+      L->wMaskL[2 * w + 1] = mhi;
+    }
     return w;
   }
   FMT_DEV void winRemove(uint32_t w) {  // swap-remove
@@ -538,6 +541,14 @@ class HugeDocT {
           S.winIdx[g] = w;
         }
       }
+      if (w < kWinLds) {
+        L->wRecL[4 * w] = a;
+        L->wRecL[4 * w + 1] = b;
+        L->wRecL[4 * w + 2] = c;
+        L->wRecL[4 * w + 3] = d;
+        L->wMaskL[2 * w] = ml;
+        L->wMaskL[2 * w + 1] = mh;
+      }
     }
     st1(S.winIdx + id, kNone);
     nWin = last;
@@ -545,10 +556,32 @@ class HugeDocT {
 
   FMT_DEV uint32_t* wWord(uint32_t w, int f) const { return S.wRec + static_cast<size_t>(w) * 4 + f; }
   FMT_DEV uint32_t* wWord3(uint32_t w) const { return wWord(w, 3); }
-  // an entry's leaf moved to block b (of group g)
+  // (uniform w) record word f of entry w, in HBM and in the LDS mirror
+  FMT_DEV void wSet(uint32_t w, int f, uint32_t v) {
+    st1(wWord(w, f), v);
+    if (w < kWinLds) L->wRecL[4 * w + f] = v;
+  }
+  FMT_DEV void wSetMask(uint32_t w, uint32_t lo, uint32_t hi) {
+    st1(S.wMask + 2 * w, lo);
+    st1(S.wMask + 2 * w + 1, hi);
+    if (w < kWinLds) {
+      L->wMaskL[2 * w] = lo;
+      L->wMaskL[2 * w + 1] = hi;
+    }
+  }
+  // (lane-level) an entry's leaf moved to block b (of group g)
   FMT_DEV void wRetag(uint32_t w, uint32_t b, uint32_t g) {
     S.wBlk[w] = b;
-    *wWord3(w) = (rd(wWord3(w)) & kWMetaMask) | (g << kWGroupShift);
+    const uint32_t v = (rd(wWord3(w)) & kWMetaMask) | (g << kWGroupShift);
+    *wWord3(w) = v;
+    if (w < kWinLds) L->wRecL[4 * w + 3] = v;
+  }
+  // (lane-level) the record and mask of entry w for a pass: from the LDS mirror when it holds it
+  FMT_DEV u32x4 wRecOf(uint32_t w) const {
+    return w < kWinLds ? *reinterpret_cast<const u32x4*>(&L->wRecL[4 * w]) : ld4(S.wRec + static_cast<size_t>(w) * 4);
+  }
+  FMT_DEV u32x2 wMaskOf(uint32_t w) const {
+    return w < kWinLds ? *reinterpret_cast<const u32x2*>(&L->wMaskL[2 * w]) : ld2(S.wMask + static_cast<size_t>(w) * 2);
   }
 
   // ------------------------------------------------------------------ stable sums
@@ -768,7 +801,11 @@ class HugeDocT {
         const uint32_t w = base + l;
         if (w < nWin) {
           const uint32_t m = rd(wWord3(w));
-          if ((m >> kWGroupShift) == g) *wWord3(w) = (m & kWMetaMask) | (rd(S.bGroup + (rd(S.wBlk + w))) << kWGroupShift);
+          if ((m >> kWGroupShift) == g) {
+            const uint32_t v = (m & kWMetaMask) | (rd(S.bGroup + (rd(S.wBlk + w))) << kWGroupShift);
+            *wWord3(w) = v;
+            if (w < kWinLds) L->wRecL[4 * w + 3] = v;
+          }
         }
       }
     }
@@ -786,15 +823,13 @@ class HugeDocT {
   // command in LDS and the kWaves waves (one per SIMD) each take every kWaves-th step of it, between
   // workgroup barriers. (Host emulation: wave 0 runs every share itself.)
   static constexpr int kWaves = 4;
-  static constexpr int kListPerWave = kWinList / kWaves;
   enum : int { kCmdExit = 0, kCmdGroups = 1, kCmdSlots = 2 };
   struct PassCmd {
     int op, r, c;
     uint32_t g, nWin;
-    int useList;  // slot pass: take group g's entries from the group pass' LDS lists
   };
-  FMT_DEV void runPass(int op, int r, int c, uint32_t g, int useList = 0) {
-    const PassCmd cmd{op, r, c, g, nWin, useList};
+  FMT_DEV void runPass(int op, int r, int c, uint32_t g) {
+    const PassCmd cmd{op, r, c, g, nWin};
     FOR_LANES(l) {
       if (l == 0) {
         L->cmd[0] = op;
@@ -802,7 +837,6 @@ class HugeDocT {
         L->cmd[2] = c;
         L->cmd[3] = static_cast<int32_t>(g);
         L->cmd[4] = static_cast<int32_t>(nWin);
-        L->cmd[5] = useList;
       }
     }
     waveSync();
@@ -828,7 +862,7 @@ class HugeDocT {
     for (;;) {
       groupBarrier();
       const PassCmd cmd{uni(L->cmd[0]), uni(L->cmd[1]), uni(L->cmd[2]), static_cast<uint32_t>(uni(L->cmd[3])),
-                        static_cast<uint32_t>(uni(L->cmd[4])), uni(L->cmd[5])};
+                        static_cast<uint32_t>(uni(L->cmd[4]))};
       if (cmd.op == kCmdExit) return;
       if (cmd.op == kCmdSlots) {
         slotShare(cmd, wave);
@@ -888,56 +922,17 @@ class HugeDocT {
     waveSync();
   }
 
-  // This wave's steps of one pass over the window table, 2 x 64 records per step with every load of
-  // a step in flight together (one 16-byte load per record): for each entry of positive view length,
-  // add it to gCorr[group] (kCmdGroups); or (kCmdSlots) for each such entry of group cmd.g, add it
-  // to sLen[slot of its block] — those entries are first listed in this wave's part of the LDS list,
-  // then their blocks' slots are loaded for the whole list at once.
+  // This wave's steps of one pass over the window table (entries below kWinLds from the LDS mirror,
+  // the rest from HBM, kPassU x 64 per step with every load of a step in flight together): each entry
+  // of positive view length is added to gCorr[group] and its chunk's cCorr (kCmdGroups), or, if it
+  // belongs to group cmd.g, to sLen[slot of its block] (kCmdSlots: few entries per group, so their
+  // block / slot lookups are per lane).
   static constexpr int kPassU = 2;
-  static constexpr int kGlPerWave = kGlCap / kWaves;
   FMT_DEV void windowShare(const PassCmd& cmd, int wave) {
     const int r = cmd.r, c = cmd.c;
     const uint32_t n = cmd.nWin;
     const bool bySlot = cmd.op == kCmdSlots;
     const uint32_t only = bySlot ? cmd.g : kNone;
-    uint32_t* lEnt = L->wlEnt + wave * kListPerWave;
-    int32_t* lVis = L->wlVis + wave * kListPerWave;
-    int nList = 0;
-    if (bySlot && cmd.useList) {  // group g's visible entries, from this wave's group-pass list
-      const int gn = L->glN[wave];
-      const uint32_t* gE = L->glEnt + wave * kGlPerWave;
-      const int32_t* gV = L->glVis + wave * kGlPerWave;
-      for (int base = 0; base < gn; base += 64) {
-        Lane<bool> hit;
-        Lane<uint32_t> ent;
-        FOR_LANES(l) {
-          const uint32_t e = base + l < gn ? gE[base + l] : kNone;
-          LANE(ent) = e;
-          LANE(hit) = base + l < gn && (e >> kGlEntBits) == only;
-        }
-        const uint64_t m = ballot(hit);
-        if (!m) continue;
-        if (nList + 64 > kListPerWave) {
-          flushSlotList(lEnt, lVis, nList);
-          nList = 0;
-        }
-        FOR_LANES(l) {
-          if ((m >> l) & 1ull) {
-            const int at = nList + __builtin_popcountll(m & ((1ull << l) - 1));
-            lEnt[at] = LANE(ent) & ((1u << kGlEntBits) - 1);
-            lVis[at] = gV[base + l];
-          }
-        }
-        nList += __builtin_popcountll(m);
-      }
-      if (nList) flushSlotList(lEnt, lVis, nList);
-      waveSync();
-      return;
-    }
-    int glN = 0;  // group pass: this wave's list of visible entries
-    uint32_t* gE = L->glEnt + wave * kGlPerWave;
-    int32_t* gV = L->glVis + wave * kGlPerWave;
-    // 64-record pieces dealt round-robin to the waves: piece (u * kWaves + wave) of each step
     for (uint32_t base = 0; base < n; base += kWaves * 64 * kPassU) {
       Lane<u32x4> rec[kPassU];
       Lane<u32x2> msk[kPassU];
@@ -950,93 +945,33 @@ class HugeDocT {
           FOR_LANES(l) {
             const uint32_t w = p0 + l;
             if (w < n) {
-              LANE(rec[u]) = ld4(S.wRec + static_cast<size_t>(w) * 4);
-              LANE(msk[u]) = ld2(S.wMask + static_cast<size_t>(w) * 2);
+              LANE(rec[u]) = wRecOf(w);
+              LANE(msk[u]) = wMaskOf(w);
             }
           }
         }
       }
-      Lane<uint32_t> vis[kPassU];
       FOR_LANES(l) {
 #pragma unroll
         for (int u = 0; u < kPassU; u++) {
           const uint32_t w = base + static_cast<uint32_t>(u * kWaves + wave) * 64 + l;
-          uint32_t v = 0;
           if (u < nu && w < n) {
             const u32x4 x = LANE(rec[u]);
             const uint32_t grp = x[3] >> kWGroupShift;
             if (only == kNone || grp == only) {
               const u32x2 mk = LANE(msk[u]);
-              v = c < 64 ? static_cast<uint32_t>(winVis(static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, mk[0], mk[1], r, c))
+              const uint32_t v =
+                  c < 64 ? static_cast<uint32_t>(winVis(static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), x[2], x[3] & kWMetaMask, mk[0], mk[1], r, c))
                          : static_cast<uint32_t>(visAny(x[2], static_cast<int32_t>(x[0]), static_cast<int32_t>(x[1]), 0u, 0u,
                                                         mClient(x[3]), r, c, rd(S.wLeaf + w)));
               if (v && !bySlot) {
                 atomicAddLds(&L->gCorr[grp], static_cast<int>(v));
                 atomicAddLds(&L->cCorr[L->gPos[grp] >> 5], static_cast<int>(v));
               }
+              if (v && bySlot) atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + w))], static_cast<int>(v));
             }
           }
-          LANE(vis[u]) = v;
         }
-      }
-      if (!bySlot && glN >= 0) {
-#pragma unroll
-        for (int u = 0; u < kPassU; u++) {
-          Lane<bool> hit;
-          FOR_LANES(l) { LANE(hit) = u < nu && LANE(vis[u]) != 0; }
-          const uint64_t m = ballot(hit);
-          if (!m || glN < 0) continue;
-          if (glN + __builtin_popcountll(m) > kGlPerWave || base + static_cast<uint32_t>((u * kWaves + wave + 1) * 64) > (1u << kGlEntBits)) {
-            glN = -1;
-            continue;
-          }
-          FOR_LANES(l) {
-            if ((m >> l) & 1ull) {
-              const int at = glN + __builtin_popcountll(m & ((1ull << l) - 1));
-              const uint32_t w = base + static_cast<uint32_t>(u * kWaves + wave) * 64 + l;
-              gE[at] = w | ((LANE(rec[u])[3] >> kWGroupShift) << kGlEntBits);
-              gV[at] = static_cast<int32_t>(LANE(vis[u]));
-            }
-          }
-          glN += __builtin_popcountll(m);
-        }
-      }
-      if (bySlot) {
-#pragma unroll
-        for (int u = 0; u < kPassU; u++) {
-          Lane<bool> hit;
-          FOR_LANES(l) { LANE(hit) = u < nu && LANE(vis[u]) != 0; }
-          const uint64_t m = ballot(hit);
-          if (!m) continue;
-          if (nList + 64 > kListPerWave) {
-            flushSlotList(lEnt, lVis, nList);
-            nList = 0;
-          }
-          FOR_LANES(l) {
-            if ((m >> l) & 1ull) {
-              const int at = nList + __builtin_popcountll(m & ((1ull << l) - 1));
-              lEnt[at] = base + static_cast<uint32_t>(u * kWaves + wave) * 64 + l;
-              lVis[at] = static_cast<int32_t>(LANE(vis[u]));
-            }
-          }
-          nList += __builtin_popcountll(m);
-        }
-      }
-    }
-    if (bySlot && nList) flushSlotList(lEnt, lVis, nList);
-    if (!bySlot) {
-      FOR_LANES(l) {
-        if (l == 0) L->glN[wave] = glN;
-      }
-    }
-    waveSync();
-  }
-  // sLen[slot of the block of listed entry i] += its view length, for the n listed entries.
-  FMT_DEV void flushSlotList(const uint32_t* lEnt, const int32_t* lVis, int n) {
-    waveSync();
-    for (int base = 0; base < n; base += 64) {
-      FOR_LANES(l) {
-        if (base + l < n) atomicAddLds(&L->sLen[rd(S.bSlot + rd(S.wBlk + lEnt[base + l]))], lVis[base + l]);
       }
     }
     waveSync();
@@ -1054,7 +989,6 @@ class HugeDocT {
     prof[19] += static_cast<uint64_t>(nGroups);
     runPass(kCmdGroups, r, c, kNone);
     corrValid = true;
-    glEpoch = epoch;
   }
 
   // View length of the groups at positions [k0, k0 + 64) (lane l: position k0 + l; 0 past the end).
@@ -1088,9 +1022,7 @@ class HugeDocT {
     slotCacheEpoch = epoch;
     ProfScope ps_(prof[2]);
     prof[17]++;
-    bool lists = corrValid && glEpoch == epoch;
-    for (int w = 0; w < kWaves && lists; w++) lists = uni(L->glN[w]) >= 0;
-    runPass(kCmdSlots, r, c, g, lists ? 1 : 0);
+    runPass(kCmdSlots, r, c, g);
   }
 
   // ------------------------------------------------------------------ the hierarchical search
@@ -1854,7 +1786,7 @@ class HugeDocT {
     const uint32_t w = readlane(R.wi, k);
     uint32_t wy = kNone;
     if (w != kNone) {
-      st1(wWord(w, 2), x.len);
+      wSet(w, 2, x.len);
       wy = winAdd(y.id, y.ins, y.rm, y.len, ldu(wWord3(w)) & kWMetaMask, R.g, b, y.mlo, y.mhi);
     } else {
       st1(S.winIdx + y.id, kNone);
@@ -2233,13 +2165,12 @@ class HugeDocT {
     }
     if (!was) {
       const uint32_t m3 = ldu(wWord3(w));
-      st1(wWord(w, 1), static_cast<uint32_t>(x.rm));
-      st1(wWord3(w), (m3 & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(c) << 8));
+      wSet(w, 1, static_cast<uint32_t>(x.rm));
+      wSet(w, 3, (m3 & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(c) << 8));
     } else {
-      st1(wWord3(w), ldu(wWord3(w)) | (1u << 16));  // a later remover
+      wSet(w, 3, ldu(wWord3(w)) | (1u << 16));  // a later remover
     }
-    st1(S.wMask + 2 * w, x.mlo);
-    st1(S.wMask + 2 * w + 1, x.mhi);
+    wSetMask(w, x.mlo, x.mhi);
     return 0;
   }
 
@@ -2501,10 +2432,9 @@ class HugeDocT {
     if (S.hiMask != nullptr) hiPut(id, hlo, hhi);
     const uint32_t w = ldu(S.winIdx + id);  // (a new leaf: always a window entry)
     const bool more = __builtin_popcount(mlo) + __builtin_popcount(mhi) + __builtin_popcount(hlo) + __builtin_popcount(hhi) > 1;
-    st1(wWord(w, 1), static_cast<uint32_t>(minSeqOther));
-    st1(wWord3(w), (ldu(wWord3(w)) & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(firstCl) << 8) | (more ? 1u << 16 : 0u));
-    st1(S.wMask + 2 * w, mlo);
-    st1(S.wMask + 2 * w + 1, mhi);
+    wSet(w, 1, static_cast<uint32_t>(minSeqOther));
+    wSet(w, 3, (ldu(wWord3(w)) & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(firstCl) << 8) | (more ? 1u << 16 : 0u));
+    wSetMask(w, mlo, mhi);
     invalidate();
   }
 
@@ -2906,8 +2836,9 @@ class HugeDocT {
         const uint32_t i = base + l;
         bool g = false;
         if (i < nWin) {
-          const int32_t rm = static_cast<int32_t>(rd(wWord(i, 1)));
-          g = static_cast<int32_t>(rd(wWord(i, 0))) <= minSeq && (rm == kNotRemoved || rm <= minSeq);
+          const u32x4 x = wRecOf(i);
+          const int32_t rm = static_cast<int32_t>(x[1]);
+          g = static_cast<int32_t>(x[0]) <= minSeq && (rm == kNotRemoved || rm <= minSeq);
         }
         LANE(q) = g;
       }
@@ -4295,6 +4226,11 @@ class HugeDocT {
       if (sum != L->gStable[g]) return bad("group stable", sum, L->gStable[g]);
     }
     if (nw != static_cast<long>(nWin)) bad("window count", nw, nWin);
+    for (uint32_t w = 0; w < nWin && w < kWinLds; w++) {  // the LDS mirror of the window table
+      for (int f = 0; f < 4; f++)
+        if (L->wRecL[4 * w + f] != S.wRec[4 * w + f]) return bad("window mirror", w, f);
+      if (L->wMaskL[2 * w] != S.wMask[2 * w] || L->wMaskL[2 * w + 1] != S.wMask[2 * w + 1]) return bad("window mirror mask", w, 0);
+    }
     for (int c = 0; c * 32 < nGroups; c++) {  // the group scan's chunk sums and positions
       long sum = 0;
       for (int k = c * 32; k < c * 32 + 32 && k < nGroups; k++) {

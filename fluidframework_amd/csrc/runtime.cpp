@@ -240,7 +240,8 @@ struct fmt_ctx {
   bool mtHasAdjust = false;
   uint32_t mtNAdjusts = 0, mtNValues = 0, mtNNumSorted = 0;
   DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
-  // f4 (local-client records): every document replays in the large tier's Loc variant; its pending
+  // f4 (local-client records): every document replays in the compact tier's Loc variant first, the ones
+  // it cannot hold in the large tier's (round 6; mergetree_local.hip); its pending
   // groups, group records, PropertiesManager records, regenerated ops / text and normalization
   // scratch live in per-document slabs (mt_engine.h LocalTables)
   bool mtLocal = false;
@@ -251,7 +252,6 @@ struct fmt_ctx {
   DevBuf<uint16_t> mtLocRegenText;
   DevBuf<fmt_mt::LocalTables> mtLocTab;
   std::vector<uint64_t> mtLocRegenOffsHost, mtLocRegenTextOffsHost;
-  std::vector<uint32_t> mtLocIds;            // [n, 0, 1, .. n-1]: the large tier's document list
   uint32_t mtNSmall = 0;
   DevBuf<fmt_huge::HugeState> hugeStates;
   DevBuf<fmt_huge::HugeInputs> hugeInputs;
@@ -1289,9 +1289,6 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     FMT_HIP(c, cp(c->mtLocTab.p, &T, sizeof T));
     c->mtLocRegenOffsHost.assign(offs.begin() + 3 * (n + 1ull), offs.begin() + 4 * (n + 1ull));
     c->mtLocRegenTextOffsHost.assign(offs.begin() + 4 * (n + 1ull), offs.begin() + 5 * (n + 1ull));
-    c->mtLocIds.resize(n + 1ull);
-    c->mtLocIds[0] = n;
-    for (uint32_t d = 0; d < n; d++) c->mtLocIds[d + 1] = d;
     FMT_HIP(c, hipStreamSynchronize(c->stream));  // (offs / T are about to go out of scope)
   }
   FMT_HIP(c, stagedCopy(c, c->mtOps.p, b->ops, b->n_ops * sizeof(fmt_mt_op), true));
@@ -1498,19 +1495,12 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipMemsetAsync(c->mtSched.p, 0, 4 * sizeof(uint32_t), c->stream));
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   const bool hasHuge = c->mtHugeLoaded > 0, list = c->mtUseList;
-  if (c->mtLocal) {  // every document goes straight to the large tier's Loc variant
-    std::vector<uint32_t> ids;
-    if (list) {
-      ids.push_back(c->mtNSmall);
-      std::vector<uint8_t> skip(c->mtDocs, 0);
-      for (uint32_t d : c->mtRefused) skip[d] = 1;
-      for (uint32_t d = 0; d < c->mtDocs; d++)
-        if (!skip[d]) ids.push_back(d);
-      ids[0] = static_cast<uint32_t>(ids.size() - 1);
-    }
-    const std::vector<uint32_t>& L = list ? ids : c->mtLocIds;
-    FMT_HIP(c, hipMemcpyAsync(c->mtEsc.p, L.data(), L.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    FMT_HIP(c, hipStreamSynchronize(c->stream));  // (ids goes out of scope)
+  if (c->mtLocal) {
+    // f4 (round 6): the compact tier's local variant over every document; the ones it cannot hold
+    // are listed in mtEsc and replay from their first op in the large tier's local variant below
+    if (!list || c->mtNSmall > 0)
+      FMT_HIP(c, fmt_kernels::launchMergeTreeLocal(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
+                                                   c->mtEsc.p, c->numCUs, c->stream, c->mtSched.p));
   } else if (!list || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,

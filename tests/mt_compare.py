@@ -34,7 +34,7 @@ def emu_lib():
         L.emu_mt_capacity.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.emu_mt_numbers.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
         L.emu_mt_legacy_props.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
-        L.emu_mt_replay_local.argtypes = [ctypes.c_void_p] * 5
+        L.emu_mt_replay_local.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int]
         L.emu_mt_regen.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                    ctypes.POINTER(ctypes.c_uint32)]
         L.emu_mt_replay_large_ckpt.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p]
@@ -259,9 +259,11 @@ def emu_replay(batch, cap_catchup=0, force_ob=False, large=False, cap_rm=0):
     return out
 
 
-def emu_replay_local(batch):
-    """f4 batches (local submissions / acks / rollbacks / reconnects) through the large tier's local
-    variant under host emulation: (headers, leaves, chars, props) at large-tier strides."""
+def emu_replay_local(batch, large_only=False):
+    """f4 batches (local submissions / acks / rollbacks / reconnects) under host emulation, as the
+    runtime runs them: the compact tier's local variant, then the large tier's for the documents it
+    could not hold (large_only: every document in the large tier). (headers, leaves, chars, props) at
+    large-tier strides."""
     cl, cc, cp = emu_caps(True)
     n = batch.n_docs
     hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
@@ -269,7 +271,7 @@ def emu_replay_local(batch):
     chars = np.zeros(n * cc, dtype="<u2")
     props = np.zeros(n * cp, dtype=PROPSET_DTYPE)
     b, keep = batch_struct(batch)
-    emu_lib().emu_mt_replay_local(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props))
+    emu_lib().emu_mt_replay_local(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props), 1 if large_only else 0)
     del keep
     return hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp)
 

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from fluidframework_amd.streams import MT_F_LOCAL, MT_F_ROLLBACK, MT_OBLITERATE, MergeTreeStreamBuilder
-from local_farm import fixture_local_batch, local_farm_batch
+from local_farm import LocalFarm, fixture_local_batch, local_farm_batch
 from mt_compare import compare_doc, emu_caps, emu_regen, emu_replay_local, visible_text
 
 FMT_E_USAGE, FMT_E_DATA, FMT_E_UNSUPPORTED = -1, -2, -5
@@ -116,6 +116,26 @@ def test_emulated_engine_local_farms_with_new_client_ids_match_oracle(orc, farms
     assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen) > 20
 
 
+@pytest.fixture(scope="module")
+def farms_long():
+    """Local farms whose documents outgrow the compact tier's 2048 UTF-16 units mid-stream (initial
+    text 1990 units) or start past it (2100): the runtime replays them again, from their first op,
+    in the large tier (round 6: local batches start in the compact tier)."""
+    b = MergeTreeStreamBuilder()
+    farms = [LocalFarm(s, builder=b, n_clients=4, initial=("ab" * 1100)[:n], min_length=2300).run(300)
+             for s, n in ((40, 1990), (41, 1990), (42, 2100))]
+    return b.finish(), farms
+
+
+def test_emulated_local_farms_past_the_compact_tier_match_oracle(orc, farms_long):
+    batch, farms = farms_long
+    rc, oh, ol, oc, op = _oracle(orc, batch)
+    assert rc == 0 and int(oh["n_chars"].max()) > 2048
+    n_regen = _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen)
+    # the same with every document in the large tier (round 5's path)
+    assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch, large_only=True), emu_regen) == n_regen
+
+
 def test_emulated_engine_local_usage_and_data_errors(orc):
     """An out-of-range local op is FMT_E_USAGE (client.ts:797-810); an ack or rollback that does not
     match the pending queue is FMT_E_DATA (mergeTree.ts:1336, 2392). Oracle and engine agree."""
@@ -188,6 +208,12 @@ def test_gpu_local_farms_match_oracle_and_regenerate_the_same_ops(orc, engine, f
 def test_gpu_local_farms_with_new_client_ids_match_oracle(orc, engine, farms_new_ids):
     batch, _ = farms_new_ids
     assert _check_engine_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen) > 20
+
+
+@pytest.mark.gpu
+def test_gpu_local_farms_past_the_compact_tier_match_oracle(orc, engine, farms_long):
+    batch, _ = farms_long
+    _check_engine_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen)
 
 
 @pytest.mark.gpu

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--docs", type=int, default=20000)
     ap.add_argument("--unique", type=int, default=2000)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--workload", choices=["mt", "map", "t3", "ob"], default="mt")
+    ap.add_argument("--workload", choices=["mt", "map", "t3", "ob", "local"], default="mt")
     ap.add_argument("--segments", type=int, default=2_000_000, help="t3: segments of the loaded document")
     ap.add_argument("--t3-ops", type=int, default=200_000, help="t3: ops replayed")
     ap.add_argument("variants", nargs="*")
@@ -34,6 +34,11 @@ def main():
         return bench_map(a, paths)
     if a.workload == "t3":
         batch = workloads.t3_stream(a.segments, a.t3_ops)
+    elif a.workload == "local":  # f4 writer views of the reference farms cycled to --docs (bench.py local)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from local_farm import fixture_local_docs
+
+        batch = workloads.replicate_batches([f[1] for f in fixture_local_docs()], a.docs)
     elif a.workload == "ob":  # the reference's obliterate farms cycled to --docs documents (bench.py ob)
         sys.path.insert(0, os.path.join(REPO, "tests"))
         from golden_data import replay_fixtures

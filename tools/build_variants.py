@@ -44,7 +44,7 @@ def build(name, edits, rev=None, flags=()):
     objs = [os.path.join(REPO, "build", "fmt", f) for f in ("map_lww.o", "map_sparse.o", "map_pending.o", "summary.o", "digest.o", "transfer.o")]
     only = [x for x in os.environ.get("VARIANT_ONLY", "").split(",") if x]
     procs = []
-    for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip", "hugedoc.hip"]:
+    for f in ["runtime.cpp", "mergetree.hip", "mergetree_compact.hip", "mergetree_large.hip", "mergetree_local.hip", "hugedoc.hip"]:
         if only and f not in only:
             objs.append(os.path.join(REPO, "build", "fmt", f.split(".")[0] + ".o"))
             continue
@@ -58,6 +58,9 @@ def build(name, edits, rev=None, flags=()):
             raise SystemExit(f"{name}: compile failed")
     out = os.path.join(root, "libfmt.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o", out] + objs, check=True)
+    if os.environ.get("NO_REPORT"):  # (skip the compact tier's resource report: minutes per variant)
+        print(name, "| built")
+        return out
     r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-Wno-unused-variable", *flags,
                         "-c", "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage",
                         os.path.join(csrc, "mergetree_compact.hip")], capture_output=True, text=True)
@@ -204,6 +207,9 @@ SHIFT4 = [("mt_engine.h", """    const int count = nChars - from;
 VISBF = [("mt_engine.h", '  FMT_DEV void visLengths(int refSeq, int client, Lane<VR>& vis, int nr) const {\n    FOR_ROWS(r, 0, nr) {\n      FOR_LANES(l) {\n        const uint32_t w0 = LANE(W[0])[r];\n        const int32_t ins = static_cast<int32_t>(LANE(W[1])[r]);\n        const int32_t rm = static_cast<int32_t>(LANE(W[2])[r]);\n        const int32_t ic = fClient(LANE(W[4])[r]);\n        const bool present = (ins <= refSeq || ic == client) && !(rm <= refSeq || removedBy(l, r, client));\n        LANE(vis)[r] = present ? fLen(w0) : 0u;\n      }\n    }\n  }', '  FMT_DEV void visLengths(int refSeq, int client, Lane<VR>& vis, int nr) const {\n    // branch-free: every term is a 0/1 word in a VGPR (shifts of differences, which cannot overflow:\n    // stamps are in [0, 2^31)), so no lane masks are combined in scalar registers\n    const bool hiW = C::kWords > 5 && client >= 32;\n    const uint32_t sh = client < 0 ? 0u : static_cast<uint32_t>(client & 31);\n    const uint32_t cm = client < 0 ? 0u : 1u;\n    const uint32_t cl8 = static_cast<uint32_t>(client) & 0xFFu;\n    FOR_ROWS(r, 0, nr) {\n      FOR_LANES(l) {\n        const uint32_t w0 = LANE(W[0])[r];\n        const uint32_t ins = LANE(W[1])[r];\n        const uint32_t rm = LANE(W[2])[r];\n        const uint32_t insLE = ((static_cast<uint32_t>(refSeq) - ins) >> 31) ^ 1u;\n        const uint32_t rmLE = ((static_cast<uint32_t>(refSeq) - rm) >> 31) ^ 1u;\n        const uint32_t icEq = (((LANE(W[4])[r] >> 24) ^ cl8) - 1u) >> 31;\n        const uint32_t rmb = ((hiW ? LANE(W[C::kWords > 5 ? 5 : 3])[r] : LANE(W[3])[r]) >> sh) & cm;\n        const uint32_t present = (insLE | icEq) & ((rmLE | rmb) ^ 1u);\n        LANE(vis)[r] = fLen(w0) * present;\n      }\n    }\n  }')]
 
 VARIANTS = {
+    # f4 local batches' compact tier at 2 waves/SIMD (256 VGPRs: no spills) instead of 3
+    "loc2": [("mergetree_local.hip", "kMtWavesLocal, 3, false, true>", "kMtWavesLocal, 2, false, true>")],
+    "loc3": [],
     # huge tier without its per-phase shader-clock reads (ProfScope's s_memtime pairs)
     "t3noclk": [("huge_engine.h", "    return __builtin_amdgcn_s_memtime();", "    return 0;")],
     "visbf": VISBF,
