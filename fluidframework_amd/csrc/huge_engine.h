@@ -1108,6 +1108,19 @@ class HugeDocT {
 
   // Search one leaf block whose view start is bst.
   FMT_DEV bool leafInBlock(uint32_t b, int bst, int p, int r, int c, Hit& h) {
+    // the block's 8 leaf slots are loaded beside its count (one memory round trip, not two: slots past
+    // the count hold stale fields and are masked after)
+    Lane<uint32_t> fl, fi, fr, flo, fhi, fm, fid;
+    FOR_LANES(l) {
+      const size_t i = static_cast<size_t>(b) * 8 + (l & 7);
+      LANE(fl) = rd(S.lLen + i);
+      LANE(fi) = static_cast<uint32_t>(rd(S.lIns + i));
+      LANE(fr) = static_cast<uint32_t>(rd(S.lRm + i));
+      LANE(flo) = rd(S.lMlo + i);
+      LANE(fhi) = rd(S.lMhi + i);
+      LANE(fm) = rd(S.lMeta + i);
+      LANE(fid) = c < 64 ? 0u : rd(S.lId + i);
+    }
     const uint32_t cnt = ldu(S.bCount + b);
     Lane<uint32_t> vis;
     Lane<bool> skipped;
@@ -1115,10 +1128,9 @@ class HugeDocT {
       uint32_t v = 0;
       bool sk = false;
       if (l < static_cast<int>(cnt)) {
-        const size_t i = static_cast<size_t>(b) * 8 + l;
-        const int32_t rm = rd(S.lRm + i);
-        v = static_cast<uint32_t>(visAny(rd(S.lLen + i), rd(S.lIns + i), rm, rd(S.lMlo + i), rd(S.lMhi + i), mClient(rd(S.lMeta + i)), r, c,
-                                         c < 64 ? 0u : rd(S.lId + i)));
+        const int32_t rm = static_cast<int32_t>(LANE(fr));
+        v = static_cast<uint32_t>(visAny(LANE(fl), static_cast<int32_t>(LANE(fi)), rm, LANE(flo), LANE(fhi), mClient(LANE(fm)), r, c,
+                                         LANE(fid)));
         sk = rm <= minSeq && !(b == lastBlk && l == static_cast<int>(cnt) - 1);
       }
       LANE(vis) = v;
@@ -2005,12 +2017,14 @@ class HugeDocT {
   FMT_DEV Lane<uint32_t> blockVis(uint32_t b, uint32_t cnt, int r, int c) const {
     Lane<uint32_t> vis;
     FOR_LANES(l) {
+      // (all 8 slots loaded, masked by the count after; a stale slot's id indexes nothing: visAny reads
+      // the hiMask side table by id only for the block's own leaves)
+      const size_t i = li(b, l & 7);
+      const uint32_t len = rd(S.lLen + i), mlo = rd(S.lMlo + i), mhi = rd(S.lMhi + i), meta = rd(S.lMeta + i);
+      const int32_t ins = rd(S.lIns + i), rm = rd(S.lRm + i);
+      const uint32_t id = c < 64 ? 0u : rd(S.lId + i);
       uint32_t v = 0;
-      if (l < static_cast<int>(cnt)) {
-        const size_t i = li(b, l);
-        v = static_cast<uint32_t>(visAny(rd(S.lLen + i), rd(S.lIns + i), rd(S.lRm + i), rd(S.lMlo + i), rd(S.lMhi + i),
-                                         mClient(rd(S.lMeta + i)), r, c, c < 64 ? 0u : rd(S.lId + i)));
-      }
+      if (l < static_cast<int>(cnt)) v = static_cast<uint32_t>(visAny(len, ins, rm, mlo, mhi, mClient(meta), r, c, id));
       LANE(vis) = v;
     }
     return vis;
@@ -2091,7 +2105,7 @@ class HugeDocT {
       bool scour = ldi(S.bScour + b) == 1;
       Lane<uint32_t> f[8], wi, vis;
       FOR_LANES(l) {
-        const size_t i = li(b, l < static_cast<int>(cnt) ? l : 0);
+        const size_t i = li(b, l & 7);  // (all 8 slots: the loads do not wait for the count)
         LANE(f[0]) = rd(S.lLen + i);
         LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
         LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
@@ -2102,7 +2116,8 @@ class HugeDocT {
         LANE(f[7]) = rd(S.lMeta + i);
       }
       FOR_LANES(l) {
-        LANE(wi) = rd(S.winIdx + LANE(f[5]));
+        // (slots past the count hold stale fields, possibly never-written memory: no index from them)
+        LANE(wi) = l < static_cast<int>(cnt) ? rd(S.winIdx + LANE(f[5])) : kNone;
         LANE(vis) = l < static_cast<int>(cnt)
                         ? static_cast<uint32_t>(visAny(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
                                                        LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c, LANE(f[5])))
@@ -2480,7 +2495,7 @@ class HugeDocT {
       bool scour = ldi(S.bScour + b) == 1;
       Lane<uint32_t> f[8], wi, vis;
       FOR_LANES(l) {
-        const size_t i = li(b, l < static_cast<int>(cnt) ? l : 0);
+        const size_t i = li(b, l & 7);  // (all 8 slots: the loads do not wait for the count)
         LANE(f[0]) = rd(S.lLen + i);
         LANE(f[1]) = static_cast<uint32_t>(rd(S.lIns + i));
         LANE(f[2]) = static_cast<uint32_t>(rd(S.lRm + i));
@@ -2491,7 +2506,8 @@ class HugeDocT {
         LANE(f[7]) = rd(S.lMeta + i);
       }
       FOR_LANES(l) {
-        LANE(wi) = rd(S.winIdx + LANE(f[5]));
+        // (slots past the count hold stale fields, possibly never-written memory: no index from them)
+        LANE(wi) = l < static_cast<int>(cnt) ? rd(S.winIdx + LANE(f[5])) : kNone;
         LANE(vis) = l < static_cast<int>(cnt)
                         ? static_cast<uint32_t>(visAny(LANE(f[0]), static_cast<int32_t>(LANE(f[1])), static_cast<int32_t>(LANE(f[2])),
                                                        LANE(f[3]), LANE(f[4]), mClient(LANE(f[7])), r, c, LANE(f[5])))
@@ -3182,9 +3198,8 @@ class HugeDocT {
 
   // scourNode over leaf block b: drops leaves removed at/below minSeq, appends acked same-props
   // appendable leaves onto the previous kept leaf. Returns the new leaf count.
-  FMT_DEV int scourLeaves(uint32_t b) {
+  FMT_DEV int scourLeaves(uint32_t b, int cnt) {
     ProfScope ps_(prof[8]);
-    const int cnt = static_cast<int>(ldu(S.bCount + b));
     if (cnt == 0) return 0;
     Lane<uint32_t> blk, f[8], lastCh;
     Lane<int> cntL;
@@ -3481,13 +3496,15 @@ class HugeDocT {
       const HeapEnt e = heapGet();
       const uint32_t b = ldu(S.leafBlk + e.leafId);
       if (b == kNone) continue;  // unlinked or appended
-      if (ldi(S.bScour + b) == 0) continue;
+      // (the block's flag, count and parent in one memory round trip; the scour changes no parent)
+      const int32_t flag = ldi(S.bScour + b);
       const int oldCount = static_cast<int>(ldu(S.bCount + b));
-      const int kept = scourLeaves(b);
+      const uint32_t parent = ldu(S.bParent + b);
+      if (flag == 0) continue;
+      const int kept = scourLeaves(b, oldCount);
       if (status != FMT_OK) return;
       st1(S.bScour + b, 0);
       if (kept >= oldCount) continue;
-      const uint32_t parent = ldu(S.bParent + b);
       if (kept >= kMaxNodes / 2 || parent == kNone) continue;
       packLeafParent(parent);
       if (status != FMT_OK) return;

@@ -241,7 +241,7 @@ struct fmt_ctx {
   uint32_t mtNAdjusts = 0, mtNValues = 0, mtNNumSorted = 0;
   DevBuf<uint32_t> mtSmallList;              // the other documents (small tier), when huge ones exist
   // f4 (local-client records): every document replays in the compact tier's Loc variant first, the ones
-  // it cannot hold in the large tier's (round 6; mergetree_local.hip); its pending
+  // it cannot hold in the small tier's, then the large tier's (round 6; mergetree_local.hip); its pending
   // groups, group records, PropertiesManager records, regenerated ops / text and normalization
   // scratch live in per-document slabs (mt_engine.h LocalTables)
   bool mtLocal = false;
@@ -1496,11 +1496,12 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   const bool hasHuge = c->mtHugeLoaded > 0, list = c->mtUseList;
   if (c->mtLocal) {
-    // f4 (round 6): the compact tier's local variant over every document; the ones it cannot hold
-    // are listed in mtEsc and replay from their first op in the large tier's local variant below
+    // f4 (round 6): the compact tier's local variant over every document, the ones it cannot hold
+    // in the small tier's, and those listed in mtEsc replay from their first op in the large tier's
+    // local variant below (mergetree_local.hip)
     if (!list || c->mtNSmall > 0)
       FMT_HIP(c, fmt_kernels::launchMergeTreeLocal(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
-                                                   c->mtEsc.p, c->numCUs, c->stream, c->mtSched.p));
+                                                   c->mtEsc.p, c->mtEsc2.p, c->numCUs, c->stream, c->mtSched.p));
   } else if (!list || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,

@@ -125,25 +125,28 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
     for (uint64_t k = sd.first_seg; k < sd.first_seg + N; k++) docChars += b->snapshot_segs[k].len & ~FMT_MT_SEG_MARKER;
   uint64_t textCap = b->text_len + std::max<uint64_t>((loaded ? 256 : 1024) * nOps + 65536, 4 * docChars + 131072);
   if (const char* e = std::getenv("FMT_EMU_TEXTCAP")) textCap = std::strtoull(e, nullptr, 10);
-  std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6);
-  std::vector<int32_t> i32(static_cast<size_t>(S.blockCap) * 8 * 2);
+  // (device buffers start with arbitrary contents: hipMalloc, no memset, runtime.cpp setupHugeDoc; so the
+  // emulated ones start poisoned, and a read of a never-written slot shows as a wild value here too)
+  constexpr uint32_t kPoison = 0xCDCDCDCDu;
+  std::vector<uint32_t> u32(static_cast<size_t>(S.blockCap) * 8 * 6, kPoison);
+  std::vector<int32_t> i32(static_cast<size_t>(S.blockCap) * 8 * 2, static_cast<int32_t>(kPoison));
   size_t o = 0, oi = 0;
   auto U = [&](size_t n) { uint32_t* p = u32.data() + o; o += n; return p; };
   auto I = [&](size_t n) { int32_t* p = i32.data() + oi; oi += n; return p; };
   const size_t nl = static_cast<size_t>(S.blockCap) * 8;
   S.lLen = U(nl); S.lMlo = U(nl); S.lMhi = U(nl); S.lId = U(nl); S.lText = U(nl); S.lMeta = U(nl);
   S.lIns = I(nl); S.lRm = I(nl);
-  std::vector<uint32_t> blk(static_cast<size_t>(S.blockCap) * 14);
-  std::vector<int32_t> bsc(S.blockCap);
+  std::vector<uint32_t> blk(static_cast<size_t>(S.blockCap) * 14, kPoison);
+  std::vector<int32_t> bsc(S.blockCap, static_cast<int32_t>(kPoison));
   S.bCount = blk.data(); S.bParent = S.bCount + S.blockCap; S.bLeaf = S.bParent + S.blockCap;
   S.bChild = S.bLeaf + S.blockCap; S.bGroup = S.bChild + 8ull * S.blockCap; S.bSlot = S.bGroup + S.blockCap;
   S.freeBlk = S.bSlot + S.blockCap; S.bScour = bsc.data();
-  std::vector<uint32_t> gsb(static_cast<size_t>(kGroupCap) * kSlotCap);
-  std::vector<int32_t> gss(static_cast<size_t>(kGroupCap) * kSlotCap);
+  std::vector<uint32_t> gsb(static_cast<size_t>(kGroupCap) * kSlotCap, kPoison);
+  std::vector<int32_t> gss(static_cast<size_t>(kGroupCap) * kSlotCap, static_cast<int32_t>(kPoison));
   S.gSlotBlk = gsb.data(); S.gSlotStable = gss.data();
   std::vector<uint32_t> ids(2ull * S.idCap, kNone);
   S.leafBlk = ids.data(); S.winIdx = ids.data() + S.idCap;
-  std::vector<uint32_t> wu(8ull * S.winCap);
+  std::vector<uint32_t> wu(8ull * S.winCap, kPoison);
   S.wRec = wu.data(); S.wMask = S.wRec + 4ull * S.winCap; S.wBlk = S.wMask + 2ull * S.winCap; S.wLeaf = S.wBlk + S.winCap;
   // the merge area only: the batch text is read in place (runtime.cpp setupHugeDoc)
   std::vector<uint16_t> text(textCap - b->text_len);

@@ -371,9 +371,10 @@ int emu_mt_replay_large_ckpt(const fmt_mt_batch* b, fmt_mt_doc_result* headers, 
 uint32_t emu_huge_ckpt_words() { return fmt_ckpt::kWords; }
 
 // f4 batches (local submissions, acks, rollbacks, reconnects), as the runtime runs them (round 6): the
-// compact tier's Loc variant over every document, then the large tier's Loc variant over the documents
-// the compact tier could not hold, from their first op (results at large strides). largeOnly: every
-// document in the large tier (round 5's path).
+// small tier's Loc variant over every document, then the large tier's over the documents it could not
+// hold, from their first op (results at large strides). Mode 3: the compact tier's Loc variant first,
+// the small tier's over what it could not hold, then the large tier's (FMT_LOCAL_PATH 2). largeOnly: every
+// document in the large tier (round 5's path); 2: the compact tier alone (its statuses, diagnostics).
 int emu_mt_replay_local(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                         fmt_mt_propset* props, int largeOnly) {
   g_nums.clear();
@@ -382,16 +383,22 @@ int emu_mt_replay_local(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_m
   using G = fmt_mt::LargeTier;
   using K = fmt_mt::CompactTier;
   using S = fmt_mt::SmallTier;
-  if (largeOnly) return replayAll<false, G, false, false, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0);
+  if (largeOnly == 1) return replayAll<false, G, false, false, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0);
   using DS = fmt_mt::Doc<false, S>;
   using DL = fmt_mt::Doc<false, G, false, false, true>;
   const size_t n = b->n_docs;
   std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
   std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
   std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
-  replayAll<false, K, false, false, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr, false,
-                                          DS::kCapLeaves, S::kCapChars);
-  for (size_t d = 0; d < n; d++) {  // documents done in the compact tier: results to the large strides
+  if (largeOnly == 2 || largeOnly == 3)
+    replayAll<false, K, false, false, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr, false,
+                                            DS::kCapLeaves, S::kCapChars);
+  if (largeOnly == 2) return FMT_OK;  // (diagnostics: the compact tier's statuses alone)
+  // the small tier's local variant over the documents the compact tier could not hold (from op 0);
+  // mode 0 (the runtime's default, mergetree_local.hip FMT_LOCAL_PATH 1) starts here with every document
+  replayAll<false, S, false, false, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr,
+                                          largeOnly == 3);
+  for (size_t d = 0; d < n; d++) {  // documents done below the large tier: results to the large strides
     const fmt_mt_doc_result& h = headers[d];
     if (h.status == FMT_E_CAPACITY) continue;
     std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));

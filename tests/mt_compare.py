@@ -259,10 +259,11 @@ def emu_replay(batch, cap_catchup=0, force_ob=False, large=False, cap_rm=0):
     return out
 
 
-def emu_replay_local(batch, large_only=False):
+def emu_replay_local(batch, large_only=False, compact_first=False):
     """f4 batches (local submissions / acks / rollbacks / reconnects) under host emulation, as the
-    runtime runs them: the compact tier's local variant, then the large tier's for the documents it
-    could not hold (large_only: every document in the large tier). (headers, leaves, chars, props) at
+    runtime runs them: the small tier's local variant, then the large tier's for the documents it
+    could not hold (large_only: every document in the large tier; compact_first: the compact tier's
+    local variant first, then the small and the large tier's). (headers, leaves, chars, props) at
     large-tier strides."""
     cl, cc, cp = emu_caps(True)
     n = batch.n_docs
@@ -271,7 +272,7 @@ def emu_replay_local(batch, large_only=False):
     chars = np.zeros(n * cc, dtype="<u2")
     props = np.zeros(n * cp, dtype=PROPSET_DTYPE)
     b, keep = batch_struct(batch)
-    emu_lib().emu_mt_replay_local(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props), 1 if large_only else 0)
+    emu_lib().emu_mt_replay_local(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props), 1 if large_only else 3 if compact_first else 0)
     del keep
     return hdr, leaves.reshape(n, cl), chars.reshape(n, cc), props.reshape(n, cp)
 

@@ -127,17 +127,22 @@ def test_t3_million_segments(orc, engine):
 
 
 def test_t3_ten_million_segments_digest(orc, engine):
-    """T3 at its full document size (BASELINE config 5: 10M segments, 63 writers, refSeq lag up to
-    4096) over a 2e5-op slice: the whole document's state digest (every leaf field, props by value,
-    text, header; fmt_mt_state_digest) equals the oracle's digest of its own replay. The full 1e7-op
+    """T3 at its full document size (BASELINE config 5: 10M segments loaded from a legacy summary's
+    header + body, as bench.py loads it; 63 writers, refSeq lag up to 4096) over a 2e5-op slice: the
+    whole document's state digest (every leaf field, props by value, text, header;
+    fmt_mt_state_digest) equals the oracle's digest of its own replay. The full 1e7-op
     run is bench.py --workload t3 --t3-check."""
-    batch = workloads.t3_stream(10_000_000, 200_000, n_clients=63, max_lag=4096, seed=14)
+    batch = workloads.as_legacy_load(workloads.t3_stream(10_000_000, 200_000, n_clients=63, max_lag=4096, seed=14))
     engine.mt_load(batch)
     engine.mt_run()
     hdrs = engine.mt_headers()
     assert int(hdrs[0]["status"]) == 0, (int(hdrs[0]["status"]), int(hdrs[0]["fail_seq"]))
     got = engine.mt_digests()
-    rc, exp, st, _ = orc.mt_replay_digest(batch, 0, 1, threads=1)
+    orc.set_index(True)  # (the oracle's remote-length index: the T3 CPU baseline's own configuration)
+    try:
+        rc, exp, st, _ = orc.mt_replay_digest(batch, 0, 1, threads=1)
+    finally:
+        orc.set_index(False)
     assert rc == 0 and int(st[0]) == 0
     assert int(got[0]) == int(exp[0])
 

@@ -119,21 +119,29 @@ def test_emulated_engine_local_farms_with_new_client_ids_match_oracle(orc, farms
 @pytest.fixture(scope="module")
 def farms_long():
     """Local farms whose documents outgrow the compact tier's 2048 UTF-16 units mid-stream (initial
-    text 1990 units) or start past it (2100): the runtime replays them again, from their first op,
-    in the large tier (round 6: local batches start in the compact tier)."""
+    text 1990 units) or start past it (2100), and past the small tier's 6144 (6200): the runtime
+    replays them again, from their first op, in the small and then the large tier (round 6: local
+    batches start in the compact tier)."""
     b = MergeTreeStreamBuilder()
-    farms = [LocalFarm(s, builder=b, n_clients=4, initial=("ab" * 1100)[:n], min_length=2300).run(300)
-             for s, n in ((40, 1990), (41, 1990), (42, 2100))]
+    farms = [LocalFarm(s, builder=b, n_clients=4, initial=("ab" * 3200)[:n], min_length=n + 300).run(300)
+             for s, n in ((40, 1990), (41, 1990), (42, 2100), (43, 6200))]
     return b.finish(), farms
 
 
 def test_emulated_local_farms_past_the_compact_tier_match_oracle(orc, farms_long):
     batch, farms = farms_long
     rc, oh, ol, oc, op = _oracle(orc, batch)
-    assert rc == 0 and int(oh["n_chars"].max()) > 2048
+    assert rc == 0 and int(oh["n_chars"].max()) > 6144
     n_regen = _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen)
-    # the same with every document in the large tier (round 5's path)
+    # the same with every document in the large tier (round 5's path), and with the compact tier first
     assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch, large_only=True), emu_regen) == n_regen
+    assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch, compact_first=True), emu_regen) == n_regen
+
+
+def test_emulated_compact_local_variant_matches_oracle(orc, fixtures_local, farms_local):
+    """The compact tier's local variant (FMT_LOCAL_PATH 2) on the fixture views and farms."""
+    for batch in (fixtures_local[0], farms_local[0]):
+        _check_engine_vs_oracle(orc, batch, emu_replay_local(batch, compact_first=True), emu_regen)
 
 
 def test_emulated_engine_local_usage_and_data_errors(orc):

@@ -208,8 +208,10 @@ VISBF = [("mt_engine.h", '  FMT_DEV void visLengths(int refSeq, int client, Lane
 
 VARIANTS = {
     # f4 local batches' compact tier at 2 waves/SIMD (256 VGPRs: no spills) instead of 3
-    "loc2": [("mergetree_local.hip", "kMtWavesLocal, 3, false, true>", "kMtWavesLocal, 2, false, true>")],
-    "loc3": [],
+    "locCL": [("mergetree_local.hip", "#define FMT_LOCAL_PATH 2", "#define FMT_LOCAL_PATH 0")],
+    "locSL": [("mergetree_local.hip", "#define FMT_LOCAL_PATH 2", "#define FMT_LOCAL_PATH 1")],
+    "locCSL": [],
+    "t3lat": [],  # (working tree: huge tier with its block count / flags loaded beside the leaf fields)
     # huge tier without its per-phase shader-clock reads (ProfScope's s_memtime pairs)
     "t3noclk": [("huge_engine.h", "    return __builtin_amdgcn_s_memtime();", "    return 0;")],
     "visbf": VISBF,
