@@ -3963,6 +3963,40 @@ class HugeDocT {
       }
       waveSync();
     }
+    // relative positions: every Marker leaf still in the tree joins the marker list (in document
+    // order; the engine's pick among markers with one id does not depend on the list's order, and a
+    // marker zamboni unlinked before the checkpoint is one the list skips anyway)
+    if (S.mkIds != nullptr) {
+      for (uint32_t base = 0; base < nLeafBlk * 8 && status == FMT_OK; base += 64) {
+        Lane<bool> mk;
+        Lane<uint32_t> ids;
+        FOR_LANES(l) {
+          const uint32_t x = base + l, o = x >> 3, k = x & 7;
+          bool v = false;
+          uint32_t id = 0;
+          if (o < nLeafBlk) {
+            const uint32_t b = rd(S.gSlotBlk + slotOf(o));
+            if (k < rd(S.bCount + b)) {
+              const size_t i = li(b, static_cast<int>(k));
+              v = mMarker(rd(S.lMeta + i));
+              id = rd(S.lId + i);
+            }
+          }
+          LANE(mk) = v;
+          LANE(ids) = id;
+        }
+        for (uint64_t m = ballot(mk); m != 0 && status == FMT_OK; m &= m - 1) markerAdd(readlane(ids, ctz64(m)));
+      }
+    }
+    // annotate-adjust: the PropertiesManager records stay in the document's slab (same layout), and
+    // its computed numbers with their count in theirs
+    if constexpr (Adj) {
+      pmN = static_cast<int>(ldu(ck + K::kPmN));
+      if (pmN < 0 || pmN > pmCap()) {
+        fail(FMT_E_DATA);
+        return 0;
+      }
+    }
     invalidate();
     return next;
   }

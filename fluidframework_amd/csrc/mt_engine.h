@@ -397,8 +397,11 @@ class Doc {
   // large → huge (round 5; huge_ckpt.h): a plain document the large tier is about to outgrow stops
   // before the op, writes its result slabs and the checkpoint record, and the huge tier replays on
   // from that op with the same tree.
-  static constexpr bool kSavesHuge = C::kHbmChars && !Rm && !Loc && !Adj;
+  // (annotate-adjust documents too: their PropertiesManager records and computed numbers stay in
+  // the batch's HBM slabs, which the huge tier reads with the same layout; the record carries pmN)
+  static constexpr bool kSavesHuge = C::kHbmChars && !Rm && !Loc;
   uint32_t* hugeCkpt = nullptr;
+  bool savingHuge = false;  // (writeOutputs: no legacy getAtSeq view, it would mark the records)
   FMT_DEV void saveHuge(uint64_t next) {
     namespace K = fmt_ckpt;
     uint32_t* ck = hugeCkpt;
@@ -419,6 +422,7 @@ class Doc {
         ck[K::kObCounts] = Ob ? static_cast<uint32_t>(obSeqN) | (static_cast<uint32_t>(obStartN) << 16) : 0u;
         ck[K::kObUsedLo] = Ob ? static_cast<uint32_t>(obUsed) : 0u;
         ck[K::kObUsedHi] = Ob ? static_cast<uint32_t>(obUsed >> 32) : 0u;
+        ck[K::kPmN] = Adj ? static_cast<uint32_t>(pmN) : 0u;
       }
     }
     static_assert(!kSavesHuge || (kCapLeaves == K::kLeaves && kMaxBlocks == K::kBlocks && kHeapCap + 1 == K::kHeap &&
@@ -3887,7 +3891,7 @@ class Doc {
       }
     }
     if constexpr (Adj) {
-      if (out.legacyProps != nullptr && status == FMT_OK) {
+      if (out.legacyProps != nullptr && status == FMT_OK && !savingHuge) {
         pmLegacyProps(out.legacyProps);
         if (status != FMT_OK) {
           // the legacy getAtSeq view did not fit the prop-set table. Small tier: escalate (the large
@@ -4003,6 +4007,7 @@ class Doc {
     profT = __builtin_amdgcn_s_memtime();
 #endif
     in = inputs;
+    savingHuge = false;
     cuOut = out.catchup;
     cuCap = out.catchup ? out.catchupCap : 0u;
     cuN = 0;
@@ -4043,6 +4048,7 @@ class Doc {
     if constexpr (kSavesHuge) {
       if (status == kCkptEscalate) {  // the huge tier resumes: the result slabs, then the record
         status = FMT_OK;
+        savingHuge = true;
         writeOutputs(out);
         saveHuge(ckptNext);
         FOR_LANES(l) {

@@ -80,6 +80,12 @@ const fmt_mt_leaf* g_ckLeaves = nullptr;
 const uint16_t* g_ckChars = nullptr;
 const fmt_mt_propset* g_ckProps = nullptr;
 uint64_t g_resumedAt = 0;
+// emu_huge_resume_adj: the large tier's PropertiesManager records and computed numbers of the document
+// (in the runtime the huge tier reads the same HBM slabs; the two emulators keep their own)
+const uint32_t* g_seedPm = nullptr;
+uint32_t g_seedPmRecs = 0;
+const double* g_seedNums = nullptr;
+uint32_t g_seedNumN = 0;
 }  // namespace
 
 extern "C" {
@@ -176,6 +182,11 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));
   const fmt_mt::AdjustTables* adj = prepareNumbers(b);
+  if (adj != nullptr && g_seedPm != nullptr) {
+    std::copy(g_seedPm, g_seedPm + 4ull * std::min(g_seedPmRecs, kEmuPmCap), g_pm.begin());
+    std::copy(g_seedNums, g_seedNums + std::min(g_seedNumN, kEmuNumCap), g_nums.begin());
+    g_numCount[d] = std::min(g_seedNumN, kEmuNumCap);
+  }
   auto replay = [&](auto* doc) {  // (HugeDocT<true> for annotate-adjust batches, as the runtime launches)
   doc->S = S;
   doc->L = lds.get();
@@ -265,6 +276,35 @@ int emu_huge_resume(const fmt_mt_batch* b, uint32_t d, const uint32_t* ck, const
   g_ckLeaves = nullptr;
   g_ckChars = nullptr;
   g_ckProps = nullptr;
+  if (resumedAt) *resumedAt = g_resumedAt;
+  return st;
+}
+
+// emu_huge_resume for an annotate-adjust batch: pm (pmRecs records) and nums (nNumsIn) are the
+// document's slabs as the large tier left them (emu_mt_adj_slab); legacy / nums / *nNums as
+// emu_huge_replay_adj.
+int emu_huge_resume_adj(const fmt_mt_batch* b, uint32_t d, const uint32_t* ck, const fmt_mt_leaf* ckLeaves,
+                        const uint16_t* ckChars, const fmt_mt_propset* ckProps, const uint32_t* pm, uint32_t pmRecs,
+                        const double* numsIn, uint32_t nNumsIn, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves,
+                        uint64_t capLeaves, uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, uint16_t* legacy,
+                        double* nums, uint32_t capNums, uint32_t* nNums, uint64_t* resumedAt) {
+  g_ck = ck;
+  g_ckLeaves = ckLeaves;
+  g_ckChars = ckChars;
+  g_ckProps = ckProps;
+  g_seedPm = pm;
+  g_seedPmRecs = pmRecs;
+  g_seedNums = numsIn;
+  g_seedNumN = nNumsIn;
+  g_resumedAt = 0;
+  const int st = emu_huge_replay_adj(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0, nullptr, 0, legacy,
+                                     nums, capNums, nNums);
+  g_ck = nullptr;
+  g_ckLeaves = nullptr;
+  g_ckChars = nullptr;
+  g_ckProps = nullptr;
+  g_seedPm = nullptr;
+  g_seedNums = nullptr;
   if (resumedAt) *resumedAt = g_resumedAt;
   return st;
 }

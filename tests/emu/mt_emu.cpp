@@ -355,10 +355,21 @@ int emu_mt_replay(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf
 // The large tier over every document from its first op, each document it is about to outgrow
 // stopping with its large → huge checkpoint (hugeCk: fmt_ckpt::kWords words per document; header
 // status fmt_ckpt::kStatusHuge) for emu_huge_resume (results at large strides).
+// Annotate-adjust batches run the large tier's Adj variant (Doc<true, G, false, true>, as the runtime):
+// the legacy views of the documents it finishes via emu_mt_legacy_props, and each document's
+// PropertiesManager records and computed numbers, which the huge tier resumes with, via emu_mt_adj_slab.
 int emu_mt_replay_large_ckpt(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                              fmt_mt_propset* props, fmt_mt_catchup_range* catchup, uint32_t capCatchup, uint32_t* hugeCk) {
   g_nums.clear();
   g_legacyStride = 0;
+  if (b->adjusts != nullptr) {
+    prepareNumbers(b);
+    using DL = fmt_mt::Doc<true, fmt_mt::LargeTier, false, true>;
+    g_legacyStride = DL::kCapLeaves;
+    g_legacy.assign(static_cast<size_t>(b->n_docs) * g_legacyStride, 0xFFFFu);
+    return replayAll<true, fmt_mt::LargeTier, false, true>(b, headers, leaves, chars, props, catchup, capCatchup, nullptr, 0,
+                                                           nullptr, false, 0, 0, nullptr, nullptr, g_legacy.data(), hugeCk);
+  }
   bool ob = false;
   for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE || b->ops[i].type == FMT_MT_OBLITERATE_SIDED;
   using G = fmt_mt::LargeTier;
@@ -425,6 +436,17 @@ int emu_mt_legacy_props(uint32_t d, uint16_t* out, uint32_t cap) {
   if (g_legacyStride == 0 || (d + 1) * g_legacyStride > g_legacy.size()) return 0;
   for (uint32_t k = 0; k < cap && k < g_legacyStride; k++) out[k] = g_legacy[d * g_legacyStride + k];
   return static_cast<int>(g_legacyStride);
+}
+
+// Document d's annotate-adjust slabs after the last emu_mt_replay_large_ckpt: its PropertiesManager
+// records (capRecs x 4 words from the slab's start) and computed numbers (<= capNums, *nNums = count).
+int emu_mt_adj_slab(uint32_t d, uint32_t* pm, uint32_t capRecs, double* nums, uint32_t capNums, uint32_t* nNums) {
+  if (g_nums.empty() || d >= g_numCount.size()) return -1;
+  for (size_t k = 0; k < 4ull * capRecs && k < 4ull * kEmuPmCap; k++) pm[k] = g_pm[static_cast<size_t>(d) * kEmuPmCap * 4 + k];
+  const uint32_t n = g_numCount[d];
+  for (uint32_t k = 0; k < n && k < capNums; k++) nums[k] = g_nums[static_cast<size_t>(d) * kEmuNumCap + k];
+  *nNums = n;
+  return 0;
 }
 
 // Document d's computed numbers after the last emu_mt_replay: returns their count, copies <= cap.

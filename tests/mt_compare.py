@@ -39,6 +39,8 @@ def emu_lib():
                                    ctypes.POINTER(ctypes.c_uint32)]
         L.emu_mt_replay_large_ckpt.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p]
         L.emu_huge_ckpt_words.restype = ctypes.c_uint32
+        L.emu_mt_adj_slab.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_uint32)]
         _emu = L
     return _emu
 
@@ -71,6 +73,11 @@ def huge_emu_lib(tiny_groups=False):
         L.emu_huge_resume.argtypes = ([ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 6 +
                                       [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)])
+        L.emu_huge_resume_adj.argtypes = ([ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 5 +
+                                          [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)])
         _huge[tiny_groups] = L
     return _huge[tiny_groups]
 
@@ -161,7 +168,9 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
     """The runtime's large → huge path under host emulation: the large tier over every document from
     its first op, each document it is about to outgrow stopping at its checkpoint (huge_ckpt.h), then
     the huge tier resuming it from there. Returns per document (header, leaves, chars, props[, catch-up
-    ranges]) and the op index each resumed at (0: the large tier finished it)."""
+    ranges][, legacy prop sets per leaf, computed numbers: annotate-adjust batches]) and the op index
+    each resumed at (0: the large tier finished it)."""
+    adjust = batch.adjusts is not None
     cl, cc, cp = emu_caps(True)
     n = batch.n_docs
     hdr = np.zeros(n, dtype=DOC_RESULT_DTYPE)
@@ -183,6 +192,9 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
                    props[d * cp: d * cp + int(h["n_props"])])
             if cap_catchup:
                 res = res + (cu[d * cap_catchup: d * cap_catchup + int(h["n_catchup"])],)
+            if adjust:
+                lg = emu_legacy_props(d)
+                res = res + (lg[: int(h["n_leaves"])] if lg is not None else None, emu_numbers(d))
             out.append(res)
             resumed.append(0)
             continue
@@ -198,13 +210,30 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
         if cap_catchup:
             cud[:cap_catchup] = cu[d * cap_catchup: (d + 1) * cap_catchup]
         at = ctypes.c_uint64(0)
-        huge_emu_lib(tiny_groups).emu_huge_resume(
-            ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
-            _p(h1), _p(lv), hcl, _p(ch), hcc, _p(pr), _p(cud) if cap_catchup else None, cap_catchup, ctypes.byref(at))
+        if adjust:
+            assert not cap_catchup
+            pm_recs = int(ck[d * words + 15])  # (fmt_ckpt::kPmN)
+            pm = np.zeros(4 * max(pm_recs, 1), dtype=np.uint32)
+            nums_in = np.zeros(4096, dtype=np.float64)
+            n_in = ctypes.c_uint32(0)
+            assert L.emu_mt_adj_slab(d, _p(pm), pm_recs, _p(nums_in), len(nums_in), ctypes.byref(n_in)) == 0
+            legacy = np.zeros(hcl, dtype="<u2")
+            nums = np.zeros(1 << 16, dtype=np.float64)
+            nn = ctypes.c_uint32(0)
+            huge_emu_lib(tiny_groups).emu_huge_resume_adj(
+                ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
+                _p(pm), pm_recs, _p(nums_in), n_in.value, _p(h1), _p(lv), hcl, _p(ch), hcc, _p(pr), _p(legacy),
+                _p(nums), len(nums), ctypes.byref(nn), ctypes.byref(at))
+        else:
+            huge_emu_lib(tiny_groups).emu_huge_resume(
+                ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
+                _p(h1), _p(lv), hcl, _p(ch), hcc, _p(pr), _p(cud) if cap_catchup else None, cap_catchup, ctypes.byref(at))
         h = h1[0]
         res = (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
         if cap_catchup:
             res = res + (cud[: int(h["n_catchup"])],)
+        if adjust:
+            res = res + (legacy[: int(h["n_leaves"])], nums[: nn.value])
         out.append(res)
         resumed.append(int(at.value))
     del keep
