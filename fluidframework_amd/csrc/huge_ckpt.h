@@ -1,9 +1,9 @@
 // huge_ckpt.h — the large → huge tier checkpoint record (mt_engine.h Doc::saveHuge writes it,
 // huge_engine.h HugeDoc::loadFromLarge reads it).
 //
-// A document (no remove-order recording or local events; relative positions and annotate-adjust since
-// round 6: the marker list is rebuilt from the leaves, the PropertiesManager records stay in their HBM
-// slab and kPmN carries their count) that the large tier is about to outgrow — an op that could add more leaves than its 2048 rows,
+// A document (no local events; relative positions, annotate-adjust and remove-order recording since
+// round 6: the marker list is rebuilt from the leaves, the PropertiesManager records and remove-order
+// entries stay in their HBM slabs, kPmN / kRmN carry their counts) that the large tier is about to outgrow — an op that could add more leaves than its 2048 rows,
 // more text than 131071 units, take its last blocks or prop sets, or that names a writer past 63 —
 // stops before that op. The large tier then writes its result slabs as at the end of a replay
 // (leaves in document order with stamps, remove-client sets, char offsets, prop-set ids; its text;
@@ -27,7 +27,8 @@ constexpr int kObSlots = 64;   // fmt_mt::kObCap
 enum : int {
   kNextLo = 0, kNextHi = 1, kN = 2, kNChars = 3, kRoot = 4, kNFree = 5, kHeapN = 6, kNProps = 7,
   kCurSeq = 8, kMinSeq = 9, kNextId = 10, kCuN = 11, kObCounts = 12 /* obSeqN | obStartN << 16 */,
-  kObUsedLo = 13, kObUsedHi = 14, kPmN = 15 /* annotate-adjust: PropertiesManager records */, kHeadWords = 16
+  kObUsedLo = 13, kObUsedHi = 14, kPmN = 15 /* annotate-adjust: PropertiesManager records */,
+  kRmN = 16 /* remove-order entries (leaf ids) in the document's slab */, kHeadWords = 17
 };
 // sections
 constexpr int kLeafW4 = kHeadWords;             // [kLeaves] W4: leaf id | Marker << 23 | insert client << 24

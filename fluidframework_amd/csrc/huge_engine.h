@@ -82,8 +82,9 @@ FMT_DEV uint32_t mix32(uint32_t x) {  // (a 32-bit finalizer: prop-set hashes)
 // record's word 3 adds the entry's group << 17
 // NOT reliable after a large → huge checkpoint (loadFromLarge): the large tier keeps the remove-client
 // set, not which remover came first, so the lowest id stands in there. Nothing reads it today (the
-// passes use the set; SnapshotV1's removedClientIds come from the remove-order slab, which checkpointed
-// batches never carry); a future reader must carry the first remover through huge_ckpt.h first.
+// passes use the set; SnapshotV1's removedClientIds come from the op at the leaf's rm_seq and the
+// remove-order entries, which the checkpoint carries); a future reader must carry the first remover
+// through huge_ckpt.h first.
 FMT_DEV uint32_t wFirstRm(uint32_t m) { return (m >> 8) & 0xFFu; }
 constexpr uint32_t kWMetaMask = 0x1FFFFu;
 constexpr int kWGroupShift = 17;
@@ -3775,6 +3776,15 @@ class HugeDocT {
       p += cnt > FMT_MT_PROPS_MAX ? static_cast<int>((cnt + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1;
     }
     if (status != FMT_OK) return 0;
+    // (device memory starts arbitrary: the ids of leaves zamboni dropped before the checkpoint, which
+    // remove-order entries and PropertiesManager records may still name, read as no leaf)
+    FOR_LANES(l) {
+      for (uint32_t k = static_cast<uint32_t>(l); k < nextIdL; k += 64) {
+        S.leafBlk[k] = kNone;
+        S.winIdx[k] = kNone;
+      }
+    }
+    waveSync();
     minSeq = static_cast<int>(ldu(ck + K::kMinSeq));
     curSeq = static_cast<int>(ldu(ck + K::kCurSeq));
     // the text, into the merge area
@@ -3993,6 +4003,15 @@ class HugeDocT {
     if constexpr (Adj) {
       pmN = static_cast<int>(ldu(ck + K::kPmN));
       if (pmN < 0 || pmN > pmCap()) {
+        fail(FMT_E_DATA);
+        return 0;
+      }
+    }
+    // remove order: the large tier's entries stay in the document's slab with their leaf ids (ids are
+    // kept across the checkpoint; one of a leaf zamboni dropped before it is in no block: GONE at output)
+    if constexpr (Rm) {
+      rmN = ldu(ck + K::kRmN);
+      if (rmN > 0 && (in.rmOrder == nullptr || rmN > in.rmOrderCap)) {
         fail(FMT_E_DATA);
         return 0;
       }

@@ -397,11 +397,13 @@ class Doc {
   // large → huge (round 5; huge_ckpt.h): a plain document the large tier is about to outgrow stops
   // before the op, writes its result slabs and the checkpoint record, and the huge tier replays on
   // from that op with the same tree.
-  // (annotate-adjust documents too: their PropertiesManager records and computed numbers stay in
-  // the batch's HBM slabs, which the huge tier reads with the same layout; the record carries pmN)
-  static constexpr bool kSavesHuge = C::kHbmChars && !Rm && !Loc;
+  // (annotate-adjust and remove-order documents too: their PropertiesManager records, computed
+  // numbers and remove-order entries stay in the batch's HBM slabs, which the huge tier reads with the
+  // same layout; the record carries pmN and rmN, the entries keep their leaf ids)
+  static constexpr bool kSavesHuge = C::kHbmChars && !Loc;
   uint32_t* hugeCkpt = nullptr;
-  bool savingHuge = false;  // (writeOutputs: no legacy getAtSeq view, it would mark the records)
+  bool savingHuge = false;  // (writeOutputs: no legacy getAtSeq view, it would mark the records; no
+                            // remove-order index conversion)
   FMT_DEV void saveHuge(uint64_t next) {
     namespace K = fmt_ckpt;
     uint32_t* ck = hugeCkpt;
@@ -423,6 +425,7 @@ class Doc {
         ck[K::kObUsedLo] = Ob ? static_cast<uint32_t>(obUsed) : 0u;
         ck[K::kObUsedHi] = Ob ? static_cast<uint32_t>(obUsed >> 32) : 0u;
         ck[K::kPmN] = Adj ? static_cast<uint32_t>(pmN) : 0u;
+        ck[K::kRmN] = Rm ? rmN : 0u;
       }
     }
     static_assert(!kSavesHuge || (kCapLeaves == K::kLeaves && kMaxBlocks == K::kBlocks && kHeapCap + 1 == K::kHeap &&
@@ -3970,8 +3973,9 @@ class Doc {
         for (int t = l; t < nProps * kPW; t += 64) dst[t] = src[t];
       }
     }
-    // remove-order entries: leaf id -> final leaf index (FMT_MT_LEAF_GONE once zamboni dropped it)
-    for (uint32_t k = 0; Rm && k < rmN; k++) {
+    // remove-order entries: leaf id -> final leaf index (FMT_MT_LEAF_GONE once zamboni dropped it;
+    // at a stop for the huge tier they keep their ids, which it goes on with)
+    for (uint32_t k = 0; Rm && !savingHuge && k < rmN; k++) {
       const uint32_t id = uni(loadCoherent(&rmOut[k].leaf));
       const int j = findLeafById(id);
       FOR_LANES(l) {

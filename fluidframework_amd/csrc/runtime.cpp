@@ -1523,10 +1523,10 @@ int fmt_mt_run(fmt_ctx* c) {
     FMT_HIP(c, c->mtBigChars.reserve(static_cast<size_t>(nEsc) * big.chars));
     FMT_HIP(c, c->mtBigProps.reserve(static_cast<size_t>(nEsc) * big.props));
     if (c->mtHasAdjust) FMT_HIP(c, c->mtBigLegacy.reserve(static_cast<size_t>(nEsc) * big.leaves));
-    // plain and annotate-adjust batches: a document the large tier is about to outgrow leaves a
-    // checkpoint for the huge tier (huge_ckpt.h) instead of failing; without the slab it restarts
-    // there from its first op
-    const bool hugeCk = !c->mtHasRmOrder && !c->mtLocal &&
+    // every batch but a local one: a document the large tier is about to outgrow leaves a checkpoint
+    // for the huge tier (huge_ckpt.h) instead of failing; without the slab it restarts there from its
+    // first op
+    const bool hugeCk = !c->mtLocal &&
                         c->mtHugeCk.reserve(static_cast<size_t>(nEsc) * fmt_ckpt::kWords) == hipSuccess;
     if (!hugeCk) (void)hipGetLastError();
     fmt_kernels::MtDeviceOut bout{c->mtHdr.p, c->mtBigLeaves.p, c->mtBigChars.p, c->mtBigProps.p,

@@ -150,7 +150,7 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   std::vector<uint32_t> gsb(static_cast<size_t>(kGroupCap) * kSlotCap, kPoison);
   std::vector<int32_t> gss(static_cast<size_t>(kGroupCap) * kSlotCap, static_cast<int32_t>(kPoison));
   S.gSlotBlk = gsb.data(); S.gSlotStable = gss.data();
-  std::vector<uint32_t> ids(2ull * S.idCap, kNone);
+  std::vector<uint32_t> ids(2ull * S.idCap, kPoison);
   S.leafBlk = ids.data(); S.winIdx = ids.data() + S.idCap;
   std::vector<uint32_t> wu(8ull * S.winCap, kPoison);
   S.wRec = wu.data(); S.wMask = S.wRec + 4ull * S.winCap; S.wBlk = S.wMask + 2ull * S.winCap; S.wLeaf = S.wBlk + S.winCap;
@@ -272,6 +272,26 @@ int emu_huge_resume(const fmt_mt_batch* b, uint32_t d, const uint32_t* ck, const
   g_ckProps = ckProps;
   g_resumedAt = 0;
   const int st = emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, catchup, capCatchup, nullptr, 0);
+  g_ck = nullptr;
+  g_ckLeaves = nullptr;
+  g_ckChars = nullptr;
+  g_ckProps = nullptr;
+  if (resumedAt) *resumedAt = g_resumedAt;
+  return st;
+}
+
+// emu_huge_resume for a batch with remove-order recording: rmOrder[capRm] holds the document's entries
+// as the large tier left them (leaf ids; the count is in the record) and receives the final ones.
+int emu_huge_resume_rm(const fmt_mt_batch* b, uint32_t d, const uint32_t* ck, const fmt_mt_leaf* ckLeaves,
+                       const uint16_t* ckChars, const fmt_mt_propset* ckProps, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves,
+                       uint64_t capLeaves, uint16_t* chars, uint64_t capChars, fmt_mt_propset* props,
+                       fmt_mt_remove_order* rmOrder, uint32_t capRm, uint64_t* resumedAt) {
+  g_ck = ck;
+  g_ckLeaves = ckLeaves;
+  g_ckChars = ckChars;
+  g_ckProps = ckProps;
+  g_resumedAt = 0;
+  const int st = emu_huge_replay_rec(b, d, hdr, leaves, capLeaves, chars, capChars, props, nullptr, 0, rmOrder, capRm);
   g_ck = nullptr;
   g_ckLeaves = nullptr;
   g_ckChars = nullptr;

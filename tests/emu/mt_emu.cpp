@@ -379,6 +379,21 @@ int emu_mt_replay_large_ckpt(const fmt_mt_batch* b, fmt_mt_doc_result* headers, 
                                   nullptr, nullptr, nullptr, hugeCk);
 }
 
+// As emu_mt_replay_large_ckpt for a batch with remove-order recording (the large tier's Rm variant):
+// rmOrder[n_docs x capRm] receives the entries, which keep their leaf ids in a stopped document.
+int emu_mt_replay_large_ckpt_rm(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                                fmt_mt_propset* props, fmt_mt_remove_order* rmOrder, uint32_t capRm, uint32_t* hugeCk) {
+  g_nums.clear();
+  g_legacyStride = 0;
+  bool ob = false;
+  for (uint64_t i = 0; i < b->n_ops && !ob; i++) ob = b->ops[i].type == FMT_MT_OBLITERATE || b->ops[i].type == FMT_MT_OBLITERATE_SIDED;
+  using G = fmt_mt::LargeTier;
+  return ob ? replayAll<true, G, true>(b, headers, leaves, chars, props, nullptr, 0, rmOrder, capRm, nullptr, false, 0, 0,
+                                       nullptr, nullptr, nullptr, hugeCk)
+            : replayAll<false, G, true>(b, headers, leaves, chars, props, nullptr, 0, rmOrder, capRm, nullptr, false, 0, 0,
+                                        nullptr, nullptr, nullptr, hugeCk);
+}
+
 uint32_t emu_huge_ckpt_words() { return fmt_ckpt::kWords; }
 
 // f4 batches (local submissions, acks, rollbacks, reconnects), as the runtime runs them (round 6): the

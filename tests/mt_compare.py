@@ -39,6 +39,7 @@ def emu_lib():
                                    ctypes.POINTER(ctypes.c_uint32)]
         L.emu_mt_replay_large_ckpt.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p]
         L.emu_huge_ckpt_words.restype = ctypes.c_uint32
+        L.emu_mt_replay_large_ckpt_rm.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_void_p]
         L.emu_mt_adj_slab.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.POINTER(ctypes.c_uint32)]
         _emu = L
@@ -78,6 +79,9 @@ def huge_emu_lib(tiny_groups=False):
                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64)])
+        L.emu_huge_resume_rm.argtypes = ([ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 6 +
+                                         [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)])
         _huge[tiny_groups] = L
     return _huge[tiny_groups]
 
@@ -164,12 +168,12 @@ def emu_huge_replay_hi(batch, doc=0, tiny_groups=False, cap_props=65534):
     return h, leaves[:n], chars[: int(h["n_chars"])], props[: int(h["n_props"])], hi[:n]
 
 
-def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
+def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0, cap_rm=0):
     """The runtime's large → huge path under host emulation: the large tier over every document from
     its first op, each document it is about to outgrow stopping at its checkpoint (huge_ckpt.h), then
     the huge tier resuming it from there. Returns per document (header, leaves, chars, props[, catch-up
-    ranges][, legacy prop sets per leaf, computed numbers: annotate-adjust batches]) and the op index
-    each resumed at (0: the large tier finished it)."""
+    ranges][, remove-order entries: cap_rm > 0][, legacy prop sets per leaf, computed numbers:
+    annotate-adjust batches]) and the op index each resumed at (0: the large tier finished it)."""
     adjust = batch.adjusts is not None
     cl, cc, cp = emu_caps(True)
     n = batch.n_docs
@@ -181,8 +185,14 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
     L = emu_lib()
     ck = np.zeros(n * int(L.emu_huge_ckpt_words()), dtype=np.uint32)
     b, keep = batch_struct(batch)
-    L.emu_mt_replay_large_ckpt(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props),
-                               _p(cu) if cap_catchup else None, cap_catchup, _p(ck))
+    rm = np.zeros(max(n * cap_rm, 1), dtype=RM_ORDER_DTYPE)
+    if cap_rm:
+        assert not cap_catchup and not adjust
+        L.emu_mt_replay_large_ckpt_rm(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props), _p(rm), cap_rm,
+                                      _p(ck))
+    else:
+        L.emu_mt_replay_large_ckpt(ctypes.addressof(b), _p(hdr), _p(leaves), _p(chars), _p(props),
+                                   _p(cu) if cap_catchup else None, cap_catchup, _p(ck))
     words = int(L.emu_huge_ckpt_words())
     out, resumed = [], []
     for d in range(n):
@@ -192,6 +202,8 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
                    props[d * cp: d * cp + int(h["n_props"])])
             if cap_catchup:
                 res = res + (cu[d * cap_catchup: d * cap_catchup + int(h["n_catchup"])],)
+            if cap_rm:
+                res = res + (rm[d * cap_rm: d * cap_rm + int(h["n_rm_order"])],)
             if adjust:
                 lg = emu_legacy_props(d)
                 res = res + (lg[: int(h["n_leaves"])] if lg is not None else None, emu_numbers(d))
@@ -224,6 +236,11 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
                 ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
                 _p(pm), pm_recs, _p(nums_in), n_in.value, _p(h1), _p(lv), hcl, _p(ch), hcc, _p(pr), _p(legacy),
                 _p(nums), len(nums), ctypes.byref(nn), ctypes.byref(at))
+        elif cap_rm:
+            rmd = rm[d * cap_rm: (d + 1) * cap_rm].copy()
+            huge_emu_lib(tiny_groups).emu_huge_resume_rm(
+                ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
+                _p(h1), _p(lv), hcl, _p(ch), hcc, _p(pr), _p(rmd), cap_rm, ctypes.byref(at))
         else:
             huge_emu_lib(tiny_groups).emu_huge_resume(
                 ctypes.addressof(b), d, _p(ck[d * words:]), _p(leaves[d * cl:]), _p(chars[d * cc:]), _p(props[d * cp:]),
@@ -232,6 +249,8 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0):
         res = (h, lv[: int(h["n_leaves"])], ch[: int(h["n_chars"])], pr[: int(h["n_props"])])
         if cap_catchup:
             res = res + (cud[: int(h["n_catchup"])],)
+        if cap_rm:
+            res = res + (rmd[: int(h["n_rm_order"])],)
         if adjust:
             res = res + (legacy[: int(h["n_leaves"])], nums[: nn.value])
         out.append(res)

@@ -142,6 +142,72 @@ def test_relative_position_document_resumes_in_the_huge_tier_on_gpu(orc):
         eng.close()
 
 
+def _rm_growth():
+    """A growing document with remove-order recording (FMT_MT_F_RMORDER on every op) and overlapping
+    removes — after most removes a dedicated writer removes the same range from the same refSeq —
+    that crosses the large tier at op 4527 and ends 10 ops later, so removes from before the
+    checkpoint are still above the final minSeq and their later stamps are entries the large tier
+    recorded (without the carried count the emulated stamp lists lose them)."""
+    import random
+
+    from growth import growth_messages
+
+    from fluidframework_amd.streams import MergeTreeStreamBuilder, flag_remove_order
+    rnd = random.Random(112)
+    seqmap, out, last_dup = {0: 0}, [], 0
+    for m in growth_messages(n_ops=4700, seed=13):
+        s = len(out) + 1
+        seqmap[m["sequenceNumber"]] = s
+        ref, msn = seqmap[m["referenceSequenceNumber"]], seqmap[m["minimumSequenceNumber"]]
+        out.append(dict(m, sequenceNumber=s, referenceSequenceNumber=ref, minimumSequenceNumber=msn))
+        # (the same view and range: the visible length does not change, so later positions stand)
+        if m["contents"]["type"] == 1 and ref >= last_dup and rnd.random() < 0.7:
+            out.append(dict(m, clientId="wd", sequenceNumber=s + 1, referenceSequenceNumber=ref, minimumSequenceNumber=msn))
+            last_dup = s + 1
+    b = MergeTreeStreamBuilder()
+    d = b.begin_doc("", observer="observer")
+    for m in out[:4537]:
+        d.add_message(m)
+    batch = b.finish()
+    flag_remove_order(batch.ops, batch.doc_op_offsets)
+    return batch
+
+
+def test_emulated_checkpoint_with_remove_order(orc):
+    from test_huge_emulated import _oracle_doc, _removers_match
+
+    batch = _rm_growth()
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    got, resumed = emu_grow_replay(batch, cap_rm=1 << 16)
+    assert resumed[0] > 0
+    assert int(got[0][0]["status"]) == 0
+    assert compare_doc(exp, got[0][:4]) == []
+    assert _removers_match(orc, batch, got[0], got[0][4]) > 0
+
+
+@pytest.mark.gpu
+def test_remove_order_document_resumes_in_the_huge_tier_on_gpu(orc):
+    from test_huge_emulated import _oracle_doc, _removers_match
+
+    batch = _rm_growth()
+    rc, exp = _oracle_doc(orc, batch)
+    assert rc == 0
+    eng = native.Engine(0)
+    try:
+        eng.mt_load(batch)
+        eng.mt_run()
+        hdrs = eng.mt_headers()
+        assert int(hdrs[0]["status"]) == 0
+        lv, ch, pr = eng.mt_doc(0, hdrs[0])
+        assert compare_doc(exp, (hdrs[0], lv, ch, pr)) == []
+        assert eng.huge_profile(0)["resumed_at"] > 0
+        rm = eng.mt_remove_order(0, hdrs[0])
+        assert _removers_match(orc, batch, (hdrs[0], lv), rm) > 0
+    finally:
+        eng.close()
+
+
 def _adjust_growth():
     """A marker-rich document whose annotates adjust "weight", past the large tier — round 6:
     annotate-adjust batches checkpoint too (the PropertiesManager records and computed numbers stay in
