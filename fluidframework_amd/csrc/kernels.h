@@ -132,13 +132,14 @@ hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& o
                                 uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
                                 uint32_t* next, bool adjust, bool local = false);
 
-// f4 local-client batches (round 6): the compact tier's local variant over docList[0..count) (or
-// every document), the documents it cannot hold (listed in esc2) again in the small tier's, the ones
-// that one cannot hold listed in esc (esc[0] = count, then ids) for launchMergeTreeLarge(..., local =
+// f4 local-client batches (round 6): the small tier's local variant over docList[0..count) (or every
+// document; FMT_LOCAL_PATH selects a compact-tier pass first, documents it cannot hold listed in esc2),
+// the ones it cannot hold listed in esc (esc[0] = count, then ids) for launchMergeTreeLarge(..., local =
 // true). esc[0] and esc2[0] zeroed by the caller; sched: zeroed dealing counters (compact, small).
+// adjust: annotate-adjust batches, the small tier's Adj local variant.
 hipError_t launchMergeTreeLocal(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                 uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
-                                uint32_t* sched);
+                                uint32_t* sched, bool adjust = false);
 
 // Diagnostic: per-phase cycle totals of a FMT_PROFILE=1 build (all zero otherwise).
 int mergeTreeProfile(uint64_t* out, int n, bool reset);

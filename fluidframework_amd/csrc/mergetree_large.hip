@@ -12,6 +12,8 @@ hipError_t launchMergeTreeLarge(const MtDeviceBatch& batch, const MtDeviceOut& o
                                 uint32_t count, int numCUs, hipStream_t stream, bool obliterate, bool removeOrder,
                                 uint32_t* next, bool adjust, bool local) {
   using G = fmt_mt::LargeTier;
+  if (local && adjust)  // f4 with annotate-adjust
+    return launchTier<false, G, false, kMtWavesLarge, 1, true, true>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (local)  // f4: the local client's submissions, acks, rollbacks and reconnects (plain ops otherwise)
     return launchTier<false, G, false, kMtWavesLarge, 1, false, true>(batch, out, docList, count, nullptr, numCUs, stream, nullptr, next);
   if (adjust && removeOrder)

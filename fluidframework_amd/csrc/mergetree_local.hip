@@ -23,10 +23,14 @@ constexpr int kMtWavesLocal = 4;  // 4 documents per workgroup
 
 hipError_t launchMergeTreeLocal(const MtDeviceBatch& batch, const MtDeviceOut& out, const uint32_t* docList,
                                 uint32_t count, uint32_t* esc, uint32_t* esc2, int numCUs, hipStream_t stream,
-                                uint32_t* sched) {
+                                uint32_t* sched, bool adjust) {
   using K = fmt_mt::CompactTier;
   using S = fmt_mt::SmallTier;
   uint32_t* n0 = sched, * n1 = sched ? sched + 1 : nullptr;
+  // annotate-adjust batches (round 6): the PropertiesManager's remote and local change lists with
+  // adjust folding (Doc<..., Adj, Loc>), small tier first whatever FMT_LOCAL_PATH says
+  if (adjust)
+    return launchTier<false, S, false, kMtWavesLocal, 2, true, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);
   if constexpr (FMT_LOCAL_PATH == 0)
     return launchTier<false, K, false, kMtWavesLocal, 3, false, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n0);
   if constexpr (FMT_LOCAL_PATH == 1)

@@ -1366,7 +1366,8 @@ class Doc {
 
   // updateMsn(msn) on the manager of leaf `leaf`.
   FMT_DEV void pmUpdateMsn(uint32_t leaf, int msn) {
-    for (int h = pmFind(leaf, 0u, 0x10000u); h >= 0 && status == FMT_OK; h = pmFind(leaf, 0u, 0x10000u, h + 1)) {
+    // (heads: records of kind 0; Loc's local changes, kind 2, are neither heads nor folded)
+    for (int h = pmFind(leaf, 0u, 0x30000u); h >= 0 && status == FMT_OK; h = pmFind(leaf, 0u, 0x30000u, h + 1)) {
       const uint32_t key = pmWord(h, 1) & 0xFFFFu;
       const uint32_t* R = pmBase();
       int last = -1;
@@ -1388,6 +1389,7 @@ class Doc {
         }
       }
       if (last >= 0) pmSet(h, 3, pmWord(last, 3));  // (a deleted record keeps its value word)
+      if constexpr (Loc) pending = pending || pmFind(leaf, key | 0x20000u, 0x3FFFFu, h + 1) >= 0;
       if (!pending) pmSet(h, 0, 0u);
     }
   }
@@ -1500,7 +1502,7 @@ class Doc {
         Lane<bool> p;
         FOR_LANES(l) {
           const int i = base + l;
-          LANE(p) = i < pmN && loadCoherent(R + 4 * i) != 0u && (loadCoherent(R + 4 * i + 1) & 0x10000u) == 0u &&
+          LANE(p) = i < pmN && loadCoherent(R + 4 * i) != 0u && (loadCoherent(R + 4 * i + 1) & 0x30000u) == 0u &&
                     (loadCoherent(R + 4 * i + 2) & 0x80000000u) == 0u;
         }
         const uint64_t m = ballot(p);
@@ -1513,7 +1515,7 @@ class Doc {
       if (j >= 0) {
         cnt = loadWork(propsAt(j));
       }
-      for (int g = h; g >= 0 && status == FMT_OK; g = pmFind(leaf, 0u, 0x10000u, g + 1)) {
+      for (int g = h; g >= 0 && status == FMT_OK; g = pmFind(leaf, 0u, 0x30000u, g + 1)) {
         pmSet(g, 2, 0x80000000u);  // (done: a head's seq word is otherwise unused)
         if (j < 0) continue;
         const uint32_t key = pmWord(g, 1) & 0xFFFFu;
@@ -2360,7 +2362,7 @@ class Doc {
       }
     } else {
       // annotateRange (mergeTree.ts:2009-2081): one prop-set transition per distinct old set
-      if constexpr (Adj) {  // each hit leaf's PropertiesManager, in nodeMap order
+      if constexpr (Adj && !Loc) {  // each hit leaf's PropertiesManager, in nodeMap order
         for (Lane<uint32_t> t = hits;;) {
           const int j = firstSet(t, nr);
           if (j < 0 || status != FMT_OK) break;
@@ -2383,15 +2385,22 @@ class Doc {
             locPmLocal(j, op.payload, group);
           }
           if (status != FMT_OK) return false;
-        } else if (pmN > 0) {  // leaves whose managers hold local changes keep those keys' local values
+        } else if (pmN > 0 || (Adj && opHasAdjust(op.payload))) {
+          // leaves whose managers hold local changes keep those keys' local values; annotate-adjust
+          // batches: every leaf an adjust reaches, or whose manager has records, runs handleProperties
+          // in full (remote changes join the remote list)
+          const bool adj = Adj && opHasAdjust(op.payload);
           for (Lane<uint32_t> t = hits;;) {
             const int j = firstSet(t, nr);
             if (j < 0 || status != FMT_OK) break;
             FOR_LANES(l) {
               if (l == (j & 63)) LANE(t) &= ~(1u << (j >> 6));
             }
-            if (pmFind(fId(readField(j, 4)), 0u, 0x30000u) < 0) continue;  // (no head: the shared path)
-            const uint32_t nw = locRemoteAnnotate(j, op.payload);
+            const uint32_t leaf = fId(readField(j, 4));
+            if (!adj && pmFind(leaf, 0u, Adj ? 0u : 0x30000u) < 0) continue;  // (no manager: the shared path)
+            uint32_t nw;
+            if constexpr (Adj) nw = locAdjRemote(j, op.payload, seq);
+            else nw = locRemoteAnnotate(j, op.payload);
             if (status != FMT_OK) return false;
             const int rj = j >> 6, lane = j & 63;
             FOR_ROWS(r, rj, rj + 1) {
@@ -2625,7 +2634,11 @@ class Doc {
     return static_cast<int>(total);
   }
 
-  // --- the local client's PropertiesManager records (raw values; adjusts are refused at load)
+  // --- the local client's PropertiesManager records: heads {leaf, key, 0, msnConsensus}, local
+  // changes {leaf, key | 0x20000, group serial, change}; with annotate-adjust (Adj) also the remote
+  // changes {leaf, key | 0x10000, seq, value after it} of the shared Adj model above. A change word is
+  // a raw value id, or kLocAdjust | the adjust row (segmentPropertiesManager.ts:45-52 PropertyChange).
+  static constexpr uint32_t kLocAdjust = 0x80000000u;
   FMT_DEV int locHead(uint32_t leaf, uint32_t key) const { return pmFind(leaf, key, 0x3FFFFu); }
   FMT_DEV int locLocalFirst(uint32_t leaf, uint32_t key) const { return pmFind(leaf, key | 0x20000u, 0x3FFFFu); }
   FMT_DEV int locLocalLast(uint32_t leaf, uint32_t key) const {
@@ -2676,23 +2689,108 @@ class Doc {
     return cnt;
   }
 
+  // The op's change at payload word t (an adjust takes the next word, its row): the change word, and
+  // the index of the op's next change.
+  FMT_DEV uint32_t locChange(uint32_t t, uint32_t b, uint32_t* next) {
+    const uint32_t e = uni(in.propsKv[t]);
+    *next = t + 1;
+    if ((e & 0xFFFFu) != FMT_MT_VALUE_ADJUST) return e & 0xFFFFu;
+    if (!Adj || t + 1 >= b) {  // (adjusts: the Adj variants; a row must follow)
+      fail(Adj ? FMT_E_DATA : FMT_E_UNSUPPORTED);
+      return 0u;
+    }
+    *next = t + 2;
+    return kLocAdjust | uni(in.propsKv[t + 1]);
+  }
+  // computePropertyValue of one change onto v (segmentPropertiesManager.ts:54-78).
+  FMT_DEV uint32_t locApply(uint32_t v, uint32_t change) {
+    if ((change & kLocAdjust) == 0u) return change;
+    if constexpr (Adj) {
+      const uint32_t r = adjustFold(in.adj, in.doc, v, change & ~kLocAdjust);
+      if (r == kAdjFailData || r == kAdjFailCap) {
+        fail(r == kAdjFailData ? FMT_E_DATA : kCapFinal);
+        return 0u;
+      }
+      return r;
+    }
+    fail(FMT_E_UNSUPPORTED);
+    return 0u;
+  }
+  // msnConsensus folded with the remote changes: the last remote change's value, else msnConsensus.
+  FMT_DEV uint32_t locRemoteTop(uint32_t leaf, uint32_t key) {
+    const int h = locHead(leaf, key);
+    uint32_t v = pmWord(h, 3);
+    for (int i = pmFind(leaf, key | 0x10000u, 0x3FFFFu, h + 1); i >= 0; i = pmFind(leaf, key | 0x10000u, 0x3FFFFu, i + 1))
+      v = pmWord(i, 3);
+    return v;
+  }
+  // ... then with the local changes, oldest first: properties[key] (:221-225).
+  FMT_DEV uint32_t locFoldLocal(uint32_t leaf, uint32_t key, uint32_t v) {
+    for (int i = locLocalFirst(leaf, key); i >= 0 && status == FMT_OK; i = pmFind(leaf, key | 0x20000u, 0x3FFFFu, i + 1))
+      v = locApply(v, pmWord(i, 3));
+    return v;
+  }
+  FMT_DEV bool locHasRemote(uint32_t leaf, uint32_t key) { return pmFind(leaf, key | 0x10000u, 0x3FFFFu) >= 0; }
+
   // handleProperties for a local change (segmentPropertiesManager.ts:199-211): a key's entry starts at
   // its current value, the change joins its local list. (The visible set follows the op's values,
-  // applied by the caller.)
+  // applied by the caller: a local adjust folds onto the current value, which is the fold of
+  // everything before it.)
   FMT_DEV void locPmLocal(int j, uint32_t opId, uint32_t g) {
     const uint32_t leaf = fId(readField(j, 4));
     const uint32_t props = propsAt(j);
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
-    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
-      const uint32_t e = uni(in.propsKv[t]);
-      const uint32_t key = e >> 16;
-      if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
-        fail(FMT_E_UNSUPPORTED);
-        return;
-      }
+    for (uint32_t t = a, nx; t < b && status == FMT_OK; t = nx) {
+      const uint32_t key = uni(in.propsKv[t]) >> 16;
+      const uint32_t ch = locChange(t, b, &nx);
+      if (status != FMT_OK) return;
       if (locHead(leaf, key) < 0 && !pmAppend(leaf, key, 0, keyValue(props, key))) return;
-      if (!pmAppend(leaf, key | 0x20000u, static_cast<int>(g), e & 0xFFFFu)) return;
+      if (!pmAppend(leaf, key | 0x20000u, static_cast<int>(g), ch)) return;
     }
+    if constexpr (Adj) pmUpdateMsn(leaf, minSeq);
+  }
+
+  // handleProperties for a remote change in an annotate-adjust batch (segmentPropertiesManager.ts:
+  // 199-238): the key's entry starts at its current value; a raw change folds into msnConsensus while
+  // no remote change is pending, else it (and any adjust) joins the remote list with the value it
+  // leaves; properties[key] = that fold, then the key's local changes; updateMsn(minSeq). Returns the
+  // leaf's new prop set.
+  FMT_DEV uint32_t locAdjRemote(int j, uint32_t opId, int seq) {
+    const uint32_t leaf = fId(readField(j, 4));
+    uint32_t cnt = loadWork(propsAt(j));
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a, nx; t < b && status == FMT_OK; t = nx) {
+      const uint32_t key = uni(in.propsKv[t]) >> 16;
+      const uint32_t ch = locChange(t, b, &nx);
+      if (status != FMT_OK) return 0u;
+      uint32_t prev = 0u;
+      for (uint32_t k = 0; k < cnt; k++)
+        if ((uni(s->kvWork[k]) >> 16) == key) prev = uni(s->kvWork[k]) & 0xFFFFu;
+      int h = locHead(leaf, key);
+      if (h < 0) {
+        if (!pmAppend(leaf, key, 0, prev)) return 0u;
+        h = pmN - 1;
+      }
+      if ((ch & kLocAdjust) == 0u && !locHasRemote(leaf, key)) {
+        pmSet(h, 3, ch);
+      } else {
+        const uint32_t v = locApply(locRemoteTop(leaf, key), ch);
+        if (status != FMT_OK || !pmAppend(leaf, key | 0x10000u, seq, v)) return 0u;
+      }
+      waveSync();
+      const uint32_t v = locFoldLocal(leaf, key, locRemoteTop(leaf, key));
+      if (status != FMT_OK) return 0u;
+      cnt = workSetKey(cnt, key, v);
+    }
+    pmUpdateMsn(leaf, minSeq);
+    return status == FMT_OK ? internWork(cnt) : 0u;
+  }
+
+  FMT_DEV bool opHasAdjust(uint32_t opId) const {
+    const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
+    for (uint32_t t = a; t < b; t++)
+      if ((uni(in.propsKv[t]) & 0xFFFFu) == FMT_MT_VALUE_ADJUST) return true;
+    return false;
   }
 
   // A remote annotate on a leaf whose manager has local changes (segmentPropertiesManager.ts:213-227):
@@ -2718,22 +2816,37 @@ class Doc {
 
   // PropertiesManager.ack (segmentPropertiesManager.ts:248-267) + updateMsn: each key's oldest local
   // change leaves, msnConsensus takes the acknowledged value; a key left without changes loses its entry.
-  FMT_DEV void locPmAck(uint32_t leaf, uint32_t opId) {
+  // (Adj: a raw change folds into msnConsensus while no remote change is pending, else the change
+  // joins the remote list at the ack's seq; then updateMsn with the message's minSeq, :248-267)
+  FMT_DEV void locPmAck(uint32_t leaf, uint32_t opId, int seq, int msn) {
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
-    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
-      const uint32_t e = uni(in.propsKv[t]);
-      const uint32_t key = e >> 16;
+    for (uint32_t t = a, nx; t < b && status == FMT_OK; t = nx) {
+      const uint32_t key = uni(in.propsKv[t]) >> 16;
+      const uint32_t ch = locChange(t, b, &nx);
+      if (status != FMT_OK) return;
       const int c = locLocalFirst(leaf, key), h = locHead(leaf, key);
       if (c < 0 || h < 0) {  // "must have local change to ack" (0xa71)
         fail(FMT_E_DATA);
         return;
       }
       pmSet(c, 0, 0u);
-      pmSet(h, 3, e & 0xFFFFu);
-      waveSync();
-      if (locLocalFirst(leaf, key) < 0) pmSet(h, 0, 0u);
-      waveSync();
+      if constexpr (Adj) {
+        waveSync();
+        if ((ch & kLocAdjust) == 0u && !locHasRemote(leaf, key)) {
+          pmSet(h, 3, ch);
+        } else {
+          const uint32_t v = locApply(locRemoteTop(leaf, key), ch);
+          if (status != FMT_OK || !pmAppend(leaf, key | 0x10000u, seq, v)) return;
+        }
+        waveSync();
+      } else {
+        pmSet(h, 3, ch);
+        waveSync();
+        if (locLocalFirst(leaf, key) < 0) pmSet(h, 0, 0u);
+        waveSync();
+      }
     }
+    if constexpr (Adj) pmUpdateMsn(leaf, msn);
   }
 
   // rollbackProperties (segmentPropertiesManager.ts:140-173, collaborating): each key of the op drops
@@ -2743,8 +2856,10 @@ class Doc {
     const uint32_t leaf = fId(readField(j, 4));
     uint32_t cnt = loadWork(propsAt(j));  // (`seg.properties ??= {}`: a set even if empty)
     const uint32_t a = uni(in.propsOff[opId]), b = uni(in.propsOff[opId + 1]);
-    for (uint32_t t = a; t < b && status == FMT_OK; t++) {
+    for (uint32_t t = a, nx; t < b && status == FMT_OK; t = nx) {
       const uint32_t key = uni(in.propsKv[t]) >> 16;
+      locChange(t, b, &nx);
+      if (status != FMT_OK) return;
       const int h = locHead(leaf, key);
       if (h < 0) {  // "Pending changes must exist for rollback when collaborating" (0xa6f)
         fail(FMT_E_DATA);
@@ -2753,9 +2868,15 @@ class Doc {
       const int c = locLocalLast(leaf, key);
       if (c >= 0) pmSet(c, 0, 0u);
       waveSync();
-      const int c2 = locLocalLast(leaf, key);
-      const uint32_t v = c2 >= 0 ? pmWord(c2, 3) : pmWord(h, 3);
-      if (c2 < 0) pmSet(h, 0, 0u);
+      uint32_t v;
+      if constexpr (Adj) {  // computePropertyValue(msnConsensus, remote, local) (:157-162)
+        v = locFoldLocal(leaf, key, locRemoteTop(leaf, key));
+        if (locLocalFirst(leaf, key) < 0 && !locHasRemote(leaf, key)) pmSet(h, 0, 0u);
+      } else {
+        const int c2 = locLocalLast(leaf, key);
+        v = c2 >= 0 ? pmWord(c2, 3) : pmWord(h, 3);
+        if (c2 < 0) pmSet(h, 0, 0u);
+      }
       waveSync();
       cnt = workSetKey(cnt, key, v);
     }
@@ -2789,6 +2910,28 @@ class Doc {
     } else {
       fail(FMT_E_UNSUPPORTED);
       return;
+    }
+    if constexpr (Adj) {
+      // annotateAdjustRangeLocal (client.ts:286-301): min greater than max is a UsageError (a JSON null
+      // bound compares as 0)
+      if (op.type == FMT_MT_ANNOTATE) {
+        const uint32_t a = uni(in.propsOff[op.payload]), b = uni(in.propsOff[op.payload + 1]);
+        for (uint32_t t = a; t + 1 < b; t++) {
+          if ((uni(in.propsKv[t]) & 0xFFFFu) != FMT_MT_VALUE_ADJUST) continue;
+          const uint32_t row = uni(in.propsKv[++t]);
+          if (in.adj == nullptr || row >= in.adj->nAdjusts) {
+            fail(FMT_E_DATA);
+            return;
+          }
+          const fmt_mt_adjust* R = in.adj->adjusts + row;
+          const uint32_t fl = uni(R->flags);
+          const double mn = (fl & FMT_MT_ADJ_MIN_NULL) ? 0.0 : uniD(R->min), mx = (fl & FMT_MT_ADJ_MAX_NULL) ? 0.0 : uniD(R->max);
+          if ((fl & FMT_MT_ADJ_MIN) && (fl & FMT_MT_ADJ_MAX) && mn > mx) {
+            fail(FMT_E_USAGE);
+            return;
+          }
+        }
+      }
     }
     const uint32_t ls = ++locSeq;  // mintNextLocalOperationStamp (mergeTreeNodes.ts:685-695)
     const uint32_t marker = (op.flags & FMT_MT_F_MARKER) != 0 ? 1u : 0u;
@@ -2840,7 +2983,7 @@ class Doc {
           return;
         }
       } else {
-        locPmAck(leaf, op.payload);
+        locPmAck(leaf, op.payload, op.seq, op.min_seq);
       }
       pendAdd(j, -1);
       lruForLeaf(j, static_cast<int>(fBlk(readField(j, 0))), op.seq);

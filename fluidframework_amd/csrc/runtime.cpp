@@ -1028,12 +1028,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     if (S.err != nullptr && (firstBad == nullptr || S.errAt < firstBad->errAt)) firstBad = &S;
   }
   if (firstBad != nullptr) return setErr(c, firstBad->errCode, firstBad->err);
-  // f4 batches run the large tier's Loc variant alone: features it does not combine with are refused
-  if (local && (obliterates || catchupOps || rmOrderOps || b->relpos != nullptr || b->adjusts != nullptr ||
-                b->snapshot_info != nullptr))
+  // f4 batches run the Loc variants (annotate-adjust too since round 6): features they do not combine
+  // with are refused
+  if (local && (obliterates || catchupOps || rmOrderOps || b->relpos != nullptr || b->snapshot_info != nullptr))
     return setErr(c, FMT_E_UNSUPPORTED,
                   "local-client records (FMT_MT_F_LOCAL_ANY) do not combine with obliterate, catch-up, remove order, "
-                  "relative positions, annotate-adjust or SnapshotV1 merge info");
+                  "relative positions or SnapshotV1 merge info");
   if (b->snapshots) {
     for (uint32_t d = 0; d < n; d++) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];
@@ -1248,8 +1248,9 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     // Per-document slabs, sized from the document's local records (a document that needs more reports
     // FMT_E_CAPACITY): 4 + 2 pending groups per submission (a reconnect replaces a group by one per
     // segment), 32 group records per submission (hits and split copies; deleted ones compact away),
-    // 64 PropertiesManager records per key of a local annotate, regenerated ops / text per reconnect,
-    // and normalization scratch for a document that reconnects.
+    // 64 PropertiesManager records per key of a local annotate (annotate-adjust batches: + 32 per key
+    // of any annotate, whose remote changes stay listed until minSeq passes them), regenerated ops /
+    // text per reconnect, and normalization scratch for a document that reconnects.
     const fmt_kernels::MtCaps big = fmt_kernels::mergeTreeCaps(true);
     std::vector<uint64_t> offs(6 * (n + 1ull), 0);
     for (uint32_t d = 0; d < n; d++) {
@@ -1257,6 +1258,8 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
       for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
         const fmt_mt_op& op = b->ops[i];
         if (op.flags & FMT_MT_F_REGEN) regens++;
+        if (anyAdjust && op.type == FMT_MT_ANNOTATE && !(op.flags & (FMT_MT_F_LOCAL | FMT_MT_F_ROLLBACK)))
+          keys += (b->props_off[op.payload + 1] - b->props_off[op.payload] + 1) / 2;
         if (!(op.flags & FMT_MT_F_LOCAL)) continue;
         sub++;
         if (op.type == FMT_MT_INSERT) text += fmt_mt_op_len(&op);
@@ -1496,12 +1499,13 @@ int fmt_mt_run(fmt_ctx* c) {
   FMT_HIP(c, hipEventRecord(c->ev0, c->stream));
   const bool hasHuge = c->mtHugeLoaded > 0, list = c->mtUseList;
   if (c->mtLocal) {
-    // f4 (round 6): the compact tier's local variant over every document, the ones it cannot hold
-    // in the small tier's, and those listed in mtEsc replay from their first op in the large tier's
+    // f4 (round 6): the small tier's local variant over every document (its Adj variant for
+    // annotate-adjust batches); those listed in mtEsc replay from their first op in the large tier's
     // local variant below (mergetree_local.hip)
     if (!list || c->mtNSmall > 0)
       FMT_HIP(c, fmt_kernels::launchMergeTreeLocal(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
-                                                   c->mtEsc.p, c->mtEsc2.p, c->numCUs, c->stream, c->mtSched.p));
+                                                   c->mtEsc.p, c->mtEsc2.p, c->numCUs, c->stream, c->mtSched.p,
+                                                   c->mtHasAdjust));
   } else if (!list || c->mtNSmall > 0)
     FMT_HIP(c, fmt_kernels::launchMergeTree(db, dout, list ? c->mtSmallList.p : nullptr, list ? c->mtNSmall : c->mtDocs,
                                             c->mtEsc.p, c->mtEsc2.p, c->mtEsc3.p, c->numCUs, c->stream,

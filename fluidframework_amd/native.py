@@ -413,7 +413,7 @@ class Engine:
         (fmt_mt_fetch_headers returns the first failure), else returns them all."""
         out = np.zeros(self._mt_docs, dtype=DOC_RESULT_DTYPE)
         rc = self.L.fmt_mt_fetch_headers(self.h, _ptr(out))
-        if raise_on_failed_docs or rc not in (FMT_OK, FMT_E_DATA, FMT_E_CAPACITY, FMT_E_UNSUPPORTED):
+        if raise_on_failed_docs or rc not in (FMT_OK, FMT_E_USAGE, FMT_E_DATA, FMT_E_CAPACITY, FMT_E_UNSUPPORTED):
             self._check(rc)
         return out
 

@@ -254,6 +254,17 @@ int orc_mt_apply_ops(void* h, const fmt_mt_op* ops, uint64_t n, const uint16_t* 
   return applyOps(static_cast<MergeTree*>(h), ops, n, arena, propsOff, propsKv, nullptr);
 }
 
+// Annotate-adjust rows and the value numbers (NaN: not a number) for the ops applied next to the
+// interactive document (batch-global value ids; computed numbers take ids of their own).
+void orc_mt_set_adjusts(void* h, const fmt_mt_adjust* adjusts, uint32_t nAdjusts, const double* valueNum,
+                        uint32_t nValues) {
+  MergeTree* mt = static_cast<MergeTree*>(h);
+  mt->adjusts = adjusts;
+  mt->nAdjusts = nAdjusts;
+  mt->valueNum = valueNum;
+  mt->nValues = valueNum ? nValues : 0u;
+}
+
 // Returns the text length; copies min(len, cap) UTF-16 units.
 // f4: the local length (getLength, client.ts:1696) and the ops REGEN events produced since the last
 // take (their insert text in `text`, payloads relative to it); *nOps / *nText are the full counts. With

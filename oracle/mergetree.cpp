@@ -1019,8 +1019,18 @@ void MergeTree::applyLocal(const fmt_mt_op& op, const uint16_t* arena, const uin
     stamp.localSeq = ++localSeq;
     markRangeRemoved(start, end, lp, stamp);
   } else {
+    const std::vector<PropChange> changes = opChanges(op, propsOff, propsKv);
+    // annotateAdjustRangeLocal (client.ts:286-301): min greater than max is a UsageError, before the
+    // op applies (a JSON null bound compares as 0)
+    for (const PropChange& ch : changes) {
+      if (ch.adjust < 0) continue;
+      if (adjusts == nullptr || static_cast<uint32_t>(ch.adjust) >= nAdjusts) throw DataError("adjust row out of range");
+      const fmt_mt_adjust& a = adjusts[ch.adjust];
+      const double mn = (a.flags & FMT_MT_ADJ_MIN_NULL) ? 0.0 : a.min, mx = (a.flags & FMT_MT_ADJ_MAX_NULL) ? 0.0 : a.max;
+      if ((a.flags & FMT_MT_ADJ_MIN) && (a.flags & FMT_MT_ADJ_MAX) && mn > mx) throw UsageError("min is greater than max");
+    }
     stamp.localSeq = ++localSeq;
-    annotateRange(start, end, opChanges(op, propsOff, propsKv), lp, stamp);
+    annotateRange(start, end, changes, lp, stamp);
   }
   if (pendingSegments_.size() != groupsBefore + 1) throw DataError("local op created no segment group");
   SegmentGroup* g = pendingSegments_.back();

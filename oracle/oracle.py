@@ -36,6 +36,8 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_remove_local.argtypes = [P, ctypes.c_int, ctypes.c_int]
         L.orc_mt_start_collab.argtypes = [P, ctypes.c_int]
         L.orc_mt_apply_ops.argtypes = [P, P, ctypes.c_uint64, P, P, P]
+        L.orc_mt_set_adjusts.argtypes = [P, P, ctypes.c_uint32, P, ctypes.c_uint32]
+        L.orc_mt_set_adjusts.restype = None
         L.orc_mt_text.argtypes = [P, P, ctypes.c_int]
         L.orc_mt_dump.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_mt_summary.argtypes = [P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P,
@@ -117,6 +119,12 @@ class MergeTreeDoc:
         ops = np.ascontiguousarray(ops)
         self._check(lib().orc_mt_apply_ops(self.h, _ptr(ops), len(ops), _ptr(arena), _ptr(props_off),
                                            _ptr(props_kv)))
+
+    def set_adjusts(self, adjusts: np.ndarray, value_num: np.ndarray):
+        """Annotate-adjust rows (ADJUST_DTYPE) and per value id its number (NaN: none) for the ops
+        applied next; the arrays must outlive those calls (kept here)."""
+        self._adj = (np.ascontiguousarray(adjusts), np.ascontiguousarray(value_num, dtype=np.float64))
+        lib().orc_mt_set_adjusts(self.h, _ptr(self._adj[0]), len(self._adj[0]), _ptr(self._adj[1]), len(self._adj[1]))
 
     def local_length(self) -> int:
         """getLength() from the local perspective (client.ts:1696)."""

@@ -287,6 +287,48 @@ static int adjustCascade(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_
                                               true, 0, 0, nullptr, nullptr, g_legacy.data());
 }
 
+template <bool Adj>
+static int replayLocal(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
+                       fmt_mt_propset* props, int largeOnly) {
+  using G = fmt_mt::LargeTier;
+  using K = fmt_mt::CompactTier;
+  using S = fmt_mt::SmallTier;
+  using DS = fmt_mt::Doc<false, S>;
+  using DL = fmt_mt::Doc<false, G, false, Adj, true>;
+  const size_t n = b->n_docs;
+  // (annotate-adjust batches: the legacy getAtSeq views, emu_mt_legacy_props, at large strides)
+  std::vector<uint16_t> smallLegacy(Adj ? n * DS::kCapLeaves : 0, 0xFFFFu);
+  if (Adj) {
+    g_legacyStride = DL::kCapLeaves;
+    g_legacy.assign(n * g_legacyStride, 0xFFFFu);
+  }
+  if (largeOnly == 1)
+    return replayAll<false, G, false, Adj, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0, nullptr, false, 0,
+                                                 0, nullptr, nullptr, Adj ? g_legacy.data() : nullptr);
+  std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
+  std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
+  std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
+  if (largeOnly == 2 || largeOnly == 3)
+    replayAll<false, K, false, Adj, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr, false,
+                                          DS::kCapLeaves, S::kCapChars, nullptr, nullptr,
+                                          Adj ? smallLegacy.data() : nullptr);
+  if (largeOnly == 2) return FMT_OK;  // (diagnostics: the compact tier's statuses alone)
+  // the small tier's local variant over the documents the compact tier could not hold (from op 0);
+  // mode 0 (the runtime's default, mergetree_local.hip FMT_LOCAL_PATH 1) starts here with every document
+  replayAll<false, S, false, Adj, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr,
+                                        largeOnly == 3, 0, 0, nullptr, nullptr, Adj ? smallLegacy.data() : nullptr);
+  for (size_t d = 0; d < n; d++) {  // documents done below the large tier: results to the large strides
+    const fmt_mt_doc_result& h = headers[d];
+    if (h.status == FMT_E_CAPACITY) continue;
+    std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));
+    std::memcpy(chars + d * G::kCapChars, sc.get() + d * S::kCapChars, h.n_chars * sizeof(uint16_t));
+    std::memcpy(props + d * G::kPropCap, sp.get() + d * S::kPropCap, h.n_props * sizeof(fmt_mt_propset));
+    if (Adj) std::memcpy(g_legacy.data() + d * DL::kCapLeaves, smallLegacy.data() + d * DS::kCapLeaves, h.n_leaves * sizeof(uint16_t));
+  }
+  return replayAll<false, G, false, Adj, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0, nullptr, true, 0, 0,
+                                               nullptr, nullptr, Adj ? g_legacy.data() : nullptr);
+}
+
 extern "C" {
 
 // large = 0: the small tier (registers + LDS text); 1: the large tier (HBM text) that the runtime
@@ -401,37 +443,18 @@ uint32_t emu_huge_ckpt_words() { return fmt_ckpt::kWords; }
 // hold, from their first op (results at large strides). Mode 3: the compact tier's Loc variant first,
 // the small tier's over what it could not hold, then the large tier's (FMT_LOCAL_PATH 2). largeOnly: every
 // document in the large tier (round 5's path); 2: the compact tier alone (its statuses, diagnostics).
+// Annotate-adjust batches run the Adj local variants (Doc<false, C, false, true, true>), with the
+// batch's number tables (emu_mt_numbers) and legacy views (emu_mt_legacy_props).
 int emu_mt_replay_local(const fmt_mt_batch* b, fmt_mt_doc_result* headers, fmt_mt_leaf* leaves, uint16_t* chars,
                         fmt_mt_propset* props, int largeOnly) {
   g_nums.clear();
   g_legacyStride = 0;
   prepareLocal(b->n_docs);
-  using G = fmt_mt::LargeTier;
-  using K = fmt_mt::CompactTier;
-  using S = fmt_mt::SmallTier;
-  if (largeOnly == 1) return replayAll<false, G, false, false, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0);
-  using DS = fmt_mt::Doc<false, S>;
-  using DL = fmt_mt::Doc<false, G, false, false, true>;
-  const size_t n = b->n_docs;
-  std::unique_ptr<fmt_mt_leaf[]> sl(new fmt_mt_leaf[n * DS::kCapLeaves]);
-  std::unique_ptr<uint16_t[]> sc(new uint16_t[n * S::kCapChars]);
-  std::unique_ptr<fmt_mt_propset[]> sp(new fmt_mt_propset[n * S::kPropCap]);
-  if (largeOnly == 2 || largeOnly == 3)
-    replayAll<false, K, false, false, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr, false,
-                                            DS::kCapLeaves, S::kCapChars);
-  if (largeOnly == 2) return FMT_OK;  // (diagnostics: the compact tier's statuses alone)
-  // the small tier's local variant over the documents the compact tier could not hold (from op 0);
-  // mode 0 (the runtime's default, mergetree_local.hip FMT_LOCAL_PATH 1) starts here with every document
-  replayAll<false, S, false, false, true>(b, headers, sl.get(), sc.get(), sp.get(), nullptr, 0, nullptr, 0, nullptr,
-                                          largeOnly == 3);
-  for (size_t d = 0; d < n; d++) {  // documents done below the large tier: results to the large strides
-    const fmt_mt_doc_result& h = headers[d];
-    if (h.status == FMT_E_CAPACITY) continue;
-    std::memcpy(leaves + d * DL::kCapLeaves, sl.get() + d * DS::kCapLeaves, h.n_leaves * sizeof(fmt_mt_leaf));
-    std::memcpy(chars + d * G::kCapChars, sc.get() + d * S::kCapChars, h.n_chars * sizeof(uint16_t));
-    std::memcpy(props + d * G::kPropCap, sp.get() + d * S::kPropCap, h.n_props * sizeof(fmt_mt_propset));
+  if (b->adjusts != nullptr) {
+    prepareNumbers(b);
+    return replayLocal<true>(b, headers, leaves, chars, props, largeOnly);
   }
-  return replayAll<false, G, false, false, true>(b, headers, leaves, chars, props, nullptr, 0, nullptr, 0, nullptr, true);
+  return replayLocal<false>(b, headers, leaves, chars, props, largeOnly);
 }
 
 // Document d's regenerated ops (and their text) after the last emu_mt_replay_local: copies <= the

@@ -107,6 +107,9 @@ class _Participant:
         if self.applied < len(self.doc.ops):
             recs = np.array(self.doc.ops[self.applied:], dtype=MT_OP_DTYPE)
             arena, poff, pkv = self.farm.tables()
+            adj = self.farm.adjust_tables()
+            if adj is not None:
+                self.orc.set_adjusts(*adj)
             self.orc.apply(recs, arena, poff, pkv)
             self.applied = len(self.doc.ops)
 
@@ -119,8 +122,11 @@ class LocalFarm:
     """A generated multi-client farm; every participant's own event stream is one document."""
 
     def __init__(self, seed, n_clients=4, initial="", min_length=8, keys=("a", "b", "c"), markers=True,
-                 builder: MergeTreeStreamBuilder | None = None, new_ids=False):
+                 builder: MergeTreeStreamBuilder | None = None, new_ids=False, adjust=False):
         self.rnd = random.Random(seed)
+        # adjust: half the annotates adjust the numeric key "w" (annotateAdjustRangeLocal, client.ts:286),
+        # which raw annotates also set (numbers and a string, which an adjust reads as 0)
+        self.adjust = adjust
         # new_ids: every reconnect comes back under a new clientId (as a real reconnect does); the
         # local client keeps its short id (startOrUpdateCollaboration, client.ts:1719-1725)
         self.new_ids = new_ids
@@ -157,6 +163,18 @@ class LocalFarm:
             self._props_n = len(self.b.props_list)
         return self._arena, self._props[0], self._props[1]
 
+    def adjust_tables(self):
+        """(ADJUST_DTYPE rows, value numbers) of the builder so far, or None without adjusts."""
+        from fluidframework_amd.streams import ADJUST_DTYPE, value_numbers
+
+        if not self.b.adjusts:
+            return None
+        key = (len(self.b.adjusts), len(self.b.values.items))
+        if getattr(self, "_adj_key", None) != key:
+            self._adj = (np.array(self.b.adjusts, dtype=ADJUST_DTYPE), value_numbers(self.b.values.items))
+            self._adj_key = key
+        return self._adj
+
     def _gen_op(self, p: _Participant):
         r = self.rnd
         n = p.length()
@@ -173,6 +191,15 @@ class LocalFarm:
         end = r.randint(start + 1, min(n, start + 1 + r.randint(1, 12)))
         if r.random() < 0.5:
             return {"type": MT_REMOVE, "pos1": start, "pos2": end}
+        if self.adjust and r.random() < 0.5:
+            a = {"delta": r.randint(-3, 3)}
+            if r.random() < 0.3:
+                a["min"] = r.randint(-4, 0)
+            if r.random() < 0.3:
+                a["max"] = r.randint(1, 6)
+            return {"type": MT_ANNOTATE, "pos1": start, "pos2": end, "adjust": {"w": a}}
+        if self.adjust and r.random() < 0.3:
+            return {"type": MT_ANNOTATE, "pos1": start, "pos2": end, "props": {"w": r.choice([None, 0, 2, 5, "s"])}}
         props = {}
         for k in r.sample(self.keys, r.randint(1, len(self.keys))):
             props[k] = None if r.random() < 0.2 else r.choice([1, 2, 3, p.name, "x"])
@@ -265,6 +292,8 @@ class LocalFarm:
             return {"type": MT_INSERT, "pos1": int(r["pos1"]), "seg": new}
         if t == MT_REMOVE:
             return {"type": MT_REMOVE, "pos1": int(r["pos1"]), "pos2": int(r["pos2"])}
+        if "adjust" in orig:  # (regeneratePendingOp: an adjust op regenerates as one, client.ts:1186-1196)
+            return {"type": MT_ANNOTATE, "pos1": int(r["pos1"]), "pos2": int(r["pos2"]), "adjust": orig["adjust"]}
         return {"type": MT_ANNOTATE, "pos1": int(r["pos1"]), "pos2": int(r["pos2"]), "props": orig["props"]}
 
     def run(self, steps, p_submit=0.45, p_rollback=0.08, p_reconnect=0.03, drain=True):

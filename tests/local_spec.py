@@ -161,11 +161,21 @@ class SpecRun:
         return b, where
 
 
-def _props_dict(batch, table, pid):
+VALUE_COMPUTED = 0x8000  # fmt.h FMT_MT_VALUE_COMPUTED: annotate-adjust results, the document's numbers
+
+
+def _value(batch, v, numbers):
+    if v >= VALUE_COMPUTED:
+        x = float(numbers[v - VALUE_COMPUTED])
+        return int(x) if x.is_integer() else x
+    return json.loads(batch.values[v])
+
+
+def _props_dict(batch, table, pid, numbers=()):
     kv = resolve_props(int(pid), table)
     if kv is None:
         return {}
-    return {batch.keys[e >> 16]: json.loads(batch.values[e & 0xFFFF]) for e in kv}
+    return {batch.keys[e >> 16]: _value(batch, e & 0xFFFF, numbers) for e in kv}
 
 
 def _local_view(leaves):
@@ -178,10 +188,10 @@ def _local_view(leaves):
     return out
 
 
-def _props_at(batch, leaves, table, pos):
+def _props_at(batch, leaves, table, pos, numbers=()):
     for L, s in _local_view(leaves):
         if s <= pos < s + int(L["len"]):
-            return _props_dict(batch, table, L["props"])
+            return _props_dict(batch, table, L["props"], numbers)
     raise AssertionError(f"position {pos} outside the local view")
 
 
@@ -199,14 +209,19 @@ def _regen_insert_props(batch, ops, k):
             for e in batch.props_kv[batch.props_off[pos2 - 1]: batch.props_off[pos2 - 1 + 1]]}
 
 
-def evaluate(batch, where, results, regen_of):
+def evaluate(batch, where, results, regen_of, numbers_of=None):
     """results[d] = (header, leaves[:n], chars, props table) of checkpoint document d; regen_of(d) =
-    (ops, text). Returns a list of failures."""
+    (ops, text); numbers_of(d) = its computed annotate-adjust numbers (adjust batches). Returns a list
+    of failures."""
     fails = []
     texts: dict = {}
     for d, (name, c, expect, k) in enumerate(where):
         h, leaves, chars, props = results[d]
         tag = f"{name} / step {k} / client {c}"
+        if "status" in expect:
+            if int(h["status"]) != expect["status"]:
+                fails.append(f"{tag}: status {int(h['status'])} != {expect['status']}")
+            continue
         if int(h["status"]) != 0:
             fails.append(f"{tag}: status {int(h['status'])}")
             continue
@@ -222,8 +237,9 @@ def evaluate(batch, where, results, regen_of):
             elif key in ("props", "props_range"):
                 items = ([(int(p), p, e) for p, e in v.items()] if key == "props"
                          else [(i, i, e) for s, t, e in v for i in range(s, t)])
+                nums = numbers_of(d) if numbers_of is not None else ()
                 for pos, _, e in items:
-                    got = _props_at(batch, leaves, props, pos)
+                    got = _props_at(batch, leaves, props, pos, nums)
                     for pk, pv in e.items():
                         if got.get(pk) != pv:
                             fails.append(f"{tag}: props at {pos}: {pk}={got.get(pk)!r} != {pv!r}")
@@ -258,11 +274,14 @@ def evaluate(batch, where, results, regen_of):
     return fails
 
 
-def spec_batch(cases=None):
-    """Every case's checkpoint documents in one batch: (batch, where)."""
+def spec_batch(cases=None, adjust=False):
+    """Every case's checkpoint documents in one batch: (batch, where). adjust: the annotate-adjust
+    cases ("adjust": true), which run as a batch of their own, instead of the others."""
     b = MergeTreeStreamBuilder()
     where = []
     for case in load_cases() if cases is None else cases:
+        if bool(case.get("adjust")) != adjust:
+            continue
         _, w = SpecRun(case).checkpoint_batch(b)
         where += w
     return b.finish(), where

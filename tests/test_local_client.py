@@ -117,6 +117,63 @@ def test_emulated_engine_local_farms_with_new_client_ids_match_oracle(orc, farms
 
 
 @pytest.fixture(scope="module")
+def farms_adjust():
+    """Farms where half the annotates adjust the numeric key "w" (annotateAdjustRangeLocal,
+    client.ts:286) and raw annotates set it too: local and remote adjusts combine through each
+    segment's PropertiesManager (segmentPropertiesManager.ts:188-267), through acks, rollbacks and
+    reconnects."""
+    batch, farms = local_farm_batch(range(20, 26), steps=500, n_clients=5, min_length=120, adjust=True)
+    assert batch.adjusts is not None and len(batch.adjusts) > 5
+    assert sum(f.regens for f in farms) >= 10 and sum(f.rollbacks for f in farms) >= 10
+    return batch, farms
+
+
+def _char_props(batch, h, leaves, chars, props, nums):
+    """Per visible char: its properties as JSON values (computed numbers resolved)."""
+    from local_spec import _props_dict
+
+    out = []
+    for L in leaves[: int(h["n_leaves"])]:
+        if int(L["rm_seq"]) == 0x7FFFFFFF:
+            out += [_props_dict(batch, props, L["props"], nums)] * int(L["len"])
+    return out
+
+
+def _oracle_adjust_docs(orc, batch):
+    cl, cc, cp = emu_caps(True)
+    nums = []
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024,
+                                                numbers=nums)
+    assert rc == 0
+    return (oh, ol, oc, op), nums
+
+
+def test_oracle_local_adjust_farms_converge(orc, farms_adjust):
+    """Every participant of a farm ends with the same text and the same property values per char
+    (adjusts are not commutative; the manager's remote/local lists make them converge)."""
+    batch, farms = farms_adjust
+    (oh, ol, oc, op), nums = _oracle_adjust_docs(orc, batch)
+    n_w = 0
+    for f in farms:
+        views = [_char_props(batch, oh[p.index], ol[p.index], oc[p.index], op[p.index], nums[p.index]) for p in f.parts]
+        texts = [visible_text(oh[p.index], ol[p.index], oc[p.index]) for p in f.parts]
+        assert all(t == texts[0] for t in texts), texts
+        assert all(v == views[0] for v in views)
+        n_w += sum(1 for c in views[0] if isinstance(c.get("w"), (int, float)))
+    assert n_w > 50  # (adjusted numbers survive in the final state)
+
+
+def test_emulated_engine_local_adjust_farms_match_oracle(orc, farms_adjust):
+    from mt_compare import emu_numbers
+
+    batch, _ = farms_adjust
+    assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen) > 20
+    _, nums = _oracle_adjust_docs(orc, batch)
+    for d in range(batch.n_docs):
+        assert np.array_equal(emu_numbers(d), np.asarray(nums[d], dtype=np.float64)), d
+
+
+@pytest.fixture(scope="module")
 def farms_long():
     """Local farms whose documents outgrow the compact tier's 2048 UTF-16 units mid-stream (initial
     text 1990 units) or start past it (2100), and past the small tier's 6144 (6200): the runtime
@@ -126,6 +183,40 @@ def farms_long():
     farms = [LocalFarm(s, builder=b, n_clients=4, initial=("ab" * 3200)[:n], min_length=n + 300).run(300)
              for s, n in ((40, 1990), (41, 1990), (42, 2100), (43, 6200))]
     return b.finish(), farms
+
+
+@pytest.fixture(scope="module")
+def farms_long_adjust():
+    """Local adjust farms past the small tier's 6144 units (initial text 6200): the large tier's Adj
+    local variant replays them (after the small tier's reports FMT_E_CAPACITY), and one that fits."""
+    b = MergeTreeStreamBuilder()
+    farms = [LocalFarm(s, builder=b, n_clients=4, initial=("ab" * 3200)[:n], min_length=n + 300, adjust=True).run(400)
+             for s, n in ((44, 6200), (45, 6200), (46, 1990))]
+    return b.finish(), farms
+
+
+def _check_adjust_vs_oracle(orc, batch, got, regen_of, numbers_of):
+    n = _check_engine_vs_oracle(orc, batch, got, regen_of)
+    _, nums = _oracle_adjust_docs(orc, batch)
+    for d in range(batch.n_docs):
+        assert np.array_equal(numbers_of(d), np.asarray(nums[d], dtype=np.float64)), d
+    return n
+
+
+def test_emulated_local_adjust_farms_past_the_small_tier_match_oracle(orc, farms_long_adjust):
+    from mt_compare import emu_numbers
+
+    batch, farms = farms_long_adjust
+    (oh, ol, oc, op), _ = _oracle_adjust_docs(orc, batch)
+    assert int(oh["n_chars"].max()) > 6144 and batch.adjusts is not None
+    n = _check_adjust_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen, emu_numbers)
+    assert _check_adjust_vs_oracle(orc, batch, emu_replay_local(batch, large_only=True), emu_regen, emu_numbers) == n
+
+
+@pytest.mark.gpu
+def test_gpu_local_adjust_farms_past_the_small_tier_match_oracle(orc, engine, farms_long_adjust):
+    batch, _ = farms_long_adjust
+    _check_adjust_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen, engine.mt_numbers)
 
 
 def test_emulated_local_farms_past_the_compact_tier_match_oracle(orc, farms_long):
@@ -222,6 +313,23 @@ def test_gpu_local_farms_with_new_client_ids_match_oracle(orc, engine, farms_new
 def test_gpu_local_farms_past_the_compact_tier_match_oracle(orc, engine, farms_long):
     batch, _ = farms_long
     _check_engine_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen)
+
+
+@pytest.mark.gpu
+def test_gpu_local_adjust_farms_match_oracle(orc, engine, farms_adjust):
+    """Local annotate-adjust on the GPU (the small and large tiers' Adj local variants): state,
+    regenerated ops and the computed numbers == oracle, and every farm converges."""
+    batch, farms = farms_adjust
+    got = _gpu(engine, batch)
+    assert _check_engine_vs_oracle(orc, batch, got, engine.mt_regen) > 20
+    _, nums = _oracle_adjust_docs(orc, batch)
+    for d in range(batch.n_docs):
+        assert np.array_equal(engine.mt_numbers(d), np.asarray(nums[d], dtype=np.float64)), d
+    hdr, leaves, chars, props = got
+    for f in farms:
+        views = [_char_props(batch, hdr[p.index], leaves[p.index], chars[p.index], props[p.index],
+                             engine.mt_numbers(p.index)) for p in f.parts]
+        assert all(v == views[0] for v in views)
 
 
 @pytest.mark.gpu

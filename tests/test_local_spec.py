@@ -23,11 +23,38 @@ def _oracle(orc, batch):
     return oh, ol, oc, op
 
 
-def test_spec_cases_are_transcribed(specs):
+@pytest.fixture(scope="module")
+def adjust_specs():
+    return spec_batch(adjust=True)
+
+
+def test_spec_cases_are_transcribed(specs, adjust_specs):
     cases = load_cases()
-    assert len(cases) >= 55
+    assert len(cases) >= 60
     batch, where = specs
-    assert len({w[0] for w in where}) == len(cases)  # every case has a checkpoint
+    _, awhere = adjust_specs
+    n_adj = sum(1 for c in cases if c.get("adjust"))
+    assert n_adj == 5
+    assert len({w[0] for w in where}) == len(cases) - n_adj  # every case has a checkpoint
+    assert len({w[0] for w in awhere}) == n_adj
+    assert adjust_specs[0].adjusts is not None and specs[0].adjusts is None
+
+
+def _oracle_adjust(orc, batch):
+    cl, cc, cp = emu_caps(True)
+    nums = []
+    rc, oh, ol, oc, op, _ = orc.mt_replay_batch(batch, threads=8, cap_leaves=cl, cap_chars=cc, cap_props=1024,
+                                                numbers=nums)
+    return (oh, ol, oc, op), nums
+
+
+def test_oracle_meets_the_adjust_spec_assertions(orc, adjust_specs):
+    """annotateRangeAdjust with local ops (client.applyMsg.spec.ts:730-921): local and remote adjusts
+    combine through the PropertiesManager's remote and local change lists, min > max is a UsageError."""
+    batch, where = adjust_specs
+    out, nums = _oracle_adjust(orc, batch)
+    fails = evaluate(batch, where, _results(*out), lambda d: orc.mt_replay_regen(batch, d)[1:], lambda d: nums[d])
+    assert not fails, fails[:10]
 
 
 def test_oracle_meets_the_spec_assertions(orc, specs):
@@ -46,6 +73,24 @@ def test_emulated_engine_meets_the_spec_assertions_and_matches_the_oracle(orc, s
     for d in range(batch.n_docs):
         diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (got[0][d], got[1][d], got[2][d], got[3][d]))
         assert not diffs, f"{where[d][:2]} step {where[d][3]}: {diffs[:4]}"
+
+
+def test_emulated_engine_meets_the_adjust_spec_assertions_and_matches_the_oracle(orc, adjust_specs):
+    import numpy as np
+
+    from mt_compare import emu_numbers
+    batch, where = adjust_specs
+    got = emu_replay_local(batch)
+    fails = evaluate(batch, where, _results(*got), emu_regen, emu_numbers)
+    assert not fails, fails[:10]
+    (oh, ol, oc, op), nums = _oracle_adjust(orc, batch)
+    for d in range(batch.n_docs):
+        if int(oh[d]["status"]) != 0:
+            assert int(got[0][d]["status"]) == int(oh[d]["status"]), where[d][:2]
+            continue
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), (got[0][d], got[1][d], got[2][d], got[3][d]))
+        assert not diffs, f"{where[d][:2]} step {where[d][3]}: {diffs[:4]}"
+        assert np.array_equal(emu_numbers(d), np.asarray(nums[d], dtype=np.float64)), where[d][:2]
 
 
 @pytest.mark.gpu
@@ -76,3 +121,42 @@ def test_gpu_meets_the_spec_assertions_and_matches_the_oracle(orc, specs):
         assert not diffs, f"{where[d][:2]} step {where[d][3]}: {diffs[:4]}"
         o_ops = orc.mt_replay_regen(batch, d)[1]
         assert np.array_equal(o_ops, regen[d][0]), f"{where[d][:2]}: regenerated ops differ"
+
+
+@pytest.mark.gpu
+def test_gpu_meets_the_adjust_spec_assertions_and_matches_the_oracle(orc, adjust_specs):
+    import numpy as np
+
+    from fluidframework_amd import native
+
+    batch, where = adjust_specs
+    e = native.Engine(0)
+    try:
+        e.mt_load(batch)
+        e.mt_run()
+        e.sync()
+        hdr = e.mt_headers(raise_on_failed_docs=False)
+        res, nums = [], []
+        regen = []
+        for d in range(batch.n_docs):
+            if int(hdr[d]["status"]) != 0:  # (the min > max case: FMT_E_USAGE, nothing to fetch)
+                res.append((hdr[d], None, None, None))
+                nums.append(None)
+                regen.append(None)
+                continue
+            leaves, chars, props = e.mt_doc(d, hdr[d])
+            res.append((hdr[d], leaves, chars, props))
+            nums.append(e.mt_numbers(d))
+            regen.append(e.mt_regen(d))
+    finally:
+        e.close()
+    fails = evaluate(batch, where, res, lambda d: regen[d], lambda d: nums[d])
+    assert not fails, fails[:10]
+    (oh, ol, oc, op), onums = _oracle_adjust(orc, batch)
+    for d in range(batch.n_docs):
+        if int(oh[d]["status"]) != 0:
+            assert int(hdr[d]["status"]) == int(oh[d]["status"]), where[d][:2]
+            continue
+        diffs = compare_doc((oh[d], ol[d], oc[d], op[d]), res[d])
+        assert not diffs, f"{where[d][:2]} step {where[d][3]}: {diffs[:4]}"
+        assert np.array_equal(nums[d], np.asarray(onums[d], dtype=np.float64)), where[d][:2]
