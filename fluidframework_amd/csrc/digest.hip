@@ -2,7 +2,7 @@
 //
 // A 64-bit fingerprint of everything the parity tests compare field by field (tests/mt_compare.py):
 // the header (status, collab window, counts, depth, visible length), every leaf in document order
-// (stamps, remove-client set — tag 10 for short ids 64..127, only on leaves that have one — char
+// (stamps, remove-client set — tags 10 / 11 / 12 for short ids 64..127 / 128..191 / 192..253, only on leaves that have one — char
 // offset, length, insert client, parent block ordinal, marker bit),
 // each leaf's properties BY VALUE (document-local prop-set ids are not part of it) and the text. The
 // definition is an order-sensitive sum of mixed elements, so one wave per document
@@ -70,10 +70,12 @@ __global__ __launch_bounds__(64 * kDigWaves) void stateDigestKernel(const fmt_mt
           }
         }
       }
-      if (V.rmHi != nullptr) {  // remove clients 64..127: leaves that have any
+      if (V.rmHi != nullptr) {  // remove clients 64..127 (tag 10), 128..191 (11), 192..253 (12): leaves that have any
         for (uint32_t i = lane; i < h.n_leaves; i += 64) {
-          const uint64_t hi = V.rmHi[i];
-          if (hi != 0) acc += digElem(10, i, hi);
+          for (int k = 0; k < 3; k++) {
+            const uint64_t hi = V.rmHi[3 * static_cast<size_t>(i) + k];
+            if (hi != 0) acc += digElem(10 + k, i, hi);
+          }
         }
       }
       for (uint32_t u = lane; u < h.n_chars; u += 64) acc += digElem(8, u, V.chars[u]);

@@ -93,7 +93,7 @@ struct FlatSeg {
   int insSeq;
   int insClient;
   int rmSeq;      // lowest remove seq, INT_MAX if not removed
-  uint64_t rmMask[2];  // remove clients 0..127
+  uint64_t rmMask[4];  // remove clients 0..253
 };
 
 class FlatDoc {
@@ -113,7 +113,7 @@ class FlatDoc {
       if (rem == 0) break;
       rem -= present(segs_[i], refSeq, client) ? segs_[i].len : 0;
     }
-    segs_.insert(segs_.begin() + static_cast<long>(i), FlatSeg{len, seq, client, 0x7fffffff, {0, 0}});
+    segs_.insert(segs_.begin() + static_cast<long>(i), FlatSeg{len, seq, client, 0x7fffffff, {0, 0, 0, 0}});
   }
   void removeRange(int start, int end, int seq, int refSeq, int client) {
     splitAt(start, refSeq, client);
@@ -282,7 +282,7 @@ struct CfHandle {
 void* fmtgen_conflict_farm_new(uint32_t n_docs, uint32_t n_clients, uint32_t ops_per_doc,
                                uint32_t min_length_fixed, uint32_t seed, uint32_t annotate_props_base,
                                uint32_t threads, uint64_t* n_ops, uint64_t* n_text, uint32_t doc_base) {
-  if (n_clients == 0 || n_clients > 127) return nullptr;
+  if (n_clients == 0 || n_clients > 253) return nullptr;  // (short ids 1..253; 0xFE names NonCollab)
   auto* h = new CfHandle();
   h->docs.resize(n_docs);
   parallelFor(n_docs, threads, [&](uint32_t i) {
@@ -344,7 +344,7 @@ void fmtgen_free(void* handle) { delete static_cast<CfHandle*>(handle); }
 int64_t fmtgen_t3(uint32_t n_segments, uint32_t n_ops, uint32_t n_clients, uint32_t max_lag, uint32_t max_range,
                   uint32_t seed, uint32_t annotate_props_base, fmt_mt_snapshot_seg* out_segs, uint16_t* out_text,
                   fmt_mt_op* out_ops) {
-  if (n_clients == 0 || n_clients > 127 || max_lag == 0 || max_range == 0) return FMT_E_USAGE;
+  if (n_clients == 0 || n_clients > 253 || max_lag == 0 || max_range == 0) return FMT_E_USAGE;
   Rng rng(0xdeadbeefu, 0xfeedbedu, 0x7733u, seed);
   uint64_t t = 0;
   int64_t chars = 0;

@@ -61,10 +61,18 @@ constexpr int kPropLds = 2048;        // match classes of the first sets cached 
 constexpr uint32_t kPropHash = 1u << 17;  // buckets per prop-set hash table (exact content, match class)
 constexpr int kPropWords = 1 + FMT_MT_PROPS_MAX;  // a prop set in HBM: n, kv[]
 constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
-constexpr int kMaxClient = 127;       // short client ids 0..127 (remove-client sets: two mask words + HugeState::hiMask)
+// short client ids 0..253 (0xFE: FMT_MT_CLIENT_NONCOLLAB); remove-client sets: two mask words for ids
+// 0..63 + HugeState::hiMask, kHiWords per leaf id for ids 64..253 (round 6: was 127, two words)
+constexpr int kMaxClient = 253;
+constexpr int kHiWords = (kMaxClient + 1 - 64 + 31) / 32;
+constexpr int kHiOutWords = kHiWords / 2;  // (writeOutputs: 64-bit words per leaf, ids 64..127, 128..191, 192..255)
 
 // Leaf meta word: insert client (int8) | prop set id << 8 (0xFFFF = properties undefined)
-FMT_DEV int32_t mClient(uint32_t m) { return static_cast<int32_t>(static_cast<int8_t>(m & 0xFFu)); }
+// (0..253 a short id; 0xFE NonCollab = -2, 0xFF = -1: the reference's special client ids)
+FMT_DEV int32_t mClient(uint32_t m) {
+  const int32_t v = static_cast<int32_t>(m & 0xFFu);
+  return v >= 0xFE ? v - 256 : v;
+}
 FMT_DEV uint32_t mProps(uint32_t m) { return (m >> 8) & 0xFFFFu; }
 FMT_DEV uint32_t mkMeta(int32_t client, uint32_t props) { return (static_cast<uint32_t>(client) & 0xFFu) | (props << 8); }
 constexpr uint32_t kMetaMarker = 1u << 24;  // the leaf is a Marker (mergeTreeNodes.ts:495-564)
@@ -185,8 +193,8 @@ struct HugeState {
   FMT_HBM uint32_t* mkIds;    // [mkCap]: every marker leaf ever in the document, in insertion order (relative
   uint32_t mkCap;     //   positions; nullptr: the batch has none)
   FMT_HBM uint32_t* outIdx;   // [idCap]: at output, leaf id -> output index (annotate-adjust batches; else nullptr)
-  // [idCap * 2]: per leaf id, the remove clients with short ids 64..127 (bit c - 64), beyond the two
-  // mask words every leaf and window entry carry (nullptr: the batch has no such client; zeroed)
+  // [idCap * kHiWords]: per leaf id, the remove clients with short ids 64..253 (bit c - 64), beyond the
+  // two mask words every leaf and window entry carry (nullptr: the batch has no such client; zeroed)
   FMT_HBM uint32_t* hiMask;
   // live obliterates (Obliterates, mergeTree.ts:515-635), [obCap] each: per slot its record
   // {startId, startOff, endId, endOff, seq, client} (obRec, 6 words) and whether it is in use, and the
@@ -431,11 +439,24 @@ class HugeDocT {
     const bool present = (ins <= r || ic == c) && !(rm <= r || removedBy(mlo, mhi, c));
     return present ? static_cast<int>(len) : 0;
   }
-  // ---- remove clients 64..127 (getOrAddShortClientId interns without bound, client.ts:831-855): a
+  // ---- remove clients 64..253 (getOrAddShortClientId interns without bound, client.ts:831-855): a
   // per-leaf-id side table; a perspective of such a client (wave-uniform c) reads it, others never do
+  // (a set of them in registers: bit c - 64 of w)
+  struct HiSet {
+    uint32_t w[kHiWords];
+    FMT_DEV void clear() {
+      for (int k = 0; k < kHiWords; k++) w[k] = 0u;
+    }
+    FMT_DEV void add(int c) { w[(c - 64) >> 5] |= 1u << ((c - 64) & 31); }
+    FMT_DEV int count() const {
+      int n = 0;
+      for (int k = 0; k < kHiWords; k++) n += __builtin_popcount(w[k]);
+      return n;
+    }
+  };
   FMT_DEV bool hiRemovedBy(uint32_t id, int c) const {
     const uint32_t b = static_cast<uint32_t>(c - 64);
-    return ((rd(S.hiMask + 2 * static_cast<size_t>(id) + (b >> 5)) >> (b & 31u)) & 1u) != 0;
+    return ((rd(S.hiMask + kHiWords * static_cast<size_t>(id) + (b >> 5)) >> (b & 31u)) & 1u) != 0;
   }
   // PriorPerspective(r, c) of leaf `id` for any c (the mask words for c < 64, the side table above)
   FMT_DEV int visAny(uint32_t len, int32_t ins, int32_t rm, uint32_t mlo, uint32_t mhi, int32_t ic, int r, int c,
@@ -444,25 +465,24 @@ class HugeDocT {
     const bool present = (ins <= r || ic == c) && !(rm <= r || (S.hiMask != nullptr && hiRemovedBy(id, c)));
     return present ? static_cast<int>(len) : 0;
   }
-  FMT_DEV void hiSet(uint32_t id, int c) {  // (c in 64..127, S.hiMask present)
+  FMT_DEV void hiSet(uint32_t id, int c) {  // (c in 64..253, S.hiMask present)
     const uint32_t b = static_cast<uint32_t>(c - 64);
-    uint32_t* p = S.hiMask + 2 * static_cast<size_t>(id) + (b >> 5);
+    uint32_t* p = S.hiMask + kHiWords * static_cast<size_t>(id) + (b >> 5);
     const uint32_t v = ldu(p) | (1u << (b & 31u));
     st1(p, v);
   }
-  FMT_DEV void hiPut(uint32_t id, uint32_t lo, uint32_t hi) {
+  FMT_DEV void hiPut(uint32_t id, const HiSet& h) {
     FOR_LANES(l) {
-      if (l == 0) {
-        S.hiMask[2 * static_cast<size_t>(id)] = lo;
-        S.hiMask[2 * static_cast<size_t>(id) + 1] = hi;
-      }
+      if (l == 0)
+        for (int k = 0; k < kHiWords; k++) S.hiMask[kHiWords * static_cast<size_t>(id) + k] = h.w[k];
     }
   }
-  FMT_DEV int hiCount(uint32_t id) const {
-    return S.hiMask == nullptr ? 0
-                               : __builtin_popcount(ldu(S.hiMask + 2 * static_cast<size_t>(id))) +
-                                     __builtin_popcount(ldu(S.hiMask + 2 * static_cast<size_t>(id) + 1));
+  FMT_DEV HiSet hiGet(uint32_t id) const {
+    HiSet h;
+    for (int k = 0; k < kHiWords; k++) h.w[k] = ldu(S.hiMask + kHiWords * static_cast<size_t>(id) + k);
+    return h;
   }
+  FMT_DEV int hiCount(uint32_t id) const { return S.hiMask == nullptr ? 0 : hiGet(id).count(); }
 
   FMT_DEV uint32_t allocBlk(uint32_t leaf) {
     uint32_t b;
@@ -1808,7 +1828,7 @@ class HugeDocT {
     regsInsert(R, k + 1, y, wy);
     st1(S.leafBlk + y.id, b);
     obRefsMove(x.id, y.id, o, -o);  // the right part takes the references at/after the split
-    if (S.hiMask != nullptr) hiPut(y.id, ldu(S.hiMask + 2 * static_cast<size_t>(x.id)), ldu(S.hiMask + 2 * static_cast<size_t>(x.id) + 1));
+    if (S.hiMask != nullptr) hiPut(y.id, hiGet(x.id));
     if constexpr (Adj) {
       if (pmN > 0) pmCopy(x.id, y.id);  // copyTo (segmentPropertiesManager.ts:300-316)
     }
@@ -1869,7 +1889,8 @@ class HugeDocT {
     int client;
     bool boundary;
     int32_t rm;
-    uint32_t mlo, mhi, hlo, hhi, firstRm;  // (hlo, hhi: remove clients 64..127)
+    uint32_t mlo, mhi, firstRm;
+    HiSet hs;  // (remove clients 64..253)
     bool moreRm;
   };
   FMT_DEV void insertText(const fmt_mt_op& op, const LoadStamp* ld = nullptr) {
@@ -1950,7 +1971,11 @@ class HugeDocT {
       st1(S.winIdx + x.id, kNone);
     }
     if ((op.flags & FMT_MT_F_MARKER) != 0) markerAdd(x.id);
-    if (S.hiMask != nullptr) hiPut(x.id, ld ? ld->hlo : 0u, ld ? ld->hhi : 0u);
+    if (S.hiMask != nullptr) {
+      HiSet none;
+      none.clear();
+      hiPut(x.id, ld ? ld->hs : none);
+    }
     regsInsert(R, k, x, wx);
     st1(S.leafBlk + x.id, b);
     const uint32_t nb = commitBlock(R);
@@ -1983,7 +2008,8 @@ class HugeDocT {
     ld.boundary = (op.flags & FMT_MT_F_GROUP_CONT) == 0;
     ld.rm = kNotRemoved;
     ld.firstRm = 0;
-    uint64_t mask = 0, hmask = 0;
+    uint64_t mask = 0;
+    ld.hs.clear();
     const fmt_mt_snapshot_info inf = in.infoAll[op.pos1];
     for (uint32_t t = 0; t < inf.rm_count; t++) {
       const fmt_mt_stamp st = in.stamps[inf.rm_first + t];
@@ -1997,13 +2023,11 @@ class HugeDocT {
         ld.firstRm = static_cast<uint32_t>(sc);
       }
       if (sc < 64) mask |= 1ull << sc;
-      else hmask |= 1ull << (sc - 64);
+      else ld.hs.add(sc);
     }
     ld.mlo = static_cast<uint32_t>(mask);
     ld.mhi = static_cast<uint32_t>(mask >> 32);
-    ld.hlo = static_cast<uint32_t>(hmask);
-    ld.hhi = static_cast<uint32_t>(hmask >> 32);
-    ld.moreRm = __builtin_popcountll(mask) + __builtin_popcountll(hmask) > 1;
+    ld.moreRm = __builtin_popcountll(mask) + ld.hs.count() > 1;
     invalidate();
     groupCorrections(kLocalSeq, ld.client);  // the local length: every leaf not removed
     const int local = totalView();
@@ -2392,7 +2416,9 @@ class HugeDocT {
   FMT_DEV void obliterateOnInsert(uint32_t id, int refSeq, int client) {
     const int64_t k = ordOf(id);
     int minSeqOther = kNotRemoved, newestSeq = -1, newestClient = -1, firstCl = 0;
-    uint32_t mlo = 0, mhi = 0, hlo = 0, hhi = 0;
+    uint32_t mlo = 0, mhi = 0;
+    HiSet hs;
+    hs.clear();
     bool any = false;
     for (int i = 0; i < obStartN; i++) {  // Obliterates.findOverlapping (:566-582)
       const int slot = obU(S.obStart, i);
@@ -2406,8 +2432,7 @@ class HugeDocT {
         any = true;
         if (ocl < 32) mlo |= 1u << ocl;
         else if (ocl < 64) mhi |= 1u << (ocl - 32);
-        else if (ocl < 96) hlo |= 1u << (ocl - 64);
-        else hhi |= 1u << (ocl - 96);
+        else hs.add(ocl);
         if (oseq < minSeqOther) {
           minSeqOther = oseq;
           firstCl = ocl;
@@ -2445,9 +2470,9 @@ class HugeDocT {
     st1(S.lRm + i, static_cast<int32_t>(minSeqOther));
     st1(S.lMlo + i, mlo);
     st1(S.lMhi + i, mhi);
-    if (S.hiMask != nullptr) hiPut(id, hlo, hhi);
+    if (S.hiMask != nullptr) hiPut(id, hs);
     const uint32_t w = ldu(S.winIdx + id);  // (a new leaf: always a window entry)
-    const bool more = __builtin_popcount(mlo) + __builtin_popcount(mhi) + __builtin_popcount(hlo) + __builtin_popcount(hhi) > 1;
+    const bool more = __builtin_popcount(mlo) + __builtin_popcount(mhi) + hs.count() > 1;
     wSet(w, 1, static_cast<uint32_t>(minSeqOther));
     wSet(w, 3, (ldu(wWord3(w)) & ~(kWMetaMask ^ 0xFFu)) | (static_cast<uint32_t>(firstCl) << 8) | (more ? 1u << 16 : 0u));
     wSetMask(w, mlo, mhi);
@@ -3622,7 +3647,9 @@ class HugeDocT {
             const fmt_mt_snapshot_seg sg = in.segs[j];
             const uint32_t len = sg.len & ~FMT_MT_SEG_MARKER;
             int32_t ins = 0, rm = kNotRemoved, client = in.initClient;
-            uint64_t mask = 0, hmask = 0;
+            uint64_t mask = 0;
+            HiSet hs;
+            hs.clear();
             if (in.info != nullptr) {  // merge info: the insert stamp, the remove stamps folded
               const fmt_mt_snapshot_info inf = in.info[j];
               ins = inf.ins_seq;
@@ -3632,14 +3659,12 @@ class HugeDocT {
                 rm = st.seq < rm ? st.seq : rm;
                 if (st.client < 0 || st.client > kMaxClient || (st.client > 63 && S.hiMask == nullptr)) LANE(wideL) = true;
                 else if (st.client < 64) mask |= 1ull << st.client;
-                else hmask |= 1ull << (st.client - 64);
+                else hs.add(st.client);
               }
               if (client > kMaxClient) LANE(wideL) = true;
             }
-            if (S.hiMask != nullptr) {
-              S.hiMask[2 * static_cast<size_t>(j + 1)] = static_cast<uint32_t>(hmask);
-              S.hiMask[2 * static_cast<size_t>(j + 1) + 1] = static_cast<uint32_t>(hmask >> 32);
-            }
+            if (S.hiMask != nullptr)
+              for (int q = 0; q < kHiWords; q++) S.hiMask[kHiWords * static_cast<size_t>(j + 1) + q] = hs.w[q];
             S.lLen[i] = len;
             S.lIns[i] = ins;
             S.lRm[i] = rm;
@@ -3864,10 +3889,8 @@ class HugeDocT {
             S.lMeta[i] = mkMeta(x.ins_client, props) | ((w4 & (1u << 23)) != 0 ? kMetaMarker : 0u);
             S.leafBlk[id] = b;
             S.winIdx[id] = kNone;
-            if (S.hiMask != nullptr) {
-              S.hiMask[2 * static_cast<size_t>(id)] = 0u;
-              S.hiMask[2 * static_cast<size_t>(id) + 1] = 0u;
-            }
+            if (S.hiMask != nullptr)
+              for (int q = 0; q < kHiWords; q++) S.hiMask[kHiWords * static_cast<size_t>(id) + q] = 0u;
             const bool win = x.ins_seq > minSeq || (x.rm_seq != kNotRemoved && x.rm_seq > minSeq);
             if (win) LANE(winL) = true;
             else if (x.rm_seq == kNotRemoved) sum += static_cast<int>(x.len);
@@ -4418,9 +4441,11 @@ class HugeDocT {
             x.ins_seq = rd(S.lIns + i);
             x.rm_seq = rd(S.lRm + i);
             x.rm_clients = static_cast<uint64_t>(rd(S.lMlo + i)) | (static_cast<uint64_t>(rd(S.lMhi + i)) << 32);
-            if (outHi != nullptr) {  // (remove clients 64..127)
-              const size_t q = 2 * static_cast<size_t>(rd(S.lId + i));
-              outHi[o] = static_cast<uint64_t>(rd(S.hiMask + q)) | (static_cast<uint64_t>(rd(S.hiMask + q + 1)) << 32);
+            if (outHi != nullptr) {  // (remove clients 64..253: kHiOutWords 64-bit words per leaf)
+              const size_t q = kHiWords * static_cast<size_t>(rd(S.lId + i));
+              for (int k = 0; k < kHiOutWords; k++)
+                outHi[kHiOutWords * o + k] = static_cast<uint64_t>(rd(S.hiMask + q + 2 * k)) |
+                                             (static_cast<uint64_t>(rd(S.hiMask + q + 2 * k + 1)) << 32);
             }
             x.char_off = static_cast<uint32_t>(co);
             x.len = LANE(len);

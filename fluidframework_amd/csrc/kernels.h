@@ -85,8 +85,8 @@ struct SumView {
   const uint16_t* legacyProps;  // per leaf: the prop set the legacy summary reads, or nullptr (leaf.props)
   const uint32_t* cls;          // per prop set its match class as the engine interned it (huge documents,
                                 // up to 65534 sets), or nullptr: the summary kernel derives it in LDS
-  const uint64_t* rmHi;         // per leaf its remove clients 64..127 (huge documents of batches with such
-                                // clients), or nullptr: none
+  const uint64_t* rmHi;         // per leaf its remove clients 64..253 (3 words: 64..127, 128..191, 192..253;
+                                // huge documents of batches with such clients), or nullptr: none
 };
 struct SumRun {
   uint32_t len;    // UTF-16 units of the merged segment
@@ -164,7 +164,8 @@ struct HugeOut {
   uint16_t* legacy;          // annotate-adjust batches: per leaf the getAtSeq(minSeq) prop set, else nullptr
   const uint32_t* cls;       // the engine's match class per prop set (HugeState::pClass)
   unsigned long long* prof;  // [24] shader-clock totals per phase (huge_engine.h HugeDoc::prof)
-  uint64_t* leavesHi;        // per leaf its remove clients 64..127 (bit c - 64; fmt_mt_fetch_rm_clients_hi), or nullptr
+  uint64_t* leavesHi;        // per leaf its remove clients 64..253 (3 words, bit (c - 64) % 64 of word (c - 64) / 64;
+                             // fmt_mt_fetch_rm_clients_hi / _hi2), or nullptr
 };
 size_t hugeLdsBytes();
 hipError_t launchHugeDocs(const fmt_huge::HugeState* states, const fmt_huge::HugeInputs* inputs, const HugeOut* outs,

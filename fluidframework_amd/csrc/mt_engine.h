@@ -318,7 +318,7 @@ class Doc {
   static constexpr int kPropW = C::kWords - 1;
   static constexpr int kPendW = C::kWords;
   static constexpr int kMaxClient = C::kMaxClient;
-  static constexpr int kTopClient = 127;  // the huge tier's writer ceiling (huge_engine.h kMaxClient)
+  static constexpr int kTopClient = 253;  // the huge tier's writer ceiling (huge_engine.h kMaxClient)
   Lane<VR> W[kWords];  // W[f] element r of lane l = field f of leaf 64 r + l
   FMT_LDS Scratch<C>* s;  // (an LDS-space pointer: per-lane LDS addresses stay 32-bit)
   uint16_t* gch = nullptr;  // large tier: the document's text, in its HBM output slab
@@ -2213,7 +2213,7 @@ class Doc {
       const fmt_mt_stamp st = in.stampsAll[inf.rm_first + t];
       rm = uni(st.seq) < rm ? uni(st.seq) : rm;
       const int c = uni(st.client);
-      if (c < 0 || c > kMaxClient) {  // (ids past this tier's sets: a bigger tier, up to the huge tier's 127)
+      if (c < 0 || c > kMaxClient) {  // (ids past this tier's sets: a bigger tier, up to the huge tier's 253)
         fail(c >= 0 && c <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
         return;
       }
@@ -3987,7 +3987,7 @@ class Doc {
       if (loader) {
         if (op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient) loadBodySegment(op, text);
         else fail(op.client <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
-      } else if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63, the huge 127
+      } else if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63, the huge 253
         fail(op.client <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
       else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
         fail(FMT_E_UNSUPPORTED);

@@ -245,7 +245,7 @@ struct fmt_ctx {
   // groups, group records, PropertiesManager records, regenerated ops / text and normalization
   // scratch live in per-document slabs (mt_engine.h LocalTables)
   bool mtLocal = false;
-  bool mtHiClients = false;  // some op or merge-info stamp names a short client id 64..127 (huge tier only)
+  bool mtHiClients = false;  // some op or merge-info stamp names a short client id 64..253 (huge tier only)
   DevBuf<uint32_t> mtLocGroups, mtLocRecs, mtLocPm, mtLocScratch, mtLocRegenCount;
   DevBuf<uint64_t> mtLocOffs;                // 6 offset arrays of n + 1: groups, recs, pm, regen, text, scratch
   DevBuf<fmt_mt_op> mtLocRegen;
@@ -947,14 +947,16 @@ static int setupHugeDoc(fmt_ctx* c, uint64_t textLen, uint32_t nPropsOps, uint32
     S.obSeq = S.obUsed + S.obCap;
     S.obStart = S.obSeq + S.obCap;
   }
-  // remove clients 64..127: the per-leaf-id side table (zeroed) and its per-leaf output
+  // remove clients 64..253: the per-leaf-id side table (zeroed, kHiWords words per id) and its per-leaf
+  // output (kHiOutWords 64-bit words per leaf: ids 64..127, 128..191, 192..253)
   S.hiMask = nullptr;
   O.leavesHi = nullptr;
   if (c->mtHiClients) {
-    if ((e = alloc(2ull * S.idCap * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
-    FMT_HIP(c, hipMemsetAsync(p, 0, 2ull * S.idCap * sizeof(uint32_t), c->stream));
+    constexpr size_t kW = fmt_huge::kHiWords;
+    if ((e = alloc(kW * S.idCap * sizeof(uint32_t), &p)) != hipSuccess) return drop(e);
+    FMT_HIP(c, hipMemsetAsync(p, 0, kW * S.idCap * sizeof(uint32_t), c->stream));
     S.hiMask = static_cast<uint32_t*>(p);
-    if ((e = alloc(O.capLeaves * sizeof(uint64_t), &p)) != hipSuccess) return drop(e);
+    if ((e = alloc(O.capLeaves * fmt_huge::kHiOutWords * sizeof(uint64_t), &p)) != hipSuccess) return drop(e);
     O.leavesHi = static_cast<uint64_t*>(p);
   }
   return FMT_OK;
@@ -2097,17 +2099,33 @@ int fmt_mt_fetch_remove_order(fmt_ctx* c, uint32_t doc, fmt_mt_remove_order* out
   return FMT_OK;
 }
 
-int fmt_mt_fetch_rm_clients_hi(fmt_ctx* c, uint32_t doc, uint64_t* out, uint32_t cap) {
+// word 0 of every leaf (ids 64..127), or words 1 and 2 (ids 128..191, 192..253) with `upper`
+static int fetchRmClientsHi(fmt_ctx* c, uint32_t doc, uint64_t* out, uint32_t cap, bool upper, const char* what) {
   if (c == nullptr || !c->mtLoaded || doc >= c->mtDocs || (out == nullptr && cap > 0))
-    return setErr(c, FMT_E_USAGE, "fmt_mt_fetch_rm_clients_hi: bad arguments");
+    return setErr(c, FMT_E_USAGE, std::string(what) + ": bad arguments");
   fmt_mt_doc_result h;
   FMT_HIP(c, hipMemcpy(&h, c->mtHdr.p + doc, sizeof h, hipMemcpyDeviceToHost));
-  const uint32_t m = h.n_leaves < cap ? h.n_leaves : cap;
+  const uint32_t per = upper ? fmt_huge::kHiOutWords - 1 : 1;
+  const uint32_t m = h.n_leaves < cap / per ? h.n_leaves : cap / per;
   const int32_t hs = doc < c->mtHugeSlot.size() ? c->mtHugeSlot[doc] : -1;
   const uint64_t* src = hs >= 0 ? c->huge[static_cast<size_t>(hs)].out.leavesHi : nullptr;
-  if (src != nullptr && m) FMT_HIP(c, hipMemcpy(out, src, m * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  else if (m) std::memset(out, 0, m * sizeof(uint64_t));  // (the other tiers hold ids 0..63 only)
+  if (src != nullptr && m) {
+    std::vector<uint64_t> all(static_cast<size_t>(m) * fmt_huge::kHiOutWords);
+    FMT_HIP(c, hipMemcpy(all.data(), src, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < m; i++)
+      for (uint32_t k = 0; k < per; k++) out[static_cast<size_t>(i) * per + k] = all[static_cast<size_t>(i) * fmt_huge::kHiOutWords + (upper ? 1 + k : 0)];
+  } else if (m) {
+    std::memset(out, 0, static_cast<size_t>(m) * per * sizeof(uint64_t));  // (the other tiers hold ids 0..63 only)
+  }
   return FMT_OK;
+}
+
+int fmt_mt_fetch_rm_clients_hi(fmt_ctx* c, uint32_t doc, uint64_t* out, uint32_t cap) {
+  return fetchRmClientsHi(c, doc, out, cap, false, "fmt_mt_fetch_rm_clients_hi");
+}
+
+int fmt_mt_fetch_rm_clients_hi2(fmt_ctx* c, uint32_t doc, uint64_t* out, uint32_t cap) {
+  return fetchRmClientsHi(c, doc, out, cap, true, "fmt_mt_fetch_rm_clients_hi2");
 }
 
 int fmt_mt_fetch_legacy_props(fmt_ctx* c, uint32_t doc, uint16_t* out, uint32_t cap) {

@@ -47,7 +47,7 @@ function markerRefType(spec) {
 	if (!Number.isInteger(r) || r < 0 || r > 0xffff) throw new UnsupportedOp("marker refType");
 	return r;
 }
-const MAX_CLIENTS = 127; // small tier 31 writers, large 63, huge 127 (streams.py)
+const MAX_CLIENTS = 253; // small tier 31 writers, large 63, huge 253 (streams.py; 0xFE names NonCollab)
 const RECYCLE_FROM = 32; // fresh short ids up to the small tier's 31 writers, then recycled (streams.py)
 const NOT_REMOVED = 0x7fffffff;
 const MT_OP_BYTES = 32, MAP_OP_BYTES = 16, LEAF_BYTES = 32, DOC_RESULT_BYTES = 48, PROPSET_BYTES = 36;

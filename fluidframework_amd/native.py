@@ -245,6 +245,7 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.fmt_mt_capacity.argtypes = [ctypes.POINTER(U32)] * 3
         for name, args in (("fmt_mt_state_digest", [P, P]), ("fmt_mt_fetch_legacy_props", [P, U32, P, U32]),
                            ("fmt_mt_fetch_rm_clients_hi", [P, U32, P, U32]),
+                           ("fmt_mt_fetch_rm_clients_hi2", [P, U32, P, U32]),
                            ("fmt_map_pending_run", [P, P, U64, P]),
                            ("fmt_mt_fetch_regen", [P, U32, P, U32, P, U32, ctypes.POINTER(U32), ctypes.POINTER(U32)]),
                            ("fmt_map_pending_fetch", [P, P, P, P, U64, ctypes.POINTER(U64)])):
@@ -262,7 +263,7 @@ EXPORTED_SYMBOLS = [
     "fmt_mt_load", "fmt_mt_run", "fmt_mt_fetch_headers", "fmt_mt_fetch_doc", "fmt_mt_fetch_catchup",
     "fmt_mt_fetch_catchup_all", "fmt_mt_fetch_remove_order", "fmt_mt_fetch_numbers", "fmt_mt_capacity",
     "fmt_mt_state_digest", "fmt_mt_fetch_legacy_props", "fmt_map_pending_run", "fmt_map_pending_fetch",
-    "fmt_mt_fetch_regen", "fmt_mt_fetch_rm_clients_hi",
+    "fmt_mt_fetch_regen", "fmt_mt_fetch_rm_clients_hi", "fmt_mt_fetch_rm_clients_hi2",
 ]
 
 
@@ -472,6 +473,15 @@ class Engine:
         out = np.zeros(max(n, 1), dtype=np.uint64)
         self._check(self.L.fmt_mt_fetch_rm_clients_hi(self.h, doc, _ptr(out), n))
         return out[:n]
+
+    def mt_rm_clients_hi2(self, doc: int, hdr=None) -> np.ndarray:
+        """Per leaf, its remove clients with short ids 128..191 and 192..253 ((n, 2): bit c - 128, c - 192)."""
+        if hdr is None:
+            hdr = self.mt_headers(raise_on_failed_docs=False)[doc]
+        n = int(hdr["n_leaves"])
+        out = np.zeros(max(2 * n, 2), dtype=np.uint64)
+        self._check(self.L.fmt_mt_fetch_rm_clients_hi2(self.h, doc, _ptr(out), 2 * n))
+        return out[: 2 * n].reshape(n, 2)
 
     def mt_numbers(self, doc: int) -> np.ndarray:
         """The document's computed annotate-adjust numbers (value ids FMT_MT_VALUE_COMPUTED + index)."""

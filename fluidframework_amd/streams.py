@@ -122,8 +122,9 @@ MAP_SET, MAP_DELETE, MAP_CLEAR = 0, 1, 2
 MAP_KIND_SHIFT = 30
 MAP_VALUE_UNDEFINED = 0x3FFFFFFF
 MAP_ABSENT = 0xFFFFFFFF
-MAX_CLIENTS = 127  # short ids 1..127 (the observer is 0): the small tier keeps 31 writers, the large 63, the
-# huge tier 127 (two mask words per leaf plus a side table for ids 64..127); documents grow to fit
+MAX_CLIENTS = 253  # short ids 1..253 (the observer is 0; 0xFE names NonCollab): the small tier keeps 31 writers,
+# the large 63, the huge tier 253 (two mask words per leaf plus a side table for ids 64..253); documents
+# grow to fit
 # Short ids up to 31 (the small tier's writers) are handed out fresh; past that a new client takes the
 # id of a client whose every stamp is at or below the engine's minSeq (see _DocBuilder.short_client).
 RECYCLE_FROM = 32
@@ -329,7 +330,7 @@ class _DocBuilder:
         """The short id of a long client id (getOrAddShortClientId, client.ts:831-855), noting a
         stamp at `seq`. The reference never forgets a long id; here ids are recycled, because every
         reconnect brings a new clientId and the engine's remove-client sets hold 31 (small tier), 63
-        (large tier) or 127 (huge tier) writers. A short id matters only through stamps above minSeq: a perspective
+        (large tier) or 253 (huge tier) writers. A short id matters only through stamps above minSeq: a perspective
         (refSeq >= minSeq, client) sees a stamp at or below minSeq by its seq whoever made it, and
         merge info (SnapshotV1, catch-up) is written only for stamps above the final minSeq. So once
         every stamp of a client is at or below the engine's minSeq, its id can pass to a new client

@@ -77,7 +77,7 @@ class _LazyValues:
 
 CLIENT_NAMES = [chr(ord("A") + i) for i in range(26)] + [chr(ord("a") + i) for i in range(26)] + [
     chr(ord("0") + i) for i in range(12)
-] + [f"w{i}" for i in range(64, 128)]  # (short ids 64..127: the huge tier's writers)
+] + [f"w{i}" for i in range(64, 254)]  # (short ids 64..253: the huge tier's writers)
 
 
 def conflict_farm(n_docs: int, n_clients: int = 8, ops_per_doc: int = 2000, min_length: int = 0,

@@ -161,8 +161,8 @@ typedef struct fmt_mt_op {
   int32_t pos2;     /* op.pos2; INSERT: props-op id + 1 of a {text, props} segment, <= 0 for a string */
   uint32_t payload; /* INSERT: offset of the text in the UTF-16 arena; ANNOTATE: props-op id */
   uint16_t len;     /* INSERT: text length in UTF-16 units (> 0), low 16 bits (FMT_MT_F_LEN_HI_SHIFT) */
-  uint8_t client;   /* short client id (client.ts:831-855): 1..127 in order of first appearance; ids
-                       64..127 are kept by the huge tier only (the others grow such a document) */
+  uint8_t client;   /* short client id (client.ts:831-855): 1..253 in order of first appearance; ids
+                       64..253 are kept by the huge tier only (the others grow such a document) */
   uint8_t type;     /* FMT_MT_* */
   uint32_t flags;   /* FMT_MT_F_* */
 } fmt_mt_op;
@@ -314,7 +314,7 @@ typedef struct fmt_mt_leaf {
   int32_t ins_seq;     /* insert stamp seq */
   int32_t rm_seq;      /* first (lowest) remove stamp seq, FMT_NOT_REMOVED if not removed */
   uint64_t rm_clients; /* set of short client ids 0..63 holding a remove stamp on this leaf (ids
-                          64..127: fmt_mt_fetch_rm_clients_hi) */
+                          64..127: fmt_mt_fetch_rm_clients_hi, 128..253: fmt_mt_fetch_rm_clients_hi2) */
   uint32_t char_off;   /* offset of this leaf's text in the document's char output */
   uint32_t len;        /* cachedLength (UTF-16 units) */
   int16_t ins_client;  /* insert stamp client */
@@ -586,6 +586,10 @@ int fmt_mt_fetch_legacy_props(fmt_ctx* ctx, uint32_t doc, uint16_t* out, uint32_
  * (getOrAddShortClientId interns without bound, client.ts:831-855). Zero for documents that no such
  * client touched. fmt_mt_state_digest folds them in (tag 10). */
 int fmt_mt_fetch_rm_clients_hi(fmt_ctx* ctx, uint32_t doc, uint64_t* out, uint32_t cap);
+/* The same for short ids 128..253 (round 6): two words per leaf, ids 128..191 (bit c - 128) then
+ * 192..253 (bit c - 192), the first min(n_leaves, cap / 2) leaves. fmt_mt_state_digest folds them in
+ * (tags 11, 12). */
+int fmt_mt_fetch_rm_clients_hi2(fmt_ctx* ctx, uint32_t doc, uint64_t* out, uint32_t cap);
 /* f4: one document's regenerated ops after the last fmt_mt_run, what regeneratePendingOp returned at
  * each FMT_MT_F_REGEN record in order (client.ts:1452-1542; replaces Client.regeneratePendingOp as the
  * host's resubmit source). Each op: type, pos1 / pos2 in the reconnect view, seq = the pending op's

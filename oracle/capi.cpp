@@ -67,7 +67,8 @@ int applyOps(MergeTree* mt, const fmt_mt_op* ops, uint64_t n, const uint16_t* ar
   return FMT_OK;
 }
 
-// rmHi (optional): per leaf, its remove clients with short ids 64..127 (fmt_mt_fetch_rm_clients_hi).
+// rmHi (optional): per leaf, its remove clients with short ids 64..253 as three words (64..127, 128..191,
+// 192..253: fmt_mt_fetch_rm_clients_hi / _hi2).
 void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint32_t capLeaves,
              uint16_t* chars, uint32_t capChars, fmt_mt_propset* props, uint32_t capProps,
              std::vector<uint64_t>* rmHi = nullptr) {
@@ -75,7 +76,7 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
   std::vector<int> blockOf;
   int nBlocks = 0, depth = 0;
   mt->collectLeaves(segs, blockOf, &nBlocks, &depth);
-  if (rmHi) rmHi->assign(segs.size(), 0);
+  if (rmHi) rmHi->assign(3 * segs.size(), 0);
   std::vector<const orc::PropMap*> sets;
   std::vector<uint32_t> setRec;  // first record of each set (a set wider than 8 entries takes several)
   uint32_t nRec = 0;
@@ -106,7 +107,7 @@ void dumpDoc(const MergeTree* mt, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, u
       uint64_t mask = 0;
       for (const auto& r : s->removes) {
         if (r.client >= 0 && r.client < 64) mask |= 1ull << r.client;
-        else if (r.client >= 64 && r.client < 128 && rmHi) (*rmHi)[i] |= 1ull << (r.client - 64);
+        else if (r.client >= 64 && r.client < 256 && rmHi) (*rmHi)[3 * i + (r.client - 64) / 64] |= 1ull << ((r.client - 64) % 64);
       }
       L.rm_clients = mask;
       L.char_off = charOff;
@@ -182,9 +183,10 @@ uint64_t digestOf(const fmt_mt_doc_result& h, const fmt_mt_leaf* leaves, const u
       }
     }
   }
-  if (rmHi)  // remove clients 64..127, on the leaves that have any
-    for (uint32_t i = 0; i < h.n_leaves && i < rmHi->size(); i++)
-      if ((*rmHi)[i] != 0) acc += dgElem(10, i, (*rmHi)[i]);
+  if (rmHi)  // remove clients 64..127 / 128..191 / 192..253 (tags 10 / 11 / 12), on the leaves that have any
+    for (uint32_t i = 0; i < h.n_leaves && 3 * i + 2 < rmHi->size(); i++)
+      for (int k = 0; k < 3; k++)
+        if ((*rmHi)[3 * i + k] != 0) acc += dgElem(10 + k, i, (*rmHi)[3 * i + k]);
   for (uint32_t u = 0; u < h.n_chars; u++) acc += dgElem(8, u, chars[u]);
   return dgMix(acc);
 }

@@ -25,7 +25,7 @@ def _sum(a):
     return int(np.asarray(a, dtype=np.uint64).sum(dtype=np.uint64)) if np.size(a) else 0
 
 
-def state_digest(hdr, leaves, chars, props, rm_hi=None) -> int:
+def state_digest(hdr, leaves, chars, props, rm_hi=None, rm_hi2=None) -> int:
     """Digest of one document from its header, leaves[:n_leaves], chars[:n_chars] and prop sets."""
     u32 = lambda v: int(v) & 0xFFFFFFFF  # noqa: E731
     if int(hdr["status"]) != 0:
@@ -61,6 +61,12 @@ def state_digest(hdr, leaves, chars, props, rm_hi=None) -> int:
         at = np.nonzero(hi)[0]
         if len(at):
             acc += _sum(_elems(10, at.astype(np.uint64), hi[at]))
+    if rm_hi2 is not None:  # remove clients 128..191 (tag 11) and 192..253 (tag 12), (n, 2)
+        hi2 = np.asarray(rm_hi2[:n], dtype=np.uint64).reshape(-1, 2)
+        for k in range(2):
+            at = np.nonzero(hi2[:, k])[0]
+            if len(at):
+                acc += _sum(_elems(11 + k, at.astype(np.uint64), hi2[at, k]))
     nc = int(hdr["n_chars"])
     acc += _sum(_elems(8, np.arange(nc), chars[:nc]))
     return int(_mix(np.uint64(acc & M64)))

@@ -72,7 +72,8 @@ const fmt_mt::AdjustTables* prepareNumbers(const fmt_mt_batch* b) {
   g_adj.pm = g_pm.data();
   return &g_adj;
 }
-// emu_huge_replay_hi: the per-leaf output of remove clients 64..127 for the next replay (or nullptr)
+// emu_huge_replay_hi: the per-leaf output of remove clients 64..253 (kHiOutWords words per leaf) for the
+// next replay (or nullptr)
 uint64_t* g_hiOut = nullptr;
 // emu_huge_resume: the large tier's checkpoint record and result slabs for the next replay (or nullptr)
 const uint32_t* g_ck = nullptr;
@@ -177,7 +178,7 @@ int emu_huge_replay_adj(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hd
   S.obUsed = obl ? obTab.data() + 6ull * obCap : nullptr;
   S.obSeq = obl ? S.obUsed + obCap : nullptr;
   S.obStart = obl ? S.obSeq + obCap : nullptr;
-  std::vector<uint32_t> hiMask(g_hiOut != nullptr ? 2ull * S.idCap : 0, 0u);  // (runtime.cpp: zeroed)
+  std::vector<uint32_t> hiMask(g_hiOut != nullptr ? static_cast<size_t>(kHiWords) * S.idCap : 0, 0u);  // (runtime.cpp: zeroed)
   S.hiMask = g_hiOut != nullptr ? hiMask.data() : nullptr;
   auto lds = std::make_unique<HugeLds>();
   std::memset(lds.get(), 0xCD, sizeof(HugeLds));
@@ -329,8 +330,9 @@ int emu_huge_resume_adj(const fmt_mt_batch* b, uint32_t d, const uint32_t* ck, c
   return st;
 }
 
-// As emu_huge_replay, with the remove-client side table for short ids 64..127 (the runtime allocates
-// it for batches that name such clients): hi[capLeaves] receives each leaf's ids 64..127.
+// As emu_huge_replay, with the remove-client side table for short ids 64..253 (the runtime allocates
+// it for batches that name such clients): hi[capLeaves x kHiOutWords] receives each leaf's ids 64..127,
+// 128..191 and 192..253.
 int emu_huge_replay_hi(const fmt_mt_batch* b, uint32_t d, fmt_mt_doc_result* hdr, fmt_mt_leaf* leaves, uint64_t capLeaves,
                        uint16_t* chars, uint64_t capChars, fmt_mt_propset* props, uint64_t* hi) {
   g_hiOut = hi;

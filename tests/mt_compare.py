@@ -145,9 +145,10 @@ def emu_huge_replay(batch, doc=0, cap_leaves=None, cap_chars=None, tiny_groups=F
     return out
 
 
-def emu_huge_replay_hi(batch, doc=0, tiny_groups=False, cap_props=65534):
-    """(header, leaves, chars, props, remove clients 64..127 per leaf) of document `doc` replayed by
-    the emulated huge engine with its side table for short ids 64..127."""
+def emu_huge_replay_hi(batch, doc=0, tiny_groups=False, cap_props=65534, hi2=False):
+    """(header, leaves, chars, props, remove clients 64..127 per leaf[, (n, 2) remove clients 128..191
+    and 192..253 with hi2]) of document `doc` replayed by the emulated huge engine with its side table
+    for short ids 64..253."""
     from fluidframework_amd.native import DOC_RESULT_DTYPE, LEAF_DTYPE, PROPSET_DTYPE, batch_struct
 
     sd = batch.snapshots[doc] if batch.snapshots is not None else None
@@ -158,14 +159,15 @@ def emu_huge_replay_hi(batch, doc=0, tiny_groups=False, cap_props=65534):
     leaves = np.zeros(cap_leaves, dtype=LEAF_DTYPE)
     chars = np.zeros(cap_chars, dtype="<u2")
     props = np.zeros(cap_props, dtype=PROPSET_DTYPE)
-    hi = np.zeros(cap_leaves, dtype=np.uint64)
+    hi = np.zeros((cap_leaves, 3), dtype=np.uint64)  # (huge_engine.h kHiOutWords per leaf)
     b, keep = batch_struct(batch)
     huge_emu_lib(tiny_groups).emu_huge_replay_hi(ctypes.addressof(b), doc, _p(hdr), _p(leaves), cap_leaves, _p(chars),
                                                  cap_chars, _p(props), _p(hi))
     del keep
     h = hdr[0]
     n = int(h["n_leaves"])
-    return h, leaves[:n], chars[: int(h["n_chars"])], props[: int(h["n_props"])], hi[:n]
+    out = h, leaves[:n], chars[: int(h["n_chars"])], props[: int(h["n_props"])], hi[:n, 0].copy()
+    return out + (hi[:n, 1:].copy(),) if hi2 else out
 
 
 def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0, cap_rm=0):
@@ -257,6 +259,18 @@ def emu_grow_replay(batch, tiny_groups=False, cap_catchup=0, cap_rm=0):
         resumed.append(int(at.value))
     del keep
     return out, resumed
+
+
+def oracle_rm_clients_hi2(batch, doc, n_leaves):
+    """The oracle's remove clients 128..191 and 192..253 per final leaf ((n, 2), from every remove stamp)."""
+    import oracle
+
+    hi = np.zeros((n_leaves, 2), dtype=np.uint64)
+    for leaf, stamps in oracle.mt_removers(batch, doc).items():
+        for client, _, _ in stamps:
+            if 128 <= client < 256:
+                hi[leaf, (client - 128) // 64] |= np.uint64(1) << np.uint64((client - 128) % 64)
+    return hi
 
 
 def oracle_rm_clients_hi(batch, doc, n_leaves):

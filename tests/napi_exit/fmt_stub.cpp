@@ -121,6 +121,9 @@ int fmt_mt_fetch_legacy_props(fmt_ctx* ctx, uint32_t, uint16_t*, uint32_t) {
 int fmt_mt_fetch_rm_clients_hi(fmt_ctx* ctx, uint32_t, uint64_t*, uint32_t) {
   return unsupported(ctx, "fmt_mt_fetch_rm_clients_hi");
 }
+int fmt_mt_fetch_rm_clients_hi2(fmt_ctx* ctx, uint32_t, uint64_t*, uint32_t) {
+  return unsupported(ctx, "fmt_mt_fetch_rm_clients_hi2");
+}
 int fmt_mt_fetch_regen(fmt_ctx* ctx, uint32_t, fmt_mt_op*, uint32_t, uint16_t*, uint32_t, uint32_t*, uint32_t*) {
   return unsupported(ctx, "fmt_mt_fetch_regen");
 }

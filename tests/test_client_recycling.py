@@ -100,15 +100,15 @@ def test_emulated_engine_matches_oracle_on_recycled_ids(orc, farms):
             summary.v1_summary(oh[d], ol[d], oc[d], op[d], chd.keys, chd.values, chd.clients[d], want), d
 
 
-def test_more_than_127_concurrent_writers_is_refused():
-    """Recycling needs a client whose stamps are all at or below minSeq: 128 writers with stamps above
-    it cannot share 127 ids (the huge tier's writer ceiling; tests/test_writer_ceiling.py)."""
+def test_more_than_253_concurrent_writers_is_refused():
+    """Recycling needs a client whose stamps are all at or below minSeq: 254 writers with stamps above
+    it cannot share 253 ids (the huge tier's writer ceiling since round 6; tests/test_writer_ceiling.py)."""
     from fluidframework_amd.streams import MergeTreeStreamBuilder, UnsupportedOp
 
     b = MergeTreeStreamBuilder()
     d = b.begin_doc("x", observer="o")
     with pytest.raises(UnsupportedOp):
-        for k in range(128):
+        for k in range(254):
             d.add_message({"clientId": f"c{k}", "sequenceNumber": k + 1, "referenceSequenceNumber": 0,
                            "minimumSequenceNumber": 0, "type": "op",
                            "contents": {"pos1": 0, "seg": "a", "type": 0}})

@@ -182,7 +182,7 @@ def test_huge_loaded_markers(orc, engine):
 
 def test_unsupported_huge_document_fails_alone(orc, engine):
     """A summary-loaded document past the large tier that asks for something the huge tier does not
-    replay (here a writer with short id 200: the huge tier keeps ids up to 127) fails alone, with
+    replay (here a writer with short id 255: the huge tier keeps ids up to 253) fails alone, with
     FMT_E_UNSUPPORTED in its own header; one holding a loader segment (FMT_MT_F_LOADSEG, which the
     huge tier replays since round 5) equals the oracle; the ordinary and huge documents beside them
     replay as in a batch without them."""
@@ -202,7 +202,7 @@ def test_unsupported_huge_document_fails_alone(orc, engine):
     ops["flags"][first_insert] |= MT_F_LOADSEG
     ops["pos1"][first_insert] = 0  # (merge-info row 0)
     o1 = int(batch.doc_op_offsets[farm.n_docs + 2])
-    ops["client"][o1 + 10] = 200  # (a writer past the huge tier's 127)
+    ops["client"][o1 + 10] = 255  # (a writer past the huge tier's 253; 254 names NonCollab)
     batch = dataclasses.replace(batch, ops=ops, snapshot_info=info, snapshot_stamps=np.zeros(1, dtype=STAMP_DTYPE))
     engine.mt_load(batch)
     engine.mt_run()
