@@ -211,6 +211,10 @@ VARIANTS = {
     "locCL": [("mergetree_local.hip", "#define FMT_LOCAL_PATH 2", "#define FMT_LOCAL_PATH 0")],
     "locSL": [("mergetree_local.hip", "#define FMT_LOCAL_PATH 2", "#define FMT_LOCAL_PATH 1")],
     "locCSL": [],
+    # the local small tier at 1 wave/SIMD (512 registers with AGPRs: no spills) instead of 2
+    "locW1": [("mergetree_local.hip",
+               "return launchTier<false, S, false, kMtWavesLocal, 2, false, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);",
+               "return launchTier<false, S, false, kMtWavesLocal, 1, false, true>(batch, out, docList, count, esc, numCUs, stream, nullptr, n1);")],
     "t3lat": [],  # (working tree: huge tier with its block count / flags loaded beside the leaf fields)
     # huge tier without its per-phase shader-clock reads (ProfScope's s_memtime pairs)
     "t3noclk": [("huge_engine.h", "    return __builtin_amdgcn_s_memtime();", "    return 0;")],
