@@ -1030,12 +1030,12 @@ int fmt_mt_load(fmt_ctx* c, const fmt_mt_batch* b) {
     if (S.err != nullptr && (firstBad == nullptr || S.errAt < firstBad->errAt)) firstBad = &S;
   }
   if (firstBad != nullptr) return setErr(c, firstBad->errCode, firstBad->err);
-  // f4 batches run the Loc variants (annotate-adjust too since round 6): features they do not combine
-  // with are refused
-  if (local && (obliterates || catchupOps || rmOrderOps || b->relpos != nullptr || b->snapshot_info != nullptr))
+  // f4 batches run the Loc variants (annotate-adjust and remote ops with relative positions too since
+  // round 6): features they do not combine with are refused
+  if (local && (obliterates || catchupOps || rmOrderOps || b->snapshot_info != nullptr))
     return setErr(c, FMT_E_UNSUPPORTED,
-                  "local-client records (FMT_MT_F_LOCAL_ANY) do not combine with obliterate, catch-up, remove order, "
-                  "relative positions or SnapshotV1 merge info");
+                  "local-client records (FMT_MT_F_LOCAL_ANY) do not combine with obliterate, catch-up, remove order "
+                  "or SnapshotV1 merge info");
   if (b->snapshots) {
     for (uint32_t d = 0; d < n; d++) {
       const fmt_mt_snapshot_doc& sd = b->snapshots[d];

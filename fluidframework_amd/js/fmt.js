@@ -228,7 +228,7 @@ class MergeTreeDocBuilder {
 		const ack = this.local && client === 0;
 		if (this.owner.keepMessages) this.messages.push({ message: msg, firstOp: this.nOps, count: members.length });
 		members.forEach((op, k) => {
-			this.noteOp(op);
+			if (!ack) this.noteOp(op); // (an ack repeats the local op noted at its submission)
 			let flags = k > 0 ? FMT_MT_F_GROUP_CONT : 0;
 			if (ack) {
 				if (op === null || this.pending.length === 0 || this.pending[0][0] !== op.type) {

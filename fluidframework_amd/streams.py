@@ -379,7 +379,8 @@ class _DocBuilder:
         if self.owner.keep_messages:
             self.messages.append((msg, len(self.ops), len(members)))
         for k, op in enumerate(members):
-            self._note_op(op)
+            if not ack:  # (an ack repeats the local op noted at its submission: the same marker)
+                self._note_op(op)
             rec = self.owner._pack(op, seq, ref, msn, client)
             if k > 0:  # later members of a GROUP message (FMT_MT_F_GROUP_CONT)
                 rec = rec[:-1] + (rec[-1] | 1,)

@@ -267,6 +267,21 @@ void orc_mt_set_adjusts(void* h, const fmt_mt_adjust* adjusts, uint32_t nAdjusts
   mt->nValues = valueNum ? nValues : 0u;
 }
 
+// Legacy relative positions for the ops applied next to the interactive document: the batch's
+// relpos table (fmt_mt_relpos rows) and the key id of "markerId".
+void orc_mt_set_relpos(void* h, const fmt_mt_relpos* relpos, uint32_t n, uint32_t markerIdKey) {
+  MergeTree* mt = static_cast<MergeTree*>(h);
+  mt->relpos = relpos;
+  mt->nRelpos = n;
+  mt->markerIdKey = markerIdKey;
+}
+
+// 1 when a marker whose "markerId" is value id `id` is in the interactive document and not removed
+// (getMarkerFromId, mergeTree.ts:1450-1453: a locally removed one counts as removed), else 0.
+int orc_mt_marker_present(void* h, uint32_t id) {
+  return static_cast<const MergeTree*>(h)->markerPresent(id) ? 1 : 0;
+}
+
 // Returns the text length; copies min(len, cap) UTF-16 units.
 // f4: the local length (getLength, client.ts:1696) and the ops REGEN events produced since the last
 // take (their insert text in `text`, payloads relative to it); *nOps / *nText are the full counts. With

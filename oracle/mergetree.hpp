@@ -328,6 +328,11 @@ class MergeTree {
   uint32_t markerIdKey = FMT_MT_NO_MARKER;
 
   // Readouts.
+  // getMarkerFromId (mergeTree.ts:1450-1453) finds a marker with this markerId value id (not removed).
+  bool markerPresent(uint32_t id) const {
+    const fmt_mt_relpos rp{id, 0, 0, 0};
+    return posFromRelativePos(rp, Perspective{true, 0, 0}) >= 0;
+  }
   std::u16string getText() const;     // MergeTreeTextHelper.ts:28-87 (local perspective)
   int getLocalLength() const;
   void collectLeaves(std::vector<const Seg*>& out, std::vector<int>& blockOfLeaf,

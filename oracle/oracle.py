@@ -38,6 +38,9 @@ def lib() -> ctypes.CDLL:
         L.orc_mt_apply_ops.argtypes = [P, P, ctypes.c_uint64, P, P, P]
         L.orc_mt_set_adjusts.argtypes = [P, P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_mt_set_adjusts.restype = None
+        L.orc_mt_set_relpos.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_mt_set_relpos.restype = None
+        L.orc_mt_marker_present.argtypes = [P, ctypes.c_uint32]
         L.orc_mt_text.argtypes = [P, P, ctypes.c_int]
         L.orc_mt_dump.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.orc_mt_summary.argtypes = [P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P,
@@ -125,6 +128,15 @@ class MergeTreeDoc:
         applied next; the arrays must outlive those calls (kept here)."""
         self._adj = (np.ascontiguousarray(adjusts), np.ascontiguousarray(value_num, dtype=np.float64))
         lib().orc_mt_set_adjusts(self.h, _ptr(self._adj[0]), len(self._adj[0]), _ptr(self._adj[1]), len(self._adj[1]))
+
+    def set_relpos(self, relpos: np.ndarray, marker_id_key: int):
+        """The relpos table (RELPOS_DTYPE) and "markerId" key id for the ops applied next (kept here)."""
+        self._rel = np.ascontiguousarray(relpos)
+        lib().orc_mt_set_relpos(self.h, _ptr(self._rel), len(self._rel), marker_id_key)
+
+    def marker_present(self, marker_value_id: int) -> bool:
+        """A marker with that markerId value is in the document and not removed (locally or not)."""
+        return bool(lib().orc_mt_marker_present(self.h, marker_value_id))
 
     def local_length(self) -> int:
         """getLength() from the local perspective (client.ts:1696)."""

@@ -110,6 +110,9 @@ class _Participant:
             adj = self.farm.adjust_tables()
             if adj is not None:
                 self.orc.set_adjusts(*adj)
+            rel = self.farm.relpos_tables()
+            if rel is not None:
+                self.orc.set_relpos(*rel)
             self.orc.apply(recs, arena, poff, pkv)
             self.applied = len(self.doc.ops)
 
@@ -122,8 +125,13 @@ class LocalFarm:
     """A generated multi-client farm; every participant's own event stream is one document."""
 
     def __init__(self, seed, n_clients=4, initial="", min_length=8, keys=("a", "b", "c"), markers=True,
-                 builder: MergeTreeStreamBuilder | None = None, new_ids=False, adjust=False):
+                 builder: MergeTreeStreamBuilder | None = None, new_ids=False, adjust=False, legacy=False):
         self.rnd = random.Random(seed)
+        # legacy: a writer outside the farm ("R", an older client) whose sequenced inserts name their
+        # position relative to a marker (relativePos1, client.ts:758-767 / mergeTree.ts:1462-1483)
+        self.legacy = legacy
+        self.legacy_ops = 0
+        self.marker_ids: list[str] = []  # markerIds of the markers every participant has sequenced
         # adjust: half the annotates adjust the numeric key "w" (annotateAdjustRangeLocal, client.ts:286),
         # which raw annotates also set (numbers and a string, which an adjust reads as 0)
         self.adjust = adjust
@@ -162,6 +170,53 @@ class LocalFarm:
             self._props = (np.asarray(off, dtype=np.uint32), np.asarray(kv, dtype=np.uint32))
             self._props_n = len(self.b.props_list)
         return self._arena, self._props[0], self._props[1]
+
+    def relpos_tables(self):
+        """(RELPOS_DTYPE table, "markerId" key id) of the builder so far, or None without any."""
+        from fluidframework_amd.streams import MARKER_ID_KEY, NO_MARKER, RELPOS_DTYPE
+
+        if not self.b.relpos and not self.legacy:
+            return None
+        # (a legacy farm from its first op: markers register under the markerId key as they arrive)
+        key = (len(self.b.relpos), self.b.keys.ids.get(MARKER_ID_KEY, NO_MARKER))
+        if getattr(self, "_rel_key", None) != key:
+            self._rel = (np.array(self.b.relpos or [(NO_MARKER, 0, 0, 0)], dtype=RELPOS_DTYPE), key[1])
+            self._rel_key = key
+        return self._rel
+
+    def legacy_op(self) -> bool:
+        """R's relativePos1 insert next to a marker that every participant still holds unremoved
+        (getMarkerFromId, mergeTree.ts:1450-1453: else the op names no marker), sequenced at once at
+        the current seq (it reaches the service before anything in flight)."""
+        from fluidframework_amd.streams import js_json
+
+        r = self.rnd
+        for _ in range(4):
+            if not self.marker_ids:
+                return False
+            mid = r.choice(self.marker_ids)
+            vid = self.b.values.ids.get(js_json(mid))
+            if vid is None:
+                return False
+            ok = True
+            for p in self.parts:
+                p.sync()
+                ok = ok and p.orc.marker_present(vid)
+            if ok:
+                break
+        else:
+            return False
+        self.seq += 1
+        msg = {"clientId": "R", "sequenceNumber": self.seq, "referenceSequenceNumber": self.seq - 1,
+               "minimumSequenceNumber": self.msn, "type": "op",
+               "contents": {"type": MT_INSERT, "relativePos1": {"id": mid, "before": r.random() < 0.5},
+                            "seg": "rr"}}
+        for q in self.parts:
+            self.log.append((q.index, "add_message", msg))
+            q.doc.add_message(msg)
+            q.cur_seq = self.seq
+        self.legacy_ops += 1
+        return True
 
     def adjust_tables(self):
         """(ADJUST_DTYPE rows, value numbers) of the builder so far, or None without adjusts."""
@@ -228,6 +283,8 @@ class LocalFarm:
             q.doc.add_message(msg)
             q.cur_seq = self.seq
         p.pending.pop(0)
+        if op["type"] == MT_INSERT and isinstance(op.get("seg"), dict) and "marker" in op["seg"]:
+            self.marker_ids.append(op["seg"]["props"]["markerId"])
 
     def rollback(self, p: _Participant) -> bool:
         """Roll back p's newest pending op if it is still unsent (the reference rolls back ops of a
@@ -307,6 +364,8 @@ class LocalFarm:
                 self.rollback(r.choice(writers))
             elif x < p_submit + p_rollback + p_reconnect:
                 self.reconnect(r.choice(writers))
+            elif self.legacy and x < p_submit + p_rollback + p_reconnect + 0.1:
+                self.legacy_op()
             else:
                 self.sequence_one()
         if drain:

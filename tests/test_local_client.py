@@ -186,6 +186,36 @@ def farms_long():
 
 
 @pytest.fixture(scope="module")
+def farms_legacy():
+    """Farms with an older client outside them ("R") whose inserts name their position relative to a
+    marker (relativePos1, client.ts:758-767 / mergeTree.ts:1462-1483), between the local clients'
+    submissions, acks, rollbacks and reconnects: each local client resolves them in R's perspective,
+    where its own pending segments are invisible (round 6: relative positions in local batches)."""
+    batch, farms = local_farm_batch(range(30, 35), steps=500, n_clients=5, min_length=120, legacy=True)
+    assert batch.relpos is not None and sum(f.legacy_ops for f in farms) >= 40
+    return batch, farms
+
+
+def test_oracle_local_farms_with_relative_positions_converge(orc, farms_legacy):
+    batch, farms = farms_legacy
+    for f in farms:
+        texts = f.texts()
+        assert all(t == texts[0] for t in texts), texts
+        assert "rr" in texts[0]
+
+
+def test_emulated_engine_local_farms_with_relative_positions_match_oracle(orc, farms_legacy):
+    batch, _ = farms_legacy
+    assert _check_engine_vs_oracle(orc, batch, emu_replay_local(batch), emu_regen) > 20
+
+
+@pytest.mark.gpu
+def test_gpu_local_farms_with_relative_positions_match_oracle(orc, engine, farms_legacy):
+    batch, _ = farms_legacy
+    assert _check_engine_vs_oracle(orc, batch, _gpu(engine, batch), engine.mt_regen) > 20
+
+
+@pytest.fixture(scope="module")
 def farms_long_adjust():
     """Local adjust farms past the small tier's 6144 units (initial text 6200): the large tier's Adj
     local variant replays them (after the small tier's reports FMT_E_CAPACITY), and one that fits."""
