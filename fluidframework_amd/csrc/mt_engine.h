@@ -3984,14 +3984,30 @@ class Doc {
           continue;
         }
       }
+      // The op's checks first: a failing one leaves the loop at once, so its path (leaf rows unchanged)
+      // does not join the ones that change the rows, where the compiler would keep both copies of them
+      // live (the obliterate small tier spilled 16 VGPRs per op at that join).
+      int bad = FMT_OK;
       if (loader) {
-        if (op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient) loadBodySegment(op, text);
-        else fail(op.client <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
-      } else if (op.client > kMaxClient)  // the small tier's 31 writers: the large tier takes 63, the huge 253
-        fail(op.client <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED);
-      else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED)))
-        fail(FMT_E_UNSUPPORTED);
-      else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) fail(FMT_E_DATA);
+        if (!(op.client == FMT_MT_CLIENT_NONCOLLAB || op.client <= kMaxClient))
+          bad = op.client <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED;
+      } else if (op.client > kMaxClient) {  // the small tier's 31 writers: the large tier takes 63, the huge 253
+        bad = op.client <= kTopClient ? FMT_E_CAPACITY : FMT_E_UNSUPPORTED;
+      } else if (op.type > FMT_MT_ANNOTATE && !(Ob && (op.type == FMT_MT_OBLITERATE || op.type == FMT_MT_OBLITERATE_SIDED))) {
+        bad = FMT_E_UNSUPPORTED;
+      } else if (op.type == FMT_MT_ANNOTATE && op.payload >= in.nPropsOps) {
+        bad = FMT_E_DATA;
+      }
+      // (Rm variants keep the checks' failures on the joined path: the early exit costs them spills)
+      if constexpr (!Rm) {
+        if (bad != FMT_OK) {
+          fail(bad);
+          failSeq = op.seq;
+          break;
+        }
+      }
+      if (bad != FMT_OK) fail(bad);
+      else if (loader) loadBodySegment(op, text);
       else if (Loc && (op.flags & FMT_MT_F_ACK)) ackOp(op);
       else if ((op.flags & (FMT_MT_F_REL1 | FMT_MT_F_REL2)) == 0 || resolveRelative(op)) applyOp(op, text);
       if constexpr (Rm) {

@@ -19,6 +19,14 @@ EMU_PATH = os.path.join(HERE, "_build", "libmt_emu.so")
 _emu = None
 
 
+def _build_atomic(cmd, out, src):
+    """Compile to a private file, then rename over `out`: parallel test workers that find the library
+    stale at once never load one another's half-written output."""
+    tmp = f"{out}.{os.getpid()}.tmp"
+    subprocess.run(cmd + ["-o", tmp, src], check=True)
+    os.replace(tmp, out)
+
+
 def emu_lib():
     global _emu
     if _emu is None:
@@ -26,8 +34,7 @@ def emu_lib():
         deps = [src, os.path.join(HERE, "..", "include", "fmt.h")] + [os.path.join(HERE, "..", "fluidframework_amd", "csrc", f) for f in ("mt_engine.h", "wave.h", "huge_ckpt.h", "adjust.h")]
         if not os.path.exists(EMU_PATH) or os.path.getmtime(EMU_PATH) < max(os.path.getmtime(d) for d in deps):
             os.makedirs(os.path.dirname(EMU_PATH), exist_ok=True)
-            subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas", "-o",
-                            EMU_PATH, src], check=True)
+            _build_atomic(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas"], EMU_PATH, src)
         L = ctypes.CDLL(EMU_PATH)
         L.emu_mt_replay.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
                                                               ctypes.c_void_p, ctypes.c_uint32]
@@ -61,8 +68,8 @@ def huge_emu_lib(tiny_groups=False):
         if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(d) for d in deps):
             os.makedirs(os.path.dirname(path), exist_ok=True)
             extra = ["-DFMT_HUGE_SLOTCAP=16", "-DFMT_HUGE_FILL=8"] if tiny_groups else []
-            subprocess.run(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
-                            "-DFMT_HUGE_CHECK_BUILD"] + extra + ["-o", path, src], check=True)
+            _build_atomic(["g++", "-O2", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+                           "-DFMT_HUGE_CHECK_BUILD"] + extra, path, src)
         L = ctypes.CDLL(path)
         L.emu_huge_replay.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
