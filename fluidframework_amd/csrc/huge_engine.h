@@ -60,6 +60,8 @@ constexpr int kPropCap = 65534;       // interned prop sets per document (ids fi
 constexpr int kPropLds = 2048;        // match classes of the first sets cached in LDS
 constexpr uint32_t kPropHash = 1u << 17;  // buckets per prop-set hash table (exact content, match class)
 constexpr int kPropWords = 1 + FMT_MT_PROPS_MAX;  // a prop set in HBM: n, kv[]
+constexpr int kKeyChunks = FMT_MT_PROPS_KEYS_MAX / 64;  // working-set slot k = chunk k / 64, lane k % 64
+static_assert(FMT_MT_PROPS_KEYS_MAX % 64 == 0, "prop-set slots come in whole waves");
 constexpr int kFill = FMT_HUGE_FILL;  // leaf blocks per group at load
 // short client ids 0..253 (0xFE: FMT_MT_CLIENT_NONCOLLAB); remove-client sets: two mask words for ids
 // 0..63 + HugeState::hiMask, kHiWords per leaf id for ids 64..253 (round 6: was 127, two words)
@@ -223,9 +225,9 @@ struct HugeLds {
   int32_t sLen[kSlotCap];        // the group being searched: view length per slot
   uint32_t sBlk[kSlotCap];
   HeapEnt heap[kHeapCap + 1];    // 1-based (heap.ts)
-  uint32_t tmp[256];
+  uint32_t tmp[128];             // (indices < 128: a split's counts [0, 64) and sources [64, 128))
   uint16_t pClass[kPropLds];     // S.pClass of the first kPropLds sets
-  uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (lane k = entry k)
+  uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (slot k = entry k)
   int32_t cmd[8];                // pass command from wave 0 to the helper waves (HugeDoc::PassCmd)
 };
 
@@ -1473,14 +1475,20 @@ class HugeDocT {
   }
   FMT_DEV bool propsMatch(uint32_t a, uint32_t b) const { return a == b || uni(propClass(a)) == uni(propClass(b)); }
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
-  // The working set lives in LDS (kvWork, lane k = entry k); a set wider than FMT_MT_PROPS_MAX entries
-  // takes consecutive records (fmt.h fmt_mt_propset).
+  // The working set lives in LDS (kvWork, slot k = lane k % 64 of chunk k / 64; slots past the set's
+  // count are never read); a set wider than FMT_MT_PROPS_MAX entries takes consecutive records (fmt.h
+  // fmt_mt_propset).
   FMT_DEV uint32_t setKv(uint32_t p, uint32_t k) const {
     return rd(S.props + ((static_cast<size_t>(p) + k / FMT_MT_PROPS_MAX) * kPropWords + 1 + k % FMT_MT_PROPS_MAX));
   }
   FMT_DEV uint32_t loadWork(uint32_t old) {
     const uint32_t cnt = old != kNoProps ? ldu(S.props + old * kPropWords) : 0u;
-    FOR_LANES(l) { L->kvWork[l] = l < static_cast<int>(cnt) ? setKv(old, static_cast<uint32_t>(l)) : 0u; }
+    for (int c = 0; c < kKeyChunks && c * 64 < static_cast<int>(cnt); c++) {
+      FOR_LANES(l) {
+        const int k = c * 64 + l;
+        if (k < static_cast<int>(cnt)) L->kvWork[k] = setKv(old, static_cast<uint32_t>(k));
+      }
+    }
     waveSync();
     return cnt;
   }
@@ -1492,10 +1500,16 @@ class HugeDocT {
     const uint32_t a = ldu(in.propsOff + opId), b = ldu(in.propsOff + opId + 1);
     for (uint32_t t = a; t < b; t++) {
       uint32_t e = ldu(in.propsKv + t);
-      Lane<bool> hit;
-      FOR_LANES(l) { LANE(hit) = l < static_cast<int>(cnt) && (L->kvWork[l] >> 16) == (e >> 16); }
-      const uint64_t m = ballot(hit);
-      const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
+      uint32_t pos = cnt;
+      for (int c = 0; c < kKeyChunks && pos == cnt && c * 64 < static_cast<int>(cnt); c++) {
+        Lane<bool> hit;
+        FOR_LANES(l) {
+          const int k = c * 64 + l;
+          LANE(hit) = k < static_cast<int>(cnt) && (L->kvWork[k] >> 16) == (e >> 16);
+        }
+        const uint64_t m = ballot(hit);
+        if (m) pos = static_cast<uint32_t>(c * 64 + ctz64(m));
+      }
       if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {
         if constexpr (Adj) {
           if (!adjSite || in.adj == nullptr || ++t >= b) {
@@ -1515,19 +1529,25 @@ class HugeDocT {
         }
       }
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
-        if (pos < cnt) {
-          Lane<uint32_t> v;
-          FOR_LANES(l) { LANE(v) = (l < kKeysMax - 1 && l >= static_cast<int>(pos)) ? L->kvWork[l + 1] : 0u; }
-          waveSync();
-          FOR_LANES(l) {
-            if (l >= static_cast<int>(pos) && l + 1 < static_cast<int>(cnt)) L->kvWork[l] = LANE(v);
-            if (l + 1 == static_cast<int>(cnt)) L->kvWork[l] = 0u;
+        if (pos < cnt) {  // entries pos+1 .. cnt-1 move down one slot, a chunk at a time in slot order
+          for (int c = static_cast<int>(pos) / 64; c < kKeyChunks && c * 64 < static_cast<int>(cnt); c++) {
+            Lane<uint32_t> v;
+            FOR_LANES(l) {
+              const int k = c * 64 + l;
+              LANE(v) = (k < kKeysMax - 1 && k >= static_cast<int>(pos)) ? L->kvWork[k + 1] : 0u;
+            }
+            waveSync();
+            FOR_LANES(l) {
+              const int k = c * 64 + l;
+              if (k >= static_cast<int>(pos) && k + 1 < static_cast<int>(cnt)) L->kvWork[k] = LANE(v);
+            }
+            waveSync();
           }
           cnt--;
         }
       } else if (pos < cnt) {
         FOR_LANES(l) {
-          if (l == static_cast<int>(pos)) L->kvWork[l] = e;
+          if (l == static_cast<int>(pos % 64)) L->kvWork[pos] = e;
         }
       } else {
         if (cnt >= static_cast<uint32_t>(kKeysMax)) {
@@ -1535,7 +1555,7 @@ class HugeDocT {
           return kNoProps;
         }
         FOR_LANES(l) {
-          if (l == static_cast<int>(cnt)) L->kvWork[l] = e;
+          if (l == static_cast<int>(cnt % 64)) L->kvWork[cnt] = e;
         }
         cnt++;
       }
@@ -1547,24 +1567,37 @@ class HugeDocT {
   FMT_DEV uint32_t internWork(uint32_t cnt) {
     // Interned already? Sets are found through two hash tables in HBM: one keyed by the ordered
     // entries (the same set), one by the entries in any order (its match class).
-    Lane<uint32_t> ho, hu;
-    FOR_LANES(l) {
-      const bool on = l < static_cast<int>(cnt);
-      const uint32_t e = on ? L->kvWork[l] : 0u;
-      LANE(ho) = on ? mix32(e ^ (0x9E3779B9u * static_cast<uint32_t>(l + 1))) : 0u;
-      LANE(hu) = on ? mix32(e) : 0u;
+    uint32_t so = 0, su = 0;
+    for (int c = 0; c < kKeyChunks && c * 64 < static_cast<int>(cnt); c++) {
+      Lane<uint32_t> ho, hu;
+      FOR_LANES(l) {
+        const int k = c * 64 + l;
+        const bool on = k < static_cast<int>(cnt);
+        const uint32_t e = on ? L->kvWork[k] : 0u;
+        LANE(ho) = on ? mix32(e ^ (0x9E3779B9u * static_cast<uint32_t>(k + 1))) : 0u;
+        LANE(hu) = on ? mix32(e) : 0u;
+      }
+      uint32_t to, tu;
+      waveExclusiveSum(ho, &to);
+      waveExclusiveSum(hu, &tu);
+      so += to;
+      su += tu;
     }
-    uint32_t so, su;
-    waveExclusiveSum(ho, &so);
-    waveExclusiveSum(hu, &su);
     const uint32_t bo = mix32(so + cnt) & (kPropHash - 1);
     const uint32_t bu = kPropHash + (mix32(su ^ (cnt * 0x85EBCA6Bu)) & (kPropHash - 1));
     for (uint32_t p = ldu(S.pHead + bo); p != 0; p = ldu(S.pNext + 2 * (p - 1))) {
       const uint32_t q = p - 1;
       if (ldu(S.props + q * kPropWords) != cnt) continue;
-      Lane<bool> diff;
-      FOR_LANES(l) { LANE(diff) = l < static_cast<int>(cnt) && setKv(q, static_cast<uint32_t>(l)) != L->kvWork[l]; }
-      if (ballot(diff) == 0) return q;
+      bool same = true;
+      for (int c = 0; same && c * 64 < static_cast<int>(cnt); c++) {
+        Lane<bool> diff;
+        FOR_LANES(l) {
+          const int k = c * 64 + l;
+          LANE(diff) = k < static_cast<int>(cnt) && setKv(q, static_cast<uint32_t>(k)) != L->kvWork[k];
+        }
+        same = ballot(diff) == 0;
+      }
+      if (same) return q;
     }
     const int rec = cnt > FMT_MT_PROPS_MAX ? static_cast<int>((cnt + FMT_MT_PROPS_MAX - 1) / FMT_MT_PROPS_MAX) : 1;
     if (nProps + rec > kPropCap) {
@@ -1576,27 +1609,36 @@ class HugeDocT {
     for (uint32_t p = cnt > 0 ? ldu(S.pHead + bu) : 0u; p != 0 && cls == id; p = ldu(S.pNext + 2 * (p - 1) + 1)) {
       const uint32_t q = p - 1;                //  only the first set of each class)
       if (ldu(S.props + q * kPropWords) != cnt) continue;
-      Lane<bool> miss;
-      FOR_LANES(l) {
-        bool found = l >= static_cast<int>(cnt);
-        for (uint32_t j = 0; !found && j < cnt; j++) found = setKv(q, j) == L->kvWork[l];
-        LANE(miss) = !found;
+      bool all = true;
+      for (int c = 0; all && c * 64 < static_cast<int>(cnt); c++) {
+        Lane<bool> miss;
+        FOR_LANES(l) {
+          const int k = c * 64 + l;
+          bool found = k >= static_cast<int>(cnt);
+          for (uint32_t j = 0; !found && j < cnt; j++) found = setKv(q, j) == L->kvWork[k];
+          LANE(miss) = !found;
+        }
+        all = ballot(miss) == 0;
       }
-      if (ballot(miss) == 0) cls = q;
+      if (all) cls = q;
     }
     const uint32_t headO = ldu(S.pHead + bo), headU = ldu(S.pHead + bu);
-    FOR_LANES(l) {
-      const int q = l / FMT_MT_PROPS_MAX, k = l % FMT_MT_PROPS_MAX;
-      if (q < rec) {
-        const size_t r = static_cast<size_t>(id + q) * kPropWords;
-        if (k == 0) {
-          const uint32_t c = q == 0 ? cls : 0xFFFEu;
-          S.props[r] = q == 0 ? cnt : FMT_MT_PROPS_CONT;
-          S.pClass[id + q] = c;
-          if (id + q < static_cast<uint32_t>(kPropLds)) L->pClass[id + q] = static_cast<uint16_t>(c);
+    for (int ch = 0; ch * 64 < rec * FMT_MT_PROPS_MAX; ch++) {  // (slots past cnt: unused entries, 0)
+      FOR_LANES(l) {
+        const int j = ch * 64 + l, q = j / FMT_MT_PROPS_MAX, k = j % FMT_MT_PROPS_MAX;
+        if (q < rec) {
+          const size_t r = static_cast<size_t>(id + q) * kPropWords;
+          if (k == 0) {
+            const uint32_t c = q == 0 ? cls : 0xFFFEu;
+            S.props[r] = q == 0 ? cnt : FMT_MT_PROPS_CONT;
+            S.pClass[id + q] = c;
+            if (id + q < static_cast<uint32_t>(kPropLds)) L->pClass[id + q] = static_cast<uint16_t>(c);
+          }
+          S.props[r + 1 + k] = j < static_cast<int>(cnt) ? L->kvWork[j] : 0u;
         }
-        S.props[r + 1 + k] = L->kvWork[l];
       }
+    }
+    FOR_LANES(l) {
       if (l == 0) {
         S.pNext[2 * id] = headO;
         S.pHead[bo] = id + 1;
@@ -3789,8 +3831,11 @@ class HugeDocT {
         fail(FMT_E_DATA);
         return 0;
       }
-      FOR_LANES(l) {
-        if (l < static_cast<int>(cnt)) L->kvWork[l] = rd(&in.ckProps[p + l / FMT_MT_PROPS_MAX].kv[l % FMT_MT_PROPS_MAX]);
+      for (int c = 0; c * 64 < static_cast<int>(cnt); c++) {
+        FOR_LANES(l) {
+          const int k = c * 64 + l;
+          if (k < static_cast<int>(cnt)) L->kvWork[k] = rd(&in.ckProps[p + k / FMT_MT_PROPS_MAX].kv[k % FMT_MT_PROPS_MAX]);
+        }
       }
       waveSync();
       const uint32_t id = internWork(cnt);

@@ -48,7 +48,9 @@ namespace fmt_mt {
 constexpr int kMaxNodes = 8;         // MaxNodesInBlock (mergeTreeNodes.ts:248)
 constexpr int kGranularity = 256;    // TextSegmentGranularity (textSegment.ts:21)
 constexpr int kObCap = 64;           // obliterates alive in the collab window (seq > minSeq)
-constexpr int kKeysMax = FMT_MT_PROPS_KEYS_MAX;  // keys of one prop set (one working-set lane each)
+constexpr int kKeysMax = FMT_MT_PROPS_KEYS_MAX;  // keys of one prop set (working-set slots)
+constexpr int kKeyChunks = kKeysMax / 64;        // slot k = chunk k / 64, lane k % 64
+static_assert(kKeysMax % 64 == 0, "prop-set slots come in whole waves");
 constexpr int32_t kNotRemoved = 0x7fffffff;
 constexpr int kCapacityFinal = -33;  // internal status (small tier only), never leaves the runtime
 constexpr int kCkptEscalate = -34;   // internal status: the compact tier stopped at a checkpoint (Doc::saveCkpt)
@@ -151,7 +153,7 @@ struct Scratch {
   HeapEnt heap[C::kHeapCap + 1];  // 1-based
   PropSet props[C::kPropCap];
   uint16_t propCls[C::kPropCap];  // match class: the first interned set with the same content (empty: 0xFFFF)
-  uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (lane k = entry k)
+  uint32_t kvWork[FMT_MT_PROPS_KEYS_MAX];  // applyProps' working set (slot k = entry k)
   typename C::BId freeList[C::kMaxBlocks];
   uint32_t tmp[64];
   ObEnt ob[kObCap];          // slots
@@ -1172,7 +1174,8 @@ class Doc {
   }
 
   // `seg.properties ??= {}` then raw LWW per key, null deletes (segmentPropertiesManager.ts:188-238).
-  // The working set lives in LDS (kvWork, lane k = key slot k), so the sets' width costs no registers.
+  // The working set lives in LDS (kvWork, slot k = lane k % 64 of chunk k / 64), so the sets' width
+  // costs no registers; the chunks past the set's entries are skipped.
   // (AdjSite: the annotate call site, the only one whose props ops can hold annotate-adjust entries)
   template <bool AdjSite = false>
   FMT_DEV uint32_t applyProps(uint32_t old, uint32_t opId) {
@@ -1181,10 +1184,16 @@ class Doc {
     for (uint32_t t = a; t < b; t++) {
       uint32_t e = uni(in.propsKv[t]);
       const uint32_t key = e >> 16;
-      Lane<bool> hit;
-      FOR_LANES(l) { LANE(hit) = l < static_cast<int>(cnt) && (s->kvWork[l] >> 16) == key; }
-      const uint64_t m = ballot(hit);
-      const uint32_t pos = m ? static_cast<uint32_t>(ctz64(m)) : cnt;
+      uint32_t pos = cnt;
+      for (int c = 0; c < kKeyChunks && pos == cnt && c * 64 < static_cast<int>(cnt); c++) {
+        Lane<bool> hit;
+        FOR_LANES(l) {
+          const int k = c * 64 + l;
+          LANE(hit) = k < static_cast<int>(cnt) && (s->kvWork[k] >> 16) == key;
+        }
+        const uint64_t m = ballot(hit);
+        if (m) pos = static_cast<uint32_t>(c * 64 + ctz64(m));
+      }
       if ((e & 0xFFFFu) == FMT_MT_VALUE_ADJUST) {  // annotate-adjust: fold into the current value
         // (an insert's or a loaded segment's props hold raw values only; batches with adjusts run the
         // Adj variant)
@@ -1206,18 +1215,25 @@ class Doc {
         }
       }
       if ((e & 0xFFFFu) == 0) {  // null: delete the key
-        if (pos < cnt) {
-          Lane<uint32_t> v;
-          FOR_LANES(l) { LANE(v) = (l < kKeysMax - 1 && l >= static_cast<int>(pos)) ? s->kvWork[l + 1] : 0u; }
-          waveSync();
-          FOR_LANES(l) {
-            if (l >= static_cast<int>(pos) && l + 1 < static_cast<int>(cnt)) s->kvWork[l] = LANE(v);
+        if (pos < cnt) {  // entries pos+1 .. cnt-1 move down one slot, a chunk at a time in slot order
+          for (int c = static_cast<int>(pos) / 64; c < kKeyChunks && c * 64 < static_cast<int>(cnt); c++) {
+            Lane<uint32_t> v;
+            FOR_LANES(l) {
+              const int k = c * 64 + l;
+              LANE(v) = (k < kKeysMax - 1 && k >= static_cast<int>(pos)) ? s->kvWork[k + 1] : 0u;
+            }
+            waveSync();
+            FOR_LANES(l) {
+              const int k = c * 64 + l;
+              if (k >= static_cast<int>(pos) && k + 1 < static_cast<int>(cnt)) s->kvWork[k] = LANE(v);
+            }
+            waveSync();
           }
           cnt--;
         }
       } else if (pos < cnt) {
         FOR_LANES(l) {
-          if (l == static_cast<int>(pos)) s->kvWork[l] = e;
+          if (l == static_cast<int>(pos % 64)) s->kvWork[pos] = e;
         }
       } else {
         if (cnt >= static_cast<uint32_t>(kKeysMax)) {
@@ -1225,7 +1241,7 @@ class Doc {
           return 0;
         }
         FOR_LANES(l) {
-          if (l == static_cast<int>(cnt)) s->kvWork[l] = e;
+          if (l == static_cast<int>(cnt % 64)) s->kvWork[cnt] = e;
         }
         cnt++;
       }
@@ -1255,12 +1271,14 @@ class Doc {
       return 0;
     }
     propsIndex(nProps, cnt);
-    FOR_LANES(l) {
-      const int q = l / FMT_MT_PROPS_MAX, k = l % FMT_MT_PROPS_MAX;
-      if (q < rec) {
-        if (k == 0) s->props[nProps + q].n = q == 0 ? cnt : FMT_MT_PROPS_CONT;
-        s->props[nProps + q].kv[k] = s->kvWork[l];
-        if (k == 0 && q > 0) s->propCls[nProps + q] = 0xFFFEu;  // (a continuation: no leaf names it)
+    for (int c = 0; c * 64 < rec * FMT_MT_PROPS_MAX; c++) {  // (slots past cnt: the record's unused entries, 0)
+      FOR_LANES(l) {
+        const int j = c * 64 + l, q = j / FMT_MT_PROPS_MAX, k = j % FMT_MT_PROPS_MAX;
+        if (q < rec) {
+          if (k == 0) s->props[nProps + q].n = q == 0 ? cnt : FMT_MT_PROPS_CONT;
+          s->props[nProps + q].kv[k] = j < static_cast<int>(cnt) ? s->kvWork[j] : 0u;
+          if (k == 0 && q > 0) s->propCls[nProps + q] = 0xFFFEu;  // (a continuation: no leaf names it)
+        }
       }
     }
     waveSync();
@@ -1270,10 +1288,16 @@ class Doc {
   }
   // entry k of the prop set whose first record is p
   FMT_DEV uint32_t setKv(int p, uint32_t k) const { return s->props[p + static_cast<int>(k / FMT_MT_PROPS_MAX)].kv[k % FMT_MT_PROPS_MAX]; }
-  // the working set = the entries of set `old` (kPropsUndef: none); returns their count
+  // the working set = the entries of set `old` (kPropsUndef: none); returns their count (slots past
+  // it are never read)
   FMT_DEV uint32_t loadWork(uint32_t old) {
     const uint32_t cnt = old != kPropsUndef ? uni(s->props[old].n) : 0u;
-    FOR_LANES(l) { s->kvWork[l] = l < static_cast<int>(cnt) ? setKv(static_cast<int>(old), static_cast<uint32_t>(l)) : 0u; }
+    for (int c = 0; c < kKeyChunks && c * 64 < static_cast<int>(cnt); c++) {
+      FOR_LANES(l) {
+        const int k = c * 64 + l;
+        if (k < static_cast<int>(cnt)) s->kvWork[k] = setKv(static_cast<int>(old), static_cast<uint32_t>(k));
+      }
+    }
     waveSync();
     return cnt;
   }

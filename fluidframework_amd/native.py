@@ -61,7 +61,7 @@ from .streams import (NO_MARKER, RELPOS_DTYPE, SNAPSHOT_DOC_DTYPE, SNAPSHOT_INFO
                       STAMP_DTYPE)  # (include/fmt.h layouts)
 
 PROPS_MAX = 8        # fmt.h FMT_MT_PROPS_MAX: entries per prop-set record
-PROPS_KEYS_MAX = 64  # fmt.h FMT_MT_PROPS_KEYS_MAX: entries per prop set
+PROPS_KEYS_MAX = 128  # fmt.h FMT_MT_PROPS_KEYS_MAX: entries per prop set
 PROPS_CONT = 0xFFFFFFFF  # fmt.h FMT_MT_PROPS_CONT: n of a continuation record
 MAP_PENDING_MAX_EVENTS = 16384  # fmt.h FMT_MAP_PENDING_MAX_EVENTS: local events per document
 PROPSET_DTYPE = np.dtype([("n", "<u4"), ("kv", "<u4", (PROPS_MAX,))])

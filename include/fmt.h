@@ -374,7 +374,7 @@ typedef struct fmt_mt_remove_order {
  * one n = FMT_MT_PROPS_CONT and the next 8 entries (unused entries 0). Leaf prop-set ids name first
  * records; fmt_mt_doc_result.n_props counts records. */
 #define FMT_MT_PROPS_MAX 8
-#define FMT_MT_PROPS_KEYS_MAX 64
+#define FMT_MT_PROPS_KEYS_MAX 128
 #define FMT_MT_PROPS_CONT 0xffffffffu
 typedef struct fmt_mt_propset {
   uint32_t n;

@@ -153,8 +153,8 @@ def _wide_messages(n_keys):
     return m
 
 
-@pytest.mark.parametrize("n_keys", [5, 8, 9, 17, 40, 64])
-def test_prop_sets_up_to_64_keys_match_oracle(orc, n_keys):
+@pytest.mark.parametrize("n_keys", [5, 8, 9, 17, 40, 64, 65, 100, 128])
+def test_prop_sets_up_to_128_keys_match_oracle(orc, n_keys):
     b = MergeTreeStreamBuilder()
     d = b.begin_doc("", observer="A")
     for msg in _wide_messages(n_keys):
@@ -173,10 +173,11 @@ def test_prop_sets_up_to_64_keys_match_oracle(orc, n_keys):
         assert max(int(p["n"]) for p in op[0][: int(oh[0]["n_props"])] if int(p["n"]) != PROPS_CONT) == n_keys
 
 
-def test_prop_set_beyond_64_keys_is_a_capacity_error():
+def test_prop_set_beyond_128_keys_is_a_capacity_error():
+    """128 keys per set since round 6 (64 before): the working set's slots span two waves' lanes."""
     b = MergeTreeStreamBuilder()
     d = b.begin_doc("", observer="A")
-    for msg in _wide_messages(65):
+    for msg in _wide_messages(129):
         d.add_message(msg)
     hdr, *_ = emu_replay(b.finish(), large=True)
     assert int(hdr[0]["status"]) == -3  # FMT_E_CAPACITY (include/fmt.h FMT_MT_PROPS_KEYS_MAX)
