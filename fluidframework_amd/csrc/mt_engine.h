@@ -64,7 +64,7 @@ constexpr int kCkptEscalate = -34;   // internal status: the compact tier stoppe
 struct SmallTier {
   static constexpr int kRows = 8;          // rows of 64 leaves (one VR element per row)
   // UTF-16 units per document (tombstones included): the LDS left per wave at 2 waves/SIMD (8 per
-  // CU: 8 × 19168 B of Scratch fits the 160 KiB)
+  // CU: 8 × 19424 B of Scratch fits the 160 KiB)
   static constexpr int kCapChars = 6144;
   static constexpr int kMaxBlocks = 128;
   static constexpr int kHeapCap = 255;
@@ -85,7 +85,7 @@ struct SmallTier {
 // outgrows it replays again in the small tier (runtime cascade).
 struct CompactTier : SmallTier {
   static constexpr int kRows = 4;
-  static constexpr int kCapChars = 2048;  // 12 waves/CU × 10976 B of Scratch
+  static constexpr int kCapChars = 2048;  // 12 waves/CU × 11232 B of Scratch
   using VR = V4;
 };
 
